@@ -1,0 +1,100 @@
+"""ctypes loader for the oracle (test infrastructure only; see vp8_oracle.h).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_lib = None
+
+
+class Config(C.Structure):
+    _fields_ = [("quality", C.c_float), ("method", C.c_int), ("segments", C.c_int),
+                ("sns_strength", C.c_int), ("filter_strength", C.c_int),
+                ("filter_sharpness", C.c_int), ("filter_type", C.c_int),
+                ("partition_limit", C.c_int), ("preprocessing", C.c_int),
+                ("emulate_jpeg_size", C.c_int)]
+
+
+class MBTrace(C.Structure):
+    _fields_ = [("segment", C.c_uint8), ("type", C.c_uint8), ("uv_mode", C.c_uint8),
+                ("skip", C.c_uint8), ("modes", C.c_uint8 * 16), ("alpha", C.c_uint8),
+                ("pad", C.c_uint8 * 3), ("y_dc", C.c_int16 * 16),
+                ("y_ac", C.c_int16 * 256), ("uv", C.c_int16 * 128)]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = os.path.join(_HERE, "_build", "libvp8oracle.so")
+        if not os.path.exists(path):
+            build()
+        _lib = C.CDLL(path)
+        _lib.vp8o_encode_rgba.restype = C.c_size_t
+        _lib.vp8o_encode_yuv.restype = C.c_size_t
+        _lib.vp8o_import_rgba.restype = C.c_int
+        vp, i = C.c_void_p, C.c_int
+        _lib.vp8o_import_rgba.argtypes = [vp, i, i, i, vp, vp, vp]
+        _lib.vp8o_encode_yuv.argtypes = [vp, vp, vp, i, i, i, i, vp, vp, vp]
+        _lib.vp8o_encode_rgba.argtypes = [vp, i, i, i, vp, vp]
+        _lib.vp8o_analyze.argtypes = [vp, vp, vp, i, i, i, i, vp, vp, vp]
+        _lib.vp8o_free.argtypes = [vp]
+        _lib.vp8o_default_config.argtypes = [vp]
+    return _lib
+
+
+def build():
+    import subprocess
+    subprocess.check_call(
+        ["make", "-s", "oracle",
+         "CFLAGS=-O2 -fPIC -Wall -Wno-unused-function -Wno-missing-braces -I../libwebp_amd/csrc"],
+        cwd=_HERE)
+
+
+def config(quality=75.0, method=4, **kw):
+    c = Config()
+    lib().vp8o_default_config(C.byref(c))
+    c.quality = quality
+    c.method = method
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def import_rgba(rgba):
+    rgba = np.ascontiguousarray(rgba, np.uint8)
+    h, w = rgba.shape[:2]
+    uw, uh = (w + 1) // 2, (h + 1) // 2
+    y = np.empty((h, w), np.uint8)
+    u = np.empty((uh, uw), np.uint8)
+    v = np.empty((uh, uw), np.uint8)
+    ok = lib().vp8o_import_rgba(rgba.ctypes.data, w, h, 4 * w, y.ctypes.data,
+                                u.ctypes.data, v.ctypes.data)
+    if not ok:
+        raise ValueError("non-opaque input is not restated by the oracle")
+    return y, u, v
+
+
+def encode_yuv(y, u, v, quality=75.0, method=4, trace=False, **kw):
+    h, w = y.shape
+    cfg = config(quality, method, **kw)
+    out = C.POINTER(C.c_uint8)()
+    nmb = ((w + 15) // 16) * ((h + 15) // 16)
+    tr = (MBTrace * nmb)() if trace else None
+    n = lib().vp8o_encode_yuv(y.ctypes.data, u.ctypes.data, v.ctypes.data, w, h,
+                              y.strides[0], u.strides[0], C.byref(cfg), C.byref(out),
+                              tr)
+    if n == 0:
+        raise RuntimeError("oracle encode failed")
+    data = C.string_at(out, n)
+    lib().vp8o_free(out)
+    return (data, tr) if trace else data
+
+
+def encode_rgba(rgba, quality=75.0, method=4, **kw):
+    y, u, v = import_rgba(rgba)
+    return encode_yuv(y, u, v, quality, method, **kw)

@@ -1,0 +1,67 @@
+/* Test infrastructure ONLY: a scalar CPU restatement of libwebp v1.3.2's
+ * lossy (VP8) encode path, used by tests/ and bench.py's cpu_baseline leg as
+ * the checker for the HIP product path. Never linked into libwebp_amd.
+ * Every function in vp8_oracle.c cites the reference file:line it follows.
+ * Pinned by the known-answer SHA-256s of SURVEY.md §8(d) and by the reference
+ * build in oracle/_ref (tests/test_oracle.py). */
+#ifndef VP8_ORACLE_H_
+#define VP8_ORACLE_H_
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  float quality;          /* 0..100 */
+  int method;             /* 3..6 supported (token-buffer path) */
+  int segments;           /* 1..4 */
+  int sns_strength;       /* 0..100 */
+  int filter_strength;    /* 0..100 */
+  int filter_sharpness;   /* 0..7 */
+  int filter_type;        /* 0 simple, 1 strong */
+  int partition_limit;    /* 0..100 */
+  int preprocessing;      /* bit0: segment smoothing */
+  int emulate_jpeg_size;  /* 0/1 */
+} vp8o_config;
+
+/* per-macroblock decisions, for stage-by-stage comparison with the GPU */
+typedef struct {
+  uint8_t segment, type, uv_mode, skip;
+  uint8_t modes[16];        /* i16: modes[0..15] all equal the i16 mode */
+  uint8_t alpha;            /* analysis susceptibility (after k-means remap) */
+  uint8_t pad[3];
+  int16_t y_dc[16];
+  int16_t y_ac[16][16];
+  int16_t uv[8][16];
+} vp8o_mb_trace;
+
+void vp8o_default_config(vp8o_config* cfg);
+
+/* RGBA -> YUV420 (ImportYUVAFromRGBA, opaque path). Returns 0 if the input
+ * has non-opaque alpha (that path is not restated). */
+int vp8o_import_rgba(const uint8_t* rgba, int w, int h, int stride,
+                     uint8_t* y, uint8_t* u, uint8_t* v);
+
+/* Full lossy encode from YUV420 planes. Returns the .webp size (malloc'ed
+ * into *out, free with vp8o_free) or 0 on error. trace may be NULL. */
+size_t vp8o_encode_yuv(const uint8_t* y, const uint8_t* u, const uint8_t* v,
+                       int w, int h, int y_stride, int uv_stride,
+                       const vp8o_config* cfg, uint8_t** out,
+                       vp8o_mb_trace* trace);
+
+size_t vp8o_encode_rgba(const uint8_t* rgba, int w, int h, int stride,
+                        const vp8o_config* cfg, uint8_t** out);
+
+/* analysis only: per-MB alpha (pre-k-means) and the 256-bin histogram */
+void vp8o_analyze(const uint8_t* y, const uint8_t* u, const uint8_t* v,
+                  int w, int h, int y_stride, int uv_stride,
+                  uint8_t* mb_alpha, int* uv_alpha_sum, int* histo256);
+
+void vp8o_free(void* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

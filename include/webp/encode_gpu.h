@@ -1,0 +1,88 @@
+/* libwebp_amd -- batched MI355X extension of the libwebp encoder ABI.
+ *
+ * The reference has no batch entry point: its unit of work is one
+ * WebPEncode(config, picture) call (src/webp/encode.h:544,
+ * src/enc/webp_enc.c:330-410). This header adds the batched form that the
+ * GPU needs for occupancy: many same-sized frames resident in HBM are
+ * converted, analysed, rate-distortion searched and tokenised in one set of
+ * kernel launches, then the boolean-coder tail runs on a host thread pool.
+ * The bitstream of every frame is byte-identical to what WebPEncode() of the
+ * reference produces for the same pixels and config.
+ *
+ * All pointers are plain device or host addresses; streams are hipStream_t
+ * passed as void*. No framework types cross this boundary.
+ */
+#ifndef WEBP_WEBP_ENCODE_GPU_H_
+#define WEBP_WEBP_ENCODE_GPU_H_
+
+#include "./encode.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct WebPGpuBatch WebPGpuBatch;
+
+/* Create an encoder for up to max_frames frames of width x height, on HIP
+ * device `device`, with `config` (lossy, method 3..6). host_threads <= 0
+ * picks a default (env WEBP_AMD_THREADS, else min(16, online CPUs)).
+ * Returns NULL on error (no GPU, bad config, out of memory). */
+WEBP_EXTERN WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height,
+                                          int max_frames,
+                                          const WebPConfig* config,
+                                          int host_threads);
+WEBP_EXTERN void WebPGpuBatchDelete(WebPGpuBatch* batch);
+
+/* Encode num_frames RGBA frames already in device memory: frame f starts at
+ * (const uint8_t*)rgba_dev + f * frame_stride, rows are row_stride bytes.
+ * `stream` (hipStream_t or NULL) orders the device work after the caller's
+ * producer kernels. Returns 1 on success; per-frame status via
+ * WebPGpuBatchError(). Outputs stay valid until the next call. */
+WEBP_EXTERN int WebPGpuBatchEncodeRGBA(WebPGpuBatch* batch,
+                                       const void* rgba_dev,
+                                       size_t frame_stride, int row_stride,
+                                       int num_frames, void* stream);
+
+/* Same, from host memory (includes the PCIe upload). */
+WEBP_EXTERN int WebPGpuBatchEncodeRGBAHost(WebPGpuBatch* batch,
+                                           const uint8_t* rgba_host,
+                                           size_t frame_stride, int row_stride,
+                                           int num_frames);
+
+/* Results of the last encode call. */
+WEBP_EXTERN size_t WebPGpuBatchOutputSize(const WebPGpuBatch* batch, int frame);
+WEBP_EXTERN const uint8_t* WebPGpuBatchOutput(const WebPGpuBatch* batch,
+                                              int frame);
+WEBP_EXTERN int WebPGpuBatchError(const WebPGpuBatch* batch, int frame);
+
+/* Per-stage wall times of the last call in microseconds:
+ * [0] import+analysis kernels, [1] host segment setup, [2] RD/token kernel,
+ * [3] device->host copies, [4] host tail (emit + assembly), [5] total. */
+WEBP_EXTERN void WebPGpuBatchTimings(const WebPGpuBatch* batch,
+                                     double timings_us[8]);
+
+/* Debug/parity hooks (used by tests): copy the device YUV420 planes of frame
+ * f (Y | U | V, contiguous, strides width and (width+1)/2), and the per-MB
+ * decisions (20 bytes per MB: type, uv_mode, segment, skip, modes[16]). */
+WEBP_EXTERN int WebPGpuBatchGetYUV(const WebPGpuBatch* batch, int frame,
+                                   uint8_t* dst);
+WEBP_EXTERN int WebPGpuBatchGetMBInfo(const WebPGpuBatch* batch, int frame,
+                                      uint8_t* dst);
+
+/* Benchmark/test utility: write frames first_frame .. first_frame+n-1 of
+ * the syn-v1 synthetic RGBA sequence into device memory. */
+WEBP_EXTERN int WebPGpuSynthRGBA(void* rgba_dev, size_t frame_stride, int width,
+                                 int height, int first_frame, int num_frames,
+                                 int seed, void* stream);
+
+/* Text of the first HIP/runtime error seen by this thread ("" if none). */
+WEBP_EXTERN const char* WebPGpuLastError(void);
+
+/* Number of HIP devices visible (0 when no GPU / no driver). */
+WEBP_EXTERN int WebPGpuDeviceCount(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WEBP_WEBP_ENCODE_GPU_H_ */

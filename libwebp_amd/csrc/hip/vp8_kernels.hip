@@ -1,0 +1,1411 @@
+// HIP/CDNA4 kernels for the batched VP8 lossy encoder (gfx950).
+//
+//   K1 k_import    RGBA -> YUV420 with gamma-linear chroma averaging
+//                  (picture_csp_enc.c:375-619; yuv.h:186-204). One thread per
+//                  2x2 luma quad, coalesced 8-byte RGBA reads. HBM-bound.
+//   K2 k_analyze   per-macroblock susceptibility (analysis_enc.c:230-333):
+//                  one wavefront per MB, 48 4x4 DCTs on 48 lanes, LDS
+//                  histograms.
+//   K3 k_encode    the raster-order RD macroblock loop of VP8EncTokenLoop
+//                  (frame_enc.c:783-894): one wavefront owns one frame and
+//                  walks its MBs in order (the only exact order for the
+//                  token statistics / cost-refresh epochs); inside an MB the
+//                  I16 (4 modes x 16 blocks = 64 lanes), I4 (10 modes) and
+//                  UV (4 modes x 8 blocks) candidates run lane-parallel out
+//                  of LDS, then the MB's tokens are generated 25 blocks
+//                  in parallel and folded into exact saturating statistics.
+//
+// No MFMA: there is no dense contraction on this path.
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+
+#include "../vp8_gpu.h"
+
+#define VP8T_DECL static __constant__ const
+#include "../vp8_tables.h"
+
+#define BPS 32
+#define QFIX 17
+#define MAX_LEVEL 2047
+#define MAX_VLEVEL 67
+#define NSLOT VP8G_NUM_SLOTS
+#define MAX_COST ((long long)0x7fffffffffffffLL)
+
+typedef long long score_t;
+
+// zigzag scan as constexpr functions so unrolled loops index registers
+// statically (a __constant__ table would force private arrays to scratch)
+__device__ __forceinline__ constexpr int zz(int n) {
+  return n == 0 ? 0 : n == 1 ? 1 : n == 2 ? 4 : n == 3 ? 8 : n == 4 ? 5 : n == 5 ? 2 :
+         n == 6 ? 3 : n == 7 ? 6 : n == 8 ? 9 : n == 9 ? 12 : n == 10 ? 13 : n == 11 ? 10 :
+         n == 12 ? 7 : n == 13 ? 11 : n == 14 ? 14 : 15;
+}
+static __constant__ const uint8_t dZzInv[16] = {0, 1, 5, 6, 2, 4, 7, 12, 3, 8, 11, 13, 9, 10, 14, 15};
+static __constant__ const uint8_t dBand[17] = {0, 1, 2, 3, 6, 4, 5, 6, 6, 6, 6, 6, 6, 6, 6, 7, 0};
+
+// 4x4 intra predictor as data: pred[m][p] = f(edges e[0..12]) with
+// e = L K J I X A B C D E F G H (src/dsp/enc.c:351-512). kind: 0 AVG3(a,b,c)
+// 1 AVG2(a,b) 2 copy(a) 3 TM clip(e[5+x] + e[3-y] - X) 4 DC.
+struct P4Op { uint8_t kind, a, b, c; };
+#define A3(a, b, c) {0, a, b, c}
+#define A2(a, b) {1, a, b, 0}
+#define CP(a) {2, a, 0, 0}
+enum { eL = 0, eK, eJ, eI, eX, eA, eB, eC, eD, eE, eF, eG, eH };
+static __constant__ const P4Op kP4[10][16] = {
+  // DC
+  {{4,0,0,0},{4,0,0,0},{4,0,0,0},{4,0,0,0},{4,0,0,0},{4,0,0,0},{4,0,0,0},{4,0,0,0},
+   {4,0,0,0},{4,0,0,0},{4,0,0,0},{4,0,0,0},{4,0,0,0},{4,0,0,0},{4,0,0,0},{4,0,0,0}},
+  // TM
+  {{3,0,0,0},{3,0,0,0},{3,0,0,0},{3,0,0,0},{3,0,0,0},{3,0,0,0},{3,0,0,0},{3,0,0,0},
+   {3,0,0,0},{3,0,0,0},{3,0,0,0},{3,0,0,0},{3,0,0,0},{3,0,0,0},{3,0,0,0},{3,0,0,0}},
+  // VE
+  {A3(eX,eA,eB),A3(eA,eB,eC),A3(eB,eC,eD),A3(eC,eD,eE), A3(eX,eA,eB),A3(eA,eB,eC),A3(eB,eC,eD),A3(eC,eD,eE),
+   A3(eX,eA,eB),A3(eA,eB,eC),A3(eB,eC,eD),A3(eC,eD,eE), A3(eX,eA,eB),A3(eA,eB,eC),A3(eB,eC,eD),A3(eC,eD,eE)},
+  // HE
+  {A3(eX,eI,eJ),A3(eX,eI,eJ),A3(eX,eI,eJ),A3(eX,eI,eJ), A3(eI,eJ,eK),A3(eI,eJ,eK),A3(eI,eJ,eK),A3(eI,eJ,eK),
+   A3(eJ,eK,eL),A3(eJ,eK,eL),A3(eJ,eK,eL),A3(eJ,eK,eL), A3(eK,eL,eL),A3(eK,eL,eL),A3(eK,eL,eL),A3(eK,eL,eL)},
+  // RD
+  {A3(eA,eX,eI),A3(eB,eA,eX),A3(eC,eB,eA),A3(eD,eC,eB), A3(eX,eI,eJ),A3(eA,eX,eI),A3(eB,eA,eX),A3(eC,eB,eA),
+   A3(eI,eJ,eK),A3(eX,eI,eJ),A3(eA,eX,eI),A3(eB,eA,eX), A3(eJ,eK,eL),A3(eI,eJ,eK),A3(eX,eI,eJ),A3(eA,eX,eI)},
+  // VR
+  {A2(eX,eA),A2(eA,eB),A2(eB,eC),A2(eC,eD), A3(eI,eX,eA),A3(eX,eA,eB),A3(eA,eB,eC),A3(eB,eC,eD),
+   A3(eJ,eI,eX),A2(eX,eA),A2(eA,eB),A2(eB,eC), A3(eK,eJ,eI),A3(eI,eX,eA),A3(eX,eA,eB),A3(eA,eB,eC)},
+  // LD
+  {A3(eA,eB,eC),A3(eB,eC,eD),A3(eC,eD,eE),A3(eD,eE,eF), A3(eB,eC,eD),A3(eC,eD,eE),A3(eD,eE,eF),A3(eE,eF,eG),
+   A3(eC,eD,eE),A3(eD,eE,eF),A3(eE,eF,eG),A3(eF,eG,eH), A3(eD,eE,eF),A3(eE,eF,eG),A3(eF,eG,eH),A3(eG,eH,eH)},
+  // VL
+  {A2(eA,eB),A2(eB,eC),A2(eC,eD),A2(eD,eE), A3(eA,eB,eC),A3(eB,eC,eD),A3(eC,eD,eE),A3(eD,eE,eF),
+   A2(eB,eC),A2(eC,eD),A2(eD,eE),A3(eE,eF,eG), A3(eB,eC,eD),A3(eC,eD,eE),A3(eD,eE,eF),A3(eF,eG,eH)},
+  // HD
+  {A2(eI,eX),A3(eI,eX,eA),A3(eX,eA,eB),A3(eA,eB,eC), A2(eJ,eI),A3(eJ,eI,eX),A2(eI,eX),A3(eI,eX,eA),
+   A2(eK,eJ),A3(eK,eJ,eI),A2(eJ,eI),A3(eJ,eI,eX), A2(eL,eK),A3(eL,eK,eJ),A2(eK,eJ),A3(eK,eJ,eI)},
+  // HU
+  {A2(eI,eJ),A3(eI,eJ,eK),A2(eJ,eK),A3(eJ,eK,eL), A2(eJ,eK),A3(eJ,eK,eL),A2(eK,eL),A3(eK,eL,eL),
+   A2(eK,eL),A3(eK,eL,eL),CP(eL),CP(eL), CP(eL),CP(eL),CP(eL),CP(eL)},
+};
+#undef A3
+#undef A2
+#undef CP
+
+__device__ __forceinline__ int clip8(int v) { return (v & ~0xff) == 0 ? v : (v < 0 ? 0 : 255); }
+__device__ __forceinline__ int iabs_(int v) { return v < 0 ? -v : v; }
+__device__ __forceinline__ int bit_cost(int bit, int p) {
+  return kVP8EntropyCost[bit ? 255 - p : p];
+}
+
+// ---------------------------------------------------------------------------
+// 4x4 transforms (src/dsp/enc.c:112-222, src/dsp/dec.c:137-162)
+
+__device__ __forceinline__ void fdct4(const uint8_t* src, int ss, const uint8_t* ref, int rs,
+                                      int out[16]) {
+  int t[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int d0 = src[i * ss + 0] - ref[i * rs + 0];
+    const int d1 = src[i * ss + 1] - ref[i * rs + 1];
+    const int d2 = src[i * ss + 2] - ref[i * rs + 2];
+    const int d3 = src[i * ss + 3] - ref[i * rs + 3];
+    const int a0 = d0 + d3, a1 = d1 + d2, a2 = d1 - d2, a3 = d0 - d3;
+    t[4 * i + 0] = (a0 + a1) * 8;
+    t[4 * i + 1] = (a2 * 2217 + a3 * 5352 + 1812) >> 9;
+    t[4 * i + 2] = (a0 - a1) * 8;
+    t[4 * i + 3] = (a3 * 2217 - a2 * 5352 + 937) >> 9;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int a0 = t[i] + t[12 + i], a1 = t[4 + i] + t[8 + i];
+    const int a2 = t[4 + i] - t[8 + i], a3 = t[i] - t[12 + i];
+    out[i] = (int16_t)((a0 + a1 + 7) >> 4);
+    out[4 + i] = (int16_t)(((a2 * 2217 + a3 * 5352 + 12000) >> 16) + (a3 != 0));
+    out[8 + i] = (int16_t)((a0 - a1 + 7) >> 4);
+    out[12 + i] = (int16_t)((a3 * 2217 - a2 * 5352 + 51000) >> 16);
+  }
+}
+
+#define IMUL(a, b) (((a) * (b)) >> 16)
+__device__ __forceinline__ void idct4(const uint8_t* ref, int rs, const int in[16], uint8_t* dst,
+                                      int ds) {
+  const int c1 = 20091 + (1 << 16), c2 = 35468;
+  int t[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int a = in[i] + in[8 + i], b = in[i] - in[8 + i];
+    const int c = IMUL(in[4 + i], c2) - IMUL(in[12 + i], c1);
+    const int d = IMUL(in[4 + i], c1) + IMUL(in[12 + i], c2);
+    t[4 * i + 0] = a + d; t[4 * i + 1] = b + c;
+    t[4 * i + 2] = b - c; t[4 * i + 3] = a - d;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int dc = t[i] + 4;
+    const int a = dc + t[8 + i], b = dc - t[8 + i];
+    const int c = IMUL(t[4 + i], c2) - IMUL(t[12 + i], c1);
+    const int d = IMUL(t[4 + i], c1) + IMUL(t[12 + i], c2);
+    dst[i * ds + 0] = clip8(ref[i * rs + 0] + ((a + d) >> 3));
+    dst[i * ds + 1] = clip8(ref[i * rs + 1] + ((b + c) >> 3));
+    dst[i * ds + 2] = clip8(ref[i * rs + 2] + ((b - c) >> 3));
+    dst[i * ds + 3] = clip8(ref[i * rs + 3] + ((a - d) >> 3));
+  }
+}
+
+// Hadamard texture measure (src/dsp/enc.c:590-622)
+__device__ __forceinline__ int hadamard_w(const uint8_t* in, int st) {
+  int t[16], sum = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint8_t* p = in + i * st;
+    const int a0 = p[0] + p[2], a1 = p[1] + p[3], a2 = p[1] - p[3], a3 = p[0] - p[2];
+    t[4 * i + 0] = a0 + a1; t[4 * i + 1] = a3 + a2;
+    t[4 * i + 2] = a3 - a2; t[4 * i + 3] = a0 - a1;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int a0 = t[i] + t[8 + i], a1 = t[4 + i] + t[12 + i];
+    const int a2 = t[4 + i] - t[12 + i], a3 = t[i] - t[8 + i];
+    sum += kVP8WeightY[i] * iabs_(a0 + a1) + kVP8WeightY[4 + i] * iabs_(a3 + a2) +
+           kVP8WeightY[8 + i] * iabs_(a3 - a2) + kVP8WeightY[12 + i] * iabs_(a0 - a1);
+  }
+  return sum;
+}
+
+__device__ __forceinline__ int sse4(const uint8_t* a, int as, const uint8_t* b, int bs) {
+  int s = 0;
+#pragma unroll
+  for (int y = 0; y < 4; ++y)
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int d = a[y * as + x] - b[y * bs + x];
+      s += d * d;
+    }
+  return s;
+}
+
+// QuantizeBlock_C on natural-order coefficients c[] (int16 semantics),
+// writes zigzag-order levels to lv[] (LDS), dequantises c[] in place.
+__device__ __forceinline__ int quantize_block(int c[16], int16_t* lv, const vp8g_mtx* m) {
+  int nz = 0;
+#pragma unroll
+  for (int n = 0; n < 16; ++n) {
+    const int j = zz(n);
+    const int neg = c[j] < 0;
+    const uint32_t coeff = (uint32_t)(neg ? -c[j] : c[j]) + m->sharpen[j];
+    int level = 0;
+    if (coeff > m->zthresh[j]) {
+      level = (int)((coeff * m->iq[j] + m->bias[j]) >> QFIX);
+      if (level > MAX_LEVEL) level = MAX_LEVEL;
+      if (neg) level = -level;
+    }
+    c[j] = (int16_t)(level * (int)m->q[j]);
+    lv[n] = (int16_t)level;
+    nz |= level;
+  }
+  return nz != 0;
+}
+
+// ---------------------------------------------------------------------------
+// K1: RGBA -> YUV420
+
+__device__ __forceinline__ int lin_to_gamma(const int* l2g, uint32_t sum, int shift) {
+  const int v = (int)(sum << shift);
+  const int pos = v >> 9, frac = v & 511;
+  return (l2g[pos + 1] * frac + l2g[pos] * (512 - frac) + 64) >> 7;
+}
+__device__ __forceinline__ int rgb_to_y(int r, int g, int b) {
+  return (16839 * r + 33059 * g + 6420 * b + (1 << 15) + (16 << 16)) >> 16;
+}
+__device__ __forceinline__ int clip_uv(int v) {
+  v = (v + (1 << 17) + (128 << 18)) >> 18;
+  return (v & ~0xff) == 0 ? v : (v < 0 ? 0 : 255);
+}
+
+__global__ __launch_bounds__(256) void k_import(const uint8_t* __restrict__ rgba,
+                                                size_t fstride, int rstride, int w, int h,
+                                                uint8_t* __restrict__ yuv, size_t yfb,
+                                                uint32_t* __restrict__ aflags,
+                                                const uint16_t* __restrict__ g_g2l,
+                                                const int32_t* __restrict__ g_l2g) {
+  __shared__ uint16_t g2l[256];
+  __shared__ int l2g[33];
+  const int t = threadIdx.x;
+  g2l[t] = g_g2l[t];
+  if (t < 33) l2g[t] = g_l2g[t];
+  __syncthreads();
+  const int uvw = (w + 1) >> 1, uvh = (h + 1) >> 1;
+  const int i = blockIdx.x * blockDim.x + t;   // chroma column
+  const int j = blockIdx.y;                    // chroma row
+  const int f = blockIdx.z;
+  if (i >= uvw) return;
+  const uint8_t* src = rgba + f * fstride;
+  uint8_t* Y = yuv + f * yfb;
+  uint8_t* U = Y + (size_t)w * h;
+  uint8_t* V = U + (size_t)uvw * uvh;
+  const int x0 = 2 * i, y0 = 2 * j;
+  const bool two_cols = x0 + 1 < w, two_rows = y0 + 1 < h;
+  const uint8_t* r0 = src + (size_t)y0 * rstride + 4 * x0;
+  const uint8_t* r1 = two_rows ? r0 + rstride : r0;
+  uint8_t p[2][2][4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    p[0][0][k] = r0[k];
+    p[1][0][k] = r1[k];
+    p[0][1][k] = two_cols ? r0[4 + k] : 0;
+    p[1][1][k] = two_cols ? r1[4 + k] : 0;
+  }
+  uint32_t alpha_bad = (p[0][0][3] != 0xff) | (p[1][0][3] != 0xff);
+  if (two_cols) alpha_bad |= (p[0][1][3] != 0xff) | (p[1][1][3] != 0xff);
+  if (alpha_bad) atomicOr(aflags + f, 1u);
+  uint8_t* yrow = Y + (size_t)y0 * w + x0;
+  yrow[0] = rgb_to_y(p[0][0][0], p[0][0][1], p[0][0][2]);
+  if (two_cols) yrow[1] = rgb_to_y(p[0][1][0], p[0][1][1], p[0][1][2]);
+  if (two_rows) {
+    yrow[w] = rgb_to_y(p[1][0][0], p[1][0][1], p[1][0][2]);
+    if (two_cols) yrow[w + 1] = rgb_to_y(p[1][1][0], p[1][1][1], p[1][1][2]);
+  }
+  int c[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (two_cols) {
+      c[k] = lin_to_gamma(l2g, (uint32_t)g2l[p[0][0][k]] + g2l[p[0][1][k]] + g2l[p[1][0][k]] +
+                                   g2l[p[1][1][k]], 0);
+    } else {
+      c[k] = lin_to_gamma(l2g, (uint32_t)g2l[p[0][0][k]] + g2l[p[1][0][k]], 1);
+    }
+  }
+  U[(size_t)j * uvw + i] = clip_uv(-9719 * c[0] - 19081 * c[1] + 28800 * c[2]);
+  V[(size_t)j * uvw + i] = clip_uv(28800 * c[0] - 24116 * c[1] - 4684 * c[2]);
+}
+
+// ---------------------------------------------------------------------------
+// Shared MB helpers: cache import with edge replication (iterator_enc.c:107-145)
+
+// Loads the 16x16 Y / 8x8 U / 8x8 V block of MB (x,y) into a BPS=32 cache
+// (Y at col 0, U at col 16, V at col 24), replicating right/bottom edges.
+__device__ __forceinline__ void load_mb(const uint8_t* Yp, const uint8_t* Up, const uint8_t* Vp,
+                                        int w, int h, int x, int y, uint8_t* cache, int lane,
+                                        int nlanes) {
+  const int uvw = (w + 1) >> 1;
+  const int bw = min(w - 16 * x, 16), bh = min(h - 16 * y, 16);
+  const int cw = (bw + 1) >> 1, ch = (bh + 1) >> 1;
+  for (int k = lane; k < 16 * 16 + 2 * 64; k += nlanes) {
+    if (k < 256) {
+      const int r = k >> 4, c = k & 15;
+      const int rr = min(r, bh - 1), cc = min(c, bw - 1);
+      cache[r * BPS + c] = Yp[(size_t)(16 * y + rr) * w + 16 * x + cc];
+    } else {
+      const int kk = k - 256, pl = kk >> 6, r = (kk >> 3) & 7, c = kk & 7;
+      const int rr = min(r, ch - 1), cc = min(c, cw - 1);
+      const uint8_t* P = pl ? Vp : Up;
+      cache[r * BPS + 16 + 8 * pl + c] = P[(size_t)(8 * y + rr) * uvw + 8 * x + cc];
+    }
+  }
+}
+
+// 16x16 / 8x8 predictor sample (src/dsp/enc.c:238-342). left/top arrays with
+// index -1 = corner; has_left/has_top select the 127/129 fall-backs.
+__device__ __forceinline__ int pred_sample(int mode, int n, int px, int py, const uint8_t* left,
+                                           const uint8_t* top, bool hl, bool ht, int dc) {
+  switch (mode) {
+    case 0: return dc;
+    case 1:  // TM
+      if (hl && ht) return clip8(top[px] + left[py] - left[-1]);
+      if (hl) return left[py];
+      if (ht) return top[px];
+      return 129;
+    case 2: return ht ? top[px] : 127;   // VE
+    default: return hl ? left[py] : 129; // HE
+  }
+}
+__device__ __forceinline__ int dc_value(const uint8_t* left, const uint8_t* top, bool hl, bool ht,
+                                        int n, int shift) {
+  int dc = 0;
+  if (ht) {
+    for (int j = 0; j < n; ++j) dc += top[j];
+    if (hl) { for (int j = 0; j < n; ++j) dc += left[j]; }
+    else dc += dc;
+    return (dc + n) >> shift;
+  }
+  if (hl) {
+    for (int j = 0; j < n; ++j) dc += left[j];
+    dc += dc;
+    return (dc + n) >> shift;
+  }
+  return 0x80;
+}
+
+// ---------------------------------------------------------------------------
+// K2: analysis (analysis_enc.c:230-333, iterator_enc.c:147-173; histogram
+// dsp/enc.c:46-81). One wavefront per MB, 4 MBs per 256-thread workgroup.
+
+struct K2Wave {
+  uint8_t yin[16 * BPS];
+  uint8_t p16[2][256];
+  uint8_t puv[2][128];
+  uint8_t yl[17], ul[9], vl[9];
+  uint8_t top[32];
+  int hist[4][32];
+};
+
+__global__ __launch_bounds__(256) void k_analyze(const uint8_t* __restrict__ yuv, size_t yfb,
+                                                 int w, int h, int nmb,
+                                                 uint8_t* __restrict__ mb_alpha,
+                                                 uint16_t* __restrict__ mb_uva) {
+  __shared__ K2Wave S[4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int mb = blockIdx.x * 4 + wave;
+  const int f = blockIdx.y;
+  if (mb >= nmb) return;
+  K2Wave& L = S[wave];
+  const int mbw = (w + 15) >> 4;
+  const int x = mb % mbw, y = mb / mbw;
+  const int uvw = (w + 1) >> 1, uvh = (h + 1) >> 1;
+  const uint8_t* Yp = yuv + f * yfb;
+  const uint8_t* Up = Yp + (size_t)w * h;
+  const uint8_t* Vp = Up + (size_t)uvw * uvh;
+  load_mb(Yp, Up, Vp, w, h, x, y, L.yin, lane, 64);
+  const int bw = min(w - 16 * x, 16), bh = min(h - 16 * y, 16);
+  const int cw = (bw + 1) >> 1, ch = (bh + 1) >> 1;
+  uint8_t* yl = L.yl + 1;
+  uint8_t* ul = L.ul + 1;
+  uint8_t* vl = L.vl + 1;
+  // source boundary
+  if (lane < 32) {
+    const int i = lane;
+    if (x == 0) {
+      if (i < 16) yl[i] = 129;
+      if (i < 8) { ul[i] = 129; vl[i] = 129; }
+      if (i == 0) yl[-1] = ul[-1] = vl[-1] = (y > 0) ? 129 : 127;
+    } else {
+      if (i < 16) yl[i] = Yp[(size_t)(16 * y + min(i, bh - 1)) * w + 16 * x - 1];
+      if (i < 8) {
+        ul[i] = Up[(size_t)(8 * y + min(i, ch - 1)) * uvw + 8 * x - 1];
+        vl[i] = Vp[(size_t)(8 * y + min(i, ch - 1)) * uvw + 8 * x - 1];
+      }
+      if (i == 0) {
+        if (y == 0) {
+          yl[-1] = ul[-1] = vl[-1] = 127;
+        } else {
+          yl[-1] = Yp[(size_t)(16 * y - 1) * w + 16 * x - 1];
+          ul[-1] = Up[(size_t)(8 * y - 1) * uvw + 8 * x - 1];
+          vl[-1] = Vp[(size_t)(8 * y - 1) * uvw + 8 * x - 1];
+        }
+      }
+    }
+    if (y == 0) {
+      L.top[i] = 127;
+    } else if (i < 16) {
+      L.top[i] = Yp[(size_t)(16 * y - 1) * w + 16 * x + min(i, bw - 1)];
+    } else {
+      const int k = i & 7;
+      const uint8_t* P = (i < 24) ? Up : Vp;
+      L.top[i] = P[(size_t)(8 * y - 1) * uvw + 8 * x + min(k, cw - 1)];
+    }
+  }
+  for (int k = lane; k < 4 * 32; k += 64) (&L.hist[0][0])[k] = 0;
+  __syncthreads();
+  const bool hl = x > 0, ht = y > 0;
+  {
+    const int dcy = dc_value(yl, L.top, hl, ht, 16, 5);
+    for (int k = lane; k < 512; k += 64) {
+      const int m = k >> 8, p = k & 255;
+      L.p16[m][p] = pred_sample(m, 16, p & 15, p >> 4, yl, L.top, hl, ht, dcy);
+    }
+    const int dcu = dc_value(ul, L.top + 16, hl, ht, 8, 4);
+    const int dcv = dc_value(vl, L.top + 24, hl, ht, 8, 4);
+    for (int k = lane; k < 256; k += 64) {
+      const int m = k >> 7, p = k & 127, px = p & 15, py = p >> 4;
+      const int c = px >> 3;
+      L.puv[m][p] = pred_sample(m, 8, px & 7, py, c ? vl : ul, L.top + 16 + 8 * c, hl, ht,
+                                c ? dcv : dcu);
+    }
+  }
+  __syncthreads();
+  if (lane < 48) {
+    int coeffs[16], hsel;
+    if (lane < 32) {
+      const int m = lane >> 4, b = lane & 15;
+      fdct4(L.yin + (b >> 2) * 4 * BPS + (b & 3) * 4, BPS, L.p16[m] + (b >> 2) * 64 + (b & 3) * 4,
+            16, coeffs);
+      hsel = m;
+    } else {
+      const int m = (lane - 32) >> 3, b = lane & 7, c = b >> 2, k = b & 3;
+      fdct4(L.yin + 16 + 8 * c + (k >> 1) * 4 * BPS + (k & 1) * 4, BPS,
+            L.puv[m] + 8 * c + (k >> 1) * 64 + (k & 1) * 4, 16, coeffs);
+      hsel = 2 + m;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int v = min(iabs_(coeffs[k]) >> 3, 31);
+      atomicAdd(&L.hist[hsel][v], 1);
+    }
+  }
+  __syncthreads();
+  if (lane == 0) {
+    int alpha[4];
+    for (int hh = 0; hh < 4; ++hh) {
+      int maxv = 0, last = 1;
+      for (int k = 0; k < 32; ++k) {
+        const int v = L.hist[hh][k];
+        if (v > 0) { if (v > maxv) maxv = v; last = k; }
+      }
+      alpha[hh] = maxv > 1 ? 510 * last / maxv : 0;
+    }
+    int best = -1;
+    if (alpha[0] > best) best = alpha[0];
+    if (alpha[1] > best) best = alpha[1];
+    int best_uv = -1;
+    if (alpha[2] > best_uv) best_uv = alpha[2];
+    if (alpha[3] > best_uv) best_uv = alpha[3];
+    int a = (3 * best + best_uv + 2) >> 2;
+    a = 255 - a;
+    a = a < 0 ? 0 : a > 255 ? 255 : a;
+    mb_alpha[(size_t)f * nmb + mb] = (uint8_t)a;
+    mb_uva[(size_t)f * nmb + mb] = (uint16_t)best_uv;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K3: RD search + tokens + statistics, one wavefront per frame.
+
+struct K3Lds {
+  uint32_t stats[NSLOT];
+  uint32_t delta[NSLOT];
+  uint16_t lcost[96][MAX_VLEVEL + 1];  // [type*24 + band*3 + ctx][level]
+  uint8_t coeffs[NSLOT];
+  uint32_t mark[33];
+  vp8g_seg seg[4];
+  uint8_t yin[16 * BPS];
+  uint8_t yout[16 * BPS];
+  uint8_t p16[4][256];
+  uint8_t puv[4][128];
+  uint8_t rec16[4][256];
+  uint8_t recuv[4][128];
+  int16_t lv16[4][16][16];
+  int16_t lvdc[4][16];
+  int16_t whtq[4][16];
+  int16_t dcs[4][16];
+  int16_t lvuv[4][8][16];
+  int16_t uvdc[4][8];
+  int8_t uvderr[4][2][3];
+  int16_t fin_dc[16];
+  int16_t fin_ac[16][16];
+  int16_t fin_uv[8][16];
+  uint8_t modes[16];
+  uint8_t canvas[17][24];
+  uint8_t edges[16];
+  uint8_t pred4[10][16];
+  int16_t lv4[10][16];
+  uint8_t rec4[10][16];
+  int32_t r4[10][8];
+  int16_t acc_ac[16][16];
+  uint8_t acc_out[256];          // I4 reconstruction, stride 16
+  int32_t mres[4][4];
+  int32_t blkinfo[32];            // per token block: type | first<<4 | ctx<<8
+  int32_t max_edge[4];
+  uint8_t yl_mem[17], ul_mem[9], vl_mem[9];
+  uint8_t predleft[4];
+  int8_t lderr[2][2];
+};
+
+// per-MB non-zero context (iterator_enc.c:234-265) as bit masks:
+// bit i of t = top_nz[i], bit i of l = left_nz[i]
+struct MBCtx {
+  uint32_t t, l;
+  __device__ __forceinline__ int top(int i) const { return (t >> i) & 1; }
+  __device__ __forceinline__ int left(int i) const { return (l >> i) & 1; }
+};
+
+__device__ __forceinline__ int level_cost(const uint16_t* tab, int v) {
+  return kVP8LevelFixedCost[v] + tab[v > MAX_VLEVEL ? MAX_VLEVEL : v];
+}
+
+// GetResidualCost_C (src/dsp/cost.c:322-355); lv in zigzag order.
+__device__ __forceinline__ int residual_cost(const K3Lds& L, int ctx0, int type, int first,
+                                             const int16_t* lv) {
+  int last = -1;
+  for (int n = 15; n >= first; --n)
+    if (lv[n]) { last = n; break; }
+  const int p0 = L.coeffs[((type * 8 + first) * 3 + ctx0) * 11];
+  if (last < 0) return bit_cost(0, p0);
+  int cost = ctx0 == 0 ? bit_cost(1, p0) : 0;
+  const uint16_t* t = L.lcost[type * 24 + dBand[first] * 3 + ctx0];
+  int n = first;
+  for (; n < last; ++n) {
+    const int v = iabs_(lv[n]);
+    cost += level_cost(t, v);
+    t = L.lcost[type * 24 + dBand[n + 1] * 3 + (v >= 2 ? 2 : v)];
+  }
+  const int v = iabs_(lv[n]);
+  cost += level_cost(t, v);
+  if (n < 15) cost += bit_cost(0, L.coeffs[((type * 8 + dBand[n + 1]) * 3 + (v == 1 ? 1 : 2)) * 11]);
+  return cost;
+}
+
+// FinalizeTokenProbas (frame_enc.c:146-180): returns "changed" (dirty)
+__device__ int finalize_probas(K3Lds& L, int lane) {
+  int changed = 0;
+  for (int s = lane; s < NSLOT; s += 64) {
+    const uint32_t st = L.stats[s];
+    const int nb = st & 0xffff, total = (st >> 16) & 0xffff;
+    const int upd = (&kVP8CoeffUpdateProba[0][0][0][0])[s];
+    const int old_p = (&kVP8CoeffProba0[0][0][0][0])[s];
+    const int new_p = nb ? (255 - nb * 255 / total) : 255;
+    const int old_cost = nb * bit_cost(1, old_p) + (total - nb) * bit_cost(0, old_p) + bit_cost(0, upd);
+    const int new_cost =
+        nb * bit_cost(1, new_p) + (total - nb) * bit_cost(0, new_p) + bit_cost(1, upd) + 8 * 256;
+    if (old_cost > new_cost) {
+      L.coeffs[s] = new_p;
+      changed |= (new_p != old_p);
+    } else {
+      L.coeffs[s] = old_p;
+    }
+  }
+  __syncthreads();
+  return __any(changed);
+}
+
+// VP8CalculateLevelCosts (cost_enc.c:42-90)
+__device__ void level_costs(K3Lds& L, int lane) {
+  for (int k = lane; k < 96 * (MAX_VLEVEL + 1); k += 64) {
+    const int tbc = k / (MAX_VLEVEL + 1), v = k % (MAX_VLEVEL + 1);
+    const uint8_t* p = L.coeffs + tbc * 11;
+    const int ctx = tbc % 3;
+    const int c0 = ctx > 0 ? bit_cost(1, p[0]) : 0;
+    int cost;
+    if (v == 0) {
+      cost = bit_cost(0, p[1]) + c0;
+    } else {
+      cost = bit_cost(1, p[1]) + c0;
+      int pat = kVP8LevelCodes[v - 1][0], bits = kVP8LevelCodes[v - 1][1];
+      for (int i = 2; pat; ++i, pat >>= 1, bits >>= 1)
+        if (pat & 1) cost += bit_cost(bits & 1, p[i]);
+    }
+    L.lcost[tbc][v] = (uint16_t)cost;
+  }
+  __syncthreads();
+}
+
+// VP8RecordStats (cost_enc.h:45-56)
+__device__ __forceinline__ void record_stat(uint32_t* s, int bit) {
+  uint32_t p = *s;
+  if (p >= 0xfffe0000u) p = ((p + 1u) >> 1) & 0x7fff7fffu;
+  *s = p + 0x00010000u + bit;
+}
+
+// Token generation for one block (token_enc.c:113-193). mode 0: count only;
+// 1: write tokens + accumulate LDS stat deltas; 2: replay stats for marked
+// slots (exact saturation order).
+template <int MODE>
+__device__ int gen_tokens(K3Lds& L, const int16_t* lv, int type, int first, int ctx,
+                          uint16_t* out, int* nz_out) {
+  int last = -1;
+  for (int n = 15; n >= first; --n)
+    if (lv[n]) { last = n; break; }
+  int count = 0;
+  auto dyn = [&](int bit, int pid, int sid) -> int {
+    if (MODE == 1) {
+      out[count] = (uint16_t)((bit << 15) | pid);
+      atomicAdd(&L.delta[sid], 0x10000u + bit);
+    } else if (MODE == 2) {
+      if (L.mark[sid >> 5] & (1u << (sid & 31))) record_stat(&L.stats[sid], bit);
+    }
+    ++count;
+    return bit;
+  };
+  auto fix = [&](int bit, int proba) {
+    if (MODE == 1) out[count] = (uint16_t)((bit << 15) | (1 << 14) | proba);
+    ++count;
+  };
+  int n = first;
+  int base = 11 * (ctx + 3 * (dBand[n] + 8 * type));
+  *nz_out = last >= 0;
+  if (!dyn(last >= 0, base + 0, base + 0)) return count;
+  while (n < 16) {
+    const int c = lv[n++];
+    const int neg = c < 0;
+    const uint32_t v = neg ? -c : c;
+    if (!dyn(v != 0, base + 1, base + 1)) {
+      base = 11 * (0 + 3 * (dBand[n] + 8 * type));
+      continue;
+    }
+    if (!dyn(v > 1, base + 2, base + 2)) {
+      base = 11 * (1 + 3 * (dBand[n] + 8 * type));
+    } else {
+      if (!dyn(v > 4, base + 3, base + 3)) {
+        if (dyn(v != 2, base + 4, base + 4)) dyn(v == 4, base + 5, base + 5);
+      } else if (!dyn(v > 10, base + 6, base + 6)) {
+        if (!dyn(v > 6, base + 7, base + 7)) {
+          fix(v == 6, 159);
+        } else {
+          fix(v >= 9, 165);
+          fix(!(v & 1), 145);
+        }
+      } else {
+        const uint8_t* tab;
+        int mask;
+        uint32_t res = v - 3;
+        if (res < (8 << 1)) {
+          dyn(0, base + 8, base + 8); dyn(0, base + 9, base + 9);
+          res -= 8 << 0; mask = 1 << 2; tab = kVP8Cat3;
+        } else if (res < (8 << 2)) {
+          dyn(0, base + 8, base + 8); dyn(1, base + 9, base + 9);
+          res -= 8 << 1; mask = 1 << 3; tab = kVP8Cat4;
+        } else if (res < (8 << 3)) {
+          dyn(1, base + 8, base + 8); dyn(0, base + 10, base + 9);  // token_enc.c:168
+          res -= 8 << 2; mask = 1 << 4; tab = kVP8Cat5;
+        } else {
+          dyn(1, base + 8, base + 8); dyn(1, base + 10, base + 9);
+          res -= 8 << 3; mask = 1 << 10; tab = kVP8Cat6;
+        }
+        for (; mask; mask >>= 1) fix((res & mask) != 0, *tab++);
+      }
+      base = 11 * (2 + 3 * (dBand[n] + 8 * type));
+    }
+    fix(neg, 128);
+    if (n == 16 || !dyn(n <= last, base + 0, base + 0)) return count;
+  }
+  return count;
+}
+
+__device__ __forceinline__ void nz_flags(uint32_t t, uint32_t l, int left_dc, MBCtx& c) {
+  c.t = ((t >> 12) & 0xf) | (((t >> 18) & 3) << 4) | (((t >> 22) & 3) << 6) | (((t >> 24) & 1) << 8);
+  c.l = ((l >> 3) & 1) | (((l >> 7) & 1) << 1) | (((l >> 11) & 1) << 2) | (((l >> 15) & 1) << 3) |
+        (((l >> 17) & 1) << 4) | (((l >> 19) & 1) << 5) | (((l >> 21) & 1) << 6) |
+        (((l >> 23) & 1) << 7) | ((uint32_t)left_dc << 8);
+}
+
+// Block list of an MB for token order (frame_enc.c:411-453):
+// idx 0 = I16 DC (only if i16), 1..16 = Y raster, 17..20 = U, 21..24 = V.
+__device__ __forceinline__ const int16_t* blk_levels(const K3Lds& L, int k) {
+  return k == 0 ? L.fin_dc : (k <= 16 ? L.fin_ac[k - 1] : L.fin_uv[k - 17]);
+}
+
+struct K3Args {
+  const uint8_t* yuv;
+  size_t yfb;
+  int w, h, mbw, mbh;
+  const uint8_t* segmap;
+  const vp8g_frame_params* params;
+  uint16_t* tokens;
+  size_t tok_cap;
+  uint8_t* mbinfo;
+  vp8g_frame_result* results;
+};
+
+__global__ __launch_bounds__(64) void k_encode(K3Args a) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  K3Lds& L = *reinterpret_cast<K3Lds*>(smem);
+  const int mbw = a.mbw, mbh = a.mbh, nmb = mbw * mbh;
+  uint8_t* ytop = smem + sizeof(K3Lds);          // 16*mbw + 4
+  uint8_t* uvtop = ytop + 16 * mbw + 16;         // 16*mbw
+  uint32_t* nzw = reinterpret_cast<uint32_t*>(uvtop + 16 * mbw) + 1;   // [-1..mbw-1]
+  uint8_t* predtop = reinterpret_cast<uint8_t*>(nzw + mbw);           // 4*mbw
+  int8_t* topderr = reinterpret_cast<int8_t*>(predtop + 4 * mbw);     // 4*mbw
+
+  const int f = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int w = a.w, h = a.h;
+  const int uvw = (w + 1) >> 1, uvh = (h + 1) >> 1;
+  const uint8_t* Yp = a.yuv + f * a.yfb;
+  const uint8_t* Up = Yp + (size_t)w * h;
+  const uint8_t* Vp = Up + (size_t)uvw * uvh;
+  const vp8g_frame_params* P = a.params + f;
+  const uint8_t* segmap = a.segmap + (size_t)f * nmb;
+  uint16_t* tok_base = a.tokens + f * a.tok_cap;
+  uint8_t* mbinfo = a.mbinfo + (size_t)f * nmb * VP8G_MBINFO_BYTES;
+
+  // ---- frame init
+  for (int s = lane; s < NSLOT; s += 64) {
+    L.stats[s] = 0;
+    L.delta[s] = 0;
+    L.coeffs[s] = (&kVP8CoeffProba0[0][0][0][0])[s];
+  }
+  for (int k = lane; k < 33; k += 64) L.mark[k] = 0;
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(P->seg);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(L.seg);
+    for (int k = lane; k < (int)(sizeof(L.seg) / 4); k += 64) dst[k] = src[k];
+  }
+  for (int k = lane; k < 16 * mbw + 16; k += 64) ytop[k] = 127;
+  for (int k = lane; k < 16 * mbw; k += 64) uvtop[k] = 127;
+  for (int k = lane - 1; k < mbw; k += 64) nzw[k] = 0;
+  for (int k = lane; k < 4 * mbw; k += 64) { predtop[k] = 0; topderr[k] = 0; }
+  __syncthreads();
+  level_costs(L, lane);
+
+  const int rd_opt = P->rd_opt;
+  const int max_i4_bits = P->max_i4_header_bits;
+  const int use_derr = P->use_derr;
+  const int max_count = P->max_count;
+  int cnt = max_count;
+  if (lane < 4) L.max_edge[lane] = 0;
+  uint64_t size_p0 = 0, sse_acc[3] = {0, 0, 0};
+  int nb_i4 = 0, nb_i16 = 0, nb_skip = 0;
+  uint32_t ntok = 0;
+  int tok_err = 0;
+  int left_dc = 0;
+  uint8_t* yl = L.yl_mem + 1;
+  uint8_t* ul = L.ul_mem + 1;
+  uint8_t* vl = L.vl_mem + 1;
+
+  for (int mb = 0; mb < nmb; ++mb) {
+    const int x = mb % mbw, y = mb / mbw;
+    if (x == 0) {   // InitLeft (iterator_enc.c:22-32)
+      if (lane < 16) yl[lane] = 129;
+      if (lane < 8) { ul[lane] = 129; vl[lane] = 129; }
+      if (lane == 0) {
+        yl[-1] = ul[-1] = vl[-1] = (y > 0) ? 129 : 127;
+        L.lderr[0][0] = L.lderr[0][1] = L.lderr[1][0] = L.lderr[1][1] = 0;
+      }
+      if (lane < 4) L.predleft[lane] = 0;
+      left_dc = 0;
+    }
+    load_mb(Yp, Up, Vp, w, h, x, y, L.yin, lane, 64);
+    if (--cnt < 0) {
+      if (finalize_probas(L, lane)) level_costs(L, lane);
+      cnt = max_count;
+    }
+    __syncthreads();
+    const int segid = segmap[mb];
+    const vp8g_seg& S = L.seg[segid];
+    const bool hl = x > 0, ht = y > 0;
+    const uint8_t* yt = ytop + 16 * x;
+    const uint8_t* uvt = uvtop + 16 * x;
+    MBCtx ctx;
+    nz_flags(nzw[x], nzw[x - 1], left_dc, ctx);
+
+    // ---- predictions (quant_enc.c:469-479)
+    {
+      const int dcy = dc_value(yl, yt, hl, ht, 16, 5);
+      for (int k = lane; k < 1024; k += 64) {
+        const int m = k >> 8, p = k & 255;
+        L.p16[m][p] = pred_sample(m, 16, p & 15, p >> 4, yl, yt, hl, ht, dcy);
+      }
+      const int dcu = dc_value(ul, uvt, hl, ht, 8, 4);
+      const int dcv = dc_value(vl, uvt + 8, hl, ht, 8, 4);
+      for (int k = lane; k < 512; k += 64) {
+        const int m = k >> 7, p = k & 127, px = p & 15, py = p >> 4, c = px >> 3;
+        L.puv[m][p] = pred_sample(m, 8, px & 7, py, c ? vl : ul, uvt + 8 * c, hl, ht, c ? dcv : dcu);
+      }
+    }
+    __syncthreads();
+
+    // ---- Intra16 (quant_enc.c:772-822, 1002-1058)
+    score_t best16_score;
+    int best16;
+    uint32_t nz16;
+    score_t D16, SD16, H16, R16;
+    {
+      const int m = lane >> 4, b = lane & 15, bx = b & 3, by = b >> 2;
+      int c[16];
+      const uint8_t* src = L.yin + by * 4 * BPS + bx * 4;
+      const uint8_t* ref = L.p16[m] + by * 64 + bx * 4;
+      fdct4(src, BPS, ref, 16, c);
+      L.dcs[m][b] = (int16_t)c[0];
+      __syncthreads();
+      {   // WHT coefficient b of mode m, quantised with y2 (natural index b)
+        const int16_t* d = L.dcs[m];
+        const int r = b >> 2, col = b & 3;
+        int t0[4];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int a0 = d[4 * rr + 0] + d[4 * rr + 2], a1 = d[4 * rr + 1] + d[4 * rr + 3];
+          const int a2 = d[4 * rr + 1] - d[4 * rr + 3], a3 = d[4 * rr + 0] - d[4 * rr + 2];
+          t0[rr] = col == 0 ? a0 + a1 : col == 1 ? a3 + a2 : col == 2 ? a3 - a2 : a0 - a1;
+        }
+        const int a0 = t0[0] + t0[2], a1 = t0[1] + t0[3], a2 = t0[1] - t0[3], a3 = t0[0] - t0[2];
+        int v = r == 0 ? a0 + a1 : r == 1 ? a3 + a2 : r == 2 ? a3 - a2 : a0 - a1;
+        v = (int16_t)(v >> 1);
+        const vp8g_mtx& M = S.y2;
+        const int neg = v < 0;
+        const uint32_t coeff = (uint32_t)(neg ? -v : v) + M.sharpen[b];
+        int level = 0;
+        if (coeff > M.zthresh[b]) {
+          level = (int)((coeff * M.iq[b] + M.bias[b]) >> QFIX);
+          if (level > MAX_LEVEL) level = MAX_LEVEL;
+          if (neg) level = -level;
+        }
+        L.lvdc[m][dZzInv[b]] = (int16_t)level;
+        L.whtq[m][b] = (int16_t)(level * (int)M.q[b]);
+      }
+      // AC quantisation of own block with DC zeroed (quant_enc.c:805-812)
+      c[0] = 0;
+      const int nzb = quantize_block(c, L.lv16[m][b], &S.y1);
+      __syncthreads();
+      {   // inverse WHT -> DC of block b (dec.c:137-162)
+        const int16_t* q = L.whtq[m];
+        const int r = b >> 2, col = b & 3;
+        int t[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int a0 = q[i] + q[12 + i], a1 = q[4 + i] + q[8 + i];
+          const int a2 = q[4 + i] - q[8 + i], a3 = q[i] - q[12 + i];
+          t[i] = r == 0 ? a0 + a1 : r == 1 ? a3 + a2 : r == 2 ? a0 - a1 : a3 - a2;
+        }
+        // t[i] = tmp[4*r + i]; second pass uses row r of tmp
+        const int dd = t[0] + 3;
+        const int a0 = dd + t[3], a1 = t[1] + t[2], a2 = t[1] - t[2], a3 = dd - t[3];
+        c[0] = (int16_t)((col == 0 ? a0 + a1 : col == 1 ? a3 + a2 : col == 2 ? a0 - a1 : a3 - a2) >> 3);
+      }
+      idct4(ref, 16, c, L.rec16[m] + by * 64 + bx * 4, 16);
+      __syncthreads();
+      const uint8_t* rec = L.rec16[m] + by * 64 + bx * 4;
+      int d = sse4(src, BPS, rec, 16);
+      int td = iabs_(hadamard_w(rec, 16) - hadamard_w(src, BPS)) >> 5;
+      const uint64_t nzmask_all = __ballot(nzb);
+      const uint32_t nzm = (uint32_t)(nzmask_all >> (16 * m)) & 0xffff;
+      const int tctx = by == 0 ? ctx.top(bx) : ((nzm >> (b - 4)) & 1);
+      const int lctx = bx == 0 ? ctx.left(by) : ((nzm >> (b - 1)) & 1);
+      int r = residual_cost(L, tctx + lctx, 0, 1, L.lv16[m][b]);
+      int dcnz = 0;
+      for (int k = 0; k < 16; ++k) dcnz |= L.lvdc[m][k];
+      if (b == 0) r += residual_cost(L, ctx.top(8) + ctx.left(8), 1, 0, L.lvdc[m]);
+      // reduce over the 16 lanes of this mode
+#pragma unroll
+      for (int off = 8; off >= 1; off >>= 1) {
+        d += __shfl_xor(d, off, 16);
+        td += __shfl_xor(td, off, 16);
+        r += __shfl_xor(r, off, 16);
+      }
+      if (b == 0) {
+        L.mres[m][0] = d;
+        L.mres[m][1] = td;
+        L.mres[m][2] = r;
+        L.mres[m][3] = (int)(nzm | (dcnz ? (1u << 24) : 0u));
+      }
+      __syncthreads();
+      // sequential mode choice, identical in every lane
+      int flat = 1;
+      {
+        const int v0 = L.yin[0];
+        int same = 1;
+        for (int k = lane; k < 256; k += 64) same &= (L.yin[(k >> 4) * BPS + (k & 15)] == v0);
+        flat = __all(same);
+      }
+      best16 = 0;
+      best16_score = 0;
+      for (int mm = 0; mm < 4; ++mm) {
+        score_t Dm = L.mres[mm][0];
+        score_t SDm = S.tlambda ? (score_t)((S.tlambda * L.mres[mm][1] + 128) >> 8) : 0;
+        const score_t Hm = kVP8ModeCostI16[mm];
+        const score_t Rm = L.mres[mm][2];
+        if (flat) {
+          flat = (L.mres[mm][3] & 0xffff) == 0;
+          if (flat) { Dm *= 2; SDm *= 2; }
+        }
+        const score_t sc = (Rm + Hm) * S.lambda_i16 + 256 * (Dm + SDm);
+        if (mm == 0 || sc < best16_score) {
+          best16_score = sc; best16 = mm;
+          D16 = Dm; SD16 = SDm; H16 = Hm; R16 = Rm;
+          nz16 = (uint32_t)L.mres[mm][3];
+        }
+      }
+    }
+    // commit I16 as current best
+    for (int k = lane; k < 256; k += 64) L.yout[(k >> 4) * BPS + (k & 15)] = L.rec16[best16][k];
+    for (int k = lane; k < 256; k += 64) (&L.fin_ac[0][0])[k] = (&L.lv16[best16][0][0])[k];
+    if (lane < 16) { L.fin_dc[lane] = L.lvdc[best16][lane]; L.modes[lane] = best16; }
+    score_t rd_score = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
+    score_t rdD = D16, rdSD = SD16, rdH = H16, rdR = R16;
+    uint32_t rd_nz = nz16;
+    int is_i16 = 1;
+    if ((rd_nz & 0x100ffff) == 0x1000000 && D16 > S.min_disto) {
+      int mv = iabs_(L.lvdc[best16][1]);
+      mv = max(mv, iabs_(L.lvdc[best16][2]));
+      mv = max(mv, iabs_(L.lvdc[best16][4]));
+      if (lane == 0 && mv > L.max_edge[segid]) L.max_edge[segid] = mv;
+    }
+    __syncthreads();
+
+    // ---- Intra4 (quant_enc.c:1072-1165)
+    if (max_i4_bits > 0) {
+      // canvas: row 0 = corner + top + top-right, col 0 = left
+      for (int k = lane; k < 21; k += 64) {
+        uint8_t v;
+        if (k == 0) v = yl[-1];
+        else if (k <= 16) v = yt[k - 1];
+        else v = (x < mbw - 1) ? yt[16 + k - 17] : yt[15];
+        L.canvas[0][k] = v;
+      }
+      if (lane < 16) L.canvas[1 + lane][0] = yl[lane];
+      uint32_t tnz = ctx.t & 0xf, lnz = ctx.l & 0xf;
+      score_t accD = 0, accSD = 0, accR = 0, accH = 211, acc_score;
+      uint32_t acc_nz = 0;
+      acc_score = accH * S.lambda_mode;
+      int total_hdr = 0;
+      int ok4 = 1;
+      __syncthreads();
+      for (int i4 = 0; i4 < 16 && ok4; ++i4) {
+        const int bx = i4 & 3, by = i4 >> 2;
+        const int left_m = bx == 0 ? L.predleft[by] : L.modes[i4 - 1];
+        const int top_m = by == 0 ? predtop[4 * x + bx] : L.modes[i4 - 4];
+        // edges e[0..12] = L K J I X A..D E..H
+        if (lane < 13) {
+          const int r = 4 * by, cc = 4 * bx;
+          uint8_t v;
+          if (lane < 4) v = L.canvas[r + 4 - lane][cc];
+          else if (lane == 4) v = L.canvas[r][cc];
+          else if (lane < 9) v = L.canvas[r][cc + 1 + (lane - 5)];
+          else v = (by > 0 && bx == 3) ? L.canvas[0][17 + lane - 9] : L.canvas[r][cc + 5 + lane - 9];
+          L.edges[lane] = v;
+        }
+        __syncthreads();
+        for (int k = lane; k < 160; k += 64) {
+          const int m = k >> 4, p = k & 15;
+          const P4Op op = kP4[m][p];
+          const uint8_t* e = L.edges;
+          int v;
+          if (op.kind == 0) v = (e[op.a] + 2 * e[op.b] + e[op.c] + 2) >> 2;
+          else if (op.kind == 1) v = (e[op.a] + e[op.b] + 1) >> 1;
+          else if (op.kind == 2) v = e[op.a];
+          else if (op.kind == 3) v = clip8(e[5 + (p & 3)] + e[3 - (p >> 2)] - e[4]);
+          else v = (4 + e[0] + e[1] + e[2] + e[3] + e[5] + e[6] + e[7] + e[8]) >> 3;
+          L.pred4[m][p] = (uint8_t)v;
+        }
+        __syncthreads();
+        if (lane < 10) {
+          const int m = lane;
+          const uint8_t* src = L.yin + by * 4 * BPS + bx * 4;
+          int c[16];
+          fdct4(src, BPS, L.pred4[m], 4, c);
+          const int nz = quantize_block(c, L.lv4[m], &S.y1);
+          idct4(L.pred4[m], 4, c, L.rec4[m], 4);
+          const int D = sse4(src, BPS, L.rec4[m], 4);
+          const int SD = S.tlambda ? (S.tlambda * (iabs_(hadamard_w(L.rec4[m], 4) -
+                                                          hadamard_w(src, BPS)) >> 5) + 128) >> 8
+                                   : 0;
+          int cntnz = 0;
+          for (int i = 1; i < 16; ++i) cntnz += L.lv4[m][i] != 0;
+          const int R0 = (m > 0 && cntnz <= 3) ? 140 : 0;
+          const int Rc = residual_cost(L, ((tnz >> bx) & 1) + ((lnz >> by) & 1), 3, 0, L.lv4[m]);
+          L.r4[m][0] = D; L.r4[m][1] = SD; L.r4[m][2] = kVP8ModeCostI4[top_m][left_m][m];
+          L.r4[m][3] = R0; L.r4[m][4] = Rc; L.r4[m][5] = nz;
+        }
+        __syncthreads();
+        int bm = -1;
+        score_t bscore = MAX_COST, bD = 0, bSD = 0, bR = 0, bH = 0;
+        int bnz = 0;
+        for (int m = 0; m < 10; ++m) {
+          const score_t D = L.r4[m][0], SD = L.r4[m][1], H = L.r4[m][2];
+          score_t R = L.r4[m][3];
+          score_t sc = (R + H) * S.lambda_i4 + 256 * (D + SD);
+          if (bm >= 0 && sc >= bscore) continue;
+          R += L.r4[m][4];
+          sc = (R + H) * S.lambda_i4 + 256 * (D + SD);
+          if (bm < 0 || sc < bscore) {
+            bm = m; bscore = sc; bD = D; bSD = SD; bR = R; bH = H; bnz = L.r4[m][5];
+          }
+        }
+        const score_t bsm = (bR + bH) * S.lambda_mode + 256 * (bD + bSD);
+        accD += bD; accSD += bSD; accR += bR; accH += bH; acc_score += bsm;
+        acc_nz |= (uint32_t)(bnz ? 1 : 0) << i4;
+        if (acc_score >= rd_score) { ok4 = 0; break; }
+        total_hdr += (int)bH;
+        if (total_hdr > max_i4_bits) { ok4 = 0; break; }
+        if (lane < 16) {
+          const int py = lane >> 2, px = lane & 3;
+          const uint8_t v = L.rec4[bm][lane];
+          L.canvas[4 * by + 1 + py][4 * bx + 1 + px] = v;
+          L.acc_out[(4 * by + py) * 16 + 4 * bx + px] = v;
+          L.acc_ac[i4][lane] = L.lv4[bm][lane];
+        }
+        if (lane == 0) L.modes[i4] = (uint8_t)bm;
+        tnz = (tnz & ~(1u << bx)) | ((bnz ? 1u : 0u) << bx);
+        lnz = (lnz & ~(1u << by)) | ((bnz ? 1u : 0u) << by);
+        __syncthreads();
+      }
+      __syncthreads();
+      if (ok4) {
+        is_i16 = 0;
+        rdD = accD; rdSD = accSD; rdR = accR; rdH = accH; rd_score = acc_score;
+        rd_nz = acc_nz;
+        for (int k = lane; k < 256; k += 64) {
+          L.yout[(k >> 4) * BPS + (k & 15)] = L.acc_out[k];
+          (&L.fin_ac[0][0])[k] = (&L.acc_ac[0][0])[k];
+        }
+      } else {
+        if (lane < 16) L.modes[lane] = best16;   // restore (early exit wrote some)
+      }
+      __syncthreads();
+    }
+
+    // ---- UV (quant_enc.c:875-969, 1169-1217)
+    {
+      int d = 0, r = 0, flatc = 0, nzb = 0;
+      const int m = lane >> 3, b = lane & 7;
+      int c[16];
+      const int ch = b >> 2, k4 = b & 3;
+      const uint8_t* src = L.yin + 16 + 8 * ch + (k4 >> 1) * 4 * BPS + (k4 & 1) * 4;
+      const uint8_t* ref = L.puv[m & 3] + 8 * ch + (k4 >> 1) * 64 + (k4 & 1) * 4;
+      if (lane < 32) {
+        fdct4(src, BPS, ref, 16, c);
+        L.uvdc[m][b] = (int16_t)c[0];
+      }
+      __syncthreads();
+      if (use_derr && lane < 8) {   // CorrectDCValues per (mode, channel)
+        const int mm = lane >> 1, cch = lane & 1;
+        const vp8g_mtx& M = S.uv;
+        const int8_t* top = topderr + 4 * x + 2 * cch;
+        const int8_t* left = L.lderr[cch];
+        int16_t* cc = &L.uvdc[mm][4 * cch];
+        int err[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          int add;
+          if (k == 0) add = (7 * top[0] + 8 * left[0]) >> 3;
+          else if (k == 1) add = (7 * top[1] + 8 * err[0]) >> 3;
+          else if (k == 2) add = (7 * err[0] + 8 * left[1]) >> 3;
+          else add = (7 * err[1] + 8 * err[2]) >> 3;
+          int V = (int16_t)(cc[k] + add);
+          const int neg = V < 0;
+          if (neg) V = -V;
+          if (V > (int)M.zthresh[0]) {
+            const int qV = (int)(((uint32_t)V * M.iq[0] + M.bias[0]) >> QFIX) * M.q[0];
+            const int e = V - qV;
+            cc[k] = (int16_t)(neg ? -qV : qV);
+            err[k] = (neg ? -e : e) >> 1;
+          } else {
+            cc[k] = 0;
+            err[k] = (neg ? -V : V) >> 1;
+          }
+        }
+        L.uvderr[mm][cch][0] = (int8_t)err[1];
+        L.uvderr[mm][cch][1] = (int8_t)err[2];
+        L.uvderr[mm][cch][2] = (int8_t)err[3];
+      }
+      __syncthreads();
+      if (lane < 32) {
+        c[0] = L.uvdc[m][b];
+        nzb = quantize_block(c, L.lvuv[m][b], &S.uv);
+        idct4(ref, 16, c, L.recuv[m] + 8 * ch + (k4 >> 1) * 64 + (k4 & 1) * 4, 16);
+      }
+      __syncthreads();
+      const uint64_t nzall = __ballot(lane < 32 && nzb);
+      if (lane < 32) {
+        const uint8_t* rec = L.recuv[m] + 8 * ch + (k4 >> 1) * 64 + (k4 & 1) * 4;
+        d = sse4(src, BPS, rec, 16);
+        const uint32_t nzm = (uint32_t)(nzall >> (8 * m)) & 0xff;
+        const int bxx = k4 & 1, byy = k4 >> 1;
+        const int tctx = byy == 0 ? ctx.top(4 + 2 * ch + bxx) : ((nzm >> (b - 2)) & 1);
+        const int lctx = bxx == 0 ? ctx.left(4 + 2 * ch + byy) : ((nzm >> (b - 1)) & 1);
+        r = residual_cost(L, tctx + lctx, 2, 0, L.lvuv[m][b]);
+        for (int i = 1; i < 16; ++i) flatc += L.lvuv[m][b][i] != 0;
+#pragma unroll
+        for (int off = 4; off >= 1; off >>= 1) {
+          d += __shfl_xor(d, off, 8);
+          r += __shfl_xor(r, off, 8);
+          flatc += __shfl_xor(flatc, off, 8);
+        }
+        if (b == 0) {
+          L.mres[m][0] = d; L.mres[m][1] = r; L.mres[m][2] = flatc; L.mres[m][3] = (int)nzm;
+        }
+      }
+      __syncthreads();
+      int bu = 0;
+      score_t bsc = 0, bD = 0, bR = 0, bH = 0;
+      for (int mm = 0; mm < 4; ++mm) {
+        const score_t Dm = L.mres[mm][0], Hm = kVP8ModeCostUV[mm];
+        score_t Rm = L.mres[mm][1];
+        if (mm > 0 && L.mres[mm][2] <= 2) Rm += 140 * 8;
+        const score_t sc = (Rm + Hm) * S.lambda_uv + 256 * Dm;
+        if (mm == 0 || sc < bsc) { bsc = sc; bu = mm; bD = Dm; bR = Rm; bH = Hm; }
+      }
+      rdD += bD; rdR += bR; rdH += bH; rd_score += bsc;
+      rd_nz |= (uint32_t)L.mres[bu][3] << 16;
+      for (int k = lane; k < 128; k += 64) {
+        L.yout[(k >> 4) * BPS + 16 + (k & 15)] = L.recuv[bu][k];
+        (&L.fin_uv[0][0])[k] = (&L.lvuv[bu][0][0])[k];
+      }
+      if (use_derr && lane < 2) {   // StoreDiffusionErrors (quant_enc.c:909-920)
+        const int cch = lane;
+        int8_t* top = topderr + 4 * x + 2 * cch;
+        int8_t* left = L.lderr[cch];
+        const int8_t* e = L.uvderr[bu][cch];
+        left[0] = e[0];
+        left[1] = (int8_t)(3 * e[2] >> 2);
+        top[0] = e[1];
+        top[1] = (int8_t)(e[2] - left[1]);
+      }
+      __syncthreads();
+      // ---- per-MB info + stats side info
+      const int skip = rd_nz == 0;
+      if (lane == 0) {
+        uint8_t* info = mbinfo + (size_t)mb * VP8G_MBINFO_BYTES;
+        info[0] = is_i16; info[1] = bu; info[2] = segid; info[3] = skip;
+        if (is_i16) ++nb_i16; else ++nb_i4;
+        if (skip) ++nb_skip;
+        size_p0 += rdH;
+      }
+      if (lane < 16) mbinfo[(size_t)mb * VP8G_MBINFO_BYTES + 4 + lane] = L.modes[lane];
+      (void)rdD; (void)rdSD; (void)rdR; (void)rd_score;
+    }
+    // SSE for WebPAuxStats (frame_enc.c:480-489)
+    {
+      int sy = 0, su = 0, sv = 0;
+      for (int k = lane; k < 256; k += 64) {
+        const int o = (k >> 4) * BPS + (k & 15);
+        const int dd = L.yin[o] - L.yout[o];
+        sy += dd * dd;
+      }
+      {
+        const int o = (lane >> 3) * BPS + 16 + (lane & 7);
+        const int du = L.yin[o] - L.yout[o], dv = L.yin[o + 8] - L.yout[o + 8];
+        su = du * du; sv = dv * dv;
+      }
+      for (int off = 32; off >= 1; off >>= 1) {
+        sy += __shfl_xor(sy, off);
+        su += __shfl_xor(su, off);
+        sv += __shfl_xor(sv, off);
+      }
+      sse_acc[0] += sy; sse_acc[1] += su; sse_acc[2] += sv;
+    }
+
+    // ---- tokens + exact statistics (frame_enc.c:411-453, token_enc.c:113-193)
+    {
+      // per-block nz flags from final levels -> contexts
+      const int first_blk = is_i16 ? 0 : 1;
+      int my_ctx = 0, my_type = 0, my_first = 0;
+      const int k = lane;                    // block index 0..24
+      const bool active = k >= first_blk && k < 25;
+      int nzk = 0;
+      if (active) {
+        const int16_t* lv = blk_levels(L, k);
+        for (int i = 0; i < 16; ++i) nzk |= lv[i];
+      }
+      const uint64_t nzb = __ballot(active && nzk != 0);
+      if (active) {
+        if (k == 0) {
+          my_type = 1; my_first = 0; my_ctx = ctx.top(8) + ctx.left(8);
+        } else if (k <= 16) {
+          const int b = k - 1, bx = b & 3, by = b >> 2;
+          my_type = is_i16 ? 0 : 3; my_first = is_i16 ? 1 : 0;
+          const int t = by == 0 ? ctx.top(bx) : (int)((nzb >> (k - 4)) & 1);
+          const int l = bx == 0 ? ctx.left(by) : (int)((nzb >> (k - 1)) & 1);
+          my_ctx = t + l;
+        } else {
+          const int b = k - 17, ch = b >> 2, k4 = b & 3, bx = k4 & 1, by = k4 >> 1;
+          my_type = 2; my_first = 0;
+          const int t = by == 0 ? ctx.top(4 + 2 * ch + bx) : (int)((nzb >> (k - 2)) & 1);
+          const int l = bx == 0 ? ctx.left(4 + 2 * ch + by) : (int)((nzb >> (k - 1)) & 1);
+          my_ctx = t + l;
+        }
+      }
+      if (active) L.blkinfo[k] = my_type | (my_first << 4) | (my_ctx << 8);
+      int nzdummy;
+      const int mycount = active ? gen_tokens<0>(L, blk_levels(L, k), my_type, my_first, my_ctx,
+                                                 nullptr, &nzdummy)
+                                 : 0;
+      // exclusive prefix sum over lanes
+      int incl = mycount;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(incl, off);
+        if (lane >= off) incl += v;
+      }
+      const int total = __shfl(incl, 63);
+      const int excl = incl - mycount;
+      if (ntok + (uint32_t)total > a.tok_cap) tok_err = 1;
+      if (!tok_err && active)
+        gen_tokens<1>(L, blk_levels(L, k), my_type, my_first, my_ctx, tok_base + ntok + excl,
+                      &nzdummy);
+      if (!tok_err) ntok += total;
+      __syncthreads();
+      // fold deltas into the statistics; slots that cross the halving
+      // threshold inside this MB are replayed in token order.
+      int any_mark = 0;
+      for (int s = lane; s < NSLOT; s += 64) {
+        const uint32_t dlt = L.delta[s];
+        if (dlt) {
+          const uint32_t p = L.stats[s];
+          if ((p >> 16) + (dlt >> 16) < 0xffffu) {
+            L.stats[s] = p + dlt;
+          } else {
+            atomicOr(&L.mark[s >> 5], 1u << (s & 31));
+            any_mark = 1;
+          }
+          L.delta[s] = 0;
+        }
+      }
+      __syncthreads();
+      if (__any(any_mark)) {
+        if (lane == 0) {
+          for (int kk = first_blk; kk < 25; ++kk) {
+            const int bi = L.blkinfo[kk];
+            gen_tokens<2>(L, blk_levels(L, kk), bi & 15, (bi >> 4) & 15, bi >> 8, nullptr,
+                          &nzdummy);
+          }
+        }
+        __syncthreads();
+        for (int kk = lane; kk < 33; kk += 64) L.mark[kk] = 0;
+        __syncthreads();
+      }
+      // update nz context (iterator_enc.c:267-283) and the left DC flag
+      {
+        int tn[9], ln[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) { tn[i] = ctx.top(i); ln[i] = ctx.left(i); }
+        if (is_i16) { tn[8] = ln[8] = (int)(nzb & 1); }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          tn[i] = (int)((nzb >> (1 + 12 + i)) & 1);      // block (i, 3)
+          ln[i] = (int)((nzb >> (1 + 4 * i + 3)) & 1);   // block (3, i)
+        }
+#pragma unroll
+        for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            tn[4 + 2 * ch + i] = (int)((nzb >> (17 + 4 * ch + 2 + i)) & 1);
+            ln[4 + 2 * ch + i] = (int)((nzb >> (17 + 4 * ch + 2 * i + 1)) & 1);
+          }
+        uint32_t word = 0;
+        word |= (tn[0] << 12) | (tn[1] << 13) | (tn[2] << 14) | (tn[3] << 15) |
+                (tn[4] << 18) | (tn[5] << 19) | (tn[6] << 22) | (tn[7] << 23) | (tn[8] << 24);
+        word |= (ln[0] << 3) | (ln[1] << 7) | (ln[2] << 11) | (ln[4] << 17) | (ln[6] << 21);
+        left_dc = ln[8];
+        __syncthreads();
+        if (lane == 0) nzw[x] = word;
+      }
+    }
+
+    // ---- boundary save (iterator_enc.c:290-313) + mode context
+    __syncthreads();
+    if (x < mbw - 1) {
+      if (lane < 16) yl[lane] = L.yout[15 + lane * BPS];
+      if (lane < 8) { ul[lane] = L.yout[16 + 7 + lane * BPS]; vl[lane] = L.yout[24 + 7 + lane * BPS]; }
+      if (lane == 0) { yl[-1] = yt[15]; ul[-1] = uvt[7]; vl[-1] = uvt[15]; }
+    }
+    __syncthreads();
+    if (y < mbh - 1) {
+      if (lane < 16) {
+        ytop[16 * x + lane] = L.yout[15 * BPS + lane];
+        uvtop[16 * x + lane] = L.yout[7 * BPS + 16 + lane];
+      }
+    }
+    if (lane < 4) {
+      predtop[4 * x + lane] = L.modes[12 + lane];
+      L.predleft[lane] = L.modes[4 * lane + 3];
+    }
+    __syncthreads();
+  }
+
+  // ---- frame epilogue: final probabilities and side results
+  finalize_probas(L, lane);
+  vp8g_frame_result* R = a.results + f;
+  for (int s = lane; s < NSLOT; s += 64) R->probas[s] = L.coeffs[s];
+  if (lane == 0) {
+    R->ntokens = ntok;
+    R->error = tok_err;
+    for (int s = 0; s < 4; ++s) R->max_edge[s] = L.max_edge[s];
+    R->size_p0 = size_p0;
+    R->sse[0] = sse_acc[0]; R->sse[1] = sse_acc[1]; R->sse[2] = sse_acc[2];
+    R->block_count[0] = nb_i4; R->block_count[1] = nb_i16; R->block_count[2] = nb_skip;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// syn-v1 generator for benchmarks: counter-based, so any
+// frame is produced directly in HBM.
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void k_synth(uint8_t* rgba, size_t fstride, int w, int h, int f0, int seed) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  const int f = f0 + blockIdx.z;
+  if (x >= w) return;
+  const uint64_t hh = splitmix64(((uint64_t)seed << 48) ^ ((uint64_t)f << 32) ^
+                                 ((uint64_t)y << 16) ^ (uint64_t)x);
+  const int region = ((x >> 5) ^ (y >> 5) ^ f) & 3;
+  const int n = (int)(hh & 31) - 16;
+  const int gx = w > 1 ? x * 255 / (w - 1) : 0, gy = h > 1 ? y * 255 / (h - 1) : 0;
+  int r, g, b;
+  if (region == 0) { r = g = b = (f * 37 + 64) & 255; }
+  else if (region == 1) { r = gx + n; g = gy + n; b = (x ^ y) & 255; }
+  else if (region == 2) { r = (hh >> 8) & 255; g = (hh >> 16) & 255; b = (hh >> 24) & 255; }
+  else { r = g = b = (((x + y + f) >> 2) & 1) ? 235 : 20; }
+  uint8_t* p = rgba + blockIdx.z * fstride + ((size_t)y * w + x) * 4;
+  p[0] = min(max(r, 0), 255); p[1] = min(max(g, 0), 255); p[2] = min(max(b, 0), 255); p[3] = 255;
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+
+static size_t k3_lds_bytes(int mbw) {
+  return sizeof(K3Lds) + (16 * mbw + 16) + 16 * mbw + 4 * (mbw + 1) + 4 * mbw + 4 * mbw + 16;
+}
+
+static int g_sync_mode = -1;
+static int launch_check(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) {
+    if (g_sync_mode < 0) {
+      const char* v = getenv("WEBP_AMD_SYNC");
+      g_sync_mode = (v && v[0] == '1') ? 1 : 0;
+    }
+    if (g_sync_mode) e = hipDeviceSynchronize();
+  }
+  if (e != hipSuccess) {
+    vp8g_set_error(what, hipGetErrorString(e));
+    return 0;
+  }
+  return 1;
+}
+
+extern "C" {
+
+int vp8g_launch_import(const uint8_t* rgba, size_t fstride, int rstride, int w, int h, int n,
+                       uint8_t* yuv, size_t yfb, uint32_t* aflags, const uint16_t g2l[256],
+                       const int32_t l2g[33], void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int uvw = (w + 1) >> 1, uvh = (h + 1) >> 1;
+  dim3 grid((uvw + 255) / 256, uvh, n);
+  hipLaunchKernelGGL(k_import, grid, dim3(256), 0, st, rgba, fstride, rstride, w, h, yuv, yfb,
+                     aflags, g2l, l2g);
+  return launch_check("k_import");
+}
+
+int vp8g_launch_analysis(const uint8_t* yuv, size_t yfb, int w, int h, int n, uint8_t* mb_alpha,
+                         uint16_t* mb_uva, void* stream) {
+  const int nmb = ((w + 15) >> 4) * ((h + 15) >> 4);
+  dim3 grid((nmb + 3) / 4, n);
+  hipLaunchKernelGGL(k_analyze, grid, dim3(256), 0, (hipStream_t)stream, yuv, yfb, w, h, nmb,
+                     mb_alpha, mb_uva);
+  return launch_check("k_analyze");
+}
+
+int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, int n,
+                       const uint8_t* segmap, const vp8g_frame_params* params, uint16_t* tokens,
+                       size_t tok_cap, uint8_t* mbinfo, vp8g_frame_result* results,
+                       void* stream) {
+  K3Args a;
+  a.yuv = yuv; a.yfb = yfb; a.w = w; a.h = h;
+  a.mbw = (w + 15) >> 4; a.mbh = (h + 15) >> 4;
+  a.segmap = segmap; a.params = params; a.tokens = tokens; a.tok_cap = tok_cap;
+  a.mbinfo = mbinfo; a.results = results;
+  const size_t lds = k3_lds_bytes(a.mbw);
+  if (lds > 160 * 1024) {
+    vp8g_set_error("k_encode", "frame too wide for the LDS budget");
+    return 0;
+  }
+  static int attr_done = 0;
+  if (!attr_done) {
+    (void)hipFuncSetAttribute((const void*)k_encode, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    attr_done = 1;
+  }
+  hipLaunchKernelGGL(k_encode, dim3(n), dim3(64), lds, (hipStream_t)stream, a);
+  return launch_check("k_encode");
+}
+
+int vp8g_launch_synth(uint8_t* rgba, size_t fstride, int w, int h, int f0, int n, int seed,
+                      void* stream) {
+  dim3 grid((w + 255) / 256, h, n);
+  hipLaunchKernelGGL(k_synth, grid, dim3(256), 0, (hipStream_t)stream, rgba, fstride, w, h, f0,
+                     seed);
+  return launch_check("k_synth");
+}
+
+}  // extern "C"

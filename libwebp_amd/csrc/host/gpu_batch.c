@@ -1,0 +1,397 @@
+/* Batched GPU engine: device buffers, the K1 -> K2 -> host setup -> K3
+ * pipeline, and the host thread pool that runs the boolean-coder tail.
+ * Host C over the HIP runtime C API; kernels live in hip/vp8_kernels.hip. */
+#include <math.h>
+#include <stdio.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "gpu_engine.h"
+#include "vp8_host.h"
+#include "webp/encode_gpu.h"
+
+static double now_us(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
+/* gamma tables for the RGB->YUV import (picture_csp_enc.c:103-117) */
+static uint16_t g_g2l[256];
+static int32_t g_l2g[33];
+static pthread_once_t g_gamma_once = PTHREAD_ONCE_INIT;
+static void gamma_init(void) {
+  const double scale = (double)(1 << 7) / 4095;
+  const double norm = 1. / 255.;
+  for (int v = 0; v < 256; ++v) g_g2l[v] = (uint16_t)(pow(norm * v, 0.80) * 4095 + .5);
+  for (int v = 0; v <= 32; ++v) g_l2g[v] = (int)(255. * pow(scale * v, 1. / 0.80) + .5);
+}
+
+int WebPGpuSynthRGBA(void* rgba, size_t fstride, int w, int h, int first, int n, int seed,
+                     void* stream) {
+  if (!rgba || w <= 0 || h <= 0 || n <= 0 || fstride < (size_t)w * h * 4) return 0;
+  if (!vp8g_launch_synth((uint8_t*)rgba, fstride, w, h, first, n, seed, stream)) return 0;
+  return hipStreamSynchronize((hipStream_t)stream) == hipSuccess;
+}
+
+int WebPGpuDeviceCount(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+static int default_threads(void) {
+  const char* e = getenv("WEBP_AMD_THREADS");
+  if (e && atoi(e) > 0) return atoi(e);
+  long n = sysconf(_SC_NPROCESSORS_ONLN);
+  if (n < 1) n = 1;
+  return n > 16 ? 16 : (int)n;
+}
+
+static __thread char g_last_error[256];
+
+void vp8g_set_error(const char* where, const char* what) {
+  snprintf(g_last_error, sizeof(g_last_error), "%s: %s", where, what);
+}
+
+const char* WebPGpuLastError(void) { return g_last_error; }
+
+#define CHK(x)                                                         \
+  do {                                                                 \
+    const hipError_t e_ = (x);                                         \
+    if (e_ != hipSuccess) {                                            \
+      char loc_[64];                                                   \
+      snprintf(loc_, sizeof(loc_), "gpu_batch.c:%d", __LINE__);        \
+      vp8g_set_error(loc_, hipGetErrorString(e_));                     \
+      goto fail;                                                       \
+    }                                                                  \
+  } while (0)
+
+WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
+                              const WebPConfig* config, int host_threads) {
+  if (!config || width <= 0 || height <= 0 || width > WEBP_MAX_DIMENSION ||
+      height > WEBP_MAX_DIMENSION || max_frames <= 0)
+    return NULL;
+  if (!WebPValidateConfig(config) || config->lossless) return NULL;
+  WebPGpuBatch* b = (WebPGpuBatch*)calloc(1, sizeof(*b));
+  if (!b) return NULL;
+  vp8h_frame probe;
+  if (!vp8h_frame_init(&probe, config, width, height)) { free(b); return NULL; }
+  pthread_once(&g_gamma_once, gamma_init);
+  b->device = device;
+  b->w = width; b->h = height;
+  b->max_frames = max_frames;
+  b->cfg = *config;
+  b->mbw = (width + 15) >> 4; b->mbh = (height + 15) >> 4;
+  b->nmb = b->mbw * b->mbh;
+  b->uvw = (width + 1) >> 1; b->uvh = (height + 1) >> 1;
+  b->yfb = (size_t)width * height + 2 * (size_t)b->uvw * b->uvh;
+  b->yfb = (b->yfb + 255) & ~(size_t)255;
+  b->tok_cap = (size_t)b->nmb * VP8G_MAX_TOKENS_PER_MB;
+  b->threads = host_threads > 0 ? host_threads : default_threads();
+  const size_t N = (size_t)max_frames, nmb = (size_t)b->nmb;
+  CHK(hipSetDevice(device));
+  CHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+  CHK(hipMalloc((void**)&b->d_g2l, 256 * sizeof(uint16_t) + 33 * sizeof(int32_t)));
+  b->d_l2g = (int32_t*)(b->d_g2l + 256);
+  CHK(hipMemcpy(b->d_g2l, g_g2l, 256 * sizeof(uint16_t), hipMemcpyHostToDevice));
+  CHK(hipMemcpy(b->d_l2g, g_l2g, 33 * sizeof(int32_t), hipMemcpyHostToDevice));
+  CHK(hipMalloc((void**)&b->d_yuv, N * b->yfb));
+  CHK(hipMalloc((void**)&b->d_aflags, N * sizeof(uint32_t)));
+  CHK(hipMalloc((void**)&b->d_alpha, N * nmb));
+  CHK(hipMalloc((void**)&b->d_uva, N * nmb * sizeof(uint16_t)));
+  CHK(hipMalloc((void**)&b->d_segmap, N * nmb));
+  CHK(hipMalloc((void**)&b->d_params, N * sizeof(vp8g_frame_params)));
+  CHK(hipMalloc((void**)&b->d_tokens, N * b->tok_cap * sizeof(uint16_t)));
+  CHK(hipMalloc((void**)&b->d_mbinfo, N * nmb * VP8G_MBINFO_BYTES));
+  CHK(hipMalloc((void**)&b->d_results, N * sizeof(vp8g_frame_result)));
+  CHK(hipHostMalloc((void**)&b->h_aflags, N * sizeof(uint32_t), 0));
+  CHK(hipHostMalloc((void**)&b->h_alpha, N * nmb, 0));
+  CHK(hipHostMalloc((void**)&b->h_uva, N * nmb * sizeof(uint16_t), 0));
+  CHK(hipHostMalloc((void**)&b->h_segmap, N * nmb, 0));
+  CHK(hipHostMalloc((void**)&b->h_params, N * sizeof(vp8g_frame_params), 0));
+  CHK(hipHostMalloc((void**)&b->h_mbinfo, N * nmb * VP8G_MBINFO_BYTES, 0));
+  CHK(hipHostMalloc((void**)&b->h_results, N * sizeof(vp8g_frame_result), 0));
+  b->frames = (vp8h_frame*)calloc(N, sizeof(vp8h_frame));
+  b->tok_off = (size_t*)calloc(N + 1, sizeof(size_t));
+  b->out = (uint8_t**)calloc(N, sizeof(uint8_t*));
+  b->out_size = (size_t*)calloc(N, sizeof(size_t));
+  b->err = (int*)calloc(N, sizeof(int));
+  b->hdr = (int*)calloc(2 * N, sizeof(int));
+  if (!b->frames || !b->tok_off || !b->out || !b->out_size || !b->err || !b->hdr) goto fail;
+  return b;
+fail:
+  WebPGpuBatchDelete(b);
+  return NULL;
+}
+
+void WebPGpuBatchDelete(WebPGpuBatch* b) {
+  if (!b) return;
+  hipSetDevice(b->device);
+  if (b->stream) hipStreamSynchronize(b->stream);
+  hipFree(b->d_g2l); hipFree(b->d_rgba); hipFree(b->d_yuv); hipFree(b->d_aflags); hipFree(b->d_alpha);
+  hipFree(b->d_uva); hipFree(b->d_segmap); hipFree(b->d_params); hipFree(b->d_tokens);
+  hipFree(b->d_mbinfo); hipFree(b->d_results);
+  hipHostFree(b->h_aflags); hipHostFree(b->h_alpha); hipHostFree(b->h_uva);
+  hipHostFree(b->h_segmap); hipHostFree(b->h_params); hipHostFree(b->h_mbinfo);
+  hipHostFree(b->h_results); hipHostFree(b->h_tokens);
+  if (b->stream) hipStreamDestroy(b->stream);
+  if (b->out)
+    for (int i = 0; i < b->max_frames; ++i) free(b->out[i]);
+  free(b->out); free(b->out_size); free(b->err); free(b->hdr);
+  free(b->frames); free(b->tok_off);
+  free(b);
+}
+
+/* ---- host thread pool for the per-frame tail ---- */
+
+typedef struct {
+  WebPGpuBatch* b;
+  int n;
+  atomic_int next;
+} TailJob;
+
+static void frame_tail(WebPGpuBatch* b, int f) {
+  vp8h_frame* fr = &b->frames[f];
+  const vp8g_frame_result* res = &b->h_results[f];
+  free(b->out[f]);
+  b->out[f] = NULL;
+  b->out_size[f] = 0;
+  if (b->err[f] != VP8_ENC_OK) return;
+  if (res->error) { b->err[f] = VP8_ENC_ERROR_OUT_OF_MEMORY; return; }
+  /* partition-0 overflow retry (frame_enc.c:869-876) is not implemented on
+   * the GPU path yet: report it instead of emitting a different stream */
+  if (fr->max_i4_header_bits > 0 &&
+      res->size_p0 + (uint64_t)fr->seg_hdr_size > VP8H_P0_LIMIT) {
+    b->err[f] = VP8_ENC_ERROR_PARTITION0_OVERFLOW;
+    return;
+  }
+  vp8h_bw part1;
+  vp8h_bw_init(&part1, (size_t)res->ntokens / 8 + 4096);
+  vp8h_emit_tokens(&part1, b->h_tokens + b->tok_off[f], res->ntokens, res->probas);
+  vp8h_bw_finish(&part1);
+  int err = VP8_ENC_OK;
+  b->out_size[f] = vp8h_assemble(fr, res, b->h_mbinfo + (size_t)f * b->nmb * VP8G_MBINFO_BYTES,
+                                 &part1, &b->out[f], &err, b->hdr + 2 * f);
+  b->err[f] = err;
+  vp8h_bw_free(&part1);
+}
+
+static void* tail_worker(void* arg) {
+  TailJob* j = (TailJob*)arg;
+  for (;;) {
+    const int f = atomic_fetch_add(&j->next, 1);
+    if (f >= j->n) break;
+    frame_tail(j->b, f);
+  }
+  return NULL;
+}
+
+static void run_tails(WebPGpuBatch* b, int n) {
+  TailJob job;
+  job.b = b; job.n = n;
+  atomic_init(&job.next, 0);
+  int nt = b->threads < n ? b->threads : n;
+  if (nt <= 1) { tail_worker(&job); return; }
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nt);
+  int started = 0;
+  for (int i = 1; i < nt; ++i)
+    if (pthread_create(&th[started], NULL, tail_worker, &job) == 0) ++started;
+  tail_worker(&job);
+  for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
+  free(th);
+}
+
+/* ---- pipeline ---- */
+
+int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
+  const size_t nmb = (size_t)b->nmb;
+  double t0 = now_us(), t1, t2, t3, t4;
+  hipStream_t st = b->stream;
+  if (!vp8g_launch_analysis(b->d_yuv, b->yfb, b->w, b->h, n, b->d_alpha, b->d_uva, st)) return 0;
+  CHK(hipMemcpyAsync(b->h_alpha, b->d_alpha, n * nmb, hipMemcpyDeviceToHost, st));
+  CHK(hipMemcpyAsync(b->h_uva, b->d_uva, n * nmb * sizeof(uint16_t), hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  t1 = now_us();
+  for (int f = 0; f < n; ++f) {
+    if (b->err[f] != VP8_ENC_OK) continue;
+    vp8h_frame_init(&b->frames[f], &b->cfg, b->w, b->h);
+    vp8h_setup_segments(&b->frames[f], b->h_alpha + f * nmb, b->h_uva + f * nmb,
+                        b->h_segmap + f * nmb, &b->h_params[f]);
+  }
+  CHK(hipMemcpyAsync(b->d_segmap, b->h_segmap, n * nmb, hipMemcpyHostToDevice, st));
+  CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
+                     hipMemcpyHostToDevice, st));
+  t2 = now_us();
+  if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
+                          b->tok_cap, b->d_mbinfo, b->d_results, st))
+    return 0;
+  CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
+                     hipMemcpyDeviceToHost, st));
+  CHK(hipMemcpyAsync(b->h_mbinfo, b->d_mbinfo, n * nmb * VP8G_MBINFO_BYTES,
+                     hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  t3 = now_us();
+  b->tok_off[0] = 0;
+  for (int f = 0; f < n; ++f) b->tok_off[f + 1] = b->tok_off[f] + b->h_results[f].ntokens;
+  const size_t total = b->tok_off[n];
+  if (total > b->h_tok_cap) {
+    hipHostFree(b->h_tokens);
+    b->h_tokens = NULL;
+    b->h_tok_cap = 0;
+    const size_t cap = total + total / 4 + 1024;
+    CHK(hipHostMalloc((void**)&b->h_tokens, cap * sizeof(uint16_t), 0));
+    b->h_tok_cap = cap;
+  }
+  for (int f = 0; f < n; ++f)
+    if (b->h_results[f].ntokens)
+      CHK(hipMemcpyAsync(b->h_tokens + b->tok_off[f], b->d_tokens + (size_t)f * b->tok_cap,
+                         b->h_results[f].ntokens * sizeof(uint16_t), hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  t4 = now_us();
+  run_tails(b, n);
+  const double t5 = now_us();
+  b->timings[1] = t2 - t1;
+  b->timings[2] = t3 - t2;
+  b->timings[3] = t4 - t3;
+  b->timings[4] = t5 - t4;
+  b->timings[0] += t1 - t0;
+  b->last_n = n;
+  return 1;
+fail:
+  return 0;
+}
+
+static int run_rgba(WebPGpuBatch* b, const void* rgba_dev, size_t fstride, int rstride, int n,
+                    void* stream) {
+  const double t0 = now_us();
+  if (n <= 0 || n > b->max_frames) return 0;
+  if (rstride < 4 * b->w) return 0;
+  CHK(hipSetDevice(b->device));
+  for (int f = 0; f < n; ++f) b->err[f] = VP8_ENC_OK;
+  if (stream) {   /* order after the caller's producer work */
+    hipEvent_t ev;
+    CHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    CHK(hipEventRecord(ev, (hipStream_t)stream));
+    CHK(hipStreamWaitEvent(b->stream, ev, 0));
+    hipEventDestroy(ev);
+  }
+  CHK(hipMemsetAsync(b->d_aflags, 0, n * sizeof(uint32_t), b->stream));
+  if (!vp8g_launch_import((const uint8_t*)rgba_dev, fstride, rstride, b->w, b->h, n, b->d_yuv,
+                          b->yfb, b->d_aflags, b->d_g2l, b->d_l2g, b->stream))
+    return 0;
+  CHK(hipMemcpyAsync(b->h_aflags, b->d_aflags, n * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                     b->stream));
+  CHK(hipStreamSynchronize(b->stream));
+  for (int f = 0; f < n; ++f)   /* transparent input needs the ALPH path */
+    if (b->h_aflags[f]) b->err[f] = VP8_ENC_ERROR_INVALID_CONFIGURATION;
+  b->timings[0] = now_us() - t0;
+  const int ok = vp8g_engine_run_yuv(b, n);
+  b->timings[5] = now_us() - t0;
+  return ok;
+fail:
+  return 0;
+}
+
+int WebPGpuBatchEncodeRGBA(WebPGpuBatch* b, const void* rgba_dev, size_t fstride, int rstride,
+                           int n, void* stream) {
+  if (!b || !rgba_dev) return 0;
+  return run_rgba(b, rgba_dev, fstride, rstride, n, stream);
+}
+
+int WebPGpuBatchEncodeRGBAHost(WebPGpuBatch* b, const uint8_t* rgba, size_t fstride, int rstride,
+                               int n) {
+  if (!b || !rgba || n <= 0 || n > b->max_frames) return 0;
+  CHK(hipSetDevice(b->device));
+  const size_t need = (size_t)n * fstride;
+  if (need > b->d_rgba_cap) {
+    hipFree(b->d_rgba);
+    b->d_rgba = NULL;
+    b->d_rgba_cap = 0;
+    CHK(hipMalloc((void**)&b->d_rgba, need));
+    b->d_rgba_cap = need;
+  }
+  CHK(hipMemcpyAsync(b->d_rgba, rgba, need, hipMemcpyHostToDevice, b->stream));
+  return run_rgba(b, b->d_rgba, fstride, rstride, n, NULL);
+fail:
+  return 0;
+}
+
+size_t WebPGpuBatchOutputSize(const WebPGpuBatch* b, int f) {
+  return (b && f >= 0 && f < b->last_n) ? b->out_size[f] : 0;
+}
+const uint8_t* WebPGpuBatchOutput(const WebPGpuBatch* b, int f) {
+  return (b && f >= 0 && f < b->last_n) ? b->out[f] : NULL;
+}
+int WebPGpuBatchError(const WebPGpuBatch* b, int f) {
+  return (b && f >= 0 && f < b->last_n) ? b->err[f] : VP8_ENC_ERROR_NULL_PARAMETER;
+}
+void WebPGpuBatchTimings(const WebPGpuBatch* b, double t[8]) {
+  for (int i = 0; i < 8; ++i) t[i] = b ? b->timings[i] : 0.;
+}
+
+int WebPGpuBatchGetYUV(const WebPGpuBatch* b, int f, uint8_t* dst) {
+  if (!b || f < 0 || f >= b->max_frames || !dst) return 0;
+  const size_t bytes = (size_t)b->w * b->h + 2 * (size_t)b->uvw * b->uvh;
+  hipSetDevice(b->device);
+  return hipMemcpy(dst, b->d_yuv + (size_t)f * b->yfb, bytes, hipMemcpyDeviceToHost) == hipSuccess;
+}
+
+int WebPGpuBatchGetMBInfo(const WebPGpuBatch* b, int f, uint8_t* dst) {
+  if (!b || f < 0 || f >= b->last_n || !dst) return 0;
+  memcpy(dst, b->h_mbinfo + (size_t)f * b->nmb * VP8G_MBINFO_BYTES,
+         (size_t)b->nmb * VP8G_MBINFO_BYTES);
+  return 1;
+}
+
+int vp8g_engine_upload_yuv(WebPGpuBatch* b, int f, const uint8_t* y, int ys, const uint8_t* u,
+                           const uint8_t* v, int uvs) {
+  uint8_t* dst = b->d_yuv + (size_t)f * b->yfb;
+  if (hipSetDevice(b->device) != hipSuccess) return 0;
+  if (hipMemcpy2D(dst, b->w, y, ys, b->w, b->h, hipMemcpyHostToDevice) != hipSuccess) return 0;
+  dst += (size_t)b->w * b->h;
+  if (hipMemcpy2D(dst, b->uvw, u, uvs, b->uvw, b->uvh, hipMemcpyHostToDevice) != hipSuccess)
+    return 0;
+  dst += (size_t)b->uvw * b->uvh;
+  if (hipMemcpy2D(dst, b->uvw, v, uvs, b->uvw, b->uvh, hipMemcpyHostToDevice) != hipSuccess)
+    return 0;
+  b->err[f] = VP8_ENC_OK;
+  return 1;
+}
+
+int vp8g_engine_import(WebPGpuBatch* b, const uint8_t* rgba, int stride, uint8_t* y,
+                       uint8_t* u, uint8_t* v, int* has_alpha) {
+  /* synchronous single-frame RGBA -> YUV through K1 (used by the
+   * WebPPictureImport* API); output written to the caller's host planes */
+  if (hipSetDevice(b->device) != hipSuccess) return 0;
+  const size_t need = (size_t)stride * b->h;
+  if (need > b->d_rgba_cap) {
+    hipFree(b->d_rgba);
+    b->d_rgba = NULL;
+    b->d_rgba_cap = 0;
+    if (hipMalloc((void**)&b->d_rgba, need) != hipSuccess) return 0;
+    b->d_rgba_cap = need;
+  }
+  if (hipMemcpy(b->d_rgba, rgba, need, hipMemcpyHostToDevice) != hipSuccess) return 0;
+  if (hipMemsetAsync(b->d_aflags, 0, sizeof(uint32_t), b->stream) != hipSuccess) return 0;
+  if (!vp8g_launch_import(b->d_rgba, need, stride, b->w, b->h, 1, b->d_yuv, b->yfb, b->d_aflags,
+                          b->d_g2l, b->d_l2g, b->stream))
+    return 0;
+  if (hipStreamSynchronize(b->stream) != hipSuccess) return 0;
+  uint32_t flag = 0;
+  if (hipMemcpy(&flag, b->d_aflags, 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  *has_alpha = flag != 0;
+  const uint8_t* src = b->d_yuv;
+  if (hipMemcpy(y, src, (size_t)b->w * b->h, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  src += (size_t)b->w * b->h;
+  if (hipMemcpy(u, src, (size_t)b->uvw * b->uvh, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  src += (size_t)b->uvw * b->uvh;
+  if (hipMemcpy(v, src, (size_t)b->uvw * b->uvh, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  return 1;
+}

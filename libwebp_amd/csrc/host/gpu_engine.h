@@ -1,0 +1,62 @@
+/* Internal: the batched GPU engine behind WebPGpuBatch and WebPEncode. */
+#ifndef LIBWEBP_AMD_GPU_ENGINE_H_
+#define LIBWEBP_AMD_GPU_ENGINE_H_
+
+#include <hip/hip_runtime_api.h>
+
+#include "../vp8_gpu.h"
+#include "vp8_host.h"
+#include "webp/encode.h"
+
+/* partition-0 size guard of VP8EncTokenLoop (frame_enc.c:32, :869) */
+#define VP8H_P0_LIMIT ((((uint64_t)1 << 19) - 2048ULL) << 11)
+
+struct WebPGpuBatch {
+  int device, w, h, max_frames, mbw, mbh, nmb, uvw, uvh, threads, last_n;
+  WebPConfig cfg;
+  size_t yfb, tok_cap, d_rgba_cap, h_tok_cap;
+  hipStream_t stream;
+  /* device (HBM) */
+  uint8_t* d_rgba;
+  uint16_t* d_g2l;   /* gamma tables: 256 x u16 then 33 x i32 */
+  int32_t* d_l2g;
+  uint8_t* d_yuv;
+  uint32_t* d_aflags;
+  uint8_t* d_alpha;
+  uint16_t* d_uva;
+  uint8_t* d_segmap;
+  vp8g_frame_params* d_params;
+  uint16_t* d_tokens;
+  uint8_t* d_mbinfo;
+  vp8g_frame_result* d_results;
+  /* host (pinned) */
+  uint32_t* h_aflags;
+  uint8_t* h_alpha;
+  uint16_t* h_uva;
+  uint8_t* h_segmap;
+  vp8g_frame_params* h_params;
+  uint8_t* h_mbinfo;
+  vp8g_frame_result* h_results;
+  uint16_t* h_tokens;
+  size_t* tok_off;
+  vp8h_frame* frames;
+  /* outputs of the last call */
+  uint8_t** out;
+  size_t* out_size;
+  int* err;
+  int* hdr;
+  double timings[8];
+};
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+int vp8g_engine_run_yuv(struct WebPGpuBatch* b, int n);
+int vp8g_engine_upload_yuv(struct WebPGpuBatch* b, int f, const uint8_t* y, int ys,
+                           const uint8_t* u, const uint8_t* v, int uvs);
+int vp8g_engine_import(struct WebPGpuBatch* b, const uint8_t* rgba, int stride, uint8_t* y,
+                       uint8_t* u, uint8_t* v, int* has_alpha);
+#ifdef __cplusplus
+}
+#endif
+#endif

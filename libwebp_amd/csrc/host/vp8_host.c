@@ -1,0 +1,552 @@
+/* Host C: per-frame segment setup and the boolean-coder / bitstream tail of
+ * the VP8 lossy encoder. Reference behaviour cited per function. */
+#include "vp8_host.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define VP8T_DECL static const
+#include "../vp8_tables.h"
+
+#define QFIX 17
+
+static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
+static inline int iabs(int v) { return v < 0 ? -v : v; }
+static inline int bit_cost(int bit, int p) {   /* cost_enc.h:59-61 */
+  return bit ? kVP8EntropyCost[255 - p] : kVP8EntropyCost[p];
+}
+
+int vp8h_frame_init(vp8h_frame* fr, const WebPConfig* cfg, int w, int h) {
+  memset(fr, 0, sizeof(*fr));
+  if (cfg->method < 3 || cfg->method > 6) return 0;   /* m0-2: non-token loop */
+  if (cfg->pass != 1 || cfg->target_size > 0 || cfg->target_PSNR > 0) return 0;
+  if (cfg->autofilter || cfg->low_memory || cfg->use_sharp_yuv) return 0;
+  fr->w = w; fr->h = h;
+  fr->mbw = (w + 15) >> 4; fr->mbh = (h + 15) >> 4;
+  fr->method = cfg->method;
+  fr->rd_opt = cfg->method >= 6 ? 3 : cfg->method >= 5 ? 2 : 1;
+  {
+    const int lim = 100 - cfg->partition_limit;
+    fr->max_i4_header_bits = 256 * 16 * 16 * (lim * lim) / (100 * 100);
+  }
+  {
+    const int use_filter = cfg->filter_strength > 0 || cfg->autofilter > 0;
+    fr->profile = use_filter ? ((cfg->filter_type == 1) ? 0 : 1) : 2;
+  }
+  fr->quality = cfg->quality;
+  fr->sns_strength = cfg->sns_strength;
+  fr->filter_strength = cfg->filter_strength;
+  fr->filter_sharpness = cfg->filter_sharpness;
+  fr->filter_type = cfg->filter_type;
+  fr->preprocessing = cfg->preprocessing;
+  fr->emulate_jpeg_size = cfg->emulate_jpeg_size;
+  fr->cfg_segments = cfg->segments;
+  fr->num_segments = cfg->segments;
+  fr->update_map = fr->num_segments > 1;
+  memset(fr->seg_probas, 255, 3);
+  fr->f_simple = 1;     /* ResetFilterHeader, webp_enc.c:47-53 */
+  fr->f_level = 0;
+  fr->f_sharpness = 0;
+  return 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* k-means segmentation: analysis_enc.c:28-216 */
+
+static void smooth_map(uint8_t* seg, int w, int h) {
+  uint8_t* tmp = (uint8_t*)malloc((size_t)w * h);
+  if (!tmp) return;
+  for (int y = 1; y < h - 1; ++y)
+    for (int x = 1; x < w - 1; ++x) {
+      const uint8_t* s = seg + x + w * y;
+      int cnt[4] = {0, 0, 0, 0}, maj = s[0];
+      cnt[s[-w - 1]]++; cnt[s[-w]]++; cnt[s[-w + 1]]++; cnt[s[-1]]++;
+      cnt[s[1]]++; cnt[s[w - 1]]++; cnt[s[w]]++; cnt[s[w + 1]]++;
+      for (int n = 0; n < 4; ++n)
+        if (cnt[n] >= 5) { maj = n; break; }
+      tmp[x + y * w] = (uint8_t)maj;
+    }
+  for (int y = 1; y < h - 1; ++y)
+    for (int x = 1; x < w - 1; ++x) seg[x + w * y] = tmp[x + y * w];
+  free(tmp);
+}
+
+static void kmeans_segments(vp8h_frame* fr, const uint8_t* mb_alpha, uint8_t* segmap) {
+  const int nmb = fr->mbw * fr->mbh;
+  const int nb = fr->num_segments < 4 ? fr->num_segments : 4;
+  int alphas[256], map[256], centers[4], accum[4], dist[4];
+  int n, k, wavg = 0;
+  memset(alphas, 0, sizeof(alphas));
+  memset(map, 0, sizeof(map));
+  for (int i = 0; i < nmb; ++i) alphas[mb_alpha[i]]++;
+  for (n = 0; n <= 255 && alphas[n] == 0; ++n) {}
+  const int min_a = n;
+  for (n = 255; n > min_a && alphas[n] == 0; --n) {}
+  const int max_a = n;
+  const int range = max_a - min_a;
+  for (k = 0, n = 1; k < nb; ++k, n += 2) centers[k] = min_a + (n * range) / (2 * nb);
+  for (k = 0; k < 6; ++k) {
+    int tw = 0, moved = 0;
+    for (n = 0; n < nb; ++n) accum[n] = dist[n] = 0;
+    n = 0;
+    for (int a = min_a; a <= max_a; ++a) {
+      if (!alphas[a]) continue;
+      while (n + 1 < nb && iabs(a - centers[n + 1]) < iabs(a - centers[n])) n++;
+      map[a] = n;
+      dist[n] += a * alphas[a];
+      accum[n] += alphas[a];
+    }
+    wavg = 0;
+    for (n = 0; n < nb; ++n) {
+      if (!accum[n]) continue;
+      const int c = (dist[n] + accum[n] / 2) / accum[n];
+      moved += iabs(centers[n] - c);
+      centers[n] = c;
+      wavg += c * accum[n];
+      tw += accum[n];
+    }
+    wavg = (wavg + tw / 2) / tw;
+    if (moved < 5) break;
+  }
+  for (int i = 0; i < nmb; ++i) segmap[i] = (uint8_t)map[mb_alpha[i]];
+  if (nb > 1 && (fr->preprocessing & 1)) smooth_map(segmap, fr->mbw, fr->mbh);
+  int mn = centers[0], mx = centers[0];
+  if (nb > 1)
+    for (n = 0; n < nb; ++n) {
+      if (mn > centers[n]) mn = centers[n];
+      if (mx < centers[n]) mx = centers[n];
+    }
+  if (mx == mn) mx = mn + 1;
+  for (n = 0; n < nb; ++n) {
+    fr->seg_alpha[n] = clampi(255 * (centers[n] - wavg) / (mx - mn), -127, 127);
+    fr->seg_beta[n] = clampi(255 * (centers[n] - mn) / (mx - mn), 0, 255);
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* quant_enc.c:205-455 */
+
+static int fill_matrix(vp8g_mtx* m, int type, int q_dc, int q_ac) {
+  m->q[0] = (uint16_t)q_dc;
+  m->q[1] = (uint16_t)q_ac;
+  for (int i = 0; i < 2; ++i) {
+    m->iq[i] = (uint16_t)((1 << QFIX) / m->q[i]);
+    m->bias[i] = (uint32_t)kVP8BiasMtx[type][i > 0] << (QFIX - 8);
+    m->zthresh[i] = ((1u << QFIX) - 1 - m->bias[i]) / m->iq[i];
+  }
+  for (int i = 2; i < 16; ++i) {
+    m->q[i] = m->q[1]; m->iq[i] = m->iq[1];
+    m->bias[i] = m->bias[1]; m->zthresh[i] = m->zthresh[1];
+  }
+  int sum = 0;
+  for (int i = 0; i < 16; ++i) {
+    m->sharpen[i] = (uint16_t)(type == 0 ? (kVP8FreqSharpen[i] * m->q[i]) >> 11 : 0);
+    sum += m->q[i];
+  }
+  return (sum + 8) >> 4;
+}
+
+static double q_to_compression(double c) {
+  const double lin = (c < 0.75) ? c * (2. / 3.) : 2. * c - 1.;
+  return pow(lin, 1 / 3.);
+}
+static double q_to_jpeg_compression(double c, double alpha) {
+  const double amin = 0.30, amax = 0.85, emin = 0.4, emax = 0.9;
+  const double slope = (emin - emax) / (amax - amin);
+  const double e = (alpha > amax) ? emin : (alpha < amin) ? emax : emax + slope * (alpha - amin);
+  return pow(c, e);
+}
+
+static int get_proba(int a, int b) {
+  const int t = a + b;
+  return t == 0 ? 255 : (255 * a + t / 2) / t;
+}
+
+void vp8h_setup_segments(vp8h_frame* fr, const uint8_t* mb_alpha, const uint16_t* mb_uva,
+                         uint8_t* segmap, vp8g_frame_params* P) {
+  const int nmb = fr->mbw * fr->mbh;
+  /* VP8EncAnalyze tail (analysis_enc.c:422-482) */
+  const int do_seg = fr->emulate_jpeg_size || fr->num_segments > 1;
+  if (do_seg) {
+    long sa = 0, suva = 0;
+    for (int i = 0; i < nmb; ++i) { sa += mb_alpha[i]; suva += mb_uva[i]; }
+    fr->alpha = (int)(sa / nmb);
+    fr->uv_alpha = (int)(suva / nmb);
+    kmeans_segments(fr, mb_alpha, segmap);
+  } else {
+    memset(segmap, 0, (size_t)nmb);
+    fr->seg_alpha[0] = fr->seg_beta[0] = 0;
+    fr->alpha = fr->uv_alpha = 0;
+  }
+  /* VP8SetSegmentParams */
+  const int ns = fr->num_segments;
+  const double amp = 0.9 * fr->sns_strength / 100. / 128.;
+  const double Q = fr->quality / 100.;
+  const double cbase = fr->emulate_jpeg_size ? q_to_jpeg_compression(Q, fr->alpha / 255.)
+                                             : q_to_compression(Q);
+  for (int i = 0; i < ns; ++i) {
+    const double expn = 1. - amp * fr->seg_alpha[i];
+    fr->seg_quant[i] = clampi((int)(127. * (1. - pow(cbase, expn))), 0, 127);
+  }
+  fr->base_quant = fr->seg_quant[0];
+  for (int i = ns; i < 4; ++i) fr->seg_quant[i] = fr->base_quant;
+  int dq_uv_ac = (fr->uv_alpha - 64) * (6 - (-4)) / (100 - 30);
+  dq_uv_ac = dq_uv_ac * fr->sns_strength / 100;
+  fr->dq_uv_ac = clampi(dq_uv_ac, -4, 6);
+  fr->dq_uv_dc = clampi(-4 * fr->sns_strength / 100, -15, 15);
+  /* SetupFilterStrength: uses the header sharpness *before* it is set */
+  const int level0 = 5 * fr->filter_strength;
+  for (int i = 0; i < 4; ++i) {
+    const int qstep = kVP8AcQ[clampi(fr->seg_quant[i], 0, 127)] >> 2;
+    const int base = kVP8LevelsFromDelta[fr->f_sharpness][qstep < 64 ? qstep : 63];
+    const int f = base * level0 / (256 + fr->seg_beta[i]);
+    fr->seg_fstrength[i] = (f < 2) ? 0 : (f > 63) ? 63 : f;
+  }
+  fr->f_level = fr->seg_fstrength[0];
+  fr->f_simple = (fr->filter_type == 0);
+  fr->f_sharpness = fr->filter_sharpness;
+  /* SimplifySegments */
+  if (ns > 1) {
+    int map[4] = {0, 1, 2, 3}, nfinal = 1;
+    for (int s1 = 1; s1 < ns; ++s1) {
+      int s2, found = 0;
+      for (s2 = 0; s2 < nfinal; ++s2)
+        if (fr->seg_quant[s1] == fr->seg_quant[s2] &&
+            fr->seg_fstrength[s1] == fr->seg_fstrength[s2]) {
+          found = 1;
+          break;
+        }
+      map[s1] = s2;
+      if (!found) {
+        if (nfinal != s1) {
+          fr->seg_quant[nfinal] = fr->seg_quant[s1];
+          fr->seg_fstrength[nfinal] = fr->seg_fstrength[s1];
+          fr->seg_alpha[nfinal] = fr->seg_alpha[s1];
+          fr->seg_beta[nfinal] = fr->seg_beta[s1];
+        }
+        ++nfinal;
+      }
+    }
+    if (nfinal < ns) {
+      for (int i = 0; i < nmb; ++i) segmap[i] = (uint8_t)map[segmap[i]];
+      fr->num_segments = nfinal;
+      for (int i = nfinal; i < ns; ++i) {
+        fr->seg_quant[i] = fr->seg_quant[nfinal - 1];
+        fr->seg_fstrength[i] = fr->seg_fstrength[nfinal - 1];
+        fr->seg_alpha[i] = fr->seg_alpha[nfinal - 1];
+        fr->seg_beta[i] = fr->seg_beta[nfinal - 1];
+      }
+    }
+  }
+  /* SetupMatrices */
+  memset(P, 0, sizeof(*P));
+  const int tls = fr->method >= 4 ? fr->sns_strength : 0;
+  for (int i = 0; i < fr->num_segments; ++i) {
+    vp8g_seg* m = &P->seg[i];
+    const int q = fr->seg_quant[i];
+    const int q_i4 = fill_matrix(&m->y1, 0, kVP8DcQ[clampi(q, 0, 127)], kVP8AcQ[clampi(q, 0, 127)]);
+    const int q_i16 = fill_matrix(&m->y2, 1, kVP8DcQ[clampi(q, 0, 127)] * 2,
+                                  kVP8AcQ2[clampi(q, 0, 127)]);
+    const int q_uv = fill_matrix(&m->uv, 2, kVP8DcQ[clampi(q + fr->dq_uv_dc, 0, 117)],
+                                 kVP8AcQ[clampi(q + fr->dq_uv_ac, 0, 127)]);
+#define AT_LEAST_1(v) ((v) < 1 ? 1 : (v))
+    m->lambda_i4 = AT_LEAST_1((3 * q_i4 * q_i4) >> 7);
+    m->lambda_i16 = AT_LEAST_1(3 * q_i16 * q_i16);
+    m->lambda_uv = AT_LEAST_1((3 * q_uv * q_uv) >> 6);
+    m->lambda_mode = AT_LEAST_1((1 * q_i4 * q_i4) >> 7);
+    m->lambda_trellis_i4 = AT_LEAST_1((7 * q_i4 * q_i4) >> 3);
+    m->lambda_trellis_i16 = AT_LEAST_1((q_i16 * q_i16) >> 2);
+    m->lambda_trellis_uv = AT_LEAST_1((q_uv * q_uv) << 1);
+    m->tlambda = AT_LEAST_1((tls * q_i4) >> 5);
+#undef AT_LEAST_1
+    m->min_disto = 20 * m->y1.q[0];
+    fr->seg_y2ac[i] = m->y2.q[1];
+  }
+  for (int i = fr->num_segments; i < 4; ++i) fr->seg_y2ac[i] = 0;
+  /* SetSegmentProbas (frame_enc.c:198-231) */
+  int p[4] = {0, 0, 0, 0};
+  for (int i = 0; i < nmb; ++i) p[segmap[i]]++;
+  for (int i = 0; i < 4; ++i) fr->segment_size[i] = p[i];
+  if (fr->num_segments > 1) {
+    uint8_t* pr = fr->seg_probas;
+    pr[0] = (uint8_t)get_proba(p[0] + p[1], p[2] + p[3]);
+    pr[1] = (uint8_t)get_proba(p[0], p[1]);
+    pr[2] = (uint8_t)get_proba(p[2], p[3]);
+    fr->update_map = (pr[0] != 255) || (pr[1] != 255) || (pr[2] != 255);
+    if (!fr->update_map) memset(segmap, 0, (size_t)nmb);
+    fr->seg_hdr_size = p[0] * (bit_cost(0, pr[0]) + bit_cost(0, pr[1])) +
+                       p[1] * (bit_cost(0, pr[0]) + bit_cost(1, pr[1])) +
+                       p[2] * (bit_cost(1, pr[0]) + bit_cost(0, pr[2])) +
+                       p[3] * (bit_cost(1, pr[0]) + bit_cost(1, pr[2]));
+  } else {
+    fr->update_map = 0;
+    fr->seg_hdr_size = 0;
+  }
+  P->max_i4_header_bits = fr->max_i4_header_bits;
+  P->rd_opt = fr->rd_opt;
+  P->method = fr->method;
+  P->use_derr = fr->quality <= 98;
+  P->max_count = (nmb >> 3) < 96 ? 96 : (nmb >> 3);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Boolean coder: bit_writer_utils.c:26-179. Renormalisation shift is
+ * 7 - floor(log2(range + 1)) (the kNorm / kNewRange tables). */
+
+void vp8h_bw_init(vp8h_bw* bw, size_t expected) {
+  memset(bw, 0, sizeof(*bw));
+  bw->range = 254;
+  bw->nb_bits = -8;
+  if (expected) {
+    bw->buf = (uint8_t*)malloc(expected);
+    if (bw->buf) bw->cap = expected; else bw->error = 1;
+  }
+}
+
+void vp8h_bw_free(vp8h_bw* bw) {
+  free(bw->buf);
+  bw->buf = NULL;
+  bw->cap = bw->pos = 0;
+}
+
+static int bw_grow(vp8h_bw* bw, size_t extra) {
+  if (bw->pos + extra <= bw->cap) return 1;
+  size_t n = 2 * bw->cap;
+  if (n < bw->pos + extra) n = bw->pos + extra;
+  if (n < 1024) n = 1024;
+  uint8_t* nb = (uint8_t*)realloc(bw->buf, n);
+  if (!nb) { bw->error = 1; return 0; }
+  bw->buf = nb;
+  bw->cap = n;
+  return 1;
+}
+
+static void bw_flush(vp8h_bw* bw) {
+  const int s = 8 + bw->nb_bits;
+  const int32_t bits = bw->value >> s;
+  bw->value -= bits << s;
+  bw->nb_bits -= 8;
+  if ((bits & 0xff) != 0xff) {
+    size_t pos = bw->pos;
+    if (!bw_grow(bw, bw->run + 1)) return;
+    if ((bits & 0x100) && pos > 0) bw->buf[pos - 1]++;
+    const uint8_t fillv = (bits & 0x100) ? 0x00 : 0xff;
+    for (; bw->run > 0; --bw->run) bw->buf[pos++] = fillv;
+    bw->buf[pos++] = (uint8_t)(bits & 0xff);
+    bw->pos = pos;
+  } else {
+    bw->run++;
+  }
+}
+
+static inline int bw_put(vp8h_bw* bw, int bit, int prob) {
+  const int split = (bw->range * prob) >> 8;
+  if (bit) { bw->value += split + 1; bw->range -= split + 1; }
+  else { bw->range = split; }
+  if (bw->range < 127) {
+    const int shift = __builtin_clz((unsigned)(bw->range + 1)) - 24;
+    bw->range = ((bw->range + 1) << shift) - 1;
+    bw->value <<= shift;
+    bw->nb_bits += shift;
+    if (bw->nb_bits > 0) bw_flush(bw);
+  }
+  return bit;
+}
+
+static inline int bw_put_uniform(vp8h_bw* bw, int bit) { return bw_put(bw, bit, 128); }
+
+static void bw_put_bits(vp8h_bw* bw, uint32_t v, int n) {
+  for (uint32_t m = 1u << (n - 1); m; m >>= 1) bw_put_uniform(bw, (v & m) != 0);
+}
+static void bw_put_signed(vp8h_bw* bw, int v, int n) {
+  if (!bw_put_uniform(bw, v != 0)) return;
+  if (v < 0) bw_put_bits(bw, ((uint32_t)(-v) << 1) | 1, n + 1);
+  else bw_put_bits(bw, (uint32_t)v << 1, n + 1);
+}
+
+void vp8h_bw_finish(vp8h_bw* bw) {
+  bw_put_bits(bw, 0, 9 - bw->nb_bits);
+  bw->nb_bits = 0;
+  bw_flush(bw);
+}
+
+void vp8h_emit_tokens(vp8h_bw* bw, const uint16_t* tok, size_t n, const uint8_t* probas) {
+  /* hot loop: keep the coder state in registers, spill only to flush */
+  int32_t range = bw->range, value = bw->value;
+  int nb_bits = bw->nb_bits;
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t t = tok[i];
+    const int bit = (int)(t >> 15);
+    const int p = (t & 0x4000) ? (int)(t & 0xff) : probas[t & 0x3fff];
+    const int split = (range * p) >> 8;
+    const int32_t one = split + 1;
+    value += bit ? one : 0;
+    range = bit ? range - one : split;
+    if (range < 127) {
+      const int shift = __builtin_clz((unsigned)(range + 1)) - 24;
+      range = ((range + 1) << shift) - 1;
+      value <<= shift;
+      nb_bits += shift;
+      if (nb_bits > 0) {
+        bw->range = range; bw->value = value; bw->nb_bits = nb_bits;
+        bw_flush(bw);
+        value = bw->value; nb_bits = bw->nb_bits;
+      }
+    }
+  }
+  bw->range = range; bw->value = value; bw->nb_bits = nb_bits;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Partition 0 (syntax_enc.c:187-310, tree_enc.c:270-347,485-504) and the
+ * RIFF container (syntax_enc.c:37-185,320-389). */
+
+static void code_intra_modes(vp8h_bw* bw, const vp8h_frame* fr, const uint8_t* mbinfo) {
+  const int mbw = fr->mbw;
+  uint8_t* top_modes = (uint8_t*)calloc(4 * (size_t)mbw, 1);   /* B_DC_PRED border */
+  if (!top_modes) { bw->error = 1; return; }
+  for (int y = 0; y < fr->mbh; ++y) {
+    uint8_t left_modes[4] = {0, 0, 0, 0};
+    for (int x = 0; x < mbw; ++x) {
+      const uint8_t* info = mbinfo + ((size_t)y * mbw + x) * VP8G_MBINFO_BYTES;
+      const uint8_t* modes = info + 4;
+      if (fr->update_map) {
+        const int s = info[2];
+        const uint8_t* p = fr->seg_probas;
+        if (bw_put(bw, s >= 2, p[0])) p += 1;
+        bw_put(bw, s & 1, p[1]);
+      }
+      if (bw_put(bw, info[0] != 0, 145)) {   /* intra16 */
+        const int m = modes[0];
+        if (bw_put(bw, m == 1 || m == 3, 156)) bw_put(bw, m == 1, 128);
+        else bw_put(bw, m == 2, 163);
+      } else {
+        for (int yy = 0; yy < 4; ++yy) {
+          int left = left_modes[yy];
+          for (int xx = 0; xx < 4; ++xx) {
+            const int top = yy == 0 ? top_modes[4 * x + xx] : modes[4 * (yy - 1) + xx];
+            const uint8_t* pr = kVP8BModeProba[top][left];
+            const int m = modes[4 * yy + xx];
+            if (bw_put(bw, m != 0, pr[0]) && bw_put(bw, m != 1, pr[1]) &&
+                bw_put(bw, m != 2, pr[2])) {
+              if (!bw_put(bw, m >= 6, pr[3])) {
+                if (bw_put(bw, m != 3, pr[4])) bw_put(bw, m != 4, pr[5]);
+              } else if (bw_put(bw, m != 6, pr[6])) {
+                if (bw_put(bw, m != 7, pr[7])) bw_put(bw, m != 8, pr[8]);
+              }
+            }
+            left = m;
+          }
+        }
+      }
+      const int uvm = info[1];
+      if (bw_put(bw, uvm != 0, 142) && bw_put(bw, uvm != 2, 114)) bw_put(bw, uvm != 3, 183);
+      for (int k = 0; k < 4; ++k) {
+        top_modes[4 * x + k] = modes[12 + k];
+        left_modes[k] = modes[4 * k + 3];
+      }
+    }
+  }
+  free(top_modes);
+}
+
+static void put_le32(uint8_t* p, uint32_t v) {
+  p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
+}
+
+size_t vp8h_assemble(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* mbinfo,
+                     vp8h_bw* part1, uint8_t** out, int* err, int* hdr_bytes) {
+  /* VP8AdjustFilterStrength without autofilter */
+  if (fr->filter_strength > 0) {
+    int max_level = 0;
+    for (int s = 0; s < 4; ++s) {
+      const int delta = (res->max_edge[s] * fr->seg_y2ac[s]) >> 3;
+      const int lvl = kVP8LevelsFromDelta[fr->f_sharpness][delta < 64 ? delta : 63];
+      if (lvl > fr->seg_fstrength[s]) fr->seg_fstrength[s] = lvl;
+      if (max_level < fr->seg_fstrength[s]) max_level = fr->seg_fstrength[s];
+    }
+    fr->f_level = max_level;
+  }
+  vp8h_bw bw;
+  vp8h_bw_init(&bw, (size_t)fr->mbw * fr->mbh * 7 / 8 + 1024);
+  bw_put_uniform(&bw, 0);   /* colorspace */
+  bw_put_uniform(&bw, 0);   /* clamping type */
+  if (bw_put_uniform(&bw, fr->num_segments > 1)) {
+    bw_put_uniform(&bw, fr->update_map);
+    bw_put_uniform(&bw, 1);   /* update segment feature data */
+    bw_put_uniform(&bw, 1);   /* absolute values */
+    for (int s = 0; s < 4; ++s) bw_put_signed(&bw, fr->seg_quant[s], 7);
+    for (int s = 0; s < 4; ++s) bw_put_signed(&bw, fr->seg_fstrength[s], 6);
+    if (fr->update_map)
+      for (int s = 0; s < 3; ++s)
+        if (bw_put_uniform(&bw, fr->seg_probas[s] != 255u)) bw_put_bits(&bw, fr->seg_probas[s], 8);
+  }
+  bw_put_uniform(&bw, fr->f_simple);
+  bw_put_bits(&bw, (uint32_t)fr->f_level, 6);
+  bw_put_bits(&bw, (uint32_t)fr->f_sharpness, 3);
+  bw_put_uniform(&bw, 0);          /* no loop-filter deltas */
+  bw_put_bits(&bw, 0, 2);          /* a single token partition */
+  bw_put_bits(&bw, (uint32_t)fr->base_quant, 7);
+  bw_put_signed(&bw, 0, 4);        /* dq_y1_dc */
+  bw_put_signed(&bw, 0, 4);        /* dq_y2_dc */
+  bw_put_signed(&bw, 0, 4);        /* dq_y2_ac */
+  bw_put_signed(&bw, fr->dq_uv_dc, 4);
+  bw_put_signed(&bw, fr->dq_uv_ac, 4);
+  bw_put_uniform(&bw, 0);          /* no probability refresh */
+  const uint8_t* p0 = &kVP8CoeffProba0[0][0][0][0];
+  const uint8_t* pu = &kVP8CoeffUpdateProba[0][0][0][0];
+  for (int s = 0; s < VP8G_NUM_SLOTS; ++s) {
+    const int v = res->probas[s];
+    if (bw_put(&bw, v != p0[s], pu[s])) bw_put_bits(&bw, (uint32_t)v, 8);
+  }
+  bw_put_uniform(&bw, 0);          /* no skip probability */
+  const size_t hdr_pos = bw.pos;
+  code_intra_modes(&bw, fr, mbinfo);
+  vp8h_bw_finish(&bw);
+  if (hdr_bytes) { hdr_bytes[0] = (int)hdr_pos; hdr_bytes[1] = (int)(bw.pos - hdr_pos); }
+  if (bw.error || part1->error) {
+    vp8h_bw_free(&bw);
+    *err = VP8_ENC_ERROR_OUT_OF_MEMORY;
+    return 0;
+  }
+  const size_t size0 = bw.pos, size1 = part1->pos;
+  if (size0 >= (1u << 19)) {
+    vp8h_bw_free(&bw);
+    *err = VP8_ENC_ERROR_PARTITION0_OVERFLOW;
+    return 0;
+  }
+  size_t vp8_size = 10 + size0 + size1;
+  const size_t pad = vp8_size & 1;
+  vp8_size += pad;
+  const size_t riff_size = 4 + 8 + vp8_size;
+  if (riff_size > 0xfffffffeU) {
+    vp8h_bw_free(&bw);
+    *err = VP8_ENC_ERROR_FILE_TOO_BIG;
+    return 0;
+  }
+  const size_t total = 8 + riff_size;
+  uint8_t* o = (uint8_t*)malloc(total);
+  if (!o) {
+    vp8h_bw_free(&bw);
+    *err = VP8_ENC_ERROR_OUT_OF_MEMORY;
+    return 0;
+  }
+  memcpy(o, "RIFF", 4);
+  put_le32(o + 4, (uint32_t)riff_size);
+  memcpy(o + 8, "WEBPVP8 ", 8);
+  put_le32(o + 16, (uint32_t)vp8_size);
+  const uint32_t bits = (uint32_t)(fr->profile << 1) | (1u << 4) | ((uint32_t)size0 << 5);
+  uint8_t* fh = o + 20;
+  fh[0] = (uint8_t)bits; fh[1] = (uint8_t)(bits >> 8); fh[2] = (uint8_t)(bits >> 16);
+  fh[3] = 0x9d; fh[4] = 0x01; fh[5] = 0x2a;   /* VP8 keyframe signature */
+  fh[6] = (uint8_t)(fr->w & 0xff); fh[7] = (uint8_t)(fr->w >> 8);
+  fh[8] = (uint8_t)(fr->h & 0xff); fh[9] = (uint8_t)(fr->h >> 8);
+  memcpy(o + 30, bw.buf, size0);
+  if (size1) memcpy(o + 30 + size0, part1->buf, size1);
+  if (pad) o[30 + size0 + size1] = 0;
+  vp8h_bw_free(&bw);
+  *out = o;
+  *err = VP8_ENC_OK;
+  return total;
+}

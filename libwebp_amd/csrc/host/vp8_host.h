@@ -1,0 +1,72 @@
+/* Host-side (C) parts of the VP8 lossy path that are per-frame and serial:
+ * segment/quantiser setup between the analysis and RD kernels, and the
+ * boolean-coder tail + bitstream assembly after them. */
+#ifndef LIBWEBP_AMD_VP8_HOST_H_
+#define LIBWEBP_AMD_VP8_HOST_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../vp8_gpu.h"
+#include "webp/encode.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Frame-level encoder state that lives on the host (a slice of the
+ * reference's VP8Encoder, src/enc/vp8i_enc.h:346-413). */
+typedef struct {
+  int w, h, mbw, mbh;
+  /* config-derived (webp_enc.c:95-123, 144-252) */
+  int method, rd_opt, max_i4_header_bits, profile;
+  float quality;
+  int sns_strength, filter_strength, filter_sharpness, filter_type;
+  int preprocessing, emulate_jpeg_size, cfg_segments;
+  /* segment header + per-segment values */
+  int num_segments, update_map, seg_hdr_size;
+  uint8_t seg_probas[3];
+  int alpha, uv_alpha, base_quant, dq_uv_dc, dq_uv_ac;
+  int seg_alpha[4], seg_beta[4], seg_quant[4], seg_fstrength[4], seg_y2ac[4];
+  int segment_size[4];
+  /* filter header */
+  int f_simple, f_level, f_sharpness;
+} vp8h_frame;
+
+/* Initialise from a validated config (lossy, method 3..6). Returns 0 if the
+ * config is outside what the GPU path implements. */
+int vp8h_frame_init(vp8h_frame* fr, const WebPConfig* cfg, int w, int h);
+
+/* Segment analysis + parameters (analysis_enc.c:76-216, quant_enc.c:205-455,
+ * frame_enc.c:198-231). Inputs: per-MB analysis alphas from the GPU.
+ * Outputs: final per-MB segment ids and the kernel parameter block. */
+void vp8h_setup_segments(vp8h_frame* fr, const uint8_t* mb_alpha, const uint16_t* mb_uva,
+                         uint8_t* segmap, vp8g_frame_params* params);
+
+/* Boolean coder (bit_writer_utils.c). */
+typedef struct {
+  int32_t range, value;
+  int run, nb_bits;
+  uint8_t* buf;
+  size_t pos, cap;
+  int error;
+} vp8h_bw;
+
+void vp8h_bw_init(vp8h_bw* bw, size_t expected);
+void vp8h_bw_free(vp8h_bw* bw);
+void vp8h_bw_finish(vp8h_bw* bw);
+
+/* VP8EmitTokens (token_enc.c:200-223): replay the GPU token stream through
+ * the boolean coder with the final probabilities. */
+void vp8h_emit_tokens(vp8h_bw* bw, const uint16_t* tokens, size_t n, const uint8_t* probas);
+
+/* Assemble the complete RIFF/WEBP/VP8 file (syntax_enc.c:269-389) into a
+ * malloc'ed buffer. Applies VP8AdjustFilterStrength (filter_enc.c:194-233)
+ * first. Returns the size, 0 on error (*err set). */
+size_t vp8h_assemble(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* mbinfo,
+                     vp8h_bw* part1, uint8_t** out, int* err, int* hdr_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

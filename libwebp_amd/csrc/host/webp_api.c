@@ -1,0 +1,525 @@
+/* The libwebp encoder C ABI (include/webp/encode.h) on top of the GPU
+ * engine. Behaviour follows the reference API functions cited per item. */
+#include <limits.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "gpu_engine.h"
+#include "vp8_host.h"
+#include "webp/encode.h"
+#include "webp/encode_gpu.h"
+
+/* ---- misc (webp_enc.c:32-34, utils.c) ---- */
+
+int WebPGetEncoderVersion(void) { return (1 << 16) | (3 << 8) | 2; }
+void* WebPMalloc(size_t size) { return malloc(size); }
+void WebPFree(void* ptr) { free(ptr); }
+
+static int set_error(const WebPPicture* pic, WebPEncodingError e) {   /* webp_enc.c:306-315 */
+  if (pic->error_code == VP8_ENC_OK) ((WebPPicture*)pic)->error_code = e;
+  return 0;
+}
+
+/* ---- WebPConfig (config_enc.c:24-157) ---- */
+
+int WebPConfigInitInternal(WebPConfig* c, WebPPreset preset, float quality, int version) {
+  if (WEBP_ABI_IS_INCOMPATIBLE(version, WEBP_ENCODER_ABI_VERSION)) return 0;
+  if (c == NULL) return 0;
+  memset(c, 0, sizeof(*c));
+  c->quality = quality;
+  c->method = 4;
+  c->sns_strength = 50;
+  c->filter_strength = 60;
+  c->filter_type = 1;
+  c->segments = 4;
+  c->pass = 1;
+  c->qmax = 100;
+  c->alpha_compression = 1;
+  c->alpha_filtering = 1;
+  c->alpha_quality = 100;
+  c->near_lossless = 100;
+  c->image_hint = WEBP_HINT_DEFAULT;
+  switch (preset) {
+    case WEBP_PRESET_PICTURE:
+      c->sns_strength = 80; c->filter_sharpness = 4; c->filter_strength = 35;
+      c->preprocessing &= ~2;
+      break;
+    case WEBP_PRESET_PHOTO:
+      c->sns_strength = 80; c->filter_sharpness = 3; c->filter_strength = 30;
+      c->preprocessing |= 2;
+      break;
+    case WEBP_PRESET_DRAWING:
+      c->sns_strength = 25; c->filter_sharpness = 6; c->filter_strength = 10;
+      break;
+    case WEBP_PRESET_ICON:
+      c->sns_strength = 0; c->filter_strength = 0; c->preprocessing &= ~2;
+      break;
+    case WEBP_PRESET_TEXT:
+      c->sns_strength = 0; c->filter_strength = 0; c->preprocessing &= ~2; c->segments = 2;
+      break;
+    default:
+      break;
+  }
+  return WebPValidateConfig(c);
+}
+
+#define IN_RANGE(v, lo, hi) ((v) >= (lo) && (v) <= (hi))
+int WebPValidateConfig(const WebPConfig* c) {
+  if (c == NULL) return 0;
+  return IN_RANGE(c->quality, 0, 100) && c->target_size >= 0 && c->target_PSNR >= 0 &&
+         IN_RANGE(c->method, 0, 6) && IN_RANGE(c->segments, 1, 4) &&
+         IN_RANGE(c->sns_strength, 0, 100) && IN_RANGE(c->filter_strength, 0, 100) &&
+         IN_RANGE(c->filter_sharpness, 0, 7) && IN_RANGE(c->filter_type, 0, 1) &&
+         IN_RANGE(c->autofilter, 0, 1) && IN_RANGE(c->pass, 1, 10) && c->qmin >= 0 &&
+         c->qmax <= 100 && c->qmin <= c->qmax && IN_RANGE(c->show_compressed, 0, 1) &&
+         IN_RANGE(c->preprocessing, 0, 7) && IN_RANGE(c->partitions, 0, 3) &&
+         IN_RANGE(c->partition_limit, 0, 100) && c->alpha_compression >= 0 &&
+         c->alpha_filtering >= 0 && IN_RANGE(c->alpha_quality, 0, 100) &&
+         IN_RANGE(c->lossless, 0, 1) && IN_RANGE(c->near_lossless, 0, 100) &&
+         c->image_hint < WEBP_HINT_LAST && IN_RANGE(c->emulate_jpeg_size, 0, 1) &&
+         IN_RANGE(c->thread_level, 0, 1) && IN_RANGE(c->low_memory, 0, 1) &&
+         IN_RANGE(c->exact, 0, 1) && IN_RANGE(c->use_delta_palette, 0, 1) &&
+         IN_RANGE(c->use_sharp_yuv, 0, 1);
+}
+
+int WebPConfigLosslessPreset(WebPConfig* c, int level) {
+  static const uint8_t kMethod[10] = {0, 1, 2, 3, 3, 4, 4, 4, 5, 6};
+  static const uint8_t kQuality[10] = {0, 20, 25, 30, 50, 50, 75, 90, 90, 100};
+  if (c == NULL || level < 0 || level > 9) return 0;
+  c->lossless = 1;
+  c->method = kMethod[level];
+  c->quality = kQuality[level];
+  return 1;
+}
+
+/* ---- WebPPicture (picture_enc.c:25-183) ---- */
+
+static int DummyWriter(const uint8_t* d, size_t n, const WebPPicture* p) {
+  (void)d; (void)n; (void)p;
+  return 1;
+}
+
+int WebPPictureInitInternal(WebPPicture* pic, int version) {
+  if (WEBP_ABI_IS_INCOMPATIBLE(version, WEBP_ENCODER_ABI_VERSION)) return 0;
+  if (pic != NULL) {
+    memset(pic, 0, sizeof(*pic));
+    pic->writer = DummyWriter;
+    pic->error_code = VP8_ENC_OK;
+  }
+  return 1;
+}
+
+static int validate_picture(const WebPPicture* pic) {
+  if (pic == NULL) return 0;
+  if (pic->width <= 0 || pic->height <= 0 || pic->width / 4 > INT_MAX / 4 ||
+      pic->height / 4 > INT_MAX / 4)
+    return set_error(pic, VP8_ENC_ERROR_BAD_DIMENSION);
+  if (pic->colorspace != WEBP_YUV420 && pic->colorspace != WEBP_YUV420A)
+    return set_error(pic, VP8_ENC_ERROR_INVALID_CONFIGURATION);
+  return 1;
+}
+
+static void reset_argb(WebPPicture* p) { p->memory_argb_ = NULL; p->argb = NULL; p->argb_stride = 0; }
+static void reset_yuva(WebPPicture* p) {
+  p->memory_ = NULL;
+  p->y = p->u = p->v = p->a = NULL;
+  p->y_stride = p->uv_stride = p->a_stride = 0;
+}
+
+static int alloc_argb(WebPPicture* p) {
+  if (!validate_picture(p)) return 0;
+  free(p->memory_argb_);
+  reset_argb(p);
+  void* m = malloc((size_t)p->width * p->height * 4 + 64);
+  if (!m) return set_error(p, VP8_ENC_ERROR_OUT_OF_MEMORY);
+  p->memory_argb_ = m;
+  p->argb = (uint32_t*)(((uintptr_t)m + 31) & ~(uintptr_t)31);
+  p->argb_stride = p->width;
+  return 1;
+}
+
+static int alloc_yuva(WebPPicture* p) {
+  if (!validate_picture(p)) return 0;
+  const int has_alpha = (int)p->colorspace & WEBP_CSP_ALPHA_BIT;
+  const int w = p->width, h = p->height;
+  const int uvw = (int)(((int64_t)w + 1) >> 1), uvh = (int)(((int64_t)h + 1) >> 1);
+  const uint64_t ys = (uint64_t)w * h, uvs = (uint64_t)uvw * uvh;
+  const uint64_t as = has_alpha ? (uint64_t)w * h : 0;
+  free(p->memory_);
+  reset_yuva(p);
+  uint8_t* m = (uint8_t*)malloc(ys + as + 2 * uvs);
+  if (!m) return set_error(p, VP8_ENC_ERROR_OUT_OF_MEMORY);
+  p->memory_ = m;
+  p->y_stride = w;
+  p->uv_stride = uvw;
+  p->a_stride = has_alpha ? w : 0;
+  p->y = m;
+  p->u = m + ys;
+  p->v = p->u + uvs;
+  if (as) p->a = p->v + uvs;
+  return 1;
+}
+
+int WebPPictureAlloc(WebPPicture* p) {
+  if (p != NULL) {
+    WebPPictureFree(p);
+    return p->use_argb ? alloc_argb(p) : alloc_yuva(p);
+  }
+  return 1;
+}
+
+void WebPPictureFree(WebPPicture* p) {
+  if (p != NULL) {
+    free(p->memory_);
+    free(p->memory_argb_);
+    reset_argb(p);
+    reset_yuva(p);
+  }
+}
+
+int WebPPictureCopy(const WebPPicture* src, WebPPicture* dst) {   /* picture_rescale_enc.c */
+  if (src == NULL || dst == NULL) return 0;
+  if (src == dst) return 1;
+  *dst = *src;
+  reset_argb(dst);
+  reset_yuva(dst);
+  if (!WebPPictureAlloc(dst)) return 0;
+  if (!src->use_argb) {
+    const int uvw = (src->width + 1) >> 1, uvh = (src->height + 1) >> 1;
+    for (int y = 0; y < src->height; ++y)
+      memcpy(dst->y + y * dst->y_stride, src->y + y * src->y_stride, src->width);
+    for (int y = 0; y < uvh; ++y) {
+      memcpy(dst->u + y * dst->uv_stride, src->u + y * src->uv_stride, uvw);
+      memcpy(dst->v + y * dst->uv_stride, src->v + y * src->uv_stride, uvw);
+    }
+    if (dst->a)
+      for (int y = 0; y < src->height; ++y)
+        memcpy(dst->a + y * dst->a_stride, src->a + y * src->a_stride, src->width);
+  } else {
+    for (int y = 0; y < src->height; ++y)
+      memcpy(dst->argb + y * dst->argb_stride, src->argb + y * src->argb_stride,
+             4 * (size_t)src->width);
+  }
+  return 1;
+}
+
+/* ---- WebPMemoryWriter (picture_enc.c:188-233) ---- */
+
+void WebPMemoryWriterInit(WebPMemoryWriter* w) {
+  w->mem = NULL;
+  w->size = 0;
+  w->max_size = 0;
+}
+
+void WebPMemoryWriterClear(WebPMemoryWriter* w) {
+  if (w != NULL) {
+    free(w->mem);
+    WebPMemoryWriterInit(w);
+  }
+}
+
+int WebPMemoryWrite(const uint8_t* data, size_t n, const WebPPicture* pic) {
+  WebPMemoryWriter* const w = (WebPMemoryWriter*)pic->custom_ptr;
+  if (w == NULL) return 1;
+  const uint64_t next = (uint64_t)w->size + n;
+  if (next > w->max_size) {
+    uint64_t cap = 2ULL * w->max_size;
+    if (cap < next) cap = next;
+    if (cap < 8192ULL) cap = 8192ULL;
+    uint8_t* m = (uint8_t*)malloc((size_t)cap);
+    if (m == NULL) return 0;
+    if (w->size > 0) memcpy(m, w->mem, w->size);
+    free(w->mem);
+    w->mem = m;
+    w->max_size = (size_t)cap;
+  }
+  if (n > 0) {
+    memcpy(w->mem + w->size, data, n);
+    w->size += n;
+  }
+  return 1;
+}
+
+/* ---- single-picture GPU engine (one cached instance per process) ---- */
+
+static pthread_mutex_t g_engine_lock = PTHREAD_MUTEX_INITIALIZER;
+static WebPGpuBatch* g_engine = NULL;
+
+static WebPGpuBatch* engine_for(const WebPConfig* cfg, int w, int h) {
+  if (g_engine && (g_engine->w != w || g_engine->h != h)) {
+    WebPGpuBatchDelete(g_engine);
+    g_engine = NULL;
+  }
+  if (!g_engine) {
+    if (WebPGpuDeviceCount() <= 0) return NULL;
+    g_engine = WebPGpuBatchNew(0, w, h, 1, cfg, 1);
+  }
+  if (g_engine) g_engine->cfg = *cfg;
+  return g_engine;
+}
+
+/* ---- import (picture_csp_enc.c:474-619, 732-844) ---- */
+
+static int import_packed(WebPPicture* pic, const uint8_t* src, int stride, int step, int swap_rb,
+                         int with_alpha) {
+  const int w = pic->width, h = pic->height;
+  if (abs(stride) < (with_alpha ? 4 : step) * w) return 0;
+  const int ri = swap_rb ? 2 : 0, bi = swap_rb ? 0 : 2;
+  if (pic->use_argb) {   /* ARGB container for the (unsupported) lossless path */
+    if (!WebPPictureAlloc(pic)) return 0;
+    for (int y = 0; y < h; ++y) {
+      const uint8_t* s = src + (size_t)y * stride;
+      for (int x = 0; x < w; ++x, s += step) {
+        const uint32_t a = with_alpha ? s[3] : 0xff;
+        pic->argb[y * pic->argb_stride + x] =
+            (a << 24) | ((uint32_t)s[ri] << 16) | ((uint32_t)s[1] << 8) | s[bi];
+      }
+    }
+    return 1;
+  }
+  /* repack to RGBA (alpha forced opaque when the source has none), convert
+   * on the GPU (K1) */
+  uint8_t* rgba = (uint8_t*)malloc((size_t)w * h * 4);
+  if (!rgba) return set_error(pic, VP8_ENC_ERROR_OUT_OF_MEMORY);
+  for (int y = 0; y < h; ++y) {
+    const uint8_t* s = src + (size_t)y * stride;
+    uint8_t* d = rgba + (size_t)y * w * 4;
+    for (int x = 0; x < w; ++x, s += step, d += 4) {
+      d[0] = s[ri]; d[1] = s[1]; d[2] = s[bi]; d[3] = with_alpha ? s[3] : 0xff;
+    }
+  }
+  pic->colorspace = WEBP_YUV420;
+  int ok = alloc_yuva(pic);
+  if (ok) {
+    pthread_mutex_lock(&g_engine_lock);
+    WebPConfig cfg;
+    WebPConfigInitInternal(&cfg, WEBP_PRESET_DEFAULT, 75.f, WEBP_ENCODER_ABI_VERSION);
+    WebPGpuBatch* e = engine_for(&cfg, w, h);
+    int has_alpha = 0;
+    ok = e != NULL && vp8g_engine_import(e, rgba, 4 * w, pic->y, pic->u, pic->v, &has_alpha);
+    pthread_mutex_unlock(&g_engine_lock);
+    if (!ok) {
+      set_error(pic, VP8_ENC_ERROR_OUT_OF_MEMORY);
+    } else if (has_alpha) {
+      /* translucent input needs the alpha-weighted import + ALPH chunk,
+       * which this build does not implement: fail loudly */
+      ok = set_error(pic, VP8_ENC_ERROR_INVALID_CONFIGURATION);
+    }
+  }
+  free(rgba);
+  return ok;
+}
+
+int WebPPictureImportRGB(WebPPicture* p, const uint8_t* s, int st) {
+  return (p && s) ? import_packed(p, s, st, 3, 0, 0) : 0;
+}
+int WebPPictureImportRGBA(WebPPicture* p, const uint8_t* s, int st) {
+  return (p && s) ? import_packed(p, s, st, 4, 0, 1) : 0;
+}
+int WebPPictureImportRGBX(WebPPicture* p, const uint8_t* s, int st) {
+  return (p && s) ? import_packed(p, s, st, 4, 0, 0) : 0;
+}
+int WebPPictureImportBGR(WebPPicture* p, const uint8_t* s, int st) {
+  return (p && s) ? import_packed(p, s, st, 3, 1, 0) : 0;
+}
+int WebPPictureImportBGRA(WebPPicture* p, const uint8_t* s, int st) {
+  return (p && s) ? import_packed(p, s, st, 4, 1, 1) : 0;
+}
+int WebPPictureImportBGRX(WebPPicture* p, const uint8_t* s, int st) {
+  return (p && s) ? import_packed(p, s, st, 4, 1, 0) : 0;
+}
+
+int WebPPictureARGBToYUVA(WebPPicture* p, WebPEncCSP csp) {   /* picture_csp_enc.c:629-656 */
+  if (p == NULL) return 0;
+  if (p->argb == NULL) return set_error(p, VP8_ENC_ERROR_NULL_PARAMETER);
+  if ((csp & WEBP_CSP_UV_MASK) != WEBP_YUV420)
+    return set_error(p, VP8_ENC_ERROR_INVALID_CONFIGURATION);
+  const int w = p->width, h = p->height;
+  uint8_t* bgra = (uint8_t*)malloc((size_t)w * h * 4);
+  if (!bgra) return set_error(p, VP8_ENC_ERROR_OUT_OF_MEMORY);
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      const uint32_t v = p->argb[y * p->argb_stride + x];
+      uint8_t* d = bgra + ((size_t)y * w + x) * 4;
+      d[0] = v & 0xff; d[1] = (v >> 8) & 0xff; d[2] = (v >> 16) & 0xff; d[3] = v >> 24;
+    }
+  void* keep_argb = p->memory_argb_;
+  uint32_t* keep_ptr = p->argb;
+  const int keep_stride = p->argb_stride;
+  p->use_argb = 0;
+  p->memory_argb_ = NULL;   /* keep ARGB alive across the YUV allocation */
+  const int ok = import_packed(p, bgra, 4 * w, 4, 1, 1);
+  p->memory_argb_ = keep_argb;
+  p->argb = keep_ptr;
+  p->argb_stride = keep_stride;
+  free(bgra);
+  return ok;
+}
+
+int WebPPictureHasTransparency(const WebPPicture* p) {   /* picture_csp_enc.c:69-81 */
+  if (p == NULL) return 0;
+  if (p->use_argb) {
+    if (p->argb == NULL) return 0;
+    for (int y = 0; y < p->height; ++y)
+      for (int x = 0; x < p->width; ++x)
+        if ((p->argb[y * p->argb_stride + x] >> 24) != 0xff) return 1;
+    return 0;
+  }
+  if (p->a == NULL) return 0;
+  for (int y = 0; y < p->height; ++y)
+    for (int x = 0; x < p->width; ++x)
+      if (p->a[y * p->a_stride + x] != 0xff) return 1;
+  return 0;
+}
+
+/* ---- WebPEncode (webp_enc.c:330-410) ---- */
+
+static int report(const WebPPicture* pic, int percent) {
+  if (pic->progress_hook && !pic->progress_hook(percent, pic))
+    return set_error(pic, VP8_ENC_ERROR_USER_ABORT);
+  return 1;
+}
+
+static double psnr(uint64_t err, uint64_t size) {
+  return (err > 0 && size > 0) ? 10. * log10(255. * 255. * size / err) : 99.;
+}
+
+int WebPEncode(const WebPConfig* config, WebPPicture* pic) {
+  if (pic == NULL) return 0;
+  pic->error_code = VP8_ENC_OK;
+  if (config == NULL) return set_error(pic, VP8_ENC_ERROR_NULL_PARAMETER);
+  if (!WebPValidateConfig(config)) return set_error(pic, VP8_ENC_ERROR_INVALID_CONFIGURATION);
+  if (!validate_picture(pic)) return 0;
+  if (pic->width > WEBP_MAX_DIMENSION || pic->height > WEBP_MAX_DIMENSION)
+    return set_error(pic, VP8_ENC_ERROR_BAD_DIMENSION);
+  if (pic->stats != NULL) memset(pic->stats, 0, sizeof(*pic->stats));
+  if (config->lossless) return set_error(pic, VP8_ENC_ERROR_INVALID_CONFIGURATION);
+  vp8h_frame probe;
+  if (!vp8h_frame_init(&probe, config, pic->width, pic->height) ||
+      (config->preprocessing & 2) || (config->preprocessing & 4))
+    return set_error(pic, VP8_ENC_ERROR_INVALID_CONFIGURATION);
+  if (pic->use_argb || pic->y == NULL || pic->u == NULL || pic->v == NULL) {
+    if (!WebPPictureARGBToYUVA(pic, WEBP_YUV420)) return 0;
+  }
+  if (pic->a != NULL && WebPPictureHasTransparency(pic))
+    return set_error(pic, VP8_ENC_ERROR_INVALID_CONFIGURATION);
+
+  pthread_mutex_lock(&g_engine_lock);
+  WebPGpuBatch* e = engine_for(config, pic->width, pic->height);
+  int ok = e != NULL;
+  if (!ok) {
+    pthread_mutex_unlock(&g_engine_lock);
+    return set_error(pic, VP8_ENC_ERROR_OUT_OF_MEMORY);
+  }
+  ok = vp8g_engine_upload_yuv(e, 0, pic->y, pic->y_stride, pic->u, pic->v, pic->uv_stride) &&
+       report(pic, 20) && vp8g_engine_run_yuv(e, 1);
+  int err = ok ? e->err[0] : VP8_ENC_ERROR_OUT_OF_MEMORY;
+  uint8_t* out = ok ? e->out[0] : NULL;
+  const size_t size = ok ? e->out_size[0] : 0;
+  if (ok) e->out[0] = NULL;   /* take ownership */
+  vp8h_frame fr;
+  vp8g_frame_result res;
+  memset(&fr, 0, sizeof(fr));
+  memset(&res, 0, sizeof(res));
+  int hdr[2] = {0, 0};
+  if (ok) {
+    fr = e->frames[0];
+    res = e->h_results[0];
+    hdr[0] = e->hdr[0];
+    hdr[1] = e->hdr[1];
+  }
+  pthread_mutex_unlock(&g_engine_lock);
+  if (pic->error_code != VP8_ENC_OK) { free(out); return 0; }
+  if (!ok || err != VP8_ENC_OK || out == NULL) {
+    free(out);
+    return set_error(pic, err != VP8_ENC_OK ? (WebPEncodingError)err : VP8_ENC_ERROR_OUT_OF_MEMORY);
+  }
+  ok = report(pic, 90) && pic->writer(out, size, pic);
+  free(out);
+  if (!ok) return pic->error_code != VP8_ENC_OK ? 0 : set_error(pic, VP8_ENC_ERROR_BAD_WRITE);
+  if (pic->stats != NULL) {   /* StoreStats, webp_enc.c:271-304 */
+    WebPAuxStats* s = pic->stats;
+    const uint64_t count = (uint64_t)fr.mbw * fr.mbh * 256;
+    s->coded_size = (int)size;
+    s->PSNR[0] = (float)psnr(res.sse[0], count);
+    s->PSNR[1] = (float)psnr(res.sse[1], count / 4);
+    s->PSNR[2] = (float)psnr(res.sse[2], count / 4);
+    s->PSNR[3] = (float)psnr(res.sse[0] + res.sse[1] + res.sse[2], count * 3 / 2);
+    s->PSNR[4] = (float)psnr(0, count);
+    for (int i = 0; i < 3; ++i) s->block_count[i] = res.block_count[i];
+    s->header_bytes[0] = hdr[0];
+    s->header_bytes[1] = hdr[1];
+    for (int i = 0; i < 4; ++i) {
+      s->segment_size[i] = fr.segment_size[i];
+      s->segment_quant[i] = fr.seg_quant[i];
+      s->segment_level[i] = fr.seg_fstrength[i];
+    }
+  }
+  return report(pic, 100);
+}
+
+/* ---- one-shot API (picture_enc.c:238-302) ---- */
+
+typedef int (*Importer)(WebPPicture*, const uint8_t*, int);
+
+static size_t encode_oneshot(const uint8_t* px, int w, int h, int stride, Importer imp, float q,
+                             uint8_t** output) {
+  WebPPicture pic;
+  WebPConfig cfg;
+  WebPMemoryWriter wrt;
+  if (output == NULL) return 0;
+  if (!WebPConfigInitInternal(&cfg, WEBP_PRESET_DEFAULT, q, WEBP_ENCODER_ABI_VERSION) ||
+      !WebPPictureInitInternal(&pic, WEBP_ENCODER_ABI_VERSION))
+    return 0;
+  pic.width = w;
+  pic.height = h;
+  pic.writer = WebPMemoryWrite;
+  pic.custom_ptr = &wrt;
+  WebPMemoryWriterInit(&wrt);
+  const int ok = imp(&pic, px, stride) && WebPEncode(&cfg, &pic);
+  WebPPictureFree(&pic);
+  if (!ok) {
+    WebPMemoryWriterClear(&wrt);
+    *output = NULL;
+    return 0;
+  }
+  *output = wrt.mem;
+  return wrt.size;
+}
+
+size_t WebPEncodeRGB(const uint8_t* p, int w, int h, int s, float q, uint8_t** o) {
+  return encode_oneshot(p, w, h, s, WebPPictureImportRGB, q, o);
+}
+size_t WebPEncodeBGR(const uint8_t* p, int w, int h, int s, float q, uint8_t** o) {
+  return encode_oneshot(p, w, h, s, WebPPictureImportBGR, q, o);
+}
+size_t WebPEncodeRGBA(const uint8_t* p, int w, int h, int s, float q, uint8_t** o) {
+  return encode_oneshot(p, w, h, s, WebPPictureImportRGBA, q, o);
+}
+size_t WebPEncodeBGRA(const uint8_t* p, int w, int h, int s, float q, uint8_t** o) {
+  return encode_oneshot(p, w, h, s, WebPPictureImportBGRA, q, o);
+}
+
+/* lossless (VP8L) is not part of this build */
+static size_t no_lossless(uint8_t** o) {
+  if (o) *o = NULL;
+  return 0;
+}
+size_t WebPEncodeLosslessRGB(const uint8_t* p, int w, int h, int s, uint8_t** o) {
+  (void)p; (void)w; (void)h; (void)s;
+  return no_lossless(o);
+}
+size_t WebPEncodeLosslessBGR(const uint8_t* p, int w, int h, int s, uint8_t** o) {
+  (void)p; (void)w; (void)h; (void)s;
+  return no_lossless(o);
+}
+size_t WebPEncodeLosslessRGBA(const uint8_t* p, int w, int h, int s, uint8_t** o) {
+  (void)p; (void)w; (void)h; (void)s;
+  return no_lossless(o);
+}
+size_t WebPEncodeLosslessBGRA(const uint8_t* p, int w, int h, int s, uint8_t** o) {
+  (void)p; (void)w; (void)h; (void)s;
+  return no_lossless(o);
+}

@@ -1,0 +1,95 @@
+/* Data layouts shared by the host C engine and the HIP kernels.
+ *
+ * HBM layout per batch (N frames of W x H, mbw = ceil(W/16), mbh = ceil(H/16)):
+ *   rgba      N x (row_stride * H)          caller-owned input
+ *   yuv       N x (W*H + 2*uvw*uvh)         Y | U | V planes, the WebPPicture
+ *                                           memory_ layout (picture_enc.c:104-162)
+ *   mb_alpha  N x nmb  uint8                analysis susceptibility (K2)
+ *   mb_uva    N x nmb  uint16               analysis uv susceptibility (K2)
+ *   segmap    N x nmb  uint8                final segment per MB (host)
+ *   params    N x vp8g_frame_params         quantisers / lambdas (host)
+ *   tokens    N x tok_cap uint16            VP8 token stream (K3), the
+ *                                           reference's token_t format
+ *                                           (token_enc.c:31-35)
+ *   mbinfo    N x nmb x VP8G_MBINFO_BYTES   modes for partition 0 (K3)
+ *   results   N x vp8g_frame_result         final probas, stats (K3)
+ */
+#ifndef LIBWEBP_AMD_VP8_GPU_H_
+#define LIBWEBP_AMD_VP8_GPU_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VP8G_NUM_SLOTS 1056        /* 4 types x 8 bands x 3 ctx x 11 probas */
+#define VP8G_MBINFO_BYTES 20       /* type, uv_mode, segment, skip, modes[16] */
+#define VP8G_MAX_TOKENS_PER_MB 7680 /* 25 blocks x 16 coeffs x 19 tokens + EOBs */
+
+/* one quantiser matrix, src/enc/vp8i_enc.h:181-187 */
+typedef struct {
+  uint16_t q[16], iq[16];
+  uint32_t bias[16], zthresh[16];
+  uint16_t sharpen[16];
+} vp8g_mtx;
+
+/* per-segment parameters, src/enc/vp8i_enc.h:189-205 */
+typedef struct {
+  vp8g_mtx y1, y2, uv;
+  int32_t lambda_i16, lambda_i4, lambda_uv, lambda_mode, tlambda, min_disto;
+  int32_t lambda_trellis_i16, lambda_trellis_i4, lambda_trellis_uv, pad0;
+} vp8g_seg;
+
+typedef struct {
+  vp8g_seg seg[4];
+  int32_t max_i4_header_bits;
+  int32_t rd_opt;        /* 1 basic (m3/m4), 2 trellis-final (m5), 3 trellis-all (m6) */
+  int32_t method;
+  int32_t use_derr;      /* U/V DC error diffusion (quality <= 98) */
+  int32_t max_count;     /* cost-refresh period (frame_enc.c:785,800) */
+  int32_t pad[3];
+} vp8g_frame_params;
+
+typedef struct {
+  uint32_t ntokens;
+  uint32_t error;        /* nonzero: token buffer overflow */
+  int32_t max_edge[4];
+  uint64_t size_p0;      /* sum of per-MB header-bit estimates (frame_enc.c:839) */
+  uint64_t sse[3];
+  int32_t block_count[3];
+  int32_t pad;
+  uint8_t probas[VP8G_NUM_SLOTS];   /* final coefficient probabilities */
+} vp8g_frame_result;
+
+/* first-error capture for diagnostics (host side, thread-local) */
+void vp8g_set_error(const char* where, const char* what);
+
+/* --- kernel launchers (HIP side, extern "C") --- */
+
+/* RGB(A)->YUV420 for n frames. g2l/l2g are DEVICE pointers to the
+ * host-computed gamma tables (picture_csp_enc.c:103-117). Sets
+ * alpha_flags[f] bit 0 if frame f has a non-0xff alpha sample. */
+int vp8g_launch_import(const uint8_t* rgba, size_t frame_stride, int row_stride,
+                       int w, int h, int n, uint8_t* yuv, size_t yuv_frame_bytes,
+                       uint32_t* alpha_flags, const uint16_t* g2l_dev,
+                       const int32_t* l2g_dev, void* stream);
+
+int vp8g_launch_analysis(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h,
+                         int n, uint8_t* mb_alpha, uint16_t* mb_uva, void* stream);
+
+int vp8g_launch_encode(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h,
+                       int n, const uint8_t* segmap,
+                       const vp8g_frame_params* params, uint16_t* tokens,
+                       size_t tok_cap, uint8_t* mbinfo,
+                       vp8g_frame_result* results, void* stream);
+
+/* synthetic syn-v1 frames straight into device memory */
+int vp8g_launch_synth(uint8_t* rgba, size_t frame_stride, int w, int h,
+                      int first_frame, int n, int seed, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

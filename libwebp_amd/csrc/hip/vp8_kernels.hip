@@ -500,6 +500,8 @@ struct K3Lds {
   uint8_t acc_out[256];          // I4 reconstruction, stride 16
   int32_t mres[4][4];
   int32_t blkinfo[32];            // per token block: type | first<<4 | ctx<<8
+  uint32_t trnz[4];               // per-mode trellis nz bits (I16 anti-diagonals)
+  uint32_t tnodes[64][32];        // per-lane trellis node scratch
   int32_t max_edge[4];
   uint8_t yl_mem[17], ul_mem[9], vl_mem[9];
   uint8_t predleft[4];
@@ -538,6 +540,91 @@ __device__ __forceinline__ int residual_cost(const K3Lds& L, int ctx0, int type,
   cost += level_cost(t, v);
   if (n < 15) cost += bit_cost(0, L.coeffs[((type * 8 + dBand[n + 1]) * 3 + (v == 1 ? 1 : 2)) * 11]);
   return cost;
+}
+
+// TrellisQuantizeBlock (quant_enc.c:593-763). c[]: natural-order DCT
+// coefficients (int16 semantics), dequantised in place; lv: zigzag levels.
+// nodes: 32 words of LDS scratch owned by the calling lane. The position
+// loops are fully unrolled so c[zz(n)] stays in registers.
+__device__ __noinline__ int trellis_quant(const K3Lds& L, uint32_t* nodes, int c[16],
+                                          int16_t* lv, int ctx0, int type,
+                                          const vp8g_mtx* m, int lambda) {
+  const int first = type == 0 ? 1 : 0;
+  const int thresh = m->q[1] * m->q[1] / 4;
+  const int last_proba = L.coeffs[((type * 8 + first) * 3 + ctx0) * 11];
+  int last = first - 1;
+#pragma unroll
+  for (int n = 0; n < 16; ++n)
+    if (n >= first && c[zz(n)] * c[zz(n)] > thresh) last = n;
+  if (last < 15) ++last;
+  score_t best_score = (score_t)bit_cost(0, last_proba) * lambda;
+  score_t sp0, sp1;
+  int tp0, tp1;   // lcost row index of each predecessor node
+  sp0 = sp1 = (score_t)(ctx0 == 0 ? bit_cost(1, last_proba) : 0) * lambda;
+  tp0 = tp1 = type * 24 + first * 3 + ctx0;
+  int bp_n = -1, bp_k = 0, bp_prev = 0;
+#pragma unroll
+  for (int n = 0; n < 16; ++n) {
+    if (n >= first && n <= last) {
+      const int j = zz(n);
+      const uint32_t Q = m->q[j], iQ = m->iq[j];
+      const int neg = c[j] < 0;
+      const uint32_t coeff0 = (uint32_t)(neg ? -c[j] : c[j]) + m->sharpen[j];
+      int level0 = (int)((coeff0 * iQ) >> QFIX);
+      int thr = (int)((coeff0 * iQ + (0x80u << (QFIX - 8))) >> QFIX);
+      if (thr > MAX_LEVEL) thr = MAX_LEVEL;
+      if (level0 > MAX_LEVEL) level0 = MAX_LEVEL;
+      const int band = dBand[n + 1];
+      score_t sc0 = MAX_COST, sc1 = MAX_COST;
+      int tc0 = 0, tc1 = 0;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int level = level0 + k;
+        const int ctx = level > 2 ? 2 : level;
+        const int tc = type * 24 + band * 3 + ctx;
+        score_t cur = MAX_COST;
+        if (level <= thr) {
+          const int new_err = (int)coeff0 - level * (int)Q;
+          const int delta = kVP8WeightTrellis[j] * (new_err * new_err - (int)(coeff0 * coeff0));
+          score_t best = sp0 + (score_t)level_cost(L.lcost[tp0], level) * lambda;
+          int bprev = 0;
+          const score_t s1 = sp1 + (score_t)level_cost(L.lcost[tp1], level) * lambda;
+          if (s1 < best) { best = s1; bprev = 1; }
+          best += (score_t)256 * delta;
+          nodes[2 * n + k] = (uint32_t)level | ((uint32_t)neg << 16) | ((uint32_t)bprev << 17);
+          cur = best;
+          if (level != 0 && best < best_score) {
+            const score_t lc =
+                (n < 15) ? bit_cost(0, L.coeffs[((type * 8 + band) * 3 + ctx) * 11]) : 0;
+            const score_t sc = best + lc * lambda;
+            if (sc < best_score) { best_score = sc; bp_n = n; bp_k = k; bp_prev = bprev; }
+          }
+        }
+        if (k == 0) { sc0 = cur; tc0 = tc; } else { sc1 = cur; tc1 = tc; }
+      }
+      sp0 = sc0; sp1 = sc1; tp0 = tc0; tp1 = tc1;
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < 16; ++n) {
+    if (n >= first) { c[zz(n)] = 0; lv[n] = 0; }
+  }
+  if (bp_n < 0) return 0;
+  nodes[2 * bp_n + bp_k] = (nodes[2 * bp_n + bp_k] & ~(1u << 17)) | ((uint32_t)bp_prev << 17);
+  int nz = 0, node = bp_k;
+#pragma unroll
+  for (int n = 15; n >= 0; --n) {
+    if (n <= bp_n && n >= first) {
+      const uint32_t nd = nodes[2 * n + node];
+      const int level = (int)(nd & 0xffff);
+      const int v = (nd >> 16) & 1 ? -level : level;
+      lv[n] = (int16_t)v;
+      nz |= level;
+      c[zz(n)] = (int16_t)(v * (int)m->q[zz(n)]);
+      node = (nd >> 17) & 1;
+    }
+  }
+  return nz != 0;
 }
 
 // FinalizeTokenProbas (frame_enc.c:146-180): returns "changed" (dirty)
@@ -679,6 +766,316 @@ __device__ __forceinline__ const int16_t* blk_levels(const K3Lds& L, int k) {
   return k == 0 ? L.fin_dc : (k <= 16 ? L.fin_ac[k - 1] : L.fin_uv[k - 17]);
 }
 
+// I16 candidates: lane = mode*16 + block (quant_enc.c:772-822,
+// cost_enc.c:232-256). Fills rec16 / lv16 / lvdc and
+// mres[m] = {SSE, texture distortion, rate, nz (ac bits | dc << 24)}.
+// With trellis (m6 search, m5 final pass) the AC blocks are trellis-quantised
+// in anti-diagonal waves so each block sees its top/left neighbours' nz.
+__device__ void eval_i16(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane, bool trellis) {
+  const int m = lane >> 4, b = lane & 15, bx = b & 3, by = b >> 2;
+  int c[16];
+  const uint8_t* src = L.yin + by * 4 * BPS + bx * 4;
+  const uint8_t* ref = L.p16[m] + by * 64 + bx * 4;
+  fdct4(src, BPS, ref, 16, c);
+  L.dcs[m][b] = (int16_t)c[0];
+  if (lane < 4) L.trnz[lane] = 0;
+  __syncthreads();
+  {   // WHT coefficient b of mode m, quantised with y2 (natural index b)
+    const int16_t* d = L.dcs[m];
+    const int r = b >> 2, col = b & 3;
+    int t0[4];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int a0 = d[4 * rr + 0] + d[4 * rr + 2], a1 = d[4 * rr + 1] + d[4 * rr + 3];
+      const int a2 = d[4 * rr + 1] - d[4 * rr + 3], a3 = d[4 * rr + 0] - d[4 * rr + 2];
+      t0[rr] = col == 0 ? a0 + a1 : col == 1 ? a3 + a2 : col == 2 ? a3 - a2 : a0 - a1;
+    }
+    const int a0 = t0[0] + t0[2], a1 = t0[1] + t0[3], a2 = t0[1] - t0[3], a3 = t0[0] - t0[2];
+    int v = r == 0 ? a0 + a1 : r == 1 ? a3 + a2 : r == 2 ? a3 - a2 : a0 - a1;
+    v = (int16_t)(v >> 1);
+    const vp8g_mtx& M = S.y2;
+    const int neg = v < 0;
+    const uint32_t coeff = (uint32_t)(neg ? -v : v) + M.sharpen[b];
+    int level = 0;
+    if (coeff > M.zthresh[b]) {
+      level = (int)((coeff * M.iq[b] + M.bias[b]) >> QFIX);
+      if (level > MAX_LEVEL) level = MAX_LEVEL;
+      if (neg) level = -level;
+    }
+    L.lvdc[m][dZzInv[b]] = (int16_t)level;
+    L.whtq[m][b] = (int16_t)(level * (int)M.q[b]);
+  }
+  int nzb = 0;
+  if (trellis) {   // quant_enc.c:790-803
+    for (int st = 0; st < 7; ++st) {
+      if (bx + by == st) {
+        const uint32_t tm = L.trnz[m];
+        const int tc = by == 0 ? ctx.top(bx) : (int)((tm >> (b - 4)) & 1);
+        const int lc = bx == 0 ? ctx.left(by) : (int)((tm >> (b - 1)) & 1);
+        nzb = trellis_quant(L, L.tnodes[lane], c, L.lv16[m][b], tc + lc, 0, &S.y1,
+                            S.lambda_trellis_i16);
+        L.lv16[m][b][0] = 0;
+        if (nzb) atomicOr(&L.trnz[m], 1u << b);
+      }
+      __syncthreads();
+    }
+  } else {         // quant_enc.c:805-812: DC position zeroed first
+    c[0] = 0;
+    nzb = quantize_block(c, L.lv16[m][b], &S.y1);
+  }
+  __syncthreads();
+  {   // inverse WHT -> DC of block b (dec.c:137-162)
+    const int16_t* q = L.whtq[m];
+    const int r = b >> 2, col = b & 3;
+    int t[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int a0 = q[i] + q[12 + i], a1 = q[4 + i] + q[8 + i];
+      const int a2 = q[4 + i] - q[8 + i], a3 = q[i] - q[12 + i];
+      t[i] = r == 0 ? a0 + a1 : r == 1 ? a3 + a2 : r == 2 ? a0 - a1 : a3 - a2;
+    }
+    const int dd = t[0] + 3;
+    const int a0 = dd + t[3], a1 = t[1] + t[2], a2 = t[1] - t[2], a3 = dd - t[3];
+    c[0] = (int16_t)((col == 0 ? a0 + a1 : col == 1 ? a3 + a2 : col == 2 ? a0 - a1 : a3 - a2) >> 3);
+  }
+  idct4(ref, 16, c, L.rec16[m] + by * 64 + bx * 4, 16);
+  __syncthreads();
+  const uint8_t* rec = L.rec16[m] + by * 64 + bx * 4;
+  int d = sse4(src, BPS, rec, 16);
+  int td = iabs_(hadamard_w(rec, 16) - hadamard_w(src, BPS)) >> 5;
+  const uint64_t nzmask_all = __ballot(nzb);
+  const uint32_t nzm = (uint32_t)(nzmask_all >> (16 * m)) & 0xffff;
+  const int tctx = by == 0 ? ctx.top(bx) : (int)((nzm >> (b - 4)) & 1);
+  const int lctx = bx == 0 ? ctx.left(by) : (int)((nzm >> (b - 1)) & 1);
+  int r = residual_cost(L, tctx + lctx, 0, 1, L.lv16[m][b]);
+  int dcnz = 0;
+  for (int k = 0; k < 16; ++k) dcnz |= L.lvdc[m][k];
+  if (b == 0) r += residual_cost(L, ctx.top(8) + ctx.left(8), 1, 0, L.lvdc[m]);
+#pragma unroll
+  for (int off = 8; off >= 1; off >>= 1) {
+    d += __shfl_xor(d, off, 16);
+    td += __shfl_xor(td, off, 16);
+    r += __shfl_xor(r, off, 16);
+  }
+  if (b == 0) {
+    L.mres[m][0] = d;
+    L.mres[m][1] = td;
+    L.mres[m][2] = r;
+    L.mres[m][3] = (int)(nzm | (dcnz ? (1u << 24) : 0u));
+  }
+  __syncthreads();
+}
+
+// UV candidates: lane = mode*8 + block, lanes 0..31 (quant_enc.c:875-969,
+// cost_enc.c:258-278). Fills recuv / lvuv / uvderr and
+// mres[m] = {SSE, rate, non-zero AC count, nz bits}.
+__device__ void eval_uv(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane, int x,
+                        const int8_t* topderr, int use_derr) {
+  int d = 0, r = 0, flatc = 0, nzb = 0;
+  const int m = lane >> 3, b = lane & 7;
+  int c[16];
+  const int ch = b >> 2, k4 = b & 3;
+  const uint8_t* src = L.yin + 16 + 8 * ch + (k4 >> 1) * 4 * BPS + (k4 & 1) * 4;
+  const uint8_t* ref = L.puv[m & 3] + 8 * ch + (k4 >> 1) * 64 + (k4 & 1) * 4;
+  if (lane < 32) {
+    fdct4(src, BPS, ref, 16, c);
+    L.uvdc[m][b] = (int16_t)c[0];
+  }
+  __syncthreads();
+  if (use_derr && lane < 8) {   // CorrectDCValues per (mode, channel)
+    const int mm = lane >> 1, cch = lane & 1;
+    const vp8g_mtx& M = S.uv;
+    const int8_t* top = topderr + 4 * x + 2 * cch;
+    const int8_t* left = L.lderr[cch];
+    int16_t* cc = &L.uvdc[mm][4 * cch];
+    int err[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      int add;
+      if (k == 0) add = (7 * top[0] + 8 * left[0]) >> 3;
+      else if (k == 1) add = (7 * top[1] + 8 * err[0]) >> 3;
+      else if (k == 2) add = (7 * err[0] + 8 * left[1]) >> 3;
+      else add = (7 * err[1] + 8 * err[2]) >> 3;
+      int V = (int16_t)(cc[k] + add);
+      const int neg = V < 0;
+      if (neg) V = -V;
+      if (V > (int)M.zthresh[0]) {
+        const int qV = (int)(((uint32_t)V * M.iq[0] + M.bias[0]) >> QFIX) * M.q[0];
+        const int e = V - qV;
+        cc[k] = (int16_t)(neg ? -qV : qV);
+        err[k] = (neg ? -e : e) >> 1;
+      } else {
+        cc[k] = 0;
+        err[k] = (neg ? -V : V) >> 1;
+      }
+    }
+    L.uvderr[mm][cch][0] = (int8_t)err[1];
+    L.uvderr[mm][cch][1] = (int8_t)err[2];
+    L.uvderr[mm][cch][2] = (int8_t)err[3];
+  }
+  __syncthreads();
+  if (lane < 32) {
+    c[0] = L.uvdc[m][b];
+    nzb = quantize_block(c, L.lvuv[m][b], &S.uv);
+    idct4(ref, 16, c, L.recuv[m] + 8 * ch + (k4 >> 1) * 64 + (k4 & 1) * 4, 16);
+  }
+  __syncthreads();
+  const uint64_t nzall = __ballot(lane < 32 && nzb);
+  if (lane < 32) {
+    const uint8_t* rec = L.recuv[m] + 8 * ch + (k4 >> 1) * 64 + (k4 & 1) * 4;
+    d = sse4(src, BPS, rec, 16);
+    const uint32_t nzm = (uint32_t)(nzall >> (8 * m)) & 0xff;
+    const int bxx = k4 & 1, byy = k4 >> 1;
+    const int tctx = byy == 0 ? ctx.top(4 + 2 * ch + bxx) : (int)((nzm >> (b - 2)) & 1);
+    const int lctx = bxx == 0 ? ctx.left(4 + 2 * ch + byy) : (int)((nzm >> (b - 1)) & 1);
+    r = residual_cost(L, tctx + lctx, 2, 0, L.lvuv[m][b]);
+    for (int i = 1; i < 16; ++i) flatc += L.lvuv[m][b][i] != 0;
+#pragma unroll
+    for (int off = 4; off >= 1; off >>= 1) {
+      d += __shfl_xor(d, off, 8);
+      r += __shfl_xor(r, off, 8);
+      flatc += __shfl_xor(flatc, off, 8);
+    }
+    if (b == 0) {
+      L.mres[m][0] = d; L.mres[m][1] = r; L.mres[m][2] = flatc; L.mres[m][3] = (int)nzm;
+    }
+  }
+  __syncthreads();
+}
+
+struct I4Result {
+  int ok;
+  score_t H, score;
+  uint32_t nz;
+};
+
+// Intra4 sub-block loop (quant_enc.c:1072-1165). search: RD mode choice with
+// the reference's early-outs; !search: the m5 SimpleQuantize pass over the
+// already chosen L.modes (quant_enc.c:1230-1240), whose trellis contexts are
+// the macroblock-boundary flags only (the reference never updates them
+// inside that loop). Reconstruction lands in acc_out, levels in acc_ac.
+__device__ I4Result run_i4(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane, int x,
+                           int mbw, const uint8_t* predtop, const uint8_t* yl,
+                           const uint8_t* yt, bool search, bool trellis, score_t rd_score,
+                           int max_bits) {
+  for (int k = lane; k < 21; k += 64) {
+    uint8_t v;
+    if (k == 0) v = yl[-1];
+    else if (k <= 16) v = yt[k - 1];
+    else v = (x < mbw - 1) ? yt[16 + k - 17] : yt[15];
+    L.canvas[0][k] = v;
+  }
+  if (lane < 16) L.canvas[1 + lane][0] = yl[lane];
+  uint32_t tnz = ctx.t & 0xf, lnz = ctx.l & 0xf;
+  score_t accD = 0, accSD = 0, accR = 0, accH = 211;
+  score_t acc_score = accH * S.lambda_mode;
+  uint32_t acc_nz = 0;
+  int total_hdr = 0;
+  I4Result res;
+  res.ok = 1;
+  __syncthreads();
+  for (int i4 = 0; i4 < 16; ++i4) {
+    const int bx = i4 & 3, by = i4 >> 2;
+    const int left_m = bx == 0 ? L.predleft[by] : L.modes[i4 - 1];
+    const int top_m = by == 0 ? predtop[4 * x + bx] : L.modes[i4 - 4];
+    if (lane < 13) {   // edges e[0..12] = L K J I X A..D E..H
+      const int r = 4 * by, cc = 4 * bx;
+      uint8_t v;
+      if (lane < 4) v = L.canvas[r + 4 - lane][cc];
+      else if (lane == 4) v = L.canvas[r][cc];
+      else if (lane < 9) v = L.canvas[r][cc + 1 + (lane - 5)];
+      else v = (by > 0 && bx == 3) ? L.canvas[0][17 + lane - 9] : L.canvas[r][cc + 5 + lane - 9];
+      L.edges[lane] = v;
+    }
+    __syncthreads();
+    for (int k = lane; k < 160; k += 64) {
+      const int m = k >> 4, p = k & 15;
+      const P4Op op = kP4[m][p];
+      const uint8_t* e = L.edges;
+      int v;
+      if (op.kind == 0) v = (e[op.a] + 2 * e[op.b] + e[op.c] + 2) >> 2;
+      else if (op.kind == 1) v = (e[op.a] + e[op.b] + 1) >> 1;
+      else if (op.kind == 2) v = e[op.a];
+      else if (op.kind == 3) v = clip8(e[5 + (p & 3)] + e[3 - (p >> 2)] - e[4]);
+      else v = (4 + e[0] + e[1] + e[2] + e[3] + e[5] + e[6] + e[7] + e[8]) >> 3;
+      L.pred4[m][p] = (uint8_t)v;
+    }
+    __syncthreads();
+    if (lane < 10) {
+      const int m = lane;
+      const uint8_t* src = L.yin + by * 4 * BPS + bx * 4;
+      int c[16];
+      fdct4(src, BPS, L.pred4[m], 4, c);
+      const int ctx4 = (int)((tnz >> bx) & 1) + (int)((lnz >> by) & 1);
+      const int nz = trellis ? trellis_quant(L, L.tnodes[lane], c, L.lv4[m], ctx4, 3, &S.y1,
+                                             S.lambda_trellis_i4)
+                             : quantize_block(c, L.lv4[m], &S.y1);
+      idct4(L.pred4[m], 4, c, L.rec4[m], 4);
+      if (search) {
+        const int D = sse4(src, BPS, L.rec4[m], 4);
+        const int SD = S.tlambda ? (S.tlambda * (iabs_(hadamard_w(L.rec4[m], 4) -
+                                                        hadamard_w(src, BPS)) >> 5) + 128) >> 8
+                                 : 0;
+        int cntnz = 0;
+        for (int i = 1; i < 16; ++i) cntnz += L.lv4[m][i] != 0;
+        const int R0 = (m > 0 && cntnz <= 3) ? 140 : 0;
+        const int Rc = residual_cost(L, ctx4, 3, 0, L.lv4[m]);
+        L.r4[m][0] = D; L.r4[m][1] = SD; L.r4[m][2] = kVP8ModeCostI4[top_m][left_m][m];
+        L.r4[m][3] = R0; L.r4[m][4] = Rc;
+      }
+      L.r4[m][5] = nz;
+    }
+    __syncthreads();
+    int bm;
+    int bnz;
+    if (search) {
+      bm = -1;
+      score_t bscore = MAX_COST, bD = 0, bSD = 0, bR = 0, bH = 0;
+      bnz = 0;
+      for (int m = 0; m < 10; ++m) {
+        const score_t D = L.r4[m][0], SD = L.r4[m][1], H = L.r4[m][2];
+        score_t R = L.r4[m][3];
+        score_t sc = (R + H) * S.lambda_i4 + 256 * (D + SD);
+        if (bm >= 0 && sc >= bscore) continue;
+        R += L.r4[m][4];
+        sc = (R + H) * S.lambda_i4 + 256 * (D + SD);
+        if (bm < 0 || sc < bscore) {
+          bm = m; bscore = sc; bD = D; bSD = SD; bR = R; bH = H; bnz = L.r4[m][5];
+        }
+      }
+      const score_t bsm = (bR + bH) * S.lambda_mode + 256 * (bD + bSD);
+      accD += bD; accSD += bSD; accR += bR; accH += bH; acc_score += bsm;
+      acc_nz |= (uint32_t)(bnz ? 1 : 0) << i4;
+      if (acc_score >= rd_score) { res.ok = 0; break; }
+      total_hdr += (int)bH;
+      if (total_hdr > max_bits) { res.ok = 0; break; }
+    } else {
+      bm = L.modes[i4];
+      bnz = L.r4[bm][5];
+      acc_nz |= (uint32_t)(bnz ? 1 : 0) << i4;
+    }
+    if (lane < 16) {
+      const int py = lane >> 2, px = lane & 3;
+      const uint8_t v = L.rec4[bm][lane];
+      L.canvas[4 * by + 1 + py][4 * bx + 1 + px] = v;
+      L.acc_out[(4 * by + py) * 16 + 4 * bx + px] = v;
+      L.acc_ac[i4][lane] = L.lv4[bm][lane];
+    }
+    if (search) {
+      if (lane == 0) L.modes[i4] = (uint8_t)bm;
+      tnz = (tnz & ~(1u << bx)) | ((bnz ? 1u : 0u) << bx);
+      lnz = (lnz & ~(1u << by)) | ((bnz ? 1u : 0u) << by);
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  res.H = accH;
+  res.score = acc_score;
+  res.nz = acc_nz;
+  (void)accD; (void)accSD; (void)accR;
+  return res;
+}
+
 struct K3Args {
   const uint8_t* yuv;
   size_t yfb;
@@ -789,100 +1186,18 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
     }
     __syncthreads();
 
-    // ---- Intra16 (quant_enc.c:772-822, 1002-1058)
-    score_t best16_score;
-    int best16;
-    uint32_t nz16;
-    score_t D16, SD16, H16, R16;
+    // ---- Intra16 (quant_enc.c:1002-1058)
+    const bool trellis_all = rd_opt >= 3;
+    eval_i16(L, S, ctx, lane, trellis_all);
+    score_t best16_score = 0;
+    int best16 = 0;
+    uint32_t nz16 = 0;
+    score_t D16 = 0, SD16 = 0, H16 = 0, R16 = 0;
     {
-      const int m = lane >> 4, b = lane & 15, bx = b & 3, by = b >> 2;
-      int c[16];
-      const uint8_t* src = L.yin + by * 4 * BPS + bx * 4;
-      const uint8_t* ref = L.p16[m] + by * 64 + bx * 4;
-      fdct4(src, BPS, ref, 16, c);
-      L.dcs[m][b] = (int16_t)c[0];
-      __syncthreads();
-      {   // WHT coefficient b of mode m, quantised with y2 (natural index b)
-        const int16_t* d = L.dcs[m];
-        const int r = b >> 2, col = b & 3;
-        int t0[4];
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int a0 = d[4 * rr + 0] + d[4 * rr + 2], a1 = d[4 * rr + 1] + d[4 * rr + 3];
-          const int a2 = d[4 * rr + 1] - d[4 * rr + 3], a3 = d[4 * rr + 0] - d[4 * rr + 2];
-          t0[rr] = col == 0 ? a0 + a1 : col == 1 ? a3 + a2 : col == 2 ? a3 - a2 : a0 - a1;
-        }
-        const int a0 = t0[0] + t0[2], a1 = t0[1] + t0[3], a2 = t0[1] - t0[3], a3 = t0[0] - t0[2];
-        int v = r == 0 ? a0 + a1 : r == 1 ? a3 + a2 : r == 2 ? a3 - a2 : a0 - a1;
-        v = (int16_t)(v >> 1);
-        const vp8g_mtx& M = S.y2;
-        const int neg = v < 0;
-        const uint32_t coeff = (uint32_t)(neg ? -v : v) + M.sharpen[b];
-        int level = 0;
-        if (coeff > M.zthresh[b]) {
-          level = (int)((coeff * M.iq[b] + M.bias[b]) >> QFIX);
-          if (level > MAX_LEVEL) level = MAX_LEVEL;
-          if (neg) level = -level;
-        }
-        L.lvdc[m][dZzInv[b]] = (int16_t)level;
-        L.whtq[m][b] = (int16_t)(level * (int)M.q[b]);
-      }
-      // AC quantisation of own block with DC zeroed (quant_enc.c:805-812)
-      c[0] = 0;
-      const int nzb = quantize_block(c, L.lv16[m][b], &S.y1);
-      __syncthreads();
-      {   // inverse WHT -> DC of block b (dec.c:137-162)
-        const int16_t* q = L.whtq[m];
-        const int r = b >> 2, col = b & 3;
-        int t[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int a0 = q[i] + q[12 + i], a1 = q[4 + i] + q[8 + i];
-          const int a2 = q[4 + i] - q[8 + i], a3 = q[i] - q[12 + i];
-          t[i] = r == 0 ? a0 + a1 : r == 1 ? a3 + a2 : r == 2 ? a0 - a1 : a3 - a2;
-        }
-        // t[i] = tmp[4*r + i]; second pass uses row r of tmp
-        const int dd = t[0] + 3;
-        const int a0 = dd + t[3], a1 = t[1] + t[2], a2 = t[1] - t[2], a3 = dd - t[3];
-        c[0] = (int16_t)((col == 0 ? a0 + a1 : col == 1 ? a3 + a2 : col == 2 ? a0 - a1 : a3 - a2) >> 3);
-      }
-      idct4(ref, 16, c, L.rec16[m] + by * 64 + bx * 4, 16);
-      __syncthreads();
-      const uint8_t* rec = L.rec16[m] + by * 64 + bx * 4;
-      int d = sse4(src, BPS, rec, 16);
-      int td = iabs_(hadamard_w(rec, 16) - hadamard_w(src, BPS)) >> 5;
-      const uint64_t nzmask_all = __ballot(nzb);
-      const uint32_t nzm = (uint32_t)(nzmask_all >> (16 * m)) & 0xffff;
-      const int tctx = by == 0 ? ctx.top(bx) : ((nzm >> (b - 4)) & 1);
-      const int lctx = bx == 0 ? ctx.left(by) : ((nzm >> (b - 1)) & 1);
-      int r = residual_cost(L, tctx + lctx, 0, 1, L.lv16[m][b]);
-      int dcnz = 0;
-      for (int k = 0; k < 16; ++k) dcnz |= L.lvdc[m][k];
-      if (b == 0) r += residual_cost(L, ctx.top(8) + ctx.left(8), 1, 0, L.lvdc[m]);
-      // reduce over the 16 lanes of this mode
-#pragma unroll
-      for (int off = 8; off >= 1; off >>= 1) {
-        d += __shfl_xor(d, off, 16);
-        td += __shfl_xor(td, off, 16);
-        r += __shfl_xor(r, off, 16);
-      }
-      if (b == 0) {
-        L.mres[m][0] = d;
-        L.mres[m][1] = td;
-        L.mres[m][2] = r;
-        L.mres[m][3] = (int)(nzm | (dcnz ? (1u << 24) : 0u));
-      }
-      __syncthreads();
-      // sequential mode choice, identical in every lane
-      int flat = 1;
-      {
-        const int v0 = L.yin[0];
-        int same = 1;
-        for (int k = lane; k < 256; k += 64) same &= (L.yin[(k >> 4) * BPS + (k & 15)] == v0);
-        flat = __all(same);
-      }
-      best16 = 0;
-      best16_score = 0;
+      int same = 1;
+      const int v0 = L.yin[0];
+      for (int k = lane; k < 256; k += 64) same &= (L.yin[(k >> 4) * BPS + (k & 15)] == v0);
+      int flat = __all(same);
       for (int mm = 0; mm < 4; ++mm) {
         score_t Dm = L.mres[mm][0];
         score_t SDm = S.tlambda ? (score_t)((S.tlambda * L.mres[mm][1] + 128) >> 8) : 0;
@@ -905,7 +1220,7 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
     for (int k = lane; k < 256; k += 64) (&L.fin_ac[0][0])[k] = (&L.lv16[best16][0][0])[k];
     if (lane < 16) { L.fin_dc[lane] = L.lvdc[best16][lane]; L.modes[lane] = best16; }
     score_t rd_score = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
-    score_t rdD = D16, rdSD = SD16, rdH = H16, rdR = R16;
+    score_t rdH = H16;
     uint32_t rd_nz = nz16;
     int is_i16 = 1;
     if ((rd_nz & 0x100ffff) == 0x1000000 && D16 > S.min_disto) {
@@ -918,198 +1233,37 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
 
     // ---- Intra4 (quant_enc.c:1072-1165)
     if (max_i4_bits > 0) {
-      // canvas: row 0 = corner + top + top-right, col 0 = left
-      for (int k = lane; k < 21; k += 64) {
-        uint8_t v;
-        if (k == 0) v = yl[-1];
-        else if (k <= 16) v = yt[k - 1];
-        else v = (x < mbw - 1) ? yt[16 + k - 17] : yt[15];
-        L.canvas[0][k] = v;
-      }
-      if (lane < 16) L.canvas[1 + lane][0] = yl[lane];
-      uint32_t tnz = ctx.t & 0xf, lnz = ctx.l & 0xf;
-      score_t accD = 0, accSD = 0, accR = 0, accH = 211, acc_score;
-      uint32_t acc_nz = 0;
-      acc_score = accH * S.lambda_mode;
-      int total_hdr = 0;
-      int ok4 = 1;
-      __syncthreads();
-      for (int i4 = 0; i4 < 16 && ok4; ++i4) {
-        const int bx = i4 & 3, by = i4 >> 2;
-        const int left_m = bx == 0 ? L.predleft[by] : L.modes[i4 - 1];
-        const int top_m = by == 0 ? predtop[4 * x + bx] : L.modes[i4 - 4];
-        // edges e[0..12] = L K J I X A..D E..H
-        if (lane < 13) {
-          const int r = 4 * by, cc = 4 * bx;
-          uint8_t v;
-          if (lane < 4) v = L.canvas[r + 4 - lane][cc];
-          else if (lane == 4) v = L.canvas[r][cc];
-          else if (lane < 9) v = L.canvas[r][cc + 1 + (lane - 5)];
-          else v = (by > 0 && bx == 3) ? L.canvas[0][17 + lane - 9] : L.canvas[r][cc + 5 + lane - 9];
-          L.edges[lane] = v;
-        }
-        __syncthreads();
-        for (int k = lane; k < 160; k += 64) {
-          const int m = k >> 4, p = k & 15;
-          const P4Op op = kP4[m][p];
-          const uint8_t* e = L.edges;
-          int v;
-          if (op.kind == 0) v = (e[op.a] + 2 * e[op.b] + e[op.c] + 2) >> 2;
-          else if (op.kind == 1) v = (e[op.a] + e[op.b] + 1) >> 1;
-          else if (op.kind == 2) v = e[op.a];
-          else if (op.kind == 3) v = clip8(e[5 + (p & 3)] + e[3 - (p >> 2)] - e[4]);
-          else v = (4 + e[0] + e[1] + e[2] + e[3] + e[5] + e[6] + e[7] + e[8]) >> 3;
-          L.pred4[m][p] = (uint8_t)v;
-        }
-        __syncthreads();
-        if (lane < 10) {
-          const int m = lane;
-          const uint8_t* src = L.yin + by * 4 * BPS + bx * 4;
-          int c[16];
-          fdct4(src, BPS, L.pred4[m], 4, c);
-          const int nz = quantize_block(c, L.lv4[m], &S.y1);
-          idct4(L.pred4[m], 4, c, L.rec4[m], 4);
-          const int D = sse4(src, BPS, L.rec4[m], 4);
-          const int SD = S.tlambda ? (S.tlambda * (iabs_(hadamard_w(L.rec4[m], 4) -
-                                                          hadamard_w(src, BPS)) >> 5) + 128) >> 8
-                                   : 0;
-          int cntnz = 0;
-          for (int i = 1; i < 16; ++i) cntnz += L.lv4[m][i] != 0;
-          const int R0 = (m > 0 && cntnz <= 3) ? 140 : 0;
-          const int Rc = residual_cost(L, ((tnz >> bx) & 1) + ((lnz >> by) & 1), 3, 0, L.lv4[m]);
-          L.r4[m][0] = D; L.r4[m][1] = SD; L.r4[m][2] = kVP8ModeCostI4[top_m][left_m][m];
-          L.r4[m][3] = R0; L.r4[m][4] = Rc; L.r4[m][5] = nz;
-        }
-        __syncthreads();
-        int bm = -1;
-        score_t bscore = MAX_COST, bD = 0, bSD = 0, bR = 0, bH = 0;
-        int bnz = 0;
-        for (int m = 0; m < 10; ++m) {
-          const score_t D = L.r4[m][0], SD = L.r4[m][1], H = L.r4[m][2];
-          score_t R = L.r4[m][3];
-          score_t sc = (R + H) * S.lambda_i4 + 256 * (D + SD);
-          if (bm >= 0 && sc >= bscore) continue;
-          R += L.r4[m][4];
-          sc = (R + H) * S.lambda_i4 + 256 * (D + SD);
-          if (bm < 0 || sc < bscore) {
-            bm = m; bscore = sc; bD = D; bSD = SD; bR = R; bH = H; bnz = L.r4[m][5];
-          }
-        }
-        const score_t bsm = (bR + bH) * S.lambda_mode + 256 * (bD + bSD);
-        accD += bD; accSD += bSD; accR += bR; accH += bH; acc_score += bsm;
-        acc_nz |= (uint32_t)(bnz ? 1 : 0) << i4;
-        if (acc_score >= rd_score) { ok4 = 0; break; }
-        total_hdr += (int)bH;
-        if (total_hdr > max_i4_bits) { ok4 = 0; break; }
-        if (lane < 16) {
-          const int py = lane >> 2, px = lane & 3;
-          const uint8_t v = L.rec4[bm][lane];
-          L.canvas[4 * by + 1 + py][4 * bx + 1 + px] = v;
-          L.acc_out[(4 * by + py) * 16 + 4 * bx + px] = v;
-          L.acc_ac[i4][lane] = L.lv4[bm][lane];
-        }
-        if (lane == 0) L.modes[i4] = (uint8_t)bm;
-        tnz = (tnz & ~(1u << bx)) | ((bnz ? 1u : 0u) << bx);
-        lnz = (lnz & ~(1u << by)) | ((bnz ? 1u : 0u) << by);
-        __syncthreads();
-      }
-      __syncthreads();
-      if (ok4) {
+      I4Result r4 = run_i4(L, S, ctx, lane, x, mbw, predtop, yl, yt, true, trellis_all,
+                           rd_score, max_i4_bits);
+      if (r4.ok) {
         is_i16 = 0;
-        rdD = accD; rdSD = accSD; rdR = accR; rdH = accH; rd_score = acc_score;
-        rd_nz = acc_nz;
+        rdH = r4.H;
+        rd_score = r4.score;
+        rd_nz = r4.nz;
         for (int k = lane; k < 256; k += 64) {
           L.yout[(k >> 4) * BPS + (k & 15)] = L.acc_out[k];
           (&L.fin_ac[0][0])[k] = (&L.acc_ac[0][0])[k];
         }
       } else {
-        if (lane < 16) L.modes[lane] = best16;   // restore (early exit wrote some)
+        if (lane < 16) L.modes[lane] = best16;   // the aborted search wrote some
       }
       __syncthreads();
     }
 
-    // ---- UV (quant_enc.c:875-969, 1169-1217)
+    // ---- UV (quant_enc.c:1169-1217)
+    int bu = 0;
     {
-      int d = 0, r = 0, flatc = 0, nzb = 0;
-      const int m = lane >> 3, b = lane & 7;
-      int c[16];
-      const int ch = b >> 2, k4 = b & 3;
-      const uint8_t* src = L.yin + 16 + 8 * ch + (k4 >> 1) * 4 * BPS + (k4 & 1) * 4;
-      const uint8_t* ref = L.puv[m & 3] + 8 * ch + (k4 >> 1) * 64 + (k4 & 1) * 4;
-      if (lane < 32) {
-        fdct4(src, BPS, ref, 16, c);
-        L.uvdc[m][b] = (int16_t)c[0];
-      }
-      __syncthreads();
-      if (use_derr && lane < 8) {   // CorrectDCValues per (mode, channel)
-        const int mm = lane >> 1, cch = lane & 1;
-        const vp8g_mtx& M = S.uv;
-        const int8_t* top = topderr + 4 * x + 2 * cch;
-        const int8_t* left = L.lderr[cch];
-        int16_t* cc = &L.uvdc[mm][4 * cch];
-        int err[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          int add;
-          if (k == 0) add = (7 * top[0] + 8 * left[0]) >> 3;
-          else if (k == 1) add = (7 * top[1] + 8 * err[0]) >> 3;
-          else if (k == 2) add = (7 * err[0] + 8 * left[1]) >> 3;
-          else add = (7 * err[1] + 8 * err[2]) >> 3;
-          int V = (int16_t)(cc[k] + add);
-          const int neg = V < 0;
-          if (neg) V = -V;
-          if (V > (int)M.zthresh[0]) {
-            const int qV = (int)(((uint32_t)V * M.iq[0] + M.bias[0]) >> QFIX) * M.q[0];
-            const int e = V - qV;
-            cc[k] = (int16_t)(neg ? -qV : qV);
-            err[k] = (neg ? -e : e) >> 1;
-          } else {
-            cc[k] = 0;
-            err[k] = (neg ? -V : V) >> 1;
-          }
-        }
-        L.uvderr[mm][cch][0] = (int8_t)err[1];
-        L.uvderr[mm][cch][1] = (int8_t)err[2];
-        L.uvderr[mm][cch][2] = (int8_t)err[3];
-      }
-      __syncthreads();
-      if (lane < 32) {
-        c[0] = L.uvdc[m][b];
-        nzb = quantize_block(c, L.lvuv[m][b], &S.uv);
-        idct4(ref, 16, c, L.recuv[m] + 8 * ch + (k4 >> 1) * 64 + (k4 & 1) * 4, 16);
-      }
-      __syncthreads();
-      const uint64_t nzall = __ballot(lane < 32 && nzb);
-      if (lane < 32) {
-        const uint8_t* rec = L.recuv[m] + 8 * ch + (k4 >> 1) * 64 + (k4 & 1) * 4;
-        d = sse4(src, BPS, rec, 16);
-        const uint32_t nzm = (uint32_t)(nzall >> (8 * m)) & 0xff;
-        const int bxx = k4 & 1, byy = k4 >> 1;
-        const int tctx = byy == 0 ? ctx.top(4 + 2 * ch + bxx) : ((nzm >> (b - 2)) & 1);
-        const int lctx = bxx == 0 ? ctx.left(4 + 2 * ch + byy) : ((nzm >> (b - 1)) & 1);
-        r = residual_cost(L, tctx + lctx, 2, 0, L.lvuv[m][b]);
-        for (int i = 1; i < 16; ++i) flatc += L.lvuv[m][b][i] != 0;
-#pragma unroll
-        for (int off = 4; off >= 1; off >>= 1) {
-          d += __shfl_xor(d, off, 8);
-          r += __shfl_xor(r, off, 8);
-          flatc += __shfl_xor(flatc, off, 8);
-        }
-        if (b == 0) {
-          L.mres[m][0] = d; L.mres[m][1] = r; L.mres[m][2] = flatc; L.mres[m][3] = (int)nzm;
-        }
-      }
-      __syncthreads();
-      int bu = 0;
-      score_t bsc = 0, bD = 0, bR = 0, bH = 0;
+      eval_uv(L, S, ctx, lane, x, topderr, use_derr);
+      score_t bsc = 0, bH = 0;
       for (int mm = 0; mm < 4; ++mm) {
         const score_t Dm = L.mres[mm][0], Hm = kVP8ModeCostUV[mm];
         score_t Rm = L.mres[mm][1];
         if (mm > 0 && L.mres[mm][2] <= 2) Rm += 140 * 8;
         const score_t sc = (Rm + Hm) * S.lambda_uv + 256 * Dm;
-        if (mm == 0 || sc < bsc) { bsc = sc; bu = mm; bD = Dm; bR = Rm; bH = Hm; }
+        if (mm == 0 || sc < bsc) { bsc = sc; bu = mm; bH = Hm; }
       }
-      rdD += bD; rdR += bR; rdH += bH; rd_score += bsc;
+      rdH += bH;
+      rd_score += bsc;
       rd_nz |= (uint32_t)L.mres[bu][3] << 16;
       for (int k = lane; k < 128; k += 64) {
         L.yout[(k >> 4) * BPS + 16 + (k & 15)] = L.recuv[bu][k];
@@ -1126,6 +1280,40 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
         top[1] = (int8_t)(e[2] - left[1]);
       }
       __syncthreads();
+    }
+
+    // ---- m5: final re-quantisation of the chosen modes with trellis
+    // (SimpleQuantize, quant_enc.c:1222-1245; RD_OPT_TRELLIS, :1384-1387)
+    if (rd_opt == 2) {
+      uint32_t nzq = 0;
+      if (is_i16) {
+        eval_i16(L, S, ctx, lane, true);
+        for (int k = lane; k < 256; k += 64) {
+          L.yout[(k >> 4) * BPS + (k & 15)] = L.rec16[best16][k];
+          (&L.fin_ac[0][0])[k] = (&L.lv16[best16][0][0])[k];
+        }
+        if (lane < 16) L.fin_dc[lane] = L.lvdc[best16][lane];
+        nzq = (uint32_t)L.mres[best16][3];
+      } else {
+        I4Result r4 = run_i4(L, S, ctx, lane, x, mbw, predtop, yl, yt, false, true, 0, 0);
+        for (int k = lane; k < 256; k += 64) {
+          L.yout[(k >> 4) * BPS + (k & 15)] = L.acc_out[k];
+          (&L.fin_ac[0][0])[k] = (&L.acc_ac[0][0])[k];
+        }
+        nzq = r4.nz;
+      }
+      __syncthreads();
+      eval_uv(L, S, ctx, lane, x, topderr, use_derr);   // derr state already updated
+      for (int k = lane; k < 128; k += 64) {
+        L.yout[(k >> 4) * BPS + 16 + (k & 15)] = L.recuv[bu][k];
+        (&L.fin_uv[0][0])[k] = (&L.lvuv[bu][0][0])[k];
+      }
+      rd_nz = nzq | ((uint32_t)L.mres[bu][3] << 16);
+      __syncthreads();
+    }
+    (void)rd_score;
+    {
+
       // ---- per-MB info + stats side info
       const int skip = rd_nz == 0;
       if (lane == 0) {
@@ -1136,7 +1324,6 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
         size_p0 += rdH;
       }
       if (lane < 16) mbinfo[(size_t)mb * VP8G_MBINFO_BYTES + 4 + lane] = L.modes[lane];
-      (void)rdD; (void)rdSD; (void)rdR; (void)rd_score;
     }
     // SSE for WebPAuxStats (frame_enc.c:480-489)
     {

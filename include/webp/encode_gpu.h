@@ -57,9 +57,16 @@ WEBP_EXTERN int WebPGpuBatchError(const WebPGpuBatch* batch, int frame);
 
 /* Per-stage wall times of the last call in microseconds:
  * [0] import+analysis kernels, [1] host segment setup, [2] RD/token kernel,
- * [3] device->host copies, [4] host tail (emit + assembly), [5] total. */
+ * [3] device->host copies, [4] host tail (emit + assembly), [5] total,
+ * [6] k_encode device time and [7] k_import + k_analyze device time, both
+ * from HIP events recorded on the batch's stream around the launches. */
 WEBP_EXTERN void WebPGpuBatchTimings(const WebPGpuBatch* batch,
                                      double timings_us[8]);
+
+/* Number of 16-bit VP8 tokens the RD/token kernel produced for frame f of
+ * the last call (token_enc.c:31-35 format); used to price the kernel's HBM
+ * traffic in benchmarks. */
+WEBP_EXTERN size_t WebPGpuBatchTokenCount(const WebPGpuBatch* batch, int frame);
 
 /* Debug/parity hooks (used by tests): copy the device YUV420 planes of frame
  * f (Y | U | V, contiguous, strides width and (width+1)/2), and the per-MB

@@ -42,6 +42,7 @@ def load():
         "WebPGpuBatchOutputSize": (sz, [vp, i]),
         "WebPGpuBatchOutput": (vp, [vp, i]),
         "WebPGpuBatchError": (i, [vp, i]),
+        "WebPGpuBatchTokenCount": (sz, [vp, i]),
         "WebPGpuBatchTimings": (None, [vp, C.POINTER(C.c_double)]),
         "WebPGpuBatchGetYUV": (i, [vp, i, vp]),
         "WebPGpuBatchGetMBInfo": (i, [vp, i, vp]),
@@ -128,6 +129,9 @@ class GpuBatch:
             raise RuntimeError("frame %d: %s" % (f, abi.ENC_ERRORS[err]))
         size = self._lib.WebPGpuBatchOutputSize(self._h, f)
         return C.string_at(self._lib.WebPGpuBatchOutput(self._h, f), size)
+
+    def token_count(self, f):
+        return self._lib.WebPGpuBatchTokenCount(self._h, f)
 
     def output_size(self, f):
         return self._lib.WebPGpuBatchOutputSize(self._h, f)

@@ -98,6 +98,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   const size_t N = (size_t)max_frames, nmb = (size_t)b->nmb;
   CHK(hipSetDevice(device));
   CHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+  for (int i = 0; i < 4; ++i) CHK(hipEventCreate(&b->ev[i]));
   CHK(hipMalloc((void**)&b->d_g2l, 256 * sizeof(uint16_t) + 33 * sizeof(int32_t)));
   b->d_l2g = (int32_t*)(b->d_g2l + 256);
   CHK(hipMemcpy(b->d_g2l, g_g2l, 256 * sizeof(uint16_t), hipMemcpyHostToDevice));
@@ -141,6 +142,8 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipHostFree(b->h_aflags); hipHostFree(b->h_alpha); hipHostFree(b->h_uva);
   hipHostFree(b->h_segmap); hipHostFree(b->h_params); hipHostFree(b->h_mbinfo);
   hipHostFree(b->h_results); hipHostFree(b->h_tokens);
+  for (int i = 0; i < 4; ++i)
+    if (b->ev[i]) hipEventDestroy(b->ev[i]);
   if (b->stream) hipStreamDestroy(b->stream);
   if (b->out)
     for (int i = 0; i < b->max_frames; ++i) free(b->out[i]);
@@ -214,7 +217,10 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   const size_t nmb = (size_t)b->nmb;
   double t0 = now_us(), t1, t2, t3, t4;
   hipStream_t st = b->stream;
+  if (!b->ev0_recorded) CHK(hipEventRecord(b->ev[0], st));
+  b->ev0_recorded = 0;
   if (!vp8g_launch_analysis(b->d_yuv, b->yfb, b->w, b->h, n, b->d_alpha, b->d_uva, st)) return 0;
+  CHK(hipEventRecord(b->ev[1], st));
   CHK(hipMemcpyAsync(b->h_alpha, b->d_alpha, n * nmb, hipMemcpyDeviceToHost, st));
   CHK(hipMemcpyAsync(b->h_uva, b->d_uva, n * nmb * sizeof(uint16_t), hipMemcpyDeviceToHost, st));
   CHK(hipStreamSynchronize(st));
@@ -229,9 +235,11 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
                      hipMemcpyHostToDevice, st));
   t2 = now_us();
+  CHK(hipEventRecord(b->ev[2], st));
   if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
                           b->tok_cap, b->d_mbinfo, b->d_results, st))
     return 0;
+  CHK(hipEventRecord(b->ev[3], st));
   CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
                      hipMemcpyDeviceToHost, st));
   CHK(hipMemcpyAsync(b->h_mbinfo, b->d_mbinfo, n * nmb * VP8G_MBINFO_BYTES,
@@ -257,6 +265,11 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   t4 = now_us();
   run_tails(b, n);
   const double t5 = now_us();
+  float k3_ms = 0.f, k12_ms = 0.f;
+  CHK(hipEventElapsedTime(&k3_ms, b->ev[2], b->ev[3]));
+  CHK(hipEventElapsedTime(&k12_ms, b->ev[0], b->ev[1]));
+  b->timings[6] = 1e3 * k3_ms;
+  b->timings[7] = 1e3 * k12_ms;
   b->timings[1] = t2 - t1;
   b->timings[2] = t3 - t2;
   b->timings[3] = t4 - t3;
@@ -283,6 +296,8 @@ static int run_rgba(WebPGpuBatch* b, const void* rgba_dev, size_t fstride, int r
     hipEventDestroy(ev);
   }
   CHK(hipMemsetAsync(b->d_aflags, 0, n * sizeof(uint32_t), b->stream));
+  CHK(hipEventRecord(b->ev[0], b->stream));
+  b->ev0_recorded = 1;
   if (!vp8g_launch_import((const uint8_t*)rgba_dev, fstride, rstride, b->w, b->h, n, b->d_yuv,
                           b->yfb, b->d_aflags, b->d_g2l, b->d_l2g, b->stream))
     return 0;
@@ -328,6 +343,9 @@ size_t WebPGpuBatchOutputSize(const WebPGpuBatch* b, int f) {
 }
 const uint8_t* WebPGpuBatchOutput(const WebPGpuBatch* b, int f) {
   return (b && f >= 0 && f < b->last_n) ? b->out[f] : NULL;
+}
+size_t WebPGpuBatchTokenCount(const WebPGpuBatch* b, int f) {
+  return (b && f >= 0 && f < b->last_n) ? b->h_results[f].ntokens : 0;
 }
 int WebPGpuBatchError(const WebPGpuBatch* b, int f) {
   return (b && f >= 0 && f < b->last_n) ? b->err[f] : VP8_ENC_ERROR_NULL_PARAMETER;

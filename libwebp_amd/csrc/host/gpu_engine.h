@@ -16,6 +16,8 @@ struct WebPGpuBatch {
   WebPConfig cfg;
   size_t yfb, tok_cap, d_rgba_cap, h_tok_cap;
   hipStream_t stream;
+  hipEvent_t ev[4];          /* K1 start, K2 end, K3 start, K3 end */
+  int ev0_recorded;
   /* device (HBM) */
   uint8_t* d_rgba;
   uint16_t* d_g2l;   /* gamma tables: 256 x u16 then 33 x i32 */

@@ -47,4 +47,8 @@ if __name__ == "__main__":
     ok = True
     for (w, h) in [(16, 16), (64, 48), (33, 17), (128, 128), (333, 257), (512, 512)]:
         ok &= compare(w, h)
+    for m in (3, 5, 6):
+        for (w, h) in [(64, 48), (128, 128)]:
+            ok &= compare(w, h, method=m)
+    ok &= compare(256, 256, quality=90, method=6)
     sys.exit(0 if ok else 1)

@@ -111,10 +111,10 @@ class GpuBatch:
         """frames: (N, H, W, 4) uint8 numpy array in host memory."""
         import numpy as np
         frames = np.ascontiguousarray(frames, dtype=np.uint8)
-        n = frames.shape[0]
-        fs = frames.strides[0]
-        ok = self._lib.WebPGpuBatchEncodeRGBAHost(self._h, frames.ctypes.data, fs,
-                                                  frames.strides[1], n)
+        n, h, w = frames.shape[:3]
+        fs = h * w * 4          # a size-1 leading axis may carry stride 0
+        assert frames.strides[1:] == (4 * w, 4, 1)
+        ok = self._lib.WebPGpuBatchEncodeRGBAHost(self._h, frames.ctypes.data, fs, 4 * w, n)
         if not ok:
             raise RuntimeError("WebPGpuBatchEncodeRGBAHost failed: %s" % last_error())
         self.n = n

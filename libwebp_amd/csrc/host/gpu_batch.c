@@ -286,6 +286,7 @@ static int run_rgba(WebPGpuBatch* b, const void* rgba_dev, size_t fstride, int r
   const double t0 = now_us();
   if (n <= 0 || n > b->max_frames) return 0;
   if (rstride < 4 * b->w) return 0;
+  if (n > 1 && fstride < (size_t)rstride * b->h) return 0;
   CHK(hipSetDevice(b->device));
   for (int f = 0; f < n; ++f) b->err[f] = VP8_ENC_OK;
   if (stream) {   /* order after the caller's producer work */
@@ -322,9 +323,10 @@ int WebPGpuBatchEncodeRGBA(WebPGpuBatch* b, const void* rgba_dev, size_t fstride
 
 int WebPGpuBatchEncodeRGBAHost(WebPGpuBatch* b, const uint8_t* rgba, size_t fstride, int rstride,
                                int n) {
-  if (!b || !rgba || n <= 0 || n > b->max_frames) return 0;
+  if (!b || !rgba || n <= 0 || n > b->max_frames || rstride < 4 * b->w) return 0;
+  if (n > 1 && fstride < (size_t)rstride * b->h) return 0;
   CHK(hipSetDevice(b->device));
-  const size_t need = (size_t)n * fstride;
+  const size_t need = (size_t)(n - 1) * fstride + (size_t)rstride * b->h;
   if (need > b->d_rgba_cap) {
     hipFree(b->d_rgba);
     b->d_rgba = NULL;
@@ -332,7 +334,11 @@ int WebPGpuBatchEncodeRGBAHost(WebPGpuBatch* b, const uint8_t* rgba, size_t fstr
     CHK(hipMalloc((void**)&b->d_rgba, need));
     b->d_rgba_cap = need;
   }
-  CHK(hipMemcpyAsync(b->d_rgba, rgba, need, hipMemcpyHostToDevice, b->stream));
+  /* the caller's buffer is pageable: an async copy of it on our
+   * non-blocking stream is not safe on this platform (the runtime may read
+   * it from the GPU directly), so drain the stream and copy synchronously */
+  CHK(hipStreamSynchronize(b->stream));
+  CHK(hipMemcpy(b->d_rgba, rgba, need, hipMemcpyHostToDevice));
   return run_rgba(b, b->d_rgba, fstride, rstride, n, NULL);
 fail:
   return 0;

@@ -31,6 +31,16 @@ def load():
     if not os.path.exists(path):
         raise RuntimeError("libwebp_amd.so is not built: run __graft_entry__.build() "
                            "(make -C libwebp_amd/csrc)")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64
+    # (same soname as /opt/rocm's). Loading torch's first makes this
+    # library bind to it, so HBM tensors, streams and our kernels share one
+    # runtime; a C caller without torch simply gets /opt/rocm's.
+    try:
+        import torch  # noqa: F401
+        if torch.version.hip is not None:
+            torch.cuda.is_available()
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     abi.bind_encoder_api(lib)
     vp, i, sz = C.c_void_p, C.c_int, C.c_size_t

@@ -68,6 +68,14 @@ WEBP_EXTERN void WebPGpuBatchTimings(const WebPGpuBatch* batch,
  * traffic in benchmarks. */
 WEBP_EXTERN size_t WebPGpuBatchTokenCount(const WebPGpuBatch* batch, int frame);
 
+/* Profiling: shader-clock cycles the RD/token kernel spent per stage of
+ * frame f, summed over its macroblocks: [0] MB load + cost refresh +
+ * predictors, [1] intra16, [2] intra4, [3] chroma (+ m5 final pass),
+ * [4] mode info + SSE, [5] token count/write, [6] statistics fold/replay,
+ * [7] context + boundary update. */
+WEBP_EXTERN int WebPGpuBatchStageCycles(const WebPGpuBatch* batch, int frame,
+                                        uint64_t cycles[8]);
+
 /* Debug/parity hooks (used by tests): copy the device YUV420 planes of frame
  * f (Y | U | V, contiguous, strides width and (width+1)/2), and the per-MB
  * decisions (20 bytes per MB: type, uv_mode, segment, skip, modes[16]). */

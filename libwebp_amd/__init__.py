@@ -53,6 +53,7 @@ def load():
         "WebPGpuBatchOutput": (vp, [vp, i]),
         "WebPGpuBatchError": (i, [vp, i]),
         "WebPGpuBatchTokenCount": (sz, [vp, i]),
+        "WebPGpuBatchStageCycles": (i, [vp, i, C.POINTER(C.c_uint64)]),
         "WebPGpuBatchTimings": (None, [vp, C.POINTER(C.c_double)]),
         "WebPGpuBatchGetYUV": (i, [vp, i, vp]),
         "WebPGpuBatchGetMBInfo": (i, [vp, i, vp]),
@@ -139,6 +140,11 @@ class GpuBatch:
             raise RuntimeError("frame %d: %s" % (f, abi.ENC_ERRORS[err]))
         size = self._lib.WebPGpuBatchOutputSize(self._h, f)
         return C.string_at(self._lib.WebPGpuBatchOutput(self._h, f), size)
+
+    def stage_cycles(self, f):
+        c = (C.c_uint64 * 8)()
+        self._lib.WebPGpuBatchStageCycles(self._h, f, c)
+        return list(c)
 
     def token_count(self, f):
         return self._lib.WebPGpuBatchTokenCount(self._h, f)

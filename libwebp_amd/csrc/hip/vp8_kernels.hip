@@ -1076,6 +1076,14 @@ __device__ I4Result run_i4(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int la
   return res;
 }
 
+// per-stage cycle accounting (s_memtime, uniform -> SGPRs); ~40 cycles each
+#define K3_STAMP(i)                                   \
+  do {                                                \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    stamps[i] += t_ - stamp_last;                     \
+    stamp_last = t_;                                  \
+  } while (0)
+
 struct K3Args {
   const uint8_t* yuv;
   size_t yfb;
@@ -1140,6 +1148,8 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
   uint32_t ntok = 0;
   int tok_err = 0;
   int left_dc = 0;
+  uint64_t stamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t stamp_last = __builtin_amdgcn_s_memtime();
   uint8_t* yl = L.yl_mem + 1;
   uint8_t* ul = L.ul_mem + 1;
   uint8_t* vl = L.vl_mem + 1;
@@ -1186,6 +1196,7 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
     }
     __syncthreads();
 
+    K3_STAMP(0);
     // ---- Intra16 (quant_enc.c:1002-1058)
     const bool trellis_all = rd_opt >= 3;
     eval_i16(L, S, ctx, lane, trellis_all);
@@ -1231,6 +1242,7 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
     }
     __syncthreads();
 
+    K3_STAMP(1);
     // ---- Intra4 (quant_enc.c:1072-1165)
     if (max_i4_bits > 0) {
       I4Result r4 = run_i4(L, S, ctx, lane, x, mbw, predtop, yl, yt, true, trellis_all,
@@ -1250,6 +1262,7 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
       __syncthreads();
     }
 
+    K3_STAMP(2);
     // ---- UV (quant_enc.c:1169-1217)
     int bu = 0;
     {
@@ -1312,6 +1325,7 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
       __syncthreads();
     }
     (void)rd_score;
+    K3_STAMP(3);
     {
 
       // ---- per-MB info + stats side info
@@ -1346,6 +1360,7 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
       sse_acc[0] += sy; sse_acc[1] += su; sse_acc[2] += sv;
     }
 
+    K3_STAMP(4);
     // ---- tokens + exact statistics (frame_enc.c:411-453, token_enc.c:113-193)
     {
       // per-block nz flags from final levels -> contexts
@@ -1396,6 +1411,7 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
                       &nzdummy);
       if (!tok_err) ntok += total;
       __syncthreads();
+      K3_STAMP(5);
       // fold deltas into the statistics; slots that cross the halving
       // threshold inside this MB are replayed in token order.
       int any_mark = 0;
@@ -1425,6 +1441,7 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
         for (int kk = lane; kk < 33; kk += 64) L.mark[kk] = 0;
         __syncthreads();
       }
+      K3_STAMP(6);
       // update nz context (iterator_enc.c:267-283) and the left DC flag
       {
         int tn[9], ln[9];
@@ -1472,6 +1489,7 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
       L.predleft[lane] = L.modes[4 * lane + 3];
     }
     __syncthreads();
+    K3_STAMP(7);
   }
 
   // ---- frame epilogue: final probabilities and side results
@@ -1485,6 +1503,7 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
     R->size_p0 = size_p0;
     R->sse[0] = sse_acc[0]; R->sse[1] = sse_acc[1]; R->sse[2] = sse_acc[2];
     R->block_count[0] = nb_i4; R->block_count[1] = nb_i16; R->block_count[2] = nb_skip;
+    for (int i = 0; i < 8; ++i) R->stamps[i] = stamps[i];
   }
 }
 

@@ -350,6 +350,11 @@ size_t WebPGpuBatchOutputSize(const WebPGpuBatch* b, int f) {
 const uint8_t* WebPGpuBatchOutput(const WebPGpuBatch* b, int f) {
   return (b && f >= 0 && f < b->last_n) ? b->out[f] : NULL;
 }
+int WebPGpuBatchStageCycles(const WebPGpuBatch* b, int f, uint64_t cycles[8]) {
+  if (!b || f < 0 || f >= b->last_n || !cycles) return 0;
+  for (int i = 0; i < 8; ++i) cycles[i] = b->h_results[f].stamps[i];
+  return 1;
+}
 size_t WebPGpuBatchTokenCount(const WebPGpuBatch* b, int f) {
   return (b && f >= 0 && f < b->last_n) ? b->h_results[f].ntokens : 0;
 }

@@ -60,6 +60,7 @@ typedef struct {
   uint64_t sse[3];
   int32_t block_count[3];
   int32_t pad;
+  uint64_t stamps[8];    /* per-stage shader-clock cycles summed over MBs (profiling) */
   uint8_t probas[VP8G_NUM_SLOTS];   /* final coefficient probabilities */
 } vp8g_frame_result;
 

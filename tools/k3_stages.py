@@ -1,0 +1,26 @@
+"""Per-stage cycle split of the RD/token kernel (K3) on one batch."""
+import os
+import sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import libwebp_amd
+
+W, H = int(sys.argv[1]), int(sys.argv[2])
+B = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+method = int(sys.argv[4]) if len(sys.argv) > 4 else 4
+names = ["load+refresh+preds", "i16", "i4", "uv(+m5)", "info+sse", "tokens", "fold", "ctx+bnd"]
+buf = torch.empty(B * W * H * 4, dtype=torch.uint8, device="cuda")
+libwebp_amd.synth_device(buf.data_ptr(), W, H, 0, B)
+torch.cuda.synchronize()
+enc = libwebp_amd.GpuBatch(W, H, B, method=method)
+enc.encode_device(buf.data_ptr(), B)
+enc.encode_device(buf.data_ptr(), B)
+t = enc.timings()
+nmb = ((W + 15) // 16) * ((H + 15) // 16)
+c = enc.stage_cycles(0)
+tot = sum(c)
+print("%dx%d batch %d m%d: k_encode %.1f ms (%.1f us/MB), tail %.1f ms" %
+      (W, H, B, method, t[6] / 1e3, t[6] / nmb, t[4] / 1e3))
+for n, v in zip(names, c):
+    print("  %-18s %6.1f%%  %8.0f cycles/MB" % (n, 100.0 * v / tot, v / nmb))
+print("  total %.0f cycles/MB -> %.1f us/MB at the implied clock" % (tot / nmb, t[6] / nmb))

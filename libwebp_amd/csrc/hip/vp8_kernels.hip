@@ -40,8 +40,14 @@ __device__ __forceinline__ constexpr int zz(int n) {
          n == 6 ? 3 : n == 7 ? 6 : n == 8 ? 9 : n == 9 ? 12 : n == 10 ? 13 : n == 11 ? 10 :
          n == 12 ? 7 : n == 13 ? 11 : n == 14 ? 14 : 15;
 }
-static __constant__ const uint8_t dZzInv[16] = {0, 1, 5, 6, 2, 4, 7, 12, 3, 8, 11, 13, 9, 10, 14, 15};
-static __constant__ const uint8_t dBand[17] = {0, 1, 2, 3, 6, 4, 5, 6, 6, 6, 6, 6, 6, 6, 6, 7, 0};
+// inverse zigzag and VP8EncBands (src/enc/cost_enc.c:...; kZigzag inverse)
+// as 4-bit fields of 64-bit immediates: register-only lookups, no memory
+__device__ __forceinline__ int zz_inv(int b) {
+  return (int)((0xfea9db83c7426510ull >> (4 * b)) & 15);
+}
+__device__ __forceinline__ int band_of(int n) {   // n in 0..16, band(16) = 0
+  return n >= 16 ? 0 : (int)((0x7666666665463210ull >> (4 * n)) & 15);
+}
 
 // 4x4 intra predictor as data: pred[m][p] = f(edges e[0..12]) with
 // e = L K J I X A B C D E F G H (src/dsp/enc.c:351-512). kind: 0 AVG3(a,b,c)
@@ -89,8 +95,9 @@ static __constant__ const P4Op kP4[10][16] = {
 
 __device__ __forceinline__ int clip8(int v) { return (v & ~0xff) == 0 ? v : (v < 0 ? 0 : 255); }
 __device__ __forceinline__ int iabs_(int v) { return v < 0 ? -v : v; }
-__device__ __forceinline__ int bit_cost(int bit, int p) {
-  return kVP8EntropyCost[bit ? 255 - p : p];
+// VP8BitCost (cost_enc.h:59-61) from the LDS copy of kVP8EntropyCost
+__device__ __forceinline__ int bit_cost(const uint16_t* ec, int bit, int p) {
+  return ec[bit ? 255 - p : p];
 }
 
 // ---------------------------------------------------------------------------
@@ -182,7 +189,8 @@ __device__ __forceinline__ int sse4(const uint8_t* a, int as, const uint8_t* b, 
 
 // QuantizeBlock_C on natural-order coefficients c[] (int16 semantics),
 // writes zigzag-order levels to lv[] (LDS), dequantises c[] in place.
-__device__ __forceinline__ int quantize_block(int c[16], int16_t* lv, const vp8g_mtx* m) {
+__device__ __forceinline__ int quantize_block(int c[16], int16_t* lv, const vp8g_mtx* m,
+                                              int lvr[16]) {
   int nz = 0;
 #pragma unroll
   for (int n = 0; n < 16; ++n) {
@@ -197,6 +205,7 @@ __device__ __forceinline__ int quantize_block(int c[16], int16_t* lv, const vp8g
     }
     c[j] = (int16_t)(level * (int)m->q[j]);
     lv[n] = (int16_t)level;
+    lvr[n] = level;
     nz |= level;
   }
   return nz != 0;
@@ -469,7 +478,10 @@ __global__ __launch_bounds__(256) void k_analyze(const uint8_t* __restrict__ yuv
 struct K3Lds {
   uint32_t stats[NSLOT];
   uint32_t delta[NSLOT];
-  uint16_t lcost[96][MAX_VLEVEL + 1];  // [type*24 + band*3 + ctx][level]
+  uint16_t lcost[96][MAX_VLEVEL + 1];  // [type*24 + band*3 + ctx][level], incl. fixed cost
+  uint16_t ecost[256];            // kVP8EntropyCost
+  uint16_t mcost4[1000];          // kVP8ModeCostI4[top][left][mode]
+  P4Op p4[160];                   // kP4
   uint8_t coeffs[NSLOT];
   uint32_t mark[33];
   vp8g_seg seg[4];
@@ -479,24 +491,24 @@ struct K3Lds {
   uint8_t puv[4][128];
   uint8_t rec16[4][256];
   uint8_t recuv[4][128];
-  int16_t lv16[4][16][16];
-  int16_t lvdc[4][16];
+  alignas(16) int16_t lv16[4][16][16];
+  alignas(16) int16_t lvdc[4][16];
   int16_t whtq[4][16];
   int16_t dcs[4][16];
-  int16_t lvuv[4][8][16];
+  alignas(16) int16_t lvuv[4][8][16];
   int16_t uvdc[4][8];
   int8_t uvderr[4][2][3];
-  int16_t fin_dc[16];
-  int16_t fin_ac[16][16];
-  int16_t fin_uv[8][16];
+  alignas(16) int16_t fin_dc[16];
+  alignas(16) int16_t fin_ac[16][16];
+  alignas(16) int16_t fin_uv[8][16];
   uint8_t modes[16];
   uint8_t canvas[17][24];
   uint8_t edges[16];
   uint8_t pred4[10][16];
-  int16_t lv4[10][16];
+  alignas(16) int16_t lv4[10][16];
   uint8_t rec4[10][16];
   int32_t r4[10][8];
-  int16_t acc_ac[16][16];
+  alignas(16) int16_t acc_ac[16][16];
   uint8_t acc_out[256];          // I4 reconstruction, stride 16
   int32_t mres[4][4];
   int32_t blkinfo[32];            // per token block: type | first<<4 | ctx<<8
@@ -516,29 +528,49 @@ struct MBCtx {
   __device__ __forceinline__ int left(int i) const { return (l >> i) & 1; }
 };
 
+// VP8LevelCost (cost_enc.h:63-66). The LDS rows already include
+// kVP8LevelFixedCost[v] for v <= MAX_VLEVEL (folded in level_costs()), so
+// only the rare v > 67 touches the global table.
 __device__ __forceinline__ int level_cost(const uint16_t* tab, int v) {
-  return kVP8LevelFixedCost[v] + tab[v > MAX_VLEVEL ? MAX_VLEVEL : v];
+  return v <= MAX_VLEVEL ? tab[v]
+                         : tab[MAX_VLEVEL] - kVP8LevelFixedCost[MAX_VLEVEL] + kVP8LevelFixedCost[v];
 }
 
-// GetResidualCost_C (src/dsp/cost.c:322-355); lv in zigzag order.
-__device__ __forceinline__ int residual_cost(const K3Lds& L, int ctx0, int type, int first,
-                                             const int16_t* lv) {
-  int last = -1;
-  for (int n = 15; n >= first; --n)
-    if (lv[n]) { last = n; break; }
-  const int p0 = L.coeffs[((type * 8 + first) * 3 + ctx0) * 11];
-  if (last < 0) return bit_cost(0, p0);
-  int cost = ctx0 == 0 ? bit_cost(1, p0) : 0;
-  const uint16_t* t = L.lcost[type * 24 + dBand[first] * 3 + ctx0];
-  int n = first;
-  for (; n < last; ++n) {
-    const int v = iabs_(lv[n]);
-    cost += level_cost(t, v);
-    t = L.lcost[type * 24 + dBand[n + 1] * 3 + (v >= 2 ? 2 : v)];
+// 16 zigzag levels from LDS into registers (two 16-byte reads)
+__device__ __forceinline__ void load_lv(const int16_t* p, int r[16]) {
+  const uint4 a = *reinterpret_cast<const uint4*>(p);
+  const uint4 b = *reinterpret_cast<const uint4*>(p + 8);
+  const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    r[2 * i] = (int)(int16_t)(w[i] & 0xffff);
+    r[2 * i + 1] = (int)(int16_t)(w[i] >> 16);
   }
-  const int v = iabs_(lv[n]);
-  cost += level_cost(t, v);
-  if (n < 15) cost += bit_cost(0, L.coeffs[((type * 8 + dBand[n + 1]) * 3 + (v == 1 ? 1 : 2)) * 11]);
+}
+
+// GetResidualCost_C (src/dsp/cost.c:322-355) on register-resident levels:
+// each position's context is the previous level, already in a register, so
+// all the LDS table reads are independent and overlap instead of chaining.
+__device__ __forceinline__ int residual_cost_r(const K3Lds& L, int ctx0, int type, int first,
+                                               const int lv[16]) {
+  int last = -1;
+#pragma unroll
+  for (int n = 0; n < 16; ++n)
+    if (n >= first && lv[n] != 0) last = n;
+  const int p0 = L.coeffs[((type * 8 + first) * 3 + ctx0) * 11];   // band(first) == first
+  if (last < 0) return bit_cost(L.ecost, 0, p0);
+  int cost = ctx0 == 0 ? bit_cost(L.ecost, 1, p0) : 0;
+  int prev = ctx0;
+#pragma unroll
+  for (int n = 0; n < 16; ++n) {
+    if (n >= first && n <= last) {
+      const int v = iabs_(lv[n]);
+      cost += level_cost(L.lcost[type * 24 + band_of(n) * 3 + prev], v);
+      prev = v >= 2 ? 2 : v;
+    }
+  }
+  if (last < 15)
+    cost += bit_cost(L.ecost, 0, L.coeffs[((type * 8 + band_of(last + 1)) * 3 + prev) * 11]);
   return cost;
 }
 
@@ -557,10 +589,10 @@ __device__ __noinline__ int trellis_quant(const K3Lds& L, uint32_t* nodes, int c
   for (int n = 0; n < 16; ++n)
     if (n >= first && c[zz(n)] * c[zz(n)] > thresh) last = n;
   if (last < 15) ++last;
-  score_t best_score = (score_t)bit_cost(0, last_proba) * lambda;
+  score_t best_score = (score_t)bit_cost(L.ecost, 0, last_proba) * lambda;
   score_t sp0, sp1;
   int tp0, tp1;   // lcost row index of each predecessor node
-  sp0 = sp1 = (score_t)(ctx0 == 0 ? bit_cost(1, last_proba) : 0) * lambda;
+  sp0 = sp1 = (score_t)(ctx0 == 0 ? bit_cost(L.ecost, 1, last_proba) : 0) * lambda;
   tp0 = tp1 = type * 24 + first * 3 + ctx0;
   int bp_n = -1, bp_k = 0, bp_prev = 0;
 #pragma unroll
@@ -574,7 +606,7 @@ __device__ __noinline__ int trellis_quant(const K3Lds& L, uint32_t* nodes, int c
       int thr = (int)((coeff0 * iQ + (0x80u << (QFIX - 8))) >> QFIX);
       if (thr > MAX_LEVEL) thr = MAX_LEVEL;
       if (level0 > MAX_LEVEL) level0 = MAX_LEVEL;
-      const int band = dBand[n + 1];
+      const int band = band_of(n + 1);
       score_t sc0 = MAX_COST, sc1 = MAX_COST;
       int tc0 = 0, tc1 = 0;
 #pragma unroll
@@ -595,7 +627,7 @@ __device__ __noinline__ int trellis_quant(const K3Lds& L, uint32_t* nodes, int c
           cur = best;
           if (level != 0 && best < best_score) {
             const score_t lc =
-                (n < 15) ? bit_cost(0, L.coeffs[((type * 8 + band) * 3 + ctx) * 11]) : 0;
+                (n < 15) ? bit_cost(L.ecost, 0, L.coeffs[((type * 8 + band) * 3 + ctx) * 11]) : 0;
             const score_t sc = best + lc * lambda;
             if (sc < best_score) { best_score = sc; bp_n = n; bp_k = k; bp_prev = bprev; }
           }
@@ -636,9 +668,9 @@ __device__ int finalize_probas(K3Lds& L, int lane) {
     const int upd = (&kVP8CoeffUpdateProba[0][0][0][0])[s];
     const int old_p = (&kVP8CoeffProba0[0][0][0][0])[s];
     const int new_p = nb ? (255 - nb * 255 / total) : 255;
-    const int old_cost = nb * bit_cost(1, old_p) + (total - nb) * bit_cost(0, old_p) + bit_cost(0, upd);
+    const int old_cost = nb * bit_cost(L.ecost, 1, old_p) + (total - nb) * bit_cost(L.ecost, 0, old_p) + bit_cost(L.ecost, 0, upd);
     const int new_cost =
-        nb * bit_cost(1, new_p) + (total - nb) * bit_cost(0, new_p) + bit_cost(1, upd) + 8 * 256;
+        nb * bit_cost(L.ecost, 1, new_p) + (total - nb) * bit_cost(L.ecost, 0, new_p) + bit_cost(L.ecost, 1, upd) + 8 * 256;
     if (old_cost > new_cost) {
       L.coeffs[s] = new_p;
       changed |= (new_p != old_p);
@@ -656,17 +688,17 @@ __device__ void level_costs(K3Lds& L, int lane) {
     const int tbc = k / (MAX_VLEVEL + 1), v = k % (MAX_VLEVEL + 1);
     const uint8_t* p = L.coeffs + tbc * 11;
     const int ctx = tbc % 3;
-    const int c0 = ctx > 0 ? bit_cost(1, p[0]) : 0;
+    const int c0 = ctx > 0 ? bit_cost(L.ecost, 1, p[0]) : 0;
     int cost;
     if (v == 0) {
-      cost = bit_cost(0, p[1]) + c0;
+      cost = bit_cost(L.ecost, 0, p[1]) + c0;
     } else {
-      cost = bit_cost(1, p[1]) + c0;
+      cost = bit_cost(L.ecost, 1, p[1]) + c0;
       int pat = kVP8LevelCodes[v - 1][0], bits = kVP8LevelCodes[v - 1][1];
       for (int i = 2; pat; ++i, pat >>= 1, bits >>= 1)
-        if (pat & 1) cost += bit_cost(bits & 1, p[i]);
+        if (pat & 1) cost += bit_cost(L.ecost, bits & 1, p[i]);
     }
-    L.lcost[tbc][v] = (uint16_t)cost;
+    L.lcost[tbc][v] = (uint16_t)(cost + kVP8LevelFixedCost[v]);
   }
   __syncthreads();
 }
@@ -703,7 +735,7 @@ __device__ int gen_tokens(K3Lds& L, const int16_t* lv, int type, int first, int 
     ++count;
   };
   int n = first;
-  int base = 11 * (ctx + 3 * (dBand[n] + 8 * type));
+  int base = 11 * (ctx + 3 * (band_of(n) + 8 * type));
   *nz_out = last >= 0;
   if (!dyn(last >= 0, base + 0, base + 0)) return count;
   while (n < 16) {
@@ -711,11 +743,11 @@ __device__ int gen_tokens(K3Lds& L, const int16_t* lv, int type, int first, int 
     const int neg = c < 0;
     const uint32_t v = neg ? -c : c;
     if (!dyn(v != 0, base + 1, base + 1)) {
-      base = 11 * (0 + 3 * (dBand[n] + 8 * type));
+      base = 11 * (0 + 3 * (band_of(n) + 8 * type));
       continue;
     }
     if (!dyn(v > 1, base + 2, base + 2)) {
-      base = 11 * (1 + 3 * (dBand[n] + 8 * type));
+      base = 11 * (1 + 3 * (band_of(n) + 8 * type));
     } else {
       if (!dyn(v > 4, base + 3, base + 3)) {
         if (dyn(v != 2, base + 4, base + 4)) dyn(v == 4, base + 5, base + 5);
@@ -745,7 +777,7 @@ __device__ int gen_tokens(K3Lds& L, const int16_t* lv, int type, int first, int 
         }
         for (; mask; mask >>= 1) fix((res & mask) != 0, *tab++);
       }
-      base = 11 * (2 + 3 * (dBand[n] + 8 * type));
+      base = 11 * (2 + 3 * (band_of(n) + 8 * type));
     }
     fix(neg, 128);
     if (n == 16 || !dyn(n <= last, base + 0, base + 0)) return count;
@@ -771,7 +803,9 @@ __device__ __forceinline__ const int16_t* blk_levels(const K3Lds& L, int k) {
 // mres[m] = {SSE, texture distortion, rate, nz (ac bits | dc << 24)}.
 // With trellis (m6 search, m5 final pass) the AC blocks are trellis-quantised
 // in anti-diagonal waves so each block sees its top/left neighbours' nz.
-__device__ void eval_i16(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane, bool trellis) {
+template <bool TRELLIS>
+__device__ void eval_i16(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane) {
+  constexpr bool trellis = TRELLIS;
   const int m = lane >> 4, b = lane & 15, bx = b & 3, by = b >> 2;
   int c[16];
   const uint8_t* src = L.yin + by * 4 * BPS + bx * 4;
@@ -802,11 +836,12 @@ __device__ void eval_i16(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane
       if (level > MAX_LEVEL) level = MAX_LEVEL;
       if (neg) level = -level;
     }
-    L.lvdc[m][dZzInv[b]] = (int16_t)level;
+    L.lvdc[m][zz_inv(b)] = (int16_t)level;
     L.whtq[m][b] = (int16_t)(level * (int)M.q[b]);
   }
   int nzb = 0;
-  if (trellis) {   // quant_enc.c:790-803
+  int lvr[16];
+  if constexpr (trellis) {   // quant_enc.c:790-803
     for (int st = 0; st < 7; ++st) {
       if (bx + by == st) {
         const uint32_t tm = L.trnz[m];
@@ -819,9 +854,20 @@ __device__ void eval_i16(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane
       }
       __syncthreads();
     }
+    load_lv(L.lv16[m][b], lvr);
   } else {         // quant_enc.c:805-812: DC position zeroed first
     c[0] = 0;
-    nzb = quantize_block(c, L.lv16[m][b], &S.y1);
+    nzb = quantize_block(c, L.lv16[m][b], &S.y1, lvr);
+  }
+  // rate of the AC levels while they are still in registers (nz contexts of
+  // the neighbouring blocks of the same mode from a ballot)
+  const uint64_t nzmask_all = __ballot(nzb);
+  const uint32_t nzm = (uint32_t)(nzmask_all >> (16 * m)) & 0xffff;
+  int r;
+  {
+    const int tctx = by == 0 ? ctx.top(bx) : (int)((nzm >> (b - 4)) & 1);
+    const int lctx = bx == 0 ? ctx.left(by) : (int)((nzm >> (b - 1)) & 1);
+    r = residual_cost_r(L, tctx + lctx, 0, 1, lvr);
   }
   __syncthreads();
   {   // inverse WHT -> DC of block b (dec.c:137-162)
@@ -843,14 +889,12 @@ __device__ void eval_i16(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane
   const uint8_t* rec = L.rec16[m] + by * 64 + bx * 4;
   int d = sse4(src, BPS, rec, 16);
   int td = iabs_(hadamard_w(rec, 16) - hadamard_w(src, BPS)) >> 5;
-  const uint64_t nzmask_all = __ballot(nzb);
-  const uint32_t nzm = (uint32_t)(nzmask_all >> (16 * m)) & 0xffff;
-  const int tctx = by == 0 ? ctx.top(bx) : (int)((nzm >> (b - 4)) & 1);
-  const int lctx = bx == 0 ? ctx.left(by) : (int)((nzm >> (b - 1)) & 1);
-  int r = residual_cost(L, tctx + lctx, 0, 1, L.lv16[m][b]);
+  int dcl[16];
+  load_lv(L.lvdc[m], dcl);
   int dcnz = 0;
-  for (int k = 0; k < 16; ++k) dcnz |= L.lvdc[m][k];
-  if (b == 0) r += residual_cost(L, ctx.top(8) + ctx.left(8), 1, 0, L.lvdc[m]);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) dcnz |= dcl[k];
+  if (b == 0) r += residual_cost_r(L, ctx.top(8) + ctx.left(8), 1, 0, dcl);
 #pragma unroll
   for (int off = 8; off >= 1; off >>= 1) {
     d += __shfl_xor(d, off, 16);
@@ -872,6 +916,7 @@ __device__ void eval_i16(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane
 __device__ void eval_uv(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane, int x,
                         const int8_t* topderr, int use_derr) {
   int d = 0, r = 0, flatc = 0, nzb = 0;
+  int lvr[16];
   const int m = lane >> 3, b = lane & 7;
   int c[16];
   const int ch = b >> 2, k4 = b & 3;
@@ -916,7 +961,7 @@ __device__ void eval_uv(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane,
   __syncthreads();
   if (lane < 32) {
     c[0] = L.uvdc[m][b];
-    nzb = quantize_block(c, L.lvuv[m][b], &S.uv);
+    nzb = quantize_block(c, L.lvuv[m][b], &S.uv, lvr);
     idct4(ref, 16, c, L.recuv[m] + 8 * ch + (k4 >> 1) * 64 + (k4 & 1) * 4, 16);
   }
   __syncthreads();
@@ -928,8 +973,9 @@ __device__ void eval_uv(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane,
     const int bxx = k4 & 1, byy = k4 >> 1;
     const int tctx = byy == 0 ? ctx.top(4 + 2 * ch + bxx) : (int)((nzm >> (b - 2)) & 1);
     const int lctx = bxx == 0 ? ctx.left(4 + 2 * ch + byy) : (int)((nzm >> (b - 1)) & 1);
-    r = residual_cost(L, tctx + lctx, 2, 0, L.lvuv[m][b]);
-    for (int i = 1; i < 16; ++i) flatc += L.lvuv[m][b][i] != 0;
+    r = residual_cost_r(L, tctx + lctx, 2, 0, lvr);
+#pragma unroll
+    for (int i = 1; i < 16; ++i) flatc += lvr[i] != 0;
 #pragma unroll
     for (int off = 4; off >= 1; off >>= 1) {
       d += __shfl_xor(d, off, 8);
@@ -954,10 +1000,11 @@ struct I4Result {
 // already chosen L.modes (quant_enc.c:1230-1240), whose trellis contexts are
 // the macroblock-boundary flags only (the reference never updates them
 // inside that loop). Reconstruction lands in acc_out, levels in acc_ac.
+template <bool TRELLIS>
 __device__ I4Result run_i4(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane, int x,
                            int mbw, const uint8_t* predtop, const uint8_t* yl,
-                           const uint8_t* yt, bool search, bool trellis, score_t rd_score,
-                           int max_bits) {
+                           const uint8_t* yt, bool search, score_t rd_score, int max_bits) {
+  constexpr bool trellis = TRELLIS;
   for (int k = lane; k < 21; k += 64) {
     uint8_t v;
     if (k == 0) v = yl[-1];
@@ -990,7 +1037,7 @@ __device__ I4Result run_i4(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int la
     __syncthreads();
     for (int k = lane; k < 160; k += 64) {
       const int m = k >> 4, p = k & 15;
-      const P4Op op = kP4[m][p];
+      const P4Op op = L.p4[k];
       const uint8_t* e = L.edges;
       int v;
       if (op.kind == 0) v = (e[op.a] + 2 * e[op.b] + e[op.c] + 2) >> 2;
@@ -1007,9 +1054,14 @@ __device__ I4Result run_i4(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int la
       int c[16];
       fdct4(src, BPS, L.pred4[m], 4, c);
       const int ctx4 = (int)((tnz >> bx) & 1) + (int)((lnz >> by) & 1);
-      const int nz = trellis ? trellis_quant(L, L.tnodes[lane], c, L.lv4[m], ctx4, 3, &S.y1,
-                                             S.lambda_trellis_i4)
-                             : quantize_block(c, L.lv4[m], &S.y1);
+      int nz;
+      int lvr[16];
+      if constexpr (trellis) {
+        nz = trellis_quant(L, L.tnodes[lane], c, L.lv4[m], ctx4, 3, &S.y1, S.lambda_trellis_i4);
+        load_lv(L.lv4[m], lvr);
+      } else {
+        nz = quantize_block(c, L.lv4[m], &S.y1, lvr);
+      }
       idct4(L.pred4[m], 4, c, L.rec4[m], 4);
       if (search) {
         const int D = sse4(src, BPS, L.rec4[m], 4);
@@ -1017,10 +1069,11 @@ __device__ I4Result run_i4(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int la
                                                         hadamard_w(src, BPS)) >> 5) + 128) >> 8
                                  : 0;
         int cntnz = 0;
-        for (int i = 1; i < 16; ++i) cntnz += L.lv4[m][i] != 0;
+#pragma unroll
+        for (int i = 1; i < 16; ++i) cntnz += lvr[i] != 0;
         const int R0 = (m > 0 && cntnz <= 3) ? 140 : 0;
-        const int Rc = residual_cost(L, ctx4, 3, 0, L.lv4[m]);
-        L.r4[m][0] = D; L.r4[m][1] = SD; L.r4[m][2] = kVP8ModeCostI4[top_m][left_m][m];
+        const int Rc = residual_cost_r(L, ctx4, 3, 0, lvr);
+        L.r4[m][0] = D; L.r4[m][1] = SD; L.r4[m][2] = L.mcost4[(top_m * 10 + left_m) * 10 + m];
         L.r4[m][3] = R0; L.r4[m][4] = Rc;
       }
       L.r4[m][5] = nz;
@@ -1125,6 +1178,9 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
     L.coeffs[s] = (&kVP8CoeffProba0[0][0][0][0])[s];
   }
   for (int k = lane; k < 33; k += 64) L.mark[k] = 0;
+  for (int k = lane; k < 256; k += 64) L.ecost[k] = kVP8EntropyCost[k];
+  for (int k = lane; k < 1000; k += 64) L.mcost4[k] = (&kVP8ModeCostI4[0][0][0])[k];
+  for (int k = lane; k < 160; k += 64) L.p4[k] = (&kP4[0][0])[k];
   {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(P->seg);
     uint32_t* dst = reinterpret_cast<uint32_t*>(L.seg);
@@ -1199,7 +1255,8 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
     K3_STAMP(0);
     // ---- Intra16 (quant_enc.c:1002-1058)
     const bool trellis_all = rd_opt >= 3;
-    eval_i16(L, S, ctx, lane, trellis_all);
+    if (trellis_all) eval_i16<true>(L, S, ctx, lane);
+    else eval_i16<false>(L, S, ctx, lane);
     score_t best16_score = 0;
     int best16 = 0;
     uint32_t nz16 = 0;
@@ -1245,8 +1302,10 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
     K3_STAMP(1);
     // ---- Intra4 (quant_enc.c:1072-1165)
     if (max_i4_bits > 0) {
-      I4Result r4 = run_i4(L, S, ctx, lane, x, mbw, predtop, yl, yt, true, trellis_all,
-                           rd_score, max_i4_bits);
+      I4Result r4 = trellis_all ? run_i4<true>(L, S, ctx, lane, x, mbw, predtop, yl, yt, true,
+                                               rd_score, max_i4_bits)
+                                : run_i4<false>(L, S, ctx, lane, x, mbw, predtop, yl, yt, true,
+                                                rd_score, max_i4_bits);
       if (r4.ok) {
         is_i16 = 0;
         rdH = r4.H;
@@ -1300,7 +1359,7 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
     if (rd_opt == 2) {
       uint32_t nzq = 0;
       if (is_i16) {
-        eval_i16(L, S, ctx, lane, true);
+        eval_i16<true>(L, S, ctx, lane);
         for (int k = lane; k < 256; k += 64) {
           L.yout[(k >> 4) * BPS + (k & 15)] = L.rec16[best16][k];
           (&L.fin_ac[0][0])[k] = (&L.lv16[best16][0][0])[k];
@@ -1308,7 +1367,7 @@ __global__ __launch_bounds__(64) void k_encode(K3Args a) {
         if (lane < 16) L.fin_dc[lane] = L.lvdc[best16][lane];
         nzq = (uint32_t)L.mres[best16][3];
       } else {
-        I4Result r4 = run_i4(L, S, ctx, lane, x, mbw, predtop, yl, yt, false, true, 0, 0);
+        I4Result r4 = run_i4<true>(L, S, ctx, lane, x, mbw, predtop, yl, yt, false, 0, 0);
         for (int k = lane; k < 256; k += 64) {
           L.yout[(k >> 4) * BPS + (k & 15)] = L.acc_out[k];
           (&L.fin_ac[0][0])[k] = (&L.acc_ac[0][0])[k];

@@ -1,0 +1,1102 @@
+// K3 k_encode: the raster-order RD macroblock loop of VP8EncTokenLoop
+// (src/enc/frame_enc.c:783-894) for CDNA4, one 256-thread workgroup
+// (4 wavefronts, one per SIMD of a CU) per frame.
+//
+// The MB order is the reference's raster order: it is the only order that
+// reproduces the token statistics, the cost-refresh epochs and the U/V DC
+// error diffusion bit-exactly. Parallelism inside an MB is per COEFFICIENT:
+// a 4x4 block lives on 16 lanes (lane = natural coefficient index), its
+// forward/inverse transforms are two 4-lane butterfly passes exchanged with
+// cross-lane shuffles, quantisation is one coefficient per lane, and the rate
+// (GetResidualCost_C) is one table term per lane plus a 16-lane reduction.
+//
+//   I16  wave = prediction mode, 4 passes of 4 blocks x 16 coefficients
+//   UV   wave = prediction mode, 2 passes of 4 blocks x 16 coefficients
+//   I4   160 lanes = 10 modes x 16 coefficients, 16 dependent sub-blocks
+//   tokens / statistics / contexts: wave 0 (25 blocks in parallel)
+//
+// Trellis quantisation (m5 final pass, m6 everywhere; quant_enc.c:593-763)
+// stays one lane per block: the Viterbi over 16 positions is inherently
+// sequential; the other lanes hand it their coefficients through LDS.
+#include "vp8_dev.h"
+
+#define K3T 256
+
+struct K3S {
+  uint32_t stats[NSLOT];
+  uint32_t delta[NSLOT];
+  uint16_t lcost[96][MAX_VLEVEL + 1];  // [type*24 + band*3 + ctx][level], incl. fixed cost
+  uint16_t ecost[256];
+  uint16_t mcost4[1000];
+  P4Op p4[160];
+  uint16_t wy[16];
+  uint8_t coeffs[NSLOT];
+  uint32_t mark[33];
+  vp8g_seg seg[4];
+  uint8_t yin[16 * BPS];
+  uint8_t yout[16 * BPS];
+  uint8_t p16[4][256];
+  uint8_t puv[4][128];
+  uint8_t rec16[4][256];
+  uint8_t recuv[4][128];
+  alignas(16) int16_t lv16[4][16][16];   // zigzag levels per mode/block
+  alignas(16) int16_t lvdc[4][16];
+  alignas(16) int16_t co16[4][16][16];   // coefficients (trellis hand-off)
+  int16_t whtq[4][16];
+  int16_t dcs[4][16];
+  alignas(16) int16_t lvuv[4][8][16];
+  int16_t uvdc[4][8];
+  int8_t uvderr[4][2][3];
+  alignas(16) int16_t fin_dc[16];
+  alignas(16) int16_t fin_ac[16][16];
+  alignas(16) int16_t fin_uv[8][16];
+  uint8_t modes[16];
+  uint8_t canvas[17][24];
+  uint8_t rec4[10][16];
+  alignas(16) int16_t lv4[10][16];
+  alignas(16) int16_t co4[10][16];
+  alignas(8) score_t sc4[10];
+  int32_t r4[10][4];               // D, SD, R, nz
+  alignas(16) int16_t acc_ac[16][16];
+  uint8_t acc_out[256];
+  int32_t mres[4][4];
+  int32_t blkinfo[32];
+  uint32_t trnz[4];
+  uint32_t tnodes[64][32];
+  int32_t max_edge[4];
+  int32_t flag;          // dirty flag of finalize_probas_wg
+  int32_t flag_mark;     // some statistics slot needs the in-order replay
+  int32_t flag_ldc;      // left DC nz flag hand-off from wave 0
+  uint8_t yl_mem[17], ul_mem[9], vl_mem[9];
+  uint8_t predleft[4];
+  int8_t lderr[2][2];
+};
+
+// ---------------------------------------------------------------------------
+// 16-lane block primitives. g = first lane of the block's group in the wave,
+// j = natural coefficient / pixel index (x = j & 3, y = j >> 2).
+
+__device__ __forceinline__ int zz_rt(int n) {   // kZigzag[n] for a runtime n
+  return (int)((0xfeb7adc963258410ull >> (4 * n)) & 15);
+}
+
+// FTransform_C (src/dsp/enc.c:157-191): lane holds the residual of pixel
+// (x, y); returns output coefficient j (int16 like the reference's out[]).
+__device__ __forceinline__ int fdct_lane(int d, int g, int x, int y) {
+  const int r = g + 4 * y;
+  const int d0 = __shfl(d, r), d1 = __shfl(d, r + 1), d2 = __shfl(d, r + 2), d3 = __shfl(d, r + 3);
+  const int a0 = d0 + d3, a1 = d1 + d2, a2 = d1 - d2, a3 = d0 - d3;
+  const int t = x == 0 ? (a0 + a1) * 8
+              : x == 1 ? (a2 * 2217 + a3 * 5352 + 1812) >> 9
+              : x == 2 ? (a0 - a1) * 8
+                       : (a3 * 2217 - a2 * 5352 + 937) >> 9;
+  const int t0 = __shfl(t, g + x), t1 = __shfl(t, g + 4 + x);
+  const int t2 = __shfl(t, g + 8 + x), t3 = __shfl(t, g + 12 + x);
+  const int b0 = t0 + t3, b1 = t1 + t2, b2 = t1 - t2, b3 = t0 - t3;
+  const int o = y == 0 ? (b0 + b1 + 7) >> 4
+              : y == 1 ? ((b2 * 2217 + b3 * 5352 + 12000) >> 16) + (b3 != 0)
+              : y == 2 ? (b0 - b1 + 7) >> 4
+                       : (b3 * 2217 - b2 * 5352 + 51000) >> 16;
+  return (int16_t)o;
+}
+
+// ITransformOne (src/dsp/enc.c:116-147): lane holds dequantised coefficient
+// j and the prediction sample of pixel (x, y); returns the reconstruction.
+__device__ __forceinline__ int idct_lane(int c, int pr, int g, int x, int y) {
+  const int c1 = 20091 + (1 << 16), c2 = 35468;
+  const int i0 = __shfl(c, g + x), i1 = __shfl(c, g + 4 + x);
+  const int i2 = __shfl(c, g + 8 + x), i3 = __shfl(c, g + 12 + x);
+  const int a = i0 + i2, b = i0 - i2;
+  const int cc = IMUL(i1, c2) - IMUL(i3, c1), dd = IMUL(i1, c1) + IMUL(i3, c2);
+  const int t = y == 0 ? a + dd : y == 1 ? b + cc : y == 2 ? b - cc : a - dd;  // tmp[4x + y]
+  const int r = g + 4 * y;
+  const int t0 = __shfl(t, r), t1 = __shfl(t, r + 1), t2 = __shfl(t, r + 2), t3 = __shfl(t, r + 3);
+  const int dc = t0 + 4;
+  const int A = dc + t2, B = dc - t2;
+  const int C = IMUL(t1, c2) - IMUL(t3, c1), D = IMUL(t1, c1) + IMUL(t3, c2);
+  const int v = x == 0 ? A + D : x == 1 ? B + C : x == 2 ? B - C : A - D;
+  return clip8(pr + (v >> 3));
+}
+
+// One lane's term of TTransform (src/dsp/enc.c:590-622): weighted |Hadamard
+// coefficient j| of the 4x4 samples p.
+__device__ __forceinline__ int ttrans_lane(int p, int g, int x, int y, int wj) {
+  const int r = g + 4 * y;
+  const int i0 = __shfl(p, r), i1 = __shfl(p, r + 1), i2 = __shfl(p, r + 2), i3 = __shfl(p, r + 3);
+  const int a0 = i0 + i2, a1 = i1 + i3, a2 = i1 - i3, a3 = i0 - i2;
+  const int t = x == 0 ? a0 + a1 : x == 1 ? a3 + a2 : x == 2 ? a3 - a2 : a0 - a1;
+  const int t0 = __shfl(t, g + x), t1 = __shfl(t, g + 4 + x);
+  const int t2 = __shfl(t, g + 8 + x), t3 = __shfl(t, g + 12 + x);
+  const int b0 = t0 + t2, b1 = t1 + t3, b2 = t1 - t3, b3 = t0 - t2;
+  const int o = y == 0 ? b0 + b1 : y == 1 ? b3 + b2 : y == 2 ? b3 - b2 : b0 - b1;
+  return wj * iabs_(o);
+}
+
+__device__ __forceinline__ int sum16(int v) {
+  v += __shfl_xor(v, 8, 16);
+  v += __shfl_xor(v, 4, 16);
+  v += __shfl_xor(v, 2, 16);
+  v += __shfl_xor(v, 1, 16);
+  return v;
+}
+__device__ __forceinline__ int max16(int v) {
+  v = max(v, __shfl_xor(v, 8, 16));
+  v = max(v, __shfl_xor(v, 4, 16));
+  v = max(v, __shfl_xor(v, 2, 16));
+  v = max(v, __shfl_xor(v, 1, 16));
+  return v;
+}
+__device__ __forceinline__ int sum64(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// QuantizeBlock_C for coefficient j (src/dsp/enc.c:653-677)
+__device__ __forceinline__ int quant_lane(int cv, int j, const vp8g_mtx& M, int& dq) {
+  const int neg = cv < 0;
+  const uint32_t coeff = (uint32_t)(neg ? -cv : cv) + M.sharpen[j];
+  int level = 0;
+  if (coeff > M.zthresh[j]) {
+    level = (int)((coeff * M.iq[j] + M.bias[j]) >> QFIX);
+    if (level > MAX_LEVEL) level = MAX_LEVEL;
+    if (neg) level = -level;
+  }
+  dq = (int16_t)(level * (int)M.q[j]);
+  return level;
+}
+
+// GetResidualCost_C (src/dsp/cost.c:322-355) with one zigzag position per
+// lane: the context of position n is the previous position's level (a
+// shuffle), the table reads are independent, and a 16-lane reduction sums.
+__device__ __forceinline__ int rate_lane(const K3S& L, int level, int j, int g, int ctx0, int type,
+                                         int first) {
+  const int n = zz_inv(j);
+  const int v = iabs_(level);
+  const int last = max16((v != 0 && n >= first) ? n : -1);
+  const int vprev = iabs_(__shfl(level, g + zz_rt(n > 0 ? n - 1 : 0)));
+  int cost = 0;
+  if (n >= first && n <= last) {
+    const int ctxp = n == first ? ctx0 : (vprev >= 2 ? 2 : vprev);
+    cost = level_cost(L.lcost[type * 24 + band_of(n) * 3 + ctxp], v);
+    if (n == last && n < 15)
+      cost += bit_cost(L.ecost, 0,
+                       L.coeffs[((type * 8 + band_of(n + 1)) * 3 + (v >= 2 ? 2 : v)) * 11]);
+  }
+  if (j == 0) {
+    const int p0 = L.coeffs[((type * 8 + first) * 3 + ctx0) * 11];   // band(first) == first
+    cost += last < 0 ? bit_cost(L.ecost, 0, p0) : (ctx0 == 0 ? bit_cost(L.ecost, 1, p0) : 0);
+  }
+  return sum16(cost);
+}
+
+// ---------------------------------------------------------------------------
+// Intra16 candidates (quant_enc.c:772-822 ReconstructIntra16, cost_enc.c:232-256
+// VP8GetCostLuma16). Wave m = mode m. Fills rec16/lv16/lvdc and
+// mres[m] = {SSE, texture distortion, rate, nz (ac bits | dc << 24)}.
+
+template <bool TRELLIS>
+__device__ void eval_i16(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid) {
+  const int m = tid >> 6, lane = tid & 63, g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
+  const int bsub = lane >> 4;
+  int co[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int b = 4 * p + bsub, px = 4 * (b & 3) + x, py = 4 * (b >> 2) + y;
+    const int d = L.yin[py * BPS + px] - L.p16[m][py * 16 + px];
+    co[p] = fdct_lane(d, g, x, y);
+    if (j == 0) L.dcs[m][b] = (int16_t)co[p];
+    if (TRELLIS) L.co16[m][b][j] = (int16_t)co[p];
+  }
+  if (lane < 4) L.trnz[lane] = 0;
+  __syncthreads();
+  if (lane < 16) {   // FTransformWHT + y2 quantisation, coefficient b = lane
+    const int16_t* d = L.dcs[m];
+    const int b = lane, r = b >> 2, col = b & 3;
+    int t0[4];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int a0 = d[4 * rr + 0] + d[4 * rr + 2], a1 = d[4 * rr + 1] + d[4 * rr + 3];
+      const int a2 = d[4 * rr + 1] - d[4 * rr + 3], a3 = d[4 * rr + 0] - d[4 * rr + 2];
+      t0[rr] = col == 0 ? a0 + a1 : col == 1 ? a3 + a2 : col == 2 ? a3 - a2 : a0 - a1;
+    }
+    const int a0 = t0[0] + t0[2], a1 = t0[1] + t0[3], a2 = t0[1] - t0[3], a3 = t0[0] - t0[2];
+    int v = r == 0 ? a0 + a1 : r == 1 ? a3 + a2 : r == 2 ? a3 - a2 : a0 - a1;
+    v = (int16_t)(v >> 1);
+    int dq;
+    const int level = quant_lane(v, b, S.y2, dq);
+    L.lvdc[m][zz_inv(b)] = (int16_t)level;
+    L.whtq[m][b] = (int16_t)dq;
+  }
+  int lv[4], dq[4];
+  if constexpr (TRELLIS) {   // quant_enc.c:790-803, anti-diagonal order
+    for (int st = 0; st < 7; ++st) {
+      if (lane < 16) {
+        const int b = lane, bx = b & 3, by = b >> 2;
+        if (bx + by == st) {
+          const uint32_t tm = L.trnz[m];
+          const int tc = by == 0 ? ctx.top(bx) : (int)((tm >> (b - 4)) & 1);
+          const int lc = bx == 0 ? ctx.left(by) : (int)((tm >> (b - 1)) & 1);
+          int c[16];
+#pragma unroll
+          for (int k = 0; k < 16; ++k) c[k] = L.co16[m][b][k];
+          const int nz = trellis_quant(L, L.tnodes[m * 16 + b], c, L.lv16[m][b], tc + lc, 0, &S.y1,
+                                       S.lambda_trellis_i16);
+          L.lv16[m][b][0] = 0;
+#pragma unroll
+          for (int k = 1; k < 16; ++k) L.co16[m][b][k] = (int16_t)c[k];
+          if (nz) atomicOr(&L.trnz[m], 1u << b);
+        }
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int b = 4 * p + bsub;
+      lv[p] = j == 0 ? 0 : L.lv16[m][b][zz_inv(j)];
+      dq[p] = j == 0 ? 0 : L.co16[m][b][j];
+    }
+  } else {   // quant_enc.c:805-812: DC position zeroed before QuantizeBlock
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int b = 4 * p + bsub;
+      lv[p] = quant_lane(j == 0 ? 0 : co[p], j, S.y1, dq[p]);
+      L.lv16[m][b][zz_inv(j)] = (int16_t)lv[p];
+    }
+  }
+  // nz bit per block of this mode
+  uint32_t nzm = 0;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const uint64_t bal = __ballot(lv[p] != 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      nzm |= (((bal >> (16 * q)) & 0xffff) ? 1u : 0u) << (4 * p + q);
+  }
+  // AC rate while the levels are in registers
+  int rate = 0;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int b = 4 * p + bsub, bx = b & 3, by = b >> 2;
+    const int tctx = by == 0 ? ctx.top(bx) : (int)((nzm >> (b - 4)) & 1);
+    const int lctx = bx == 0 ? ctx.left(by) : (int)((nzm >> (b - 1)) & 1);
+    const int r = rate_lane(L, lv[p], j, g, tctx + lctx, 0, 1);
+    if (j == 0) rate += r;
+  }
+  __syncthreads();   // whtq complete
+  // inverse WHT: the DC of each block (dec.c:137-162)
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    if (j == 0) {
+      const int b = 4 * p + bsub;
+      const int16_t* q = L.whtq[m];
+      const int r = b >> 2, col = b & 3;
+      int t[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int a0 = q[i] + q[12 + i], a1 = q[4 + i] + q[8 + i];
+        const int a2 = q[4 + i] - q[8 + i], a3 = q[i] - q[12 + i];
+        t[i] = r == 0 ? a0 + a1 : r == 1 ? a3 + a2 : r == 2 ? a0 - a1 : a3 - a2;
+      }
+      const int dd = t[0] + 3;
+      const int a0 = dd + t[3], a1 = t[1] + t[2], a2 = t[1] - t[2], a3 = dd - t[3];
+      dq[p] = (int16_t)((col == 0 ? a0 + a1 : col == 1 ? a3 + a2 : col == 2 ? a0 - a1 : a3 - a2) >> 3);
+    }
+  }
+  // reconstruction, SSE, texture distortion
+  int sse = 0, tds = 0;
+  const int wj = L.wy[j];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int b = 4 * p + bsub, px = 4 * (b & 3) + x, py = 4 * (b >> 2) + y;
+    const int pr = L.p16[m][py * 16 + px];
+    const int src = L.yin[py * BPS + px];
+    const int rec = idct_lane(dq[p], pr, g, x, y);
+    L.rec16[m][py * 16 + px] = (uint8_t)rec;
+    sse += (src - rec) * (src - rec);
+    const int td = sum16(ttrans_lane(rec, g, x, y, wj) - ttrans_lane(src, g, x, y, wj));
+    if (j == 0) tds += iabs_(td) >> 5;
+  }
+  sse = sum64(sse);
+  tds = sum64(tds);
+  rate = sum64(rate);
+  // DC block rate: lanes 0..15 hold the WHT levels in natural order
+  int dcl = 0;
+  if (lane < 16) dcl = L.lvdc[m][zz_inv(lane)];
+  const int dcnz = __ballot(lane < 16 && dcl != 0) != 0;
+  const int rdc = rate_lane(L, dcl, lane & 15, 0, ctx.top(8) + ctx.left(8), 1, 0);
+  if (lane == 0) {
+    L.mres[m][0] = sse;
+    L.mres[m][1] = tds;
+    L.mres[m][2] = rate + rdc;
+    L.mres[m][3] = (int)(nzm | (dcnz ? (1u << 24) : 0u));
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Chroma candidates (quant_enc.c:875-969 ReconstructUV + CorrectDCValues,
+// cost_enc.c:258-278 VP8GetCostUV). Wave m = mode m, 8 blocks in 2 passes.
+// mres[m] = {SSE, rate, non-zero AC count, nz bits}.
+
+__device__ void eval_uv(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, int x0,
+                        const int8_t* topderr, int use_derr) {
+  const int m = tid >> 6, lane = tid & 63, g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
+  const int bsub = lane >> 4;
+  int co[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int b = 4 * p + bsub, ch = b >> 2, k4 = b & 3;
+    const int px = 8 * ch + 4 * (k4 & 1) + x, py = 4 * (k4 >> 1) + y;
+    const int d = L.yin[py * BPS + 16 + px] - L.puv[m][py * 16 + px];
+    co[p] = fdct_lane(d, g, x, y);
+    if (j == 0) L.uvdc[m][b] = (int16_t)co[p];
+  }
+  __syncthreads();
+  if (use_derr && lane < 2) {   // CorrectDCValues (quant_enc.c:875-906)
+    const int cch = lane;
+    const vp8g_mtx& M = S.uv;
+    const int8_t* top = topderr + 4 * x0 + 2 * cch;
+    const int8_t* left = L.lderr[cch];
+    int16_t* cc = &L.uvdc[m][4 * cch];
+    int err[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      int add;
+      if (k == 0) add = (7 * top[0] + 8 * left[0]) >> 3;
+      else if (k == 1) add = (7 * top[1] + 8 * err[0]) >> 3;
+      else if (k == 2) add = (7 * err[0] + 8 * left[1]) >> 3;
+      else add = (7 * err[1] + 8 * err[2]) >> 3;
+      int V = (int16_t)(cc[k] + add);
+      const int neg = V < 0;
+      if (neg) V = -V;
+      if (V > (int)M.zthresh[0]) {
+        const int qV = (int)(((uint32_t)V * M.iq[0] + M.bias[0]) >> QFIX) * M.q[0];
+        const int e = V - qV;
+        cc[k] = (int16_t)(neg ? -qV : qV);
+        err[k] = (neg ? -e : e) >> 1;
+      } else {
+        cc[k] = 0;
+        err[k] = (neg ? -V : V) >> 1;
+      }
+    }
+    L.uvderr[m][cch][0] = (int8_t)err[1];
+    L.uvderr[m][cch][1] = (int8_t)err[2];
+    L.uvderr[m][cch][2] = (int8_t)err[3];
+  }
+  __syncthreads();
+  int lv[2], dq[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int b = 4 * p + bsub;
+    const int cv = j == 0 ? L.uvdc[m][b] : co[p];
+    lv[p] = quant_lane(cv, j, S.uv, dq[p]);
+    L.lvuv[m][b][zz_inv(j)] = (int16_t)lv[p];
+  }
+  uint32_t nzm = 0;
+  int flatc = 0;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const uint64_t bal = __ballot(lv[p] != 0);
+    const uint64_t bac = __ballot(lv[p] != 0 && j != 0);
+    flatc += __popcll(bac);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      nzm |= (((bal >> (16 * q)) & 0xffff) ? 1u : 0u) << (4 * p + q);
+  }
+  int rate = 0, sse = 0;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int b = 4 * p + bsub, ch = b >> 2, k4 = b & 3, bx = k4 & 1, by = k4 >> 1;
+    const int tctx = by == 0 ? ctx.top(4 + 2 * ch + bx) : (int)((nzm >> (b - 2)) & 1);
+    const int lctx = bx == 0 ? ctx.left(4 + 2 * ch + by) : (int)((nzm >> (b - 1)) & 1);
+    const int r = rate_lane(L, lv[p], j, g, tctx + lctx, 2, 0);
+    if (j == 0) rate += r;
+    const int px = 8 * ch + 4 * bx + x, py = 4 * by + y;
+    const int pr = L.puv[m][py * 16 + px];
+    const int src = L.yin[py * BPS + 16 + px];
+    const int rec = idct_lane(dq[p], pr, g, x, y);
+    L.recuv[m][py * 16 + px] = (uint8_t)rec;
+    sse += (src - rec) * (src - rec);
+  }
+  sse = sum64(sse);
+  rate = sum64(rate);
+  if (lane == 0) {
+    L.mres[m][0] = sse;
+    L.mres[m][1] = rate;
+    L.mres[m][2] = flatc;
+    L.mres[m][3] = (int)nzm;
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Intra4 (quant_enc.c:1072-1165 PickBestIntra4; ReconstructIntra4 :825-858).
+// Threads 0..159 = 10 modes x 16 coefficients. search: RD choice; the
+// reference's early-skip inside the mode loop never changes the winner
+// (the skipped score only grows), so the choice is an argmin with ties to
+// the lower mode. !search: the m5 SimpleQuantize pass over L.modes
+// (quant_enc.c:1230-1240), with trellis contexts from the MB boundary only,
+// as in the reference. Reconstruction lands in acc_out, levels in acc_ac.
+
+struct I4Result {
+  int ok;
+  score_t H, score;
+  uint32_t nz;
+};
+
+__device__ __forceinline__ uint8_t canvas_edge(const K3S& L, int k, int bx, int by) {
+  const int r = 4 * by, cc = 4 * bx;
+  if (k < 4) return L.canvas[r + 4 - k][cc];                // L K J I
+  if (k == 4) return L.canvas[r][cc];                       // X
+  if (k < 9) return L.canvas[r][cc + 1 + (k - 5)];          // A..D
+  return (by > 0 && bx == 3) ? L.canvas[0][17 + k - 9]      // E..H (top-right)
+                             : L.canvas[r][cc + 5 + k - 9];
+}
+
+template <bool TRELLIS>
+__device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, int x0,
+                           int mbw, const uint8_t* predtop, const uint8_t* yl,
+                           const uint8_t* yt, bool search, score_t rd_score, int max_bits) {
+  for (int k = tid; k < 21; k += K3T) {
+    uint8_t v;
+    if (k == 0) v = yl[-1];
+    else if (k <= 16) v = yt[k - 1];
+    else v = (x0 < mbw - 1) ? yt[16 + k - 17] : yt[15];
+    L.canvas[0][k] = v;
+  }
+  if (tid < 16) L.canvas[1 + tid][0] = yl[tid];
+  const int m = tid >> 4, j = tid & 15, g = (tid & 63) & 48, x = j & 3, y = j >> 2;
+  const bool act = tid < 160;
+  const int wj = L.wy[j];
+  uint32_t tnz = ctx.t & 0xf, lnz = ctx.l & 0xf;
+  score_t acc_score = (score_t)211 * S.lambda_mode, accH = 211;
+  uint32_t acc_nz = 0;
+  int total_hdr = 0;
+  I4Result res;
+  res.ok = 1;
+  __syncthreads();
+  for (int i4 = 0; i4 < 16; ++i4) {
+    const int bx = i4 & 3, by = i4 >> 2;
+    const int left_m = bx == 0 ? L.predleft[by] : L.modes[i4 - 1];
+    const int top_m = by == 0 ? predtop[4 * x0 + bx] : L.modes[i4 - 4];
+    const int ctx4 = (int)((tnz >> bx) & 1) + (int)((lnz >> by) & 1);
+    int pr = 0, src = 0, level = 0, dq = 0, rec = 0;
+    if (act) {
+      const P4Op op = L.p4[tid];
+      if (op.kind == 0) {
+        pr = (canvas_edge(L, op.a, bx, by) + 2 * canvas_edge(L, op.b, bx, by) +
+              canvas_edge(L, op.c, bx, by) + 2) >> 2;
+      } else if (op.kind == 1) {
+        pr = (canvas_edge(L, op.a, bx, by) + canvas_edge(L, op.b, bx, by) + 1) >> 1;
+      } else if (op.kind == 2) {
+        pr = canvas_edge(L, op.a, bx, by);
+      } else if (op.kind == 3) {
+        pr = clip8(canvas_edge(L, 5 + x, bx, by) + canvas_edge(L, 3 - y, bx, by) -
+                   canvas_edge(L, 4, bx, by));
+      } else {
+        int s = 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s += canvas_edge(L, k, bx, by) + canvas_edge(L, 5 + k, bx, by);
+        pr = s >> 3;
+      }
+      src = L.yin[(4 * by + y) * BPS + 4 * bx + x];
+    }
+    const int c = fdct_lane(src - pr, g, x, y);
+    if constexpr (TRELLIS) {
+      if (act) L.co4[m][j] = (int16_t)c;
+      __syncthreads();
+      if (act && j == 0) {
+        int cc[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) cc[k] = L.co4[m][k];
+        trellis_quant(L, L.tnodes[m], cc, L.lv4[m], ctx4, 3, &S.y1, S.lambda_trellis_i4);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) L.co4[m][k] = (int16_t)cc[k];
+      }
+      __syncthreads();
+      if (act) {
+        level = L.lv4[m][zz_inv(j)];
+        dq = L.co4[m][j];
+      }
+    } else {
+      if (act) {
+        level = quant_lane(c, j, S.y1, dq);
+        L.lv4[m][zz_inv(j)] = (int16_t)level;
+      }
+    }
+    rec = idct_lane(dq, pr, g, x, y);
+    if (act) L.rec4[m][j] = (uint8_t)rec;
+    const uint64_t bnz = __ballot(act && level != 0);
+    const uint64_t bac = __ballot(act && level != 0 && j != 0);
+    const int gsh = (tid & 63) & 48;
+    const int nzb = ((bnz >> gsh) & 0xffff) != 0;
+    if (search) {
+      const int D = sum16(act ? (src - rec) * (src - rec) : 0);
+      int SD = 0;
+      if (S.tlambda) {
+        const int td = sum16(ttrans_lane(rec, g, x, y, wj) - ttrans_lane(src, g, x, y, wj));
+        SD = (S.tlambda * (iabs_(td) >> 5) + 128) >> 8;
+      }
+      const int cntnz = __popcll((bac >> gsh) & 0xffff);
+      const int R0 = (m > 0 && cntnz <= 3) ? 140 : 0;
+      const int Rc = rate_lane(L, level, j, g, ctx4, 3, 0);
+      if (act && j == 0) {
+        const int H = L.mcost4[(top_m * 10 + left_m) * 10 + m];
+        L.sc4[m] = (score_t)(R0 + Rc + H) * S.lambda_i4 + 256 * (score_t)(D + SD);
+        L.r4[m][0] = D; L.r4[m][1] = SD; L.r4[m][2] = R0 + Rc; L.r4[m][3] = nzb;
+      }
+    } else if (act && j == 0) {
+      L.r4[m][3] = nzb;
+    }
+    __syncthreads();
+    int bm;
+    if (search) {
+      bm = 0;
+      score_t bs = L.sc4[0];
+#pragma unroll
+      for (int k = 1; k < 10; ++k) {
+        const score_t sk = L.sc4[k];
+        if (sk < bs) { bs = sk; bm = k; }
+      }
+      const score_t H = L.mcost4[(top_m * 10 + left_m) * 10 + bm];
+      const score_t bsm = (score_t)(L.r4[bm][2] + H) * S.lambda_mode +
+                          256 * (score_t)(L.r4[bm][0] + L.r4[bm][1]);
+      accH += H;
+      acc_score += bsm;
+      const int bnzv = L.r4[bm][3];
+      acc_nz |= (uint32_t)bnzv << i4;
+      if (acc_score >= rd_score) { res.ok = 0; break; }
+      total_hdr += (int)H;
+      if (total_hdr > max_bits) { res.ok = 0; break; }
+      tnz = (tnz & ~(1u << bx)) | ((uint32_t)bnzv << bx);
+      lnz = (lnz & ~(1u << by)) | ((uint32_t)bnzv << by);
+    } else {
+      bm = L.modes[i4];
+      acc_nz |= (uint32_t)L.r4[bm][3] << i4;
+    }
+    if (tid < 16) {
+      const int py = tid >> 2, px = tid & 3;
+      const uint8_t v = L.rec4[bm][tid];
+      L.canvas[4 * by + 1 + py][4 * bx + 1 + px] = v;
+      L.acc_out[(4 * by + py) * 16 + 4 * bx + px] = v;
+      L.acc_ac[i4][tid] = L.lv4[bm][tid];
+    }
+    if (search && tid == 0) L.modes[i4] = (uint8_t)bm;
+    __syncthreads();
+  }
+  __syncthreads();
+  res.H = accH;
+  res.score = acc_score;
+  res.nz = acc_nz;
+  return res;
+}
+
+// ---------------------------------------------------------------------------
+
+// FinalizeTokenProbas (frame_enc.c:146-180) over the workgroup; returns the
+// reference's "dirty" flag (some probability differs from the default).
+__device__ int finalize_probas_wg(K3S& L, int tid) {
+  if (tid == 0) L.flag = 0;
+  __syncthreads();
+  int changed = 0;
+  for (int s = tid; s < NSLOT; s += K3T) {
+    const uint32_t st = L.stats[s];
+    const int nb = st & 0xffff, total = (st >> 16) & 0xffff;
+    const int upd = (&kVP8CoeffUpdateProba[0][0][0][0])[s];
+    const int old_p = (&kVP8CoeffProba0[0][0][0][0])[s];
+    const int new_p = nb ? (255 - nb * 255 / total) : 255;
+    const int old_cost = nb * bit_cost(L.ecost, 1, old_p) + (total - nb) * bit_cost(L.ecost, 0, old_p) +
+                         bit_cost(L.ecost, 0, upd);
+    const int new_cost = nb * bit_cost(L.ecost, 1, new_p) + (total - nb) * bit_cost(L.ecost, 0, new_p) +
+                         bit_cost(L.ecost, 1, upd) + 8 * 256;
+    if (old_cost > new_cost) {
+      L.coeffs[s] = new_p;
+      changed |= (new_p != old_p);
+    } else {
+      L.coeffs[s] = old_p;
+    }
+  }
+  if (changed) L.flag = 1;
+  __syncthreads();
+  return L.flag;
+}
+
+#define K3_STAMP(i)                                   \
+  do {                                                \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    stamps[i] += t_ - stamp_last;                     \
+    stamp_last = t_;                                  \
+  } while (0)
+
+struct K3Args {
+  const uint8_t* yuv;
+  size_t yfb;
+  int w, h, mbw, mbh;
+  const uint8_t* segmap;
+  const vp8g_frame_params* params;
+  uint16_t* tokens;
+  size_t tok_cap;
+  uint8_t* mbinfo;
+  vp8g_frame_result* results;
+};
+
+__global__ __launch_bounds__(K3T) void k_encode(K3Args a) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  K3S& L = *reinterpret_cast<K3S*>(smem);
+  const int mbw = a.mbw, mbh = a.mbh, nmb = mbw * mbh;
+  uint8_t* ytop = smem + sizeof(K3S);            // 16*mbw + 16
+  uint8_t* uvtop = ytop + 16 * mbw + 16;         // 16*mbw
+  uint32_t* nzw = reinterpret_cast<uint32_t*>(uvtop + 16 * mbw) + 1;   // [-1..mbw-1]
+  uint8_t* predtop = reinterpret_cast<uint8_t*>(nzw + mbw);           // 4*mbw
+  int8_t* topderr = reinterpret_cast<int8_t*>(predtop + 4 * mbw);     // 4*mbw
+
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const bool w0 = tid < 64;
+  const int w = a.w, h = a.h;
+  const int uvw = (w + 1) >> 1, uvh = (h + 1) >> 1;
+  const uint8_t* Yp = a.yuv + f * a.yfb;
+  const uint8_t* Up = Yp + (size_t)w * h;
+  const uint8_t* Vp = Up + (size_t)uvw * uvh;
+  const vp8g_frame_params* P = a.params + f;
+  const uint8_t* segmap = a.segmap + (size_t)f * nmb;
+  uint16_t* tok_base = a.tokens + f * a.tok_cap;
+  uint8_t* mbinfo = a.mbinfo + (size_t)f * nmb * VP8G_MBINFO_BYTES;
+
+  // ---- frame init
+  for (int s = tid; s < NSLOT; s += K3T) {
+    L.stats[s] = 0;
+    L.delta[s] = 0;
+    L.coeffs[s] = (&kVP8CoeffProba0[0][0][0][0])[s];
+  }
+  for (int k = tid; k < 33; k += K3T) L.mark[k] = 0;
+  for (int k = tid; k < 256; k += K3T) L.ecost[k] = kVP8EntropyCost[k];
+  for (int k = tid; k < 1000; k += K3T) L.mcost4[k] = (&kVP8ModeCostI4[0][0][0])[k];
+  for (int k = tid; k < 160; k += K3T) L.p4[k] = (&kP4[0][0])[k];
+  if (tid < 16) L.wy[tid] = kVP8WeightY[tid];
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(P->seg);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(L.seg);
+    for (int k = tid; k < (int)(sizeof(L.seg) / 4); k += K3T) dst[k] = src[k];
+  }
+  for (int k = tid; k < 16 * mbw + 16; k += K3T) ytop[k] = 127;
+  for (int k = tid; k < 16 * mbw; k += K3T) uvtop[k] = 127;
+  for (int k = tid - 1; k < mbw; k += K3T) nzw[k] = 0;
+  for (int k = tid; k < 4 * mbw; k += K3T) { predtop[k] = 0; topderr[k] = 0; }
+  if (tid < 4) L.max_edge[tid] = 0;
+  __syncthreads();
+  level_costs(L, tid, K3T);
+  __syncthreads();
+
+  const int rd_opt = P->rd_opt;
+  const int max_i4_bits = P->max_i4_header_bits;
+  const int use_derr = P->use_derr;
+  const int max_count = P->max_count;
+  int cnt = max_count;
+  uint64_t size_p0 = 0, sse_acc[3] = {0, 0, 0};
+  int nb_i4 = 0, nb_i16 = 0, nb_skip = 0;
+  uint32_t ntok = 0;
+  int tok_err = 0;
+  int left_dc = 0;
+  uint64_t stamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t stamp_last = __builtin_amdgcn_s_memtime();
+  uint8_t* yl = L.yl_mem + 1;
+  uint8_t* ul = L.ul_mem + 1;
+  uint8_t* vl = L.vl_mem + 1;
+
+  for (int mb = 0; mb < nmb; ++mb) {
+    const int x = mb % mbw, y = mb / mbw;
+    if (x == 0) {   // InitLeft (iterator_enc.c:22-32)
+      if (tid < 16) yl[tid] = 129;
+      if (tid < 8) { ul[tid] = 129; vl[tid] = 129; }
+      if (tid == 0) {
+        yl[-1] = ul[-1] = vl[-1] = (y > 0) ? 129 : 127;
+        L.lderr[0][0] = L.lderr[0][1] = L.lderr[1][0] = L.lderr[1][1] = 0;
+      }
+      if (tid < 4) L.predleft[tid] = 0;
+      left_dc = 0;
+    }
+    load_mb(Yp, Up, Vp, w, h, x, y, L.yin, tid, K3T);
+    if (--cnt < 0) {   // frame_enc.c:828-832
+      if (finalize_probas_wg(L, tid)) level_costs(L, tid, K3T);
+      cnt = max_count;
+    }
+    __syncthreads();
+    const int segid = segmap[mb];
+    const vp8g_seg& S = L.seg[segid];
+    const bool hl = x > 0, ht = y > 0;
+    const uint8_t* yt = ytop + 16 * x;
+    const uint8_t* uvt = uvtop + 16 * x;
+    MBCtx ctx;
+    nz_flags(nzw[x], nzw[x - 1], left_dc, ctx);
+
+    // ---- predictions (quant_enc.c:469-479)
+    {
+      const int dcy = dc_value(yl, yt, hl, ht, 16, 5);
+      for (int k = tid; k < 1024; k += K3T) {
+        const int m = k >> 8, p = k & 255;
+        L.p16[m][p] = pred_sample(m, 16, p & 15, p >> 4, yl, yt, hl, ht, dcy);
+      }
+      const int dcu = dc_value(ul, uvt, hl, ht, 8, 4);
+      const int dcv = dc_value(vl, uvt + 8, hl, ht, 8, 4);
+      for (int k = tid; k < 512; k += K3T) {
+        const int m = k >> 7, p = k & 127, px = p & 15, py = p >> 4, c = px >> 3;
+        L.puv[m][p] = pred_sample(m, 8, px & 7, py, c ? vl : ul, uvt + 8 * c, hl, ht, c ? dcv : dcu);
+      }
+    }
+    __syncthreads();
+
+    K3_STAMP(0);
+    // ---- Intra16 (quant_enc.c:1002-1058)
+    const bool trellis_all = rd_opt >= 3;
+    if (trellis_all) eval_i16<true>(L, S, ctx, tid);
+    else eval_i16<false>(L, S, ctx, tid);
+    int best16 = 0;
+    uint32_t nz16 = 0;
+    score_t D16 = 0, SD16 = 0, H16 = 0, R16 = 0;
+    {
+      int same = 1;
+      const int v0 = L.yin[0];
+      same = L.yin[(tid >> 4) * BPS + (tid & 15)] == v0;
+      const int flat0 = __syncthreads_and(same);
+      int flat = flat0;
+      score_t best16_score = 0;
+      for (int mm = 0; mm < 4; ++mm) {
+        score_t Dm = L.mres[mm][0];
+        score_t SDm = S.tlambda ? (score_t)((S.tlambda * L.mres[mm][1] + 128) >> 8) : 0;
+        const score_t Hm = kVP8ModeCostI16[mm];
+        const score_t Rm = L.mres[mm][2];
+        if (flat) {
+          flat = (L.mres[mm][3] & 0xffff) == 0;
+          if (flat) { Dm *= 2; SDm *= 2; }
+        }
+        const score_t sc = (Rm + Hm) * S.lambda_i16 + 256 * (Dm + SDm);
+        if (mm == 0 || sc < best16_score) {
+          best16_score = sc; best16 = mm;
+          D16 = Dm; SD16 = SDm; H16 = Hm; R16 = Rm;
+          nz16 = (uint32_t)L.mres[mm][3];
+        }
+      }
+    }
+    // commit I16 as current best
+    L.yout[(tid >> 4) * BPS + (tid & 15)] = L.rec16[best16][tid];
+    (&L.fin_ac[0][0])[tid] = (&L.lv16[best16][0][0])[tid];
+    if (tid < 16) { L.fin_dc[tid] = L.lvdc[best16][tid]; L.modes[tid] = best16; }
+    score_t rd_score = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
+    score_t rdH = H16;
+    uint32_t rd_nz = nz16;
+    int is_i16 = 1;
+    if ((rd_nz & 0x100ffff) == 0x1000000 && D16 > S.min_disto) {   // StoreMaxDelta
+      int mv = iabs_(L.lvdc[best16][1]);
+      mv = max(mv, iabs_(L.lvdc[best16][2]));
+      mv = max(mv, iabs_(L.lvdc[best16][4]));
+      if (tid == 0 && mv > L.max_edge[segid]) L.max_edge[segid] = mv;
+    }
+    __syncthreads();
+
+    K3_STAMP(1);
+    // ---- Intra4 (quant_enc.c:1072-1165)
+    if (max_i4_bits > 0) {
+      I4Result r4 = trellis_all ? run_i4<true>(L, S, ctx, tid, x, mbw, predtop, yl, yt, true,
+                                               rd_score, max_i4_bits)
+                                : run_i4<false>(L, S, ctx, tid, x, mbw, predtop, yl, yt, true,
+                                                rd_score, max_i4_bits);
+      if (r4.ok) {
+        is_i16 = 0;
+        rdH = r4.H;
+        rd_score = r4.score;
+        rd_nz = r4.nz;
+        L.yout[(tid >> 4) * BPS + (tid & 15)] = L.acc_out[tid];
+        (&L.fin_ac[0][0])[tid] = (&L.acc_ac[0][0])[tid];
+      } else {
+        if (tid < 16) L.modes[tid] = best16;   // the aborted search wrote some
+      }
+      __syncthreads();
+    }
+
+    K3_STAMP(2);
+    // ---- UV (quant_enc.c:1169-1217)
+    int bu = 0;
+    {
+      eval_uv(L, S, ctx, tid, x, topderr, use_derr);
+      score_t bsc = 0, bH = 0;
+      for (int mm = 0; mm < 4; ++mm) {
+        const score_t Dm = L.mres[mm][0], Hm = kVP8ModeCostUV[mm];
+        score_t Rm = L.mres[mm][1];
+        if (mm > 0 && L.mres[mm][2] <= 2) Rm += 140 * 8;
+        const score_t sc = (Rm + Hm) * S.lambda_uv + 256 * Dm;
+        if (mm == 0 || sc < bsc) { bsc = sc; bu = mm; bH = Hm; }
+      }
+      rdH += bH;
+      rd_score += bsc;
+      rd_nz |= (uint32_t)L.mres[bu][3] << 16;
+      if (tid < 128) {
+        L.yout[(tid >> 4) * BPS + 16 + (tid & 15)] = L.recuv[bu][tid];
+        (&L.fin_uv[0][0])[tid] = (&L.lvuv[bu][0][0])[tid];
+      }
+      if (use_derr && tid < 2) {   // StoreDiffusionErrors (quant_enc.c:909-920)
+        const int cch = tid;
+        int8_t* top = topderr + 4 * x + 2 * cch;
+        int8_t* left = L.lderr[cch];
+        const int8_t* e = L.uvderr[bu][cch];
+        left[0] = e[0];
+        left[1] = (int8_t)(3 * e[2] >> 2);
+        top[0] = e[1];
+        top[1] = (int8_t)(e[2] - left[1]);
+      }
+      __syncthreads();
+    }
+
+    // ---- m5: final re-quantisation of the chosen modes with trellis
+    // (SimpleQuantize, quant_enc.c:1222-1245; RD_OPT_TRELLIS, :1384-1387)
+    if (rd_opt == 2) {
+      uint32_t nzq = 0;
+      if (is_i16) {
+        eval_i16<true>(L, S, ctx, tid);
+        L.yout[(tid >> 4) * BPS + (tid & 15)] = L.rec16[best16][tid];
+        (&L.fin_ac[0][0])[tid] = (&L.lv16[best16][0][0])[tid];
+        if (tid < 16) L.fin_dc[tid] = L.lvdc[best16][tid];
+        nzq = (uint32_t)L.mres[best16][3];
+      } else {
+        I4Result r4 = run_i4<true>(L, S, ctx, tid, x, mbw, predtop, yl, yt, false, 0, 0);
+        L.yout[(tid >> 4) * BPS + (tid & 15)] = L.acc_out[tid];
+        (&L.fin_ac[0][0])[tid] = (&L.acc_ac[0][0])[tid];
+        nzq = r4.nz;
+      }
+      __syncthreads();
+      eval_uv(L, S, ctx, tid, x, topderr, use_derr);   // derr state already updated
+      if (tid < 128) {
+        L.yout[(tid >> 4) * BPS + 16 + (tid & 15)] = L.recuv[bu][tid];
+        (&L.fin_uv[0][0])[tid] = (&L.lvuv[bu][0][0])[tid];
+      }
+      rd_nz = nzq | ((uint32_t)L.mres[bu][3] << 16);
+      __syncthreads();
+    }
+    (void)rd_score;
+    K3_STAMP(3);
+
+    // ---- per-MB info + stats side info
+    const int skip = rd_nz == 0;
+    if (tid == 0) {
+      uint8_t* info = mbinfo + (size_t)mb * VP8G_MBINFO_BYTES;
+      info[0] = is_i16; info[1] = bu; info[2] = segid; info[3] = skip;
+      if (is_i16) ++nb_i16; else ++nb_i4;
+      if (skip) ++nb_skip;
+      size_p0 += rdH;
+    }
+    if (tid < 16) mbinfo[(size_t)mb * VP8G_MBINFO_BYTES + 4 + tid] = L.modes[tid];
+    // SSE for WebPAuxStats (frame_enc.c:480-489), wave 0
+    if (w0) {
+      int sy = 0, su = 0, sv = 0;
+      for (int k = lane; k < 256; k += 64) {
+        const int o = (k >> 4) * BPS + (k & 15);
+        const int dd = L.yin[o] - L.yout[o];
+        sy += dd * dd;
+      }
+      {
+        const int o = (lane >> 3) * BPS + 16 + (lane & 7);
+        const int du = L.yin[o] - L.yout[o], dv = L.yin[o + 8] - L.yout[o + 8];
+        su = du * du; sv = dv * dv;
+      }
+      sy = sum64(sy); su = sum64(su); sv = sum64(sv);
+      sse_acc[0] += sy; sse_acc[1] += su; sse_acc[2] += sv;
+    }
+    K3_STAMP(4);
+
+    // ---- tokens + exact statistics (frame_enc.c:411-453, token_enc.c:113-193)
+    const int first_blk = is_i16 ? 0 : 1;
+    uint64_t nzb = 0;
+    int total = 0;
+    if (w0) {
+      int my_ctx = 0, my_type = 0, my_first = 0;
+      const int k = lane;                    // block index 0..24
+      const bool active = k >= first_blk && k < 25;
+      int nzk = 0;
+      if (active) {
+        const int16_t* lvp = blk_levels(L, k);
+        for (int i = 0; i < 16; ++i) nzk |= lvp[i];
+      }
+      nzb = __ballot(active && nzk != 0);
+      if (active) {
+        if (k == 0) {
+          my_type = 1; my_first = 0; my_ctx = ctx.top(8) + ctx.left(8);
+        } else if (k <= 16) {
+          const int b = k - 1, bx = b & 3, by = b >> 2;
+          my_type = is_i16 ? 0 : 3; my_first = is_i16 ? 1 : 0;
+          const int t = by == 0 ? ctx.top(bx) : (int)((nzb >> (k - 4)) & 1);
+          const int l = bx == 0 ? ctx.left(by) : (int)((nzb >> (k - 1)) & 1);
+          my_ctx = t + l;
+        } else {
+          const int b = k - 17, ch = b >> 2, k4 = b & 3, bx = k4 & 1, by = k4 >> 1;
+          my_type = 2; my_first = 0;
+          const int t = by == 0 ? ctx.top(4 + 2 * ch + bx) : (int)((nzb >> (k - 2)) & 1);
+          const int l = bx == 0 ? ctx.left(4 + 2 * ch + by) : (int)((nzb >> (k - 1)) & 1);
+          my_ctx = t + l;
+        }
+        L.blkinfo[k] = my_type | (my_first << 4) | (my_ctx << 8);
+      }
+      int nzdummy;
+      const int mycount = active ? gen_tokens<0>(L, blk_levels(L, k), my_type, my_first, my_ctx,
+                                                 nullptr, &nzdummy)
+                                 : 0;
+      int incl = mycount;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(incl, off);
+        if (lane >= off) incl += v;
+      }
+      total = __shfl(incl, 63);
+      const int excl = incl - mycount;
+      if (ntok + (uint32_t)total > a.tok_cap) tok_err = 1;
+      if (!tok_err && active)
+        gen_tokens<1>(L, blk_levels(L, k), my_type, my_first, my_ctx, tok_base + ntok + excl,
+                      &nzdummy);
+      if (!tok_err) ntok += total;
+    }
+    if (tid == 0) L.flag_mark = 0;
+    __syncthreads();
+    K3_STAMP(5);
+    // fold deltas into the statistics; slots that cross the halving
+    // threshold inside this MB are replayed in token order.
+    {
+      int any_mark = 0;
+      for (int s = tid; s < NSLOT; s += K3T) {
+        const uint32_t dlt = L.delta[s];
+        if (dlt) {
+          const uint32_t p = L.stats[s];
+          if ((p >> 16) + (dlt >> 16) < 0xffffu) {
+            L.stats[s] = p + dlt;
+          } else {
+            atomicOr(&L.mark[s >> 5], 1u << (s & 31));
+            any_mark = 1;
+          }
+          L.delta[s] = 0;
+        }
+      }
+      if (any_mark) L.flag_mark = 1;
+      __syncthreads();
+      if (L.flag_mark) {
+        if (tid == 0) {
+          int nzdummy;
+          for (int kk = first_blk; kk < 25; ++kk) {
+            const int bi = L.blkinfo[kk];
+            gen_tokens<2>(L, blk_levels(L, kk), bi & 15, (bi >> 4) & 15, bi >> 8, nullptr,
+                          &nzdummy);
+          }
+        }
+        __syncthreads();
+        for (int kk = tid; kk < 33; kk += K3T) L.mark[kk] = 0;
+        __syncthreads();
+      }
+    }
+    K3_STAMP(6);
+    // update nz context (iterator_enc.c:267-283) and the left DC flag; nzb
+    // (wave 0) goes to the other waves through LDS
+    if (tid == 0) {
+      int tn[9], ln[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) { tn[i] = ctx.top(i); ln[i] = ctx.left(i); }
+      if (is_i16) { tn[8] = ln[8] = (int)(nzb & 1); }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        tn[i] = (int)((nzb >> (1 + 12 + i)) & 1);      // block (i, 3)
+        ln[i] = (int)((nzb >> (1 + 4 * i + 3)) & 1);   // block (3, i)
+      }
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          tn[4 + 2 * ch + i] = (int)((nzb >> (17 + 4 * ch + 2 + i)) & 1);
+          ln[4 + 2 * ch + i] = (int)((nzb >> (17 + 4 * ch + 2 * i + 1)) & 1);
+        }
+      uint32_t word = 0;
+      word |= (tn[0] << 12) | (tn[1] << 13) | (tn[2] << 14) | (tn[3] << 15) |
+              (tn[4] << 18) | (tn[5] << 19) | (tn[6] << 22) | (tn[7] << 23) | (tn[8] << 24);
+      word |= (ln[0] << 3) | (ln[1] << 7) | (ln[2] << 11) | (ln[4] << 17) | (ln[6] << 21);
+      nzw[x] = word;
+      L.flag_ldc = ln[8];
+    }
+    __syncthreads();
+    left_dc = L.flag_ldc;
+
+    // ---- boundary save (iterator_enc.c:290-313) + mode context
+    if (x < mbw - 1) {
+      if (tid < 16) yl[tid] = L.yout[15 + tid * BPS];
+      if (tid < 8) { ul[tid] = L.yout[16 + 7 + tid * BPS]; vl[tid] = L.yout[24 + 7 + tid * BPS]; }
+      if (tid == 0) { yl[-1] = yt[15]; ul[-1] = uvt[7]; vl[-1] = uvt[15]; }
+    }
+    __syncthreads();
+    if (y < mbh - 1) {
+      if (tid < 16) {
+        ytop[16 * x + tid] = L.yout[15 * BPS + tid];
+        uvtop[16 * x + tid] = L.yout[7 * BPS + 16 + tid];
+      }
+    }
+    if (tid < 4) {
+      predtop[4 * x + tid] = L.modes[12 + tid];
+      L.predleft[tid] = L.modes[4 * tid + 3];
+    }
+    __syncthreads();
+    K3_STAMP(7);
+  }
+
+  // ---- frame epilogue: final probabilities and side results
+  finalize_probas_wg(L, tid);
+  vp8g_frame_result* R = a.results + f;
+  for (int s = tid; s < NSLOT; s += K3T) R->probas[s] = L.coeffs[s];
+  if (tid == 0) {
+    R->ntokens = ntok;
+    R->error = tok_err;
+    for (int s = 0; s < 4; ++s) R->max_edge[s] = L.max_edge[s];
+    R->size_p0 = size_p0;
+    R->sse[0] = sse_acc[0]; R->sse[1] = sse_acc[1]; R->sse[2] = sse_acc[2];
+    R->block_count[0] = nb_i4; R->block_count[1] = nb_i16; R->block_count[2] = nb_skip;
+    for (int i = 0; i < 8; ++i) R->stamps[i] = stamps[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+
+static size_t k3_lds_bytes(int mbw) {
+  return sizeof(K3S) + (16 * mbw + 16) + 16 * mbw + 4 * (mbw + 1) + 4 * mbw + 4 * mbw + 16;
+}
+
+extern "C" int vp8g_launch_encode_w1(const uint8_t* yuv, size_t yfb, int w, int h, int n,
+                                     const uint8_t* segmap, const vp8g_frame_params* params,
+                                     uint16_t* tokens, size_t tok_cap, uint8_t* mbinfo,
+                                     vp8g_frame_result* results, void* stream);
+extern "C" int vp8g_launch_check(const char* what);
+
+extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, int n,
+                                  const uint8_t* segmap, const vp8g_frame_params* params,
+                                  uint16_t* tokens, size_t tok_cap, uint8_t* mbinfo,
+                                  vp8g_frame_result* results, void* stream) {
+  static int variant = -1;
+  if (variant < 0) {
+    const char* v = getenv("WEBP_AMD_K3");
+    variant = (v && v[0] == '1') ? 1 : 2;
+  }
+  if (variant == 1)   // single-wavefront reference kernel (A/B and debugging)
+    return vp8g_launch_encode_w1(yuv, yfb, w, h, n, segmap, params, tokens, tok_cap, mbinfo,
+                                 results, stream);
+  K3Args a;
+  a.yuv = yuv; a.yfb = yfb; a.w = w; a.h = h;
+  a.mbw = (w + 15) >> 4; a.mbh = (h + 15) >> 4;
+  a.segmap = segmap; a.params = params; a.tokens = tokens; a.tok_cap = tok_cap;
+  a.mbinfo = mbinfo; a.results = results;
+  const size_t lds = k3_lds_bytes(a.mbw);
+  if (lds > 160 * 1024) {
+    vp8g_set_error("k_encode", "frame too wide for the LDS budget");
+    return 0;
+  }
+  static int attr_done = 0;
+  if (!attr_done) {
+    (void)hipFuncSetAttribute((const void*)k_encode, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr_done = 1;
+  }
+  hipLaunchKernelGGL(k_encode, dim3(n), dim3(K3T), lds, (hipStream_t)stream, a);
+  return vp8g_launch_check("k_encode");
+}

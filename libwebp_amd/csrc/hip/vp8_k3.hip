@@ -20,6 +20,8 @@
 // sequential; the other lanes hand it their coefficients through LDS.
 #include "vp8_dev.h"
 
+#include <stdio.h>
+
 #define K3T 256
 
 struct K3S {
@@ -1091,12 +1093,30 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
     vp8g_set_error("k_encode", "frame too wide for the LDS budget");
     return 0;
   }
-  static int attr_done = 0;
-  if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)k_encode, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr_done = 1;
+  if (lds > 64 * 1024) {   // beyond the default dynamic-LDS limit: opt in
+    static size_t attr_bytes = 0;
+    if (lds > attr_bytes) {
+      const hipError_t e = hipFuncSetAttribute(
+          (const void*)k_encode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) {
+        vp8g_set_error("k_encode dynamic LDS opt-in", hipGetErrorString(e));
+        return 0;
+      }
+      attr_bytes = lds;
+    }
   }
   hipLaunchKernelGGL(k_encode, dim3(n), dim3(K3T), lds, (hipStream_t)stream, a);
+  if (hipPeekAtLastError() != hipSuccess) {
+    hipFuncAttributes fa;
+    char msg[256];
+    if (hipFuncGetAttributes(&fa, (const void*)k_encode) == hipSuccess) {
+      snprintf(msg, sizeof(msg), "launch failed: lds=%zu static=%zu maxdyn=%d regs=%d maxthr=%d",
+               lds, (size_t)fa.sharedSizeBytes, fa.maxDynamicSharedSizeBytes, fa.numRegs,
+               fa.maxThreadsPerBlock);
+      vp8g_set_error("k_encode", msg);
+      (void)hipGetLastError();
+      return 0;
+    }
+  }
   return vp8g_launch_check("k_encode");
 }

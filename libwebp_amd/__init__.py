@@ -19,7 +19,8 @@ _lib = None
 
 
 def lib_path():
-    return os.path.join(_HERE, "libwebp_amd.so")
+    # WEBP_AMD_LIB selects a diagnostic build (e.g. the K3 sub-stage profile)
+    return os.environ.get("WEBP_AMD_LIB") or os.path.join(_HERE, "libwebp_amd.so")
 
 
 def load():

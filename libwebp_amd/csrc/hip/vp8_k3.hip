@@ -32,6 +32,7 @@ struct K3S {
   uint16_t mcost4[1000];
   P4Op p4[160];
   uint16_t wy[16];
+  uint16_t hc[96][2];              // VP8BitCost(0/1, proba[type][band][ctx][0]) of this epoch
   uint8_t coeffs[NSLOT];
   uint32_t mark[33];
   vp8g_seg seg[4];
@@ -57,12 +58,16 @@ struct K3S {
   uint8_t rec4[10][16];
   alignas(16) int16_t lv4[10][16];
   alignas(16) int16_t co4[10][16];
-  alignas(8) score_t sc4[10];
-  int32_t r4[10][4];               // D, SD, R, nz
+  alignas(8) score_t sc4[10];      // intra4 candidate scores (lambda_i4)
+  alignas(8) score_t sm4[10];      // the same with lambda_mode
+  int32_t r4[10][4];               // H, nz
+  int32_t hsrc[16];                // sum_j w_j |Hadamard(src block)_j| per luma block
   alignas(16) int16_t acc_ac[16][16];
   uint8_t acc_out[256];
   int32_t mres[4][4];
   int32_t blkinfo[32];
+  int32_t blast[32];               // last non-zero zigzag position per token block
+  int32_t wsum[2][4];              // per-wave token-count totals (scan)
   uint32_t trnz[4];
   uint32_t tnodes[64][32];
   int32_t max_edge[4];
@@ -82,113 +87,183 @@ __device__ __forceinline__ int zz_rt(int n) {   // kZigzag[n] for a runtime n
   return (int)((0xfeb7adc963258410ull >> (4 * n)) & 15);
 }
 
+// Cross-lane exchange inside a 16-lane group with DPP (no LDS round trip):
+// quad_perm broadcasts lane k of each 4-lane row of the block, row_ror:4/8/12
+// fetch the same column from the other three rows.
+template <int C>
+__device__ __forceinline__ int dpp(int v) {
+  return __builtin_amdgcn_mov_dpp(v, C, 0xf, 0xf, false);
+}
+#define DPP_QB(k) ((k) | ((k) << 2) | ((k) << 4) | ((k) << 6))
+#define DPP_ROR(n) (0x120 + (n))   // lane i reads lane (i - n) mod 16
+
+// the 4 values of this lane's 4-lane row, in x order
+__device__ __forceinline__ void row4(int v, int& r0, int& r1, int& r2, int& r3) {
+  r0 = dpp<DPP_QB(0)>(v);
+  r1 = dpp<DPP_QB(1)>(v);
+  r2 = dpp<DPP_QB(2)>(v);
+  r3 = dpp<DPP_QB(3)>(v);
+}
+// the 4 values of this lane's column, ROTATED: u_s = row (y - s) & 3
+__device__ __forceinline__ void colrot(int v, int& u0, int& u1, int& u2, int& u3) {
+  u0 = v;
+  u1 = dpp<DPP_ROR(4)>(v);
+  u2 = dpp<DPP_ROR(8)>(v);
+  u3 = dpp<DPP_ROR(12)>(v);
+}
+
+// Per-lane constants that turn the 4x4 butterflies into straight-line
+// multiply-adds (no data-dependent selects or branches): lane j = 4y + x.
+// Column passes see their inputs rotated by the lane's row y (colrot), so
+// their constants are rotated the same way once, here.
+struct TLane {
+  int x, y;
+  int fr[4], frr;          // FTransform row pass: t = (sum fr*d + frr) >> 9
+  int fc[4], fcr, fy1;     // FTransform column pass: (sum fc*u + fcr) >> 16 (+ b3 != 0 on row 1)
+  int ia[4], ib[4], ig[4]; // ITransform vertical: sum ia*u + ib*MUL(u, ig)
+  int is2, ig1, is1, ig3, is3;   // ITransform horizontal
+  int hr[4], hc[4];        // TTransform row / column signs
+};
+
+__device__ __forceinline__ TLane make_tlane(int j) {
+  TLane T;
+  const int x = j & 3, y = j >> 2;
+  T.x = x; T.y = y;
+  const int kC1 = 20091 + (1 << 16), kC2 = 35468;
+  // FTransform_C (src/dsp/enc.c:157-191) row-pass outputs as dot products
+  // with (d0, d1, d2, d3), scaled to a common >> 9
+  const int FR[4][5] = {{4096, 4096, 4096, 4096, 0},
+                        {5352, 2217, -2217, -5352, 1812},
+                        {4096, -4096, -4096, 4096, 0},
+                        {2217, -5352, 5352, -2217, 937}};
+  // column-pass outputs as dot products with (t0, t1, t2, t3), common >> 16
+  const int FC[4][5] = {{4096, 4096, 4096, 4096, 7 * 4096},
+                        {5352, 2217, -2217, -5352, 12000},
+                        {4096, -4096, -4096, 4096, 7 * 4096},
+                        {2217, -5352, 5352, -2217, 51000}};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) T.fr[k] = FR[x][k];
+  T.frr = FR[x][4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) T.fc[s] = FC[y][(y - s) & 3];
+  T.fcr = FC[y][4];
+  T.fy1 = y == 1;
+  // ITransformOne vertical pass (src/dsp/enc.c:116-133): output index y of
+  // column x is +-in0 +-in2 +-MUL(in1, c) +-MUL(in3, c')
+  const int VA[4][4] = {{1, 0, 1, 0}, {1, 0, -1, 0}, {1, 0, -1, 0}, {1, 0, 1, 0}};
+  const int VB[4][4] = {{0, 1, 0, 1}, {0, 1, 0, -1}, {0, -1, 0, 1}, {0, -1, 0, -1}};
+  const int VG[4][4] = {{0, kC1, 0, kC2}, {0, kC2, 0, kC1}, {0, kC2, 0, kC1}, {0, kC1, 0, kC2}};
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int k = (y - s) & 3;
+    T.ia[s] = VA[y][k]; T.ib[s] = VB[y][k]; T.ig[s] = VG[y][k];
+  }
+  // horizontal pass (:134-146): dc + 4 +-t2 +-MUL(t1, c) +-MUL(t3, c')
+  const int HS2[4] = {1, -1, -1, 1};
+  const int HG1[4] = {kC1, kC2, kC2, kC1}, HS1[4] = {1, 1, -1, -1};
+  const int HG3[4] = {kC2, kC1, kC1, kC2}, HS3[4] = {1, -1, 1, -1};
+  T.is2 = HS2[x]; T.ig1 = HG1[x]; T.is1 = HS1[x]; T.ig3 = HG3[x]; T.is3 = HS3[x];
+  // TTransform (:590-622): both passes are +-1 sums
+  const int TS[4][4] = {{1, 1, 1, 1}, {1, 1, -1, -1}, {1, -1, -1, 1}, {1, -1, 1, -1}};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) T.hr[k] = TS[x][k];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) T.hc[s] = TS[y][(y - s) & 3];
+  return T;
+}
+
 // FTransform_C (src/dsp/enc.c:157-191): lane holds the residual of pixel
 // (x, y); returns output coefficient j (int16 like the reference's out[]).
-__device__ __forceinline__ int fdct_lane(int d, int g, int x, int y) {
-  const int r = g + 4 * y;
-  const int d0 = __shfl(d, r), d1 = __shfl(d, r + 1), d2 = __shfl(d, r + 2), d3 = __shfl(d, r + 3);
-  const int a0 = d0 + d3, a1 = d1 + d2, a2 = d1 - d2, a3 = d0 - d3;
-  const int t = x == 0 ? (a0 + a1) * 8
-              : x == 1 ? (a2 * 2217 + a3 * 5352 + 1812) >> 9
-              : x == 2 ? (a0 - a1) * 8
-                       : (a3 * 2217 - a2 * 5352 + 937) >> 9;
-  const int t0 = __shfl(t, g + x), t1 = __shfl(t, g + 4 + x);
-  const int t2 = __shfl(t, g + 8 + x), t3 = __shfl(t, g + 12 + x);
-  const int b0 = t0 + t3, b1 = t1 + t2, b2 = t1 - t2, b3 = t0 - t3;
-  const int o = y == 0 ? (b0 + b1 + 7) >> 4
-              : y == 1 ? ((b2 * 2217 + b3 * 5352 + 12000) >> 16) + (b3 != 0)
-              : y == 2 ? (b0 - b1 + 7) >> 4
-                       : (b3 * 2217 - b2 * 5352 + 51000) >> 16;
+__device__ __forceinline__ int fdct_lane(int d, const TLane& T) {
+  int d0, d1, d2, d3;
+  row4(d, d0, d1, d2, d3);
+  const int t = (T.fr[0] * d0 + T.fr[1] * d1 + T.fr[2] * d2 + T.fr[3] * d3 + T.frr) >> 9;
+  int u0, u1, u2, u3;
+  colrot(t, u0, u1, u2, u3);
+  const int o = ((T.fc[0] * u0 + T.fc[1] * u1 + T.fc[2] * u2 + T.fc[3] * u3 + T.fcr) >> 16) +
+                (T.fy1 & (u1 != u2));   // row 1: + (a3 != 0), a3 = t0 - t3 = u1 - u2
   return (int16_t)o;
 }
 
 // ITransformOne (src/dsp/enc.c:116-147): lane holds dequantised coefficient
 // j and the prediction sample of pixel (x, y); returns the reconstruction.
-__device__ __forceinline__ int idct_lane(int c, int pr, int g, int x, int y) {
-  const int c1 = 20091 + (1 << 16), c2 = 35468;
-  const int i0 = __shfl(c, g + x), i1 = __shfl(c, g + 4 + x);
-  const int i2 = __shfl(c, g + 8 + x), i3 = __shfl(c, g + 12 + x);
-  const int a = i0 + i2, b = i0 - i2;
-  const int cc = IMUL(i1, c2) - IMUL(i3, c1), dd = IMUL(i1, c1) + IMUL(i3, c2);
-  const int t = y == 0 ? a + dd : y == 1 ? b + cc : y == 2 ? b - cc : a - dd;  // tmp[4x + y]
-  const int r = g + 4 * y;
-  const int t0 = __shfl(t, r), t1 = __shfl(t, r + 1), t2 = __shfl(t, r + 2), t3 = __shfl(t, r + 3);
-  const int dc = t0 + 4;
-  const int A = dc + t2, B = dc - t2;
-  const int C = IMUL(t1, c2) - IMUL(t3, c1), D = IMUL(t1, c1) + IMUL(t3, c2);
-  const int v = x == 0 ? A + D : x == 1 ? B + C : x == 2 ? B - C : A - D;
+__device__ __forceinline__ int idct_lane(int c, int pr, const TLane& T) {
+  int u0, u1, u2, u3;
+  colrot(c, u0, u1, u2, u3);
+  const int t = T.ia[0] * u0 + T.ib[0] * IMUL(u0, T.ig[0]) + T.ia[1] * u1 +
+                T.ib[1] * IMUL(u1, T.ig[1]) + T.ia[2] * u2 + T.ib[2] * IMUL(u2, T.ig[2]) +
+                T.ia[3] * u3 + T.ib[3] * IMUL(u3, T.ig[3]);   // tmp[4x + y]
+  int t0, t1, t2, t3;
+  row4(t, t0, t1, t2, t3);
+  const int v = t0 + 4 + T.is2 * t2 + T.is1 * IMUL(t1, T.ig1) + T.is3 * IMUL(t3, T.ig3);
   return clip8(pr + (v >> 3));
 }
 
 // One lane's term of TTransform (src/dsp/enc.c:590-622): weighted |Hadamard
 // coefficient j| of the 4x4 samples p.
-__device__ __forceinline__ int ttrans_lane(int p, int g, int x, int y, int wj) {
-  const int r = g + 4 * y;
-  const int i0 = __shfl(p, r), i1 = __shfl(p, r + 1), i2 = __shfl(p, r + 2), i3 = __shfl(p, r + 3);
-  const int a0 = i0 + i2, a1 = i1 + i3, a2 = i1 - i3, a3 = i0 - i2;
-  const int t = x == 0 ? a0 + a1 : x == 1 ? a3 + a2 : x == 2 ? a3 - a2 : a0 - a1;
-  const int t0 = __shfl(t, g + x), t1 = __shfl(t, g + 4 + x);
-  const int t2 = __shfl(t, g + 8 + x), t3 = __shfl(t, g + 12 + x);
-  const int b0 = t0 + t2, b1 = t1 + t3, b2 = t1 - t3, b3 = t0 - t2;
-  const int o = y == 0 ? b0 + b1 : y == 1 ? b3 + b2 : y == 2 ? b3 - b2 : b0 - b1;
+__device__ __forceinline__ int ttrans_lane(int p, const TLane& T, int wj) {
+  int i0, i1, i2, i3;
+  row4(p, i0, i1, i2, i3);
+  const int t = T.hr[0] * i0 + T.hr[1] * i1 + T.hr[2] * i2 + T.hr[3] * i3;
+  int u0, u1, u2, u3;
+  colrot(t, u0, u1, u2, u3);
+  const int o = T.hc[0] * u0 + T.hc[1] * u1 + T.hc[2] * u2 + T.hc[3] * u3;
   return wj * iabs_(o);
 }
 
 __device__ __forceinline__ int sum16(int v) {
-  v += __shfl_xor(v, 8, 16);
-  v += __shfl_xor(v, 4, 16);
-  v += __shfl_xor(v, 2, 16);
-  v += __shfl_xor(v, 1, 16);
+  v += dpp<DPP_ROR(8)>(v);
+  v += dpp<DPP_ROR(4)>(v);
+  v += dpp<DPP_ROR(2)>(v);
+  v += dpp<DPP_ROR(1)>(v);
   return v;
 }
 __device__ __forceinline__ int max16(int v) {
-  v = max(v, __shfl_xor(v, 8, 16));
-  v = max(v, __shfl_xor(v, 4, 16));
-  v = max(v, __shfl_xor(v, 2, 16));
-  v = max(v, __shfl_xor(v, 1, 16));
+  v = max(v, dpp<DPP_ROR(8)>(v));
+  v = max(v, dpp<DPP_ROR(4)>(v));
+  v = max(v, dpp<DPP_ROR(2)>(v));
+  v = max(v, dpp<DPP_ROR(1)>(v));
   return v;
 }
+// wave total (uniform): 16-lane sums, then the four row results
 __device__ __forceinline__ int sum64(int v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v = sum16(v);
+  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) +
+         __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
 }
 
 // QuantizeBlock_C for coefficient j (src/dsp/enc.c:653-677)
 __device__ __forceinline__ int quant_lane(int cv, int j, const vp8g_mtx& M, int& dq) {
   const int neg = cv < 0;
   const uint32_t coeff = (uint32_t)(neg ? -cv : cv) + M.sharpen[j];
-  int level = 0;
-  if (coeff > M.zthresh[j]) {
-    level = (int)((coeff * M.iq[j] + M.bias[j]) >> QFIX);
-    if (level > MAX_LEVEL) level = MAX_LEVEL;
-    if (neg) level = -level;
-  }
+  int level = min((int)((coeff * M.iq[j] + M.bias[j]) >> QFIX), MAX_LEVEL);
+  level = coeff > M.zthresh[j] ? level : 0;
+  level = neg ? -level : level;
   dq = (int16_t)(level * (int)M.q[j]);
   return level;
 }
 
 // GetResidualCost_C (src/dsp/cost.c:322-355) with one zigzag position per
-// lane: the context of position n is the previous position's level (a
-// shuffle), the table reads are independent, and a 16-lane reduction sums.
+// lane: the context of position n is the previous position's level (one
+// bpermute), every lane does its table reads unconditionally (no divergent
+// branches) and a 16-lane reduction sums the terms.
 __device__ __forceinline__ int rate_lane(const K3S& L, int level, int j, int g, int ctx0, int type,
                                          int first) {
   const int n = zz_inv(j);
   const int v = iabs_(level);
   const int last = max16((v != 0 && n >= first) ? n : -1);
   const int vprev = iabs_(__shfl(level, g + zz_rt(n > 0 ? n - 1 : 0)));
-  int cost = 0;
-  if (n >= first && n <= last) {
-    const int ctxp = n == first ? ctx0 : (vprev >= 2 ? 2 : vprev);
-    cost = level_cost(L.lcost[type * 24 + band_of(n) * 3 + ctxp], v);
-    if (n == last && n < 15)
-      cost += bit_cost(L.ecost, 0,
-                       L.coeffs[((type * 8 + band_of(n + 1)) * 3 + (v >= 2 ? 2 : v)) * 11]);
-  }
-  if (j == 0) {
-    const int p0 = L.coeffs[((type * 8 + first) * 3 + ctx0) * 11];   // band(first) == first
-    cost += last < 0 ? bit_cost(L.ecost, 0, p0) : (ctx0 == 0 ? bit_cost(L.ecost, 1, p0) : 0);
-  }
+  const int ctxp = n == first ? ctx0 : min(vprev, 2);
+  int cost = L.lcost[type * 24 + band_of(n) * 3 + ctxp][min(v, MAX_VLEVEL)];
+  if (v > MAX_VLEVEL)   // rare: beyond the LDS rows
+    cost += kVP8LevelFixedCost[v] - kVP8LevelFixedCost[MAX_VLEVEL];
+  const int eob = L.hc[type * 24 + band_of(n + 1) * 3 + min(v, 2)][0];
+  cost += (n == last && n < 15) ? eob : 0;
+  cost = (n >= first && n <= last) ? cost : 0;
+  const int t0 = type * 24 + first * 3 + ctx0;   // band(first) == first
+  const int h0 = L.hc[t0][0], h1 = L.hc[t0][1];
+  const int hdr = last < 0 ? h0 : (ctx0 == 0 ? h1 : 0);
+  cost += j == 0 ? hdr : 0;
   return sum16(cost);
 }
 
@@ -201,12 +276,13 @@ template <bool TRELLIS>
 __device__ void eval_i16(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid) {
   const int m = tid >> 6, lane = tid & 63, g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
   const int bsub = lane >> 4;
+  const TLane T = make_tlane(j);
   int co[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const int b = 4 * p + bsub, px = 4 * (b & 3) + x, py = 4 * (b >> 2) + y;
     const int d = L.yin[py * BPS + px] - L.p16[m][py * 16 + px];
-    co[p] = fdct_lane(d, g, x, y);
+    co[p] = fdct_lane(d, T);
     if (j == 0) L.dcs[m][b] = (int16_t)co[p];
     if (TRELLIS) L.co16[m][b][j] = (int16_t)co[p];
   }
@@ -313,10 +389,10 @@ __device__ void eval_i16(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid) {
     const int b = 4 * p + bsub, px = 4 * (b & 3) + x, py = 4 * (b >> 2) + y;
     const int pr = L.p16[m][py * 16 + px];
     const int src = L.yin[py * BPS + px];
-    const int rec = idct_lane(dq[p], pr, g, x, y);
+    const int rec = idct_lane(dq[p], pr, T);
     L.rec16[m][py * 16 + px] = (uint8_t)rec;
     sse += (src - rec) * (src - rec);
-    const int td = sum16(ttrans_lane(rec, g, x, y, wj) - ttrans_lane(src, g, x, y, wj));
+    const int td = sum16(ttrans_lane(rec, T, wj)) - L.hsrc[b];
     if (j == 0) tds += iabs_(td) >> 5;
   }
   sse = sum64(sse);
@@ -345,13 +421,14 @@ __device__ void eval_uv(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, in
                         const int8_t* topderr, int use_derr) {
   const int m = tid >> 6, lane = tid & 63, g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
   const int bsub = lane >> 4;
+  const TLane T = make_tlane(j);
   int co[2];
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     const int b = 4 * p + bsub, ch = b >> 2, k4 = b & 3;
     const int px = 8 * ch + 4 * (k4 & 1) + x, py = 4 * (k4 >> 1) + y;
     const int d = L.yin[py * BPS + 16 + px] - L.puv[m][py * 16 + px];
-    co[p] = fdct_lane(d, g, x, y);
+    co[p] = fdct_lane(d, T);
     if (j == 0) L.uvdc[m][b] = (int16_t)co[p];
   }
   __syncthreads();
@@ -417,7 +494,7 @@ __device__ void eval_uv(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, in
     const int px = 8 * ch + 4 * bx + x, py = 4 * by + y;
     const int pr = L.puv[m][py * 16 + px];
     const int src = L.yin[py * BPS + 16 + px];
-    const int rec = idct_lane(dq[p], pr, g, x, y);
+    const int rec = idct_lane(dq[p], pr, T);
     L.recuv[m][py * 16 + px] = (uint8_t)rec;
     sse += (src - rec) * (src - rec);
   }
@@ -441,6 +518,28 @@ __device__ void eval_uv(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, in
 // (quant_enc.c:1230-1240), with trellis contexts from the MB boundary only,
 // as in the reference. Reconstruction lands in acc_out, levels in acc_ac.
 
+// Diagnostic build only (-DK3_SUBPROF): cycle split of the intra4 loop; a
+// stamp waits for outstanding LDS ops, so that build's total runs slower.
+#ifdef K3_SUBPROF
+__device__ __forceinline__ uint64_t k3_clock() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define SUBST(i)                      \
+  do {                                \
+    const uint64_t t_ = k3_clock();   \
+    sp[i] += t_ - sp_last;            \
+    sp_last = t_;                     \
+  } while (0)
+#else
+#define SUBST(i) \
+  do {           \
+  } while (0)
+#endif
+
 struct I4Result {
   int ok;
   score_t H, score;
@@ -456,10 +555,48 @@ __device__ __forceinline__ uint8_t canvas_edge(const K3S& L, int k, int bx, int 
                              : L.canvas[r][cc + 5 + k - 9];
 }
 
+// Branch-free 4x4 intra predictor sample (src/dsp/enc.c:351-512) for this
+// lane's (mode, pixel): pred = clip((wa*ea + wb*eb + wc*ec + rnd) >> sh) over
+// edge samples e = L K J I X A B C D E F G H read straight from the canvas;
+// DC averages 8 edges.
+struct P4Lane {
+  int8_t ia, ib, ic, wa, wb, wc, rnd, sh;
+  int dc;
+};
+__device__ __forceinline__ P4Lane p4_lane(const P4Op& op, int x, int y) {
+  P4Lane r;
+  r.dc = op.kind == 4;
+  if (op.kind == 0) {        // AVG3(a, b, c) = (a + 2b + c + 2) >> 2
+    r.ia = op.a; r.ib = op.b; r.ic = op.c; r.wa = 1; r.wb = 2; r.wc = 1; r.rnd = 2; r.sh = 2;
+  } else if (op.kind == 1) { // AVG2(a, b) = (a + b + 1) >> 1
+    r.ia = op.a; r.ib = op.b; r.ic = 0; r.wa = 1; r.wb = 1; r.wc = 0; r.rnd = 1; r.sh = 1;
+  } else if (op.kind == 2) { // copy
+    r.ia = op.a; r.ib = 0; r.ic = 0; r.wa = 1; r.wb = 0; r.wc = 0; r.rnd = 0; r.sh = 0;
+  } else if (op.kind == 3) { // TM: clip(top[x] + left[y] - corner)
+    r.ia = 5 + x; r.ib = 3 - y; r.ic = 4; r.wa = 1; r.wb = 1; r.wc = -1; r.rnd = 0; r.sh = 0;
+  } else {                   // DC
+    r.ia = 0; r.ib = 0; r.ic = 0; r.wa = 0; r.wb = 0; r.wc = 0; r.rnd = 0; r.sh = 0;
+  }
+  return r;
+}
+// canvas byte offset of edge k of sub-block (bx, by): rows of 24 bytes,
+// row 0 = the row above the MB, column 0 = the column left of it
+__device__ __forceinline__ int edge_off(int k, int bx, int by) {
+  const int r = 4 * by, cc = 4 * bx;
+  const bool tr = k >= 9 && by > 0 && bx == 3;   // top-right from the MB above
+  const int row = k < 4 ? r + 4 - k : (tr ? 0 : r);
+  const int col = k < 4 ? cc : (tr ? k + 8 : cc + k - 4);
+  return row * 24 + col;
+}
+
 template <bool TRELLIS>
 __device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, int x0,
                            int mbw, const uint8_t* predtop, const uint8_t* yl,
-                           const uint8_t* yt, bool search, score_t rd_score, int max_bits) {
+                           const uint8_t* yt, bool search, score_t rd_score, int max_bits,
+                           uint64_t* sp) {
+#ifdef K3_SUBPROF
+  uint64_t sp_last = k3_clock();
+#endif
   for (int k = tid; k < 21; k += K3T) {
     uint8_t v;
     if (k == 0) v = yl[-1];
@@ -471,6 +608,13 @@ __device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid,
   const int m = tid >> 4, j = tid & 15, g = (tid & 63) & 48, x = j & 3, y = j >> 2;
   const bool act = tid < 160;
   const int wj = L.wy[j];
+  const TLane T = make_tlane(j);
+  const P4Lane pl = p4_lane(L.p4[act ? tid : 0], x, y);
+  // this lane's y1 quantiser entries, once per MB
+  const vp8g_mtx& M = S.y1;
+  const uint32_t q_sh = M.sharpen[j], q_zt = M.zthresh[j], q_iq = M.iq[j], q_bias = M.bias[j];
+  const int q_q = M.q[j];
+  const uint8_t* cv = &L.canvas[0][0];
   uint32_t tnz = ctx.t & 0xf, lnz = ctx.l & 0xf;
   score_t acc_score = (score_t)211 * S.lambda_mode, accH = 211;
   uint32_t acc_nz = 0;
@@ -483,28 +627,24 @@ __device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid,
     const int left_m = bx == 0 ? L.predleft[by] : L.modes[i4 - 1];
     const int top_m = by == 0 ? predtop[4 * x0 + bx] : L.modes[i4 - 4];
     const int ctx4 = (int)((tnz >> bx) & 1) + (int)((lnz >> by) & 1);
-    int pr = 0, src = 0, level = 0, dq = 0, rec = 0;
-    if (act) {
-      const P4Op op = L.p4[tid];
-      if (op.kind == 0) {
-        pr = (canvas_edge(L, op.a, bx, by) + 2 * canvas_edge(L, op.b, bx, by) +
-              canvas_edge(L, op.c, bx, by) + 2) >> 2;
-      } else if (op.kind == 1) {
-        pr = (canvas_edge(L, op.a, bx, by) + canvas_edge(L, op.b, bx, by) + 1) >> 1;
-      } else if (op.kind == 2) {
-        pr = canvas_edge(L, op.a, bx, by);
-      } else if (op.kind == 3) {
-        pr = clip8(canvas_edge(L, 5 + x, bx, by) + canvas_edge(L, 3 - y, bx, by) -
-                   canvas_edge(L, 4, bx, by));
-      } else {
-        int s = 4;
+    const int src = L.yin[(4 * by + y) * BPS + 4 * bx + x];
+    int pr;
+    {
+      const int ea = cv[edge_off(pl.ia, bx, by)];
+      const int eb = cv[edge_off(pl.ib, bx, by)];
+      const int ec = cv[edge_off(pl.ic, bx, by)];
+      pr = clip8((pl.wa * ea + pl.wb * eb + pl.wc * ec + pl.rnd) >> pl.sh);
+      if (pl.dc) {
+        int s4 = 4;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) s += canvas_edge(L, k, bx, by) + canvas_edge(L, 5 + k, bx, by);
-        pr = s >> 3;
+        for (int k = 0; k < 4; ++k) s4 += cv[edge_off(k, bx, by)] + cv[edge_off(5 + k, bx, by)];
+        pr = s4 >> 3;
       }
-      src = L.yin[(4 * by + y) * BPS + 4 * bx + x];
     }
-    const int c = fdct_lane(src - pr, g, x, y);
+    SUBST(0);
+    const int c = fdct_lane(src - pr, T);
+    SUBST(1);
+    int level = 0, dq = 0;
     if constexpr (TRELLIS) {
       if (act) L.co4[m][j] = (int16_t)c;
       __syncthreads();
@@ -521,71 +661,74 @@ __device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid,
         level = L.lv4[m][zz_inv(j)];
         dq = L.co4[m][j];
       }
-    } else {
-      if (act) {
-        level = quant_lane(c, j, S.y1, dq);
-        L.lv4[m][zz_inv(j)] = (int16_t)level;
-      }
+    } else {   // QuantizeBlock_C (src/dsp/enc.c:653-677)
+      const int neg = c < 0;
+      const uint32_t coeff = (uint32_t)(neg ? -c : c) + q_sh;
+      level = min((int)((coeff * q_iq + q_bias) >> QFIX), MAX_LEVEL);
+      level = coeff > q_zt ? level : 0;
+      level = neg ? -level : level;
+      dq = (int16_t)(level * q_q);
     }
-    rec = idct_lane(dq, pr, g, x, y);
-    if (act) L.rec4[m][j] = (uint8_t)rec;
+    SUBST(2);
+    const int rec = idct_lane(dq, pr, T);
     const uint64_t bnz = __ballot(act && level != 0);
     const uint64_t bac = __ballot(act && level != 0 && j != 0);
-    const int gsh = (tid & 63) & 48;
-    const int nzb = ((bnz >> gsh) & 0xffff) != 0;
+    const int nzb = ((bnz >> g) & 0xffff) != 0;
+    SUBST(3);
     if (search) {
-      const int D = sum16(act ? (src - rec) * (src - rec) : 0);
+      const int D = sum16((src - rec) * (src - rec));
       int SD = 0;
       if (S.tlambda) {
-        const int td = sum16(ttrans_lane(rec, g, x, y, wj) - ttrans_lane(src, g, x, y, wj));
+        const int td = sum16(ttrans_lane(rec, T, wj)) - L.hsrc[i4];
         SD = (S.tlambda * (iabs_(td) >> 5) + 128) >> 8;
       }
-      const int cntnz = __popcll((bac >> gsh) & 0xffff);
+      SUBST(4);
+      const int cntnz = __popcll((bac >> g) & 0xffff);
       const int R0 = (m > 0 && cntnz <= 3) ? 140 : 0;
       const int Rc = rate_lane(L, level, j, g, ctx4, 3, 0);
       if (act && j == 0) {
         const int H = L.mcost4[(top_m * 10 + left_m) * 10 + m];
-        L.sc4[m] = (score_t)(R0 + Rc + H) * S.lambda_i4 + 256 * (score_t)(D + SD);
-        L.r4[m][0] = D; L.r4[m][1] = SD; L.r4[m][2] = R0 + Rc; L.r4[m][3] = nzb;
+        const score_t dist = 256 * (score_t)(D + SD);
+        L.sc4[m] = (score_t)(R0 + Rc + H) * S.lambda_i4 + dist;
+        L.sm4[m] = (score_t)(R0 + Rc + H) * S.lambda_mode + dist;
+        L.r4[m][0] = H;
+        L.r4[m][1] = nzb;
       }
-    } else if (act && j == 0) {
-      L.r4[m][3] = nzb;
     }
+    SUBST(5);
     __syncthreads();
     int bm;
     if (search) {
       bm = 0;
       score_t bs = L.sc4[0];
 #pragma unroll
-      for (int k = 1; k < 10; ++k) {
+      for (int k = 1; k < 10; ++k) {   // argmin, ties to the lower mode
         const score_t sk = L.sc4[k];
         if (sk < bs) { bs = sk; bm = k; }
       }
-      const score_t H = L.mcost4[(top_m * 10 + left_m) * 10 + bm];
-      const score_t bsm = (score_t)(L.r4[bm][2] + H) * S.lambda_mode +
-                          256 * (score_t)(L.r4[bm][0] + L.r4[bm][1]);
+      const int H = L.r4[bm][0], bnzv = L.r4[bm][1];
       accH += H;
-      acc_score += bsm;
-      const int bnzv = L.r4[bm][3];
+      acc_score += L.sm4[bm];
       acc_nz |= (uint32_t)bnzv << i4;
       if (acc_score >= rd_score) { res.ok = 0; break; }
-      total_hdr += (int)H;
+      total_hdr += H;
       if (total_hdr > max_bits) { res.ok = 0; break; }
       tnz = (tnz & ~(1u << bx)) | ((uint32_t)bnzv << bx);
       lnz = (lnz & ~(1u << by)) | ((uint32_t)bnzv << by);
     } else {
       bm = L.modes[i4];
-      acc_nz |= (uint32_t)L.r4[bm][3] << i4;
     }
-    if (tid < 16) {
-      const int py = tid >> 2, px = tid & 3;
-      const uint8_t v = L.rec4[bm][tid];
-      L.canvas[4 * by + 1 + py][4 * bx + 1 + px] = v;
-      L.acc_out[(4 * by + py) * 16 + 4 * bx + px] = v;
-      L.acc_ac[i4][tid] = L.lv4[bm][tid];
+    SUBST(6);
+    if (act && m == bm) {   // the winning mode's lanes commit their own results
+      L.canvas[4 * by + 1 + y][4 * bx + 1 + x] = (uint8_t)rec;
+      L.acc_out[(4 * by + y) * 16 + 4 * bx + x] = (uint8_t)rec;
+      L.acc_ac[i4][zz_inv(j)] = (int16_t)level;
+      if (!search && j == 0) L.r4[0][2] = nzb;
     }
     if (search && tid == 0) L.modes[i4] = (uint8_t)bm;
     __syncthreads();
+    if (!search) acc_nz |= (uint32_t)L.r4[0][2] << i4;
+    SUBST(7);
   }
   __syncthreads();
   res.H = accH;
@@ -595,6 +738,74 @@ __device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid,
 }
 
 // ---------------------------------------------------------------------------
+
+// The tokens of zigzag position n of one block (VP8RecordCoeffTokens,
+// token_enc.c:113-193, restated per position): the "more coefficients"
+// check (only at the first position and after a non-zero level), the zero
+// check and, for a non-zero level, its value tokens and sign. The context of
+// position n is the previous level. Returns the token count; EMIT writes the
+// tokens and adds their statistics deltas.
+template <bool EMIT>
+__device__ __forceinline__ int pos_tokens(K3S& L, int type, int first, int ctx0, int n, int c,
+                                          int cprev, int last, uint16_t* out) {
+  if (n < first) return 0;
+  const int vprev = iabs_(cprev);
+  if (n > first && vprev == 0 && n > last) return 0;
+  const int ctx = n == first ? ctx0 : (vprev >= 2 ? 2 : vprev);
+  const int base = 11 * (ctx + 3 * (band_of(n) + 8 * type));
+  int count = 0;
+  auto dyn = [&](int bit, int pid, int sid) -> int {
+    if (EMIT) {
+      out[count] = (uint16_t)((bit << 15) | pid);
+      atomicAdd(&L.delta[sid], 0x10000u + bit);
+    }
+    ++count;
+    return bit;
+  };
+  auto fix = [&](int bit, int proba) {
+    if (EMIT) out[count] = (uint16_t)((bit << 15) | (1 << 14) | proba);
+    ++count;
+  };
+  if (n == first || vprev != 0) {
+    if (!dyn(n <= last, base + 0, base + 0)) return count;
+  }
+  const int neg = c < 0;
+  const uint32_t v = neg ? -c : c;
+  if (!dyn(v != 0, base + 1, base + 1)) return count;
+  if (!dyn(v > 1, base + 2, base + 2)) {
+  } else {
+    if (!dyn(v > 4, base + 3, base + 3)) {
+      if (dyn(v != 2, base + 4, base + 4)) dyn(v == 4, base + 5, base + 5);
+    } else if (!dyn(v > 10, base + 6, base + 6)) {
+      if (!dyn(v > 6, base + 7, base + 7)) {
+        fix(v == 6, 159);
+      } else {
+        fix(v >= 9, 165);
+        fix(!(v & 1), 145);
+      }
+    } else {
+      const uint8_t* tab;
+      int mask;
+      uint32_t res = v - 3;
+      if (res < (8 << 1)) {
+        dyn(0, base + 8, base + 8); dyn(0, base + 9, base + 9);
+        res -= 8 << 0; mask = 1 << 2; tab = kVP8Cat3;
+      } else if (res < (8 << 2)) {
+        dyn(0, base + 8, base + 8); dyn(1, base + 9, base + 9);
+        res -= 8 << 1; mask = 1 << 3; tab = kVP8Cat4;
+      } else if (res < (8 << 3)) {
+        dyn(1, base + 8, base + 8); dyn(0, base + 10, base + 9);  // token_enc.c:168
+        res -= 8 << 2; mask = 1 << 4; tab = kVP8Cat5;
+      } else {
+        dyn(1, base + 8, base + 8); dyn(1, base + 10, base + 9);
+        res -= 8 << 3; mask = 1 << 10; tab = kVP8Cat6;
+      }
+      for (; mask; mask >>= 1) fix((res & mask) != 0, *tab++);
+    }
+  }
+  fix(neg, 128);
+  return count;
+}
 
 // FinalizeTokenProbas (frame_enc.c:146-180) over the workgroup; returns the
 // reference's "dirty" flag (some probability differs from the default).
@@ -622,6 +833,18 @@ __device__ int finalize_probas_wg(K3S& L, int tid) {
   if (changed) L.flag = 1;
   __syncthreads();
   return L.flag;
+}
+
+// bit costs of the first probability of every (type, band, ctx): read by
+// rate_lane for the block-header and end-of-block bits; refreshed at every
+// FinalizeTokenProbas since the probabilities change even when the level
+// cost tables are not recomputed
+__device__ __forceinline__ void refresh_hc(K3S& L, int tid) {
+  for (int k = tid; k < 96; k += K3T) {
+    const int p = L.coeffs[k * 11];
+    L.hc[k][0] = bit_cost(L.ecost, 0, p);
+    L.hc[k][1] = bit_cost(L.ecost, 1, p);
+  }
 }
 
 #define K3_STAMP(i)                                   \
@@ -690,6 +913,7 @@ __global__ __launch_bounds__(K3T) void k_encode(K3Args a) {
   if (tid < 4) L.max_edge[tid] = 0;
   __syncthreads();
   level_costs(L, tid, K3T);
+  refresh_hc(L, tid);
   __syncthreads();
 
   const int rd_opt = P->rd_opt;
@@ -703,6 +927,11 @@ __global__ __launch_bounds__(K3T) void k_encode(K3Args a) {
   int tok_err = 0;
   int left_dc = 0;
   uint64_t stamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#ifdef K3_SUBPROF
+  uint64_t substamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#else
+  uint64_t* substamps = nullptr;
+#endif
   uint64_t stamp_last = __builtin_amdgcn_s_memtime();
   uint8_t* yl = L.yl_mem + 1;
   uint8_t* ul = L.ul_mem + 1;
@@ -723,6 +952,7 @@ __global__ __launch_bounds__(K3T) void k_encode(K3Args a) {
     load_mb(Yp, Up, Vp, w, h, x, y, L.yin, tid, K3T);
     if (--cnt < 0) {   // frame_enc.c:828-832
       if (finalize_probas_wg(L, tid)) level_costs(L, tid, K3T);
+      refresh_hc(L, tid);
       cnt = max_count;
     }
     __syncthreads();
@@ -747,6 +977,12 @@ __global__ __launch_bounds__(K3T) void k_encode(K3Args a) {
         const int m = k >> 7, p = k & 127, px = p & 15, py = p >> 4, c = px >> 3;
         L.puv[m][p] = pred_sample(m, 8, px & 7, py, c ? vl : ul, uvt + 8 * c, hl, ht, c ? dcv : dcu);
       }
+      // texture (Hadamard) measure of the 16 source blocks, shared by the
+      // intra16 and intra4 distortions (VP8TDisto4x4 / 16x16)
+      const int b = tid >> 4, j = tid & 15;
+      const int src = L.yin[(4 * (b >> 2) + (j >> 2)) * BPS + 4 * (b & 3) + (j & 3)];
+      const int hs = sum16(ttrans_lane(src, make_tlane(j), L.wy[j]));
+      if (j == 0) L.hsrc[b] = hs;
     }
     __syncthreads();
 
@@ -802,9 +1038,9 @@ __global__ __launch_bounds__(K3T) void k_encode(K3Args a) {
     // ---- Intra4 (quant_enc.c:1072-1165)
     if (max_i4_bits > 0) {
       I4Result r4 = trellis_all ? run_i4<true>(L, S, ctx, tid, x, mbw, predtop, yl, yt, true,
-                                               rd_score, max_i4_bits)
+                                               rd_score, max_i4_bits, substamps)
                                 : run_i4<false>(L, S, ctx, tid, x, mbw, predtop, yl, yt, true,
-                                                rd_score, max_i4_bits);
+                                                rd_score, max_i4_bits, substamps);
       if (r4.ok) {
         is_i16 = 0;
         rdH = r4.H;
@@ -862,7 +1098,7 @@ __global__ __launch_bounds__(K3T) void k_encode(K3Args a) {
         if (tid < 16) L.fin_dc[tid] = L.lvdc[best16][tid];
         nzq = (uint32_t)L.mres[best16][3];
       } else {
-        I4Result r4 = run_i4<true>(L, S, ctx, tid, x, mbw, predtop, yl, yt, false, 0, 0);
+        I4Result r4 = run_i4<true>(L, S, ctx, tid, x, mbw, predtop, yl, yt, false, 0, 0, substamps);
         L.yout[(tid >> 4) * BPS + (tid & 15)] = L.acc_out[tid];
         (&L.fin_ac[0][0])[tid] = (&L.acc_ac[0][0])[tid];
         nzq = r4.nz;
@@ -908,20 +1144,33 @@ __global__ __launch_bounds__(K3T) void k_encode(K3Args a) {
     K3_STAMP(4);
 
     // ---- tokens + exact statistics (frame_enc.c:411-453, token_enc.c:113-193)
+    // One (block, zigzag position) item per thread: its tokens depend only
+    // on its level, the previous level and the block's last non-zero
+    // position, so counts, a workgroup scan and the writes are all parallel.
     const int first_blk = is_i16 ? 0 : 1;
     uint64_t nzb = 0;
-    int total = 0;
-    if (w0) {
-      int my_ctx = 0, my_type = 0, my_first = 0;
-      const int k = lane;                    // block index 0..24
-      const bool active = k >= first_blk && k < 25;
-      int nzk = 0;
-      if (active) {
-        const int16_t* lvp = blk_levels(L, k);
-        for (int i = 0; i < 16; ++i) nzk |= lvp[i];
+    int lvi[2], lvp[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {   // items tid and tid + 256 = block*16 + pos
+      const int item = tid + K3T * q, k = item >> 4, n = item & 15;
+      int v = 0, vp = 0;
+      if (k < 25 && k >= first_blk) {
+        const int16_t* lvb = blk_levels(L, k);
+        v = lvb[n];
+        vp = n > 0 ? lvb[n - 1] : 0;
       }
-      nzb = __ballot(active && nzk != 0);
+      lvi[q] = v;
+      lvp[q] = vp;
+      const int last = max16(v != 0 ? n : -1);
+      if (n == 0 && k < 32) L.blast[k] = last;
+    }
+    __syncthreads();
+    if (w0) {
+      const int k = lane;
+      const bool active = k >= first_blk && k < 25;
+      nzb = __ballot(active && L.blast[k] >= 0);
       if (active) {
+        int my_type, my_first, my_ctx;
         if (k == 0) {
           my_type = 1; my_first = 0; my_ctx = ctx.top(8) + ctx.left(8);
         } else if (k <= 16) {
@@ -938,24 +1187,52 @@ __global__ __launch_bounds__(K3T) void k_encode(K3Args a) {
           my_ctx = t + l;
         }
         L.blkinfo[k] = my_type | (my_first << 4) | (my_ctx << 8);
+      } else if (k < 32) {
+        L.blkinfo[k] = -1;
       }
-      int nzdummy;
-      const int mycount = active ? gen_tokens<0>(L, blk_levels(L, k), my_type, my_first, my_ctx,
-                                                 nullptr, &nzdummy)
-                                 : 0;
-      int incl = mycount;
+    }
+    __syncthreads();
+    {
+      int cnt[2], bi[2], last[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int item = tid + K3T * q, k = item >> 4, n = item & 15;
+        bi[q] = k < 25 ? L.blkinfo[k] : -1;
+        last[q] = k < 25 ? L.blast[k] : -1;
+        cnt[q] = bi[q] < 0 ? 0
+                           : pos_tokens<false>(L, bi[q] & 15, (bi[q] >> 4) & 15, bi[q] >> 8, n,
+                                               lvi[q], lvp[q], last[q], nullptr);
+      }
+      // workgroup exclusive scan over items 0..511 (item order = token order)
+      int inc0 = cnt[0], inc1 = cnt[1];
 #pragma unroll
       for (int off = 1; off < 64; off <<= 1) {
-        const int v = __shfl_up(incl, off);
-        if (lane >= off) incl += v;
+        const int v0 = __shfl_up(inc0, off), v1 = __shfl_up(inc1, off);
+        if (lane >= off) { inc0 += v0; inc1 += v1; }
       }
-      total = __shfl(incl, 63);
-      const int excl = incl - mycount;
+      const int wv = tid >> 6;
+      if (lane == 63) { L.wsum[0][wv] = inc0; L.wsum[1][wv] = inc1; }
+      __syncthreads();
+      int pre0 = 0, pre1 = 0, tot0 = 0, tot1 = 0;
+#pragma unroll
+      for (int w2 = 0; w2 < 4; ++w2) {
+        const int s0 = L.wsum[0][w2], s1 = L.wsum[1][w2];
+        if (w2 < wv) { pre0 += s0; pre1 += s1; }
+        tot0 += s0; tot1 += s1;
+      }
+      const int total = tot0 + tot1;
       if (ntok + (uint32_t)total > a.tok_cap) tok_err = 1;
-      if (!tok_err && active)
-        gen_tokens<1>(L, blk_levels(L, k), my_type, my_first, my_ctx, tok_base + ntok + excl,
-                      &nzdummy);
-      if (!tok_err) ntok += total;
+      if (!tok_err) {
+        const int off0 = pre0 + inc0 - cnt[0];
+        const int off1 = tot0 + pre1 + inc1 - cnt[1];
+        if (cnt[0])
+          pos_tokens<true>(L, bi[0] & 15, (bi[0] >> 4) & 15, bi[0] >> 8, tid & 15, lvi[0], lvp[0],
+                           last[0], tok_base + ntok + off0);
+        if (cnt[1])
+          pos_tokens<true>(L, bi[1] & 15, (bi[1] >> 4) & 15, bi[1] >> 8, tid & 15, lvi[1], lvp[1],
+                           last[1], tok_base + ntok + off1);
+        ntok += total;
+      }
     }
     if (tid == 0) L.flag_mark = 0;
     __syncthreads();
@@ -1055,7 +1332,11 @@ __global__ __launch_bounds__(K3T) void k_encode(K3Args a) {
     R->size_p0 = size_p0;
     R->sse[0] = sse_acc[0]; R->sse[1] = sse_acc[1]; R->sse[2] = sse_acc[2];
     R->block_count[0] = nb_i4; R->block_count[1] = nb_i16; R->block_count[2] = nb_skip;
+#ifdef K3_SUBPROF
+    for (int i = 0; i < 8; ++i) R->stamps[i] = substamps[i];
+#else
     for (int i = 0; i < 8; ++i) R->stamps[i] = stamps[i];
+#endif
   }
 }
 

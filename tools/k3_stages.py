@@ -9,6 +9,9 @@ W, H = int(sys.argv[1]), int(sys.argv[2])
 B = int(sys.argv[3]) if len(sys.argv) > 3 else 8
 method = int(sys.argv[4]) if len(sys.argv) > 4 else 4
 names = ["load+refresh+preds", "i16", "i4", "uv(+m5)", "info+sse", "tokens", "fold", "ctx+bnd"]
+if os.environ.get("WEBP_AMD_LIB", "").endswith("_prof.so"):
+    names = ["i4:pred", "i4:fdct", "i4:quant", "i4:idct", "i4:distortion", "i4:rate+score",
+             "i4:select", "i4:commit"]
 buf = torch.empty(B * W * H * 4, dtype=torch.uint8, device="cuda")
 libwebp_amd.synth_device(buf.data_ptr(), W, H, 0, B)
 torch.cuda.synchronize()

@@ -141,12 +141,11 @@ def main():
         step()
     barrier()
     t0 = time.perf_counter()
-    k3_us, k12_us, tails = 0.0, 0.0, []
+    k3_us, tails = 0.0, []
     for _ in range(args.steps):
         step()
         t = enc.timings()
         k3_us += t[6]
-        k12_us += t[7]
         tails.append(t)
     barrier()
     elapsed = time.perf_counter() - t0
@@ -208,7 +207,8 @@ def main():
         "stage_ms": {k: round(sum(t[i] for t in tails) / len(tails) / 1e3, 3) for k, i in
                      (("import_analysis", 0), ("host_setup", 1), ("rd_tokens", 2),
                       ("d2h", 3), ("host_tail", 4), ("total", 5),
-                      ("k_encode_events", 6), ("k_import_analyze_events", 7))},
+                      ("k_encode_events", 6), ("k_import_analyze_events", 7),
+                      ("k_emit_events", 8))},
         "output_bytes_per_frame": round(total_bytes / (world * B), 1),
     }
     if host_rate is not None:

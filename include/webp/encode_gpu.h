@@ -55,13 +55,13 @@ WEBP_EXTERN const uint8_t* WebPGpuBatchOutput(const WebPGpuBatch* batch,
                                               int frame);
 WEBP_EXTERN int WebPGpuBatchError(const WebPGpuBatch* batch, int frame);
 
-/* Per-stage wall times of the last call in microseconds:
- * [0] import+analysis kernels, [1] host segment setup, [2] RD/token kernel,
- * [3] device->host copies, [4] host tail (emit + assembly), [5] total,
- * [6] k_encode device time and [7] k_import + k_analyze device time, both
- * from HIP events recorded on the batch's stream around the launches. */
+/* Per-stage times of the last call in microseconds:
+ * [0] import+analysis kernels (wall), [1] host segment setup, [2] RD/token
+ * and boolean-coder kernels + result copies (wall), [3] partition copies,
+ * [4] host tail (partition 0 + assembly), [5] total; from HIP events on the
+ * batch's stream: [6] k_encode, [7] k_import + k_analyze, [8] k_emit. */
 WEBP_EXTERN void WebPGpuBatchTimings(const WebPGpuBatch* batch,
-                                     double timings_us[8]);
+                                     double timings_us[10]);
 
 /* Number of 16-bit VP8 tokens the RD/token kernel produced for frame f of
  * the last call (token_enc.c:31-35 format); used to price the kernel's HBM

@@ -157,7 +157,7 @@ class GpuBatch:
         return [self.output(f) for f in range(self.n)]
 
     def timings(self):
-        t = (C.c_double * 8)()
+        t = (C.c_double * 10)()
         self._lib.WebPGpuBatchTimings(self._h, t)
         return list(t)
 

@@ -1,0 +1,284 @@
+// K4: the VP8 boolean coder for the token partition on the GPU, parallel
+// INSIDE each frame (VP8EmitTokens, src/enc/token_enc.c:200-223; VP8PutBit /
+// Flush / VP8BitWriterFinish, src/utils/bit_writer_utils.c:55-124,199-206).
+//
+// The coder's only serial state that matters is the 8-bit range (the "low"
+// register is linear): the output bytes are exactly the big-endian bytes of
+// N >> 1 on L = (S + 7) / 8 bytes, where N = sum_i c_i * 2^(E_i), c_i is the
+// amount token i adds to the low register (split + 1 for a 1 bit, else 0),
+// E_i the number of renormalisation shifts from token i (inclusive) to the
+// end of the stream including the finishing pad bits, and S the total shift
+// count. (Checked against the reference coder; tests/test_emit_model.py.)
+// So a frame's tokens are cut into segments and:
+//   E0 k_emit_resolve  token -> (bit, probability) in place, all tokens
+//   E1 k_emit_maps     per segment, the end range and shift count for each of
+//                      the 128 possible start ranges (one lane per range)
+//   E2 k_emit_compose  per frame, chain the segment maps: every segment's true
+//                      start range and bit offset, pad bits, S and L
+//   E3 k_emit_seg      per segment (one lane each): forward pass with the true
+//                      start range -> (c_i, shift_i); reverse pass accumulating
+//                      the segment's part of N least-significant word first;
+//                      its low S_s bits tile N exactly (plain stores inside,
+//                      atomicOr on the two shared boundary words), the <= 8
+//                      bits above go to H_s
+//   E4 k_emit_carry    adds every H_s at its segment's top with atomicAdd and
+//                      ripple carry (additions commute, so order is free)
+//   E5 k_emit_bytes    output byte k = bits [1 + 8(L-1-k), +8) of N, written
+//                      over the frame's (consumed) token buffer
+#include "vp8_dev.h"
+
+#define EMIT_SEG VP8G_EMIT_SEG   // tokens per segment
+
+namespace {
+
+__device__ __forceinline__ int renorm(int& r) {   // range_ in [0, 254] -> [127, 254]
+  const int sh = __clz(r + 1) - 24;
+  r = ((r + 1) << sh) - 1;
+  return sh;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_emit_resolve(uint16_t* __restrict__ tokens,
+                                                      size_t tok_cap,
+                                                      const vp8g_frame_result* __restrict__ results,
+                                                      const vp8g_emit_meta* __restrict__ meta) {
+  __shared__ uint8_t prob[VP8G_NUM_SLOTS];
+  const int f = blockIdx.y;
+  const vp8g_frame_result* R = results + f;
+  for (int s = threadIdx.x; s < VP8G_NUM_SLOTS; s += 256) prob[s] = R->probas[s];
+  __syncthreads();
+  const uint32_t ntok = meta[f].ntok;
+  const uint32_t i0 = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i0 >= ntok) return;
+  uint16_t* tok = tokens + (size_t)f * tok_cap + i0;
+  uint4 w = *reinterpret_cast<const uint4*>(tok);
+  uint32_t v[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t t = (v[k] >> (16 * h)) & 0xffff;
+      const uint32_t p = (t & 0x4000) ? (t & 0xff) : prob[t & 0x3fff & 2047];
+      r |= (((t >> 15) << 8) | p) << (16 * h);
+    }
+    v[k] = r;
+  }
+  *reinterpret_cast<uint4*>(tok) = make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+__global__ __launch_bounds__(128) void k_emit_maps(const uint16_t* __restrict__ tokens,
+                                                   size_t tok_cap,
+                                                   const vp8g_emit_meta* __restrict__ meta,
+                                                   uint8_t* __restrict__ emap,
+                                                   uint16_t* __restrict__ eshift) {
+  __shared__ __align__(16) uint16_t stage[EMIT_SEG];
+  const int f = blockIdx.y, s = blockIdx.x, t = threadIdx.x;
+  const vp8g_emit_meta M = meta[f];
+  if ((uint32_t)s >= M.nseg) return;
+  const uint32_t i0 = (uint32_t)s * EMIT_SEG;
+  const uint32_t cnt = min((uint32_t)EMIT_SEG, M.ntok - i0);
+  const uint16_t* tok = tokens + (size_t)f * tok_cap + i0;
+  for (uint32_t k = t * 8; k < cnt; k += 128 * 8)   // 16-byte loads (tail padded by the buffer)
+    *reinterpret_cast<uint4*>(stage + k) = *reinterpret_cast<const uint4*>(tok + k);
+  __syncthreads();
+  int r = 127 + t;
+  uint32_t S = 0;
+  uint32_t i = 0;
+  for (; i + 8 <= cnt; i += 8) {
+    const uint4 q = *reinterpret_cast<const uint4*>(stage + i);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t pb = (w[k >> 1] >> (16 * (k & 1))) & 0xffff;
+      const int split = (r * (int)(pb & 0xff)) >> 8;
+      r = (pb >> 8) ? r - split - 1 : split;
+      S += renorm(r);
+    }
+  }
+  for (; i < cnt; ++i) {
+    const uint32_t pb = stage[i];
+    const int split = (r * (int)(pb & 0xff)) >> 8;
+    r = (pb >> 8) ? r - split - 1 : split;
+    S += renorm(r);
+  }
+  const size_t o = ((size_t)M.seg_base + s) * 128 + t;
+  emap[o] = (uint8_t)r;
+  eshift[o] = (uint16_t)S;
+}
+
+__global__ __launch_bounds__(64) void k_emit_compose(vp8g_emit_meta* __restrict__ meta,
+                                                     const uint8_t* __restrict__ emap,
+                                                     const uint16_t* __restrict__ eshift,
+                                                     vp8g_emit_seg* __restrict__ segs,
+                                                     uint32_t* __restrict__ out_size) {
+  const int f = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  vp8g_emit_meta M = meta[f];
+  int r = 254;
+  uint32_t cum = 0;
+  for (uint32_t s = 0; s < M.nseg; ++s) {
+    const size_t o = ((size_t)M.seg_base + s) * 128 + (r - 127);
+    const uint32_t Ss = eshift[o];
+    segs[M.seg_base + s].rs = (uint8_t)r;
+    segs[M.seg_base + s].S = Ss;
+    segs[M.seg_base + s].T = cum;   // provisional: shifts BEFORE the segment
+    cum += Ss;
+    r = emap[o];
+  }
+  // VP8BitWriterFinish pads 9 - nb_bits zero bits at probability 1/2, where
+  // nb_bits is what the flushes left after cum shifts from -8
+  const int t = (int)cum - 8;
+  const int nb = t <= 0 ? t : t - 8 * ((t + 7) / 8);
+  uint32_t spad = 0;
+  for (int k = 0; k < 9 - nb; ++k) {
+    r = (r * 128) >> 8;
+    spad += renorm(r);
+  }
+  M.S = cum + spad;
+  M.L = (M.S + 7) / 8;
+  meta[f] = M;
+  out_size[f] = M.L;
+  for (uint32_t s = 0; s < M.nseg; ++s) {   // T_s = bit offset of the segment's bottom in N
+    vp8g_emit_seg& g = segs[M.seg_base + s];
+    g.T = M.S - (g.T + g.S);
+  }
+}
+
+__global__ __launch_bounds__(64) void k_emit_seg(uint16_t* __restrict__ tokens, size_t tok_cap,
+                                                 const vp8g_emit_meta* __restrict__ meta,
+                                                 vp8g_emit_seg* __restrict__ segs,
+                                                 uint32_t* __restrict__ nbuf) {
+  const int f = blockIdx.y;
+  const uint32_t s = blockIdx.x * 64 + threadIdx.x;
+  const vp8g_emit_meta M = meta[f];
+  if (s >= M.nseg) return;
+  vp8g_emit_seg& g = segs[M.seg_base + s];
+  const uint32_t i0 = s * EMIT_SEG;
+  const uint32_t cnt = min((uint32_t)EMIT_SEG, M.ntok - i0);
+  uint16_t* tok = tokens + (size_t)f * tok_cap + i0;
+  // forward: true range chain -> (c, shift) packed in place
+  int r = g.rs;
+  for (uint32_t i = 0; i < cnt; ++i) {
+    const uint32_t pb = tok[i];
+    const int split = (r * (int)(pb & 0xff)) >> 8;
+    const int bit = pb >> 8;
+    const int c = bit ? split + 1 : 0;
+    r = bit ? r - split - 1 : split;
+    const int sh = renorm(r);
+    tok[i] = (uint16_t)(c | (sh << 8));
+  }
+  // reverse: least-significant first; bits below the current position are final
+  uint32_t* W = nbuf + M.nb_base;
+  const uint32_t T = g.T, top = T + g.S;
+  uint32_t wb = T & ~31u;      // global bit index of acc's bit 0
+  uint64_t acc = 0;
+  uint32_t E = 0;
+  for (uint32_t i = cnt; i-- > 0;) {
+    const uint32_t pk = tok[i];
+    E += pk >> 8;
+    const uint32_t G = T + E;
+    while (G >= wb + 32) {   // word [wb, wb+32) is final
+      const uint32_t lo = (uint32_t)acc;
+      const uint32_t mlo = wb < T ? (~0u << (T - wb)) : ~0u;
+      if (mlo != ~0u) atomicOr(W + (wb >> 5), lo & mlo);
+      else W[wb >> 5] = lo;
+      acc >>= 32;
+      wb += 32;
+    }
+    acc += (uint64_t)(pk & 0xff) << (G - wb);
+  }
+  // remaining words up to the region top; bits above it are H_s
+  while (wb < top) {
+    const uint32_t lo = (uint32_t)acc;
+    uint32_t m = ~0u;
+    if (wb < T) m &= ~0u << (T - wb);
+    if (top < wb + 32) m &= (1u << (top - wb)) - 1u;
+    if (m != ~0u) atomicOr(W + (wb >> 5), lo & m);
+    else W[wb >> 5] = lo;
+    if (top < wb + 32) break;
+    acc >>= 32;
+    wb += 32;
+  }
+  g.H = (uint8_t)((acc >> (top - wb)) & 0xff);
+}
+
+// big-number add of h at bit b (h < 256) with ripple carry, via atomics
+__device__ __forceinline__ void big_add(uint32_t* W, uint32_t b, uint32_t h) {
+  const uint64_t v = (uint64_t)h << (b & 31);
+  uint32_t w = b >> 5;
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  uint32_t old = atomicAdd(W + w, lo);
+  uint32_t carry = (old + lo) < old;
+  ++w;
+  uint32_t add = hi + carry;   // hi < 256, no overflow
+  while (add) {
+    old = atomicAdd(W + w, add);
+    add = (old + add) < old;
+    ++w;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_emit_carry(const vp8g_emit_meta* __restrict__ meta,
+                                                   const vp8g_emit_seg* __restrict__ segs,
+                                                   uint32_t* __restrict__ nbuf) {
+  const int f = blockIdx.y;
+  const uint32_t s = blockIdx.x * 64 + threadIdx.x;
+  const vp8g_emit_meta M = meta[f];
+  if (s >= M.nseg) return;
+  const vp8g_emit_seg g = segs[M.seg_base + s];
+  if (g.H) big_add(nbuf + M.nb_base, g.T + g.S, g.H);
+}
+
+__global__ __launch_bounds__(256) void k_emit_bytes(uint16_t* __restrict__ tokens, size_t tok_cap,
+                                                    const vp8g_emit_meta* __restrict__ meta,
+                                                    const uint32_t* __restrict__ nbuf) {
+  const int f = blockIdx.y;
+  const vp8g_emit_meta M = meta[f];
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= M.L) return;
+  const uint32_t* W = nbuf + M.nb_base;
+  const uint32_t b = 1 + 8 * (M.L - 1 - k);   // lowest bit of output byte k
+  const uint64_t two = (uint64_t)W[b >> 5] | ((uint64_t)W[(b >> 5) + 1] << 32);
+  reinterpret_cast<uint8_t*>(tokens + (size_t)f * tok_cap)[k] = (uint8_t)(two >> (b & 31));
+}
+
+extern "C" int vp8g_launch_check(const char* what);
+
+extern "C" int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
+                                const vp8g_frame_result* results, vp8g_emit_meta* meta,
+                                uint32_t max_ntok, uint32_t max_seg, uint8_t* emap,
+                                uint16_t* eshift, vp8g_emit_seg* segs, uint32_t* nbuf,
+                                uint32_t* out_size, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (n <= 0) return 1;
+  const uint32_t rb = (max_ntok + 2047) / 2048;
+  if (rb) {
+    hipLaunchKernelGGL(k_emit_resolve, dim3(rb, n), dim3(256), 0, st, tokens, tok_cap, results,
+                       (const vp8g_emit_meta*)meta);
+    if (!vp8g_launch_check("k_emit_resolve")) return 0;
+  }
+  if (max_seg) {
+    hipLaunchKernelGGL(k_emit_maps, dim3(max_seg, n), dim3(128), 0, st, (const uint16_t*)tokens,
+                       tok_cap, (const vp8g_emit_meta*)meta, emap, eshift);
+    if (!vp8g_launch_check("k_emit_maps")) return 0;
+  }
+  hipLaunchKernelGGL(k_emit_compose, dim3(n), dim3(64), 0, st, meta, (const uint8_t*)emap,
+                     (const uint16_t*)eshift, segs, out_size);
+  if (!vp8g_launch_check("k_emit_compose")) return 0;
+  const uint32_t sb = (max_seg + 63) / 64;
+  if (sb) {
+    hipLaunchKernelGGL(k_emit_seg, dim3(sb, n), dim3(64), 0, st, tokens, tok_cap,
+                       (const vp8g_emit_meta*)meta, segs, nbuf);
+    if (!vp8g_launch_check("k_emit_seg")) return 0;
+    hipLaunchKernelGGL(k_emit_carry, dim3(sb, n), dim3(64), 0, st, (const vp8g_emit_meta*)meta,
+                       (const vp8g_emit_seg*)segs, nbuf);
+    if (!vp8g_launch_check("k_emit_carry")) return 0;
+  }
+  // output bytes: at most (7 * ntok + 40) / 8 + 1 per frame
+  const uint32_t maxL = (7u * max_ntok + 48) / 8 + 2;
+  hipLaunchKernelGGL(k_emit_bytes, dim3((maxL + 255) / 256, n), dim3(256), 0, st, tokens, tok_cap,
+                     (const vp8g_emit_meta*)meta, (const uint32_t*)nbuf);
+  return vp8g_launch_check("k_emit_bytes");
+}

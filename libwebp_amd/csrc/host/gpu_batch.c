@@ -95,10 +95,14 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   b->yfb = (b->yfb + 255) & ~(size_t)255;
   b->tok_cap = (size_t)b->nmb * VP8G_MAX_TOKENS_PER_MB;
   b->threads = host_threads > 0 ? host_threads : default_threads();
+  {   /* WEBP_AMD_HOST_EMIT=1: boolean-code partition 1 on the host threads */
+    const char* he = getenv("WEBP_AMD_HOST_EMIT");
+    b->host_emit = he && he[0] == '1';
+  }
   const size_t N = (size_t)max_frames, nmb = (size_t)b->nmb;
   CHK(hipSetDevice(device));
   CHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
-  for (int i = 0; i < 4; ++i) CHK(hipEventCreate(&b->ev[i]));
+  for (int i = 0; i < 6; ++i) CHK(hipEventCreate(&b->ev[i]));
   CHK(hipMalloc((void**)&b->d_g2l, 256 * sizeof(uint16_t) + 33 * sizeof(int32_t)));
   b->d_l2g = (int32_t*)(b->d_g2l + 256);
   CHK(hipMemcpy(b->d_g2l, g_g2l, 256 * sizeof(uint16_t), hipMemcpyHostToDevice));
@@ -112,6 +116,8 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   CHK(hipMalloc((void**)&b->d_tokens, N * b->tok_cap * sizeof(uint16_t)));
   CHK(hipMalloc((void**)&b->d_mbinfo, N * nmb * VP8G_MBINFO_BYTES));
   CHK(hipMalloc((void**)&b->d_results, N * sizeof(vp8g_frame_result)));
+  CHK(hipMalloc((void**)&b->d_psize, N * sizeof(uint32_t)));
+  CHK(hipMalloc((void**)&b->d_emeta, N * sizeof(vp8g_emit_meta)));
   CHK(hipHostMalloc((void**)&b->h_aflags, N * sizeof(uint32_t), 0));
   CHK(hipHostMalloc((void**)&b->h_alpha, N * nmb, 0));
   CHK(hipHostMalloc((void**)&b->h_uva, N * nmb * sizeof(uint16_t), 0));
@@ -119,13 +125,16 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   CHK(hipHostMalloc((void**)&b->h_params, N * sizeof(vp8g_frame_params), 0));
   CHK(hipHostMalloc((void**)&b->h_mbinfo, N * nmb * VP8G_MBINFO_BYTES, 0));
   CHK(hipHostMalloc((void**)&b->h_results, N * sizeof(vp8g_frame_result), 0));
+  CHK(hipHostMalloc((void**)&b->h_psize, N * sizeof(uint32_t), 0));
+  CHK(hipHostMalloc((void**)&b->h_emeta, N * sizeof(vp8g_emit_meta), 0));
   b->frames = (vp8h_frame*)calloc(N, sizeof(vp8h_frame));
   b->tok_off = (size_t*)calloc(N + 1, sizeof(size_t));
+  b->part_off = (size_t*)calloc(N + 1, sizeof(size_t));
   b->out = (uint8_t**)calloc(N, sizeof(uint8_t*));
   b->out_size = (size_t*)calloc(N, sizeof(size_t));
   b->err = (int*)calloc(N, sizeof(int));
   b->hdr = (int*)calloc(2 * N, sizeof(int));
-  if (!b->frames || !b->tok_off || !b->out || !b->out_size || !b->err || !b->hdr) goto fail;
+  if (!b->frames || !b->tok_off || !b->part_off || !b->out || !b->out_size || !b->err || !b->hdr) goto fail;
   return b;
 fail:
   WebPGpuBatchDelete(b);
@@ -138,17 +147,19 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   if (b->stream) hipStreamSynchronize(b->stream);
   hipFree(b->d_g2l); hipFree(b->d_rgba); hipFree(b->d_yuv); hipFree(b->d_aflags); hipFree(b->d_alpha);
   hipFree(b->d_uva); hipFree(b->d_segmap); hipFree(b->d_params); hipFree(b->d_tokens);
-  hipFree(b->d_mbinfo); hipFree(b->d_results);
+  hipFree(b->d_mbinfo); hipFree(b->d_results); hipFree(b->d_psize); hipFree(b->d_emeta);
+  hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs); hipFree(b->d_nbuf);
   hipHostFree(b->h_aflags); hipHostFree(b->h_alpha); hipHostFree(b->h_uva);
   hipHostFree(b->h_segmap); hipHostFree(b->h_params); hipHostFree(b->h_mbinfo);
-  hipHostFree(b->h_results); hipHostFree(b->h_tokens);
-  for (int i = 0; i < 4; ++i)
+  hipHostFree(b->h_results); hipHostFree(b->h_tokens); hipHostFree(b->h_psize);
+  hipHostFree(b->h_part); hipHostFree(b->h_emeta);
+  for (int i = 0; i < 6; ++i)
     if (b->ev[i]) hipEventDestroy(b->ev[i]);
   if (b->stream) hipStreamDestroy(b->stream);
   if (b->out)
     for (int i = 0; i < b->max_frames; ++i) free(b->out[i]);
   free(b->out); free(b->out_size); free(b->err); free(b->hdr);
-  free(b->frames); free(b->tok_off);
+  free(b->frames); free(b->tok_off); free(b->part_off);
   free(b);
 }
 
@@ -176,14 +187,20 @@ static void frame_tail(WebPGpuBatch* b, int f) {
     return;
   }
   vp8h_bw part1;
-  vp8h_bw_init(&part1, (size_t)res->ntokens / 8 + 4096);
-  vp8h_emit_tokens(&part1, b->h_tokens + b->tok_off[f], res->ntokens, res->probas);
-  vp8h_bw_finish(&part1);
+  if (b->host_emit) {   /* boolean-code the tokens here (token_enc.c:200-223) */
+    vp8h_bw_init(&part1, (size_t)res->ntokens / 8 + 4096);
+    vp8h_emit_tokens(&part1, b->h_tokens + b->tok_off[f], res->ntokens, res->probas);
+    vp8h_bw_finish(&part1);
+  } else {              /* partition 1 already coded by K4 */
+    memset(&part1, 0, sizeof(part1));
+    part1.buf = b->h_part + b->part_off[f];
+    part1.pos = b->h_psize[f];
+  }
   int err = VP8_ENC_OK;
   b->out_size[f] = vp8h_assemble(fr, res, b->h_mbinfo + (size_t)f * b->nmb * VP8G_MBINFO_BYTES,
                                  &part1, &b->out[f], &err, b->hdr + 2 * f);
   b->err[f] = err;
-  vp8h_bw_free(&part1);
+  if (b->host_emit) vp8h_bw_free(&part1);
 }
 
 static void* tail_worker(void* arg) {
@@ -245,31 +262,93 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   CHK(hipMemcpyAsync(b->h_mbinfo, b->d_mbinfo, n * nmb * VP8G_MBINFO_BYTES,
                      hipMemcpyDeviceToHost, st));
   CHK(hipStreamSynchronize(st));
-  t3 = now_us();
-  b->tok_off[0] = 0;
-  for (int f = 0; f < n; ++f) b->tok_off[f + 1] = b->tok_off[f] + b->h_results[f].ntokens;
-  const size_t total = b->tok_off[n];
-  if (total > b->h_tok_cap) {
-    hipHostFree(b->h_tokens);
-    b->h_tokens = NULL;
-    b->h_tok_cap = 0;
-    const size_t cap = total + total / 4 + 1024;
-    CHK(hipHostMalloc((void**)&b->h_tokens, cap * sizeof(uint16_t), 0));
-    b->h_tok_cap = cap;
+  if (!b->host_emit) {   /* K4 on the device, sized from the token counts */
+    uint32_t max_ntok = 0, max_seg = 0;
+    size_t segs = 0, words = 0;
+    for (int f = 0; f < n; ++f) {
+      vp8g_emit_meta* m = &b->h_emeta[f];
+      m->ntok = b->h_results[f].error ? 0 : b->h_results[f].ntokens;
+      m->nseg = (m->ntok + VP8G_EMIT_SEG - 1) / VP8G_EMIT_SEG;
+      m->seg_base = (uint32_t)segs;
+      m->nb_base = (uint32_t)words;
+      m->S = m->L = 0;
+      segs += m->nseg;
+      words += (7 * (size_t)m->ntok + 17 + 8 + 63) / 32 + 4;
+      if (m->ntok > max_ntok) max_ntok = m->ntok;
+      if (m->nseg > max_seg) max_seg = m->nseg;
+    }
+    if (segs > b->emit_seg_cap) {
+      hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs);
+      b->d_emap = NULL; b->d_eshift = NULL; b->d_esegs = NULL; b->emit_seg_cap = 0;
+      const size_t cap = segs + segs / 4 + 64;
+      CHK(hipMalloc((void**)&b->d_emap, cap * 128));
+      CHK(hipMalloc((void**)&b->d_eshift, cap * 128 * sizeof(uint16_t)));
+      CHK(hipMalloc((void**)&b->d_esegs, cap * sizeof(vp8g_emit_seg)));
+      b->emit_seg_cap = cap;
+    }
+    if (words > b->emit_word_cap) {
+      hipFree(b->d_nbuf);
+      b->d_nbuf = NULL; b->emit_word_cap = 0;
+      const size_t cap = words + words / 4 + 256;
+      CHK(hipMalloc((void**)&b->d_nbuf, cap * sizeof(uint32_t)));
+      b->emit_word_cap = cap;
+    }
+    CHK(hipEventRecord(b->ev[5], st));
+    CHK(hipMemsetAsync(b->d_nbuf, 0, words * sizeof(uint32_t), st));
+    CHK(hipMemcpyAsync(b->d_emeta, b->h_emeta, n * sizeof(vp8g_emit_meta),
+                       hipMemcpyHostToDevice, st));
+    if (!vp8g_launch_emit(b->d_tokens, b->tok_cap, n, b->d_results, b->d_emeta, max_ntok,
+                          max_seg, b->d_emap, b->d_eshift, b->d_esegs, b->d_nbuf, b->d_psize, st))
+      return 0;
+    CHK(hipEventRecord(b->ev[4], st));
+    CHK(hipMemcpyAsync(b->h_psize, b->d_psize, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    CHK(hipStreamSynchronize(st));
   }
-  for (int f = 0; f < n; ++f)
-    if (b->h_results[f].ntokens)
-      CHK(hipMemcpyAsync(b->h_tokens + b->tok_off[f], b->d_tokens + (size_t)f * b->tok_cap,
-                         b->h_results[f].ntokens * sizeof(uint16_t), hipMemcpyDeviceToHost, st));
+  t3 = now_us();
+  if (b->host_emit) {
+    b->tok_off[0] = 0;
+    for (int f = 0; f < n; ++f) b->tok_off[f + 1] = b->tok_off[f] + b->h_results[f].ntokens;
+    const size_t total = b->tok_off[n];
+    if (total > b->h_tok_cap) {
+      hipHostFree(b->h_tokens);
+      b->h_tokens = NULL;
+      b->h_tok_cap = 0;
+      const size_t cap = total + total / 4 + 1024;
+      CHK(hipHostMalloc((void**)&b->h_tokens, cap * sizeof(uint16_t), 0));
+      b->h_tok_cap = cap;
+    }
+    for (int f = 0; f < n; ++f)
+      if (b->h_results[f].ntokens)
+        CHK(hipMemcpyAsync(b->h_tokens + b->tok_off[f], b->d_tokens + (size_t)f * b->tok_cap,
+                           b->h_results[f].ntokens * sizeof(uint16_t), hipMemcpyDeviceToHost, st));
+  } else {
+    b->part_off[0] = 0;
+    for (int f = 0; f < n; ++f) b->part_off[f + 1] = b->part_off[f] + b->h_psize[f];
+    const size_t total = b->part_off[n];
+    if (total > b->h_part_cap) {
+      hipHostFree(b->h_part);
+      b->h_part = NULL;
+      b->h_part_cap = 0;
+      const size_t cap = total + total / 4 + 4096;
+      CHK(hipHostMalloc((void**)&b->h_part, cap, 0));
+      b->h_part_cap = cap;
+    }
+    for (int f = 0; f < n; ++f)
+      if (b->h_psize[f])
+        CHK(hipMemcpyAsync(b->h_part + b->part_off[f], b->d_tokens + (size_t)f * b->tok_cap,
+                           b->h_psize[f], hipMemcpyDeviceToHost, st));
+  }
   CHK(hipStreamSynchronize(st));
   t4 = now_us();
   run_tails(b, n);
   const double t5 = now_us();
-  float k3_ms = 0.f, k12_ms = 0.f;
+  float k3_ms = 0.f, k12_ms = 0.f, k4_ms = 0.f;
   CHK(hipEventElapsedTime(&k3_ms, b->ev[2], b->ev[3]));
   CHK(hipEventElapsedTime(&k12_ms, b->ev[0], b->ev[1]));
+  if (!b->host_emit) CHK(hipEventElapsedTime(&k4_ms, b->ev[5], b->ev[4]));
   b->timings[6] = 1e3 * k3_ms;
   b->timings[7] = 1e3 * k12_ms;
+  b->timings[8] = 1e3 * k4_ms;
   b->timings[1] = t2 - t1;
   b->timings[2] = t3 - t2;
   b->timings[3] = t4 - t3;
@@ -361,8 +440,8 @@ size_t WebPGpuBatchTokenCount(const WebPGpuBatch* b, int f) {
 int WebPGpuBatchError(const WebPGpuBatch* b, int f) {
   return (b && f >= 0 && f < b->last_n) ? b->err[f] : VP8_ENC_ERROR_NULL_PARAMETER;
 }
-void WebPGpuBatchTimings(const WebPGpuBatch* b, double t[8]) {
-  for (int i = 0; i < 8; ++i) t[i] = b ? b->timings[i] : 0.;
+void WebPGpuBatchTimings(const WebPGpuBatch* b, double t[10]) {
+  for (int i = 0; i < 10; ++i) t[i] = b ? b->timings[i] : 0.;
 }
 
 int WebPGpuBatchGetYUV(const WebPGpuBatch* b, int f, uint8_t* dst) {

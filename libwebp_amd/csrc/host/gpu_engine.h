@@ -16,7 +16,7 @@ struct WebPGpuBatch {
   WebPConfig cfg;
   size_t yfb, tok_cap, d_rgba_cap, h_tok_cap;
   hipStream_t stream;
-  hipEvent_t ev[4];          /* K1 start, K2 end, K3 start, K3 end */
+  hipEvent_t ev[6];          /* K1 start, K2 end, K3 start, K3 end, K4 start, K4 end */
   int ev0_recorded;
   /* device (HBM) */
   uint8_t* d_rgba;
@@ -31,6 +31,14 @@ struct WebPGpuBatch {
   uint16_t* d_tokens;
   uint8_t* d_mbinfo;
   vp8g_frame_result* d_results;
+  uint32_t* d_psize;         /* partition-1 bytes per frame (K4) */
+  vp8g_emit_meta* d_emeta;   /* K4 per-frame bookkeeping */
+  vp8g_emit_meta* h_emeta;
+  uint8_t* d_emap;           /* K4 scratch, grown on demand */
+  uint16_t* d_eshift;
+  vp8g_emit_seg* d_esegs;
+  uint32_t* d_nbuf;
+  size_t emit_seg_cap, emit_word_cap;
   /* host (pinned) */
   uint32_t* h_aflags;
   uint8_t* h_alpha;
@@ -39,6 +47,10 @@ struct WebPGpuBatch {
   vp8g_frame_params* h_params;
   uint8_t* h_mbinfo;
   vp8g_frame_result* h_results;
+  uint32_t* h_psize;
+  uint8_t* h_part;           /* pinned partition-1 bytes of all frames */
+  size_t h_part_cap;
+  size_t* part_off;
   uint16_t* h_tokens;
   size_t* tok_off;
   vp8h_frame* frames;
@@ -47,7 +59,8 @@ struct WebPGpuBatch {
   size_t* out_size;
   int* err;
   int* hdr;
-  double timings[8];
+  double timings[10];
+  int host_emit;             /* partition 1 coded on the host (A/B, WEBP_AMD_HOST_EMIT=1) */
 };
 
 #ifdef __cplusplus

@@ -86,6 +86,26 @@ int vp8g_launch_encode(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h,
                        size_t tok_cap, uint8_t* mbinfo,
                        vp8g_frame_result* results, void* stream);
 
+/* K4: boolean coder for the token partition, parallel inside each frame
+ * (hip/vp8_emit.hip). Per-frame bookkeeping: ntok, the segment count and the
+ * first segment / first N-array word of the frame (host), S and L (device). */
+typedef struct {
+  uint32_t ntok, nseg, seg_base, nb_base, S, L;
+} vp8g_emit_meta;
+typedef struct {
+  uint32_t T;      /* bit offset of the segment's part of N */
+  uint16_t S;      /* renormalisation shifts inside the segment */
+  uint8_t rs;      /* true range at the segment start */
+  uint8_t H;       /* bits of the segment's partial sum above its region */
+} vp8g_emit_seg;
+#define VP8G_EMIT_SEG 2048
+/* partition-1 bytes replace the tokens at the start of each frame's token
+ * buffer; out_size[f] = their count */
+int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
+                     const vp8g_frame_result* results, vp8g_emit_meta* meta,
+                     uint32_t max_ntok, uint32_t max_seg, uint8_t* emap, uint16_t* eshift,
+                     vp8g_emit_seg* segs, uint32_t* nbuf, uint32_t* out_size, void* stream);
+
 /* synthetic syn-v1 frames straight into device memory */
 int vp8g_launch_synth(uint8_t* rgba, size_t frame_stride, int w, int h,
                       int first_frame, int n, int seed, void* stream);

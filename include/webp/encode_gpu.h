@@ -81,6 +81,11 @@ WEBP_EXTERN int WebPGpuBatchStageCycles(const WebPGpuBatch* batch, int frame,
  * decisions (20 bytes per MB: type, uv_mode, segment, skip, modes[16]). */
 WEBP_EXTERN int WebPGpuBatchGetYUV(const WebPGpuBatch* batch, int frame,
                                    uint8_t* dst);
+/* Debug: frame f's VP8 token stream (token_enc.c:31-35 format) and the final
+ * probabilities, available when the batch codes partition 1 on the host
+ * (WEBP_AMD_HOST_EMIT=1); returns 0 otherwise. */
+WEBP_EXTERN int WebPGpuBatchGetTokens(const WebPGpuBatch* batch, int frame, uint16_t* dst,
+                                      size_t max_tokens);
 WEBP_EXTERN int WebPGpuBatchGetMBInfo(const WebPGpuBatch* batch, int frame,
                                       uint8_t* dst);
 

@@ -58,6 +58,7 @@ def load():
         "WebPGpuBatchTimings": (None, [vp, C.POINTER(C.c_double)]),
         "WebPGpuBatchGetYUV": (i, [vp, i, vp]),
         "WebPGpuBatchGetMBInfo": (i, [vp, i, vp]),
+        "WebPGpuBatchGetTokens": (i, [vp, i, vp, sz]),
         "WebPGpuSynthRGBA": (i, [vp, sz, i, i, i, i, i, vp]),
         "WebPGpuDeviceCount": (i, []),
         "WebPGpuLastError": (C.c_char_p, []),

@@ -11,8 +11,11 @@
 // count. (Checked against the reference coder; tests/test_emit_model.py.)
 // So a frame's tokens are cut into segments and:
 //   E0 k_emit_resolve  token -> (bit, probability) in place, all tokens
-//   E1 k_emit_maps     per segment, the end range and shift count for each of
-//                      the 128 possible start ranges (one lane per range)
+//   E1 k_emit_img      per segment, the few ranges it can start with (the end
+//                      states of the previous segment's last 256 tokens run
+//                      from all 128 ranges; typically 4-10 survive)
+//      k_emit_maps     per segment, the end range and shift count from each
+//                      of those start ranges (16 lanes per segment)
 //   E2 k_emit_compose  per frame, chain the segment maps: every segment's true
 //                      start range and bit offset, pad bits, S and L
 //   E3 k_emit_seg      per segment (one lane each): forward pass with the true
@@ -68,44 +71,102 @@ __global__ __launch_bounds__(256) void k_emit_resolve(uint16_t* __restrict__ tok
   *reinterpret_cast<uint4*>(tok) = make_uint4(v[0], v[1], v[2], v[3]);
 }
 
-__global__ __launch_bounds__(128) void k_emit_maps(const uint16_t* __restrict__ tokens,
-                                                   size_t tok_cap,
-                                                   const vp8g_emit_meta* __restrict__ meta,
-                                                   uint8_t* __restrict__ emap,
-                                                   uint16_t* __restrict__ eshift) {
-  __shared__ __align__(16) uint16_t stage[EMIT_SEG];
+// One range-chain step: returns the renormalisation shift.
+__device__ __forceinline__ int chain_step(int& r, uint32_t pb) {
+  const int split = (r * (int)(pb & 0xff)) >> 8;
+  r = (pb >> 8) ? r - split - 1 : split;
+  return renorm(r);
+}
+
+// E1a: the range a segment can start with is the end state of the previous
+// segment, whatever state that one was in EMIT_IMG tokens before its end:
+// run those last tokens from all 128 ranges and keep the distinct end states
+// (a handful: the chains merge quickly). Segment 0 starts at 254.
+#define EMIT_IMG 256
+#define EMIT_SLOTS 16
+__global__ __launch_bounds__(128) void k_emit_img(const uint16_t* __restrict__ tokens,
+                                                  size_t tok_cap,
+                                                  const vp8g_emit_meta* __restrict__ meta,
+                                                  uint8_t* __restrict__ img) {
+  __shared__ __align__(16) uint16_t stage[EMIT_IMG];
+  __shared__ uint32_t seen[4];
   const int f = blockIdx.y, s = blockIdx.x, t = threadIdx.x;
   const vp8g_emit_meta M = meta[f];
   if ((uint32_t)s >= M.nseg) return;
-  const uint32_t i0 = (uint32_t)s * EMIT_SEG;
-  const uint32_t cnt = min((uint32_t)EMIT_SEG, M.ntok - i0);
-  const uint16_t* tok = tokens + (size_t)f * tok_cap + i0;
-  for (uint32_t k = t * 8; k < cnt; k += 128 * 8)   // 16-byte loads (tail padded by the buffer)
-    *reinterpret_cast<uint4*>(stage + k) = *reinterpret_cast<const uint4*>(tok + k);
+  uint8_t* out = img + ((size_t)M.seg_base + s) * (EMIT_SLOTS + 1);
+  if (s == 0) {
+    if (t == 0) { out[0] = 1; out[1] = 254; }
+    return;
+  }
+  const uint16_t* tok = tokens + (size_t)f * tok_cap + (size_t)s * EMIT_SEG - EMIT_IMG;
+  if (t < EMIT_IMG / 8)
+    *reinterpret_cast<uint4*>(stage + 8 * t) = *reinterpret_cast<const uint4*>(tok + 8 * t);
+  if (t < 4) seen[t] = 0;
   __syncthreads();
   int r = 127 + t;
-  uint32_t S = 0;
-  uint32_t i = 0;
-  for (; i + 8 <= cnt; i += 8) {
+  for (int i = 0; i < EMIT_IMG; i += 8) {
     const uint4 q = *reinterpret_cast<const uint4*>(stage + i);
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint32_t pb = (w[k >> 1] >> (16 * (k & 1))) & 0xffff;
-      const int split = (r * (int)(pb & 0xff)) >> 8;
-      r = (pb >> 8) ? r - split - 1 : split;
-      S += renorm(r);
+    for (int k = 0; k < 8; ++k) chain_step(r, (w[k >> 1] >> (16 * (k & 1))) & 0xffff);
+  }
+  atomicOr(&seen[(r - 127) >> 5], 1u << ((r - 127) & 31));
+  __syncthreads();
+  if (t == 0) {
+    int cnt = 0;
+    for (int wv = 0; wv < 4; ++wv) cnt += __popc(seen[wv]);
+    if (cnt > EMIT_SLOTS) {
+      out[0] = 0xff;   // too many: the map kernel covers all 128 ranges
+    } else {
+      out[0] = (uint8_t)cnt;
+      int k = 1;
+      for (int wv = 0; wv < 4; ++wv)
+        for (uint32_t m = seen[wv]; m; m &= m - 1) out[k++] = (uint8_t)(127 + 32 * wv + __ffs(m) - 1);
     }
   }
-  for (; i < cnt; ++i) {
-    const uint32_t pb = stage[i];
-    const int split = (r * (int)(pb & 0xff)) >> 8;
-    r = (pb >> 8) ? r - split - 1 : split;
-    S += renorm(r);
+}
+
+// E1b: per segment, the end range and shift count from each possible start
+// range: 4 segments per wavefront, 16 lanes (start ranges) each.
+__global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ tokens,
+                                                  size_t tok_cap,
+                                                  const vp8g_emit_meta* __restrict__ meta,
+                                                  const uint8_t* __restrict__ img,
+                                                  uint8_t* __restrict__ emap,
+                                                  uint16_t* __restrict__ eshift) {
+  const int f = blockIdx.y, lane = threadIdx.x;
+  const vp8g_emit_meta M = meta[f];
+  const uint32_t s = blockIdx.x * 4 + (lane >> 4);
+  const int slot = lane & 15;
+  const bool valid = s < M.nseg;
+  const uint32_t cnt = valid ? min((uint32_t)EMIT_SEG, M.ntok - s * EMIT_SEG) : 0u;
+  const uint8_t* im = img + ((size_t)M.seg_base + (valid ? s : 0)) * (EMIT_SLOTS + 1);
+  const int ni = valid ? im[0] : 0;
+  const int rounds = ni == 0xff ? 128 / EMIT_SLOTS : 1;
+  const uint16_t* tok = tokens + (size_t)f * tok_cap + (size_t)(valid ? s : 0) * EMIT_SEG;
+  for (int rd = 0; rd < rounds; ++rd) {
+    const bool live = valid && (ni == 0xff || slot < ni);
+    const int r0 = ni == 0xff ? 127 + EMIT_SLOTS * rd + slot : (live ? im[1 + slot] : 127);
+    int r = r0;
+    uint32_t S = 0;
+    for (uint32_t i = 0; i < cnt; i += 8) {   // segment starts are 16-byte aligned
+      const uint4 q = *reinterpret_cast<const uint4*>(tok + i);
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        int rr = r;
+        const int sh = chain_step(rr, (w[k >> 1] >> (16 * (k & 1))) & 0xffff);
+        const bool in = i + k < cnt;
+        r = in ? rr : r;
+        S += in ? sh : 0;
+      }
+    }
+    if (live) {
+      const size_t o = ((size_t)M.seg_base + s) * 128 + (r0 - 127);
+      emap[o] = (uint8_t)r;
+      eshift[o] = (uint16_t)S;
+    }
   }
-  const size_t o = ((size_t)M.seg_base + s) * 128 + t;
-  emap[o] = (uint8_t)r;
-  eshift[o] = (uint16_t)S;
 }
 
 __global__ __launch_bounds__(64) void k_emit_compose(vp8g_emit_meta* __restrict__ meta,
@@ -158,16 +219,28 @@ __global__ __launch_bounds__(64) void k_emit_seg(uint16_t* __restrict__ tokens, 
   const uint32_t i0 = s * EMIT_SEG;
   const uint32_t cnt = min((uint32_t)EMIT_SEG, M.ntok - i0);
   uint16_t* tok = tokens + (size_t)f * tok_cap + i0;
-  // forward: true range chain -> (c, shift) packed in place
+  // forward: true range chain -> (c, shift) packed in place, 8 tokens per
+  // 16-byte access (the segment start is 16-byte aligned; the tail chunk may
+  // run past cnt inside the buffer and is masked)
   int r = g.rs;
-  for (uint32_t i = 0; i < cnt; ++i) {
-    const uint32_t pb = tok[i];
-    const int split = (r * (int)(pb & 0xff)) >> 8;
-    const int bit = pb >> 8;
-    const int c = bit ? split + 1 : 0;
-    r = bit ? r - split - 1 : split;
-    const int sh = renorm(r);
-    tok[i] = (uint16_t)(c | (sh << 8));
+  for (uint32_t i = 0; i < cnt; i += 8) {
+    uint4 q = *reinterpret_cast<const uint4*>(tok + i);
+    uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t pb = (w[k >> 1] >> (16 * (k & 1))) & 0xffff;
+      const int split = (r * (int)(pb & 0xff)) >> 8;
+      const int bit = (pb >> 8) & 1;
+      const int c = bit ? split + 1 : 0;
+      const int rn = bit ? r - split - 1 : split;
+      int rr = rn;
+      const int sh = renorm(rr);
+      const bool live = i + k < cnt;
+      r = live ? rr : r;
+      const uint32_t pk = live ? (uint32_t)(c | (sh << 8)) : 0u;
+      w[k >> 1] = (w[k >> 1] & ~(0xffffu << (16 * (k & 1)))) | (pk << (16 * (k & 1)));
+    }
+    *reinterpret_cast<uint4*>(tok + i) = make_uint4(w[0], w[1], w[2], w[3]);
   }
   // reverse: least-significant first; bits below the current position are final
   uint32_t* W = nbuf + M.nb_base;
@@ -175,19 +248,25 @@ __global__ __launch_bounds__(64) void k_emit_seg(uint16_t* __restrict__ tokens, 
   uint32_t wb = T & ~31u;      // global bit index of acc's bit 0
   uint64_t acc = 0;
   uint32_t E = 0;
-  for (uint32_t i = cnt; i-- > 0;) {
-    const uint32_t pk = tok[i];
-    E += pk >> 8;
-    const uint32_t G = T + E;
-    while (G >= wb + 32) {   // word [wb, wb+32) is final
-      const uint32_t lo = (uint32_t)acc;
-      const uint32_t mlo = wb < T ? (~0u << (T - wb)) : ~0u;
-      if (mlo != ~0u) atomicOr(W + (wb >> 5), lo & mlo);
-      else W[wb >> 5] = lo;
-      acc >>= 32;
-      wb += 32;
+  const uint32_t last8 = (cnt + 7) & ~7u;   // padded entries are (c=0, shift=0)
+  for (uint32_t i = last8; i > 0; i -= 8) {
+    const uint4 q = *reinterpret_cast<const uint4*>(tok + i - 8);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 7; k >= 0; --k) {
+      const uint32_t pk = (w[k >> 1] >> (16 * (k & 1))) & 0xffff;
+      E += pk >> 8;
+      const uint32_t G = T + E;
+      while (G >= wb + 32) {   // word [wb, wb+32) is final
+        const uint32_t lo = (uint32_t)acc;
+        const uint32_t mlo = wb < T ? (~0u << (T - wb)) : ~0u;
+        if (mlo != ~0u) atomicOr(W + (wb >> 5), lo & mlo);
+        else W[wb >> 5] = lo;
+        acc >>= 32;
+        wb += 32;
+      }
+      acc += (uint64_t)(pk & 0xff) << (G - wb);
     }
-    acc += (uint64_t)(pk & 0xff) << (G - wb);
   }
   // remaining words up to the region top; bits above it are H_s
   while (wb < top) {
@@ -249,8 +328,8 @@ extern "C" int vp8g_launch_check(const char* what);
 extern "C" int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
                                 const vp8g_frame_result* results, vp8g_emit_meta* meta,
                                 uint32_t max_ntok, uint32_t max_seg, uint8_t* emap,
-                                uint16_t* eshift, vp8g_emit_seg* segs, uint32_t* nbuf,
-                                uint32_t* out_size, void* stream) {
+                                uint16_t* eshift, uint8_t* img, vp8g_emit_seg* segs,
+                                uint32_t* nbuf, uint32_t* out_size, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (n <= 0) return 1;
   const uint32_t rb = (max_ntok + 2047) / 2048;
@@ -260,8 +339,12 @@ extern "C" int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
     if (!vp8g_launch_check("k_emit_resolve")) return 0;
   }
   if (max_seg) {
-    hipLaunchKernelGGL(k_emit_maps, dim3(max_seg, n), dim3(128), 0, st, (const uint16_t*)tokens,
-                       tok_cap, (const vp8g_emit_meta*)meta, emap, eshift);
+    hipLaunchKernelGGL(k_emit_img, dim3(max_seg, n), dim3(128), 0, st, (const uint16_t*)tokens,
+                       tok_cap, (const vp8g_emit_meta*)meta, img);
+    if (!vp8g_launch_check("k_emit_img")) return 0;
+    hipLaunchKernelGGL(k_emit_maps, dim3((max_seg + 3) / 4, n), dim3(64), 0, st,
+                       (const uint16_t*)tokens, tok_cap, (const vp8g_emit_meta*)meta,
+                       (const uint8_t*)img, emap, eshift);
     if (!vp8g_launch_check("k_emit_maps")) return 0;
   }
   hipLaunchKernelGGL(k_emit_compose, dim3(n), dim3(64), 0, st, meta, (const uint8_t*)emap,

@@ -149,6 +149,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipFree(b->d_uva); hipFree(b->d_segmap); hipFree(b->d_params); hipFree(b->d_tokens);
   hipFree(b->d_mbinfo); hipFree(b->d_results); hipFree(b->d_psize); hipFree(b->d_emeta);
   hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs); hipFree(b->d_nbuf);
+  hipFree(b->d_eimg);
   hipHostFree(b->h_aflags); hipHostFree(b->h_alpha); hipHostFree(b->h_uva);
   hipHostFree(b->h_segmap); hipHostFree(b->h_params); hipHostFree(b->h_mbinfo);
   hipHostFree(b->h_results); hipHostFree(b->h_tokens); hipHostFree(b->h_psize);
@@ -278,12 +279,14 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
       if (m->nseg > max_seg) max_seg = m->nseg;
     }
     if (segs > b->emit_seg_cap) {
-      hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs);
-      b->d_emap = NULL; b->d_eshift = NULL; b->d_esegs = NULL; b->emit_seg_cap = 0;
+      hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs); hipFree(b->d_eimg);
+      b->d_emap = NULL; b->d_eshift = NULL; b->d_esegs = NULL; b->d_eimg = NULL;
+      b->emit_seg_cap = 0;
       const size_t cap = segs + segs / 4 + 64;
       CHK(hipMalloc((void**)&b->d_emap, cap * 128));
       CHK(hipMalloc((void**)&b->d_eshift, cap * 128 * sizeof(uint16_t)));
       CHK(hipMalloc((void**)&b->d_esegs, cap * sizeof(vp8g_emit_seg)));
+      CHK(hipMalloc((void**)&b->d_eimg, cap * 17));
       b->emit_seg_cap = cap;
     }
     if (words > b->emit_word_cap) {
@@ -298,7 +301,8 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
     CHK(hipMemcpyAsync(b->d_emeta, b->h_emeta, n * sizeof(vp8g_emit_meta),
                        hipMemcpyHostToDevice, st));
     if (!vp8g_launch_emit(b->d_tokens, b->tok_cap, n, b->d_results, b->d_emeta, max_ntok,
-                          max_seg, b->d_emap, b->d_eshift, b->d_esegs, b->d_nbuf, b->d_psize, st))
+                          max_seg, b->d_emap, b->d_eshift, b->d_eimg, b->d_esegs, b->d_nbuf,
+                          b->d_psize, st))
       return 0;
     CHK(hipEventRecord(b->ev[4], st));
     CHK(hipMemcpyAsync(b->h_psize, b->d_psize, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -449,6 +453,14 @@ int WebPGpuBatchGetYUV(const WebPGpuBatch* b, int f, uint8_t* dst) {
   const size_t bytes = (size_t)b->w * b->h + 2 * (size_t)b->uvw * b->uvh;
   hipSetDevice(b->device);
   return hipMemcpy(dst, b->d_yuv + (size_t)f * b->yfb, bytes, hipMemcpyDeviceToHost) == hipSuccess;
+}
+
+int WebPGpuBatchGetTokens(const WebPGpuBatch* b, int f, uint16_t* dst, size_t max_tokens) {
+  if (!b || f < 0 || f >= b->last_n || !dst || !b->host_emit) return 0;
+  const size_t n = b->h_results[f].ntokens < max_tokens ? b->h_results[f].ntokens : max_tokens;
+  hipSetDevice(b->device);
+  return hipMemcpy(dst, b->d_tokens + (size_t)f * b->tok_cap, n * sizeof(uint16_t),
+                   hipMemcpyDeviceToHost) == hipSuccess;
 }
 
 int WebPGpuBatchGetMBInfo(const WebPGpuBatch* b, int f, uint8_t* dst) {

@@ -36,6 +36,7 @@ struct WebPGpuBatch {
   vp8g_emit_meta* h_emeta;
   uint8_t* d_emap;           /* K4 scratch, grown on demand */
   uint16_t* d_eshift;
+  uint8_t* d_eimg;           /* possible start ranges per segment (17 B each) */
   vp8g_emit_seg* d_esegs;
   uint32_t* d_nbuf;
   size_t emit_seg_cap, emit_word_cap;

@@ -104,7 +104,8 @@ typedef struct {
 int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
                      const vp8g_frame_result* results, vp8g_emit_meta* meta,
                      uint32_t max_ntok, uint32_t max_seg, uint8_t* emap, uint16_t* eshift,
-                     vp8g_emit_seg* segs, uint32_t* nbuf, uint32_t* out_size, void* stream);
+                     uint8_t* img, vp8g_emit_seg* segs, uint32_t* nbuf, uint32_t* out_size,
+                     void* stream);
 
 /* synthetic syn-v1 frames straight into device memory */
 int vp8g_launch_synth(uint8_t* rgba, size_t frame_stride, int w, int h,

@@ -58,7 +58,7 @@ struct K3S {
   uint8_t rec4[10][16];
   alignas(16) int16_t lv4[10][16];
   alignas(16) int16_t co4[10][16];
-  alignas(8) score_t sc4[10];      // intra4 candidate scores (lambda_i4)
+  alignas(8) unsigned long long best4[2];   // intra4 argmin key (score << 4 | mode), 2 buffers
   alignas(8) score_t sm4[10];      // the same with lambda_mode
   int32_t r4[10][4];               // H, nz
   int32_t hsrc[16];                // sum_j w_j |Hadamard(src block)_j| per luma block
@@ -71,6 +71,10 @@ struct K3S {
   uint32_t trnz[4];
   uint32_t tnodes[64][32];
   int32_t max_edge[4];
+  struct {
+    uint64_t size_p0, sse[3];
+    int32_t nb[3];
+  } fs;                            // per-frame side statistics (frame_enc.c:480-489, :839)
   int32_t flag;          // dirty flag of finalize_probas_wg
   int32_t flag_mark;     // some statistics slot needs the in-order replay
   int32_t flag_ldc;      // left DC nz flag hand-off from wave 0
@@ -124,6 +128,14 @@ struct TLane {
   int is2, ig1, is1, ig3, is3;   // ITransform horizontal
   int hr[4], hc[4];        // TTransform row / column signs
 };
+
+// An optimisation barrier on a per-lane value: constants derived from it are
+// rebuilt where they are used instead of being hoisted out of the MB loop and
+// held in registers (and spilled) across the whole kernel.
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
 
 __device__ __forceinline__ TLane make_tlane(int j) {
   TLane T;
@@ -276,7 +288,7 @@ template <bool TRELLIS>
 __device__ void eval_i16(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid) {
   const int m = tid >> 6, lane = tid & 63, g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
   const int bsub = lane >> 4;
-  const TLane T = make_tlane(j);
+  const TLane T = make_tlane(opaque(j));
   int co[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
@@ -421,7 +433,7 @@ __device__ void eval_uv(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, in
                         const int8_t* topderr, int use_derr) {
   const int m = tid >> 6, lane = tid & 63, g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
   const int bsub = lane >> 4;
-  const TLane T = make_tlane(j);
+  const TLane T = make_tlane(opaque(j));
   int co[2];
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
@@ -608,7 +620,7 @@ __device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid,
   const int m = tid >> 4, j = tid & 15, g = (tid & 63) & 48, x = j & 3, y = j >> 2;
   const bool act = tid < 160;
   const int wj = L.wy[j];
-  const TLane T = make_tlane(j);
+  const TLane T = make_tlane(opaque(j));
   const P4Lane pl = p4_lane(L.p4[act ? tid : 0], x, y);
   // this lane's y1 quantiser entries, once per MB
   const vp8g_mtx& M = S.y1;
@@ -621,6 +633,7 @@ __device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid,
   int total_hdr = 0;
   I4Result res;
   res.ok = 1;
+  if (tid == 0) L.best4[0] = ~0ull;
   __syncthreads();
   for (int i4 = 0; i4 < 16; ++i4) {
     const int bx = i4 & 3, by = i4 >> 2;
@@ -689,7 +702,8 @@ __device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid,
       if (act && j == 0) {
         const int H = L.mcost4[(top_m * 10 + left_m) * 10 + m];
         const score_t dist = 256 * (score_t)(D + SD);
-        L.sc4[m] = (score_t)(R0 + Rc + H) * S.lambda_i4 + dist;
+        const score_t sc = (score_t)(R0 + Rc + H) * S.lambda_i4 + dist;
+        atomicMin(&L.best4[i4 & 1], ((unsigned long long)sc << 4) | (unsigned)m);
         L.sm4[m] = (score_t)(R0 + Rc + H) * S.lambda_mode + dist;
         L.r4[m][0] = H;
         L.r4[m][1] = nzb;
@@ -699,13 +713,8 @@ __device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid,
     __syncthreads();
     int bm;
     if (search) {
-      bm = 0;
-      score_t bs = L.sc4[0];
-#pragma unroll
-      for (int k = 1; k < 10; ++k) {   // argmin, ties to the lower mode
-        const score_t sk = L.sc4[k];
-        if (sk < bs) { bs = sk; bm = k; }
-      }
+      bm = (int)(L.best4[i4 & 1] & 15);   // argmin, ties to the lower mode
+      if (tid == 0) L.best4[(i4 + 1) & 1] = ~0ull;
       const int H = L.r4[bm][0], bnzv = L.r4[bm][1];
       accH += H;
       acc_score += L.sm4[bm];
@@ -847,12 +856,21 @@ __device__ __forceinline__ void refresh_hc(K3S& L, int tid) {
   }
 }
 
+// Stage cycle accounting only in the diagnostic builds (-DK3_STAMPS for the
+// coarse stages, -DK3_SUBPROF for the intra4 split): the production kernel
+// keeps no timers live across the MB loop.
+#ifdef K3_STAMPS
 #define K3_STAMP(i)                                   \
   do {                                                \
     const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
     stamps[i] += t_ - stamp_last;                     \
     stamp_last = t_;                                  \
   } while (0)
+#else
+#define K3_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
 
 struct K3Args {
   const uint8_t* yuv;
@@ -921,18 +939,24 @@ __global__ __launch_bounds__(K3T) void k_encode(K3Args a) {
   const int use_derr = P->use_derr;
   const int max_count = P->max_count;
   int cnt = max_count;
-  uint64_t size_p0 = 0, sse_acc[3] = {0, 0, 0};
-  int nb_i4 = 0, nb_i16 = 0, nb_skip = 0;
+  // per-frame side statistics live in LDS (tid 0 / wave 0 update them) so
+  // they do not occupy scalar registers across the MB loop
+  if (tid == 0) {
+    L.fs.size_p0 = 0; L.fs.sse[0] = L.fs.sse[1] = L.fs.sse[2] = 0;
+    L.fs.nb[0] = L.fs.nb[1] = L.fs.nb[2] = 0;
+  }
   uint32_t ntok = 0;
   int tok_err = 0;
   int left_dc = 0;
+#ifdef K3_STAMPS
   uint64_t stamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t stamp_last = __builtin_amdgcn_s_memtime();
+#endif
 #ifdef K3_SUBPROF
   uint64_t substamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #else
   uint64_t* substamps = nullptr;
 #endif
-  uint64_t stamp_last = __builtin_amdgcn_s_memtime();
   uint8_t* yl = L.yl_mem + 1;
   uint8_t* ul = L.ul_mem + 1;
   uint8_t* vl = L.vl_mem + 1;
@@ -1120,9 +1144,9 @@ __global__ __launch_bounds__(K3T) void k_encode(K3Args a) {
     if (tid == 0) {
       uint8_t* info = mbinfo + (size_t)mb * VP8G_MBINFO_BYTES;
       info[0] = is_i16; info[1] = bu; info[2] = segid; info[3] = skip;
-      if (is_i16) ++nb_i16; else ++nb_i4;
-      if (skip) ++nb_skip;
-      size_p0 += rdH;
+      ++L.fs.nb[is_i16 ? 1 : 0];
+      if (skip) ++L.fs.nb[2];
+      L.fs.size_p0 += rdH;
     }
     if (tid < 16) mbinfo[(size_t)mb * VP8G_MBINFO_BYTES + 4 + tid] = L.modes[tid];
     // SSE for WebPAuxStats (frame_enc.c:480-489), wave 0
@@ -1139,7 +1163,7 @@ __global__ __launch_bounds__(K3T) void k_encode(K3Args a) {
         su = du * du; sv = dv * dv;
       }
       sy = sum64(sy); su = sum64(su); sv = sum64(sv);
-      sse_acc[0] += sy; sse_acc[1] += su; sse_acc[2] += sv;
+      if (lane == 0) { L.fs.sse[0] += sy; L.fs.sse[1] += su; L.fs.sse[2] += sv; }
     }
     K3_STAMP(4);
 
@@ -1329,13 +1353,15 @@ __global__ __launch_bounds__(K3T) void k_encode(K3Args a) {
     R->ntokens = ntok;
     R->error = tok_err;
     for (int s = 0; s < 4; ++s) R->max_edge[s] = L.max_edge[s];
-    R->size_p0 = size_p0;
-    R->sse[0] = sse_acc[0]; R->sse[1] = sse_acc[1]; R->sse[2] = sse_acc[2];
-    R->block_count[0] = nb_i4; R->block_count[1] = nb_i16; R->block_count[2] = nb_skip;
-#ifdef K3_SUBPROF
+    R->size_p0 = L.fs.size_p0;
+    R->sse[0] = L.fs.sse[0]; R->sse[1] = L.fs.sse[1]; R->sse[2] = L.fs.sse[2];
+    R->block_count[0] = L.fs.nb[0]; R->block_count[1] = L.fs.nb[1]; R->block_count[2] = L.fs.nb[2];
+#if defined(K3_SUBPROF)
     for (int i = 0; i < 8; ++i) R->stamps[i] = substamps[i];
-#else
+#elif defined(K3_STAMPS)
     for (int i = 0; i < 8; ++i) R->stamps[i] = stamps[i];
+#else
+    for (int i = 0; i < 8; ++i) R->stamps[i] = 0;
 #endif
   }
 }

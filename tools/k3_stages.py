@@ -9,7 +9,7 @@ W, H = int(sys.argv[1]), int(sys.argv[2])
 B = int(sys.argv[3]) if len(sys.argv) > 3 else 8
 method = int(sys.argv[4]) if len(sys.argv) > 4 else 4
 names = ["load+refresh+preds", "i16", "i4", "uv(+m5)", "info+sse", "tokens", "fold", "ctx+bnd"]
-if os.environ.get("WEBP_AMD_LIB", "").endswith("_prof.so"):
+if os.environ.get("WEBP_AMD_LIB", "").endswith("_sub.so"):
     names = ["i4:pred", "i4:fdct", "i4:quant", "i4:idct", "i4:distortion", "i4:rate+score",
              "i4:select", "i4:commit"]
 buf = torch.empty(B * W * H * 4, dtype=torch.uint8, device="cuda")
@@ -22,6 +22,10 @@ t = enc.timings()
 nmb = ((W + 15) // 16) * ((H + 15) // 16)
 c = enc.stage_cycles(0)
 tot = sum(c)
+if tot == 0:
+    print("%dx%d batch %d m%d: k_encode %.1f ms (%.1f us/MB); stage cycles need a diagnostic build "
+          "(WEBP_AMD_LIB=libwebp_amd/libwebp_amd_prof.so)" % (W, H, B, method, t[6] / 1e3, t[6] / nmb))
+    sys.exit(0)
 print("%dx%d batch %d m%d: k_encode %.1f ms (%.1f us/MB), tail %.1f ms" %
       (W, H, B, method, t[6] / 1e3, t[6] / nmb, t[4] / 1e3))
 for n, v in zip(names, c):

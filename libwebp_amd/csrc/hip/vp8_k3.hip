@@ -24,7 +24,9 @@
 
 #define K3T 256
 
-struct K3S {
+// LDS shared by all of a frame's workers: cost tables of the current epoch,
+// token statistics, quantiser/segment parameters and frame-level counters.
+struct K3G {
   uint32_t stats[NSLOT];
   uint32_t delta[NSLOT];
   uint16_t lcost[96][MAX_VLEVEL + 1];  // [type*24 + band*3 + ctx][level], incl. fixed cost
@@ -36,6 +38,22 @@ struct K3S {
   uint8_t coeffs[NSLOT];
   uint32_t mark[33];
   vp8g_seg seg[4];
+  int32_t max_edge[4];
+  struct {
+    unsigned long long size_p0, sse[3];
+    int32_t nb[3];
+  } fs;                            // per-frame side statistics (frame_enc.c:480-489, :839)
+  int32_t dirty;                   // FinalizeTokenProbas result
+  int32_t flag_mark;               // some statistics slot needs the in-order replay
+  uint32_t fold_ptr;               // raster MBs whose tokens are folded into stats
+  uint32_t ntok;                   // tokens in the frame's compact stream
+  int32_t tok_err;
+  int32_t epoch;                   // cost-table epochs published
+  int32_t abort;                   // a cross-worker wait timed out (bug guard)
+};
+
+// LDS private to one worker (4 wavefronts) and the MB it is encoding.
+struct K3S {
   uint8_t yin[16 * BPS];
   uint8_t yout[16 * BPS];
   uint8_t p16[4][256];
@@ -55,11 +73,10 @@ struct K3S {
   alignas(16) int16_t fin_uv[8][16];
   uint8_t modes[16];
   uint8_t canvas[17][24];
-  uint8_t rec4[10][16];
   alignas(16) int16_t lv4[10][16];
   alignas(16) int16_t co4[10][16];
   alignas(8) unsigned long long best4[2];   // intra4 argmin key (score << 4 | mode), 2 buffers
-  alignas(8) score_t sm4[10];      // the same with lambda_mode
+  alignas(8) score_t sm4[10];      // intra4 candidate scores with lambda_mode
   int32_t r4[10][4];               // H, nz
   int32_t hsrc[16];                // sum_j w_j |Hadamard(src block)_j| per luma block
   alignas(16) int16_t acc_ac[16][16];
@@ -68,20 +85,38 @@ struct K3S {
   int32_t blkinfo[32];
   int32_t blast[32];               // last non-zero zigzag position per token block
   int32_t wsum[2][4];              // per-wave token-count totals (scan)
+  int32_t redw[4];                 // per-wave reduction slots
   uint32_t trnz[4];
-  uint32_t tnodes[64][32];
-  int32_t max_edge[4];
-  struct {
-    uint64_t size_p0, sse[3];
-    int32_t nb[3];
-  } fs;                            // per-frame side statistics (frame_enc.c:480-489, :839)
-  int32_t flag;          // dirty flag of finalize_probas_wg
-  int32_t flag_mark;     // some statistics slot needs the in-order replay
-  int32_t flag_ldc;      // left DC nz flag hand-off from wave 0
+  uint32_t bar;                    // worker barrier counter
+  int32_t myabort;
+  int32_t flag_ldc;                // left DC nz flag hand-off from wave 0
+  uint32_t mark_any;
   uint8_t yl_mem[17], ul_mem[9], vl_mem[9];
   uint8_t predleft[4];
   int8_t lderr[2][2];
 };
+
+// Barrier over the 4 wavefronts of one worker (s_barrier would stop the whole
+// workgroup, i.e. every worker). Arrivals count up an LDS word; a wave
+// waits for the next multiple of 4. Called in worker-uniform control flow.
+__device__ __forceinline__ void wbar(K3S& L) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  uint32_t target = 0;
+  if ((threadIdx.x & 63) == 0) target = (atomicAdd(&L.bar, 1u) & ~3u) + 4u;
+  target = __builtin_amdgcn_readfirstlane(target);
+  while (__hip_atomic_load(&L.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+    __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+#define WB() wbar(L)
+
+// all-threads AND over the worker
+__device__ __forceinline__ int wbar_and(K3S& L, int v) {
+  const int all = __all(v);
+  if ((threadIdx.x & 63) == 0) L.redw[(threadIdx.x >> 6) & 3] = all;
+  wbar(L);
+  return L.redw[0] & L.redw[1] & L.redw[2] & L.redw[3];
+}
 
 // ---------------------------------------------------------------------------
 // 16-lane block primitives. g = first lane of the block's group in the wave,
@@ -259,21 +294,21 @@ __device__ __forceinline__ int quant_lane(int cv, int j, const vp8g_mtx& M, int&
 // lane: the context of position n is the previous position's level (one
 // bpermute), every lane does its table reads unconditionally (no divergent
 // branches) and a 16-lane reduction sums the terms.
-__device__ __forceinline__ int rate_lane(const K3S& L, int level, int j, int g, int ctx0, int type,
+__device__ __forceinline__ int rate_lane(const K3G& G, int level, int j, int g, int ctx0, int type,
                                          int first) {
   const int n = zz_inv(j);
   const int v = iabs_(level);
   const int last = max16((v != 0 && n >= first) ? n : -1);
   const int vprev = iabs_(__shfl(level, g + zz_rt(n > 0 ? n - 1 : 0)));
   const int ctxp = n == first ? ctx0 : min(vprev, 2);
-  int cost = L.lcost[type * 24 + band_of(n) * 3 + ctxp][min(v, MAX_VLEVEL)];
+  int cost = G.lcost[type * 24 + band_of(n) * 3 + ctxp][min(v, MAX_VLEVEL)];
   if (v > MAX_VLEVEL)   // rare: beyond the LDS rows
     cost += kVP8LevelFixedCost[v] - kVP8LevelFixedCost[MAX_VLEVEL];
-  const int eob = L.hc[type * 24 + band_of(n + 1) * 3 + min(v, 2)][0];
+  const int eob = G.hc[type * 24 + band_of(n + 1) * 3 + min(v, 2)][0];
   cost += (n == last && n < 15) ? eob : 0;
   cost = (n >= first && n <= last) ? cost : 0;
   const int t0 = type * 24 + first * 3 + ctx0;   // band(first) == first
-  const int h0 = L.hc[t0][0], h1 = L.hc[t0][1];
+  const int h0 = G.hc[t0][0], h1 = G.hc[t0][1];
   const int hdr = last < 0 ? h0 : (ctx0 == 0 ? h1 : 0);
   cost += j == 0 ? hdr : 0;
   return sum16(cost);
@@ -285,7 +320,8 @@ __device__ __forceinline__ int rate_lane(const K3S& L, int level, int j, int g, 
 // mres[m] = {SSE, texture distortion, rate, nz (ac bits | dc << 24)}.
 
 template <bool TRELLIS>
-__device__ void eval_i16(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid) {
+__device__ void eval_i16(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_seg& S,
+                         const MBCtx& ctx, int tid) {
   const int m = tid >> 6, lane = tid & 63, g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
   const int bsub = lane >> 4;
   const TLane T = make_tlane(opaque(j));
@@ -299,7 +335,7 @@ __device__ void eval_i16(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid) {
     if (TRELLIS) L.co16[m][b][j] = (int16_t)co[p];
   }
   if (lane < 4) L.trnz[lane] = 0;
-  __syncthreads();
+  WB();
   if (lane < 16) {   // FTransformWHT + y2 quantisation, coefficient b = lane
     const int16_t* d = L.dcs[m];
     const int b = lane, r = b >> 2, col = b & 3;
@@ -330,7 +366,7 @@ __device__ void eval_i16(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid) {
           int c[16];
 #pragma unroll
           for (int k = 0; k < 16; ++k) c[k] = L.co16[m][b][k];
-          const int nz = trellis_quant(L, L.tnodes[m * 16 + b], c, L.lv16[m][b], tc + lc, 0, &S.y1,
+          const int nz = trellis_quant(G, tn[m * 16 + b], c, L.lv16[m][b], tc + lc, 0, &S.y1,
                                        S.lambda_trellis_i16);
           L.lv16[m][b][0] = 0;
 #pragma unroll
@@ -338,7 +374,7 @@ __device__ void eval_i16(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid) {
           if (nz) atomicOr(&L.trnz[m], 1u << b);
         }
       }
-      __syncthreads();
+      WB();
     }
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
@@ -370,10 +406,10 @@ __device__ void eval_i16(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid) {
     const int b = 4 * p + bsub, bx = b & 3, by = b >> 2;
     const int tctx = by == 0 ? ctx.top(bx) : (int)((nzm >> (b - 4)) & 1);
     const int lctx = bx == 0 ? ctx.left(by) : (int)((nzm >> (b - 1)) & 1);
-    const int r = rate_lane(L, lv[p], j, g, tctx + lctx, 0, 1);
+    const int r = rate_lane(G, lv[p], j, g, tctx + lctx, 0, 1);
     if (j == 0) rate += r;
   }
-  __syncthreads();   // whtq complete
+  WB();   // whtq complete
   // inverse WHT: the DC of each block (dec.c:137-162)
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
@@ -395,7 +431,7 @@ __device__ void eval_i16(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid) {
   }
   // reconstruction, SSE, texture distortion
   int sse = 0, tds = 0;
-  const int wj = L.wy[j];
+  const int wj = G.wy[j];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const int b = 4 * p + bsub, px = 4 * (b & 3) + x, py = 4 * (b >> 2) + y;
@@ -414,14 +450,14 @@ __device__ void eval_i16(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid) {
   int dcl = 0;
   if (lane < 16) dcl = L.lvdc[m][zz_inv(lane)];
   const int dcnz = __ballot(lane < 16 && dcl != 0) != 0;
-  const int rdc = rate_lane(L, dcl, lane & 15, 0, ctx.top(8) + ctx.left(8), 1, 0);
+  const int rdc = rate_lane(G, dcl, lane & 15, 0, ctx.top(8) + ctx.left(8), 1, 0);
   if (lane == 0) {
     L.mres[m][0] = sse;
     L.mres[m][1] = tds;
     L.mres[m][2] = rate + rdc;
     L.mres[m][3] = (int)(nzm | (dcnz ? (1u << 24) : 0u));
   }
-  __syncthreads();
+  WB();
 }
 
 // ---------------------------------------------------------------------------
@@ -429,7 +465,7 @@ __device__ void eval_i16(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid) {
 // cost_enc.c:258-278 VP8GetCostUV). Wave m = mode m, 8 blocks in 2 passes.
 // mres[m] = {SSE, rate, non-zero AC count, nz bits}.
 
-__device__ void eval_uv(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, int x0,
+__device__ void eval_uv(const K3G& G, K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, int x0,
                         const int8_t* topderr, int use_derr) {
   const int m = tid >> 6, lane = tid & 63, g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
   const int bsub = lane >> 4;
@@ -443,7 +479,7 @@ __device__ void eval_uv(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, in
     co[p] = fdct_lane(d, T);
     if (j == 0) L.uvdc[m][b] = (int16_t)co[p];
   }
-  __syncthreads();
+  WB();
   if (use_derr && lane < 2) {   // CorrectDCValues (quant_enc.c:875-906)
     const int cch = lane;
     const vp8g_mtx& M = S.uv;
@@ -475,7 +511,7 @@ __device__ void eval_uv(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, in
     L.uvderr[m][cch][1] = (int8_t)err[2];
     L.uvderr[m][cch][2] = (int8_t)err[3];
   }
-  __syncthreads();
+  WB();
   int lv[2], dq[2];
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
@@ -501,7 +537,7 @@ __device__ void eval_uv(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, in
     const int b = 4 * p + bsub, ch = b >> 2, k4 = b & 3, bx = k4 & 1, by = k4 >> 1;
     const int tctx = by == 0 ? ctx.top(4 + 2 * ch + bx) : (int)((nzm >> (b - 2)) & 1);
     const int lctx = bx == 0 ? ctx.left(4 + 2 * ch + by) : (int)((nzm >> (b - 1)) & 1);
-    const int r = rate_lane(L, lv[p], j, g, tctx + lctx, 2, 0);
+    const int r = rate_lane(G, lv[p], j, g, tctx + lctx, 2, 0);
     if (j == 0) rate += r;
     const int px = 8 * ch + 4 * bx + x, py = 4 * by + y;
     const int pr = L.puv[m][py * 16 + px];
@@ -518,7 +554,7 @@ __device__ void eval_uv(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, in
     L.mres[m][2] = flatc;
     L.mres[m][3] = (int)nzm;
   }
-  __syncthreads();
+  WB();
 }
 
 // ---------------------------------------------------------------------------
@@ -558,14 +594,6 @@ struct I4Result {
   uint32_t nz;
 };
 
-__device__ __forceinline__ uint8_t canvas_edge(const K3S& L, int k, int bx, int by) {
-  const int r = 4 * by, cc = 4 * bx;
-  if (k < 4) return L.canvas[r + 4 - k][cc];                // L K J I
-  if (k == 4) return L.canvas[r][cc];                       // X
-  if (k < 9) return L.canvas[r][cc + 1 + (k - 5)];          // A..D
-  return (by > 0 && bx == 3) ? L.canvas[0][17 + k - 9]      // E..H (top-right)
-                             : L.canvas[r][cc + 5 + k - 9];
-}
 
 // Branch-free 4x4 intra predictor sample (src/dsp/enc.c:351-512) for this
 // lane's (mode, pixel): pred = clip((wa*ea + wb*eb + wc*ec + rnd) >> sh) over
@@ -602,7 +630,8 @@ __device__ __forceinline__ int edge_off(int k, int bx, int by) {
 }
 
 template <bool TRELLIS>
-__device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, int x0,
+__device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_seg& S,
+                           const MBCtx& ctx, int tid, int x0,
                            int mbw, const uint8_t* predtop, const uint8_t* yl,
                            const uint8_t* yt, bool search, score_t rd_score, int max_bits,
                            uint64_t* sp) {
@@ -619,9 +648,9 @@ __device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid,
   if (tid < 16) L.canvas[1 + tid][0] = yl[tid];
   const int m = tid >> 4, j = tid & 15, g = (tid & 63) & 48, x = j & 3, y = j >> 2;
   const bool act = tid < 160;
-  const int wj = L.wy[j];
+  const int wj = G.wy[j];
   const TLane T = make_tlane(opaque(j));
-  const P4Lane pl = p4_lane(L.p4[act ? tid : 0], x, y);
+  const P4Lane pl = p4_lane(G.p4[act ? tid : 0], x, y);
   // this lane's y1 quantiser entries, once per MB
   const vp8g_mtx& M = S.y1;
   const uint32_t q_sh = M.sharpen[j], q_zt = M.zthresh[j], q_iq = M.iq[j], q_bias = M.bias[j];
@@ -634,7 +663,7 @@ __device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid,
   I4Result res;
   res.ok = 1;
   if (tid == 0) L.best4[0] = ~0ull;
-  __syncthreads();
+  WB();
   for (int i4 = 0; i4 < 16; ++i4) {
     const int bx = i4 & 3, by = i4 >> 2;
     const int left_m = bx == 0 ? L.predleft[by] : L.modes[i4 - 1];
@@ -660,16 +689,16 @@ __device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid,
     int level = 0, dq = 0;
     if constexpr (TRELLIS) {
       if (act) L.co4[m][j] = (int16_t)c;
-      __syncthreads();
+      WB();
       if (act && j == 0) {
         int cc[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) cc[k] = L.co4[m][k];
-        trellis_quant(L, L.tnodes[m], cc, L.lv4[m], ctx4, 3, &S.y1, S.lambda_trellis_i4);
+        trellis_quant(G, tn[m], cc, L.lv4[m], ctx4, 3, &S.y1, S.lambda_trellis_i4);
 #pragma unroll
         for (int k = 0; k < 16; ++k) L.co4[m][k] = (int16_t)cc[k];
       }
-      __syncthreads();
+      WB();
       if (act) {
         level = L.lv4[m][zz_inv(j)];
         dq = L.co4[m][j];
@@ -698,9 +727,9 @@ __device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid,
       SUBST(4);
       const int cntnz = __popcll((bac >> g) & 0xffff);
       const int R0 = (m > 0 && cntnz <= 3) ? 140 : 0;
-      const int Rc = rate_lane(L, level, j, g, ctx4, 3, 0);
+      const int Rc = rate_lane(G, level, j, g, ctx4, 3, 0);
       if (act && j == 0) {
-        const int H = L.mcost4[(top_m * 10 + left_m) * 10 + m];
+        const int H = G.mcost4[(top_m * 10 + left_m) * 10 + m];
         const score_t dist = 256 * (score_t)(D + SD);
         const score_t sc = (score_t)(R0 + Rc + H) * S.lambda_i4 + dist;
         atomicMin(&L.best4[i4 & 1], ((unsigned long long)sc << 4) | (unsigned)m);
@@ -710,7 +739,7 @@ __device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid,
       }
     }
     SUBST(5);
-    __syncthreads();
+    WB();
     int bm;
     if (search) {
       bm = (int)(L.best4[i4 & 1] & 15);   // argmin, ties to the lower mode
@@ -735,11 +764,11 @@ __device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid,
       if (!search && j == 0) L.r4[0][2] = nzb;
     }
     if (search && tid == 0) L.modes[i4] = (uint8_t)bm;
-    __syncthreads();
+    WB();
     if (!search) acc_nz |= (uint32_t)L.r4[0][2] << i4;
     SUBST(7);
   }
-  __syncthreads();
+  WB();
   res.H = accH;
   res.score = acc_score;
   res.nz = acc_nz;
@@ -755,7 +784,7 @@ __device__ I4Result run_i4(K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid,
 // position n is the previous level. Returns the token count; EMIT writes the
 // tokens and adds their statistics deltas.
 template <bool EMIT>
-__device__ __forceinline__ int pos_tokens(K3S& L, int type, int first, int ctx0, int n, int c,
+__device__ __forceinline__ int pos_tokens(int type, int first, int ctx0, int n, int c,
                                           int cprev, int last, uint16_t* out) {
   if (n < first) return 0;
   const int vprev = iabs_(cprev);
@@ -766,7 +795,7 @@ __device__ __forceinline__ int pos_tokens(K3S& L, int type, int first, int ctx0,
   auto dyn = [&](int bit, int pid, int sid) -> int {
     if (EMIT) {
       out[count] = (uint16_t)((bit << 15) | pid);
-      atomicAdd(&L.delta[sid], 0x10000u + bit);
+      (void)sid;   // statistics are accumulated from the tokens at fold time
     }
     ++count;
     return bit;
@@ -818,41 +847,41 @@ __device__ __forceinline__ int pos_tokens(K3S& L, int type, int first, int ctx0,
 
 // FinalizeTokenProbas (frame_enc.c:146-180) over the workgroup; returns the
 // reference's "dirty" flag (some probability differs from the default).
-__device__ int finalize_probas_wg(K3S& L, int tid) {
-  if (tid == 0) L.flag = 0;
-  __syncthreads();
+__device__ int finalize_probas_wg(K3G& G, K3S& L, int tid) {
+  if (tid == 0) G.dirty = 0;
+  WB();
   int changed = 0;
   for (int s = tid; s < NSLOT; s += K3T) {
-    const uint32_t st = L.stats[s];
+    const uint32_t st = G.stats[s];
     const int nb = st & 0xffff, total = (st >> 16) & 0xffff;
     const int upd = (&kVP8CoeffUpdateProba[0][0][0][0])[s];
     const int old_p = (&kVP8CoeffProba0[0][0][0][0])[s];
     const int new_p = nb ? (255 - nb * 255 / total) : 255;
-    const int old_cost = nb * bit_cost(L.ecost, 1, old_p) + (total - nb) * bit_cost(L.ecost, 0, old_p) +
-                         bit_cost(L.ecost, 0, upd);
-    const int new_cost = nb * bit_cost(L.ecost, 1, new_p) + (total - nb) * bit_cost(L.ecost, 0, new_p) +
-                         bit_cost(L.ecost, 1, upd) + 8 * 256;
+    const int old_cost = nb * bit_cost(G.ecost, 1, old_p) + (total - nb) * bit_cost(G.ecost, 0, old_p) +
+                         bit_cost(G.ecost, 0, upd);
+    const int new_cost = nb * bit_cost(G.ecost, 1, new_p) + (total - nb) * bit_cost(G.ecost, 0, new_p) +
+                         bit_cost(G.ecost, 1, upd) + 8 * 256;
     if (old_cost > new_cost) {
-      L.coeffs[s] = new_p;
+      G.coeffs[s] = new_p;
       changed |= (new_p != old_p);
     } else {
-      L.coeffs[s] = old_p;
+      G.coeffs[s] = old_p;
     }
   }
-  if (changed) L.flag = 1;
-  __syncthreads();
-  return L.flag;
+  if (changed) G.dirty = 1;
+  WB();
+  return G.dirty;
 }
 
 // bit costs of the first probability of every (type, band, ctx): read by
 // rate_lane for the block-header and end-of-block bits; refreshed at every
 // FinalizeTokenProbas since the probabilities change even when the level
 // cost tables are not recomputed
-__device__ __forceinline__ void refresh_hc(K3S& L, int tid) {
+__device__ __forceinline__ void refresh_hc(K3G& G, int tid) {
   for (int k = tid; k < 96; k += K3T) {
-    const int p = L.coeffs[k * 11];
-    L.hc[k][0] = bit_cost(L.ecost, 0, p);
-    L.hc[k][1] = bit_cost(L.ecost, 1, p);
+    const int p = G.coeffs[k * 11];
+    G.hc[k][0] = bit_cost(G.ecost, 0, p);
+    G.hc[k][1] = bit_cost(G.ecost, 1, p);
   }
 }
 
@@ -872,6 +901,122 @@ __device__ __forceinline__ void refresh_hc(K3S& L, int tid) {
   } while (0)
 #endif
 
+// ---------------------------------------------------------------------------
+// Frame-level machinery: several workers encode MBs of different rows at the
+// same time (a wavefront: row y may encode MB x once row y-1 has finished
+// MB x+1, exactly the data the reference's iterator carries down: top,
+// top-right, nz, I4 modes, U/V DC errors). The cost tables only change at the
+// refresh points of VP8EncTokenLoop (frame_enc.c:785-832), so inside an
+// epoch the wavefront reproduces the raster loop bit for bit; at an epoch
+// boundary everything before it is finished and folded first. Token
+// statistics are folded strictly in raster order (the saturating counters
+// are order dependent) by the owner of each row at its row end, which also
+// moves the row's tokens from per-MB slots to the compact stream.
+
+// VP8CalculateLevelCosts (cost_enc.c:42-90) over one worker, no barrier
+__device__ void level_costs_w(K3G& G, int tid) {
+  for (int k = tid; k < 96 * (MAX_VLEVEL + 1); k += K3T) {
+    const int tbc = k / (MAX_VLEVEL + 1), v = k % (MAX_VLEVEL + 1);
+    const uint8_t* p = G.coeffs + tbc * 11;
+    const int ctx = tbc % 3;
+    const int c0 = ctx > 0 ? bit_cost(G.ecost, 1, p[0]) : 0;
+    int cost;
+    if (v == 0) {
+      cost = bit_cost(G.ecost, 0, p[1]) + c0;
+    } else {
+      cost = bit_cost(G.ecost, 1, p[1]) + c0;
+      int pat = kVP8LevelCodes[v - 1][0], bits = kVP8LevelCodes[v - 1][1];
+      for (int i = 2; pat; ++i, pat >>= 1, bits >>= 1)
+        if (pat & 1) cost += bit_cost(G.ecost, bits & 1, p[i]);
+    }
+    G.lcost[tbc][v] = (uint16_t)(cost + kVP8LevelFixedCost[v]);
+  }
+}
+
+// statistics slot of a dynamic token: its probability slot, except the
+// second bit of the cat5/cat6 prefix, coded with probability base+10 but
+// counted at base+9 (token_enc.c:168)
+__device__ __forceinline__ int tok_stat_slot(uint32_t t) {
+  const int id = (int)(t & 0x3fff);
+  return (id % 11 == 10) ? id - 1 : id;
+}
+
+#define K3_SPIN_LIMIT (1 << 24)
+
+// worker-uniform wait until *p >= v (another worker publishes *p)
+__device__ bool wait_ge(K3G& G, K3S& L, const int32_t* p, int32_t v) {
+  int spins = 0;
+  while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) {
+    if (__hip_atomic_load(&G.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
+        ++spins > K3_SPIN_LIMIT) {
+      L.myabort = 1;
+      G.abort = 1;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  wbar(L);
+  return L.myabort == 0;
+}
+
+__device__ __forceinline__ void publish(int32_t* p, int32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Fold MBs [i0, i1) into the statistics in raster order: each MB's tokens
+// move from its slot to the compact stream while their statistics deltas
+// accumulate; counters that would cross the halving threshold inside the MB
+// are replayed token by token (VP8RecordStats, cost_enc.h:45-56).
+__device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint16_t* tok_base,
+                         const uint16_t* mbcnt) {
+  for (uint32_t i = i0; i < i1; ++i) {
+    const uint32_t n = mbcnt[i];
+    const uint16_t* src = tok_base + (size_t)i * VP8G_MAX_TOKENS_PER_MB;
+    uint16_t* dst = tok_base + G.ntok;
+    for (uint32_t c0 = 0; c0 < n; c0 += K3T) {
+      const bool v = c0 + tid < n;
+      const uint32_t t = v ? src[c0 + tid] : 0u;
+      wbar(L);   // the whole chunk is read before any of it is overwritten (dst <= src)
+      if (v) {
+        dst[c0 + tid] = (uint16_t)t;
+        if (!(t & 0x4000)) atomicAdd(&G.delta[tok_stat_slot(t)], 0x10000u + (t >> 15));
+      }
+    }
+    if (tid == 0) L.mark_any = 0;
+    wbar(L);
+    for (int s = tid; s < NSLOT; s += K3T) {
+      const uint32_t dlt = G.delta[s];
+      if (dlt) {
+        const uint32_t p = G.stats[s];
+        if ((p >> 16) + (dlt >> 16) < 0xffffu) {
+          G.stats[s] = p + dlt;
+        } else {
+          atomicOr(&G.mark[s >> 5], 1u << (s & 31));
+          L.mark_any = 1;
+        }
+        G.delta[s] = 0;
+      }
+    }
+    wbar(L);
+    if (L.mark_any) {   // rare: exact in-order replay of the marked counters
+      if (tid == 0) {
+        for (uint32_t k = 0; k < n; ++k) {
+          const uint32_t t = dst[k];
+          if (t & 0x4000) continue;
+          const int s = tok_stat_slot(t);
+          if (G.mark[s >> 5] & (1u << (s & 31))) record_stat(&G.stats[s], (int)(t >> 15));
+        }
+      }
+      wbar(L);
+      for (int k = tid; k < 33; k += K3T) G.mark[k] = 0;
+      wbar(L);
+    }
+    if (tid == 0) G.ntok += n;
+    wbar(L);
+  }
+  if (tid == 0) publish((int32_t*)&G.fold_ptr, (int32_t)i1);
+}
+
 struct K3Args {
   const uint8_t* yuv;
   size_t yfb;
@@ -881,21 +1026,29 @@ struct K3Args {
   uint16_t* tokens;
   size_t tok_cap;
   uint8_t* mbinfo;
+  uint16_t* mbcnt;
   vp8g_frame_result* results;
 };
 
-__global__ __launch_bounds__(K3T) void k_encode(K3Args a) {
+template <int NW>
+__global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   extern __shared__ __align__(16) uint8_t smem[];
-  K3S& L = *reinterpret_cast<K3S*>(smem);
   const int mbw = a.mbw, mbh = a.mbh, nmb = mbw * mbh;
-  uint8_t* ytop = smem + sizeof(K3S);            // 16*mbw + 16
-  uint8_t* uvtop = ytop + 16 * mbw + 16;         // 16*mbw
+  K3G& G = *reinterpret_cast<K3G*>(smem);
+  const int wk = threadIdx.x / K3T;        // worker
+  const int tid = threadIdx.x % K3T;       // thread within the worker
+  K3S& L = reinterpret_cast<K3S*>(smem + sizeof(K3G))[wk];
+  uint8_t* ytop = smem + sizeof(K3G) + NW * sizeof(K3S);   // 16*mbw + 16
+  uint8_t* uvtop = ytop + 16 * mbw + 16;                      // 16*mbw
   uint32_t* nzw = reinterpret_cast<uint32_t*>(uvtop + 16 * mbw) + 1;   // [-1..mbw-1]
   uint8_t* predtop = reinterpret_cast<uint8_t*>(nzw + mbw);           // 4*mbw
   int8_t* topderr = reinterpret_cast<int8_t*>(predtop + 4 * mbw);     // 4*mbw
+  int32_t* rowdone = reinterpret_cast<int32_t*>(topderr + 4 * mbw);   // mbh
+  uint32_t (*tnall)[32] = reinterpret_cast<uint32_t (*)[32]>(rowdone + mbh);   // NW*64 (trellis)
+  uint32_t (*tn)[32] = tnall + 64 * wk;
 
   const int f = blockIdx.x;
-  const int tid = threadIdx.x;
+  const int gt = threadIdx.x;
   const int lane = tid & 63;
   const bool w0 = tid < 64;
   const int w = a.w, h = a.h;
@@ -907,469 +1060,441 @@ __global__ __launch_bounds__(K3T) void k_encode(K3Args a) {
   const uint8_t* segmap = a.segmap + (size_t)f * nmb;
   uint16_t* tok_base = a.tokens + f * a.tok_cap;
   uint8_t* mbinfo = a.mbinfo + (size_t)f * nmb * VP8G_MBINFO_BYTES;
+  uint16_t* mbcnt = a.mbcnt + (size_t)f * nmb;
 
-  // ---- frame init
-  for (int s = tid; s < NSLOT; s += K3T) {
-    L.stats[s] = 0;
-    L.delta[s] = 0;
-    L.coeffs[s] = (&kVP8CoeffProba0[0][0][0][0])[s];
+  // ---- frame init (whole workgroup)
+  for (int s = gt; s < NSLOT; s += NW * K3T) {
+    G.stats[s] = 0;
+    G.delta[s] = 0;
+    G.coeffs[s] = (&kVP8CoeffProba0[0][0][0][0])[s];
   }
-  for (int k = tid; k < 33; k += K3T) L.mark[k] = 0;
-  for (int k = tid; k < 256; k += K3T) L.ecost[k] = kVP8EntropyCost[k];
-  for (int k = tid; k < 1000; k += K3T) L.mcost4[k] = (&kVP8ModeCostI4[0][0][0])[k];
-  for (int k = tid; k < 160; k += K3T) L.p4[k] = (&kP4[0][0])[k];
-  if (tid < 16) L.wy[tid] = kVP8WeightY[tid];
+  for (int k = gt; k < 33; k += NW * K3T) G.mark[k] = 0;
+  for (int k = gt; k < 256; k += NW * K3T) G.ecost[k] = kVP8EntropyCost[k];
+  for (int k = gt; k < 1000; k += NW * K3T) G.mcost4[k] = (&kVP8ModeCostI4[0][0][0])[k];
+  for (int k = gt; k < 160; k += NW * K3T) G.p4[k] = (&kP4[0][0])[k];
+  if (gt < 16) G.wy[gt] = kVP8WeightY[gt];
   {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(P->seg);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(L.seg);
-    for (int k = tid; k < (int)(sizeof(L.seg) / 4); k += K3T) dst[k] = src[k];
+    uint32_t* dst = reinterpret_cast<uint32_t*>(G.seg);
+    for (int k = gt; k < (int)(sizeof(G.seg) / 4); k += NW * K3T) dst[k] = src[k];
   }
-  for (int k = tid; k < 16 * mbw + 16; k += K3T) ytop[k] = 127;
-  for (int k = tid; k < 16 * mbw; k += K3T) uvtop[k] = 127;
-  for (int k = tid - 1; k < mbw; k += K3T) nzw[k] = 0;
-  for (int k = tid; k < 4 * mbw; k += K3T) { predtop[k] = 0; topderr[k] = 0; }
-  if (tid < 4) L.max_edge[tid] = 0;
+  for (int k = gt; k < 16 * mbw + 16; k += NW * K3T) ytop[k] = 127;
+  for (int k = gt; k < 16 * mbw; k += NW * K3T) uvtop[k] = 127;
+  for (int k = gt - 1; k < mbw; k += NW * K3T) nzw[k] = 0;
+  for (int k = gt; k < 4 * mbw; k += NW * K3T) { predtop[k] = 0; topderr[k] = 0; }
+  for (int k = gt; k < mbh; k += NW * K3T) rowdone[k] = 0;
+  if (gt < 4) G.max_edge[gt] = 0;
+  if (gt == 0) {
+    G.fs.size_p0 = 0; G.fs.sse[0] = G.fs.sse[1] = G.fs.sse[2] = 0;
+    G.fs.nb[0] = G.fs.nb[1] = G.fs.nb[2] = 0;
+    G.fold_ptr = 0; G.ntok = 0; G.tok_err = 0; G.epoch = 0; G.abort = 0;
+  }
+  if (tid == 0) { L.bar = 0; L.myabort = 0; }
   __syncthreads();
-  level_costs(L, tid, K3T);
-  refresh_hc(L, tid);
+  if (wk == 0) {
+    level_costs_w(G, tid);
+    refresh_hc(G, tid);
+  }
   __syncthreads();
 
   const int rd_opt = P->rd_opt;
   const int max_i4_bits = P->max_i4_header_bits;
   const int use_derr = P->use_derr;
   const int max_count = P->max_count;
-  int cnt = max_count;
-  // per-frame side statistics live in LDS (tid 0 / wave 0 update them) so
-  // they do not occupy scalar registers across the MB loop
-  if (tid == 0) {
-    L.fs.size_p0 = 0; L.fs.sse[0] = L.fs.sse[1] = L.fs.sse[2] = 0;
-    L.fs.nb[0] = L.fs.nb[1] = L.fs.nb[2] = 0;
-  }
-  uint32_t ntok = 0;
-  int tok_err = 0;
-  int left_dc = 0;
-#ifdef K3_STAMPS
-  uint64_t stamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t stamp_last = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef K3_SUBPROF
-  uint64_t substamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#else
+  const bool trellis_all = rd_opt >= 3;
   uint64_t* substamps = nullptr;
-#endif
   uint8_t* yl = L.yl_mem + 1;
   uint8_t* ul = L.ul_mem + 1;
   uint8_t* vl = L.vl_mem + 1;
 
-  for (int mb = 0; mb < nmb; ++mb) {
-    const int x = mb % mbw, y = mb / mbw;
-    if (x == 0) {   // InitLeft (iterator_enc.c:22-32)
-      if (tid < 16) yl[tid] = 129;
-      if (tid < 8) { ul[tid] = 129; vl[tid] = 129; }
-      if (tid == 0) {
-        yl[-1] = ul[-1] = vl[-1] = (y > 0) ? 129 : 127;
-        L.lderr[0][0] = L.lderr[0][1] = L.lderr[1][0] = L.lderr[1][1] = 0;
-      }
-      if (tid < 4) L.predleft[tid] = 0;
-      left_dc = 0;
-    }
-    load_mb(Yp, Up, Vp, w, h, x, y, L.yin, tid, K3T);
-    if (--cnt < 0) {   // frame_enc.c:828-832
-      if (finalize_probas_wg(L, tid)) level_costs(L, tid, K3T);
-      refresh_hc(L, tid);
-      cnt = max_count;
-    }
-    __syncthreads();
-    const int segid = segmap[mb];
-    const vp8g_seg& S = L.seg[segid];
-    const bool hl = x > 0, ht = y > 0;
-    const uint8_t* yt = ytop + 16 * x;
-    const uint8_t* uvt = uvtop + 16 * x;
-    MBCtx ctx;
-    nz_flags(nzw[x], nzw[x - 1], left_dc, ctx);
-
-    // ---- predictions (quant_enc.c:469-479)
-    {
-      const int dcy = dc_value(yl, yt, hl, ht, 16, 5);
-      for (int k = tid; k < 1024; k += K3T) {
-        const int m = k >> 8, p = k & 255;
-        L.p16[m][p] = pred_sample(m, 16, p & 15, p >> 4, yl, yt, hl, ht, dcy);
-      }
-      const int dcu = dc_value(ul, uvt, hl, ht, 8, 4);
-      const int dcv = dc_value(vl, uvt + 8, hl, ht, 8, 4);
-      for (int k = tid; k < 512; k += K3T) {
-        const int m = k >> 7, p = k & 127, px = p & 15, py = p >> 4, c = px >> 3;
-        L.puv[m][p] = pred_sample(m, 8, px & 7, py, c ? vl : ul, uvt + 8 * c, hl, ht, c ? dcv : dcu);
-      }
-      // texture (Hadamard) measure of the 16 source blocks, shared by the
-      // intra16 and intra4 distortions (VP8TDisto4x4 / 16x16)
-      const int b = tid >> 4, j = tid & 15;
-      const int src = L.yin[(4 * (b >> 2) + (j >> 2)) * BPS + 4 * (b & 3) + (j & 3)];
-      const int hs = sum16(ttrans_lane(src, make_tlane(j), L.wy[j]));
-      if (j == 0) L.hsrc[b] = hs;
-    }
-    __syncthreads();
-
-    K3_STAMP(0);
-    // ---- Intra16 (quant_enc.c:1002-1058)
-    const bool trellis_all = rd_opt >= 3;
-    if (trellis_all) eval_i16<true>(L, S, ctx, tid);
-    else eval_i16<false>(L, S, ctx, tid);
-    int best16 = 0;
-    uint32_t nz16 = 0;
-    score_t D16 = 0, SD16 = 0, H16 = 0, R16 = 0;
-    {
-      int same = 1;
-      const int v0 = L.yin[0];
-      same = L.yin[(tid >> 4) * BPS + (tid & 15)] == v0;
-      const int flat0 = __syncthreads_and(same);
-      int flat = flat0;
-      score_t best16_score = 0;
-      for (int mm = 0; mm < 4; ++mm) {
-        score_t Dm = L.mres[mm][0];
-        score_t SDm = S.tlambda ? (score_t)((S.tlambda * L.mres[mm][1] + 128) >> 8) : 0;
-        const score_t Hm = kVP8ModeCostI16[mm];
-        const score_t Rm = L.mres[mm][2];
-        if (flat) {
-          flat = (L.mres[mm][3] & 0xffff) == 0;
-          if (flat) { Dm *= 2; SDm *= 2; }
-        }
-        const score_t sc = (Rm + Hm) * S.lambda_i16 + 256 * (Dm + SDm);
-        if (mm == 0 || sc < best16_score) {
-          best16_score = sc; best16 = mm;
-          D16 = Dm; SD16 = SDm; H16 = Hm; R16 = Rm;
-          nz16 = (uint32_t)L.mres[mm][3];
-        }
-      }
-    }
-    // commit I16 as current best
-    L.yout[(tid >> 4) * BPS + (tid & 15)] = L.rec16[best16][tid];
-    (&L.fin_ac[0][0])[tid] = (&L.lv16[best16][0][0])[tid];
-    if (tid < 16) { L.fin_dc[tid] = L.lvdc[best16][tid]; L.modes[tid] = best16; }
-    score_t rd_score = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
-    score_t rdH = H16;
-    uint32_t rd_nz = nz16;
-    int is_i16 = 1;
-    if ((rd_nz & 0x100ffff) == 0x1000000 && D16 > S.min_disto) {   // StoreMaxDelta
-      int mv = iabs_(L.lvdc[best16][1]);
-      mv = max(mv, iabs_(L.lvdc[best16][2]));
-      mv = max(mv, iabs_(L.lvdc[best16][4]));
-      if (tid == 0 && mv > L.max_edge[segid]) L.max_edge[segid] = mv;
-    }
-    __syncthreads();
-
-    K3_STAMP(1);
-    // ---- Intra4 (quant_enc.c:1072-1165)
-    if (max_i4_bits > 0) {
-      I4Result r4 = trellis_all ? run_i4<true>(L, S, ctx, tid, x, mbw, predtop, yl, yt, true,
-                                               rd_score, max_i4_bits, substamps)
-                                : run_i4<false>(L, S, ctx, tid, x, mbw, predtop, yl, yt, true,
-                                                rd_score, max_i4_bits, substamps);
-      if (r4.ok) {
-        is_i16 = 0;
-        rdH = r4.H;
-        rd_score = r4.score;
-        rd_nz = r4.nz;
-        L.yout[(tid >> 4) * BPS + (tid & 15)] = L.acc_out[tid];
-        (&L.fin_ac[0][0])[tid] = (&L.acc_ac[0][0])[tid];
-      } else {
-        if (tid < 16) L.modes[tid] = best16;   // the aborted search wrote some
-      }
-      __syncthreads();
-    }
-
-    K3_STAMP(2);
-    // ---- UV (quant_enc.c:1169-1217)
-    int bu = 0;
-    {
-      eval_uv(L, S, ctx, tid, x, topderr, use_derr);
-      score_t bsc = 0, bH = 0;
-      for (int mm = 0; mm < 4; ++mm) {
-        const score_t Dm = L.mres[mm][0], Hm = kVP8ModeCostUV[mm];
-        score_t Rm = L.mres[mm][1];
-        if (mm > 0 && L.mres[mm][2] <= 2) Rm += 140 * 8;
-        const score_t sc = (Rm + Hm) * S.lambda_uv + 256 * Dm;
-        if (mm == 0 || sc < bsc) { bsc = sc; bu = mm; bH = Hm; }
-      }
-      rdH += bH;
-      rd_score += bsc;
-      rd_nz |= (uint32_t)L.mres[bu][3] << 16;
-      if (tid < 128) {
-        L.yout[(tid >> 4) * BPS + 16 + (tid & 15)] = L.recuv[bu][tid];
-        (&L.fin_uv[0][0])[tid] = (&L.lvuv[bu][0][0])[tid];
-      }
-      if (use_derr && tid < 2) {   // StoreDiffusionErrors (quant_enc.c:909-920)
-        const int cch = tid;
-        int8_t* top = topderr + 4 * x + 2 * cch;
-        int8_t* left = L.lderr[cch];
-        const int8_t* e = L.uvderr[bu][cch];
-        left[0] = e[0];
-        left[1] = (int8_t)(3 * e[2] >> 2);
-        top[0] = e[1];
-        top[1] = (int8_t)(e[2] - left[1]);
-      }
-      __syncthreads();
-    }
-
-    // ---- m5: final re-quantisation of the chosen modes with trellis
-    // (SimpleQuantize, quant_enc.c:1222-1245; RD_OPT_TRELLIS, :1384-1387)
-    if (rd_opt == 2) {
-      uint32_t nzq = 0;
-      if (is_i16) {
-        eval_i16<true>(L, S, ctx, tid);
-        L.yout[(tid >> 4) * BPS + (tid & 15)] = L.rec16[best16][tid];
-        (&L.fin_ac[0][0])[tid] = (&L.lv16[best16][0][0])[tid];
-        if (tid < 16) L.fin_dc[tid] = L.lvdc[best16][tid];
-        nzq = (uint32_t)L.mres[best16][3];
-      } else {
-        I4Result r4 = run_i4<true>(L, S, ctx, tid, x, mbw, predtop, yl, yt, false, 0, 0, substamps);
-        L.yout[(tid >> 4) * BPS + (tid & 15)] = L.acc_out[tid];
-        (&L.fin_ac[0][0])[tid] = (&L.acc_ac[0][0])[tid];
-        nzq = r4.nz;
-      }
-      __syncthreads();
-      eval_uv(L, S, ctx, tid, x, topderr, use_derr);   // derr state already updated
-      if (tid < 128) {
-        L.yout[(tid >> 4) * BPS + 16 + (tid & 15)] = L.recuv[bu][tid];
-        (&L.fin_uv[0][0])[tid] = (&L.lvuv[bu][0][0])[tid];
-      }
-      rd_nz = nzq | ((uint32_t)L.mres[bu][3] << 16);
-      __syncthreads();
-    }
-    (void)rd_score;
-    K3_STAMP(3);
-
-    // ---- per-MB info + stats side info
-    const int skip = rd_nz == 0;
+  for (int y = wk; y < mbh && !L.myabort; y += NW) {
+    // InitLeft (iterator_enc.c:22-32)
+    if (tid < 16) yl[tid] = 129;
+    if (tid < 8) { ul[tid] = 129; vl[tid] = 129; }
     if (tid == 0) {
-      uint8_t* info = mbinfo + (size_t)mb * VP8G_MBINFO_BYTES;
-      info[0] = is_i16; info[1] = bu; info[2] = segid; info[3] = skip;
-      ++L.fs.nb[is_i16 ? 1 : 0];
-      if (skip) ++L.fs.nb[2];
-      L.fs.size_p0 += rdH;
+      yl[-1] = ul[-1] = vl[-1] = (y > 0) ? 129 : 127;
+      L.lderr[0][0] = L.lderr[0][1] = L.lderr[1][0] = L.lderr[1][1] = 0;
     }
-    if (tid < 16) mbinfo[(size_t)mb * VP8G_MBINFO_BYTES + 4 + tid] = L.modes[tid];
-    // SSE for WebPAuxStats (frame_enc.c:480-489), wave 0
-    if (w0) {
-      int sy = 0, su = 0, sv = 0;
-      for (int k = lane; k < 256; k += 64) {
-        const int o = (k >> 4) * BPS + (k & 15);
-        const int dd = L.yin[o] - L.yout[o];
-        sy += dd * dd;
-      }
-      {
-        const int o = (lane >> 3) * BPS + 16 + (lane & 7);
-        const int du = L.yin[o] - L.yout[o], dv = L.yin[o + 8] - L.yout[o + 8];
-        su = du * du; sv = dv * dv;
-      }
-      sy = sum64(sy); su = sum64(su); sv = sum64(sv);
-      if (lane == 0) { L.fs.sse[0] += sy; L.fs.sse[1] += su; L.fs.sse[2] += sv; }
-    }
-    K3_STAMP(4);
-
-    // ---- tokens + exact statistics (frame_enc.c:411-453, token_enc.c:113-193)
-    // One (block, zigzag position) item per thread: its tokens depend only
-    // on its level, the previous level and the block's last non-zero
-    // position, so counts, a workgroup scan and the writes are all parallel.
-    const int first_blk = is_i16 ? 0 : 1;
-    uint64_t nzb = 0;
-    int lvi[2], lvp[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {   // items tid and tid + 256 = block*16 + pos
-      const int item = tid + K3T * q, k = item >> 4, n = item & 15;
-      int v = 0, vp = 0;
-      if (k < 25 && k >= first_blk) {
-        const int16_t* lvb = blk_levels(L, k);
-        v = lvb[n];
-        vp = n > 0 ? lvb[n - 1] : 0;
-      }
-      lvi[q] = v;
-      lvp[q] = vp;
-      const int last = max16(v != 0 ? n : -1);
-      if (n == 0 && k < 32) L.blast[k] = last;
-    }
-    __syncthreads();
-    if (w0) {
-      const int k = lane;
-      const bool active = k >= first_blk && k < 25;
-      nzb = __ballot(active && L.blast[k] >= 0);
-      if (active) {
-        int my_type, my_first, my_ctx;
-        if (k == 0) {
-          my_type = 1; my_first = 0; my_ctx = ctx.top(8) + ctx.left(8);
-        } else if (k <= 16) {
-          const int b = k - 1, bx = b & 3, by = b >> 2;
-          my_type = is_i16 ? 0 : 3; my_first = is_i16 ? 1 : 0;
-          const int t = by == 0 ? ctx.top(bx) : (int)((nzb >> (k - 4)) & 1);
-          const int l = bx == 0 ? ctx.left(by) : (int)((nzb >> (k - 1)) & 1);
-          my_ctx = t + l;
+    if (tid < 4) L.predleft[tid] = 0;
+    int left_dc = 0;
+    uint32_t fold_from = (uint32_t)y * mbw;   // first MB of this row not folded yet
+    wbar(L);
+    for (int x = 0; x < mbw; ++x) {
+      const uint32_t mb = (uint32_t)y * mbw + x;
+      // ---- cost-table epoch (frame_enc.c:828-832): refresh before MB k with
+      // k = max_count + e * (max_count + 1)
+      const int ep = (int)mb < max_count ? 0 : ((int)mb - max_count) / (max_count + 1) + 1;
+      if (ep > __hip_atomic_load(&G.epoch, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        const bool refresher = (int)mb == max_count + (ep - 1) * (max_count + 1);
+        if (refresher) {
+          // everything before this MB: rows above folded by their owners,
+          // this row's earlier MBs folded here
+          if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from)) break;
+          fold_mbs(G, L, tid, fold_from, mb, tok_base, mbcnt);
+          fold_from = mb;
+          wbar(L);
+          const int dirty = finalize_probas_wg(G, L, tid);
+          if (dirty) level_costs_w(G, tid);
+          refresh_hc(G, tid);
+          wbar(L);
+          if (tid == 0) publish(&G.epoch, ep);
         } else {
-          const int b = k - 17, ch = b >> 2, k4 = b & 3, bx = k4 & 1, by = k4 >> 1;
-          my_type = 2; my_first = 0;
-          const int t = by == 0 ? ctx.top(4 + 2 * ch + bx) : (int)((nzb >> (k - 2)) & 1);
-          const int l = bx == 0 ? ctx.left(4 + 2 * ch + by) : (int)((nzb >> (k - 1)) & 1);
-          my_ctx = t + l;
+          if (!wait_ge(G, L, &G.epoch, ep)) break;
         }
-        L.blkinfo[k] = my_type | (my_first << 4) | (my_ctx << 8);
-      } else if (k < 32) {
-        L.blkinfo[k] = -1;
       }
-    }
-    __syncthreads();
-    {
-      int cnt[2], bi[2], last[2];
+      // ---- wavefront dependency: MB x+1 of the row above (top-right) is done
+      if (y > 0 && !wait_ge(G, L, &rowdone[y - 1], min(x + 2, mbw))) break;
+
+      load_mb(Yp, Up, Vp, w, h, x, y, L.yin, tid, K3T);
+      wbar(L);
+      const int segid = segmap[mb];
+      const vp8g_seg& S = G.seg[segid];
+      const bool hl = x > 0, ht = y > 0;
+      const uint8_t* yt = ytop + 16 * x;
+      const uint8_t* uvt = uvtop + 16 * x;
+      MBCtx ctx;
+      nz_flags(nzw[x], nzw[x - 1], left_dc, ctx);
+
+      // ---- predictions (quant_enc.c:469-479)
+      {
+        const int dcy = dc_value(yl, yt, hl, ht, 16, 5);
+        for (int k = tid; k < 1024; k += K3T) {
+          const int m = k >> 8, p = k & 255;
+          L.p16[m][p] = pred_sample(m, 16, p & 15, p >> 4, yl, yt, hl, ht, dcy);
+        }
+        const int dcu = dc_value(ul, uvt, hl, ht, 8, 4);
+        const int dcv = dc_value(vl, uvt + 8, hl, ht, 8, 4);
+        for (int k = tid; k < 512; k += K3T) {
+          const int m = k >> 7, p = k & 127, px = p & 15, py = p >> 4, c = px >> 3;
+          L.puv[m][p] = pred_sample(m, 8, px & 7, py, c ? vl : ul, uvt + 8 * c, hl, ht, c ? dcv : dcu);
+        }
+        // texture (Hadamard) measure of the 16 source blocks, shared by the
+        // intra16 and intra4 distortions (VP8TDisto4x4 / 16x16)
+        const int b = tid >> 4, j = tid & 15;
+        const int src = L.yin[(4 * (b >> 2) + (j >> 2)) * BPS + 4 * (b & 3) + (j & 3)];
+        const int hs = sum16(ttrans_lane(src, make_tlane(opaque(j)), G.wy[j]));
+        if (j == 0) L.hsrc[b] = hs;
+      }
+      wbar(L);
+
+      // ---- Intra16 (quant_enc.c:1002-1058)
+      if (trellis_all) eval_i16<true>(G, L, tn, S, ctx, tid);
+      else eval_i16<false>(G, L, tn, S, ctx, tid);
+      int best16 = 0;
+      uint32_t nz16 = 0;
+      score_t D16 = 0, SD16 = 0, H16 = 0, R16 = 0;
+      {
+        const int v0 = L.yin[0];
+        const int same = L.yin[(tid >> 4) * BPS + (tid & 15)] == v0;
+        int flat = wbar_and(L, same);
+        score_t best16_score = 0;
+        for (int mm = 0; mm < 4; ++mm) {
+          score_t Dm = L.mres[mm][0];
+          score_t SDm = S.tlambda ? (score_t)((S.tlambda * L.mres[mm][1] + 128) >> 8) : 0;
+          const score_t Hm = kVP8ModeCostI16[mm];
+          const score_t Rm = L.mres[mm][2];
+          if (flat) {
+            flat = (L.mres[mm][3] & 0xffff) == 0;
+            if (flat) { Dm *= 2; SDm *= 2; }
+          }
+          const score_t sc = (Rm + Hm) * S.lambda_i16 + 256 * (Dm + SDm);
+          if (mm == 0 || sc < best16_score) {
+            best16_score = sc; best16 = mm;
+            D16 = Dm; SD16 = SDm; H16 = Hm; R16 = Rm;
+            nz16 = (uint32_t)L.mres[mm][3];
+          }
+        }
+      }
+      // commit I16 as current best
+      L.yout[(tid >> 4) * BPS + (tid & 15)] = L.rec16[best16][tid];
+      (&L.fin_ac[0][0])[tid] = (&L.lv16[best16][0][0])[tid];
+      if (tid < 16) { L.fin_dc[tid] = L.lvdc[best16][tid]; L.modes[tid] = best16; }
+      score_t rd_score = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
+      score_t rdH = H16;
+      uint32_t rd_nz = nz16;
+      int is_i16 = 1;
+      if ((rd_nz & 0x100ffff) == 0x1000000 && D16 > S.min_disto) {   // StoreMaxDelta
+        int mv = iabs_(L.lvdc[best16][1]);
+        mv = max(mv, iabs_(L.lvdc[best16][2]));
+        mv = max(mv, iabs_(L.lvdc[best16][4]));
+        if (tid == 0) atomicMax(&G.max_edge[segid], mv);
+      }
+      wbar(L);
+
+      // ---- Intra4 (quant_enc.c:1072-1165)
+      if (max_i4_bits > 0) {
+        I4Result r4 = trellis_all ? run_i4<true>(G, L, tn, S, ctx, tid, x, mbw, predtop, yl, yt, true,
+                                                 rd_score, max_i4_bits, substamps)
+                                  : run_i4<false>(G, L, tn, S, ctx, tid, x, mbw, predtop, yl, yt,
+                                                  true, rd_score, max_i4_bits, substamps);
+        if (r4.ok) {
+          is_i16 = 0;
+          rdH = r4.H;
+          rd_score = r4.score;
+          rd_nz = r4.nz;
+          L.yout[(tid >> 4) * BPS + (tid & 15)] = L.acc_out[tid];
+          (&L.fin_ac[0][0])[tid] = (&L.acc_ac[0][0])[tid];
+        } else {
+          if (tid < 16) L.modes[tid] = best16;   // the aborted search wrote some
+        }
+        wbar(L);
+      }
+
+      // ---- UV (quant_enc.c:1169-1217)
+      int bu = 0;
+      {
+        eval_uv(G, L, S, ctx, tid, x, topderr, use_derr);
+        score_t bsc = 0, bH = 0;
+        for (int mm = 0; mm < 4; ++mm) {
+          const score_t Dm = L.mres[mm][0], Hm = kVP8ModeCostUV[mm];
+          score_t Rm = L.mres[mm][1];
+          if (mm > 0 && L.mres[mm][2] <= 2) Rm += 140 * 8;
+          const score_t sc = (Rm + Hm) * S.lambda_uv + 256 * Dm;
+          if (mm == 0 || sc < bsc) { bsc = sc; bu = mm; bH = Hm; }
+        }
+        rdH += bH;
+        rd_score += bsc;
+        rd_nz |= (uint32_t)L.mres[bu][3] << 16;
+        if (tid < 128) {
+          L.yout[(tid >> 4) * BPS + 16 + (tid & 15)] = L.recuv[bu][tid];
+          (&L.fin_uv[0][0])[tid] = (&L.lvuv[bu][0][0])[tid];
+        }
+        if (use_derr && tid < 2) {   // StoreDiffusionErrors (quant_enc.c:909-920)
+          const int cch = tid;
+          int8_t* top = topderr + 4 * x + 2 * cch;
+          int8_t* left = L.lderr[cch];
+          const int8_t* e = L.uvderr[bu][cch];
+          left[0] = e[0];
+          left[1] = (int8_t)(3 * e[2] >> 2);
+          top[0] = e[1];
+          top[1] = (int8_t)(e[2] - left[1]);
+        }
+        wbar(L);
+      }
+
+      // ---- m5: final re-quantisation of the chosen modes with trellis
+      // (SimpleQuantize, quant_enc.c:1222-1245; RD_OPT_TRELLIS, :1384-1387)
+      if (rd_opt == 2) {
+        uint32_t nzq = 0;
+        if (is_i16) {
+          eval_i16<true>(G, L, tn, S, ctx, tid);
+          L.yout[(tid >> 4) * BPS + (tid & 15)] = L.rec16[best16][tid];
+          (&L.fin_ac[0][0])[tid] = (&L.lv16[best16][0][0])[tid];
+          if (tid < 16) L.fin_dc[tid] = L.lvdc[best16][tid];
+          nzq = (uint32_t)L.mres[best16][3];
+        } else {
+          I4Result r4 = run_i4<true>(G, L, tn, S, ctx, tid, x, mbw, predtop, yl, yt, false, 0, 0,
+                                     substamps);
+          L.yout[(tid >> 4) * BPS + (tid & 15)] = L.acc_out[tid];
+          (&L.fin_ac[0][0])[tid] = (&L.acc_ac[0][0])[tid];
+          nzq = r4.nz;
+        }
+        wbar(L);
+        eval_uv(G, L, S, ctx, tid, x, topderr, use_derr);   // derr state already updated
+        if (tid < 128) {
+          L.yout[(tid >> 4) * BPS + 16 + (tid & 15)] = L.recuv[bu][tid];
+          (&L.fin_uv[0][0])[tid] = (&L.lvuv[bu][0][0])[tid];
+        }
+        rd_nz = nzq | ((uint32_t)L.mres[bu][3] << 16);
+        wbar(L);
+      }
+      (void)rd_score;
+
+      // ---- per-MB info + side statistics
+      const int skip = rd_nz == 0;
+      if (tid == 0) {
+        uint8_t* info = mbinfo + (size_t)mb * VP8G_MBINFO_BYTES;
+        info[0] = is_i16; info[1] = bu; info[2] = segid; info[3] = skip;
+        atomicAdd(&G.fs.nb[is_i16 ? 1 : 0], 1);
+        if (skip) atomicAdd(&G.fs.nb[2], 1);
+        atomicAdd(&G.fs.size_p0, (unsigned long long)rdH);
+      }
+      if (tid < 16) mbinfo[(size_t)mb * VP8G_MBINFO_BYTES + 4 + tid] = L.modes[tid];
+      if (w0) {   // SSE for WebPAuxStats (frame_enc.c:480-489)
+        int sy = 0, su = 0, sv = 0;
+        for (int k = lane; k < 256; k += 64) {
+          const int o = (k >> 4) * BPS + (k & 15);
+          const int dd = L.yin[o] - L.yout[o];
+          sy += dd * dd;
+        }
+        {
+          const int o = (lane >> 3) * BPS + 16 + (lane & 7);
+          const int du = L.yin[o] - L.yout[o], dv = L.yin[o + 8] - L.yout[o + 8];
+          su = du * du; sv = dv * dv;
+        }
+        sy = sum64(sy); su = sum64(su); sv = sum64(sv);
+        if (lane == 0) {
+          atomicAdd(&G.fs.sse[0], (unsigned long long)sy);
+          atomicAdd(&G.fs.sse[1], (unsigned long long)su);
+          atomicAdd(&G.fs.sse[2], (unsigned long long)sv);
+        }
+      }
+
+      // ---- tokens (token_enc.c:113-193) into this MB's slot; one (block,
+      // zigzag position) item per thread, counts + scan + writes in parallel
+      const int first_blk = is_i16 ? 0 : 1;
+      uint64_t nzb = 0;
+      int lvi[2], lvp[2];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
+      for (int q = 0; q < 2; ++q) {   // items tid and tid + 256 = block*16 + pos
         const int item = tid + K3T * q, k = item >> 4, n = item & 15;
-        bi[q] = k < 25 ? L.blkinfo[k] : -1;
-        last[q] = k < 25 ? L.blast[k] : -1;
-        cnt[q] = bi[q] < 0 ? 0
-                           : pos_tokens<false>(L, bi[q] & 15, (bi[q] >> 4) & 15, bi[q] >> 8, n,
-                                               lvi[q], lvp[q], last[q], nullptr);
+        int v = 0, vp = 0;
+        if (k < 25 && k >= first_blk) {
+          const int16_t* lvb = blk_levels(L, k);
+          v = lvb[n];
+          vp = n > 0 ? lvb[n - 1] : 0;
+        }
+        lvi[q] = v;
+        lvp[q] = vp;
+        const int last = max16(v != 0 ? n : -1);
+        if (n == 0 && k < 32) L.blast[k] = last;
       }
-      // workgroup exclusive scan over items 0..511 (item order = token order)
-      int inc0 = cnt[0], inc1 = cnt[1];
+      wbar(L);
+      if (w0) {
+        const int k = lane;
+        const bool active = k >= first_blk && k < 25;
+        nzb = __ballot(active && L.blast[k] >= 0);
+        if (active) {
+          int my_type, my_first, my_ctx;
+          if (k == 0) {
+            my_type = 1; my_first = 0; my_ctx = ctx.top(8) + ctx.left(8);
+          } else if (k <= 16) {
+            const int b = k - 1, bx = b & 3, by = b >> 2;
+            my_type = is_i16 ? 0 : 3; my_first = is_i16 ? 1 : 0;
+            const int t = by == 0 ? ctx.top(bx) : (int)((nzb >> (k - 4)) & 1);
+            const int l = bx == 0 ? ctx.left(by) : (int)((nzb >> (k - 1)) & 1);
+            my_ctx = t + l;
+          } else {
+            const int b = k - 17, ch = b >> 2, k4 = b & 3, bx = k4 & 1, by = k4 >> 1;
+            my_type = 2; my_first = 0;
+            const int t = by == 0 ? ctx.top(4 + 2 * ch + bx) : (int)((nzb >> (k - 2)) & 1);
+            const int l = bx == 0 ? ctx.left(4 + 2 * ch + by) : (int)((nzb >> (k - 1)) & 1);
+            my_ctx = t + l;
+          }
+          L.blkinfo[k] = my_type | (my_first << 4) | (my_ctx << 8);
+        } else if (k < 32) {
+          L.blkinfo[k] = -1;
+        }
+      }
+      wbar(L);
+      {
+        int cnt[2], bi[2], last[2];
 #pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const int v0 = __shfl_up(inc0, off), v1 = __shfl_up(inc1, off);
-        if (lane >= off) { inc0 += v0; inc1 += v1; }
-      }
-      const int wv = tid >> 6;
-      if (lane == 63) { L.wsum[0][wv] = inc0; L.wsum[1][wv] = inc1; }
-      __syncthreads();
-      int pre0 = 0, pre1 = 0, tot0 = 0, tot1 = 0;
+        for (int q = 0; q < 2; ++q) {
+          const int item = tid + K3T * q, k = item >> 4, n = item & 15;
+          bi[q] = k < 25 ? L.blkinfo[k] : -1;
+          last[q] = k < 25 ? L.blast[k] : -1;
+          cnt[q] = bi[q] < 0 ? 0
+                             : pos_tokens<false>(bi[q] & 15, (bi[q] >> 4) & 15, bi[q] >> 8, n,
+                                                 lvi[q], lvp[q], last[q], nullptr);
+        }
+        int inc0 = cnt[0], inc1 = cnt[1];
 #pragma unroll
-      for (int w2 = 0; w2 < 4; ++w2) {
-        const int s0 = L.wsum[0][w2], s1 = L.wsum[1][w2];
-        if (w2 < wv) { pre0 += s0; pre1 += s1; }
-        tot0 += s0; tot1 += s1;
-      }
-      const int total = tot0 + tot1;
-      if (ntok + (uint32_t)total > a.tok_cap) tok_err = 1;
-      if (!tok_err) {
+        for (int off = 1; off < 64; off <<= 1) {
+          const int v0 = __shfl_up(inc0, off), v1 = __shfl_up(inc1, off);
+          if (lane >= off) { inc0 += v0; inc1 += v1; }
+        }
+        const int wv = tid >> 6;
+        if (lane == 63) { L.wsum[0][wv] = inc0; L.wsum[1][wv] = inc1; }
+        wbar(L);
+        int pre0 = 0, pre1 = 0, tot0 = 0, tot1 = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < 4; ++w2) {
+          const int s0 = L.wsum[0][w2], s1 = L.wsum[1][w2];
+          if (w2 < wv) { pre0 += s0; pre1 += s1; }
+          tot0 += s0; tot1 += s1;
+        }
+        uint16_t* slot = tok_base + (size_t)mb * VP8G_MAX_TOKENS_PER_MB;
         const int off0 = pre0 + inc0 - cnt[0];
         const int off1 = tot0 + pre1 + inc1 - cnt[1];
         if (cnt[0])
-          pos_tokens<true>(L, bi[0] & 15, (bi[0] >> 4) & 15, bi[0] >> 8, tid & 15, lvi[0], lvp[0],
-                           last[0], tok_base + ntok + off0);
+          pos_tokens<true>(bi[0] & 15, (bi[0] >> 4) & 15, bi[0] >> 8, tid & 15, lvi[0], lvp[0],
+                           last[0], slot + off0);
         if (cnt[1])
-          pos_tokens<true>(L, bi[1] & 15, (bi[1] >> 4) & 15, bi[1] >> 8, tid & 15, lvi[1], lvp[1],
-                           last[1], tok_base + ntok + off1);
-        ntok += total;
+          pos_tokens<true>(bi[1] & 15, (bi[1] >> 4) & 15, bi[1] >> 8, tid & 15, lvi[1], lvp[1],
+                           last[1], slot + off1);
+        if (tid == 0) mbcnt[mb] = (uint16_t)(tot0 + tot1);
       }
-    }
-    if (tid == 0) L.flag_mark = 0;
-    __syncthreads();
-    K3_STAMP(5);
-    // fold deltas into the statistics; slots that cross the halving
-    // threshold inside this MB are replayed in token order.
-    {
-      int any_mark = 0;
-      for (int s = tid; s < NSLOT; s += K3T) {
-        const uint32_t dlt = L.delta[s];
-        if (dlt) {
-          const uint32_t p = L.stats[s];
-          if ((p >> 16) + (dlt >> 16) < 0xffffu) {
-            L.stats[s] = p + dlt;
-          } else {
-            atomicOr(&L.mark[s >> 5], 1u << (s & 31));
-            any_mark = 1;
+      // update nz context (iterator_enc.c:267-283) and the left DC flag
+      if (tid == 0) {
+        int tn9[9], ln[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) { tn9[i] = ctx.top(i); ln[i] = ctx.left(i); }
+        if (is_i16) { tn9[8] = ln[8] = (int)(nzb & 1); }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          tn9[i] = (int)((nzb >> (1 + 12 + i)) & 1);      // block (i, 3)
+          ln[i] = (int)((nzb >> (1 + 4 * i + 3)) & 1);    // block (3, i)
+        }
+#pragma unroll
+        for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            tn9[4 + 2 * ch + i] = (int)((nzb >> (17 + 4 * ch + 2 + i)) & 1);
+            ln[4 + 2 * ch + i] = (int)((nzb >> (17 + 4 * ch + 2 * i + 1)) & 1);
           }
-          L.delta[s] = 0;
-        }
+        uint32_t word = 0;
+        word |= (tn9[0] << 12) | (tn9[1] << 13) | (tn9[2] << 14) | (tn9[3] << 15) |
+                (tn9[4] << 18) | (tn9[5] << 19) | (tn9[6] << 22) | (tn9[7] << 23) | (tn9[8] << 24);
+        word |= (ln[0] << 3) | (ln[1] << 7) | (ln[2] << 11) | (ln[4] << 17) | (ln[6] << 21);
+        nzw[x] = word;
+        L.flag_ldc = ln[8];
       }
-      if (any_mark) L.flag_mark = 1;
-      __syncthreads();
-      if (L.flag_mark) {
-        if (tid == 0) {
-          int nzdummy;
-          for (int kk = first_blk; kk < 25; ++kk) {
-            const int bi = L.blkinfo[kk];
-            gen_tokens<2>(L, blk_levels(L, kk), bi & 15, (bi >> 4) & 15, bi >> 8, nullptr,
-                          &nzdummy);
-          }
-        }
-        __syncthreads();
-        for (int kk = tid; kk < 33; kk += K3T) L.mark[kk] = 0;
-        __syncthreads();
-      }
-    }
-    K3_STAMP(6);
-    // update nz context (iterator_enc.c:267-283) and the left DC flag; nzb
-    // (wave 0) goes to the other waves through LDS
-    if (tid == 0) {
-      int tn[9], ln[9];
-#pragma unroll
-      for (int i = 0; i < 9; ++i) { tn[i] = ctx.top(i); ln[i] = ctx.left(i); }
-      if (is_i16) { tn[8] = ln[8] = (int)(nzb & 1); }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        tn[i] = (int)((nzb >> (1 + 12 + i)) & 1);      // block (i, 3)
-        ln[i] = (int)((nzb >> (1 + 4 * i + 3)) & 1);   // block (3, i)
-      }
-#pragma unroll
-      for (int ch = 0; ch < 2; ++ch)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          tn[4 + 2 * ch + i] = (int)((nzb >> (17 + 4 * ch + 2 + i)) & 1);
-          ln[4 + 2 * ch + i] = (int)((nzb >> (17 + 4 * ch + 2 * i + 1)) & 1);
-        }
-      uint32_t word = 0;
-      word |= (tn[0] << 12) | (tn[1] << 13) | (tn[2] << 14) | (tn[3] << 15) |
-              (tn[4] << 18) | (tn[5] << 19) | (tn[6] << 22) | (tn[7] << 23) | (tn[8] << 24);
-      word |= (ln[0] << 3) | (ln[1] << 7) | (ln[2] << 11) | (ln[4] << 17) | (ln[6] << 21);
-      nzw[x] = word;
-      L.flag_ldc = ln[8];
-    }
-    __syncthreads();
-    left_dc = L.flag_ldc;
+      wbar(L);
+      left_dc = L.flag_ldc;
 
-    // ---- boundary save (iterator_enc.c:290-313) + mode context
-    if (x < mbw - 1) {
-      if (tid < 16) yl[tid] = L.yout[15 + tid * BPS];
-      if (tid < 8) { ul[tid] = L.yout[16 + 7 + tid * BPS]; vl[tid] = L.yout[24 + 7 + tid * BPS]; }
-      if (tid == 0) { yl[-1] = yt[15]; ul[-1] = uvt[7]; vl[-1] = uvt[15]; }
-    }
-    __syncthreads();
-    if (y < mbh - 1) {
-      if (tid < 16) {
-        ytop[16 * x + tid] = L.yout[15 * BPS + tid];
-        uvtop[16 * x + tid] = L.yout[7 * BPS + 16 + tid];
+      // ---- boundary save (iterator_enc.c:290-313) + mode context
+      if (x < mbw - 1) {
+        if (tid < 16) yl[tid] = L.yout[15 + tid * BPS];
+        if (tid < 8) { ul[tid] = L.yout[16 + 7 + tid * BPS]; vl[tid] = L.yout[24 + 7 + tid * BPS]; }
+        if (tid == 0) { yl[-1] = yt[15]; ul[-1] = uvt[7]; vl[-1] = uvt[15]; }
       }
+      wbar(L);
+      if (y < mbh - 1) {
+        if (tid < 16) {
+          ytop[16 * x + tid] = L.yout[15 * BPS + tid];
+          uvtop[16 * x + tid] = L.yout[7 * BPS + 16 + tid];
+        }
+      }
+      if (tid < 4) {
+        predtop[4 * x + tid] = L.modes[12 + tid];
+        L.predleft[tid] = L.modes[4 * tid + 3];
+      }
+      wbar(L);
+      if (tid == 0) publish(&rowdone[y], x + 1);
     }
-    if (tid < 4) {
-      predtop[4 * x + tid] = L.modes[12 + tid];
-      L.predleft[tid] = L.modes[4 * tid + 3];
-    }
-    __syncthreads();
-    K3_STAMP(7);
+    if (L.myabort) break;
+    // row end: fold this row's remaining MBs once the rows above are folded
+    if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from)) break;
+    fold_mbs(G, L, tid, fold_from, (uint32_t)(y + 1) * mbw, tok_base, mbcnt);
+    wbar(L);
   }
 
   // ---- frame epilogue: final probabilities and side results
-  finalize_probas_wg(L, tid);
-  vp8g_frame_result* R = a.results + f;
-  for (int s = tid; s < NSLOT; s += K3T) R->probas[s] = L.coeffs[s];
-  if (tid == 0) {
-    R->ntokens = ntok;
-    R->error = tok_err;
-    for (int s = 0; s < 4; ++s) R->max_edge[s] = L.max_edge[s];
-    R->size_p0 = L.fs.size_p0;
-    R->sse[0] = L.fs.sse[0]; R->sse[1] = L.fs.sse[1]; R->sse[2] = L.fs.sse[2];
-    R->block_count[0] = L.fs.nb[0]; R->block_count[1] = L.fs.nb[1]; R->block_count[2] = L.fs.nb[2];
-#if defined(K3_SUBPROF)
-    for (int i = 0; i < 8; ++i) R->stamps[i] = substamps[i];
-#elif defined(K3_STAMPS)
-    for (int i = 0; i < 8; ++i) R->stamps[i] = stamps[i];
-#else
-    for (int i = 0; i < 8; ++i) R->stamps[i] = 0;
-#endif
+  __syncthreads();
+  if (wk == 0) {
+    finalize_probas_wg(G, L, tid);
+    vp8g_frame_result* R = a.results + f;
+    for (int s = tid; s < NSLOT; s += K3T) R->probas[s] = G.coeffs[s];
+    if (tid == 0) {
+      R->ntokens = G.ntok;
+      R->error = G.abort ? 2 : G.tok_err;
+      for (int s = 0; s < 4; ++s) R->max_edge[s] = G.max_edge[s];
+      R->size_p0 = G.fs.size_p0;
+      R->sse[0] = G.fs.sse[0]; R->sse[1] = G.fs.sse[1]; R->sse[2] = G.fs.sse[2];
+      R->block_count[0] = G.fs.nb[0]; R->block_count[1] = G.fs.nb[1];
+      R->block_count[2] = G.fs.nb[2];
+      for (int i = 0; i < 8; ++i) R->stamps[i] = 0;
+    }
   }
 }
 
 // ---------------------------------------------------------------------------
 
-static size_t k3_lds_bytes(int mbw) {
-  return sizeof(K3S) + (16 * mbw + 16) + 16 * mbw + 4 * (mbw + 1) + 4 * mbw + 4 * mbw + 16;
+template <int NW>
+static size_t k3_lds_bytes(int mbw, int mbh, bool trellis) {
+  return sizeof(K3G) + NW * sizeof(K3S) + (16 * mbw + 16) + 16 * mbw + 4 * (mbw + 1) + 4 * mbw +
+         4 * mbw + 4 * mbh + (trellis ? (size_t)NW * 64 * 32 * 4 : 0) + 16;
 }
 
 extern "C" int vp8g_launch_encode_w1(const uint8_t* yuv, size_t yfb, int w, int h, int n,
@@ -1378,24 +1503,9 @@ extern "C" int vp8g_launch_encode_w1(const uint8_t* yuv, size_t yfb, int w, int 
                                      vp8g_frame_result* results, void* stream);
 extern "C" int vp8g_launch_check(const char* what);
 
-extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, int n,
-                                  const uint8_t* segmap, const vp8g_frame_params* params,
-                                  uint16_t* tokens, size_t tok_cap, uint8_t* mbinfo,
-                                  vp8g_frame_result* results, void* stream) {
-  static int variant = -1;
-  if (variant < 0) {
-    const char* v = getenv("WEBP_AMD_K3");
-    variant = (v && v[0] == '1') ? 1 : 2;
-  }
-  if (variant == 1)   // single-wavefront reference kernel (A/B and debugging)
-    return vp8g_launch_encode_w1(yuv, yfb, w, h, n, segmap, params, tokens, tok_cap, mbinfo,
-                                 results, stream);
-  K3Args a;
-  a.yuv = yuv; a.yfb = yfb; a.w = w; a.h = h;
-  a.mbw = (w + 15) >> 4; a.mbh = (h + 15) >> 4;
-  a.segmap = segmap; a.params = params; a.tokens = tokens; a.tok_cap = tok_cap;
-  a.mbinfo = mbinfo; a.results = results;
-  const size_t lds = k3_lds_bytes(a.mbw);
+template <int NW>
+static int launch_k3(const K3Args& a, int n, bool trellis, void* stream) {
+  const size_t lds = k3_lds_bytes<NW>(a.mbw, a.mbh, trellis);
   if (lds > 160 * 1024) {
     vp8g_set_error("k_encode", "frame too wide for the LDS budget");
     return 0;
@@ -1404,7 +1514,7 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
     static size_t attr_bytes = 0;
     if (lds > attr_bytes) {
       const hipError_t e = hipFuncSetAttribute(
-          (const void*)k_encode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+          (const void*)k_encode<NW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) {
         vp8g_set_error("k_encode dynamic LDS opt-in", hipGetErrorString(e));
         return 0;
@@ -1412,18 +1522,30 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
       attr_bytes = lds;
     }
   }
-  hipLaunchKernelGGL(k_encode, dim3(n), dim3(K3T), lds, (hipStream_t)stream, a);
-  if (hipPeekAtLastError() != hipSuccess) {
-    hipFuncAttributes fa;
-    char msg[256];
-    if (hipFuncGetAttributes(&fa, (const void*)k_encode) == hipSuccess) {
-      snprintf(msg, sizeof(msg), "launch failed: lds=%zu static=%zu maxdyn=%d regs=%d maxthr=%d",
-               lds, (size_t)fa.sharedSizeBytes, fa.maxDynamicSharedSizeBytes, fa.numRegs,
-               fa.maxThreadsPerBlock);
-      vp8g_set_error("k_encode", msg);
-      (void)hipGetLastError();
-      return 0;
-    }
-  }
+  hipLaunchKernelGGL(k_encode<NW>, dim3(n), dim3(NW * K3T), lds, (hipStream_t)stream, a);
   return vp8g_launch_check("k_encode");
+}
+
+extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, int n,
+                                  const uint8_t* segmap, const vp8g_frame_params* params,
+                                  uint16_t* tokens, size_t tok_cap, uint8_t* mbinfo,
+                                  uint16_t* mbcnt, int trellis, vp8g_frame_result* results,
+                                  void* stream) {
+  static int variant = -1;
+  if (variant < 0) {   // WEBP_AMD_K3: 1 = single-wavefront reference kernel, 2 = one worker,
+                       // default: two workers per frame
+    const char* v = getenv("WEBP_AMD_K3");
+    variant = (v && v[0] >= '1' && v[0] <= '4') ? v[0] - '0' : 3;
+  }
+  if (variant == 1)
+    return vp8g_launch_encode_w1(yuv, yfb, w, h, n, segmap, params, tokens, tok_cap, mbinfo,
+                                 results, stream);
+  K3Args a;
+  a.yuv = yuv; a.yfb = yfb; a.w = w; a.h = h;
+  a.mbw = (w + 15) >> 4; a.mbh = (h + 15) >> 4;
+  a.segmap = segmap; a.params = params; a.tokens = tokens; a.tok_cap = tok_cap;
+  a.mbinfo = mbinfo; a.mbcnt = mbcnt; a.results = results;
+  if (variant == 2) return launch_k3<1>(a, n, trellis != 0, stream);
+  if (variant == 4) return launch_k3<4>(a, n, trellis != 0, stream);
+  return launch_k3<2>(a, n, trellis != 0, stream);
 }

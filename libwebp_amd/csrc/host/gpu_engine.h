@@ -30,6 +30,7 @@ struct WebPGpuBatch {
   vp8g_frame_params* d_params;
   uint16_t* d_tokens;
   uint8_t* d_mbinfo;
+  uint16_t* d_mbcnt;         /* K3 scratch: tokens per MB */
   vp8g_frame_result* d_results;
   uint32_t* d_psize;         /* partition-1 bytes per frame (K4) */
   vp8g_emit_meta* d_emeta;   /* K4 per-frame bookkeeping */

@@ -80,10 +80,14 @@ int vp8g_launch_import(const uint8_t* rgba, size_t frame_stride, int row_stride,
 int vp8g_launch_analysis(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h,
                          int n, uint8_t* mb_alpha, uint16_t* mb_uva, void* stream);
 
+/* K3: RD search + tokens. Each frame's tokens end up as one compact stream
+ * at the start of its tok_cap region (per-MB slots of
+ * VP8G_MAX_TOKENS_PER_MB are used as scratch); mbcnt is scratch of n * nmb
+ * uint16. trellis != 0 reserves the trellis LDS (method >= 5). */
 int vp8g_launch_encode(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h,
                        int n, const uint8_t* segmap,
                        const vp8g_frame_params* params, uint16_t* tokens,
-                       size_t tok_cap, uint8_t* mbinfo,
+                       size_t tok_cap, uint8_t* mbinfo, uint16_t* mbcnt, int trellis,
                        vp8g_frame_result* results, void* stream);
 
 /* K4: boolean coder for the token partition, parallel inside each frame

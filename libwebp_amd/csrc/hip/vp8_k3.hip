@@ -1030,7 +1030,9 @@ struct K3Args {
   vp8g_frame_result* results;
 };
 
-template <int NW>
+// TR: the method >= 5 instantiation carries the trellis paths; m3/m4 frames
+// run a kernel without them (smaller register footprint).
+template <int NW, bool TR>
 __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   extern __shared__ __align__(16) uint8_t smem[];
   const int mbw = a.mbw, mbh = a.mbh, nmb = mbw * mbh;
@@ -1101,7 +1103,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   const int max_i4_bits = P->max_i4_header_bits;
   const int use_derr = P->use_derr;
   const int max_count = P->max_count;
-  const bool trellis_all = rd_opt >= 3;
+  const bool trellis_all = TR && rd_opt >= 3;
   uint64_t* substamps = nullptr;
   uint8_t* yl = L.yl_mem + 1;
   uint8_t* ul = L.ul_mem + 1;
@@ -1178,8 +1180,12 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
       wbar(L);
 
       // ---- Intra16 (quant_enc.c:1002-1058)
-      if (trellis_all) eval_i16<true>(G, L, tn, S, ctx, tid);
-      else eval_i16<false>(G, L, tn, S, ctx, tid);
+      if constexpr (TR) {
+        if (trellis_all) eval_i16<true>(G, L, tn, S, ctx, tid);
+        else eval_i16<false>(G, L, tn, S, ctx, tid);
+      } else {
+        eval_i16<false>(G, L, tn, S, ctx, tid);
+      }
       int best16 = 0;
       uint32_t nz16 = 0;
       score_t D16 = 0, SD16 = 0, H16 = 0, R16 = 0;
@@ -1223,10 +1229,16 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
 
       // ---- Intra4 (quant_enc.c:1072-1165)
       if (max_i4_bits > 0) {
-        I4Result r4 = trellis_all ? run_i4<true>(G, L, tn, S, ctx, tid, x, mbw, predtop, yl, yt, true,
-                                                 rd_score, max_i4_bits, substamps)
-                                  : run_i4<false>(G, L, tn, S, ctx, tid, x, mbw, predtop, yl, yt,
-                                                  true, rd_score, max_i4_bits, substamps);
+        I4Result r4;
+        if constexpr (TR) {
+          r4 = trellis_all ? run_i4<true>(G, L, tn, S, ctx, tid, x, mbw, predtop, yl, yt, true,
+                                          rd_score, max_i4_bits, substamps)
+                           : run_i4<false>(G, L, tn, S, ctx, tid, x, mbw, predtop, yl, yt, true,
+                                           rd_score, max_i4_bits, substamps);
+        } else {
+          r4 = run_i4<false>(G, L, tn, S, ctx, tid, x, mbw, predtop, yl, yt, true, rd_score,
+                             max_i4_bits, substamps);
+        }
         if (r4.ok) {
           is_i16 = 0;
           rdH = r4.H;
@@ -1274,9 +1286,10 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
 
       // ---- m5: final re-quantisation of the chosen modes with trellis
       // (SimpleQuantize, quant_enc.c:1222-1245; RD_OPT_TRELLIS, :1384-1387)
-      if (rd_opt == 2) {
+      if (TR && rd_opt == 2) {
         uint32_t nzq = 0;
-        if (is_i16) {
+        if constexpr (!TR) {
+        } else if (is_i16) {
           eval_i16<true>(G, L, tn, S, ctx, tid);
           L.yout[(tid >> 4) * BPS + (tid & 15)] = L.rec16[best16][tid];
           (&L.fin_ac[0][0])[tid] = (&L.lv16[best16][0][0])[tid];
@@ -1503,8 +1516,8 @@ extern "C" int vp8g_launch_encode_w1(const uint8_t* yuv, size_t yfb, int w, int 
                                      vp8g_frame_result* results, void* stream);
 extern "C" int vp8g_launch_check(const char* what);
 
-template <int NW>
-static int launch_k3(const K3Args& a, int n, bool trellis, void* stream) {
+template <int NW, bool TR>
+static int launch_k3_t(const K3Args& a, int n, bool trellis, void* stream) {
   const size_t lds = k3_lds_bytes<NW>(a.mbw, a.mbh, trellis);
   if (lds > 160 * 1024) {
     vp8g_set_error("k_encode", "frame too wide for the LDS budget");
@@ -1514,7 +1527,7 @@ static int launch_k3(const K3Args& a, int n, bool trellis, void* stream) {
     static size_t attr_bytes = 0;
     if (lds > attr_bytes) {
       const hipError_t e = hipFuncSetAttribute(
-          (const void*)k_encode<NW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+          (const void*)k_encode<NW, TR>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) {
         vp8g_set_error("k_encode dynamic LDS opt-in", hipGetErrorString(e));
         return 0;
@@ -1522,8 +1535,21 @@ static int launch_k3(const K3Args& a, int n, bool trellis, void* stream) {
       attr_bytes = lds;
     }
   }
-  hipLaunchKernelGGL(k_encode<NW>, dim3(n), dim3(NW * K3T), lds, (hipStream_t)stream, a);
+  hipLaunchKernelGGL((k_encode<NW, TR>), dim3(n), dim3(NW * K3T), lds, (hipStream_t)stream, a);
   return vp8g_launch_check("k_encode");
+}
+
+template <int NW>
+static int launch_k3(const K3Args& a, int n, bool trellis, void* stream) {
+  return trellis ? launch_k3_t<NW, true>(a, n, true, stream)
+                 : launch_k3_t<NW, false>(a, n, false, stream);
+}
+
+// default: 4 MB workers for m3/m4 frames, 2 when the trellis paths (and
+// their registers and LDS) are in the kernel
+static int launch_k3_default(const K3Args& a, int n, bool trellis, void* stream) {
+  return trellis ? launch_k3_t<2, true>(a, n, true, stream)
+                 : launch_k3_t<4, false>(a, n, false, stream);
 }
 
 extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, int n,
@@ -1532,10 +1558,10 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
                                   uint16_t* mbcnt, int trellis, vp8g_frame_result* results,
                                   void* stream) {
   static int variant = -1;
-  if (variant < 0) {   // WEBP_AMD_K3: 1 = single-wavefront reference kernel, 2 = one worker,
-                       // default: two workers per frame
+  if (variant < 0) {   // WEBP_AMD_K3: 1 = single-wavefront reference kernel, 2/3/4 = 1/2/4
+                       // MB workers per frame, unset = 4 (m3/m4) or 2 (trellis)
     const char* v = getenv("WEBP_AMD_K3");
-    variant = (v && v[0] >= '1' && v[0] <= '4') ? v[0] - '0' : 3;
+    variant = (v && v[0] >= '1' && v[0] <= '4') ? v[0] - '0' : 0;
   }
   if (variant == 1)
     return vp8g_launch_encode_w1(yuv, yfb, w, h, n, segmap, params, tokens, tok_cap, mbinfo,
@@ -1547,5 +1573,6 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   a.mbinfo = mbinfo; a.mbcnt = mbcnt; a.results = results;
   if (variant == 2) return launch_k3<1>(a, n, trellis != 0, stream);
   if (variant == 4) return launch_k3<4>(a, n, trellis != 0, stream);
-  return launch_k3<2>(a, n, trellis != 0, stream);
+  if (variant == 3) return launch_k3<2>(a, n, trellis != 0, stream);
+  return launch_k3_default(a, n, trellis != 0, stream);
 }

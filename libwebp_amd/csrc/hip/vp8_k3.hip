@@ -136,6 +136,11 @@ __device__ __forceinline__ int dpp(int v) {
 #define DPP_QB(k) ((k) | ((k) << 2) | ((k) << 4) | ((k) << 6))
 #define DPP_ROR(n) (0x120 + (n))   // lane i reads lane (i - n) mod 16
 
+// MUL of ITransformOne with a 24-bit multiply: |a| < 2^23 and the constants
+// are 17-bit, and v_mul_i32_i24 returns the low 32 bits of the product, as
+// the reference's int arithmetic does
+#define IMUL24(a, b) (__mul24((a), (b)) >> 16)
+
 // the 4 values of this lane's 4-lane row, in x order
 __device__ __forceinline__ void row4(int v, int& r0, int& r1, int& r2, int& r3) {
   r0 = dpp<DPP_QB(0)>(v);
@@ -224,10 +229,12 @@ __device__ __forceinline__ TLane make_tlane(int j) {
 __device__ __forceinline__ int fdct_lane(int d, const TLane& T) {
   int d0, d1, d2, d3;
   row4(d, d0, d1, d2, d3);
-  const int t = (T.fr[0] * d0 + T.fr[1] * d1 + T.fr[2] * d2 + T.fr[3] * d3 + T.frr) >> 9;
+  const int t = (__mul24(T.fr[0], d0) + __mul24(T.fr[1], d1) + __mul24(T.fr[2], d2) +
+                 __mul24(T.fr[3], d3) + T.frr) >> 9;
   int u0, u1, u2, u3;
   colrot(t, u0, u1, u2, u3);
-  const int o = ((T.fc[0] * u0 + T.fc[1] * u1 + T.fc[2] * u2 + T.fc[3] * u3 + T.fcr) >> 16) +
+  const int o = ((__mul24(T.fc[0], u0) + __mul24(T.fc[1], u1) + __mul24(T.fc[2], u2) +
+                  __mul24(T.fc[3], u3) + T.fcr) >> 16) +
                 (T.fy1 & (u1 != u2));   // row 1: + (a3 != 0), a3 = t0 - t3 = u1 - u2
   return (int16_t)o;
 }
@@ -237,12 +244,14 @@ __device__ __forceinline__ int fdct_lane(int d, const TLane& T) {
 __device__ __forceinline__ int idct_lane(int c, int pr, const TLane& T) {
   int u0, u1, u2, u3;
   colrot(c, u0, u1, u2, u3);
-  const int t = T.ia[0] * u0 + T.ib[0] * IMUL(u0, T.ig[0]) + T.ia[1] * u1 +
-                T.ib[1] * IMUL(u1, T.ig[1]) + T.ia[2] * u2 + T.ib[2] * IMUL(u2, T.ig[2]) +
-                T.ia[3] * u3 + T.ib[3] * IMUL(u3, T.ig[3]);   // tmp[4x + y]
+  const int t = __mul24(T.ia[0], u0) + __mul24(T.ib[0], IMUL24(u0, T.ig[0])) +
+                __mul24(T.ia[1], u1) + __mul24(T.ib[1], IMUL24(u1, T.ig[1])) +
+                __mul24(T.ia[2], u2) + __mul24(T.ib[2], IMUL24(u2, T.ig[2])) +
+                __mul24(T.ia[3], u3) + __mul24(T.ib[3], IMUL24(u3, T.ig[3]));   // tmp[4x + y]
   int t0, t1, t2, t3;
   row4(t, t0, t1, t2, t3);
-  const int v = t0 + 4 + T.is2 * t2 + T.is1 * IMUL(t1, T.ig1) + T.is3 * IMUL(t3, T.ig3);
+  const int v = t0 + 4 + __mul24(T.is2, t2) + __mul24(T.is1, IMUL24(t1, T.ig1)) +
+                __mul24(T.is3, IMUL24(t3, T.ig3));
   return clip8(pr + (v >> 3));
 }
 
@@ -251,11 +260,13 @@ __device__ __forceinline__ int idct_lane(int c, int pr, const TLane& T) {
 __device__ __forceinline__ int ttrans_lane(int p, const TLane& T, int wj) {
   int i0, i1, i2, i3;
   row4(p, i0, i1, i2, i3);
-  const int t = T.hr[0] * i0 + T.hr[1] * i1 + T.hr[2] * i2 + T.hr[3] * i3;
+  const int t = __mul24(T.hr[0], i0) + __mul24(T.hr[1], i1) + __mul24(T.hr[2], i2) +
+                __mul24(T.hr[3], i3);
   int u0, u1, u2, u3;
   colrot(t, u0, u1, u2, u3);
-  const int o = T.hc[0] * u0 + T.hc[1] * u1 + T.hc[2] * u2 + T.hc[3] * u3;
-  return wj * iabs_(o);
+  const int o = __mul24(T.hc[0], u0) + __mul24(T.hc[1], u1) + __mul24(T.hc[2], u2) +
+                __mul24(T.hc[3], u3);
+  return __mul24(wj, iabs_(o));
 }
 
 __device__ __forceinline__ int sum16(int v) {
@@ -283,10 +294,10 @@ __device__ __forceinline__ int sum64(int v) {
 __device__ __forceinline__ int quant_lane(int cv, int j, const vp8g_mtx& M, int& dq) {
   const int neg = cv < 0;
   const uint32_t coeff = (uint32_t)(neg ? -cv : cv) + M.sharpen[j];
-  int level = min((int)((coeff * M.iq[j] + M.bias[j]) >> QFIX), MAX_LEVEL);
+  int level = min((int)((__umul24(coeff, M.iq[j]) + M.bias[j]) >> QFIX), MAX_LEVEL);
   level = coeff > M.zthresh[j] ? level : 0;
   level = neg ? -level : level;
-  dq = (int16_t)(level * (int)M.q[j]);
+  dq = (int16_t)__mul24(level, (int)M.q[j]);
   return level;
 }
 
@@ -706,10 +717,10 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
     } else {   // QuantizeBlock_C (src/dsp/enc.c:653-677)
       const int neg = c < 0;
       const uint32_t coeff = (uint32_t)(neg ? -c : c) + q_sh;
-      level = min((int)((coeff * q_iq + q_bias) >> QFIX), MAX_LEVEL);
+      level = min((int)((__umul24(coeff, q_iq) + q_bias) >> QFIX), MAX_LEVEL);
       level = coeff > q_zt ? level : 0;
       level = neg ? -level : level;
-      dq = (int16_t)(level * q_q);
+      dq = (int16_t)__mul24(level, q_q);
     }
     SUBST(2);
     const int rec = idct_lane(dq, pr, T);
@@ -1052,7 +1063,11 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   const int f = blockIdx.x;
   const int gt = threadIdx.x;
   const int lane = tid & 63;
-  const bool w0 = tid < 64;
+  // thread id rotated by one wave per worker: stages that leave a wave idle
+  // (intra4's 160 lanes, the token tail, wave-0 bookkeeping) put the idle wave
+  // on a different SIMD for each worker
+  const int rtid = (tid + 64 * (wk & 3)) & (K3T - 1);
+  const bool w0 = rtid < 64;
   const int w = a.w, h = a.h;
   const int uvw = (w + 1) >> 1, uvh = (h + 1) >> 1;
   const uint8_t* Yp = a.yuv + f * a.yfb;
@@ -1231,12 +1246,12 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
       if (max_i4_bits > 0) {
         I4Result r4;
         if constexpr (TR) {
-          r4 = trellis_all ? run_i4<true>(G, L, tn, S, ctx, tid, x, mbw, predtop, yl, yt, true,
+          r4 = trellis_all ? run_i4<true>(G, L, tn, S, ctx, rtid, x, mbw, predtop, yl, yt, true,
                                           rd_score, max_i4_bits, substamps)
-                           : run_i4<false>(G, L, tn, S, ctx, tid, x, mbw, predtop, yl, yt, true,
+                           : run_i4<false>(G, L, tn, S, ctx, rtid, x, mbw, predtop, yl, yt, true,
                                            rd_score, max_i4_bits, substamps);
         } else {
-          r4 = run_i4<false>(G, L, tn, S, ctx, tid, x, mbw, predtop, yl, yt, true, rd_score,
+          r4 = run_i4<false>(G, L, tn, S, ctx, rtid, x, mbw, predtop, yl, yt, true, rd_score,
                              max_i4_bits, substamps);
         }
         if (r4.ok) {
@@ -1296,7 +1311,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
           if (tid < 16) L.fin_dc[tid] = L.lvdc[best16][tid];
           nzq = (uint32_t)L.mres[best16][3];
         } else {
-          I4Result r4 = run_i4<true>(G, L, tn, S, ctx, tid, x, mbw, predtop, yl, yt, false, 0, 0,
+          I4Result r4 = run_i4<true>(G, L, tn, S, ctx, rtid, x, mbw, predtop, yl, yt, false, 0, 0,
                                      substamps);
           L.yout[(tid >> 4) * BPS + (tid & 15)] = L.acc_out[tid];
           (&L.fin_ac[0][0])[tid] = (&L.acc_ac[0][0])[tid];
@@ -1349,8 +1364,8 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
       uint64_t nzb = 0;
       int lvi[2], lvp[2];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {   // items tid and tid + 256 = block*16 + pos
-        const int item = tid + K3T * q, k = item >> 4, n = item & 15;
+      for (int q = 0; q < 2; ++q) {   // items rtid and rtid + 256 = block*16 + pos
+        const int item = rtid + K3T * q, k = item >> 4, n = item & 15;
         int v = 0, vp = 0;
         if (k < 25 && k >= first_blk) {
           const int16_t* lvb = blk_levels(L, k);
@@ -1394,7 +1409,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
         int cnt[2], bi[2], last[2];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          const int item = tid + K3T * q, k = item >> 4, n = item & 15;
+          const int item = rtid + K3T * q, k = item >> 4, n = item & 15;
           bi[q] = k < 25 ? L.blkinfo[k] : -1;
           last[q] = k < 25 ? L.blast[k] : -1;
           cnt[q] = bi[q] < 0 ? 0
@@ -1407,7 +1422,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
           const int v0 = __shfl_up(inc0, off), v1 = __shfl_up(inc1, off);
           if (lane >= off) { inc0 += v0; inc1 += v1; }
         }
-        const int wv = tid >> 6;
+        const int wv = rtid >> 6;
         if (lane == 63) { L.wsum[0][wv] = inc0; L.wsum[1][wv] = inc1; }
         wbar(L);
         int pre0 = 0, pre1 = 0, tot0 = 0, tot1 = 0;
@@ -1421,15 +1436,15 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
         const int off0 = pre0 + inc0 - cnt[0];
         const int off1 = tot0 + pre1 + inc1 - cnt[1];
         if (cnt[0])
-          pos_tokens<true>(bi[0] & 15, (bi[0] >> 4) & 15, bi[0] >> 8, tid & 15, lvi[0], lvp[0],
+          pos_tokens<true>(bi[0] & 15, (bi[0] >> 4) & 15, bi[0] >> 8, rtid & 15, lvi[0], lvp[0],
                            last[0], slot + off0);
         if (cnt[1])
-          pos_tokens<true>(bi[1] & 15, (bi[1] >> 4) & 15, bi[1] >> 8, tid & 15, lvi[1], lvp[1],
+          pos_tokens<true>(bi[1] & 15, (bi[1] >> 4) & 15, bi[1] >> 8, rtid & 15, lvi[1], lvp[1],
                            last[1], slot + off1);
-        if (tid == 0) mbcnt[mb] = (uint16_t)(tot0 + tot1);
+        if (rtid == 0) mbcnt[mb] = (uint16_t)(tot0 + tot1);
       }
       // update nz context (iterator_enc.c:267-283) and the left DC flag
-      if (tid == 0) {
+      if (rtid == 0) {
         int tn9[9], ln[9];
 #pragma unroll
         for (int i = 0; i < 9; ++i) { tn9[i] = ctx.top(i); ln[i] = ctx.left(i); }

@@ -365,3 +365,30 @@ extern "C" int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
                      (const vp8g_emit_meta*)meta, (const uint32_t*)nbuf);
   return vp8g_launch_check("k_emit_bytes");
 }
+
+// Gather every frame's partition-1 bytes (at the head of its token slab) into
+// one packed buffer at 16-byte aligned offsets, so the host pulls the whole
+// batch back with a single DMA instead of one copy per frame.
+__global__ __launch_bounds__(256) void k_pack(const uint8_t* __restrict__ src, size_t pitch,
+                                              const uint64_t* __restrict__ off,
+                                              const uint32_t* __restrict__ size,
+                                              uint8_t* __restrict__ dst) {
+  const int f = blockIdx.y;
+  const uint32_t n16 = (size[f] + 15) >> 4;
+  const uint4* s4 = reinterpret_cast<const uint4*>(src + (size_t)f * pitch);
+  uint4* d4 = reinterpret_cast<uint4*>(dst + off[f]);
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) d4[i] = s4[i];
+}
+
+extern "C" int vp8g_launch_pack(const uint16_t* tokens, size_t tok_cap, int n,
+                                const uint64_t* off, const uint32_t* size, uint32_t max_size,
+                                uint8_t* dst, void* stream) {
+  if (n <= 0 || max_size == 0) return 1;
+  if ((tok_cap * sizeof(uint16_t)) & 15) return 0;
+  uint32_t gx = (max_size + 16 * 256 - 1) / (16 * 256);
+  if (gx > 64) gx = 64;
+  hipLaunchKernelGGL(k_pack, dim3(gx, n), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const uint8_t*>(tokens), tok_cap * sizeof(uint16_t), off,
+                     size, dst);
+  return vp8g_launch_check("k_pack");
+}

@@ -127,15 +127,17 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   CHK(hipHostMalloc((void**)&b->h_mbinfo, N * nmb * VP8G_MBINFO_BYTES, 0));
   CHK(hipHostMalloc((void**)&b->h_results, N * sizeof(vp8g_frame_result), 0));
   CHK(hipHostMalloc((void**)&b->h_psize, N * sizeof(uint32_t), 0));
+  CHK(hipHostMalloc((void**)&b->h_poff, (N + 1) * sizeof(uint64_t), 0));
+  CHK(hipMalloc((void**)&b->d_poff, (N + 1) * sizeof(uint64_t)));
   CHK(hipHostMalloc((void**)&b->h_emeta, N * sizeof(vp8g_emit_meta), 0));
   b->frames = (vp8h_frame*)calloc(N, sizeof(vp8h_frame));
   b->tok_off = (size_t*)calloc(N + 1, sizeof(size_t));
-  b->part_off = (size_t*)calloc(N + 1, sizeof(size_t));
+  b->p0 = (vp8h_bw*)calloc(N, sizeof(vp8h_bw));
   b->out = (uint8_t**)calloc(N, sizeof(uint8_t*));
   b->out_size = (size_t*)calloc(N, sizeof(size_t));
   b->err = (int*)calloc(N, sizeof(int));
   b->hdr = (int*)calloc(2 * N, sizeof(int));
-  if (!b->frames || !b->tok_off || !b->part_off || !b->out || !b->out_size || !b->err || !b->hdr) goto fail;
+  if (!b->frames || !b->tok_off || !b->p0 || !b->out || !b->out_size || !b->err || !b->hdr) goto fail;
   return b;
 fail:
   WebPGpuBatchDelete(b);
@@ -149,36 +151,45 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipFree(b->d_g2l); hipFree(b->d_rgba); hipFree(b->d_yuv); hipFree(b->d_aflags); hipFree(b->d_alpha);
   hipFree(b->d_uva); hipFree(b->d_segmap); hipFree(b->d_params); hipFree(b->d_tokens);
   hipFree(b->d_mbinfo); hipFree(b->d_mbcnt); hipFree(b->d_results); hipFree(b->d_psize); hipFree(b->d_emeta);
+  hipFree(b->d_poff); hipFree(b->d_part);
   hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs); hipFree(b->d_nbuf);
   hipFree(b->d_eimg);
   hipHostFree(b->h_aflags); hipHostFree(b->h_alpha); hipHostFree(b->h_uva);
   hipHostFree(b->h_segmap); hipHostFree(b->h_params); hipHostFree(b->h_mbinfo);
   hipHostFree(b->h_results); hipHostFree(b->h_tokens); hipHostFree(b->h_psize);
-  hipHostFree(b->h_part); hipHostFree(b->h_emeta);
+  hipHostFree(b->h_part); hipHostFree(b->h_emeta); hipHostFree(b->h_poff);
   for (int i = 0; i < 6; ++i)
     if (b->ev[i]) hipEventDestroy(b->ev[i]);
   if (b->stream) hipStreamDestroy(b->stream);
   if (b->out)
     for (int i = 0; i < b->max_frames; ++i) free(b->out[i]);
   free(b->out); free(b->out_size); free(b->err); free(b->hdr);
-  free(b->frames); free(b->tok_off); free(b->part_off);
+  if (b->p0)
+    for (int i = 0; i < b->max_frames; ++i) vp8h_bw_free(&b->p0[i]);
+  free(b->frames); free(b->tok_off); free(b->p0);
   free(b);
 }
 
 /* ---- host thread pool for the per-frame tail ---- */
 
+#define TAIL_MAX_THREADS 64
+
 typedef struct {
   WebPGpuBatch* b;
-  int n;
+  int n, phase;   /* phase 0: partition 0; phase 1: partition 1 + RIFF write */
   atomic_int next;
+  pthread_t th[TAIL_MAX_THREADS];
+  int started;
 } TailJob;
 
-static void frame_tail(WebPGpuBatch* b, int f) {
+/* Partition 0 of frame f: needs only K3's results and modes. */
+static void frame_head(WebPGpuBatch* b, int f) {
   vp8h_frame* fr = &b->frames[f];
   const vp8g_frame_result* res = &b->h_results[f];
   free(b->out[f]);
   b->out[f] = NULL;
   b->out_size[f] = 0;
+  vp8h_bw_free(&b->p0[f]);
   if (b->err[f] != VP8_ENC_OK) return;
   if (res->error) { b->err[f] = VP8_ENC_ERROR_OUT_OF_MEMORY; return; }
   /* partition-0 overflow retry (frame_enc.c:869-876) is not implemented on
@@ -188,6 +199,15 @@ static void frame_tail(WebPGpuBatch* b, int f) {
     b->err[f] = VP8_ENC_ERROR_PARTITION0_OVERFLOW;
     return;
   }
+  b->err[f] = vp8h_build_p0(fr, res, b->h_mbinfo + (size_t)f * b->nmb * VP8G_MBINFO_BYTES,
+                            &b->p0[f], b->hdr + 2 * f);
+}
+
+/* Join partition 0 with partition 1 (K4's bytes, or coded here under
+ * WEBP_AMD_HOST_EMIT=1) into the RIFF/WEBP file. */
+static void frame_finish(WebPGpuBatch* b, int f) {
+  const vp8g_frame_result* res = &b->h_results[f];
+  if (b->err[f] != VP8_ENC_OK) { vp8h_bw_free(&b->p0[f]); return; }
   vp8h_bw part1;
   if (b->host_emit) {   /* boolean-code the tokens here (token_enc.c:200-223) */
     vp8h_bw_init(&part1, (size_t)res->ntokens / 8 + 4096);
@@ -195,12 +215,11 @@ static void frame_tail(WebPGpuBatch* b, int f) {
     vp8h_bw_finish(&part1);
   } else {              /* partition 1 already coded by K4 */
     memset(&part1, 0, sizeof(part1));
-    part1.buf = b->h_part + b->part_off[f];
+    part1.buf = b->h_part + b->h_poff[f];
     part1.pos = b->h_psize[f];
   }
   int err = VP8_ENC_OK;
-  b->out_size[f] = vp8h_assemble(fr, res, b->h_mbinfo + (size_t)f * b->nmb * VP8G_MBINFO_BYTES,
-                                 &part1, &b->out[f], &err, b->hdr + 2 * f);
+  b->out_size[f] = vp8h_write_riff(&b->frames[f], &b->p0[f], &part1, &b->out[f], &err);
   b->err[f] = err;
   if (b->host_emit) vp8h_bw_free(&part1);
 }
@@ -210,24 +229,32 @@ static void* tail_worker(void* arg) {
   for (;;) {
     const int f = atomic_fetch_add(&j->next, 1);
     if (f >= j->n) break;
-    frame_tail(j->b, f);
+    if (j->phase == 0) frame_head(j->b, f);
+    else frame_finish(j->b, f);
   }
   return NULL;
 }
 
-static void run_tails(WebPGpuBatch* b, int n) {
+/* start up to `extra` helper threads on the job; the caller joins in later */
+static void tail_spawn(TailJob* j, WebPGpuBatch* b, int n, int phase, int extra) {
+  j->b = b; j->n = n; j->phase = phase; j->started = 0;
+  atomic_init(&j->next, 0);
+  if (extra > n) extra = n;
+  if (extra > TAIL_MAX_THREADS) extra = TAIL_MAX_THREADS;
+  for (int i = 0; i < extra; ++i)
+    if (pthread_create(&j->th[j->started], NULL, tail_worker, j) == 0) ++j->started;
+}
+
+static void tail_join(TailJob* j) {
+  tail_worker(j);   /* the caller takes frames too until none are left */
+  for (int i = 0; i < j->started; ++i) pthread_join(j->th[i], NULL);
+  j->started = 0;
+}
+
+static void run_tails(WebPGpuBatch* b, int n, int phase) {
   TailJob job;
-  job.b = b; job.n = n;
-  atomic_init(&job.next, 0);
-  int nt = b->threads < n ? b->threads : n;
-  if (nt <= 1) { tail_worker(&job); return; }
-  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nt);
-  int started = 0;
-  for (int i = 1; i < nt; ++i)
-    if (pthread_create(&th[started], NULL, tail_worker, &job) == 0) ++started;
-  tail_worker(&job);
-  for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
-  free(th);
+  tail_spawn(&job, b, n, phase, b->threads - 1);
+  tail_join(&job);
 }
 
 /* ---- pipeline ---- */
@@ -236,6 +263,8 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   const size_t nmb = (size_t)b->nmb;
   double t0 = now_us(), t1, t2, t3, t4;
   hipStream_t st = b->stream;
+  TailJob head;
+  int head_running = 0;
   if (!b->ev0_recorded) CHK(hipEventRecord(b->ev[0], st));
   b->ev0_recorded = 0;
   if (!vp8g_launch_analysis(b->d_yuv, b->yfb, b->w, b->h, n, b->d_alpha, b->d_uva, st)) return 0;
@@ -308,6 +337,9 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
       return 0;
     CHK(hipEventRecord(b->ev[4], st));
     CHK(hipMemcpyAsync(b->h_psize, b->d_psize, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    /* partition 0 on the host threads while K4 runs on the device */
+    tail_spawn(&head, b, n, 0, b->threads - 1);
+    head_running = 1;
     CHK(hipStreamSynchronize(st));
   }
   t3 = now_us();
@@ -328,9 +360,14 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
         CHK(hipMemcpyAsync(b->h_tokens + b->tok_off[f], b->d_tokens + (size_t)f * b->tok_cap,
                            b->h_results[f].ntokens * sizeof(uint16_t), hipMemcpyDeviceToHost, st));
   } else {
-    b->part_off[0] = 0;
-    for (int f = 0; f < n; ++f) b->part_off[f + 1] = b->part_off[f] + b->h_psize[f];
-    const size_t total = b->part_off[n];
+    /* one packed D2H of every frame's partition 1 (k_pack) */
+    uint32_t max_size = 0;
+    b->h_poff[0] = 0;
+    for (int f = 0; f < n; ++f) {
+      b->h_poff[f + 1] = b->h_poff[f] + ((b->h_psize[f] + 15u) & ~15u);
+      if (b->h_psize[f] > max_size) max_size = b->h_psize[f];
+    }
+    const size_t total = b->h_poff[n];
     if (total > b->h_part_cap) {
       hipHostFree(b->h_part);
       b->h_part = NULL;
@@ -339,14 +376,32 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
       CHK(hipHostMalloc((void**)&b->h_part, cap, 0));
       b->h_part_cap = cap;
     }
-    for (int f = 0; f < n; ++f)
-      if (b->h_psize[f])
-        CHK(hipMemcpyAsync(b->h_part + b->part_off[f], b->d_tokens + (size_t)f * b->tok_cap,
-                           b->h_psize[f], hipMemcpyDeviceToHost, st));
+    if (total > b->d_part_cap) {
+      hipFree(b->d_part);
+      b->d_part = NULL;
+      b->d_part_cap = 0;
+      const size_t cap = total + total / 4 + 4096;
+      CHK(hipMalloc((void**)&b->d_part, cap));
+      b->d_part_cap = cap;
+    }
+    if (total) {
+      CHK(hipMemcpyAsync(b->d_poff, b->h_poff, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
+                         st));
+      if (!vp8g_launch_pack(b->d_tokens, b->tok_cap, n, b->d_poff, b->d_psize, max_size, b->d_part,
+                            st))
+        goto fail;
+      CHK(hipMemcpyAsync(b->h_part, b->d_part, total, hipMemcpyDeviceToHost, st));
+    }
   }
   CHK(hipStreamSynchronize(st));
   t4 = now_us();
-  run_tails(b, n);
+  if (head_running) {
+    tail_join(&head);
+    head_running = 0;
+  } else {
+    run_tails(b, n, 0);
+  }
+  run_tails(b, n, 1);
   const double t5 = now_us();
   float k3_ms = 0.f, k12_ms = 0.f, k4_ms = 0.f;
   CHK(hipEventElapsedTime(&k3_ms, b->ev[2], b->ev[3]));
@@ -363,6 +418,7 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   b->last_n = n;
   return 1;
 fail:
+  if (head_running) tail_join(&head);
   return 0;
 }
 

@@ -52,7 +52,11 @@ struct WebPGpuBatch {
   uint32_t* h_psize;
   uint8_t* h_part;           /* pinned partition-1 bytes of all frames */
   size_t h_part_cap;
-  size_t* part_off;
+  uint64_t* h_poff;          /* pinned: 16-byte aligned offset of each frame in h_part */
+  uint64_t* d_poff;
+  uint8_t* d_part;           /* packed partition-1 bytes (k_pack), grown on demand */
+  size_t d_part_cap;
+  vp8h_bw* p0;               /* partition 0 of each frame, coded while K4 runs */
   uint16_t* h_tokens;
   size_t* tok_off;
   vp8h_frame* frames;

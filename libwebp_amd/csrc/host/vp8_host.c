@@ -455,8 +455,8 @@ static void put_le32(uint8_t* p, uint32_t v) {
   p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
 }
 
-size_t vp8h_assemble(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* mbinfo,
-                     vp8h_bw* part1, uint8_t** out, int* err, int* hdr_bytes) {
+int vp8h_build_p0(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* mbinfo,
+                  vp8h_bw* out0, int* hdr_bytes) {
   /* VP8AdjustFilterStrength without autofilter */
   if (fr->filter_strength > 0) {
     int max_level = 0;
@@ -470,6 +470,7 @@ size_t vp8h_assemble(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t
   }
   vp8h_bw bw;
   vp8h_bw_init(&bw, (size_t)fr->mbw * fr->mbh * 7 / 8 + 1024);
+  *out0 = bw;   /* handed back even on error so the caller can free it */
   bw_put_uniform(&bw, 0);   /* colorspace */
   bw_put_uniform(&bw, 0);   /* clamping type */
   if (bw_put_uniform(&bw, fr->num_segments > 1)) {
@@ -504,18 +505,23 @@ size_t vp8h_assemble(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t
   const size_t hdr_pos = bw.pos;
   code_intra_modes(&bw, fr, mbinfo);
   vp8h_bw_finish(&bw);
+  *out0 = bw;
   if (hdr_bytes) { hdr_bytes[0] = (int)hdr_pos; hdr_bytes[1] = (int)(bw.pos - hdr_pos); }
-  if (bw.error || part1->error) {
+  if (bw.error) return VP8_ENC_ERROR_OUT_OF_MEMORY;
+  if (bw.pos >= (1u << 19)) return VP8_ENC_ERROR_PARTITION0_OVERFLOW;
+  return VP8_ENC_OK;
+}
+
+size_t vp8h_write_riff(const vp8h_frame* fr, vp8h_bw* p0, const vp8h_bw* part1, uint8_t** out,
+                       int* err) {
+  vp8h_bw bw = *p0;
+  memset(p0, 0, sizeof(*p0));
+  if (part1->error) {
     vp8h_bw_free(&bw);
     *err = VP8_ENC_ERROR_OUT_OF_MEMORY;
     return 0;
   }
   const size_t size0 = bw.pos, size1 = part1->pos;
-  if (size0 >= (1u << 19)) {
-    vp8h_bw_free(&bw);
-    *err = VP8_ENC_ERROR_PARTITION0_OVERFLOW;
-    return 0;
-  }
   size_t vp8_size = 10 + size0 + size1;
   const size_t pad = vp8_size & 1;
   vp8_size += pad;
@@ -549,4 +555,15 @@ size_t vp8h_assemble(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t
   *out = o;
   *err = VP8_ENC_OK;
   return total;
+}
+
+size_t vp8h_assemble(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* mbinfo,
+                     vp8h_bw* part1, uint8_t** out, int* err, int* hdr_bytes) {
+  vp8h_bw p0;
+  *err = vp8h_build_p0(fr, res, mbinfo, &p0, hdr_bytes);
+  if (*err != VP8_ENC_OK) {
+    vp8h_bw_free(&p0);
+    return 0;
+  }
+  return vp8h_write_riff(fr, &p0, part1, out, err);
 }

@@ -63,6 +63,13 @@ void vp8h_emit_tokens(vp8h_bw* bw, const uint16_t* tokens, size_t n, const uint8
 /* Assemble the complete RIFF/WEBP/VP8 file (syntax_enc.c:269-389) into a
  * malloc'ed buffer. Applies VP8AdjustFilterStrength (filter_enc.c:194-233)
  * first. Returns the size, 0 on error (*err set). */
+/* The two halves of vp8h_assemble: partition 0 (frame header + intra modes,
+ * syntax_enc.c:183-245, tree_enc.c:378-411) needs only K3's outputs and can be
+ * coded while K4 codes partition 1; the RIFF write joins them. */
+int vp8h_build_p0(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* mbinfo,
+                  vp8h_bw* p0, int* hdr_bytes);
+size_t vp8h_write_riff(const vp8h_frame* fr, vp8h_bw* p0, const vp8h_bw* part1, uint8_t** out,
+                       int* err);
 size_t vp8h_assemble(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* mbinfo,
                      vp8h_bw* part1, uint8_t** out, int* err, int* hdr_bytes);
 

@@ -111,6 +111,11 @@ int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
                      uint8_t* img, vp8g_emit_seg* segs, uint32_t* nbuf, uint32_t* out_size,
                      void* stream);
 
+/* K4 tail: copy each frame's partition-1 bytes (size[f] bytes at the head of
+ * its token slab) to dst + off[f]; off[f] must be 16-byte aligned. */
+int vp8g_launch_pack(const uint16_t* tokens, size_t tok_cap, int n, const uint64_t* off,
+                     const uint32_t* size, uint32_t max_size, uint8_t* dst, void* stream);
+
 /* synthetic syn-v1 frames straight into device memory */
 int vp8g_launch_synth(uint8_t* rgba, size_t frame_stride, int w, int h,
                       int first_frame, int n, int seed, void* stream);

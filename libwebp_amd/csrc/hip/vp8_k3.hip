@@ -28,7 +28,6 @@
 // token statistics, quantiser/segment parameters and frame-level counters.
 struct K3G {
   uint32_t stats[NSLOT];
-  uint32_t delta[NSLOT];
   uint16_t lcost[96][MAX_VLEVEL + 1];  // [type*24 + band*3 + ctx][level], incl. fixed cost
   uint16_t ecost[256];
   uint16_t mcost4[1000];
@@ -94,6 +93,10 @@ struct K3S {
   uint8_t yl_mem[17], ul_mem[9], vl_mem[9];
   uint8_t predleft[4];
   int8_t lderr[2][2];
+  // statistics of this worker's tokens not folded yet (counted as they are
+  // written), and the token count of each MB of its current row
+  uint32_t rdelta[NSLOT];
+  uint16_t rowcnt[1024];           // mbw <= 1024 (width <= 16383)
 };
 
 // Barrier over the 4 wavefronts of one worker (s_barrier would stop the whole
@@ -793,10 +796,10 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
 // check (only at the first position and after a non-zero level), the zero
 // check and, for a non-zero level, its value tokens and sign. The context of
 // position n is the previous level. Returns the token count; EMIT writes the
-// tokens and adds their statistics deltas.
+// tokens and adds their statistics to the worker's pending deltas.
 template <bool EMIT>
 __device__ __forceinline__ int pos_tokens(int type, int first, int ctx0, int n, int c,
-                                          int cprev, int last, uint16_t* out) {
+                                          int cprev, int last, uint16_t* out, uint32_t* delta) {
   if (n < first) return 0;
   const int vprev = iabs_(cprev);
   if (n > first && vprev == 0 && n > last) return 0;
@@ -806,7 +809,7 @@ __device__ __forceinline__ int pos_tokens(int type, int first, int ctx0, int n, 
   auto dyn = [&](int bit, int pid, int sid) -> int {
     if (EMIT) {
       out[count] = (uint16_t)((bit << 15) | pid);
-      (void)sid;   // statistics are accumulated from the tokens at fold time
+      atomicAdd(&delta[sid], 0x10000u + (uint32_t)bit);   // folded in raster order later
     }
     ++count;
     return bit;
@@ -978,54 +981,109 @@ __device__ __forceinline__ void publish(int32_t* p, int32_t v) {
 // move from its slot to the compact stream while their statistics deltas
 // accumulate; counters that would cross the halving threshold inside the MB
 // are replayed token by token (VP8RecordStats, cost_enc.h:45-56).
-__device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint16_t* tok_base,
-                         const uint16_t* mbcnt) {
-  for (uint32_t i = i0; i < i1; ++i) {
-    const uint32_t n = mbcnt[i];
-    const uint16_t* src = tok_base + (size_t)i * VP8G_MAX_TOKENS_PER_MB;
-    uint16_t* dst = tok_base + G.ntok;
-    for (uint32_t c0 = 0; c0 < n; c0 += K3T) {
-      const bool v = c0 + tid < n;
-      const uint32_t t = v ? src[c0 + tid] : 0u;
-      wbar(L);   // the whole chunk is read before any of it is overwritten (dst <= src)
-      if (v) {
-        dst[c0 + tid] = (uint16_t)t;
-        if (!(t & 0x4000)) atomicAdd(&G.delta[tok_stat_slot(t)], 0x10000u + (t >> 15));
-      }
-    }
-    if (tid == 0) L.mark_any = 0;
-    wbar(L);
-    for (int s = tid; s < NSLOT; s += K3T) {
-      const uint32_t dlt = G.delta[s];
-      if (dlt) {
-        const uint32_t p = G.stats[s];
-        if ((p >> 16) + (dlt >> 16) < 0xffffu) {
-          G.stats[s] = p + dlt;
-        } else {
-          atomicOr(&G.mark[s >> 5], 1u << (s & 31));
-          L.mark_any = 1;
+__device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t row0,
+                         uint16_t* tok_base) {
+  // MBs [i0, i1) of this worker's row (first MB row0): append their tokens to
+  // the frame's compact stream, then add their statistics in one step.
+  // Called once every earlier MB is folded (G.fold_ptr == i0).
+  const uint32_t base = G.ntok;
+  const uint32_t wv = (uint32_t)tid >> 6, ln = (uint32_t)tid & 63;
+  uint32_t off = 0;
+  uint32_t total = 0;
+  for (uint32_t i = i0; i < i1; ++i) total += L.rowcnt[i - row0];
+  if ((uint64_t)base + total <= (uint64_t)i0 * VP8G_MAX_TOKENS_PER_MB) {
+    // the destination lies below every source slot of the range: the four
+    // waves copy whole MBs round-robin, loads of different MBs in flight
+    for (uint32_t i = i0; i < i1; ++i) {
+      const uint32_t n = L.rowcnt[i - row0];
+      if (((i - i0) & 3) == wv) {
+        const uint16_t* src = tok_base + (size_t)i * VP8G_MAX_TOKENS_PER_MB;
+        uint16_t* dst = tok_base + base + off;
+        uint32_t c = ln;
+        for (; c + 192 < n; c += 256) {
+          const uint16_t t0 = src[c], t1 = src[c + 64], t2 = src[c + 128], t3 = src[c + 192];
+          dst[c] = t0; dst[c + 64] = t1; dst[c + 128] = t2; dst[c + 192] = t3;
         }
-        G.delta[s] = 0;
+        for (; c < n; c += 64) dst[c] = src[c];
+      }
+      off += n;
+    }
+  } else {
+    // first rows of a dense frame: destination may overlap a later source;
+    // chunk by chunk, each chunk read before any of it is overwritten
+    for (uint32_t i = i0; i < i1; ++i) {
+      const uint32_t n = L.rowcnt[i - row0];
+      const uint16_t* src = tok_base + (size_t)i * VP8G_MAX_TOKENS_PER_MB;
+      uint16_t* dst = tok_base + base + off;
+      for (uint32_t c0 = 0; c0 < n; c0 += K3T) {
+        const bool v = c0 + tid < n;
+        const uint16_t t = v ? src[c0 + tid] : (uint16_t)0;
+        wbar(L);
+        if (v) dst[c0 + tid] = t;
+      }
+      off += n;
+    }
+  }
+  if (tid == 0) L.mark_any = 0;
+  wbar(L);
+  // statistics: one add per counter unless it would reach the halving point
+  // (VP8RecordStats, cost_enc.h:50-57), then an in-order replay of that counter
+  for (int s = tid; s < NSLOT; s += K3T) {
+    const uint32_t dlt = L.rdelta[s];
+    if (dlt) {
+      const uint32_t p = G.stats[s];
+      if ((p >> 16) + (dlt >> 16) < 0xffffu) {
+        G.stats[s] = p + dlt;
+      } else {
+        atomicOr(&G.mark[s >> 5], 1u << (s & 31));
+        L.mark_any = 1;
+      }
+      L.rdelta[s] = 0;
+    }
+  }
+  wbar(L);
+  if (L.mark_any) {
+    // exact in-order replay of the marked counters by wave 0: 64 tokens at a
+    // time; the tokens of one marked counter in a group are applied at once
+    // unless the group reaches the halving point, then one by one
+    if (tid < 64) {
+      const uint16_t* tk = tok_base + base;
+      uint32_t nxt = ln < total ? tk[ln] : 0x4000u;
+      for (uint32_t k0 = 0; k0 < total; k0 += 64) {
+        const uint32_t t = nxt;
+        nxt = (k0 + 64 + ln < total) ? tk[k0 + 64 + ln] : 0x4000u;
+        const int sl = (t & 0x4000) ? 0 : tok_stat_slot(t);
+        const bool pend = !(t & 0x4000) && ((G.mark[sl >> 5] >> (sl & 31)) & 1u);
+        uint64_t pm = __ballot(pend);
+        while (pm) {
+          const int ss = __builtin_amdgcn_readlane(sl, (int)__builtin_ctzll(pm));
+          const uint64_t mm = __ballot(pend && sl == ss);
+          const uint64_t ones = __ballot(pend && sl == ss && (t >> 15));
+          if (ln == 0) {
+            uint32_t p = G.stats[ss];
+            const uint32_t cnt = (uint32_t)__popcll(mm);
+            if ((p >> 16) + cnt < 0xffffu) {
+              p += (cnt << 16) + (uint32_t)__popcll(ones);
+            } else {
+              for (uint64_t b = mm; b; b &= b - 1) {
+                if (p >= 0xfffe0000u) p = ((p + 1u) >> 1) & 0x7fff7fffu;
+                p += 0x00010000u + (uint32_t)((ones >> __builtin_ctzll(b)) & 1u);
+              }
+            }
+            G.stats[ss] = p;
+          }
+          pm &= ~mm;
+        }
       }
     }
     wbar(L);
-    if (L.mark_any) {   // rare: exact in-order replay of the marked counters
-      if (tid == 0) {
-        for (uint32_t k = 0; k < n; ++k) {
-          const uint32_t t = dst[k];
-          if (t & 0x4000) continue;
-          const int s = tok_stat_slot(t);
-          if (G.mark[s >> 5] & (1u << (s & 31))) record_stat(&G.stats[s], (int)(t >> 15));
-        }
-      }
-      wbar(L);
-      for (int k = tid; k < 33; k += K3T) G.mark[k] = 0;
-      wbar(L);
-    }
-    if (tid == 0) G.ntok += n;
+    for (int k = tid; k < 33; k += K3T) G.mark[k] = 0;
     wbar(L);
   }
-  if (tid == 0) publish((int32_t*)&G.fold_ptr, (int32_t)i1);
+  if (tid == 0) {
+    G.ntok = base + total;
+    publish((int32_t*)&G.fold_ptr, (int32_t)i1);
+  }
 }
 
 struct K3Args {
@@ -1077,14 +1135,13 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   const uint8_t* segmap = a.segmap + (size_t)f * nmb;
   uint16_t* tok_base = a.tokens + f * a.tok_cap;
   uint8_t* mbinfo = a.mbinfo + (size_t)f * nmb * VP8G_MBINFO_BYTES;
-  uint16_t* mbcnt = a.mbcnt + (size_t)f * nmb;
 
   // ---- frame init (whole workgroup)
   for (int s = gt; s < NSLOT; s += NW * K3T) {
     G.stats[s] = 0;
-    G.delta[s] = 0;
     G.coeffs[s] = (&kVP8CoeffProba0[0][0][0][0])[s];
   }
+  for (int s = tid; s < NSLOT; s += K3T) L.rdelta[s] = 0;
   for (int k = gt; k < 33; k += NW * K3T) G.mark[k] = 0;
   for (int k = gt; k < 256; k += NW * K3T) G.ecost[k] = kVP8EntropyCost[k];
   for (int k = gt; k < 1000; k += NW * K3T) G.mcost4[k] = (&kVP8ModeCostI4[0][0][0])[k];
@@ -1120,6 +1177,10 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   const int max_count = P->max_count;
   const bool trellis_all = TR && rd_opt >= 3;
   uint64_t* substamps = nullptr;
+#ifdef K3_STAMPS
+  uint64_t stamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t stamp_last = __builtin_amdgcn_s_memtime();
+#endif
   uint8_t* yl = L.yl_mem + 1;
   uint8_t* ul = L.ul_mem + 1;
   uint8_t* vl = L.vl_mem + 1;
@@ -1147,7 +1208,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
           // everything before this MB: rows above folded by their owners,
           // this row's earlier MBs folded here
           if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from)) break;
-          fold_mbs(G, L, tid, fold_from, mb, tok_base, mbcnt);
+          fold_mbs(G, L, tid, fold_from, mb, (uint32_t)y * mbw, tok_base);
           fold_from = mb;
           wbar(L);
           const int dirty = finalize_probas_wg(G, L, tid);
@@ -1161,6 +1222,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
       }
       // ---- wavefront dependency: MB x+1 of the row above (top-right) is done
       if (y > 0 && !wait_ge(G, L, &rowdone[y - 1], min(x + 2, mbw))) break;
+      K3_STAMP(0);
 
       load_mb(Yp, Up, Vp, w, h, x, y, L.yin, tid, K3T);
       wbar(L);
@@ -1193,6 +1255,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
         if (j == 0) L.hsrc[b] = hs;
       }
       wbar(L);
+      K3_STAMP(1);
 
       // ---- Intra16 (quant_enc.c:1002-1058)
       if constexpr (TR) {
@@ -1241,6 +1304,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
         if (tid == 0) atomicMax(&G.max_edge[segid], mv);
       }
       wbar(L);
+      K3_STAMP(2);
 
       // ---- Intra4 (quant_enc.c:1072-1165)
       if (max_i4_bits > 0) {
@@ -1266,6 +1330,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
         }
         wbar(L);
       }
+      K3_STAMP(3);
 
       // ---- UV (quant_enc.c:1169-1217)
       int bu = 0;
@@ -1327,6 +1392,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
         wbar(L);
       }
       (void)rd_score;
+      K3_STAMP(4);
 
       // ---- per-MB info + side statistics
       const int skip = rd_nz == 0;
@@ -1414,7 +1480,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
           last[q] = k < 25 ? L.blast[k] : -1;
           cnt[q] = bi[q] < 0 ? 0
                              : pos_tokens<false>(bi[q] & 15, (bi[q] >> 4) & 15, bi[q] >> 8, n,
-                                                 lvi[q], lvp[q], last[q], nullptr);
+                                                 lvi[q], lvp[q], last[q], nullptr, nullptr);
         }
         int inc0 = cnt[0], inc1 = cnt[1];
 #pragma unroll
@@ -1437,12 +1503,13 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
         const int off1 = tot0 + pre1 + inc1 - cnt[1];
         if (cnt[0])
           pos_tokens<true>(bi[0] & 15, (bi[0] >> 4) & 15, bi[0] >> 8, rtid & 15, lvi[0], lvp[0],
-                           last[0], slot + off0);
+                           last[0], slot + off0, L.rdelta);
         if (cnt[1])
           pos_tokens<true>(bi[1] & 15, (bi[1] >> 4) & 15, bi[1] >> 8, rtid & 15, lvi[1], lvp[1],
-                           last[1], slot + off1);
-        if (rtid == 0) mbcnt[mb] = (uint16_t)(tot0 + tot1);
+                           last[1], slot + off1, L.rdelta);
+        if (rtid == 0) L.rowcnt[x] = (uint16_t)(tot0 + tot1);
       }
+      K3_STAMP(5);
       // update nz context (iterator_enc.c:267-283) and the left DC flag
       if (rtid == 0) {
         int tn9[9], ln[9];
@@ -1490,12 +1557,14 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
       }
       wbar(L);
       if (tid == 0) publish(&rowdone[y], x + 1);
+      K3_STAMP(6);
     }
     if (L.myabort) break;
     // row end: fold this row's remaining MBs once the rows above are folded
     if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from)) break;
-    fold_mbs(G, L, tid, fold_from, (uint32_t)(y + 1) * mbw, tok_base, mbcnt);
+    fold_mbs(G, L, tid, fold_from, (uint32_t)(y + 1) * mbw, (uint32_t)y * mbw, tok_base);
     wbar(L);
+    K3_STAMP(7);
   }
 
   // ---- frame epilogue: final probabilities and side results
@@ -1512,7 +1581,11 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
       R->sse[0] = G.fs.sse[0]; R->sse[1] = G.fs.sse[1]; R->sse[2] = G.fs.sse[2];
       R->block_count[0] = G.fs.nb[0]; R->block_count[1] = G.fs.nb[1];
       R->block_count[2] = G.fs.nb[2];
+#ifdef K3_STAMPS
+      for (int i = 0; i < 8; ++i) R->stamps[i] = stamps[i];   // worker 0, wave 0
+#else
       for (int i = 0; i < 8; ++i) R->stamps[i] = 0;
+#endif
     }
   }
 }
@@ -1560,11 +1633,12 @@ static int launch_k3(const K3Args& a, int n, bool trellis, void* stream) {
                  : launch_k3_t<NW, false>(a, n, false, stream);
 }
 
-// default: 4 MB workers for m3/m4 frames, 2 when the trellis paths (and
-// their registers and LDS) are in the kernel
+// default: 3 MB workers for m3/m4 frames (4 spill registers to scratch and
+// are no faster: the CU's vector issue is already saturated), 2 when the
+// trellis paths (and their registers and LDS) are in the kernel
 static int launch_k3_default(const K3Args& a, int n, bool trellis, void* stream) {
   return trellis ? launch_k3_t<2, true>(a, n, true, stream)
-                 : launch_k3_t<4, false>(a, n, false, stream);
+                 : launch_k3_t<3, false>(a, n, false, stream);
 }
 
 extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, int n,
@@ -1573,10 +1647,10 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
                                   uint16_t* mbcnt, int trellis, vp8g_frame_result* results,
                                   void* stream) {
   static int variant = -1;
-  if (variant < 0) {   // WEBP_AMD_K3: 1 = single-wavefront reference kernel, 2/3/4 = 1/2/4
-                       // MB workers per frame, unset = 4 (m3/m4) or 2 (trellis)
+  if (variant < 0) {   // WEBP_AMD_K3: 1 = single-wavefront reference kernel, 2/3/5/4 =
+                       // 1/2/3/4 MB workers per frame, unset = default above
     const char* v = getenv("WEBP_AMD_K3");
-    variant = (v && v[0] >= '1' && v[0] <= '4') ? v[0] - '0' : 0;
+    variant = (v && v[0] >= '1' && v[0] <= '5') ? v[0] - '0' : 0;
   }
   if (variant == 1)
     return vp8g_launch_encode_w1(yuv, yfb, w, h, n, segmap, params, tokens, tok_cap, mbinfo,
@@ -1589,5 +1663,6 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   if (variant == 2) return launch_k3<1>(a, n, trellis != 0, stream);
   if (variant == 4) return launch_k3<4>(a, n, trellis != 0, stream);
   if (variant == 3) return launch_k3<2>(a, n, trellis != 0, stream);
+  if (variant == 5) return launch_k3<3>(a, n, trellis != 0, stream);
   return launch_k3_default(a, n, trellis != 0, stream);
 }

@@ -26,7 +26,7 @@
 
 // LDS shared by all of a frame's workers: cost tables of the current epoch,
 // token statistics, quantiser/segment parameters and frame-level counters.
-struct K3G {
+struct alignas(16) K3G {
   uint32_t stats[NSLOT];
   uint16_t lcost[96][MAX_VLEVEL + 1];  // [type*24 + band*3 + ctx][level], incl. fixed cost
   uint16_t ecost[256];
@@ -308,12 +308,24 @@ __device__ __forceinline__ int quant_lane(int cv, int j, const vp8g_mtx& M, int&
 // lane: the context of position n is the previous position's level (one
 // bpermute), every lane does its table reads unconditionally (no divergent
 // branches) and a 16-lane reduction sums the terms.
+// The level at the previous zigzag position, from its lane of the same
+// 16-lane block: natural index j reads j-1, j-3, j-4 or j+3 (DPP row shifts,
+// no LDS round trip). Lane j = 0 (zigzag 0) has no predecessor.
+__device__ __forceinline__ int zz_prev(int v, int j) {
+  const int m1 = dpp<0x111>(v);   // row_shr:1
+  const int m3 = dpp<0x113>(v);   // row_shr:3
+  const int m4 = dpp<0x114>(v);   // row_shr:4
+  const int p3 = dpp<0x103>(v);   // row_shl:3
+  const uint32_t bit = 1u << j;
+  return (bit & 0xA00Au) ? m1 : (bit & 0x5250u) ? m3 : (bit & 0x0900u) ? m4 : p3;
+}
+
 __device__ __forceinline__ int rate_lane(const K3G& G, int level, int j, int g, int ctx0, int type,
                                          int first) {
   const int n = zz_inv(j);
   const int v = iabs_(level);
   const int last = max16((v != 0 && n >= first) ? n : -1);
-  const int vprev = iabs_(__shfl(level, g + zz_rt(n > 0 ? n - 1 : 0)));
+  const int vprev = iabs_(zz_prev(level, j));
   const int ctxp = n == first ? ctx0 : min(vprev, 2);
   int cost = G.lcost[type * 24 + band_of(n) * 3 + ctxp][min(v, MAX_VLEVEL)];
   if (v > MAX_VLEVEL)   // rare: beyond the LDS rows
@@ -663,7 +675,6 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
   const int m = tid >> 4, j = tid & 15, g = (tid & 63) & 48, x = j & 3, y = j >> 2;
   const bool act = tid < 160;
   const int wj = G.wy[j];
-  const TLane T = make_tlane(opaque(j));
   const P4Lane pl = p4_lane(G.p4[act ? tid : 0], x, y);
   // this lane's y1 quantiser entries, once per MB
   const vp8g_mtx& M = S.y1;
@@ -698,7 +709,7 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
       }
     }
     SUBST(0);
-    const int c = fdct_lane(src - pr, T);
+    const int c = fdct_lane(src - pr, make_tlane(opaque(j)));
     SUBST(1);
     int level = 0, dq = 0;
     if constexpr (TRELLIS) {
@@ -726,7 +737,7 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
       dq = (int16_t)__mul24(level, q_q);
     }
     SUBST(2);
-    const int rec = idct_lane(dq, pr, T);
+    const int rec = idct_lane(dq, pr, make_tlane(opaque(j)));
     const uint64_t bnz = __ballot(act && level != 0);
     const uint64_t bac = __ballot(act && level != 0 && j != 0);
     const int nzb = ((bnz >> g) & 0xffff) != 0;
@@ -735,7 +746,7 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
       const int D = sum16((src - rec) * (src - rec));
       int SD = 0;
       if (S.tlambda) {
-        const int td = sum16(ttrans_lane(rec, T, wj)) - L.hsrc[i4];
+        const int td = sum16(ttrans_lane(rec, make_tlane(opaque(j)), wj)) - L.hsrc[i4];
         SD = (S.tlambda * (iabs_(td) >> 5) + 128) >> 8;
       }
       SUBST(4);
@@ -1107,7 +1118,8 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   const int mbw = a.mbw, mbh = a.mbh, nmb = mbw * mbh;
   K3G& G = *reinterpret_cast<K3G*>(smem);
   const int wk = threadIdx.x / K3T;        // worker
-  const int tid = threadIdx.x % K3T;       // thread within the worker
+  const int tid_k = threadIdx.x % K3T;     // thread within the worker
+  const int tid = tid_k;
   K3S& L = reinterpret_cast<K3S*>(smem + sizeof(K3G))[wk];
   uint8_t* ytop = smem + sizeof(K3G) + NW * sizeof(K3S);   // 16*mbw + 16
   uint8_t* uvtop = ytop + 16 * mbw + 16;                      // 16*mbw
@@ -1120,12 +1132,10 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
 
   const int f = blockIdx.x;
   const int gt = threadIdx.x;
-  const int lane = tid & 63;
   // thread id rotated by one wave per worker: stages that leave a wave idle
   // (intra4's 160 lanes, the token tail, wave-0 bookkeeping) put the idle wave
   // on a different SIMD for each worker
-  const int rtid = (tid + 64 * (wk & 3)) & (K3T - 1);
-  const bool w0 = rtid < 64;
+  const int rtid_k = (tid + 64 * (wk & 3)) & (K3T - 1);
   const int w = a.w, h = a.h;
   const int uvw = (w + 1) >> 1, uvh = (h + 1) >> 1;
   const uint8_t* Yp = a.yuv + f * a.yfb;
@@ -1176,7 +1186,12 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   const int use_derr = P->use_derr;
   const int max_count = P->max_count;
   const bool trellis_all = TR && rd_opt >= 3;
+#ifdef K3_SUBPROF
+  uint64_t subacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t* substamps = subacc;
+#else
   uint64_t* substamps = nullptr;
+#endif
 #ifdef K3_STAMPS
   uint64_t stamps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t stamp_last = __builtin_amdgcn_s_memtime();
@@ -1198,6 +1213,11 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
     uint32_t fold_from = (uint32_t)y * mbw;   // first MB of this row not folded yet
     wbar(L);
     for (int x = 0; x < mbw; ++x) {
+      // per-lane ids re-derived every MB (opaque): values computed from them
+      // stay next to their uses instead of being hoisted out of the MB loop
+      // and held in registers across it
+      const int tid = opaque(tid_k), rtid = opaque(rtid_k), lane = tid & 63;
+      const bool w0 = rtid < 64;
       const uint32_t mb = (uint32_t)y * mbw + x;
       // ---- cost-table epoch (frame_enc.c:828-832): refresh before MB k with
       // k = max_count + e * (max_count + 1)
@@ -1581,8 +1601,10 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
       R->sse[0] = G.fs.sse[0]; R->sse[1] = G.fs.sse[1]; R->sse[2] = G.fs.sse[2];
       R->block_count[0] = G.fs.nb[0]; R->block_count[1] = G.fs.nb[1];
       R->block_count[2] = G.fs.nb[2];
-#ifdef K3_STAMPS
+#if defined(K3_STAMPS)
       for (int i = 0; i < 8; ++i) R->stamps[i] = stamps[i];   // worker 0, wave 0
+#elif defined(K3_SUBPROF)
+      for (int i = 0; i < 8; ++i) R->stamps[i] = subacc[i];
 #else
       for (int i = 0; i < 8; ++i) R->stamps[i] = 0;
 #endif
@@ -1661,8 +1683,8 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   a.segmap = segmap; a.params = params; a.tokens = tokens; a.tok_cap = tok_cap;
   a.mbinfo = mbinfo; a.mbcnt = mbcnt; a.results = results;
   if (variant == 2) return launch_k3<1>(a, n, trellis != 0, stream);
-  if (variant == 4) return launch_k3<4>(a, n, trellis != 0, stream);
   if (variant == 3) return launch_k3<2>(a, n, trellis != 0, stream);
+  if (variant == 4) return launch_k3<4>(a, n, trellis != 0, stream);
   if (variant == 5) return launch_k3<3>(a, n, trellis != 0, stream);
   return launch_k3_default(a, n, trellis != 0, stream);
 }

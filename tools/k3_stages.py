@@ -11,8 +11,8 @@ method = int(sys.argv[4]) if len(sys.argv) > 4 else 4
 names = ["epoch+rowdone wait", "load+preds", "i16", "i4", "uv(+m5)", "info+sse+tokens",
          "ctx+boundary", "row-end fold"]
 if os.environ.get("WEBP_AMD_LIB", "").endswith("_sub.so"):
-    names = ["i4:pred", "i4:fdct", "i4:quant", "i4:idct", "i4:distortion", "i4:rate+score",
-             "i4:select", "i4:commit"]
+    names = ["i4:decide+commit prev", "i4:edges+pred", "i4:fdct+quant+idct", "i4:distortion",
+             "i4:rate+score", "i4:barrier", "-", "-"]
 buf = torch.empty(B * W * H * 4, dtype=torch.uint8, device="cuda")
 libwebp_amd.synth_device(buf.data_ptr(), W, H, 0, B)
 torch.cuda.synchronize()

@@ -114,3 +114,16 @@ def test_transparent_input_is_rejected(gpu):
     enc.encode_host(img[None])
     assert enc.error(0) != 0
     enc.close()
+
+
+def test_survey_kat_4096_q90_m6(gpu, kat):
+    """Config 4: one 4096x4096 frame at q90 m6 (trellis on
+    every block), bit-exact against the reference's known answer."""
+    (c,) = [c for c in kat["survey"] if c["w"] == 4096]
+    enc = gpu.GpuBatch(4096, 4096, 1, **c["params"])
+    enc.encode_host(syn_v1(4096, 4096, c["frame"])[None])
+    out = enc.output(0)
+    st = enc.timings()
+    enc.close()
+    assert len(out) == c["size"] and sha(out) == c["sha256"]
+    print("4096x4096 q90 m6: k_encode %.0f ms" % (st[6] / 1e3))

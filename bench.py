@@ -4,8 +4,9 @@ frames on MI355X, BASELINE.json configs[1] (1 GPU) / configs[2] (8 GPUs).
 
 One "step" = one WebPGpuBatchEncodeRGBA call over the rank's batch of
 HBM-resident syn-v1 frames: K1 import, K2 analysis, host
-segment setup, K3 RD search + tokens, D2H of the tokens, host boolean-coder
-tail and RIFF assembly, ending with every .webp in host memory. Frames are
+segment setup, K3 RD search + tokens, K4 boolean coder on the device (host
+codes partition 0 meanwhile), one D2H of the packed partitions and the RIFF
+write, ending with every .webp in host memory. Frames are
 synthesised on the device before timing starts (value = throughput with the
 input resident in HBM); the PCIe-inclusive host-input rate is measured
 separately by `--host-input` and documented in DESIGN.md.
@@ -61,6 +62,20 @@ def cpu_baseline(width, height, quality, method, seconds):
             "sample": "%d syn-v1 %dx%d frames (f=1..%d), q%d m%d, WebPPictureImportRGBA+"
                       "WebPEncode, single thread, %.1f s" % (frames, width, height, frames,
                                                              quality, method, elapsed)}
+
+
+def measured_traffic(kernel, B, W, H, quality, method):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    passes (profiles/r1_pmc_hbm.csv: FETCH_SIZE + WRITE_SIZE in KB, one
+    launch of this same default workload), or None for another workload."""
+    import csv
+    path = os.path.join(HERE, "profiles", "r1_pmc_hbm.csv")
+    if not os.path.exists(path) or (B, W, H, quality, method) != (256, 1920, 1080, 75.0, 4):
+        return None
+    for r in csv.DictReader(open(path)):
+        if r["kernel"] == kernel:
+            return int(1000 * (float(r["FETCH_SIZE_KB"]) + float(r["WRITE_SIZE_KB"])))
+    return None
 
 
 def shard(rank, frames_per_rank):
@@ -201,7 +216,11 @@ def main():
                    "parallelism": "frames sharded %d ways" % world},
         "roofline": {"bound": "hbm", "kernel": "k_encode", "achieved": round(achieved, 3),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 6),
+                     "traffic": measured_traffic("k_encode<3, false>", B, W, H, args.quality,
+                                                 args.method),
+                     "traffic_source": "profiles/r1_pmc_hbm.csv (rocprofv3 --pmc FETCH_SIZE, "
+                                       "WRITE_SIZE passes of this workload; bytes per launch)",
                      "k_encode_ms": round(1e3 * k3_avg_s, 3),
                      "algorithmic_bytes_per_launch": k3_bytes},
         "stage_ms": {k: round(sum(t[i] for t in tails) / len(tails) / 1e3, 3) for k, i in

@@ -149,18 +149,14 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
     const int r0 = ni == 0xff ? 127 + EMIT_SLOTS * rd + slot : (live ? im[1 + slot] : 127);
     int r = r0;
     uint32_t S = 0;
-    for (uint32_t i = 0; i < cnt; i += 8) {   // segment starts are 16-byte aligned
+    const uint32_t full = cnt & ~7u;   // segment starts are 16-byte aligned
+    for (uint32_t i = 0; i < full; i += 8) {
       const uint4 q = *reinterpret_cast<const uint4*>(tok + i);
       const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        int rr = r;
-        const int sh = chain_step(rr, (w[k >> 1] >> (16 * (k & 1))) & 0xffff);
-        const bool in = i + k < cnt;
-        r = in ? rr : r;
-        S += in ? sh : 0;
-      }
+      for (int k = 0; k < 8; ++k) S += chain_step(r, (w[k >> 1] >> (16 * (k & 1))) & 0xffff);
     }
+    for (uint32_t i = full; i < cnt; ++i) S += chain_step(r, tok[i]);   // frame's last segment
     if (live) {
       const size_t o = ((size_t)M.seg_base + s) * 128 + (r0 - 127);
       emap[o] = (uint8_t)r;
@@ -207,40 +203,86 @@ __global__ __launch_bounds__(64) void k_emit_compose(vp8g_emit_meta* __restrict_
   }
 }
 
+// One wave = 64 segments, one lane each. The segments' tokens are staged
+// through LDS 64 tokens at a time: the wave loads a chunk of all 64 segments
+// with 128-byte runs per segment (a lane-per-segment walk would touch 64
+// lines 4 KB apart per load), each lane then walks its own row.
+#define SEG_CH 64                   // tokens per segment per chunk
+#define SEG_ROW (SEG_CH / 2 + 1)    // LDS row in dwords, +1: conflict-free rows
+
+__device__ __forceinline__ void seg_chunk_load(uint32_t* lds, const uint16_t* base, uint32_t s0,
+                                               uint32_t nseg, uint32_t ntok, uint32_t c0,
+                                               int lane) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int q = lane + 64 * t, sg = q >> 3, part = q & 7;
+    const uint32_t i = (s0 + sg) * EMIT_SEG + c0 + 8 * part;   // frame token index
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (s0 + sg < nseg && i < ntok) v = *reinterpret_cast<const uint4*>(base + i);
+    uint32_t* d = lds + sg * SEG_ROW + 4 * part;
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  }
+}
+
+__device__ __forceinline__ void seg_chunk_store(const uint32_t* lds, uint16_t* base, uint32_t s0,
+                                                uint32_t nseg, uint32_t ntok, uint32_t c0,
+                                                int lane) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int q = lane + 64 * t, sg = q >> 3, part = q & 7;
+    const uint32_t i = (s0 + sg) * EMIT_SEG + c0 + 8 * part;
+    const uint32_t* d = lds + sg * SEG_ROW + 4 * part;
+    if (s0 + sg < nseg && i < ntok)
+      *reinterpret_cast<uint4*>(base + i) = make_uint4(d[0], d[1], d[2], d[3]);
+  }
+}
+
 __global__ __launch_bounds__(64) void k_emit_seg(uint16_t* __restrict__ tokens, size_t tok_cap,
                                                  const vp8g_emit_meta* __restrict__ meta,
                                                  vp8g_emit_seg* __restrict__ segs,
                                                  uint32_t* __restrict__ nbuf) {
-  const int f = blockIdx.y;
-  const uint32_t s = blockIdx.x * 64 + threadIdx.x;
+  __shared__ uint32_t lds[64 * SEG_ROW];
+  const int f = blockIdx.y, lane = threadIdx.x;
+  const uint32_t s0 = blockIdx.x * 64, s = s0 + lane;
   const vp8g_emit_meta M = meta[f];
-  if (s >= M.nseg) return;
-  vp8g_emit_seg& g = segs[M.seg_base + s];
+  if (s0 >= M.nseg) return;   // whole wave
+  const bool valid = s < M.nseg;
+  vp8g_emit_seg g = valid ? segs[M.seg_base + s] : vp8g_emit_seg{0, 0, 254, 0};
   const uint32_t i0 = s * EMIT_SEG;
-  const uint32_t cnt = min((uint32_t)EMIT_SEG, M.ntok - i0);
-  uint16_t* tok = tokens + (size_t)f * tok_cap + i0;
-  // forward: true range chain -> (c, shift) packed in place, 8 tokens per
-  // 16-byte access (the segment start is 16-byte aligned; the tail chunk may
-  // run past cnt inside the buffer and is masked)
+  const uint32_t cnt = valid ? min((uint32_t)EMIT_SEG, M.ntok - i0) : 0u;
+  uint16_t* base = tokens + (size_t)f * tok_cap;
+  uint32_t* row = lds + lane * SEG_ROW;
+  // the chunks this wave needs: up to its longest segment
+  const uint32_t last_s = min(s0 + 64, M.nseg) - 1;
+  const uint32_t span = min((uint32_t)EMIT_SEG, M.ntok - last_s * EMIT_SEG) == EMIT_SEG || last_s > s0
+                            ? (uint32_t)EMIT_SEG
+                            : M.ntok - last_s * EMIT_SEG;
+  // forward: true range chain -> (c, shift) packed in place
   int r = g.rs;
-  for (uint32_t i = 0; i < cnt; i += 8) {
-    uint4 q = *reinterpret_cast<const uint4*>(tok + i);
-    uint32_t w[4] = {q.x, q.y, q.z, q.w};
+  for (uint32_t c0 = 0; c0 < span; c0 += SEG_CH) {
+    seg_chunk_load(lds, base, s0, M.nseg, M.ntok, c0, lane);
+    __syncthreads();
+#pragma unroll 4
+    for (int k = 0; k < SEG_CH / 2; ++k) {
+      uint32_t w = row[k];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint32_t pb = (w[k >> 1] >> (16 * (k & 1))) & 0xffff;
-      const int split = (r * (int)(pb & 0xff)) >> 8;
-      const int bit = (pb >> 8) & 1;
-      const int c = bit ? split + 1 : 0;
-      const int rn = bit ? r - split - 1 : split;
-      int rr = rn;
-      const int sh = renorm(rr);
-      const bool live = i + k < cnt;
-      r = live ? rr : r;
-      const uint32_t pk = live ? (uint32_t)(c | (sh << 8)) : 0u;
-      w[k >> 1] = (w[k >> 1] & ~(0xffffu << (16 * (k & 1)))) | (pk << (16 * (k & 1)));
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t pb = (w >> (16 * h)) & 0xffff;
+        const int split = (r * (int)(pb & 0xff)) >> 8;
+        const int bit = (pb >> 8) & 1;
+        const int c = bit ? split + 1 : 0;
+        int rr = bit ? r - split - 1 : split;
+        const int sh = renorm(rr);
+        const bool live = c0 + 2 * k + h < cnt;
+        r = live ? rr : r;
+        const uint32_t pk = live ? (uint32_t)(c | (sh << 8)) : 0u;
+        w = (w & ~(0xffffu << (16 * h))) | (pk << (16 * h));
+      }
+      row[k] = w;
     }
-    *reinterpret_cast<uint4*>(tok + i) = make_uint4(w[0], w[1], w[2], w[3]);
+    __syncthreads();
+    seg_chunk_store(lds, base, s0, M.nseg, M.ntok, c0, lane);
+    __syncthreads();
   }
   // reverse: least-significant first; bits below the current position are final
   uint32_t* W = nbuf + M.nb_base;
@@ -248,26 +290,32 @@ __global__ __launch_bounds__(64) void k_emit_seg(uint16_t* __restrict__ tokens, 
   uint32_t wb = T & ~31u;      // global bit index of acc's bit 0
   uint64_t acc = 0;
   uint32_t E = 0;
-  const uint32_t last8 = (cnt + 7) & ~7u;   // padded entries are (c=0, shift=0)
-  for (uint32_t i = last8; i > 0; i -= 8) {
-    const uint4 q = *reinterpret_cast<const uint4*>(tok + i - 8);
-    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+  const uint32_t nch = (span + SEG_CH - 1) / SEG_CH;
+  for (uint32_t ch = nch; ch > 0; --ch) {
+    const uint32_t c0 = (ch - 1) * SEG_CH;
+    seg_chunk_load(lds, base, s0, M.nseg, M.ntok, c0, lane);   // (c, shift); 0 past the end
+    __syncthreads();
+    for (int k = SEG_CH / 2 - 1; k >= 0; --k) {
+      const uint32_t w = row[k];
 #pragma unroll
-    for (int k = 7; k >= 0; --k) {
-      const uint32_t pk = (w[k >> 1] >> (16 * (k & 1))) & 0xffff;
-      E += pk >> 8;
-      const uint32_t G = T + E;
-      while (G >= wb + 32) {   // word [wb, wb+32) is final
-        const uint32_t lo = (uint32_t)acc;
-        const uint32_t mlo = wb < T ? (~0u << (T - wb)) : ~0u;
-        if (mlo != ~0u) atomicOr(W + (wb >> 5), lo & mlo);
-        else W[wb >> 5] = lo;
-        acc >>= 32;
-        wb += 32;
+      for (int h = 1; h >= 0; --h) {
+        const uint32_t pk = c0 + 2 * k + h < cnt ? (w >> (16 * h)) & 0xffff : 0u;
+        E += pk >> 8;
+        const uint32_t G = T + E;
+        while (G >= wb + 32) {   // word [wb, wb+32) is final
+          const uint32_t lo = (uint32_t)acc;
+          const uint32_t mlo = wb < T ? (~0u << (T - wb)) : ~0u;
+          if (mlo != ~0u) atomicOr(W + (wb >> 5), lo & mlo);
+          else W[wb >> 5] = lo;
+          acc >>= 32;
+          wb += 32;
+        }
+        acc += (uint64_t)(pk & 0xff) << (G - wb);
       }
-      acc += (uint64_t)(pk & 0xff) << (G - wb);
     }
+    __syncthreads();
   }
+  if (!valid) return;
   // remaining words up to the region top; bits above it are H_s
   while (wb < top) {
     const uint32_t lo = (uint32_t)acc;
@@ -280,7 +328,7 @@ __global__ __launch_bounds__(64) void k_emit_seg(uint16_t* __restrict__ tokens, 
     acc >>= 32;
     wb += 32;
   }
-  g.H = (uint8_t)((acc >> (top - wb)) & 0xff);
+  segs[M.seg_base + s].H = (uint8_t)((acc >> (top - wb)) & 0xff);
 }
 
 // big-number add of h at bit b (h < 256) with ripple carry, via atomics

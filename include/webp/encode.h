@@ -259,6 +259,13 @@ WEBP_EXTERN int WebPPictureImportBGRX(WebPPicture* picture,
 /* ref encode.h:480-482, :508 */
 WEBP_EXTERN int WebPPictureARGBToYUVA(WebPPicture* picture,
                                       WebPEncCSP colorspace);
+/* ref encode.h:493-509: dithered (only dithering == 0 is accepted here) and
+ * sharp (iterative, GPU kernels hip/vp8_sharp.hip) ARGB -> YUV420. */
+WEBP_EXTERN int WebPPictureARGBToYUVADithered(WebPPicture* picture,
+                                              WebPEncCSP colorspace,
+                                              float dithering);
+WEBP_EXTERN int WebPPictureSharpARGBToYUVA(WebPPicture* picture);
+WEBP_EXTERN int WebPPictureSmartARGBToYUVA(WebPPicture* picture);
 WEBP_EXTERN int WebPPictureHasTransparency(const WebPPicture* picture);
 
 /* Main entry point, ref encode.h:544. Returns 0 on error, reason in

@@ -101,6 +101,9 @@ def bind_encoder_api(lib):
         "WebPPictureImportRGBA": (C.c_int, [P(WebPPicture), C.c_void_p, C.c_int]),
         "WebPPictureImportRGB": (C.c_int, [P(WebPPicture), C.c_void_p, C.c_int]),
         "WebPPictureImportBGRA": (C.c_int, [P(WebPPicture), C.c_void_p, C.c_int]),
+        "WebPPictureSharpARGBToYUVA": (C.c_int, [P(WebPPicture)]),
+        "WebPPictureSmartARGBToYUVA": (C.c_int, [P(WebPPicture)]),
+        "WebPPictureARGBToYUVA": (C.c_int, [P(WebPPicture), C.c_int]),
         "WebPMemoryWriterInit": (None, [P(WebPMemoryWriter)]),
         "WebPMemoryWriterClear": (None, [P(WebPMemoryWriter)]),
         "WebPEncode": (C.c_int, [P(WebPConfig), P(WebPPicture)]),
@@ -128,8 +131,12 @@ def make_config(lib, quality=75.0, method=4, preset=WEBP_PRESET_DEFAULT, **kw):
     return cfg
 
 
-def encode_rgba(lib, rgba, quality=75.0, method=4, stats=False, **kw):
+def encode_rgba(lib, rgba, quality=75.0, method=4, stats=False, use_argb=None, **kw):
     """Encode an (H, W, 4) uint8 array through `lib`'s WebPEncode().
+
+    use_argb: import into the ARGB container first (what cwebp does for
+    -sharp_yuv, examples/cwebp.c); defaults to on when use_sharp_yuv is set,
+    since WebPEncode only re-converts an ARGB picture.
 
     Returns (bytes, WebPAuxStats or None). Raises on encoder error.
     """
@@ -141,6 +148,9 @@ def encode_rgba(lib, rgba, quality=75.0, method=4, stats=False, **kw):
     if not lib.WebPPictureInitInternal(C.byref(pic), WEBP_ENCODER_ABI_VERSION):
         raise RuntimeError("WebPPictureInitInternal failed")
     pic.width, pic.height = w, h
+    if use_argb is None:
+        use_argb = bool(kw.get("use_sharp_yuv", 0))
+    pic.use_argb = int(use_argb)
     wrt = WebPMemoryWriter()
     lib.WebPMemoryWriterInit(C.byref(wrt))
     pic.writer = lib.WebPMemoryWrite_addr
@@ -160,17 +170,21 @@ def encode_rgba(lib, rgba, quality=75.0, method=4, stats=False, **kw):
     return data, st
 
 
-def picture_yuv(lib, rgba):
-    """Run WebPPictureImportRGBA through `lib` and return (Y, U, V) arrays."""
+def picture_yuv(lib, rgba, sharp=False):
+    """Run WebPPictureImportRGBA through `lib` and return (Y, U, V) arrays.
+    sharp=True: import into ARGB, then WebPPictureSharpARGBToYUVA."""
     import numpy as np
     rgba = np.ascontiguousarray(rgba, dtype=np.uint8)
     h, w = rgba.shape[:2]
     pic = WebPPicture()
     lib.WebPPictureInitInternal(C.byref(pic), WEBP_ENCODER_ABI_VERSION)
     pic.width, pic.height = w, h
+    pic.use_argb = 1 if sharp else 0
     try:
         if not lib.WebPPictureImportRGBA(C.byref(pic), rgba.ctypes.data, 4 * w):
             raise RuntimeError("import failed")
+        if sharp and not lib.WebPPictureSharpARGBToYUVA(C.byref(pic)):
+            raise RuntimeError("sharp conversion failed")
         uw, uh = (w + 1) // 2, (h + 1) // 2
         y = np.ctypeslib.as_array(pic.y, shape=(h * pic.y_stride,)).reshape(h, pic.y_stride)[:, :w].copy()
         u = np.ctypeslib.as_array(pic.u, shape=(uh * pic.uv_stride,)).reshape(uh, pic.uv_stride)[:, :uw].copy()

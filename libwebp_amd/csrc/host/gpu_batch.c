@@ -94,6 +94,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   b->yfb = (size_t)width * height + 2 * (size_t)b->uvw * b->uvh;
   b->yfb = (b->yfb + 255) & ~(size_t)255;
   b->tok_cap = (size_t)b->nmb * VP8G_MAX_TOKENS_PER_MB;
+  b->sharp = vp8h_use_sharp(config, width, height);
   b->threads = host_threads > 0 ? host_threads : default_threads();
   {   /* WEBP_AMD_HOST_EMIT=1: boolean-code partition 1 on the host threads */
     const char* he = getenv("WEBP_AMD_HOST_EMIT");
@@ -154,6 +155,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipFree(b->d_poff); hipFree(b->d_part);
   hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs); hipFree(b->d_nbuf);
   hipFree(b->d_eimg);
+  hipFree(b->d_stabs); hipFree(b->d_sharp); hipFree(b->d_sstate);
   hipHostFree(b->h_aflags); hipHostFree(b->h_alpha); hipHostFree(b->h_uva);
   hipHostFree(b->h_segmap); hipHostFree(b->h_params); hipHostFree(b->h_mbinfo);
   hipHostFree(b->h_results); hipHostFree(b->h_tokens); hipHostFree(b->h_psize);
@@ -422,6 +424,28 @@ fail:
   return 0;
 }
 
+/* RGBA -> YUV420 of n frames on the engine stream: K1, or the sharp-YUV
+ * kernels (hip/vp8_sharp.hip) when requested. */
+static int launch_import(WebPGpuBatch* b, const uint8_t* rgba, size_t fstride, int rstride, int n,
+                         int sharp) {
+  if (!sharp)
+    return vp8g_launch_import(rgba, fstride, rstride, b->w, b->h, n, b->d_yuv, b->yfb,
+                              b->d_aflags, b->d_g2l, b->d_l2g, b->stream);
+  if (!b->d_sharp) {   /* first sharp call: scratch for max_frames frames */
+    const uint32_t *g2l, *l2g;
+    vp8h_sharp_tables(&g2l, &l2g);
+    CHK(hipMalloc((void**)&b->d_stabs, (1026 + 514) * sizeof(uint32_t)));
+    CHK(hipMemcpy(b->d_stabs, g2l, 1026 * sizeof(uint32_t), hipMemcpyHostToDevice));
+    CHK(hipMemcpy(b->d_stabs + 1026, l2g, 514 * sizeof(uint32_t), hipMemcpyHostToDevice));
+    CHK(hipMalloc((void**)&b->d_sstate, b->max_frames * sizeof(vp8g_sharp_state)));
+    CHK(hipMalloc((void**)&b->d_sharp, b->max_frames * vp8g_sharp_frame_bytes(b->w, b->h)));
+  }
+  return vp8g_launch_sharp(rgba, fstride, rstride, b->w, b->h, n, b->d_yuv, b->yfb, b->d_aflags,
+                           b->d_sharp, b->d_sstate, b->d_stabs, b->d_stabs + 1026, b->stream);
+fail:
+  return 0;
+}
+
 static int run_rgba(WebPGpuBatch* b, const void* rgba_dev, size_t fstride, int rstride, int n,
                     void* stream) {
   const double t0 = now_us();
@@ -440,9 +464,7 @@ static int run_rgba(WebPGpuBatch* b, const void* rgba_dev, size_t fstride, int r
   CHK(hipMemsetAsync(b->d_aflags, 0, n * sizeof(uint32_t), b->stream));
   CHK(hipEventRecord(b->ev[0], b->stream));
   b->ev0_recorded = 1;
-  if (!vp8g_launch_import((const uint8_t*)rgba_dev, fstride, rstride, b->w, b->h, n, b->d_yuv,
-                          b->yfb, b->d_aflags, b->d_g2l, b->d_l2g, b->stream))
-    return 0;
+  if (!launch_import(b, (const uint8_t*)rgba_dev, fstride, rstride, n, b->sharp)) return 0;
   CHK(hipMemcpyAsync(b->h_aflags, b->d_aflags, n * sizeof(uint32_t), hipMemcpyDeviceToHost,
                      b->stream));
   CHK(hipStreamSynchronize(b->stream));
@@ -544,7 +566,7 @@ int vp8g_engine_upload_yuv(WebPGpuBatch* b, int f, const uint8_t* y, int ys, con
 }
 
 int vp8g_engine_import(WebPGpuBatch* b, const uint8_t* rgba, int stride, uint8_t* y,
-                       uint8_t* u, uint8_t* v, int* has_alpha) {
+                       uint8_t* u, uint8_t* v, int* has_alpha, int sharp) {
   /* synchronous single-frame RGBA -> YUV through K1 (used by the
    * WebPPictureImport* API); output written to the caller's host planes */
   if (hipSetDevice(b->device) != hipSuccess) return 0;
@@ -558,9 +580,7 @@ int vp8g_engine_import(WebPGpuBatch* b, const uint8_t* rgba, int stride, uint8_t
   }
   if (hipMemcpy(b->d_rgba, rgba, need, hipMemcpyHostToDevice) != hipSuccess) return 0;
   if (hipMemsetAsync(b->d_aflags, 0, sizeof(uint32_t), b->stream) != hipSuccess) return 0;
-  if (!vp8g_launch_import(b->d_rgba, need, stride, b->w, b->h, 1, b->d_yuv, b->yfb, b->d_aflags,
-                          b->d_g2l, b->d_l2g, b->stream))
-    return 0;
+  if (!launch_import(b, b->d_rgba, need, stride, 1, sharp && b->w >= 4 && b->h >= 4)) return 0;
   if (hipStreamSynchronize(b->stream) != hipSuccess) return 0;
   uint32_t flag = 0;
   if (hipMemcpy(&flag, b->d_aflags, 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;

@@ -41,6 +41,11 @@ struct WebPGpuBatch {
   vp8g_emit_seg* d_esegs;
   uint32_t* d_nbuf;
   size_t emit_seg_cap, emit_word_cap;
+  /* sharp-YUV import (allocated on first use) */
+  int sharp;                 /* config asks for it and the frame is >= 4x4 */
+  uint32_t* d_stabs;         /* 1026 gamma->linear + 514 linear->gamma */
+  uint8_t* d_sharp;          /* per-frame W/RGB planes */
+  vp8g_sharp_state* d_sstate;
   /* host (pinned) */
   uint32_t* h_aflags;
   uint8_t* h_alpha;
@@ -76,7 +81,7 @@ int vp8g_engine_run_yuv(struct WebPGpuBatch* b, int n);
 int vp8g_engine_upload_yuv(struct WebPGpuBatch* b, int f, const uint8_t* y, int ys,
                            const uint8_t* u, const uint8_t* v, int uvs);
 int vp8g_engine_import(struct WebPGpuBatch* b, const uint8_t* rgba, int stride, uint8_t* y,
-                       uint8_t* u, uint8_t* v, int* has_alpha);
+                       uint8_t* u, uint8_t* v, int* has_alpha, int sharp);
 #ifdef __cplusplus
 }
 #endif

@@ -3,6 +3,7 @@
 #include "vp8_host.h"
 
 #include <math.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -17,11 +18,38 @@ static inline int bit_cost(int bit, int p) {   /* cost_enc.h:59-61 */
   return bit ? kVP8EntropyCost[255 - p] : kVP8EntropyCost[p];
 }
 
+static uint32_t g_sg2l[1026], g_sl2g[514];
+static pthread_once_t g_sharp_once = PTHREAD_ONCE_INIT;
+static void sharp_tables_init(void) {
+  const double a = 0.09929682680944, lin_thresh = 0.018053968510807;
+  const double scale = 65536.;
+  for (int i = 0; i <= 1024; ++i) {   /* gamma -> linear */
+    const double g = (1. / 1024) * i;
+    const double x = g <= lin_thresh * 4.5 ? g / 4.5 : pow((1. / (1. + a)) * (g + a), 1. / 0.45);
+    g_sg2l[i] = (uint32_t)(x * scale + .5);
+  }
+  g_sg2l[1025] = g_sg2l[1024];
+  for (int i = 0; i <= 512; ++i) {    /* linear -> gamma */
+    const double l = (1. / 512) * i;
+    const double x = l <= lin_thresh ? 4.5 * l : (1. + a) * pow(l, 1. / (1. / 0.45)) - a;
+    g_sl2g[i] = (uint32_t)(scale * x + .5);
+  }
+  g_sl2g[513] = g_sl2g[512];
+}
+void vp8h_sharp_tables(const uint32_t** g2l, const uint32_t** l2g) {
+  pthread_once(&g_sharp_once, sharp_tables_init);
+  *g2l = g_sg2l;
+  *l2g = g_sl2g;
+}
+int vp8h_use_sharp(const WebPConfig* cfg, int w, int h) {
+  return (cfg->use_sharp_yuv || (cfg->preprocessing & 4)) && w >= 4 && h >= 4;
+}
+
 int vp8h_frame_init(vp8h_frame* fr, const WebPConfig* cfg, int w, int h) {
   memset(fr, 0, sizeof(*fr));
   if (cfg->method < 3 || cfg->method > 6) return 0;   /* m0-2: non-token loop */
   if (cfg->pass != 1 || cfg->target_size > 0 || cfg->target_PSNR > 0) return 0;
-  if (cfg->autofilter || cfg->low_memory || cfg->use_sharp_yuv) return 0;
+  if (cfg->autofilter || cfg->low_memory || (cfg->preprocessing & 2)) return 0;
   fr->w = w; fr->h = h;
   fr->mbw = (w + 15) >> 4; fr->mbh = (h + 15) >> 4;
   fr->method = cfg->method;

@@ -35,6 +35,15 @@ typedef struct {
 
 /* Initialise from a validated config (lossy, method 3..6). Returns 0 if the
  * config is outside what the GPU path implements. */
+/* sRGB gamma tables of the sharp-YUV import (sharpyuv/sharpyuv_gamma.c:33-78):
+ * 1026 gamma->linear and 514 linear->gamma entries, double pow like the
+ * reference. Thread-safe, computed once. */
+void vp8h_sharp_tables(const uint32_t** g2l, const uint32_t** l2g);
+/* whether an encode with this config on a w x h picture takes the sharp
+ * import (use_sharp_yuv or preprocessing & 4, and both dimensions >= 4,
+ * webp_enc.c:352-356, picture_csp_enc.c:493-496) */
+int vp8h_use_sharp(const WebPConfig* cfg, int w, int h);
+
 int vp8h_frame_init(vp8h_frame* fr, const WebPConfig* cfg, int w, int h);
 
 /* Segment analysis + parameters (analysis_enc.c:76-216, quant_enc.c:205-455,

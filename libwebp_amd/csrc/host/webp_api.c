@@ -263,7 +263,7 @@ static WebPGpuBatch* engine_for(const WebPConfig* cfg, int w, int h) {
 /* ---- import (picture_csp_enc.c:474-619, 732-844) ---- */
 
 static int import_packed(WebPPicture* pic, const uint8_t* src, int stride, int step, int swap_rb,
-                         int with_alpha) {
+                         int with_alpha, int sharp) {
   const int w = pic->width, h = pic->height;
   if (abs(stride) < (with_alpha ? 4 : step) * w) return 0;
   const int ri = swap_rb ? 2 : 0, bi = swap_rb ? 0 : 2;
@@ -298,7 +298,8 @@ static int import_packed(WebPPicture* pic, const uint8_t* src, int stride, int s
     WebPConfigInitInternal(&cfg, WEBP_PRESET_DEFAULT, 75.f, WEBP_ENCODER_ABI_VERSION);
     WebPGpuBatch* e = engine_for(&cfg, w, h);
     int has_alpha = 0;
-    ok = e != NULL && vp8g_engine_import(e, rgba, 4 * w, pic->y, pic->u, pic->v, &has_alpha);
+    ok = e != NULL &&
+         vp8g_engine_import(e, rgba, 4 * w, pic->y, pic->u, pic->v, &has_alpha, sharp);
     pthread_mutex_unlock(&g_engine_lock);
     if (!ok) {
       set_error(pic, VP8_ENC_ERROR_OUT_OF_MEMORY);
@@ -313,25 +314,27 @@ static int import_packed(WebPPicture* pic, const uint8_t* src, int stride, int s
 }
 
 int WebPPictureImportRGB(WebPPicture* p, const uint8_t* s, int st) {
-  return (p && s) ? import_packed(p, s, st, 3, 0, 0) : 0;
+  return (p && s) ? import_packed(p, s, st, 3, 0, 0, 0) : 0;
 }
 int WebPPictureImportRGBA(WebPPicture* p, const uint8_t* s, int st) {
-  return (p && s) ? import_packed(p, s, st, 4, 0, 1) : 0;
+  return (p && s) ? import_packed(p, s, st, 4, 0, 1, 0) : 0;
 }
 int WebPPictureImportRGBX(WebPPicture* p, const uint8_t* s, int st) {
-  return (p && s) ? import_packed(p, s, st, 4, 0, 0) : 0;
+  return (p && s) ? import_packed(p, s, st, 4, 0, 0, 0) : 0;
 }
 int WebPPictureImportBGR(WebPPicture* p, const uint8_t* s, int st) {
-  return (p && s) ? import_packed(p, s, st, 3, 1, 0) : 0;
+  return (p && s) ? import_packed(p, s, st, 3, 1, 0, 0) : 0;
 }
 int WebPPictureImportBGRA(WebPPicture* p, const uint8_t* s, int st) {
-  return (p && s) ? import_packed(p, s, st, 4, 1, 1) : 0;
+  return (p && s) ? import_packed(p, s, st, 4, 1, 1, 0) : 0;
 }
 int WebPPictureImportBGRX(WebPPicture* p, const uint8_t* s, int st) {
-  return (p && s) ? import_packed(p, s, st, 4, 1, 0) : 0;
+  return (p && s) ? import_packed(p, s, st, 4, 1, 0, 0) : 0;
 }
 
-int WebPPictureARGBToYUVA(WebPPicture* p, WebPEncCSP csp) {   /* picture_csp_enc.c:629-656 */
+/* picture_csp_enc.c:622-664: ARGB container -> YUV420 through K1, or the
+ * sharp-YUV kernels when `sharp` */
+static int argb_to_yuva(WebPPicture* p, WebPEncCSP csp, int sharp) {
   if (p == NULL) return 0;
   if (p->argb == NULL) return set_error(p, VP8_ENC_ERROR_NULL_PARAMETER);
   if ((csp & WEBP_CSP_UV_MASK) != WEBP_YUV420)
@@ -350,12 +353,25 @@ int WebPPictureARGBToYUVA(WebPPicture* p, WebPEncCSP csp) {   /* picture_csp_enc
   const int keep_stride = p->argb_stride;
   p->use_argb = 0;
   p->memory_argb_ = NULL;   /* keep ARGB alive across the YUV allocation */
-  const int ok = import_packed(p, bgra, 4 * w, 4, 1, 1);
+  const int ok = import_packed(p, bgra, 4 * w, 4, 1, 1, sharp);
   p->memory_argb_ = keep_argb;
   p->argb = keep_ptr;
   p->argb_stride = keep_stride;
   free(bgra);
   return ok;
+}
+
+int WebPPictureARGBToYUVA(WebPPicture* p, WebPEncCSP csp) { return argb_to_yuva(p, csp, 0); }
+
+int WebPPictureSharpARGBToYUVA(WebPPicture* p) { return argb_to_yuva(p, WEBP_YUV420, 1); }
+int WebPPictureSmartARGBToYUVA(WebPPicture* p) { return WebPPictureSharpARGBToYUVA(p); }
+
+int WebPPictureARGBToYUVADithered(WebPPicture* p, WebPEncCSP csp, float dithering) {
+  /* dithered chroma (VP8Random, picture_csp_enc.c:520-560) is not part of
+   * this build: only dithering == 0 (the plain conversion) is accepted */
+  if (p == NULL) return 0;
+  if (dithering > 0.f) return set_error(p, VP8_ENC_ERROR_INVALID_CONFIGURATION);
+  return argb_to_yuva(p, csp, 0);
 }
 
 int WebPPictureHasTransparency(const WebPPicture* p) {   /* picture_csp_enc.c:69-81 */
@@ -397,11 +413,13 @@ int WebPEncode(const WebPConfig* config, WebPPicture* pic) {
   if (pic->stats != NULL) memset(pic->stats, 0, sizeof(*pic->stats));
   if (config->lossless) return set_error(pic, VP8_ENC_ERROR_INVALID_CONFIGURATION);
   vp8h_frame probe;
-  if (!vp8h_frame_init(&probe, config, pic->width, pic->height) ||
-      (config->preprocessing & 2) || (config->preprocessing & 4))
+  if (!vp8h_frame_init(&probe, config, pic->width, pic->height))
     return set_error(pic, VP8_ENC_ERROR_INVALID_CONFIGURATION);
   if (pic->use_argb || pic->y == NULL || pic->u == NULL || pic->v == NULL) {
-    if (!WebPPictureARGBToYUVA(pic, WEBP_YUV420)) return 0;
+    /* webp_enc.c:351-367 */
+    const int sharp = config->use_sharp_yuv || (config->preprocessing & 4);
+    if (!(sharp ? WebPPictureSharpARGBToYUVA(pic) : WebPPictureARGBToYUVA(pic, WEBP_YUV420)))
+      return 0;
   }
   if (pic->a != NULL && WebPPictureHasTransparency(pic))
     return set_error(pic, VP8_ENC_ERROR_INVALID_CONFIGURATION);

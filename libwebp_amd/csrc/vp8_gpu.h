@@ -116,6 +116,21 @@ int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
 int vp8g_launch_pack(const uint16_t* tokens, size_t tok_cap, int n, const uint64_t* off,
                      const uint32_t* size, uint32_t max_size, uint8_t* dst, void* stream);
 
+/* Sharp (iterative) RGB->YUV420 for n frames (hip/vp8_sharp.hip), the
+ * use_sharp_yuv import (sharpyuv/sharpyuv.c). scratch holds
+ * vp8g_sharp_frame_bytes(w, h) per frame, state one entry per frame; g2l/l2g
+ * are DEVICE copies of the sRGB tables (1026 + 514 entries, vp8h_sharp_tables).
+ * w and h must be >= 4 (smaller pictures take vp8g_launch_import). */
+typedef struct {
+  unsigned long long prev_sum;
+  int done, iters;
+} vp8g_sharp_state;
+size_t vp8g_sharp_frame_bytes(int w, int h);
+int vp8g_launch_sharp(const uint8_t* rgba, size_t frame_stride, int row_stride, int w, int h,
+                      int n, uint8_t* yuv, size_t yuv_frame_bytes, uint32_t* alpha_flags,
+                      uint8_t* scratch, vp8g_sharp_state* state, const uint32_t* g2l_dev,
+                      const uint32_t* l2g_dev, void* stream);
+
 /* synthetic syn-v1 frames straight into device memory */
 int vp8g_launch_synth(uint8_t* rgba, size_t frame_stride, int w, int h,
                       int first_frame, int n, int seed, void* stream);

@@ -17,7 +17,7 @@ class Config(C.Structure):
                 ("sns_strength", C.c_int), ("filter_strength", C.c_int),
                 ("filter_sharpness", C.c_int), ("filter_type", C.c_int),
                 ("partition_limit", C.c_int), ("preprocessing", C.c_int),
-                ("emulate_jpeg_size", C.c_int)]
+                ("emulate_jpeg_size", C.c_int), ("use_sharp_yuv", C.c_int)]
 
 
 class MBTrace(C.Structure):
@@ -39,6 +39,8 @@ def lib():
         _lib.vp8o_import_rgba.restype = C.c_int
         vp, i = C.c_void_p, C.c_int
         _lib.vp8o_import_rgba.argtypes = [vp, i, i, i, vp, vp, vp]
+        _lib.vp8o_sharp_import_rgba.argtypes = [vp, i, i, i, vp, vp, vp]
+        _lib.vp8o_sharp_tables.argtypes = [vp, vp]
         _lib.vp8o_encode_yuv.argtypes = [vp, vp, vp, i, i, i, i, vp, vp, vp]
         _lib.vp8o_encode_rgba.argtypes = [vp, i, i, i, vp, vp]
         _lib.vp8o_analyze.argtypes = [vp, vp, vp, i, i, i, i, vp, vp, vp]
@@ -65,15 +67,23 @@ def config(quality=75.0, method=4, **kw):
     return c
 
 
-def import_rgba(rgba):
+def import_rgba(rgba, sharp=False):
+    """RGBA -> (Y, U, V). sharp=True: the iterative sharp-YUV conversion the
+    reference applies for use_sharp_yuv (only from 4x4 up, like the
+    reference; smaller pictures take the regular conversion)."""
     rgba = np.ascontiguousarray(rgba, np.uint8)
     h, w = rgba.shape[:2]
     uw, uh = (w + 1) // 2, (h + 1) // 2
     y = np.empty((h, w), np.uint8)
     u = np.empty((uh, uw), np.uint8)
     v = np.empty((uh, uw), np.uint8)
-    ok = lib().vp8o_import_rgba(rgba.ctypes.data, w, h, 4 * w, y.ctypes.data,
-                                u.ctypes.data, v.ctypes.data)
+    if sharp and w >= 4 and h >= 4:
+        if (rgba[..., 3] != 255).any():
+            raise ValueError("non-opaque input is not restated by the oracle")
+        fn = lib().vp8o_sharp_import_rgba
+    else:
+        fn = lib().vp8o_import_rgba
+    ok = fn(rgba.ctypes.data, w, h, 4 * w, y.ctypes.data, u.ctypes.data, v.ctypes.data)
     if not ok:
         raise ValueError("non-opaque input is not restated by the oracle")
     return y, u, v
@@ -95,6 +105,13 @@ def encode_yuv(y, u, v, quality=75.0, method=4, trace=False, **kw):
     return (data, tr) if trace else data
 
 
+def sharp_tables():
+    g2l = np.empty(1026, np.uint32)
+    l2g = np.empty(514, np.uint32)
+    lib().vp8o_sharp_tables(g2l.ctypes.data, l2g.ctypes.data)
+    return g2l, l2g
+
+
 def encode_rgba(rgba, quality=75.0, method=4, **kw):
-    y, u, v = import_rgba(rgba)
+    y, u, v = import_rgba(rgba, sharp=bool(kw.pop("use_sharp_yuv", 0)))
     return encode_yuv(y, u, v, quality, method, **kw)

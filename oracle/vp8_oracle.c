@@ -1879,7 +1879,14 @@ size_t vp8o_encode_rgba(const uint8_t* rgba, int w, int h, int stride,
   if (!buf) return 0;
   uint8_t *Y = buf, *U = buf + (size_t)w * h, *V = U + (size_t)uw * uh;
   size_t r = 0;
-  if (vp8o_import_rgba(rgba, w, h, stride, Y, U, V))
+  /* sharp conversion only from 4x4 up (picture_csp_enc.c:165,493-496) */
+  const int sharp = cfg->use_sharp_yuv && w >= 4 && h >= 4;
+  int opaque = 1;
+  for (int j = 0; j < h && opaque; ++j)
+    for (int i = 0; i < w; ++i)
+      if (rgba[(size_t)j * stride + 4 * i + 3] != 0xff) { opaque = 0; break; }
+  if (opaque && (sharp ? vp8o_sharp_import_rgba(rgba, w, h, stride, Y, U, V)
+                       : vp8o_import_rgba(rgba, w, h, stride, Y, U, V)))
     r = vp8o_encode_yuv(Y, U, V, w, h, w, uw, cfg, out, NULL);
   free(buf);
   return r;

@@ -24,6 +24,7 @@ typedef struct {
   int partition_limit;    /* 0..100 */
   int preprocessing;      /* bit0: segment smoothing */
   int emulate_jpeg_size;  /* 0/1 */
+  int use_sharp_yuv;      /* 0/1: iterative RGB->YUV (sharp_oracle.c) */
 } vp8o_config;
 
 /* per-macroblock decisions, for stage-by-stage comparison with the GPU */
@@ -58,6 +59,13 @@ size_t vp8o_encode_rgba(const uint8_t* rgba, int w, int h, int stride,
 void vp8o_analyze(const uint8_t* y, const uint8_t* u, const uint8_t* v,
                   int w, int h, int y_stride, int uv_stride,
                   uint8_t* mb_alpha, int* uv_alpha_sum, int* histo256);
+
+/* sharp (iterative) RGBA -> YUV420 (sharp_oracle.c; sharpyuv/sharpyuv.c).
+ * Opaque input, width and height >= 4. */
+int vp8o_sharp_import_rgba(const uint8_t* rgba, int w, int h, int stride,
+                           uint8_t* y, uint8_t* u, uint8_t* v);
+/* the sRGB gamma tables of the sharp path (either pointer may be NULL) */
+void vp8o_sharp_tables(uint32_t g2l[1026], uint32_t l2g[514]);
 
 void vp8o_free(void* p);
 

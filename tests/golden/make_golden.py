@@ -38,7 +38,39 @@ def case(w, h, f, **kw):
             "segment_level": list(st.segment_level)}
 
 
+def sharp_section():
+    """use_sharp_yuv (sharpyuv/sharpyuv.c): plane hashes of
+    WebPPictureSharpARGBToYUVA and full bitstreams of WebPEncode on an ARGB
+    picture with use_sharp_yuv=1 (what cwebp -sharp_yuv does)."""
+    import numpy as np
+    sec = {"import": [], "encode": []}
+    for (w, h, f) in [(4, 4, 0), (5, 7, 1), (3, 9, 2), (17, 9, 2), (64, 48, 3), (333, 257, 3),
+                      (512, 512, 0), (1920, 1080, 0)]:
+        y, u, v = abi.picture_yuv(ref, syn_v1(w, h, f), sharp=True)
+        sec["import"].append({"w": w, "h": h, "frame": f, "y": sha(y.tobytes()),
+                              "u": sha(u.tobytes()), "v": sha(v.tobytes())})
+    # white noise: exercises the 10-bit clipping of the refinement
+    img = np.random.RandomState(11).randint(0, 256, (130, 200, 4)).astype(np.uint8)
+    img[..., 3] = 255
+    y, u, v = abi.picture_yuv(ref, img, sharp=True)
+    sec["noise_200x130_seed11"] = {"y": sha(y.tobytes()), "u": sha(u.tobytes()),
+                                   "v": sha(v.tobytes())}
+    for (w, h, f, q, m) in [(64, 48, 0, 75.0, 4), (333, 257, 5, 50.0, 6), (3, 3, 0, 75.0, 4),
+                            (128, 77, 2, 90.0, 5), (512, 512, 0, 75.0, 4),
+                            (1920, 1080, 0, 75.0, 4), (1920, 1080, 1, 75.0, 4)]:
+        sec["encode"].append(case(w, h, f, quality=q, method=m, use_sharp_yuv=1))
+    return sec
+
+
 def main():
+    if "--only-sharp" in sys.argv:
+        path = os.path.join(HERE, "kat.json")
+        kat = json.load(open(path))
+        kat["sharp"] = sharp_section()
+        with open(path, "w") as fh:
+            json.dump(kat, fh, indent=1)
+        print("updated sharp section")
+        return
     kat = {"survey": [], "sweep": [], "import": [], "bitstreams": {}}
     for f in (0, 7):
         kat["survey"].append(case(512, 512, f, quality=75.0, method=4))
@@ -77,6 +109,7 @@ def main():
         layout = json.loads(subprocess.check_output([exe]))
     with open(os.path.join(HERE, "abi_layout.json"), "w") as fh:
         json.dump(layout, fh, indent=1)
+    kat["sharp"] = sharp_section()
     with open(os.path.join(HERE, "kat.json"), "w") as fh:
         json.dump(kat, fh, indent=1)
     print("wrote", len(kat["survey"]), "survey,", len(kat["sweep"]), "sweep cases")

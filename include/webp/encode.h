@@ -268,6 +268,26 @@ WEBP_EXTERN int WebPPictureSharpARGBToYUVA(WebPPicture* picture);
 WEBP_EXTERN int WebPPictureSmartARGBToYUVA(WebPPicture* picture);
 WEBP_EXTERN int WebPPictureHasTransparency(const WebPPicture* picture);
 
+/* Picture utilities beside the encode path (host C, host buffers):
+ * ref encode.h:377-456, 510-529. */
+WEBP_EXTERN int WebPPlaneDistortion(const uint8_t* src, size_t src_stride,
+                                    const uint8_t* ref, size_t ref_stride,
+                                    int width, int height, size_t x_step,
+                                    int type, float* distortion, float* result);
+WEBP_EXTERN int WebPPictureDistortion(const WebPPicture* src,
+                                      const WebPPicture* ref, int metric_type,
+                                      float result[5]);
+WEBP_EXTERN int WebPPictureCrop(WebPPicture* picture, int left, int top,
+                                int width, int height);
+WEBP_EXTERN int WebPPictureView(const WebPPicture* src, int left, int top,
+                                int width, int height, WebPPicture* dst);
+WEBP_EXTERN int WebPPictureIsView(const WebPPicture* picture);
+WEBP_EXTERN int WebPPictureRescale(WebPPicture* picture, int width,
+                                   int height);
+WEBP_EXTERN int WebPPictureYUVAToARGB(WebPPicture* picture);
+WEBP_EXTERN void WebPCleanupTransparentArea(WebPPicture* picture);
+WEBP_EXTERN void WebPBlendAlpha(WebPPicture* picture, uint32_t background_rgb);
+
 /* Main entry point, ref encode.h:544. Returns 0 on error, reason in
  * picture->error_code (first error wins). */
 WEBP_EXTERN int WebPEncode(const WebPConfig* config, WebPPicture* picture);

@@ -110,6 +110,21 @@ def bind_encoder_api(lib):
         "WebPEncodeRGBA": (C.c_size_t, [C.c_void_p, C.c_int, C.c_int, C.c_int,
                                         C.c_float, P(P(C.c_uint8))]),
         "WebPFree": (None, [C.c_void_p]),
+        "WebPPictureCopy": (C.c_int, [P(WebPPicture), P(WebPPicture)]),
+        "WebPPlaneDistortion": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                          C.c_int, C.c_int, C.c_size_t, C.c_int,
+                                          P(C.c_float), P(C.c_float)]),
+        "WebPPictureDistortion": (C.c_int, [P(WebPPicture), P(WebPPicture), C.c_int,
+                                            P(C.c_float)]),
+        "WebPPictureCrop": (C.c_int, [P(WebPPicture), C.c_int, C.c_int, C.c_int, C.c_int]),
+        "WebPPictureView": (C.c_int, [P(WebPPicture), C.c_int, C.c_int, C.c_int, C.c_int,
+                                      P(WebPPicture)]),
+        "WebPPictureIsView": (C.c_int, [P(WebPPicture)]),
+        "WebPPictureRescale": (C.c_int, [P(WebPPicture), C.c_int, C.c_int]),
+        "WebPPictureYUVAToARGB": (C.c_int, [P(WebPPicture)]),
+        "WebPCleanupTransparentArea": (None, [P(WebPPicture)]),
+        "WebPBlendAlpha": (None, [P(WebPPicture), C.c_uint32]),
+        "WebPPictureHasTransparency": (C.c_int, [P(WebPPicture)]),
     }
     for name, (res, args) in sigs.items():
         if hasattr(lib, name):

@@ -10,6 +10,9 @@
 #include "vp8_host.h"
 #include "webp/encode.h"
 #include "webp/encode_gpu.h"
+#include "picture_internal.h"
+
+#define set_error vp8h_pic_error
 
 /* ---- misc (webp_enc.c:32-34, utils.c) ---- */
 
@@ -17,7 +20,7 @@ int WebPGetEncoderVersion(void) { return (1 << 16) | (3 << 8) | 2; }
 void* WebPMalloc(size_t size) { return malloc(size); }
 void WebPFree(void* ptr) { free(ptr); }
 
-static int set_error(const WebPPicture* pic, WebPEncodingError e) {   /* webp_enc.c:306-315 */
+int vp8h_pic_error(const WebPPicture* pic, WebPEncodingError e) {   /* webp_enc.c:306-315 */
   if (pic->error_code == VP8_ENC_OK) ((WebPPicture*)pic)->error_code = e;
   return 0;
 }
@@ -121,17 +124,17 @@ static int validate_picture(const WebPPicture* pic) {
   return 1;
 }
 
-static void reset_argb(WebPPicture* p) { p->memory_argb_ = NULL; p->argb = NULL; p->argb_stride = 0; }
-static void reset_yuva(WebPPicture* p) {
+void vp8h_pic_reset_argb(WebPPicture* p) { p->memory_argb_ = NULL; p->argb = NULL; p->argb_stride = 0; }
+void vp8h_pic_reset_yuva(WebPPicture* p) {
   p->memory_ = NULL;
   p->y = p->u = p->v = p->a = NULL;
   p->y_stride = p->uv_stride = p->a_stride = 0;
 }
 
-static int alloc_argb(WebPPicture* p) {
+int vp8h_pic_alloc_argb(WebPPicture* p) {
   if (!validate_picture(p)) return 0;
   free(p->memory_argb_);
-  reset_argb(p);
+  vp8h_pic_reset_argb(p);
   void* m = malloc((size_t)p->width * p->height * 4 + 64);
   if (!m) return set_error(p, VP8_ENC_ERROR_OUT_OF_MEMORY);
   p->memory_argb_ = m;
@@ -140,7 +143,7 @@ static int alloc_argb(WebPPicture* p) {
   return 1;
 }
 
-static int alloc_yuva(WebPPicture* p) {
+int vp8h_pic_alloc_yuva(WebPPicture* p) {
   if (!validate_picture(p)) return 0;
   const int has_alpha = (int)p->colorspace & WEBP_CSP_ALPHA_BIT;
   const int w = p->width, h = p->height;
@@ -148,7 +151,7 @@ static int alloc_yuva(WebPPicture* p) {
   const uint64_t ys = (uint64_t)w * h, uvs = (uint64_t)uvw * uvh;
   const uint64_t as = has_alpha ? (uint64_t)w * h : 0;
   free(p->memory_);
-  reset_yuva(p);
+  vp8h_pic_reset_yuva(p);
   uint8_t* m = (uint8_t*)malloc(ys + as + 2 * uvs);
   if (!m) return set_error(p, VP8_ENC_ERROR_OUT_OF_MEMORY);
   p->memory_ = m;
@@ -165,7 +168,7 @@ static int alloc_yuva(WebPPicture* p) {
 int WebPPictureAlloc(WebPPicture* p) {
   if (p != NULL) {
     WebPPictureFree(p);
-    return p->use_argb ? alloc_argb(p) : alloc_yuva(p);
+    return p->use_argb ? vp8h_pic_alloc_argb(p) : vp8h_pic_alloc_yuva(p);
   }
   return 1;
 }
@@ -174,8 +177,8 @@ void WebPPictureFree(WebPPicture* p) {
   if (p != NULL) {
     free(p->memory_);
     free(p->memory_argb_);
-    reset_argb(p);
-    reset_yuva(p);
+    vp8h_pic_reset_argb(p);
+    vp8h_pic_reset_yuva(p);
   }
 }
 
@@ -183,8 +186,8 @@ int WebPPictureCopy(const WebPPicture* src, WebPPicture* dst) {   /* picture_res
   if (src == NULL || dst == NULL) return 0;
   if (src == dst) return 1;
   *dst = *src;
-  reset_argb(dst);
-  reset_yuva(dst);
+  vp8h_pic_reset_argb(dst);
+  vp8h_pic_reset_yuva(dst);
   if (!WebPPictureAlloc(dst)) return 0;
   if (!src->use_argb) {
     const int uvw = (src->width + 1) >> 1, uvh = (src->height + 1) >> 1;
@@ -291,7 +294,7 @@ static int import_packed(WebPPicture* pic, const uint8_t* src, int stride, int s
     }
   }
   pic->colorspace = WEBP_YUV420;
-  int ok = alloc_yuva(pic);
+  int ok = vp8h_pic_alloc_yuva(pic);
   if (ok) {
     pthread_mutex_lock(&g_engine_lock);
     WebPConfig cfg;
@@ -421,6 +424,7 @@ int WebPEncode(const WebPConfig* config, WebPPicture* pic) {
     if (!(sharp ? WebPPictureSharpARGBToYUVA(pic) : WebPPictureARGBToYUVA(pic, WEBP_YUV420)))
       return 0;
   }
+  if (!config->exact) WebPCleanupTransparentArea(pic);   /* webp_enc.c:369-371 */
   if (pic->a != NULL && WebPPictureHasTransparency(pic))
     return set_error(pic, VP8_ENC_ERROR_INVALID_CONFIGURATION);
 

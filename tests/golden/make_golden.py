@@ -62,14 +62,30 @@ def sharp_section():
     return sec
 
 
+def tools_section():
+    """Picture utilities (crop/rescale/YUVA->ARGB/distortion/cleanup/blend):
+    the reference's answers on the fixed inputs of
+    tests/test_picture_tools.tools_answers."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_picture_tools import tools_answers
+    return tools_answers(ref)
+
+
+SECTIONS = {"sharp": sharp_section, "tools": tools_section}
+
+
 def main():
+    only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--only=")]
     if "--only-sharp" in sys.argv:
+        only.append("sharp")
+    if only:   # refresh some sections of an existing kat.json
         path = os.path.join(HERE, "kat.json")
         kat = json.load(open(path))
-        kat["sharp"] = sharp_section()
+        for name in only:
+            kat[name] = SECTIONS[name]()
         with open(path, "w") as fh:
             json.dump(kat, fh, indent=1)
-        print("updated sharp section")
+        print("updated", only)
         return
     kat = {"survey": [], "sweep": [], "import": [], "bitstreams": {}}
     for f in (0, 7):
@@ -110,6 +126,7 @@ def main():
     with open(os.path.join(HERE, "abi_layout.json"), "w") as fh:
         json.dump(layout, fh, indent=1)
     kat["sharp"] = sharp_section()
+    kat["tools"] = tools_section()
     with open(os.path.join(HERE, "kat.json"), "w") as fh:
         json.dump(kat, fh, indent=1)
     print("wrote", len(kat["survey"]), "survey,", len(kat["sweep"]), "sweep cases")

@@ -1108,6 +1108,7 @@ struct K3Args {
   uint8_t* mbinfo;
   uint16_t* mbcnt;
   vp8g_frame_result* results;
+  uint8_t* rerun;   // n x VP8G_RERUN_STATE_BYTES
 };
 
 // TR: the method >= 5 instantiation carries the trellis paths; m3/m4 frames
@@ -1146,10 +1147,16 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   uint16_t* tok_base = a.tokens + f * a.tok_cap;
   uint8_t* mbinfo = a.mbinfo + (size_t)f * nmb * VP8G_MBINFO_BYTES;
 
+  // partition-0 re-run (frame_enc.c:869-876): only the frames that overflowed
+  // run again, from the cost state their previous pass ended with
+  if (P->pass_mode == 2) return;
+  const bool rerun = P->pass_mode == 1;
+  uint8_t* rstate = a.rerun + (size_t)f * VP8G_RERUN_STATE_BYTES;
+
   // ---- frame init (whole workgroup)
   for (int s = gt; s < NSLOT; s += NW * K3T) {
     G.stats[s] = 0;
-    G.coeffs[s] = (&kVP8CoeffProba0[0][0][0][0])[s];
+    G.coeffs[s] = rerun ? rstate[s] : (&kVP8CoeffProba0[0][0][0][0])[s];
   }
   for (int s = tid; s < NSLOT; s += K3T) L.rdelta[s] = 0;
   for (int k = gt; k < 33; k += NW * K3T) G.mark[k] = 0;
@@ -1175,10 +1182,15 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   }
   if (tid == 0) { L.bar = 0; L.myabort = 0; }
   __syncthreads();
-  if (wk == 0) {
-    level_costs_w(G, tid);
-    refresh_hc(G, tid);
+  if (wk == 0) level_costs_w(G, tid);
+  __syncthreads();
+  if (rerun) {   // the level costs came from rstate[0..]; the probabilities are the loop-end ones
+    for (int s = gt; s < NSLOT; s += NW * K3T) G.coeffs[s] = rstate[NSLOT + s];
+    __syncthreads();
+  } else {       // first pass: the level costs are those of the default probabilities
+    for (int s = gt; s < NSLOT; s += NW * K3T) rstate[s] = G.coeffs[s];
   }
+  if (wk == 0) refresh_hc(G, tid);
   __syncthreads();
 
   const int rd_opt = P->rd_opt;
@@ -1232,7 +1244,10 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
           fold_from = mb;
           wbar(L);
           const int dirty = finalize_probas_wg(G, L, tid);
-          if (dirty) level_costs_w(G, tid);
+          if (dirty) {
+            level_costs_w(G, tid);
+            for (int s = tid; s < NSLOT; s += K3T) rstate[s] = G.coeffs[s];
+          }
           refresh_hc(G, tid);
           wbar(L);
           if (tid == 0) publish(&G.epoch, ep);
@@ -1590,6 +1605,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   // ---- frame epilogue: final probabilities and side results
   __syncthreads();
   if (wk == 0) {
+    for (int s = tid; s < NSLOT; s += K3T) rstate[NSLOT + s] = G.coeffs[s];
     finalize_probas_wg(G, L, tid);
     vp8g_frame_result* R = a.results + f;
     for (int s = tid; s < NSLOT; s += K3T) R->probas[s] = G.coeffs[s];
@@ -1667,7 +1683,7 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
                                   const uint8_t* segmap, const vp8g_frame_params* params,
                                   uint16_t* tokens, size_t tok_cap, uint8_t* mbinfo,
                                   uint16_t* mbcnt, int trellis, vp8g_frame_result* results,
-                                  void* stream) {
+                                  uint8_t* rerun_state, void* stream) {
   static int variant = -1;
   if (variant < 0) {   // WEBP_AMD_K3: 1 = single-wavefront reference kernel, 2/3/5/4 =
                        // 1/2/3/4 MB workers per frame, unset = default above
@@ -1681,7 +1697,7 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   a.yuv = yuv; a.yfb = yfb; a.w = w; a.h = h;
   a.mbw = (w + 15) >> 4; a.mbh = (h + 15) >> 4;
   a.segmap = segmap; a.params = params; a.tokens = tokens; a.tok_cap = tok_cap;
-  a.mbinfo = mbinfo; a.mbcnt = mbcnt; a.results = results;
+  a.mbinfo = mbinfo; a.mbcnt = mbcnt; a.results = results; a.rerun = rerun_state;
   if (variant == 2) return launch_k3<1>(a, n, trellis != 0, stream);
   if (variant == 3) return launch_k3<2>(a, n, trellis != 0, stream);
   if (variant == 4) return launch_k3<4>(a, n, trellis != 0, stream);

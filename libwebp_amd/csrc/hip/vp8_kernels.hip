@@ -645,6 +645,12 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
   const uint8_t* segmap = a.segmap + (size_t)f * nmb;
   uint16_t* tok_base = a.tokens + f * a.tok_cap;
   uint8_t* mbinfo = a.mbinfo + (size_t)f * nmb * VP8G_MBINFO_BYTES;
+  // this single-wavefront diagnostic kernel keeps no re-run state: it skips
+  // final frames and refuses a partition-0 re-run (error 3)
+  if (P->pass_mode != 0) {
+    if (P->pass_mode == 1 && lane == 0) a.results[f].error = 3;
+    return;
+  }
 
   // ---- frame init
   for (int s = lane; s < NSLOT; s += 64) {

@@ -117,6 +117,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   CHK(hipMalloc((void**)&b->d_tokens, N * b->tok_cap * sizeof(uint16_t)));
   CHK(hipMalloc((void**)&b->d_mbinfo, N * nmb * VP8G_MBINFO_BYTES));
   CHK(hipMalloc((void**)&b->d_mbcnt, N * nmb * sizeof(uint16_t)));
+  CHK(hipMalloc((void**)&b->d_rerun, N * VP8G_RERUN_STATE_BYTES));
   CHK(hipMalloc((void**)&b->d_results, N * sizeof(vp8g_frame_result)));
   CHK(hipMalloc((void**)&b->d_psize, N * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&b->d_emeta, N * sizeof(vp8g_emit_meta)));
@@ -151,7 +152,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   if (b->stream) hipStreamSynchronize(b->stream);
   hipFree(b->d_g2l); hipFree(b->d_rgba); hipFree(b->d_yuv); hipFree(b->d_aflags); hipFree(b->d_alpha);
   hipFree(b->d_uva); hipFree(b->d_segmap); hipFree(b->d_params); hipFree(b->d_tokens);
-  hipFree(b->d_mbinfo); hipFree(b->d_mbcnt); hipFree(b->d_results); hipFree(b->d_psize); hipFree(b->d_emeta);
+  hipFree(b->d_mbinfo); hipFree(b->d_mbcnt); hipFree(b->d_rerun); hipFree(b->d_results); hipFree(b->d_psize); hipFree(b->d_emeta);
   hipFree(b->d_poff); hipFree(b->d_part);
   hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs); hipFree(b->d_nbuf);
   hipFree(b->d_eimg);
@@ -194,13 +195,6 @@ static void frame_head(WebPGpuBatch* b, int f) {
   vp8h_bw_free(&b->p0[f]);
   if (b->err[f] != VP8_ENC_OK) return;
   if (res->error) { b->err[f] = VP8_ENC_ERROR_OUT_OF_MEMORY; return; }
-  /* partition-0 overflow retry (frame_enc.c:869-876) is not implemented on
-   * the GPU path yet: report it instead of emitting a different stream */
-  if (fr->max_i4_header_bits > 0 &&
-      res->size_p0 + (uint64_t)fr->seg_hdr_size > VP8H_P0_LIMIT) {
-    b->err[f] = VP8_ENC_ERROR_PARTITION0_OVERFLOW;
-    return;
-  }
   b->err[f] = vp8h_build_p0(fr, res, b->h_mbinfo + (size_t)f * b->nmb * VP8G_MBINFO_BYTES,
                             &b->p0[f], b->hdr + 2 * f);
 }
@@ -280,6 +274,7 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
     vp8h_frame_init(&b->frames[f], &b->cfg, b->w, b->h);
     vp8h_setup_segments(&b->frames[f], b->h_alpha + f * nmb, b->h_uva + f * nmb,
                         b->h_segmap + f * nmb, &b->h_params[f]);
+    b->h_params[f].pass_mode = 0;
   }
   CHK(hipMemcpyAsync(b->d_segmap, b->h_segmap, n * nmb, hipMemcpyHostToDevice, st));
   CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
@@ -288,7 +283,7 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   CHK(hipEventRecord(b->ev[2], st));
   if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
                           b->tok_cap, b->d_mbinfo, b->d_mbcnt, b->cfg.method >= 5, b->d_results,
-                          st))
+                          b->d_rerun, st))
     return 0;
   CHK(hipEventRecord(b->ev[3], st));
   CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
@@ -296,6 +291,39 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   CHK(hipMemcpyAsync(b->h_mbinfo, b->d_mbinfo, n * nmb * VP8G_MBINFO_BYTES,
                      hipMemcpyDeviceToHost, st));
   CHK(hipStreamSynchronize(st));
+  /* partition-0 overflow (frame_enc.c:869-876): the frames whose header
+   * estimate exceeds the limit encode again with half the I4 header budget,
+   * starting from the cost state their previous pass ended with (K3
+   * pass_mode 1); the others are skipped (pass_mode 2). Until none overflows
+   * or the budget reaches 0. */
+  for (;;) {
+    int reruns = 0;
+    for (int f = 0; f < n; ++f) {
+      vp8h_frame* fr = &b->frames[f];
+      vp8g_frame_params* P = &b->h_params[f];
+      P->pass_mode = 2;
+      if (b->err[f] != VP8_ENC_OK || b->h_results[f].error) continue;
+      if (fr->max_i4_header_bits > 0 &&
+          b->h_results[f].size_p0 + (uint64_t)fr->seg_hdr_size > VP8H_P0_LIMIT) {
+        fr->max_i4_header_bits >>= 1;
+        P->max_i4_header_bits = fr->max_i4_header_bits;
+        P->pass_mode = 1;
+        ++reruns;
+      }
+    }
+    if (!reruns) break;
+    CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
+                       hipMemcpyHostToDevice, st));
+    if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params,
+                            b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mbcnt, b->cfg.method >= 5,
+                            b->d_results, b->d_rerun, st))
+      return 0;
+    CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
+                       hipMemcpyDeviceToHost, st));
+    CHK(hipMemcpyAsync(b->h_mbinfo, b->d_mbinfo, n * nmb * VP8G_MBINFO_BYTES,
+                       hipMemcpyDeviceToHost, st));
+    CHK(hipStreamSynchronize(st));
+  }
   if (!b->host_emit) {   /* K4 on the device, sized from the token counts */
     uint32_t max_ntok = 0, max_seg = 0;
     size_t segs = 0, words = 0;

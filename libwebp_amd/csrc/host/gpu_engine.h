@@ -31,6 +31,7 @@ struct WebPGpuBatch {
   uint16_t* d_tokens;
   uint8_t* d_mbinfo;
   uint16_t* d_mbcnt;         /* K3 scratch: tokens per MB */
+  uint8_t* d_rerun;          /* K3 cost state for partition-0 re-runs */
   vp8g_frame_result* d_results;
   uint32_t* d_psize;         /* partition-1 bytes per frame (K4) */
   vp8g_emit_meta* d_emeta;   /* K4 per-frame bookkeeping */

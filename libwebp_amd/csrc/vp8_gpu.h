@@ -49,8 +49,16 @@ typedef struct {
   int32_t method;
   int32_t use_derr;      /* U/V DC error diffusion (quality <= 98) */
   int32_t max_count;     /* cost-refresh period (frame_enc.c:785,800) */
-  int32_t pad[3];
+  int32_t pass_mode;     /* 0 first pass; 1 partition-0 re-run (frame_enc.c:869-876):
+                            start from the previous pass's cost state in
+                            rerun_state; 2 frame already final: skip */
+  int32_t pad[2];
 } vp8g_frame_params;
+
+/* per-frame cost state K3 leaves for a partition-0 re-run: the
+ * probabilities the level-cost tables were last computed from, then the
+ * probabilities at the end of the MB loop (before the final refresh) */
+#define VP8G_RERUN_STATE_BYTES (2 * VP8G_NUM_SLOTS)
 
 typedef struct {
   uint32_t ntokens;
@@ -88,7 +96,7 @@ int vp8g_launch_encode(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h,
                        int n, const uint8_t* segmap,
                        const vp8g_frame_params* params, uint16_t* tokens,
                        size_t tok_cap, uint8_t* mbinfo, uint16_t* mbcnt, int trellis,
-                       vp8g_frame_result* results, void* stream);
+                       vp8g_frame_result* results, uint8_t* rerun_state, void* stream);
 
 /* K4: boolean coder for the token partition, parallel inside each frame
  * (hip/vp8_emit.hip). Per-frame bookkeeping: ntok, the segment count and the

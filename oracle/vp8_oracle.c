@@ -20,6 +20,9 @@
 
 typedef int64_t score_t;
 
+static int g_passes;   /* passes of the last encode (> 1: partition-0 retry) */
+static uint64_t g_size_p0;   /* header estimate of the last pass (1/256 bit) */
+
 static const uint8_t kZz[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
 static const uint8_t kBand[17] = {0, 1, 2, 3, 6, 4, 5, 6, 6, 6, 6, 6, 6, 6, 6, 7, 0};
 
@@ -1798,6 +1801,7 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
   analyze(e);
 
   /* VP8EncTokenLoop with pass = 1 (and the partition-0 overflow retry) */
+  g_passes = 0;
   const int max_count = (nmb >> 3) < 96 ? 96 : (nmb >> 3);
   BW part1;
   bw_init(&part1);
@@ -1838,6 +1842,8 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
       it_save_boundary(&it, e);
     } while (it_next(&it, e));
     size_p0 += e->seg_hdr_size;
+    ++g_passes;
+    g_size_p0 = size_p0;
     if (e->max_i4_header_bits > 0 && size_p0 > P0_LIMIT) {
       e->max_i4_header_bits >>= 1;
       continue;
@@ -1893,3 +1899,5 @@ size_t vp8o_encode_rgba(const uint8_t* rgba, int w, int h, int stride,
 }
 
 void vp8o_free(void* p) { free(p); }
+int vp8o_last_pass_count(void) { return g_passes; }
+double vp8o_last_p0_fraction(void) { return (double)g_size_p0 / (double)P0_LIMIT; }

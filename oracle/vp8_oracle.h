@@ -68,6 +68,11 @@ int vp8o_sharp_import_rgba(const uint8_t* rgba, int w, int h, int stride,
 void vp8o_sharp_tables(uint32_t g2l[1026], uint32_t l2g[514]);
 
 void vp8o_free(void* p);
+/* number of MB-loop passes of the last vp8o_encode_* call (> 1 when the
+ * partition-0 overflow retry of frame_enc.c:869-876 ran) */
+int vp8o_last_pass_count(void);
+/* header-bit estimate of the last pass over the partition-0 limit */
+double vp8o_last_p0_fraction(void);
 
 #ifdef __cplusplus
 }

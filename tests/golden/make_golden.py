@@ -71,7 +71,18 @@ def tools_section():
     return tools_answers(ref)
 
 
-SECTIONS = {"sharp": sharp_section, "tools": tools_section}
+def p0_section():
+    """Partition-0 overflow retry (frame_enc.c:869-876): a 5120x5120 syn-v1
+    frame at q95 m4 overflows the partition-0 estimate twice and is encoded in
+    3 passes (pass count from the oracle restatement)."""
+    from oracle import oracle
+    c = case(5120, 5120, 0, quality=95.0, method=4)
+    oracle.encode_rgba(syn_v1(5120, 5120, 0), quality=95.0, method=4)
+    c["passes"] = oracle.lib().vp8o_last_pass_count()
+    return [c]
+
+
+SECTIONS = {"sharp": sharp_section, "tools": tools_section, "p0_overflow": p0_section}
 
 
 def main():
@@ -127,6 +138,7 @@ def main():
         json.dump(layout, fh, indent=1)
     kat["sharp"] = sharp_section()
     kat["tools"] = tools_section()
+    kat["p0_overflow"] = p0_section()
     with open(os.path.join(HERE, "kat.json"), "w") as fh:
         json.dump(kat, fh, indent=1)
     print("wrote", len(kat["survey"]), "survey,", len(kat["sweep"]), "sweep cases")

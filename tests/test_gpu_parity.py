@@ -127,3 +127,22 @@ def test_survey_kat_4096_q90_m6(gpu, kat):
     enc.close()
     assert len(out) == c["size"] and sha(out) == c["sha256"]
     print("4096x4096 q90 m6: k_encode %.0f ms" % (st[6] / 1e3))
+
+
+def test_p0_overflow_rerun(gpu, kat):
+    """Partition-0 overflow retry on the GPU (K3 pass_mode 1): a 5120x5120
+    syn-v1 frame at q95 m4 needs 3 passes; the bitstream equals the
+    reference's."""
+    import torch
+    (c,) = kat["p0_overflow"]
+    w, h = c["w"], c["h"]
+    buf = torch.empty(w * h * 4, dtype=torch.uint8, device="cuda")
+    gpu.synth_device(buf.data_ptr(), w, h, c["frame"], 1)
+    torch.cuda.synchronize()
+    enc = gpu.GpuBatch(w, h, 1, **c["params"])
+    enc.encode_device(buf.data_ptr(), 1)
+    out = enc.output(0)
+    err = enc.error(0)
+    enc.close()
+    assert err == 0
+    assert len(out) == c["size"] and sha(out) == c["sha256"]

@@ -74,3 +74,13 @@ def test_oracle_rejects_transparency():
     img[3, 3, 3] = 7
     with pytest.raises(ValueError):
         oracle.import_rgba(img)
+
+
+def test_oracle_p0_overflow_retry(kat):
+    """Partition-0 overflow: the restatement re-runs the MB loop with a halved
+    I4 header budget (frame_enc.c:869-876) and lands on the reference's
+    bitstream (5120x5120 q95 m4: 3 passes)."""
+    (c,) = kat["p0_overflow"]
+    out = oracle.encode_rgba(syn_v1(c["w"], c["h"], c["frame"]), **c["params"])
+    assert oracle.lib().vp8o_last_pass_count() == c["passes"] > 1
+    assert len(out) == c["size"] and sha(out) == c["sha256"]

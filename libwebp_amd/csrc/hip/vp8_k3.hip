@@ -993,46 +993,20 @@ __device__ __forceinline__ void publish(int32_t* p, int32_t v) {
 // accumulate; counters that would cross the halving threshold inside the MB
 // are replayed token by token (VP8RecordStats, cost_enc.h:45-56).
 __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t row0,
-                         uint16_t* tok_base) {
-  // MBs [i0, i1) of this worker's row (first MB row0): append their tokens to
-  // the frame's compact stream, then add their statistics in one step.
+                         uint16_t* tok_base, uint32_t* mboff) {
+  // MBs [i0, i1) of this worker's row (first MB row0): record where their
+  // tokens go in the frame's compact stream (moved there at frame end, see
+  // compact_tokens), then add their statistics in one step.
   // Called once every earlier MB is folded (G.fold_ptr == i0).
   const uint32_t base = G.ntok;
-  const uint32_t wv = (uint32_t)tid >> 6, ln = (uint32_t)tid & 63;
-  uint32_t off = 0;
+  const uint32_t ln = (uint32_t)tid & 63;
   uint32_t total = 0;
   for (uint32_t i = i0; i < i1; ++i) total += L.rowcnt[i - row0];
-  if ((uint64_t)base + total <= (uint64_t)i0 * VP8G_MAX_TOKENS_PER_MB) {
-    // the destination lies below every source slot of the range: the four
-    // waves copy whole MBs round-robin, loads of different MBs in flight
+  if (tid == 0) {
+    uint32_t off = base;
     for (uint32_t i = i0; i < i1; ++i) {
-      const uint32_t n = L.rowcnt[i - row0];
-      if (((i - i0) & 3) == wv) {
-        const uint16_t* src = tok_base + (size_t)i * VP8G_MAX_TOKENS_PER_MB;
-        uint16_t* dst = tok_base + base + off;
-        uint32_t c = ln;
-        for (; c + 192 < n; c += 256) {
-          const uint16_t t0 = src[c], t1 = src[c + 64], t2 = src[c + 128], t3 = src[c + 192];
-          dst[c] = t0; dst[c + 64] = t1; dst[c + 128] = t2; dst[c + 192] = t3;
-        }
-        for (; c < n; c += 64) dst[c] = src[c];
-      }
-      off += n;
-    }
-  } else {
-    // first rows of a dense frame: destination may overlap a later source;
-    // chunk by chunk, each chunk read before any of it is overwritten
-    for (uint32_t i = i0; i < i1; ++i) {
-      const uint32_t n = L.rowcnt[i - row0];
-      const uint16_t* src = tok_base + (size_t)i * VP8G_MAX_TOKENS_PER_MB;
-      uint16_t* dst = tok_base + base + off;
-      for (uint32_t c0 = 0; c0 < n; c0 += K3T) {
-        const bool v = c0 + tid < n;
-        const uint16_t t = v ? src[c0 + tid] : (uint16_t)0;
-        wbar(L);
-        if (v) dst[c0 + tid] = t;
-      }
-      off += n;
+      mboff[i] = off;
+      off += L.rowcnt[i - row0];
     }
   }
   if (tid == 0) L.mark_any = 0;
@@ -1054,15 +1028,18 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
   }
   wbar(L);
   if (L.mark_any) {
-    // exact in-order replay of the marked counters by wave 0: 64 tokens at a
-    // time; the tokens of one marked counter in a group are applied at once
-    // unless the group reaches the halving point, then one by one
+    // exact in-order replay of the marked counters by wave 0, MB by MB from
+    // the per-MB token slots, 64 tokens at a time; the tokens of one marked
+    // counter in a group are applied at once unless the group reaches the
+    // halving point, then one by one
     if (tid < 64) {
-      const uint16_t* tk = tok_base + base;
-      uint32_t nxt = ln < total ? tk[ln] : 0x4000u;
-      for (uint32_t k0 = 0; k0 < total; k0 += 64) {
+     for (uint32_t i = i0; i < i1; ++i) {
+      const uint32_t n = L.rowcnt[i - row0];
+      const uint16_t* tk = tok_base + (size_t)i * VP8G_MAX_TOKENS_PER_MB;
+      uint32_t nxt = ln < n ? tk[ln] : 0x4000u;
+      for (uint32_t k0 = 0; k0 < n; k0 += 64) {
         const uint32_t t = nxt;
-        nxt = (k0 + 64 + ln < total) ? tk[k0 + 64 + ln] : 0x4000u;
+        nxt = (k0 + 64 + ln < n) ? tk[k0 + 64 + ln] : 0x4000u;
         const int sl = (t & 0x4000) ? 0 : tok_stat_slot(t);
         const bool pend = !(t & 0x4000) && ((G.mark[sl >> 5] >> (sl & 31)) & 1u);
         uint64_t pm = __ballot(pend);
@@ -1086,6 +1063,7 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
           pm &= ~mm;
         }
       }
+     }
     }
     wbar(L);
     for (int k = tid; k < 33; k += K3T) G.mark[k] = 0;
@@ -1097,6 +1075,67 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
   }
 }
 
+// Frame end: move every MB's tokens from its VP8G_MAX_TOKENS_PER_MB slot to
+// its offset in the compact stream (mboff, raster order), with the whole
+// workgroup. A destination never lies above its own source, but it may
+// overlap an EARLIER MB's slot, so MBs go in windows [i0, i1) whose
+// destinations all lie below slot i0: inside a window every copy is
+// independent. An MB whose destination reaches into its own slot is moved
+// alone, chunk by chunk (each chunk read before it is written; writes stay
+// below the next chunk). The windows grow geometrically (a handful per frame).
+__device__ void compact_tokens(K3G& G, uint16_t* tok_base, const uint32_t* mboff, int nmb) {
+  const int T = blockDim.x, t = threadIdx.x, wv = t >> 6, nwv = T >> 6, ln = t & 63;
+  const uint32_t total = G.ntok;
+  uint32_t i0 = 1;   // MB 0 is already in place
+  while (i0 < (uint32_t)nmb) {
+    if (t == 0) {    // largest i1 with end(i1 - 1) <= slot(i0)
+      const uint64_t lim = (uint64_t)i0 * VP8G_MAX_TOKENS_PER_MB;
+      uint32_t lo = i0, hi = (uint32_t)nmb;   // end(k - 1) = mboff[k] (or total)
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        const uint64_t e = mid < (uint32_t)nmb ? mboff[mid] : total;
+        if (e <= lim) lo = mid; else hi = mid - 1;
+      }
+      G.mark[0] = lo;
+    }
+    __syncthreads();
+    const uint32_t i1 = G.mark[0];
+    __syncthreads();
+    if (i1 > i0) {
+      for (uint32_t i = i0 + wv; i < i1; i += nwv) {
+        const uint32_t d = mboff[i];
+        const uint32_t n = (i + 1 < (uint32_t)nmb ? mboff[i + 1] : total) - d;
+        const uint16_t* src = tok_base + (size_t)i * VP8G_MAX_TOKENS_PER_MB;
+        uint16_t* dst = tok_base + d;
+        if (dst == src) continue;
+        uint32_t c = ln;
+        for (; c + 192 < n; c += 256) {
+          const uint16_t t0 = src[c], t1 = src[c + 64], t2 = src[c + 128], t3 = src[c + 192];
+          dst[c] = t0; dst[c + 64] = t1; dst[c + 128] = t2; dst[c + 192] = t3;
+        }
+        for (; c < n; c += 64) dst[c] = src[c];
+      }
+      i0 = i1;
+    } else {
+      const uint32_t d = mboff[i0];
+      const uint32_t n = (i0 + 1 < (uint32_t)nmb ? mboff[i0 + 1] : total) - d;
+      const uint16_t* src = tok_base + (size_t)i0 * VP8G_MAX_TOKENS_PER_MB;
+      uint16_t* dst = tok_base + d;
+      if (dst != src) {
+        for (uint32_t c0 = 0; c0 < n; c0 += (uint32_t)T) {
+          const uint32_t c = c0 + (uint32_t)t;
+          const uint16_t v = c < n ? src[c] : (uint16_t)0;
+          __syncthreads();
+          if (c < n) dst[c] = v;
+        }
+      }
+      i0 += 1;
+    }
+    __syncthreads();
+  }
+  if (t == 0) G.mark[0] = 0;
+}
+
 struct K3Args {
   const uint8_t* yuv;
   size_t yfb;
@@ -1106,7 +1145,7 @@ struct K3Args {
   uint16_t* tokens;
   size_t tok_cap;
   uint8_t* mbinfo;
-  uint16_t* mbcnt;
+  uint32_t* mboff;   // n x nmb: compact-stream offset of each MB's tokens
   vp8g_frame_result* results;
   uint8_t* rerun;   // n x VP8G_RERUN_STATE_BYTES
 };
@@ -1146,6 +1185,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   const uint8_t* segmap = a.segmap + (size_t)f * nmb;
   uint16_t* tok_base = a.tokens + f * a.tok_cap;
   uint8_t* mbinfo = a.mbinfo + (size_t)f * nmb * VP8G_MBINFO_BYTES;
+  uint32_t* mboff = a.mboff + (size_t)f * nmb;
 
   // partition-0 re-run (frame_enc.c:869-876): only the frames that overflowed
   // run again, from the cost state their previous pass ended with
@@ -1240,7 +1280,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
           // everything before this MB: rows above folded by their owners,
           // this row's earlier MBs folded here
           if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from)) break;
-          fold_mbs(G, L, tid, fold_from, mb, (uint32_t)y * mbw, tok_base);
+          fold_mbs(G, L, tid, fold_from, mb, (uint32_t)y * mbw, tok_base, mboff);
           fold_from = mb;
           wbar(L);
           const int dirty = finalize_probas_wg(G, L, tid);
@@ -1597,12 +1637,15 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
     if (L.myabort) break;
     // row end: fold this row's remaining MBs once the rows above are folded
     if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from)) break;
-    fold_mbs(G, L, tid, fold_from, (uint32_t)(y + 1) * mbw, (uint32_t)y * mbw, tok_base);
+    fold_mbs(G, L, tid, fold_from, (uint32_t)(y + 1) * mbw, (uint32_t)y * mbw, tok_base,
+             mboff);
     wbar(L);
     K3_STAMP(7);
   }
 
   // ---- frame epilogue: final probabilities and side results
+  __syncthreads();
+  if (!G.abort && !G.tok_err) compact_tokens(G, tok_base, mboff, nmb);
   __syncthreads();
   if (wk == 0) {
     for (int s = tid; s < NSLOT; s += K3T) rstate[NSLOT + s] = G.coeffs[s];
@@ -1682,7 +1725,7 @@ static int launch_k3_default(const K3Args& a, int n, bool trellis, void* stream)
 extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, int n,
                                   const uint8_t* segmap, const vp8g_frame_params* params,
                                   uint16_t* tokens, size_t tok_cap, uint8_t* mbinfo,
-                                  uint16_t* mbcnt, int trellis, vp8g_frame_result* results,
+                                  uint32_t* mboff, int trellis, vp8g_frame_result* results,
                                   uint8_t* rerun_state, void* stream) {
   static int variant = -1;
   if (variant < 0) {   // WEBP_AMD_K3: 1 = single-wavefront reference kernel, 2/3/5/4 =
@@ -1697,7 +1740,7 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   a.yuv = yuv; a.yfb = yfb; a.w = w; a.h = h;
   a.mbw = (w + 15) >> 4; a.mbh = (h + 15) >> 4;
   a.segmap = segmap; a.params = params; a.tokens = tokens; a.tok_cap = tok_cap;
-  a.mbinfo = mbinfo; a.mbcnt = mbcnt; a.results = results; a.rerun = rerun_state;
+  a.mbinfo = mbinfo; a.mboff = mboff; a.results = results; a.rerun = rerun_state;
   if (variant == 2) return launch_k3<1>(a, n, trellis != 0, stream);
   if (variant == 3) return launch_k3<2>(a, n, trellis != 0, stream);
   if (variant == 4) return launch_k3<4>(a, n, trellis != 0, stream);

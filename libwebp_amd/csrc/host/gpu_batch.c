@@ -116,7 +116,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   CHK(hipMalloc((void**)&b->d_params, N * sizeof(vp8g_frame_params)));
   CHK(hipMalloc((void**)&b->d_tokens, N * b->tok_cap * sizeof(uint16_t)));
   CHK(hipMalloc((void**)&b->d_mbinfo, N * nmb * VP8G_MBINFO_BYTES));
-  CHK(hipMalloc((void**)&b->d_mbcnt, N * nmb * sizeof(uint16_t)));
+  CHK(hipMalloc((void**)&b->d_mboff, N * nmb * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&b->d_rerun, N * VP8G_RERUN_STATE_BYTES));
   CHK(hipMalloc((void**)&b->d_results, N * sizeof(vp8g_frame_result)));
   CHK(hipMalloc((void**)&b->d_psize, N * sizeof(uint32_t)));
@@ -152,7 +152,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   if (b->stream) hipStreamSynchronize(b->stream);
   hipFree(b->d_g2l); hipFree(b->d_rgba); hipFree(b->d_yuv); hipFree(b->d_aflags); hipFree(b->d_alpha);
   hipFree(b->d_uva); hipFree(b->d_segmap); hipFree(b->d_params); hipFree(b->d_tokens);
-  hipFree(b->d_mbinfo); hipFree(b->d_mbcnt); hipFree(b->d_rerun); hipFree(b->d_results); hipFree(b->d_psize); hipFree(b->d_emeta);
+  hipFree(b->d_mbinfo); hipFree(b->d_mboff); hipFree(b->d_rerun); hipFree(b->d_results); hipFree(b->d_psize); hipFree(b->d_emeta);
   hipFree(b->d_poff); hipFree(b->d_part);
   hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs); hipFree(b->d_nbuf);
   hipFree(b->d_eimg);
@@ -282,7 +282,7 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   t2 = now_us();
   CHK(hipEventRecord(b->ev[2], st));
   if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
-                          b->tok_cap, b->d_mbinfo, b->d_mbcnt, b->cfg.method >= 5, b->d_results,
+                          b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5, b->d_results,
                           b->d_rerun, st))
     return 0;
   CHK(hipEventRecord(b->ev[3], st));
@@ -315,7 +315,7 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
     CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
                        hipMemcpyHostToDevice, st));
     if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params,
-                            b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mbcnt, b->cfg.method >= 5,
+                            b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5,
                             b->d_results, b->d_rerun, st))
       return 0;
     CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),

@@ -30,7 +30,7 @@ struct WebPGpuBatch {
   vp8g_frame_params* d_params;
   uint16_t* d_tokens;
   uint8_t* d_mbinfo;
-  uint16_t* d_mbcnt;         /* K3 scratch: tokens per MB */
+  uint32_t* d_mboff;         /* K3 scratch: compact-stream offset per MB */
   uint8_t* d_rerun;          /* K3 cost state for partition-0 re-runs */
   vp8g_frame_result* d_results;
   uint32_t* d_psize;         /* partition-1 bytes per frame (K4) */

@@ -90,12 +90,13 @@ int vp8g_launch_analysis(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int 
 
 /* K3: RD search + tokens. Each frame's tokens end up as one compact stream
  * at the start of its tok_cap region (per-MB slots of
- * VP8G_MAX_TOKENS_PER_MB are used as scratch); mbcnt is scratch of n * nmb
- * uint16. trellis != 0 reserves the trellis LDS (method >= 5). */
+ * VP8G_MAX_TOKENS_PER_MB are used as scratch); mboff is scratch of n * nmb
+ * uint32 (each MB's offset in the compact stream). trellis != 0 reserves the
+ * trellis LDS (method >= 5). */
 int vp8g_launch_encode(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h,
                        int n, const uint8_t* segmap,
                        const vp8g_frame_params* params, uint16_t* tokens,
-                       size_t tok_cap, uint8_t* mbinfo, uint16_t* mbcnt, int trellis,
+                       size_t tok_cap, uint8_t* mbinfo, uint32_t* mboff, int trellis,
                        vp8g_frame_result* results, uint8_t* rerun_state, void* stream);
 
 /* K4: boolean coder for the token partition, parallel inside each frame

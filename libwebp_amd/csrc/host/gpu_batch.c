@@ -78,9 +78,22 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   if (!config || width <= 0 || height <= 0 || width > WEBP_MAX_DIMENSION ||
       height > WEBP_MAX_DIMENSION || max_frames <= 0)
     return NULL;
-  if (!WebPValidateConfig(config) || config->lossless) return NULL;
+  if (!WebPValidateConfig(config)) return NULL;
   WebPGpuBatch* b = (WebPGpuBatch*)calloc(1, sizeof(*b));
   if (!b) return NULL;
+  if (config->lossless) {   /* VP8L engine (host/vp8l_batch.c) */
+    b->device = device;
+    b->w = width; b->h = height;
+    b->max_frames = max_frames;
+    b->cfg = *config;
+    b->threads = host_threads > 0 ? host_threads : default_threads();
+    CHK(hipSetDevice(device));
+    CHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+    for (int i = 0; i < 6; ++i) CHK(hipEventCreate(&b->ev[i]));
+    b->l = vp8l_engine_new(width, height, max_frames, config->method);
+    if (!b->l) goto fail;
+    return b;
+  }
   vp8h_frame probe;
   if (!vp8h_frame_init(&probe, config, width, height)) { free(b); return NULL; }
   pthread_once(&g_gamma_once, gamma_init);
@@ -161,6 +174,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipHostFree(b->h_segmap); hipHostFree(b->h_params); hipHostFree(b->h_mbinfo);
   hipHostFree(b->h_results); hipHostFree(b->h_tokens); hipHostFree(b->h_psize);
   hipHostFree(b->h_part); hipHostFree(b->h_emeta); hipHostFree(b->h_poff);
+  vp8l_engine_free(b->l);
   for (int i = 0; i < 6; ++i)
     if (b->ev[i]) hipEventDestroy(b->ev[i]);
   if (b->stream) hipStreamDestroy(b->stream);
@@ -481,7 +495,6 @@ static int run_rgba(WebPGpuBatch* b, const void* rgba_dev, size_t fstride, int r
   if (rstride < 4 * b->w) return 0;
   if (n > 1 && fstride < (size_t)rstride * b->h) return 0;
   CHK(hipSetDevice(b->device));
-  for (int f = 0; f < n; ++f) b->err[f] = VP8_ENC_OK;
   if (stream) {   /* order after the caller's producer work */
     hipEvent_t ev;
     CHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -489,6 +502,12 @@ static int run_rgba(WebPGpuBatch* b, const void* rgba_dev, size_t fstride, int r
     CHK(hipStreamWaitEvent(b->stream, ev, 0));
     hipEventDestroy(ev);
   }
+  if (b->l) {   /* lossless (VP8L) */
+    const int ok = vp8l_engine_run(b, (const uint8_t*)rgba_dev, fstride, rstride, n);
+    b->timings[5] = now_us() - t0;
+    return ok;
+  }
+  for (int f = 0; f < n; ++f) b->err[f] = VP8_ENC_OK;
   CHK(hipMemsetAsync(b->d_aflags, 0, n * sizeof(uint32_t), b->stream));
   CHK(hipEventRecord(b->ev[0], b->stream));
   b->ev0_recorded = 1;
@@ -536,21 +555,25 @@ fail:
 }
 
 size_t WebPGpuBatchOutputSize(const WebPGpuBatch* b, int f) {
-  return (b && f >= 0 && f < b->last_n) ? b->out_size[f] : 0;
+  if (!b || f < 0 || f >= b->last_n) return 0;
+  return b->l ? b->l->out_size[f] : b->out_size[f];
 }
 const uint8_t* WebPGpuBatchOutput(const WebPGpuBatch* b, int f) {
-  return (b && f >= 0 && f < b->last_n) ? b->out[f] : NULL;
+  if (!b || f < 0 || f >= b->last_n) return NULL;
+  if (b->l) return b->l->out_size[f] ? b->l->h_out + b->l->out_off[f] : NULL;
+  return b->out[f];
 }
 int WebPGpuBatchStageCycles(const WebPGpuBatch* b, int f, uint64_t cycles[8]) {
-  if (!b || f < 0 || f >= b->last_n || !cycles) return 0;
+  if (!b || b->l || f < 0 || f >= b->last_n || !cycles) return 0;
   for (int i = 0; i < 8; ++i) cycles[i] = b->h_results[f].stamps[i];
   return 1;
 }
 size_t WebPGpuBatchTokenCount(const WebPGpuBatch* b, int f) {
-  return (b && f >= 0 && f < b->last_n) ? b->h_results[f].ntokens : 0;
+  return (b && !b->l && f >= 0 && f < b->last_n) ? b->h_results[f].ntokens : 0;
 }
 int WebPGpuBatchError(const WebPGpuBatch* b, int f) {
-  return (b && f >= 0 && f < b->last_n) ? b->err[f] : VP8_ENC_ERROR_NULL_PARAMETER;
+  if (!b || f < 0 || f >= b->last_n) return VP8_ENC_ERROR_NULL_PARAMETER;
+  return b->l ? b->l->err[f] : b->err[f];
 }
 void WebPGpuBatchTimings(const WebPGpuBatch* b, double t[10]) {
   for (int i = 0; i < 10; ++i) t[i] = b ? b->timings[i] : 0.;

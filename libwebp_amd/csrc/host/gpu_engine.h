@@ -6,6 +6,7 @@
 
 #include "../vp8_gpu.h"
 #include "vp8_host.h"
+#include "vp8l_batch.h"
 #include "webp/encode.h"
 
 /* partition-0 size guard of VP8EncTokenLoop (frame_enc.c:32, :869) */
@@ -73,6 +74,7 @@ struct WebPGpuBatch {
   int* hdr;
   double timings[10];
   int host_emit;             /* partition 1 coded on the host (A/B, WEBP_AMD_HOST_EMIT=1) */
+  vp8l_engine* l;            /* config->lossless: the VP8L engine (lossy buffers unused) */
 };
 
 #ifdef __cplusplus

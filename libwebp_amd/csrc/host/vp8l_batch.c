@@ -1,0 +1,261 @@
+/* Lossless (VP8L) batch engine: device buffers, the L1 -> L5 kernels, the
+ * per-frame header on host threads, the L6/L7 bit writer and the RIFF
+ * assembly. One call encodes n same-sized RGBA frames resident in HBM;
+ * every .webp lands in one pinned host buffer. */
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "gpu_engine.h"
+#include "vp8l_batch.h"
+#include "vp8l_host.h"
+
+static double now_us(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
+#define CHK(x)                                                         \
+  do {                                                                 \
+    const hipError_t e_ = (x);                                         \
+    if (e_ != hipSuccess) {                                            \
+      char loc_[64];                                                   \
+      snprintf(loc_, sizeof(loc_), "vp8l_batch.c:%d", __LINE__);       \
+      vp8g_set_error(loc_, hipGetErrorString(e_));                     \
+      goto fail;                                                       \
+    }                                                                  \
+  } while (0)
+
+static int sub_sample(int size, int bits) { return (size + (1 << bits) - 1) >> bits; }
+
+void vp8l_engine_free(vp8l_engine* l) {
+  if (!l) return;
+  hipFree(l->d_tabs); hipFree(l->d_argb); hipFree(l->d_modes); hipFree(l->d_mult);
+  hipFree(l->d_aflag); hipFree(l->d_hits); hipFree(l->d_ops); hipFree(l->d_feat);
+  hipFree(l->d_hc); hipFree(l->d_assign); hipFree(l->d_ctab); hipFree(l->d_gtile);
+  hipFree(l->d_start); hipFree(l->d_bsum); hipFree(l->d_boff); hipFree(l->d_end); hipFree(l->d_out);
+  hipHostFree(l->h_modes); hipHostFree(l->h_mult); hipHostFree(l->h_aflag); hipHostFree(l->h_hc);
+  hipHostFree(l->h_assign); hipHostFree(l->h_ctab); hipHostFree(l->h_gtile);
+  hipHostFree(l->h_start); hipHostFree(l->h_end); hipHostFree(l->h_hdr); hipHostFree(l->h_out);
+  free(l->hdr_bytes); free(l->out_off); free(l->out_size); free(l->err);
+  free(l);
+}
+
+vp8l_engine* vp8l_engine_new(int w, int h, int max_frames, int method) {
+  vp8l_engine* l = (vp8l_engine*)calloc(1, sizeof(*l));
+  if (!l) return NULL;
+  vp8l_setup_params(&l->p, w, h, max_frames, method);
+  l->max_frames = max_frames;
+  l->npix = (size_t)w * h;
+  l->ntt = sub_sample(w, l->p.tb) * sub_sample(h, l->p.tb);
+  l->nht = sub_sample(w, l->p.hb) * sub_sample(h, l->p.hb);
+  l->nblk = (int)((l->npix + VP8L_BLOCK - 1) / VP8L_BLOCK);
+  l->hdr_cap = ((size_t)16 * l->ntt + (size_t)8 * l->nht + ((size_t)256 << 10) + 255) & ~(size_t)255;
+  l->out_cap = (l->npix * 5 + l->hdr_cap + 255) & ~(size_t)255;
+  const size_t N = (size_t)max_frames, np = l->npix;
+  CHK(hipMalloc((void**)&l->d_tabs, (4097 + 1024) * sizeof(int32_t)));
+  CHK(hipMemcpy(l->d_tabs, vp8l_nlogn_table(), 4097 * sizeof(int32_t), hipMemcpyHostToDevice));
+  CHK(hipMemcpy(l->d_tabs + 4097, vp8l_flog2_table(), 1024 * sizeof(int32_t),
+                hipMemcpyHostToDevice));
+  CHK(hipMalloc((void**)&l->d_argb, N * np * sizeof(uint32_t)));
+  CHK(hipMalloc((void**)&l->d_ops, N * np * sizeof(uint32_t)));
+  CHK(hipMalloc((void**)&l->d_hits, N * ((np + 63) >> 6) * sizeof(uint64_t)));
+  CHK(hipMalloc((void**)&l->d_modes, N * l->ntt));
+  CHK(hipMalloc((void**)&l->d_mult, N * l->ntt * sizeof(uint32_t)));
+  CHK(hipMalloc((void**)&l->d_aflag, N * sizeof(uint32_t)));
+  CHK(hipMalloc((void**)&l->d_feat, N * l->nht * sizeof(int64_t)));
+  CHK(hipMalloc((void**)&l->d_hc, N * VP8L_KMAX * VP8L_NS * sizeof(uint32_t)));
+  CHK(hipMalloc((void**)&l->d_assign, N * l->nht));
+  CHK(hipMalloc((void**)&l->d_ctab, N * VP8L_KMAX * VP8L_NS * sizeof(uint32_t)));
+  CHK(hipMalloc((void**)&l->d_gtile, N * l->nht));
+  CHK(hipMalloc((void**)&l->d_start, N * sizeof(uint64_t)));
+  CHK(hipMalloc((void**)&l->d_end, N * sizeof(uint64_t)));
+  CHK(hipMalloc((void**)&l->d_bsum, N * l->nblk * sizeof(uint32_t)));
+  CHK(hipMalloc((void**)&l->d_boff, N * l->nblk * sizeof(uint64_t)));
+  CHK(hipMalloc((void**)&l->d_out, N * l->out_cap));
+  CHK(hipHostMalloc((void**)&l->h_modes, N * l->ntt, 0));
+  CHK(hipHostMalloc((void**)&l->h_mult, N * l->ntt * sizeof(uint32_t), 0));
+  CHK(hipHostMalloc((void**)&l->h_aflag, N * sizeof(uint32_t), 0));
+  CHK(hipHostMalloc((void**)&l->h_hc, N * VP8L_KMAX * VP8L_NS * sizeof(uint32_t), 0));
+  CHK(hipHostMalloc((void**)&l->h_assign, N * l->nht, 0));
+  CHK(hipHostMalloc((void**)&l->h_ctab, N * VP8L_KMAX * VP8L_NS * sizeof(uint32_t), 0));
+  CHK(hipHostMalloc((void**)&l->h_gtile, N * l->nht, 0));
+  CHK(hipHostMalloc((void**)&l->h_start, N * sizeof(uint64_t), 0));
+  CHK(hipHostMalloc((void**)&l->h_end, N * sizeof(uint64_t), 0));
+  CHK(hipHostMalloc((void**)&l->h_hdr, N * l->hdr_cap, 0));
+  l->hdr_bytes = (size_t*)calloc(N, sizeof(size_t));
+  l->out_off = (size_t*)calloc(N + 1, sizeof(size_t));
+  l->out_size = (size_t*)calloc(N, sizeof(size_t));
+  l->err = (int*)calloc(N, sizeof(int));
+  if (!l->hdr_bytes || !l->out_off || !l->out_size || !l->err) goto fail;
+  return l;
+fail:
+  vp8l_engine_free(l);
+  return NULL;
+}
+
+/* ---- per-frame headers on host threads ---- */
+
+typedef struct {
+  vp8l_engine* l;
+  int n;
+  atomic_int next;
+} HdrJob;
+
+static void frame_header(vp8l_engine* l, int f) {
+  vp8l_bw bw;
+  const vp8l_params* p = &l->p;
+  vp8l_bw_init(&bw, 1 << 16);
+  const int ok = vp8l_build_header(p, l->h_aflag[f] != 0, l->h_modes + (size_t)f * l->ntt,
+                                   l->h_mult + (size_t)f * l->ntt,
+                                   l->h_hc + (size_t)f * VP8L_KMAX * VP8L_NS,
+                                   l->h_assign + (size_t)f * l->nht, &bw,
+                                   l->h_ctab + (size_t)f * VP8L_KMAX * VP8L_NS,
+                                   l->h_gtile + (size_t)f * l->nht);
+  l->h_start[f] = bw.nbits;
+  const size_t nb = vp8l_bw_finish(&bw);
+  if (!ok || bw.oom) {
+    l->err[f] = VP8_ENC_ERROR_OUT_OF_MEMORY;
+  } else if (nb > l->hdr_cap) {
+    l->err[f] = VP8_ENC_ERROR_BITSTREAM_OUT_OF_MEMORY;
+  } else {
+    uint8_t* d = l->h_hdr + (size_t)f * l->hdr_cap;
+    memcpy(d, bw.buf, nb);
+    memset(d + nb, 0, ((nb + 3) & ~(size_t)3) - nb);
+    l->hdr_bytes[f] = nb;
+  }
+  if (l->err[f]) { l->h_start[f] = 0; l->hdr_bytes[f] = 0; }
+  vp8l_bw_free(&bw);
+}
+
+static void* hdr_worker(void* arg) {
+  HdrJob* j = (HdrJob*)arg;
+  for (;;) {
+    const int f = atomic_fetch_add(&j->next, 1);
+    if (f >= j->n) break;
+    frame_header(j->l, f);
+  }
+  return NULL;
+}
+
+static void run_headers(vp8l_engine* l, int n, int threads) {
+  HdrJob job;
+  job.l = l; job.n = n;
+  atomic_init(&job.next, 0);
+  pthread_t th[64];
+  int started = 0;
+  if (threads > 64) threads = 64;
+  for (int i = 0; i < threads - 1 && i < n - 1; ++i)
+    if (pthread_create(&th[started], NULL, hdr_worker, &job) == 0) ++started;
+  hdr_worker(&job);
+  for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
+}
+
+/* ---- pipeline ---- */
+
+int vp8l_engine_run(struct WebPGpuBatch* b, const uint8_t* rgba, size_t fstride, int rstride, int n) {
+  vp8l_engine* l = b->l;
+  hipStream_t st = b->stream;
+  const size_t N = (size_t)n;
+  double t0 = now_us(), t1, t2, t3, t4, t5;
+  vp8l_params p = l->p;
+  p.n = n;
+  for (int f = 0; f < n; ++f) l->err[f] = VP8_ENC_OK;
+  CHK(hipMemsetAsync(l->d_aflag, 0, N * sizeof(uint32_t), st));
+  CHK(hipEventRecord(b->ev[0], st));
+  if (!vp8l_launch_transform(rgba, fstride, rstride, &p, l->d_tabs, l->d_argb, l->d_modes,
+                             l->d_mult, l->d_aflag, st))
+    goto fail;
+  CHK(hipEventRecord(b->ev[1], st));
+  if (!vp8l_launch_analyze(l->d_argb, &p, l->d_tabs + 4097, l->d_hits, l->d_ops, l->d_feat,
+                           l->d_hc, l->d_assign, st))
+    goto fail;
+  CHK(hipEventRecord(b->ev[2], st));
+  CHK(hipMemcpyAsync(l->h_modes, l->d_modes, N * l->ntt, hipMemcpyDeviceToHost, st));
+  CHK(hipMemcpyAsync(l->h_mult, l->d_mult, N * l->ntt * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                     st));
+  CHK(hipMemcpyAsync(l->h_aflag, l->d_aflag, N * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  CHK(hipMemcpyAsync(l->h_hc, l->d_hc, N * VP8L_KMAX * VP8L_NS * sizeof(uint32_t),
+                     hipMemcpyDeviceToHost, st));
+  CHK(hipMemcpyAsync(l->h_assign, l->d_assign, N * l->nht, hipMemcpyDeviceToHost, st));
+  /* the output slabs must start zeroed (the bit writer ORs its edge words) */
+  CHK(hipMemsetAsync(l->d_out, 0, N * l->out_cap, st));
+  CHK(hipStreamSynchronize(st));
+  t1 = now_us();
+  run_headers(l, n, b->threads);
+  t2 = now_us();
+  for (int f = 0; f < n; ++f)
+    if (l->hdr_bytes[f])
+      CHK(hipMemcpyAsync(l->d_out + (size_t)f * l->out_cap, l->h_hdr + (size_t)f * l->hdr_cap,
+                         (l->hdr_bytes[f] + 3) & ~(size_t)3, hipMemcpyHostToDevice, st));
+  CHK(hipMemcpyAsync(l->d_ctab, l->h_ctab, N * VP8L_KMAX * VP8L_NS * sizeof(uint32_t),
+                     hipMemcpyHostToDevice, st));
+  CHK(hipMemcpyAsync(l->d_gtile, l->h_gtile, N * l->nht, hipMemcpyHostToDevice, st));
+  CHK(hipMemcpyAsync(l->d_start, l->h_start, N * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  CHK(hipEventRecord(b->ev[3], st));
+  if (!vp8l_launch_write(l->d_argb, l->d_ops, &p, l->d_ctab, l->d_gtile, l->d_start, l->d_bsum,
+                         l->d_boff, l->d_end, l->d_out, l->out_cap, st))
+    goto fail;
+  CHK(hipEventRecord(b->ev[4], st));
+  CHK(hipMemcpyAsync(l->h_end, l->d_end, N * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  t3 = now_us();
+  /* packed pinned output: per frame 20-byte RIFF/VP8L header, payload, pad */
+  l->out_off[0] = 0;
+  for (int f = 0; f < n; ++f) {
+    size_t sz = 0;
+    if (!l->err[f]) {
+      const size_t bytes = (size_t)((l->h_end[f] + 7) >> 3);
+      if (bytes > l->out_cap) l->err[f] = VP8_ENC_ERROR_BITSTREAM_OUT_OF_MEMORY;
+      else sz = 20 + bytes + (bytes & 1);
+    }
+    l->out_size[f] = sz;
+    l->out_off[f + 1] = l->out_off[f] + ((sz + 15) & ~(size_t)15);
+  }
+  if (l->out_off[n] > l->h_out_cap) {
+    hipHostFree(l->h_out);
+    l->h_out = NULL;
+    l->h_out_cap = 0;
+    const size_t cap = l->out_off[n] + l->out_off[n] / 4 + 4096;
+    CHK(hipHostMalloc((void**)&l->h_out, cap, 0));
+    l->h_out_cap = cap;
+  }
+  for (int f = 0; f < n; ++f)
+    if (l->out_size[f])
+      CHK(hipMemcpyAsync(l->h_out + l->out_off[f] + 20, l->d_out + (size_t)f * l->out_cap,
+                         l->out_size[f] - 20, hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  t4 = now_us();
+  for (int f = 0; f < n; ++f) {
+    if (!l->out_size[f]) continue;
+    uint8_t* o = l->h_out + l->out_off[f];
+    const size_t bytes = (size_t)((l->h_end[f] + 7) >> 3);
+    vp8l_riff_header(o, bytes);
+    if (bytes & 1) o[20 + bytes] = 0;
+  }
+  t5 = now_us();
+  {
+    float k_ms = 0.f, a_ms = 0.f, w_ms = 0.f;
+    CHK(hipEventElapsedTime(&k_ms, b->ev[0], b->ev[1]));
+    CHK(hipEventElapsedTime(&a_ms, b->ev[1], b->ev[2]));
+    CHK(hipEventElapsedTime(&w_ms, b->ev[3], b->ev[4]));
+    b->timings[0] = t1 - t0;   /* transform + analysis kernels + side copies (wall) */
+    b->timings[1] = t2 - t1;   /* host headers */
+    b->timings[2] = t3 - t2;   /* header upload + bit writer (wall) */
+    b->timings[3] = t4 - t3;   /* output copies */
+    b->timings[4] = t5 - t4;   /* RIFF */
+    b->timings[6] = 1e3 * a_ms;   /* cache + parse + tiles + clustering */
+    b->timings[7] = 1e3 * k_ms;   /* transform */
+    b->timings[8] = 1e3 * w_ms;   /* bit writer */
+  }
+  b->last_n = n;
+  return 1;
+fail:
+  return 0;
+}

@@ -1,0 +1,64 @@
+/* Internal: the lossless (VP8L) side of WebPGpuBatch (config->lossless). */
+#ifndef LIBWEBP_AMD_VP8L_BATCH_H_
+#define LIBWEBP_AMD_VP8L_BATCH_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../vp8l_gpu.h"
+
+struct WebPGpuBatch;
+
+typedef struct vp8l_engine {
+  vp8l_params p;               /* n = max_frames; per call a copy with n set */
+  int max_frames, ntt, nht, nblk;
+  size_t npix, hdr_cap, out_cap;
+  /* device (HBM) */
+  int32_t* d_tabs;             /* nlogn (4097) | log2 fraction (1024) */
+  uint32_t* d_argb;
+  uint32_t* d_ops;
+  uint64_t* d_hits;
+  uint8_t* d_modes;
+  uint32_t* d_mult;
+  uint32_t* d_aflag;
+  int64_t* d_feat;
+  uint32_t* d_hc;
+  uint8_t* d_assign;
+  uint32_t* d_ctab;
+  uint8_t* d_gtile;
+  uint64_t* d_start;
+  uint64_t* d_end;
+  uint32_t* d_bsum;
+  uint64_t* d_boff;
+  uint8_t* d_out;
+  /* host (pinned) */
+  uint8_t* h_modes;
+  uint32_t* h_mult;
+  uint32_t* h_aflag;
+  uint32_t* h_hc;
+  uint8_t* h_assign;
+  uint32_t* h_ctab;
+  uint8_t* h_gtile;
+  uint64_t* h_start;
+  uint64_t* h_end;
+  uint8_t* h_hdr;              /* per frame hdr_cap bytes of header */
+  uint8_t* h_out;              /* packed .webp files of the last call */
+  size_t h_out_cap;
+  size_t* hdr_bytes;
+  size_t* out_off;
+  size_t* out_size;
+  int* err;
+} vp8l_engine;
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+vp8l_engine* vp8l_engine_new(int w, int h, int max_frames, int method);
+void vp8l_engine_free(vp8l_engine* l);
+int vp8l_engine_run(struct WebPGpuBatch* b, const uint8_t* rgba, size_t fstride, int rstride,
+                    int n);
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LIBWEBP_AMD_VP8L_BATCH_H_ */

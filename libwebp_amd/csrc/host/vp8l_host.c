@@ -1,0 +1,459 @@
+/* Host side of the lossless (VP8L) path: Huffman codes, the header bits and
+ * the RIFF container. Every choice here is the one oracle/vp8l_model.py
+ * states (same function names), so the GPU bitstream can be checked bit for
+ * bit against the model; the format is the reference decoder's:
+ *   header / transforms / cache / meta codes   src/dec/vp8l_dec.c:126-135, 1330-1380, 1455-1490, 364-420
+ *   Huffman code reading                       src/dec/vp8l_dec.c:255-356
+ * The code-length layout follows the reference writer's structure
+ * (src/enc/vp8l_enc.c:476-643: storage order, simple codes, single-symbol
+ * codes written with zero bits). */
+#include "vp8l_host.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---------------------------------------------------------------- writer */
+
+void vp8l_bw_init(vp8l_bw* bw, size_t cap) {
+  memset(bw, 0, sizeof(*bw));
+  bw->buf = (uint8_t*)malloc(cap ? cap : 1);
+  bw->cap = bw->buf ? cap : 0;
+  bw->oom = bw->buf == NULL;
+}
+
+void vp8l_bw_free(vp8l_bw* bw) {
+  free(bw->buf);
+  memset(bw, 0, sizeof(*bw));
+}
+
+static void bw_byte(vp8l_bw* bw, uint8_t v) {
+  if (bw->pos == bw->cap) {
+    const size_t cap = bw->cap ? 2 * bw->cap : 1024;
+    uint8_t* nb = (uint8_t*)realloc(bw->buf, cap);
+    if (!nb) { bw->oom = 1; return; }
+    bw->buf = nb;
+    bw->cap = cap;
+  }
+  bw->buf[bw->pos++] = v;
+}
+
+void vp8l_bw_put(vp8l_bw* bw, uint32_t v, int nbits) {
+  if (nbits <= 0) return;
+  bw->acc |= (uint64_t)(v & (uint32_t)((1ull << nbits) - 1)) << bw->used;
+  bw->used += nbits;
+  bw->nbits += (uint64_t)nbits;
+  while (bw->used >= 8) {
+    bw_byte(bw, (uint8_t)bw->acc);
+    bw->acc >>= 8;
+    bw->used -= 8;
+  }
+}
+
+size_t vp8l_bw_finish(vp8l_bw* bw) {
+  if (bw->used) {
+    bw_byte(bw, (uint8_t)bw->acc);
+    bw->acc = 0;
+    bw->used = 0;
+  }
+  return bw->pos;
+}
+
+/* ---------------------------------------------------------------- params */
+
+static int sub_sample(int size, int bits) { return (size + (1 << bits) - 1) >> bits; }
+
+int vp8l_histo_bits(int method, int w, int h) {
+  int b = 7 - method;
+  while (sub_sample(w, b) * sub_sample(h, b) > VP8L_MAX_HUFF_IMAGE) ++b;
+  return b < 2 ? 2 : b > 9 ? 9 : b;
+}
+
+int vp8l_transform_bits(int method, int hb) {
+  const int mx = method < 4 ? 6 : method > 4 ? 4 : 5;
+  return hb > mx ? mx : hb;
+}
+
+static const uint8_t kCodeToPlane[120] = {
+  0x18, 0x07, 0x17, 0x19, 0x28, 0x06, 0x27, 0x29, 0x16, 0x1a,
+  0x26, 0x2a, 0x38, 0x05, 0x37, 0x39, 0x15, 0x1b, 0x36, 0x3a,
+  0x25, 0x2b, 0x48, 0x04, 0x47, 0x49, 0x14, 0x1c, 0x35, 0x3b,
+  0x46, 0x4a, 0x24, 0x2c, 0x58, 0x45, 0x4b, 0x34, 0x3c, 0x03,
+  0x57, 0x59, 0x13, 0x1d, 0x56, 0x5a, 0x23, 0x2d, 0x44, 0x4c,
+  0x55, 0x5b, 0x33, 0x3d, 0x68, 0x02, 0x67, 0x69, 0x12, 0x1e,
+  0x66, 0x6a, 0x22, 0x2e, 0x54, 0x5c, 0x43, 0x4d, 0x65, 0x6b,
+  0x32, 0x3e, 0x78, 0x01, 0x77, 0x79, 0x53, 0x5d, 0x11, 0x1f,
+  0x64, 0x6c, 0x42, 0x4e, 0x76, 0x7a, 0x21, 0x2f, 0x75, 0x7b,
+  0x31, 0x3f, 0x63, 0x6d, 0x52, 0x5e, 0x00, 0x74, 0x7c, 0x41,
+  0x4f, 0x10, 0x20, 0x62, 0x6e, 0x30, 0x73, 0x7d, 0x51, 0x5f,
+  0x40, 0x72, 0x7e, 0x61, 0x6f, 0x50, 0x71, 0x7f, 0x60, 0x70};
+
+/* src/dec/vp8l_dec.c:176-186 */
+static int plane_code_to_distance(int w, int code) {
+  if (code > 120) return code - 120;
+  const int dc = kCodeToPlane[code - 1];
+  const int d = (dc >> 4) * w + 8 - (dc & 0xf);
+  return d >= 1 ? d : 1;
+}
+
+static int distance_code(int w, int d) {
+  for (int c = 1; c <= 120; ++c)
+    if (plane_code_to_distance(w, c) == d) return c;
+  return d + 120;
+}
+
+void vp8l_setup_params(vp8l_params* p, int w, int h, int n, int method) {
+  memset(p, 0, sizeof(*p));
+  p->w = w; p->h = h; p->n = n;
+  p->hb = vp8l_histo_bits(method, w, h);
+  p->tb = vp8l_transform_bits(method, p->hb);
+  const int nht = sub_sample(w, p->hb) * sub_sample(h, p->hb);
+  p->k = nht < VP8L_KMAX ? nht : VP8L_KMAX;
+  const int cand[4] = {w, 1, w + 1, w - 1};
+  int nc = 0;
+  for (int i = 0; i < 4; ++i) {
+    const int d = cand[i];
+    int dup = d < 1;
+    for (int j = 0; j < nc; ++j) dup |= p->dist[j] == d;
+    if (dup) continue;
+    p->dist[nc] = d;
+    p->dcode[nc] = distance_code(w, d);
+    ++nc;
+  }
+}
+
+static int32_t g_nlogn[4097];
+static int32_t g_flog2[1024];
+static pthread_once_t g_tab_once = PTHREAD_ONCE_INIT;
+static void tables_init(void) {
+  g_nlogn[0] = g_nlogn[1] = 0;
+  for (int n = 2; n <= 4096; ++n) g_nlogn[n] = (int32_t)floor(n * log2((double)n) * 4096 + 0.5);
+  for (int m = 0; m < 1024; ++m) g_flog2[m] = (int32_t)floor(4096 * log2(1 + m / 1024.0) + 0.5);
+}
+const int32_t* vp8l_nlogn_table(void) { pthread_once(&g_tab_once, tables_init); return g_nlogn; }
+const int32_t* vp8l_flog2_table(void) { pthread_once(&g_tab_once, tables_init); return g_flog2; }
+
+/* ---------------------------------------------------------------- Huffman */
+
+typedef struct { uint64_t w; int s; } Leaf;
+
+static int leaf_cmp(const void* a, const void* b) {
+  const Leaf* x = (const Leaf*)a;
+  const Leaf* y = (const Leaf*)b;
+  if (x->w != y->w) return x->w < y->w ? -1 : 1;
+  return x->s - y->s;
+}
+
+/* model: huffman_lengths -- two-queue Huffman on (max(count, count_min),
+ * symbol)-sorted leaves, count_min doubling until the depth fits. */
+static int huffman_lengths(const uint32_t* hist, int n, int limit, uint8_t* len) {
+  memset(len, 0, (size_t)n);
+  int nu = 0, last = -1;
+  for (int s = 0; s < n; ++s)
+    if (hist[s]) { ++nu; last = s; }
+  if (nu == 0) return 1;
+  if (nu == 1) { len[last] = 1; return 1; }
+  Leaf* lv = (Leaf*)malloc(sizeof(Leaf) * nu);
+  uint64_t* iw = (uint64_t*)malloc(sizeof(uint64_t) * nu);
+  int* lpar = (int*)malloc(sizeof(int) * nu);
+  int* ipar = (int*)malloc(sizeof(int) * nu);
+  int* idep = (int*)malloc(sizeof(int) * nu);
+  int ok = lv && iw && lpar && ipar && idep;
+  for (uint64_t cmin = 1; ok; cmin *= 2) {
+    int k = 0;
+    for (int s = 0; s < n; ++s)
+      if (hist[s]) { lv[k].w = hist[s] > cmin ? hist[s] : cmin; lv[k].s = s; ++k; }
+    qsort(lv, (size_t)nu, sizeof(Leaf), leaf_cmp);
+    int i1 = 0, i2 = 0, n2 = 0;
+    while ((nu - i1) + (n2 - i2) > 1) {
+      int node[2];
+      uint64_t wsum = 0;
+      for (int t = 0; t < 2; ++t) {
+        if (i2 >= n2 || (i1 < nu && lv[i1].w <= iw[i2])) {
+          wsum += lv[i1].w; node[t] = i1++;
+        } else {
+          wsum += iw[i2]; node[t] = -1 - i2++;
+        }
+      }
+      for (int t = 0; t < 2; ++t) {
+        if (node[t] >= 0) lpar[node[t]] = n2;
+        else ipar[-1 - node[t]] = n2;
+      }
+      iw[n2++] = wsum;
+    }
+    idep[n2 - 1] = 0;
+    for (int j = n2 - 2; j >= 0; --j) idep[j] = idep[ipar[j]] + 1;
+    int mx = 0;
+    for (int j = 0; j < nu; ++j) {
+      const int d = idep[lpar[j]] + 1;
+      len[lv[j].s] = (uint8_t)d;
+      if (d > mx) mx = d;
+    }
+    if (mx <= limit) break;
+  }
+  free(lv); free(iw); free(lpar); free(ipar); free(idep);
+  return ok;
+}
+
+/* model: canonical_codes (deflate order, bit-reversed for LSB-first) */
+static void canonical_codes(const uint8_t* len, int n, uint16_t* codes) {
+  int bl[17] = {0}, next[17] = {0};
+  for (int s = 0; s < n; ++s) bl[len[s]]++;
+  bl[0] = 0;
+  int code = 0;
+  for (int b = 1; b <= 16; ++b) {
+    code = (code + bl[b - 1]) << 1;
+    next[b] = code;
+  }
+  for (int s = 0; s < n; ++s) {
+    codes[s] = 0;
+    if (!len[s]) continue;
+    const int c = next[len[s]]++;
+    int r = 0;
+    for (int i = 0; i < len[s]; ++i) r |= ((c >> i) & 1) << (len[s] - 1 - i);
+    codes[s] = (uint16_t)r;
+  }
+}
+
+#define MAX_ALPH VP8L_GS
+
+typedef struct {
+  int n;                 /* alphabet size */
+  int nused, used0, used1;
+  uint8_t len[MAX_ALPH];
+  uint8_t wlen[MAX_ALPH];
+  uint16_t codes[MAX_ALPH];
+} Code;
+
+/* model: Code.__init__ */
+static int code_build(Code* c, const uint32_t* hist, int n) {
+  c->n = n;
+  c->nused = 0; c->used0 = c->used1 = 0;
+  for (int s = 0; s < n; ++s)
+    if (hist[s]) {
+      if (c->nused == 0) c->used0 = s;
+      else if (c->nused == 1) c->used1 = s;
+      ++c->nused;
+    }
+  if (!huffman_lengths(hist, n, 15, c->len)) return 0;
+  canonical_codes(c->len, n, c->codes);
+  if (c->nused <= 1) memset(c->wlen, 0, (size_t)n);
+  else memcpy(c->wlen, c->len, (size_t)n);
+  return 1;
+}
+
+static const uint8_t kStorageOrder[19] = {17, 18, 0, 1, 2, 3, 4, 5, 16, 6, 7, 8, 9, 10, 11,
+                                          12, 13, 14, 15};
+
+/* model: code_length_tokens */
+static int cl_tokens(const uint8_t* len, int n, uint8_t* tc, uint8_t* te) {
+  int k = 0, i = 0;
+  while (i < n) {
+    const int v = len[i];
+    int j = i;
+    while (j < n && len[j] == v) ++j;
+    int run = j - i;
+    if (v == 0) {
+      while (run > 0) {
+        if (run < 3) {
+          for (; run > 0; --run) { tc[k] = 0; te[k++] = 0; }
+        } else if (run <= 10) {
+          tc[k] = 17; te[k++] = (uint8_t)(run - 3); run = 0;
+        } else {
+          const int r = run < 138 ? run : 138;
+          tc[k] = 18; te[k++] = (uint8_t)(r - 11); run -= r;
+        }
+      }
+    } else {
+      tc[k] = (uint8_t)v; te[k++] = 0; --run;
+      while (run > 0) {
+        if (run < 3) {
+          for (; run > 0; --run) { tc[k] = (uint8_t)v; te[k++] = 0; }
+        } else {
+          const int r = run < 6 ? run : 6;
+          tc[k] = 16; te[k++] = (uint8_t)(r - 3); run -= r;
+        }
+      }
+    }
+    i = j;
+  }
+  return k;
+}
+
+/* model: Code.store */
+static void code_store(const Code* c, vp8l_bw* bw) {
+  if (c->nused == 0) {
+    vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 0, 1); vp8l_bw_put(bw, 0, 1); vp8l_bw_put(bw, 0, 1);
+    return;
+  }
+  const int maxu = c->nused == 1 ? c->used0 : c->used1;
+  if (c->nused <= 2 && maxu < 256) {
+    vp8l_bw_put(bw, 1, 1);
+    vp8l_bw_put(bw, (uint32_t)(c->nused - 1), 1);
+    if (c->used0 <= 1) { vp8l_bw_put(bw, 0, 1); vp8l_bw_put(bw, (uint32_t)c->used0, 1); }
+    else { vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, (uint32_t)c->used0, 8); }
+    if (c->nused == 2) vp8l_bw_put(bw, (uint32_t)c->used1, 8);
+    return;
+  }
+  vp8l_bw_put(bw, 0, 1);
+  uint8_t tc[MAX_ALPH], te[MAX_ALPH];
+  const int nt = cl_tokens(c->len, c->n, tc, te);
+  uint32_t th[19] = {0};
+  for (int i = 0; i < nt; ++i) th[tc[i]]++;
+  uint8_t cl[19];
+  uint16_t cc[19];
+  huffman_lengths(th, 19, 7, cl);
+  canonical_codes(cl, 19, cc);
+  int ncodes = 19;
+  while (ncodes > 4 && cl[kStorageOrder[ncodes - 1]] == 0) --ncodes;
+  vp8l_bw_put(bw, (uint32_t)(ncodes - 4), 4);
+  for (int i = 0; i < ncodes; ++i) vp8l_bw_put(bw, cl[kStorageOrder[i]], 3);
+  int nz = 0;
+  for (int i = 0; i < 19; ++i) nz += cl[i] != 0;
+  const int single = nz <= 1;
+  vp8l_bw_put(bw, 0, 1);   /* no max_symbol */
+  for (int i = 0; i < nt; ++i) {
+    if (!single) vp8l_bw_put(bw, cc[tc[i]], cl[tc[i]]);
+    if (tc[i] == 16) vp8l_bw_put(bw, te[i], 2);
+    else if (tc[i] == 17) vp8l_bw_put(bw, te[i], 3);
+    else if (tc[i] == 18) vp8l_bw_put(bw, te[i], 7);
+  }
+}
+
+static void code_put(const Code* c, vp8l_bw* bw, int s) { vp8l_bw_put(bw, c->codes[s], c->wlen[s]); }
+
+/* model: write_sub_image -- level > 0 image, no cache, literals only */
+static int write_sub_image(vp8l_bw* bw, const uint32_t* pix, int n) {
+  uint32_t* h = (uint32_t*)calloc(280 + 3 * 256 + 40, sizeof(uint32_t));
+  Code* c = (Code*)malloc(5 * sizeof(Code));
+  if (!h || !c) { free(h); free(c); return 0; }
+  uint32_t* hg = h; uint32_t* hr = h + 280; uint32_t* hbl = hr + 256; uint32_t* ha = hbl + 256;
+  uint32_t* hd = ha + 256;
+  for (int i = 0; i < n; ++i) {
+    hg[(pix[i] >> 8) & 255]++; hr[(pix[i] >> 16) & 255]++;
+    hbl[pix[i] & 255]++; ha[pix[i] >> 24]++;
+  }
+  int ok = code_build(&c[0], hg, 280) && code_build(&c[1], hr, 256) &&
+           code_build(&c[2], hbl, 256) && code_build(&c[3], ha, 256) && code_build(&c[4], hd, 40);
+  if (ok) {
+    vp8l_bw_put(bw, 0, 1);   /* no colour cache */
+    for (int k = 0; k < 5; ++k) code_store(&c[k], bw);
+    for (int i = 0; i < n; ++i) {
+      code_put(&c[0], bw, (pix[i] >> 8) & 255); code_put(&c[1], bw, (pix[i] >> 16) & 255);
+      code_put(&c[2], bw, pix[i] & 255); code_put(&c[3], bw, pix[i] >> 24);
+    }
+  }
+  free(h); free(c);
+  return ok;
+}
+
+/* ---------------------------------------------------------------- header */
+
+static const int kAlphOff[5] = {0, VP8L_GS, VP8L_GS + 256, VP8L_GS + 512, VP8L_GS + 768};
+static const int kAlphSize[5] = {VP8L_GS, 256, 256, 256, 40};
+
+static uint64_t data_bits(const Code* g, const uint32_t* h) {
+  uint64_t b = 0;
+  for (int a = 0; a < 5; ++a)
+    for (int s = 0; s < kAlphSize[a]; ++s) b += (uint64_t)h[kAlphOff[a] + s] * g[a].wlen[s];
+  return b;
+}
+
+/* model: encode() from the cluster histograms on */
+int vp8l_build_header(const vp8l_params* p, int has_alpha, const uint8_t* modes,
+                      const uint32_t* mult, const uint32_t* hc, const uint8_t* assign,
+                      vp8l_bw* bw, uint32_t* ctab, uint8_t* gtile) {
+  const int W = p->w, H = p->h, tb = p->tb, hb = p->hb;
+  const int ntt = sub_sample(W, tb) * sub_sample(H, tb);
+  const int nht = sub_sample(W, hb) * sub_sample(H, hb);
+  int ok = 1;
+  int remap[VP8L_KMAX], used[VP8L_KMAX], ng = 0;
+  for (int k = 0; k < VP8L_KMAX; ++k) remap[k] = -1;
+  for (int t = 0; t < nht; ++t) remap[assign[t]] = 0;
+  for (int k = 0; k < VP8L_KMAX; ++k)
+    if (remap[k] == 0) { remap[k] = ng; used[ng++] = k; }
+  uint32_t* tot = (uint32_t*)calloc(VP8L_NS, sizeof(uint32_t));
+  uint32_t* pix = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(ntt > nht ? ntt : nht));
+  Code* groups = (Code*)malloc(sizeof(Code) * 5 * (size_t)(ng + 1));
+  if (!tot || !pix || !groups) { ok = 0; goto done; }
+  for (int g = 0; g < ng; ++g)
+    for (int i = 0; i < VP8L_NS; ++i) tot[i] += hc[(size_t)used[g] * VP8L_NS + i];
+  Code* single = groups + 5 * ng;
+  for (int a = 0; a < 5; ++a) ok &= code_build(&single[a], tot + kAlphOff[a], kAlphSize[a]);
+  for (int g = 0; g < ng; ++g)
+    for (int a = 0; a < 5; ++a)
+      ok &= code_build(&groups[5 * g + a], hc + (size_t)used[g] * VP8L_NS + kAlphOff[a],
+                       kAlphSize[a]);
+  if (!ok) goto done;
+  for (int t = 0; t < nht; ++t) pix[t] = (uint32_t)remap[assign[t]] << 8;
+  int meta = 0;
+  if (ng > 1) {   /* model: cost(...) -- exact bits with headers */
+    vp8l_bw tmp;
+    vp8l_bw_init(&tmp, 1 << 16);
+    vp8l_bw_put(&tmp, 1, 1); vp8l_bw_put(&tmp, (uint32_t)(hb - 2), 3);
+    ok &= write_sub_image(&tmp, pix, nht);
+    uint64_t cm = 0;
+    for (int g = 0; g < ng; ++g) {
+      for (int a = 0; a < 5; ++a) code_store(&groups[5 * g + a], &tmp);
+      cm += data_bits(&groups[5 * g], hc + (size_t)used[g] * VP8L_NS);
+    }
+    cm += tmp.nbits;
+    vp8l_bw_free(&tmp);
+    vp8l_bw_init(&tmp, 1 << 14);
+    for (int a = 0; a < 5; ++a) code_store(&single[a], &tmp);
+    const uint64_t cs = tmp.nbits + data_bits(single, tot);
+    ok &= !tmp.oom;
+    vp8l_bw_free(&tmp);
+    meta = cm < cs;
+  }
+  /* image header + transforms (subtract green, predictor, cross colour) */
+  vp8l_bw_put(bw, 0x2f, 8);
+  vp8l_bw_put(bw, (uint32_t)(W - 1), 14);
+  vp8l_bw_put(bw, (uint32_t)(H - 1), 14);
+  vp8l_bw_put(bw, has_alpha ? 1 : 0, 1);
+  vp8l_bw_put(bw, 0, 3);
+  vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 2, 2);
+  vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 0, 2); vp8l_bw_put(bw, (uint32_t)(tb - 2), 3);
+  for (int t = 0; t < ntt; ++t) pix[t] = 0xff000000u | ((uint32_t)modes[t] << 8);
+  ok &= write_sub_image(bw, pix, ntt);
+  vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 1, 2); vp8l_bw_put(bw, (uint32_t)(tb - 2), 3);
+  for (int t = 0; t < ntt; ++t) pix[t] = 0xff000000u | (mult[t] & 0xffffffu);
+  ok &= write_sub_image(bw, pix, ntt);
+  vp8l_bw_put(bw, 0, 1);
+  vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, VP8L_CACHE_BITS, 4);
+  if (meta) {
+    vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, (uint32_t)(hb - 2), 3);
+    for (int t = 0; t < nht; ++t) pix[t] = (uint32_t)remap[assign[t]] << 8;
+    ok &= write_sub_image(bw, pix, nht);
+  } else {
+    vp8l_bw_put(bw, 0, 1);
+  }
+  const int nout = meta ? ng : 1;
+  for (int g = 0; g < nout; ++g) {
+    const Code* gc = meta ? &groups[5 * g] : single;
+    for (int a = 0; a < 5; ++a) {
+      code_store(&gc[a], bw);
+      for (int s = 0; s < kAlphSize[a]; ++s)
+        ctab[(size_t)g * VP8L_NS + kAlphOff[a] + s] =
+            (uint32_t)gc[a].codes[s] | ((uint32_t)gc[a].wlen[s] << 16);
+    }
+  }
+  for (int t = 0; t < nht; ++t) gtile[t] = meta ? (uint8_t)remap[assign[t]] : 0;
+  ok &= !bw->oom;
+done:
+  free(tot); free(pix); free(groups);
+  return ok;
+}
+
+static void put_le32(uint8_t* d, uint32_t v) {
+  d[0] = (uint8_t)v; d[1] = (uint8_t)(v >> 8); d[2] = (uint8_t)(v >> 16); d[3] = (uint8_t)(v >> 24);
+}
+
+void vp8l_riff_header(uint8_t out[20], size_t size) {
+  const size_t pad = size & 1;
+  memcpy(out, "RIFF", 4);
+  put_le32(out + 4, (uint32_t)(4 + 8 + size + pad));
+  memcpy(out + 8, "WEBPVP8L", 8);
+  put_le32(out + 16, (uint32_t)size);
+}

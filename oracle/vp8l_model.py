@@ -1,0 +1,862 @@
+"""CPU model of the GPU lossless (VP8L) encoder -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module; the product is libwebp_amd/csrc/hip/vp8l_kernels.hip +
+libwebp_amd/csrc/host/vp8l_host.c.
+
+What this is, and what it is not
+--------------------------------
+The reference lossless encoder (src/enc/vp8l_enc.c:1809 VP8LEncodeImage and
+its crunch configs, predictor_enc.c, backward_references_enc.c,
+histogram_enc.c) makes its choices with float entropy estimates, a serial
+hash chain and stochastic histogram clustering. Its *bitstream* is not the
+parity target: SURVEY.md §8(d) asks for a pixel-exact decode and a size within
+a stated tolerance of the reference's. So the GPU encoder has its own,
+data-parallel decisions, and this file states them in plain numpy/Python so
+that
+
+  * the bitstream format can be checked here (no GPU) by decoding with the
+    reference decoder (oracle/_ref, src/dec/vp8l_dec.c), and
+  * the GPU kernels can be checked bit-for-bit against this model on small
+    frames (tests/test_vp8l.py).
+
+The *real* oracle for lossless is the reference decoder: decode(encode(x)) == x.
+
+Format (decoder side, cited so every writer below can be checked):
+  header            src/dec/vp8l_dec.c:126-135 (0x2f, 14+14 bits size-1, alpha, version)
+  transforms        :1330-1380 (PREDICTOR=0, CROSS_COLOR=1, SUBTRACT_GREEN=2),
+                    inverse order of appearance (:1585-1600 ApplyInverseTransforms)
+  colour cache      :1474-1482 (1 bit, 4 bits size), hash src/utils/color_cache_utils.h:34-38
+  meta Huffman      :389-... (level 0 only)
+  Huffman codes     :324-356 (simple / code-length coded), :255-317 lengths (16/17/18)
+  pixel loop        :1138-1275 (green/len/cache alphabet, prefix-coded lengths and
+                    distances :159-186 with the 120 plane codes :64-79)
+  predictors        src/dsp/lossless.c:28-180, inverse :215-257
+  cross colour      src/dsp/lossless.c:274-303
+"""
+import math
+import struct
+
+import numpy as np
+
+# ---------------------------------------------------------------- constants
+
+NUM_LITERAL = 256
+NUM_LENGTH = 24
+NUM_DIST = 40
+MAX_LENGTH = 4096
+CODE_LENGTH_ORDER = [17, 18, 0, 1, 2, 3, 4, 5, 16, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15]
+CODE_TO_PLANE = [
+    0x18, 0x07, 0x17, 0x19, 0x28, 0x06, 0x27, 0x29, 0x16, 0x1a,
+    0x26, 0x2a, 0x38, 0x05, 0x37, 0x39, 0x15, 0x1b, 0x36, 0x3a,
+    0x25, 0x2b, 0x48, 0x04, 0x47, 0x49, 0x14, 0x1c, 0x35, 0x3b,
+    0x46, 0x4a, 0x24, 0x2c, 0x58, 0x45, 0x4b, 0x34, 0x3c, 0x03,
+    0x57, 0x59, 0x13, 0x1d, 0x56, 0x5a, 0x23, 0x2d, 0x44, 0x4c,
+    0x55, 0x5b, 0x33, 0x3d, 0x68, 0x02, 0x67, 0x69, 0x12, 0x1e,
+    0x66, 0x6a, 0x22, 0x2e, 0x54, 0x5c, 0x43, 0x4d, 0x65, 0x6b,
+    0x32, 0x3e, 0x78, 0x01, 0x77, 0x79, 0x53, 0x5d, 0x11, 0x1f,
+    0x64, 0x6c, 0x42, 0x4e, 0x76, 0x7a, 0x21, 0x2f, 0x75, 0x7b,
+    0x31, 0x3f, 0x63, 0x6d, 0x52, 0x5e, 0x00, 0x74, 0x7c, 0x41,
+    0x4f, 0x10, 0x20, 0x62, 0x6e, 0x30, 0x73, 0x7d, 0x51, 0x5f,
+    0x40, 0x72, 0x7e, 0x61, 0x6f, 0x50, 0x71, 0x7f, 0x60, 0x70]
+HASH_MUL = 0x1E35A7BD
+NLOGN_SCALE = 4096          # nlogn table: round(n*log2(n)*4096), n <= 4096
+MAX_HUFF_IMAGE_SIZE = 2600  # src/enc/vp8l_enc.c (GetHistoBits)
+# copy/literal decision thresholds of the greedy row parse
+MIN_COPY = 3
+
+
+def nlogn_table(nmax=4096):
+    t = np.zeros(nmax + 1, dtype=np.int64)
+    for n in range(2, nmax + 1):
+        t[n] = int(math.floor(n * math.log2(n) * NLOGN_SCALE + 0.5))
+    return t
+
+
+NLOGN = nlogn_table()
+
+
+def sub_sample(size, bits):
+    return (size + (1 << bits) - 1) >> bits
+
+
+def histo_bits(method, w, h):
+    """GetHistoBits (src/enc/vp8l_enc.c:234-245), no palette."""
+    b = 7 - method
+    while sub_sample(w, b) * sub_sample(h, b) > MAX_HUFF_IMAGE_SIZE:
+        b += 1
+    return min(max(b, 2), 9)
+
+
+def transform_bits(method, hb):
+    """GetTransformBits (src/enc/vp8l_enc.c:247-253)."""
+    mx = 6 if method < 4 else (4 if method > 4 else 5)
+    return min(hb, mx)
+
+
+def plane_code_to_distance(w, code):
+    """src/dec/vp8l_dec.c:176-186."""
+    if code > 120:
+        return code - 120
+    dc = CODE_TO_PLANE[code - 1]
+    d = (dc >> 4) * w + 8 - (dc & 0xF)
+    return d if d >= 1 else 1
+
+
+def distance_code(w, d):
+    """Smallest code the decoder maps back to distance d."""
+    for c in range(1, 121):
+        if plane_code_to_distance(w, c) == d:
+            return c
+    return d + 120
+
+
+def prefix_encode(v):
+    """value v >= 1 -> (symbol, extra_bits_count, extra_value); inverse of
+    GetCopyDistance (src/dec/vp8l_dec.c:159-168)."""
+    d = v - 1
+    if d < 4:
+        return d, 0, 0
+    h = d.bit_length() - 1
+    s = (d >> (h - 1)) & 1
+    return 2 * h + s, h - 1, d & ((1 << (h - 1)) - 1)
+
+
+def candidate_distances(w):
+    """Distances the match search tries, in tie-break order (cheapest code
+    first): up, left, up-left, up-right."""
+    out = []
+    for d in (w, 1, w + 1, w - 1):
+        if d >= 1 and d not in out:
+            out.append(d)
+    return out
+
+
+# ---------------------------------------------------------------- transforms
+
+def _avg2(a, b):
+    return (a + b) >> 1
+
+
+def _clip(v):
+    return np.clip(v, 0, 255)
+
+
+def predict(mode, L, T, TL, TR):
+    """Channel arrays (..., 4) int64 -> prediction (src/dsp/lossless.c:103-180)."""
+    if mode == 0:
+        p = np.zeros_like(L)
+        p[..., 0] = 255          # ARGB_BLACK: alpha 0xff (channel 0 = A)
+        return p
+    if mode == 1:
+        return L
+    if mode == 2:
+        return T
+    if mode == 3:
+        return TR
+    if mode == 4:
+        return TL
+    if mode == 5:
+        return _avg2(_avg2(L, TR), T)
+    if mode == 6:
+        return _avg2(L, TL)
+    if mode == 7:
+        return _avg2(L, T)
+    if mode == 8:
+        return _avg2(TL, T)
+    if mode == 9:
+        return _avg2(T, TR)
+    if mode == 10:
+        return _avg2(_avg2(L, TL), _avg2(T, TR))
+    if mode == 11:
+        s = (np.abs(L - TL) - np.abs(T - TL)).sum(axis=-1, keepdims=True)
+        return np.where(s <= 0, T, L)
+    if mode == 12:
+        return _clip(L + T - TL)
+    if mode == 13:
+        a = _avg2(L, T)
+        x = a - TL
+        half = np.where(x >= 0, x // 2, -((-x) // 2))
+        return _clip(a + half)
+    raise ValueError(mode)
+
+
+def neighbours(P):
+    """P: (H, W, 4) int64 channels A,R,G,B of the sub-green image. Returns
+    L, T, TL, TR with TR taken from the linear index (y-1)*W + x + 1 (the
+    rightmost column reads the first pixel of the current row, as the
+    decoder's `top[1]` does)."""
+    H, W, _ = P.shape
+    flat = P.reshape(-1, 4)
+    idx = np.arange(H * W).reshape(H, W)
+    L = flat[np.maximum(idx - 1, 0)]
+    T = flat[np.maximum(idx - W, 0)]
+    TL = flat[np.maximum(idx - W - 1, 0)]
+    TR = flat[np.maximum(idx - W + 1, 0)]
+    return L, T, TL, TR
+
+
+def fixed_mode_mask(H, W):
+    """-1 where the tile mode applies; else the fixed mode (0 at (0,0), 1 on
+    row 0, 2 on column 0) -- PredictorInverseTransform_C :219-239."""
+    m = np.full((H, W), -1, dtype=np.int64)
+    m[0, :] = 1
+    m[:, 0] = 2
+    m[0, 0] = 0
+    return m
+
+
+def tile_sums(values, tb, H, W):
+    """Histogram-entropy score S = sum over channels/bins of nlogn(count) for
+    each tile. values: (H, W, C) int64 in 0..255."""
+    tw, th = sub_sample(W, tb), sub_sample(H, tb)
+    ty = (np.arange(H) >> tb)[:, None]
+    tx = (np.arange(W) >> tb)[None, :]
+    tile = (ty * tw + tx)
+    C_ = values.shape[-1]
+    key = (tile[..., None] * C_ + np.arange(C_)) * 256 + values
+    cnt = np.bincount(key.ravel(), minlength=tw * th * C_ * 256)
+    return NLOGN[cnt].reshape(tw * th, C_ * 256).sum(axis=1)
+
+
+def to_s8(v):
+    v = np.asarray(v, dtype=np.int64) & 255
+    return np.where(v >= 128, v - 256, v)
+
+
+def ctd(t, c):
+    """ColorTransformDelta (src/dsp/lossless.c:274-277): signed 8-bit."""
+    return (np.asarray(t, dtype=np.int64) * to_s8(c)) >> 5
+
+
+def ls_multiplier(sxy, sxx):
+    """round(32 * sxy / sxx) half away from zero, clamped to int8."""
+    if sxx == 0:
+        return 0
+    num = 32 * sxy
+    q = (2 * abs(num) + sxx) // (2 * sxx)
+    q = q if num >= 0 else -q
+    return int(max(-128, min(127, q)))
+
+
+def candidates(ls):
+    out = [0]
+    for c in (ls - 1, ls, ls + 1):
+        out.append(max(-128, min(127, c)))
+    return out
+
+
+def choose_cross_color(res, tb, H, W):
+    """res: (H, W, 4) predictor residuals (A,R,G,B). Per tile choose
+    (g2r, g2b, r2b) -- least squares start + entropy check of 4 candidates
+    each. Returns (tiles, 3) int and the transformed residual image."""
+    tw, th = sub_sample(W, tb), sub_sample(H, tb)
+    out = res.copy()
+    mult = np.zeros((th * tw, 3), dtype=np.int64)
+    for ty in range(th):
+        for tx in range(tw):
+            blk = res[ty << tb:(ty + 1) << tb, tx << tb:(tx + 1) << tb].reshape(-1, 4)
+            g = to_s8(blk[:, 2]); r = to_s8(blk[:, 1]); b = blk[:, 3]
+            sgg = int((g * g).sum())
+            best = None
+            for t in candidates(ls_multiplier(int((g * r).sum()), sgg)):
+                s = int(NLOGN[np.bincount((blk[:, 1] - ctd(t, g)) & 255, minlength=256)].sum())
+                if best is None or s > best[0]:
+                    best = (s, t)
+            g2r = best[1]
+            best = None
+            for t in candidates(ls_multiplier(int((g * to_s8(b)).sum()), sgg)):
+                s = int(NLOGN[np.bincount((b - ctd(t, g)) & 255, minlength=256)].sum())
+                if best is None or s > best[0]:
+                    best = (s, t)
+            g2b = best[1]
+            bb = (b - ctd(g2b, g)) & 255
+            srr = int((r * r).sum())
+            best = None
+            for t in candidates(ls_multiplier(int((r * to_s8(bb)).sum()), srr)):
+                s = int(NLOGN[np.bincount((bb - ctd(t, r)) & 255, minlength=256)].sum())
+                if best is None or s > best[0]:
+                    best = (s, t)
+            r2b = best[1]
+            k = ty * tw + tx
+            mult[k] = (g2r, g2b, r2b)
+            o = out[ty << tb:(ty + 1) << tb, tx << tb:(tx + 1) << tb]
+            og = to_s8(o[..., 2]); orr = to_s8(o[..., 1])
+            o[..., 3] = (o[..., 3] - ctd(g2b, og) - ctd(r2b, orr)) & 255
+            o[..., 1] = (o[..., 1] - ctd(g2r, og)) & 255
+    return mult, out
+
+
+def transform_image(rgba, tb):
+    """Subtract green -> predictor (per-tile best of 14 by histogram entropy)
+    -> cross colour. Returns (modes (tiles,), mult (tiles,3), residual ARGB
+    uint32 (H, W))."""
+    H, W, _ = rgba.shape
+    a = rgba[..., 3].astype(np.int64); r = rgba[..., 0].astype(np.int64)
+    g = rgba[..., 1].astype(np.int64); b = rgba[..., 2].astype(np.int64)
+    P = np.stack([a, (r - g) & 255, g, (b - g) & 255], axis=-1)
+    L, T, TL, TR = neighbours(P)
+    fixed = fixed_mode_mask(H, W)
+    preds = [predict(m, L, T, TL, TR) for m in range(14)]
+    fres = np.zeros_like(P)
+    for m in (0, 1, 2):
+        sel = fixed == m
+        fres[sel] = (P[sel] - preds[m][sel]) & 255
+    scores = []
+    for m in range(14):
+        rm = np.where((fixed >= 0)[..., None], fres, (P - preds[m]) & 255)
+        scores.append(tile_sums(rm, tb, H, W))
+    scores = np.stack(scores)               # (14, tiles)
+    modes = np.argmax(scores, axis=0)       # first maximum = lowest mode on ties
+    tw = sub_sample(W, tb)
+    tmode = modes[((np.arange(H) >> tb)[:, None] * tw + (np.arange(W) >> tb)[None, :])]
+    res = fres.copy()
+    for m in range(14):
+        sel = (tmode == m) & (fixed < 0)
+        res[sel] = (P[sel] - preds[m][sel]) & 255
+    mult, res = choose_cross_color(res, tb, H, W)
+    argb = (res[..., 0] << 24) | (res[..., 1] << 16) | (res[..., 2] << 8) | res[..., 3]
+    return modes, mult, argb.astype(np.uint32)
+
+
+# ---------------------------------------------------------------- LZ77 / cache
+
+def cache_hits(argb_flat, bits):
+    """hit[p] = 1 when the decoder's colour cache (every earlier pixel
+    inserted in order, src/dec/vp8l_dec.c:1209-1213,1245-1248) holds argb[p]
+    at its key."""
+    if bits == 0:
+        return np.zeros(len(argb_flat), dtype=bool)
+    keys = ((argb_flat.astype(np.uint64) * HASH_MUL) & 0xFFFFFFFF) >> (32 - bits)
+    keys = keys.astype(np.int64)
+    # previous position with the same key
+    order = np.argsort(keys, kind="stable")
+    ks = keys[order]
+    prev = np.full(len(keys), -1, dtype=np.int64)
+    same = ks[1:] == ks[:-1]
+    prev[order[1:][same]] = order[:-1][same]
+    # the decoder's cache starts zeroed (VP8LColorCacheInit calloc)
+    held = np.where(prev >= 0, argb_flat[np.maximum(prev, 0)], 0)
+    return held == argb_flat
+
+
+def match_lengths(argb, dists):
+    """len[k, y, x]: run of argb[p+i] == argb[p+i-d] for candidate k, within
+    the row (copies never cross a row end), capped at MAX_LENGTH."""
+    H, W = argb.shape
+    flat = argb.ravel()
+    out = np.zeros((len(dists), H, W), dtype=np.int64)
+    idx = np.arange(H * W)
+    for k, d in enumerate(dists):
+        eq = np.zeros(H * W, dtype=bool)
+        eq[d:] = flat[d:] == flat[:-d]
+        eq = eq.reshape(H, W)
+        run = np.zeros((H, W + 1), dtype=np.int64)
+        for x in range(W - 1, -1, -1):
+            run[:, x] = np.where(eq[:, x], run[:, x + 1] + 1, 0)
+        out[k] = np.minimum(run[:, :W], MAX_LENGTH)
+    return out
+
+
+def parse(argb, bits, dists):
+    """Greedy parse, each row on its own (one GPU thread per row). Per pixel:
+    act 0 literal, 1 cache hit, 2 copy start, 3 inside a copy; clen/ccode =
+    length and distance code of a copy start. Rule: copy when the best
+    candidate run is >= MIN_COPY, or == 2 and the pixel is no cache hit;
+    else cache hit; else literal."""
+    H, W = argb.shape
+    flat = argb.ravel()
+    hit = cache_hits(flat, bits).reshape(H, W)
+    lens = match_lengths(argb, dists)
+    best = np.argmax(lens, axis=0)                  # first maximum
+    blen = np.take_along_axis(lens, best[None], axis=0)[0]
+    dcode = np.array([distance_code(W, d) for d in dists], dtype=np.int64)
+    act = np.zeros((H, W), dtype=np.int64)
+    clen = np.zeros((H, W), dtype=np.int64)
+    for y in range(H):
+        bl = blen[y].tolist(); ht = hit[y].tolist()
+        ar = act[y]
+        x = 0
+        while x < W:
+            n = bl[x]
+            if n >= MIN_COPY or (n == 2 and not ht[x]):
+                ar[x] = 2
+                ar[x + 1:x + n] = 3
+                clen[y, x] = n
+                x += n
+            else:
+                ar[x] = 1 if ht[x] else 0
+                x += 1
+    ccode = np.where(act == 2, dcode[best], 0)
+    return act, clen, ccode
+
+
+def prefix_arrays(v):
+    """Vectorised prefix_encode for v >= 1 (0 where v == 0)."""
+    v = np.asarray(v, dtype=np.int64)
+    d = np.maximum(v - 1, 0)
+    h = np.frexp(d.astype(np.float64))[1].astype(np.int64) - 1   # floor(log2 d), d >= 1
+    small = d < 4
+    s = np.where(small, d, 2 * h + ((d >> np.maximum(h - 1, 0)) & 1))
+    nb = np.where(small, 0, h - 1)
+    e = np.where(small, 0, d & ((1 << np.maximum(nb, 0)) - 1))
+    return s, nb, e
+
+
+class Alphabets:
+    """Concatenated symbol space G | R | B | A | D of one code group."""
+
+    def __init__(self, cache_bits):
+        self.gs = NUM_LITERAL + NUM_LENGTH + ((1 << cache_bits) if cache_bits else 0)
+        self.sizes = [self.gs, 256, 256, 256, NUM_DIST]
+        self.off = [0, self.gs, self.gs + 256, self.gs + 512, self.gs + 768]
+        self.ns = self.gs + 768 + NUM_DIST
+
+    def split(self, h):
+        return [h[o:o + n] for o, n in zip(self.off, self.sizes)]
+
+
+def pixel_symbols(argb, act, clen, ccode, bits, al):
+    """Per pixel, the symbols it writes (index in the concatenated space, -1
+    for none) and the two extra-bit fields, in write order
+    s0, x0, s1, x1, s2, s3 (src/dec/vp8l_dec.c:1183-1222)."""
+    a = argb.astype(np.int64)
+    g = (a >> 8) & 255; r = (a >> 16) & 255; b = a & 255; al_ = (a >> 24) & 255
+    S = np.full(a.shape + (4,), -1, dtype=np.int64)
+    X = np.zeros(a.shape + (4,), dtype=np.int64)   # x0 value, x0 bits, x1 value, x1 bits
+    lit = act == 0
+    S[lit, 0] = g[lit]; S[lit, 1] = al.off[1] + r[lit]
+    S[lit, 2] = al.off[2] + b[lit]; S[lit, 3] = al.off[3] + al_[lit]
+    if bits:
+        keys = (((a.astype(np.uint64) * HASH_MUL) & 0xFFFFFFFF) >> (32 - bits)).astype(np.int64)
+        ch = act == 1
+        S[ch, 0] = 280 + keys[ch]
+    cp = act == 2
+    ls, lnb, le = prefix_arrays(clen[cp])
+    ds, dnb, de = prefix_arrays(ccode[cp])
+    S[cp, 0] = 256 + ls; S[cp, 1] = al.off[4] + ds
+    X[cp, 0] = le; X[cp, 1] = lnb; X[cp, 2] = de; X[cp, 3] = dnb
+    return S, X
+
+
+# ---------------------------------------------------------------- Huffman
+
+def huffman_lengths(hist, limit):
+    """Two-queue Huffman on (max(count, count_min), symbol)-sorted leaves;
+    count_min doubles until the depth fits `limit` (the same retry idea as
+    src/utils/huffman_encode_utils.c GenerateOptimalTree)."""
+    hist = list(hist)
+    n = len(hist)
+    lengths = [0] * n
+    syms = [s for s in range(n) if hist[s] > 0]
+    if not syms:
+        return lengths
+    if len(syms) == 1:
+        lengths[syms[0]] = 1
+        return lengths
+    count_min = 1
+    while True:
+        leaves = sorted((max(hist[s], count_min), s) for s in syms)
+        parent = {}
+        q1 = [(w, ("l", s)) for w, s in leaves]
+        q2 = []
+        i1 = i2 = 0
+        nid = 0
+
+        def pop():
+            nonlocal i1, i2
+            if i2 >= len(q2) or (i1 < len(q1) and q1[i1][0] <= q2[i2][0]):
+                i1 += 1
+                return q1[i1 - 1]
+            i2 += 1
+            return q2[i2 - 1]
+
+        while (len(q1) - i1) + (len(q2) - i2) > 1:
+            a = pop(); b = pop()
+            node = ("n", nid); nid += 1
+            parent[a[1]] = node; parent[b[1]] = node
+            q2.append((a[0] + b[0], node))
+        depth = {}
+
+        def dep(k):
+            if k not in parent:
+                return 0
+            if k not in depth:
+                depth[k] = dep(parent[k]) + 1
+            return depth[k]
+
+        for s in syms:
+            lengths[s] = dep(("l", s))
+        if max(lengths) <= limit:
+            return lengths
+        count_min *= 2
+
+
+def canonical_codes(lengths):
+    """Deflate canonical codes, bit-reversed for the LSB-first writer."""
+    maxl = max(lengths) if lengths else 0
+    bl = [0] * (maxl + 2)
+    for l in lengths:
+        if l:
+            bl[l] += 1
+    code = 0
+    nxt = [0] * (maxl + 2)
+    for b in range(1, maxl + 1):
+        code = (code + bl[b - 1]) << 1
+        nxt[b] = code
+    codes = [0] * len(lengths)
+    for s, l in enumerate(lengths):
+        if l:
+            c = nxt[l]; nxt[l] += 1
+            codes[s] = int(format(c, "0%db" % l)[::-1], 2)
+    return codes
+
+
+class BitWriter:
+    def __init__(self):
+        self.out = bytearray()
+        self.acc = 0
+        self.used = 0     # bits in acc
+        self.n = 0        # total bits
+
+    def put(self, v, nbits):
+        if nbits:
+            self.acc |= (v & ((1 << nbits) - 1)) << self.used
+            self.used += nbits
+            self.n += nbits
+            while self.used >= 8:
+                self.out.append(self.acc & 255)
+                self.acc >>= 8
+                self.used -= 8
+
+    def bytes(self):
+        tail = bytes([self.acc & 255]) if self.used else b""
+        return bytes(self.out) + tail
+
+
+def code_length_tokens(lengths):
+    """RLE of code lengths with 16 (repeat previous 3..6), 17 (zeros 3..10),
+    18 (zeros 11..138) -- decoder :255-317."""
+    toks = []
+    i, n = 0, len(lengths)
+    while i < n:
+        v = lengths[i]
+        j = i
+        while j < n and lengths[j] == v:
+            j += 1
+        run = j - i
+        if v == 0:
+            while run > 0:
+                if run < 3:
+                    toks += [(0, 0)] * run
+                    run = 0
+                elif run <= 10:
+                    toks.append((17, run - 3)); run = 0
+                else:
+                    r = min(run, 138)
+                    toks.append((18, r - 11)); run -= r
+        else:
+            toks.append((v, 0)); run -= 1
+            while run > 0:
+                if run < 3:
+                    toks += [(v, 0)] * run
+                    run = 0
+                else:
+                    r = min(run, 6)
+                    toks.append((16, r - 3)); run -= r
+        i = j
+    return toks
+
+
+class Code:
+    """A Huffman code as written: bits per symbol used by the data writer
+    (0 for codes with <= 1 used symbol, which the decoder reads with 0 bits)."""
+
+    def __init__(self, hist):
+        self.hist = list(hist)
+        self.lengths = huffman_lengths(self.hist, 15)
+        used = [s for s, c in enumerate(self.hist) if c > 0]
+        self.used = used
+        self.codes = canonical_codes(self.lengths)
+        self.wlen = list(self.lengths)
+        if len(used) <= 1:
+            self.wlen = [0] * len(self.lengths)
+
+    def store(self, bw):
+        used = self.used
+        if not used:
+            bw.put(1, 1); bw.put(0, 1); bw.put(0, 1); bw.put(0, 1)
+            return
+        if len(used) <= 2 and max(used) < 256:
+            bw.put(1, 1)
+            bw.put(len(used) - 1, 1)
+            if used[0] <= 1:
+                bw.put(0, 1); bw.put(used[0], 1)
+            else:
+                bw.put(1, 1); bw.put(used[0], 8)
+            if len(used) == 2:
+                bw.put(used[1], 8)
+            return
+        bw.put(0, 1)
+        toks = code_length_tokens(self.lengths)
+        th = [0] * 19
+        for c, _ in toks:
+            th[c] += 1
+        cl = huffman_lengths(th, 7)
+        cc = canonical_codes(cl)
+        ncodes = 19
+        while ncodes > 4 and cl[CODE_LENGTH_ORDER[ncodes - 1]] == 0:
+            ncodes -= 1
+        bw.put(ncodes - 4, 4)
+        for i in range(ncodes):
+            bw.put(cl[CODE_LENGTH_ORDER[i]], 3)
+        single = sum(1 for l in cl if l) <= 1
+        bw.put(0, 1)   # no max_symbol
+        for c, e in toks:
+            if not single:
+                bw.put(cc[c], cl[c])
+            if c == 16:
+                bw.put(e, 2)
+            elif c == 17:
+                bw.put(e, 3)
+            elif c == 18:
+                bw.put(e, 7)
+
+    def put(self, bw, s):
+        bw.put(self.codes[s], self.wlen[s])
+
+
+def write_sub_image(bw, pix):
+    """A transform / entropy sub-image (level > 0, src/dec/vp8l_dec.c:1455-1483
+    with is_level0 = 0): no colour cache, no meta codes, literals only."""
+    pix = np.asarray(pix, dtype=np.int64)
+    hs = [np.bincount((pix >> 8) & 255, minlength=NUM_LITERAL + NUM_LENGTH),
+          np.bincount((pix >> 16) & 255, minlength=256),
+          np.bincount(pix & 255, minlength=256),
+          np.bincount((pix >> 24) & 255, minlength=256), np.zeros(NUM_DIST, dtype=np.int64)]
+    codes = [Code(h) for h in hs]
+    bw.put(0, 1)   # no colour cache
+    for c in codes:
+        c.store(bw)
+    G, R, B, A, _ = codes
+    for v in pix.tolist():
+        G.put(bw, (v >> 8) & 255); R.put(bw, (v >> 16) & 255)
+        B.put(bw, v & 255); A.put(bw, (v >> 24) & 255)
+
+
+def riff(payload):
+    pad = len(payload) & 1
+    chunk = b"VP8L" + struct.pack("<I", len(payload)) + payload + (b"\0" if pad else b"")
+    return b"RIFF" + struct.pack("<I", 4 + len(chunk)) + b"WEBP" + chunk
+
+
+# ---------------------------------------------------------------- clustering
+
+def _flog2_frac():
+    return np.array([int(math.floor(4096 * math.log2(1 + m / 1024.0) + 0.5))
+                     for m in range(1024)], dtype=np.int64)
+
+
+FLOG2_FRAC = _flog2_frac()
+
+
+def flog2(v):
+    """Fixed-point log2 in 1/4096 bit for integers v >= 1: exponent from the
+    leading one, fraction from the next 10 bits (table)."""
+    v = np.asarray(v, dtype=np.int64)
+    e = np.frexp(v.astype(np.float64))[1].astype(np.int64) - 1
+    m = np.where(e >= 10, v >> np.maximum(e - 10, 0), v << np.maximum(10 - e, 0)) & 1023
+    return (e << 12) + FLOG2_FRAC[m]
+
+
+KMAX = 16
+CLUSTER_ITERS = 6
+
+
+def symbol_costs(Hc, al):
+    """Per cluster, estimated bits (1/256, fits 16 bits) of each symbol:
+    log2((10 N + A) / (10 n + 1)) within its alphabet."""
+    L = np.zeros_like(Hc)
+    for o, n in zip(al.off, al.sizes):
+        h = Hc[:, o:o + n]
+        N = h.sum(axis=1, keepdims=True)
+        L[:, o:o + n] = (flog2(10 * N + n) - flog2(10 * h + 1)) >> 4
+    return L
+
+
+def tile_histograms(S, tile, nt, al):
+    k = (tile[..., None] * al.ns + S)[S >= 0]
+    return np.bincount(k.ravel(), minlength=nt * al.ns).reshape(nt, al.ns)
+
+
+def cluster_tiles(Ht, npix, al, K):
+    """k-means over tile histograms with integer entropy costs. Init: tiles
+    ranked by their own Shannon bits per pixel, cut into K quantiles.
+    Returns the assignment (nt,)."""
+    nt = Ht.shape[0]
+    own = np.zeros(nt, dtype=np.int64)
+    for o, n in zip(al.off, al.sizes):
+        h = Ht[:, o:o + n]
+        N = h.sum(axis=1)
+        own += N * np.where(N > 0, flog2(np.maximum(N, 1)), 0) - \
+            (h * np.where(h > 0, flog2(np.maximum(h, 1)), 0)).sum(axis=1)
+    feat = own // np.maximum(npix, 1)
+    rank = np.empty(nt, dtype=np.int64)
+    rank[np.lexsort((np.arange(nt), feat))] = np.arange(nt)
+    assign = rank * K // nt
+    for _ in range(CLUSTER_ITERS):
+        Hc = np.zeros((K, al.ns), dtype=np.int64)
+        np.add.at(Hc, assign, Ht)
+        C = Ht @ symbol_costs(Hc, al).T          # (nt, K)
+        assign = np.argmin(C, axis=1)            # first minimum
+    return assign
+
+
+# ---------------------------------------------------------------- data bits
+
+def group_bits(codes_of_group, al):
+    """Table (ngroups, ns) of (code, bits) for the data writer."""
+    ng = len(codes_of_group)
+    code = np.zeros((ng, al.ns), dtype=np.int64)
+    nb = np.zeros((ng, al.ns), dtype=np.int64)
+    for gi, codes in enumerate(codes_of_group):
+        for o, c in zip(al.off, codes):
+            code[gi, o:o + len(c.codes)] = c.codes
+            nb[gi, o:o + len(c.codes)] = c.wlen
+    return code, nb
+
+
+def pixel_fields(S, X, grp, code, nb):
+    """Per pixel the 6 fields s0, x0, s1, x1, s2, s3 as (value, bits)."""
+    Sg = np.where(S >= 0, S, 0)
+    v = np.zeros(S.shape[:-1] + (6,), dtype=np.int64)
+    b = np.zeros_like(v)
+    for i, f in ((0, 0), (1, 2), (2, 4), (3, 5)):
+        ok = S[..., i] >= 0
+        v[..., f] = np.where(ok, code[grp, Sg[..., i]], 0)
+        b[..., f] = np.where(ok, nb[grp, Sg[..., i]], 0)
+    v[..., 1] = X[..., 0]; b[..., 1] = X[..., 1]
+    v[..., 3] = X[..., 2]; b[..., 3] = X[..., 3]
+    return v.reshape(-1), b.reshape(-1)
+
+
+def pack_fields(v, b, start_bit):
+    """OR every field into 32-bit words at its running bit offset (what the
+    GPU writer does with atomics). Returns (words, end_bit)."""
+    off = start_bit + np.concatenate([[0], np.cumsum(b)[:-1]])
+    end = int(start_bit + b.sum())
+    words = np.zeros(((end + 31) >> 5) + 2, dtype=np.uint64)
+    m = b > 0
+    v, b, off = v[m].astype(np.uint64), b[m], off[m]
+    w = (off >> 5).astype(np.int64); sh = (off & 31).astype(np.uint64)
+    np.bitwise_or.at(words, w, (v << sh) & np.uint64(0xFFFFFFFF))
+    spill = (sh + b.astype(np.uint64)) > 32
+    np.bitwise_or.at(words, w[spill] + 1, v[spill] >> (np.uint64(32) - sh[spill]))
+    return words.astype(np.uint32), end
+
+
+DEFAULT_CACHE_BITS = 8
+
+
+def encode(rgba, method=4, cache_bits=DEFAULT_CACHE_BITS, kmax=KMAX, return_parts=False):
+    """rgba: (H, W, 4) uint8 -> .webp bytes (VP8L)."""
+    H, W, _ = rgba.shape
+    hb = histo_bits(method, W, H)
+    tb = transform_bits(method, hb)
+    modes, mult, argb = transform_image(rgba, tb)
+    act, clen, ccode = parse(argb, cache_bits, candidate_distances(W))
+    al = Alphabets(cache_bits)
+    S, X = pixel_symbols(argb, act, clen, ccode, cache_bits, al)
+    tw, th = sub_sample(W, hb), sub_sample(H, hb)
+    nt = tw * th
+    tile = (np.arange(H) >> hb)[:, None] * tw + (np.arange(W) >> hb)[None, :]
+    Ht = tile_histograms(S, tile, nt, al)
+    npix = np.bincount(tile.ravel(), minlength=nt)
+    K = min(kmax, nt)
+    assign = cluster_tiles(Ht, npix, al, K) if K > 1 else np.zeros(nt, dtype=np.int64)
+    assign_raw = assign.copy()
+    hc_raw = np.zeros((KMAX, al.ns), dtype=np.int64)
+    np.add.at(hc_raw, assign_raw, Ht)
+    # drop empty clusters, keep order
+    used = sorted(set(assign.tolist()))
+    remap = {c: i for i, c in enumerate(used)}
+    assign = np.array([remap[c] for c in assign.tolist()], dtype=np.int64)
+    Hc = np.zeros((len(used), al.ns), dtype=np.int64)
+    np.add.at(Hc, assign, Ht)
+    groups = [[Code(h) for h in al.split(Hc[k])] for k in range(len(used))]
+    single = [Code(h) for h in al.split(Hc.sum(axis=0))]
+    # keep the meta codes only when they are cheaper, exact bits incl. headers
+    def cost(groups_, hist_rows, meta):
+        bw = BitWriter()
+        if meta:
+            bw.put(1, 1); bw.put(hb - 2, 3)
+            write_sub_image(bw, [int(a) << 8 for a in assign])
+        for codes in groups_:
+            for c in codes:
+                c.store(bw)
+        data = sum(int((h * np.array(c.wlen)).sum())
+                   for hr, codes in zip(hist_rows, groups_) for h, c in zip(al.split(hr), codes))
+        return bw.n + data
+    meta = len(used) > 1 and cost(groups, Hc, True) < cost([single], [Hc.sum(axis=0)], False)
+    if not meta:
+        groups = [single]
+        assign = np.zeros(nt, dtype=np.int64)
+    bw = BitWriter()
+    bw.put(0x2F, 8); bw.put(W - 1, 14); bw.put(H - 1, 14)
+    bw.put(int((rgba[..., 3] != 255).any()), 1); bw.put(0, 3)
+    # SUBTRACT_GREEN, PREDICTOR, CROSS_COLOR (applied in this order)
+    bw.put(1, 1); bw.put(2, 2)
+    bw.put(1, 1); bw.put(0, 2); bw.put(tb - 2, 3)
+    write_sub_image(bw, [0xFF000000 | (int(m) << 8) for m in modes])
+    bw.put(1, 1); bw.put(1, 2); bw.put(tb - 2, 3)
+    write_sub_image(bw, [0xFF000000 | ((int(c[2]) & 255) << 16) | ((int(c[1]) & 255) << 8)
+                         | (int(c[0]) & 255) for c in mult])
+    bw.put(0, 1)   # no more transforms
+    if cache_bits:
+        bw.put(1, 1); bw.put(cache_bits, 4)
+    else:
+        bw.put(0, 1)
+    if meta:
+        bw.put(1, 1); bw.put(hb - 2, 3)
+        write_sub_image(bw, [int(a) << 8 for a in assign])
+    else:
+        bw.put(0, 1)
+    for codes in groups:
+        for c in codes:
+            c.store(bw)
+    header_bits = bw.n
+    header = bw.bytes()
+    code, nb = group_bits(groups, al)
+    grp = assign[tile]
+    v, b = pixel_fields(S, X, grp, code, nb)
+    words, end = pack_fields(v, b, header_bits)
+    head = np.frombuffer(bw.bytes() + b"\0" * 8, dtype=np.uint8)
+    buf = words.view(np.uint8).copy()
+    hb_bytes = (header_bits + 7) // 8
+    buf[:hb_bytes] |= head[:hb_bytes]
+    payload = buf[:(end + 7) // 8].tobytes()
+    out = riff(payload)
+    if return_parts:
+        return out, dict(modes=modes, mult=mult, argb=argb, act=act, clen=clen, ccode=ccode,
+                         assign=assign, groups=len(groups), header_bits=header_bits, tb=tb,
+                         hb=hb, Hc=Hc, assign_raw=assign_raw, hc_raw=hc_raw, header=header,
+                         code=code, nb=nb, k=K)
+    return out
+
+
+# ---------------------------------------------------------------- decode check
+
+def ref_decode(lib, data):
+    """Decode with the reference decoder (oracle/_ref): (H, W, 4) RGBA."""
+    import ctypes as C
+    lib.WebPDecodeRGBA.restype = C.c_void_p
+    lib.WebPDecodeRGBA.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_int),
+                                   C.POINTER(C.c_int)]
+    lib.WebPFree.argtypes = [C.c_void_p]
+    w = C.c_int(); h = C.c_int()
+    p = lib.WebPDecodeRGBA(data, len(data), C.byref(w), C.byref(h))
+    if not p:
+        raise ValueError("reference decoder rejected the bitstream")
+    out = np.frombuffer(C.string_at(p, w.value * h.value * 4), dtype=np.uint8)
+    lib.WebPFree(p)
+    return out.reshape(h.value, w.value, 4).copy()

@@ -1,0 +1,210 @@
+"""Lossless (VP8L) path.
+
+Parity contract (SURVEY.md §8(d), configs[4]): the bitstream must decode --
+with the reference decoder -- to exactly the input pixels, and its size must
+stay within VP8L_SIZE_TOL of the reference encoder's on the same frame. The
+GPU bitstream is also checked bit for bit against oracle/vp8l_model.py, the
+plain statement of the GPU algorithm (small frames), and the host header code
+(vp8l_host.c) against the same model on CPU.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from libwebp_amd.synth import syn_v1
+from oracle import vp8l_model as M
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# size of our lossless output relative to the reference encoder's (-lossless
+# -m 4 -q 75) on syn-v1 frames: measured +3.5% at 512x512 and +6.2% at 1080p
+VP8L_SIZE_TOL = 0.08
+
+CASES = [(64, 48, 0), (33, 17, 3), (1, 1, 0), (7, 5, 1), (2, 130, 4), (130, 3, 2)]
+
+
+def ref_decoder():
+    path = os.path.join(ROOT, "oracle", "_ref", "libwebp_ref.so")
+    if not os.path.exists(path):
+        pytest.skip("reference build oracle/_ref not present")
+    return C.CDLL(path)
+
+
+def with_alpha(img, seed):
+    rng = np.random.default_rng(seed)
+    out = img.copy()
+    out[..., 3] = rng.integers(0, 256, size=img.shape[:2], dtype=np.uint8)
+    out[: img.shape[0] // 2, :, 3] = 255
+    return out
+
+
+# ------------------------------------------------------------------ model
+
+@pytest.mark.parametrize("w,h,f", CASES)
+def test_model_decodes_exact(w, h, f):
+    lib = ref_decoder()
+    img = syn_v1(w, h, f)
+    assert np.array_equal(M.ref_decode(lib, M.encode(img)), img)
+
+
+def test_model_decodes_exact_alpha_and_methods():
+    lib = ref_decoder()
+    img = with_alpha(syn_v1(96, 80, 5), 3)
+    for method in (0, 3, 4, 6):
+        assert np.array_equal(M.ref_decode(lib, M.encode(img, method=method)), img)
+
+
+def test_model_size_vs_reference_512():
+    lib = ref_decoder()
+    from libwebp_amd import abi
+    ref = abi.bind_encoder_api(lib)
+    img = syn_v1(512, 512, 0)
+    ours = M.encode(img)
+    theirs, _ = abi.encode_rgba(ref, img, quality=75.0, method=4, lossless=1, use_argb=True)
+    assert len(ours) <= len(theirs) * (1 + VP8L_SIZE_TOL), (len(ours), len(theirs))
+
+
+def test_prefix_and_distance_codes():
+    for v in list(range(1, 70)) + [4095, 4096, 100000]:
+        s, nb, e = M.prefix_encode(v)
+        # GetCopyDistance (src/dec/vp8l_dec.c:159-168)
+        if s < 4:
+            back = s + 1
+        else:
+            xb = (s - 2) >> 1
+            back = ((2 + (s & 1)) << xb) + e + 1
+            assert xb == nb
+        assert back == v
+    for w in (1, 2, 7, 64, 1920):
+        for d in M.candidate_distances(w):
+            assert M.plane_code_to_distance(w, M.distance_code(w, d)) == d
+
+
+# ------------------------------------------------------------------ host C vs model
+
+class Params(C.Structure):
+    _fields_ = [("w", C.c_int), ("h", C.c_int), ("n", C.c_int), ("tb", C.c_int),
+                ("hb", C.c_int), ("k", C.c_int), ("dist", C.c_int * 4), ("dcode", C.c_int * 4)]
+
+
+class BW(C.Structure):
+    _fields_ = [("buf", C.c_void_p), ("cap", C.c_size_t), ("pos", C.c_size_t),
+                ("acc", C.c_uint64), ("used", C.c_int), ("nbits", C.c_uint64), ("oom", C.c_int)]
+
+
+@pytest.fixture(scope="module")
+def host_lib(tmp_path_factory):
+    """vp8l_host.c compiled on its own (default visibility) for the test."""
+    out = str(tmp_path_factory.mktemp("vp8l") / "libvp8lhost.so")
+    src = os.path.join(ROOT, "libwebp_amd", "csrc", "host", "vp8l_host.c")
+    subprocess.check_call(["gcc", "-O1", "-shared", "-fPIC", "-I",
+                           os.path.join(ROOT, "libwebp_amd", "csrc"), src, "-o", out,
+                           "-lm", "-lpthread"])
+    lib = C.CDLL(out)
+    vp = C.c_void_p
+    lib.vp8l_build_header.restype = C.c_int
+    lib.vp8l_build_header.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp]
+    lib.vp8l_bw_finish.restype = C.c_size_t
+    lib.vp8l_bw_finish.argtypes = [vp]
+    lib.vp8l_bw_init.argtypes = [vp, C.c_size_t]
+    lib.vp8l_bw_free.argtypes = [vp]
+    lib.vp8l_setup_params.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int]
+    return lib
+
+
+def vp8l_ns():
+    return M.Alphabets(M.DEFAULT_CACHE_BITS).ns
+
+
+@pytest.mark.parametrize("w,h,f,alpha,method", [
+    (64, 48, 0, False, 4), (33, 17, 3, False, 4), (1, 1, 0, False, 4), (256, 192, 2, False, 4),
+    (200, 130, 6, True, 4), (160, 96, 1, False, 6), (97, 61, 2, False, 3)])
+def test_host_header_matches_model(host_lib, w, h, f, alpha, method):
+    img = syn_v1(w, h, f)
+    if alpha:
+        img = with_alpha(img, f)
+    _, P = M.encode(img, method=method, return_parts=True)
+    p = Params()
+    host_lib.vp8l_setup_params(C.byref(p), w, h, 1, method)
+    assert (p.tb, p.hb, p.k) == (P["tb"], P["hb"], P["k"])
+    dists = M.candidate_distances(w)
+    assert list(p.dist)[:len(dists)] == dists
+    assert list(p.dcode)[:len(dists)] == [M.distance_code(w, d) for d in dists]
+    ns = vp8l_ns()
+    modes = np.ascontiguousarray(P["modes"], dtype=np.uint8)
+    mult = np.ascontiguousarray((P["mult"][:, 0] & 255) | ((P["mult"][:, 1] & 255) << 8) |
+                                ((P["mult"][:, 2] & 255) << 16), dtype=np.uint32)
+    hc = np.ascontiguousarray(P["hc_raw"], dtype=np.uint32)
+    assert hc.shape == (16, ns)
+    assign = np.ascontiguousarray(P["assign_raw"], dtype=np.uint8)
+    ctab = np.zeros((16, ns), dtype=np.uint32)
+    gtile = np.zeros(len(assign), dtype=np.uint8)
+    bw = BW()
+    host_lib.vp8l_bw_init(C.byref(bw), C.c_size_t(1 << 16))
+    ok = host_lib.vp8l_build_header(C.byref(p), int(alpha), modes.ctypes.data, mult.ctypes.data,
+                                    hc.ctypes.data, assign.ctypes.data, C.byref(bw),
+                                    ctab.ctypes.data, gtile.ctypes.data)
+    assert ok
+    nbits = bw.nbits
+    nb = host_lib.vp8l_bw_finish(C.byref(bw))
+    got = C.string_at(bw.buf, nb)
+    host_lib.vp8l_bw_free(C.byref(bw))
+    assert nbits == P["header_bits"]
+    assert got == P["header"]
+    G = P["groups"]
+    want = (P["code"] | (P["nb"] << 16)).astype(np.uint32)
+    assert np.array_equal(ctab[:G], want)
+    assert np.array_equal(gtile, P["assign"].astype(np.uint8))
+
+
+# ------------------------------------------------------------------ GPU
+
+def gpu_encode(gpu, frames, method=4):
+    import torch
+    n, h, w, _ = frames.shape
+    enc = gpu.GpuBatch(w, h, n, quality=75.0, method=method, lossless=1)
+    buf = torch.from_numpy(np.ascontiguousarray(frames)).to("cuda:0")
+    torch.cuda.synchronize()
+    enc.encode_device(buf.data_ptr(), n)
+    out = [enc.output(f) for f in range(n)]
+    enc.close()
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,f", CASES + [(256, 192, 2)])
+def test_gpu_matches_model(gpu, w, h, f):
+    img = syn_v1(w, h, f)
+    got = gpu_encode(gpu, img[None])[0]
+    assert got == M.encode(img)
+
+
+@pytest.mark.gpu
+def test_gpu_alpha_methods_match_model(gpu):
+    img = with_alpha(syn_v1(200, 130, 6), 6)
+    for method in (3, 4, 6):
+        assert gpu_encode(gpu, img[None], method=method)[0] == M.encode(img, method=method)
+
+
+@pytest.mark.gpu
+def test_gpu_batch_frames_match_model(gpu):
+    frames = np.stack([syn_v1(160, 96, f) for f in range(5)])
+    got = gpu_encode(gpu, frames)
+    for f in range(5):
+        assert got[f] == M.encode(frames[f]), "frame %d" % f
+
+
+@pytest.mark.gpu
+def test_gpu_1080p_decodes_exact_and_size(gpu):
+    lib = ref_decoder()
+    import json
+    kat = json.load(open(os.path.join(ROOT, "tests", "golden", "kat.json")))
+    sizes = {c["frame"]: c["size"] for c in kat.get("lossless", [])}
+    frames = np.stack([syn_v1(1920, 1080, f) for f in range(3)])
+    got = gpu_encode(gpu, frames)
+    for f in range(3):
+        assert np.array_equal(M.ref_decode(lib, got[f]), frames[f]), "frame %d" % f
+        if f in sizes:
+            assert len(got[f]) <= sizes[f] * (1 + VP8L_SIZE_TOL), (f, len(got[f]), sizes[f])

@@ -29,7 +29,7 @@ sys.path.insert(0, HERE)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
-def cpu_baseline(width, height, quality, method, seconds):
+def cpu_baseline(width, height, quality, method, seconds, lossless=False):
     """Reference libwebp (compiled from /root/reference sources into
     oracle/_ref by oracle/Makefile) timed single-threaded on this host:
     WebPPictureImportRGBA + WebPEncode into a memory writer, syn-v1 frames
@@ -43,7 +43,13 @@ def cpu_baseline(width, height, quality, method, seconds):
     if os.path.exists(ref):
         lib = C.CDLL(ref)
         abi.bind_encoder_api(lib)
-        enc = lambda img: abi.encode_rgba(lib, img, quality=quality, method=method)
+        if lossless:   # ARGB picture, like cwebp -lossless
+            enc = lambda img: abi.encode_rgba(lib, img, quality=quality, method=method,
+                                              lossless=1, use_argb=True)
+        else:
+            enc = lambda img: abi.encode_rgba(lib, img, quality=quality, method=method)
+    elif lossless:
+        return None
     else:   # the C restatement (oracle/), also single-threaded
         from oracle import oracle as orc
         kind = "port"
@@ -59,9 +65,10 @@ def cpu_baseline(width, height, quality, method, seconds):
         f += 1
     mps = frames * width * height / elapsed / 1e6
     return {"value": round(mps, 3), "unit": "MP/s", "cores": 1, "kind": kind,
-            "sample": "%d syn-v1 %dx%d frames (f=1..%d), q%d m%d, WebPPictureImportRGBA+"
-                      "WebPEncode, single thread, %.1f s" % (frames, width, height, frames,
-                                                             quality, method, elapsed)}
+            "sample": "%d syn-v1 %dx%d frames (f=1..%d), q%d m%d%s, WebPPictureImportRGBA+"
+                      "WebPEncode, single thread, %.1f s" % (
+                          frames, width, height, frames, quality, method,
+                          " lossless" if lossless else "", elapsed)}
 
 
 def measured_traffic(kernel, B, W, H, quality, method):
@@ -105,12 +112,61 @@ def max_over_ranks(seconds, world, device):
     return float(t.item())
 
 
+def lossless_line(args, world, B, W, H, elapsed, tails, total_bytes):
+    """configs[4] line: VP8L encode. Dominant kernel: the L1 transform tile
+    kernel (k_vp8l_transform); algorithmic bytes per launch = RGBA read
+    (4 B/px) + residual ARGB written (4 B/px) + per-tile modes/multipliers."""
+    mp = world * B * W * H * args.steps / 1e6
+    steps = len(tails)
+    avg = lambda i: sum(t[i] for t in tails) / steps
+    tb = 5 if args.method == 4 else (6 if args.method < 4 else 4)
+    ntt = ((W + (1 << tb) - 1) >> tb) * ((H + (1 << tb) - 1) >> tb)
+    l1_bytes = B * (8 * W * H + 5 * ntt)
+    l1_s = avg(7) / 1e6
+    achieved = l1_bytes / l1_s / 1e9 if l1_s > 0 else 0.0
+    line = {
+        "metric": "megapixels/sec encoded (cwebp -lossless -m 4, 1920x1080 batch)",
+        "value": round(mp / elapsed, 3),
+        "unit": "MP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8/u32",
+        "data": "synthetic syn-v1 RGBA frames generated in HBM (SURVEY.md 8(d))",
+        "config": {"workload": "batch of %d %dx%d RGBA frames per GPU, -lossless -q %g -m %d" %
+                               (B, W, H, args.quality, args.method),
+                   "frames_per_gpu": B, "width": W, "height": H, "quality": args.quality,
+                   "method": args.method, "parallelism": "frames sharded %d ways" % world},
+        "roofline": {"bound": "hbm", "kernel": "k_vp8l_transform", "achieved": round(achieved, 3),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                     "k_ms": round(1e3 * l1_s, 3), "algorithmic_bytes_per_launch": l1_bytes},
+        "stage_ms": {k: round(avg(i) / 1e3, 3) for k, i in
+                     (("transform_analysis", 0), ("host_headers", 1), ("bit_writer", 2),
+                      ("d2h", 3), ("riff", 4), ("total", 5), ("k_transform_events", 7),
+                      ("k_cache_parse_cluster_events", 6), ("k_write_events", 8))},
+        "output_bytes_per_frame": round(total_bytes / (world * B), 1),
+    }
+    if not args.no_cpu:
+        cb = cpu_baseline(W, H, int(args.quality), args.method, args.cpu_seconds, lossless=True)
+        if cb:
+            line["cpu_baseline"] = cb
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=256, help="frames per GPU per step")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per GPU per step (0: 256 lossy, 1024 lossless)")
+    ap.add_argument("--lossless", action="store_true",
+                    help="configs[4]: -lossless -m 4 (VP8L) instead of the lossy headline")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--quality", type=float, default=75.0)
@@ -136,7 +192,8 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     import libwebp_amd
-    W, H, B = args.width, args.height, args.batch
+    W, H = args.width, args.height
+    B = args.batch or (1024 if args.lossless else 256)
     fs = 4 * W * H
     rgba = torch.empty(B * fs, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -144,7 +201,8 @@ def main():
     libwebp_amd.synth_device(rgba.data_ptr(), W, H, first, B, seed=1, stream=stream)
     torch.cuda.synchronize(dev)
     enc = libwebp_amd.GpuBatch(W, H, B, quality=args.quality, method=args.method, device=local,
-                               threads=args.threads, use_sharp_yuv=int(args.sharp_yuv))
+                               threads=args.threads, use_sharp_yuv=int(args.sharp_yuv),
+                               lossless=int(args.lossless))
 
     def step():
         enc.encode_device(rgba.data_ptr(), B, stream=stream)
@@ -187,6 +245,14 @@ def main():
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
+        return
+    if args.lossless:
+        print(json.dumps(lossless_line(args, world, B, W, H, elapsed, tails, total_bytes)),
+              flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        enc.close()
         return
     mp = world * B * W * H * args.steps / 1e6
     value = mp / elapsed

@@ -9,7 +9,8 @@
 //                        check), residual ARGB to HBM
 //   L2 k_vp8l_cache      one wave per frame, 64 pixels per step: colour-cache
 //                        hit bits (same-key lanes found with CACHE_BITS ballots)
-//   L3 k_vp8l_parse      one thread per row: greedy copy / cache / literal
+//   L3 k_vp8l_match      one wave per row: best candidate run per pixel (ballots)
+//      k_vp8l_parse      one thread per row: greedy copy / cache / literal
 //   L4 k_vp8l_tilefeat   one workgroup per histogram tile: own entropy/pixel
 //   L5 k_vp8l_cluster    one workgroup per frame: k-means of histogram tiles
 //                        into <= KMAX code groups (histograms + costs in LDS)
@@ -116,19 +117,35 @@ __device__ __forceinline__ V wave_sum(V v) {
 
 // ------------------------------------------------------------------ L1
 
-#define TMAX 64   // max transform tile side (tb <= 6)
+// Histograms of up to 4096 pixels: two 16-bit counters per 32-bit LDS word
+// halve the footprint (more workgroups per CU); same fast path as hadd.
+__device__ __forceinline__ void hadd16(uint32_t* h, uint32_t bin) {
+  const uint64_t act = __ballot(1);
+  const uint32_t first = __builtin_amdgcn_readfirstlane(bin);
+  const uint64_t same = __ballot(bin == first);
+  if (same == act) {
+    if (lane_id() == __ffsll((long long)act) - 1)
+      atomicAdd(&h[first >> 1], (uint32_t)__popcll(act) << ((first & 1) * 16));
+  } else {
+    atomicAdd(&h[bin >> 1], 1u << ((bin & 1) * 16));
+  }
+}
+__device__ __forceinline__ uint32_t hget16(const uint32_t* h, int bin) {
+  return (h[bin >> 1] >> ((bin & 1) * 16)) & 0xffffu;
+}
 
+template <int T>
 struct TransformSmem {
-  uint32_t src[(TMAX + 1) * (TMAX + 2)];   // rows y0-1.., cols x0-1..x0+tw
-  uint32_t first[TMAX];                    // P(0, y) for the right-edge TR wrap
-  uint32_t res[TMAX * TMAX];
-  uint32_t hist[14 * 4 * 256];
+  uint32_t src[(T + 1) * (T + 2)];   // rows y0-1.., cols x0-1..x0+tw
+  uint32_t first[T];                 // P(0, y) for the right-edge TR wrap
+  uint32_t res[T * T];
+  uint32_t hist[14 * 4 * 128];       // [mode][channel][256 bins], 16-bit counters
   uint32_t score[16];
   long long sums[4];
   int best;
-  int mult[3];
 };
 
+template <int T>
 __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restrict__ rgba,
                                                         size_t fstride, int rstride, vp8l_params p,
                                                         const int32_t* __restrict__ nlogn,
@@ -136,18 +153,21 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
                                                         uint8_t* __restrict__ modes,
                                                         uint32_t* __restrict__ mult,
                                                         uint32_t* __restrict__ alpha_flag) {
-  __shared__ TransformSmem S;
+  __shared__ TransformSmem<T> S;
+  __shared__ int all_opaque;
   const int tid = threadIdx.x, f = blockIdx.z;
-  const int W = p.w, H = p.h, tb = p.tb;
-  const int x0 = blockIdx.x << tb, y0 = blockIdx.y << tb;
-  const int tw = min(1 << tb, W - x0), th = min(1 << tb, H - y0);
+  const int W = p.w, H = p.h;
+  const int x0 = blockIdx.x * T, y0 = blockIdx.y * T;
+  const int tw = min(T, W - x0), th = min(T, H - y0);
   const int sw = tw + 2;   // LDS source row width (cols x0-1 .. x0+tw)
   const uint8_t* img = rgba + (size_t)f * fstride;
-  const int tiles_x = (W + (1 << tb) - 1) >> tb;
+  const int tiles_x = (W + T - 1) / T;
   const int tile = blockIdx.y * tiles_x + blockIdx.x;
+  if (tid == 0) all_opaque = 1;
+  __syncthreads();
 
   // load sub-green pixels (A, R-G, G, B-G) with a 1-pixel border
-  bool opaque = true;
+  bool opaque = true, tile_alpha = false;
   for (int i = tid; i < (th + 1) * sw; i += 256) {
     const int ly = i / sw, lx = i - ly * sw;
     const int y = y0 - 1 + ly, x = x0 - 1 + lx;
@@ -156,7 +176,10 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
       const uint8_t* q = img + (size_t)y * rstride + 4 * x;
       const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
       v = (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255);
-      if (ly > 0 && lx > 0 && lx <= tw && a != 255) opaque = false;
+      if (a != 255) {
+        opaque = false;
+        if (ly > 0 && lx > 0 && lx <= tw) tile_alpha = true;
+      }
     }
     S.src[i] = v;
   }
@@ -165,12 +188,17 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
       const uint8_t* q = img + (size_t)(y0 + i) * rstride;
       const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
       S.first[i] = (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255);
+      if (a != 255) opaque = false;
     }
   }
-  if (__any(!opaque) && lane_id() == 0) atomicOr(&alpha_flag[f], 1u);
-  for (int i = tid; i < 14 * 4 * 256; i += 256) S.hist[i] = 0;
+  if (__any(tile_alpha) && lane_id() == 0) atomicOr(&alpha_flag[f], 1u);
+  if (__any(!opaque) && lane_id() == 0) all_opaque = 0;
+  for (int i = tid; i < 14 * 4 * 128; i += 256) S.hist[i] = 0;
   if (tid < 16) S.score[tid] = 0;
   __syncthreads();
+  // every real pixel the predictors read is opaque: the alpha residual is 0
+  // for all 14 modes, its histogram adds the same score to each -> skip it
+  const int c0 = all_opaque ? 1 : 0;
 
   auto at = [&](int lx, int ly) -> uint32_t { return S.src[(ly + 1) * sw + lx + 1]; };
   auto tr = [&](int lx, int ly) -> uint32_t {   // (y-1)*W + x + 1, linear
@@ -183,16 +211,16 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
   for (int i = tid; i < np; i += 256) {
     const int ly = i / tw, lx = i - ly * tw;
     const int x = x0 + lx, y = y0 + ly;
-    const uint32_t P = at(lx, ly), L = at(lx - 1, ly), T = at(lx, ly - 1), TL = at(lx - 1, ly - 1);
+    const uint32_t P = at(lx, ly), L = at(lx - 1, ly), T_ = at(lx, ly - 1), TL = at(lx - 1, ly - 1);
     const uint32_t TR = tr(lx, ly);
     const int fm = fixed_mode(x, y);
     for (int m = 0; m < 14; ++m) {
-      const uint32_t r = sub_pixels(P, predict(fm >= 0 ? fm : m, L, T, TL, TR));
-      uint32_t* h = S.hist + m * 1024;
-      hadd(h, r >> 24);
-      hadd(h + 256, (r >> 16) & 255);
-      hadd(h + 512, (r >> 8) & 255);
-      hadd(h + 768, r & 255);
+      const uint32_t r = sub_pixels(P, predict(fm >= 0 ? fm : m, L, T_, TL, TR));
+      uint32_t* h = S.hist + m * 512;
+      if (!c0) hadd16(h, r >> 24);
+      hadd16(h + 128, (r >> 16) & 255);
+      hadd16(h + 256, (r >> 8) & 255);
+      hadd16(h + 384, r & 255);
     }
   }
   __syncthreads();
@@ -201,7 +229,8 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     uint32_t sc[14];
     for (int m = 0; m < 14; ++m) {
       uint32_t s = 0;
-      for (int k = tid; k < 1024; k += 256) s += (uint32_t)nlogn[S.hist[m * 1024 + k]];
+      for (int k = tid + c0 * 256; k < 1024; k += 256)
+        s += (uint32_t)nlogn[hget16(S.hist + m * 512, k)];
       sc[m] = wave_sum(s);
     }
     if (lane_id() == 0)
@@ -244,7 +273,7 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     else { sxy = S.sums[3]; sxx = S.sums[2]; }   // round 2: sums reloaded below
     const int ls = ls_multiplier(sxy, sxx);
     cand[0] = 0; cand[1] = clamp8(ls - 1); cand[2] = clamp8(ls); cand[3] = clamp8(ls + 1);
-    for (int i = tid; i < 4 * 256; i += 256) S.hist[i] = 0;
+    for (int i = tid; i < 4 * 128; i += 256) S.hist[i] = 0;
     if (tid < 4) S.score[tid] = 0;
     __syncthreads();
     for (int i = tid; i < np; i += 256) {
@@ -255,15 +284,14 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
         if (round == 0) v = (rr - ctd(cand[c], g)) & 255;
         else if (round == 1) v = (bb - ctd(cand[c], g)) & 255;
         else v = ((bb - ctd(g2b, g)) - ctd(cand[c], rr)) & 255;
-        hadd(S.hist + c * 256, (uint32_t)v);
+        hadd16(S.hist + c * 128, (uint32_t)v);
       }
     }
     __syncthreads();
     {
-      uint32_t s = (uint32_t)nlogn[S.hist[tid]];   // 1024 bins, 256 threads x 4
       uint32_t sc[4];
-      for (int c = 0; c < 4; ++c) sc[c] = wave_sum((uint32_t)nlogn[S.hist[c * 256 + tid]]);
-      (void)s;
+      for (int c = 0; c < 4; ++c)
+        sc[c] = wave_sum((uint32_t)nlogn[hget16(S.hist + c * 128, tid)]);
       if (lane_id() == 0)
         for (int c = 0; c < 4; ++c) atomicAdd(&S.score[c], sc[c]);
     }
@@ -307,7 +335,7 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     out[(size_t)(y0 + ly) * W + x0 + lx] = (r & 0xff00ff00u) | ((uint32_t)nr << 16) | (uint32_t)nb;
   }
   if (tid == 0) {
-    const int ntt = tiles_x * ((H + (1 << tb) - 1) >> tb);
+    const int ntt = tiles_x * ((H + T - 1) / T);
     modes[(size_t)f * ntt + tile] = (uint8_t)best;
     mult[(size_t)f * ntt + tile] =
         (uint32_t)(g2r & 255) | ((uint32_t)(g2b & 255) << 8) | ((uint32_t)(r2b & 255) << 16);
@@ -374,40 +402,66 @@ __global__ __launch_bounds__(64) void k_vp8l_cache(const uint32_t* __restrict__ 
 
 // ------------------------------------------------------------------ L3
 
-__global__ __launch_bounds__(64) void k_vp8l_parse(const uint32_t* __restrict__ argb,
+// One wave per row, chunks of 64 pixels right to left: for each candidate
+// distance the run of equal pixels starting at every x (ballot of the 64
+// comparisons; count trailing ones; a run reaching the chunk end continues
+// with the run at the next chunk's start), the longest (first on ties,
+// capped at MAX_LENGTH) and the cache-hit bit, packed per pixel as
+// len | cand << 13 | hit << 15 for the parse.
+__global__ __launch_bounds__(64) void k_vp8l_match(const uint32_t* __restrict__ argb,
                                                    const uint64_t* __restrict__ hits, vp8l_params p,
-                                                   uint32_t* __restrict__ ops) {
+                                                   uint32_t* __restrict__ bm) {
+  const int f = blockIdx.y, y = blockIdx.x, ln = lane_id();
+  const int W = p.w;
+  const size_t npix = (size_t)W * p.h;
+  const uint32_t* E = argb + f * npix;
+  const uint64_t* hb = hits + (size_t)f * ((npix + 63) >> 6);
+  uint32_t* O = bm + f * npix;
+  const size_t row = (size_t)y * W;
+  int carry[VP8L_NUM_CAND] = {0, 0, 0, 0};
+  for (int c = (W - 1) >> 6; c >= 0; --c) {
+    const int x = (c << 6) + ln;
+    const bool valid = x < W;
+    const size_t q = row + (size_t)x;
+    const uint32_t e = valid ? E[q] : 0u;
+    int bn = 0, bk = 0;
+#pragma unroll
+    for (int k = 0; k < VP8L_NUM_CAND; ++k) {
+      const int d = p.dist[k];
+      const bool ok = valid && d > 0 && (size_t)d <= q && E[q - d] == e;
+      const uint64_t mask = __ballot(ok);
+      int run = (int)__builtin_ctzll(~(mask >> ln));
+      if (run == 64 - ln) run += carry[k];
+      carry[k] = __shfl(run, 0);
+      const int n = min(run, VP8L_MAX_LENGTH);
+      if (n > bn) { bn = n; bk = k; }
+    }
+    if (valid) {
+      const uint32_t hit = (uint32_t)((hb[q >> 6] >> (q & 63)) & 1);
+      O[q] = (uint32_t)bn | ((uint32_t)bk << 13) | (hit << 15);
+    }
+  }
+}
+
+// One thread per row: greedy copy / cache / literal over the packed match
+// words (model: parse), rewriting them in place as parse ops.
+__global__ __launch_bounds__(64) void k_vp8l_parse(vp8l_params p, uint32_t* __restrict__ ops) {
   const int f = blockIdx.y, y = blockIdx.x * 64 + threadIdx.x;
   const int W = p.w, H = p.h;
   if (y >= H) return;
   const size_t npix = (size_t)W * H;
-  const uint32_t* E = argb + f * npix;
-  const uint64_t* hb = hits + (size_t)f * ((npix + 63) >> 6);
-  uint32_t* O = ops + f * npix;
-  const size_t row = (size_t)y * W;
+  uint32_t* O = ops + f * npix + (size_t)y * W;
   int x = 0;
   while (x < W) {
-    const size_t q = row + x;
-    const uint32_t e = E[q];
-    int bn = 0, bk = 0;
-    for (int k = 0; k < VP8L_NUM_CAND; ++k) {
-      const int d = p.dist[k];
-      if (d <= 0 || (size_t)d > q) continue;
-      int n = 0;
-      const int lim = min(W - x, VP8L_MAX_LENGTH);
-      if (E[q - d] == e) {
-        n = 1;
-        while (n < lim && E[q + n] == E[q + n - d]) ++n;
-      }
-      if (n > bn) { bn = n; bk = k; }
-    }
-    const bool hit = (hb[q >> 6] >> (q & 63)) & 1;
+    const uint32_t m = O[x];
+    const int bn = (int)(m & 0x1fff), bk = (int)((m >> 13) & 3);
+    const bool hit = (m >> 15) & 1;
     if (bn >= VP8L_MIN_COPY || (bn == 2 && !hit)) {
-      O[q] = 2u | ((uint32_t)bn << 2) | ((uint32_t)p.dcode[bk] << 15);
-      for (int i = 1; i < bn; ++i) O[q + i] = 3u;
+      O[x] = 2u | ((uint32_t)bn << 2) | ((uint32_t)p.dcode[bk] << 15);
+      for (int i = 1; i < bn; ++i) O[x + i] = 3u;
       x += bn;
     } else {
-      O[q] = hit ? 1u : 0u;
+      O[x] = hit ? 1u : 0u;
       ++x;
     }
   }
@@ -474,21 +528,29 @@ __device__ __forceinline__ long long flog2_fx64(const int32_t* frac, unsigned lo
 
 // ------------------------------------------------------------------ L4
 
+// One workgroup per histogram tile: the tile's symbol histogram in LDS, its
+// own entropy per pixel (the clustering's initial order), and the histogram
+// as a sparse list (symbol | count << 12) for the clustering passes.
 __global__ __launch_bounds__(256) void k_vp8l_tilefeat(const uint32_t* __restrict__ argb,
                                                        const uint32_t* __restrict__ ops,
                                                        vp8l_params p,
                                                        const int32_t* __restrict__ frac,
-                                                       int64_t* __restrict__ feat) {
+                                                       int64_t* __restrict__ feat,
+                                                       uint32_t* __restrict__ tl,
+                                                       uint32_t* __restrict__ tn) {
   __shared__ uint32_t h[VP8L_NS];
   __shared__ unsigned long long acc[6];
+  __shared__ uint32_t nnz;
   const int tid = threadIdx.x, f = blockIdx.y, t = blockIdx.x;
   const int W = p.w, H = p.h, hb = p.hb;
   const int tx_n = (W + (1 << hb) - 1) >> hb;
+  const int tiles = tx_n * ((H + (1 << hb) - 1) >> hb);
   const int x0 = (t % tx_n) << hb, y0 = (t / tx_n) << hb;
   const int tw = min(1 << hb, W - x0), th = min(1 << hb, H - y0);
   const size_t npix = (size_t)W * H;
   for (int i = tid; i < VP8L_NS; i += 256) h[i] = 0;
   if (tid < 6) acc[tid] = 0;
+  if (tid == 0) nnz = 0;
   __syncthreads();
   for (int i = tid; i < tw * th; i += 256) {
     const int ly = i / tw, lx = i - ly * tw;
@@ -496,16 +558,19 @@ __global__ __launch_bounds__(256) void k_vp8l_tilefeat(const uint32_t* __restric
     PixSym s;
     pix_symbols(ops[q], argb[q], s);
     for (int k = 0; k < 4; ++k)
-      if (s.s[k] >= 0) atomicAdd(&h[s.s[k]], 1u);
+      if (s.s[k] >= 0) hadd(h, (uint32_t)s.s[k]);
   }
   __syncthreads();
   // per alphabet: N, then own = sum_a N_a log N_a - sum h log h
   unsigned long long n[5] = {0, 0, 0, 0, 0};
   unsigned long long hl = 0;
+  const size_t cap = VP8L_TILE_CAP(hb);
+  uint32_t* out = tl + ((size_t)f * tiles + t) * cap;
   for (int i = tid; i < VP8L_NS; i += 256) {
     const uint32_t c = h[i];
     n[alph_of(i)] += c;
     if (c > 1) hl += (unsigned long long)c * (unsigned long long)flog2_fx(frac, c);
+    if (c) out[atomicAdd(&nnz, 1u)] = (uint32_t)i | (c << 12);
   }
   for (int a = 0; a < 5; ++a) n[a] = wave_sum(n[a]);
   hl = wave_sum(hl);
@@ -519,8 +584,8 @@ __global__ __launch_bounds__(256) void k_vp8l_tilefeat(const uint32_t* __restric
     for (int a = 0; a < 5; ++a)
       if (acc[a] > 1) own += (long long)acc[a] * flog2_fx64(frac, acc[a]);
     own -= (long long)acc[5];
-    const int tiles = tx_n * ((H + (1 << hb) - 1) >> hb);
     feat[(size_t)f * tiles + t] = own / (long long)(tw * th);
+    tn[(size_t)f * tiles + t] = nnz;
   }
 }
 
@@ -536,11 +601,14 @@ struct ClusterSmem {
   uint32_t nsum[VP8L_KMAX * 5];
 };
 
-__global__ __launch_bounds__(1024) void k_vp8l_cluster(const uint32_t* __restrict__ argb,
-                                                       const uint32_t* __restrict__ ops,
-                                                       vp8l_params p,
+// One workgroup per frame (16 waves): k-means of the histogram tiles over
+// their sparse histograms (model: cluster_tiles). A wave owns a tile at a
+// time in both the accumulation and the reassignment passes.
+__global__ __launch_bounds__(1024) void k_vp8l_cluster(vp8l_params p,
                                                        const int32_t* __restrict__ frac,
                                                        const int64_t* __restrict__ feat,
+                                                       const uint32_t* __restrict__ tl,
+                                                       const uint32_t* __restrict__ tn,
                                                        uint32_t* __restrict__ hc_out,
                                                        uint8_t* __restrict__ assign_out) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
@@ -549,9 +617,9 @@ __global__ __launch_bounds__(1024) void k_vp8l_cluster(const uint32_t* __restric
   const int W = p.w, H = p.h, hb = p.hb, K = p.k;
   const int tx_n = (W + (1 << hb) - 1) >> hb, ty_n = (H + (1 << hb) - 1) >> hb;
   const int nt = tx_n * ty_n;
-  const size_t npix = (size_t)W * H;
-  const uint32_t* E = argb + f * npix;
-  const uint32_t* O = ops + f * npix;
+  const size_t cap = VP8L_TILE_CAP(hb);
+  const uint32_t* TL = tl + (size_t)f * nt * cap;
+  const uint32_t* TN = tn + (size_t)f * nt;
 
   // init: rank by (feature, tile), K quantiles
   for (int t = tid; t < nt; t += 1024) S.u.feat[t] = feat[(size_t)f * nt + t];
@@ -571,16 +639,14 @@ __global__ __launch_bounds__(1024) void k_vp8l_cluster(const uint32_t* __restric
     // accumulate cluster histograms
     for (int i = tid; i < K * VP8L_NS; i += 1024) S.hc[i] = 0;
     __syncthreads();
-    int y = tid / W, x = tid - (tid / W) * W;
-    for (uint32_t q = tid; q < (uint32_t)npix; q += 1024) {
-      const int c = S.assign[(y >> hb) * tx_n + (x >> hb)];
-      PixSym s;
-      pix_symbols(O[q], E[q], s);
-      uint32_t* hcc = S.hc + c * VP8L_NS;
-      for (int k = 0; k < 4; ++k)
-        if (s.s[k] >= 0) atomicAdd(&hcc[s.s[k]], 1u);
-      x += 1024;
-      while (x >= W) { x -= W; ++y; }
+    for (int t = wv; t < nt; t += 16) {
+      uint32_t* hcc = S.hc + S.assign[t] * VP8L_NS;
+      const uint32_t* e = TL + (size_t)t * cap;
+      const int m = (int)TN[t];
+      for (int i = ln; i < m; i += 64) {
+        const uint32_t v = e[i];
+        atomicAdd(&hcc[v & 4095], v >> 12);
+      }
     }
     __syncthreads();
     if (it == VP8L_CLUSTER_ITERS) break;
@@ -606,22 +672,18 @@ __global__ __launch_bounds__(1024) void k_vp8l_cluster(const uint32_t* __restric
     __syncthreads();
     // reassign: one wave per tile
     for (int t = wv; t < nt; t += 16) {
-      const int tx0 = (t % tx_n) << hb, ty0 = (t / tx_n) << hb;
-      const int tw = min(1 << hb, W - tx0), th = min(1 << hb, H - ty0);
+      const uint32_t* e = TL + (size_t)t * cap;
+      const int m = (int)TN[t];
       unsigned long long cost[VP8L_KMAX];
 #pragma unroll
       for (int c = 0; c < VP8L_KMAX; ++c) cost[c] = 0;
-      for (int i = ln; i < tw * th; i += 64) {
-        const int ly = i / tw, lx = i - ly * tw;
-        const size_t q = (size_t)(ty0 + ly) * W + tx0 + lx;
-        PixSym s;
-        pix_symbols(O[q], E[q], s);
-        for (int k = 0; k < 4; ++k) {
-          if (s.s[k] < 0) continue;
+      for (int i = ln; i < m; i += 64) {
+        const uint32_t v = e[i];
+        const int sym = (int)(v & 4095);
+        const uint32_t cnt = v >> 12;
 #pragma unroll
-          for (int c = 0; c < VP8L_KMAX; ++c)
-            if (c < K) cost[c] += S.u.lc[c * VP8L_NS + s.s[k]];
-        }
+        for (int c = 0; c < VP8L_KMAX; ++c)
+          if (c < K) cost[c] += (unsigned long long)cnt * S.u.lc[c * VP8L_NS + sym];
       }
       int bc = 0;
       unsigned long long bv = ~0ull;
@@ -777,12 +839,45 @@ __global__ __launch_bounds__(256) void k_vp8l_write(const uint32_t* __restrict__
   uint32_t* O = reinterpret_cast<uint32_t*>(out + (size_t)f * out_cap);
   for (int i = tid; i < nw; i += 256) {
     const uint32_t v = words[i];
+    if ((w0 + i + 1) * 4 > out_cap) break;   // overflow: the host reports it from end_bit
     if (i == 0 || i == nw - 1) {
       if (v) atomicOr(&O[w0 + i], v);
     } else {
       O[w0 + i] = v;
     }
   }
+}
+
+// ------------------------------------------------------------------ staging
+
+// headers packed back to back (4-byte aligned offsets hoff[f], word counts
+// hwords[f]) -> the start of each frame's output slab
+__global__ __launch_bounds__(256) void k_vp8l_put_headers(const uint32_t* __restrict__ hdr,
+                                                          const uint64_t* __restrict__ hoff,
+                                                          const uint32_t* __restrict__ hwords,
+                                                          uint8_t* __restrict__ out,
+                                                          size_t out_cap) {
+  const int f = blockIdx.y;
+  const uint32_t n = hwords[f];
+  const uint32_t* src = hdr + (hoff[f] >> 2);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(out + (size_t)f * out_cap);
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) dst[i] = src[i];
+}
+
+// payloads (bytes[f]) -> one packed buffer at poff[f] + 20, 16-byte aligned
+// frame starts, for a single device-to-host copy
+__global__ __launch_bounds__(256) void k_vp8l_pack(const uint8_t* __restrict__ out, size_t out_cap,
+                                                   const uint64_t* __restrict__ poff,
+                                                   const uint64_t* __restrict__ end_bit,
+                                                   uint8_t* __restrict__ packed) {
+  const int f = blockIdx.y;
+  if (poff[f + 1] == poff[f]) return;   // frame failed on the host: nothing to copy
+  const size_t bytes = (size_t)((end_bit[f] + 7) >> 3);
+  const size_t words = (bytes + 3) >> 2;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(out + (size_t)f * out_cap);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(packed + poff[f] + 20);   // poff 16-aligned
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < words; i += (size_t)gridDim.x * 256)
+    dst[i] = src[i];
 }
 
 // ------------------------------------------------------------------ launchers
@@ -795,23 +890,34 @@ extern "C" int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rs
                                      void* stream) {
   if (p->tb < 2 || p->tb > 6 || p->w <= 0 || p->h <= 0 || p->n <= 0) return 0;
   dim3 grid((p->w + (1 << p->tb) - 1) >> p->tb, (p->h + (1 << p->tb) - 1) >> p->tb, p->n);
-  hipLaunchKernelGGL(k_vp8l_transform, grid, dim3(256), 0, (hipStream_t)stream, rgba, fstride,
-                     rstride, *p, nlogn, argb, modes, mult, alpha_flag);
+  hipStream_t st = (hipStream_t)stream;
+#define L1(T)                                                                              \
+  hipLaunchKernelGGL(k_vp8l_transform<T>, grid, dim3(256), 0, st, rgba, fstride, rstride, *p, \
+                     nlogn, argb, modes, mult, alpha_flag)
+  switch (p->tb) {
+    case 2: L1(4); break;
+    case 3: L1(8); break;
+    case 4: L1(16); break;
+    case 5: L1(32); break;
+    default: L1(64); break;
+  }
+#undef L1
   return check_launch();
 }
 
 extern "C" int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
                                    const int32_t* flog2, uint64_t* hits, uint32_t* ops,
-                                   int64_t* feat, uint32_t* hc, uint8_t* assign, void* stream) {
+                                   int64_t* feat, uint32_t* tl, uint32_t* tn, uint32_t* hc,
+                                   uint8_t* assign, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int npix = p->w * p->h;
   const int tx_n = (p->w + (1 << p->hb) - 1) >> p->hb, ty_n = (p->h + (1 << p->hb) - 1) >> p->hb;
   if (tx_n * ty_n > VP8L_MAX_HUFF_IMAGE || p->k < 1 || p->k > VP8L_KMAX) return 0;
   hipLaunchKernelGGL(k_vp8l_cache, dim3(p->n), dim3(64), 0, st, argb, npix, hits);
-  hipLaunchKernelGGL(k_vp8l_parse, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, argb, hits, *p,
-                     ops);
+  hipLaunchKernelGGL(k_vp8l_match, dim3(p->h, p->n), dim3(64), 0, st, argb, hits, *p, ops);
+  hipLaunchKernelGGL(k_vp8l_parse, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, *p, ops);
   hipLaunchKernelGGL(k_vp8l_tilefeat, dim3(tx_n * ty_n, p->n), dim3(256), 0, st, argb, ops, *p,
-                     flog2, feat);
+                     flog2, feat, tl, tn);
   static int attr = 0;
   if (!attr) {
     if (hipFuncSetAttribute((const void*)k_vp8l_cluster,
@@ -820,8 +926,8 @@ extern "C" int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
       return 0;
     attr = 1;
   }
-  hipLaunchKernelGGL(k_vp8l_cluster, dim3(p->n), dim3(1024), sizeof(ClusterSmem), st, argb, ops,
-                     *p, flog2, feat, hc, assign);
+  hipLaunchKernelGGL(k_vp8l_cluster, dim3(p->n), dim3(1024), sizeof(ClusterSmem), st, *p, flog2,
+                     feat, tl, tn, hc, assign);
   return check_launch();
 }
 
@@ -839,5 +945,20 @@ extern "C" int vp8l_launch_write(const uint32_t* argb, const uint32_t* ops, cons
                      end_bit);
   hipLaunchKernelGGL(k_vp8l_write, dim3(nblk, p->n), dim3(256), 0, st, argb, ops, *p, ctab, gtile,
                      bsum, boff, out, out_cap);
+  return check_launch();
+}
+
+extern "C" int vp8l_launch_put_headers(const uint32_t* hdr, const uint64_t* hoff,
+                                       const uint32_t* hwords, int n, uint8_t* out,
+                                       size_t out_cap, void* stream) {
+  hipLaunchKernelGGL(k_vp8l_put_headers, dim3(8, n), dim3(256), 0, (hipStream_t)stream, hdr, hoff,
+                     hwords, out, out_cap);
+  return check_launch();
+}
+
+extern "C" int vp8l_launch_pack(const uint8_t* out, size_t out_cap, const uint64_t* poff,
+                                const uint64_t* end_bit, int n, uint8_t* packed, void* stream) {
+  hipLaunchKernelGGL(k_vp8l_pack, dim3(64, n), dim3(256), 0, (hipStream_t)stream, out, out_cap,
+                     poff, end_bit, packed);
   return check_launch();
 }

@@ -37,12 +37,15 @@ static int sub_sample(int size, int bits) { return (size + (1 << bits) - 1) >> b
 void vp8l_engine_free(vp8l_engine* l) {
   if (!l) return;
   hipFree(l->d_tabs); hipFree(l->d_argb); hipFree(l->d_modes); hipFree(l->d_mult);
-  hipFree(l->d_aflag); hipFree(l->d_hits); hipFree(l->d_ops); hipFree(l->d_feat);
+  hipFree(l->d_aflag); hipFree(l->d_hits); hipFree(l->d_ops); hipFree(l->d_feat); hipFree(l->d_tl); hipFree(l->d_tn);
   hipFree(l->d_hc); hipFree(l->d_assign); hipFree(l->d_ctab); hipFree(l->d_gtile);
   hipFree(l->d_start); hipFree(l->d_bsum); hipFree(l->d_boff); hipFree(l->d_end); hipFree(l->d_out);
+  hipFree(l->d_packed); hipFree(l->d_poff); hipFree(l->d_hpack); hipFree(l->d_hoff);
+  hipFree(l->d_hwords);
   hipHostFree(l->h_modes); hipHostFree(l->h_mult); hipHostFree(l->h_aflag); hipHostFree(l->h_hc);
   hipHostFree(l->h_assign); hipHostFree(l->h_ctab); hipHostFree(l->h_gtile);
   hipHostFree(l->h_start); hipHostFree(l->h_end); hipHostFree(l->h_hdr); hipHostFree(l->h_out);
+  hipHostFree(l->h_poff); hipHostFree(l->h_hpack); hipHostFree(l->h_hoff); hipHostFree(l->h_hwords);
   free(l->hdr_bytes); free(l->out_off); free(l->out_size); free(l->err);
   free(l);
 }
@@ -70,6 +73,8 @@ vp8l_engine* vp8l_engine_new(int w, int h, int max_frames, int method) {
   CHK(hipMalloc((void**)&l->d_mult, N * l->ntt * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&l->d_aflag, N * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&l->d_feat, N * l->nht * sizeof(int64_t)));
+  CHK(hipMalloc((void**)&l->d_tl, N * l->nht * VP8L_TILE_CAP(l->p.hb) * sizeof(uint32_t)));
+  CHK(hipMalloc((void**)&l->d_tn, N * l->nht * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&l->d_hc, N * VP8L_KMAX * VP8L_NS * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&l->d_assign, N * l->nht));
   CHK(hipMalloc((void**)&l->d_ctab, N * VP8L_KMAX * VP8L_NS * sizeof(uint32_t)));
@@ -89,6 +94,12 @@ vp8l_engine* vp8l_engine_new(int w, int h, int max_frames, int method) {
   CHK(hipHostMalloc((void**)&l->h_start, N * sizeof(uint64_t), 0));
   CHK(hipHostMalloc((void**)&l->h_end, N * sizeof(uint64_t), 0));
   CHK(hipHostMalloc((void**)&l->h_hdr, N * l->hdr_cap, 0));
+  CHK(hipMalloc((void**)&l->d_poff, (N + 1) * sizeof(uint64_t)));
+  CHK(hipMalloc((void**)&l->d_hoff, (N + 1) * sizeof(uint64_t)));
+  CHK(hipMalloc((void**)&l->d_hwords, N * sizeof(uint32_t)));
+  CHK(hipHostMalloc((void**)&l->h_poff, (N + 1) * sizeof(uint64_t), 0));
+  CHK(hipHostMalloc((void**)&l->h_hoff, (N + 1) * sizeof(uint64_t), 0));
+  CHK(hipHostMalloc((void**)&l->h_hwords, N * sizeof(uint32_t), 0));
   l->hdr_bytes = (size_t*)calloc(N, sizeof(size_t));
   l->out_off = (size_t*)calloc(N + 1, sizeof(size_t));
   l->out_size = (size_t*)calloc(N, sizeof(size_t));
@@ -174,7 +185,7 @@ int vp8l_engine_run(struct WebPGpuBatch* b, const uint8_t* rgba, size_t fstride,
     goto fail;
   CHK(hipEventRecord(b->ev[1], st));
   if (!vp8l_launch_analyze(l->d_argb, &p, l->d_tabs + 4097, l->d_hits, l->d_ops, l->d_feat,
-                           l->d_hc, l->d_assign, st))
+                           l->d_tl, l->d_tn, l->d_hc, l->d_assign, st))
     goto fail;
   CHK(hipEventRecord(b->ev[2], st));
   CHK(hipMemcpyAsync(l->h_modes, l->d_modes, N * l->ntt, hipMemcpyDeviceToHost, st));
@@ -190,10 +201,30 @@ int vp8l_engine_run(struct WebPGpuBatch* b, const uint8_t* rgba, size_t fstride,
   t1 = now_us();
   run_headers(l, n, b->threads);
   t2 = now_us();
+  /* headers back to back (4-byte aligned), one upload, scattered on device */
+  l->h_hoff[0] = 0;
+  for (int f = 0; f < n; ++f) {
+    l->h_hwords[f] = (uint32_t)((l->hdr_bytes[f] + 3) >> 2);
+    l->h_hoff[f + 1] = l->h_hoff[f] + 4 * (uint64_t)l->h_hwords[f];
+  }
+  if (l->h_hoff[n] > l->h_hpack_cap) {
+    hipHostFree(l->h_hpack); hipFree(l->d_hpack);
+    l->h_hpack = NULL; l->d_hpack = NULL;
+    l->h_hpack_cap = l->d_hpack_cap = 0;
+    const size_t cap = l->h_hoff[n] + l->h_hoff[n] / 4 + 4096;
+    CHK(hipHostMalloc((void**)&l->h_hpack, cap, 0));
+    l->h_hpack_cap = cap;
+    CHK(hipMalloc((void**)&l->d_hpack, cap));
+    l->d_hpack_cap = cap;
+  }
   for (int f = 0; f < n; ++f)
-    if (l->hdr_bytes[f])
-      CHK(hipMemcpyAsync(l->d_out + (size_t)f * l->out_cap, l->h_hdr + (size_t)f * l->hdr_cap,
-                         (l->hdr_bytes[f] + 3) & ~(size_t)3, hipMemcpyHostToDevice, st));
+    memcpy(l->h_hpack + l->h_hoff[f], l->h_hdr + (size_t)f * l->hdr_cap, 4 * (size_t)l->h_hwords[f]);
+  if (l->h_hoff[n])
+    CHK(hipMemcpyAsync(l->d_hpack, l->h_hpack, l->h_hoff[n], hipMemcpyHostToDevice, st));
+  CHK(hipMemcpyAsync(l->d_hoff, l->h_hoff, N * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  CHK(hipMemcpyAsync(l->d_hwords, l->h_hwords, N * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  if (!vp8l_launch_put_headers(l->d_hpack, l->d_hoff, l->d_hwords, n, l->d_out, l->out_cap, st))
+    goto fail;
   CHK(hipMemcpyAsync(l->d_ctab, l->h_ctab, N * VP8L_KMAX * VP8L_NS * sizeof(uint32_t),
                      hipMemcpyHostToDevice, st));
   CHK(hipMemcpyAsync(l->d_gtile, l->h_gtile, N * l->nht, hipMemcpyHostToDevice, st));
@@ -218,18 +249,22 @@ int vp8l_engine_run(struct WebPGpuBatch* b, const uint8_t* rgba, size_t fstride,
     l->out_size[f] = sz;
     l->out_off[f + 1] = l->out_off[f] + ((sz + 15) & ~(size_t)15);
   }
-  if (l->out_off[n] > l->h_out_cap) {
-    hipHostFree(l->h_out);
-    l->h_out = NULL;
-    l->h_out_cap = 0;
+  if (l->out_off[n] + 16 > l->h_out_cap) {
+    hipHostFree(l->h_out); hipFree(l->d_packed);
+    l->h_out = NULL; l->d_packed = NULL;
+    l->h_out_cap = l->d_packed_cap = 0;
     const size_t cap = l->out_off[n] + l->out_off[n] / 4 + 4096;
     CHK(hipHostMalloc((void**)&l->h_out, cap, 0));
     l->h_out_cap = cap;
+    CHK(hipMalloc((void**)&l->d_packed, cap));
+    l->d_packed_cap = cap;
   }
-  for (int f = 0; f < n; ++f)
-    if (l->out_size[f])
-      CHK(hipMemcpyAsync(l->h_out + l->out_off[f] + 20, l->d_out + (size_t)f * l->out_cap,
-                         l->out_size[f] - 20, hipMemcpyDeviceToHost, st));
+  /* one gather kernel + one device-to-host copy of every frame */
+  for (int f = 0; f <= n; ++f) l->h_poff[f] = l->out_off[f];
+  CHK(hipMemcpyAsync(l->d_poff, l->h_poff, (N + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  if (!vp8l_launch_pack(l->d_out, l->out_cap, l->d_poff, l->d_end, n, l->d_packed, st)) goto fail;
+  CHK(hipMemcpyAsync(l->h_out, l->d_packed, l->out_off[n] + 16 <= l->d_packed_cap ?
+                     l->out_off[n] + 16 : l->out_off[n], hipMemcpyDeviceToHost, st));
   CHK(hipStreamSynchronize(st));
   t4 = now_us();
   for (int f = 0; f < n; ++f) {

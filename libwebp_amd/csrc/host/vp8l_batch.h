@@ -22,6 +22,8 @@ typedef struct vp8l_engine {
   uint32_t* d_mult;
   uint32_t* d_aflag;
   int64_t* d_feat;
+  uint32_t* d_tl;
+  uint32_t* d_tn;
   uint32_t* d_hc;
   uint8_t* d_assign;
   uint32_t* d_ctab;
@@ -31,6 +33,13 @@ typedef struct vp8l_engine {
   uint32_t* d_bsum;
   uint64_t* d_boff;
   uint8_t* d_out;
+  uint8_t* d_packed;           /* packed .webp files (k_vp8l_pack), grown on demand */
+  size_t d_packed_cap;
+  uint64_t* d_poff;
+  uint32_t* d_hpack;           /* packed headers, grown on demand */
+  size_t d_hpack_cap;
+  uint64_t* d_hoff;
+  uint32_t* d_hwords;
   /* host (pinned) */
   uint8_t* h_modes;
   uint32_t* h_mult;
@@ -43,6 +52,11 @@ typedef struct vp8l_engine {
   uint64_t* h_end;
   uint8_t* h_hdr;              /* per frame hdr_cap bytes of header */
   uint8_t* h_out;              /* packed .webp files of the last call */
+  uint64_t* h_poff;
+  uint8_t* h_hpack;
+  size_t h_hpack_cap;
+  uint64_t* h_hoff;
+  uint32_t* h_hwords;
   size_t h_out_cap;
   size_t* hdr_bytes;
   size_t* out_off;

@@ -12,6 +12,8 @@
  *   hits      N x ceil(npix/64) uint64   colour-cache hit bit per pixel (L2)
  *   ops       N x npix uint32            parse: act | len << 2 | dist_code << 15 (L3)
  *   feat      N x nht  int64             histogram-tile entropy feature (L4)
+ *   tl / tn   N x nht x tile_cap uint32  sparse tile histograms: symbol | count << 12,
+ *             N x nht uint32             and their lengths (L4)
  *   hc        N x KMAX x NS uint32       cluster histograms (L5)
  *   assign    N x nht  uint8             cluster per histogram tile (L5)
  *   ctab      N x KMAX x NS uint32       code | bits << 16 per group/symbol (host)
@@ -41,6 +43,11 @@ extern "C" {
 #define VP8L_BLOCK 1024            /* pixels per bit-writer block */
 #define VP8L_MAX_HUFF_IMAGE 2600   /* MAX_HUFF_IMAGE_SIZE, src/enc/vp8l_enc.c */
 
+/* entries of one sparse tile histogram: at most NS symbols, at most 4 per
+ * pixel of a (1 << hb)^2 tile */
+#define VP8L_TILE_CAP(hb) \
+  ((((size_t)4 << (2 * (hb))) < (size_t)VP8L_NS) ? ((size_t)4 << (2 * (hb))) : (size_t)VP8L_NS)
+
 typedef struct {
   int w, h, n;
   int tb, hb;                      /* transform / histogram tile bits */
@@ -60,8 +67,8 @@ int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rstride,
  * table (1024 entries) of the fraction of log2 in 1/4096 bit. */
 int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
                         const int32_t* flog2, uint64_t* hits, uint32_t* ops,
-                        int64_t* feat, uint32_t* hc, uint8_t* assign,
-                        void* stream);
+                        int64_t* feat, uint32_t* tl, uint32_t* tn, uint32_t* hc,
+                        uint8_t* assign, void* stream);
 /* L6/L7: per-block bit counts, per-frame scan from start_bit[f], and the
  * bit writer into out (n x out_cap bytes, zeroed except the header words the
  * host placed at the start). end_bit[f] = total payload bits. */
@@ -70,6 +77,14 @@ int vp8l_launch_write(const uint32_t* argb, const uint32_t* ops,
                       const uint8_t* gtile, const uint64_t* start_bit,
                       uint32_t* bsum, uint64_t* boff, uint64_t* end_bit,
                       uint8_t* out, size_t out_cap, void* stream);
+
+/* staging: headers packed at 4-byte aligned offsets hoff (hwords words each)
+ * into the slabs; payloads into one buffer at poff[f] + 20 (16-aligned). */
+int vp8l_launch_put_headers(const uint32_t* hdr, const uint64_t* hoff,
+                            const uint32_t* hwords, int n, uint8_t* out,
+                            size_t out_cap, void* stream);
+int vp8l_launch_pack(const uint8_t* out, size_t out_cap, const uint64_t* poff,
+                     const uint64_t* end_bit, int n, uint8_t* packed, void* stream);
 
 #ifdef __cplusplus
 }

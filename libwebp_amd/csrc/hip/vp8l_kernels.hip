@@ -4,9 +4,9 @@
 // HBM/LDS bound, no MFMA.
 //
 //   L1 k_vp8l_transform  one workgroup per transform tile: subtract green,
-//                        best of 14 predictors by histogram entropy,
-//                        cross-colour multipliers (least squares + entropy
-//                        check), residual ARGB to HBM
+//                        best of 14 predictors by a bit-length cost,
+//                        cross-colour multipliers (least squares + 6
+//                        candidates), residual ARGB to HBM
 //   L2 k_vp8l_cache      one wave per frame, 64 pixels per step: colour-cache
 //                        hit bits (same-key lanes found with CACHE_BITS ballots)
 //   L3 k_vp8l_match      one wave per row: best candidate run per pixel (ballots)
@@ -117,21 +117,11 @@ __device__ __forceinline__ V wave_sum(V v) {
 
 // ------------------------------------------------------------------ L1
 
-// Histograms of up to 4096 pixels: two 16-bit counters per 32-bit LDS word
-// halve the footprint (more workgroups per CU); same fast path as hadd.
-__device__ __forceinline__ void hadd16(uint32_t* h, uint32_t bin) {
-  const uint64_t act = __ballot(1);
-  const uint32_t first = __builtin_amdgcn_readfirstlane(bin);
-  const uint64_t same = __ballot(bin == first);
-  if (same == act) {
-    if (lane_id() == __ffsll((long long)act) - 1)
-      atomicAdd(&h[first >> 1], (uint32_t)__popcll(act) << ((first & 1) * 16));
-  } else {
-    atomicAdd(&h[bin >> 1], 1u << ((bin & 1) * 16));
-  }
-}
-__device__ __forceinline__ uint32_t hget16(const uint32_t* h, int bin) {
-  return (h[bin >> 1] >> ((bin & 1) * 16)) & 0xffffu;
+// bits of |v| for the signed 8-bit view of each residual byte, summed over
+// the bytes of a pixel (model: bitlen) -- the search cost, pure VALU
+__device__ __forceinline__ int bitlen8(int b) { return 32 - __clz(abs(s8(b))); }
+__device__ __forceinline__ int pixel_bits(uint32_t r) {
+  return bitlen8(ch(r, 0)) + bitlen8(ch(r, 8)) + bitlen8(ch(r, 16)) + bitlen8(ch(r, 24));
 }
 
 template <int T>
@@ -139,8 +129,7 @@ struct TransformSmem {
   uint32_t src[(T + 1) * (T + 2)];   // rows y0-1.., cols x0-1..x0+tw
   uint32_t first[T];                 // P(0, y) for the right-edge TR wrap
   uint32_t res[T * T];
-  uint32_t hist[14 * 4 * 128];       // [mode][channel][256 bins], 16-bit counters
-  uint32_t score[16];
+  int score[16];
   long long sums[4];
   int best;
 };
@@ -148,13 +137,11 @@ struct TransformSmem {
 template <int T>
 __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restrict__ rgba,
                                                         size_t fstride, int rstride, vp8l_params p,
-                                                        const int32_t* __restrict__ nlogn,
                                                         uint32_t* __restrict__ argb_out,
                                                         uint8_t* __restrict__ modes,
                                                         uint32_t* __restrict__ mult,
                                                         uint32_t* __restrict__ alpha_flag) {
   __shared__ TransformSmem<T> S;
-  __shared__ int all_opaque;
   const int tid = threadIdx.x, f = blockIdx.z;
   const int W = p.w, H = p.h;
   const int x0 = blockIdx.x * T, y0 = blockIdx.y * T;
@@ -163,11 +150,9 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
   const uint8_t* img = rgba + (size_t)f * fstride;
   const int tiles_x = (W + T - 1) / T;
   const int tile = blockIdx.y * tiles_x + blockIdx.x;
-  if (tid == 0) all_opaque = 1;
-  __syncthreads();
 
   // load sub-green pixels (A, R-G, G, B-G) with a 1-pixel border
-  bool opaque = true, tile_alpha = false;
+  bool tile_alpha = false;
   for (int i = tid; i < (th + 1) * sw; i += 256) {
     const int ly = i / sw, lx = i - ly * sw;
     const int y = y0 - 1 + ly, x = x0 - 1 + lx;
@@ -176,10 +161,7 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
       const uint8_t* q = img + (size_t)y * rstride + 4 * x;
       const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
       v = (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255);
-      if (a != 255) {
-        opaque = false;
-        if (ly > 0 && lx > 0 && lx <= tw) tile_alpha = true;
-      }
+      if (a != 255 && ly > 0 && lx > 0 && lx <= tw) tile_alpha = true;
     }
     S.src[i] = v;
   }
@@ -188,17 +170,11 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
       const uint8_t* q = img + (size_t)(y0 + i) * rstride;
       const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
       S.first[i] = (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255);
-      if (a != 255) opaque = false;
     }
   }
   if (__any(tile_alpha) && lane_id() == 0) atomicOr(&alpha_flag[f], 1u);
-  if (__any(!opaque) && lane_id() == 0) all_opaque = 0;
-  for (int i = tid; i < 14 * 4 * 128; i += 256) S.hist[i] = 0;
   if (tid < 16) S.score[tid] = 0;
   __syncthreads();
-  // every real pixel the predictors read is opaque: the alpha residual is 0
-  // for all 14 modes, its histogram adds the same score to each -> skip it
-  const int c0 = all_opaque ? 1 : 0;
 
   auto at = [&](int lx, int ly) -> uint32_t { return S.src[(ly + 1) * sw + lx + 1]; };
   auto tr = [&](int lx, int ly) -> uint32_t {   // (y-1)*W + x + 1, linear
@@ -208,41 +184,33 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
   // fixed predictors: (0,0) black, row 0 left, column 0 top (lossless.c:219-239)
   auto fixed_mode = [&](int x, int y) -> int { return y == 0 ? (x == 0 ? 0 : 1) : (x == 0 ? 2 : -1); };
 
-  for (int i = tid; i < np; i += 256) {
-    const int ly = i / tw, lx = i - ly * tw;
-    const int x = x0 + lx, y = y0 + ly;
-    const uint32_t P = at(lx, ly), L = at(lx - 1, ly), T_ = at(lx, ly - 1), TL = at(lx - 1, ly - 1);
-    const uint32_t TR = tr(lx, ly);
-    const int fm = fixed_mode(x, y);
-    for (int m = 0; m < 14; ++m) {
-      const uint32_t r = sub_pixels(P, predict(fm >= 0 ? fm : m, L, T_, TL, TR));
-      uint32_t* h = S.hist + m * 512;
-      if (!c0) hadd16(h, r >> 24);
-      hadd16(h + 128, (r >> 16) & 255);
-      hadd16(h + 256, (r >> 8) & 255);
-      hadd16(h + 384, r & 255);
-    }
-  }
-  __syncthreads();
-  // entropy score per mode: sum nlogn(count) (maximise)
+  // cost of each of the 14 predictors over the tile (smallest wins, first on ties)
   {
-    uint32_t sc[14];
-    for (int m = 0; m < 14; ++m) {
-      uint32_t s = 0;
-      for (int k = tid + c0 * 256; k < 1024; k += 256)
-        s += (uint32_t)nlogn[hget16(S.hist + m * 512, k)];
-      sc[m] = wave_sum(s);
+    int sc[14];
+#pragma unroll
+    for (int m = 0; m < 14; ++m) sc[m] = 0;
+    for (int i = tid; i < np; i += 256) {
+      const int ly = i / tw, lx = i - ly * tw;
+      const uint32_t P = at(lx, ly), L = at(lx - 1, ly), T_ = at(lx, ly - 1), TL = at(lx - 1, ly - 1);
+      const uint32_t TR = tr(lx, ly);
+      const int fm = fixed_mode(x0 + lx, y0 + ly);
+#pragma unroll
+      for (int m = 0; m < 14; ++m)
+        sc[m] += pixel_bits(sub_pixels(P, predict(fm >= 0 ? fm : m, L, T_, TL, TR)));
     }
-    if (lane_id() == 0)
-      for (int m = 0; m < 14; ++m) atomicAdd(&S.score[m], sc[m]);
+#pragma unroll
+    for (int m = 0; m < 14; ++m) {
+      const int v = wave_sum(sc[m]);
+      if (lane_id() == 0) atomicAdd(&S.score[m], v);
+    }
   }
   __syncthreads();
   if (tid == 0) {
     int best = 0;
     for (int m = 1; m < 14; ++m)
-      if (S.score[m] > S.score[best]) best = m;
+      if (S.score[m] < S.score[best]) best = m;
     S.best = best;
-    S.sums[0] = S.sums[1] = S.sums[2] = 0;
+    S.sums[0] = S.sums[1] = S.sums[2] = S.sums[3] = 0;
   }
   __syncthreads();
   const int best = S.best;
@@ -263,42 +231,44 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     atomicAdd((unsigned long long*)&S.sums[2], (unsigned long long)sgb);
   }
   __syncthreads();
-  // three rounds of 4 candidates: g2r on red, g2b on blue, r2b on blue'
-  int cand[4];
+  // cross colour (model: choose_cross_color): three rounds, each the best of
+  // 6 candidates {0, ls-2 .. ls+2} by the bitlen cost
   int g2r = 0, g2b = 0, r2b = 0;
   for (int round = 0; round < 3; ++round) {
     long long sxy, sxx;
     if (round == 0) { sxy = S.sums[1]; sxx = S.sums[0]; }
     else if (round == 1) { sxy = S.sums[2]; sxx = S.sums[0]; }
-    else { sxy = S.sums[3]; sxx = S.sums[2]; }   // round 2: sums reloaded below
+    else { sxy = S.sums[3]; sxx = S.sums[2]; }   // r2b sums, computed in round 1
     const int ls = ls_multiplier(sxy, sxx);
-    cand[0] = 0; cand[1] = clamp8(ls - 1); cand[2] = clamp8(ls); cand[3] = clamp8(ls + 1);
-    for (int i = tid; i < 4 * 128; i += 256) S.hist[i] = 0;
-    if (tid < 4) S.score[tid] = 0;
-    __syncthreads();
+    int cand[6];
+    cand[0] = 0;
+#pragma unroll
+    for (int c = 1; c < 6; ++c) cand[c] = clamp8(ls + c - 3);
+    int cs[6] = {0, 0, 0, 0, 0, 0};
     for (int i = tid; i < np; i += 256) {
       const uint32_t r = S.res[i];
       const int g = ch(r, 8), rr = ch(r, 16), bb = ch(r, 0);
-      for (int c = 0; c < 4; ++c) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
         int v;
-        if (round == 0) v = (rr - ctd(cand[c], g)) & 255;
-        else if (round == 1) v = (bb - ctd(cand[c], g)) & 255;
-        else v = ((bb - ctd(g2b, g)) - ctd(cand[c], rr)) & 255;
-        hadd16(S.hist + c * 128, (uint32_t)v);
+        if (round == 0) v = rr - ctd(cand[c], g);
+        else if (round == 1) v = bb - ctd(cand[c], g);
+        else v = (bb - ctd(g2b, g)) - ctd(cand[c], rr);
+        cs[c] += bitlen8(v & 255);
       }
     }
+    __syncthreads();   // everyone has read S.score / S.sums of the previous step
+    if (tid < 6) S.score[tid] = 0;
     __syncthreads();
-    {
-      uint32_t sc[4];
-      for (int c = 0; c < 4; ++c)
-        sc[c] = wave_sum((uint32_t)nlogn[hget16(S.hist + c * 128, tid)]);
-      if (lane_id() == 0)
-        for (int c = 0; c < 4; ++c) atomicAdd(&S.score[c], sc[c]);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      const int v = wave_sum(cs[c]);
+      if (lane_id() == 0) atomicAdd(&S.score[c], v);
     }
     __syncthreads();
     int bc = 0;
-    for (int c = 1; c < 4; ++c)
-      if (S.score[c] > S.score[bc]) bc = c;
+    for (int c = 1; c < 6; ++c)
+      if (S.score[c] < S.score[bc]) bc = c;
     const int chosen = cand[bc];
     if (round == 0) g2r = chosen;
     else if (round == 1) {
@@ -885,7 +855,7 @@ __global__ __launch_bounds__(256) void k_vp8l_pack(const uint8_t* __restrict__ o
 static int check_launch() { return hipGetLastError() == hipSuccess; }
 
 extern "C" int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rstride,
-                                     const vp8l_params* p, const int32_t* nlogn, uint32_t* argb,
+                                     const vp8l_params* p, uint32_t* argb,
                                      uint8_t* modes, uint32_t* mult, uint32_t* alpha_flag,
                                      void* stream) {
   if (p->tb < 2 || p->tb > 6 || p->w <= 0 || p->h <= 0 || p->n <= 0) return 0;
@@ -893,7 +863,7 @@ extern "C" int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rs
   hipStream_t st = (hipStream_t)stream;
 #define L1(T)                                                                              \
   hipLaunchKernelGGL(k_vp8l_transform<T>, grid, dim3(256), 0, st, rgba, fstride, rstride, *p, \
-                     nlogn, argb, modes, mult, alpha_flag)
+                     argb, modes, mult, alpha_flag)
   switch (p->tb) {
     case 2: L1(4); break;
     case 3: L1(8); break;

@@ -180,7 +180,7 @@ int vp8l_engine_run(struct WebPGpuBatch* b, const uint8_t* rgba, size_t fstride,
   for (int f = 0; f < n; ++f) l->err[f] = VP8_ENC_OK;
   CHK(hipMemsetAsync(l->d_aflag, 0, N * sizeof(uint32_t), st));
   CHK(hipEventRecord(b->ev[0], st));
-  if (!vp8l_launch_transform(rgba, fstride, rstride, &p, l->d_tabs, l->d_argb, l->d_modes,
+  if (!vp8l_launch_transform(rgba, fstride, rstride, &p, l->d_argb, l->d_modes,
                              l->d_mult, l->d_aflag, st))
     goto fail;
   CHK(hipEventRecord(b->ev[1], st));

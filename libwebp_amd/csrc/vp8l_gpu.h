@@ -58,9 +58,9 @@ typedef struct {
 
 /* L1: subtract green + per-tile predictor + cross colour. rgba frames at
  * fstride bytes, rows at rstride bytes. alpha_flag[f] |= 1 if any alpha
- * != 255. nlogn: DEVICE table of round(n*log2(n)*4096), n <= 4096. */
+ * != 255. */
 int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rstride,
-                          const vp8l_params* p, const int32_t* nlogn,
+                          const vp8l_params* p,
                           uint32_t* argb, uint8_t* modes, uint32_t* mult,
                           uint32_t* alpha_flag, void* stream);
 /* L2..L5: cache hits, row parse, tile features, clustering. flog2: DEVICE

@@ -60,20 +60,9 @@ CODE_TO_PLANE = [
     0x4f, 0x10, 0x20, 0x62, 0x6e, 0x30, 0x73, 0x7d, 0x51, 0x5f,
     0x40, 0x72, 0x7e, 0x61, 0x6f, 0x50, 0x71, 0x7f, 0x60, 0x70]
 HASH_MUL = 0x1E35A7BD
-NLOGN_SCALE = 4096          # nlogn table: round(n*log2(n)*4096), n <= 4096
 MAX_HUFF_IMAGE_SIZE = 2600  # src/enc/vp8l_enc.c (GetHistoBits)
 # copy/literal decision thresholds of the greedy row parse
 MIN_COPY = 3
-
-
-def nlogn_table(nmax=4096):
-    t = np.zeros(nmax + 1, dtype=np.int64)
-    for n in range(2, nmax + 1):
-        t[n] = int(math.floor(n * math.log2(n) * NLOGN_SCALE + 0.5))
-    return t
-
-
-NLOGN = nlogn_table()
 
 
 def sub_sample(size, bits):
@@ -206,17 +195,22 @@ def fixed_mode_mask(H, W):
     return m
 
 
+def bitlen(v):
+    """Bits of |v| for the signed 8-bit view of residual bytes (0 for 0):
+    the per-value cost of the predictor and cross-colour searches (a
+    Laplacian-like proxy for the coded size that needs no histogram)."""
+    return np.frexp(np.abs(to_s8(v)).astype(np.float64))[1].astype(np.int64)
+
+
 def tile_sums(values, tb, H, W):
-    """Histogram-entropy score S = sum over channels/bins of nlogn(count) for
-    each tile. values: (H, W, C) int64 in 0..255."""
+    """Score per tile (larger is better): minus the sum of bitlen over all
+    pixels and channels. values: (H, W, C) int64 in 0..255."""
     tw, th = sub_sample(W, tb), sub_sample(H, tb)
     ty = (np.arange(H) >> tb)[:, None]
     tx = (np.arange(W) >> tb)[None, :]
     tile = (ty * tw + tx)
-    C_ = values.shape[-1]
-    key = (tile[..., None] * C_ + np.arange(C_)) * 256 + values
-    cnt = np.bincount(key.ravel(), minlength=tw * th * C_ * 256)
-    return NLOGN[cnt].reshape(tw * th, C_ * 256).sum(axis=1)
+    return -np.bincount(tile.ravel(), weights=bitlen(values).sum(axis=-1).ravel(),
+                        minlength=tw * th).astype(np.int64)
 
 
 def to_s8(v):
@@ -241,15 +235,16 @@ def ls_multiplier(sxy, sxx):
 
 def candidates(ls):
     out = [0]
-    for c in (ls - 1, ls, ls + 1):
+    for c in (ls - 2, ls - 1, ls, ls + 1, ls + 2):
         out.append(max(-128, min(127, c)))
     return out
 
 
 def choose_cross_color(res, tb, H, W):
     """res: (H, W, 4) predictor residuals (A,R,G,B). Per tile choose
-    (g2r, g2b, r2b) -- least squares start + entropy check of 4 candidates
-    each. Returns (tiles, 3) int and the transformed residual image."""
+    (g2r, g2b, r2b) -- least squares start, then the best of 6 candidates
+    (0 and ls-2..ls+2) by the bitlen score. Returns (tiles, 3) int and the
+    transformed residual image."""
     tw, th = sub_sample(W, tb), sub_sample(H, tb)
     out = res.copy()
     mult = np.zeros((th * tw, 3), dtype=np.int64)
@@ -260,13 +255,13 @@ def choose_cross_color(res, tb, H, W):
             sgg = int((g * g).sum())
             best = None
             for t in candidates(ls_multiplier(int((g * r).sum()), sgg)):
-                s = int(NLOGN[np.bincount((blk[:, 1] - ctd(t, g)) & 255, minlength=256)].sum())
+                s = -int(bitlen((blk[:, 1] - ctd(t, g)) & 255).sum())
                 if best is None or s > best[0]:
                     best = (s, t)
             g2r = best[1]
             best = None
             for t in candidates(ls_multiplier(int((g * to_s8(b)).sum()), sgg)):
-                s = int(NLOGN[np.bincount((b - ctd(t, g)) & 255, minlength=256)].sum())
+                s = -int(bitlen((b - ctd(t, g)) & 255).sum())
                 if best is None or s > best[0]:
                     best = (s, t)
             g2b = best[1]
@@ -274,7 +269,7 @@ def choose_cross_color(res, tb, H, W):
             srr = int((r * r).sum())
             best = None
             for t in candidates(ls_multiplier(int((r * to_s8(bb)).sum()), srr)):
-                s = int(NLOGN[np.bincount((bb - ctd(t, r)) & 255, minlength=256)].sum())
+                s = -int(bitlen((bb - ctd(t, r)) & 255).sum())
                 if best is None or s > best[0]:
                     best = (s, t)
             r2b = best[1]
@@ -288,7 +283,7 @@ def choose_cross_color(res, tb, H, W):
 
 
 def transform_image(rgba, tb):
-    """Subtract green -> predictor (per-tile best of 14 by histogram entropy)
+    """Subtract green -> predictor (per-tile best of 14 by the bitlen score)
     -> cross colour. Returns (modes (tiles,), mult (tiles,3), residual ARGB
     uint32 (H, W))."""
     H, W, _ = rgba.shape

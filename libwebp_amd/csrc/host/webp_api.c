@@ -263,6 +263,22 @@ static WebPGpuBatch* engine_for(const WebPConfig* cfg, int w, int h) {
   return g_engine;
 }
 
+/* lossless (VP8L) engine, cached per size and method */
+static WebPGpuBatch* g_lengine = NULL;
+
+static WebPGpuBatch* lossless_engine_for(const WebPConfig* cfg, int w, int h) {
+  if (g_lengine && (g_lengine->w != w || g_lengine->h != h ||
+                    g_lengine->cfg.method != cfg->method)) {
+    WebPGpuBatchDelete(g_lengine);
+    g_lengine = NULL;
+  }
+  if (!g_lengine) {
+    if (WebPGpuDeviceCount() <= 0) return NULL;
+    g_lengine = WebPGpuBatchNew(0, w, h, 1, cfg, 1);
+  }
+  return g_lengine;
+}
+
 /* ---- import (picture_csp_enc.c:474-619, 732-844) ---- */
 
 static int import_packed(WebPPicture* pic, const uint8_t* src, int stride, int step, int swap_rb,
@@ -270,7 +286,7 @@ static int import_packed(WebPPicture* pic, const uint8_t* src, int stride, int s
   const int w = pic->width, h = pic->height;
   if (abs(stride) < (with_alpha ? 4 : step) * w) return 0;
   const int ri = swap_rb ? 2 : 0, bi = swap_rb ? 0 : 2;
-  if (pic->use_argb) {   /* ARGB container for the (unsupported) lossless path */
+  if (pic->use_argb) {   /* ARGB container (lossless path, WebPPictureARGBToYUVA) */
     if (!WebPPictureAlloc(pic)) return 0;
     for (int y = 0; y < h; ++y) {
       const uint8_t* s = src + (size_t)y * stride;
@@ -405,6 +421,45 @@ static double psnr(uint64_t err, uint64_t size) {
   return (err > 0 && size > 0) ? 10. * log10(255. * 255. * size / err) : 99.;
 }
 
+/* webp_enc.c:396-407: ARGB samples (converted from YUVA when needed),
+ * fully transparent pixels zeroed unless `exact`, then the VP8L engine
+ * (host/vp8l_batch.c) on one frame. */
+static int encode_lossless(const WebPConfig* config, WebPPicture* pic) {
+  if (pic->argb == NULL && !WebPPictureYUVAToARGB(pic)) return 0;
+  const int w = pic->width, h = pic->height;
+  uint8_t* rgba = (uint8_t*)malloc((size_t)w * h * 4);
+  if (!rgba) return set_error(pic, VP8_ENC_ERROR_OUT_OF_MEMORY);
+  for (int y = 0; y < h; ++y) {
+    const uint32_t* s = pic->argb + (size_t)y * pic->argb_stride;
+    uint8_t* d = rgba + (size_t)y * w * 4;
+    for (int x = 0; x < w; ++x, d += 4) {
+      uint32_t v = s[x];
+      if (!config->exact && (v >> 24) == 0) v = 0;   /* WebPReplaceTransparentPixels */
+      d[0] = (uint8_t)(v >> 16); d[1] = (uint8_t)(v >> 8); d[2] = (uint8_t)v;
+      d[3] = (uint8_t)(v >> 24);
+    }
+  }
+  if (!report(pic, 5)) { free(rgba); return 0; }
+  pthread_mutex_lock(&g_engine_lock);
+  WebPGpuBatch* e = lossless_engine_for(config, w, h);
+  int ok = e != NULL && WebPGpuBatchEncodeRGBAHost(e, rgba, (size_t)w * h * 4, 4 * w, 1);
+  free(rgba);
+  const int err = ok ? WebPGpuBatchError(e, 0) : VP8_ENC_ERROR_OUT_OF_MEMORY;
+  const size_t size = ok && !err ? WebPGpuBatchOutputSize(e, 0) : 0;
+  uint8_t* out = size ? (uint8_t*)malloc(size) : NULL;
+  if (out) memcpy(out, WebPGpuBatchOutput(e, 0), size);
+  pthread_mutex_unlock(&g_engine_lock);
+  if (!ok || err != VP8_ENC_OK || out == NULL) {
+    free(out);
+    return set_error(pic, err != VP8_ENC_OK ? (WebPEncodingError)err : VP8_ENC_ERROR_OUT_OF_MEMORY);
+  }
+  ok = report(pic, 90) && pic->writer(out, size, pic);
+  free(out);
+  if (!ok) return pic->error_code != VP8_ENC_OK ? 0 : set_error(pic, VP8_ENC_ERROR_BAD_WRITE);
+  if (pic->stats != NULL) pic->stats->coded_size = (int)size;
+  return report(pic, 100);
+}
+
 int WebPEncode(const WebPConfig* config, WebPPicture* pic) {
   if (pic == NULL) return 0;
   pic->error_code = VP8_ENC_OK;
@@ -414,7 +469,7 @@ int WebPEncode(const WebPConfig* config, WebPPicture* pic) {
   if (pic->width > WEBP_MAX_DIMENSION || pic->height > WEBP_MAX_DIMENSION)
     return set_error(pic, VP8_ENC_ERROR_BAD_DIMENSION);
   if (pic->stats != NULL) memset(pic->stats, 0, sizeof(*pic->stats));
-  if (config->lossless) return set_error(pic, VP8_ENC_ERROR_INVALID_CONFIGURATION);
+  if (config->lossless) return encode_lossless(config, pic);
   vp8h_frame probe;
   if (!vp8h_frame_init(&probe, config, pic->width, pic->height))
     return set_error(pic, VP8_ENC_ERROR_INVALID_CONFIGURATION);
@@ -487,7 +542,7 @@ int WebPEncode(const WebPConfig* config, WebPPicture* pic) {
 typedef int (*Importer)(WebPPicture*, const uint8_t*, int);
 
 static size_t encode_oneshot(const uint8_t* px, int w, int h, int stride, Importer imp, float q,
-                             uint8_t** output) {
+                             int lossless, uint8_t** output) {
   WebPPicture pic;
   WebPConfig cfg;
   WebPMemoryWriter wrt;
@@ -495,6 +550,8 @@ static size_t encode_oneshot(const uint8_t* px, int w, int h, int stride, Import
   if (!WebPConfigInitInternal(&cfg, WEBP_PRESET_DEFAULT, q, WEBP_ENCODER_ABI_VERSION) ||
       !WebPPictureInitInternal(&pic, WEBP_ENCODER_ABI_VERSION))
     return 0;
+  cfg.lossless = !!lossless;
+  pic.use_argb = !!lossless;
   pic.width = w;
   pic.height = h;
   pic.writer = WebPMemoryWrite;
@@ -512,36 +569,29 @@ static size_t encode_oneshot(const uint8_t* px, int w, int h, int stride, Import
 }
 
 size_t WebPEncodeRGB(const uint8_t* p, int w, int h, int s, float q, uint8_t** o) {
-  return encode_oneshot(p, w, h, s, WebPPictureImportRGB, q, o);
+  return encode_oneshot(p, w, h, s, WebPPictureImportRGB, q, 0, o);
 }
 size_t WebPEncodeBGR(const uint8_t* p, int w, int h, int s, float q, uint8_t** o) {
-  return encode_oneshot(p, w, h, s, WebPPictureImportBGR, q, o);
+  return encode_oneshot(p, w, h, s, WebPPictureImportBGR, q, 0, o);
 }
 size_t WebPEncodeRGBA(const uint8_t* p, int w, int h, int s, float q, uint8_t** o) {
-  return encode_oneshot(p, w, h, s, WebPPictureImportRGBA, q, o);
+  return encode_oneshot(p, w, h, s, WebPPictureImportRGBA, q, 0, o);
 }
 size_t WebPEncodeBGRA(const uint8_t* p, int w, int h, int s, float q, uint8_t** o) {
-  return encode_oneshot(p, w, h, s, WebPPictureImportBGRA, q, o);
+  return encode_oneshot(p, w, h, s, WebPPictureImportBGRA, q, 0, o);
 }
 
-/* lossless (VP8L) is not part of this build */
-static size_t no_lossless(uint8_t** o) {
-  if (o) *o = NULL;
-  return 0;
-}
+/* picture_enc.c:285-297: lossless one-shot API at quality 70 */
+#define LOSSLESS_DEFAULT_QUALITY 70.f
 size_t WebPEncodeLosslessRGB(const uint8_t* p, int w, int h, int s, uint8_t** o) {
-  (void)p; (void)w; (void)h; (void)s;
-  return no_lossless(o);
+  return encode_oneshot(p, w, h, s, WebPPictureImportRGB, LOSSLESS_DEFAULT_QUALITY, 1, o);
 }
 size_t WebPEncodeLosslessBGR(const uint8_t* p, int w, int h, int s, uint8_t** o) {
-  (void)p; (void)w; (void)h; (void)s;
-  return no_lossless(o);
+  return encode_oneshot(p, w, h, s, WebPPictureImportBGR, LOSSLESS_DEFAULT_QUALITY, 1, o);
 }
 size_t WebPEncodeLosslessRGBA(const uint8_t* p, int w, int h, int s, uint8_t** o) {
-  (void)p; (void)w; (void)h; (void)s;
-  return no_lossless(o);
+  return encode_oneshot(p, w, h, s, WebPPictureImportRGBA, LOSSLESS_DEFAULT_QUALITY, 1, o);
 }
 size_t WebPEncodeLosslessBGRA(const uint8_t* p, int w, int h, int s, uint8_t** o) {
-  (void)p; (void)w; (void)h; (void)s;
-  return no_lossless(o);
+  return encode_oneshot(p, w, h, s, WebPPictureImportBGRA, LOSSLESS_DEFAULT_QUALITY, 1, o);
 }

@@ -41,6 +41,7 @@ __global__ __launch_bounds__(256) void k_import(const uint8_t* __restrict__ rgba
                                                 size_t fstride, int rstride, int w, int h,
                                                 uint8_t* __restrict__ yuv, size_t yfb,
                                                 uint32_t* __restrict__ aflags,
+                                                uint8_t* __restrict__ aplane,
                                                 const uint16_t* __restrict__ g_g2l,
                                                 const int32_t* __restrict__ g_l2g) {
   __shared__ uint16_t g2l[256];
@@ -73,6 +74,15 @@ __global__ __launch_bounds__(256) void k_import(const uint8_t* __restrict__ rgba
   uint32_t alpha_bad = (p[0][0][3] != 0xff) | (p[1][0][3] != 0xff);
   if (two_cols) alpha_bad |= (p[0][1][3] != 0xff) | (p[1][1][3] != 0xff);
   if (alpha_bad) atomicOr(aflags + f, 1u);
+  {   // the WebPPicture alpha plane (WebPExtractAlpha), stride w
+    uint8_t* arow = aplane + (size_t)f * w * h + (size_t)y0 * w + x0;
+    arow[0] = p[0][0][3];
+    if (two_cols) arow[1] = p[0][1][3];
+    if (two_rows) {
+      arow[w] = p[1][0][3];
+      if (two_cols) arow[w + 1] = p[1][1][3];
+    }
+  }
   uint8_t* yrow = Y + (size_t)y0 * w + x0;
   yrow[0] = rgb_to_y(p[0][0][0], p[0][0][1], p[0][0][2]);
   if (two_cols) yrow[1] = rgb_to_y(p[0][1][0], p[0][1][1], p[0][1][2]);
@@ -80,10 +90,27 @@ __global__ __launch_bounds__(256) void k_import(const uint8_t* __restrict__ rgba
     yrow[w] = rgb_to_y(p[1][0][0], p[1][0][1], p[1][0][2]);
     if (two_cols) yrow[w + 1] = rgb_to_y(p[1][1][0], p[1][1][1], p[1][1][2]);
   }
+  // AccumulateRGBA (picture_csp_enc.c:388-424): 2x2 blocks with partial
+  // alpha average in linear light weighted by alpha, divided through
+  // kInvAlpha[a] = 2^19 / a (LinearToGammaWeighted, :359-373); opaque and
+  // fully transparent blocks take the plain average (AccumulateRGB)
+  const uint32_t asum = two_cols ? (uint32_t)p[0][0][3] + p[1][0][3] + p[0][1][3] + p[1][1][3]
+                                 : 2u * ((uint32_t)p[0][0][3] + p[1][0][3]);
+  const bool weighted = asum != 0 && asum != 4 * 0xff;
   int c[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    if (two_cols) {
+    if (weighted) {
+      uint64_t sum;
+      if (two_cols) {
+        sum = (uint64_t)p[0][0][3] * g2l[p[0][0][k]] + (uint64_t)p[0][1][3] * g2l[p[0][1][k]] +
+              (uint64_t)p[1][0][3] * g2l[p[1][0][k]] + (uint64_t)p[1][1][3] * g2l[p[1][1][k]];
+      } else {
+        sum = 2 * ((uint64_t)p[0][0][3] * g2l[p[0][0][k]] + (uint64_t)p[1][0][3] * g2l[p[1][0][k]]);
+      }
+      const uint32_t inv = (1u << 19) / asum;
+      c[k] = lin_to_gamma(l2g, (uint32_t)((sum * inv) >> 17), 0);
+    } else if (two_cols) {
       c[k] = lin_to_gamma(l2g, (uint32_t)g2l[p[0][0][k]] + g2l[p[0][1][k]] + g2l[p[1][0][k]] +
                                    g2l[p[1][1][k]], 0);
     } else {
@@ -92,6 +119,72 @@ __global__ __launch_bounds__(256) void k_import(const uint8_t* __restrict__ rgba
   }
   U[(size_t)j * uvw + i] = clip_uv(-9719 * c[0] - 19081 * c[1] + 28800 * c[2]);
   V[(size_t)j * uvw + i] = clip_uv(28800 * c[0] - 24116 * c[1] - 4684 * c[2]);
+}
+
+// alpha plane of the sharp-YUV path (WebPExtractAlpha)
+__global__ __launch_bounds__(256) void k_extract_alpha(const uint8_t* __restrict__ rgba,
+                                                       size_t fstride, int rstride, int w, int h,
+                                                       uint8_t* __restrict__ aplane) {
+  const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+  if (x >= w) return;
+  aplane[(size_t)f * w * h + (size_t)y * w + x] = rgba[f * fstride + (size_t)y * rstride + 4 * x + 3];
+}
+
+// WebPCleanupTransparentArea for YUVA (picture_tools_enc.c:99-168), frames
+// with alpha only. One workgroup per 8-row strip: 8x8 blocks with some
+// transparent pixels get those pixels' luma set to the average of the
+// visible ones (SmoothenBlock :53-84); fully transparent blocks of a full
+// strip are flattened to the Y/U/V values of the first block of their run
+// (`need_reset`), which no thread changes (its own flatten rewrites the same
+// values), so the runs resolve in parallel.
+__global__ __launch_bounds__(256) void k_cleanup_alpha(uint8_t* __restrict__ yuv, size_t yfb,
+                                                       const uint8_t* __restrict__ aplane,
+                                                       const uint32_t* __restrict__ aflags,
+                                                       int w, int h) {
+  __shared__ uint8_t transparent[16384 / 8 + 1];
+  const int f = blockIdx.y, y0 = blockIdx.x * 8, t = threadIdx.x;
+  if (!aflags[f]) return;
+  const int uvw = (w + 1) >> 1, uvh = (h + 1) >> 1;
+  uint8_t* Y = yuv + (size_t)f * yfb;
+  uint8_t* U = Y + (size_t)w * h;
+  uint8_t* V = U + (size_t)uvw * uvh;
+  const uint8_t* A = aplane + (size_t)f * w * h;
+  const int bh = min(8, h - y0);
+  const int nfull = w / 8, nb = (w + 7) / 8;
+  for (int b = t; b < nb; b += 256) {
+    const int x0 = b * 8, bw = min(8, w - x0);
+    int sum = 0, count = 0;
+    for (int y = 0; y < bh; ++y)
+      for (int x = 0; x < bw; ++x)
+        if (A[(size_t)(y0 + y) * w + x0 + x] != 0) {
+          ++count;
+          sum += Y[(size_t)(y0 + y) * w + x0 + x];
+        }
+    if (count > 0 && count < bw * bh) {
+      const uint8_t avg = (uint8_t)(sum / count);
+      for (int y = 0; y < bh; ++y)
+        for (int x = 0; x < bw; ++x)
+          if (A[(size_t)(y0 + y) * w + x0 + x] == 0) Y[(size_t)(y0 + y) * w + x0 + x] = avg;
+    }
+    transparent[b] = (count == 0 && bh == 8 && b < nfull);
+  }
+  __syncthreads();
+  if (bh != 8) return;   // the partial last strip is only smoothed
+  for (int b = t; b < nfull; b += 256) {
+    if (!transparent[b]) continue;
+    int s0 = b;
+    while (s0 > 0 && transparent[s0 - 1]) --s0;
+    const uint8_t vy = Y[(size_t)y0 * w + 8 * s0];
+    const uint8_t vu = U[(size_t)(y0 >> 1) * uvw + 4 * s0];
+    const uint8_t vv = V[(size_t)(y0 >> 1) * uvw + 4 * s0];
+    for (int y = 0; y < 8; ++y)
+      for (int x = 0; x < 8; ++x) Y[(size_t)(y0 + y) * w + 8 * b + x] = vy;
+    for (int y = 0; y < 4; ++y)
+      for (int x = 0; x < 4; ++x) {
+        U[(size_t)((y0 >> 1) + y) * uvw + 4 * b + x] = vu;
+        V[(size_t)((y0 >> 1) + y) * uvw + 4 * b + x] = vv;
+      }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1105,14 +1198,30 @@ extern "C" int vp8g_launch_check(const char* what) {
 extern "C" {
 
 int vp8g_launch_import(const uint8_t* rgba, size_t fstride, int rstride, int w, int h, int n,
-                       uint8_t* yuv, size_t yfb, uint32_t* aflags, const uint16_t g2l[256],
-                       const int32_t l2g[33], void* stream) {
+                       uint8_t* yuv, size_t yfb, uint32_t* aflags, uint8_t* aplane,
+                       const uint16_t g2l[256], const int32_t l2g[33], void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int uvw = (w + 1) >> 1, uvh = (h + 1) >> 1;
   dim3 grid((uvw + 255) / 256, uvh, n);
   hipLaunchKernelGGL(k_import, grid, dim3(256), 0, st, rgba, fstride, rstride, w, h, yuv, yfb,
-                     aflags, g2l, l2g);
+                     aflags, aplane, g2l, l2g);
   return launch_check("k_import");
+}
+
+int vp8g_launch_extract_alpha(const uint8_t* rgba, size_t fstride, int rstride, int w, int h,
+                              int n, uint8_t* aplane, void* stream) {
+  dim3 grid((w + 255) / 256, h, n);
+  hipLaunchKernelGGL(k_extract_alpha, grid, dim3(256), 0, (hipStream_t)stream, rgba, fstride,
+                     rstride, w, h, aplane);
+  return launch_check("k_extract_alpha");
+}
+
+int vp8g_launch_cleanup_alpha(uint8_t* yuv, size_t yfb, const uint8_t* aplane,
+                              const uint32_t* aflags, int w, int h, int n, void* stream) {
+  dim3 grid((h + 7) / 8, n);
+  hipLaunchKernelGGL(k_cleanup_alpha, grid, dim3(256), 0, (hipStream_t)stream, yuv, yfb, aplane,
+                     aflags, w, h);
+  return launch_check("k_cleanup_alpha");
 }
 
 int vp8g_launch_analysis(const uint8_t* yuv, size_t yfb, int w, int h, int n, uint8_t* mb_alpha,

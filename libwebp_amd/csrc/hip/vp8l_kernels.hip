@@ -158,18 +158,26 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     const int y = y0 - 1 + ly, x = x0 - 1 + lx;
     uint32_t v = 0;
     if (y >= 0 && x >= 0 && x < W) {
-      const uint8_t* q = img + (size_t)y * rstride + 4 * x;
-      const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
-      v = (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255);
-      if (a != 255 && ly > 0 && lx > 0 && lx <= tw) tile_alpha = true;
+      if (p.alpha) {   // ALPH: the alpha plane as green, no subtract green
+        v = (uint32_t)img[(size_t)y * rstride + x] << 8;
+      } else {
+        const uint8_t* q = img + (size_t)y * rstride + 4 * x;
+        const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
+        v = (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255);
+        if (a != 255 && ly > 0 && lx > 0 && lx <= tw) tile_alpha = true;
+      }
     }
     S.src[i] = v;
   }
   if (x0 + tw == W) {
     for (int i = tid; i < th; i += 256) {
       const uint8_t* q = img + (size_t)(y0 + i) * rstride;
-      const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
-      S.first[i] = (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255);
+      if (p.alpha) {
+        S.first[i] = (uint32_t)q[0] << 8;
+      } else {
+        const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
+        S.first[i] = (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255);
+      }
     }
   }
   if (__any(tile_alpha) && lane_id() == 0) atomicOr(&alpha_flag[f], 1u);
@@ -883,7 +891,12 @@ extern "C" int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
   const int npix = p->w * p->h;
   const int tx_n = (p->w + (1 << p->hb) - 1) >> p->hb, ty_n = (p->h + (1 << p->hb) - 1) >> p->hb;
   if (tx_n * ty_n > VP8L_MAX_HUFF_IMAGE || p->k < 1 || p->k > VP8L_KMAX) return 0;
-  hipLaunchKernelGGL(k_vp8l_cache, dim3(p->n), dim3(64), 0, st, argb, npix, hits);
+  if (p->cache_bits) {
+    hipLaunchKernelGGL(k_vp8l_cache, dim3(p->n), dim3(64), 0, st, argb, npix, hits);
+  } else if (hipMemsetAsync(hits, 0, (size_t)p->n * ((npix + 63) >> 6) * sizeof(uint64_t), st) !=
+             hipSuccess) {
+    return 0;
+  }
   hipLaunchKernelGGL(k_vp8l_match, dim3(p->h, p->n), dim3(64), 0, st, argb, hits, *p, ops);
   hipLaunchKernelGGL(k_vp8l_parse, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, *p, ops);
   hipLaunchKernelGGL(k_vp8l_tilefeat, dim3(tx_n * ty_n, p->n), dim3(256), 0, st, argb, ops, *p,

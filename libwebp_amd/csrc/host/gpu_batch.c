@@ -90,7 +90,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
     CHK(hipSetDevice(device));
     CHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
     for (int i = 0; i < 6; ++i) CHK(hipEventCreate(&b->ev[i]));
-    b->l = vp8l_engine_new(width, height, max_frames, config->method);
+    b->l = vp8l_engine_new(width, height, max_frames, config->method, 0);
     if (!b->l) goto fail;
     return b;
   }
@@ -123,6 +123,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   CHK(hipMemcpy(b->d_l2g, g_l2g, 33 * sizeof(int32_t), hipMemcpyHostToDevice));
   CHK(hipMalloc((void**)&b->d_yuv, N * b->yfb));
   CHK(hipMalloc((void**)&b->d_aflags, N * sizeof(uint32_t)));
+  CHK(hipMalloc((void**)&b->d_aplane, N * (size_t)width * height));
   CHK(hipMalloc((void**)&b->d_alpha, N * nmb));
   CHK(hipMalloc((void**)&b->d_uva, N * nmb * sizeof(uint16_t)));
   CHK(hipMalloc((void**)&b->d_segmap, N * nmb));
@@ -152,7 +153,10 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   b->out_size = (size_t*)calloc(N, sizeof(size_t));
   b->err = (int*)calloc(N, sizeof(int));
   b->hdr = (int*)calloc(2 * N, sizeof(int));
-  if (!b->frames || !b->tok_off || !b->p0 || !b->out || !b->out_size || !b->err || !b->hdr) goto fail;
+  b->araw = (uint8_t**)calloc(N, sizeof(uint8_t*));
+  if (!b->frames || !b->tok_off || !b->p0 || !b->out || !b->out_size || !b->err || !b->hdr ||
+      !b->araw)
+    goto fail;
   return b;
 fail:
   WebPGpuBatchDelete(b);
@@ -175,6 +179,11 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipHostFree(b->h_results); hipHostFree(b->h_tokens); hipHostFree(b->h_psize);
   hipHostFree(b->h_part); hipHostFree(b->h_emeta); hipHostFree(b->h_poff);
   vp8l_engine_free(b->l);
+  vp8l_engine_free(b->la);
+  hipFree(b->d_aplane);
+  if (b->araw)
+    for (int i = 0; i < b->max_frames; ++i) free(b->araw[i]);
+  free(b->araw);
   for (int i = 0; i < 6; ++i)
     if (b->ev[i]) hipEventDestroy(b->ev[i]);
   if (b->stream) hipStreamDestroy(b->stream);
@@ -229,7 +238,20 @@ static void frame_finish(WebPGpuBatch* b, int f) {
     part1.pos = b->h_psize[f];
   }
   int err = VP8_ENC_OK;
-  b->out_size[f] = vp8h_write_riff(&b->frames[f], &b->p0[f], &part1, &b->out[f], &err);
+  vp8h_alpha alpha, *ap = NULL;
+  if (b->h_aflags[f]) {   /* ALPH chunk (alpha_enc.c:110-182) */
+    if (b->araw[f]) {
+      alpha.header = 0;   /* ALPHA_NO_COMPRESSION */
+      alpha.data = b->araw[f];
+      alpha.size = (size_t)b->w * b->h;
+    } else {
+      alpha.header = 1;   /* ALPHA_LOSSLESS_COMPRESSION, no filter, no level reduction */
+      alpha.data = vp8l_engine_output(b->la, f);
+      alpha.size = b->la->out_size[f];
+    }
+    ap = &alpha;
+  }
+  b->out_size[f] = vp8h_write_riff(&b->frames[f], &b->p0[f], &part1, ap, &b->out[f], &err);
   b->err[f] = err;
   if (b->host_emit) vp8h_bw_free(&part1);
 }
@@ -269,12 +291,46 @@ static void run_tails(WebPGpuBatch* b, int n, int phase) {
 
 /* ---- pipeline ---- */
 
+/* ALPH chunks of the frames with alpha (h_aflags): the alpha planes in
+ * d_aplane through the VP8L engine in ALPH mode (alpha_enc.c:50-98), or raw
+ * (alpha_compression 0, or when the stream would not be smaller). */
+static int encode_alpha(WebPGpuBatch* b, int n) {
+  int any = 0;
+  for (int f = 0; f < n; ++f) {
+    free(b->araw[f]);
+    b->araw[f] = NULL;
+    any |= b->h_aflags[f] != 0;
+  }
+  if (!any) return 1;
+  const size_t plane = (size_t)b->w * b->h;
+  double t[10] = {0};
+  if (b->cfg.alpha_compression) {
+    if (!b->la) b->la = vp8l_engine_new(b->w, b->h, b->max_frames, b->cfg.method, 1);
+    if (!b->la) return 0;
+    if (!vp8l_engine_encode(b->la, b->stream, b->threads, b->d_aplane, plane, b->w, n, t))
+      return 0;
+  }
+  for (int f = 0; f < n; ++f) {
+    if (!b->h_aflags[f]) continue;
+    if (b->cfg.alpha_compression && !b->la->err[f] && b->la->out_size[f] <= plane) continue;
+    b->araw[f] = (uint8_t*)malloc(plane);
+    if (!b->araw[f] ||
+        hipMemcpy(b->araw[f], b->d_aplane + (size_t)f * plane, plane, hipMemcpyDeviceToHost) !=
+            hipSuccess)
+      return 0;
+  }
+  b->timings[9] = t[0] + t[1] + t[2] + t[3] + t[4];
+  return 1;
+}
+
 int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   const size_t nmb = (size_t)b->nmb;
   double t0 = now_us(), t1, t2, t3, t4;
   hipStream_t st = b->stream;
   TailJob head;
   int head_running = 0;
+  b->timings[9] = 0;
+  if (!encode_alpha(b, n)) return 0;
   if (!b->ev0_recorded) CHK(hipEventRecord(b->ev[0], st));
   b->ev0_recorded = 0;
   if (!vp8g_launch_analysis(b->d_yuv, b->yfb, b->w, b->h, n, b->d_alpha, b->d_uva, st)) return 0;
@@ -472,7 +528,9 @@ static int launch_import(WebPGpuBatch* b, const uint8_t* rgba, size_t fstride, i
                          int sharp) {
   if (!sharp)
     return vp8g_launch_import(rgba, fstride, rstride, b->w, b->h, n, b->d_yuv, b->yfb,
-                              b->d_aflags, b->d_g2l, b->d_l2g, b->stream);
+                              b->d_aflags, b->d_aplane, b->d_g2l, b->d_l2g, b->stream);
+  if (!vp8g_launch_extract_alpha(rgba, fstride, rstride, b->w, b->h, n, b->d_aplane, b->stream))
+    return 0;
   if (!b->d_sharp) {   /* first sharp call: scratch for max_frames frames */
     const uint32_t *g2l, *l2g;
     vp8h_sharp_tables(&g2l, &l2g);
@@ -515,8 +573,20 @@ static int run_rgba(WebPGpuBatch* b, const void* rgba_dev, size_t fstride, int r
   CHK(hipMemcpyAsync(b->h_aflags, b->d_aflags, n * sizeof(uint32_t), hipMemcpyDeviceToHost,
                      b->stream));
   CHK(hipStreamSynchronize(b->stream));
-  for (int f = 0; f < n; ++f)   /* transparent input needs the ALPH path */
-    if (b->h_aflags[f]) b->err[f] = VP8_ENC_ERROR_INVALID_CONFIGURATION;
+  {
+    int any = 0;
+    for (int f = 0; f < n; ++f) {
+      any |= b->h_aflags[f] != 0;
+      /* alpha level quantisation (alpha_quality < 100, QuantizeLevels) is
+       * not implemented: fail loudly rather than encode differently */
+      if (b->h_aflags[f] && b->cfg.alpha_quality < 100) b->err[f] = VP8_ENC_ERROR_INVALID_CONFIGURATION;
+    }
+    /* webp_enc.c:369-371: smooth/flatten the fully transparent areas */
+    if (any && !b->cfg.exact &&
+        !vp8g_launch_cleanup_alpha(b->d_yuv, b->yfb, b->d_aplane, b->d_aflags, b->w, b->h, n,
+                                   b->stream))
+      return 0;
+  }
   b->timings[0] = now_us() - t0;
   const int ok = vp8g_engine_run_yuv(b, n);
   b->timings[5] = now_us() - t0;
@@ -560,7 +630,7 @@ size_t WebPGpuBatchOutputSize(const WebPGpuBatch* b, int f) {
 }
 const uint8_t* WebPGpuBatchOutput(const WebPGpuBatch* b, int f) {
   if (!b || f < 0 || f >= b->last_n) return NULL;
-  if (b->l) return b->l->out_size[f] ? b->l->h_out + b->l->out_off[f] : NULL;
+  if (b->l) return vp8l_engine_output(b->l, f);
   return b->out[f];
 }
 int WebPGpuBatchStageCycles(const WebPGpuBatch* b, int f, uint64_t cycles[8]) {
@@ -602,7 +672,7 @@ int WebPGpuBatchGetMBInfo(const WebPGpuBatch* b, int f, uint8_t* dst) {
 }
 
 int vp8g_engine_upload_yuv(WebPGpuBatch* b, int f, const uint8_t* y, int ys, const uint8_t* u,
-                           const uint8_t* v, int uvs) {
+                           const uint8_t* v, int uvs, const uint8_t* a, int as) {
   uint8_t* dst = b->d_yuv + (size_t)f * b->yfb;
   if (hipSetDevice(b->device) != hipSuccess) return 0;
   if (hipMemcpy2D(dst, b->w, y, ys, b->w, b->h, hipMemcpyHostToDevice) != hipSuccess) return 0;
@@ -612,12 +682,16 @@ int vp8g_engine_upload_yuv(WebPGpuBatch* b, int f, const uint8_t* y, int ys, con
   dst += (size_t)b->uvw * b->uvh;
   if (hipMemcpy2D(dst, b->uvw, v, uvs, b->uvw, b->uvh, hipMemcpyHostToDevice) != hipSuccess)
     return 0;
+  b->h_aflags[f] = a != NULL;   /* the caller passes a plane only when it is not opaque */
+  if (a && hipMemcpy2D(b->d_aplane + (size_t)f * b->w * b->h, b->w, a, as, b->w, b->h,
+                       hipMemcpyHostToDevice) != hipSuccess)
+    return 0;
   b->err[f] = VP8_ENC_OK;
   return 1;
 }
 
 int vp8g_engine_import(WebPGpuBatch* b, const uint8_t* rgba, int stride, uint8_t* y,
-                       uint8_t* u, uint8_t* v, int* has_alpha, int sharp) {
+                       uint8_t* u, uint8_t* v, uint8_t* a, int* has_alpha, int sharp) {
   /* synchronous single-frame RGBA -> YUV through K1 (used by the
    * WebPPictureImport* API); output written to the caller's host planes */
   if (hipSetDevice(b->device) != hipSuccess) return 0;
@@ -642,5 +716,7 @@ int vp8g_engine_import(WebPGpuBatch* b, const uint8_t* rgba, int stride, uint8_t
   if (hipMemcpy(u, src, (size_t)b->uvw * b->uvh, hipMemcpyDeviceToHost) != hipSuccess) return 0;
   src += (size_t)b->uvw * b->uvh;
   if (hipMemcpy(v, src, (size_t)b->uvw * b->uvh, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  if (a && hipMemcpy(a, b->d_aplane, (size_t)b->w * b->h, hipMemcpyDeviceToHost) != hipSuccess)
+    return 0;
   return 1;
 }

@@ -25,6 +25,9 @@ struct WebPGpuBatch {
   int32_t* d_l2g;
   uint8_t* d_yuv;
   uint32_t* d_aflags;
+  uint8_t* d_aplane;         /* alpha planes, n x w*h (K1 / upload) */
+  vp8l_engine* la;           /* ALPH-chunk VP8L engine, created on first use */
+  uint8_t** araw;            /* raw alpha planes (alpha_compression 0 / fallback) */
   uint8_t* d_alpha;
   uint16_t* d_uva;
   uint8_t* d_segmap;
@@ -82,9 +85,10 @@ extern "C" {
 #endif
 int vp8g_engine_run_yuv(struct WebPGpuBatch* b, int n);
 int vp8g_engine_upload_yuv(struct WebPGpuBatch* b, int f, const uint8_t* y, int ys,
-                           const uint8_t* u, const uint8_t* v, int uvs);
+                           const uint8_t* u, const uint8_t* v, int uvs, const uint8_t* a,
+                           int as);
 int vp8g_engine_import(struct WebPGpuBatch* b, const uint8_t* rgba, int stride, uint8_t* y,
-                       uint8_t* u, uint8_t* v, int* has_alpha, int sharp);
+                       uint8_t* u, uint8_t* v, uint8_t* a, int* has_alpha, int sharp);
 #ifdef __cplusplus
 }
 #endif

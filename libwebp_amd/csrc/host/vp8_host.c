@@ -540,8 +540,11 @@ int vp8h_build_p0(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* m
   return VP8_ENC_OK;
 }
 
-size_t vp8h_write_riff(const vp8h_frame* fr, vp8h_bw* p0, const vp8h_bw* part1, uint8_t** out,
-                       int* err) {
+size_t vp8h_write_riff(const vp8h_frame* fr, vp8h_bw* p0, const vp8h_bw* part1,
+                       const vp8h_alpha* alpha, uint8_t** out, int* err) {
+  /* VP8EncWrite + PutWebPHeaders (syntax_enc.c:149-185, 320-392): RIFF,
+   * [VP8X + ALPH when the picture has alpha], 'VP8 ', frame header,
+   * partition 0, partition 1, pad byte */
   vp8h_bw bw = *p0;
   memset(p0, 0, sizeof(*p0));
   if (part1->error) {
@@ -553,7 +556,9 @@ size_t vp8h_write_riff(const vp8h_frame* fr, vp8h_bw* p0, const vp8h_bw* part1, 
   size_t vp8_size = 10 + size0 + size1;
   const size_t pad = vp8_size & 1;
   vp8_size += pad;
-  const size_t riff_size = 4 + 8 + vp8_size;
+  size_t riff_size = 4 + 8 + vp8_size;
+  const size_t asize = alpha ? 1 + alpha->size : 0;   /* header byte + data */
+  if (alpha) riff_size += 8 + 10 + 8 + asize + (asize & 1);   /* VP8X + ALPH chunks */
   if (riff_size > 0xfffffffeU) {
     vp8h_bw_free(&bw);
     *err = VP8_ENC_ERROR_FILE_TOO_BIG;
@@ -568,17 +573,35 @@ size_t vp8h_write_riff(const vp8h_frame* fr, vp8h_bw* p0, const vp8h_bw* part1, 
   }
   memcpy(o, "RIFF", 4);
   put_le32(o + 4, (uint32_t)riff_size);
-  memcpy(o + 8, "WEBPVP8 ", 8);
-  put_le32(o + 16, (uint32_t)vp8_size);
+  memcpy(o + 8, "WEBP", 4);
+  uint8_t* q = o + 12;
+  if (alpha) {
+    memcpy(q, "VP8X", 4);
+    put_le32(q + 4, 10);
+    put_le32(q + 8, 0x10);   /* ALPHA_FLAG */
+    q[12] = (uint8_t)(fr->w - 1); q[13] = (uint8_t)((fr->w - 1) >> 8);
+    q[14] = (uint8_t)((fr->w - 1) >> 16);
+    q[15] = (uint8_t)(fr->h - 1); q[16] = (uint8_t)((fr->h - 1) >> 8);
+    q[17] = (uint8_t)((fr->h - 1) >> 16);
+    q += 18;
+    memcpy(q, "ALPH", 4);
+    put_le32(q + 4, (uint32_t)asize);
+    q[8] = alpha->header;
+    if (alpha->size) memcpy(q + 9, alpha->data, alpha->size);
+    q += 8 + asize;
+    if (asize & 1) *q++ = 0;
+  }
+  memcpy(q, "VP8 ", 4);
+  put_le32(q + 4, (uint32_t)vp8_size);
   const uint32_t bits = (uint32_t)(fr->profile << 1) | (1u << 4) | ((uint32_t)size0 << 5);
-  uint8_t* fh = o + 20;
+  uint8_t* fh = q + 8;
   fh[0] = (uint8_t)bits; fh[1] = (uint8_t)(bits >> 8); fh[2] = (uint8_t)(bits >> 16);
   fh[3] = 0x9d; fh[4] = 0x01; fh[5] = 0x2a;   /* VP8 keyframe signature */
   fh[6] = (uint8_t)(fr->w & 0xff); fh[7] = (uint8_t)(fr->w >> 8);
   fh[8] = (uint8_t)(fr->h & 0xff); fh[9] = (uint8_t)(fr->h >> 8);
-  memcpy(o + 30, bw.buf, size0);
-  if (size1) memcpy(o + 30 + size0, part1->buf, size1);
-  if (pad) o[30 + size0 + size1] = 0;
+  memcpy(fh + 10, bw.buf, size0);
+  if (size1) memcpy(fh + 10 + size0, part1->buf, size1);
+  if (pad) fh[10 + size0 + size1] = 0;
   vp8h_bw_free(&bw);
   *out = o;
   *err = VP8_ENC_OK;
@@ -593,5 +616,5 @@ size_t vp8h_assemble(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t
     vp8h_bw_free(&p0);
     return 0;
   }
-  return vp8h_write_riff(fr, &p0, part1, out, err);
+  return vp8h_write_riff(fr, &p0, part1, NULL, out, err);
 }

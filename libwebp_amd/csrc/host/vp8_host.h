@@ -77,8 +77,15 @@ void vp8h_emit_tokens(vp8h_bw* bw, const uint16_t* tokens, size_t n, const uint8
  * coded while K4 codes partition 1; the RIFF write joins them. */
 int vp8h_build_p0(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* mbinfo,
                   vp8h_bw* p0, int* hdr_bytes);
-size_t vp8h_write_riff(const vp8h_frame* fr, vp8h_bw* p0, const vp8h_bw* part1, uint8_t** out,
-                       int* err);
+/* ALPH chunk payload: header byte (compression | filter << 2 | levels << 4,
+ * alpha_enc.c:168-170) and the data (bare VP8L stream or raw plane) */
+typedef struct {
+  uint8_t header;
+  const uint8_t* data;
+  size_t size;
+} vp8h_alpha;
+size_t vp8h_write_riff(const vp8h_frame* fr, vp8h_bw* p0, const vp8h_bw* part1,
+                       const vp8h_alpha* alpha, uint8_t** out, int* err);
 size_t vp8h_assemble(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* mbinfo,
                      vp8h_bw* part1, uint8_t** out, int* err, int* hdr_bytes);
 

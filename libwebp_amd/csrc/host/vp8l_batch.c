@@ -47,13 +47,15 @@ void vp8l_engine_free(vp8l_engine* l) {
   hipHostFree(l->h_start); hipHostFree(l->h_end); hipHostFree(l->h_hdr); hipHostFree(l->h_out);
   hipHostFree(l->h_poff); hipHostFree(l->h_hpack); hipHostFree(l->h_hoff); hipHostFree(l->h_hwords);
   free(l->hdr_bytes); free(l->out_off); free(l->out_size); free(l->err);
+  for (int i = 0; i < 5; ++i)
+    if (l->ev[i]) hipEventDestroy(l->ev[i]);
   free(l);
 }
 
-vp8l_engine* vp8l_engine_new(int w, int h, int max_frames, int method) {
+vp8l_engine* vp8l_engine_new(int w, int h, int max_frames, int method, int alpha) {
   vp8l_engine* l = (vp8l_engine*)calloc(1, sizeof(*l));
   if (!l) return NULL;
-  vp8l_setup_params(&l->p, w, h, max_frames, method);
+  vp8l_setup_params(&l->p, w, h, max_frames, method, alpha);
   l->max_frames = max_frames;
   l->npix = (size_t)w * h;
   l->ntt = sub_sample(w, l->p.tb) * sub_sample(h, l->p.tb);
@@ -62,6 +64,7 @@ vp8l_engine* vp8l_engine_new(int w, int h, int max_frames, int method) {
   l->hdr_cap = ((size_t)16 * l->ntt + (size_t)8 * l->nht + ((size_t)256 << 10) + 255) & ~(size_t)255;
   l->out_cap = (l->npix * 5 + l->hdr_cap + 255) & ~(size_t)255;
   const size_t N = (size_t)max_frames, np = l->npix;
+  for (int i = 0; i < 5; ++i) CHK(hipEventCreate(&l->ev[i]));
   CHK(hipMalloc((void**)&l->d_tabs, (4097 + 1024) * sizeof(int32_t)));
   CHK(hipMemcpy(l->d_tabs, vp8l_nlogn_table(), 4097 * sizeof(int32_t), hipMemcpyHostToDevice));
   CHK(hipMemcpy(l->d_tabs + 4097, vp8l_flog2_table(), 1024 * sizeof(int32_t),
@@ -171,23 +174,30 @@ static void run_headers(vp8l_engine* l, int n, int threads) {
 /* ---- pipeline ---- */
 
 int vp8l_engine_run(struct WebPGpuBatch* b, const uint8_t* rgba, size_t fstride, int rstride, int n) {
-  vp8l_engine* l = b->l;
-  hipStream_t st = b->stream;
+  const int ok = vp8l_engine_encode(b->l, b->stream, b->threads, rgba, fstride, rstride, n,
+                                    b->timings);
+  if (ok) b->last_n = n;
+  return ok;
+}
+
+int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t* rgba,
+                       size_t fstride, int rstride, int n, double timings[10]) {
+  hipStream_t st = (hipStream_t)stream;
   const size_t N = (size_t)n;
   double t0 = now_us(), t1, t2, t3, t4, t5;
   vp8l_params p = l->p;
   p.n = n;
   for (int f = 0; f < n; ++f) l->err[f] = VP8_ENC_OK;
   CHK(hipMemsetAsync(l->d_aflag, 0, N * sizeof(uint32_t), st));
-  CHK(hipEventRecord(b->ev[0], st));
+  CHK(hipEventRecord(l->ev[0], st));
   if (!vp8l_launch_transform(rgba, fstride, rstride, &p, l->d_argb, l->d_modes,
                              l->d_mult, l->d_aflag, st))
     goto fail;
-  CHK(hipEventRecord(b->ev[1], st));
+  CHK(hipEventRecord(l->ev[1], st));
   if (!vp8l_launch_analyze(l->d_argb, &p, l->d_tabs + 4097, l->d_hits, l->d_ops, l->d_feat,
                            l->d_tl, l->d_tn, l->d_hc, l->d_assign, st))
     goto fail;
-  CHK(hipEventRecord(b->ev[2], st));
+  CHK(hipEventRecord(l->ev[2], st));
   CHK(hipMemcpyAsync(l->h_modes, l->d_modes, N * l->ntt, hipMemcpyDeviceToHost, st));
   CHK(hipMemcpyAsync(l->h_mult, l->d_mult, N * l->ntt * sizeof(uint32_t), hipMemcpyDeviceToHost,
                      st));
@@ -199,7 +209,7 @@ int vp8l_engine_run(struct WebPGpuBatch* b, const uint8_t* rgba, size_t fstride,
   CHK(hipMemsetAsync(l->d_out, 0, N * l->out_cap, st));
   CHK(hipStreamSynchronize(st));
   t1 = now_us();
-  run_headers(l, n, b->threads);
+  run_headers(l, n, threads);
   t2 = now_us();
   /* headers back to back (4-byte aligned), one upload, scattered on device */
   l->h_hoff[0] = 0;
@@ -229,11 +239,11 @@ int vp8l_engine_run(struct WebPGpuBatch* b, const uint8_t* rgba, size_t fstride,
                      hipMemcpyHostToDevice, st));
   CHK(hipMemcpyAsync(l->d_gtile, l->h_gtile, N * l->nht, hipMemcpyHostToDevice, st));
   CHK(hipMemcpyAsync(l->d_start, l->h_start, N * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-  CHK(hipEventRecord(b->ev[3], st));
+  CHK(hipEventRecord(l->ev[3], st));
   if (!vp8l_launch_write(l->d_argb, l->d_ops, &p, l->d_ctab, l->d_gtile, l->d_start, l->d_bsum,
                          l->d_boff, l->d_end, l->d_out, l->out_cap, st))
     goto fail;
-  CHK(hipEventRecord(b->ev[4], st));
+  CHK(hipEventRecord(l->ev[4], st));
   CHK(hipMemcpyAsync(l->h_end, l->d_end, N * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   CHK(hipStreamSynchronize(st));
   t3 = now_us();
@@ -244,7 +254,7 @@ int vp8l_engine_run(struct WebPGpuBatch* b, const uint8_t* rgba, size_t fstride,
     if (!l->err[f]) {
       const size_t bytes = (size_t)((l->h_end[f] + 7) >> 3);
       if (bytes > l->out_cap) l->err[f] = VP8_ENC_ERROR_BITSTREAM_OUT_OF_MEMORY;
-      else sz = 20 + bytes + (bytes & 1);
+      else sz = 20 + bytes + (bytes & 1);   /* ALPH mode: the 20-byte slot stays unused */
     }
     l->out_size[f] = sz;
     l->out_off[f + 1] = l->out_off[f] + ((sz + 15) & ~(size_t)15);
@@ -271,26 +281,34 @@ int vp8l_engine_run(struct WebPGpuBatch* b, const uint8_t* rgba, size_t fstride,
     if (!l->out_size[f]) continue;
     uint8_t* o = l->h_out + l->out_off[f];
     const size_t bytes = (size_t)((l->h_end[f] + 7) >> 3);
+    if (l->p.alpha) {   /* bare VP8L stream for an ALPH chunk */
+      l->out_size[f] = bytes;
+      continue;
+    }
     vp8l_riff_header(o, bytes);
     if (bytes & 1) o[20 + bytes] = 0;
   }
   t5 = now_us();
   {
     float k_ms = 0.f, a_ms = 0.f, w_ms = 0.f;
-    CHK(hipEventElapsedTime(&k_ms, b->ev[0], b->ev[1]));
-    CHK(hipEventElapsedTime(&a_ms, b->ev[1], b->ev[2]));
-    CHK(hipEventElapsedTime(&w_ms, b->ev[3], b->ev[4]));
-    b->timings[0] = t1 - t0;   /* transform + analysis kernels + side copies (wall) */
-    b->timings[1] = t2 - t1;   /* host headers */
-    b->timings[2] = t3 - t2;   /* header upload + bit writer (wall) */
-    b->timings[3] = t4 - t3;   /* output copies */
-    b->timings[4] = t5 - t4;   /* RIFF */
-    b->timings[6] = 1e3 * a_ms;   /* cache + parse + tiles + clustering */
-    b->timings[7] = 1e3 * k_ms;   /* transform */
-    b->timings[8] = 1e3 * w_ms;   /* bit writer */
+    CHK(hipEventElapsedTime(&k_ms, l->ev[0], l->ev[1]));
+    CHK(hipEventElapsedTime(&a_ms, l->ev[1], l->ev[2]));
+    CHK(hipEventElapsedTime(&w_ms, l->ev[3], l->ev[4]));
+    timings[0] = t1 - t0;   /* transform + analysis kernels + side copies (wall) */
+    timings[1] = t2 - t1;   /* host headers */
+    timings[2] = t3 - t2;   /* header upload + bit writer (wall) */
+    timings[3] = t4 - t3;   /* output copies */
+    timings[4] = t5 - t4;   /* RIFF */
+    timings[6] = 1e3 * a_ms;   /* cache + parse + tiles + clustering */
+    timings[7] = 1e3 * k_ms;   /* transform */
+    timings[8] = 1e3 * w_ms;   /* bit writer */
   }
-  b->last_n = n;
   return 1;
 fail:
   return 0;
+}
+
+const uint8_t* vp8l_engine_output(const vp8l_engine* l, int f) {
+  if (!l->out_size[f]) return NULL;
+  return l->h_out + l->out_off[f] + (l->p.alpha ? 20 : 0);
 }

@@ -5,11 +5,14 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <hip/hip_runtime_api.h>
+
 #include "../vp8l_gpu.h"
 
 struct WebPGpuBatch;
 
 typedef struct vp8l_engine {
+  hipEvent_t ev[5];            /* stage boundaries of the last call */
   vp8l_params p;               /* n = max_frames; per call a copy with n set */
   int max_frames, ntt, nht, nblk;
   size_t npix, hdr_cap, out_cap;
@@ -67,10 +70,17 @@ typedef struct vp8l_engine {
 #ifdef __cplusplus
 extern "C" {
 #endif
-vp8l_engine* vp8l_engine_new(int w, int h, int max_frames, int method);
+/* alpha != 0: ALPH-chunk engine, input = alpha planes (1 byte per pixel);
+ * outputs are bare VP8L streams at vp8l_engine_output() */
+vp8l_engine* vp8l_engine_new(int w, int h, int max_frames, int method, int alpha);
+const uint8_t* vp8l_engine_output(const vp8l_engine* l, int f);
 void vp8l_engine_free(vp8l_engine* l);
 int vp8l_engine_run(struct WebPGpuBatch* b, const uint8_t* rgba, size_t fstride, int rstride,
                     int n);
+/* one call on `stream` (hipStream_t) with `threads` host threads; stage
+ * times (us) into timings[0..8] as WebPGpuBatchTimings documents */
+int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t* in,
+                       size_t fstride, int rstride, int n, double timings[10]);
 #ifdef __cplusplus
 }
 #endif

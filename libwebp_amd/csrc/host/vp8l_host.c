@@ -103,9 +103,11 @@ static int distance_code(int w, int d) {
   return d + 120;
 }
 
-void vp8l_setup_params(vp8l_params* p, int w, int h, int n, int method) {
+void vp8l_setup_params(vp8l_params* p, int w, int h, int n, int method, int alpha) {
   memset(p, 0, sizeof(*p));
   p->w = w; p->h = h; p->n = n;
+  p->alpha = alpha != 0;
+  p->cache_bits = alpha ? 0 : VP8L_CACHE_BITS;
   p->hb = vp8l_histo_bits(method, w, h);
   p->tb = vp8l_transform_bits(method, p->hb);
   const int nht = sub_sample(w, p->hb) * sub_sample(h, p->hb);
@@ -356,7 +358,7 @@ static const int kAlphSize[5] = {VP8L_GS, 256, 256, 256, 40};
 static uint64_t data_bits(const Code* g, const uint32_t* h) {
   uint64_t b = 0;
   for (int a = 0; a < 5; ++a)
-    for (int s = 0; s < kAlphSize[a]; ++s) b += (uint64_t)h[kAlphOff[a] + s] * g[a].wlen[s];
+    for (int s = 0; s < g[a].n; ++s) b += (uint64_t)h[kAlphOff[a] + s] * g[a].wlen[s];
   return b;
 }
 
@@ -379,12 +381,16 @@ int vp8l_build_header(const vp8l_params* p, int has_alpha, const uint8_t* modes,
   if (!tot || !pix || !groups) { ok = 0; goto done; }
   for (int g = 0; g < ng; ++g)
     for (int i = 0; i < VP8L_NS; ++i) tot[i] += hc[(size_t)used[g] * VP8L_NS + i];
+  /* the green alphabet has no cache symbols without a colour cache */
+  int asize[5];
+  for (int a = 0; a < 5; ++a) asize[a] = kAlphSize[a];
+  if (!p->cache_bits) asize[0] = 256 + 24;
   Code* single = groups + 5 * ng;
-  for (int a = 0; a < 5; ++a) ok &= code_build(&single[a], tot + kAlphOff[a], kAlphSize[a]);
+  for (int a = 0; a < 5; ++a) ok &= code_build(&single[a], tot + kAlphOff[a], asize[a]);
   for (int g = 0; g < ng; ++g)
     for (int a = 0; a < 5; ++a)
       ok &= code_build(&groups[5 * g + a], hc + (size_t)used[g] * VP8L_NS + kAlphOff[a],
-                       kAlphSize[a]);
+                       asize[a]);
   if (!ok) goto done;
   for (int t = 0; t < nht; ++t) pix[t] = (uint32_t)remap[assign[t]] << 8;
   int meta = 0;
@@ -407,13 +413,16 @@ int vp8l_build_header(const vp8l_params* p, int has_alpha, const uint8_t* modes,
     vp8l_bw_free(&tmp);
     meta = cm < cs;
   }
-  /* image header + transforms (subtract green, predictor, cross colour) */
-  vp8l_bw_put(bw, 0x2f, 8);
-  vp8l_bw_put(bw, (uint32_t)(W - 1), 14);
-  vp8l_bw_put(bw, (uint32_t)(H - 1), 14);
-  vp8l_bw_put(bw, has_alpha ? 1 : 0, 1);
-  vp8l_bw_put(bw, 0, 3);
-  vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 2, 2);
+  /* image header + transforms (subtract green, predictor, cross colour);
+   * the ALPH form has neither the image header nor subtract green */
+  if (!p->alpha) {
+    vp8l_bw_put(bw, 0x2f, 8);
+    vp8l_bw_put(bw, (uint32_t)(W - 1), 14);
+    vp8l_bw_put(bw, (uint32_t)(H - 1), 14);
+    vp8l_bw_put(bw, has_alpha ? 1 : 0, 1);
+    vp8l_bw_put(bw, 0, 3);
+    vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 2, 2);
+  }
   vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 0, 2); vp8l_bw_put(bw, (uint32_t)(tb - 2), 3);
   for (int t = 0; t < ntt; ++t) pix[t] = 0xff000000u | ((uint32_t)modes[t] << 8);
   ok &= write_sub_image(bw, pix, ntt);
@@ -421,7 +430,11 @@ int vp8l_build_header(const vp8l_params* p, int has_alpha, const uint8_t* modes,
   for (int t = 0; t < ntt; ++t) pix[t] = 0xff000000u | (mult[t] & 0xffffffu);
   ok &= write_sub_image(bw, pix, ntt);
   vp8l_bw_put(bw, 0, 1);
-  vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, VP8L_CACHE_BITS, 4);
+  if (p->cache_bits) {
+    vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, (uint32_t)p->cache_bits, 4);
+  } else {
+    vp8l_bw_put(bw, 0, 1);
+  }
   if (meta) {
     vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, (uint32_t)(hb - 2), 3);
     for (int t = 0; t < nht; ++t) pix[t] = (uint32_t)remap[assign[t]] << 8;
@@ -434,7 +447,7 @@ int vp8l_build_header(const vp8l_params* p, int has_alpha, const uint8_t* modes,
     const Code* gc = meta ? &groups[5 * g] : single;
     for (int a = 0; a < 5; ++a) {
       code_store(&gc[a], bw);
-      for (int s = 0; s < kAlphSize[a]; ++s)
+      for (int s = 0; s < asize[a]; ++s)
         ctab[(size_t)g * VP8L_NS + kAlphOff[a] + s] =
             (uint32_t)gc[a].codes[s] | ((uint32_t)gc[a].wlen[s] << 16);
     }

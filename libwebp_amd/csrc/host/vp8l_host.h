@@ -28,8 +28,9 @@ size_t vp8l_bw_finish(vp8l_bw* bw);
 /* GetHistoBits / GetTransformBits (src/enc/vp8l_enc.c:234-253), no palette */
 int vp8l_histo_bits(int method, int w, int h);
 int vp8l_transform_bits(int method, int histo_bits);
-/* candidate distances and their codes (model: candidate_distances, distance_code) */
-void vp8l_setup_params(vp8l_params* p, int w, int h, int n, int method);
+/* candidate distances and their codes (model: candidate_distances,
+ * distance_code); alpha != 0: the ALPH-chunk form (model: alpha_plane) */
+void vp8l_setup_params(vp8l_params* p, int w, int h, int n, int method, int alpha);
 
 /* nlogn table (4097 entries, round(n log2 n * 4096)) and the log2 fraction
  * table (1024 entries) uploaded to the device */

@@ -309,7 +309,11 @@ static int import_packed(WebPPicture* pic, const uint8_t* src, int stride, int s
       d[0] = s[ri]; d[1] = s[1]; d[2] = s[bi]; d[3] = with_alpha ? s[3] : 0xff;
     }
   }
-  pic->colorspace = WEBP_YUV420;
+  /* CheckNonOpaque (picture_csp_enc.c:52-66): YUV420A only with alpha */
+  int translucent = 0;
+  if (with_alpha)
+    for (size_t i = 0; i < (size_t)w * h && !translucent; ++i) translucent = rgba[4 * i + 3] != 0xff;
+  pic->colorspace = translucent ? WEBP_YUV420A : WEBP_YUV420;
   int ok = vp8h_pic_alloc_yuva(pic);
   if (ok) {
     pthread_mutex_lock(&g_engine_lock);
@@ -317,16 +321,10 @@ static int import_packed(WebPPicture* pic, const uint8_t* src, int stride, int s
     WebPConfigInitInternal(&cfg, WEBP_PRESET_DEFAULT, 75.f, WEBP_ENCODER_ABI_VERSION);
     WebPGpuBatch* e = engine_for(&cfg, w, h);
     int has_alpha = 0;
-    ok = e != NULL &&
-         vp8g_engine_import(e, rgba, 4 * w, pic->y, pic->u, pic->v, &has_alpha, sharp);
+    ok = e != NULL && vp8g_engine_import(e, rgba, 4 * w, pic->y, pic->u, pic->v,
+                                         translucent ? pic->a : NULL, &has_alpha, sharp);
     pthread_mutex_unlock(&g_engine_lock);
-    if (!ok) {
-      set_error(pic, VP8_ENC_ERROR_OUT_OF_MEMORY);
-    } else if (has_alpha) {
-      /* translucent input needs the alpha-weighted import + ALPH chunk,
-       * which this build does not implement: fail loudly */
-      ok = set_error(pic, VP8_ENC_ERROR_INVALID_CONFIGURATION);
-    }
+    if (!ok) set_error(pic, VP8_ENC_ERROR_OUT_OF_MEMORY);
   }
   free(rgba);
   return ok;
@@ -480,7 +478,8 @@ int WebPEncode(const WebPConfig* config, WebPPicture* pic) {
       return 0;
   }
   if (!config->exact) WebPCleanupTransparentArea(pic);   /* webp_enc.c:369-371 */
-  if (pic->a != NULL && WebPPictureHasTransparency(pic))
+  const int has_alpha = pic->a != NULL && WebPPictureHasTransparency(pic);
+  if (has_alpha && config->alpha_quality < 100)   /* QuantizeLevels not implemented */
     return set_error(pic, VP8_ENC_ERROR_INVALID_CONFIGURATION);
 
   pthread_mutex_lock(&g_engine_lock);
@@ -490,7 +489,8 @@ int WebPEncode(const WebPConfig* config, WebPPicture* pic) {
     pthread_mutex_unlock(&g_engine_lock);
     return set_error(pic, VP8_ENC_ERROR_OUT_OF_MEMORY);
   }
-  ok = vp8g_engine_upload_yuv(e, 0, pic->y, pic->y_stride, pic->u, pic->v, pic->uv_stride) &&
+  ok = vp8g_engine_upload_yuv(e, 0, pic->y, pic->y_stride, pic->u, pic->v, pic->uv_stride,
+                              has_alpha ? pic->a : NULL, pic->a_stride) &&
        report(pic, 20) && vp8g_engine_run_yuv(e, 1);
   int err = ok ? e->err[0] : VP8_ENC_ERROR_OUT_OF_MEMORY;
   uint8_t* out = ok ? e->out[0] : NULL;

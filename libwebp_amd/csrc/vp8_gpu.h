@@ -82,8 +82,15 @@ void vp8g_set_error(const char* where, const char* what);
  * alpha_flags[f] bit 0 if frame f has a non-0xff alpha sample. */
 int vp8g_launch_import(const uint8_t* rgba, size_t frame_stride, int row_stride,
                        int w, int h, int n, uint8_t* yuv, size_t yuv_frame_bytes,
-                       uint32_t* alpha_flags, const uint16_t* g2l_dev,
+                       uint32_t* alpha_flags, uint8_t* alpha_plane, const uint16_t* g2l_dev,
                        const int32_t* l2g_dev, void* stream);
+/* alpha planes (n x w*h, stride w) of RGBA frames (sharp-YUV path) */
+int vp8g_launch_extract_alpha(const uint8_t* rgba, size_t frame_stride, int row_stride, int w,
+                              int h, int n, uint8_t* alpha_plane, void* stream);
+/* WebPCleanupTransparentArea on the YUV planes of the frames whose
+ * alpha_flags are set (config->exact == 0) */
+int vp8g_launch_cleanup_alpha(uint8_t* yuv, size_t yuv_frame_bytes, const uint8_t* alpha_plane,
+                              const uint32_t* alpha_flags, int w, int h, int n, void* stream);
 
 int vp8g_launch_analysis(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h,
                          int n, uint8_t* mb_alpha, uint16_t* mb_uva, void* stream);

@@ -54,6 +54,10 @@ typedef struct {
   int k;                           /* clusters = min(KMAX, nht) */
   int dist[VP8L_NUM_CAND];         /* candidate distances (0 = unused) */
   int dcode[VP8L_NUM_CAND];        /* their distance codes */
+  int alpha;                       /* ALPH mode: input is an alpha plane (1 B/px,
+                                      coded as green), bare stream (no image
+                                      header), no subtract green, no colour cache */
+  int cache_bits;                  /* VP8L_CACHE_BITS, or 0 in ALPH mode */
 } vp8l_params;
 
 /* L1: subtract green + per-tile predictor + cross colour. rgba frames at

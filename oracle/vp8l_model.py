@@ -282,14 +282,17 @@ def choose_cross_color(res, tb, H, W):
     return mult, out
 
 
-def transform_image(rgba, tb):
-    """Subtract green -> predictor (per-tile best of 14 by the bitlen score)
-    -> cross colour. Returns (modes (tiles,), mult (tiles,3), residual ARGB
-    uint32 (H, W))."""
+def transform_image(rgba, tb, subgreen=True):
+    """Subtract green (unless `subgreen` is off) -> predictor (per-tile best
+    of 14 by the bitlen score) -> cross colour. Returns (modes (tiles,), mult
+    (tiles,3), residual ARGB uint32 (H, W))."""
     H, W, _ = rgba.shape
     a = rgba[..., 3].astype(np.int64); r = rgba[..., 0].astype(np.int64)
     g = rgba[..., 1].astype(np.int64); b = rgba[..., 2].astype(np.int64)
-    P = np.stack([a, (r - g) & 255, g, (b - g) & 255], axis=-1)
+    if subgreen:
+        P = np.stack([a, (r - g) & 255, g, (b - g) & 255], axis=-1)
+    else:
+        P = np.stack([a, r, g, b], axis=-1)
     L, T, TL, TR = neighbours(P)
     fixed = fixed_mode_mask(H, W)
     preds = [predict(m, L, T, TL, TR) for m in range(14)]
@@ -753,12 +756,23 @@ def pack_fields(v, b, start_bit):
 DEFAULT_CACHE_BITS = 8
 
 
-def encode(rgba, method=4, cache_bits=DEFAULT_CACHE_BITS, kmax=KMAX, return_parts=False):
-    """rgba: (H, W, 4) uint8 -> .webp bytes (VP8L)."""
+def encode(rgba, method=4, cache_bits=DEFAULT_CACHE_BITS, kmax=KMAX, return_parts=False,
+           alpha_plane=False):
+    """rgba: (H, W, 4) uint8 -> .webp bytes (VP8L).
+
+    alpha_plane=True: the ALPH-chunk form (src/enc/alpha_enc.c:50-98 +
+    src/dec/alpha_dec.c): rgba is the alpha plane (H, W) uint8, coded as the
+    green channel of an image with R = B = A = 0, as a bare VP8L stream (no
+    RIFF, no 5-byte image header, no colour cache), no subtract-green."""
+    if alpha_plane:
+        a = np.asarray(rgba, dtype=np.uint8)
+        rgba = np.zeros(a.shape + (4,), dtype=np.uint8)
+        rgba[..., 1] = a
+        cache_bits = 0
     H, W, _ = rgba.shape
     hb = histo_bits(method, W, H)
     tb = transform_bits(method, hb)
-    modes, mult, argb = transform_image(rgba, tb)
+    modes, mult, argb = transform_image(rgba, tb, subgreen=not alpha_plane)
     act, clen, ccode = parse(argb, cache_bits, candidate_distances(W))
     al = Alphabets(cache_bits)
     S, X = pixel_symbols(argb, act, clen, ccode, cache_bits, al)
@@ -797,10 +811,11 @@ def encode(rgba, method=4, cache_bits=DEFAULT_CACHE_BITS, kmax=KMAX, return_part
         groups = [single]
         assign = np.zeros(nt, dtype=np.int64)
     bw = BitWriter()
-    bw.put(0x2F, 8); bw.put(W - 1, 14); bw.put(H - 1, 14)
-    bw.put(int((rgba[..., 3] != 255).any()), 1); bw.put(0, 3)
-    # SUBTRACT_GREEN, PREDICTOR, CROSS_COLOR (applied in this order)
-    bw.put(1, 1); bw.put(2, 2)
+    if not alpha_plane:
+        bw.put(0x2F, 8); bw.put(W - 1, 14); bw.put(H - 1, 14)
+        bw.put(int((rgba[..., 3] != 255).any()), 1); bw.put(0, 3)
+        # SUBTRACT_GREEN, PREDICTOR, CROSS_COLOR (applied in this order)
+        bw.put(1, 1); bw.put(2, 2)
     bw.put(1, 1); bw.put(0, 2); bw.put(tb - 2, 3)
     write_sub_image(bw, [0xFF000000 | (int(m) << 8) for m in modes])
     bw.put(1, 1); bw.put(1, 2); bw.put(tb - 2, 3)
@@ -830,7 +845,7 @@ def encode(rgba, method=4, cache_bits=DEFAULT_CACHE_BITS, kmax=KMAX, return_part
     hb_bytes = (header_bits + 7) // 8
     buf[:hb_bytes] |= head[:hb_bytes]
     payload = buf[:(end + 7) // 8].tobytes()
-    out = riff(payload)
+    out = payload if alpha_plane else riff(payload)
     if return_parts:
         return out, dict(modes=modes, mult=mult, argb=argb, act=act, clen=clen, ccode=ccode,
                          assign=assign, groups=len(groups), header_bits=header_bits, tb=tb,
@@ -855,3 +870,33 @@ def ref_decode(lib, data):
     out = np.frombuffer(C.string_at(p, w.value * h.value * 4), dtype=np.uint8)
     lib.WebPFree(p)
     return out.reshape(h.value, w.value, 4).copy()
+
+
+# ---------------------------------------------------------------- containers
+
+def riff_chunks(data):
+    """[(fourcc, payload)] of a RIFF/WEBP file."""
+    assert data[:4] == b"RIFF" and data[8:12] == b"WEBP"
+    out, pos = [], 12
+    while pos + 8 <= len(data):
+        tag = data[pos:pos + 4]
+        n = struct.unpack("<I", data[pos + 4:pos + 8])[0]
+        out.append((tag, data[pos + 8:pos + 8 + n]))
+        pos += 8 + n + (n & 1)
+    return out
+
+
+def alph_chunk(alpha_vp8l, filt=0, levels=0):
+    """ALPH payload: header byte (compression 1 = lossless | filter << 2 |
+    pre-processing << 4, src/enc/alpha_enc.c:168-170) + bare VP8L stream."""
+    return bytes([1 | (filt << 2) | (levels << 4)]) + alpha_vp8l
+
+
+def riff_vp8x(w, h, alph, vp8):
+    """RIFF + VP8X (alpha flag) + ALPH + 'VP8 ' (src/enc/syntax_enc.c:50-110,
+    PutWebPHeaders)."""
+    def chunk(tag, p):
+        return tag + struct.pack("<I", len(p)) + p + (b"\0" if len(p) & 1 else b"")
+    vp8x = struct.pack("<I", 0x10) + struct.pack("<I", w - 1)[:3] + struct.pack("<I", h - 1)[:3]
+    body = chunk(b"VP8X", vp8x) + chunk(b"ALPH", alph) + chunk(b"VP8 ", vp8)
+    return b"RIFF" + struct.pack("<I", 4 + len(body)) + b"WEBP" + body

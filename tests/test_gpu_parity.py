@@ -107,10 +107,17 @@ def test_oracle_random_small(gpu):
         enc.close()
 
 
-def test_transparent_input_is_rejected(gpu):
+def test_transparent_input_gets_alph_chunk(gpu):
+    """One translucent pixel: VP8X + ALPH + VP8 (tests/test_alpha.py has the
+    parity checks); alpha_quality < 100 is refused, not approximated."""
     img = syn_v1(32, 32, 0).copy()
     img[5, 5, 3] = 10
     enc = gpu.GpuBatch(32, 32, 1)
+    enc.encode_host(img[None])
+    assert enc.error(0) == 0
+    assert enc.output(0)[12:16] == b"VP8X"
+    enc.close()
+    enc = gpu.GpuBatch(32, 32, 1, alpha_quality=90)
     enc.encode_host(img[None])
     assert enc.error(0) != 0
     enc.close()

@@ -87,7 +87,8 @@ def test_prefix_and_distance_codes():
 
 class Params(C.Structure):
     _fields_ = [("w", C.c_int), ("h", C.c_int), ("n", C.c_int), ("tb", C.c_int),
-                ("hb", C.c_int), ("k", C.c_int), ("dist", C.c_int * 4), ("dcode", C.c_int * 4)]
+                ("hb", C.c_int), ("k", C.c_int), ("dist", C.c_int * 4), ("dcode", C.c_int * 4),
+                ("alpha", C.c_int), ("cache_bits", C.c_int)]
 
 
 class BW(C.Structure):
@@ -111,7 +112,7 @@ def host_lib(tmp_path_factory):
     lib.vp8l_bw_finish.argtypes = [vp]
     lib.vp8l_bw_init.argtypes = [vp, C.c_size_t]
     lib.vp8l_bw_free.argtypes = [vp]
-    lib.vp8l_setup_params.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int]
+    lib.vp8l_setup_params.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
     return lib
 
 
@@ -119,16 +120,27 @@ def vp8l_ns():
     return M.Alphabets(M.DEFAULT_CACHE_BITS).ns
 
 
-@pytest.mark.parametrize("w,h,f,alpha,method", [
-    (64, 48, 0, False, 4), (33, 17, 3, False, 4), (1, 1, 0, False, 4), (256, 192, 2, False, 4),
-    (200, 130, 6, True, 4), (160, 96, 1, False, 6), (97, 61, 2, False, 3)])
-def test_host_header_matches_model(host_lib, w, h, f, alpha, method):
-    img = syn_v1(w, h, f)
+def alpha_plane(w, h, f):
+    """A synthetic alpha plane: ramps, a transparent block and noise."""
+    yy, xx = np.mgrid[0:h, 0:w]
+    a = ((xx * 3 + yy + 17 * f) % 300).clip(0, 255).astype(np.uint8)
+    a[: h // 3, : w // 3] = 0
+    rng = np.random.default_rng(f)
+    a[h // 2:, w // 2:] = rng.integers(0, 256, size=a[h // 2:, w // 2:].shape, dtype=np.uint8)
+    return a
+
+
+@pytest.mark.parametrize("w,h,f,alpha,method,plane", [
+    (64, 48, 0, False, 4, False), (33, 17, 3, False, 4, False), (1, 1, 0, False, 4, False),
+    (256, 192, 2, False, 4, False), (200, 130, 6, True, 4, False), (160, 96, 1, False, 6, False),
+    (97, 61, 2, False, 3, False), (120, 77, 1, False, 4, True), (1, 1, 0, False, 4, True)])
+def test_host_header_matches_model(host_lib, w, h, f, alpha, method, plane):
+    img = alpha_plane(w, h, f) if plane else syn_v1(w, h, f)
     if alpha:
         img = with_alpha(img, f)
-    _, P = M.encode(img, method=method, return_parts=True)
+    _, P = M.encode(img, method=method, return_parts=True, alpha_plane=plane)
     p = Params()
-    host_lib.vp8l_setup_params(C.byref(p), w, h, 1, method)
+    host_lib.vp8l_setup_params(C.byref(p), w, h, 1, method, int(plane))
     assert (p.tb, p.hb, p.k) == (P["tb"], P["hb"], P["k"])
     dists = M.candidate_distances(w)
     assert list(p.dist)[:len(dists)] == dists
@@ -137,7 +149,11 @@ def test_host_header_matches_model(host_lib, w, h, f, alpha, method):
     modes = np.ascontiguousarray(P["modes"], dtype=np.uint8)
     mult = np.ascontiguousarray((P["mult"][:, 0] & 255) | ((P["mult"][:, 1] & 255) << 8) |
                                 ((P["mult"][:, 2] & 255) << 16), dtype=np.uint32)
-    hc = np.ascontiguousarray(P["hc_raw"], dtype=np.uint32)
+    hc = P["hc_raw"]
+    if plane:   # the device keeps the cache-sized green alphabet layout
+        hc = np.concatenate([hc[:, :280], np.zeros((16, ns - hc.shape[1]), hc.dtype), hc[:, 280:]],
+                            axis=1)
+    hc = np.ascontiguousarray(hc, dtype=np.uint32)
     assert hc.shape == (16, ns)
     assign = np.ascontiguousarray(P["assign_raw"], dtype=np.uint8)
     ctab = np.zeros((16, ns), dtype=np.uint32)
@@ -156,7 +172,11 @@ def test_host_header_matches_model(host_lib, w, h, f, alpha, method):
     assert got == P["header"]
     G = P["groups"]
     want = (P["code"] | (P["nb"] << 16)).astype(np.uint32)
-    assert np.array_equal(ctab[:G], want)
+    if plane:   # no cache: the model's green alphabet stops at 280
+        got = np.concatenate([ctab[:G, :280], ctab[:G, M.Alphabets(8).gs:]], axis=1)
+        assert np.array_equal(got, want)
+    else:
+        assert np.array_equal(ctab[:G], want)
     assert np.array_equal(gtile, P["assign"].astype(np.uint8))
 
 

@@ -17,7 +17,9 @@ class Config(C.Structure):
                 ("sns_strength", C.c_int), ("filter_strength", C.c_int),
                 ("filter_sharpness", C.c_int), ("filter_type", C.c_int),
                 ("partition_limit", C.c_int), ("preprocessing", C.c_int),
-                ("emulate_jpeg_size", C.c_int), ("use_sharp_yuv", C.c_int)]
+                ("emulate_jpeg_size", C.c_int), ("use_sharp_yuv", C.c_int),
+                ("pass_", C.c_int), ("target_size", C.c_int), ("target_PSNR", C.c_float),
+                ("qmin", C.c_int), ("qmax", C.c_int)]
 
 
 class MBTrace(C.Structure):
@@ -63,7 +65,7 @@ def config(quality=75.0, method=4, **kw):
     c.quality = quality
     c.method = method
     for k, v in kw.items():
-        setattr(c, k, v)
+        setattr(c, "pass_" if k == "pass" else k, v)
     return c
 
 

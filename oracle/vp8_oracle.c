@@ -1011,8 +1011,11 @@ static void level_costs(Enc* e) {
   e->dirty = 0;
 }
 
-static void finalize_token_probas(Enc* e) {
-  int changed = 0;
+/* FinalizeTokenProbas (frame_enc.c:146-180): a pure function of the
+ * statistics (old_p is the default table, not the previous value); returns
+ * the header cost of the proba updates in 1/256 bits */
+static int finalize_token_probas(Enc* e) {
+  int changed = 0, size = 0;
   for (int t = 0; t < 4; ++t)
     for (int b = 0; b < 8; ++b)
       for (int c = 0; c < 3; ++c)
@@ -1025,14 +1028,18 @@ static void finalize_token_probas(Enc* e) {
           const int old_cost = nb * bit_cost(1, old_p) + (total - nb) * bit_cost(0, old_p) + bit_cost(0, upd);
           const int new_cost = nb * bit_cost(1, new_p) + (total - nb) * bit_cost(0, new_p) +
                                bit_cost(1, upd) + 8 * 256;
-          if (old_cost > new_cost) {
+          const int use_new = old_cost > new_cost;
+          size += bit_cost(use_new, upd);
+          if (use_new) {
             e->coeffs[t][b][c][p] = new_p;
             changed |= (new_p != old_p);
+            size += 8 * 256;
           } else {
             e->coeffs[t][b][c][p] = old_p;
           }
         }
   e->dirty = changed;
+  return size;
 }
 
 static inline int level_cost(const uint16_t* tab, int level) {
@@ -1757,10 +1764,76 @@ static size_t write_stream(Enc* e, BW* part1, uint8_t** out) {
   return total;
 }
 
+
+/* ------------------------------------------------------------------------ */
+/* Multi-pass convergence: frame_enc.c:26-80, 554-556, token_enc.c:226-247 */
+
+#define DQ_LIMIT 0.4
+#define HEADER_SIZE_ESTIMATE (12 + 8 + 10)
+
+typedef struct {
+  int is_first;
+  float dq;
+  float q, last_q;
+  float qmin, qmax;
+  double value, last_value;
+  double target;
+  int do_size_search;
+} PassStats;
+
+static float clampf(float v, float lo, float hi) { return (v < lo) ? lo : (v > hi) ? hi : v; }
+
+static void init_pass_stats(PassStats* s, const vp8o_config* cfg) {
+  const uint64_t target_size = (uint64_t)cfg->target_size;
+  const int do_size_search = (target_size != 0);
+  const float target_PSNR = cfg->target_PSNR;
+  s->is_first = 1;
+  s->dq = 10.f;
+  s->qmin = 1.f * cfg->qmin;
+  s->qmax = 1.f * cfg->qmax;
+  s->q = s->last_q = clampf(cfg->quality, s->qmin, s->qmax);
+  s->target = do_size_search ? (double)target_size : (target_PSNR > 0.) ? target_PSNR : 40.;
+  s->value = s->last_value = 0.;
+  s->do_size_search = do_size_search;
+}
+
+static float compute_next_q(PassStats* s) {
+  float dq;
+  if (s->is_first) {
+    dq = (s->value > s->target) ? -s->dq : s->dq;
+    s->is_first = 0;
+  } else if (s->value != s->last_value) {
+    const double slope = (s->target - s->value) / (s->last_value - s->value);
+    dq = (float)(slope * (s->last_q - s->q));
+  } else {
+    dq = 0.;
+  }
+  s->dq = clampf(dq, -30.f, 30.f);
+  s->last_q = s->q;
+  s->last_value = s->value;
+  s->q = clampf(s->q + s->dq, s->qmin, s->qmax);
+  return s->q;
+}
+
+static double psnr_of(uint64_t mse, uint64_t size) {
+  return (mse > 0 && size > 0) ? 10. * log10(255. * 255. * size / mse) : 99;
+}
+
+static uint64_t estimate_token_size(const Enc* e) {
+  uint64_t size = 0;
+  for (size_t k = 0; k < e->ntok; ++k) {
+    const uint16_t t = e->tok[k];
+    const int bit = (t >> 15) & 1;
+    size += bit_cost(bit, (t & (1u << 14)) ? (t & 0xffu) : ((const uint8_t*)e->coeffs)[t & 0x3fffu]);
+  }
+  return size;
+}
+
 void vp8o_default_config(vp8o_config* c) {   /* config_enc.c:24-98 */
   memset(c, 0, sizeof(*c));
   c->quality = 75.f; c->method = 4; c->segments = 4; c->sns_strength = 50;
   c->filter_strength = 60; c->filter_sharpness = 0; c->filter_type = 1;
+  c->pass = 1; c->qmin = 0; c->qmax = 100;
 }
 
 size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
@@ -1800,22 +1873,31 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
 
   analyze(e);
 
-  /* VP8EncTokenLoop with pass = 1 (and the partition-0 overflow retry) */
+  /* VP8EncTokenLoop (frame_enc.c:783-894): `pass` entropy passes, the
+   * size / PSNR search of InitPassStats / ComputeNextQ (:47-80) and the
+   * partition-0 overflow retry (:869-876) */
   g_passes = 0;
   const int max_count = (nmb >> 3) < 96 ? 96 : (nmb >> 3);
   BW part1;
   bw_init(&part1);
   It it;
-  for (;;) {
-    uint64_t size_p0 = 0;
+  PassStats ps;
+  init_pass_stats(&ps, cfg);
+  const int do_search = cfg->target_size > 0 || cfg->target_PSNR > 0;
+  const uint64_t pixel_count = (uint64_t)nmb * 384;
+  int num_pass_left = cfg->pass < 1 ? 1 : cfg->pass;
+  while (num_pass_left-- > 0) {
+    const int is_last_pass = (fabs(ps.dq) <= DQ_LIMIT) || (num_pass_left == 0) ||
+                             (e->max_i4_header_bits == 0);
+    uint64_t size_p0 = 0, distortion = 0;
     int cnt = max_count;
     it_reset(&it, e);
-    float q = cfg->quality;
-    q = q < 0.f ? 0.f : q > 100.f ? 100.f : q;
+    /* SetLoopParams (:563-572) */
+    const float q = ps.q < 0.f ? 0.f : ps.q > 100.f ? 100.f : ps.q;
     set_segment_params(e, q);
     set_segment_probas(e);
     level_costs(e);
-    memset(e->stats, 0, sizeof(e->stats));
+    if (is_last_pass) memset(e->stats, 0, sizeof(e->stats));
     e->ntok = 0;
     do {
       Score rd;
@@ -1828,7 +1910,8 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
       decimate(&it, e, &rd);
       record_tokens(&it, e, &rd);
       size_p0 += rd.H;
-      if (trace) {
+      distortion += rd.D;
+      if (trace && is_last_pass) {
         vp8o_mb_trace* t = &trace[it.y * e->mbw + it.x];
         const int mi = it.y * e->mbw + it.x;
         t->segment = e->mb_seg[mi]; t->type = e->mb_type[mi];
@@ -1844,11 +1927,23 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
     size_p0 += e->seg_hdr_size;
     ++g_passes;
     g_size_p0 = size_p0;
+    if (e->tok_err) break;
+    if (ps.do_size_search) {
+      uint64_t size = (uint64_t)finalize_token_probas(e);
+      size += estimate_token_size(e);
+      size = (size + size_p0 + 1024) >> 11;
+      size += HEADER_SIZE_ESTIMATE;
+      ps.value = (double)size;
+    } else {
+      ps.value = psnr_of(distortion, pixel_count);
+    }
     if (e->max_i4_header_bits > 0 && size_p0 > P0_LIMIT) {
+      ++num_pass_left;
       e->max_i4_header_bits >>= 1;
       continue;
     }
-    break;
+    if (is_last_pass) break;
+    if (do_search) compute_next_q(&ps);
   }
   if (e->tok_err) goto done;
   finalize_token_probas(e);

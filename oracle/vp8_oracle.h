@@ -25,6 +25,10 @@ typedef struct {
   int preprocessing;      /* bit0: segment smoothing */
   int emulate_jpeg_size;  /* 0/1 */
   int use_sharp_yuv;      /* 0/1: iterative RGB->YUV (sharp_oracle.c) */
+  int pass;               /* 1..10 entropy passes */
+  int target_size;        /* bytes, 0 = off */
+  float target_PSNR;      /* dB, 0 = off */
+  int qmin, qmax;         /* 0..100 */
 } vp8o_config;
 
 /* per-macroblock decisions, for stage-by-stage comparison with the GPU */

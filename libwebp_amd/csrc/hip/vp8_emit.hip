@@ -440,3 +440,53 @@ extern "C" int vp8g_launch_pack(const uint16_t* tokens, size_t tok_cap, int n,
                      size, dst);
   return vp8g_launch_check("k_pack");
 }
+
+// VP8EstimateTokenSize (token_enc.c:226-247) between the passes of a size
+// search: sum of VP8BitCost(bit, p) over a frame's compact token stream, p the
+// fixed probability of the token or the frame's probability table entry.
+// Grid (chunks, n); probability and entropy tables staged in LDS; one
+// 64-bit atomic per workgroup.
+__global__ __launch_bounds__(256) void k_token_cost(const uint16_t* __restrict__ tokens,
+                                                    size_t tok_cap,
+                                                    const vp8g_frame_result* __restrict__ res,
+                                                    const uint8_t* __restrict__ state,
+                                                    const uint8_t* __restrict__ active,
+                                                    unsigned long long* __restrict__ bits) {
+  const int f = blockIdx.y;
+  if (!active[f] || res[f].error) return;
+  __shared__ uint8_t prob[VP8G_NUM_SLOTS];
+  __shared__ uint16_t ecost[256];
+  __shared__ unsigned long long wsum[4];
+  const uint8_t* coeffs = state + (size_t)f * VP8G_RERUN_STATE_BYTES + VP8G_STATE_COEFFS;
+  for (int s = threadIdx.x; s < VP8G_NUM_SLOTS; s += 256) prob[s] = coeffs[s];
+  ecost[threadIdx.x] = kVP8EntropyCost[threadIdx.x];
+  __syncthreads();
+  const uint32_t nt = res[f].ntokens;
+  const uint16_t* t = tokens + (size_t)f * tok_cap;
+  uint32_t acc = 0;   // < 2^32: a chunk of the grid stride holds few tokens per thread
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nt; i += gridDim.x * 256) {
+    const uint32_t tk = t[i];
+    const int p = (tk & 0x4000u) ? (int)(tk & 0xffu) : (int)prob[tk & 0x3fffu];
+    acc += (tk & 0x8000u) ? ecost[255 - p] : ecost[p];
+  }
+  unsigned long long v = acc;
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(&bits[f], wsum[0] + wsum[1] + wsum[2] + wsum[3]);
+}
+
+extern "C" int vp8g_launch_token_cost(const uint16_t* tokens, size_t tok_cap, int n,
+                                      const vp8g_frame_result* results, const uint8_t* state,
+                                      const uint8_t* active, unsigned long long* bits,
+                                      void* stream) {
+  if (n <= 0) return 1;
+  if (hipMemsetAsync(bits, 0, (size_t)n * sizeof(*bits), (hipStream_t)stream) != hipSuccess)
+    return vp8g_launch_check("k_token_cost memset");
+  // 128 chunks per frame: 7.6 M tokens at 1080p -> ~230 per thread, and
+  // each token costs < 2^12, so the 32-bit per-thread sum cannot wrap below
+  // 2^20 tokens per thread (2.7e10 tokens per frame)
+  hipLaunchKernelGGL(k_token_cost, dim3(128, n), dim3(256), 0, (hipStream_t)stream, tokens,
+                     tok_cap, results, state, active, bits);
+  return vp8g_launch_check("k_token_cost");
+}

@@ -39,7 +39,7 @@ struct alignas(16) K3G {
   vp8g_seg seg[4];
   int32_t max_edge[4];
   struct {
-    unsigned long long size_p0, sse[3];
+    unsigned long long size_p0, sse[3], dist;
     int32_t nb[3];
   } fs;                            // per-frame side statistics (frame_enc.c:480-489, :839)
   int32_t dirty;                   // FinalizeTokenProbas result
@@ -89,6 +89,8 @@ struct K3S {
   uint32_t bar;                    // worker barrier counter
   int32_t myabort;
   int32_t flag_ldc;                // left DC nz flag hand-off from wave 0
+  int32_t mdist;                   // VP8ModeScore D of the MB (thread 0 only)
+  int32_t d4acc;                   // intra4 D of the blocks chosen so far (thread 0 only)
   uint32_t mark_any;
   uint8_t yl_mem[17], ul_mem[9], vl_mem[9];
   uint8_t predleft[4];
@@ -687,7 +689,7 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
   int total_hdr = 0;
   I4Result res;
   res.ok = 1;
-  if (tid == 0) L.best4[0] = ~0ull;
+  if (tid == 0) { L.best4[0] = ~0ull; L.d4acc = 0; }
   WB();
   for (int i4 = 0; i4 < 16; ++i4) {
     const int bx = i4 & 3, by = i4 >> 2;
@@ -761,6 +763,7 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
         L.sm4[m] = (score_t)(R0 + Rc + H) * S.lambda_mode + dist;
         L.r4[m][0] = H;
         L.r4[m][1] = nzb;
+        L.r4[m][3] = D;
       }
     }
     SUBST(5);
@@ -768,7 +771,7 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
     int bm;
     if (search) {
       bm = (int)(L.best4[i4 & 1] & 15);   // argmin, ties to the lower mode
-      if (tid == 0) L.best4[(i4 + 1) & 1] = ~0ull;
+      if (tid == 0) { L.best4[(i4 + 1) & 1] = ~0ull; L.d4acc += L.r4[bm][3]; }
       const int H = L.r4[bm][0], bnzv = L.r4[bm][1];
       accH += H;
       acc_score += L.sm4[bm];
@@ -1190,12 +1193,14 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   // partition-0 re-run (frame_enc.c:869-876): only the frames that overflowed
   // run again, from the cost state their previous pass ended with
   if (P->pass_mode == 2) return;
-  const bool rerun = P->pass_mode == 1;
+  const bool rerun = P->pass_mode == 1 || P->pass_mode == 3;
   uint8_t* rstate = a.rerun + (size_t)f * VP8G_RERUN_STATE_BYTES;
+  uint32_t* rstats = reinterpret_cast<uint32_t*>(rstate + VP8G_STATE_STATS);
 
-  // ---- frame init (whole workgroup)
+  // ---- frame init (whole workgroup); a non-last pass (mode 3) keeps the
+  // token statistics of the passes before it (frame_enc.c:820-823)
   for (int s = gt; s < NSLOT; s += NW * K3T) {
-    G.stats[s] = 0;
+    G.stats[s] = P->pass_mode == 3 ? rstats[s] : 0u;
     G.coeffs[s] = rerun ? rstate[s] : (&kVP8CoeffProba0[0][0][0][0])[s];
   }
   for (int s = tid; s < NSLOT; s += K3T) L.rdelta[s] = 0;
@@ -1216,7 +1221,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   for (int k = gt; k < mbh; k += NW * K3T) rowdone[k] = 0;
   if (gt < 4) G.max_edge[gt] = 0;
   if (gt == 0) {
-    G.fs.size_p0 = 0; G.fs.sse[0] = G.fs.sse[1] = G.fs.sse[2] = 0;
+    G.fs.size_p0 = 0; G.fs.sse[0] = G.fs.sse[1] = G.fs.sse[2] = 0; G.fs.dist = 0;
     G.fs.nb[0] = G.fs.nb[1] = G.fs.nb[2] = 0;
     G.fold_ptr = 0; G.ntok = 0; G.tok_err = 0; G.epoch = 0; G.abort = 0;
   }
@@ -1372,6 +1377,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
       score_t rdH = H16;
       uint32_t rd_nz = nz16;
       int is_i16 = 1;
+      if (tid < 64) L.mdist = (int32_t)D16;   // whole wave 0: a lone-lane store here spills
       if ((rd_nz & 0x100ffff) == 0x1000000 && D16 > S.min_disto) {   // StoreMaxDelta
         int mv = iabs_(L.lvdc[best16][1]);
         mv = max(mv, iabs_(L.lvdc[best16][2]));
@@ -1395,6 +1401,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
         }
         if (r4.ok) {
           is_i16 = 0;
+          if (tid == 0) L.mdist = L.d4acc;
           rdH = r4.H;
           rd_score = r4.score;
           rd_nz = r4.nz;
@@ -1421,6 +1428,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
         }
         rdH += bH;
         rd_score += bsc;
+        if (tid == 0) L.mdist += L.mres[bu][0];
         rd_nz |= (uint32_t)L.mres[bu][3] << 16;
         if (tid < 128) {
           L.yout[(tid >> 4) * BPS + 16 + (tid & 15)] = L.recuv[bu][tid];
@@ -1477,6 +1485,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
         atomicAdd(&G.fs.nb[is_i16 ? 1 : 0], 1);
         if (skip) atomicAdd(&G.fs.nb[2], 1);
         atomicAdd(&G.fs.size_p0, (unsigned long long)rdH);
+        atomicAdd(&G.fs.dist, (unsigned long long)L.mdist);
       }
       if (tid < 16) mbinfo[(size_t)mb * VP8G_MBINFO_BYTES + 4 + tid] = L.modes[tid];
       if (w0) {   // SSE for WebPAuxStats (frame_enc.c:480-489)
@@ -1648,7 +1657,10 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   if (!G.abort && !G.tok_err) compact_tokens(G, tok_base, mboff, nmb);
   __syncthreads();
   if (wk == 0) {
-    for (int s = tid; s < NSLOT; s += K3T) rstate[NSLOT + s] = G.coeffs[s];
+    for (int s = tid; s < NSLOT; s += K3T) {
+      rstate[NSLOT + s] = G.coeffs[s];
+      rstats[s] = G.stats[s];
+    }
     finalize_probas_wg(G, L, tid);
     vp8g_frame_result* R = a.results + f;
     for (int s = tid; s < NSLOT; s += K3T) R->probas[s] = G.coeffs[s];
@@ -1658,6 +1670,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
       for (int s = 0; s < 4; ++s) R->max_edge[s] = G.max_edge[s];
       R->size_p0 = G.fs.size_p0;
       R->sse[0] = G.fs.sse[0]; R->sse[1] = G.fs.sse[1]; R->sse[2] = G.fs.sse[2];
+      R->distortion = G.fs.dist;
       R->block_count[0] = G.fs.nb[0]; R->block_count[1] = G.fs.nb[1];
       R->block_count[2] = G.fs.nb[2];
 #if defined(K3_STAMPS)

@@ -741,7 +741,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
   // this single-wavefront diagnostic kernel keeps no re-run state: it skips
   // final frames and refuses a partition-0 re-run (error 3)
   if (P->pass_mode != 0) {
-    if (P->pass_mode == 1 && lane == 0) a.results[f].error = 3;
+    if ((P->pass_mode == 1 || P->pass_mode == 3) && lane == 0) a.results[f].error = 3;
     return;
   }
 

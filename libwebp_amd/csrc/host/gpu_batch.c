@@ -154,8 +154,10 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   b->err = (int*)calloc(N, sizeof(int));
   b->hdr = (int*)calloc(2 * N, sizeof(int));
   b->araw = (uint8_t**)calloc(N, sizeof(uint8_t*));
+  b->fin_cost = (int*)calloc(N, sizeof(int));
+  b->pass_act = (uint8_t*)calloc(N, 1);
   if (!b->frames || !b->tok_off || !b->p0 || !b->out || !b->out_size || !b->err || !b->hdr ||
-      !b->araw)
+      !b->araw || !b->fin_cost || !b->pass_act)
     goto fail;
   return b;
 fail:
@@ -174,6 +176,8 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs); hipFree(b->d_nbuf);
   hipFree(b->d_eimg);
   hipFree(b->d_stabs); hipFree(b->d_sharp); hipFree(b->d_sstate);
+  hipFree(b->d_active); hipFree(b->d_tbits);
+  hipHostFree(b->h_state); hipHostFree(b->h_active); hipHostFree(b->h_tbits);
   hipHostFree(b->h_aflags); hipHostFree(b->h_alpha); hipHostFree(b->h_uva);
   hipHostFree(b->h_segmap); hipHostFree(b->h_params); hipHostFree(b->h_mbinfo);
   hipHostFree(b->h_results); hipHostFree(b->h_tokens); hipHostFree(b->h_psize);
@@ -184,6 +188,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   if (b->araw)
     for (int i = 0; i < b->max_frames; ++i) free(b->araw[i]);
   free(b->araw);
+  free(b->fin_cost); free(b->pass_act);
   for (int i = 0; i < 6; ++i)
     if (b->ev[i]) hipEventDestroy(b->ev[i]);
   if (b->stream) hipStreamDestroy(b->stream);
@@ -323,6 +328,108 @@ static int encode_alpha(WebPGpuBatch* b, int n) {
   return 1;
 }
 
+/* VP8EncTokenLoop's pass loop (frame_enc.c:808-880) for every frame of the
+ * batch in lock step. Each round sets the loop parameters of each unfinished
+ * frame for its pass (SetLoopParams with the frame's current q) and runs K3
+ * over the batch (finished frames skip it, pass_mode 2). A size search
+ * (target_size) then finalises the probabilities from each frame's token
+ * statistics on the host and estimates the token bits on the device
+ * (k_token_cost); each frame decides on its own whether another pass follows
+ * (search step, or the partition-0 overflow retry of :869-876). */
+static int run_passes(WebPGpuBatch* b, int n) {
+  const size_t nmb = (size_t)b->nmb;
+  hipStream_t st = b->stream;
+  int* fin_cost = b->fin_cost;
+  uint8_t* act = b->pass_act;
+  for (int f = 0; f < n; ++f) act[f] = b->err[f] == VP8_ENC_OK && vp8h_pass_start(&b->frames[f]);
+  int round = 0;
+  for (;;) {
+    int nact = 0, nsize = 0;
+    for (int f = 0; f < n; ++f) {
+      vp8g_frame_params* P = &b->h_params[f];
+      if (!act[f]) { P->pass_mode = 2; continue; }
+      vp8h_frame* fr = &b->frames[f];
+      vp8h_set_loop_params(fr, fr->ps_q, b->h_segmap + f * nmb, P);
+      P->pass_mode = fr->npass == 0 ? 0 : fr->is_last_pass ? 1 : 3;
+      ++fr->npass;
+      ++nact;
+      nsize += fr->do_size_search && !fr->is_last_pass;
+    }
+    if (!nact) break;
+    CHK(hipMemcpyAsync(b->d_segmap, b->h_segmap, n * nmb, hipMemcpyHostToDevice, st));
+    CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
+                       hipMemcpyHostToDevice, st));
+    if (round == 0) CHK(hipEventRecord(b->ev[2], st));
+    if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params,
+                            b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5,
+                            b->d_results, b->d_rerun, st))
+      return 0;
+    CHK(hipEventRecord(b->ev[3], st));
+    CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
+                       hipMemcpyDeviceToHost, st));
+    if (nsize) {
+      if (!b->h_state) {
+        CHK(hipHostMalloc((void**)&b->h_state, (size_t)b->max_frames * VP8G_RERUN_STATE_BYTES, 0));
+        CHK(hipHostMalloc((void**)&b->h_active, b->max_frames, 0));
+        CHK(hipHostMalloc((void**)&b->h_tbits, b->max_frames * sizeof(unsigned long long), 0));
+        CHK(hipMalloc((void**)&b->d_active, b->max_frames));
+        CHK(hipMalloc((void**)&b->d_tbits, b->max_frames * sizeof(unsigned long long)));
+      }
+      CHK(hipMemcpyAsync(b->h_state, b->d_rerun, (size_t)n * VP8G_RERUN_STATE_BYTES,
+                         hipMemcpyDeviceToHost, st));
+    }
+    CHK(hipStreamSynchronize(st));
+    if (nsize) {   /* FinalizeTokenProbas, then VP8EstimateTokenSize on the device */
+      for (int f = 0; f < n; ++f) {
+        vp8h_frame* fr = &b->frames[f];
+        b->h_active[f] = act[f] && fr->do_size_search && !fr->is_last_pass &&
+                         !b->h_results[f].error;
+        if (!b->h_active[f]) continue;
+        uint8_t* S = b->h_state + (size_t)f * VP8G_RERUN_STATE_BYTES;
+        int dirty = 0;
+        fin_cost[f] = vp8h_finalize_probas((const uint32_t*)(S + VP8G_STATE_STATS),
+                                           S + VP8G_STATE_COEFFS, &dirty);
+        /* VP8CalculateLevelCosts at the next pass start recomputes the level
+         * costs only when the update left a non-default probability */
+        if (dirty) memcpy(S, S + VP8G_STATE_COEFFS, VP8G_NUM_SLOTS);
+      }
+      CHK(hipMemcpyAsync(b->d_rerun, b->h_state, (size_t)n * VP8G_RERUN_STATE_BYTES,
+                         hipMemcpyHostToDevice, st));
+      CHK(hipMemcpyAsync(b->d_active, b->h_active, n, hipMemcpyHostToDevice, st));
+      if (!vp8g_launch_token_cost(b->d_tokens, b->tok_cap, n, b->d_results, b->d_rerun,
+                                  b->d_active, b->d_tbits, st))
+        return 0;
+      CHK(hipMemcpyAsync(b->h_tbits, b->d_tbits, n * sizeof(unsigned long long),
+                         hipMemcpyDeviceToHost, st));
+      CHK(hipStreamSynchronize(st));
+    }
+    for (int f = 0; f < n; ++f) {
+      if (!act[f]) continue;
+      vp8h_frame* fr = &b->frames[f];
+      const vp8g_frame_result* R = &b->h_results[f];
+      if (R->error) { act[f] = 0; continue; }
+      const uint64_t size_p0 = R->size_p0 + (uint64_t)fr->seg_hdr_size;
+      if (fr->do_size_search)
+        fr->ps_value = fr->is_last_pass ? 0.
+                     : vp8h_pass_size_value((uint64_t)fin_cost[f], b->h_tbits[f], size_p0);
+      else
+        fr->ps_value = vp8h_psnr(R->distortion, (uint64_t)nmb * 384);
+      act[f] = vp8h_pass_finish(fr, size_p0) && vp8h_pass_start(fr);
+    }
+    ++round;
+  }
+  if (round == 0) {   /* no frame to encode: keep the K3 timing events valid */
+    CHK(hipEventRecord(b->ev[2], st));
+    CHK(hipEventRecord(b->ev[3], st));
+  }
+  CHK(hipMemcpyAsync(b->h_mbinfo, b->d_mbinfo, n * nmb * VP8G_MBINFO_BYTES,
+                     hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  return 1;
+fail:
+  return 0;
+}
+
 int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   const size_t nmb = (size_t)b->nmb;
   double t0 = now_us(), t1, t2, t3, t4;
@@ -342,58 +449,11 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   for (int f = 0; f < n; ++f) {
     if (b->err[f] != VP8_ENC_OK) continue;
     vp8h_frame_init(&b->frames[f], &b->cfg, b->w, b->h);
-    vp8h_setup_segments(&b->frames[f], b->h_alpha + f * nmb, b->h_uva + f * nmb,
-                        b->h_segmap + f * nmb, &b->h_params[f]);
-    b->h_params[f].pass_mode = 0;
+    vp8h_analyze_segments(&b->frames[f], b->h_alpha + f * nmb, b->h_uva + f * nmb,
+                          b->h_segmap + f * nmb);
   }
-  CHK(hipMemcpyAsync(b->d_segmap, b->h_segmap, n * nmb, hipMemcpyHostToDevice, st));
-  CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
-                     hipMemcpyHostToDevice, st));
   t2 = now_us();
-  CHK(hipEventRecord(b->ev[2], st));
-  if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
-                          b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5, b->d_results,
-                          b->d_rerun, st))
-    return 0;
-  CHK(hipEventRecord(b->ev[3], st));
-  CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
-                     hipMemcpyDeviceToHost, st));
-  CHK(hipMemcpyAsync(b->h_mbinfo, b->d_mbinfo, n * nmb * VP8G_MBINFO_BYTES,
-                     hipMemcpyDeviceToHost, st));
-  CHK(hipStreamSynchronize(st));
-  /* partition-0 overflow (frame_enc.c:869-876): the frames whose header
-   * estimate exceeds the limit encode again with half the I4 header budget,
-   * starting from the cost state their previous pass ended with (K3
-   * pass_mode 1); the others are skipped (pass_mode 2). Until none overflows
-   * or the budget reaches 0. */
-  for (;;) {
-    int reruns = 0;
-    for (int f = 0; f < n; ++f) {
-      vp8h_frame* fr = &b->frames[f];
-      vp8g_frame_params* P = &b->h_params[f];
-      P->pass_mode = 2;
-      if (b->err[f] != VP8_ENC_OK || b->h_results[f].error) continue;
-      if (fr->max_i4_header_bits > 0 &&
-          b->h_results[f].size_p0 + (uint64_t)fr->seg_hdr_size > VP8H_P0_LIMIT) {
-        fr->max_i4_header_bits >>= 1;
-        P->max_i4_header_bits = fr->max_i4_header_bits;
-        P->pass_mode = 1;
-        ++reruns;
-      }
-    }
-    if (!reruns) break;
-    CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
-                       hipMemcpyHostToDevice, st));
-    if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params,
-                            b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5,
-                            b->d_results, b->d_rerun, st))
-      return 0;
-    CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
-                       hipMemcpyDeviceToHost, st));
-    CHK(hipMemcpyAsync(b->h_mbinfo, b->d_mbinfo, n * nmb * VP8G_MBINFO_BYTES,
-                       hipMemcpyDeviceToHost, st));
-    CHK(hipStreamSynchronize(st));
-  }
+  if (!run_passes(b, n)) return 0;
   if (!b->host_emit) {   /* K4 on the device, sized from the token counts */
     uint32_t max_ntok = 0, max_seg = 0;
     size_t segs = 0, words = 0;

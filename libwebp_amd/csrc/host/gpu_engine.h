@@ -9,9 +9,6 @@
 #include "vp8l_batch.h"
 #include "webp/encode.h"
 
-/* partition-0 size guard of VP8EncTokenLoop (frame_enc.c:32, :869) */
-#define VP8H_P0_LIMIT ((((uint64_t)1 << 19) - 2048ULL) << 11)
-
 struct WebPGpuBatch {
   int device, w, h, max_frames, mbw, mbh, nmb, uvw, uvh, threads, last_n;
   WebPConfig cfg;
@@ -35,7 +32,15 @@ struct WebPGpuBatch {
   uint16_t* d_tokens;
   uint8_t* d_mbinfo;
   uint32_t* d_mboff;         /* K3 scratch: compact-stream offset per MB */
-  uint8_t* d_rerun;          /* K3 cost state for partition-0 re-runs */
+  uint8_t* d_rerun;          /* K3 cost state carried from pass to pass */
+  /* size search between passes (allocated on first use) */
+  uint8_t* h_state;          /* pinned copy of d_rerun */
+  uint8_t* d_active;         /* frames whose token bits are estimated */
+  uint8_t* h_active;
+  unsigned long long* d_tbits;
+  unsigned long long* h_tbits;
+  int* fin_cost;             /* FinalizeTokenProbas header cost per frame */
+  uint8_t* pass_act;         /* frames with a pass to run */
   vp8g_frame_result* d_results;
   uint32_t* d_psize;         /* partition-1 bytes per frame (K4) */
   vp8g_emit_meta* d_emeta;   /* K4 per-frame bookkeeping */

@@ -14,6 +14,9 @@
 
 static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
 static inline int iabs(int v) { return v < 0 ? -v : v; }
+static inline float clampf(float v, float lo, float hi) {   /* frame_enc.c:34-36 */
+  return (v < lo) ? lo : (v > hi) ? hi : v;
+}
 static inline int bit_cost(int bit, int p) {   /* cost_enc.h:59-61 */
   return bit ? kVP8EntropyCost[255 - p] : kVP8EntropyCost[p];
 }
@@ -48,7 +51,6 @@ int vp8h_use_sharp(const WebPConfig* cfg, int w, int h) {
 int vp8h_frame_init(vp8h_frame* fr, const WebPConfig* cfg, int w, int h) {
   memset(fr, 0, sizeof(*fr));
   if (cfg->method < 3 || cfg->method > 6) return 0;   /* m0-2: non-token loop */
-  if (cfg->pass != 1 || cfg->target_size > 0 || cfg->target_PSNR > 0) return 0;
   if (cfg->autofilter || cfg->low_memory || (cfg->preprocessing & 2)) return 0;
   fr->w = w; fr->h = h;
   fr->mbw = (w + 15) >> 4; fr->mbh = (h + 15) >> 4;
@@ -76,7 +78,95 @@ int vp8h_frame_init(vp8h_frame* fr, const WebPConfig* cfg, int w, int h) {
   fr->f_simple = 1;     /* ResetFilterHeader, webp_enc.c:47-53 */
   fr->f_level = 0;
   fr->f_sharpness = 0;
+  /* InitPassStats (frame_enc.c:47-62), enc->do_search_ (webp_enc.c:114) */
+  fr->pass_left = fr->cfg_pass = cfg->pass;
+  fr->do_search = cfg->target_size > 0 || cfg->target_PSNR > 0;
+  fr->do_size_search = cfg->target_size != 0;
+  fr->ps_is_first = 1;
+  fr->ps_dq = 10.f;
+  fr->ps_qmin = 1.f * cfg->qmin;
+  fr->ps_qmax = 1.f * cfg->qmax;
+  fr->ps_q = fr->ps_last_q = clampf(cfg->quality, fr->ps_qmin, fr->ps_qmax);
+  fr->ps_target = fr->do_size_search ? (double)(uint64_t)cfg->target_size
+                : (cfg->target_PSNR > 0.) ? cfg->target_PSNR : 40.;
+  fr->ps_value = fr->ps_last_value = 0.;
   return 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* multi-pass convergence: frame_enc.c:26-80, 146-180, 554-556, 808-880 */
+
+#define DQ_LIMIT 0.4
+#define HEADER_SIZE_ESTIMATE (12 + 8 + 10)   /* RIFF + chunk + VP8 frame headers */
+
+int vp8h_pass_start(vp8h_frame* fr) {
+  if (fr->pass_left-- <= 0) return 0;
+  fr->is_last_pass = (fabs(fr->ps_dq) <= DQ_LIMIT) || (fr->pass_left == 0) ||
+                     (fr->max_i4_header_bits == 0);
+  return 1;
+}
+
+static void compute_next_q(vp8h_frame* s) {   /* ComputeNextQ, :60-80 */
+  float dq;
+  if (s->ps_is_first) {
+    dq = (s->ps_value > s->ps_target) ? -s->ps_dq : s->ps_dq;
+    s->ps_is_first = 0;
+  } else if (s->ps_value != s->ps_last_value) {
+    const double slope = (s->ps_target - s->ps_value) / (s->ps_last_value - s->ps_value);
+    dq = (float)(slope * (s->ps_last_q - s->ps_q));
+  } else {
+    dq = 0.;
+  }
+  s->ps_dq = clampf(dq, -30.f, 30.f);
+  s->ps_last_q = s->ps_q;
+  s->ps_last_value = s->ps_value;
+  s->ps_q = clampf(s->ps_q + s->ps_dq, s->ps_qmin, s->ps_qmax);
+}
+
+int vp8h_pass_finish(vp8h_frame* fr, uint64_t size_p0) {
+  if (fr->max_i4_header_bits > 0 && size_p0 > VP8H_P0_LIMIT) {
+    ++fr->pass_left;
+    fr->max_i4_header_bits >>= 1;   /* strengthen the header bit limit and start over */
+    return 1;
+  }
+  if (fr->is_last_pass) return 0;
+  if (fr->do_search) compute_next_q(fr);
+  return fr->pass_left > 0;
+}
+
+int vp8h_finalize_probas(const uint32_t* stats, uint8_t* coeffs, int* dirty) {
+  const uint8_t* p0 = &kVP8CoeffProba0[0][0][0][0];
+  const uint8_t* pu = &kVP8CoeffUpdateProba[0][0][0][0];
+  int changed = 0, size = 0;
+  for (int s = 0; s < VP8G_NUM_SLOTS; ++s) {
+    const int nb = stats[s] & 0xffff, total = (stats[s] >> 16) & 0xffff;
+    const int old_p = p0[s], upd = pu[s];
+    const int new_p = nb ? (255 - nb * 255 / total) : 255;
+    const int old_cost = nb * bit_cost(1, old_p) + (total - nb) * bit_cost(0, old_p) + bit_cost(0, upd);
+    const int new_cost = nb * bit_cost(1, new_p) + (total - nb) * bit_cost(0, new_p) +
+                         bit_cost(1, upd) + 8 * 256;
+    const int use_new = old_cost > new_cost;
+    size += bit_cost(use_new, upd);
+    if (use_new) {
+      coeffs[s] = (uint8_t)new_p;
+      changed |= new_p != old_p;
+      size += 8 * 256;
+    } else {
+      coeffs[s] = (uint8_t)old_p;
+    }
+  }
+  *dirty = changed;
+  return size;
+}
+
+double vp8h_pass_size_value(uint64_t finalize_cost, uint64_t token_bits, uint64_t size_p0) {
+  uint64_t size = finalize_cost + token_bits;
+  size = (size + size_p0 + 1024) >> 11;
+  return (double)(size + HEADER_SIZE_ESTIMATE);
+}
+
+double vp8h_psnr(uint64_t mse, uint64_t count) {
+  return (mse > 0 && count > 0) ? 10. * log10(255. * 255. * count / mse) : 99;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -193,6 +283,12 @@ static int get_proba(int a, int b) {
 
 void vp8h_setup_segments(vp8h_frame* fr, const uint8_t* mb_alpha, const uint16_t* mb_uva,
                          uint8_t* segmap, vp8g_frame_params* P) {
+  vp8h_analyze_segments(fr, mb_alpha, mb_uva, segmap);
+  vp8h_set_loop_params(fr, fr->ps_q, segmap, P);
+}
+
+void vp8h_analyze_segments(vp8h_frame* fr, const uint8_t* mb_alpha, const uint16_t* mb_uva,
+                           uint8_t* segmap) {
   const int nmb = fr->mbw * fr->mbh;
   /* VP8EncAnalyze tail (analysis_enc.c:422-482) */
   const int do_seg = fr->emulate_jpeg_size || fr->num_segments > 1;
@@ -207,10 +303,16 @@ void vp8h_setup_segments(vp8h_frame* fr, const uint8_t* mb_alpha, const uint16_t
     fr->seg_alpha[0] = fr->seg_beta[0] = 0;
     fr->alpha = fr->uv_alpha = 0;
   }
+}
+
+void vp8h_set_loop_params(vp8h_frame* fr, float quality, uint8_t* segmap, vp8g_frame_params* P) {
+  const int nmb = fr->mbw * fr->mbh;
+  /* SetLoopParams: q clamped to [0, 100] */
+  quality = quality < 0.f ? 0.f : quality > 100.f ? 100.f : quality;
   /* VP8SetSegmentParams */
   const int ns = fr->num_segments;
   const double amp = 0.9 * fr->sns_strength / 100. / 128.;
-  const double Q = fr->quality / 100.;
+  const double Q = quality / 100.;
   const double cbase = fr->emulate_jpeg_size ? q_to_jpeg_compression(Q, fr->alpha / 255.)
                                              : q_to_compression(Q);
   for (int i = 0; i < ns; ++i) {
@@ -314,7 +416,7 @@ void vp8h_setup_segments(vp8h_frame* fr, const uint8_t* mb_alpha, const uint16_t
   P->max_i4_header_bits = fr->max_i4_header_bits;
   P->rd_opt = fr->rd_opt;
   P->method = fr->method;
-  P->use_derr = fr->quality <= 98;
+  P->use_derr = fr->quality <= 98 || fr->cfg_pass > 1;   /* webp_enc.c:162-164 */
   P->max_count = (nmb >> 3) < 96 ? 96 : (nmb >> 3);
 }
 

@@ -14,6 +14,9 @@
 extern "C" {
 #endif
 
+/* partition-0 limit on the header estimate (frame_enc.c:32) */
+#define VP8H_P0_LIMIT ((((uint64_t)1 << 19) - 2048ULL) << 11)
+
 /* Frame-level encoder state that lives on the host (a slice of the
  * reference's VP8Encoder, src/enc/vp8i_enc.h:346-413). */
 typedef struct {
@@ -31,6 +34,10 @@ typedef struct {
   int segment_size[4];
   /* filter header */
   int f_simple, f_level, f_sharpness;
+  /* multi-pass convergence (PassStats, frame_enc.c:38-80) */
+  int cfg_pass, pass_left, is_last_pass, npass, do_search, do_size_search, ps_is_first;
+  float ps_dq, ps_q, ps_last_q, ps_qmin, ps_qmax;
+  double ps_value, ps_last_value, ps_target;
 } vp8h_frame;
 
 /* Initialise from a validated config (lossy, method 3..6). Returns 0 if the
@@ -51,6 +58,33 @@ int vp8h_frame_init(vp8h_frame* fr, const WebPConfig* cfg, int w, int h);
  * Outputs: final per-MB segment ids and the kernel parameter block. */
 void vp8h_setup_segments(vp8h_frame* fr, const uint8_t* mb_alpha, const uint16_t* mb_uva,
                          uint8_t* segmap, vp8g_frame_params* params);
+/* the two halves of vp8h_setup_segments: the k-means on the analysis alphas
+ * (VP8EncAnalyze tail) once per frame, then SetLoopParams (frame_enc.c:563-572:
+ * VP8SetSegmentParams + SetupMatrices + SetSegmentProbas) at the start of
+ * every pass with that pass's quality */
+void vp8h_analyze_segments(vp8h_frame* fr, const uint8_t* mb_alpha, const uint16_t* mb_uva,
+                           uint8_t* segmap);
+void vp8h_set_loop_params(vp8h_frame* fr, float q, uint8_t* segmap, vp8g_frame_params* params);
+
+/* Pass loop of VP8EncTokenLoop (frame_enc.c:808-880), one frame:
+ *   while (vp8h_pass_start(fr)) { SetLoopParams(fr->ps_q); K3;
+ *                                 if (!vp8h_pass_finish(...)) break; }
+ * vp8h_pass_start consumes a pass and sets fr->is_last_pass (K3 resets the
+ * token statistics only on the last pass). vp8h_pass_finish takes the pass's
+ * header estimate (K3 size_p0 + segment header) and its value (estimated
+ * size in bytes or PSNR, vp8h_pass_value) and returns 1 when another pass
+ * follows: partition-0 overflow retry (:869-876) or a search step
+ * (ComputeNextQ, :60-80). */
+int vp8h_pass_start(vp8h_frame* fr);
+int vp8h_pass_finish(vp8h_frame* fr, uint64_t size_p0);
+/* FinalizeTokenProbas (frame_enc.c:146-180) from the token statistics:
+ * writes the probabilities, returns the proba-update header cost (1/256
+ * bit); *dirty = some probability differs from the default table */
+int vp8h_finalize_probas(const uint32_t* stats, uint8_t* coeffs, int* dirty);
+/* size of the pass in bytes (size search) from the finalize cost, the token
+ * bit estimate (VP8EstimateTokenSize) and the header estimate */
+double vp8h_pass_size_value(uint64_t finalize_cost, uint64_t token_bits, uint64_t size_p0);
+double vp8h_psnr(uint64_t mse, uint64_t count);   /* GetPSNR, frame_enc.c:554-556 */
 
 /* Boolean coder (bit_writer_utils.c). */
 typedef struct {

@@ -49,16 +49,24 @@ typedef struct {
   int32_t method;
   int32_t use_derr;      /* U/V DC error diffusion (quality <= 98) */
   int32_t max_count;     /* cost-refresh period (frame_enc.c:785,800) */
-  int32_t pass_mode;     /* 0 first pass; 1 partition-0 re-run (frame_enc.c:869-876):
-                            start from the previous pass's cost state in
-                            rerun_state; 2 frame already final: skip */
+  int32_t pass_mode;     /* 0 first pass (default probabilities, zero statistics);
+                            1 later pass starting from the previous pass's cost
+                            state in rerun_state with the token statistics
+                            reset (the last pass of frame_enc.c:808-880, and
+                            the partition-0 re-run of :869-876); 3 the same but
+                            the statistics continue from rerun_state (a
+                            non-last pass); 2 frame already final: skip */
   int32_t pad[2];
 } vp8g_frame_params;
 
-/* per-frame cost state K3 leaves for a partition-0 re-run: the
- * probabilities the level-cost tables were last computed from, then the
- * probabilities at the end of the MB loop (before the final refresh) */
-#define VP8G_RERUN_STATE_BYTES (2 * VP8G_NUM_SLOTS)
+/* per-frame cost state K3 leaves for the next pass: the probabilities the
+ * level-cost tables were last computed from, then the probabilities at the
+ * end of the MB loop (before the final refresh), then the token statistics
+ * (uint32 per slot, proba_t of src/enc/vp8i_enc.h:146). Between passes of a
+ * size search the host replaces the probabilities by FinalizeTokenProbas'. */
+#define VP8G_RERUN_STATE_BYTES (6 * VP8G_NUM_SLOTS)
+#define VP8G_STATE_COEFFS (VP8G_NUM_SLOTS)       /* offset of the loop-end probabilities */
+#define VP8G_STATE_STATS (2 * VP8G_NUM_SLOTS)    /* offset of the statistics */
 
 typedef struct {
   uint32_t ntokens;
@@ -66,6 +74,7 @@ typedef struct {
   int32_t max_edge[4];
   uint64_t size_p0;      /* sum of per-MB header-bit estimates (frame_enc.c:839) */
   uint64_t sse[3];
+  uint64_t distortion;   /* sum of the per-MB VP8ModeScore D (frame_enc.c:840) */
   int32_t block_count[3];
   int32_t pad;
   uint64_t stamps[8];    /* per-stage shader-clock cycles summed over MBs (profiling) */
@@ -105,6 +114,14 @@ int vp8g_launch_encode(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h,
                        const vp8g_frame_params* params, uint16_t* tokens,
                        size_t tok_cap, uint8_t* mbinfo, uint32_t* mboff, int trellis,
                        vp8g_frame_result* results, uint8_t* rerun_state, void* stream);
+
+/* VP8EstimateTokenSize (token_enc.c:226-247) of each frame's compact token
+ * stream under the probabilities at state + f * VP8G_RERUN_STATE_BYTES +
+ * VP8G_STATE_COEFFS; frames with active[f] == 0 are skipped. bits[f] (device,
+ * zeroed here) receives the sum in 1/256 bit. */
+int vp8g_launch_token_cost(const uint16_t* tokens, size_t tok_cap, int n,
+                           const vp8g_frame_result* results, const uint8_t* state,
+                           const uint8_t* active, unsigned long long* bits, void* stream);
 
 /* K4: boolean coder for the token partition, parallel inside each frame
  * (hip/vp8_emit.hip). Per-frame bookkeeping: ntok, the segment count and the

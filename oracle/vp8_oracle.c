@@ -1856,7 +1856,8 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
   e->nz = e->nz_mem + 1;
   e->y_top = (uint8_t*)calloc(2 * 16 * e->mbw, 1);
   e->uv_top = e->y_top + 16 * e->mbw;
-  if (cfg->quality <= 98) e->top_derr = calloc(e->mbw, sizeof(*e->top_derr));
+  if (cfg->quality <= 98 || cfg->pass > 1)   /* webp_enc.c:162-164 */
+    e->top_derr = calloc(e->mbw, sizeof(*e->top_derr));
   /* MapConfigToTools, webp_enc.c:95-123 */
   e->method = cfg->method;
   e->rd_opt = cfg->method >= 6 ? 3 : cfg->method >= 5 ? 2 : 1;

@@ -1750,7 +1750,8 @@ static size_t write_stream(Enc* e, BW* part1, uint8_t** out) {
   if (!o) { free(bw.buf); return 0; }
   memcpy(o, "RIFF", 4); put_le32(o + 4, (uint32_t)riff_size); memcpy(o + 8, "WEBP", 4);
   memcpy(o + 12, "VP8 ", 4); put_le32(o + 16, (uint32_t)vp8_size);
-  const int profile = (e->cfg.filter_strength > 0) ? (e->cfg.filter_type == 1 ? 0 : 1) : 2;
+  const int use_filter = e->cfg.filter_strength > 0 || e->cfg.autofilter > 0;
+  const int profile = use_filter ? (e->cfg.filter_type == 1 ? 0 : 1) : 2;
   const uint32_t bits = 0 | (profile << 1) | (1 << 4) | ((uint32_t)size0 << 5);
   uint8_t* f = o + 20;
   f[0] = bits; f[1] = bits >> 8; f[2] = bits >> 16;
@@ -1829,6 +1830,143 @@ static uint64_t estimate_token_size(const Enc* e) {
   return size;
 }
 
+
+/* ------------------------------------------------------------------------ */
+/* Autofilter (config->autofilter): per-MB SSIM of the reconstruction filtered
+ * at the candidate levels, filter_enc.c:70-233, with the in-loop filters of
+ * src/dsp/dec.c:484-692 and the SSIM of src/dsp/ssim.c:22-108 */
+
+static inline int sclip1(int v) { return v < -128 ? -128 : v > 127 ? 127 : v; }   /* VP8ksclip1 */
+static inline int sclip2(int v) { return v < -16 ? -16 : v > 15 ? 15 : v; }       /* VP8ksclip2 */
+static inline int uclip1(int v) { return v < 0 ? 0 : v > 255 ? 255 : v; }         /* VP8kclip1 */
+
+static void lf_filter2(uint8_t* p, int step) {   /* DoFilter2_C */
+  const int p1 = p[-2 * step], p0 = p[-step], q0 = p[0], q1 = p[step];
+  const int a = 3 * (q0 - p0) + sclip1(p1 - q1);
+  const int a1 = sclip2((a + 4) >> 3), a2 = sclip2((a + 3) >> 3);
+  p[-step] = uclip1(p0 + a2);
+  p[0] = uclip1(q0 - a1);
+}
+static void lf_filter4(uint8_t* p, int step) {   /* DoFilter4_C */
+  const int p1 = p[-2 * step], p0 = p[-step], q0 = p[0], q1 = p[step];
+  const int a = 3 * (q0 - p0);
+  const int a1 = sclip2((a + 4) >> 3), a2 = sclip2((a + 3) >> 3), a3 = (a1 + 1) >> 1;
+  p[-2 * step] = uclip1(p1 + a3);
+  p[-step] = uclip1(p0 + a2);
+  p[0] = uclip1(q0 - a1);
+  p[step] = uclip1(q1 - a3);
+}
+static int lf_hev(const uint8_t* p, int step, int t) {
+  return iabs(p[-2 * step] - p[-step]) > t || iabs(p[step] - p[0]) > t;
+}
+static int lf_needs(const uint8_t* p, int step, int t) {   /* NeedsFilter_C */
+  return 4 * iabs(p[-step] - p[0]) + iabs(p[-2 * step] - p[step]) <= t;
+}
+static int lf_needs2(const uint8_t* p, int step, int t, int it) {   /* NeedsFilter2_C */
+  const int p3 = p[-4 * step], p2 = p[-3 * step], p1 = p[-2 * step], p0 = p[-step];
+  const int q0 = p[0], q1 = p[step], q2 = p[2 * step], q3 = p[3 * step];
+  if (4 * iabs(p0 - q0) + iabs(p1 - q1) > t) return 0;
+  return iabs(p3 - p2) <= it && iabs(p2 - p1) <= it && iabs(p1 - p0) <= it &&
+         iabs(q3 - q2) <= it && iabs(q2 - q1) <= it && iabs(q1 - q0) <= it;
+}
+/* FilterLoop24_C: the inner-edge complex filter along one edge */
+static void lf_loop24(uint8_t* p, int hs, int vs, int size, int thresh, int ithresh, int hev) {
+  const int t2 = 2 * thresh + 1;
+  for (; size-- > 0; p += vs)
+    if (lf_needs2(p, hs, t2, ithresh)) {
+      if (lf_hev(p, hs, hev)) lf_filter2(p, hs); else lf_filter4(p, hs);
+    }
+}
+static void lf_simple(uint8_t* p, int hs, int vs, int thresh) {   /* Simple[HV]Filter16_C */
+  const int t2 = 2 * thresh + 1;
+  for (int i = 0; i < 16; ++i, p += vs)
+    if (lf_needs(p, hs, t2)) lf_filter2(p, hs);
+}
+
+static int lf_ilevel(int sharpness, int level) {   /* GetILevel, filter_enc.c:70-83 */
+  if (sharpness > 0) {
+    level >>= (sharpness > 4) ? 2 : 1;
+    if (level > 9 - sharpness) level = 9 - sharpness;
+  }
+  return level < 1 ? 1 : level;
+}
+
+static void lf_do_filter(const Enc* e, const uint8_t* rec, uint8_t* out, int level) {   /* :85-107 */
+  const int ilevel = lf_ilevel(e->cfg.filter_sharpness, level);
+  const int limit = 2 * level + ilevel;
+  memcpy(out, rec, BPS * 16);
+  if (e->f_simple) {
+    for (int k = 1; k <= 3; ++k) lf_simple(out + 4 * k, 1, BPS, limit);        /* H, 16i */
+    for (int k = 1; k <= 3; ++k) lf_simple(out + 4 * k * BPS, BPS, 1, limit);  /* V, 16i */
+  } else {
+    const int hev = (level >= 40) ? 2 : (level >= 15) ? 1 : 0;
+    for (int k = 1; k <= 3; ++k) lf_loop24(out + 4 * k, 1, BPS, 16, limit, ilevel, hev);
+    lf_loop24(out + 16 + 4, 1, BPS, 8, limit, ilevel, hev);          /* HFilter8i: u, v */
+    lf_loop24(out + 24 + 4, 1, BPS, 8, limit, ilevel, hev);
+    for (int k = 1; k <= 3; ++k) lf_loop24(out + 4 * k * BPS, BPS, 1, 16, limit, ilevel, hev);
+    lf_loop24(out + 16 + 4 * BPS, BPS, 1, 8, limit, ilevel, hev);    /* VFilter8i */
+    lf_loop24(out + 24 + 4 * BPS, BPS, 1, 8, limit, ilevel, hev);
+  }
+}
+
+static double ssim_clipped(const uint8_t* s1, const uint8_t* s2, int xo, int yo, int W, int H) {
+  static const uint32_t kW[7] = {1, 2, 3, 4, 3, 2, 1};
+  uint32_t w = 0, xm = 0, ym = 0, xxm = 0, xym = 0, yym = 0;
+  const int ymin = yo - 3 < 0 ? 0 : yo - 3, ymax = yo + 3 > H - 1 ? H - 1 : yo + 3;
+  const int xmin = xo - 3 < 0 ? 0 : xo - 3, xmax = xo + 3 > W - 1 ? W - 1 : xo + 3;
+  for (int y = ymin; y <= ymax; ++y)
+    for (int x = xmin; x <= xmax; ++x) {
+      const uint32_t wt = kW[3 + x - xo] * kW[3 + y - yo];
+      const uint32_t a = s1[y * BPS + x], b = s2[y * BPS + x];
+      w += wt; xm += wt * a; ym += wt * b;
+      xxm += wt * a * a; xym += wt * a * b; yym += wt * b * b;
+    }
+  /* SSIMCalculation with N = w (ssim.c:28-52) */
+  const uint32_t N = w, w2 = N * N;
+  const uint32_t C1 = 20 * w2, C2 = 60 * w2, C3 = 8 * 8 * w2;
+  const uint64_t xmxm = (uint64_t)xm * xm, ymym = (uint64_t)ym * ym;
+  if (xmxm + ymym >= C3) {
+    const int64_t xmym = (int64_t)xm * ym;
+    const int64_t sxy = (int64_t)xym * N - xmym;
+    const uint64_t sxx = (uint64_t)xxm * N - xmxm, syy = (uint64_t)yym * N - ymym;
+    const uint64_t num_S = (2 * (uint64_t)(sxy < 0 ? 0 : sxy) + C2) >> 8;
+    const uint64_t den_S = (sxx + syy + C2) >> 8;
+    const uint64_t fnum = (2 * xmym + C1) * num_S;
+    const uint64_t fden = (xmxm + ymym + C1) * den_S;
+    return (double)fnum / fden;
+  }
+  return 1.;
+}
+
+static double mb_ssim(const uint8_t* a, const uint8_t* b) {   /* GetMBSSIM, :112-132 */
+  double sum = 0.;
+  for (int y = 3; y < 16 - 3; ++y)
+    for (int x = 3; x < 16 - 3; ++x) sum += ssim_clipped(a, b, x, y, 16, 16);
+  for (int x = 1; x < 7; ++x)
+    for (int y = 1; y < 7; ++y) {
+      sum += ssim_clipped(a + 16, b + 16, x, y, 8, 8);
+      sum += ssim_clipped(a + 24, b + 24, x, y, 8, 8);
+    }
+  return sum;
+}
+
+static void store_filter_stats(const It* it, const Enc* e, double lf[4][64]) {   /* :156-192 */
+  const int mi = it->y * e->mbw + it->x;
+  const int s = e->mb_seg[mi];
+  const int level0 = e->dqm[s].fstrength;
+  const int dmin = -e->dqm[s].quant, dmax = e->dqm[s].quant;
+  const int step = (dmax - dmin >= 4) ? 4 : 1;
+  if (e->mb_type[mi] == 1 && e->mb_skip[mi]) return;
+  lf[s][0] += mb_ssim(it->yin, it->out);
+  uint8_t tmp[BPS * 16];
+  for (int d = dmin; d <= dmax; d += step) {
+    const int level = level0 + d;
+    if (level <= 0 || level >= 64) continue;
+    lf_do_filter(e, it->out, tmp, level);
+    lf[s][level] += mb_ssim(it->yin, tmp);
+  }
+}
+
 void vp8o_default_config(vp8o_config* c) {   /* config_enc.c:24-98 */
   memset(c, 0, sizeof(*c));
   c->quality = 75.f; c->method = 4; c->segments = 4; c->sns_strength = 50;
@@ -1887,6 +2025,7 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
   const int do_search = cfg->target_size > 0 || cfg->target_PSNR > 0;
   const uint64_t pixel_count = (uint64_t)nmb * 384;
   int num_pass_left = cfg->pass < 1 ? 1 : cfg->pass;
+  double (*lf)[64] = cfg->autofilter ? (double (*)[64])calloc(4 * 64, sizeof(double)) : NULL;
   while (num_pass_left-- > 0) {
     const int is_last_pass = (fabs(ps.dq) <= DQ_LIMIT) || (num_pass_left == 0) ||
                              (e->max_i4_header_bits == 0);
@@ -1899,6 +2038,7 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
     set_segment_probas(e);
     level_costs(e);
     if (is_last_pass) memset(e->stats, 0, sizeof(e->stats));
+    if (is_last_pass && lf) memset(lf, 0, 4 * 64 * sizeof(double));   /* VP8InitFilter */
     e->ntok = 0;
     do {
       Score rd;
@@ -1912,6 +2052,7 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
       record_tokens(&it, e, &rd);
       size_p0 += rd.H;
       distortion += rd.D;
+      if (is_last_pass && lf) store_filter_stats(&it, e, lf);
       if (trace && is_last_pass) {
         vp8o_mb_trace* t = &trace[it.y * e->mbw + it.x];
         const int mi = it.y * e->mbw + it.x;
@@ -1954,7 +2095,15 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
     bw_put(&part1, bit, (t & (1u << 14)) ? (t & 0xff) : ((const uint8_t*)e->coeffs)[t & 0x3fff]);
   }
   bw_finish(&part1);
-  if (cfg->filter_strength > 0) {   /* VP8AdjustFilterStrength without -af */
+  if (lf) {   /* VP8AdjustFilterStrength with -af (filter_enc.c:197-212) */
+    for (int sg = 0; sg < 4; ++sg) {
+      int best_level = 0;
+      double best_v = 1.00001 * lf[sg][0];
+      for (int i = 1; i < 64; ++i)
+        if (lf[sg][i] > best_v) { best_v = lf[sg][i]; best_level = i; }
+      e->dqm[sg].fstrength = best_level;
+    }
+  } else if (cfg->filter_strength > 0) {   /* VP8AdjustFilterStrength without -af */
     int max_level = 0;
     for (int s = 0; s < 4; ++s) {
       Seg* d = &e->dqm[s];
@@ -1967,6 +2116,7 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
   }
   result = write_stream(e, &part1, out);
 done:
+  free(lf);
   free(part1.buf);
   free(e->tok); free(e->mb_type); free(e->mb_uv); free(e->mb_skip); free(e->mb_seg);
   free(e->mb_alpha); free(e->preds_mem); free(e->nz_mem); free(e->y_top); free(e->top_derr);

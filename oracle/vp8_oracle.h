@@ -29,6 +29,7 @@ typedef struct {
   int target_size;        /* bytes, 0 = off */
   float target_PSNR;      /* dB, 0 = off */
   int qmin, qmax;         /* 0..100 */
+  int autofilter;         /* 0/1: SSIM-driven per-segment filter levels */
 } vp8o_config;
 
 /* per-macroblock decisions, for stage-by-stage comparison with the GPU */

@@ -1155,7 +1155,8 @@ struct K3Args {
 
 // TR: the method >= 5 instantiation carries the trellis paths; m3/m4 frames
 // run a kernel without them (smaller register footprint).
-template <int NW, bool TR>
+// AF: also store each MB's reconstruction for the autofilter
+template <int NW, bool TR, bool AF = false>
 __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   extern __shared__ __align__(16) uint8_t smem[];
   const int mbw = a.mbw, mbh = a.mbh, nmb = mbw * mbh;
@@ -1488,6 +1489,13 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
         atomicAdd(&G.fs.dist, (unsigned long long)L.mdist);
       }
       if (tid < 16) mbinfo[(size_t)mb * VP8G_MBINFO_BYTES + 4 + tid] = L.modes[tid];
+      if constexpr (AF) {   // VP8StoreFilterStats input (filter_enc.c:179)
+        // (a separate instantiation: any extra store here makes the default
+        // kernel spill at its 168-VGPR budget)
+        if (tid < 128)
+          reinterpret_cast<uint32_t*>(P->recon_addr + ((size_t)mb << 9))[tid] =
+              reinterpret_cast<const uint32_t*>(L.yout)[tid];
+      }
       if (w0) {   // SSE for WebPAuxStats (frame_enc.c:480-489)
         int sy = 0, su = 0, sv = 0;
         for (int k = lane; k < 256; k += 64) {
@@ -1698,7 +1706,7 @@ extern "C" int vp8g_launch_encode_w1(const uint8_t* yuv, size_t yfb, int w, int 
                                      vp8g_frame_result* results, void* stream);
 extern "C" int vp8g_launch_check(const char* what);
 
-template <int NW, bool TR>
+template <int NW, bool TR, bool AF = false>
 static int launch_k3_t(const K3Args& a, int n, bool trellis, void* stream) {
   const size_t lds = k3_lds_bytes<NW>(a.mbw, a.mbh, trellis);
   if (lds > 160 * 1024) {
@@ -1717,7 +1725,8 @@ static int launch_k3_t(const K3Args& a, int n, bool trellis, void* stream) {
       attr_bytes = lds;
     }
   }
-  hipLaunchKernelGGL((k_encode<NW, TR>), dim3(n), dim3(NW * K3T), lds, (hipStream_t)stream, a);
+  hipLaunchKernelGGL((k_encode<NW, TR, AF>), dim3(n), dim3(NW * K3T), lds, (hipStream_t)stream,
+                     a);
   return vp8g_launch_check("k_encode");
 }
 
@@ -1730,7 +1739,10 @@ static int launch_k3(const K3Args& a, int n, bool trellis, void* stream) {
 // default: 3 MB workers for m3/m4 frames (4 spill registers to scratch and
 // are no faster: the CU's vector issue is already saturated), 2 when the
 // trellis paths (and their registers and LDS) are in the kernel
-static int launch_k3_default(const K3Args& a, int n, bool trellis, void* stream) {
+static int launch_k3_default(const K3Args& a, int n, bool trellis, bool af, void* stream) {
+  if (af)
+    return trellis ? launch_k3_t<2, true, true>(a, n, true, stream)
+                   : launch_k3_t<3, false, true>(a, n, false, stream);
   return trellis ? launch_k3_t<2, true>(a, n, true, stream)
                  : launch_k3_t<3, false>(a, n, false, stream);
 }
@@ -1739,12 +1751,18 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
                                   const uint8_t* segmap, const vp8g_frame_params* params,
                                   uint16_t* tokens, size_t tok_cap, uint8_t* mbinfo,
                                   uint32_t* mboff, int trellis, vp8g_frame_result* results,
-                                  uint8_t* rerun_state, void* stream) {
+                                  uint8_t* rerun_state, uint8_t* recon, void* stream) {
   static int variant = -1;
   if (variant < 0) {   // WEBP_AMD_K3: 1 = single-wavefront reference kernel, 2/3/5/4 =
                        // 1/2/3/4 MB workers per frame, unset = default above
     const char* v = getenv("WEBP_AMD_K3");
     variant = (v && v[0] >= '1' && v[0] <= '5') ? v[0] - '0' : 0;
+  }
+  // recon != NULL selects the autofilter instantiation; each frame's buffer
+  // address travels in vp8g_frame_params::recon_addr
+  if (recon != nullptr && variant != 0) {
+    vp8g_set_error("k_encode", "the autofilter runs on the default K3 variant only");
+    return 0;
   }
   if (variant == 1)
     return vp8g_launch_encode_w1(yuv, yfb, w, h, n, segmap, params, tokens, tok_cap, mbinfo,
@@ -1758,5 +1776,5 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   if (variant == 3) return launch_k3<2>(a, n, trellis != 0, stream);
   if (variant == 4) return launch_k3<4>(a, n, trellis != 0, stream);
   if (variant == 5) return launch_k3<3>(a, n, trellis != 0, stream);
-  return launch_k3_default(a, n, trellis != 0, stream);
+  return launch_k3_default(a, n, trellis != 0, recon != nullptr, stream);
 }

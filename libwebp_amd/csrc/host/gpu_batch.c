@@ -177,6 +177,8 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipFree(b->d_eimg);
   hipFree(b->d_stabs); hipFree(b->d_sharp); hipFree(b->d_sstate);
   hipFree(b->d_active); hipFree(b->d_tbits);
+  hipFree(b->d_recon); hipFree(b->d_mbval); hipFree(b->d_afp); hipFree(b->d_aflevel);
+  hipHostFree(b->h_afp); hipHostFree(b->h_aflevel);
   hipHostFree(b->h_state); hipHostFree(b->h_active); hipHostFree(b->h_tbits);
   hipHostFree(b->h_aflags); hipHostFree(b->h_alpha); hipHostFree(b->h_uva);
   hipHostFree(b->h_segmap); hipHostFree(b->h_params); hipHostFree(b->h_mbinfo);
@@ -341,6 +343,20 @@ static int run_passes(WebPGpuBatch* b, int n) {
   hipStream_t st = b->stream;
   int* fin_cost = b->fin_cost;
   uint8_t* act = b->pass_act;
+  const int af = b->cfg.autofilter != 0;
+  if (af && !b->d_recon) {
+    const size_t N = (size_t)b->max_frames;
+    CHK(hipMalloc((void**)&b->d_recon, N * nmb * 512));
+    CHK(hipMalloc((void**)&b->d_mbval, N * nmb * 64 * sizeof(double)));
+    CHK(hipMalloc((void**)&b->d_afp, N * sizeof(vp8g_af_frame)));
+    CHK(hipMalloc((void**)&b->d_aflevel, N * 4));
+    CHK(hipHostMalloc((void**)&b->h_afp, N * sizeof(vp8g_af_frame), 0));
+    CHK(hipHostMalloc((void**)&b->h_aflevel, N * 4, 0));
+    if (!b->h_active) {
+      CHK(hipHostMalloc((void**)&b->h_active, N, 0));
+      CHK(hipMalloc((void**)&b->d_active, N));
+    }
+  }
   for (int f = 0; f < n; ++f) act[f] = b->err[f] == VP8_ENC_OK && vp8h_pass_start(&b->frames[f]);
   int round = 0;
   for (;;) {
@@ -351,6 +367,7 @@ static int run_passes(WebPGpuBatch* b, int n) {
       vp8h_frame* fr = &b->frames[f];
       vp8h_set_loop_params(fr, fr->ps_q, b->h_segmap + f * nmb, P);
       P->pass_mode = fr->npass == 0 ? 0 : fr->is_last_pass ? 1 : 3;
+      P->recon_addr = af ? (uint64_t)(uintptr_t)(b->d_recon + (size_t)f * nmb * 512) : 0;
       ++fr->npass;
       ++nact;
       nsize += fr->do_size_search && !fr->is_last_pass;
@@ -362,7 +379,7 @@ static int run_passes(WebPGpuBatch* b, int n) {
     if (round == 0) CHK(hipEventRecord(b->ev[2], st));
     if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params,
                             b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5,
-                            b->d_results, b->d_rerun, st))
+                            b->d_results, b->d_rerun, af ? b->d_recon : NULL, st))
       return 0;
     CHK(hipEventRecord(b->ev[3], st));
     CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
@@ -370,10 +387,12 @@ static int run_passes(WebPGpuBatch* b, int n) {
     if (nsize) {
       if (!b->h_state) {
         CHK(hipHostMalloc((void**)&b->h_state, (size_t)b->max_frames * VP8G_RERUN_STATE_BYTES, 0));
-        CHK(hipHostMalloc((void**)&b->h_active, b->max_frames, 0));
         CHK(hipHostMalloc((void**)&b->h_tbits, b->max_frames * sizeof(unsigned long long), 0));
-        CHK(hipMalloc((void**)&b->d_active, b->max_frames));
         CHK(hipMalloc((void**)&b->d_tbits, b->max_frames * sizeof(unsigned long long)));
+      }
+      if (!b->h_active) {
+        CHK(hipHostMalloc((void**)&b->h_active, b->max_frames, 0));
+        CHK(hipMalloc((void**)&b->d_active, b->max_frames));
       }
       CHK(hipMemcpyAsync(b->h_state, b->d_rerun, (size_t)n * VP8G_RERUN_STATE_BYTES,
                          hipMemcpyDeviceToHost, st));
@@ -421,6 +440,29 @@ static int run_passes(WebPGpuBatch* b, int n) {
   if (round == 0) {   /* no frame to encode: keep the K3 timing events valid */
     CHK(hipEventRecord(b->ev[2], st));
     CHK(hipEventRecord(b->ev[3], st));
+  }
+  if (af && round > 0) {   /* VP8StoreFilterStats + VP8AdjustFilterStrength on the device */
+    for (int f = 0; f < n; ++f) {
+      const vp8h_frame* fr = &b->frames[f];
+      vp8g_af_frame* A = &b->h_afp[f];
+      b->h_active[f] = b->err[f] == VP8_ENC_OK && !b->h_results[f].error;
+      A->simple = (uint8_t)fr->f_simple;
+      A->sharpness = (uint8_t)fr->filter_sharpness;
+      for (int s = 0; s < 4; ++s) {
+        A->level0[s] = (uint8_t)fr->seg_fstrength[s];
+        A->quant[s] = (uint8_t)fr->seg_quant[s];
+      }
+    }
+    CHK(hipMemcpyAsync(b->d_afp, b->h_afp, n * sizeof(vp8g_af_frame), hipMemcpyHostToDevice, st));
+    CHK(hipMemcpyAsync(b->d_active, b->h_active, n, hipMemcpyHostToDevice, st));
+    if (!vp8g_launch_autofilter(b->d_yuv, b->yfb, b->w, b->h, n, b->d_mbinfo, b->d_recon,
+                                b->d_afp, b->d_active, b->d_mbval, b->d_aflevel, st))
+      return 0;
+    CHK(hipMemcpyAsync(b->h_aflevel, b->d_aflevel, n * 4, hipMemcpyDeviceToHost, st));
+    CHK(hipStreamSynchronize(st));
+    for (int f = 0; f < n; ++f)
+      if (b->h_active[f])
+        for (int s = 0; s < 4; ++s) b->frames[f].seg_fstrength[s] = b->h_aflevel[4 * f + s];
   }
   CHK(hipMemcpyAsync(b->h_mbinfo, b->d_mbinfo, n * nmb * VP8G_MBINFO_BYTES,
                      hipMemcpyDeviceToHost, st));

@@ -40,6 +40,13 @@ struct WebPGpuBatch {
   unsigned long long* d_tbits;
   unsigned long long* h_tbits;
   int* fin_cost;             /* FinalizeTokenProbas header cost per frame */
+  /* autofilter (allocated on first use) */
+  uint8_t* d_recon;          /* reconstructed MBs, n x nmb x 512 */
+  double* d_mbval;           /* per-MB SSIM per level, n x nmb x 64 */
+  vp8g_af_frame* d_afp;
+  vp8g_af_frame* h_afp;
+  uint8_t* d_aflevel;        /* best level per frame and segment */
+  uint8_t* h_aflevel;
   uint8_t* pass_act;         /* frames with a pass to run */
   vp8g_frame_result* d_results;
   uint32_t* d_psize;         /* partition-1 bytes per frame (K4) */

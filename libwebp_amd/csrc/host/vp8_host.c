@@ -51,7 +51,7 @@ int vp8h_use_sharp(const WebPConfig* cfg, int w, int h) {
 int vp8h_frame_init(vp8h_frame* fr, const WebPConfig* cfg, int w, int h) {
   memset(fr, 0, sizeof(*fr));
   if (cfg->method < 3 || cfg->method > 6) return 0;   /* m0-2: non-token loop */
-  if (cfg->autofilter || cfg->low_memory || (cfg->preprocessing & 2)) return 0;
+  if (cfg->low_memory || (cfg->preprocessing & 2)) return 0;
   fr->w = w; fr->h = h;
   fr->mbw = (w + 15) >> 4; fr->mbh = (h + 15) >> 4;
   fr->method = cfg->method;
@@ -80,6 +80,7 @@ int vp8h_frame_init(vp8h_frame* fr, const WebPConfig* cfg, int w, int h) {
   fr->f_sharpness = 0;
   /* InitPassStats (frame_enc.c:47-62), enc->do_search_ (webp_enc.c:114) */
   fr->pass_left = fr->cfg_pass = cfg->pass;
+  fr->autofilter = cfg->autofilter;
   fr->do_search = cfg->target_size > 0 || cfg->target_PSNR > 0;
   fr->do_size_search = cfg->target_size != 0;
   fr->ps_is_first = 1;
@@ -587,8 +588,9 @@ static void put_le32(uint8_t* p, uint32_t v) {
 
 int vp8h_build_p0(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* mbinfo,
                   vp8h_bw* out0, int* hdr_bytes) {
-  /* VP8AdjustFilterStrength without autofilter */
-  if (fr->filter_strength > 0) {
+  /* VP8AdjustFilterStrength (filter_enc.c:194-233): with the autofilter the
+   * engine has already set seg_fstrength from the SSIM statistics */
+  if (!fr->autofilter && fr->filter_strength > 0) {
     int max_level = 0;
     for (int s = 0; s < 4; ++s) {
       const int delta = (res->max_edge[s] * fr->seg_y2ac[s]) >> 3;

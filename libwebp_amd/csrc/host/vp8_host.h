@@ -35,6 +35,7 @@ typedef struct {
   /* filter header */
   int f_simple, f_level, f_sharpness;
   /* multi-pass convergence (PassStats, frame_enc.c:38-80) */
+  int autofilter;   /* segment filter levels from the GPU SSIM search (filter_enc.c:156-212) */
   int cfg_pass, pass_left, is_last_pass, npass, do_search, do_size_search, ps_is_first;
   float ps_dq, ps_q, ps_last_q, ps_qmin, ps_qmax;
   double ps_value, ps_last_value, ps_target;

@@ -56,7 +56,8 @@ typedef struct {
                             the partition-0 re-run of :869-876); 3 the same but
                             the statistics continue from rerun_state (a
                             non-last pass); 2 frame already final: skip */
-  int32_t pad[2];
+  uint64_t recon_addr;   /* device address of this frame's nmb x 512 B
+                            reconstruction buffer (autofilter), or 0 */
 } vp8g_frame_params;
 
 /* per-frame cost state K3 leaves for the next pass: the probabilities the
@@ -108,12 +109,34 @@ int vp8g_launch_analysis(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int 
  * at the start of its tok_cap region (per-MB slots of
  * VP8G_MAX_TOKENS_PER_MB are used as scratch); mboff is scratch of n * nmb
  * uint32 (each MB's offset in the compact stream). trellis != 0 reserves the
- * trellis LDS (method >= 5). */
+ * trellis LDS (method >= 5). recon (n x nmb x 512 bytes, or NULL) receives
+ * each MB's reconstruction in the 32-byte-stride layout of the reference's
+ * yuv_out_ (Y | U | V side by side, src/enc/vp8i_enc.h:72-78) for the
+ * autofilter. */
 int vp8g_launch_encode(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h,
                        int n, const uint8_t* segmap,
                        const vp8g_frame_params* params, uint16_t* tokens,
                        size_t tok_cap, uint8_t* mbinfo, uint32_t* mboff, int trellis,
-                       vp8g_frame_result* results, uint8_t* rerun_state, void* stream);
+                       vp8g_frame_result* results, uint8_t* rerun_state, uint8_t* recon,
+                       void* stream);
+
+/* Autofilter (config->autofilter, filter_enc.c:156-212): per frame the
+ * segment filter levels and the filter header fields used for the search */
+typedef struct {
+  uint8_t simple, sharpness, pad[2];
+  uint8_t level0[4];   /* segment fstrength_ from SetupFilterStrength */
+  uint8_t quant[4];    /* segment quant_ */
+} vp8g_af_frame;
+/* per MB (grid nmb x n): SSIM (GetMBSSIM) of the reconstruction unfiltered
+ * and filtered at every candidate level of its segment (DoFilter) into
+ * mbval[(f * nmb + mb) * 64 + level], 0 elsewhere; then per frame the
+ * raster-order sums per segment and level and the best level per segment
+ * (VP8AdjustFilterStrength) into level[4 * f + s]. src = the source YUV
+ * planes (edge-replicated like VP8IteratorImport). */
+int vp8g_launch_autofilter(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h, int n,
+                           const uint8_t* mbinfo, const uint8_t* recon,
+                           const vp8g_af_frame* afp, const uint8_t* active, double* mbval,
+                           uint8_t* level, void* stream);
 
 /* VP8EstimateTokenSize (token_enc.c:226-247) of each frame's compact token
  * stream under the probabilities at state + f * VP8G_RERUN_STATE_BYTES +

@@ -1,0 +1,55 @@
+"""Regenerate the golden vectors of the lossy encoder-option tests with the
+reference build (oracle/_ref/libwebp_ref.so, compiled from /root/reference by
+oracle/Makefile). Dev container only:
+
+    python tests/golden/make_options_golden.py
+
+For each tests/test_<name>.py in MODULES, its CASES (w, h, syn-v1 frame,
+WebPConfig fields) are encoded by the reference and written to
+tests/golden/<name>_kat.json: input hash, output size and sha256, and the
+Y PSNR / segment levels the reference reports in WebPAuxStats.
+  multipass   config->pass > 1, target_size / target_PSNR, qmin / qmax
+              (src/enc/frame_enc.c:26-80, 783-894)
+  autofilter  config->autofilter (src/enc/filter_enc.c:156-212)
+"""
+import ctypes
+import hashlib
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+from libwebp_amd import abi  # noqa: E402
+from libwebp_amd.synth import syn_v1  # noqa: E402
+
+MODULES = ["multipass", "autofilter"]
+
+
+def main():
+    import importlib
+    ref = abi.bind_encoder_api(ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref",
+                                                        "libwebp_ref.so")))
+    for name in MODULES:
+        write(ref, name, importlib.import_module("test_" + name).CASES)
+
+
+def write(ref, name, cases):
+    out = []
+    for w, h, f, kw in cases:
+        img = syn_v1(w, h, f)
+        data, st = abi.encode_rgba(ref, img, stats=True, **kw)
+        out.append({"w": w, "h": h, "frame": f, "params": kw,
+                    "in_sha": hashlib.sha256(img.tobytes()).hexdigest()[:16],
+                    "size": len(data), "sha256": hashlib.sha256(data).hexdigest(),
+                    "psnr_y": round(float(st.PSNR[0]), 3),
+                    "segment_level": list(st.segment_level)})
+    json.dump({"generator": "tests/golden/make_options_golden.py", "cases": out},
+              open(os.path.join(HERE, name + "_kat.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

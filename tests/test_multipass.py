@@ -4,7 +4,7 @@ InitPassStats / ComputeNextQ, :47-80; VP8EstimateTokenSize,
 src/enc/token_enc.c:226-247).
 
 Parity: bit-exact bitstreams. Golden vectors from the reference build
-(tests/golden/multipass_kat.json, make_multipass_golden.py); the oracle's
+(tests/golden/multipass_kat.json, make_options_golden.py); the oracle's
 restatement is checked against them on CPU, the GPU path (batch and
 WebPEncode) against them and against the oracle.
 """

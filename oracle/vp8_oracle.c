@@ -12,6 +12,7 @@
 #include "vp8_tables.h"
 
 #define BPS 32                    /* scratch stride, src/dsp/dsp.h:28 */
+#define Y_BLK(n) (((n) >> 2) * 4 * BPS + ((n) & 3) * 4)
 #define QFIX 17                   /* src/enc/vp8i_enc.h:112 */
 #define MAX_LEVEL 2047            /* src/enc/vp8i_enc.h:39 */
 #define MAX_VLEVEL 67             /* src/enc/vp8i_enc.h:38 */
@@ -467,7 +468,7 @@ typedef struct {
 
 typedef struct {
   Mtx y1, y2, uv;
-  int alpha, beta, quant, fstrength, max_edge, min_disto;
+  int alpha, beta, quant, fstrength, max_edge, min_disto, i4_penalty;
   int lambda_i16, lambda_i4, lambda_uv, lambda_mode, tlambda;
   int lambda_trellis_i16, lambda_trellis_i4, lambda_trellis_uv;
 } Seg;
@@ -499,6 +500,10 @@ typedef struct {
   /* token buffer */
   uint16_t* tok; size_t ntok, tcap;
   int tok_err;
+  int no_tokens, no_stats;       /* RecordResiduals (stats only) / CodeResiduals (tokens only) */
+  /* VP8EncLoop (m0-2): skip probability (frame_enc.c:99-127) */
+  int nb_skip, use_skip, skip_proba;
+  score_t mb_header_limit;
 } Enc;
 
 typedef struct {
@@ -687,6 +692,28 @@ static int histo_alpha(const uint8_t* src, const uint8_t* pred, int ps,
   return maxv > 1 ? 510 * last / maxv : 0;
 }
 
+/* FastMBAnalyze (analysis_enc.c:255-276), methods 0 and 1: intra-16 DC when
+ * the 16 4x4 block sums vary little, else intra-4 DC; susceptibility 0 */
+static int fast_mb_analyze(It* it, Enc* e) {
+  const int q = (int)e->cfg.quality;
+  const uint32_t thr = 8 + (17 - 8) * q / 100;
+  uint32_t m = 0, m2 = 0;
+  for (int k = 0; k < 16; ++k) {   /* VP8Mean16x4 (dsp/enc.c:594-608): block sums */
+    uint32_t dc = 0;
+    for (int y = 0; y < 4; ++y)
+      for (int x = 0; x < 4; ++x) dc += it->yin[Y_BLK(k) + y * BPS + x];
+    m += dc;
+    m2 += dc * dc;
+  }
+  if (thr * m2 < m * m) {
+    set_i16_mode(it, e, 0);
+  } else {
+    static const uint8_t kDC4[16] = {0};
+    set_i4_modes(it, e, kDC4);
+  }
+  return 0;
+}
+
 static void mb_analyze(It* it, Enc* e, int* alphas, int* sum_a, int* sum_uva) {
   int so[16], po[16], suv[8], puv[8];
   for (int b = 0; b < 16; ++b) { so[b] = (b >> 2) * 4 * BPS + (b & 3) * 4; po[b] = (b >> 2) * 64 + (b & 3) * 4; }
@@ -697,20 +724,27 @@ static void mb_analyze(It* it, Enc* e, int* alphas, int* sum_a, int* sum_uva) {
   }
   const uint8_t* left = it->x ? it->yl : NULL;
   const uint8_t* top = it->y ? it->ytop : NULL;
+  const int mi = it->y * e->mbw + it->x;
   int best_a = -1, best_mode = 0;
-  preds16(it->p16, left, top);
-  for (int m = 0; m < 2; ++m) {   /* DC and TM only (MAX_INTRA16_MODE) */
-    const int a = histo_alpha(it->yin, it->p16[m], 16, so, po, 16);
-    if (a > best_a) { best_a = a; best_mode = m; }
+  set_i16_mode(it, e, 0);   /* MBAnalyze defaults (analysis_enc.c:312-314) */
+  if (e->method <= 1) {
+    best_a = fast_mb_analyze(it, e);
+  } else {
+    preds16(it->p16, left, top);
+    for (int m = 0; m < 2; ++m) {   /* DC and TM only (MAX_INTRA16_MODE) */
+      const int a = histo_alpha(it->yin, it->p16[m], 16, so, po, 16);
+      if (a > best_a) { best_a = a; best_mode = m; }
+    }
+    set_i16_mode(it, e, best_mode);
   }
-  (void)best_mode;
   preds_uv(it->puv, it->x ? it->ul : NULL, it->x ? it->vl : NULL, it->y ? it->uvtop : NULL);
-  int best_uv = -1, smallest = 0;
+  int best_uv = -1, smallest = 0, uv_mode = 0;
   for (int m = 0; m < 2; ++m) {
     const int a = histo_alpha(it->yin, it->puv[m], 16, suv, puv, 8);
     if (a > best_uv) best_uv = a;
-    if (m == 0 || a < smallest) smallest = a;
+    if (m == 0 || a < smallest) { smallest = a; uv_mode = m; }
   }
+  e->mb_uv[mi] = uv_mode;   /* VP8SetIntraUVMode: kept by method 0 (no UV refinement) */
   int a = (3 * best_a + best_uv + 2) >> 2;
   a = clampi(255 - a, 0, 255);
   alphas[a]++;
@@ -889,6 +923,7 @@ static void setup_matrices(Enc* e) {
     m->tlambda = ATLEAST1((tls * q_i4) >> 5);
 #undef ATLEAST1
     m->min_disto = 20 * m->y1.q[0];
+    m->i4_penalty = 1000 * q_i4 * q_i4;
     m->max_edge = 0;
   }
 }
@@ -1177,7 +1212,6 @@ static int trellis(const Enc* e, int16_t in[16], int16_t out[16], int ctx0, int 
 /* ------------------------------------------------------------------------ */
 /* Reconstruction + RD mode search: src/enc/quant_enc.c:772-1398 */
 
-#define Y_BLK(n) (((n) >> 2) * 4 * BPS + ((n) & 3) * 4)
 static const int kUVBlk[8] = {16, 20, 16 + 4 * BPS, 20 + 4 * BPS, 24, 28, 24 + 4 * BPS, 28 + 4 * BPS};
 #define P16_BLK(n) (((n) >> 2) * 64 + ((n) & 3) * 4)
 static const int kUVPred[8] = {0, 4, 64, 68, 8, 12, 72, 76};
@@ -1526,18 +1560,97 @@ static void simple_quantize(It* it, Enc* e, Score* rd) {
   rd->nz = nz;
 }
 
+/* RefineUsingDistortion (quant_enc.c:1248-1350): RD_OPT_NONE (methods 0-2)
+ * picks modes by prediction SSE plus fixed mode costs, no rate */
+static void refine_using_distortion(It* it, Enc* e, int try_both, int refine_uv, Score* rd) {
+  const int mi = it->y * e->mbw + it->x, pw = e->preds_w;
+  const Seg* dq = &e->dqm[e->mb_seg[mi]];
+  score_t best_score = MAX_COST;
+  int nz = 0;
+  int is_i16 = try_both || e->mb_type[mi] == 1;
+  score_t score_i4 = dq->i4_penalty, i4_bit_sum = 0;
+  const score_t bit_limit = try_both ? e->mb_header_limit : MAX_COST;
+  if (is_i16) {
+    int best_mode = -1;
+    for (int mode = 0; mode < 4; ++mode) {
+      const score_t score = (score_t)sse(it->yin, BPS, it->p16[mode], 16, 16, 16) * 256 +
+                            kVP8ModeCostI16[mode] * 106;
+      if (mode > 0 && kVP8ModeCostI16[mode] > bit_limit) continue;
+      if (score < best_score) { best_mode = mode; best_score = score; }
+    }
+    if ((it->x == 0 || it->y == 0) && is_flat_source16(it->yin)) {   /* bug #432 */
+      best_mode = (it->x == 0) ? 0 : 2;
+      try_both = 0;
+    }
+    set_i16_mode(it, e, best_mode);
+  }
+  if (try_both || !is_i16) {
+    Canvas cv;
+    is_i16 = 0;
+    canvas_init(&cv, it, e);
+    for (int i4 = 0; i4 < 16; ++i4) {
+      const int bx = i4 & 3, by = i4 >> 2;
+      const int left = bx == 0 ? it->preds[by * pw - 1] : rd->modes_i4[i4 - 1];
+      const int top = by == 0 ? it->preds[-pw + bx] : rd->modes_i4[i4 - 4];
+      const uint16_t* mcost = kVP8ModeCostI4[top][left];
+      const uint8_t* src = it->yin + Y_BLK(i4);
+      uint8_t ed[13], pred[10][16], rec[16];
+      int best = -1;
+      score_t best_i4 = MAX_COST;
+      canvas_edges(&cv, i4, ed);
+      preds4(pred, ed);
+      for (int mode = 0; mode < 10; ++mode) {
+        const score_t score = (score_t)sse(src, BPS, pred[mode], 4, 4, 4) * 256 + mcost[mode] * 11;
+        if (score < best_i4) { best = mode; best_i4 = score; }
+      }
+      i4_bit_sum += mcost[best];
+      rd->modes_i4[i4] = best;
+      score_i4 += best_i4;
+      if (score_i4 >= best_score || i4_bit_sum > bit_limit) { is_i16 = 1; break; }
+      nz |= recon_i4(it, e, rd->y_ac[i4], src, pred[best], rec, 4, i4) << i4;
+      for (int y = 0; y < 4; ++y) memcpy(it->out2 + Y_BLK(i4) + y * BPS, rec + 4 * y, 4);
+      canvas_put(&cv, i4, rec, 4);
+    }
+  }
+  if (!is_i16) {
+    set_i4_modes(it, e, rd->modes_i4);
+    { uint8_t* o = it->out; it->out = it->out2; it->out2 = o; }
+    best_score = score_i4;
+  } else {
+    nz = recon_i16(it, e, rd, it->out, it->preds[0]);
+  }
+  if (refine_uv) {
+    int best_mode = -1;
+    score_t best_uv = MAX_COST;
+    for (int mode = 0; mode < 4; ++mode) {
+      const score_t score = (score_t)sse(it->yin + 16, BPS, it->puv[mode], 16, 16, 8) * 256 +
+                            kVP8ModeCostUV[mode] * 120;
+      if (score < best_uv) { best_mode = mode; best_uv = score; }
+    }
+    e->mb_uv[mi] = best_mode;
+  }
+  nz |= recon_uv(it, e, rd, it->out, e->mb_uv[mi]);
+  rd->nz = nz;
+  rd->score = best_score;
+}
+
 static int decimate(It* it, Enc* e, Score* rd) {   /* :1364-1398 */
   memset(rd, 0, sizeof(*rd));
   rd->score = MAX_COST;
   preds16(it->p16, it->x ? it->yl : NULL, it->y ? it->ytop : NULL);
   preds_uv(it->puv, it->x ? it->ul : NULL, it->x ? it->vl : NULL, it->y ? it->uvtop : NULL);
-  it->do_trellis = e->rd_opt >= 3;
-  pick_i16(it, e, rd);
-  if (e->method >= 2) pick_i4(it, e, rd);
-  pick_uv(it, e, rd);
-  if (e->rd_opt == 2) {
-    it->do_trellis = 1;
-    simple_quantize(it, e, rd);
+  if (e->rd_opt == 0) {   /* RD_OPT_NONE */
+    it->do_trellis = 0;
+    refine_using_distortion(it, e, e->method >= 2, e->method >= 1, rd);
+  } else {
+    it->do_trellis = e->rd_opt >= 3;
+    pick_i16(it, e, rd);
+    if (e->method >= 2) pick_i4(it, e, rd);
+    pick_uv(it, e, rd);
+    if (e->rd_opt == 2) {
+      it->do_trellis = 1;
+      simple_quantize(it, e, rd);
+    }
   }
   const int skip = rd->nz == 0;
   e->mb_skip[it->y * e->mbw + it->x] = skip;
@@ -1549,6 +1662,7 @@ static int decimate(It* it, Enc* e, Score* rd) {   /* :1364-1398 */
  * cost_enc.h:45-56 */
 
 static inline void tok_push(Enc* e, uint32_t t) {
+  if (e->no_tokens) return;
   if (e->ntok == e->tcap) {
     size_t n = e->tcap ? 2 * e->tcap : 65536;
     uint16_t* p = (uint16_t*)realloc(e->tok, n * sizeof(*p));
@@ -1565,7 +1679,7 @@ static inline void record(uint32_t* s, int bit) {
 /* dynamic-probability token: slot id for the proba, separate stats slot */
 static inline int tok_dyn(Enc* e, int bit, int proba_id, uint32_t* stat) {
   tok_push(e, ((uint32_t)bit << 15) | proba_id);
-  record(stat, bit);
+  if (!e->no_stats) record(stat, bit);
   return bit;
 }
 static inline void tok_fix(Enc* e, int bit, int proba) {
@@ -1612,11 +1726,13 @@ static int record_block(Enc* e, int ctx, int type, int first, const int16_t* lv)
           tok_dyn(e, 0, base + 8, s + 8); tok_dyn(e, 1, base + 9, s + 9);
           res -= 8 << 1; mask = 1 << 3; tab = kVP8Cat4;
         } else if (res < (8 << 3)) {
-          /* proba slot 10, but the statistic lands in slot 9 (token_enc.c:168) */
-          tok_dyn(e, 1, base + 8, s + 8); tok_dyn(e, 0, base + 10, s + 9);
+          /* proba slot 10, but the token recorder's statistic lands in slot 9
+           * (token_enc.c:168); RecordResiduals' VP8RecordCoeffs uses slot 10
+           * (cost_enc.c:315-318) */
+          tok_dyn(e, 1, base + 8, s + 8); tok_dyn(e, 0, base + 10, s + (e->no_tokens ? 10 : 9));
           res -= 8 << 2; mask = 1 << 4; tab = kVP8Cat5;
         } else {
-          tok_dyn(e, 1, base + 8, s + 8); tok_dyn(e, 1, base + 10, s + 9);
+          tok_dyn(e, 1, base + 8, s + 8); tok_dyn(e, 1, base + 10, s + (e->no_tokens ? 10 : 9));
           res -= 8 << 3; mask = 1 << 10; tab = kVP8Cat6;
         }
         for (; mask; mask >>= 1) tok_fix(e, (res & mask) != 0, *tab++);
@@ -1669,6 +1785,7 @@ static void code_intra_modes(Enc* e, BW* bw) {
         if (bw_put(bw, s >= 2, p[0])) p += 1;
         bw_put(bw, s & 1, p[1]);
       }
+      if (e->use_skip) bw_put(bw, e->mb_skip[i], e->skip_proba);   /* tree_enc.c:323-325 */
       if (bw_put(bw, e->mb_type[i] != 0, 145)) {
         const int m = preds[0];
         if (bw_put(bw, m == 1 || m == 3, 156)) bw_put(bw, m == 1, 128);
@@ -1736,7 +1853,7 @@ static size_t write_stream(Enc* e, BW* part1, uint8_t** out) {
           if (bw_put(&bw, v != kVP8CoeffProba0[t][b][c][p], kVP8CoeffUpdateProba[t][b][c][p]))
             bw_put_bits(&bw, v, 8);
         }
-  bw_put_uniform(&bw, 0);       /* no skip proba */
+  if (bw_put_uniform(&bw, e->use_skip)) bw_put_bits(&bw, e->skip_proba, 8);   /* tree_enc.c:500-502 */
   code_intra_modes(e, &bw);
   bw_finish(&bw);
   if (bw.error || part1->error || bw.pos >= (1u << 19)) { free(bw.buf); return 0; }
@@ -1974,12 +2091,93 @@ void vp8o_default_config(vp8o_config* c) {   /* config_enc.c:24-98 */
   c->pass = 1; c->qmin = 0; c->qmax = 100;
 }
 
+/* VP8EncLoop (frame_enc.c:740-775) for methods 0-2: StatLoop (:614-674,
+ * without search) collects the token statistics over the first MBs
+ * (method 0: a quarter of them) and the skip count, then the final pass codes
+ * every MB with the final probabilities, skipping the residuals of all-zero
+ * MBs when the skip probability pays (FinalizeSkipProba, :111-127). With
+ * RD_OPT_NONE the decisions do not depend on the statistics, so both passes
+ * decide the same. */
+static void enc_loop(Enc* e, const vp8o_config* cfg, vp8o_mb_trace* trace, double (*lf)[64]) {
+  const int nmb = e->mbw * e->mbh;
+  int nb = nmb;
+  It it;
+  int stats_ok = 1;
+  if (e->method == 0) nb = (nmb > 200) ? nmb >> 2 : 50;   /* fast probe */
+  memset(e->stats, 0, sizeof(e->stats));
+  g_passes = 0;
+  for (int pass = 0; pass < (cfg->pass < 1 ? 1 : cfg->pass); ++pass) {   /* OneStatPass */
+    int left = nb;
+    it_reset(&it, e);
+    const float q = cfg->quality < (float)cfg->qmin ? (float)cfg->qmin
+                  : cfg->quality > (float)cfg->qmax ? (float)cfg->qmax : cfg->quality;
+    set_segment_params(e, q < 0.f ? 0.f : q > 100.f ? 100.f : q);
+    set_segment_probas(e);
+    level_costs(e);
+    e->nb_skip = 0;
+    e->no_tokens = 1;
+    do {
+      Score rd;
+      it_import(&it, e);
+      if (decimate(&it, e, &rd)) ++e->nb_skip;
+      record_tokens(&it, e, &rd);   /* RecordResiduals: statistics only */
+      it_save_boundary(&it, e);
+    } while (it_next(&it, e) && --left > 0);
+    ++g_passes;
+    /* OneStatPass returns the header estimate: the mode costs (0 with
+     * RD_OPT_NONE) plus the segment header, and StatLoop gives up when it is
+     * 0 (frame_enc.c:645-646), before FinalizeSkipProba/FinalizeTokenProbas:
+     * default probabilities and no skip flags then */
+    if (e->seg_hdr_size == 0) { stats_ok = 0; break; }
+    if (e->max_i4_header_bits == 0) break;   /* is_last_pass */
+  }
+  e->no_tokens = 0;
+  if (stats_ok) {   /* FinalizeSkipProba + FinalizeTokenProbas */
+    e->skip_proba = nmb ? (int)((uint64_t)(nmb - e->nb_skip) * 255 / nmb) : 255;
+    e->use_skip = e->skip_proba < 250;
+    finalize_token_probas(e);
+    level_costs(e);
+  } else {
+    e->use_skip = 0;
+  }
+  /* final pass */
+  if (lf) memset(lf, 0, 4 * 64 * sizeof(double));
+  e->no_stats = 1;
+  e->ntok = 0;
+  it_reset(&it, e);
+  do {
+    Score rd;
+    it_import(&it, e);
+    const int skip = decimate(&it, e, &rd);
+    e->no_tokens = skip && e->use_skip;   /* ResetAfterSkip == the nz of coding zeros */
+    record_tokens(&it, e, &rd);
+    e->no_tokens = 0;
+    if (trace) {
+      vp8o_mb_trace* t = &trace[it.y * e->mbw + it.x];
+      const int mi = it.y * e->mbw + it.x;
+      t->segment = e->mb_seg[mi]; t->type = e->mb_type[mi];
+      t->uv_mode = e->mb_uv[mi]; t->skip = e->mb_skip[mi];
+      t->alpha = e->mb_alpha[mi];
+      for (int k = 0; k < 16; ++k) t->modes[k] = it.preds[(k >> 2) * e->preds_w + (k & 3)];
+      memcpy(t->y_dc, rd.y_dc, sizeof(t->y_dc));
+      memcpy(t->y_ac, rd.y_ac, sizeof(t->y_ac));
+      memcpy(t->uv, rd.uv, sizeof(t->uv));
+    }
+    if (lf) store_filter_stats(&it, e, lf);
+    it_save_boundary(&it, e);
+  } while (it_next(&it, e));
+  e->no_stats = 0;
+}
+
 size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
                        int w, int h, int ys, int uvs, const vp8o_config* cfg,
                        uint8_t** out, vp8o_mb_trace* trace) {
   Enc* e = (Enc*)calloc(1, sizeof(Enc));
   size_t result = 0;
-  if (!e || cfg->method < 3 || cfg->method > 6) { free(e); return 0; }
+  if (!e || cfg->method < 0 || cfg->method > 6) { free(e); return 0; }
+  /* methods 0-2 with a size / PSNR search take StatLoop's RD_OPT_BASIC
+   * passes (frame_enc.c:614-674): not restated */
+  if (cfg->method < 3 && (cfg->target_size > 0 || cfg->target_PSNR > 0)) { free(e); return 0; }
   e->Y = Y; e->U = U; e->V = V; e->ys = ys; e->uvs = uvs; e->w = w; e->h = h;
   e->mbw = (w + 15) >> 4; e->mbh = (h + 15) >> 4;
   e->cfg = *cfg;
@@ -1998,7 +2196,8 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
     e->top_derr = calloc(e->mbw, sizeof(*e->top_derr));
   /* MapConfigToTools, webp_enc.c:95-123 */
   e->method = cfg->method;
-  e->rd_opt = cfg->method >= 6 ? 3 : cfg->method >= 5 ? 2 : 1;
+  e->rd_opt = cfg->method >= 6 ? 3 : cfg->method >= 5 ? 2 : cfg->method >= 3 ? 1 : 0;
+  e->mb_header_limit = (score_t)256 * 510 * 8 * 1024 / (e->mbw * e->mbh);   /* webp_enc.c:109 */
   {
     const int lim = 100 - cfg->partition_limit;
     e->max_i4_header_bits = 256 * 16 * 16 * (lim * lim) / (100 * 100);
@@ -2012,83 +2211,87 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
 
   analyze(e);
 
-  /* VP8EncTokenLoop (frame_enc.c:783-894): `pass` entropy passes, the
-   * size / PSNR search of InitPassStats / ComputeNextQ (:47-80) and the
-   * partition-0 overflow retry (:869-876) */
-  g_passes = 0;
-  const int max_count = (nmb >> 3) < 96 ? 96 : (nmb >> 3);
   BW part1;
   bw_init(&part1);
   It it;
-  PassStats ps;
-  init_pass_stats(&ps, cfg);
-  const int do_search = cfg->target_size > 0 || cfg->target_PSNR > 0;
-  const uint64_t pixel_count = (uint64_t)nmb * 384;
-  int num_pass_left = cfg->pass < 1 ? 1 : cfg->pass;
   double (*lf)[64] = cfg->autofilter ? (double (*)[64])calloc(4 * 64, sizeof(double)) : NULL;
-  while (num_pass_left-- > 0) {
-    const int is_last_pass = (fabs(ps.dq) <= DQ_LIMIT) || (num_pass_left == 0) ||
-                             (e->max_i4_header_bits == 0);
-    uint64_t size_p0 = 0, distortion = 0;
-    int cnt = max_count;
-    it_reset(&it, e);
-    /* SetLoopParams (:563-572) */
-    const float q = ps.q < 0.f ? 0.f : ps.q > 100.f ? 100.f : ps.q;
-    set_segment_params(e, q);
-    set_segment_probas(e);
-    level_costs(e);
-    if (is_last_pass) memset(e->stats, 0, sizeof(e->stats));
-    if (is_last_pass && lf) memset(lf, 0, 4 * 64 * sizeof(double));   /* VP8InitFilter */
-    e->ntok = 0;
-    do {
-      Score rd;
-      it_import(&it, e);
-      if (--cnt < 0) {
-        finalize_token_probas(e);
-        level_costs(e);
-        cnt = max_count;
+  if (e->rd_opt == 0) {
+    enc_loop(e, cfg, trace, lf);
+  } else {
+    /* VP8EncTokenLoop (frame_enc.c:783-894): `pass` entropy passes, the
+     * size / PSNR search of InitPassStats / ComputeNextQ (:47-80) and the
+     * partition-0 overflow retry (:869-876) */
+    g_passes = 0;
+    const int max_count = (nmb >> 3) < 96 ? 96 : (nmb >> 3);
+    PassStats ps;
+    init_pass_stats(&ps, cfg);
+    const int do_search = cfg->target_size > 0 || cfg->target_PSNR > 0;
+    const uint64_t pixel_count = (uint64_t)nmb * 384;
+    int num_pass_left = cfg->pass < 1 ? 1 : cfg->pass;
+    while (num_pass_left-- > 0) {
+      const int is_last_pass = (fabs(ps.dq) <= DQ_LIMIT) || (num_pass_left == 0) ||
+                               (e->max_i4_header_bits == 0);
+      uint64_t size_p0 = 0, distortion = 0;
+      int cnt = max_count;
+      it_reset(&it, e);
+      /* SetLoopParams (:563-572) */
+      const float q = ps.q < 0.f ? 0.f : ps.q > 100.f ? 100.f : ps.q;
+      set_segment_params(e, q);
+      set_segment_probas(e);
+      level_costs(e);
+      if (is_last_pass) memset(e->stats, 0, sizeof(e->stats));
+      if (is_last_pass && lf) memset(lf, 0, 4 * 64 * sizeof(double));   /* VP8InitFilter */
+      e->ntok = 0;
+      do {
+        Score rd;
+        it_import(&it, e);
+        if (--cnt < 0) {
+          finalize_token_probas(e);
+          level_costs(e);
+          cnt = max_count;
+        }
+        decimate(&it, e, &rd);
+        record_tokens(&it, e, &rd);
+        size_p0 += rd.H;
+        distortion += rd.D;
+        if (is_last_pass && lf) store_filter_stats(&it, e, lf);
+        if (trace && is_last_pass) {
+          vp8o_mb_trace* t = &trace[it.y * e->mbw + it.x];
+          const int mi = it.y * e->mbw + it.x;
+          t->segment = e->mb_seg[mi]; t->type = e->mb_type[mi];
+          t->uv_mode = e->mb_uv[mi]; t->skip = e->mb_skip[mi];
+          t->alpha = e->mb_alpha[mi];
+          for (int k = 0; k < 16; ++k) t->modes[k] = it.preds[(k >> 2) * e->preds_w + (k & 3)];
+          memcpy(t->y_dc, rd.y_dc, sizeof(t->y_dc));
+          memcpy(t->y_ac, rd.y_ac, sizeof(t->y_ac));
+          memcpy(t->uv, rd.uv, sizeof(t->uv));
+        }
+        it_save_boundary(&it, e);
+      } while (it_next(&it, e));
+      size_p0 += e->seg_hdr_size;
+      ++g_passes;
+      g_size_p0 = size_p0;
+      if (e->tok_err) break;
+      if (ps.do_size_search) {
+        uint64_t size = (uint64_t)finalize_token_probas(e);
+        size += estimate_token_size(e);
+        size = (size + size_p0 + 1024) >> 11;
+        size += HEADER_SIZE_ESTIMATE;
+        ps.value = (double)size;
+      } else {
+        ps.value = psnr_of(distortion, pixel_count);
       }
-      decimate(&it, e, &rd);
-      record_tokens(&it, e, &rd);
-      size_p0 += rd.H;
-      distortion += rd.D;
-      if (is_last_pass && lf) store_filter_stats(&it, e, lf);
-      if (trace && is_last_pass) {
-        vp8o_mb_trace* t = &trace[it.y * e->mbw + it.x];
-        const int mi = it.y * e->mbw + it.x;
-        t->segment = e->mb_seg[mi]; t->type = e->mb_type[mi];
-        t->uv_mode = e->mb_uv[mi]; t->skip = e->mb_skip[mi];
-        t->alpha = e->mb_alpha[mi];
-        for (int k = 0; k < 16; ++k) t->modes[k] = it.preds[(k >> 2) * e->preds_w + (k & 3)];
-        memcpy(t->y_dc, rd.y_dc, sizeof(t->y_dc));
-        memcpy(t->y_ac, rd.y_ac, sizeof(t->y_ac));
-        memcpy(t->uv, rd.uv, sizeof(t->uv));
+      if (e->max_i4_header_bits > 0 && size_p0 > P0_LIMIT) {
+        ++num_pass_left;
+        e->max_i4_header_bits >>= 1;
+        continue;
       }
-      it_save_boundary(&it, e);
-    } while (it_next(&it, e));
-    size_p0 += e->seg_hdr_size;
-    ++g_passes;
-    g_size_p0 = size_p0;
-    if (e->tok_err) break;
-    if (ps.do_size_search) {
-      uint64_t size = (uint64_t)finalize_token_probas(e);
-      size += estimate_token_size(e);
-      size = (size + size_p0 + 1024) >> 11;
-      size += HEADER_SIZE_ESTIMATE;
-      ps.value = (double)size;
-    } else {
-      ps.value = psnr_of(distortion, pixel_count);
+      if (is_last_pass) break;
+      if (do_search) compute_next_q(&ps);
     }
-    if (e->max_i4_header_bits > 0 && size_p0 > P0_LIMIT) {
-      ++num_pass_left;
-      e->max_i4_header_bits >>= 1;
-      continue;
-    }
-    if (is_last_pass) break;
-    if (do_search) compute_next_q(&ps);
   }
   if (e->tok_err) goto done;
-  finalize_token_probas(e);
+  if (e->rd_opt > 0) finalize_token_probas(e);   /* enc_loop has settled its probabilities */
   for (size_t k = 0; k < e->ntok; ++k) {
     const uint16_t t = e->tok[k];
     const int bit = t >> 15;

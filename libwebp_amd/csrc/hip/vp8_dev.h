@@ -452,8 +452,10 @@ __device__ __forceinline__ void record_stat(uint32_t* s, int bit) {
 
 // Token generation for one block (token_enc.c:113-193). mode 0: count only;
 // 1: write tokens + accumulate LDS stat deltas; 2: replay stats for marked
-// slots (exact saturation order).
-template <int MODE, class LDS>
+// slots (exact saturation order). RC: statistics with VP8RecordCoeffs' slots
+// (cost_enc.c:289-340, the statistics pass of methods 0-2), which put the
+// second category bit of cat5/cat6 in slot 10 where the token recorder uses 9.
+template <int MODE, class LDS, bool RC = false>
 __device__ int gen_tokens(LDS& L, const int16_t* lv, int type, int first, int ctx,
                           uint16_t* out, int* nz_out) {
   int last = -1;
@@ -509,10 +511,10 @@ __device__ int gen_tokens(LDS& L, const int16_t* lv, int type, int first, int ct
           dyn(0, base + 8, base + 8); dyn(1, base + 9, base + 9);
           res -= 8 << 1; mask = 1 << 3; tab = kVP8Cat4;
         } else if (res < (8 << 3)) {
-          dyn(1, base + 8, base + 8); dyn(0, base + 10, base + 9);  // token_enc.c:168
+          dyn(1, base + 8, base + 8); dyn(0, base + 10, base + (RC ? 10 : 9));  // token_enc.c:168
           res -= 8 << 2; mask = 1 << 4; tab = kVP8Cat5;
         } else {
-          dyn(1, base + 8, base + 8); dyn(1, base + 10, base + 9);
+          dyn(1, base + 8, base + 8); dyn(1, base + 10, base + (RC ? 10 : 9));
           res -= 8 << 3; mask = 1 << 10; tab = kVP8Cat6;
         }
         for (; mask; mask >>= 1) fix((res & mask) != 0, *tab++);

@@ -1679,6 +1679,8 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
       R->size_p0 = G.fs.size_p0;
       R->sse[0] = G.fs.sse[0]; R->sse[1] = G.fs.sse[1]; R->sse[2] = G.fs.sse[2];
       R->distortion = G.fs.dist;
+      R->use_skip = 0;     // the token loop never uses the skip flag (frame_enc.c:805)
+      R->skip_proba = 255;
       R->block_count[0] = G.fs.nb[0]; R->block_count[1] = G.fs.nb[1];
       R->block_count[2] = G.fs.nb[2];
 #if defined(K3_STAMPS)

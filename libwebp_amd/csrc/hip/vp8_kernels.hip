@@ -198,12 +198,14 @@ struct K2Wave {
   uint8_t yl[17], ul[9], vl[9];
   uint8_t top[32];
   int hist[4][32];
+  uint32_t dc[16];
 };
 
 __global__ __launch_bounds__(256) void k_analyze(const uint8_t* __restrict__ yuv, size_t yfb,
                                                  int w, int h, int nmb,
                                                  uint8_t* __restrict__ mb_alpha,
-                                                 uint16_t* __restrict__ mb_uva) {
+                                                 uint16_t* __restrict__ mb_uva, int fast_q,
+                                                 uint8_t* __restrict__ mb_amode) {
   __shared__ K2Wave S[4];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int mb = blockIdx.x * 4 + wave;
@@ -293,6 +295,11 @@ __global__ __launch_bounds__(256) void k_analyze(const uint8_t* __restrict__ yuv
       atomicAdd(&L.hist[hsel][v], 1);
     }
   }
+  if (fast_q >= 0 && lane < 16) {   // VP8Mean16x4 block sums (dsp/enc.c:594-608)
+    uint32_t dc = 0;
+    for (int k = 0; k < 16; ++k) dc += L.yin[(4 * (lane >> 2) + (k >> 2)) * BPS + 4 * (lane & 3) + (k & 3)];
+    L.dc[lane] = dc;
+  }
   __syncthreads();
   if (lane == 0) {
     int alpha[4];
@@ -310,6 +317,19 @@ __global__ __launch_bounds__(256) void k_analyze(const uint8_t* __restrict__ yuv
     int best_uv = -1;
     if (alpha[2] > best_uv) best_uv = alpha[2];
     if (alpha[3] > best_uv) best_uv = alpha[3];
+    // analysis modes for the RD_OPT_NONE encoder (methods 0-2): the UV mode
+    // of smallest alpha (analysis_enc.c:278-305) and, for methods 0-1,
+    // FastMBAnalyze's intra-16 / intra-4 pick with susceptibility 0 (:255-276)
+    int i4 = 0;
+    if (fast_q >= 0) {
+      const uint32_t thr = 8 + (17 - 8) * fast_q / 100;
+      uint32_t m = 0, m2 = 0;
+      for (int k = 0; k < 16; ++k) { m += L.dc[k]; m2 += L.dc[k] * L.dc[k]; }
+      i4 = !(thr * m2 < m * m);
+      best = 0;
+    }
+    if (mb_amode != nullptr)
+      mb_amode[(size_t)f * nmb + mb] = (uint8_t)((alpha[3] < alpha[2] ? 1 : 0) | (i4 << 1));
     int a = (3 * best + best_uv + 2) >> 2;
     a = 255 - a;
     a = a < 0 ? 0 : a > 255 ? 255 : a;
@@ -569,9 +589,14 @@ struct I4Result {
 // the macroblock-boundary flags only (the reference never updates them
 // inside that loop). Reconstruction lands in acc_out, levels in acc_ac.
 template <bool TRELLIS>
+// search: 0 = reconstruct L.modes; 1 = RD search (PickBestIntra4,
+// quant_enc.c:1072-1165); 2 = distortion search of RD_OPT_NONE
+// (RefineUsingDistortion, :1287-1320): prediction SSE + fixed mode cost,
+// running score from the segment's i4_penalty, abort against rd_score (the
+// intra-16 distortion score) or max_bits
 __device__ I4Result run_i4(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane, int x,
                            int mbw, const uint8_t* predtop, const uint8_t* yl,
-                           const uint8_t* yt, bool search, score_t rd_score, int max_bits) {
+                           const uint8_t* yt, int search, score_t rd_score, int max_bits) {
   constexpr bool trellis = TRELLIS;
   for (int k = lane; k < 21; k += 64) {
     uint8_t v;
@@ -583,7 +608,7 @@ __device__ I4Result run_i4(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int la
   if (lane < 16) L.canvas[1 + lane][0] = yl[lane];
   uint32_t tnz = ctx.t & 0xf, lnz = ctx.l & 0xf;
   score_t accD = 0, accSD = 0, accR = 0, accH = 211;
-  score_t acc_score = accH * S.lambda_mode;
+  score_t acc_score = search == 2 ? (score_t)S.i4_penalty : accH * S.lambda_mode;
   uint32_t acc_nz = 0;
   int total_hdr = 0;
   I4Result res;
@@ -631,7 +656,8 @@ __device__ I4Result run_i4(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int la
         nz = quantize_block(c, L.lv4[m], &S.y1, lvr);
       }
       idct4(L.pred4[m], 4, c, L.rec4[m], 4);
-      if (search) {
+      if (search == 2) L.r4[m][6] = sse4(src, BPS, L.pred4[m], 4);
+      if (search == 1) {
         const int D = sse4(src, BPS, L.rec4[m], 4);
         const int SD = S.tlambda ? (S.tlambda * (iabs_(hadamard_w(L.rec4[m], 4) -
                                                         hadamard_w(src, BPS)) >> 5) + 128) >> 8
@@ -649,7 +675,20 @@ __device__ I4Result run_i4(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int la
     __syncthreads();
     int bm;
     int bnz;
-    if (search) {
+    if (search == 2) {
+      bm = -1;
+      score_t bscore = MAX_COST;
+      for (int m = 0; m < 10; ++m) {
+        const score_t sc = (score_t)L.r4[m][6] * 256 + L.mcost4[(top_m * 10 + left_m) * 10 + m] * 11;
+        if (sc < bscore) { bm = m; bscore = sc; }
+      }
+      total_hdr += L.mcost4[(top_m * 10 + left_m) * 10 + bm];
+      acc_score += bscore;
+      if (lane == 0) L.modes[i4] = (uint8_t)bm;
+      if (acc_score >= rd_score || total_hdr > max_bits) { res.ok = 0; break; }
+      bnz = L.r4[bm][5];
+      acc_nz |= (uint32_t)(bnz ? 1 : 0) << i4;
+    } else if (search) {
       bm = -1;
       score_t bscore = MAX_COST, bD = 0, bSD = 0, bR = 0, bH = 0;
       bnz = 0;
@@ -682,7 +721,7 @@ __device__ I4Result run_i4(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int la
       L.acc_out[(4 * by + py) * 16 + 4 * bx + px] = v;
       L.acc_ac[i4][lane] = L.lv4[bm][lane];
     }
-    if (search) {
+    if (search == 1) {
       if (lane == 0) L.modes[i4] = (uint8_t)bm;
       tnz = (tnz & ~(1u << bx)) | ((bnz ? 1u : 0u) << bx);
       lnz = (lnz & ~(1u << by)) | ((bnz ? 1u : 0u) << by);
@@ -715,8 +754,15 @@ struct K3ArgsW1 {
   size_t tok_cap;
   uint8_t* mbinfo;
   vp8g_frame_result* results;
+  // RD_OPT_NONE (methods 0-2) only
+  const uint8_t* amode;   // K2 analysis modes
+  uint32_t* mboff;        // per-MB token offsets (skip compaction)
+  uint8_t* rerun;         // statistics carried between passes
 };
 
+// NONE: the methods 0-2 encoder (RefineUsingDistortion, VP8EncLoop); else the
+// single-wavefront diagnostic twin of K3 (WEBP_AMD_K3=1)
+template <bool NONE>
 __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
   extern __shared__ __align__(16) uint8_t smem[];
   K3Lds& L = *reinterpret_cast<K3Lds*>(smem);
@@ -740,14 +786,19 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
   uint8_t* mbinfo = a.mbinfo + (size_t)f * nmb * VP8G_MBINFO_BYTES;
   // this single-wavefront diagnostic kernel keeps no re-run state: it skips
   // final frames and refuses a partition-0 re-run (error 3)
-  if (P->pass_mode != 0) {
-    if ((P->pass_mode == 1 || P->pass_mode == 3) && lane == 0) a.results[f].error = 3;
+  if (P->pass_mode == 2) return;
+  if (P->pass_mode != 0 && !(NONE && P->pass_mode == 3)) {
+    if (lane == 0) a.results[f].error = 3;
     return;
   }
+  uint32_t* rstats =
+      NONE ? reinterpret_cast<uint32_t*>(a.rerun + (size_t)f * VP8G_RERUN_STATE_BYTES +
+                                         VP8G_STATE_STATS)
+           : nullptr;
 
   // ---- frame init
   for (int s = lane; s < NSLOT; s += 64) {
-    L.stats[s] = 0;
+    L.stats[s] = (NONE && P->pass_mode == 3) ? rstats[s] : 0u;   // StatLoop keeps them
     L.delta[s] = 0;
     L.coeffs[s] = (&kVP8CoeffProba0[0][0][0][0])[s];
   }
@@ -774,7 +825,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
   int cnt = max_count;
   if (lane < 4) L.max_edge[lane] = 0;
   uint64_t size_p0 = 0, sse_acc[3] = {0, 0, 0};
-  int nb_i4 = 0, nb_i16 = 0, nb_skip = 0;
+  int nb_i4 = 0, nb_i16 = 0, nb_skip = 0, nb_skip_stat = 0;
   uint32_t ntok = 0;
   int tok_err = 0;
   int left_dc = 0;
@@ -797,7 +848,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
       left_dc = 0;
     }
     load_mb(Yp, Up, Vp, w, h, x, y, L.yin, lane, 64);
-    if (--cnt < 0) {
+    if (!NONE && --cnt < 0) {   // StatLoop never refreshes the probabilities
       if (finalize_probas(L, lane)) level_costs(L, lane);
       cnt = max_count;
     }
@@ -827,137 +878,223 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
     __syncthreads();
 
     K3_STAMP(0);
-    // ---- Intra16 (quant_enc.c:1002-1058)
-    const bool trellis_all = rd_opt >= 3;
-    if (trellis_all) eval_i16<true>(L, S, ctx, lane);
-    else eval_i16<false>(L, S, ctx, lane);
-    score_t best16_score = 0;
-    int best16 = 0;
-    uint32_t nz16 = 0;
-    score_t D16 = 0, SD16 = 0, H16 = 0, R16 = 0;
-    {
-      int same = 1;
-      const int v0 = L.yin[0];
-      for (int k = lane; k < 256; k += 64) same &= (L.yin[(k >> 4) * BPS + (k & 15)] == v0);
-      int flat = __all(same);
-      for (int mm = 0; mm < 4; ++mm) {
-        score_t Dm = L.mres[mm][0];
-        score_t SDm = S.tlambda ? (score_t)((S.tlambda * L.mres[mm][1] + 128) >> 8) : 0;
-        const score_t Hm = kVP8ModeCostI16[mm];
-        const score_t Rm = L.mres[mm][2];
-        if (flat) {
-          flat = (L.mres[mm][3] & 0xffff) == 0;
-          if (flat) { Dm *= 2; SDm *= 2; }
-        }
-        const score_t sc = (Rm + Hm) * S.lambda_i16 + 256 * (Dm + SDm);
-        if (mm == 0 || sc < best16_score) {
-          best16_score = sc; best16 = mm;
-          D16 = Dm; SD16 = SDm; H16 = Hm; R16 = Rm;
-          nz16 = (uint32_t)L.mres[mm][3];
-        }
-      }
-    }
-    // commit I16 as current best
-    for (int k = lane; k < 256; k += 64) L.yout[(k >> 4) * BPS + (k & 15)] = L.rec16[best16][k];
-    for (int k = lane; k < 256; k += 64) (&L.fin_ac[0][0])[k] = (&L.lv16[best16][0][0])[k];
-    if (lane < 16) { L.fin_dc[lane] = L.lvdc[best16][lane]; L.modes[lane] = best16; }
-    score_t rd_score = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
-    score_t rdH = H16;
-    uint32_t rd_nz = nz16;
-    int is_i16 = 1;
-    if ((rd_nz & 0x100ffff) == 0x1000000 && D16 > S.min_disto) {
-      int mv = iabs_(L.lvdc[best16][1]);
-      mv = max(mv, iabs_(L.lvdc[best16][2]));
-      mv = max(mv, iabs_(L.lvdc[best16][4]));
-      if (lane == 0 && mv > L.max_edge[segid]) L.max_edge[segid] = mv;
-    }
-    __syncthreads();
-
-    K3_STAMP(1);
-    // ---- Intra4 (quant_enc.c:1072-1165)
-    if (max_i4_bits > 0) {
-      I4Result r4 = trellis_all ? run_i4<true>(L, S, ctx, lane, x, mbw, predtop, yl, yt, true,
-                                               rd_score, max_i4_bits)
-                                : run_i4<false>(L, S, ctx, lane, x, mbw, predtop, yl, yt, true,
-                                                rd_score, max_i4_bits);
-      if (r4.ok) {
-        is_i16 = 0;
-        rdH = r4.H;
-        rd_score = r4.score;
-        rd_nz = r4.nz;
-        for (int k = lane; k < 256; k += 64) {
-          L.yout[(k >> 4) * BPS + (k & 15)] = L.acc_out[k];
-          (&L.fin_ac[0][0])[k] = (&L.acc_ac[0][0])[k];
-        }
-      } else {
-        if (lane < 16) L.modes[lane] = best16;   // the aborted search wrote some
-      }
-      __syncthreads();
-    }
-
-    K3_STAMP(2);
-    // ---- UV (quant_enc.c:1169-1217)
-    int bu = 0;
-    {
-      eval_uv(L, S, ctx, lane, x, topderr, use_derr);
-      score_t bsc = 0, bH = 0;
-      for (int mm = 0; mm < 4; ++mm) {
-        const score_t Dm = L.mres[mm][0], Hm = kVP8ModeCostUV[mm];
-        score_t Rm = L.mres[mm][1];
-        if (mm > 0 && L.mres[mm][2] <= 2) Rm += 140 * 8;
-        const score_t sc = (Rm + Hm) * S.lambda_uv + 256 * Dm;
-        if (mm == 0 || sc < bsc) { bsc = sc; bu = mm; bH = Hm; }
-      }
-      rdH += bH;
-      rd_score += bsc;
-      rd_nz |= (uint32_t)L.mres[bu][3] << 16;
-      for (int k = lane; k < 128; k += 64) {
-        L.yout[(k >> 4) * BPS + 16 + (k & 15)] = L.recuv[bu][k];
-        (&L.fin_uv[0][0])[k] = (&L.lvuv[bu][0][0])[k];
-      }
-      if (use_derr && lane < 2) {   // StoreDiffusionErrors (quant_enc.c:909-920)
-        const int cch = lane;
-        int8_t* top = topderr + 4 * x + 2 * cch;
-        int8_t* left = L.lderr[cch];
-        const int8_t* e = L.uvderr[bu][cch];
-        left[0] = e[0];
-        left[1] = (int8_t)(3 * e[2] >> 2);
-        top[0] = e[1];
-        top[1] = (int8_t)(e[2] - left[1]);
-      }
-      __syncthreads();
-    }
-
-    // ---- m5: final re-quantisation of the chosen modes with trellis
-    // (SimpleQuantize, quant_enc.c:1222-1245; RD_OPT_TRELLIS, :1384-1387)
-    if (rd_opt == 2) {
-      uint32_t nzq = 0;
+    int is_i16 = 1, bu = 0, best16 = 0;
+    uint32_t rd_nz = 0;
+    score_t rdH = 0;
+    if constexpr (NONE) {
+      // ---- RefineUsingDistortion (quant_enc.c:1248-1350): modes by
+      // prediction SSE + fixed mode costs, then the chosen modes' reconstruction
+      const uint8_t am = a.amode[(size_t)f * nmb + mb];
+      int try_both = P->method >= 2;
+      const int refine_uv = P->method >= 1;
+      const score_t bit_limit = try_both ? (score_t)P->mb_header_limit : MAX_COST;
+      score_t best_score = MAX_COST;
+      is_i16 = try_both || !(am & 2);
       if (is_i16) {
-        eval_i16<true>(L, S, ctx, lane);
+        int best_mode = -1;
+        for (int mm = 0; mm < 4; ++mm) {
+          int sq = 0;
+          for (int k = lane; k < 256; k += 64) {
+            const int d = L.yin[(k >> 4) * BPS + (k & 15)] - L.p16[mm][k];
+            sq += d * d;
+          }
+          for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off);
+          const score_t sc = (score_t)sq * 256 + kVP8ModeCostI16[mm] * 106;
+          if (mm > 0 && kVP8ModeCostI16[mm] > bit_limit) continue;
+          if (sc < best_score) { best_mode = mm; best_score = sc; }
+        }
+        if (x == 0 || y == 0) {   // IsFlatSource16: avoid a border checkerboard (bug #432)
+          int same = 1;
+          const int v0 = L.yin[0];
+          for (int k = lane; k < 256; k += 64) same &= (L.yin[(k >> 4) * BPS + (k & 15)] == v0);
+          if (__all(same)) { best_mode = (x == 0) ? 0 : 2; try_both = 0; }
+        }
+        best16 = best_mode;
+        if (lane < 16) L.modes[lane] = best16;
+        __syncthreads();
+      }
+      if (try_both || !is_i16) {
+        is_i16 = 0;
+        const I4Result r4 = run_i4<false>(L, S, ctx, lane, x, mbw, predtop, yl, yt, 2, best_score,
+                                          bit_limit > 0x7fffffff ? 0x7fffffff : (int)bit_limit);
+        if (r4.ok) {
+          rd_nz = r4.nz;
+          for (int k = lane; k < 256; k += 64) {
+            L.yout[(k >> 4) * BPS + (k & 15)] = L.acc_out[k];
+            (&L.fin_ac[0][0])[k] = (&L.acc_ac[0][0])[k];
+          }
+        } else {
+          is_i16 = 1;
+          if (lane < 16) L.modes[lane] = best16;
+        }
+        __syncthreads();
+      }
+      if (is_i16) {   // ReconstructIntra16 of the chosen mode
+        eval_i16<false>(L, S, ctx, lane);
         for (int k = lane; k < 256; k += 64) {
           L.yout[(k >> 4) * BPS + (k & 15)] = L.rec16[best16][k];
           (&L.fin_ac[0][0])[k] = (&L.lv16[best16][0][0])[k];
         }
         if (lane < 16) L.fin_dc[lane] = L.lvdc[best16][lane];
-        nzq = (uint32_t)L.mres[best16][3];
-      } else {
-        I4Result r4 = run_i4<true>(L, S, ctx, lane, x, mbw, predtop, yl, yt, false, 0, 0);
-        for (int k = lane; k < 256; k += 64) {
-          L.yout[(k >> 4) * BPS + (k & 15)] = L.acc_out[k];
-          (&L.fin_ac[0][0])[k] = (&L.acc_ac[0][0])[k];
-        }
-        nzq = r4.nz;
+        rd_nz = (uint32_t)L.mres[best16][3];
       }
       __syncthreads();
-      eval_uv(L, S, ctx, lane, x, topderr, use_derr);   // derr state already updated
+      if (refine_uv) {
+        score_t best_uv = MAX_COST;
+        for (int mm = 0; mm < 4; ++mm) {
+          int sq = 0;
+          for (int k = lane; k < 128; k += 64) {
+            const int d = L.yin[(k >> 4) * BPS + 16 + (k & 15)] - L.puv[mm][k];
+            sq += d * d;
+          }
+          for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off);
+          const score_t sc = (score_t)sq * 256 + kVP8ModeCostUV[mm] * 120;
+          if (sc < best_uv) { bu = mm; best_uv = sc; }
+        }
+      } else {
+        bu = am & 1;   // method 0 keeps the analysis' UV mode
+      }
+      // ReconstructUV: the DC error diffusion reads errors that RD_OPT_NONE
+      // never stores (StoreDiffusionErrors is PickBestUV's), i.e. zeros
+      eval_uv(L, S, ctx, lane, x, topderr, use_derr);
       for (int k = lane; k < 128; k += 64) {
         L.yout[(k >> 4) * BPS + 16 + (k & 15)] = L.recuv[bu][k];
         (&L.fin_uv[0][0])[k] = (&L.lvuv[bu][0][0])[k];
       }
-      rd_nz = nzq | ((uint32_t)L.mres[bu][3] << 16);
+      rd_nz |= (uint32_t)L.mres[bu][3] << 16;
       __syncthreads();
+    } else {
+      score_t rd_score = 0;
+      // ---- Intra16 (quant_enc.c:1002-1058)
+      const bool trellis_all = rd_opt >= 3;
+      if (trellis_all) eval_i16<true>(L, S, ctx, lane);
+      else eval_i16<false>(L, S, ctx, lane);
+      score_t best16_score = 0;
+      uint32_t nz16 = 0;
+      score_t D16 = 0, SD16 = 0, H16 = 0, R16 = 0;
+      {
+        int same = 1;
+        const int v0 = L.yin[0];
+        for (int k = lane; k < 256; k += 64) same &= (L.yin[(k >> 4) * BPS + (k & 15)] == v0);
+        int flat = __all(same);
+        for (int mm = 0; mm < 4; ++mm) {
+          score_t Dm = L.mres[mm][0];
+          score_t SDm = S.tlambda ? (score_t)((S.tlambda * L.mres[mm][1] + 128) >> 8) : 0;
+          const score_t Hm = kVP8ModeCostI16[mm];
+          const score_t Rm = L.mres[mm][2];
+          if (flat) {
+            flat = (L.mres[mm][3] & 0xffff) == 0;
+            if (flat) { Dm *= 2; SDm *= 2; }
+          }
+          const score_t sc = (Rm + Hm) * S.lambda_i16 + 256 * (Dm + SDm);
+          if (mm == 0 || sc < best16_score) {
+            best16_score = sc; best16 = mm;
+            D16 = Dm; SD16 = SDm; H16 = Hm; R16 = Rm;
+            nz16 = (uint32_t)L.mres[mm][3];
+          }
+        }
+      }
+      // commit I16 as current best
+      for (int k = lane; k < 256; k += 64) L.yout[(k >> 4) * BPS + (k & 15)] = L.rec16[best16][k];
+      for (int k = lane; k < 256; k += 64) (&L.fin_ac[0][0])[k] = (&L.lv16[best16][0][0])[k];
+      if (lane < 16) { L.fin_dc[lane] = L.lvdc[best16][lane]; L.modes[lane] = best16; }
+      rd_score = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
+      rdH = H16;
+      rd_nz = nz16;
+      is_i16 = 1;
+      if ((rd_nz & 0x100ffff) == 0x1000000 && D16 > S.min_disto) {
+        int mv = iabs_(L.lvdc[best16][1]);
+        mv = max(mv, iabs_(L.lvdc[best16][2]));
+        mv = max(mv, iabs_(L.lvdc[best16][4]));
+        if (lane == 0 && mv > L.max_edge[segid]) L.max_edge[segid] = mv;
+      }
+      __syncthreads();
+
+      K3_STAMP(1);
+      // ---- Intra4 (quant_enc.c:1072-1165)
+      if (max_i4_bits > 0) {
+        I4Result r4 = trellis_all ? run_i4<true>(L, S, ctx, lane, x, mbw, predtop, yl, yt, true,
+                                                 rd_score, max_i4_bits)
+                                  : run_i4<false>(L, S, ctx, lane, x, mbw, predtop, yl, yt, true,
+                                                  rd_score, max_i4_bits);
+        if (r4.ok) {
+          is_i16 = 0;
+          rdH = r4.H;
+          rd_score = r4.score;
+          rd_nz = r4.nz;
+          for (int k = lane; k < 256; k += 64) {
+            L.yout[(k >> 4) * BPS + (k & 15)] = L.acc_out[k];
+            (&L.fin_ac[0][0])[k] = (&L.acc_ac[0][0])[k];
+          }
+        } else {
+          if (lane < 16) L.modes[lane] = best16;   // the aborted search wrote some
+        }
+        __syncthreads();
+      }
+
+      K3_STAMP(2);
+      // ---- UV (quant_enc.c:1169-1217)
+      {
+        eval_uv(L, S, ctx, lane, x, topderr, use_derr);
+        score_t bsc = 0, bH = 0;
+        for (int mm = 0; mm < 4; ++mm) {
+          const score_t Dm = L.mres[mm][0], Hm = kVP8ModeCostUV[mm];
+          score_t Rm = L.mres[mm][1];
+          if (mm > 0 && L.mres[mm][2] <= 2) Rm += 140 * 8;
+          const score_t sc = (Rm + Hm) * S.lambda_uv + 256 * Dm;
+          if (mm == 0 || sc < bsc) { bsc = sc; bu = mm; bH = Hm; }
+        }
+        rdH += bH;
+        rd_score += bsc;
+        rd_nz |= (uint32_t)L.mres[bu][3] << 16;
+        for (int k = lane; k < 128; k += 64) {
+          L.yout[(k >> 4) * BPS + 16 + (k & 15)] = L.recuv[bu][k];
+          (&L.fin_uv[0][0])[k] = (&L.lvuv[bu][0][0])[k];
+        }
+        if (use_derr && lane < 2) {   // StoreDiffusionErrors (quant_enc.c:909-920)
+          const int cch = lane;
+          int8_t* top = topderr + 4 * x + 2 * cch;
+          int8_t* left = L.lderr[cch];
+          const int8_t* e = L.uvderr[bu][cch];
+          left[0] = e[0];
+          left[1] = (int8_t)(3 * e[2] >> 2);
+          top[0] = e[1];
+          top[1] = (int8_t)(e[2] - left[1]);
+        }
+        __syncthreads();
+      }
+
+      // ---- m5: final re-quantisation of the chosen modes with trellis
+      // (SimpleQuantize, quant_enc.c:1222-1245; RD_OPT_TRELLIS, :1384-1387)
+      if (rd_opt == 2) {
+        uint32_t nzq = 0;
+        if (is_i16) {
+          eval_i16<true>(L, S, ctx, lane);
+          for (int k = lane; k < 256; k += 64) {
+            L.yout[(k >> 4) * BPS + (k & 15)] = L.rec16[best16][k];
+            (&L.fin_ac[0][0])[k] = (&L.lv16[best16][0][0])[k];
+          }
+          if (lane < 16) L.fin_dc[lane] = L.lvdc[best16][lane];
+          nzq = (uint32_t)L.mres[best16][3];
+        } else {
+          I4Result r4 = run_i4<true>(L, S, ctx, lane, x, mbw, predtop, yl, yt, false, 0, 0);
+          for (int k = lane; k < 256; k += 64) {
+            L.yout[(k >> 4) * BPS + (k & 15)] = L.acc_out[k];
+            (&L.fin_ac[0][0])[k] = (&L.acc_ac[0][0])[k];
+          }
+          nzq = r4.nz;
+        }
+        __syncthreads();
+        eval_uv(L, S, ctx, lane, x, topderr, use_derr);   // derr state already updated
+        for (int k = lane; k < 128; k += 64) {
+          L.yout[(k >> 4) * BPS + 16 + (k & 15)] = L.recuv[bu][k];
+          (&L.fin_uv[0][0])[k] = (&L.lvuv[bu][0][0])[k];
+        }
+        rd_nz = nzq | ((uint32_t)L.mres[bu][3] << 16);
+        __syncthreads();
+      }
+      (void)rd_score;
     }
-    (void)rd_score;
     K3_STAMP(3);
     {
 
@@ -968,6 +1105,13 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
         info[0] = is_i16; info[1] = bu; info[2] = segid; info[3] = skip;
         if (is_i16) ++nb_i16; else ++nb_i4;
         if (skip) ++nb_skip;
+        if (NONE && skip && mb < P->nb_stat) ++nb_skip_stat;
+        if (NONE) a.mboff[(size_t)f * nmb + mb] = ntok;
+      }
+      if (NONE && P->recon_addr != 0) {   // autofilter input (filter_enc.c:179)
+        for (int k = lane; k < 128; k += 64)
+          reinterpret_cast<uint32_t*>(P->recon_addr + ((size_t)mb << 9))[k] =
+              reinterpret_cast<const uint32_t*>(L.yout)[k];
         size_p0 += rdH;
       }
       if (lane < 16) mbinfo[(size_t)mb * VP8G_MBINFO_BYTES + 4 + lane] = L.modes[lane];
@@ -1026,8 +1170,8 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
       }
       if (active) L.blkinfo[k] = my_type | (my_first << 4) | (my_ctx << 8);
       int nzdummy;
-      const int mycount = active ? gen_tokens<0>(L, blk_levels(L, k), my_type, my_first, my_ctx,
-                                                 nullptr, &nzdummy)
+      const int mycount = active ? gen_tokens<0, K3Lds, NONE>(L, blk_levels(L, k), my_type,
+                                                              my_first, my_ctx, nullptr, &nzdummy)
                                  : 0;
       // exclusive prefix sum over lanes
       int incl = mycount;
@@ -1040,16 +1184,19 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
       const int excl = incl - mycount;
       if (ntok + (uint32_t)total > a.tok_cap) tok_err = 1;
       if (!tok_err && active)
-        gen_tokens<1>(L, blk_levels(L, k), my_type, my_first, my_ctx, tok_base + ntok + excl,
-                      &nzdummy);
+        gen_tokens<1, K3Lds, NONE>(L, blk_levels(L, k), my_type, my_first, my_ctx,
+                                   tok_base + ntok + excl, &nzdummy);
       if (!tok_err) ntok += total;
       __syncthreads();
       K3_STAMP(5);
       // fold deltas into the statistics; slots that cross the halving
       // threshold inside this MB are replayed in token order.
       int any_mark = 0;
+      // RD_OPT_NONE: only StatLoop's MBs count (frame_enc.c:631-638)
+      const bool stat_on = !NONE || mb < P->nb_stat;
       for (int s = lane; s < NSLOT; s += 64) {
-        const uint32_t dlt = L.delta[s];
+        const uint32_t dlt = stat_on ? L.delta[s] : 0u;
+        if (!stat_on) L.delta[s] = 0;
         if (dlt) {
           const uint32_t p = L.stats[s];
           if ((p >> 16) + (dlt >> 16) < 0xffffu) {
@@ -1066,8 +1213,8 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
         if (lane == 0) {
           for (int kk = first_blk; kk < 25; ++kk) {
             const int bi = L.blkinfo[kk];
-            gen_tokens<2>(L, blk_levels(L, kk), bi & 15, (bi >> 4) & 15, bi >> 8, nullptr,
-                          &nzdummy);
+            gen_tokens<2, K3Lds, NONE>(L, blk_levels(L, kk), bi & 15, (bi >> 4) & 15, bi >> 8,
+                                       nullptr, &nzdummy);
           }
         }
         __syncthreads();
@@ -1126,10 +1273,46 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
   }
 
   // ---- frame epilogue: final probabilities and side results
-  finalize_probas(L, lane);
   vp8g_frame_result* R = a.results + f;
+  int use_skip = 0, skip_proba = 255;
+  if constexpr (NONE) {
+    __syncthreads();
+    for (int s = lane; s < NSLOT; s += 64) rstats[s] = L.stats[s];
+    // StatLoop gives up before FinalizeSkipProba / FinalizeTokenProbas when
+    // its header estimate is 0 (frame_enc.c:645-646): default probabilities
+    if (P->none_finalize) {
+      finalize_probas(L, lane);
+      const int nbs = __shfl(nb_skip_stat, 0);   // counted by lane 0 only
+      skip_proba = (int)((uint64_t)(nmb - nbs) * 255 / nmb);   // CalcSkipProba
+      use_skip = skip_proba < 250;
+    }
+    if (use_skip && !tok_err) {
+      // VP8EncLoop codes no residuals for skipped MBs: drop their tokens
+      // (forward compaction, each 64-token chunk read before it is written)
+      uint32_t dst = 0;
+      for (int m = 0; m < nmb; ++m) {
+        const uint32_t b0 = a.mboff[(size_t)f * nmb + m];
+        const uint32_t b1 = m + 1 < nmb ? a.mboff[(size_t)f * nmb + m + 1] : ntok;
+        if (mbinfo[(size_t)m * VP8G_MBINFO_BYTES + 3]) continue;
+        if (dst != b0)
+          for (uint32_t i = 0; i < b1 - b0; i += 64) {
+            const bool in = i + lane < b1 - b0;
+            const uint16_t t = in ? tok_base[b0 + i + lane] : 0;
+            __builtin_amdgcn_wave_barrier();
+            if (in) tok_base[dst + i + lane] = t;
+            __builtin_amdgcn_wave_barrier();
+          }
+        dst += b1 - b0;
+      }
+      ntok = dst;
+    }
+  } else {
+    finalize_probas(L, lane);
+  }
   for (int s = lane; s < NSLOT; s += 64) R->probas[s] = L.coeffs[s];
   if (lane == 0) {
+    R->use_skip = (int16_t)use_skip;
+    R->skip_proba = (int16_t)skip_proba;
     R->ntokens = ntok;
     R->error = tok_err;
     for (int s = 0; s < 4; ++s) R->max_edge[s] = L.max_edge[s];
@@ -1225,11 +1408,11 @@ int vp8g_launch_cleanup_alpha(uint8_t* yuv, size_t yfb, const uint8_t* aplane,
 }
 
 int vp8g_launch_analysis(const uint8_t* yuv, size_t yfb, int w, int h, int n, uint8_t* mb_alpha,
-                         uint16_t* mb_uva, void* stream) {
+                         uint16_t* mb_uva, int fast_q, uint8_t* mb_amode, void* stream) {
   const int nmb = ((w + 15) >> 4) * ((h + 15) >> 4);
   dim3 grid((nmb + 3) / 4, n);
   hipLaunchKernelGGL(k_analyze, grid, dim3(256), 0, (hipStream_t)stream, yuv, yfb, w, h, nmb,
-                     mb_alpha, mb_uva);
+                     mb_alpha, mb_uva, fast_q, mb_amode);
   return launch_check("k_analyze");
 }
 
@@ -1247,14 +1430,41 @@ int vp8g_launch_encode_w1(const uint8_t* yuv, size_t yfb, int w, int h, int n,
     vp8g_set_error("k_encode", "frame too wide for the LDS budget");
     return 0;
   }
+  a.amode = nullptr; a.mboff = nullptr; a.rerun = nullptr;
   static int attr_done = 0;
   if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)k_encode_w1, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_encode_w1<false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_done = 1;
   }
-  hipLaunchKernelGGL(k_encode_w1, dim3(n), dim3(64), lds, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(k_encode_w1<false>, dim3(n), dim3(64), lds, (hipStream_t)stream, a);
   return launch_check("k_encode_w1");
+}
+
+int vp8g_launch_encode_none(const uint8_t* yuv, size_t yfb, int w, int h, int n,
+                            const uint8_t* segmap, const uint8_t* amode,
+                            const vp8g_frame_params* params, uint16_t* tokens, size_t tok_cap,
+                            uint8_t* mbinfo, uint32_t* mboff, vp8g_frame_result* results,
+                            uint8_t* rerun_state, void* stream) {
+  K3ArgsW1 a;
+  a.yuv = yuv; a.yfb = yfb; a.w = w; a.h = h;
+  a.mbw = (w + 15) >> 4; a.mbh = (h + 15) >> 4;
+  a.segmap = segmap; a.params = params; a.tokens = tokens; a.tok_cap = tok_cap;
+  a.mbinfo = mbinfo; a.results = results;
+  a.amode = amode; a.mboff = mboff; a.rerun = rerun_state;
+  const size_t lds = k3_lds_bytes(a.mbw);
+  if (lds > 160 * 1024) {
+    vp8g_set_error("k_encode_none", "frame too wide for the LDS budget");
+    return 0;
+  }
+  static int attr_done = 0;
+  if (!attr_done) {
+    (void)hipFuncSetAttribute((const void*)k_encode_w1<true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_done = 1;
+  }
+  hipLaunchKernelGGL(k_encode_w1<true>, dim3(n), dim3(64), lds, (hipStream_t)stream, a);
+  return launch_check("k_encode_none");
 }
 
 int vp8g_launch_synth(uint8_t* rgba, size_t fstride, int w, int h, int f0, int n, int seed,

@@ -126,6 +126,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   CHK(hipMalloc((void**)&b->d_aplane, N * (size_t)width * height));
   CHK(hipMalloc((void**)&b->d_alpha, N * nmb));
   CHK(hipMalloc((void**)&b->d_uva, N * nmb * sizeof(uint16_t)));
+  CHK(hipMalloc((void**)&b->d_amode, N * nmb));
   CHK(hipMalloc((void**)&b->d_segmap, N * nmb));
   CHK(hipMalloc((void**)&b->d_params, N * sizeof(vp8g_frame_params)));
   CHK(hipMalloc((void**)&b->d_tokens, N * b->tok_cap * sizeof(uint16_t)));
@@ -170,7 +171,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipSetDevice(b->device);
   if (b->stream) hipStreamSynchronize(b->stream);
   hipFree(b->d_g2l); hipFree(b->d_rgba); hipFree(b->d_yuv); hipFree(b->d_aflags); hipFree(b->d_alpha);
-  hipFree(b->d_uva); hipFree(b->d_segmap); hipFree(b->d_params); hipFree(b->d_tokens);
+  hipFree(b->d_uva); hipFree(b->d_amode); hipFree(b->d_segmap); hipFree(b->d_params); hipFree(b->d_tokens);
   hipFree(b->d_mbinfo); hipFree(b->d_mboff); hipFree(b->d_rerun); hipFree(b->d_results); hipFree(b->d_psize); hipFree(b->d_emeta);
   hipFree(b->d_poff); hipFree(b->d_part);
   hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs); hipFree(b->d_nbuf);
@@ -366,7 +367,8 @@ static int run_passes(WebPGpuBatch* b, int n) {
       if (!act[f]) { P->pass_mode = 2; continue; }
       vp8h_frame* fr = &b->frames[f];
       vp8h_set_loop_params(fr, fr->ps_q, b->h_segmap + f * nmb, P);
-      P->pass_mode = fr->npass == 0 ? 0 : fr->is_last_pass ? 1 : 3;
+      /* StatLoop (RD_OPT_NONE) never resets its statistics between passes */
+      P->pass_mode = fr->npass == 0 ? 0 : (fr->is_last_pass && fr->rd_opt > 0) ? 1 : 3;
       P->recon_addr = af ? (uint64_t)(uintptr_t)(b->d_recon + (size_t)f * nmb * 512) : 0;
       ++fr->npass;
       ++nact;
@@ -377,10 +379,17 @@ static int run_passes(WebPGpuBatch* b, int n) {
     CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
                        hipMemcpyHostToDevice, st));
     if (round == 0) CHK(hipEventRecord(b->ev[2], st));
-    if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params,
-                            b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5,
-                            b->d_results, b->d_rerun, af ? b->d_recon : NULL, st))
+    if (b->cfg.method < 3) {   /* methods 0-2: VP8EncLoop's RD_OPT_NONE encoder */
+      if (!vp8g_launch_encode_none(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_amode,
+                                   b->d_params, b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff,
+                                   b->d_results, b->d_rerun, st))
+        return 0;
+    } else if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params,
+                                   b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff,
+                                   b->cfg.method >= 5, b->d_results, b->d_rerun,
+                                   af ? b->d_recon : NULL, st)) {
       return 0;
+    }
     CHK(hipEventRecord(b->ev[3], st));
     CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
                        hipMemcpyDeviceToHost, st));
@@ -482,7 +491,9 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   if (!encode_alpha(b, n)) return 0;
   if (!b->ev0_recorded) CHK(hipEventRecord(b->ev[0], st));
   b->ev0_recorded = 0;
-  if (!vp8g_launch_analysis(b->d_yuv, b->yfb, b->w, b->h, n, b->d_alpha, b->d_uva, st)) return 0;
+  if (!vp8g_launch_analysis(b->d_yuv, b->yfb, b->w, b->h, n, b->d_alpha, b->d_uva,
+                            b->cfg.method <= 1 ? (int)b->cfg.quality : -1, b->d_amode, st))
+    return 0;
   CHK(hipEventRecord(b->ev[1], st));
   CHK(hipMemcpyAsync(b->h_alpha, b->d_alpha, n * nmb, hipMemcpyDeviceToHost, st));
   CHK(hipMemcpyAsync(b->h_uva, b->d_uva, n * nmb * sizeof(uint16_t), hipMemcpyDeviceToHost, st));

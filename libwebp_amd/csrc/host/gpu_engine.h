@@ -26,6 +26,7 @@ struct WebPGpuBatch {
   vp8l_engine* la;           /* ALPH-chunk VP8L engine, created on first use */
   uint8_t** araw;            /* raw alpha planes (alpha_compression 0 / fallback) */
   uint8_t* d_alpha;
+  uint8_t* d_amode;          /* K2 analysis modes (RD_OPT_NONE input) */
   uint16_t* d_uva;
   uint8_t* d_segmap;
   vp8g_frame_params* d_params;

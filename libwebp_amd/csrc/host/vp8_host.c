@@ -50,12 +50,17 @@ int vp8h_use_sharp(const WebPConfig* cfg, int w, int h) {
 
 int vp8h_frame_init(vp8h_frame* fr, const WebPConfig* cfg, int w, int h) {
   memset(fr, 0, sizeof(*fr));
-  if (cfg->method < 3 || cfg->method > 6) return 0;   /* m0-2: non-token loop */
+  if (cfg->method < 0 || cfg->method > 6) return 0;
+  /* methods 0-2 run VP8EncLoop (RD_OPT_NONE): its size / PSNR search passes
+   * (StatLoop with RD_OPT_BASIC, frame_enc.c:614-674) and token partitions
+   * (one bit writer per MB row modulo 2^partitions) are not implemented */
+  if (cfg->method < 3 && (cfg->target_size > 0 || cfg->target_PSNR > 0 || cfg->partitions > 0))
+    return 0;
   if (cfg->low_memory || (cfg->preprocessing & 2)) return 0;
   fr->w = w; fr->h = h;
   fr->mbw = (w + 15) >> 4; fr->mbh = (h + 15) >> 4;
   fr->method = cfg->method;
-  fr->rd_opt = cfg->method >= 6 ? 3 : cfg->method >= 5 ? 2 : 1;
+  fr->rd_opt = cfg->method >= 6 ? 3 : cfg->method >= 5 ? 2 : cfg->method >= 3 ? 1 : 0;
   {
     const int lim = 100 - cfg->partition_limit;
     fr->max_i4_header_bits = 256 * 16 * 16 * (lim * lim) / (100 * 100);
@@ -102,6 +107,7 @@ int vp8h_frame_init(vp8h_frame* fr, const WebPConfig* cfg, int w, int h) {
 
 int vp8h_pass_start(vp8h_frame* fr) {
   if (fr->pass_left-- <= 0) return 0;
+  /* StatLoop (RD_OPT_NONE, no search): no q changes, dq stays 10 */
   fr->is_last_pass = (fabs(fr->ps_dq) <= DQ_LIMIT) || (fr->pass_left == 0) ||
                      (fr->max_i4_header_bits == 0);
   return 1;
@@ -125,6 +131,7 @@ static void compute_next_q(vp8h_frame* s) {   /* ComputeNextQ, :60-80 */
 }
 
 int vp8h_pass_finish(vp8h_frame* fr, uint64_t size_p0) {
+  if (fr->rd_opt == 0 && size_p0 == 0) return 0;   /* StatLoop gives up (frame_enc.c:645) */
   if (fr->max_i4_header_bits > 0 && size_p0 > VP8H_P0_LIMIT) {
     ++fr->pass_left;
     fr->max_i4_header_bits >>= 1;   /* strengthen the header bit limit and start over */
@@ -292,7 +299,8 @@ void vp8h_analyze_segments(vp8h_frame* fr, const uint8_t* mb_alpha, const uint16
                            uint8_t* segmap) {
   const int nmb = fr->mbw * fr->mbh;
   /* VP8EncAnalyze tail (analysis_enc.c:422-482) */
-  const int do_seg = fr->emulate_jpeg_size || fr->num_segments > 1;
+  /* methods 0-1 also need the analysis' modes (analysis_enc.c:424-427) */
+  const int do_seg = fr->emulate_jpeg_size || fr->num_segments > 1 || fr->method <= 1;
   if (do_seg) {
     long sa = 0, suva = 0;
     for (int i = 0; i < nmb; ++i) { sa += mb_alpha[i]; suva += mb_uva[i]; }
@@ -390,6 +398,7 @@ void vp8h_set_loop_params(vp8h_frame* fr, float quality, uint8_t* segmap, vp8g_f
     m->lambda_trellis_i16 = AT_LEAST_1((q_i16 * q_i16) >> 2);
     m->lambda_trellis_uv = AT_LEAST_1((q_uv * q_uv) << 1);
     m->tlambda = AT_LEAST_1((tls * q_i4) >> 5);
+    m->i4_penalty = 1000 * q_i4 * q_i4;
 #undef AT_LEAST_1
     m->min_disto = 20 * m->y1.q[0];
     fr->seg_y2ac[i] = m->y2.q[1];
@@ -419,6 +428,12 @@ void vp8h_set_loop_params(vp8h_frame* fr, float quality, uint8_t* segmap, vp8g_f
   P->method = fr->method;
   P->use_derr = fr->quality <= 98 || fr->cfg_pass > 1;   /* webp_enc.c:162-164 */
   P->max_count = (nmb >> 3) < 96 ? 96 : (nmb >> 3);
+  /* RD_OPT_NONE (VP8EncLoop): no refreshes; StatLoop's probe size (:631-638)
+   * and whether it reaches its finalisation (header estimate != 0, :645) */
+  P->mb_header_limit = (int32_t)((int64_t)256 * 510 * 8 * 1024 / nmb);
+  P->nb_stat = fr->method == 0 ? ((nmb > 200) ? nmb >> 2 : 50) : nmb;
+  P->none_finalize = fr->seg_hdr_size != 0;
+  if (fr->rd_opt == 0) P->max_count = 0x7fffffff;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -533,7 +548,8 @@ void vp8h_emit_tokens(vp8h_bw* bw, const uint16_t* tok, size_t n, const uint8_t*
 /* Partition 0 (syntax_enc.c:187-310, tree_enc.c:270-347,485-504) and the
  * RIFF container (syntax_enc.c:37-185,320-389). */
 
-static void code_intra_modes(vp8h_bw* bw, const vp8h_frame* fr, const uint8_t* mbinfo) {
+static void code_intra_modes(vp8h_bw* bw, const vp8h_frame* fr, const uint8_t* mbinfo,
+                             int use_skip, int skip_proba) {
   const int mbw = fr->mbw;
   uint8_t* top_modes = (uint8_t*)calloc(4 * (size_t)mbw, 1);   /* B_DC_PRED border */
   if (!top_modes) { bw->error = 1; return; }
@@ -548,6 +564,7 @@ static void code_intra_modes(vp8h_bw* bw, const vp8h_frame* fr, const uint8_t* m
         if (bw_put(bw, s >= 2, p[0])) p += 1;
         bw_put(bw, s & 1, p[1]);
       }
+      if (use_skip) bw_put(bw, info[3], skip_proba);   /* tree_enc.c:323-325 */
       if (bw_put(bw, info[0] != 0, 145)) {   /* intra16 */
         const int m = modes[0];
         if (bw_put(bw, m == 1 || m == 3, 156)) bw_put(bw, m == 1, 128);
@@ -633,9 +650,11 @@ int vp8h_build_p0(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* m
     const int v = res->probas[s];
     if (bw_put(&bw, v != p0[s], pu[s])) bw_put_bits(&bw, (uint32_t)v, 8);
   }
-  bw_put_uniform(&bw, 0);          /* no skip probability */
+  /* skip probability (tree_enc.c:500-502): only the RD_OPT_NONE loop uses it */
+  const int use_skip = res->use_skip != 0;
+  if (bw_put_uniform(&bw, use_skip)) bw_put_bits(&bw, (uint32_t)res->skip_proba, 8);
   const size_t hdr_pos = bw.pos;
-  code_intra_modes(&bw, fr, mbinfo);
+  code_intra_modes(&bw, fr, mbinfo, use_skip, res->skip_proba);
   vp8h_bw_finish(&bw);
   *out0 = bw;
   if (hdr_bytes) { hdr_bytes[0] = (int)hdr_pos; hdr_bytes[1] = (int)(bw.pos - hdr_pos); }

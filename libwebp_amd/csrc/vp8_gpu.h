@@ -39,7 +39,8 @@ typedef struct {
 typedef struct {
   vp8g_mtx y1, y2, uv;
   int32_t lambda_i16, lambda_i4, lambda_uv, lambda_mode, tlambda, min_disto;
-  int32_t lambda_trellis_i16, lambda_trellis_i4, lambda_trellis_uv, pad0;
+  int32_t lambda_trellis_i16, lambda_trellis_i4, lambda_trellis_uv;
+  int32_t i4_penalty;    /* 1000 * q_i4^2, RD_OPT_NONE intra-4 start score (quant_enc.c:285) */
 } vp8g_seg;
 
 typedef struct {
@@ -58,6 +59,11 @@ typedef struct {
                             non-last pass); 2 frame already final: skip */
   uint64_t recon_addr;   /* device address of this frame's nmb x 512 B
                             reconstruction buffer (autofilter), or 0 */
+  /* RD_OPT_NONE (methods 0-2, VP8EncLoop) */
+  int32_t mb_header_limit;  /* webp_enc.c:109-110 */
+  int32_t nb_stat;          /* MBs of the statistics pass (StatLoop's fast probe) */
+  int32_t none_finalize;    /* the statistics pass finalises the probabilities */
+  int32_t pad1;
 } vp8g_frame_params;
 
 /* per-frame cost state K3 leaves for the next pass: the probabilities the
@@ -77,7 +83,7 @@ typedef struct {
   uint64_t sse[3];
   uint64_t distortion;   /* sum of the per-MB VP8ModeScore D (frame_enc.c:840) */
   int32_t block_count[3];
-  int32_t pad;
+  int16_t use_skip, skip_proba;   /* RD_OPT_NONE: FinalizeSkipProba (frame_enc.c:111-127) */
   uint64_t stamps[8];    /* per-stage shader-clock cycles summed over MBs (profiling) */
   uint8_t probas[VP8G_NUM_SLOTS];   /* final coefficient probabilities */
 } vp8g_frame_result;
@@ -102,8 +108,13 @@ int vp8g_launch_extract_alpha(const uint8_t* rgba, size_t frame_stride, int row_
 int vp8g_launch_cleanup_alpha(uint8_t* yuv, size_t yuv_frame_bytes, const uint8_t* alpha_plane,
                               const uint32_t* alpha_flags, int w, int h, int n, void* stream);
 
+/* K2 (analysis_enc.c:230-333). fast_q >= 0 selects the methods 0-1
+ * analysis (FastMBAnalyze with that integer quality); mb_amode (or NULL)
+ * receives per MB the analysis UV mode (bit 0) and, for methods 0-1, the
+ * intra-4 pick (bit 1), inputs of the RD_OPT_NONE encoder */
 int vp8g_launch_analysis(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h,
-                         int n, uint8_t* mb_alpha, uint16_t* mb_uva, void* stream);
+                         int n, uint8_t* mb_alpha, uint16_t* mb_uva, int fast_q,
+                         uint8_t* mb_amode, void* stream);
 
 /* K3: RD search + tokens. Each frame's tokens end up as one compact stream
  * at the start of its tok_cap region (per-MB slots of
@@ -137,6 +148,19 @@ int vp8g_launch_autofilter(const uint8_t* yuv, size_t yuv_frame_bytes, int w, in
                            const uint8_t* mbinfo, const uint8_t* recon,
                            const vp8g_af_frame* afp, const uint8_t* active, double* mbval,
                            uint8_t* level, void* stream);
+
+/* K3 for methods 0-2 (RD_OPT_NONE; VP8EncLoop, frame_enc.c:739-775): one
+ * wavefront per frame in raster order, modes by prediction SSE
+ * (RefineUsingDistortion, quant_enc.c:1248-1350), token statistics of the
+ * first params->nb_stat MBs (StatLoop), final probabilities and skip
+ * probability, then the tokens of skipped MBs dropped when the skip flag
+ * pays. amode = K2's analysis modes; mboff scratch n x nmb. rerun_state:
+ * statistics carried between passes (pass_mode 3). */
+int vp8g_launch_encode_none(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h, int n,
+                            const uint8_t* segmap, const uint8_t* amode,
+                            const vp8g_frame_params* params, uint16_t* tokens, size_t tok_cap,
+                            uint8_t* mbinfo, uint32_t* mboff, vp8g_frame_result* results,
+                            uint8_t* rerun_state, void* stream);
 
 /* VP8EstimateTokenSize (token_enc.c:226-247) of each frame's compact token
  * stream under the probabilities at state + f * VP8G_RERUN_STATE_BYTES +

@@ -11,6 +11,7 @@ Y PSNR / segment levels the reference reports in WebPAuxStats.
   multipass   config->pass > 1, target_size / target_PSNR, qmin / qmax
               (src/enc/frame_enc.c:26-80, 783-894)
   autofilter  config->autofilter (src/enc/filter_enc.c:156-212)
+  methods012  config->method 0-2 (VP8EncLoop, src/enc/frame_enc.c:614-775)
 """
 import ctypes
 import hashlib
@@ -26,7 +27,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 from libwebp_amd import abi  # noqa: E402
 from libwebp_amd.synth import syn_v1  # noqa: E402
 
-MODULES = ["multipass", "autofilter"]
+MODULES = ["multipass", "autofilter", "methods012"]
 
 
 def main():

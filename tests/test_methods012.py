@@ -1,0 +1,93 @@
+"""Methods 0-2 (cwebp -m 0/1/2): VP8EncLoop with RD_OPT_NONE
+(src/enc/frame_enc.c:614-775): FastMBAnalyze for methods 0-1
+(analysis_enc.c:255-276), modes by prediction distortion
+(RefineUsingDistortion, quant_enc.c:1248-1350), StatLoop statistics over the
+first MBs with VP8RecordCoeffs' slots (cost_enc.c:289-340), the skip
+probability and per-MB skip flags, and the tokens of skipped MBs dropped.
+
+Parity: bit-exact bitstreams. Golden vectors from the reference build
+(tests/golden/methods012_kat.json, make_options_golden.py); the oracle's
+restatement is checked against them on CPU, the GPU path (K2 fast analysis +
+the RD_OPT_NONE wavefront kernel) against them and the oracle.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from libwebp_amd.synth import syn_v1
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CASES = []
+for _m in (0, 1, 2):
+    CASES += [
+        (64, 48, 0, {"quality": 75.0, "method": _m}),
+        (128, 96, 1, {"quality": 30.0, "method": _m}),
+        (333, 257, 2, {"quality": 90.0, "method": _m}),
+        (17, 9, 3, {"quality": 50.0, "method": _m}),
+        (512, 512, 0, {"quality": 75.0, "method": _m}),
+        (200, 144, 4, {"quality": 99.0, "method": _m, "segments": 1}),   # no finalisation
+        (240, 160, 5, {"quality": 60.0, "method": _m, "pass": 3}),
+        (240, 160, 6, {"quality": 70.0, "method": _m, "autofilter": 1, "sns_strength": 90}),
+        (96, 96, 7, {"quality": 0.0, "method": _m}),
+    ]
+CASES += [(1920, 1080, 0, {"quality": 75.0, "method": 0}),
+          (1920, 1080, 1, {"quality": 75.0, "method": 2})]
+
+
+def kat():
+    return json.load(open(os.path.join(ROOT, "tests", "golden", "methods012_kat.json")))["cases"]
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+def test_golden_inputs_pinned():
+    k = kat()
+    assert len(k) == len(CASES)
+    for (w, h, f, kw), c in zip(CASES, k):
+        assert (c["w"], c["h"], c["frame"], c["params"]) == (w, h, f, kw)
+        assert sha(syn_v1(w, h, f).tobytes())[:16] == c["in_sha"]
+
+
+@pytest.mark.parametrize("i", [i for i, c in enumerate(CASES) if c[0] * c[1] < 1000000])
+def test_oracle_matches_reference(i):
+    from oracle import oracle
+    w, h, f, kw = CASES[i]
+    assert sha(oracle.encode_rgba(syn_v1(w, h, f), **kw)) == kat()[i]["sha256"]
+
+
+@pytest.mark.gpu
+def test_gpu_webpencode_methods012(gpu):
+    for (w, h, f, kw), c in zip(CASES, kat()):
+        out = gpu.encode_rgba(syn_v1(w, h, f), **kw)
+        assert (len(out), sha(out)) == (c["size"], c["sha256"]), (w, h, f, kw)
+
+
+@pytest.mark.gpu
+def test_gpu_batch_methods012(gpu):
+    import torch
+    from oracle import oracle
+    w, h, n = 176, 144, 4
+    frames = np.stack([syn_v1(w, h, f) for f in range(n)])
+    buf = torch.from_numpy(frames).to("cuda:0")
+    torch.cuda.synchronize()
+    for m in (0, 1, 2):
+        kw = {"quality": 65.0, "method": m}
+        enc = gpu.GpuBatch(w, h, n, **kw)
+        enc.encode_device(buf.data_ptr(), n)
+        for f in range(n):
+            assert enc.output(f) == oracle.encode_rgba(frames[f], **kw), (m, f)
+        enc.close()
+
+
+@pytest.mark.gpu
+def test_gpu_method012_unsupported_fail_loudly(gpu):
+    img = syn_v1(64, 48, 0)
+    for kw in ({"method": 1, "target_size": 2000, "pass": 4}, {"method": 2, "partitions": 2}):
+        with pytest.raises(RuntimeError):
+            gpu.encode_rgba(img, quality=75.0, **kw)

@@ -1378,6 +1378,45 @@ extern "C" int vp8g_launch_check(const char* what) {
   return 1;
 }
 
+// Alpha level reduction (alpha_quality < 100; QuantizeLevels,
+// src/utils/quant_levels_utils.c:31-137): per-frame 256-bin histogram of the
+// alpha plane here, the k-means over the 256 symbols on the host (doubles,
+// the reference's own order), then the symbol map applied here.
+__global__ __launch_bounds__(256) void k_alpha_hist(const uint8_t* __restrict__ aplane,
+                                                    size_t plane, const uint32_t* aflags,
+                                                    uint32_t* __restrict__ hist) {
+  const int f = blockIdx.y;
+  if (!aflags[f]) return;
+  __shared__ uint32_t hs[256];
+  hs[threadIdx.x] = 0;
+  __syncthreads();
+  const uint8_t* a = aplane + (size_t)f * plane;
+  const size_t n16 = plane >> 4;
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) {
+    const uint4 v = reinterpret_cast<const uint4*>(a)[i];
+    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) atomicAdd(&hs[(w4[k >> 2] >> (8 * (k & 3))) & 255], 1u);
+  }
+  if (blockIdx.x == 0)
+    for (size_t i = (n16 << 4) + threadIdx.x; i < plane; i += 256) atomicAdd(&hs[a[i]], 1u);
+  __syncthreads();
+  if (hs[threadIdx.x]) atomicAdd(&hist[(size_t)f * 256 + threadIdx.x], hs[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void k_alpha_remap(uint8_t* __restrict__ aplane, size_t plane,
+                                                     const uint32_t* aflags,
+                                                     const uint8_t* __restrict__ maps) {
+  const int f = blockIdx.y;
+  if (!aflags[f]) return;
+  __shared__ uint8_t m[256];
+  m[threadIdx.x] = maps[(size_t)f * 256 + threadIdx.x];
+  __syncthreads();
+  uint8_t* a = aplane + (size_t)f * plane;
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < plane; i += (size_t)gridDim.x * 256)
+    a[i] = m[a[i]];
+}
+
 extern "C" {
 
 int vp8g_launch_import(const uint8_t* rgba, size_t fstride, int rstride, int w, int h, int n,
@@ -1405,6 +1444,25 @@ int vp8g_launch_cleanup_alpha(uint8_t* yuv, size_t yfb, const uint8_t* aplane,
   hipLaunchKernelGGL(k_cleanup_alpha, grid, dim3(256), 0, (hipStream_t)stream, yuv, yfb, aplane,
                      aflags, w, h);
   return launch_check("k_cleanup_alpha");
+}
+
+int vp8g_launch_alpha_hist(const uint8_t* aplane, size_t plane, const uint32_t* aflags, int n,
+                           uint32_t* hist, void* stream) {
+  if (hipMemsetAsync(hist, 0, (size_t)n * 256 * sizeof(uint32_t), (hipStream_t)stream) !=
+      hipSuccess)
+    return launch_check("k_alpha_hist memset");
+  dim3 grid((unsigned)min((size_t)64, (plane + 4095) / 4096 + 1), n);
+  hipLaunchKernelGGL(k_alpha_hist, grid, dim3(256), 0, (hipStream_t)stream, aplane, plane, aflags,
+                     hist);
+  return launch_check("k_alpha_hist");
+}
+
+int vp8g_launch_alpha_remap(uint8_t* aplane, size_t plane, const uint32_t* aflags, int n,
+                            const uint8_t* maps, void* stream) {
+  dim3 grid((unsigned)min((size_t)256, (plane + 255) / 256), n);
+  hipLaunchKernelGGL(k_alpha_remap, grid, dim3(256), 0, (hipStream_t)stream, aplane, plane, aflags,
+                     maps);
+  return launch_check("k_alpha_remap");
 }
 
 int vp8g_launch_analysis(const uint8_t* yuv, size_t yfb, int w, int h, int n, uint8_t* mb_alpha,

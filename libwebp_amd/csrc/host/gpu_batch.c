@@ -157,8 +157,9 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   b->araw = (uint8_t**)calloc(N, sizeof(uint8_t*));
   b->fin_cost = (int*)calloc(N, sizeof(int));
   b->pass_act = (uint8_t*)calloc(N, 1);
+  b->asse = (uint64_t*)calloc(N, sizeof(uint64_t));
   if (!b->frames || !b->tok_off || !b->p0 || !b->out || !b->out_size || !b->err || !b->hdr ||
-      !b->araw || !b->fin_cost || !b->pass_act)
+      !b->araw || !b->fin_cost || !b->pass_act || !b->asse)
     goto fail;
   return b;
 fail:
@@ -178,6 +179,8 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipFree(b->d_eimg);
   hipFree(b->d_stabs); hipFree(b->d_sharp); hipFree(b->d_sstate);
   hipFree(b->d_active); hipFree(b->d_tbits);
+  hipFree(b->d_ahist); hipFree(b->d_amaps); hipHostFree(b->h_ahist); hipHostFree(b->h_amaps);
+  free(b->asse);
   hipFree(b->d_recon); hipFree(b->d_mbval); hipFree(b->d_afp); hipFree(b->d_aflevel);
   hipHostFree(b->h_afp); hipHostFree(b->h_aflevel);
   hipHostFree(b->h_state); hipHostFree(b->h_active); hipHostFree(b->h_tbits);
@@ -253,10 +256,11 @@ static void frame_finish(WebPGpuBatch* b, int f) {
       alpha.data = b->araw[f];
       alpha.size = (size_t)b->w * b->h;
     } else {
-      alpha.header = 1;   /* ALPHA_LOSSLESS_COMPRESSION, no filter, no level reduction */
+      alpha.header = 1;   /* ALPHA_LOSSLESS_COMPRESSION, no filter */
       alpha.data = vp8l_engine_output(b->la, f);
       alpha.size = b->la->out_size[f];
     }
+    if (b->cfg.alpha_quality < 100) alpha.header |= 1 << 4;   /* ALPHA_PREPROCESSED_LEVELS */
     ap = &alpha;
   }
   b->out_size[f] = vp8h_write_riff(&b->frames[f], &b->p0[f], &part1, ap, &b->out[f], &err);
@@ -312,6 +316,30 @@ static int encode_alpha(WebPGpuBatch* b, int n) {
   if (!any) return 1;
   const size_t plane = (size_t)b->w * b->h;
   double t[10] = {0};
+  const int reduce_levels = b->cfg.alpha_quality < 100;
+  if (reduce_levels) {   /* QuantizeLevels on the device planes (alpha_enc.c:342-349) */
+    if (!b->d_ahist) {
+      const size_t N = (size_t)b->max_frames;
+      CHK(hipMalloc((void**)&b->d_ahist, N * 256 * sizeof(uint32_t)));
+      CHK(hipMalloc((void**)&b->d_amaps, N * 256));
+      CHK(hipHostMalloc((void**)&b->h_ahist, N * 256 * sizeof(uint32_t), 0));
+      CHK(hipHostMalloc((void**)&b->h_amaps, N * 256, 0));
+    }
+    if (!vp8g_launch_alpha_hist(b->d_aplane, plane, b->d_aflags, n, b->d_ahist, b->stream))
+      return 0;
+    CHK(hipMemcpyAsync(b->h_ahist, b->d_ahist, n * 256 * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                       b->stream));
+    CHK(hipStreamSynchronize(b->stream));
+    const int levels = vp8h_alpha_levels(b->cfg.alpha_quality);
+    for (int f = 0; f < n; ++f)
+      if (b->h_aflags[f])
+        vp8h_quantize_levels_map(b->h_ahist + (size_t)f * 256, plane, levels,
+                                 b->h_amaps + (size_t)f * 256, &b->asse[f]);
+    CHK(hipMemcpyAsync(b->d_amaps, b->h_amaps, n * 256, hipMemcpyHostToDevice, b->stream));
+    if (!vp8g_launch_alpha_remap(b->d_aplane, plane, b->d_aflags, n, b->d_amaps, b->stream))
+      return 0;
+    CHK(hipStreamSynchronize(b->stream));
+  }
   if (b->cfg.alpha_compression) {
     if (!b->la) b->la = vp8l_engine_new(b->w, b->h, b->max_frames, b->cfg.method, 1);
     if (!b->la) return 0;
@@ -329,6 +357,8 @@ static int encode_alpha(WebPGpuBatch* b, int n) {
   }
   b->timings[9] = t[0] + t[1] + t[2] + t[3] + t[4];
   return 1;
+fail:
+  return 0;
 }
 
 /* VP8EncTokenLoop's pass loop (frame_enc.c:808-880) for every frame of the
@@ -690,9 +720,6 @@ static int run_rgba(WebPGpuBatch* b, const void* rgba_dev, size_t fstride, int r
     int any = 0;
     for (int f = 0; f < n; ++f) {
       any |= b->h_aflags[f] != 0;
-      /* alpha level quantisation (alpha_quality < 100, QuantizeLevels) is
-       * not implemented: fail loudly rather than encode differently */
-      if (b->h_aflags[f] && b->cfg.alpha_quality < 100) b->err[f] = VP8_ENC_ERROR_INVALID_CONFIGURATION;
     }
     /* webp_enc.c:369-371: smooth/flatten the fully transparent areas */
     if (any && !b->cfg.exact &&

@@ -25,6 +25,11 @@ struct WebPGpuBatch {
   uint8_t* d_aplane;         /* alpha planes, n x w*h (K1 / upload) */
   vp8l_engine* la;           /* ALPH-chunk VP8L engine, created on first use */
   uint8_t** araw;            /* raw alpha planes (alpha_compression 0 / fallback) */
+  uint32_t* d_ahist;         /* alpha level reduction: histograms, maps (first use) */
+  uint8_t* d_amaps;
+  uint32_t* h_ahist;
+  uint8_t* h_amaps;
+  uint64_t* asse;            /* alpha squared error per frame (WebPAuxStats PSNR[4]) */
   uint8_t* d_alpha;
   uint8_t* d_amode;          /* K2 analysis modes (RD_OPT_NONE input) */
   uint16_t* d_uva;

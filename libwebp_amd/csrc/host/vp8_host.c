@@ -437,6 +437,60 @@ void vp8h_set_loop_params(vp8h_frame* fr, float quality, uint8_t* segmap, vp8g_f
 }
 
 /* ------------------------------------------------------------------------ */
+/* Alpha level reduction: src/utils/quant_levels_utils.c:31-137 */
+
+int vp8h_alpha_levels(int quality) {
+  return (quality <= 70) ? (2 + quality / 5) : (16 + (quality - 70) * 8);
+}
+
+void vp8h_quantize_levels_map(const uint32_t hist[256], uint64_t count, int num_levels,
+                              uint8_t map[256], uint64_t* sse) {
+  int q_level[256] = {0};
+  double inv_q_level[256] = {0};
+  int min_s = 255, max_s = 0, num_levels_in = 0;
+  double last_err = 1.e38, err = 0.;
+  const double err_threshold = 1e-4 * (double)count;
+  for (int s = 0; s < 256; ++s) {
+    map[s] = (uint8_t)s;
+    if (hist[s]) {
+      ++num_levels_in;
+      if (min_s > s) min_s = s;
+      if (max_s < s) max_s = s;
+    }
+  }
+  if (num_levels_in > num_levels) {
+    for (int i = 0; i < num_levels; ++i)
+      inv_q_level[i] = min_s + (double)(max_s - min_s) * i / (num_levels - 1);
+    q_level[min_s] = 0;
+    q_level[max_s] = num_levels - 1;
+    for (int iter = 0; iter < 6; ++iter) {   /* k-means, MAX_ITER */
+      double q_sum[256] = {0}, q_count[256] = {0};
+      int slot = 0;
+      for (int s = min_s; s <= max_s; ++s) {
+        while (slot < num_levels - 1 && 2 * s > inv_q_level[slot] + inv_q_level[slot + 1]) ++slot;
+        if (hist[s] > 0) {
+          q_sum[slot] += s * (int)hist[s];
+          q_count[slot] += (int)hist[s];
+        }
+        q_level[s] = slot;
+      }
+      if (num_levels > 2)
+        for (slot = 1; slot < num_levels - 1; ++slot)
+          if (q_count[slot] > 0.) inv_q_level[slot] = q_sum[slot] / q_count[slot];
+      err = 0.;
+      for (int s = min_s; s <= max_s; ++s) {
+        const double e = s - inv_q_level[q_level[s]];
+        err += (int)hist[s] * e * e;
+      }
+      if (last_err - err < err_threshold) break;
+      last_err = err;
+    }
+    for (int s = min_s; s <= max_s; ++s) map[s] = (uint8_t)(inv_q_level[q_level[s]] + .5);
+  }
+  if (sse) *sse = (uint64_t)err;
+}
+
+/* ------------------------------------------------------------------------ */
 /* Boolean coder: bit_writer_utils.c:26-179. Renormalisation shift is
  * 7 - floor(log2(range + 1)) (the kNorm / kNewRange tables). */
 

@@ -87,6 +87,14 @@ int vp8h_finalize_probas(const uint32_t* stats, uint8_t* coeffs, int* dirty);
 double vp8h_pass_size_value(uint64_t finalize_cost, uint64_t token_bits, uint64_t size_p0);
 double vp8h_psnr(uint64_t mse, uint64_t count);   /* GetPSNR, frame_enc.c:554-556 */
 
+/* QuantizeLevels (src/utils/quant_levels_utils.c:31-137) from the plane's
+ * histogram: the symbol map to num_levels levels (identity when the plane has
+ * no more levels than that) and the squared error it reports. */
+void vp8h_quantize_levels_map(const uint32_t hist[256], uint64_t count, int num_levels,
+                              uint8_t map[256], uint64_t* sse);
+/* alpha_enc.c:346-347: levels for an alpha_quality < 100 */
+int vp8h_alpha_levels(int quality);
+
 /* Boolean coder (bit_writer_utils.c). */
 typedef struct {
   int32_t range, value;

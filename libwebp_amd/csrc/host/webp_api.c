@@ -479,8 +479,6 @@ int WebPEncode(const WebPConfig* config, WebPPicture* pic) {
   }
   if (!config->exact) WebPCleanupTransparentArea(pic);   /* webp_enc.c:369-371 */
   const int has_alpha = pic->a != NULL && WebPPictureHasTransparency(pic);
-  if (has_alpha && config->alpha_quality < 100)   /* QuantizeLevels not implemented */
-    return set_error(pic, VP8_ENC_ERROR_INVALID_CONFIGURATION);
 
   pthread_mutex_lock(&g_engine_lock);
   WebPGpuBatch* e = engine_for(config, pic->width, pic->height);
@@ -501,7 +499,9 @@ int WebPEncode(const WebPConfig* config, WebPPicture* pic) {
   memset(&fr, 0, sizeof(fr));
   memset(&res, 0, sizeof(res));
   int hdr[2] = {0, 0};
+  uint64_t asse = 0;
   if (ok) {
+    asse = has_alpha ? e->asse[0] : 0;
     fr = e->frames[0];
     res = e->h_results[0];
     hdr[0] = e->hdr[0];
@@ -524,7 +524,7 @@ int WebPEncode(const WebPConfig* config, WebPPicture* pic) {
     s->PSNR[1] = (float)psnr(res.sse[1], count / 4);
     s->PSNR[2] = (float)psnr(res.sse[2], count / 4);
     s->PSNR[3] = (float)psnr(res.sse[0] + res.sse[1] + res.sse[2], count * 3 / 2);
-    s->PSNR[4] = (float)psnr(0, count);
+    s->PSNR[4] = (float)psnr(asse, count);   /* enc->sse_[3], alpha_enc.c:362 */
     for (int i = 0; i < 3; ++i) s->block_count[i] = res.block_count[i];
     s->header_bytes[0] = hdr[0];
     s->header_bytes[1] = hdr[1];

@@ -112,6 +112,14 @@ int vp8g_launch_cleanup_alpha(uint8_t* yuv, size_t yuv_frame_bytes, const uint8_
  * analysis (FastMBAnalyze with that integer quality); mb_amode (or NULL)
  * receives per MB the analysis UV mode (bit 0) and, for methods 0-1, the
  * intra-4 pick (bit 1), inputs of the RD_OPT_NONE encoder */
+/* alpha level reduction (QuantizeLevels): per-frame 256-bin histograms of
+ * the alpha planes of the frames with aflags set (hist zeroed here), and the
+ * remap of those planes through maps[f * 256 + symbol] */
+int vp8g_launch_alpha_hist(const uint8_t* aplane, size_t plane, const uint32_t* aflags, int n,
+                           uint32_t* hist, void* stream);
+int vp8g_launch_alpha_remap(uint8_t* aplane, size_t plane, const uint32_t* aflags, int n,
+                            const uint8_t* maps, void* stream);
+
 int vp8g_launch_analysis(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h,
                          int n, uint8_t* mb_alpha, uint16_t* mb_uva, int fast_q,
                          uint8_t* mb_amode, void* stream);

@@ -900,3 +900,54 @@ def riff_vp8x(w, h, alph, vp8):
     vp8x = struct.pack("<I", 0x10) + struct.pack("<I", w - 1)[:3] + struct.pack("<I", h - 1)[:3]
     body = chunk(b"VP8X", vp8x) + chunk(b"ALPH", alph) + chunk(b"VP8 ", vp8)
     return b"RIFF" + struct.pack("<I", 4 + len(body)) + b"WEBP" + body
+
+
+def quantize_levels(plane, num_levels):
+    """QuantizeLevels (src/utils/quant_levels_utils.c:31-137): reduce an alpha
+    plane to num_levels values by a 1-D k-means over its 256-bin histogram
+    (at most 6 iterations, stop when the error gain < 1e-4 per sample), then
+    map every symbol to its rounded centroid. Doubles throughout, in the
+    reference's order of operations. Returns (plane, sse)."""
+    plane = np.asarray(plane, np.uint8)
+    freq = np.bincount(plane.ravel(), minlength=256).astype(np.int64)
+    nz = np.nonzero(freq)[0]
+    if len(nz) <= num_levels:
+        return plane.copy(), 0
+    min_s, max_s = int(nz[0]), int(nz[-1])
+    inv = [0.0] * 256
+    for i in range(num_levels):
+        inv[i] = min_s + float(max_s - min_s) * i / (num_levels - 1)
+    q = [0] * 256
+    q[min_s], q[max_s] = 0, num_levels - 1
+    last_err, err = 1.e38, 0.0
+    thr = 1e-4 * plane.size
+    for _ in range(6):
+        q_sum, q_cnt = [0.0] * 256, [0.0] * 256
+        slot = 0
+        for s in range(min_s, max_s + 1):
+            while slot < num_levels - 1 and 2 * s > inv[slot] + inv[slot + 1]:
+                slot += 1
+            if freq[s] > 0:
+                q_sum[slot] += s * int(freq[s])
+                q_cnt[slot] += int(freq[s])
+            q[s] = slot
+        if num_levels > 2:
+            for slot in range(1, num_levels - 1):
+                if q_cnt[slot] > 0.0:
+                    inv[slot] = q_sum[slot] / q_cnt[slot]
+        err = 0.0
+        for s in range(min_s, max_s + 1):
+            e = s - inv[q[s]]
+            err += int(freq[s]) * e * e
+        if last_err - err < thr:
+            break
+        last_err = err
+    lut = np.arange(256, dtype=np.uint8)
+    for s in range(min_s, max_s + 1):
+        lut[s] = int(inv[q[s]] + .5)
+    return lut[plane], int(err)
+
+
+def alpha_levels(quality):
+    """alpha_enc.c:346-347: levels for alpha_quality < 100."""
+    return (2 + quality // 5) if quality <= 70 else (16 + (quality - 70) * 8)

@@ -21,15 +21,21 @@ from oracle import vp8l_model as M  # noqa: E402
 from test_alpha import alpha_frame  # noqa: E402
 
 CASES = [
-    # api, w, h, frame, q, m, exact, alpha_compression
-    ("batch", 64, 48, 0, 75.0, 4, 0, 1),
-    ("batch", 333, 257, 5, 75.0, 4, 0, 1),
-    ("batch", 128, 96, 2, 90.0, 6, 1, 1),
-    ("batch", 200, 130, 3, 75.0, 4, 0, 0),
-    ("batch", 512, 384, 1, 75.0, 4, 0, 1),
-    ("webpencode", 160, 120, 4, 75.0, 4, 0, 1),
-    ("webpencode", 97, 61, 2, 80.0, 5, 0, 1),
-    ("webpencode", 96, 64, 6, 75.0, 3, 1, 0),
+    # api, w, h, frame, q, m, exact, alpha_compression, alpha_quality
+    ("batch", 64, 48, 0, 75.0, 4, 0, 1, 100),
+    ("batch", 333, 257, 5, 75.0, 4, 0, 1, 100),
+    ("batch", 128, 96, 2, 90.0, 6, 1, 1, 100),
+    ("batch", 200, 130, 3, 75.0, 4, 0, 0, 100),
+    ("batch", 512, 384, 1, 75.0, 4, 0, 1, 100),
+    ("webpencode", 160, 120, 4, 75.0, 4, 0, 1, 100),
+    ("webpencode", 97, 61, 2, 80.0, 5, 0, 1, 100),
+    ("webpencode", 96, 64, 6, 75.0, 3, 1, 0, 100),
+    # alpha_quality < 100: QuantizeLevels (src/utils/quant_levels_utils.c)
+    ("batch", 200, 130, 7, 75.0, 4, 0, 1, 50),
+    ("batch", 333, 257, 8, 75.0, 4, 0, 1, 0),
+    ("batch", 128, 96, 9, 75.0, 2, 0, 0, 85),
+    ("webpencode", 160, 120, 10, 75.0, 4, 0, 1, 90),
+    ("webpencode", 97, 61, 11, 60.0, 4, 1, 1, 20),
 ]
 
 
@@ -37,15 +43,16 @@ def main():
     lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libwebp_ref.so"))
     ref = abi.bind_encoder_api(lib)
     out = []
-    for api, w, h, f, q, m, exact, ac in CASES:
+    for api, w, h, f, q, m, exact, ac, aq in CASES:
         img = alpha_frame(w, h, f)
         data, _ = abi.encode_rgba(ref, img, quality=q, method=m, exact=exact,
-                                  alpha_compression=ac)
+                                  alpha_compression=ac, alpha_quality=aq)
         ch = dict(M.riff_chunks(data))
         dec = M.ref_decode(lib, data)
-        assert (dec[..., 3] == img[..., 3]).all()
+        assert aq < 100 or (dec[..., 3] == img[..., 3]).all()
         out.append({"api": api, "w": w, "h": h, "frame": f, "q": q, "m": m, "exact": exact,
-                    "alpha_compression": ac,
+                    "alpha_compression": ac, "alpha_quality": aq,
+                    "alpha_sha256": hashlib.sha256(dec[..., 3].tobytes()).hexdigest(),
                     "in_sha": hashlib.sha256(img.tobytes()).hexdigest()[:16],
                     "ref_size": len(data), "ref_alph_size": len(ch[b"ALPH"]),
                     "vp8_sha256": hashlib.sha256(ch[b"VP8 "]).hexdigest(),

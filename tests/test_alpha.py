@@ -65,7 +65,11 @@ def check(data, img, case):
     lib = decoder_or_none()
     if lib is not None:
         dec = M.ref_decode(lib, data)
-        assert np.array_equal(dec[..., 3], img[..., 3])
+        if case["alpha_quality"] < 100:   # the reference's level-reduced plane
+            assert hashlib.sha256(dec[..., 3].tobytes()).hexdigest() == case["alpha_sha256"]
+            assert chunks(data)[b"ALPH"][0] >> 4 == 1   # ALPHA_PREPROCESSED_LEVELS
+        else:
+            assert np.array_equal(dec[..., 3], img[..., 3])
         assert hashlib.sha256(dec[..., :3].tobytes()).hexdigest() == case["rgb_sha256"]
 
 
@@ -78,14 +82,15 @@ def test_gpu_batch_alpha_frames(gpu):
         w, h, f = case["w"], case["h"], case["frame"]
         frames = np.stack([alpha_frame(w, h, f), syn_v1(w, h, f + 1)])
         enc = gpu.GpuBatch(w, h, 2, quality=case["q"], method=case["m"], exact=case["exact"],
-                           alpha_compression=case["alpha_compression"])
+                           alpha_compression=case["alpha_compression"],
+                           alpha_quality=case["alpha_quality"])
         buf = torch.from_numpy(frames).to("cuda:0")
         torch.cuda.synchronize()
         enc.encode_device(buf.data_ptr(), 2)
         check(enc.output(0), frames[0], case)
         assert chunks(enc.output(1)).keys() == {b"VP8 "}   # opaque frame: no VP8X/ALPH
         if case["alpha_compression"] == 0:
-            assert chunks(enc.output(0))[b"ALPH"][0] == 0
+            assert chunks(enc.output(0))[b"ALPH"][0] & 3 == 0   # ALPHA_NO_COMPRESSION
         enc.close()
 
 
@@ -96,12 +101,17 @@ def test_gpu_api_alpha(gpu):
             continue
         img = alpha_frame(case["w"], case["h"], case["frame"])
         data = gpu.encode_rgba(img, quality=case["q"], method=case["m"], exact=case["exact"],
-                               alpha_compression=case["alpha_compression"])
+                               alpha_compression=case["alpha_compression"],
+                               alpha_quality=case["alpha_quality"])
         check(data, img, case)
 
 
-@pytest.mark.gpu
-def test_gpu_alpha_quality_below_100_fails_loudly(gpu):
-    img = alpha_frame(64, 48, 0)
-    with pytest.raises(RuntimeError):
-        gpu.encode_rgba(img, quality=75.0, method=4, alpha_quality=80)
+def test_quantize_levels_model_matches_reference():
+    """The oracle's QuantizeLevels restatement reproduces the level-reduced
+    alpha planes the reference's own encodes decode to."""
+    for case in kat()["cases"]:
+        if case["alpha_quality"] >= 100:
+            continue
+        img = alpha_frame(case["w"], case["h"], case["frame"])
+        q, _ = M.quantize_levels(img[..., 3], M.alpha_levels(case["alpha_quality"]))
+        assert hashlib.sha256(q.tobytes()).hexdigest() == case["alpha_sha256"]

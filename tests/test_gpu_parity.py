@@ -109,7 +109,7 @@ def test_oracle_random_small(gpu):
 
 def test_transparent_input_gets_alph_chunk(gpu):
     """One translucent pixel: VP8X + ALPH + VP8 (tests/test_alpha.py has the
-    parity checks); alpha_quality < 100 is refused, not approximated."""
+    parity checks), also with alpha level reduction (alpha_quality < 100)."""
     img = syn_v1(32, 32, 0).copy()
     img[5, 5, 3] = 10
     enc = gpu.GpuBatch(32, 32, 1)
@@ -119,7 +119,8 @@ def test_transparent_input_gets_alph_chunk(gpu):
     enc.close()
     enc = gpu.GpuBatch(32, 32, 1, alpha_quality=90)
     enc.encode_host(img[None])
-    assert enc.error(0) != 0
+    assert enc.error(0) == 0
+    assert enc.output(0)[12:16] == b"VP8X"
     enc.close()
 
 

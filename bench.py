@@ -287,7 +287,7 @@ def main():
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6),
                      "traffic": None if args.sharp_yuv else
-                     measured_traffic("k_encode<3, false>", B, W, H, args.quality, args.method),
+                     measured_traffic("k_encode<3, false, false>", B, W, H, args.quality, args.method),
                      "traffic_source": "profiles/r1_pmc_hbm.csv (rocprofv3 --pmc FETCH_SIZE, "
                                        "WRITE_SIZE passes of this workload; bytes per launch)",
                      "k_encode_ms": round(1e3 * k3_avg_s, 3),

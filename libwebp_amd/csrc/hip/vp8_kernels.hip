@@ -29,11 +29,14 @@ __device__ __forceinline__ int lin_to_gamma(const int* l2g, uint32_t sum, int sh
   const int pos = v >> 9, frac = v & 511;
   return (l2g[pos + 1] * frac + l2g[pos] * (512 - frac) + 64) >> 7;
 }
-__device__ __forceinline__ int rgb_to_y(int r, int g, int b) {
-  return (16839 * r + 33059 * g + 6420 * b + (1 << 15) + (16 << 16)) >> 16;
+// VP8RGBToY / VP8ClipUV (src/dsp/yuv.h:186-204) with the rounding term:
+// YUV_HALF (<< 2 for chroma), or the dithered one of VP8RandomBits
+// (picture_csp_enc.c:153-166) when the import dithers
+__device__ __forceinline__ int rgb_to_y(int r, int g, int b, int rnd = 1 << 15) {
+  return (16839 * r + 33059 * g + 6420 * b + rnd + (16 << 16)) >> 16;
 }
-__device__ __forceinline__ int clip_uv(int v) {
-  v = (v + (1 << 17) + (128 << 18)) >> 18;
+__device__ __forceinline__ int clip_uv(int v, int rnd = 1 << 17) {
+  v = (v + rnd + (128 << 18)) >> 18;
   return (v & ~0xff) == 0 ? v : (v < 0 ? 0 : 255);
 }
 
@@ -43,7 +46,9 @@ __global__ __launch_bounds__(256) void k_import(const uint8_t* __restrict__ rgba
                                                 uint32_t* __restrict__ aflags,
                                                 uint8_t* __restrict__ aplane,
                                                 const uint16_t* __restrict__ g_g2l,
-                                                const int32_t* __restrict__ g_l2g) {
+                                                const int32_t* __restrict__ g_l2g,
+                                                const uint16_t* __restrict__ rnd_y,
+                                                const uint32_t* __restrict__ rnd_uv) {
   __shared__ uint16_t g2l[256];
   __shared__ int l2g[33];
   const int t = threadIdx.x;
@@ -84,11 +89,16 @@ __global__ __launch_bounds__(256) void k_import(const uint8_t* __restrict__ rgba
     }
   }
   uint8_t* yrow = Y + (size_t)y0 * w + x0;
-  yrow[0] = rgb_to_y(p[0][0][0], p[0][0][1], p[0][0][2]);
-  if (two_cols) yrow[1] = rgb_to_y(p[0][1][0], p[0][1][1], p[0][1][2]);
+  const size_t yo = (size_t)y0 * w + x0;
+  const int ry00 = rnd_y ? rnd_y[yo] : 1 << 15;
+  const int ry01 = rnd_y && two_cols ? rnd_y[yo + 1] : 1 << 15;
+  const int ry10 = rnd_y && two_rows ? rnd_y[yo + w] : 1 << 15;
+  const int ry11 = rnd_y && two_rows && two_cols ? rnd_y[yo + w + 1] : 1 << 15;
+  yrow[0] = rgb_to_y(p[0][0][0], p[0][0][1], p[0][0][2], ry00);
+  if (two_cols) yrow[1] = rgb_to_y(p[0][1][0], p[0][1][1], p[0][1][2], ry01);
   if (two_rows) {
-    yrow[w] = rgb_to_y(p[1][0][0], p[1][0][1], p[1][0][2]);
-    if (two_cols) yrow[w + 1] = rgb_to_y(p[1][1][0], p[1][1][1], p[1][1][2]);
+    yrow[w] = rgb_to_y(p[1][0][0], p[1][0][1], p[1][0][2], ry10);
+    if (two_cols) yrow[w + 1] = rgb_to_y(p[1][1][0], p[1][1][1], p[1][1][2], ry11);
   }
   // AccumulateRGBA (picture_csp_enc.c:388-424): 2x2 blocks with partial
   // alpha average in linear light weighted by alpha, divided through
@@ -117,8 +127,11 @@ __global__ __launch_bounds__(256) void k_import(const uint8_t* __restrict__ rgba
       c[k] = lin_to_gamma(l2g, (uint32_t)g2l[p[0][0][k]] + g2l[p[1][0][k]], 1);
     }
   }
-  U[(size_t)j * uvw + i] = clip_uv(-9719 * c[0] - 19081 * c[1] + 28800 * c[2]);
-  V[(size_t)j * uvw + i] = clip_uv(28800 * c[0] - 24116 * c[1] - 4684 * c[2]);
+  const size_t uo = (size_t)j * uvw + i;
+  const int ru = rnd_uv ? (int)rnd_uv[2 * uo] : 1 << 17;
+  const int rv = rnd_uv ? (int)rnd_uv[2 * uo + 1] : 1 << 17;
+  U[uo] = clip_uv(-9719 * c[0] - 19081 * c[1] + 28800 * c[2], ru);
+  V[uo] = clip_uv(28800 * c[0] - 24116 * c[1] - 4684 * c[2], rv);
 }
 
 // alpha plane of the sharp-YUV path (WebPExtractAlpha)
@@ -1421,12 +1434,13 @@ extern "C" {
 
 int vp8g_launch_import(const uint8_t* rgba, size_t fstride, int rstride, int w, int h, int n,
                        uint8_t* yuv, size_t yfb, uint32_t* aflags, uint8_t* aplane,
-                       const uint16_t g2l[256], const int32_t l2g[33], void* stream) {
+                       const uint16_t g2l[256], const int32_t l2g[33], const uint16_t* rnd_y,
+                       const uint32_t* rnd_uv, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int uvw = (w + 1) >> 1, uvh = (h + 1) >> 1;
   dim3 grid((uvw + 255) / 256, uvh, n);
   hipLaunchKernelGGL(k_import, grid, dim3(256), 0, st, rgba, fstride, rstride, w, h, yuv, yfb,
-                     aflags, aplane, g2l, l2g);
+                     aflags, aplane, g2l, l2g, rnd_y, rnd_uv);
   return launch_check("k_import");
 }
 

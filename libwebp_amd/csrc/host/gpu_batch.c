@@ -108,6 +108,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   b->yfb = (b->yfb + 255) & ~(size_t)255;
   b->tok_cap = (size_t)b->nmb * VP8G_MAX_TOKENS_PER_MB;
   b->sharp = vp8h_use_sharp(config, width, height);
+  b->dither = b->sharp ? 0.f : vp8h_import_dithering(config);
   b->threads = host_threads > 0 ? host_threads : default_threads();
   {   /* WEBP_AMD_HOST_EMIT=1: boolean-code partition 1 on the host threads */
     const char* he = getenv("WEBP_AMD_HOST_EMIT");
@@ -178,6 +179,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs); hipFree(b->d_nbuf);
   hipFree(b->d_eimg);
   hipFree(b->d_stabs); hipFree(b->d_sharp); hipFree(b->d_sstate);
+  hipFree(b->d_rnd_y); hipFree(b->d_rnd_uv);
   hipFree(b->d_active); hipFree(b->d_tbits);
   hipFree(b->d_ahist); hipFree(b->d_amaps); hipHostFree(b->h_ahist); hipHostFree(b->h_amaps);
   free(b->asse);
@@ -669,9 +671,34 @@ fail:
  * kernels (hip/vp8_sharp.hip) when requested. */
 static int launch_import(WebPGpuBatch* b, const uint8_t* rgba, size_t fstride, int rstride, int n,
                          int sharp) {
-  if (!sharp)
+  if (!sharp) {
+    if (b->dither > 0.f && b->dither != b->dither_built) {
+      /* dithered import (preprocessing & 2): the VP8Random rounding terms
+       * depend only on the size and amplitude, so every frame shares them */
+      const size_t ny = (size_t)b->w * b->h, nuv = 2 * (size_t)b->uvw * b->uvh;
+      uint16_t* ry = (uint16_t*)malloc(ny * sizeof(uint16_t));
+      uint32_t* ruv = (uint32_t*)malloc(nuv * sizeof(uint32_t));
+      int ok = ry && ruv;
+      if (ok) vp8h_dither_rounders(b->w, b->h, b->dither, ry, ruv);
+      if (ok && !b->d_rnd_y)
+        ok = hipMalloc((void**)&b->d_rnd_y, ny * sizeof(uint16_t)) == hipSuccess &&
+             hipMalloc((void**)&b->d_rnd_uv, nuv * sizeof(uint32_t)) == hipSuccess;
+      ok = ok && hipMemcpy(b->d_rnd_y, ry, ny * sizeof(uint16_t), hipMemcpyHostToDevice) ==
+                     hipSuccess &&
+           hipMemcpy(b->d_rnd_uv, ruv, nuv * sizeof(uint32_t), hipMemcpyHostToDevice) == hipSuccess;
+      free(ry);
+      free(ruv);
+      if (!ok) {
+        vp8g_set_error("launch_import", "dither rounders");
+        return 0;
+      }
+      b->dither_built = b->dither;
+    }
+    const int dith = b->dither > 0.f;
     return vp8g_launch_import(rgba, fstride, rstride, b->w, b->h, n, b->d_yuv, b->yfb,
-                              b->d_aflags, b->d_aplane, b->d_g2l, b->d_l2g, b->stream);
+                              b->d_aflags, b->d_aplane, b->d_g2l, b->d_l2g,
+                              dith ? b->d_rnd_y : NULL, dith ? b->d_rnd_uv : NULL, b->stream);
+  }
   if (!vp8g_launch_extract_alpha(rgba, fstride, rstride, b->w, b->h, n, b->d_aplane, b->stream))
     return 0;
   if (!b->d_sharp) {   /* first sharp call: scratch for max_frames frames */
@@ -831,10 +858,12 @@ int vp8g_engine_upload_yuv(WebPGpuBatch* b, int f, const uint8_t* y, int ys, con
 }
 
 int vp8g_engine_import(WebPGpuBatch* b, const uint8_t* rgba, int stride, uint8_t* y,
-                       uint8_t* u, uint8_t* v, uint8_t* a, int* has_alpha, int sharp) {
+                       uint8_t* u, uint8_t* v, uint8_t* a, int* has_alpha, int sharp,
+                       float dither) {
   /* synchronous single-frame RGBA -> YUV through K1 (used by the
    * WebPPictureImport* API); output written to the caller's host planes */
   if (hipSetDevice(b->device) != hipSuccess) return 0;
+  b->dither = dither;
   const size_t need = (size_t)stride * b->h;
   if (need > b->d_rgba_cap) {
     hipFree(b->d_rgba);

@@ -66,6 +66,9 @@ struct WebPGpuBatch {
   size_t emit_seg_cap, emit_word_cap;
   /* sharp-YUV import (allocated on first use) */
   int sharp;                 /* config asks for it and the frame is >= 4x4 */
+  float dither, dither_built;   /* dithered K1 import (preprocessing & 2) */
+  uint16_t* d_rnd_y;         /* its rounding terms (VP8Random), built on first use */
+  uint32_t* d_rnd_uv;
   uint32_t* d_stabs;         /* 1026 gamma->linear + 514 linear->gamma */
   uint8_t* d_sharp;          /* per-frame W/RGB planes */
   vp8g_sharp_state* d_sstate;
@@ -106,7 +109,8 @@ int vp8g_engine_upload_yuv(struct WebPGpuBatch* b, int f, const uint8_t* y, int 
                            const uint8_t* u, const uint8_t* v, int uvs, const uint8_t* a,
                            int as);
 int vp8g_engine_import(struct WebPGpuBatch* b, const uint8_t* rgba, int stride, uint8_t* y,
-                       uint8_t* u, uint8_t* v, uint8_t* a, int* has_alpha, int sharp);
+                       uint8_t* u, uint8_t* v, uint8_t* a, int* has_alpha, int sharp,
+                       float dither);
 #ifdef __cplusplus
 }
 #endif

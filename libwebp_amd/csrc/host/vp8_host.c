@@ -56,7 +56,7 @@ int vp8h_frame_init(vp8h_frame* fr, const WebPConfig* cfg, int w, int h) {
    * (one bit writer per MB row modulo 2^partitions) are not implemented */
   if (cfg->method < 3 && (cfg->target_size > 0 || cfg->target_PSNR > 0 || cfg->partitions > 0))
     return 0;
-  if (cfg->low_memory || (cfg->preprocessing & 2)) return 0;
+  if (cfg->low_memory) return 0;
   fr->w = w; fr->h = h;
   fr->mbw = (w + 15) >> 4; fr->mbh = (h + 15) >> 4;
   fr->method = cfg->method;
@@ -434,6 +434,69 @@ void vp8h_set_loop_params(vp8h_frame* fr, float quality, uint8_t* segmap, vp8g_f
   P->nb_stat = fr->method == 0 ? ((nmb > 200) ? nmb >> 2 : 50) : nmb;
   P->none_finalize = fr->seg_hdr_size != 0;
   if (fr->rd_opt == 0) P->max_count = 0x7fffffff;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Dithered RGB -> YUV import: webp_enc.c:357-365, picture_csp_enc.c:150-166,
+ * 520-619, utils/random_utils.{h,c} */
+
+float vp8h_import_dithering(const WebPConfig* cfg) {
+  if (!(cfg->preprocessing & 2)) return 0.f;
+  const float x = cfg->quality / 100.f;
+  const float x2 = x * x;
+  return 1.0f + (0.5f - 1.0f) * x2 * x2;   /* 1 at q 0 down to 0.5 at q 100 */
+}
+
+static const uint32_t kRandomTable[55] = {   /* random_utils.c:19-29 */
+    0x0de15230, 0x03b31886, 0x775faccb, 0x1c88626a, 0x68385c55, 0x14b3b828, 0x4a85fef8,
+    0x49ddb84b, 0x64fcf397, 0x5c550289, 0x4a290000, 0x0d7ec1da, 0x5940b7ab, 0x5492577d,
+    0x4e19ca72, 0x38d38c69, 0x0c01ee65, 0x32a1755f, 0x5437f652, 0x5abb2c32, 0x0faa57b1,
+    0x73f533e7, 0x685feeda, 0x7563cce2, 0x6e990e83, 0x4730a7ed, 0x4fc0d9c6, 0x496b153c,
+    0x4f1403fa, 0x541afb0c, 0x73990b32, 0x26d7cb1c, 0x6fcc3706, 0x2cbb77d8, 0x75762f2a,
+    0x6425ccdd, 0x24b35461, 0x0a7d8715, 0x220414a8, 0x141ebf67, 0x56b41583, 0x73e502e3,
+    0x44cab16f, 0x28264d42, 0x73baaefb, 0x0a50ebed, 0x1d6ab6fb, 0x0d3ad40b, 0x35db3b68,
+    0x2b081e83, 0x77ce6b95, 0x5181e5f0, 0x78853bbc, 0x009f9494, 0x27e5ed3c};
+
+typedef struct {
+  int i1, i2, amp;
+  uint32_t tab[55];
+} DitherRng;
+
+static int rng_bits(DitherRng* rg, int num_bits) {   /* VP8RandomBits2 */
+  int diff = (int)(rg->tab[rg->i1] - rg->tab[rg->i2]);
+  if (diff < 0) diff = (int)((uint32_t)diff + (1u << 31));
+  rg->tab[rg->i1] = (uint32_t)diff;
+  if (++rg->i1 == 55) rg->i1 = 0;
+  if (++rg->i2 == 55) rg->i2 = 0;
+  diff = (int)((uint32_t)diff << 1) >> (32 - num_bits);   /* sign-extend, 0-center */
+  diff = (diff * rg->amp) >> 8;
+  return diff + (1 << (num_bits - 1));
+}
+
+void vp8h_dither_rounders(int w, int h, float dithering, uint16_t* ry, uint32_t* ruv) {
+  DitherRng rg;
+  memcpy(rg.tab, kRandomTable, sizeof(rg.tab));
+  rg.i1 = 0;
+  rg.i2 = 31;
+  rg.amp = (dithering < 0.0) ? 0 : (dithering > 1.0) ? 256 : (int)(uint32_t)(256 * dithering);
+  const int uvw = (w + 1) >> 1;
+  /* the reference's order: two Y rows, then the U,V pairs of their chroma row */
+  for (int y = 0; y < (h >> 1); ++y) {
+    for (int r = 0; r < 2; ++r)
+      for (int x = 0; x < w; ++x) ry[(size_t)(2 * y + r) * w + x] = (uint16_t)rng_bits(&rg, 16);
+    for (int i = 0; i < uvw; ++i) {
+      ruv[2 * ((size_t)y * uvw + i)] = (uint32_t)rng_bits(&rg, 18);
+      ruv[2 * ((size_t)y * uvw + i) + 1] = (uint32_t)rng_bits(&rg, 18);
+    }
+  }
+  if (h & 1) {
+    const int y = h >> 1;
+    for (int x = 0; x < w; ++x) ry[(size_t)(h - 1) * w + x] = (uint16_t)rng_bits(&rg, 16);
+    for (int i = 0; i < uvw; ++i) {
+      ruv[2 * ((size_t)y * uvw + i)] = (uint32_t)rng_bits(&rg, 18);
+      ruv[2 * ((size_t)y * uvw + i) + 1] = (uint32_t)rng_bits(&rg, 18);
+    }
+  }
 }
 
 /* ------------------------------------------------------------------------ */

@@ -87,6 +87,14 @@ int vp8h_finalize_probas(const uint32_t* stats, uint8_t* coeffs, int* dirty);
 double vp8h_pass_size_value(uint64_t finalize_cost, uint64_t token_bits, uint64_t size_p0);
 double vp8h_psnr(uint64_t mse, uint64_t count);   /* GetPSNR, frame_enc.c:554-556 */
 
+/* Dithered import (preprocessing & 2): the amplitude WebPEncode derives from
+ * the quality (webp_enc.c:357-365, 0 when off), and the rounding terms the
+ * VP8Random generator feeds RGBToY / RGBToU / RGBToV in the reference's
+ * order (picture_csp_enc.c:150-166,520-619): ry[W*H], ruv[2*uvw*uvh] (U, V
+ * interleaved per chroma sample). */
+float vp8h_import_dithering(const WebPConfig* cfg);
+void vp8h_dither_rounders(int w, int h, float dithering, uint16_t* ry, uint32_t* ruv);
+
 /* QuantizeLevels (src/utils/quant_levels_utils.c:31-137) from the plane's
  * histogram: the symbol map to num_levels levels (identity when the plane has
  * no more levels than that) and the squared error it reports. */

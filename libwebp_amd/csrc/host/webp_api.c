@@ -281,8 +281,17 @@ static WebPGpuBatch* lossless_engine_for(const WebPConfig* cfg, int w, int h) {
 
 /* ---- import (picture_csp_enc.c:474-619, 732-844) ---- */
 
+static int import_packed_d(WebPPicture* pic, const uint8_t* src, int stride, int step,
+                           int swap_rb, int with_alpha, int sharp, float dither);
 static int import_packed(WebPPicture* pic, const uint8_t* src, int stride, int step, int swap_rb,
                          int with_alpha, int sharp) {
+  return import_packed_d(pic, src, stride, step, swap_rb, with_alpha, sharp, 0.f);
+}
+
+/* dither > 0: the dithered conversion of WebPPictureARGBToYUVADithered
+ * (picture_csp_enc.c:520-619), amplitude in [0, 1] */
+static int import_packed_d(WebPPicture* pic, const uint8_t* src, int stride, int step,
+                           int swap_rb, int with_alpha, int sharp, float dither) {
   const int w = pic->width, h = pic->height;
   if (abs(stride) < (with_alpha ? 4 : step) * w) return 0;
   const int ri = swap_rb ? 2 : 0, bi = swap_rb ? 0 : 2;
@@ -322,7 +331,8 @@ static int import_packed(WebPPicture* pic, const uint8_t* src, int stride, int s
     WebPGpuBatch* e = engine_for(&cfg, w, h);
     int has_alpha = 0;
     ok = e != NULL && vp8g_engine_import(e, rgba, 4 * w, pic->y, pic->u, pic->v,
-                                         translucent ? pic->a : NULL, &has_alpha, sharp);
+                                         translucent ? pic->a : NULL, &has_alpha, sharp,
+                                         sharp ? 0.f : dither);
     pthread_mutex_unlock(&g_engine_lock);
     if (!ok) set_error(pic, VP8_ENC_ERROR_OUT_OF_MEMORY);
   }
@@ -351,7 +361,7 @@ int WebPPictureImportBGRX(WebPPicture* p, const uint8_t* s, int st) {
 
 /* picture_csp_enc.c:622-664: ARGB container -> YUV420 through K1, or the
  * sharp-YUV kernels when `sharp` */
-static int argb_to_yuva(WebPPicture* p, WebPEncCSP csp, int sharp) {
+static int argb_to_yuva(WebPPicture* p, WebPEncCSP csp, int sharp, float dither) {
   if (p == NULL) return 0;
   if (p->argb == NULL) return set_error(p, VP8_ENC_ERROR_NULL_PARAMETER);
   if ((csp & WEBP_CSP_UV_MASK) != WEBP_YUV420)
@@ -370,7 +380,7 @@ static int argb_to_yuva(WebPPicture* p, WebPEncCSP csp, int sharp) {
   const int keep_stride = p->argb_stride;
   p->use_argb = 0;
   p->memory_argb_ = NULL;   /* keep ARGB alive across the YUV allocation */
-  const int ok = import_packed(p, bgra, 4 * w, 4, 1, 1, sharp);
+  const int ok = import_packed_d(p, bgra, 4 * w, 4, 1, 1, sharp, dither);
   p->memory_argb_ = keep_argb;
   p->argb = keep_ptr;
   p->argb_stride = keep_stride;
@@ -378,17 +388,18 @@ static int argb_to_yuva(WebPPicture* p, WebPEncCSP csp, int sharp) {
   return ok;
 }
 
-int WebPPictureARGBToYUVA(WebPPicture* p, WebPEncCSP csp) { return argb_to_yuva(p, csp, 0); }
+int WebPPictureARGBToYUVA(WebPPicture* p, WebPEncCSP csp) {
+  return argb_to_yuva(p, csp, 0, 0.f);
+}
 
-int WebPPictureSharpARGBToYUVA(WebPPicture* p) { return argb_to_yuva(p, WEBP_YUV420, 1); }
+int WebPPictureSharpARGBToYUVA(WebPPicture* p) { return argb_to_yuva(p, WEBP_YUV420, 1, 0.f); }
 int WebPPictureSmartARGBToYUVA(WebPPicture* p) { return WebPPictureSharpARGBToYUVA(p); }
 
+/* picture_csp_enc.c:649-652: the VP8Random rounding terms (same for every
+ * picture of a size and amplitude, host/vp8_host.c) feed K1 */
 int WebPPictureARGBToYUVADithered(WebPPicture* p, WebPEncCSP csp, float dithering) {
-  /* dithered chroma (VP8Random, picture_csp_enc.c:520-560) is not part of
-   * this build: only dithering == 0 (the plain conversion) is accepted */
   if (p == NULL) return 0;
-  if (dithering > 0.f) return set_error(p, VP8_ENC_ERROR_INVALID_CONFIGURATION);
-  return argb_to_yuva(p, csp, 0);
+  return argb_to_yuva(p, csp, 0, dithering > 0.f ? dithering : 0.f);
 }
 
 int WebPPictureHasTransparency(const WebPPicture* p) {   /* picture_csp_enc.c:69-81 */
@@ -474,7 +485,8 @@ int WebPEncode(const WebPConfig* config, WebPPicture* pic) {
   if (pic->use_argb || pic->y == NULL || pic->u == NULL || pic->v == NULL) {
     /* webp_enc.c:351-367 */
     const int sharp = config->use_sharp_yuv || (config->preprocessing & 4);
-    if (!(sharp ? WebPPictureSharpARGBToYUVA(pic) : WebPPictureARGBToYUVA(pic, WEBP_YUV420)))
+    if (!(sharp ? WebPPictureSharpARGBToYUVA(pic)
+                : WebPPictureARGBToYUVADithered(pic, WEBP_YUV420, vp8h_import_dithering(config))))
       return 0;
   }
   if (!config->exact) WebPCleanupTransparentArea(pic);   /* webp_enc.c:369-371 */

@@ -99,7 +99,10 @@ void vp8g_set_error(const char* where, const char* what);
 int vp8g_launch_import(const uint8_t* rgba, size_t frame_stride, int row_stride,
                        int w, int h, int n, uint8_t* yuv, size_t yuv_frame_bytes,
                        uint32_t* alpha_flags, uint8_t* alpha_plane, const uint16_t* g2l_dev,
-                       const int32_t* l2g_dev, void* stream);
+                       const int32_t* l2g_dev, const uint16_t* rnd_y, const uint32_t* rnd_uv,
+                       void* stream);
+/* (rnd_y, rnd_uv: DEVICE rounding terms of the dithered import, W*H and
+ * 2 x uvw*uvh with U, V interleaved, from vp8h_dither_rounders; NULL = plain) */
 /* alpha planes (n x w*h, stride w) of RGBA frames (sharp-YUV path) */
 int vp8g_launch_extract_alpha(const uint8_t* rgba, size_t frame_stride, int row_stride, int w,
                               int h, int n, uint8_t* alpha_plane, void* stream);

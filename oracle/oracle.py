@@ -42,6 +42,7 @@ def lib():
         vp, i = C.c_void_p, C.c_int
         _lib.vp8o_import_rgba.argtypes = [vp, i, i, i, vp, vp, vp]
         _lib.vp8o_sharp_import_rgba.argtypes = [vp, i, i, i, vp, vp, vp]
+        _lib.vp8o_import_rgba_dithered.argtypes = [vp, i, i, i, C.c_float, vp, vp, vp]
         _lib.vp8o_sharp_tables.argtypes = [vp, vp]
         _lib.vp8o_encode_yuv.argtypes = [vp, vp, vp, i, i, i, i, vp, vp, vp]
         _lib.vp8o_encode_rgba.argtypes = [vp, i, i, i, vp, vp]
@@ -114,6 +115,27 @@ def sharp_tables():
     return g2l, l2g
 
 
+def import_rgba_dithered(rgba, dithering):
+    """The dithered RGBA -> (Y, U, V) of WebPPictureARGBToYUVADithered."""
+    rgba = np.ascontiguousarray(rgba, np.uint8)
+    h, w = rgba.shape[:2]
+    uw, uh = (w + 1) // 2, (h + 1) // 2
+    y = np.empty((h, w), np.uint8)
+    u = np.empty((uh, uw), np.uint8)
+    v = np.empty((uh, uw), np.uint8)
+    if not lib().vp8o_import_rgba_dithered(rgba.ctypes.data, w, h, 4 * w, dithering,
+                                           y.ctypes.data, u.ctypes.data, v.ctypes.data):
+        raise ValueError("non-opaque input is not restated by the oracle")
+    return y, u, v
+
+
 def encode_rgba(rgba, quality=75.0, method=4, **kw):
-    y, u, v = import_rgba(rgba, sharp=bool(kw.pop("use_sharp_yuv", 0)))
+    sharp = bool(kw.pop("use_sharp_yuv", 0))
+    if kw.get("preprocessing", 0) & 2 and not sharp:   # webp_enc.c:357-365
+        x = np.float32(quality) / np.float32(100)
+        x2 = x * x
+        d = np.float32(1.0) + np.float32(0.5 - 1.0) * x2 * x2
+        y, u, v = import_rgba_dithered(rgba, float(d))
+    else:
+        y, u, v = import_rgba(rgba, sharp=sharp)
     return encode_yuv(y, u, v, quality, method, **kw)

@@ -100,6 +100,75 @@ int vp8o_import_rgba(const uint8_t* rgba, int w, int h, int stride,
   return 1;
 }
 
+/* Dithered import (WebPPictureARGBToYUVADithered, picture_csp_enc.c:520-619;
+ * VP8Random, src/utils/random_utils.{h,c}; webp_enc.c:357-365 for the
+ * amplitude of preprocessing & 2): the same conversion with the rounding
+ * terms drawn from Knuth's difference generator, in the reference's order
+ * (two luma rows, then the U,V pairs of their chroma row). Opaque input. */
+typedef struct { int i1, i2, amp; uint32_t tab[55]; } Rng;
+static const uint32_t kRngTable[55] = {
+    0x0de15230, 0x03b31886, 0x775faccb, 0x1c88626a, 0x68385c55, 0x14b3b828, 0x4a85fef8,
+    0x49ddb84b, 0x64fcf397, 0x5c550289, 0x4a290000, 0x0d7ec1da, 0x5940b7ab, 0x5492577d,
+    0x4e19ca72, 0x38d38c69, 0x0c01ee65, 0x32a1755f, 0x5437f652, 0x5abb2c32, 0x0faa57b1,
+    0x73f533e7, 0x685feeda, 0x7563cce2, 0x6e990e83, 0x4730a7ed, 0x4fc0d9c6, 0x496b153c,
+    0x4f1403fa, 0x541afb0c, 0x73990b32, 0x26d7cb1c, 0x6fcc3706, 0x2cbb77d8, 0x75762f2a,
+    0x6425ccdd, 0x24b35461, 0x0a7d8715, 0x220414a8, 0x141ebf67, 0x56b41583, 0x73e502e3,
+    0x44cab16f, 0x28264d42, 0x73baaefb, 0x0a50ebed, 0x1d6ab6fb, 0x0d3ad40b, 0x35db3b68,
+    0x2b081e83, 0x77ce6b95, 0x5181e5f0, 0x78853bbc, 0x009f9494, 0x27e5ed3c};
+static int rng_bits(Rng* rg, int nb) {
+  uint32_t d = rg->tab[rg->i1] - rg->tab[rg->i2];
+  if ((int32_t)d < 0) d += 1u << 31;
+  rg->tab[rg->i1] = d;
+  rg->i1 = rg->i1 == 54 ? 0 : rg->i1 + 1;
+  rg->i2 = rg->i2 == 54 ? 0 : rg->i2 + 1;
+  int v = (int32_t)(d << 1) >> (32 - nb);
+  v = (v * rg->amp) >> 8;
+  return v + (1 << (nb - 1));
+}
+
+int vp8o_import_rgba_dithered(const uint8_t* rgba, int w, int h, int stride, float dithering,
+                              uint8_t* Y, uint8_t* U, uint8_t* V) {
+  const int uvw = (w + 1) >> 1;
+  Rng rg;
+  gamma_tables();
+  for (int j = 0; j < h; ++j)
+    for (int i = 0; i < w; ++i)
+      if (rgba[j * stride + 4 * i + 3] != 0xff) return 0;
+  memcpy(rg.tab, kRngTable, sizeof(rg.tab));
+  rg.i1 = 0; rg.i2 = 31;
+  rg.amp = dithering < 0.0 ? 0 : dithering > 1.0 ? 256 : (int)(uint32_t)(256 * dithering);
+  for (int j = 0; j < (h + 1) >> 1; ++j) {
+    for (int r = 2 * j; r < 2 * j + 2 && r < h; ++r) {
+      const uint8_t* p = rgba + r * stride;
+      for (int i = 0; i < w; ++i)
+        Y[r * w + i] = (16839 * p[4 * i] + 33059 * p[4 * i + 1] + 6420 * p[4 * i + 2] +
+                        rng_bits(&rg, 16) + (16 << 16)) >> 16;
+    }
+    const uint8_t* r0 = rgba + 2 * j * stride;
+    const uint8_t* r1 = (2 * j + 1 < h) ? r0 + stride : r0;
+    for (int i = 0; i < uvw; ++i) {
+      int c[3];
+      for (int k = 0; k < 3; ++k) {
+        if (2 * i + 1 < w) {
+          const uint32_t s = g_g2l[r0[8 * i + k]] + g_g2l[r0[8 * i + 4 + k]] +
+                             g_g2l[r1[8 * i + k]] + g_g2l[r1[8 * i + 4 + k]];
+          c[k] = lin_to_gamma(s, 0);
+        } else {
+          c[k] = lin_to_gamma(g_g2l[r0[8 * i + k]] + g_g2l[r1[8 * i + k]], 1);
+        }
+      }
+      for (int ch = 0; ch < 2; ++ch) {   /* ConvertRowsToUV: U then V */
+        const int uv = ch ? 28800 * c[0] - 24116 * c[1] - 4684 * c[2]
+                          : -9719 * c[0] - 19081 * c[1] + 28800 * c[2];
+        int v = (uv + rng_bits(&rg, 18) + (128 << 18)) >> 18;
+        v = (v & ~0xff) == 0 ? v : (v < 0 ? 0 : 255);
+        (ch ? V : U)[j * uvw + i] = (uint8_t)v;
+      }
+    }
+  }
+  return 1;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Boolean coder: src/utils/bit_writer_utils.c:26-179 */
 
@@ -2340,8 +2409,15 @@ size_t vp8o_encode_rgba(const uint8_t* rgba, int w, int h, int stride,
   for (int j = 0; j < h && opaque; ++j)
     for (int i = 0; i < w; ++i)
       if (rgba[(size_t)j * stride + 4 * i + 3] != 0xff) { opaque = 0; break; }
+  float dither = 0.f;   /* preprocessing & 2, webp_enc.c:357-365 */
+  if (cfg->preprocessing & 2) {
+    const float x = cfg->quality / 100.f;
+    const float x2 = x * x;
+    dither = 1.0f + (0.5f - 1.0f) * x2 * x2;
+  }
   if (opaque && (sharp ? vp8o_sharp_import_rgba(rgba, w, h, stride, Y, U, V)
-                       : vp8o_import_rgba(rgba, w, h, stride, Y, U, V)))
+                 : dither > 0.f ? vp8o_import_rgba_dithered(rgba, w, h, stride, dither, Y, U, V)
+                                : vp8o_import_rgba(rgba, w, h, stride, Y, U, V)))
     r = vp8o_encode_yuv(Y, U, V, w, h, w, uw, cfg, out, NULL);
   free(buf);
   return r;

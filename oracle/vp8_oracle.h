@@ -50,6 +50,10 @@ void vp8o_default_config(vp8o_config* cfg);
 int vp8o_import_rgba(const uint8_t* rgba, int w, int h, int stride,
                      uint8_t* y, uint8_t* u, uint8_t* v);
 
+/* the dithered conversion (WebPPictureARGBToYUVADithered), opaque input */
+int vp8o_import_rgba_dithered(const uint8_t* rgba, int w, int h, int stride, float dithering,
+                              uint8_t* y, uint8_t* u, uint8_t* v);
+
 /* Full lossy encode from YUV420 planes. Returns the .webp size (malloc'ed
  * into *out, free with vp8o_free) or 0 on error. trace may be NULL. */
 size_t vp8o_encode_yuv(const uint8_t* y, const uint8_t* u, const uint8_t* v,

@@ -12,6 +12,7 @@ Y PSNR / segment levels the reference reports in WebPAuxStats.
               (src/enc/frame_enc.c:26-80, 783-894)
   autofilter  config->autofilter (src/enc/filter_enc.c:156-212)
   methods012  config->method 0-2 (VP8EncLoop, src/enc/frame_enc.c:614-775)
+  dither      config->preprocessing & 2 on ARGB input (src/enc/webp_enc.c:357-365)
 """
 import ctypes
 import hashlib
@@ -27,7 +28,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 from libwebp_amd import abi  # noqa: E402
 from libwebp_amd.synth import syn_v1  # noqa: E402
 
-MODULES = ["multipass", "autofilter", "methods012"]
+MODULES = ["multipass", "autofilter", "methods012", "dither"]
 
 
 def main():

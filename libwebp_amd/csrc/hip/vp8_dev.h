@@ -397,6 +397,14 @@ __device__ __noinline__ int trellis_quant(const LDS& L, uint32_t* nodes, int c[1
   return nz != 0;
 }
 
+// Barrier of a one-wavefront worker: orders its LDS traffic across lanes
+// (the w1 / K3N kernels run one MB per wavefront, several per workgroup)
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // FinalizeTokenProbas (frame_enc.c:146-180): returns "changed" (dirty)
 template <class LDS>
 __device__ int finalize_probas(LDS& L, int lane) {
@@ -417,7 +425,7 @@ __device__ int finalize_probas(LDS& L, int lane) {
       L.coeffs[s] = old_p;
     }
   }
-  __syncthreads();
+  wsync();
   return __any(changed);
 }
 
@@ -440,7 +448,7 @@ __device__ void level_costs(LDS& L, int lane, int nthr = 64) {
     }
     L.lcost[tbc][v] = (uint16_t)(cost + kVP8LevelFixedCost[v]);
   }
-  __syncthreads();
+  wsync();
 }
 
 // VP8RecordStats (cost_enc.h:45-56)

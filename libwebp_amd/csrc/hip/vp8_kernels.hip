@@ -414,7 +414,7 @@ __device__ void eval_i16(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane
   fdct4(src, BPS, ref, 16, c);
   L.dcs[m][b] = (int16_t)c[0];
   if (lane < 4) L.trnz[lane] = 0;
-  __syncthreads();
+  wsync();
   {   // WHT coefficient b of mode m, quantised with y2 (natural index b)
     const int16_t* d = L.dcs[m];
     const int r = b >> 2, col = b & 3;
@@ -453,7 +453,7 @@ __device__ void eval_i16(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane
         L.lv16[m][b][0] = 0;
         if (nzb) atomicOr(&L.trnz[m], 1u << b);
       }
-      __syncthreads();
+      wsync();
     }
     load_lv(L.lv16[m][b], lvr);
   } else {         // quant_enc.c:805-812: DC position zeroed first
@@ -470,7 +470,7 @@ __device__ void eval_i16(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane
     const int lctx = bx == 0 ? ctx.left(by) : (int)((nzm >> (b - 1)) & 1);
     r = residual_cost_r(L, tctx + lctx, 0, 1, lvr);
   }
-  __syncthreads();
+  wsync();
   {   // inverse WHT -> DC of block b (dec.c:137-162)
     const int16_t* q = L.whtq[m];
     const int r = b >> 2, col = b & 3;
@@ -486,7 +486,7 @@ __device__ void eval_i16(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane
     c[0] = (int16_t)((col == 0 ? a0 + a1 : col == 1 ? a3 + a2 : col == 2 ? a0 - a1 : a3 - a2) >> 3);
   }
   idct4(ref, 16, c, L.rec16[m] + by * 64 + bx * 4, 16);
-  __syncthreads();
+  wsync();
   const uint8_t* rec = L.rec16[m] + by * 64 + bx * 4;
   int d = sse4(src, BPS, rec, 16);
   int td = iabs_(hadamard_w(rec, 16) - hadamard_w(src, BPS)) >> 5;
@@ -508,7 +508,7 @@ __device__ void eval_i16(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane
     L.mres[m][2] = r;
     L.mres[m][3] = (int)(nzm | (dcnz ? (1u << 24) : 0u));
   }
-  __syncthreads();
+  wsync();
 }
 
 // UV candidates: lane = mode*8 + block, lanes 0..31 (quant_enc.c:875-969,
@@ -527,7 +527,7 @@ __device__ void eval_uv(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane,
     fdct4(src, BPS, ref, 16, c);
     L.uvdc[m][b] = (int16_t)c[0];
   }
-  __syncthreads();
+  wsync();
   if (use_derr && lane < 8) {   // CorrectDCValues per (mode, channel)
     const int mm = lane >> 1, cch = lane & 1;
     const vp8g_mtx& M = S.uv;
@@ -559,13 +559,13 @@ __device__ void eval_uv(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane,
     L.uvderr[mm][cch][1] = (int8_t)err[2];
     L.uvderr[mm][cch][2] = (int8_t)err[3];
   }
-  __syncthreads();
+  wsync();
   if (lane < 32) {
     c[0] = L.uvdc[m][b];
     nzb = quantize_block(c, L.lvuv[m][b], &S.uv, lvr);
     idct4(ref, 16, c, L.recuv[m] + 8 * ch + (k4 >> 1) * 64 + (k4 & 1) * 4, 16);
   }
-  __syncthreads();
+  wsync();
   const uint64_t nzall = __ballot(lane < 32 && nzb);
   if (lane < 32) {
     const uint8_t* rec = L.recuv[m] + 8 * ch + (k4 >> 1) * 64 + (k4 & 1) * 4;
@@ -587,7 +587,7 @@ __device__ void eval_uv(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int lane,
       L.mres[m][0] = d; L.mres[m][1] = r; L.mres[m][2] = flatc; L.mres[m][3] = (int)nzm;
     }
   }
-  __syncthreads();
+  wsync();
 }
 
 struct I4Result {
@@ -626,7 +626,7 @@ __device__ I4Result run_i4(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int la
   int total_hdr = 0;
   I4Result res;
   res.ok = 1;
-  __syncthreads();
+  wsync();
   for (int i4 = 0; i4 < 16; ++i4) {
     const int bx = i4 & 3, by = i4 >> 2;
     const int left_m = bx == 0 ? L.predleft[by] : L.modes[i4 - 1];
@@ -640,7 +640,7 @@ __device__ I4Result run_i4(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int la
       else v = (by > 0 && bx == 3) ? L.canvas[0][17 + lane - 9] : L.canvas[r][cc + 5 + lane - 9];
       L.edges[lane] = v;
     }
-    __syncthreads();
+    wsync();
     for (int k = lane; k < 160; k += 64) {
       const int m = k >> 4, p = k & 15;
       const P4Op op = L.p4[k];
@@ -653,7 +653,7 @@ __device__ I4Result run_i4(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int la
       else v = (4 + e[0] + e[1] + e[2] + e[3] + e[5] + e[6] + e[7] + e[8]) >> 3;
       L.pred4[m][p] = (uint8_t)v;
     }
-    __syncthreads();
+    wsync();
     if (lane < 10) {
       const int m = lane;
       const uint8_t* src = L.yin + by * 4 * BPS + bx * 4;
@@ -685,7 +685,7 @@ __device__ I4Result run_i4(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int la
       }
       L.r4[m][5] = nz;
     }
-    __syncthreads();
+    wsync();
     int bm;
     int bnz;
     if (search == 2) {
@@ -739,9 +739,9 @@ __device__ I4Result run_i4(K3Lds& L, const vp8g_seg& S, const MBCtx& ctx, int la
       tnz = (tnz & ~(1u << bx)) | ((bnz ? 1u : 0u) << bx);
       lnz = (lnz & ~(1u << by)) | ((bnz ? 1u : 0u) << by);
     }
-    __syncthreads();
+    wsync();
   }
-  __syncthreads();
+  wsync();
   res.H = accH;
   res.score = acc_score;
   res.nz = acc_nz;
@@ -828,7 +828,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
   for (int k = lane; k < 16 * mbw; k += 64) uvtop[k] = 127;
   for (int k = lane - 1; k < mbw; k += 64) nzw[k] = 0;
   for (int k = lane; k < 4 * mbw; k += 64) { predtop[k] = 0; topderr[k] = 0; }
-  __syncthreads();
+  wsync();
   level_costs(L, lane);
 
   const int rd_opt = P->rd_opt;
@@ -865,7 +865,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
       if (finalize_probas(L, lane)) level_costs(L, lane);
       cnt = max_count;
     }
-    __syncthreads();
+    wsync();
     const int segid = segmap[mb];
     const vp8g_seg& S = L.seg[segid];
     const bool hl = x > 0, ht = y > 0;
@@ -888,7 +888,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
         L.puv[m][p] = pred_sample(m, 8, px & 7, py, c ? vl : ul, uvt + 8 * c, hl, ht, c ? dcv : dcu);
       }
     }
-    __syncthreads();
+    wsync();
 
     K3_STAMP(0);
     int is_i16 = 1, bu = 0, best16 = 0;
@@ -924,7 +924,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
         }
         best16 = best_mode;
         if (lane < 16) L.modes[lane] = best16;
-        __syncthreads();
+        wsync();
       }
       if (try_both || !is_i16) {
         is_i16 = 0;
@@ -940,7 +940,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
           is_i16 = 1;
           if (lane < 16) L.modes[lane] = best16;
         }
-        __syncthreads();
+        wsync();
       }
       if (is_i16) {   // ReconstructIntra16 of the chosen mode
         eval_i16<false>(L, S, ctx, lane);
@@ -951,7 +951,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
         if (lane < 16) L.fin_dc[lane] = L.lvdc[best16][lane];
         rd_nz = (uint32_t)L.mres[best16][3];
       }
-      __syncthreads();
+      wsync();
       if (refine_uv) {
         score_t best_uv = MAX_COST;
         for (int mm = 0; mm < 4; ++mm) {
@@ -975,7 +975,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
         (&L.fin_uv[0][0])[k] = (&L.lvuv[bu][0][0])[k];
       }
       rd_nz |= (uint32_t)L.mres[bu][3] << 16;
-      __syncthreads();
+      wsync();
     } else {
       score_t rd_score = 0;
       // ---- Intra16 (quant_enc.c:1002-1058)
@@ -1021,7 +1021,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
         mv = max(mv, iabs_(L.lvdc[best16][4]));
         if (lane == 0 && mv > L.max_edge[segid]) L.max_edge[segid] = mv;
       }
-      __syncthreads();
+      wsync();
 
       K3_STAMP(1);
       // ---- Intra4 (quant_enc.c:1072-1165)
@@ -1042,7 +1042,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
         } else {
           if (lane < 16) L.modes[lane] = best16;   // the aborted search wrote some
         }
-        __syncthreads();
+        wsync();
       }
 
       K3_STAMP(2);
@@ -1074,7 +1074,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
           top[0] = e[1];
           top[1] = (int8_t)(e[2] - left[1]);
         }
-        __syncthreads();
+        wsync();
       }
 
       // ---- m5: final re-quantisation of the chosen modes with trellis
@@ -1097,14 +1097,14 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
           }
           nzq = r4.nz;
         }
-        __syncthreads();
+        wsync();
         eval_uv(L, S, ctx, lane, x, topderr, use_derr);   // derr state already updated
         for (int k = lane; k < 128; k += 64) {
           L.yout[(k >> 4) * BPS + 16 + (k & 15)] = L.recuv[bu][k];
           (&L.fin_uv[0][0])[k] = (&L.lvuv[bu][0][0])[k];
         }
         rd_nz = nzq | ((uint32_t)L.mres[bu][3] << 16);
-        __syncthreads();
+        wsync();
       }
       (void)rd_score;
     }
@@ -1200,7 +1200,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
         gen_tokens<1, K3Lds, NONE>(L, blk_levels(L, k), my_type, my_first, my_ctx,
                                    tok_base + ntok + excl, &nzdummy);
       if (!tok_err) ntok += total;
-      __syncthreads();
+      wsync();
       K3_STAMP(5);
       // fold deltas into the statistics; slots that cross the halving
       // threshold inside this MB are replayed in token order.
@@ -1221,7 +1221,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
           L.delta[s] = 0;
         }
       }
-      __syncthreads();
+      wsync();
       if (__any(any_mark)) {
         if (lane == 0) {
           for (int kk = first_blk; kk < 25; ++kk) {
@@ -1230,9 +1230,9 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
                                        nullptr, &nzdummy);
           }
         }
-        __syncthreads();
+        wsync();
         for (int kk = lane; kk < 33; kk += 64) L.mark[kk] = 0;
-        __syncthreads();
+        wsync();
       }
       K3_STAMP(6);
       // update nz context (iterator_enc.c:267-283) and the left DC flag
@@ -1258,19 +1258,19 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
                 (tn[4] << 18) | (tn[5] << 19) | (tn[6] << 22) | (tn[7] << 23) | (tn[8] << 24);
         word |= (ln[0] << 3) | (ln[1] << 7) | (ln[2] << 11) | (ln[4] << 17) | (ln[6] << 21);
         left_dc = ln[8];
-        __syncthreads();
+        wsync();
         if (lane == 0) nzw[x] = word;
       }
     }
 
     // ---- boundary save (iterator_enc.c:290-313) + mode context
-    __syncthreads();
+    wsync();
     if (x < mbw - 1) {
       if (lane < 16) yl[lane] = L.yout[15 + lane * BPS];
       if (lane < 8) { ul[lane] = L.yout[16 + 7 + lane * BPS]; vl[lane] = L.yout[24 + 7 + lane * BPS]; }
       if (lane == 0) { yl[-1] = yt[15]; ul[-1] = uvt[7]; vl[-1] = uvt[15]; }
     }
-    __syncthreads();
+    wsync();
     if (y < mbh - 1) {
       if (lane < 16) {
         ytop[16 * x + lane] = L.yout[15 * BPS + lane];
@@ -1281,7 +1281,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
       predtop[4 * x + lane] = L.modes[12 + lane];
       L.predleft[lane] = L.modes[4 * lane + 3];
     }
-    __syncthreads();
+    wsync();
     K3_STAMP(7);
   }
 
@@ -1289,7 +1289,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
   vp8g_frame_result* R = a.results + f;
   int use_skip = 0, skip_proba = 255;
   if constexpr (NONE) {
-    __syncthreads();
+    wsync();
     for (int s = lane; s < NSLOT; s += 64) rstats[s] = L.stats[s];
     // StatLoop gives up before FinalizeSkipProba / FinalizeTokenProbas when
     // its header estimate is 0 (frame_enc.c:645-646): default probabilities
@@ -1367,6 +1367,447 @@ __global__ void k_synth(uint8_t* rgba, size_t fstride, int w, int h, int f0, int
 
 // ---------------------------------------------------------------------------
 // launchers
+
+
+// ---------------------------------------------------------------------------
+// K3N: the methods 0-2 encoder (RD_OPT_NONE, VP8EncLoop) with NW MB workers
+// of one wavefront per frame. The decisions depend only on the reconstructed
+// neighbours (no rate, no statistics feedback), so rows are dealt to the
+// waves round-robin and run as a wavefront (row y starts MB x once row y-1
+// has finished x+1: top-right dependency, iterator_enc.c:290-313); boundary
+// rows live in shared LDS like K3's. Each MB's tokens go to its own slot;
+// after the loop the workgroup replays StatLoop's statistics in raster order
+// (exact saturation), finalises, and compacts the slots into the frame's
+// stream (dropping skipped MBs when the skip flag pays).
+struct K3NShared {
+  int32_t nb[4];               // i4, i16, skip, skip among the statistics MBs
+  unsigned long long sse[3];
+  int32_t any_mark;
+  int32_t use_skip, skip_proba;
+  uint32_t ntok;
+};
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_encode_none(K3ArgsW1 a) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, tid = threadIdx.x;
+  K3Lds& L = reinterpret_cast<K3Lds*>(smem)[wv];
+  K3Lds& L0 = reinterpret_cast<K3Lds*>(smem)[0];
+  const int mbw = a.mbw, mbh = a.mbh, nmb = mbw * mbh;
+  K3NShared& G = *reinterpret_cast<K3NShared*>(smem + NW * sizeof(K3Lds));
+  uint8_t* ytop = smem + NW * sizeof(K3Lds) + sizeof(K3NShared);   // 16*mbw + 16
+  uint8_t* uvtop = ytop + 16 * mbw + 16;                             // 16*mbw
+  uint32_t* nzw = reinterpret_cast<uint32_t*>(uvtop + 16 * mbw) + 1; // [-1..mbw-1]
+  uint8_t* predtop = reinterpret_cast<uint8_t*>(nzw + mbw);         // 4*mbw
+  int8_t* topderr = reinterpret_cast<int8_t*>(predtop + 4 * mbw);   // 4*mbw, stays 0
+  int32_t* rowdone = reinterpret_cast<int32_t*>(topderr + 4 * mbw + 4 - ((4 * mbw) & 3));
+
+  const int f = blockIdx.x;
+  const int w = a.w, h = a.h;
+  const int uvw = (w + 1) >> 1, uvh = (h + 1) >> 1;
+  const uint8_t* Yp = a.yuv + f * a.yfb;
+  const uint8_t* Up = Yp + (size_t)w * h;
+  const uint8_t* Vp = Up + (size_t)uvw * uvh;
+  const vp8g_frame_params* P = a.params + f;
+  const uint8_t* segmap = a.segmap + (size_t)f * nmb;
+  uint16_t* tok_base = a.tokens + f * a.tok_cap;
+  uint8_t* mbinfo = a.mbinfo + (size_t)f * nmb * VP8G_MBINFO_BYTES;
+  uint32_t* mbcnt = a.mboff + (size_t)f * nmb;   // tokens of each MB's slot
+  if (P->pass_mode == 2) return;
+  if (P->pass_mode != 0 && P->pass_mode != 3) {
+    if (tid == 0) a.results[f].error = 3;
+    return;
+  }
+  uint32_t* rstats =
+      reinterpret_cast<uint32_t*>(a.rerun + (size_t)f * VP8G_RERUN_STATE_BYTES + VP8G_STATE_STATS);
+
+  // ---- frame init
+  for (int k = lane; k < 1000; k += 64) L.mcost4[k] = (&kVP8ModeCostI4[0][0][0])[k];
+  for (int k = lane; k < 160; k += 64) L.p4[k] = (&kP4[0][0])[k];
+  for (int k = lane; k < 256; k += 64) L.ecost[k] = kVP8EntropyCost[k];
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(P->seg);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(L.seg);
+    for (int k = lane; k < (int)(sizeof(L.seg) / 4); k += 64) dst[k] = src[k];
+  }
+  for (int k = tid; k < 16 * mbw + 16; k += NW * 64) ytop[k] = 127;
+  for (int k = tid; k < 16 * mbw; k += NW * 64) uvtop[k] = 127;
+  for (int k = tid - 1; k < mbw; k += NW * 64) nzw[k] = 0;
+  for (int k = tid; k < 4 * mbw; k += NW * 64) { predtop[k] = 0; topderr[k] = 0; }
+  for (int k = tid; k < mbh; k += NW * 64) rowdone[k] = 0;
+  if (tid < 4) G.nb[tid] = 0;
+  if (tid < 3) G.sse[tid] = 0;
+  if (tid == 0) { G.any_mark = 0; G.ntok = 0; }
+  __syncthreads();
+  // the level-cost tables only feed rates RD_OPT_NONE never looks at
+
+  const int use_derr = P->use_derr;
+  uint8_t* yl = L.yl_mem + 1;
+  uint8_t* ul = L.ul_mem + 1;
+  uint8_t* vl = L.vl_mem + 1;
+
+  for (int y = wv; y < mbh; y += NW) {
+    if (lane < 16) yl[lane] = 129;   // InitLeft (iterator_enc.c:22-32)
+    if (lane < 8) { ul[lane] = 129; vl[lane] = 129; }
+    if (lane == 0) {
+      yl[-1] = ul[-1] = vl[-1] = (y > 0) ? 129 : 127;
+      L.lderr[0][0] = L.lderr[0][1] = L.lderr[1][0] = L.lderr[1][1] = 0;
+    }
+    if (lane < 4) L.predleft[lane] = 0;
+    int left_dc = 0;
+    wsync();
+    for (int x = 0; x < mbw; ++x) {
+      const int mb = y * mbw + x;
+      if (y > 0) {   // row y-1 has finished MB x+1 (top-right samples)
+        const int need = min(x + 2, mbw);
+        if (lane == 0)
+          while (__hip_atomic_load(&rowdone[y - 1], __ATOMIC_ACQUIRE,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+            __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        wsync();
+      }
+      load_mb(Yp, Up, Vp, w, h, x, y, L.yin, lane, 64);
+      wsync();
+      const int segid = segmap[mb];
+      const vp8g_seg& S = L.seg[segid];
+      const bool hl = x > 0, ht = y > 0;
+      const uint8_t* yt = ytop + 16 * x;
+      const uint8_t* uvt = uvtop + 16 * x;
+      MBCtx ctx;
+      nz_flags(nzw[x], nzw[x - 1], left_dc, ctx);
+      {   // predictions (quant_enc.c:469-479)
+        const int dcy = dc_value(yl, yt, hl, ht, 16, 5);
+        for (int k = lane; k < 1024; k += 64) {
+          const int m = k >> 8, p = k & 255;
+          L.p16[m][p] = pred_sample(m, 16, p & 15, p >> 4, yl, yt, hl, ht, dcy);
+        }
+        const int dcu = dc_value(ul, uvt, hl, ht, 8, 4);
+        const int dcv = dc_value(vl, uvt + 8, hl, ht, 8, 4);
+        for (int k = lane; k < 512; k += 64) {
+          const int m = k >> 7, p = k & 127, px = p & 15, py = p >> 4, c = px >> 3;
+          L.puv[m][p] = pred_sample(m, 8, px & 7, py, c ? vl : ul, uvt + 8 * c, hl, ht,
+                                    c ? dcv : dcu);
+        }
+      }
+      wsync();
+      int is_i16 = 1, bu = 0, best16 = 0;
+      uint32_t rd_nz = 0;
+      {
+      // ---- RefineUsingDistortion (quant_enc.c:1248-1350): modes by
+      // prediction SSE + fixed mode costs, then the chosen modes' reconstruction
+      const uint8_t am = a.amode[(size_t)f * nmb + mb];
+      int try_both = P->method >= 2;
+      const int refine_uv = P->method >= 1;
+      const score_t bit_limit = try_both ? (score_t)P->mb_header_limit : MAX_COST;
+      score_t best_score = MAX_COST;
+      is_i16 = try_both || !(am & 2);
+      if (is_i16) {
+        int best_mode = -1;
+        for (int mm = 0; mm < 4; ++mm) {
+          int sq = 0;
+          for (int k = lane; k < 256; k += 64) {
+            const int d = L.yin[(k >> 4) * BPS + (k & 15)] - L.p16[mm][k];
+            sq += d * d;
+          }
+          for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off);
+          const score_t sc = (score_t)sq * 256 + kVP8ModeCostI16[mm] * 106;
+          if (mm > 0 && kVP8ModeCostI16[mm] > bit_limit) continue;
+          if (sc < best_score) { best_mode = mm; best_score = sc; }
+        }
+        if (x == 0 || y == 0) {   // IsFlatSource16: avoid a border checkerboard (bug #432)
+          int same = 1;
+          const int v0 = L.yin[0];
+          for (int k = lane; k < 256; k += 64) same &= (L.yin[(k >> 4) * BPS + (k & 15)] == v0);
+          if (__all(same)) { best_mode = (x == 0) ? 0 : 2; try_both = 0; }
+        }
+        best16 = best_mode;
+        if (lane < 16) L.modes[lane] = best16;
+        wsync();
+      }
+      if (try_both || !is_i16) {
+        is_i16 = 0;
+        const I4Result r4 = run_i4<false>(L, S, ctx, lane, x, mbw, predtop, yl, yt, 2, best_score,
+                                          bit_limit > 0x7fffffff ? 0x7fffffff : (int)bit_limit);
+        if (r4.ok) {
+          rd_nz = r4.nz;
+          for (int k = lane; k < 256; k += 64) {
+            L.yout[(k >> 4) * BPS + (k & 15)] = L.acc_out[k];
+            (&L.fin_ac[0][0])[k] = (&L.acc_ac[0][0])[k];
+          }
+        } else {
+          is_i16 = 1;
+          if (lane < 16) L.modes[lane] = best16;
+        }
+        wsync();
+      }
+      if (is_i16) {   // ReconstructIntra16 of the chosen mode
+        eval_i16<false>(L, S, ctx, lane);
+        for (int k = lane; k < 256; k += 64) {
+          L.yout[(k >> 4) * BPS + (k & 15)] = L.rec16[best16][k];
+          (&L.fin_ac[0][0])[k] = (&L.lv16[best16][0][0])[k];
+        }
+        if (lane < 16) L.fin_dc[lane] = L.lvdc[best16][lane];
+        rd_nz = (uint32_t)L.mres[best16][3];
+      }
+      wsync();
+      if (refine_uv) {
+        score_t best_uv = MAX_COST;
+        for (int mm = 0; mm < 4; ++mm) {
+          int sq = 0;
+          for (int k = lane; k < 128; k += 64) {
+            const int d = L.yin[(k >> 4) * BPS + 16 + (k & 15)] - L.puv[mm][k];
+            sq += d * d;
+          }
+          for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off);
+          const score_t sc = (score_t)sq * 256 + kVP8ModeCostUV[mm] * 120;
+          if (sc < best_uv) { bu = mm; best_uv = sc; }
+        }
+      } else {
+        bu = am & 1;   // method 0 keeps the analysis' UV mode
+      }
+      // ReconstructUV: the DC error diffusion reads errors that RD_OPT_NONE
+      // never stores (StoreDiffusionErrors is PickBestUV's), i.e. zeros
+      eval_uv(L, S, ctx, lane, x, topderr, use_derr);
+      for (int k = lane; k < 128; k += 64) {
+        L.yout[(k >> 4) * BPS + 16 + (k & 15)] = L.recuv[bu][k];
+        (&L.fin_uv[0][0])[k] = (&L.lvuv[bu][0][0])[k];
+      }
+      rd_nz |= (uint32_t)L.mres[bu][3] << 16;
+      wsync();
+      }
+      // ---- per-MB info + side statistics
+      const int skip = rd_nz == 0;
+      if (lane == 0) {
+        uint8_t* info = mbinfo + (size_t)mb * VP8G_MBINFO_BYTES;
+        info[0] = is_i16; info[1] = bu; info[2] = segid; info[3] = skip;
+        atomicAdd(&G.nb[is_i16 ? 1 : 0], 1);
+        if (skip) atomicAdd(&G.nb[2], 1);
+        if (skip && mb < P->nb_stat) atomicAdd(&G.nb[3], 1);
+      }
+      if (lane < 16) mbinfo[(size_t)mb * VP8G_MBINFO_BYTES + 4 + lane] = L.modes[lane];
+      if (P->recon_addr != 0)   // autofilter input (filter_enc.c:179)
+        for (int k = lane; k < 128; k += 64)
+          reinterpret_cast<uint32_t*>(P->recon_addr + ((size_t)mb << 9))[k] =
+              reinterpret_cast<const uint32_t*>(L.yout)[k];
+      {   // SSE for WebPAuxStats (frame_enc.c:480-489)
+        int sy = 0, su = 0, sv = 0;
+        for (int k = lane; k < 256; k += 64) {
+          const int o = (k >> 4) * BPS + (k & 15);
+          const int dd = L.yin[o] - L.yout[o];
+          sy += dd * dd;
+        }
+        {
+          const int o = (lane >> 3) * BPS + 16 + (lane & 7);
+          const int du = L.yin[o] - L.yout[o], dv = L.yin[o + 8] - L.yout[o + 8];
+          su = du * du; sv = dv * dv;
+        }
+        for (int off = 32; off >= 1; off >>= 1) {
+          sy += __shfl_xor(sy, off);
+          su += __shfl_xor(su, off);
+          sv += __shfl_xor(sv, off);
+        }
+        if (lane == 0) {
+          atomicAdd(&G.sse[0], (unsigned long long)sy);
+          atomicAdd(&G.sse[1], (unsigned long long)su);
+          atomicAdd(&G.sse[2], (unsigned long long)sv);
+        }
+      }
+      // ---- tokens (token_enc.c:113-193) into this MB's slot
+      {
+        const int first_blk = is_i16 ? 0 : 1;
+        int my_ctx = 0, my_type = 0, my_first = 0;
+        const int k = lane;   // block index 0..24
+        const bool active = k >= first_blk && k < 25;
+        int nzk = 0;
+        if (active) {
+          const int16_t* lv = blk_levels(L, k);
+          for (int i = 0; i < 16; ++i) nzk |= lv[i];
+        }
+        const uint64_t nzb = __ballot(active && nzk != 0);
+        if (active) {
+          if (k == 0) {
+            my_type = 1; my_first = 0; my_ctx = ctx.top(8) + ctx.left(8);
+          } else if (k <= 16) {
+            const int b = k - 1, bx = b & 3, by = b >> 2;
+            my_type = is_i16 ? 0 : 3; my_first = is_i16 ? 1 : 0;
+            const int t = by == 0 ? ctx.top(bx) : (int)((nzb >> (k - 4)) & 1);
+            const int l = bx == 0 ? ctx.left(by) : (int)((nzb >> (k - 1)) & 1);
+            my_ctx = t + l;
+          } else {
+            const int b = k - 17, ch = b >> 2, k4 = b & 3, bx = k4 & 1, by = k4 >> 1;
+            my_type = 2; my_first = 0;
+            const int t = by == 0 ? ctx.top(4 + 2 * ch + bx) : (int)((nzb >> (k - 2)) & 1);
+            const int l = bx == 0 ? ctx.left(4 + 2 * ch + by) : (int)((nzb >> (k - 1)) & 1);
+            my_ctx = t + l;
+          }
+        }
+        int nzdummy;
+        const int mycount = active ? gen_tokens<0, K3Lds, true>(L, blk_levels(L, k), my_type,
+                                                                my_first, my_ctx, nullptr, &nzdummy)
+                                   : 0;
+        int incl = mycount;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const int v = __shfl_up(incl, off);
+          if (lane >= off) incl += v;
+        }
+        const int total = __shfl(incl, 63);
+        const int excl = incl - mycount;
+        uint16_t* slot = tok_base + (size_t)mb * VP8G_MAX_TOKENS_PER_MB;
+        if (active)
+          gen_tokens<1, K3Lds, true>(L, blk_levels(L, k), my_type, my_first, my_ctx, slot + excl,
+                                     &nzdummy);
+        if (lane == 0) mbcnt[mb] = (uint32_t)total;
+        // nz contexts (iterator_enc.c:267-283) and the left DC flag
+        int tn[9], ln[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) { tn[i] = ctx.top(i); ln[i] = ctx.left(i); }
+        if (is_i16) { tn[8] = ln[8] = (int)(nzb & 1); }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          tn[i] = (int)((nzb >> (1 + 12 + i)) & 1);
+          ln[i] = (int)((nzb >> (1 + 4 * i + 3)) & 1);
+        }
+#pragma unroll
+        for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            tn[4 + 2 * ch + i] = (int)((nzb >> (17 + 4 * ch + 2 + i)) & 1);
+            ln[4 + 2 * ch + i] = (int)((nzb >> (17 + 4 * ch + 2 * i + 1)) & 1);
+          }
+        uint32_t word = 0;
+        word |= (tn[0] << 12) | (tn[1] << 13) | (tn[2] << 14) | (tn[3] << 15) |
+                (tn[4] << 18) | (tn[5] << 19) | (tn[6] << 22) | (tn[7] << 23) | (tn[8] << 24);
+        word |= (ln[0] << 3) | (ln[1] << 7) | (ln[2] << 11) | (ln[4] << 17) | (ln[6] << 21);
+        left_dc = ln[8];
+        wsync();
+        if (lane == 0) nzw[x] = word;
+      }
+      // ---- boundary save (iterator_enc.c:290-313) + mode context
+      wsync();
+      if (x < mbw - 1) {
+        if (lane < 16) yl[lane] = L.yout[15 + lane * BPS];
+        if (lane < 8) { ul[lane] = L.yout[16 + 7 + lane * BPS]; vl[lane] = L.yout[24 + 7 + lane * BPS]; }
+        if (lane == 0) { yl[-1] = yt[15]; ul[-1] = uvt[7]; vl[-1] = uvt[15]; }
+      }
+      wsync();
+      if (y < mbh - 1 && lane < 16) {
+        ytop[16 * x + lane] = L.yout[15 * BPS + lane];
+        uvtop[16 * x + lane] = L.yout[7 * BPS + 16 + lane];
+      }
+      if (lane < 4) {
+        predtop[4 * x + lane] = L.modes[12 + lane];
+        L.predleft[lane] = L.modes[4 * lane + 3];
+      }
+      wsync();
+      if (lane == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __hip_atomic_store(&rowdone[y], x + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+
+  // ---- StatLoop's statistics: the probe MBs' tokens in raster order, per
+  // slot delta + exact in-order replay of the slots reaching the halving
+  // point (VP8RecordStats, cost_enc.h:45-56). RecordCoeffs puts every
+  // dynamic token's statistic in its probability slot (gen_tokens RC).
+  for (int s = tid; s < NSLOT; s += NW * 64) {
+    L0.stats[s] = P->pass_mode == 3 ? rstats[s] : 0u;
+    L0.delta[s] = 0;
+  }
+  for (int k = tid; k < 33; k += NW * 64) L0.mark[k] = 0;
+  __syncthreads();
+  const int nb_stat = min(P->nb_stat, nmb);
+  for (int m = 0; m < nb_stat; ++m) {
+    const uint16_t* T = tok_base + (size_t)m * VP8G_MAX_TOKENS_PER_MB;
+    const uint32_t n = mbcnt[m];
+    for (uint32_t i = tid; i < n; i += NW * 64) {
+      const uint32_t tk = T[i];
+      if (!(tk & 0x4000u)) atomicAdd(&L0.delta[tk & 0x3fffu], 0x10000u + (tk >> 15));
+    }
+    __syncthreads();
+    for (int s = tid; s < NSLOT; s += NW * 64) {
+      const uint32_t d = L0.delta[s];
+      if (d) {
+        const uint32_t p = L0.stats[s];
+        if ((p >> 16) + (d >> 16) < 0xffffu) {
+          L0.stats[s] = p + d;
+        } else {
+          atomicOr(&L0.mark[s >> 5], 1u << (s & 31));
+          G.any_mark = 1;
+        }
+        L0.delta[s] = 0;
+      }
+    }
+    __syncthreads();
+    if (G.any_mark) {
+      if (tid == 0) {
+        for (uint32_t i = 0; i < n; ++i) {
+          const uint32_t tk = T[i];
+          const uint32_t sl = tk & 0x3fffu;
+          if (!(tk & 0x4000u) && (L0.mark[sl >> 5] & (1u << (sl & 31))))
+            record_stat(&L0.stats[sl], (int)(tk >> 15));
+        }
+      }
+      __syncthreads();
+      for (int k = tid; k < 33; k += NW * 64) L0.mark[k] = 0;
+      if (tid == 0) G.any_mark = 0;
+      __syncthreads();
+    }
+  }
+  for (int s = tid; s < NSLOT; s += NW * 64) rstats[s] = L0.stats[s];
+  if (wv == 0) {
+    for (int s = lane; s < NSLOT; s += 64) L0.coeffs[s] = (&kVP8CoeffProba0[0][0][0][0])[s];
+    for (int k = lane; k < 256; k += 64) L0.ecost[k] = kVP8EntropyCost[k];
+    wsync();
+    int use_skip = 0, skip_proba = 255;
+    // StatLoop gives up before FinalizeSkipProba / FinalizeTokenProbas when
+    // its header estimate is 0 (frame_enc.c:645-646): default probabilities
+    if (P->none_finalize) {
+      finalize_probas(L0, lane);
+      skip_proba = (int)((uint64_t)(nmb - G.nb[3]) * 255 / nmb);   // CalcSkipProba
+      use_skip = skip_proba < 250;
+    }
+    if (lane == 0) { G.use_skip = use_skip; G.skip_proba = skip_proba; }
+  }
+  __syncthreads();
+  // ---- the frame's token stream in raster order; VP8EncLoop codes no
+  // residuals for skipped MBs when the skip flag is used
+  uint32_t dst = 0;
+  for (int m = 0; m < nmb; ++m) {
+    if (G.use_skip && mbinfo[(size_t)m * VP8G_MBINFO_BYTES + 3]) continue;
+    const uint32_t n = mbcnt[m];
+    const uint16_t* src = tok_base + (size_t)m * VP8G_MAX_TOKENS_PER_MB;
+    if ((size_t)dst != (size_t)m * VP8G_MAX_TOKENS_PER_MB) {
+      for (uint32_t i = 0; i < n; i += NW * 64) {
+        const bool in = i + tid < n;
+        const uint16_t t = in ? src[i + tid] : 0;
+        __syncthreads();
+        if (in) tok_base[dst + i + tid] = t;
+        __threadfence_block();
+        __syncthreads();
+      }
+    }
+    dst += n;
+  }
+  vp8g_frame_result* R = a.results + f;
+  for (int s = tid; s < NSLOT; s += NW * 64) R->probas[s] = L0.coeffs[s];
+  if (tid == 0) {
+    R->use_skip = (int16_t)G.use_skip;
+    R->skip_proba = (int16_t)G.skip_proba;
+    R->ntokens = dst;
+    R->error = 0;
+    for (int s = 0; s < 4; ++s) R->max_edge[s] = 0;   // StoreMaxDelta is PickBestIntra16's
+    R->size_p0 = 0;                                   // RD_OPT_NONE has no header estimate
+    R->distortion = 0;
+    R->sse[0] = G.sse[0]; R->sse[1] = G.sse[1]; R->sse[2] = G.sse[2];
+    R->block_count[0] = G.nb[0]; R->block_count[1] = G.nb[1]; R->block_count[2] = G.nb[2];
+    for (int i = 0; i < 8; ++i) R->stamps[i] = 0;
+  }
+}
 
 static size_t k3_lds_bytes(int mbw) {
   return sizeof(K3Lds) + (16 * mbw + 16) + 16 * mbw + 4 * (mbw + 1) + 4 * mbw + 4 * mbw + 16;
@@ -1524,18 +1965,20 @@ int vp8g_launch_encode_none(const uint8_t* yuv, size_t yfb, int w, int h, int n,
   a.segmap = segmap; a.params = params; a.tokens = tokens; a.tok_cap = tok_cap;
   a.mbinfo = mbinfo; a.results = results;
   a.amode = amode; a.mboff = mboff; a.rerun = rerun_state;
-  const size_t lds = k3_lds_bytes(a.mbw);
+  constexpr int NW = 3;   // MB workers (one wavefront each) per frame
+  const size_t lds = NW * sizeof(K3Lds) + sizeof(K3NShared) + (16 * a.mbw + 16) + 16 * a.mbw +
+                     4 * (a.mbw + 1) + 4 * a.mbw + 4 * a.mbw + 8 + 4 * (size_t)a.mbh + 16;
   if (lds > 160 * 1024) {
     vp8g_set_error("k_encode_none", "frame too wide for the LDS budget");
     return 0;
   }
   static int attr_done = 0;
   if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)k_encode_w1<true>,
+    (void)hipFuncSetAttribute((const void*)k_encode_none<NW>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_done = 1;
   }
-  hipLaunchKernelGGL(k_encode_w1<true>, dim3(n), dim3(64), lds, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(k_encode_none<NW>, dim3(n), dim3(NW * 64), lds, (hipStream_t)stream, a);
   return launch_check("k_encode_none");
 }
 

@@ -434,6 +434,8 @@ static double psnr(uint64_t err, uint64_t size) {
  * fully transparent pixels zeroed unless `exact`, then the VP8L engine
  * (host/vp8l_batch.c) on one frame. */
 static int encode_lossless(const WebPConfig* config, WebPPicture* pic) {
+  /* near-lossless is not implemented by the GPU VP8L encoder (gpu_batch.c) */
+  if (config->near_lossless < 100) return set_error(pic, VP8_ENC_ERROR_INVALID_CONFIGURATION);
   if (pic->argb == NULL && !WebPPictureYUVAToARGB(pic)) return 0;
   const int w = pic->width, h = pic->height;
   uint8_t* rgba = (uint8_t*)malloc((size_t)w * h * 4);

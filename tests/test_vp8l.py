@@ -232,6 +232,18 @@ def test_gpu_1080p_decodes_exact_and_size(gpu):
 
 
 @pytest.mark.gpu
+def test_gpu_near_lossless_fails_loudly(gpu):
+    """near_lossless < 100 (near_lossless_enc.c and the residual quantisation
+    inside the reference's predictor search, predictor_enc.c) is refused, not
+    silently encoded lossless."""
+    img = syn_v1(64, 48, 0)
+    with pytest.raises(RuntimeError):
+        gpu.encode_rgba(img, quality=75.0, method=4, lossless=1, use_argb=True, near_lossless=60)
+    with pytest.raises(RuntimeError):
+        gpu.GpuBatch(64, 48, 1, lossless=1, near_lossless=60)
+
+
+@pytest.mark.gpu
 def test_gpu_webpencode_lossless_api(gpu):
     """WebPEncode with config.lossless (webp_enc.c:396-407): ARGB picture,
     transparent pixels zeroed unless `exact`; the one-shot

@@ -19,7 +19,8 @@ class Config(C.Structure):
                 ("partition_limit", C.c_int), ("preprocessing", C.c_int),
                 ("emulate_jpeg_size", C.c_int), ("use_sharp_yuv", C.c_int),
                 ("pass_", C.c_int), ("target_size", C.c_int), ("target_PSNR", C.c_float),
-                ("qmin", C.c_int), ("qmax", C.c_int), ("autofilter", C.c_int)]
+                ("qmin", C.c_int), ("qmax", C.c_int), ("autofilter", C.c_int),
+                ("low_memory", C.c_int)]
 
 
 class MBTrace(C.Structure):

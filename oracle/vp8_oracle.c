@@ -2172,11 +2172,17 @@ static void enc_loop(Enc* e, const vp8o_config* cfg, vp8o_mb_trace* trace, doubl
   int nb = nmb;
   It it;
   int stats_ok = 1;
+  /* StatLoop decides with RD_OPT_BASIC from method 3 on (low_memory), else
+   * RD_OPT_NONE; the final pass with the method's own level */
+  const int final_rd = e->rd_opt, stat_rd = e->method >= 3 ? 1 : 0;
   if (e->method == 0) nb = (nmb > 200) ? nmb >> 2 : 50;   /* fast probe */
+  if (e->method == 3) nb = (nmb > 200) ? nmb >> 1 : 100;
   memset(e->stats, 0, sizeof(e->stats));
   g_passes = 0;
-  for (int pass = 0; pass < (cfg->pass < 1 ? 1 : cfg->pass); ++pass) {   /* OneStatPass */
-    int left = nb;
+  e->rd_opt = stat_rd;
+  for (int pass = 0, npass = cfg->pass < 1 ? 1 : cfg->pass; pass < npass; ++pass) {
+    int left = nb;   /* OneStatPass */
+    uint64_t size_p0 = 0;
     it_reset(&it, e);
     const float q = cfg->quality < (float)cfg->qmin ? (float)cfg->qmin
                   : cfg->quality > (float)cfg->qmax ? (float)cfg->qmax : cfg->quality;
@@ -2190,14 +2196,21 @@ static void enc_loop(Enc* e, const vp8o_config* cfg, vp8o_mb_trace* trace, doubl
       it_import(&it, e);
       if (decimate(&it, e, &rd)) ++e->nb_skip;
       record_tokens(&it, e, &rd);   /* RecordResiduals: statistics only */
+      size_p0 += rd.H;
       it_save_boundary(&it, e);
     } while (it_next(&it, e) && --left > 0);
     ++g_passes;
+    size_p0 += e->seg_hdr_size;
+    if (e->max_i4_header_bits > 0 && size_p0 > P0_LIMIT) {   /* frame_enc.c:651-655 */
+      e->max_i4_header_bits >>= 1;
+      ++npass;
+      continue;
+    }
     /* OneStatPass returns the header estimate: the mode costs (0 with
      * RD_OPT_NONE) plus the segment header, and StatLoop gives up when it is
      * 0 (frame_enc.c:645-646), before FinalizeSkipProba/FinalizeTokenProbas:
      * default probabilities and no skip flags then */
-    if (e->seg_hdr_size == 0) { stats_ok = 0; break; }
+    if (size_p0 == 0) { stats_ok = 0; break; }
     if (e->max_i4_header_bits == 0) break;   /* is_last_pass */
   }
   e->no_tokens = 0;
@@ -2209,7 +2222,8 @@ static void enc_loop(Enc* e, const vp8o_config* cfg, vp8o_mb_trace* trace, doubl
   } else {
     e->use_skip = 0;
   }
-  /* final pass */
+  /* final pass: the method's RD level with the level costs frozen */
+  e->rd_opt = final_rd;
   if (lf) memset(lf, 0, 4 * 64 * sizeof(double));
   e->no_stats = 1;
   e->ntok = 0;
@@ -2246,7 +2260,10 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
   if (!e || cfg->method < 0 || cfg->method > 6) { free(e); return 0; }
   /* methods 0-2 with a size / PSNR search take StatLoop's RD_OPT_BASIC
    * passes (frame_enc.c:614-674): not restated */
-  if (cfg->method < 3 && (cfg->target_size > 0 || cfg->target_PSNR > 0)) { free(e); return 0; }
+  if ((cfg->method < 3 || cfg->low_memory) && (cfg->target_size > 0 || cfg->target_PSNR > 0)) {
+    free(e);
+    return 0;
+  }
   e->Y = Y; e->U = U; e->V = V; e->ys = ys; e->uvs = uvs; e->w = w; e->h = h;
   e->mbw = (w + 15) >> 4; e->mbh = (h + 15) >> 4;
   e->cfg = *cfg;
@@ -2284,7 +2301,7 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
   bw_init(&part1);
   It it;
   double (*lf)[64] = cfg->autofilter ? (double (*)[64])calloc(4 * 64, sizeof(double)) : NULL;
-  if (e->rd_opt == 0) {
+  if (e->rd_opt == 0 || cfg->low_memory) {   /* VP8EncLoop: webp_enc.c:115-122 */
     enc_loop(e, cfg, trace, lf);
   } else {
     /* VP8EncTokenLoop (frame_enc.c:783-894): `pass` entropy passes, the
@@ -2360,7 +2377,8 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
     }
   }
   if (e->tok_err) goto done;
-  if (e->rd_opt > 0) finalize_token_probas(e);   /* enc_loop has settled its probabilities */
+  if (e->rd_opt > 0 && !cfg->low_memory)   /* enc_loop has settled its probabilities */
+    finalize_token_probas(e);
   for (size_t k = 0; k < e->ntok; ++k) {
     const uint16_t t = e->tok[k];
     const int bit = t >> 15;

@@ -30,6 +30,7 @@ typedef struct {
   float target_PSNR;      /* dB, 0 = off */
   int qmin, qmax;         /* 0..100 */
   int autofilter;         /* 0/1: SSIM-driven per-segment filter levels */
+  int low_memory;         /* 0/1: VP8EncLoop for methods 3-6 too */
 } vp8o_config;
 
 /* per-macroblock decisions, for stage-by-stage comparison with the GPU */

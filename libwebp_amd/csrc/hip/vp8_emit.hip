@@ -490,3 +490,105 @@ extern "C" int vp8g_launch_token_cost(const uint16_t* tokens, size_t tok_cap, in
                      tok_cap, results, state, active, bits);
   return vp8g_launch_check("k_token_cost");
 }
+
+// low_memory (VP8EncLoop for methods 3-6, frame_enc.c:614-775) on K3's
+// compact token stream (MB m's tokens at [mboff[m], mboff[m+1])), one
+// workgroup per frame:
+//   mode 0: StatLoop's statistics — the dynamic tokens of the first
+//           nb_stat[f] MBs replayed in raster order into stats[f] (kept
+//           across passes; VP8RecordCoeffs puts each statistic in its
+//           probability slot; exact in-order replay of the counters that reach
+//           the halving point, cost_enc.h:45-56), and the skip count of those
+//           MBs into nskip[f]
+//   mode 1: drop the tokens of skipped MBs (use_skip[f]), update ntokens
+__global__ __launch_bounds__(256) void k_lowmem(uint16_t* __restrict__ tokens, size_t tok_cap,
+                                                const uint32_t* __restrict__ mboff,
+                                                vp8g_frame_result* __restrict__ res,
+                                                const uint8_t* __restrict__ mbinfo, int nmb,
+                                                const int32_t* __restrict__ nb_stat,
+                                                const uint8_t* __restrict__ active, int mode,
+                                                uint32_t* __restrict__ stats,
+                                                int32_t* __restrict__ nskip) {
+  const int f = blockIdx.x, tid = threadIdx.x;
+  if (!active[f]) return;
+  __shared__ uint32_t st[VP8G_NUM_SLOTS], dl[VP8G_NUM_SLOTS], mark[33];
+  __shared__ int any, cnt;
+  uint16_t* T = tokens + (size_t)f * tok_cap;
+  const uint32_t* off = mboff + (size_t)f * nmb;
+  const uint8_t* info = mbinfo + (size_t)f * nmb * VP8G_MBINFO_BYTES;
+  const uint32_t ntok = res[f].ntokens;
+  if (mode == 0) {
+    uint32_t* S = stats + (size_t)f * VP8G_NUM_SLOTS;
+    for (int s = tid; s < VP8G_NUM_SLOTS; s += 256) { st[s] = S[s]; dl[s] = 0; }
+    if (tid < 33) mark[tid] = 0;
+    if (tid == 0) { any = 0; cnt = 0; }
+    __syncthreads();
+    const int nb = min(nb_stat[f], nmb);
+    for (int m = 0; m < nb; ++m) {
+      const uint32_t b0 = off[m], b1 = m + 1 < nmb ? off[m + 1] : ntok;
+      if (tid == 0 && info[(size_t)m * VP8G_MBINFO_BYTES + 3]) ++cnt;
+      for (uint32_t i = b0 + tid; i < b1; i += 256) {
+        const uint32_t tk = T[i];
+        if (!(tk & 0x4000u)) atomicAdd(&dl[tk & 0x3fffu], 0x10000u + (tk >> 15));
+      }
+      __syncthreads();
+      for (int s = tid; s < VP8G_NUM_SLOTS; s += 256) {
+        const uint32_t d = dl[s];
+        if (d) {
+          if ((st[s] >> 16) + (d >> 16) < 0xffffu) {
+            st[s] += d;
+          } else {
+            atomicOr(&mark[s >> 5], 1u << (s & 31));
+            any = 1;
+          }
+          dl[s] = 0;
+        }
+      }
+      __syncthreads();
+      if (any) {
+        if (tid == 0)
+          for (uint32_t i = b0; i < b1; ++i) {
+            const uint32_t tk = T[i], sl = tk & 0x3fffu;
+            if (!(tk & 0x4000u) && (mark[sl >> 5] & (1u << (sl & 31)))) {
+              uint32_t p = st[sl];
+              if (p >= 0xfffe0000u) p = ((p + 1u) >> 1) & 0x7fff7fffu;
+              st[sl] = p + 0x00010000u + (tk >> 15);
+            }
+          }
+        __syncthreads();
+        if (tid < 33) mark[tid] = 0;
+        if (tid == 0) any = 0;
+        __syncthreads();
+      }
+    }
+    for (int s = tid; s < VP8G_NUM_SLOTS; s += 256) S[s] = st[s];
+    if (tid == 0) nskip[f] = cnt;
+  } else {
+    uint32_t dst = 0;
+    for (int m = 0; m < nmb; ++m) {
+      const uint32_t b0 = off[m], b1 = m + 1 < nmb ? off[m + 1] : ntok;
+      if (info[(size_t)m * VP8G_MBINFO_BYTES + 3]) continue;
+      if (dst != b0)
+        for (uint32_t i = 0; i < b1 - b0; i += 256) {
+          const bool in = i + tid < b1 - b0;
+          const uint16_t t = in ? T[b0 + i + tid] : 0;
+          __syncthreads();
+          if (in) T[dst + i + tid] = t;
+          __threadfence_block();
+          __syncthreads();
+        }
+      dst += b1 - b0;
+    }
+    if (tid == 0) res[f].ntokens = dst;
+  }
+}
+
+extern "C" int vp8g_launch_lowmem(uint16_t* tokens, size_t tok_cap, const uint32_t* mboff,
+                                  vp8g_frame_result* results, const uint8_t* mbinfo, int nmb,
+                                  int n, const int32_t* nb_stat, const uint8_t* active, int mode,
+                                  uint32_t* stats, int32_t* nskip, void* stream) {
+  if (n <= 0) return 1;
+  hipLaunchKernelGGL(k_lowmem, dim3(n), dim3(256), 0, (hipStream_t)stream, tokens, tok_cap, mboff,
+                     results, mbinfo, nmb, nb_stat, active, mode, stats, nskip);
+  return vp8g_launch_check("k_lowmem");
+}

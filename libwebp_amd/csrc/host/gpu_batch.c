@@ -187,6 +187,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipFree(b->d_rnd_y); hipFree(b->d_rnd_uv);
   hipFree(b->d_active); hipFree(b->d_tbits);
   hipFree(b->d_ahist); hipFree(b->d_amaps); hipHostFree(b->h_ahist); hipHostFree(b->h_amaps);
+  hipFree(b->d_lmstats); hipFree(b->d_lmi); hipHostFree(b->h_lmstats); hipHostFree(b->h_lmi);
   free(b->asse);
   hipFree(b->d_recon); hipFree(b->d_mbval); hipFree(b->d_afp); hipFree(b->d_aflevel);
   hipHostFree(b->h_afp); hipHostFree(b->h_aflevel);
@@ -368,6 +369,149 @@ fail:
   return 0;
 }
 
+/* low_memory with methods 3-6: VP8EncLoop (frame_enc.c:614-775). StatLoop
+ * passes run K3 at RD_OPT_BASIC with the default probabilities and no cost
+ * refreshes; k_lowmem replays the statistics of the probe MBs (method 3: half
+ * the frame) from the compact token stream and counts their skips. The host
+ * then finalises the probabilities and the skip flag, and the final K3 pass
+ * runs the method's RD level with those costs frozen; k_lowmem drops the
+ * tokens of skipped MBs when the skip flag pays. */
+static int lowmem_passes(WebPGpuBatch* b, int n) {
+  const size_t nmb = (size_t)b->nmb, N = (size_t)b->max_frames;
+  hipStream_t st = b->stream;
+  uint8_t* act = b->pass_act;
+  if (!b->d_lmstats) {
+    CHK(hipMalloc((void**)&b->d_lmstats, N * VP8G_NUM_SLOTS * sizeof(uint32_t)));
+    CHK(hipMalloc((void**)&b->d_lmi, 2 * N * sizeof(int32_t)));
+    CHK(hipHostMalloc((void**)&b->h_lmstats, N * VP8G_NUM_SLOTS * sizeof(uint32_t), 0));
+    CHK(hipHostMalloc((void**)&b->h_lmi, 2 * N * sizeof(int32_t), 0));
+  }
+  if (!b->h_active) {
+    CHK(hipHostMalloc((void**)&b->h_active, N, 0));
+    CHK(hipMalloc((void**)&b->d_active, N));
+  }
+  if (!b->h_state)
+    CHK(hipHostMalloc((void**)&b->h_state, N * VP8G_RERUN_STATE_BYTES, 0));
+  int32_t* h_nb = b->h_lmi;          /* probe MBs per frame */
+  int32_t* h_nskip = b->h_lmi + N;   /* their skips (last pass) */
+  const int nb = b->cfg.method == 3 ? ((nmb > 200) ? (int)(nmb >> 1) : 100) : (int)nmb;
+  CHK(hipMemsetAsync(b->d_lmstats, 0, n * VP8G_NUM_SLOTS * sizeof(uint32_t), st));
+  for (int f = 0; f < n; ++f) {
+    h_nb[f] = nb;
+    act[f] = b->err[f] == VP8_ENC_OK && vp8h_pass_start(&b->frames[f]);
+  }
+  CHK(hipMemcpyAsync(b->d_lmi, b->h_lmi, 2 * n * sizeof(int32_t), hipMemcpyHostToDevice, st));
+  int first = 1;
+  for (;;) {   /* StatLoop (frame_enc.c:614-674), no search */
+    int nact = 0;
+    for (int f = 0; f < n; ++f) {
+      vp8g_frame_params* P = &b->h_params[f];
+      b->h_active[f] = act[f];
+      if (!act[f]) { P->pass_mode = 2; continue; }
+      vp8h_frame* fr = &b->frames[f];
+      vp8h_set_loop_params(fr, fr->ps_q, b->h_segmap + f * nmb, P);
+      P->rd_opt = 1;                /* RD_OPT_BASIC */
+      P->max_count = 0x7fffffff;    /* no refreshes: the default probabilities' costs */
+      P->pass_mode = 0;
+      P->recon_addr = 0;
+      ++nact;
+    }
+    if (!nact) break;
+    CHK(hipMemcpyAsync(b->d_segmap, b->h_segmap, n * nmb, hipMemcpyHostToDevice, st));
+    CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
+                       hipMemcpyHostToDevice, st));
+    CHK(hipMemcpyAsync(b->d_active, b->h_active, n, hipMemcpyHostToDevice, st));
+    if (first) CHK(hipEventRecord(b->ev[2], st));
+    first = 0;
+    if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params,
+                            b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5,
+                            b->d_results, b->d_rerun, NULL, st))
+      return 0;
+    if (!vp8g_launch_lowmem(b->d_tokens, b->tok_cap, b->d_mboff, b->d_results, b->d_mbinfo,
+                            (int)nmb, n, b->d_lmi, b->d_active, 0, b->d_lmstats, b->d_lmi + N, st))
+      return 0;
+    CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
+                       hipMemcpyDeviceToHost, st));
+    CHK(hipStreamSynchronize(st));
+    for (int f = 0; f < n; ++f) {
+      if (!act[f]) continue;
+      vp8h_frame* fr = &b->frames[f];
+      const vp8g_frame_result* R = &b->h_results[f];
+      if (R->error) { act[f] = 0; continue; }
+      const uint64_t size_p0 = R->size_p0 + (uint64_t)fr->seg_hdr_size;   /* all MBs */
+      if (b->cfg.method == 3 && size_p0 > VP8H_P0_LIMIT) {
+        /* the probe covers half the frame: its estimate is not K3's */
+        b->err[f] = VP8_ENC_ERROR_INVALID_CONFIGURATION;
+        act[f] = 0;
+        continue;
+      }
+      act[f] = vp8h_pass_finish(fr, size_p0) && vp8h_pass_start(fr);
+    }
+  }
+  /* FinalizeSkipProba + FinalizeTokenProbas + VP8CalculateLevelCosts */
+  CHK(hipMemcpyAsync(b->h_lmstats, b->d_lmstats, n * VP8G_NUM_SLOTS * sizeof(uint32_t),
+                     hipMemcpyDeviceToHost, st));
+  CHK(hipMemcpyAsync(b->h_lmi + N, b->d_lmi + N, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  int nfinal = 0;
+  for (int f = 0; f < n; ++f) {
+    vp8g_frame_params* P = &b->h_params[f];
+    b->h_active[f] = 0;
+    if (b->err[f] != VP8_ENC_OK || b->h_results[f].error) { P->pass_mode = 2; continue; }
+    uint8_t* S = b->h_state + (size_t)f * VP8G_RERUN_STATE_BYTES;
+    int dirty = 0;
+    vp8h_finalize_probas(b->h_lmstats + (size_t)f * VP8G_NUM_SLOTS, S + VP8G_STATE_COEFFS, &dirty);
+    if (dirty) memcpy(S, S + VP8G_STATE_COEFFS, VP8G_NUM_SLOTS);
+    else vp8h_default_probas(S);
+    const int skip_proba = (int)((uint64_t)(nmb - h_nskip[f]) * 255 / nmb);
+    b->frames[f].lm_skip_proba = skip_proba;
+    b->h_active[f] = skip_proba < 250;   /* use_skip_proba */
+    P->rd_opt = b->frames[f].rd_opt;   /* the final pass: the method's RD level */
+    P->max_count = 0x7fffffff;
+    P->pass_mode = 1;                  /* costs + probabilities from the state */
+    P->max_i4_header_bits = b->frames[f].max_i4_header_bits;
+    P->recon_addr = b->cfg.autofilter ? (uint64_t)(uintptr_t)(b->d_recon + (size_t)f * nmb * 512) : 0;
+    ++nfinal;
+  }
+  if (first) CHK(hipEventRecord(b->ev[2], st));
+  if (!nfinal) {
+    CHK(hipEventRecord(b->ev[3], st));
+    return 1;
+  }
+  CHK(hipMemcpyAsync(b->d_rerun, b->h_state, n * VP8G_RERUN_STATE_BYTES, hipMemcpyHostToDevice, st));
+  CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
+                     hipMemcpyHostToDevice, st));
+  if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
+                          b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5, b->d_results,
+                          b->d_rerun, b->cfg.autofilter ? b->d_recon : NULL, st))
+    return 0;
+  CHK(hipEventRecord(b->ev[3], st));
+  CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
+                     hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  /* the emitted probabilities are StatLoop's, not the final pass's */
+  for (int f = 0; f < n; ++f) {
+    if (b->h_params[f].pass_mode != 1 || b->h_results[f].error) continue;
+    vp8g_frame_result* R = &b->h_results[f];
+    memcpy(R->probas, b->h_state + (size_t)f * VP8G_RERUN_STATE_BYTES + VP8G_STATE_COEFFS,
+           VP8G_NUM_SLOTS);
+    R->use_skip = (int16_t)b->h_active[f];
+    R->skip_proba = (int16_t)b->frames[f].lm_skip_proba;
+  }
+  CHK(hipMemcpyAsync(b->d_results, b->h_results, n * sizeof(vp8g_frame_result),
+                     hipMemcpyHostToDevice, st));
+  CHK(hipMemcpyAsync(b->d_active, b->h_active, n, hipMemcpyHostToDevice, st));
+  if (!vp8g_launch_lowmem(b->d_tokens, b->tok_cap, b->d_mboff, b->d_results, b->d_mbinfo,
+                          (int)nmb, n, b->d_lmi, b->d_active, 1, b->d_lmstats, b->d_lmi + N, st))
+    return 0;
+  CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
+                     hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  return 1;
+fail:
+  return 0;
+}
+
 /* VP8EncTokenLoop's pass loop (frame_enc.c:808-880) for every frame of the
  * batch in lock step. Each round sets the loop parameters of each unfinished
  * frame for its pass (SetLoopParams with the frame's current q) and runs K3
@@ -395,8 +539,13 @@ static int run_passes(WebPGpuBatch* b, int n) {
       CHK(hipMalloc((void**)&b->d_active, N));
     }
   }
-  for (int f = 0; f < n; ++f) act[f] = b->err[f] == VP8_ENC_OK && vp8h_pass_start(&b->frames[f]);
   int round = 0;
+  if (b->cfg.low_memory && b->cfg.method >= 3) {   /* VP8EncLoop (webp_enc.c:115-122) */
+    if (!lowmem_passes(b, n)) return 0;
+    round = 1;
+  }
+  for (int f = 0; f < n; ++f)
+    act[f] = !b->cfg.low_memory && b->err[f] == VP8_ENC_OK && vp8h_pass_start(&b->frames[f]);
   for (;;) {
     int nact = 0, nsize = 0;
     for (int f = 0; f < n; ++f) {

@@ -46,6 +46,10 @@ struct WebPGpuBatch {
   unsigned long long* d_tbits;
   unsigned long long* h_tbits;
   int* fin_cost;             /* FinalizeTokenProbas header cost per frame */
+  uint32_t* d_lmstats;       /* low_memory: StatLoop statistics (first use) */
+  uint32_t* h_lmstats;
+  int32_t* d_lmi;            /* low_memory: probe MBs, then skips, per frame */
+  int32_t* h_lmi;
   /* autofilter (allocated on first use) */
   uint8_t* d_recon;          /* reconstructed MBs, n x nmb x 512 */
   double* d_mbval;           /* per-MB SSIM per level, n x nmb x 64 */

@@ -56,7 +56,10 @@ int vp8h_frame_init(vp8h_frame* fr, const WebPConfig* cfg, int w, int h) {
    * (one bit writer per MB row modulo 2^partitions) are not implemented */
   if (cfg->method < 3 && (cfg->target_size > 0 || cfg->target_PSNR > 0 || cfg->partitions > 0))
     return 0;
-  if (cfg->low_memory) return 0;
+  /* low_memory runs VP8EncLoop for methods 3-6 too; its size / PSNR search
+   * and token partitions are not implemented */
+  if (cfg->low_memory && (cfg->target_size > 0 || cfg->target_PSNR > 0 || cfg->partitions > 0))
+    return 0;
   fr->w = w; fr->h = h;
   fr->mbw = (w + 15) >> 4; fr->mbh = (h + 15) >> 4;
   fr->method = cfg->method;
@@ -140,6 +143,10 @@ int vp8h_pass_finish(vp8h_frame* fr, uint64_t size_p0) {
   if (fr->is_last_pass) return 0;
   if (fr->do_search) compute_next_q(fr);
   return fr->pass_left > 0;
+}
+
+void vp8h_default_probas(uint8_t* coeffs) {   /* VP8DefaultCoeffProbas, tree_enc.c */
+  memcpy(coeffs, &kVP8CoeffProba0[0][0][0][0], VP8G_NUM_SLOTS);
 }
 
 int vp8h_finalize_probas(const uint32_t* stats, uint8_t* coeffs, int* dirty) {

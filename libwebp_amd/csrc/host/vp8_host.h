@@ -35,6 +35,7 @@ typedef struct {
   /* filter header */
   int f_simple, f_level, f_sharpness;
   /* multi-pass convergence (PassStats, frame_enc.c:38-80) */
+  int lm_skip_proba;   /* low_memory: StatLoop's skip probability */
   int autofilter;   /* segment filter levels from the GPU SSIM search (filter_enc.c:156-212) */
   int cfg_pass, pass_left, is_last_pass, npass, do_search, do_size_search, ps_is_first;
   float ps_dq, ps_q, ps_last_q, ps_qmin, ps_qmax;
@@ -81,6 +82,7 @@ int vp8h_pass_finish(vp8h_frame* fr, uint64_t size_p0);
 /* FinalizeTokenProbas (frame_enc.c:146-180) from the token statistics:
  * writes the probabilities, returns the proba-update header cost (1/256
  * bit); *dirty = some probability differs from the default table */
+void vp8h_default_probas(uint8_t* coeffs);   /* the default coefficient probabilities */
 int vp8h_finalize_probas(const uint32_t* stats, uint8_t* coeffs, int* dirty);
 /* size of the pass in bytes (size search) from the finalize cost, the token
  * bit estimate (VP8EstimateTokenSize) and the header estimate */

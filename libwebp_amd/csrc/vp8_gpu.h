@@ -173,6 +173,16 @@ int vp8g_launch_encode_none(const uint8_t* yuv, size_t yuv_frame_bytes, int w, i
                             uint8_t* mbinfo, uint32_t* mboff, vp8g_frame_result* results,
                             uint8_t* rerun_state, void* stream);
 
+/* low_memory on K3's compact stream (hip/vp8_emit.hip k_lowmem): mode 0
+ * adds StatLoop's statistics of the first nb_stat[f] MBs to stats[f]
+ * (NUM_SLOTS uint32) and counts their skipped MBs into nskip[f]; mode 1
+ * drops the tokens of the skipped MBs and updates results[f].ntokens.
+ * Frames with active[f] == 0 are left alone. */
+int vp8g_launch_lowmem(uint16_t* tokens, size_t tok_cap, const uint32_t* mboff,
+                       vp8g_frame_result* results, const uint8_t* mbinfo, int nmb, int n,
+                       const int32_t* nb_stat, const uint8_t* active, int mode, uint32_t* stats,
+                       int32_t* nskip, void* stream);
+
 /* VP8EstimateTokenSize (token_enc.c:226-247) of each frame's compact token
  * stream under the probabilities at state + f * VP8G_RERUN_STATE_BYTES +
  * VP8G_STATE_COEFFS; frames with active[f] == 0 are skipped. bits[f] (device,

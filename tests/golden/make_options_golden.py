@@ -13,6 +13,7 @@ Y PSNR / segment levels the reference reports in WebPAuxStats.
   autofilter  config->autofilter (src/enc/filter_enc.c:156-212)
   methods012  config->method 0-2 (VP8EncLoop, src/enc/frame_enc.c:614-775)
   dither      config->preprocessing & 2 on ARGB input (src/enc/webp_enc.c:357-365)
+  lowmem      config->low_memory with methods 3-6 (VP8EncLoop, frame_enc.c:614-775)
 """
 import ctypes
 import hashlib
@@ -28,7 +29,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 from libwebp_amd import abi  # noqa: E402
 from libwebp_amd.synth import syn_v1  # noqa: E402
 
-MODULES = ["multipass", "autofilter", "methods012", "dither"]
+MODULES = ["multipass", "autofilter", "methods012", "dither", "lowmem"]
 
 
 def main():

@@ -173,6 +173,8 @@ def main():
     ap.add_argument("--method", type=int, default=4)
     ap.add_argument("--sharp-yuv", action="store_true",
                     help="use_sharp_yuv import (cwebp -sharp_yuv); not the headline config")
+    ap.add_argument("--low-memory", action="store_true",
+                    help="config->low_memory (cwebp -low_memory, VP8EncLoop); not the headline config")
     ap.add_argument("--threads", type=int, default=0, help="host tail threads (0 = auto)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -202,7 +204,7 @@ def main():
     torch.cuda.synchronize(dev)
     enc = libwebp_amd.GpuBatch(W, H, B, quality=args.quality, method=args.method, device=local,
                                threads=args.threads, use_sharp_yuv=int(args.sharp_yuv),
-                               lossless=int(args.lossless))
+                               lossless=int(args.lossless), low_memory=int(args.low_memory))
 
     def step():
         enc.encode_device(rgba.data_ptr(), B, stream=stream)
@@ -279,14 +281,15 @@ def main():
         "data": "synthetic syn-v1 RGBA frames generated in HBM (SURVEY.md 8(d))",
         "config": {"workload": "batch of %d %dx%d RGBA frames per GPU, -q %g -m %d%s" %
                                (B, W, H, args.quality, args.method,
-                                " -sharp_yuv" if args.sharp_yuv else ""),
+                                (" -sharp_yuv" if args.sharp_yuv else "") +
+                                (" -low_memory" if args.low_memory else "")),
                    "frames_per_gpu": B, "width": W, "height": H,
                    "quality": args.quality, "method": args.method,
                    "parallelism": "frames sharded %d ways" % world},
         "roofline": {"bound": "hbm", "kernel": "k_encode", "achieved": round(achieved, 3),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6),
-                     "traffic": None if args.sharp_yuv else
+                     "traffic": None if args.sharp_yuv or args.low_memory else
                      measured_traffic("k_encode<3, false, false>", B, W, H, args.quality, args.method),
                      "traffic_source": "profiles/r1_pmc_hbm.csv (rocprofv3 --pmc FETCH_SIZE, "
                                        "WRITE_SIZE passes of this workload; bytes per launch)",

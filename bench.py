@@ -3,87 +3,166 @@
 frames on MI355X, BASELINE.json configs[1] (1 GPU) / configs[2] (8 GPUs).
 
 One "step" = one WebPGpuBatchEncodeRGBA call over the rank's batch of
-HBM-resident syn-v1 frames (SURVEY.md §8(d)): K1 import, K2 analysis, host
+HBM-resident syn-v1 frames (SURVEY.md 8(d)): K1 import, K2 analysis, host
 segment setup, K3 RD search + tokens, K4 boolean coder on the device (host
 codes partition 0 meanwhile), one D2H of the packed partitions and the RIFF
-write, ending with every .webp in host memory. Frames are
-synthesised on the device before timing starts (value = throughput with the
-input resident in HBM); the PCIe-inclusive host-input rate is measured
-separately by `--host-input` and documented in DESIGN.md.
+write, ending with every .webp in host memory. Frames are synthesised on the
+device before timing starts, so `value` is the throughput with the input
+resident in HBM. SURVEY.md 8(d)'s own MP/s definition (RGBA in host memory,
+upload included) is reported beside it as `host_input_mps`: the same frames
+from pinned host memory, the upload of step i+1 overlapping the encode of
+step i (two device buffers, one copy stream each).
 
-Multi-GPU: one process per GPU (torchrun). Rank r encodes frames
-[r*B, (r+1)*B); the only collective is an all-gather of encoded sizes (RCCL),
-plus the barrier / max-over-ranks timing required by the harness.
+Multi-GPU (configs[2]): one process per GPU. `--gpus N` without a torchrun
+environment starts `torch.distributed.run` with N ranks itself (a child
+process, before this process touches the GPU) and exits with its status.
+Rank r encodes frames [r*B, (r+1)*B); the only data-path collective is an
+all-gather of the encoded sizes (RCCL), plus the barrier / max-over-ranks
+timing of the harness contract. After the timed loop every rank checks the
+frames of its timed batch that tests/golden/shard_kat.json pins (reference
+libwebp SHA-256s) and rank 0 reports the result as `kat_check`.
 
-Output: one JSON line on rank 0 (see README contract in DESIGN.md).
+`--stub` replaces the GPU encoder by a CPU test double (gloo backend): the
+launcher, sharding, size gather and timing run exactly as on the GPU
+(tests/test_bench_dist.py).
 """
 import argparse
+import hashlib
 import json
 import os
+import subprocess
 import sys
 import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
+BOX_CORE_SHARE = 16     # host cores a one-GPU box gives a job (gpurun notes)
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks; without a torchrun environment bench.py launches them itself")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per GPU per step (0: 256 lossy, 1024 lossless)")
+    ap.add_argument("--lossless", action="store_true",
+                    help="configs[4]: -lossless -m 4 (VP8L) instead of the lossy headline")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--quality", type=float, default=75.0)
+    ap.add_argument("--method", type=int, default=4)
+    ap.add_argument("--sharp-yuv", action="store_true",
+                    help="use_sharp_yuv import (cwebp -sharp_yuv); not the headline config")
+    ap.add_argument("--low-memory", action="store_true",
+                    help="config->low_memory (cwebp -low_memory, VP8EncLoop); not the headline")
+    ap.add_argument("--threads", type=int, default=0, help="host tail threads (0 = auto)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="CPU work per baseline leg (single thread, all cores)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-host-input", action="store_true",
+                    help="skip the PCIe-inclusive host-input measurement")
+    ap.add_argument("--stub", action="store_true",
+                    help="CPU test double instead of the GPU encoder (gloo; tests only)")
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# launcher
+
+def launch_ranks(args, argv):
+    """--gpus N > 1 outside torchrun: run N ranks through torch.distributed.run
+    as a child process and return its exit status (None: run in-process)."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline: the reference libwebp (oracle/_ref, built from /root/reference
+# sources by oracle/Makefile) on this host's cores
+
+def _ref_encoder(quality, method, lossless):
+    import ctypes as C
+    from libwebp_amd import abi
+    ref = os.path.join(HERE, "oracle", "_ref", "libwebp_ref.so")
+    if os.path.exists(ref):
+        lib = abi.bind_encoder_api(C.CDLL(ref))
+        kw = {"lossless": 1, "use_argb": True} if lossless else {}
+        return "reference", lambda img: abi.encode_rgba(lib, img, quality=quality,
+                                                        method=method, **kw)
+    if lossless:
+        return None, None
+    from oracle import oracle as orc   # the C restatement, also single-threaded
+    return "port", lambda img: orc.encode_rgba(img, quality=quality, method=method)
+
+
+def _cpu_leg(width, height, quality, method, lossless, seconds, first):
+    """Encode syn-v1 frames first, first+1, ... for `seconds` of wall time
+    (after one untimed warm-up frame); returns (frames, seconds, kind)."""
+    from libwebp_amd.synth import syn_v1
+    kind, enc = _ref_encoder(quality, method, lossless)
+    if enc is None:
+        return 0, 0.0, None
+    imgs = [syn_v1(width, height, first + k) for k in range(2)]
+    enc(imgs[0])
+    frames, t0 = 0, time.perf_counter()
+    while True:
+        enc(imgs[frames & 1])
+        frames += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and frames >= 2:
+            return frames, el, kind
+
+
+def _cpu_leg_worker(a):
+    return _cpu_leg(*a)
 
 
 def cpu_baseline(width, height, quality, method, seconds, lossless=False):
-    """Reference libwebp (compiled from /root/reference sources into
-    oracle/_ref by oracle/Makefile) timed single-threaded on this host:
-    WebPPictureImportRGBA + WebPEncode into a memory writer, syn-v1 frames
-    1, 2, ... until `seconds` of CPU work (frame 0 is an untimed warm-up)."""
-    import numpy as np
-    from libwebp_amd import abi
-    from libwebp_amd.synth import syn_v1
-    import ctypes as C
-    ref = os.path.join(HERE, "oracle", "_ref", "libwebp_ref.so")
-    kind = "reference"
-    if os.path.exists(ref):
-        lib = C.CDLL(ref)
-        abi.bind_encoder_api(lib)
-        if lossless:   # ARGB picture, like cwebp -lossless
-            enc = lambda img: abi.encode_rgba(lib, img, quality=quality, method=method,
-                                              lossless=1, use_argb=True)
-        else:
-            enc = lambda img: abi.encode_rgba(lib, img, quality=quality, method=method)
-    elif lossless:
+    """WebPPictureImportRGBA + WebPEncode into a memory writer,
+    single thread (the 40x denominator) and one process per host core
+    (independent frames). Runs before this process touches the GPU (the
+    all-core leg forks)."""
+    import multiprocessing as mp
+    frames, el, kind = _cpu_leg(width, height, quality, method, lossless, seconds, 1)
+    if kind is None:
         return None
-    else:   # the C restatement (oracle/), also single-threaded
-        from oracle import oracle as orc
-        kind = "port"
-        enc = lambda img: orc.encode_rgba(img, quality=quality, method=method)
-    enc(syn_v1(width, height, 0))
-    elapsed, frames, f = 0.0, 0, 1
-    while elapsed < seconds or frames < 2:
-        img = syn_v1(width, height, f)
-        t0 = time.perf_counter()
-        enc(img)
-        elapsed += time.perf_counter() - t0
-        frames += 1
-        f += 1
-    mps = frames * width * height / elapsed / 1e6
-    return {"value": round(mps, 3), "unit": "MP/s", "cores": 1, "kind": kind,
-            "sample": "%d syn-v1 %dx%d frames (f=1..%d), q%d m%d%s, WebPPictureImportRGBA+"
-                      "WebPEncode, single thread, %.1f s" % (
-                          frames, width, height, frames, quality, method,
-                          " lossless" if lossless else "", elapsed)}
+    px = width * height
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, BOX_CORE_SHARE))
+    with mp.get_context("fork").Pool(cores) as pool:
+        legs = pool.map(_cpu_leg_worker, [(width, height, quality, method, lossless, seconds,
+                                           1 + 2 * k) for k in range(cores)])
+    all_frames = sum(l[0] for l in legs)
+    all_wall = max(l[1] for l in legs)
+    mode = " lossless" if lossless else ""
+    return {"value": round(frames * px / el / 1e6, 3), "unit": "MP/s", "cores": 1,
+            "kind": kind,
+            "sample": "%d syn-v1 %dx%d frames, q%d m%d%s, WebPPictureImportRGBA+WebPEncode, "
+                      "single thread, %.1f s" % (frames, width, height, quality, method, mode, el),
+            "all_cores": {"value": round(all_frames * px / all_wall / 1e6, 3), "unit": "MP/s",
+                          "cores": cores,
+                          "sample": "%d processes x %.1f s, %d frames in all, independent "
+                                    "frames per process" % (cores, all_wall, all_frames)}}
 
 
-def measured_traffic(kernel, B, W, H, quality, method):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
-    passes (profiles/r1_pmc_hbm.csv: FETCH_SIZE + WRITE_SIZE in KB, one
-    launch of this same default workload), or None for another workload."""
-    import csv
-    path = os.path.join(HERE, "profiles", "r1_pmc_hbm.csv")
-    if not os.path.exists(path) or (B, W, H, quality, method) != (256, 1920, 1080, 75.0, 4):
-        return None
-    for r in csv.DictReader(open(path)):
-        if r["kernel"] == kernel:
-            return int(1000 * (float(r["FETCH_SIZE_KB"]) + float(r["WRITE_SIZE_KB"])))
-    return None
-
+# ---------------------------------------------------------------------------
+# multi-rank plumbing (any backend: nccl on the GPUs, gloo in the CPU tests)
 
 def shard(rank, frames_per_rank):
     """Frames [first, first + n) owned by `rank`."""
@@ -92,7 +171,7 @@ def shard(rank, frames_per_rank):
 
 def gather_sizes(sizes, world):
     """All-gather the per-frame encoded sizes of every rank (the only
-    data-path collective). Works on any backend (nccl on GPU, gloo in tests)."""
+    data-path collective)."""
     import torch
     import torch.distributed as dist
     if world == 1:
@@ -112,11 +191,68 @@ def max_over_ranks(seconds, world, device):
     return float(t.item())
 
 
+def sum_over_ranks(values, world, device):
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(values, dtype=torch.int64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [int(v) for v in t.tolist()]
+
+
+def shard_kats(args):
+    """Known answers (frame -> sha256) for the default lossy workload, or {}."""
+    path = os.path.join(HERE, "tests", "golden", "shard_kat.json")
+    if (args.lossless or args.sharp_yuv or args.low_memory or not os.path.exists(path)):
+        return {}
+    k = json.load(open(path))
+    if (k["width"], k["height"], k["quality"], k["method"]) != (
+            args.width, args.height, args.quality, args.method):
+        return {}
+    if args.stub:   # the same frames, with the test double's own answers
+        return {int(f): hashlib.sha256(StubBatch(0).output(int(f))).hexdigest()
+                for f in k["frames"]}
+    return {int(f): v["sha256"] for f, v in k["frames"].items()}
+
+
+class StubBatch:
+    """CPU test double with GpuBatch's interface (tests only): 'encodes' frame
+    f into a deterministic 100 + f % 7 byte string, taking ~1 ms per step."""
+
+    def __init__(self, first):
+        self.first, self.n = first, 0
+
+    def encode_device(self, ptr, n, stream=None):
+        time.sleep(0.001)
+        self.n = n
+
+    def output(self, f):
+        g = self.first + f
+        return bytes([g & 255]) * (100 + g % 7)
+
+    def output_size(self, f):
+        return len(self.output(f))
+
+    def error(self, f):
+        return 0
+
+    def token_count(self, f):
+        return 0
+
+    def timings(self):
+        return [0.0] * 10
+
+    def close(self):
+        pass
+
+
+# ---------------------------------------------------------------------------
+
 def lossless_line(args, world, B, W, H, elapsed, tails, total_bytes):
     """configs[4] line: VP8L encode. Dominant kernel: the L1 transform tile
     kernel (k_vp8l_transform); algorithmic bytes per launch = RGBA read
     (4 B/px) + residual ARGB written (4 B/px) + per-tile modes/multipliers."""
-    mp = world * B * W * H * args.steps / 1e6
+    mp_ = world * B * W * H * args.steps / 1e6
     steps = len(tails)
     avg = lambda i: sum(t[i] for t in tails) / steps
     tb = 5 if args.method == 4 else (6 if args.method < 4 else 4)
@@ -124,9 +260,9 @@ def lossless_line(args, world, B, W, H, elapsed, tails, total_bytes):
     l1_bytes = B * (8 * W * H + 5 * ntt)
     l1_s = avg(7) / 1e6
     achieved = l1_bytes / l1_s / 1e9 if l1_s > 0 else 0.0
-    line = {
+    return {
         "metric": "megapixels/sec encoded (cwebp -lossless -m 4, 1920x1080 batch)",
-        "value": round(mp / elapsed, 3),
+        "value": round(mp_ / elapsed, 3),
         "unit": "MP/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -151,124 +287,185 @@ def lossless_line(args, world, B, W, H, elapsed, tails, total_bytes):
                       ("k_cache_parse_cluster_events", 6), ("k_write_events", 8))},
         "output_bytes_per_frame": round(total_bytes / (world * B), 1),
     }
-    if not args.no_cpu:
-        cb = cpu_baseline(W, H, int(args.quality), args.method, args.cpu_seconds, lossless=True)
-        if cb:
-            line["cpu_baseline"] = cb
-    return line
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=0,
-                    help="frames per GPU per step (0: 256 lossy, 1024 lossless)")
-    ap.add_argument("--lossless", action="store_true",
-                    help="configs[4]: -lossless -m 4 (VP8L) instead of the lossy headline")
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--quality", type=float, default=75.0)
-    ap.add_argument("--method", type=int, default=4)
-    ap.add_argument("--sharp-yuv", action="store_true",
-                    help="use_sharp_yuv import (cwebp -sharp_yuv); not the headline config")
-    ap.add_argument("--low-memory", action="store_true",
-                    help="config->low_memory (cwebp -low_memory, VP8EncLoop); not the headline config")
-    ap.add_argument("--threads", type=int, default=0, help="host tail threads (0 = auto)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--host-input", action="store_true",
-                    help="also time one step from host-memory RGBA (PCIe-inclusive)")
-    args = ap.parse_args()
+def measured_traffic(kernel, B, W, H, quality, method):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/hbm_traffic.json: FETCH_SIZE and WRITE_SIZE of one launch of this
+    same default workload, gfx950 corrections applied as documented there), or
+    None for another workload."""
+    path = os.path.join(HERE, "profiles", "hbm_traffic.json")
+    if not os.path.exists(path) or (B, W, H, quality, method) != (256, 1920, 1080, 75.0, 4):
+        return None, None
+    d = json.load(open(path))
+    k = d["kernels"].get(kernel)
+    return (int(k["bytes_per_launch"]) if k else None), d["source"]
+
+
+def host_input_rate(enc, rgba, B, W, H, steps, dev):
+    """SURVEY.md 8(d) MP/s: RGBA in (pinned) host memory -> .webp bytes in host
+    memory, upload included. Two device buffers, one copy stream each: the
+    upload of step i+1 overlaps the encode of step i."""
+    import torch
+    pinned = torch.empty(rgba.numel(), dtype=torch.uint8, pin_memory=True)
+    pinned.copy_(rgba)
+    bufs = [torch.empty_like(rgba), torch.empty_like(rgba)]
+    cs = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    with torch.cuda.stream(cs[0]):
+        bufs[0].copy_(pinned, non_blocking=True)
+    for i in range(steps):
+        if i + 1 < steps:
+            with torch.cuda.stream(cs[(i + 1) & 1]):
+                bufs[(i + 1) & 1].copy_(pinned, non_blocking=True)
+        enc.encode_device(bufs[i & 1].data_ptr(), B, stream=cs[i & 1].cuda_stream)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    del bufs, pinned
+    return steps * B * W * H / el / 1e6
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    rc = launch_ranks(args, argv)
+    if rc is not None:
+        return rc
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    import torch.distributed as dist
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
-
-    import libwebp_amd
+    if "WORLD_SIZE" in os.environ and args.gpus not in (1, world):
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     W, H = args.width, args.height
     B = args.batch or (1024 if args.lossless else 256)
-    fs = 4 * W * H
-    rgba = torch.empty(B * fs, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    # the CPU baseline first: before this process initialises the GPU
+    cb = None
+    if rank == 0 and world == 1 and not args.no_cpu and not args.stub:
+        cb = cpu_baseline(W, H, int(args.quality), args.method, args.cpu_seconds,
+                          lossless=args.lossless)
+
+    import torch
+    import torch.distributed as dist
+    if args.stub:
+        dev = torch.device("cpu")
+        backend = "gloo"
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        backend = "nccl"
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if args.stub:
+            dist.init_process_group(backend, rank=rank, world_size=world)
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world, device_id=dev)
+
     first, _ = shard(rank, B)
-    libwebp_amd.synth_device(rgba.data_ptr(), W, H, first, B, seed=1, stream=stream)
-    torch.cuda.synchronize(dev)
-    enc = libwebp_amd.GpuBatch(W, H, B, quality=args.quality, method=args.method, device=local,
-                               threads=args.threads, use_sharp_yuv=int(args.sharp_yuv),
-                               lossless=int(args.lossless), low_memory=int(args.low_memory))
+    if args.stub:
+        rgba, stream, enc = None, None, StubBatch(first)
+    else:
+        import libwebp_amd
+        rgba = torch.empty(B * 4 * W * H, dtype=torch.uint8, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        libwebp_amd.synth_device(rgba.data_ptr(), W, H, first, B, seed=1, stream=stream)
+        torch.cuda.synchronize(dev)
+        enc = libwebp_amd.GpuBatch(W, H, B, quality=args.quality, method=args.method,
+                                   device=local, threads=args.threads,
+                                   use_sharp_yuv=int(args.sharp_yuv),
+                                   lossless=int(args.lossless), low_memory=int(args.low_memory))
 
     def step():
-        enc.encode_device(rgba.data_ptr(), B, stream=stream)
+        enc.encode_device(rgba.data_ptr() if rgba is not None else 0, B, stream=stream)
 
     def barrier():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize(dev)
+        if not args.stub:
+            torch.cuda.synchronize(dev)
 
     for _ in range(args.warmup):
         step()
     barrier()
     t0 = time.perf_counter()
-    k3_us, tails = 0.0, []
+    tails = []
     for _ in range(args.steps):
         step()
-        t = enc.timings()
-        k3_us += t[6]
-        tails.append(t)
+        tails.append(enc.timings())
     barrier()
     elapsed = time.perf_counter() - t0
+
     errs = [enc.error(f) for f in range(B)]
     if any(errs):
         raise RuntimeError("rank %d: frame errors %s" % (rank, sorted(set(errs))))
+    # parity of the timed batch: the frames the reference's known answers pin
+    kats = shard_kats(args)
+    checked = failed = 0
+    for g, want in kats.items():
+        if first <= g < first + B:
+            checked += 1
+            failed += hashlib.sha256(enc.output(g - first)).hexdigest() != want
     sizes = torch.tensor([enc.output_size(f) for f in range(B)], dtype=torch.int64, device=dev)
     ntok = sum(enc.token_count(f) for f in range(B))
     allsizes = gather_sizes(sizes, world)
     elapsed = max_over_ranks(elapsed, world, dev)
+    checked, failed = sum_over_ranks([checked, failed], world, dev)
     total_bytes = int(sum(int(s.sum().item()) for s in allsizes))
 
     host_rate = None
-    if args.host_input and rank == 0:
-        import numpy as np
-        host = rgba.view(B, H, W, 4).cpu().numpy()
-        t1 = time.perf_counter()
-        enc.encode_host(host)
-        host_rate = B * W * H / (time.perf_counter() - t1) / 1e6
+    if rank == 0 and world == 1 and not args.stub and not args.no_host_input:
+        host_rate = host_input_rate(enc, rgba, B, W, H, max(2, min(args.steps, 4)), dev)
 
-    if rank != 0:
-        if world > 1:
-            dist.barrier()
-            dist.destroy_process_group()
-        return
-    if args.lossless:
-        print(json.dumps(lossless_line(args, world, B, W, H, elapsed, tails, total_bytes)),
-              flush=True)
-        if world > 1:
-            dist.barrier()
-            dist.destroy_process_group()
-        enc.close()
-        return
-    mp = world * B * W * H * args.steps / 1e6
-    value = mp / elapsed
+    line = None
+    if rank == 0:
+        if args.lossless:
+            line = lossless_line(args, world, B, W, H, elapsed, tails, total_bytes)
+        else:
+            line = lossy_line(args, world, B, W, H, elapsed, tails, total_bytes, ntok)
+        if kats and failed:
+            line["kat_check"] = "FAIL: %d of %d timed-batch frames differ from " \
+                                "tests/golden/shard_kat.json" % (failed, checked)
+        elif kats:
+            line["kat_check"] = "ok: %d timed-batch frames on %d rank(s) equal " \
+                                "tests/golden/shard_kat.json" % (checked, world)
+        if host_rate is not None:
+            line["host_input_mps"] = round(host_rate, 3)
+            line["host_input_note"] = ("RGBA in pinned host memory -> .webp in host memory, "
+                                       "H2D upload of step i+1 overlapped with step i")
+        if cb:
+            line["cpu_baseline"] = cb
+        if args.stub:
+            line["data"] = "stub encoder (CPU test double, no GPU)"
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    enc.close()
+    if failed:
+        raise SystemExit("timed-batch frames differ from the reference known answers")
+    return 0
+
+
+def lossy_line(args, world, B, W, H, elapsed, tails, total_bytes, ntok):
+    mp_ = world * B * W * H * args.steps / 1e6
+    steps = len(tails)
+    avg = lambda i: sum(t[i] for t in tails) / steps
     # K3 (k_encode) roofline: algorithmic bytes per launch = YUV420 planes read
     # (W*H + 2*ceil(W/2)*ceil(H/2) per frame) + 16-bit token stream written +
     # 20 B/MB mode info + the per-frame result block.
     nmb = ((W + 15) // 16) * ((H + 15) // 16)
     yuv = W * H + 2 * ((W + 1) // 2) * ((H + 1) // 2)
     k3_bytes = B * (yuv + 20 * nmb + 1160) + 2 * ntok
-    k3_avg_s = k3_us / args.steps / 1e6
-    achieved = k3_bytes / k3_avg_s / 1e9 if k3_avg_s > 0 else 0.0
-    line = {
+    k3_s = avg(6) / 1e6
+    achieved = k3_bytes / k3_s / 1e9 if k3_s > 0 else 0.0
+    traffic, tsrc = (None, None)
+    if not (args.sharp_yuv or args.low_memory or args.stub):
+        traffic, tsrc = measured_traffic("k_encode", B, W, H, args.quality, args.method)
+    return {
         "metric": "megapixels/sec encoded (cwebp -q 75, 1920x1080 batch)",
-        "value": round(value, 3),
+        "value": round(mp_ / elapsed, 3),
         "unit": "MP/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -289,30 +486,17 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "k_encode", "achieved": round(achieved, 3),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6),
-                     "traffic": None if args.sharp_yuv or args.low_memory else
-                     measured_traffic("k_encode<3, false, false>", B, W, H, args.quality, args.method),
-                     "traffic_source": "profiles/r1_pmc_hbm.csv (rocprofv3 --pmc FETCH_SIZE, "
-                                       "WRITE_SIZE passes of this workload; bytes per launch)",
-                     "k_encode_ms": round(1e3 * k3_avg_s, 3),
+                     "traffic": traffic, "traffic_source": tsrc,
+                     "k_encode_ms": round(1e3 * k3_s, 3),
                      "algorithmic_bytes_per_launch": k3_bytes},
-        "stage_ms": {k: round(sum(t[i] for t in tails) / len(tails) / 1e3, 3) for k, i in
+        "stage_ms": {k: round(avg(i) / 1e3, 3) for k, i in
                      (("import_analysis", 0), ("host_setup", 1), ("rd_tokens", 2),
                       ("d2h", 3), ("host_tail", 4), ("total", 5),
                       ("k_encode_events", 6), ("k_import_analyze_events", 7),
                       ("k_emit_events", 8))},
         "output_bytes_per_frame": round(total_bytes / (world * B), 1),
     }
-    if host_rate is not None:
-        line["host_input_mps"] = round(host_rate, 3)
-    if not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(W, H, int(args.quality), args.method,
-                                            args.cpu_seconds)
-    print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
-    enc.close()
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

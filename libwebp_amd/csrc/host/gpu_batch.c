@@ -540,12 +540,16 @@ static int run_passes(WebPGpuBatch* b, int n) {
     }
   }
   int round = 0;
-  if (b->cfg.low_memory && b->cfg.method >= 3) {   /* VP8EncLoop (webp_enc.c:115-122) */
+  /* low_memory only changes methods 3-6 (they switch to VP8EncLoop,
+   * webp_enc.c:115-122); methods 0-2 already run VP8EncLoop and encode exactly
+   * as without the flag */
+  const int lowmem = b->cfg.low_memory && b->cfg.method >= 3;
+  if (lowmem) {
     if (!lowmem_passes(b, n)) return 0;
     round = 1;
   }
   for (int f = 0; f < n; ++f)
-    act[f] = !b->cfg.low_memory && b->err[f] == VP8_ENC_OK && vp8h_pass_start(&b->frames[f]);
+    act[f] = !lowmem && b->err[f] == VP8_ENC_OK && vp8h_pass_start(&b->frames[f]);
   for (;;) {
     int nact = 0, nsize = 0;
     for (int f = 0; f < n; ++f) {

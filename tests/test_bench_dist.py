@@ -60,3 +60,28 @@ def test_shard_disjoint():
         assert not (fr & seen)
         seen |= fr
     assert seen == set(range(2048))
+
+
+def test_launcher_two_ranks_stub():
+    """`bench.py --gpus 2` outside torchrun starts torch.distributed.run with
+    two ranks itself; with the CPU test double (gloo) the full rank path runs:
+    sharding, warm-up, timed loop, size all-gather, max-over-ranks timing and
+    the timed-batch known-answer check summed over the ranks."""
+    import json
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--stub", "--gpus", "2",
+                        "--steps", "2", "--warmup", "1"], capture_output=True, text=True,
+                       timeout=240, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["steps"] == 2 and line["scaling"] == "weak"
+    # frames 0..7, 131, 255 (rank 0) and 256, 387, 511 (rank 1) are pinned
+    assert line["kat_check"].startswith("ok: 13 timed-batch frames on 2 rank(s)")
+    # the stub's sizes are 100 + f % 7 bytes for frames 0..511
+    assert line["output_bytes_per_frame"] == round(sum(100 + f % 7 for f in range(512)) / 512, 1)

@@ -34,6 +34,11 @@ CASES = [
     (240, 160, 6, {"quality": 70.0, "method": 4, "autofilter": 1, "sns_strength": 90}),
     (128, 96, 5, {"quality": 10.0, "method": 6, "filter_strength": 0}),
     (1920, 1080, 0, {"quality": 75.0, "method": 4}),
+    # methods 0-2 already run VP8EncLoop: low_memory changes nothing there
+    # (webp_enc.c:115-122), the bytes equal the encode without the flag
+    (176, 144, 2, {"quality": 70.0, "method": 0}),
+    (333, 257, 1, {"quality": 80.0, "method": 2}),
+    (64, 48, 0, {"quality": 75.0, "method": 1, "segments": 2}),
 ]
 for _c in CASES:
     _c[3]["low_memory"] = 1
@@ -77,7 +82,7 @@ def test_gpu_batch_lowmem(gpu):
     frames = np.stack([syn_v1(w, h, f) for f in range(n)])
     buf = torch.from_numpy(frames).to("cuda:0")
     torch.cuda.synchronize()
-    for m in (3, 4, 6):
+    for m in (0, 2, 3, 4, 6):
         kw = {"quality": 65.0, "method": m, "low_memory": 1}
         enc = gpu.GpuBatch(w, h, n, **kw)
         enc.encode_device(buf.data_ptr(), n)

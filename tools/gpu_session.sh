@@ -1,0 +1,52 @@
+#!/bin/bash
+# One GPU-box session: GPU tests, bench line, K3 stage split, rocprofv3 kernel
+# stats, PMC passes (HBM bytes, SQ issue counters) and the PMC calibration.
+# Usage (on the box): bash tools/gpu_session.sh <tag> [steps...]
+#   steps: tests bench stages prof pmc sq calib (default: all)
+set -o pipefail
+TAG=${1:-s}; shift
+STEPS=${*:-tests bench stages prof pmc sq calib}
+R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/$TAG; mkdir -p $O
+cd $R
+has() { [[ " $STEPS " == *" $1 "* ]]; }
+run() { echo "== $*" >> $O/steps.log; "$@"; local rc=$?; echo "   rc=$rc" >> $O/steps.log; return $rc; }
+BENCH="python3 $R/bench.py --no-cpu --no-host-input"
+if has tests; then
+  run timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+    > $O/gpu_tests.log 2>&1 || exit 1
+fi
+if has bench; then
+  run timeout -k 10 400 python3 bench.py --steps 5 --warmup 2 > $O/bench.json 2> $O/bench.err || exit 1
+fi
+if has stages; then
+  for B in 256 1; do
+    WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_prof.so run timeout -k 10 150 \
+      python3 tools/k3_stages.py 1920 1080 $B 4 > $O/stages_$B.log 2>&1 || exit 1
+  done
+fi
+cd /tmp && export TMPDIR=/tmp
+if has prof; then
+  run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run \
+    -- $BENCH --steps 2 --warmup 1 > $O/prof.log 2>&1 || exit 1
+fi
+if has pmc; then
+  for C in FETCH_SIZE WRITE_SIZE; do
+    run timeout -s KILL 200 rocprofv3 --pmc $C --output-format csv -d $O/pmc_$C -o run \
+      -- $BENCH --steps 1 --warmup 0 > $O/pmc_$C.log 2>&1 || exit 1
+  done
+fi
+if has sq; then
+  run timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+    SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU --output-format csv -d $O/sq1 -o run \
+    -- $BENCH --steps 1 --warmup 0 > $O/sq1.log 2>&1 || exit 1
+  run timeout -s KILL 200 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS \
+    SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_WAVES --output-format csv -d $O/sq2 -o run \
+    -- $BENCH --steps 1 --warmup 0 > $O/sq2.log 2>&1 || exit 1
+fi
+if has calib; then
+  for C in FETCH_SIZE WRITE_SIZE; do
+    run timeout -s KILL 60 rocprofv3 --pmc $C --output-format csv -d $O/calib_$C -o run \
+      -- $R/tools/bin/pmc_calib > $O/calib_$C.log 2>&1 || exit 1
+  done
+fi
+echo "session $TAG done" >> $O/steps.log

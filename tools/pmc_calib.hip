@@ -1,0 +1,52 @@
+// Calibration of rocprofv3 FETCH_SIZE / WRITE_SIZE on gfx950 for the access
+// widths the encoder's kernels use (MI355X_MICROARCH.md, HBM section: only
+// 16 B/lane streaming reads are calibrated there). Each kernel streams
+// exactly BYTES bytes once with one access width; the PMC pass reports what
+// the counters see. Build: hipcc --offload-arch=gfx950 -O3 -o tools/bin/pmc_calib tools/pmc_calib.hip
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#define BYTES (1ull << 30)
+
+template <typename T>
+__global__ void k_calib_read(const T* __restrict__ p, size_t n, uint32_t* out) {
+  uint32_t acc = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const T v = p[i];
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
+    for (size_t k = 0; k < (sizeof(T) + 3) / 4; ++k)
+      acc ^= sizeof(T) >= 4 ? w[k] : (uint32_t)*reinterpret_cast<const uint16_t*>(&v);
+  }
+  if (acc == 0x9e3779b9u) out[0] = acc;   // never true for a zeroed buffer
+}
+
+template <typename T>
+__global__ void k_calib_write(T* __restrict__ p, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    T v;
+    memset(&v, (int)(i & 0x7f), sizeof(T));
+    p[i] = v;
+  }
+}
+
+int main() {
+  void* buf;
+  uint32_t* out;
+  if (hipMalloc(&buf, BYTES) != hipSuccess || hipMalloc((void**)&out, 4) != hipSuccess) return 1;
+  hipMemset(buf, 0, BYTES);
+  const dim3 g(4096), b(256);
+  hipLaunchKernelGGL(k_calib_read<uint16_t>, g, b, 0, 0, (const uint16_t*)buf, BYTES / 2, out);
+  hipLaunchKernelGGL(k_calib_read<uint32_t>, g, b, 0, 0, (const uint32_t*)buf, BYTES / 4, out);
+  hipLaunchKernelGGL(k_calib_read<uint4>, g, b, 0, 0, (const uint4*)buf, BYTES / 16, out);
+  hipLaunchKernelGGL(k_calib_write<uint16_t>, g, b, 0, 0, (uint16_t*)buf, BYTES / 2);
+  hipLaunchKernelGGL(k_calib_write<uint32_t>, g, b, 0, 0, (uint32_t*)buf, BYTES / 4);
+  hipLaunchKernelGGL(k_calib_write<uint4>, g, b, 0, 0, (uint4*)buf, BYTES / 16);
+  if (hipDeviceSynchronize() != hipSuccess) return 2;
+  printf("pmc_calib: 6 kernels x %llu bytes\n", BYTES);
+  hipFree(buf);
+  hipFree(out);
+  return 0;
+}

@@ -51,6 +51,8 @@ struct alignas(16) K3G {
   int32_t abort;                   // a cross-worker wait timed out (bug guard)
 };
 
+static_assert(offsetof(K3G, coeffs) % 4 == 0, "K3X moves the probabilities as words");
+
 // LDS private to one worker (4 wavefronts) and the MB it is encoding.
 struct K3S {
   uint8_t yin[16 * BPS];
@@ -942,10 +944,11 @@ __device__ __forceinline__ void refresh_hc(K3G& G, int tid) {
 // moves the row's tokens from per-MB slots to the compact stream.
 
 // VP8CalculateLevelCosts (cost_enc.c:42-90) over one worker, no barrier
-__device__ void level_costs_w(K3G& G, int tid) {
+// from the probabilities src (G.coeffs, or the K3X copy of the last dirty epoch's)
+__device__ void level_costs_w(K3G& G, const uint8_t* src, int tid) {
   for (int k = tid; k < 96 * (MAX_VLEVEL + 1); k += K3T) {
     const int tbc = k / (MAX_VLEVEL + 1), v = k % (MAX_VLEVEL + 1);
-    const uint8_t* p = G.coeffs + tbc * 11;
+    const uint8_t* p = src + tbc * 11;
     const int ctx = tbc % 3;
     const int c0 = ctx > 0 ? bit_cost(G.ecost, 1, p[0]) : 0;
     int cost;
@@ -969,14 +972,17 @@ __device__ __forceinline__ int tok_stat_slot(uint32_t t) {
   return (id % 11 == 10) ? id - 1 : id;
 }
 
-#define K3_SPIN_LIMIT (1 << 24)
+// a cross-worker wait that has not been satisfied after this long (100 MHz
+// s_memrealtime ticks, 30 s) is a bug: the frame is aborted with an error
+// instead of hanging the GPU
+#define K3_WAIT_TICKS (30ull * 100000000ull)
 
-// worker-uniform wait until *p >= v (another worker publishes *p)
+// worker-uniform wait until *p >= v (another worker of this workgroup publishes *p)
 __device__ bool wait_ge(K3G& G, K3S& L, const int32_t* p, int32_t v) {
-  int spins = 0;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) {
     if (__hip_atomic_load(&G.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
-        ++spins > K3_SPIN_LIMIT) {
+        __builtin_amdgcn_s_memrealtime() - t0 > K3_WAIT_TICKS) {
       L.myabort = 1;
       G.abort = 1;
       break;
@@ -985,6 +991,91 @@ __device__ bool wait_ge(K3G& G, K3S& L, const int32_t* p, int32_t v) {
   }
   wbar(L);
   return L.myabort == 0;
+}
+
+// ---------------------------------------------------------------------------
+// K3X: one frame over several workgroups. Everything handed from one
+// workgroup to another goes through the frame's xsync block in HBM with
+// write-through (sc1) stores and L1-bypassing (sc1) loads, drained by the
+// storing wave before the flag that publishes it (the hand-off form of the
+// microarchitecture guide's inter-workgroup visibility table, row 1):
+//   rowdone[y]  MB columns of row y finished; rec[y][x] its boundary record
+//               (bottom Y row, bottom U|V rows, nz word, I4 modes, DC errors)
+//   fold_ptr    raster MBs whose statistics are folded; stats/ntok with it
+//   epoch       cost-table epochs published; coeffs (current probabilities)
+//               and lcoeffs/lcver (those of the last level-cost recompute)
+struct XHdr {
+  int32_t fold_ptr, epoch, abort, lcver;
+  uint32_t ntok;
+  int32_t tok_err, pad[2];
+  unsigned long long size_p0, sse[3], dist;
+  int32_t nb[3], max_edge[4], pad2;
+};
+#define XS_HDR 128
+#define XS_STATS XS_HDR
+#define XS_COEFFS (XS_STATS + 4 * NSLOT)
+#define XS_LCOEFFS (XS_COEFFS + NSLOT)
+#define XS_ROWDONE (XS_LCOEFFS + NSLOT)
+#define XS_REC_WORDS 12
+static_assert(sizeof(XHdr) <= XS_HDR, "xsync header");
+static_assert(NSLOT % 4 == 0, "probabilities move as words");
+
+__host__ __device__ inline size_t xs_rec_off(int mbh) {
+  return ((size_t)XS_ROWDONE + 4 * (size_t)mbh + 15) & ~(size_t)15;
+}
+extern "C" size_t vp8g_xsync_bytes(int w, int h) {
+  const int mbw = (w + 15) >> 4, mbh = (h + 15) >> 4;
+  return (xs_rec_off(mbh) + 4 * XS_REC_WORDS * (size_t)mbw * mbh + 255) & ~(size_t)255;
+}
+
+// LDS of one K3X workgroup beyond the K3 layout: the boundary of the row
+// above its worker 0 (pulled from rec[]) and its level-cost bookkeeping
+struct K3XL {
+  uint8_t lcoeffs[NSLOT];
+  int32_t lcver;    // lcver of the level costs in G.lcost
+  int32_t claim;    // highest epoch some worker of this workgroup refreshes to
+};
+
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int32_t ld_sc1(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(int32_t* p, int32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// worker-uniform wait until the xsync word *p >= v; every wave polls it
+// itself, so each wave's later sc1 loads follow its own matching poll
+__device__ bool wait_gx(K3G& G, K3S& L, const int32_t* p, int32_t v, XHdr* XH) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (ld_sc1(p) < v) {
+    if (__hip_atomic_load(&G.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
+        ld_sc1(&XH->abort) || __builtin_amdgcn_s_memrealtime() - t0 > K3_WAIT_TICKS) {
+      L.myabort = 1;
+      G.abort = 1;
+      st_sc1(&XH->abort, 1);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+  wbar(L);
+  return L.myabort == 0;
+}
+
+// probabilities between LDS and xsync, as words
+__device__ __forceinline__ void probas_to_x(const uint8_t* src, uint8_t* xdst, int tid) {
+  for (int k = tid; k < NSLOT / 4; k += K3T)
+    st_sc1(reinterpret_cast<uint32_t*>(xdst) + k, reinterpret_cast<const uint32_t*>(src)[k]);
+}
+__device__ __forceinline__ void probas_from_x(uint8_t* dst, const uint8_t* xsrc, int tid) {
+  for (int k = tid; k < NSLOT / 4; k += K3T)
+    reinterpret_cast<uint32_t*>(dst)[k] = ld_sc1(reinterpret_cast<const uint32_t*>(xsrc) + k);
 }
 
 __device__ __forceinline__ void publish(int32_t* p, int32_t v) {
@@ -1078,6 +1169,33 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
   }
 }
 
+// fold_mbs for the worker's own workgroup (X = false) or, in K3X, with the
+// frame's statistics and stream length taken from xsync before and handed
+// back after, then the fold pointer published (folds are serialised in
+// raster order by fold_ptr, so one worker of the frame folds at a time)
+template <bool X>
+__device__ void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t row0,
+                          uint16_t* tok_base, uint32_t* mboff, uint8_t* xs) {
+  if constexpr (X) {
+    XHdr* XH = reinterpret_cast<XHdr*>(xs);
+    uint32_t* xstats = reinterpret_cast<uint32_t*>(xs + XS_STATS);
+    if (i0 != 0) {   // before the frame's first fold the workgroup's LDS holds the start state
+      for (int s = tid; s < NSLOT; s += K3T) G.stats[s] = ld_sc1(xstats + s);
+      if (tid == 0) G.ntok = ld_sc1(&XH->ntok);
+      wbar(L);
+    }
+    fold_mbs(G, L, tid, i0, i1, row0, tok_base, mboff);
+    wbar(L);
+    for (int s = tid; s < NSLOT; s += K3T) st_sc1(xstats + s, G.stats[s]);
+    if (tid == 0) st_sc1(&XH->ntok, G.ntok);
+    vm_drain();
+    wbar(L);
+    if (tid == 0) st_sc1(&XH->fold_ptr, (int32_t)i1);
+  } else {
+    fold_mbs(G, L, tid, i0, i1, row0, tok_base, mboff);
+  }
+}
+
 // Frame end: move every MB's tokens from its VP8G_MAX_TOKENS_PER_MB slot to
 // its offset in the compact stream (mboff, raster order), with the whole
 // workgroup. A destination never lies above its own source, but it may
@@ -1151,12 +1269,17 @@ struct K3Args {
   uint32_t* mboff;   // n x nmb: compact-stream offset of each MB's tokens
   vp8g_frame_result* results;
   uint8_t* rerun;   // n x VP8G_RERUN_STATE_BYTES
+  uint8_t* xs;      // K3X: n x xs_fb bytes of cross-workgroup frame state
+  size_t xs_fb;
+  int nwg;          // K3X: workgroups per frame
 };
 
 // TR: the method >= 5 instantiation carries the trellis paths; m3/m4 frames
 // run a kernel without them (smaller register footprint).
 // AF: also store each MB's reconstruction for the autofilter
-template <int NW, bool TR, bool AF = false>
+// X: K3X, the frame's rows are dealt to a.nwg workgroups (blocks of NW rows
+// round-robin); k_encode_xtail finishes the frame
+template <int NW, bool TR, bool AF = false, bool X = false>
 __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   extern __shared__ __align__(16) uint8_t smem[];
   const int mbw = a.mbw, mbh = a.mbh, nmb = mbw * mbh;
@@ -1173,8 +1296,25 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   int32_t* rowdone = reinterpret_cast<int32_t*>(topderr + 4 * mbw);   // mbh
   uint32_t (*tnall)[32] = reinterpret_cast<uint32_t (*)[32]>(rowdone + mbh);   // NW*64 (trellis)
   uint32_t (*tn)[32] = tnall + 64 * wk;
+  // K3X: the row above worker 0 comes from another workgroup, pulled into
+  // these copies of the boundary arrays (same layout); every worker still
+  // writes its own row's boundary into the shared arrays
+  uint8_t* xbase = reinterpret_cast<uint8_t*>(tnall) + (TR ? (size_t)NW * 64 * 32 * 4 : 0);
+  K3XL& XL = *reinterpret_cast<K3XL*>(xbase);
+  uint8_t* xytop = xbase + ((sizeof(K3XL) + 15) & ~(size_t)15);
+  uint8_t* xuvtop = xytop + 16 * mbw + 16;
+  uint32_t* xnzw = reinterpret_cast<uint32_t*>(xuvtop + 16 * mbw);
+  uint8_t* xpredtop = reinterpret_cast<uint8_t*>(xnzw + mbw);
+  int8_t* xtopderr = reinterpret_cast<int8_t*>(xpredtop + 4 * mbw);
+  const bool xr = X && wk == 0;   // this worker reads the x copies
 
-  const int f = blockIdx.x;
+  const int nwg = X ? a.nwg : 1;
+  const int f = X ? (int)blockIdx.x / nwg : (int)blockIdx.x;
+  const int blk = X ? (int)blockIdx.x % nwg : 0;
+  uint8_t* xs = X ? a.xs + (size_t)f * a.xs_fb : nullptr;
+  XHdr* XH = reinterpret_cast<XHdr*>(xs);
+  int32_t* xrowdone = reinterpret_cast<int32_t*>(xs + XS_ROWDONE);
+  uint32_t* xrec = reinterpret_cast<uint32_t*>(xs + xs_rec_off(mbh));
   const int gt = threadIdx.x;
   // thread id rotated by one wave per worker: stages that leave a wave idle
   // (intra4's 160 lanes, the token tail, wave-0 bookkeeping) put the idle wave
@@ -1220,6 +1360,13 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   for (int k = gt - 1; k < mbw; k += NW * K3T) nzw[k] = 0;
   for (int k = gt; k < 4 * mbw; k += NW * K3T) { predtop[k] = 0; topderr[k] = 0; }
   for (int k = gt; k < mbh; k += NW * K3T) rowdone[k] = 0;
+  if constexpr (X) {
+    for (int k = gt; k < 16 * mbw + 16; k += NW * K3T) xytop[k] = 127;
+    for (int k = gt; k < 16 * mbw; k += NW * K3T) xuvtop[k] = 127;
+    for (int k = gt; k < mbw; k += NW * K3T) xnzw[k] = 0;
+    for (int k = gt; k < 4 * mbw; k += NW * K3T) { xpredtop[k] = 0; xtopderr[k] = 0; }
+    if (gt == 0) { XL.lcver = 0; XL.claim = 0; }
+  }
   if (gt < 4) G.max_edge[gt] = 0;
   if (gt == 0) {
     G.fs.size_p0 = 0; G.fs.sse[0] = G.fs.sse[1] = G.fs.sse[2] = 0; G.fs.dist = 0;
@@ -1228,12 +1375,12 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   }
   if (tid == 0) { L.bar = 0; L.myabort = 0; }
   __syncthreads();
-  if (wk == 0) level_costs_w(G, tid);
+  if (wk == 0) level_costs_w(G, G.coeffs, tid);
   __syncthreads();
   if (rerun) {   // the level costs came from rstate[0..]; the probabilities are the loop-end ones
     for (int s = gt; s < NSLOT; s += NW * K3T) G.coeffs[s] = rstate[NSLOT + s];
     __syncthreads();
-  } else {       // first pass: the level costs are those of the default probabilities
+  } else if (blk == 0) {   // first pass: the level costs are those of the default probabilities
     for (int s = gt; s < NSLOT; s += NW * K3T) rstate[s] = G.coeffs[s];
   }
   if (wk == 0) refresh_hc(G, tid);
@@ -1258,7 +1405,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   uint8_t* ul = L.ul_mem + 1;
   uint8_t* vl = L.vl_mem + 1;
 
-  for (int y = wk; y < mbh && !L.myabort; y += NW) {
+  for (int y = blk * NW + wk; y < mbh && !L.myabort; y += NW * nwg) {
     // InitLeft (iterator_enc.c:22-32)
     if (tid < 16) yl[tid] = 129;
     if (tid < 8) { ul[tid] = 129; vl[tid] = 129; }
@@ -1285,24 +1432,98 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
         if (refresher) {
           // everything before this MB: rows above folded by their owners,
           // this row's earlier MBs folded here
-          if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from)) break;
-          fold_mbs(G, L, tid, fold_from, mb, (uint32_t)y * mbw, tok_base, mboff);
+          if constexpr (X) {
+            if (tid == 0) atomicMax(&XL.claim, ep);
+            if (!wait_gx(G, L, &XH->fold_ptr, (int32_t)fold_from, XH)) break;
+          } else {
+            if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from)) break;
+          }
+          fold_rows<X>(G, L, tid, fold_from, mb, (uint32_t)y * mbw, tok_base, mboff, xs);
           fold_from = mb;
           wbar(L);
           const int dirty = finalize_probas_wg(G, L, tid);
-          if (dirty) {
-            level_costs_w(G, tid);
-            for (int s = tid; s < NSLOT; s += K3T) rstate[s] = G.coeffs[s];
+          if constexpr (X) {
+            // level costs: recomputed when dirty, else those of the frame's
+            // last dirty epoch (this workgroup may have skipped that epoch)
+            if (dirty) {
+              level_costs_w(G, G.coeffs, tid);
+              probas_to_x(G.coeffs, xs + XS_LCOEFFS, tid);
+              if (tid == 0) XL.lcver = ep;
+            } else {
+              const int32_t lv = ld_sc1(&XH->lcver);
+              if (lv != XL.lcver) {
+                probas_from_x(XL.lcoeffs, xs + XS_LCOEFFS, tid);
+                wbar(L);
+                level_costs_w(G, XL.lcoeffs, tid);
+                if (tid == 0) XL.lcver = lv;
+              }
+            }
+            probas_to_x(G.coeffs, xs + XS_COEFFS, tid);
+            vm_drain();
+          } else {
+            if (dirty) {
+              level_costs_w(G, G.coeffs, tid);
+              for (int s = tid; s < NSLOT; s += K3T) rstate[s] = G.coeffs[s];
+            }
           }
           refresh_hc(G, tid);
           wbar(L);
+          if constexpr (X) {
+            if (tid == 0) {
+              if (dirty) { st_sc1(&XH->lcver, ep); vm_drain(); }
+              st_sc1(&XH->epoch, ep);
+            }
+          }
           if (tid == 0) publish(&G.epoch, ep);
+        } else if (X) {
+          // the frame's refresher published epoch ep; the first worker of this
+          // workgroup to need it copies the probabilities (and, if they
+          // changed, recomputes the level costs) for the whole workgroup
+          if (!wait_gx(G, L, &XH->epoch, ep, XH)) break;
+          if (tid == 0) L.redw[0] = atomicMax(&XL.claim, ep) < ep;
+          wbar(L);
+          const int mine = L.redw[0];
+          wbar(L);
+          if (mine) {
+            const int32_t lv = ld_sc1(&XH->lcver);
+            if (lv != XL.lcver) {
+              probas_from_x(XL.lcoeffs, xs + XS_LCOEFFS, tid);
+              wbar(L);
+              level_costs_w(G, XL.lcoeffs, tid);
+              if (tid == 0) XL.lcver = lv;
+            }
+            probas_from_x(G.coeffs, xs + XS_COEFFS, tid);
+            wbar(L);
+            refresh_hc(G, tid);
+            wbar(L);
+            if (tid == 0) publish(&G.epoch, ep);
+          } else {
+            if (!wait_ge(G, L, &G.epoch, ep)) break;
+          }
         } else {
           if (!wait_ge(G, L, &G.epoch, ep)) break;
         }
       }
       // ---- wavefront dependency: MB x+1 of the row above (top-right) is done
-      if (y > 0 && !wait_ge(G, L, &rowdone[y - 1], min(x + 2, mbw))) break;
+      if (xr) {
+        if (y > 0) {
+          if (!wait_gx(G, L, &xrowdone[y - 1], min(x + 2, mbw), XH)) break;
+          // pull the boundary records of columns x, x + 1 (x = 0) or x + 1
+          const int c0 = x == 0 ? 0 : x + 1;
+          const int nc = x == 0 ? min(2, mbw) : (x + 1 < mbw ? 1 : 0);
+          if (tid < XS_REC_WORDS * nc) {
+            const int c = c0 + tid / XS_REC_WORDS, k = tid % XS_REC_WORDS;
+            const uint32_t v = ld_sc1(xrec + ((size_t)(y - 1) * mbw + c) * XS_REC_WORDS + k);
+            if (k < 4) reinterpret_cast<uint32_t*>(xytop + 16 * c)[k] = v;
+            else if (k < 8) reinterpret_cast<uint32_t*>(xuvtop + 16 * c)[k - 4] = v;
+            else if (k == 8) xnzw[c] = v;
+            else if (k == 9) reinterpret_cast<uint32_t*>(xpredtop + 4 * c)[0] = v;
+            else if (k == 10) reinterpret_cast<uint32_t*>(xtopderr + 4 * c)[0] = v;
+          }
+        }
+      } else if (y > 0 && !wait_ge(G, L, &rowdone[y - 1], min(x + 2, mbw))) {
+        break;
+      }
       K3_STAMP(0);
 
       load_mb(Yp, Up, Vp, w, h, x, y, L.yin, tid, K3T);
@@ -1310,10 +1531,12 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
       const int segid = segmap[mb];
       const vp8g_seg& S = G.seg[segid];
       const bool hl = x > 0, ht = y > 0;
-      const uint8_t* yt = ytop + 16 * x;
-      const uint8_t* uvt = uvtop + 16 * x;
+      const uint8_t* yt = (xr ? xytop : ytop) + 16 * x;
+      const uint8_t* uvt = (xr ? xuvtop : uvtop) + 16 * x;
+      const uint8_t* predrd = xr ? xpredtop : predtop;   // the row above's I4 modes
+      const int8_t* derrrd = xr ? xtopderr : topderr;     // and its DC errors
       MBCtx ctx;
-      nz_flags(nzw[x], nzw[x - 1], left_dc, ctx);
+      nz_flags(xr ? xnzw[x] : nzw[x], nzw[x - 1], left_dc, ctx);
 
       // ---- predictions (quant_enc.c:469-479)
       {
@@ -1392,12 +1615,12 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
       if (max_i4_bits > 0) {
         I4Result r4;
         if constexpr (TR) {
-          r4 = trellis_all ? run_i4<true>(G, L, tn, S, ctx, rtid, x, mbw, predtop, yl, yt, true,
+          r4 = trellis_all ? run_i4<true>(G, L, tn, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
                                           rd_score, max_i4_bits, substamps)
-                           : run_i4<false>(G, L, tn, S, ctx, rtid, x, mbw, predtop, yl, yt, true,
+                           : run_i4<false>(G, L, tn, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
                                            rd_score, max_i4_bits, substamps);
         } else {
-          r4 = run_i4<false>(G, L, tn, S, ctx, rtid, x, mbw, predtop, yl, yt, true, rd_score,
+          r4 = run_i4<false>(G, L, tn, S, ctx, rtid, x, mbw, predrd, yl, yt, true, rd_score,
                              max_i4_bits, substamps);
         }
         if (r4.ok) {
@@ -1418,7 +1641,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
       // ---- UV (quant_enc.c:1169-1217)
       int bu = 0;
       {
-        eval_uv(G, L, S, ctx, tid, x, topderr, use_derr);
+        eval_uv(G, L, S, ctx, tid, x, derrrd, use_derr);
         score_t bsc = 0, bH = 0;
         for (int mm = 0; mm < 4; ++mm) {
           const score_t Dm = L.mres[mm][0], Hm = kVP8ModeCostUV[mm];
@@ -1460,7 +1683,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
           if (tid < 16) L.fin_dc[tid] = L.lvdc[best16][tid];
           nzq = (uint32_t)L.mres[best16][3];
         } else {
-          I4Result r4 = run_i4<true>(G, L, tn, S, ctx, rtid, x, mbw, predtop, yl, yt, false, 0, 0,
+          I4Result r4 = run_i4<true>(G, L, tn, S, ctx, rtid, x, mbw, predrd, yl, yt, false, 0, 0,
                                      substamps);
           L.yout[(tid >> 4) * BPS + (tid & 15)] = L.acc_out[tid];
           (&L.fin_ac[0][0])[tid] = (&L.acc_ac[0][0])[tid];
@@ -1649,19 +1872,54 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
       }
       wbar(L);
       if (tid == 0) publish(&rowdone[y], x + 1);
+      if constexpr (X) {
+        // the last worker's row feeds worker 0 of the next workgroup: its
+        // boundary record for column x, drained, then the column count
+        if (wk == NW - 1 && y < mbh - 1 && tid < 64) {
+          if (tid < 11) {
+            uint32_t v;
+            if (tid < 4) v = reinterpret_cast<const uint32_t*>(ytop + 16 * x)[tid];
+            else if (tid < 8) v = reinterpret_cast<const uint32_t*>(uvtop + 16 * x)[tid - 4];
+            else if (tid == 8) v = nzw[x];
+            else if (tid == 9) v = reinterpret_cast<const uint32_t*>(predtop + 4 * x)[0];
+            else v = reinterpret_cast<const uint32_t*>(topderr + 4 * x)[0];
+            st_sc1(xrec + ((size_t)y * mbw + x) * XS_REC_WORDS + tid, v);
+          }
+          vm_drain();
+          if (tid == 0) st_sc1(&xrowdone[y], x + 1);
+        }
+      }
       K3_STAMP(6);
     }
     if (L.myabort) break;
     // row end: fold this row's remaining MBs once the rows above are folded
-    if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from)) break;
-    fold_mbs(G, L, tid, fold_from, (uint32_t)(y + 1) * mbw, (uint32_t)y * mbw, tok_base,
-             mboff);
+    if constexpr (X) {
+      if (!wait_gx(G, L, &XH->fold_ptr, (int32_t)fold_from, XH)) break;
+    } else {
+      if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from)) break;
+    }
+    fold_rows<X>(G, L, tid, fold_from, (uint32_t)(y + 1) * mbw, (uint32_t)y * mbw, tok_base,
+                 mboff, xs);
     wbar(L);
     K3_STAMP(7);
   }
 
   // ---- frame epilogue: final probabilities and side results
   __syncthreads();
+  if constexpr (X) {   // this workgroup's share of the side statistics; k_encode_xtail finishes
+    if (gt == 0) {
+      atomicAdd(&XH->size_p0, G.fs.size_p0);
+      for (int c = 0; c < 3; ++c) {
+        atomicAdd(&XH->sse[c], G.fs.sse[c]);
+        atomicAdd(&XH->nb[c], G.fs.nb[c]);
+      }
+      atomicAdd(&XH->dist, G.fs.dist);
+      for (int c = 0; c < 4; ++c) atomicMax(&XH->max_edge[c], G.max_edge[c]);
+      if (G.tok_err) atomicOr(&XH->tok_err, G.tok_err);
+      if (G.abort) atomicOr(&XH->abort, 1);
+    }
+    return;
+  }
   if (!G.abort && !G.tok_err) compact_tokens(G, tok_base, mboff, nmb);
   __syncthreads();
   if (wk == 0) {
@@ -1694,6 +1952,65 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   }
 }
 
+
+// K3X frame end, one 256-thread workgroup per frame after k_encode<.., X>:
+// the compact token stream, the state a later pass starts from, the final
+// probabilities and the side results, all from the frame's xsync block (the
+// k_encode epilogue, with the workgroups' shares merged)
+__global__ __launch_bounds__(K3T) void k_encode_xtail(K3Args a) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  K3G& G = *reinterpret_cast<K3G*>(smem);
+  K3S& L = *reinterpret_cast<K3S*>(smem + sizeof(K3G));
+  const int f = blockIdx.x, tid = threadIdx.x, nmb = a.mbw * a.mbh;
+  const vp8g_frame_params* P = a.params + f;
+  if (P->pass_mode == 2) return;
+  const bool rerun = P->pass_mode == 1 || P->pass_mode == 3;
+  uint8_t* rstate = a.rerun + (size_t)f * VP8G_RERUN_STATE_BYTES;
+  uint32_t* rstats = reinterpret_cast<uint32_t*>(rstate + VP8G_STATE_STATS);
+  const uint8_t* xs = a.xs + (size_t)f * a.xs_fb;
+  const XHdr* XH = reinterpret_cast<const XHdr*>(xs);
+  const uint32_t* xstats = reinterpret_cast<const uint32_t*>(xs + XS_STATS);
+  uint16_t* tok_base = a.tokens + f * a.tok_cap;
+  const uint32_t* mboff = a.mboff + (size_t)f * nmb;
+  const int32_t ep = XH->epoch, lcver = XH->lcver;
+  for (int s = tid; s < NSLOT; s += K3T) {
+    G.stats[s] = xstats[s];
+    // the loop-end probabilities: the last epoch's, else the start state's
+    G.coeffs[s] = ep > 0 ? xs[XS_COEFFS + s]
+                         : (rerun ? rstate[NSLOT + s] : (&kVP8CoeffProba0[0][0][0][0])[s]);
+  }
+  for (int k = tid; k < 256; k += K3T) G.ecost[k] = kVP8EntropyCost[k];
+  if (tid == 0) {
+    L.bar = 0; L.myabort = 0;
+    G.ntok = XH->ntok;
+    G.mark[0] = 0;
+  }
+  __syncthreads();
+  const int err = XH->abort ? 2 : XH->tok_err;
+  if (!err) compact_tokens(G, tok_base, mboff, nmb);
+  __syncthreads();
+  for (int s = tid; s < NSLOT; s += K3T) {
+    if (lcver > 0) rstate[s] = xs[XS_LCOEFFS + s];   // the level costs' probabilities
+    rstate[NSLOT + s] = G.coeffs[s];
+    rstats[s] = G.stats[s];
+  }
+  finalize_probas_wg(G, L, tid);
+  vp8g_frame_result* R = a.results + f;
+  for (int s = tid; s < NSLOT; s += K3T) R->probas[s] = G.coeffs[s];
+  if (tid == 0) {
+    R->ntokens = G.ntok;
+    R->error = err;
+    for (int s = 0; s < 4; ++s) R->max_edge[s] = XH->max_edge[s];
+    R->size_p0 = XH->size_p0;
+    R->sse[0] = XH->sse[0]; R->sse[1] = XH->sse[1]; R->sse[2] = XH->sse[2];
+    R->distortion = XH->dist;
+    R->use_skip = 0;
+    R->skip_proba = 255;
+    R->block_count[0] = XH->nb[0]; R->block_count[1] = XH->nb[1];
+    R->block_count[2] = XH->nb[2];
+    for (int i = 0; i < 8; ++i) R->stamps[i] = 0;
+  }
+}
 // ---------------------------------------------------------------------------
 
 template <int NW>
@@ -1719,7 +2036,7 @@ static int launch_k3_t(const K3Args& a, int n, bool trellis, void* stream) {
     static size_t attr_bytes = 0;
     if (lds > attr_bytes) {
       const hipError_t e = hipFuncSetAttribute(
-          (const void*)k_encode<NW, TR>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+          (const void*)k_encode<NW, TR, AF>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) {
         vp8g_set_error("k_encode dynamic LDS opt-in", hipGetErrorString(e));
         return 0;
@@ -1738,6 +2055,65 @@ static int launch_k3(const K3Args& a, int n, bool trellis, void* stream) {
                  : launch_k3_t<NW, false>(a, n, false, stream);
 }
 
+// K3X: grid n * nwg main workgroups, then the per-frame tail
+static size_t k3x_lds_extra(int mbw) {
+  return ((sizeof(K3XL) + 15) & ~(size_t)15) + 44 * (size_t)mbw + 32;
+}
+
+template <int NW, bool TR>
+static int launch_k3x(K3Args a, int n, int nwg, void* stream) {
+  const size_t lds = k3_lds_bytes<NW>(a.mbw, a.mbh, TR) + k3x_lds_extra(a.mbw);
+  const size_t lds_tail = sizeof(K3G) + sizeof(K3S);
+  if (lds > 160 * 1024) {
+    vp8g_set_error("k_encode (K3X)", "frame too wide for the LDS budget");
+    return 0;
+  }
+  static size_t attr_bytes = 0, attr_tail = 0;
+  if (lds > 64 * 1024 && lds > attr_bytes) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_encode<NW, TR, false, true>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) {
+      vp8g_set_error("k_encode (K3X) dynamic LDS opt-in", hipGetErrorString(e));
+      return 0;
+    }
+    attr_bytes = lds;
+  }
+  if (lds_tail > 64 * 1024 && attr_tail == 0) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_encode_xtail,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds_tail);
+    if (e != hipSuccess) {
+      vp8g_set_error("k_encode_xtail dynamic LDS opt-in", hipGetErrorString(e));
+      return 0;
+    }
+    attr_tail = lds_tail;
+  }
+  a.nwg = nwg;
+  if (hipMemsetAsync(a.xs, 0, (size_t)n * a.xs_fb, (hipStream_t)stream) != hipSuccess) {
+    vp8g_set_error("k_encode (K3X)", "xsync reset failed");
+    return 0;
+  }
+  hipLaunchKernelGGL((k_encode<NW, TR, false, true>), dim3(n * nwg), dim3(NW * K3T), lds,
+                     (hipStream_t)stream, a);
+  if (!vp8g_launch_check("k_encode (K3X)")) return 0;
+  hipLaunchKernelGGL(k_encode_xtail, dim3(n), dim3(K3T), lds_tail, (hipStream_t)stream, a);
+  return vp8g_launch_check("k_encode_xtail");
+}
+
+// workgroups per frame for K3X: fill the 256 CUs with the frames' MB rows
+// (NW rows per workgroup); 1 = the one-workgroup kernel
+static int k3x_split(int n, int mbh, int nw) {
+  static int mode = -1;
+  if (mode < 0) {   // WEBP_AMD_K3X=0 turns the split off (A/B)
+    const char* v = getenv("WEBP_AMD_K3X");
+    mode = (v && v[0] == '0') ? 0 : 1;
+  }
+  if (!mode || n > VP8G_XSPLIT_MAX_FRAMES) return 1;
+  const int rows = (mbh + nw - 1) / nw;
+  const int nwg = min(256 / n, rows);
+  return nwg >= 2 ? nwg : 1;
+}
+
 // default: 3 MB workers for m3/m4 frames (4 spill registers to scratch and
 // are no faster: the CU's vector issue is already saturated), 2 when the
 // trellis paths (and their registers and LDS) are in the kernel
@@ -1753,7 +2129,8 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
                                   const uint8_t* segmap, const vp8g_frame_params* params,
                                   uint16_t* tokens, size_t tok_cap, uint8_t* mbinfo,
                                   uint32_t* mboff, int trellis, vp8g_frame_result* results,
-                                  uint8_t* rerun_state, uint8_t* recon, void* stream) {
+                                  uint8_t* rerun_state, uint8_t* recon, uint8_t* xsync,
+                                  void* stream) {
   static int variant = -1;
   if (variant < 0) {   // WEBP_AMD_K3: 1 = single-wavefront reference kernel, 2/3/5/4 =
                        // 1/2/3/4 MB workers per frame, unset = default above
@@ -1774,6 +2151,13 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   a.mbw = (w + 15) >> 4; a.mbh = (h + 15) >> 4;
   a.segmap = segmap; a.params = params; a.tokens = tokens; a.tok_cap = tok_cap;
   a.mbinfo = mbinfo; a.mboff = mboff; a.results = results; a.rerun = rerun_state;
+  a.xs = xsync; a.xs_fb = vp8g_xsync_bytes(w, h); a.nwg = 1;
+  if (xsync != nullptr && recon == nullptr && variant == 0) {
+    const int nwg = k3x_split(n, a.mbh, 2);
+    if (nwg > 1)
+      return trellis ? launch_k3x<2, true>(a, n, nwg, stream)
+                     : launch_k3x<2, false>(a, n, nwg, stream);
+  }
   if (variant == 2) return launch_k3<1>(a, n, trellis != 0, stream);
   if (variant == 3) return launch_k3<2>(a, n, trellis != 0, stream);
   if (variant == 4) return launch_k3<4>(a, n, trellis != 0, stream);

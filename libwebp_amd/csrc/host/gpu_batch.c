@@ -139,6 +139,8 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   CHK(hipMalloc((void**)&b->d_mbinfo, N * nmb * VP8G_MBINFO_BYTES));
   CHK(hipMalloc((void**)&b->d_mboff, N * nmb * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&b->d_rerun, N * VP8G_RERUN_STATE_BYTES));
+  if (N <= VP8G_XSPLIT_MAX_FRAMES)   /* few frames: K3 splits each over several CUs */
+    CHK(hipMalloc((void**)&b->d_xsync, N * vp8g_xsync_bytes(width, height)));
   CHK(hipMalloc((void**)&b->d_results, N * sizeof(vp8g_frame_result)));
   CHK(hipMalloc((void**)&b->d_psize, N * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&b->d_emeta, N * sizeof(vp8g_emit_meta)));
@@ -179,7 +181,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   if (b->stream) hipStreamSynchronize(b->stream);
   hipFree(b->d_g2l); hipFree(b->d_rgba); hipFree(b->d_yuv); hipFree(b->d_aflags); hipFree(b->d_alpha);
   hipFree(b->d_uva); hipFree(b->d_amode); hipFree(b->d_segmap); hipFree(b->d_params); hipFree(b->d_tokens);
-  hipFree(b->d_mbinfo); hipFree(b->d_mboff); hipFree(b->d_rerun); hipFree(b->d_results); hipFree(b->d_psize); hipFree(b->d_emeta);
+  hipFree(b->d_mbinfo); hipFree(b->d_mboff); hipFree(b->d_rerun); hipFree(b->d_xsync); hipFree(b->d_results); hipFree(b->d_psize); hipFree(b->d_emeta);
   hipFree(b->d_poff); hipFree(b->d_part);
   hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs); hipFree(b->d_nbuf);
   hipFree(b->d_eimg);
@@ -425,7 +427,7 @@ static int lowmem_passes(WebPGpuBatch* b, int n) {
     first = 0;
     if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params,
                             b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5,
-                            b->d_results, b->d_rerun, NULL, st))
+                            b->d_results, b->d_rerun, NULL, b->d_xsync, st))
       return 0;
     if (!vp8g_launch_lowmem(b->d_tokens, b->tok_cap, b->d_mboff, b->d_results, b->d_mbinfo,
                             (int)nmb, n, b->d_lmi, b->d_active, 0, b->d_lmstats, b->d_lmi + N, st))
@@ -483,7 +485,7 @@ static int lowmem_passes(WebPGpuBatch* b, int n) {
                      hipMemcpyHostToDevice, st));
   if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
                           b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5, b->d_results,
-                          b->d_rerun, b->cfg.autofilter ? b->d_recon : NULL, st))
+                          b->d_rerun, b->cfg.autofilter ? b->d_recon : NULL, b->d_xsync, st))
     return 0;
   CHK(hipEventRecord(b->ev[3], st));
   CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
@@ -577,7 +579,7 @@ static int run_passes(WebPGpuBatch* b, int n) {
     } else if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params,
                                    b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff,
                                    b->cfg.method >= 5, b->d_results, b->d_rerun,
-                                   af ? b->d_recon : NULL, st)) {
+                                   af ? b->d_recon : NULL, b->d_xsync, st)) {
       return 0;
     }
     CHK(hipEventRecord(b->ev[3], st));

@@ -39,6 +39,7 @@ struct WebPGpuBatch {
   uint8_t* d_mbinfo;
   uint32_t* d_mboff;         /* K3 scratch: compact-stream offset per MB */
   uint8_t* d_rerun;          /* K3 cost state carried from pass to pass */
+  uint8_t* d_xsync;          /* K3X cross-workgroup frame state (max_frames <= 64) */
   /* size search between passes (allocated on first use) */
   uint8_t* h_state;          /* pinned copy of d_rerun */
   uint8_t* d_active;         /* frames whose token bits are estimated */

@@ -140,7 +140,15 @@ int vp8g_launch_encode(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h,
                        const vp8g_frame_params* params, uint16_t* tokens,
                        size_t tok_cap, uint8_t* mbinfo, uint32_t* mboff, int trellis,
                        vp8g_frame_result* results, uint8_t* rerun_state, uint8_t* recon,
-                       void* stream);
+                       uint8_t* xsync, void* stream);
+
+/* K3X: when a launch has few frames (n <= VP8G_XSPLIT_MAX_FRAMES) and xsync
+ * is not NULL, each frame's MB rows are split over several workgroups (CUs)
+ * that hand the wavefront boundary, the statistics fold and the cost epochs
+ * to each other through xsync (n x vp8g_xsync_bytes(w, h), zeroed by the
+ * launch). */
+#define VP8G_XSPLIT_MAX_FRAMES 64
+size_t vp8g_xsync_bytes(int w, int h);
 
 /* Autofilter (config->autofilter, filter_enc.c:156-212): per frame the
  * segment filter levels and the filter header fields used for the search */

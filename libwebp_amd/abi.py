@@ -177,7 +177,10 @@ def encode_rgba(lib, rgba, quality=75.0, method=4, stats=False, use_argb=None, *
         if not lib.WebPPictureImportRGBA(C.byref(pic), rgba.ctypes.data, 4 * w):
             raise RuntimeError("import failed: %s" % ENC_ERRORS[pic.error_code])
         if not lib.WebPEncode(C.byref(cfg), C.byref(pic)):
-            raise RuntimeError("WebPEncode failed: %s" % ENC_ERRORS[pic.error_code])
+            why = ""
+            if hasattr(lib, "WebPGpuLastError"):   # libwebp_amd's engine diagnostics
+                why = " (%s)" % lib.WebPGpuLastError().decode(errors="replace")
+            raise RuntimeError("WebPEncode failed: %s%s" % (ENC_ERRORS[pic.error_code], why))
         data = C.string_at(wrt.mem, wrt.size)
     finally:
         lib.WebPPictureFree(C.byref(pic))

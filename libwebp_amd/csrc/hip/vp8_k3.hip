@@ -22,6 +22,8 @@
 
 #include <stdio.h>
 
+#include <atomic>
+
 #define K3T 256
 
 // LDS shared by all of a frame's workers: cost tables of the current epoch,
@@ -2055,6 +2057,10 @@ static int launch_k3(const K3Args& a, int n, bool trellis, void* stream) {
                  : launch_k3_t<NW, false>(a, n, false, stream);
 }
 
+static std::atomic<int> g_x_free{-1};   // K3X workgroup budget (k3x_take)
+
+static void k3x_release(void* p) { g_x_free.fetch_add((int)(intptr_t)p); }
+
 // K3X: grid n * nwg main workgroups, then the per-frame tail
 static size_t k3x_lds_extra(int mbw) {
   return ((sizeof(K3XL) + 15) & ~(size_t)15) + 44 * (size_t)mbw + 32;
@@ -2100,18 +2106,51 @@ static int launch_k3x(K3Args a, int n, int nwg, void* stream) {
   return vp8g_launch_check("k_encode_xtail");
 }
 
-// workgroups per frame for K3X: fill the 256 CUs with the frames' MB rows
-// (NW rows per workgroup); 1 = the one-workgroup kernel
-static int k3x_split(int n, int mbh, int nw) {
+template <int NW, bool TR>
+static int launch_k3x_budget(const K3Args& a, int n, int nwg, void* stream) {
+  const int ok = launch_k3x<NW, TR>(a, n, nwg, stream);
+  // give the workgroups back once the stream has passed the kernels (at once
+  // if they never got enqueued)
+  if (!ok || hipLaunchHostFunc((hipStream_t)stream, k3x_release,
+                               (void*)(intptr_t)(n * nwg)) != hipSuccess) {
+    if (ok) (void)hipStreamSynchronize((hipStream_t)stream);
+    k3x_release((void*)(intptr_t)(n * nwg));
+  }
+  return ok;
+}
+
+// K3X workgroups wait on each other, so every workgroup of a launch must be
+// resident at once. Launches from several engines (concurrent WebPEncode
+// callers on their own streams) share one process-wide budget of one
+// workgroup per CU: a launch takes what it uses before it is enqueued and a
+// host callback on its stream gives it back when its kernels have finished.
+
+// workgroups per frame for K3X: fill the free CUs with the frames' MB rows
+// (NW rows per workgroup), taken from the budget; 1 = the one-workgroup kernel
+static int k3x_take(int n, int mbh, int nw) {
   static int mode = -1;
   if (mode < 0) {   // WEBP_AMD_K3X=0 turns the split off (A/B)
     const char* v = getenv("WEBP_AMD_K3X");
     mode = (v && v[0] == '0') ? 0 : 1;
   }
   if (!mode || n > VP8G_XSPLIT_MAX_FRAMES) return 1;
+  int cur = g_x_free.load();
+  if (cur < 0) {   // first use: one workgroup per CU of the device
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    int expect = -1;
+    g_x_free.compare_exchange_strong(expect, cus);
+    cur = g_x_free.load();
+  }
   const int rows = (mbh + nw - 1) / nw;
-  const int nwg = min(256 / n, rows);
-  return nwg >= 2 ? nwg : 1;
+  for (;;) {
+    const int nwg = min(cur / n, rows);
+    if (nwg < 2) return 1;
+    if (g_x_free.compare_exchange_weak(cur, cur - n * nwg)) return nwg;
+  }
 }
 
 // default: 3 MB workers for m3/m4 frames (4 spill registers to scratch and
@@ -2153,10 +2192,10 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   a.mbinfo = mbinfo; a.mboff = mboff; a.results = results; a.rerun = rerun_state;
   a.xs = xsync; a.xs_fb = vp8g_xsync_bytes(w, h); a.nwg = 1;
   if (xsync != nullptr && recon == nullptr && variant == 0) {
-    const int nwg = k3x_split(n, a.mbh, 2);
+    const int nwg = k3x_take(n, a.mbh, 2);
     if (nwg > 1)
-      return trellis ? launch_k3x<2, true>(a, n, nwg, stream)
-                     : launch_k3x<2, false>(a, n, nwg, stream);
+      return trellis ? launch_k3x_budget<2, true>(a, n, nwg, stream)
+                     : launch_k3x_budget<2, false>(a, n, nwg, stream);
   }
   if (variant == 2) return launch_k3<1>(a, n, trellis != 0, stream);
   if (variant == 3) return launch_k3<2>(a, n, trellis != 0, stream);

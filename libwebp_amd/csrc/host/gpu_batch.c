@@ -586,11 +586,13 @@ static int run_passes(WebPGpuBatch* b, int n) {
     CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
                        hipMemcpyDeviceToHost, st));
     if (nsize) {
-      if (!b->h_state) {
+      /* each buffer on its own first use: low_memory passes allocate h_state too */
+      if (!b->h_state)
         CHK(hipHostMalloc((void**)&b->h_state, (size_t)b->max_frames * VP8G_RERUN_STATE_BYTES, 0));
+      if (!b->h_tbits)
         CHK(hipHostMalloc((void**)&b->h_tbits, b->max_frames * sizeof(unsigned long long), 0));
+      if (!b->d_tbits)
         CHK(hipMalloc((void**)&b->d_tbits, b->max_frames * sizeof(unsigned long long)));
-      }
       if (!b->h_active) {
         CHK(hipHostMalloc((void**)&b->h_active, b->max_frames, 0));
         CHK(hipMalloc((void**)&b->d_active, b->max_frames));

@@ -245,38 +245,95 @@ int WebPMemoryWrite(const uint8_t* data, size_t n, const WebPPicture* pic) {
   return 1;
 }
 
-/* ---- single-picture GPU engine (one cached instance per process) ---- */
+/* ---- single-picture GPU engines: a process-wide pool ----
+ * The reference is re-entrant for distinct pictures (all state lives in the
+ * per-call VP8Encoder, webp_enc.c:330-410). Here each call takes an idle
+ * engine of its picture's size and kind from the pool (creating one when none
+ * is idle), runs on that engine's own HIP stream without any process-wide
+ * lock, and hands it back: concurrent callers encode in parallel on the GPU,
+ * and engines of other sizes stay cached instead of being torn down. */
+#define POOL_SLOTS 32
 
-static pthread_mutex_t g_engine_lock = PTHREAD_MUTEX_INITIALIZER;
-static WebPGpuBatch* g_engine = NULL;
+typedef struct {
+  WebPGpuBatch* e;   /* NULL while being created */
+  int used;          /* slot taken (engine present or being created) */
+  int busy;          /* a call is using it */
+  int w, h, lossless, method;
+  uint64_t stamp;    /* last release, for LRU eviction */
+} PoolSlot;
 
-static WebPGpuBatch* engine_for(const WebPConfig* cfg, int w, int h) {
-  if (g_engine && (g_engine->w != w || g_engine->h != h)) {
-    WebPGpuBatchDelete(g_engine);
-    g_engine = NULL;
-  }
-  if (!g_engine) {
-    if (WebPGpuDeviceCount() <= 0) return NULL;
-    g_engine = WebPGpuBatchNew(0, w, h, 1, cfg, 1);
-  }
-  if (g_engine) g_engine->cfg = *cfg;
-  return g_engine;
+static pthread_mutex_t g_pool_lock = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t g_pool_cv = PTHREAD_COND_INITIALIZER;
+static PoolSlot g_pool[POOL_SLOTS];
+static uint64_t g_pool_clock = 0;
+
+/* lossless engines are specific to the method (VP8L search effort); lossy
+ * engines take the call's config at every run */
+static int pool_match(const PoolSlot* s, int w, int h, int lossless, int method) {
+  return s->used && s->w == w && s->h == h && s->lossless == lossless &&
+         (!lossless || s->method == method);
 }
 
-/* lossless (VP8L) engine, cached per size and method */
-static WebPGpuBatch* g_lengine = NULL;
+static WebPGpuBatch* pool_get(const WebPConfig* cfg, int w, int h, int lossless) {
+  if (WebPGpuDeviceCount() <= 0) return NULL;
+  pthread_mutex_lock(&g_pool_lock);
+  for (;;) {
+    int idle = -1, empty = -1, lru = -1;
+    for (int i = 0; i < POOL_SLOTS; ++i) {
+      PoolSlot* s = &g_pool[i];
+      if (!s->used) {
+        if (empty < 0) empty = i;
+      } else if (!s->busy && s->e != NULL) {
+        if (pool_match(s, w, h, lossless, cfg->method)) { idle = i; break; }
+        if (lru < 0 || s->stamp < g_pool[lru].stamp) lru = i;
+      }
+    }
+    if (idle >= 0) {
+      PoolSlot* s = &g_pool[idle];
+      s->busy = 1;
+      pthread_mutex_unlock(&g_pool_lock);
+      if (!lossless) s->e->cfg = *cfg;
+      return s->e;
+    }
+    int slot = empty;
+    WebPGpuBatch* evict = NULL;
+    if (slot < 0 && lru >= 0) {   /* full: replace the least recently used idle engine */
+      slot = lru;
+      evict = g_pool[lru].e;
+    }
+    if (slot >= 0) {
+      PoolSlot* s = &g_pool[slot];
+      s->used = 1; s->busy = 1; s->e = NULL;
+      s->w = w; s->h = h; s->lossless = lossless; s->method = cfg->method;
+      pthread_mutex_unlock(&g_pool_lock);
+      if (evict) WebPGpuBatchDelete(evict);
+      WebPGpuBatch* e = WebPGpuBatchNew(0, w, h, 1, cfg, 1);
+      pthread_mutex_lock(&g_pool_lock);
+      if (e == NULL) {
+        s->used = 0; s->busy = 0;
+        pthread_cond_broadcast(&g_pool_cv);
+        pthread_mutex_unlock(&g_pool_lock);
+        return NULL;
+      }
+      s->e = e;
+      pthread_mutex_unlock(&g_pool_lock);
+      return e;
+    }
+    pthread_cond_wait(&g_pool_cv, &g_pool_lock);   /* every slot busy */
+  }
+}
 
-static WebPGpuBatch* lossless_engine_for(const WebPConfig* cfg, int w, int h) {
-  if (g_lengine && (g_lengine->w != w || g_lengine->h != h ||
-                    g_lengine->cfg.method != cfg->method)) {
-    WebPGpuBatchDelete(g_lengine);
-    g_lengine = NULL;
-  }
-  if (!g_lengine) {
-    if (WebPGpuDeviceCount() <= 0) return NULL;
-    g_lengine = WebPGpuBatchNew(0, w, h, 1, cfg, 1);
-  }
-  return g_lengine;
+static void pool_put(WebPGpuBatch* e) {
+  if (e == NULL) return;
+  pthread_mutex_lock(&g_pool_lock);
+  for (int i = 0; i < POOL_SLOTS; ++i)
+    if (g_pool[i].e == e) {
+      g_pool[i].busy = 0;
+      g_pool[i].stamp = ++g_pool_clock;
+      break;
+    }
+  pthread_cond_broadcast(&g_pool_cv);
+  pthread_mutex_unlock(&g_pool_lock);
 }
 
 /* ---- import (picture_csp_enc.c:474-619, 732-844) ---- */
@@ -325,15 +382,14 @@ static int import_packed_d(WebPPicture* pic, const uint8_t* src, int stride, int
   pic->colorspace = translucent ? WEBP_YUV420A : WEBP_YUV420;
   int ok = vp8h_pic_alloc_yuva(pic);
   if (ok) {
-    pthread_mutex_lock(&g_engine_lock);
     WebPConfig cfg;
     WebPConfigInitInternal(&cfg, WEBP_PRESET_DEFAULT, 75.f, WEBP_ENCODER_ABI_VERSION);
-    WebPGpuBatch* e = engine_for(&cfg, w, h);
+    WebPGpuBatch* e = pool_get(&cfg, w, h, 0);
     int has_alpha = 0;
     ok = e != NULL && vp8g_engine_import(e, rgba, 4 * w, pic->y, pic->u, pic->v,
                                          translucent ? pic->a : NULL, &has_alpha, sharp,
                                          sharp ? 0.f : dither);
-    pthread_mutex_unlock(&g_engine_lock);
+    pool_put(e);
     if (!ok) set_error(pic, VP8_ENC_ERROR_OUT_OF_MEMORY);
   }
   free(rgba);
@@ -451,15 +507,14 @@ static int encode_lossless(const WebPConfig* config, WebPPicture* pic) {
     }
   }
   if (!report(pic, 5)) { free(rgba); return 0; }
-  pthread_mutex_lock(&g_engine_lock);
-  WebPGpuBatch* e = lossless_engine_for(config, w, h);
+  WebPGpuBatch* e = pool_get(config, w, h, 1);
   int ok = e != NULL && WebPGpuBatchEncodeRGBAHost(e, rgba, (size_t)w * h * 4, 4 * w, 1);
   free(rgba);
   const int err = ok ? WebPGpuBatchError(e, 0) : VP8_ENC_ERROR_OUT_OF_MEMORY;
   const size_t size = ok && !err ? WebPGpuBatchOutputSize(e, 0) : 0;
   uint8_t* out = size ? (uint8_t*)malloc(size) : NULL;
   if (out) memcpy(out, WebPGpuBatchOutput(e, 0), size);
-  pthread_mutex_unlock(&g_engine_lock);
+  pool_put(e);
   if (!ok || err != VP8_ENC_OK || out == NULL) {
     free(out);
     return set_error(pic, err != VP8_ENC_OK ? (WebPEncodingError)err : VP8_ENC_ERROR_OUT_OF_MEMORY);
@@ -494,13 +549,9 @@ int WebPEncode(const WebPConfig* config, WebPPicture* pic) {
   if (!config->exact) WebPCleanupTransparentArea(pic);   /* webp_enc.c:369-371 */
   const int has_alpha = pic->a != NULL && WebPPictureHasTransparency(pic);
 
-  pthread_mutex_lock(&g_engine_lock);
-  WebPGpuBatch* e = engine_for(config, pic->width, pic->height);
+  WebPGpuBatch* e = pool_get(config, pic->width, pic->height, 0);
   int ok = e != NULL;
-  if (!ok) {
-    pthread_mutex_unlock(&g_engine_lock);
-    return set_error(pic, VP8_ENC_ERROR_OUT_OF_MEMORY);
-  }
+  if (!ok) return set_error(pic, VP8_ENC_ERROR_OUT_OF_MEMORY);
   ok = vp8g_engine_upload_yuv(e, 0, pic->y, pic->y_stride, pic->u, pic->v, pic->uv_stride,
                               has_alpha ? pic->a : NULL, pic->a_stride) &&
        report(pic, 20) && vp8g_engine_run_yuv(e, 1);
@@ -521,7 +572,7 @@ int WebPEncode(const WebPConfig* config, WebPPicture* pic) {
     hdr[0] = e->hdr[0];
     hdr[1] = e->hdr[1];
   }
-  pthread_mutex_unlock(&g_engine_lock);
+  pool_put(e);
   if (pic->error_code != VP8_ENC_OK) { free(out); return 0; }
   if (!ok || err != VP8_ENC_OK || out == NULL) {
     free(out);

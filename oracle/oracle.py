@@ -50,6 +50,9 @@ def lib():
         _lib.vp8o_analyze.argtypes = [vp, vp, vp, i, i, i, i, vp, vp, vp]
         _lib.vp8o_free.argtypes = [vp]
         _lib.vp8o_default_config.argtypes = [vp]
+        _lib.odec_info.argtypes = [C.c_char_p, C.c_size_t] + [C.POINTER(C.c_int)] * 4
+        _lib.odec_decode_rgba.argtypes = [C.c_char_p, C.c_size_t, vp]
+        _lib.odec_decode_yuv.argtypes = [C.c_char_p, C.c_size_t, vp, vp, vp]
     return _lib
 
 
@@ -140,3 +143,36 @@ def encode_rgba(rgba, quality=75.0, method=4, **kw):
     else:
         y, u, v = import_rgba(rgba, sharp=sharp)
     return encode_yuv(y, u, v, quality, method, **kw)
+
+
+# ---- own WebP decoder (webp_dec.c): decode checks without reference code ----
+
+def decode_info(data):
+    """(width, height, has_alpha, lossless) of a .webp file."""
+    w, h, a, ll = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    if not lib().odec_info(data, len(data), C.byref(w), C.byref(h), C.byref(a), C.byref(ll)):
+        raise ValueError("not a WebP bitstream the decoder understands")
+    return w.value, h.value, bool(a.value), bool(ll.value)
+
+
+def decode_rgba(data):
+    """(H, W, 4) RGBA, what WebPDecodeRGBA returns (fancy upsampling for VP8)."""
+    w, h, _, _ = decode_info(data)
+    out = np.empty((h, w, 4), np.uint8)
+    if not lib().odec_decode_rgba(data, len(data), out.ctypes.data):
+        raise ValueError("decoder rejected the bitstream")
+    return out
+
+
+def decode_yuv(data):
+    """(Y, U, V) planes of a lossy (VP8) .webp, cropped to the picture."""
+    w, h, _, lossless = decode_info(data)
+    if lossless:
+        raise ValueError("decode_yuv needs a VP8 (lossy) bitstream")
+    uw, uh = (w + 1) // 2, (h + 1) // 2
+    y = np.empty((h, w), np.uint8)
+    u = np.empty((uh, uw), np.uint8)
+    v = np.empty((uh, uw), np.uint8)
+    if not lib().odec_decode_yuv(data, len(data), y.ctypes.data, u.ctypes.data, v.ctypes.data):
+        raise ValueError("decoder rejected the bitstream")
+    return y, u, v

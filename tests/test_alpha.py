@@ -52,25 +52,22 @@ def test_golden_vectors_self_consistent():
         assert hashlib.sha256(img.tobytes()).hexdigest()[:16] == c["in_sha"]
 
 
-def decoder_or_none():
-    import ctypes
-    path = os.path.join(ROOT, "oracle", "_ref", "libwebp_ref.so")
-    return ctypes.CDLL(path) if os.path.exists(path) else None
 
 
 def check(data, img, case):
     ch = chunks(data)
     assert [t for t, _ in M.riff_chunks(data)] == [b"VP8X", b"ALPH", b"VP8 "]
     assert hashlib.sha256(ch[b"VP8 "]).hexdigest() == case["vp8_sha256"]
-    lib = decoder_or_none()
-    if lib is not None:
-        dec = M.ref_decode(lib, data)
-        if case["alpha_quality"] < 100:   # the reference's level-reduced plane
-            assert hashlib.sha256(dec[..., 3].tobytes()).hexdigest() == case["alpha_sha256"]
-            assert chunks(data)[b"ALPH"][0] >> 4 == 1   # ALPHA_PREPROCESSED_LEVELS
-        else:
-            assert np.array_equal(dec[..., 3], img[..., 3])
-        assert hashlib.sha256(dec[..., :3].tobytes()).hexdigest() == case["rgb_sha256"]
+    # decoded with the own decoder (oracle/webp_dec.c, pinned against the
+    # reference decoder in tests/test_decoder.py)
+    from oracle import oracle
+    dec = oracle.decode_rgba(data)
+    if case["alpha_quality"] < 100:   # the reference's level-reduced plane
+        assert hashlib.sha256(dec[..., 3].tobytes()).hexdigest() == case["alpha_sha256"]
+        assert chunks(data)[b"ALPH"][0] >> 4 == 1   # ALPHA_PREPROCESSED_LEVELS
+    else:
+        assert np.array_equal(dec[..., 3], img[..., 3])
+    assert hashlib.sha256(dec[..., :3].tobytes()).hexdigest() == case["rgb_sha256"]
 
 
 @pytest.mark.gpu

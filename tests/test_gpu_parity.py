@@ -154,3 +154,28 @@ def test_p0_overflow_rerun(gpu, kat):
     enc.close()
     assert err == 0
     assert len(out) == c["size"] and sha(out) == c["sha256"]
+
+
+def _decode_kat():
+    import json
+    return json.load(open(os.path.join(HERE, "golden", "decode_kat.json")))["cases"]
+
+
+def test_gpu_decode_equivalence(gpu):
+    """north_star's criterion: the GPU bitstreams decode (own decoder,
+    oracle/webp_dec.c) to the reference decoder's pixels for the reference
+    encoder's bitstreams -- committed decoded-pixel hashes, YUV and RGBA."""
+    import torch
+    from oracle import oracle
+    for c in _decode_kat():
+        w, h, f = c["w"], c["h"], c["frame"]
+        buf = torch.empty(w * h * 4, dtype=torch.uint8, device="cuda")
+        gpu.synth_device(buf.data_ptr(), w, h, f, 1)
+        torch.cuda.synchronize()
+        enc = gpu.GpuBatch(w, h, 1, quality=c["q"], method=c["m"])
+        enc.encode_device(buf.data_ptr(), 1)
+        data = enc.output(0)
+        enc.close()
+        y, u, v = oracle.decode_yuv(data)
+        assert sha(y.tobytes() + u.tobytes() + v.tobytes()) == c["yuv_sha256"], (w, h, f)
+        assert sha(oracle.decode_rgba(data).tobytes()) == c["rgba_sha256"], (w, h, f)

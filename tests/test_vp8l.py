@@ -27,10 +27,18 @@ CASES = [(64, 48, 0), (33, 17, 3), (1, 1, 0), (7, 5, 1), (2, 130, 4), (130, 3, 2
 
 
 def ref_decoder():
+    """the reference build (oracle/_ref), for comparisons with its ENCODER"""
     path = os.path.join(ROOT, "oracle", "_ref", "libwebp_ref.so")
     if not os.path.exists(path):
         pytest.skip("reference build oracle/_ref not present")
     return C.CDLL(path)
+
+
+def decode(data):
+    """decode through the own decoder (oracle/webp_dec.c, pinned against the
+    reference decoder in tests/test_decoder.py)"""
+    from oracle import oracle
+    return oracle.decode_rgba(data)
 
 
 def with_alpha(img, seed):
@@ -45,16 +53,14 @@ def with_alpha(img, seed):
 
 @pytest.mark.parametrize("w,h,f", CASES)
 def test_model_decodes_exact(w, h, f):
-    lib = ref_decoder()
     img = syn_v1(w, h, f)
-    assert np.array_equal(M.ref_decode(lib, M.encode(img)), img)
+    assert np.array_equal(decode(M.encode(img)), img)
 
 
 def test_model_decodes_exact_alpha_and_methods():
-    lib = ref_decoder()
     img = with_alpha(syn_v1(96, 80, 5), 3)
     for method in (0, 3, 4, 6):
-        assert np.array_equal(M.ref_decode(lib, M.encode(img, method=method)), img)
+        assert np.array_equal(decode(M.encode(img, method=method)), img)
 
 
 def test_model_size_vs_reference_512():
@@ -219,14 +225,13 @@ def test_gpu_batch_frames_match_model(gpu):
 
 @pytest.mark.gpu
 def test_gpu_1080p_decodes_exact_and_size(gpu):
-    lib = ref_decoder()
     import json
     kat = json.load(open(os.path.join(ROOT, "tests", "golden", "kat.json")))
     sizes = {c["frame"]: c["size"] for c in kat.get("lossless", [])}
     frames = np.stack([syn_v1(1920, 1080, f) for f in range(3)])
     got = gpu_encode(gpu, frames)
     for f in range(3):
-        assert np.array_equal(M.ref_decode(lib, got[f]), frames[f]), "frame %d" % f
+        assert np.array_equal(decode(got[f]), frames[f]), "frame %d" % f
         if f in sizes:
             assert len(got[f]) <= sizes[f] * (1 + VP8L_SIZE_TOL), (f, len(got[f]), sizes[f])
 
@@ -248,16 +253,15 @@ def test_gpu_webpencode_lossless_api(gpu):
     """WebPEncode with config.lossless (webp_enc.c:396-407): ARGB picture,
     transparent pixels zeroed unless `exact`; the one-shot
     WebPEncodeLosslessRGBA (picture_enc.c:285-297)."""
-    lib = ref_decoder()
     img = with_alpha(syn_v1(160, 96, 4), 9)
     img[5, :40, 3] = 0   # fully transparent run
     data = gpu.encode_rgba(img, quality=75.0, method=4, lossless=1, use_argb=True, exact=1)
     assert data == M.encode(img)
-    assert np.array_equal(M.ref_decode(lib, data), img)
+    assert np.array_equal(decode(data), img)
     data = gpu.encode_rgba(img, quality=75.0, method=4, lossless=1, use_argb=True)
     want = img.copy()
     want[want[..., 3] == 0] = 0
-    assert np.array_equal(M.ref_decode(lib, data), want)
+    assert np.array_equal(decode(data), want)
     # one-shot API
     L = gpu.load()
     L.WebPEncodeLosslessRGBA.restype = C.c_size_t
@@ -269,5 +273,5 @@ def test_gpu_webpencode_lossless_api(gpu):
     assert n > 0
     got = C.string_at(out, n)
     L.WebPFree(out)
-    assert np.array_equal(M.ref_decode(lib, got), a)
+    assert np.array_equal(decode(got), a)
     assert got == M.encode(a, method=4)

@@ -146,7 +146,19 @@ def make_config(lib, quality=75.0, method=4, preset=WEBP_PRESET_DEFAULT, **kw):
     return cfg
 
 
-def encode_rgba(lib, rgba, quality=75.0, method=4, stats=False, use_argb=None, **kw):
+def encode_rgba_map(lib, rgba, info_type, quality=75.0, method=4, **kw):
+    """encode_rgba with picture.extra_info of type `info_type` (1..7, the
+    per-MB map cwebp -map prints, src/enc/frame_enc.c:503-518): returns
+    (bytes, map as bytes, mbw * mbh)."""
+    h, w = rgba.shape[:2]
+    n = ((w + 15) >> 4) * ((h + 15) >> 4)
+    buf = (C.c_uint8 * n)(*([0xAA] * n))   # every entry must be written
+    data, _ = encode_rgba(lib, rgba, quality, method, _extra_info=(info_type, buf), **kw)
+    return data, bytes(buf)
+
+
+def encode_rgba(lib, rgba, quality=75.0, method=4, stats=False, use_argb=None, _extra_info=None,
+                **kw):
     """Encode an (H, W, 4) uint8 array through `lib`'s WebPEncode().
 
     use_argb: import into the ARGB container first (what cwebp does for
@@ -173,6 +185,9 @@ def encode_rgba(lib, rgba, quality=75.0, method=4, stats=False, use_argb=None, *
     st = WebPAuxStats() if stats else None
     if st is not None:
         pic.stats = C.pointer(st)
+    if _extra_info is not None:
+        pic.extra_info_type = _extra_info[0]
+        pic.extra_info = C.cast(_extra_info[1], C.POINTER(C.c_uint8))
     try:
         if not lib.WebPPictureImportRGBA(C.byref(pic), rgba.ctypes.data, 4 * w):
             raise RuntimeError("import failed: %s" % ENC_ERRORS[pic.error_code])

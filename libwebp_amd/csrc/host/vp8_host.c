@@ -243,6 +243,7 @@ static void kmeans_segments(vp8h_frame* fr, const uint8_t* mb_alpha, uint8_t* se
     if (moved < 5) break;
   }
   for (int i = 0; i < nmb; ++i) segmap[i] = (uint8_t)map[mb_alpha[i]];
+  for (int a = 0; a < 256; ++a) fr->alpha_center[a] = (uint8_t)centers[map[a]];
   if (nb > 1 && (fr->preprocessing & 1)) smooth_map(segmap, fr->mbw, fr->mbh);
   int mn = centers[0], mx = centers[0];
   if (nb > 1)
@@ -316,6 +317,7 @@ void vp8h_analyze_segments(vp8h_frame* fr, const uint8_t* mb_alpha, const uint16
     kmeans_segments(fr, mb_alpha, segmap);
   } else {
     memset(segmap, 0, (size_t)nmb);
+    memset(fr->alpha_center, 0, sizeof(fr->alpha_center));
     fr->seg_alpha[0] = fr->seg_beta[0] = 0;
     fr->alpha = fr->uv_alpha = 0;
   }

@@ -32,6 +32,9 @@ typedef struct {
   int alpha, uv_alpha, base_quant, dq_uv_dc, dq_uv_ac;
   int seg_alpha[4], seg_beta[4], seg_quant[4], seg_fstrength[4], seg_y2ac[4];
   int segment_size[4];
+  /* mb->alpha_ after AssignSegments (analysis_enc.c:202-207): the centre of
+   * each raw analysis alpha's class, 0 without segmentation (extra_info 7) */
+  uint8_t alpha_center[256];
   /* filter header */
   int f_simple, f_level, f_sharpness;
   /* multi-pass convergence (PassStats, frame_enc.c:38-80) */

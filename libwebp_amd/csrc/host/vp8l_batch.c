@@ -312,3 +312,14 @@ const uint8_t* vp8l_engine_output(const vp8l_engine* l, int f) {
   if (!l->out_size[f]) return NULL;
   return l->h_out + l->out_off[f] + (l->p.alpha ? 20 : 0);
 }
+
+void vp8l_engine_frame_info(const vp8l_engine* l, int f, vp8l_frame_info* info) {
+  memset(info, 0, sizeof(*info));
+  info->features = l->p.alpha ? 3 : 7;   /* predictor + cross colour (+ subtract green) */
+  info->histogram_bits = l->p.hb;
+  info->transform_bits = l->p.tb;
+  info->cache_bits = l->p.cache_bits;
+  info->palette_size = 0;
+  info->hdr_bytes = (int)((l->h_start[f] + 7) >> 3);
+  info->data_bytes = (int)((l->h_end[f] - l->h_start[f] + 7) >> 3);
+}

@@ -74,6 +74,17 @@ extern "C" {
  * outputs are bare VP8L streams at vp8l_engine_output() */
 vp8l_engine* vp8l_engine_new(int w, int h, int max_frames, int method, int alpha);
 const uint8_t* vp8l_engine_output(const vp8l_engine* l, int f);
+
+/* WebPAuxStats' lossless fields of frame f of the last call
+ * (src/enc/vp8l_enc.c:1628-1639): transforms used (1 predictor, 2 cross
+ * colour, 4 subtract green, 8 palette), tile bits, colour-cache bits,
+ * palette size, header bytes (image header + transforms + codes) and
+ * pixel-data bytes */
+typedef struct {
+  int features, histogram_bits, transform_bits, cache_bits, palette_size;
+  int hdr_bytes, data_bytes;
+} vp8l_frame_info;
+void vp8l_engine_frame_info(const vp8l_engine* l, int f, vp8l_frame_info* info);
 void vp8l_engine_free(vp8l_engine* l);
 int vp8l_engine_run(struct WebPGpuBatch* b, const uint8_t* rgba, size_t fstride, int rstride,
                     int n);

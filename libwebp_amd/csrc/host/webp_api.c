@@ -229,6 +229,31 @@ int WebPPictureARGBToYUVADithered(WebPPicture* p, WebPEncCSP csp, float ditherin
 
 /* ---- WebPEncode (webp_enc.c:330-410) ---- */
 
+/* StoreSideInfo's per-MB map (frame_enc.c:503-518) from the final pass's
+ * MB records: 1 intra type, 2 segment, 3 segment quantiser, 4 intra-16 mode
+ * (0xff for intra-4), 5 chroma mode, 7 analysis alpha (its class centre).
+ * Type 6 (coded bits per MB) is only set by the reference's VP8EncLoop path
+ * (frame_enc.c:354-355; uninitialised in its token loop) and is stored as 0
+ * here, like every other type. */
+static void store_extra_info(WebPPicture* pic, const vp8h_frame* fr, const uint8_t* mbinfo,
+                             const uint8_t* mb_alpha) {
+  const int nmb = fr->mbw * fr->mbh;
+  for (int i = 0; i < nmb; ++i) {
+    const uint8_t* m = mbinfo + (size_t)i * VP8G_MBINFO_BYTES;   /* is_i16, uv, seg, skip, modes */
+    uint8_t v;
+    switch (pic->extra_info_type) {
+      case 1: v = m[0]; break;
+      case 2: v = m[2]; break;
+      case 3: v = (uint8_t)fr->seg_quant[m[2]]; break;
+      case 4: v = m[0] ? m[4] : 0xff; break;
+      case 5: v = m[1]; break;
+      case 7: v = fr->alpha_center[mb_alpha[i]]; break;
+      default: v = 0; break;
+    }
+    pic->extra_info[i] = v;
+  }
+}
+
 static int report(const WebPPicture* pic, int percent) {
   if (pic->progress_hook && !pic->progress_hook(percent, pic))
     return set_error(pic, VP8_ENC_ERROR_USER_ABORT);
@@ -267,6 +292,9 @@ static int encode_lossless(const WebPConfig* config, WebPPicture* pic) {
   const size_t size = ok && !err ? WebPGpuBatchOutputSize(e, 0) : 0;
   uint8_t* out = size ? (uint8_t*)malloc(size) : NULL;
   if (out) memcpy(out, WebPGpuBatchOutput(e, 0), size);
+  vp8l_frame_info li;
+  memset(&li, 0, sizeof(li));
+  if (ok && !err) vp8l_engine_frame_info(e->l, 0, &li);
   pool_put(e);
   if (!ok || err != VP8_ENC_OK || out == NULL) {
     free(out);
@@ -275,7 +303,22 @@ static int encode_lossless(const WebPConfig* config, WebPPicture* pic) {
   ok = report(pic, 90) && pic->writer(out, size, pic);
   free(out);
   if (!ok) return pic->error_code != VP8_ENC_OK ? 0 : set_error(pic, VP8_ENC_ERROR_BAD_WRITE);
-  if (pic->stats != NULL) pic->stats->coded_size = (int)size;
+  if (pic->stats != NULL) {   /* vp8l_enc.c:1628-1639,1841-1881 */
+    WebPAuxStats* s = pic->stats;
+    memset(s, 0, sizeof(*s));
+    for (int i = 0; i < 5; ++i) s->PSNR[i] = 99.f;
+    s->coded_size = (int)size;
+    s->lossless_size = (int)size;
+    s->lossless_features = li.features;
+    s->histogram_bits = li.histogram_bits;
+    s->transform_bits = li.transform_bits;
+    s->cache_bits = li.cache_bits;
+    s->palette_size = li.palette_size;
+    s->lossless_hdr_size = li.hdr_bytes;
+    s->lossless_data_size = li.data_bytes;
+  }
+  if (pic->extra_info != NULL)   /* vp8l_enc.c:1884-1888 */
+    memset(pic->extra_info, 0, (size_t)((w + 15) >> 4) * ((h + 15) >> 4));
   return report(pic, 100);
 }
 
@@ -324,6 +367,8 @@ int WebPEncode(const WebPConfig* config, WebPPicture* pic) {
     res = e->h_results[0];
     hdr[0] = e->hdr[0];
     hdr[1] = e->hdr[1];
+    if (pic->extra_info != NULL && err == VP8_ENC_OK)
+      store_extra_info(pic, &fr, e->h_mbinfo, e->h_alpha);
   }
   pool_put(e);
   if (pic->error_code != VP8_ENC_OK) { free(out); return 0; }

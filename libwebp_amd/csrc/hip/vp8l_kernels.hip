@@ -3,14 +3,26 @@
 // decoder's (src/dec/vp8l_dec.c, src/dsp/lossless.c). All integer work:
 // HBM/LDS bound, no MFMA.
 //
+//   L0 k_vp8l_entropy    AnalyzeEntropy's 13 histograms per frame (row bands,
+//                        LDS histograms, one global add per bin)
+//      k_vp8l_palscan    one workgroup per frame: the colour set in an LDS hash
+//                        table, out as soon as it exceeds 256 colours
 //   L1 k_vp8l_transform  one workgroup per transform tile: subtract green,
 //                        best of 14 predictors by a bit-length cost,
 //                        cross-colour multipliers (least squares + 6
-//                        candidates), residual ARGB to HBM
-//   L2 k_vp8l_cache      one wave per frame, 64 pixels per step: colour-cache
-//                        hit bits (same-key lanes found with CACHE_BITS ballots)
+//                        candidates), residual ARGB to HBM -- or the plain
+//                        (sub-green) pixels for the non-spatial modes
+//      k_vp8l_palapply   colour indexing: binary search in the sorted palette,
+//                        2^xbits indices bundled per packed pixel
+//   L2 k_vp8l_cache      one wave per frame, 64 pixels per step: per pixel the
+//                        smallest cache size (1..9 bits) holding it; same-key
+//                        lanes found with one ballot per key bit, MSB first
 //   L3 k_vp8l_match      one wave per row: best candidate run per pixel (ballots)
 //      k_vp8l_parse      one thread per row: greedy copy / cache / literal
+//                        (once with every hit of the largest cache, then with
+//                        the frame's chosen size)
+//      k_vp8l_cachehist / k_vp8l_cachechoose  the cache size of each frame
+//                        from the provisional parse
 //   L4 k_vp8l_tilefeat   one workgroup per histogram tile: own entropy/pixel
 //   L5 k_vp8l_cluster    one workgroup per frame: k-means of histogram tiles
 //                        into <= KMAX code groups (histograms + costs in LDS)
@@ -134,9 +146,14 @@ struct TransformSmem {
   int best;
 };
 
-template <int T>
+// SG: the subtract-green instantiation; a launch of each covers every slot,
+// the blocks of slots with the other flag leave at once (a runtime flag
+// costs the spatial search 40 VGPRs and half its occupancy)
+template <int T, bool SG>
 __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restrict__ rgba,
                                                         size_t fstride, int rstride, vp8l_params p,
+                                                        const int* __restrict__ fidx,
+                                                        const uint8_t* __restrict__ fmode,
                                                         uint32_t* __restrict__ argb_out,
                                                         uint8_t* __restrict__ modes,
                                                         uint32_t* __restrict__ mult,
@@ -147,9 +164,28 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
   const int x0 = blockIdx.x * T, y0 = blockIdx.y * T;
   const int tw = min(T, W - x0), th = min(T, H - y0);
   const int sw = tw + 2;   // LDS source row width (cols x0-1 .. x0+tw)
-  const uint8_t* img = rgba + (size_t)f * fstride;
+  const uint8_t* img = rgba + (size_t)(fidx ? fidx[f] : f) * fstride;
   const int tiles_x = (W + T - 1) / T;
   const int tile = blockIdx.y * tiles_x + blockIdx.x;
+  const int emode = p.alpha ? VP8L_MODE_SPATIAL : (int)fmode[f];
+  constexpr bool subgreen = SG;
+  if (((emode & VP8L_MODE_SUBGREEN) != 0) != SG) return;
+
+  if (!(emode & VP8L_MODE_SPATIAL)) {   // direct / subtract green only: no predictor
+    bool any_alpha = false;
+    uint32_t* out = argb_out + (size_t)f * W * H;
+    for (int i = tid; i < tw * th; i += 256) {
+      const int ly = i / tw, lx = i - ly * tw;
+      const uint8_t* q = img + (size_t)(y0 + ly) * rstride + 4 * (x0 + lx);
+      const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
+      any_alpha |= a != 255;
+      out[(size_t)(y0 + ly) * W + x0 + lx] =
+          subgreen ? (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255)
+                   : (a << 24) | (r << 16) | (g << 8) | b;
+    }
+    if (__any(any_alpha) && lane_id() == 0) atomicOr(&alpha_flag[f], 1u);
+    return;
+  }
 
   // load sub-green pixels (A, R-G, G, B-G) with a 1-pixel border
   bool tile_alpha = false;
@@ -163,7 +199,8 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
       } else {
         const uint8_t* q = img + (size_t)y * rstride + 4 * x;
         const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
-        v = (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255);
+        v = subgreen ? (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255)
+                     : (a << 24) | (r << 16) | (g << 8) | b;
         if (a != 255 && ly > 0 && lx > 0 && lx <= tw) tile_alpha = true;
       }
     }
@@ -176,7 +213,8 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
         S.first[i] = (uint32_t)q[0] << 8;
       } else {
         const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
-        S.first[i] = (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255);
+        S.first[i] = subgreen ? (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255)
+                              : (a << 24) | (r << 16) | (g << 8) | b;
       }
     }
   }
@@ -320,24 +358,180 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
   }
 }
 
+// ------------------------------------------------------------------ L0
+
+__device__ __forceinline__ uint32_t rgba_argb(const uint8_t* q) {
+  return ((uint32_t)q[3] << 24) | ((uint32_t)q[0] << 16) | ((uint32_t)q[1] << 8) | q[2];
+}
+
+// AnalyzeEntropy's histograms (src/enc/vp8l_enc.c:87-141, HistoIx order
+// A, A', G, G', R, R', B, B', R-G, (R-G)', B-G, (B-G)', palette hash) over
+// one band of rows; pixels equal to their raster predecessor or to the pixel
+// above are skipped as there. One global add per non-zero bin.
+#define ENTROPY_BANDS 16
+__global__ __launch_bounds__(256) void k_vp8l_entropy(const uint8_t* __restrict__ rgba,
+                                                      size_t fstride, int rstride, int W, int H,
+                                                      uint32_t* __restrict__ ehist) {
+  __shared__ uint32_t h[VP8L_EHIST];
+  const int tid = threadIdx.x, f = blockIdx.y;
+  const uint8_t* img = rgba + (size_t)f * fstride;
+  for (int i = tid; i < VP8L_EHIST; i += 256) h[i] = 0;
+  __syncthreads();
+  const int y0 = (int)((long long)H * blockIdx.x / ENTROPY_BANDS);
+  const int y1 = (int)((long long)H * (blockIdx.x + 1) / ENTROPY_BANDS);
+  const long long n = (long long)(y1 - y0) * W;
+  for (long long i = tid; i < n; i += 256) {
+    const int y = y0 + (int)(i / W), x = (int)(i % W);
+    const uint8_t* row = img + (size_t)y * rstride;
+    const uint32_t pix = rgba_argb(row + 4 * x);
+    const uint32_t prev = x > 0 ? rgba_argb(row + 4 * (x - 1))
+                        : y > 0 ? rgba_argb(row - rstride + 4 * (W - 1)) : pix;
+    const uint32_t d = sub_pixels(pix, prev);
+    if (d == 0) continue;
+    if (y > 0 && rgba_argb(row - rstride + 4 * x) == pix) continue;
+    const int g = (int)(pix >> 8), gd = (int)(d >> 8);
+    atomicAdd(&h[0 * 256 + (pix >> 24)], 1u);
+    atomicAdd(&h[1 * 256 + (d >> 24)], 1u);
+    atomicAdd(&h[2 * 256 + (g & 255)], 1u);
+    atomicAdd(&h[3 * 256 + (gd & 255)], 1u);
+    atomicAdd(&h[4 * 256 + ((pix >> 16) & 255)], 1u);
+    atomicAdd(&h[5 * 256 + ((d >> 16) & 255)], 1u);
+    atomicAdd(&h[6 * 256 + (pix & 255)], 1u);
+    atomicAdd(&h[7 * 256 + (d & 255)], 1u);
+    atomicAdd(&h[8 * 256 + ((((int)pix >> 16) - g) & 255)], 1u);
+    atomicAdd(&h[9 * 256 + ((((int)d >> 16) - gd) & 255)], 1u);
+    atomicAdd(&h[10 * 256 + (((int)pix - g) & 255)], 1u);
+    atomicAdd(&h[11 * 256 + (((int)d - gd) & 255)], 1u);
+    const uint64_t hp = ((uint64_t)pix + (pix >> 19)) * 0x39c5fba7ull;   // HashPix :81-85
+    atomicAdd(&h[12 * 256 + (uint32_t)((hp & 0xffffffffull) >> 24)], 1u);
+  }
+  __syncthreads();
+  uint32_t* out = ehist + (size_t)f * VP8L_EHIST;
+  for (int i = tid; i < VP8L_EHIST; i += 256)
+    if (h[i]) atomicAdd(&out[i], h[i]);
+}
+
+// The colour set of a frame (GetColorPalette, src/utils/palette.c:95-148):
+// an LDS hash table with linear probing (colour 0 kept as a flag, the empty
+// slot marker), abandoned by every thread once more than 256 colours are in.
+// out: count (VP8L_MAX_PALETTE + 1 = too many) then the colours unordered.
+__global__ __launch_bounds__(256) void k_vp8l_palscan(const uint8_t* __restrict__ rgba,
+                                                      size_t fstride, int rstride, int W, int H,
+                                                      uint32_t* __restrict__ pal) {
+  __shared__ uint32_t keys[1024];
+  __shared__ uint32_t cnt, zero, over, outn;
+  const int tid = threadIdx.x, f = blockIdx.x;
+  const uint8_t* img = rgba + (size_t)f * fstride;
+  for (int i = tid; i < 1024; i += 256) keys[i] = 0;
+  if (tid == 0) { cnt = 0; zero = 0; over = 0; outn = 0; }
+  __syncthreads();
+  const long long n = (long long)W * H;
+  uint32_t last = 0;
+  bool have_last = false;
+  for (long long i = tid; i < n; i += 256) {
+    if (*(volatile uint32_t*)&over) break;
+    const int y = (int)(i / W), x = (int)(i % W);
+    const uint32_t pix = rgba_argb(img + (size_t)y * rstride + 4 * x);
+    if (have_last && pix == last) continue;
+    last = pix; have_last = true;
+    if (pix == 0) {
+      if (atomicExch(&zero, 1u) == 0 && atomicAdd(&cnt, 1u) + 1 > VP8L_MAX_PALETTE) over = 1;
+      continue;
+    }
+    uint32_t k = (pix * 0x1e35a7bdu) >> 22;
+    for (;;) {
+      const uint32_t old = atomicCAS(&keys[k], 0u, pix);
+      if (old == 0) {
+        if (atomicAdd(&cnt, 1u) + 1 > VP8L_MAX_PALETTE) over = 1;
+        break;
+      }
+      if (old == pix) break;
+      k = (k + 1) & 1023;
+    }
+  }
+  __syncthreads();
+  uint32_t* o = pal + (size_t)f * VP8L_PAL_STRIDE;
+  if (over || cnt > VP8L_MAX_PALETTE) {
+    if (tid == 0) o[0] = VP8L_MAX_PALETTE + 1;
+    return;
+  }
+  for (int i = tid; i < 1024; i += 256)
+    if (keys[i]) o[1 + atomicAdd(&outn, 1u)] = keys[i];
+  __syncthreads();
+  if (tid == 0) {
+    if (zero) o[1 + outn] = 0;
+    o[0] = cnt;
+  }
+}
+
+// Colour indexing + VP8LBundleColorMap (src/dsp/lossless_enc.c): packed
+// pixel x of row y holds the indices of pixels (x << xbits) + j in green at
+// bit 8 + j * (8 >> xbits); alpha 0xff. Index = position of the colour in the
+// sorted palette (binary search, SearchColorNoIdx) mapped to the stored order.
+__global__ __launch_bounds__(256) void k_vp8l_palapply(const uint8_t* __restrict__ rgba,
+                                                       size_t fstride, int rstride, vp8l_params p,
+                                                       const int* __restrict__ fidx,
+                                                       const uint32_t* __restrict__ sorted,
+                                                       const uint8_t* __restrict__ sidx,
+                                                       const int* __restrict__ npal,
+                                                       uint32_t* __restrict__ argb_out,
+                                                       uint32_t* __restrict__ alpha_flag) {
+  __shared__ uint32_t sp[VP8L_MAX_PALETTE];
+  __shared__ uint8_t si[VP8L_MAX_PALETTE];
+  const int tid = threadIdx.x, f = blockIdx.z, y = blockIdx.y;
+  const int np = npal[f];
+  for (int i = tid; i < np; i += 256) {
+    sp[i] = sorted[(size_t)f * VP8L_MAX_PALETTE + i];
+    si[i] = sidx[(size_t)f * VP8L_MAX_PALETTE + i];
+  }
+  __syncthreads();
+  const int x = blockIdx.x * 256 + tid;
+  if (x >= p.w) return;
+  const uint8_t* row = rgba + (size_t)(fidx ? fidx[f] : f) * fstride + (size_t)y * rstride;
+  const int xb = p.xbits, bd = 8 >> xb;
+  uint32_t code = 0;
+  bool a_any = false;
+  for (int j = 0; j < (1 << xb); ++j) {
+    const int sx = (x << xb) + j;
+    if (sx >= p.ow) break;
+    const uint32_t c = rgba_argb(row + 4 * sx);
+    a_any |= (c >> 24) != 255;
+    int lo = 0, hi = np;   // sp[lo] <= c < sp[hi]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (sp[mid] <= c) lo = mid; else hi = mid;
+    }
+    code |= (uint32_t)si[lo] << (8 + bd * j);
+  }
+  argb_out[(size_t)f * p.w * p.h + (size_t)y * p.w + x] = 0xff000000u | code;
+  if (__any(a_any) && lane_id() == 0) atomicOr(&alpha_flag[f], 1u);
+}
+
 // ------------------------------------------------------------------ L2
 
 // One wave per frame walks the pixels in stream order, 64 at a time, keeping
-// the decoder's colour cache in LDS (zero-initialised like
-// VP8LColorCacheInit). Lanes with the same key find each other with one
-// ballot per key bit; a lane's cache content is the value of its nearest
-// lower same-key lane, else the table entry; the highest lane of each key
-// group updates the table.
-#define CACHE_BATCH 16
+// the decoder's colour caches of every size b = 1..9 in LDS (zero-initialised
+// like VP8LColorCacheInit; 2 + 4 + ... + 512 entries). The keys of size b are
+// the top b bits of one 9-bit key, so the lanes sharing a key of every size
+// come from 9 ballots (most significant bit first, AND-ed). A lane's cache
+// content is the value of its nearest lower same-key lane, else the table
+// entry; the highest lane of each key group updates the table. The nine
+// sizes are independent: all lane exchanges, then all table reads, then all
+// table writes, so their latencies overlap. Out: per pixel the smallest size
+// whose cache holds it (hits are monotone in the size: the most recent
+// same-key pixel at b is also the most recent one at b + 1), one coalesced
+// byte store per 64 pixels.
+#define CACHE_BATCH 8
 __global__ __launch_bounds__(64) void k_vp8l_cache(const uint32_t* __restrict__ argb, int npix,
-                                                   uint64_t* __restrict__ hits) {
-  __shared__ uint32_t tab[1 << VP8L_CACHE_BITS];
+                                                   uint8_t* __restrict__ minb) {
+  __shared__ uint32_t tab[(2 << VP8L_MAX_CACHE_BITS) - 2];
   const int f = blockIdx.x, ln = lane_id();
   const uint32_t* E = argb + (size_t)f * npix;
-  uint64_t* out = hits + (size_t)f * ((npix + 63) >> 6);
-  for (int i = ln; i < (1 << VP8L_CACHE_BITS); i += 64) tab[i] = 0;
-  __syncthreads();
   const int nchunk = (npix + 63) >> 6;
+  uint8_t* out = minb + (size_t)f * npix;
+  for (int i = ln; i < (2 << VP8L_MAX_CACHE_BITS) - 2; i += 64) tab[i] = 0;
+  __syncthreads();
+  const uint64_t below = (1ull << ln) - 1ull;
   uint32_t cur[CACHE_BATCH], nxt[CACHE_BATCH];
 #pragma unroll
   for (int k = 0; k < CACHE_BATCH; ++k) {
@@ -350,28 +544,42 @@ __global__ __launch_bounds__(64) void k_vp8l_cache(const uint32_t* __restrict__ 
       const int q = ((c0 + CACHE_BATCH + k) << 6) + ln;
       nxt[k] = q < npix ? E[q] : 0;
     }
-#pragma unroll
+#pragma unroll 1
     for (int k = 0; k < CACHE_BATCH; ++k) {
       const int c = c0 + k;
       if (c >= nchunk) break;
       const int q = (c << 6) + ln;
       const bool valid = q < npix;
       const uint32_t v = cur[k];
-      const uint32_t key = (v * HASH_MUL) >> (32 - VP8L_CACHE_BITS);
-      uint64_t m = __ballot(valid);
+      const uint32_t key9 = (v * HASH_MUL) >> (32 - VP8L_MAX_CACHE_BITS);
+      uint64_t m[VP8L_MAX_CACHE_BITS];
+      uint32_t pv[VP8L_MAX_CACHE_BITS], tv[VP8L_MAX_CACHE_BITS];
+      uint64_t acc = __ballot(valid);
 #pragma unroll
-      for (int b = 0; b < VP8L_CACHE_BITS; ++b) {
-        const bool bit = (key >> b) & 1;
+      for (int b = 1; b <= VP8L_MAX_CACHE_BITS; ++b) {
+        const bool bit = (key9 >> (VP8L_MAX_CACHE_BITS - b)) & 1;
         const uint64_t bv = __ballot(valid && bit);
-        m &= bit ? bv : ~bv;
+        acc &= bit ? bv : ~bv;
+        m[b - 1] = acc;
       }
-      const uint64_t lower = m & ((1ull << ln) - 1ull);
-      const int j = lower ? 63 - __clzll((long long)lower) : ln;
-      const uint32_t pv = __shfl(v, j);
-      const uint32_t held = lower ? pv : tab[key];
-      const uint64_t hm = __ballot(valid && held == v);
-      if (ln == 0) out[c] = hm;
-      if (valid && (m >> ln) == 1ull) tab[key] = v;   // LDS ops of a wave stay in order
+#pragma unroll
+      for (int b = 1; b <= VP8L_MAX_CACHE_BITS; ++b) {
+        const uint64_t lower = m[b - 1] & below;
+        pv[b - 1] = __shfl(v, lower ? 63 - __clzll((long long)lower) : ln);
+        tv[b - 1] = tab[(1 << b) - 2 + (key9 >> (VP8L_MAX_CACHE_BITS - b))];
+      }
+      uint32_t mb = VP8L_NEVER_HIT;
+#pragma unroll
+      for (int b = VP8L_MAX_CACHE_BITS; b >= 1; --b) {
+        const uint32_t held = (m[b - 1] & below) ? pv[b - 1] : tv[b - 1];
+        if (held == v) mb = b;
+      }
+      if (valid) out[q] = (uint8_t)mb;
+      // LDS ops of a wave stay in order: every read above precedes these writes
+#pragma unroll
+      for (int b = 1; b <= VP8L_MAX_CACHE_BITS; ++b)
+        if (valid && (m[b - 1] >> ln) == 1ull)
+          tab[(1 << b) - 2 + (key9 >> (VP8L_MAX_CACHE_BITS - b))] = v;
     }
 #pragma unroll
     for (int k = 0; k < CACHE_BATCH; ++k) cur[k] = nxt[k];
@@ -384,16 +592,16 @@ __global__ __launch_bounds__(64) void k_vp8l_cache(const uint32_t* __restrict__ 
 // distance the run of equal pixels starting at every x (ballot of the 64
 // comparisons; count trailing ones; a run reaching the chunk end continues
 // with the run at the next chunk's start), the longest (first on ties,
-// capped at MAX_LENGTH) and the cache-hit bit, packed per pixel as
-// len | cand << 13 | hit << 15 for the parse.
+// capped at MAX_LENGTH) and the smallest cache size holding the pixel,
+// packed per pixel as len | cand << 13 | minb << 15 for the parse.
 __global__ __launch_bounds__(64) void k_vp8l_match(const uint32_t* __restrict__ argb,
-                                                   const uint64_t* __restrict__ hits, vp8l_params p,
+                                                   const uint8_t* __restrict__ minb, vp8l_params p,
                                                    uint32_t* __restrict__ bm) {
   const int f = blockIdx.y, y = blockIdx.x, ln = lane_id();
   const int W = p.w;
   const size_t npix = (size_t)W * p.h;
   const uint32_t* E = argb + f * npix;
-  const uint64_t* hb = hits + (size_t)f * ((npix + 63) >> 6);
+  const uint8_t* MB = minb + (size_t)f * npix;
   uint32_t* O = bm + f * npix;
   const size_t row = (size_t)y * W;
   int carry[VP8L_NUM_CAND] = {0, 0, 0, 0};
@@ -408,39 +616,79 @@ __global__ __launch_bounds__(64) void k_vp8l_match(const uint32_t* __restrict__ 
       const int d = p.dist[k];
       const bool ok = valid && d > 0 && (size_t)d <= q && E[q - d] == e;
       const uint64_t mask = __ballot(ok);
-      int run = (int)__builtin_ctzll(~(mask >> ln));
+      const uint64_t miss = ~(mask >> ln);   // zero when all 64 lanes from lane 0 match:
+      int run = miss ? (int)__builtin_ctzll(miss) : 64;   // ctz(0) is undefined (gives 31)
       if (run == 64 - ln) run += carry[k];
       carry[k] = __shfl(run, 0);
       const int n = min(run, VP8L_MAX_LENGTH);
       if (n > bn) { bn = n; bk = k; }
     }
-    if (valid) {
-      const uint32_t hit = (uint32_t)((hb[q >> 6] >> (q & 63)) & 1);
-      O[q] = (uint32_t)bn | ((uint32_t)bk << 13) | (hit << 15);
-    }
+    if (valid) O[q] = (uint32_t)bn | ((uint32_t)bk << 13) | ((uint32_t)MB[q] << 15);
   }
 }
 
-// One thread per row: greedy copy / cache / literal over the packed match
-// words (model: parse), rewriting them in place as parse ops.
-__global__ __launch_bounds__(64) void k_vp8l_parse(vp8l_params p, uint32_t* __restrict__ ops) {
-  const int f = blockIdx.y, y = blockIdx.x * 64 + threadIdx.x;
-  const int W = p.w, H = p.h;
-  if (y >= H) return;
+// Greedy copy / cache / literal over the packed match words (model: parse),
+// each row on its own. A wave owns 64 rows (one per lane) and walks them in
+// 64-pixel chunks staged through LDS: the chunk's 64 x 64 words are loaded
+// row by row (coalesced), every lane parses its row up to the chunk end, the
+// chunk goes back coalesced. Positions a copy from an earlier chunk covers
+// are marked when their chunk is loaded (xs[] = each row's parse position).
+// A hit is a pixel held by the cache of the frame's size. Provisional pass
+// (cbits == NULL): every hit of the largest cache, act | (len - 1) << 2 into
+// prov, the match words kept; final pass: the frame's size cbits[f], the
+// match words rewritten in place as parse ops.
+__global__ __launch_bounds__(64) void k_vp8l_parse(vp8l_params p, uint32_t* __restrict__ ops,
+                                                   uint16_t* __restrict__ prov,
+                                                   const uint8_t* __restrict__ cbits) {
+  __shared__ uint32_t tile[64][65];
+  __shared__ int xs[64];
+  const int f = blockIdx.y, ln = lane_id();
+  const int W = p.w, H = p.h, y0 = blockIdx.x * 64;
+  const int nrows = min(64, H - y0);
   const size_t npix = (size_t)W * H;
-  uint32_t* O = ops + f * npix + (size_t)y * W;
-  int x = 0;
-  while (x < W) {
-    const uint32_t m = O[x];
-    const int bn = (int)(m & 0x1fff), bk = (int)((m >> 13) & 3);
-    const bool hit = (m >> 15) & 1;
-    if (bn >= VP8L_MIN_COPY || (bn == 2 && !hit)) {
-      O[x] = 2u | ((uint32_t)bn << 2) | ((uint32_t)p.dcode[bk] << 15);
-      for (int i = 1; i < bn; ++i) O[x + i] = 3u;
-      x += bn;
-    } else {
-      O[x] = hit ? 1u : 0u;
-      ++x;
+  uint32_t* O = ops + f * npix + (size_t)y0 * W;
+  const bool final_pass = cbits != nullptr;
+  uint16_t* P = final_pass ? nullptr : prov + f * npix + (size_t)y0 * W;
+  const uint32_t cb = final_pass ? cbits[f] : (uint32_t)p.cache_bits;
+  int x = 0;   // this lane's row position
+  xs[ln] = 0;
+  for (int cx = 0; cx < W; cx += 64) {
+    const int cw = min(64, W - cx);
+    __syncthreads();
+    for (int r = 0; r < nrows; ++r) {
+      if (ln < cw) {
+        const int xp = cx + ln;
+        tile[r][ln] = xp < xs[r] ? 0xffffffffu : O[(size_t)r * W + xp];   // covered: marker
+      }
+    }
+    __syncthreads();
+    if (ln < nrows) {
+      while (x < cx + cw) {
+        const int i = x - cx;
+        const uint32_t m = tile[ln][i];
+        const int bn = (int)(m & 0x1fff), bk = (int)((m >> 13) & 3);
+        const bool hit = cb > 0 && (m >> 15) <= cb;
+        if (bn >= VP8L_MIN_COPY || (bn == 2 && !hit)) {
+          tile[ln][i] = final_pass ? 2u | ((uint32_t)bn << 2) | ((uint32_t)p.dcode[bk] << 15)
+                                   : 2u | ((uint32_t)(bn - 1) << 2);
+          const int e = min(x + bn, cx + cw);
+          for (int j = i + 1; j < e - cx; ++j) tile[ln][j] = 3u;
+          x += bn;
+        } else {
+          tile[ln][i] = hit ? 1u : 0u;
+          ++x;
+        }
+      }
+      xs[ln] = x;
+    }
+    __syncthreads();
+    for (int r = 0; r < nrows; ++r) {
+      if (ln < cw) {
+        uint32_t v = tile[r][ln];
+        if (v == 0xffffffffu) v = 3u;
+        if (final_pass) O[(size_t)r * W + cx + ln] = v;
+        else P[(size_t)r * W + cx + ln] = (uint16_t)v;
+      }
     }
   }
 }
@@ -464,7 +712,7 @@ __device__ __forceinline__ void prefix_enc(uint32_t v, int& sym, int& nb, uint32
   ex = d & ((1u << (h - 1)) - 1);
 }
 
-__device__ __forceinline__ void pix_symbols(uint32_t op, uint32_t a, PixSym& o) {
+__device__ __forceinline__ void pix_symbols(uint32_t op, uint32_t a, int cb, PixSym& o) {
   const uint32_t act = op & 3;
   o.s[0] = o.s[1] = o.s[2] = o.s[3] = -1;
   o.xv[0] = o.xv[1] = 0; o.xb[0] = o.xb[1] = 0;
@@ -474,7 +722,7 @@ __device__ __forceinline__ void pix_symbols(uint32_t op, uint32_t a, PixSym& o) 
     o.s[2] = VP8L_GS + 256 + (int)(a & 255);
     o.s[3] = VP8L_GS + 512 + (int)(a >> 24);
   } else if (act == 1) {
-    o.s[0] = 280 + (int)((a * HASH_MUL) >> (32 - VP8L_CACHE_BITS));
+    o.s[0] = 280 + (int)((a * HASH_MUL) >> (32 - cb));
   } else if (act == 2) {
     int sym, nb; uint32_t ex;
     prefix_enc((op >> 2) & 0x1fff, sym, nb, ex);
@@ -488,7 +736,11 @@ __device__ __forceinline__ void pix_symbols(uint32_t op, uint32_t a, PixSym& o) 
 __device__ __forceinline__ int alph_of(int s) {
   return s < VP8L_GS ? 0 : s < VP8L_GS + 256 ? 1 : s < VP8L_GS + 512 ? 2 : s < VP8L_GS + 768 ? 3 : 4;
 }
-__device__ __forceinline__ int alph_size(int a) { return a == 0 ? VP8L_GS : a == 4 ? 40 : 256; }
+// alphabet sizes of a frame with a colour cache of cb bits (the green
+// alphabet's cache part is 2^cb of the layout's 2^VP8L_MAX_CACHE_BITS)
+__device__ __forceinline__ int alph_size(int a, int cb) {
+  return a == 0 ? 280 + (cb ? 1 << cb : 0) : a == 4 ? 40 : 256;
+}
 
 __device__ __forceinline__ int flog2_fx(const int32_t* frac, uint32_t v) {
   // log2(v) in 1/4096 bit, v >= 1 (model: flog2)
@@ -504,6 +756,138 @@ __device__ __forceinline__ long long flog2_fx64(const int32_t* frac, unsigned lo
 
 }  // namespace
 
+// ------------------------------------------------------------------ L3b
+
+// Cache-size choice, statistics (model: choose_cache_bits): one workgroup
+// per frame over the provisional parse. A pixel coded as literal or cache hit
+// with smallest holding size c goes to class c: its G, R, B, A bytes (the
+// literal it is for every size < c) and its 9-bit key (the cache symbol it is
+// for every size >= c); copies add their length prefix.
+__global__ __launch_bounds__(1024) void k_vp8l_cachehist(const uint32_t* __restrict__ argb,
+                                                         const uint32_t* __restrict__ match,
+                                                         const uint16_t* __restrict__ prov,
+                                                         int npix, uint32_t* __restrict__ chist) {
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  uint32_t* h = reinterpret_cast<uint32_t*>(smem_raw);
+  const int tid = threadIdx.x, f = blockIdx.x;
+  for (int i = tid; i < VP8L_CHIST; i += 1024) h[i] = 0;
+  __syncthreads();
+  const size_t base = (size_t)f * npix;
+  for (int q = tid; q < npix; q += 1024) {
+    const uint32_t op = prov[base + q];
+    const uint32_t act = op & 3;
+    if (act == 3) continue;
+    if (act == 2) {
+      int sym, nb; uint32_t ex;
+      prefix_enc((op >> 2) + 1, sym, nb, ex);
+      atomicAdd(&h[VP8L_CH_LEN + sym], 1u);
+      continue;
+    }
+    const uint32_t v = argb[base + q];
+    const int c = (int)(match[base + q] >> 15);   // smallest cache size holding it
+    const uint32_t L = VP8L_CH_LIT + (uint32_t)(c - 1) * 1024;   // lanes differ in class:
+    hadd(h, L + ((v >> 8) & 255));                               // full index for hadd
+    hadd(h, L + 256 + ((v >> 16) & 255));
+    hadd(h, L + 512 + (v & 255));
+    hadd(h, L + 768 + (v >> 24));
+    if (c <= VP8L_MAX_CACHE_BITS)
+      atomicAdd(&h[VP8L_CH_KEY + (c - 1) * 512 + ((v * HASH_MUL) >> (32 - VP8L_MAX_CACHE_BITS))], 1u);
+  }
+  __syncthreads();
+  uint32_t* o = chist + (size_t)f * VP8L_CHIST;
+  for (int i = tid; i < VP8L_CHIST; i += 1024) o[i] = h[i];
+}
+
+namespace {
+// bits_entropy_fx of the model from (sum, nonzeros, max, sum of n log2 n)
+__device__ long long bits_entropy_fx(const int32_t* frac, unsigned long long sum, int nonzeros,
+                                     unsigned long long mx, long long sl) {
+  if (nonzeros <= 1) return 0;
+  const long long s = (long long)sum;
+  const long long ent = (s > 1 ? s * flog2_fx64(frac, sum) : 0) - sl;
+  if (nonzeros == 2) return (99 * s * 4096 + ent) / 100;
+  const long long mix = nonzeros == 3 ? 950 : nonzeros == 4 ? 700 : 627;
+  long long ml = (2 * s - (long long)mx) * 4096;
+  ml = (mix * ml + (1000 - mix) * ent) / 1000;
+  return ent < ml ? ml : ent;
+}
+}  // namespace
+
+// Cache-size choice (model: choose_cache_bits): for every size b = 0..9 the
+// four codes' estimates from the class histograms; the smallest (first on
+// ties) becomes cbits[f].
+__global__ __launch_bounds__(256) void k_vp8l_cachechoose(const uint32_t* __restrict__ chist,
+                                                          const int32_t* __restrict__ frac,
+                                                          int max_bits,
+                                                          uint8_t* __restrict__ cbits) {
+  __shared__ unsigned long long red[4][4][4];   // [wave][alphabet][sum, nz, max, slog]
+  const int tid = threadIdx.x, f = blockIdx.x, wv = tid >> 6;
+  const uint32_t* h = chist + (size_t)f * VP8L_CHIST;
+  long long best = 0;
+  int best_b = 0;
+  for (int b = 0; b <= max_bits; ++b) {
+    const int ng = 280 + (b ? 1 << b : 0);
+    unsigned long long sum[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0}, nz[4] = {0, 0, 0, 0};
+    long long sl[4] = {0, 0, 0, 0};
+    for (int i = tid; i < ng + 768; i += 256) {
+      int a, ch = 0, bin = 0;
+      uint32_t v = 0;
+      if (i < ng) {
+        a = 0;
+        if (i < 256) { ch = 0; bin = i; }
+        else if (i < 280) { v = h[VP8L_CH_LEN + i - 256]; ch = -1; }
+        else {   // cache symbol k of size b: classes 1..b, keys k << (9 - b) ..
+          const int k = i - 280, sh = VP8L_MAX_CACHE_BITS - b;
+          for (int c = 1; c <= b; ++c)
+            for (int j = 0; j < (1 << sh); ++j)
+              v += h[VP8L_CH_KEY + (c - 1) * 512 + (k << sh) + j];
+          ch = -1;
+        }
+      } else {
+        a = 1 + (i - ng) / 256;            // R, B, A
+        ch = a; bin = (i - ng) & 255;
+      }
+      if (ch >= 0)
+        for (int c = b + 1; c <= VP8L_NEVER_HIT; ++c) v += h[VP8L_CH_LIT + (c - 1) * 1024 + ch * 256 + bin];
+      if (v) {
+        sum[a] += v; nz[a] += 1;
+        if (v > mx[a]) mx[a] = v;
+        if (v > 1) sl[a] += (long long)v * flog2_fx(frac, v);
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      sum[a] = wave_sum(sum[a]); nz[a] = wave_sum(nz[a]); sl[a] = wave_sum(sl[a]);
+      for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long t = __shfl_xor(mx[a], o);
+        mx[a] = t > mx[a] ? t : mx[a];
+      }
+    }
+    __syncthreads();
+    if (lane_id() == 0)
+      for (int a = 0; a < 4; ++a) {
+        red[wv][a][0] = sum[a]; red[wv][a][1] = nz[a]; red[wv][a][2] = mx[a];
+        red[wv][a][3] = (unsigned long long)sl[a];
+      }
+    __syncthreads();
+    if (tid == 0) {
+      long long e = 0;
+      for (int a = 0; a < 4; ++a) {
+        unsigned long long S = 0, N = 0, X = 0;
+        long long L = 0;
+        for (int w = 0; w < 4; ++w) {
+          S += red[w][a][0]; N += red[w][a][1];
+          X = red[w][a][2] > X ? red[w][a][2] : X;
+          L += (long long)red[w][a][3];
+        }
+        e += bits_entropy_fx(frac, S, (int)N, X, L);
+      }
+      if (b == 0 || e < best) { best = e; best_b = b; }
+    }
+  }
+  if (tid == 0) cbits[f] = (uint8_t)best_b;
+}
+
 // ------------------------------------------------------------------ L4
 
 // One workgroup per histogram tile: the tile's symbol histogram in LDS, its
@@ -512,6 +896,7 @@ __device__ __forceinline__ long long flog2_fx64(const int32_t* frac, unsigned lo
 __global__ __launch_bounds__(256) void k_vp8l_tilefeat(const uint32_t* __restrict__ argb,
                                                        const uint32_t* __restrict__ ops,
                                                        vp8l_params p,
+                                                       const uint8_t* __restrict__ cbits,
                                                        const int32_t* __restrict__ frac,
                                                        int64_t* __restrict__ feat,
                                                        uint32_t* __restrict__ tl,
@@ -521,6 +906,7 @@ __global__ __launch_bounds__(256) void k_vp8l_tilefeat(const uint32_t* __restric
   __shared__ uint32_t nnz;
   const int tid = threadIdx.x, f = blockIdx.y, t = blockIdx.x;
   const int W = p.w, H = p.h, hb = p.hb;
+  const int cb = cbits[f];
   const int tx_n = (W + (1 << hb) - 1) >> hb;
   const int tiles = tx_n * ((H + (1 << hb) - 1) >> hb);
   const int x0 = (t % tx_n) << hb, y0 = (t / tx_n) << hb;
@@ -534,7 +920,7 @@ __global__ __launch_bounds__(256) void k_vp8l_tilefeat(const uint32_t* __restric
     const int ly = i / tw, lx = i - ly * tw;
     const size_t q = f * npix + (size_t)(y0 + ly) * W + x0 + lx;
     PixSym s;
-    pix_symbols(ops[q], argb[q], s);
+    pix_symbols(ops[q], argb[q], cb, s);
     for (int k = 0; k < 4; ++k)
       if (s.s[k] >= 0) hadd(h, (uint32_t)s.s[k]);
   }
@@ -583,6 +969,7 @@ struct ClusterSmem {
 // their sparse histograms (model: cluster_tiles). A wave owns a tile at a
 // time in both the accumulation and the reassignment passes.
 __global__ __launch_bounds__(1024) void k_vp8l_cluster(vp8l_params p,
+                                                       const uint8_t* __restrict__ cbits,
                                                        const int32_t* __restrict__ frac,
                                                        const int64_t* __restrict__ feat,
                                                        const uint32_t* __restrict__ tl,
@@ -593,6 +980,7 @@ __global__ __launch_bounds__(1024) void k_vp8l_cluster(vp8l_params p,
   ClusterSmem& S = *reinterpret_cast<ClusterSmem*>(smem_raw);
   const int tid = threadIdx.x, f = blockIdx.x, wv = tid >> 6, ln = lane_id();
   const int W = p.w, H = p.h, hb = p.hb, K = p.k;
+  const int cb = cbits[f];
   const int tx_n = (W + (1 << hb) - 1) >> hb, ty_n = (H + (1 << hb) - 1) >> hb;
   const int nt = tx_n * ty_n;
   const size_t cap = VP8L_TILE_CAP(hb);
@@ -643,7 +1031,7 @@ __global__ __launch_bounds__(1024) void k_vp8l_cluster(vp8l_params p,
     for (int i = tid; i < K * VP8L_NS; i += 1024) {
       const int c = i / VP8L_NS, s = i - c * VP8L_NS, a = alph_of(s);
       const uint32_t N = S.nsum[c * 5 + a];
-      const int v = flog2_fx(frac, 10u * N + (uint32_t)alph_size(a)) -
+      const int v = flog2_fx(frac, 10u * N + (uint32_t)alph_size(a, cb)) -
                     flog2_fx(frac, 10u * S.hc[i] + 1u);
       S.u.lc[i] = (uint16_t)(v >> 4);
     }
@@ -701,6 +1089,7 @@ __device__ __forceinline__ const uint32_t* pixel_codes(const vp8l_params& p, con
 __global__ __launch_bounds__(256) void k_vp8l_bitcount(const uint32_t* __restrict__ argb,
                                                        const uint32_t* __restrict__ ops,
                                                        vp8l_params p,
+                                                       const uint8_t* __restrict__ cbits,
                                                        const uint32_t* __restrict__ ctab,
                                                        const uint8_t* __restrict__ gtile,
                                                        uint32_t* __restrict__ bsum) {
@@ -715,7 +1104,7 @@ __global__ __launch_bounds__(256) void k_vp8l_bitcount(const uint32_t* __restric
     const size_t q = (size_t)blk * VP8L_BLOCK + tid * (VP8L_BLOCK / 256) + k;
     if (q >= npix) break;
     PixSym s;
-    pix_symbols(ops[f * npix + q], argb[f * npix + q], s);
+    pix_symbols(ops[f * npix + q], argb[f * npix + q], cbits[f], s);
     b += pix_bits(s, pixel_codes(p, ctab, gtile, f, q));
   }
   b = wave_sum(b);
@@ -753,6 +1142,7 @@ __global__ __launch_bounds__(1024) void k_vp8l_scan(const uint32_t* __restrict__
 
 __global__ __launch_bounds__(256) void k_vp8l_write(const uint32_t* __restrict__ argb,
                                                     const uint32_t* __restrict__ ops, vp8l_params p,
+                                                    const uint8_t* __restrict__ cbits,
                                                     const uint32_t* __restrict__ ctab,
                                                     const uint8_t* __restrict__ gtile,
                                                     const uint32_t* __restrict__ bsum,
@@ -777,7 +1167,7 @@ __global__ __launch_bounds__(256) void k_vp8l_write(const uint32_t* __restrict__
   for (int k = 0; k < VP8L_BLOCK / 256; ++k) {
     const size_t q = (size_t)blk * VP8L_BLOCK + tid * (VP8L_BLOCK / 256) + k;
     if (q < npix) {
-      pix_symbols(ops[f * npix + q], argb[f * npix + q], s[k]);
+      pix_symbols(ops[f * npix + q], argb[f * npix + q], cbits[f], s[k]);
       ct[k] = pixel_codes(p, ctab, gtile, f, q);
       mine += pix_bits(s[k], ct[k]);
     } else {
@@ -862,45 +1252,87 @@ __global__ __launch_bounds__(256) void k_vp8l_pack(const uint8_t* __restrict__ o
 
 static int check_launch() { return hipGetLastError() == hipSuccess; }
 
+extern "C" int vp8l_launch_scan(const uint8_t* rgba, size_t fstride, int rstride, int w, int h,
+                                int n, uint32_t* ehist, uint32_t* pal, void* stream) {
+  if (w <= 0 || h <= 0 || n <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_vp8l_entropy, dim3(ENTROPY_BANDS, n), dim3(256), 0, st, rgba, fstride,
+                     rstride, w, h, ehist);
+  hipLaunchKernelGGL(k_vp8l_palscan, dim3(n), dim3(256), 0, st, rgba, fstride, rstride, w, h, pal);
+  return check_launch();
+}
+
 extern "C" int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rstride,
-                                     const vp8l_params* p, uint32_t* argb,
-                                     uint8_t* modes, uint32_t* mult, uint32_t* alpha_flag,
-                                     void* stream) {
+                                     const vp8l_params* p, const int* fidx, const uint8_t* fmode,
+                                     int sg_mask, uint32_t* argb, uint8_t* modes, uint32_t* mult,
+                                     uint32_t* alpha_flag, void* stream) {
   if (p->tb < 2 || p->tb > 6 || p->w <= 0 || p->h <= 0 || p->n <= 0) return 0;
+  if (!p->alpha && !fmode) return 0;
+  if (p->alpha) sg_mask = 1;
   dim3 grid((p->w + (1 << p->tb) - 1) >> p->tb, (p->h + (1 << p->tb) - 1) >> p->tb, p->n);
   hipStream_t st = (hipStream_t)stream;
-#define L1(T)                                                                              \
-  hipLaunchKernelGGL(k_vp8l_transform<T>, grid, dim3(256), 0, st, rgba, fstride, rstride, *p, \
-                     argb, modes, mult, alpha_flag)
-  switch (p->tb) {
-    case 2: L1(4); break;
-    case 3: L1(8); break;
-    case 4: L1(16); break;
-    case 5: L1(32); break;
-    default: L1(64); break;
+#define L1(T, SG)                                                                             \
+  hipLaunchKernelGGL((k_vp8l_transform<T, SG>), grid, dim3(256), 0, st, rgba, fstride, rstride, \
+                     *p, fidx, fmode, argb, modes, mult, alpha_flag)
+  for (int sg = 0; sg < 2; ++sg) {
+    if (!((sg_mask >> sg) & 1)) continue;
+    switch (p->tb) {
+      case 2: if (sg) L1(4, true); else L1(4, false); break;
+      case 3: if (sg) L1(8, true); else L1(8, false); break;
+      case 4: if (sg) L1(16, true); else L1(16, false); break;
+      case 5: if (sg) L1(32, true); else L1(32, false); break;
+      default: if (sg) L1(64, true); else L1(64, false); break;
+    }
   }
 #undef L1
   return check_launch();
 }
 
+extern "C" int vp8l_launch_palette_apply(const uint8_t* rgba, size_t fstride, int rstride,
+                                         const vp8l_params* p, const int* fidx,
+                                         const uint32_t* sorted, const uint8_t* sidx,
+                                         const int* npal, uint32_t* argb, uint32_t* alpha_flag,
+                                         void* stream) {
+  if (!p->palette || p->xbits < 0 || p->xbits > 3 || p->w <= 0 || p->h <= 0 || p->n <= 0 ||
+      ((p->ow + (1 << p->xbits) - 1) >> p->xbits) != p->w)
+    return 0;
+  hipLaunchKernelGGL(k_vp8l_palapply, dim3((p->w + 255) / 256, p->h, p->n), dim3(256), 0,
+                     (hipStream_t)stream, rgba, fstride, rstride, *p, fidx, sorted, sidx, npal,
+                     argb, alpha_flag);
+  return check_launch();
+}
+
 extern "C" int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
-                                   const int32_t* flog2, uint64_t* hits, uint32_t* ops,
-                                   int64_t* feat, uint32_t* tl, uint32_t* tn, uint32_t* hc,
-                                   uint8_t* assign, void* stream) {
+                                   const int32_t* tabs, uint8_t* minb, uint16_t* prov,
+                                   uint32_t* chist, uint8_t* cbits, uint32_t* ops, int64_t* feat,
+                                   uint32_t* tl, uint32_t* tn, uint32_t* hc, uint8_t* assign,
+                                   void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int npix = p->w * p->h;
+  const int32_t* flog2 = tabs + 4097;
   const int tx_n = (p->w + (1 << p->hb) - 1) >> p->hb, ty_n = (p->h + (1 << p->hb) - 1) >> p->hb;
   if (tx_n * ty_n > VP8L_MAX_HUFF_IMAGE || p->k < 1 || p->k > VP8L_KMAX) return 0;
+  if (p->cache_bits < 0 || p->cache_bits > VP8L_MAX_CACHE_BITS) return 0;
   if (p->cache_bits) {
-    hipLaunchKernelGGL(k_vp8l_cache, dim3(p->n), dim3(64), 0, st, argb, npix, hits);
-  } else if (hipMemsetAsync(hits, 0, (size_t)p->n * ((npix + 63) >> 6) * sizeof(uint64_t), st) !=
-             hipSuccess) {
+    hipLaunchKernelGGL(k_vp8l_cache, dim3(p->n), dim3(64), 0, st, argb, npix, minb);
+  } else if (hipMemsetAsync(minb, VP8L_NEVER_HIT, (size_t)p->n * npix, st) != hipSuccess) {
     return 0;
   }
-  hipLaunchKernelGGL(k_vp8l_match, dim3(p->h, p->n), dim3(64), 0, st, argb, hits, *p, ops);
-  hipLaunchKernelGGL(k_vp8l_parse, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, *p, ops);
+  hipLaunchKernelGGL(k_vp8l_match, dim3(p->h, p->n), dim3(64), 0, st, argb, minb, *p, ops);
+  if (p->cache_bits) {
+    hipLaunchKernelGGL(k_vp8l_parse, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, *p, ops, prov,
+                       (const uint8_t*)nullptr);   // provisional
+    hipLaunchKernelGGL(k_vp8l_cachehist, dim3(p->n), dim3(1024), VP8L_CHIST * sizeof(uint32_t), st,
+                       argb, (const uint32_t*)ops, prov, npix, chist);
+    hipLaunchKernelGGL(k_vp8l_cachechoose, dim3(p->n), dim3(256), 0, st, chist, flog2,
+                       p->cache_bits, cbits);
+  } else if (hipMemsetAsync(cbits, 0, (size_t)p->n, st) != hipSuccess) {
+    return 0;
+  }
+  hipLaunchKernelGGL(k_vp8l_parse, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, *p, ops, prov,
+                     (const uint8_t*)cbits);
   hipLaunchKernelGGL(k_vp8l_tilefeat, dim3(tx_n * ty_n, p->n), dim3(256), 0, st, argb, ops, *p,
-                     flog2, feat, tl, tn);
+                     (const uint8_t*)cbits, flog2, feat, tl, tn);
   static int attr = 0;
   if (!attr) {
     if (hipFuncSetAttribute((const void*)k_vp8l_cluster,
@@ -909,25 +1341,25 @@ extern "C" int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
       return 0;
     attr = 1;
   }
-  hipLaunchKernelGGL(k_vp8l_cluster, dim3(p->n), dim3(1024), sizeof(ClusterSmem), st, *p, flog2,
-                     feat, tl, tn, hc, assign);
+  hipLaunchKernelGGL(k_vp8l_cluster, dim3(p->n), dim3(1024), sizeof(ClusterSmem), st, *p,
+                     (const uint8_t*)cbits, flog2, feat, tl, tn, hc, assign);
   return check_launch();
 }
 
 extern "C" int vp8l_launch_write(const uint32_t* argb, const uint32_t* ops, const vp8l_params* p,
-                                 const uint32_t* ctab, const uint8_t* gtile,
+                                 const uint8_t* cbits, const uint32_t* ctab, const uint8_t* gtile,
                                  const uint64_t* start_bit, uint32_t* bsum, uint64_t* boff,
                                  uint64_t* end_bit, uint8_t* out, size_t out_cap, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const size_t npix = (size_t)p->w * p->h;
   const int nblk = (int)((npix + VP8L_BLOCK - 1) / VP8L_BLOCK);
   if ((out_cap & 3) != 0) return 0;
-  hipLaunchKernelGGL(k_vp8l_bitcount, dim3(nblk, p->n), dim3(256), 0, st, argb, ops, *p, ctab,
-                     gtile, bsum);
+  hipLaunchKernelGGL(k_vp8l_bitcount, dim3(nblk, p->n), dim3(256), 0, st, argb, ops, *p, cbits,
+                     ctab, gtile, bsum);
   hipLaunchKernelGGL(k_vp8l_scan, dim3(p->n), dim3(1024), 0, st, bsum, nblk, start_bit, boff,
                      end_bit);
-  hipLaunchKernelGGL(k_vp8l_write, dim3(nblk, p->n), dim3(256), 0, st, argb, ops, *p, ctab, gtile,
-                     bsum, boff, out, out_cap);
+  hipLaunchKernelGGL(k_vp8l_write, dim3(nblk, p->n), dim3(256), 0, st, argb, ops, *p, cbits, ctab,
+                     gtile, bsum, boff, out, out_cap);
   return check_launch();
 }
 

@@ -955,7 +955,7 @@ fail:
 
 size_t WebPGpuBatchOutputSize(const WebPGpuBatch* b, int f) {
   if (!b || f < 0 || f >= b->last_n) return 0;
-  return b->l ? b->l->out_size[f] : b->out_size[f];
+  return b->l ? vp8l_engine_out_size(b->l, f) : b->out_size[f];
 }
 const uint8_t* WebPGpuBatchOutput(const WebPGpuBatch* b, int f) {
   if (!b || f < 0 || f >= b->last_n) return NULL;
@@ -972,7 +972,7 @@ size_t WebPGpuBatchTokenCount(const WebPGpuBatch* b, int f) {
 }
 int WebPGpuBatchError(const WebPGpuBatch* b, int f) {
   if (!b || f < 0 || f >= b->last_n) return VP8_ENC_ERROR_NULL_PARAMETER;
-  return b->l ? b->l->err[f] : b->err[f];
+  return b->l ? vp8l_engine_error(b->l, f) : b->err[f];
 }
 void WebPGpuBatchTimings(const WebPGpuBatch* b, double t[10]) {
   for (int i = 0; i < 10; ++i) t[i] = b ? b->timings[i] : 0.;

@@ -1,7 +1,9 @@
-/* Lossless (VP8L) batch engine: device buffers, the L1 -> L5 kernels, the
- * per-frame header on host threads, the L6/L7 bit writer and the RIFF
- * assembly. One call encodes n same-sized RGBA frames resident in HBM;
- * every .webp lands in one pinned host buffer. */
+/* Lossless (VP8L) batch engine: device buffers, the L0 analysis and the
+ * per-frame entropy-mode decision, the L1 -> L5 kernels, the per-frame header
+ * on host threads, the L6/L7 bit writer and the RIFF assembly. One call
+ * encodes n same-sized RGBA frames resident in HBM; every .webp lands in one
+ * pinned host buffer per engine (the root engine's for the spatial / direct
+ * frames, a palette engine's per bundling for the colour-indexed ones). */
 #include <pthread.h>
 #include <stdatomic.h>
 #include <stdio.h>
@@ -36,8 +38,16 @@ static int sub_sample(int size, int bits) { return (size + (1 << bits) - 1) >> b
 
 void vp8l_engine_free(vp8l_engine* l) {
   if (!l) return;
+  for (int i = 0; i < 4; ++i) vp8l_engine_free(l->sub[i]);
+  free(l->route_eng); free(l->route_slot);
+  hipFree(l->d_minb); hipFree(l->d_prov); hipFree(l->d_chist); hipFree(l->d_cbits);
+  hipFree(l->d_ehist); hipFree(l->d_scan); hipFree(l->d_fidx); hipFree(l->d_fmode);
+  hipFree(l->d_psort); hipFree(l->d_psidx); hipFree(l->d_npal);
+  hipHostFree(l->h_ehist); hipHostFree(l->h_scan); hipHostFree(l->h_fidx); hipHostFree(l->h_fmode);
+  hipHostFree(l->h_cbits); hipHostFree(l->h_psort); hipHostFree(l->h_psidx); hipHostFree(l->h_npal);
+  free(l->h_pal);
   hipFree(l->d_tabs); hipFree(l->d_argb); hipFree(l->d_modes); hipFree(l->d_mult);
-  hipFree(l->d_aflag); hipFree(l->d_hits); hipFree(l->d_ops); hipFree(l->d_feat); hipFree(l->d_tl); hipFree(l->d_tn);
+  hipFree(l->d_aflag); hipFree(l->d_ops); hipFree(l->d_feat); hipFree(l->d_tl); hipFree(l->d_tn);
   hipFree(l->d_hc); hipFree(l->d_assign); hipFree(l->d_ctab); hipFree(l->d_gtile);
   hipFree(l->d_start); hipFree(l->d_bsum); hipFree(l->d_boff); hipFree(l->d_end); hipFree(l->d_out);
   hipFree(l->d_packed); hipFree(l->d_poff); hipFree(l->d_hpack); hipFree(l->d_hoff);
@@ -52,10 +62,12 @@ void vp8l_engine_free(vp8l_engine* l) {
   free(l);
 }
 
-vp8l_engine* vp8l_engine_new(int w, int h, int max_frames, int method, int alpha) {
+static vp8l_engine* engine_alloc(const vp8l_params* p, int max_frames, int method, int root) {
   vp8l_engine* l = (vp8l_engine*)calloc(1, sizeof(*l));
   if (!l) return NULL;
-  vp8l_setup_params(&l->p, w, h, max_frames, method, alpha);
+  l->p = *p;
+  const int w = p->w, h = p->h;
+  l->method = method;
   l->max_frames = max_frames;
   l->npix = (size_t)w * h;
   l->ntt = sub_sample(w, l->p.tb) * sub_sample(h, l->p.tb);
@@ -71,7 +83,36 @@ vp8l_engine* vp8l_engine_new(int w, int h, int max_frames, int method, int alpha
                 hipMemcpyHostToDevice));
   CHK(hipMalloc((void**)&l->d_argb, N * np * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&l->d_ops, N * np * sizeof(uint32_t)));
-  CHK(hipMalloc((void**)&l->d_hits, N * ((np + 63) >> 6) * sizeof(uint64_t)));
+  CHK(hipMalloc((void**)&l->d_minb, N * np));
+  if (l->p.cache_bits) {
+    CHK(hipMalloc((void**)&l->d_prov, N * np * sizeof(uint16_t)));
+    CHK(hipMalloc((void**)&l->d_chist, N * VP8L_CHIST * sizeof(uint32_t)));
+  }
+  CHK(hipMalloc((void**)&l->d_cbits, N));
+  CHK(hipMalloc((void**)&l->d_fidx, N * sizeof(int)));
+  CHK(hipMalloc((void**)&l->d_fmode, N));
+  CHK(hipHostMalloc((void**)&l->h_fidx, N * sizeof(int), 0));
+  CHK(hipHostMalloc((void**)&l->h_fmode, N, 0));
+  CHK(hipHostMalloc((void**)&l->h_cbits, N, 0));
+  if (root && !l->p.alpha) {
+    CHK(hipMalloc((void**)&l->d_ehist, N * VP8L_EHIST * sizeof(uint32_t)));
+    CHK(hipMalloc((void**)&l->d_scan, N * VP8L_PAL_STRIDE * sizeof(uint32_t)));
+    CHK(hipHostMalloc((void**)&l->h_ehist, N * VP8L_EHIST * sizeof(uint32_t), 0));
+    CHK(hipHostMalloc((void**)&l->h_scan, N * VP8L_PAL_STRIDE * sizeof(uint32_t), 0));
+    l->route_eng = (vp8l_engine**)calloc(N, sizeof(*l->route_eng));
+    l->route_slot = (int*)calloc(N, sizeof(int));
+    if (!l->route_eng || !l->route_slot) goto fail;
+  }
+  if (l->p.palette) {
+    CHK(hipMalloc((void**)&l->d_psort, N * VP8L_MAX_PALETTE * sizeof(uint32_t)));
+    CHK(hipMalloc((void**)&l->d_psidx, N * VP8L_MAX_PALETTE));
+    CHK(hipMalloc((void**)&l->d_npal, N * sizeof(int)));
+    CHK(hipHostMalloc((void**)&l->h_psort, N * VP8L_MAX_PALETTE * sizeof(uint32_t), 0));
+    CHK(hipHostMalloc((void**)&l->h_psidx, N * VP8L_MAX_PALETTE, 0));
+    CHK(hipHostMalloc((void**)&l->h_npal, N * sizeof(int), 0));
+    l->h_pal = (uint32_t*)calloc(N * VP8L_MAX_PALETTE, sizeof(uint32_t));
+    if (!l->h_pal) goto fail;
+  }
   CHK(hipMalloc((void**)&l->d_modes, N * l->ntt));
   CHK(hipMalloc((void**)&l->d_mult, N * l->ntt * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&l->d_aflag, N * sizeof(uint32_t)));
@@ -114,6 +155,17 @@ fail:
   return NULL;
 }
 
+vp8l_engine* vp8l_engine_new(int w, int h, int max_frames, int method, int alpha) {
+  vp8l_params p;
+  vp8l_setup_params(&p, w, h, max_frames, method, alpha);
+  return engine_alloc(&p, max_frames, method, 1);
+}
+
+static void route(const vp8l_engine* l, int f, const vp8l_engine** e, int* s) {
+  if (l->route_eng && l->route_eng[f]) { *e = l->route_eng[f]; *s = l->route_slot[f]; }
+  else { *e = l; *s = f; }
+}
+
 /* ---- per-frame headers on host threads ---- */
 
 typedef struct {
@@ -126,7 +178,11 @@ static void frame_header(vp8l_engine* l, int f) {
   vp8l_bw bw;
   const vp8l_params* p = &l->p;
   vp8l_bw_init(&bw, 1 << 16);
-  const int ok = vp8l_build_header(p, l->h_aflag[f] != 0, l->h_modes + (size_t)f * l->ntt,
+  const int emode = p->palette ? VP8L_MODE_PALETTE : p->alpha ? VP8L_MODE_SPATIAL : l->h_fmode[f];
+  const int ok = vp8l_build_header(p, l->h_aflag[f] != 0, emode, l->h_cbits[f],
+                                   p->palette ? l->h_pal + (size_t)f * VP8L_MAX_PALETTE : NULL,
+                                   p->palette ? l->h_npal[f] : 0,
+                                   l->h_modes + (size_t)f * l->ntt,
                                    l->h_mult + (size_t)f * l->ntt,
                                    l->h_hc + (size_t)f * VP8L_KMAX * VP8L_NS,
                                    l->h_assign + (size_t)f * l->nht, &bw,
@@ -180,28 +236,71 @@ int vp8l_engine_run(struct WebPGpuBatch* b, const uint8_t* rgba, size_t fstride,
   return ok;
 }
 
-int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t* rgba,
-                       size_t fstride, int rstride, int n, double timings[10]) {
-  hipStream_t st = (hipStream_t)stream;
+/* One engine's stages over its n slots. identity: slot f = frame f (the
+ * ALPH engine); else h_fidx / h_fmode (and the palettes) were filled. */
+static int pipeline(vp8l_engine* l, hipStream_t st, int threads, const uint8_t* rgba,
+                    size_t fstride, int rstride, int n, int identity, double timings[10]) {
   const size_t N = (size_t)n;
   double t0 = now_us(), t1, t2, t3, t4, t5;
   vp8l_params p = l->p;
   p.n = n;
   for (int f = 0; f < n; ++f) l->err[f] = VP8_ENC_OK;
   CHK(hipMemsetAsync(l->d_aflag, 0, N * sizeof(uint32_t), st));
+  if (!identity) {
+    CHK(hipMemcpyAsync(l->d_fidx, l->h_fidx, N * sizeof(int), hipMemcpyHostToDevice, st));
+    CHK(hipMemcpyAsync(l->d_fmode, l->h_fmode, N, hipMemcpyHostToDevice, st));
+  }
+  if (p.palette) {
+    CHK(hipMemcpyAsync(l->d_psort, l->h_psort, N * VP8L_MAX_PALETTE * sizeof(uint32_t),
+                       hipMemcpyHostToDevice, st));
+    CHK(hipMemcpyAsync(l->d_psidx, l->h_psidx, N * VP8L_MAX_PALETTE, hipMemcpyHostToDevice, st));
+    CHK(hipMemcpyAsync(l->d_npal, l->h_npal, N * sizeof(int), hipMemcpyHostToDevice, st));
+  }
   CHK(hipEventRecord(l->ev[0], st));
-  if (!vp8l_launch_transform(rgba, fstride, rstride, &p, l->d_argb, l->d_modes,
-                             l->d_mult, l->d_aflag, st))
-    goto fail;
+  if (p.palette) {
+    if (!vp8l_launch_palette_apply(rgba, fstride, rstride, &p, identity ? NULL : l->d_fidx,
+                                   l->d_psort, l->d_psidx, l->d_npal, l->d_argb, l->d_aflag, st))
+      goto fail;
+  } else {
+    int sg_mask = 0;
+    for (int f = 0; f < n; ++f) sg_mask |= identity ? 1 : 1 << ((l->h_fmode[f] >> 1) & 1);
+    if (!vp8l_launch_transform(rgba, fstride, rstride, &p, identity ? NULL : l->d_fidx,
+                               identity ? NULL : l->d_fmode, sg_mask, l->d_argb, l->d_modes,
+                               l->d_mult, l->d_aflag, st))
+      goto fail;
+  }
   CHK(hipEventRecord(l->ev[1], st));
-  if (!vp8l_launch_analyze(l->d_argb, &p, l->d_tabs + 4097, l->d_hits, l->d_ops, l->d_feat,
-                           l->d_tl, l->d_tn, l->d_hc, l->d_assign, st))
+  if (!vp8l_launch_analyze(l->d_argb, &p, l->d_tabs, l->d_minb, l->d_prov, l->d_chist,
+                           l->d_cbits, l->d_ops, l->d_feat, l->d_tl, l->d_tn, l->d_hc,
+                           l->d_assign, st))
     goto fail;
   CHK(hipEventRecord(l->ev[2], st));
-  CHK(hipMemcpyAsync(l->h_modes, l->d_modes, N * l->ntt, hipMemcpyDeviceToHost, st));
-  CHK(hipMemcpyAsync(l->h_mult, l->d_mult, N * l->ntt * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                     st));
+  {   /* debugging aid: LIBWEBP_AMD_VP8L_DUMP=<prefix> writes slot 0's
+       * coded image, cache sizes, parse ops and cache bits */
+    const char* dump = getenv("LIBWEBP_AMD_VP8L_DUMP");
+    if (dump) {
+      const size_t np = l->npix;
+      uint8_t* buf = (uint8_t*)malloc(np * 4 + 1);
+      char path[512];
+      const struct { const void* d; size_t bytes; const char* tag; } parts[] = {
+          {l->d_argb, np * 4, "argb"}, {l->d_ops, np * 4, "ops"}, {l->d_cbits, 1, "cbits"}};
+      for (int i = 0; buf && i < 3; ++i) {
+        CHK(hipStreamSynchronize(st));
+        CHK(hipMemcpy(buf, parts[i].d, parts[i].bytes, hipMemcpyDeviceToHost));
+        snprintf(path, sizeof(path), "%s.%s", dump, parts[i].tag);
+        FILE* fp = fopen(path, "wb");
+        if (fp) { fwrite(buf, 1, parts[i].bytes, fp); fclose(fp); }
+      }
+      free(buf);
+    }
+  }
+  if (!p.palette) {
+    CHK(hipMemcpyAsync(l->h_modes, l->d_modes, N * l->ntt, hipMemcpyDeviceToHost, st));
+    CHK(hipMemcpyAsync(l->h_mult, l->d_mult, N * l->ntt * sizeof(uint32_t),
+                       hipMemcpyDeviceToHost, st));
+  }
   CHK(hipMemcpyAsync(l->h_aflag, l->d_aflag, N * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  CHK(hipMemcpyAsync(l->h_cbits, l->d_cbits, N, hipMemcpyDeviceToHost, st));
   CHK(hipMemcpyAsync(l->h_hc, l->d_hc, N * VP8L_KMAX * VP8L_NS * sizeof(uint32_t),
                      hipMemcpyDeviceToHost, st));
   CHK(hipMemcpyAsync(l->h_assign, l->d_assign, N * l->nht, hipMemcpyDeviceToHost, st));
@@ -240,8 +339,8 @@ int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t*
   CHK(hipMemcpyAsync(l->d_gtile, l->h_gtile, N * l->nht, hipMemcpyHostToDevice, st));
   CHK(hipMemcpyAsync(l->d_start, l->h_start, N * sizeof(uint64_t), hipMemcpyHostToDevice, st));
   CHK(hipEventRecord(l->ev[3], st));
-  if (!vp8l_launch_write(l->d_argb, l->d_ops, &p, l->d_ctab, l->d_gtile, l->d_start, l->d_bsum,
-                         l->d_boff, l->d_end, l->d_out, l->out_cap, st))
+  if (!vp8l_launch_write(l->d_argb, l->d_ops, &p, l->d_cbits, l->d_ctab, l->d_gtile, l->d_start,
+                         l->d_bsum, l->d_boff, l->d_end, l->d_out, l->out_cap, st))
     goto fail;
   CHK(hipEventRecord(l->ev[4], st));
   CHK(hipMemcpyAsync(l->h_end, l->d_end, N * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
@@ -294,14 +393,107 @@ int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t*
     CHK(hipEventElapsedTime(&k_ms, l->ev[0], l->ev[1]));
     CHK(hipEventElapsedTime(&a_ms, l->ev[1], l->ev[2]));
     CHK(hipEventElapsedTime(&w_ms, l->ev[3], l->ev[4]));
-    timings[0] = t1 - t0;   /* transform + analysis kernels + side copies (wall) */
-    timings[1] = t2 - t1;   /* host headers */
-    timings[2] = t3 - t2;   /* header upload + bit writer (wall) */
-    timings[3] = t4 - t3;   /* output copies */
-    timings[4] = t5 - t4;   /* RIFF */
-    timings[6] = 1e3 * a_ms;   /* cache + parse + tiles + clustering */
-    timings[7] = 1e3 * k_ms;   /* transform */
-    timings[8] = 1e3 * w_ms;   /* bit writer */
+    timings[0] += t1 - t0;   /* transform + analysis kernels + side copies (wall) */
+    timings[1] += t2 - t1;   /* host headers */
+    timings[2] += t3 - t2;   /* header upload + bit writer (wall) */
+    timings[3] += t4 - t3;   /* output copies */
+    timings[4] += t5 - t4;   /* RIFF */
+    timings[6] += 1e3 * a_ms;   /* cache + parse + tiles + clustering */
+    timings[7] += 1e3 * k_ms;   /* transform */
+    timings[8] += 1e3 * w_ms;   /* bit writer */
+  }
+  return 1;
+fail:
+  return 0;
+}
+
+static int xbits_of(int npal) { return npal <= 2 ? 3 : npal <= 4 ? 2 : npal <= 16 ? 1 : 0; }
+
+static int u32_less(const void* a, const void* b) {
+  const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+  return x < y ? -1 : x > y;
+}
+
+/* The root engine's call: L0 analysis of every frame, the entropy mode of
+ * each (AnalyzeEntropy restated, host/vp8l_host.c), then one pipeline per
+ * engine with its slots. */
+int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t* rgba,
+                       size_t fstride, int rstride, int n, double timings[10]) {
+  hipStream_t st = (hipStream_t)stream;
+  const size_t N = (size_t)n;
+  for (int i = 0; i < 10; ++i) timings[i] = 0.;
+  if (l->p.alpha) return pipeline(l, st, threads, rgba, fstride, rstride, n, 1, timings);
+  const double t0 = now_us();
+  CHK(hipMemsetAsync(l->d_ehist, 0, N * VP8L_EHIST * sizeof(uint32_t), st));
+  if (!vp8l_launch_scan(rgba, fstride, rstride, l->p.w, l->p.h, n, l->d_ehist, l->d_scan, st))
+    goto fail;
+  CHK(hipMemcpyAsync(l->h_ehist, l->d_ehist, N * VP8L_EHIST * sizeof(uint32_t),
+                     hipMemcpyDeviceToHost, st));
+  CHK(hipMemcpyAsync(l->h_scan, l->d_scan, N * VP8L_PAL_STRIDE * sizeof(uint32_t),
+                     hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  {
+    const int ntiles = l->ntt;
+    int cnt[5] = {0, 0, 0, 0, 0};   /* [0..3] palette engines by xbits, [4] root */
+    uint8_t* mode = (uint8_t*)malloc(N);
+    if (!mode) goto fail;
+    for (int f = 0; f < n; ++f) {
+      const uint32_t* sc = l->h_scan + (size_t)f * VP8L_PAL_STRIDE;
+      const int npal = sc[0] <= VP8L_MAX_PALETTE ? (int)sc[0] : 0;
+      mode[f] = (uint8_t)vp8l_entropy_choice(l->h_ehist + (size_t)f * VP8L_EHIST, npal, ntiles);
+      if (mode[f] == VP8L_MODE_PALETTE) cnt[xbits_of(npal)]++;
+      else cnt[4]++;
+    }
+    for (int xb = 0; xb < 4; ++xb) {
+      if (!cnt[xb] || (l->sub[xb] && l->sub[xb]->max_frames >= cnt[xb])) continue;
+      vp8l_engine_free(l->sub[xb]);
+      vp8l_params pp;
+      vp8l_setup_palette_params(&pp, l->p.w, l->p.h, cnt[xb], l->method, xb);
+      l->sub[xb] = engine_alloc(&pp, cnt[xb], l->method, 0);
+      if (!l->sub[xb]) { free(mode); goto fail; }
+    }
+    int used[5] = {0, 0, 0, 0, 0};
+    for (int f = 0; f < n; ++f) {
+      if (mode[f] != VP8L_MODE_PALETTE) {
+        const int s = used[4]++;
+        l->h_fidx[s] = f;
+        l->h_fmode[s] = mode[f];
+        l->route_eng[f] = l;
+        l->route_slot[f] = s;
+        continue;
+      }
+      const uint32_t* sc = l->h_scan + (size_t)f * VP8L_PAL_STRIDE;
+      const int npal = (int)sc[0], xb = xbits_of(npal);
+      vp8l_engine* e = l->sub[xb];
+      const int s = used[xb]++;
+      uint32_t* pal = e->h_pal + (size_t)s * VP8L_MAX_PALETTE;
+      memcpy(pal, sc + 1, (size_t)npal * sizeof(uint32_t));
+      vp8l_palette_order(pal, npal);
+      uint32_t* srt = e->h_psort + (size_t)s * VP8L_MAX_PALETTE;
+      memcpy(srt, pal, (size_t)npal * sizeof(uint32_t));
+      qsort(srt, (size_t)npal, sizeof(uint32_t), u32_less);
+      for (int i = 0; i < npal; ++i) {   /* stored index of each sorted colour */
+        int lo = 0, hi = npal;
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (srt[mid] <= pal[i]) lo = mid; else hi = mid;
+        }
+        e->h_psidx[(size_t)s * VP8L_MAX_PALETTE + lo] = (uint8_t)i;
+      }
+      e->h_npal[s] = npal;
+      e->h_fidx[s] = f;
+      e->h_fmode[s] = VP8L_MODE_PALETTE;
+      l->route_eng[f] = e;
+      l->route_slot[f] = s;
+    }
+    free(mode);
+    timings[9] = now_us() - t0;   /* L0 analysis + decision */
+    if (used[4] && !pipeline(l, st, threads, rgba, fstride, rstride, used[4], 0, timings))
+      goto fail;
+    for (int xb = 0; xb < 4; ++xb)
+      if (used[xb] &&
+          !pipeline(l->sub[xb], st, threads, rgba, fstride, rstride, used[xb], 0, timings))
+        goto fail;
   }
   return 1;
 fail:
@@ -309,17 +501,37 @@ fail:
 }
 
 const uint8_t* vp8l_engine_output(const vp8l_engine* l, int f) {
-  if (!l->out_size[f]) return NULL;
-  return l->h_out + l->out_off[f] + (l->p.alpha ? 20 : 0);
+  const vp8l_engine* e; int s;
+  route(l, f, &e, &s);
+  if (!e->out_size[s]) return NULL;
+  return e->h_out + e->out_off[s] + (e->p.alpha ? 20 : 0);
+}
+
+size_t vp8l_engine_out_size(const vp8l_engine* l, int f) {
+  const vp8l_engine* e; int s;
+  route(l, f, &e, &s);
+  return e->out_size[s];
+}
+
+int vp8l_engine_error(const vp8l_engine* l, int f) {
+  const vp8l_engine* e; int s;
+  route(l, f, &e, &s);
+  return e->err[s];
 }
 
 void vp8l_engine_frame_info(const vp8l_engine* l, int f, vp8l_frame_info* info) {
+  const vp8l_engine* e; int s;
+  route(l, f, &e, &s);
   memset(info, 0, sizeof(*info));
-  info->features = l->p.alpha ? 3 : 7;   /* predictor + cross colour (+ subtract green) */
-  info->histogram_bits = l->p.hb;
-  info->transform_bits = l->p.tb;
-  info->cache_bits = l->p.cache_bits;
-  info->palette_size = 0;
-  info->hdr_bytes = (int)((l->h_start[f] + 7) >> 3);
-  info->data_bytes = (int)((l->h_end[f] - l->h_start[f] + 7) >> 3);
+  const int mode = e->p.palette ? VP8L_MODE_PALETTE : e->p.alpha ? VP8L_MODE_SPATIAL : e->h_fmode[s];
+  /* transforms used (vp8l_enc.c:1628-1632): 1 predictor, 2 cross colour,
+   * 4 subtract green, 8 palette */
+  info->features = mode == VP8L_MODE_PALETTE ? 8 :
+                   ((mode & VP8L_MODE_SPATIAL) ? 3 : 0) | ((mode & VP8L_MODE_SUBGREEN) ? 4 : 0);
+  info->histogram_bits = e->p.hb;
+  info->transform_bits = e->p.palette ? l->p.tb : e->p.tb;
+  info->cache_bits = e->h_cbits[s];
+  info->palette_size = e->p.palette ? e->h_npal[s] : 0;
+  info->hdr_bytes = (int)((e->h_start[s] + 7) >> 3);
+  info->data_bytes = (int)((e->h_end[s] - e->h_start[s] + 7) >> 3);
 }

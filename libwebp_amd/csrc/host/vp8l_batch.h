@@ -14,13 +14,29 @@ struct WebPGpuBatch;
 typedef struct vp8l_engine {
   hipEvent_t ev[5];            /* stage boundaries of the last call */
   vp8l_params p;               /* n = max_frames; per call a copy with n set */
-  int max_frames, ntt, nht, nblk;
+  int max_frames, ntt, nht, nblk, method;
   size_t npix, hdr_cap, out_cap;
+  /* the root engine decides per frame: its own slots take the spatial /
+   * direct / subtract-green frames, palette engines (one per bundling,
+   * created on demand) the colour-indexed ones; route_* map frame -> slot */
+  struct vp8l_engine* sub[4];
+  struct vp8l_engine** route_eng;
+  int* route_slot;
   /* device (HBM) */
   int32_t* d_tabs;             /* nlogn (4097) | log2 fraction (1024) */
   uint32_t* d_argb;
   uint32_t* d_ops;
-  uint64_t* d_hits;
+  uint8_t* d_minb;             /* smallest cache size holding each pixel */
+  uint16_t* d_prov;            /* provisional parse */
+  uint32_t* d_chist;           /* cache-size choice histograms */
+  uint8_t* d_cbits;            /* chosen cache bits per slot */
+  uint32_t* d_ehist;           /* L0 entropy histograms (root engine) */
+  uint32_t* d_scan;            /* L0 colour sets (root engine) */
+  int* d_fidx;                 /* input frame of each slot */
+  uint8_t* d_fmode;            /* entropy mode of each slot */
+  uint32_t* d_psort;           /* palette engine: sorted palette per slot */
+  uint8_t* d_psidx;            /*   stored index of each sorted colour */
+  int* d_npal;
   uint8_t* d_modes;
   uint32_t* d_mult;
   uint32_t* d_aflag;
@@ -44,6 +60,15 @@ typedef struct vp8l_engine {
   uint64_t* d_hoff;
   uint32_t* d_hwords;
   /* host (pinned) */
+  uint32_t* h_ehist;
+  uint32_t* h_scan;
+  int* h_fidx;
+  uint8_t* h_fmode;
+  uint8_t* h_cbits;
+  uint32_t* h_psort;
+  uint8_t* h_psidx;
+  int* h_npal;
+  uint32_t* h_pal;             /* palette in stored order per slot */
   uint8_t* h_modes;
   uint32_t* h_mult;
   uint32_t* h_aflag;
@@ -73,7 +98,10 @@ extern "C" {
 /* alpha != 0: ALPH-chunk engine, input = alpha planes (1 byte per pixel);
  * outputs are bare VP8L streams at vp8l_engine_output() */
 vp8l_engine* vp8l_engine_new(int w, int h, int max_frames, int method, int alpha);
+/* results of frame f of the last call (routed to the engine that coded it) */
 const uint8_t* vp8l_engine_output(const vp8l_engine* l, int f);
+size_t vp8l_engine_out_size(const vp8l_engine* l, int f);
+int vp8l_engine_error(const vp8l_engine* l, int f);
 
 /* WebPAuxStats' lossless fields of frame f of the last call
  * (src/enc/vp8l_enc.c:1628-1639): transforms used (1 predictor, 2 cross

@@ -107,7 +107,8 @@ void vp8l_setup_params(vp8l_params* p, int w, int h, int n, int method, int alph
   memset(p, 0, sizeof(*p));
   p->w = w; p->h = h; p->n = n;
   p->alpha = alpha != 0;
-  p->cache_bits = alpha ? 0 : VP8L_CACHE_BITS;
+  p->cache_bits = alpha ? 0 : VP8L_MAX_CACHE_BITS;
+  p->ow = w;
   p->hb = vp8l_histo_bits(method, w, h);
   p->tb = vp8l_transform_bits(method, p->hb);
   const int nht = sub_sample(w, p->hb) * sub_sample(h, p->hb);
@@ -125,6 +126,22 @@ void vp8l_setup_params(vp8l_params* p, int w, int h, int n, int method, int alph
   }
 }
 
+/* the colour-indexing engine: coded width = bundled width, tile bits from
+ * GetHistoBits with use_palette on the picture size (vp8l_enc.c:234-245) */
+void vp8l_setup_palette_params(vp8l_params* p, int w, int h, int n, int method, int xbits) {
+  const int pw = sub_sample(w, xbits);
+  vp8l_setup_params(p, pw, h, n, method, 0);
+  p->palette = 1;
+  p->xbits = xbits;
+  p->ow = w;
+  int b = 9 - method;
+  while (sub_sample(w, b) * sub_sample(h, b) > VP8L_MAX_HUFF_IMAGE) ++b;
+  p->hb = b < 2 ? 2 : b > 9 ? 9 : b;
+  p->tb = 2;   /* unused: no predictor */
+  const int nht = sub_sample(pw, p->hb) * sub_sample(h, p->hb);
+  p->k = nht < VP8L_KMAX ? nht : VP8L_KMAX;
+}
+
 static int32_t g_nlogn[4097];
 static int32_t g_flog2[1024];
 static pthread_once_t g_tab_once = PTHREAD_ONCE_INIT;
@@ -135,6 +152,98 @@ static void tables_init(void) {
 }
 const int32_t* vp8l_nlogn_table(void) { pthread_once(&g_tab_once, tables_init); return g_nlogn; }
 const int32_t* vp8l_flog2_table(void) { pthread_once(&g_tab_once, tables_init); return g_flog2; }
+
+/* ---------------------------------------------------------------- analysis */
+
+/* model: flog2 -- log2(v) in 1/4096 bit, v >= 1 */
+static int64_t flog2_fx(uint64_t v) {
+  const int32_t* frac = vp8l_flog2_table();
+  int e = 63 - __builtin_clzll(v);
+  const uint64_t m = (e >= 10 ? (v >> (e - 10)) : (v << (10 - e))) & 1023;
+  return ((int64_t)e << 12) + frac[m];
+}
+
+/* model: bits_entropy_fx (VP8LBitsEntropy in fixed point) */
+int64_t vp8l_bits_entropy_fx(const uint32_t* h, int n) {
+  uint64_t s = 0, mx = 0;
+  int nz = 0;
+  int64_t sl = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!h[i]) continue;
+    s += h[i]; ++nz;
+    if (h[i] > mx) mx = h[i];
+    if (h[i] > 1) sl += (int64_t)h[i] * flog2_fx(h[i]);
+  }
+  if (nz <= 1) return 0;
+  const int64_t S = (int64_t)s;
+  const int64_t ent = (s > 1 ? S * flog2_fx(s) : 0) - sl;
+  if (nz == 2) return (99 * S * 4096 + ent) / 100;
+  const int64_t mix = nz == 3 ? 950 : nz == 4 ? 700 : 627;
+  int64_t ml = (2 * S - (int64_t)mx) * 4096;
+  ml = (mix * ml + (1000 - mix) * ent) / 1000;
+  return ent < ml ? ml : ent;
+}
+
+/* model: entropy_choice (AnalyzeEntropy's estimates, vp8l_enc.c:158-201) */
+int vp8l_entropy_choice(const uint32_t* ehist, int npal, int ntiles) {
+  if (npal > 0 && npal <= 16) return VP8L_MODE_PALETTE;
+  int64_t e[13];
+  for (int i = 0; i < 13; ++i) e[i] = vp8l_bits_entropy_fx(ehist + 256 * i, 256);
+  int64_t ent[5];
+  ent[0] = e[0] + e[4] + e[2] + e[6];
+  ent[1] = e[1] + e[5] + e[3] + e[7] + (int64_t)ntiles * flog2_fx(14);
+  ent[2] = e[0] + e[8] + e[2] + e[10];
+  ent[3] = e[1] + e[9] + e[3] + e[11] + (int64_t)ntiles * flog2_fx(24);
+  ent[4] = e[12] + (int64_t)npal * 8 * 4096;
+  const int last = npal > 0 ? VP8L_MODE_PALETTE : VP8L_MODE_SPATIAL_SUBGREEN;
+  int best = 0;
+  for (int k = 1; k <= last; ++k)
+    if (ent[best] > ent[k]) best = k;
+  return best;
+}
+
+static uint32_t sub_pixels(uint32_t a, uint32_t b) {
+  const uint32_t ag = (a | 0x00ff00ffu) - (b & 0xff00ff00u);
+  const uint32_t rb = (a | 0xff00ff00u) - (b & 0x00ff00ffu);
+  return (ag & 0xff00ff00u) | (rb & 0x00ff00ffu);
+}
+
+static int u32_cmp(const void* a, const void* b) {
+  const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+  return x < y ? -1 : x > y;
+}
+
+static uint32_t comp_dist(uint32_t v) { return v <= 128 ? v : 256 - v; }
+
+/* model: minimize_deltas -- sort ascending (GetColorPalette), then
+ * PaletteSortMinimizeDeltas (src/utils/palette.c:155-207) in place */
+void vp8l_palette_order(uint32_t* pal, int n) {
+  qsort(pal, (size_t)n, sizeof(*pal), u32_cmp);
+  uint32_t pred = 0;
+  unsigned sign = 0;
+  for (int i = 0; i < n; ++i) {
+    const uint32_t d = sub_pixels(pal[i], pred);
+    const uint32_t rd = (d >> 16) & 255, gd = (d >> 8) & 255, bd = d & 255;
+    if (rd) sign |= rd < 0x80 ? 1 : 2;
+    if (gd) sign |= gd < 0x80 ? 8 : 16;
+    if (bd) sign |= bd < 0x80 ? 64 : 128;
+    pred = pal[i];
+  }
+  if (!(sign & (sign << 1))) return;
+  pred = 0;
+  for (int i = 0; i < n; ++i) {
+    int best_ix = i;
+    uint32_t best = ~0u;
+    for (int k = i; k < n; ++k) {
+      const uint32_t d = sub_pixels(pal[k], pred);
+      const uint32_t sc = 9 * (comp_dist(d & 255) + comp_dist((d >> 8) & 255) +
+                               comp_dist((d >> 16) & 255)) + comp_dist(d >> 24);
+      if (best > sc) { best = sc; best_ix = k; }
+    }
+    const uint32_t t = pal[best_ix]; pal[best_ix] = pal[i]; pal[i] = t;
+    pred = pal[i];
+  }
+}
 
 /* ---------------------------------------------------------------- Huffman */
 
@@ -363,11 +472,12 @@ static uint64_t data_bits(const Code* g, const uint32_t* h) {
 }
 
 /* model: encode() from the cluster histograms on */
-int vp8l_build_header(const vp8l_params* p, int has_alpha, const uint8_t* modes,
+int vp8l_build_header(const vp8l_params* p, int has_alpha, int emode, int cache_bits,
+                      const uint32_t* palette, int npal, const uint8_t* modes,
                       const uint32_t* mult, const uint32_t* hc, const uint8_t* assign,
                       vp8l_bw* bw, uint32_t* ctab, uint8_t* gtile) {
   const int W = p->w, H = p->h, tb = p->tb, hb = p->hb;
-  const int ntt = sub_sample(W, tb) * sub_sample(H, tb);
+  const int ntt = p->palette ? (npal > 0 ? npal : 1) : sub_sample(W, tb) * sub_sample(H, tb);
   const int nht = sub_sample(W, hb) * sub_sample(H, hb);
   int ok = 1;
   int remap[VP8L_KMAX], used[VP8L_KMAX], ng = 0;
@@ -377,6 +487,7 @@ int vp8l_build_header(const vp8l_params* p, int has_alpha, const uint8_t* modes,
     if (remap[k] == 0) { remap[k] = ng; used[ng++] = k; }
   uint32_t* tot = (uint32_t*)calloc(VP8L_NS, sizeof(uint32_t));
   uint32_t* pix = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(ntt > nht ? ntt : nht));
+  if (p->palette && (npal < 1 || npal > VP8L_MAX_PALETTE || !palette)) ok = 0;
   Code* groups = (Code*)malloc(sizeof(Code) * 5 * (size_t)(ng + 1));
   if (!tot || !pix || !groups) { ok = 0; goto done; }
   for (int g = 0; g < ng; ++g)
@@ -384,7 +495,7 @@ int vp8l_build_header(const vp8l_params* p, int has_alpha, const uint8_t* modes,
   /* the green alphabet has no cache symbols without a colour cache */
   int asize[5];
   for (int a = 0; a < 5; ++a) asize[a] = kAlphSize[a];
-  if (!p->cache_bits) asize[0] = 256 + 24;
+  asize[0] = 256 + 24 + (cache_bits ? 1 << cache_bits : 0);
   Code* single = groups + 5 * ng;
   for (int a = 0; a < 5; ++a) ok &= code_build(&single[a], tot + kAlphOff[a], asize[a]);
   for (int g = 0; g < ng; ++g)
@@ -413,25 +524,33 @@ int vp8l_build_header(const vp8l_params* p, int has_alpha, const uint8_t* modes,
     vp8l_bw_free(&tmp);
     meta = cm < cs;
   }
-  /* image header + transforms (subtract green, predictor, cross colour);
-   * the ALPH form has neither the image header nor subtract green */
+  /* image header + transforms; the ALPH form has no image header */
   if (!p->alpha) {
     vp8l_bw_put(bw, 0x2f, 8);
-    vp8l_bw_put(bw, (uint32_t)(W - 1), 14);
+    vp8l_bw_put(bw, (uint32_t)((p->palette ? p->ow : W) - 1), 14);
     vp8l_bw_put(bw, (uint32_t)(H - 1), 14);
     vp8l_bw_put(bw, has_alpha ? 1 : 0, 1);
     vp8l_bw_put(bw, 0, 3);
-    vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 2, 2);
   }
-  vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 0, 2); vp8l_bw_put(bw, (uint32_t)(tb - 2), 3);
-  for (int t = 0; t < ntt; ++t) pix[t] = 0xff000000u | ((uint32_t)modes[t] << 8);
-  ok &= write_sub_image(bw, pix, ntt);
-  vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 1, 2); vp8l_bw_put(bw, (uint32_t)(tb - 2), 3);
-  for (int t = 0; t < ntt; ++t) pix[t] = 0xff000000u | (mult[t] & 0xffffffu);
-  ok &= write_sub_image(bw, pix, ntt);
+  if (p->palette) {   /* COLOR_INDEXING, delta-coded palette (vp8l_enc.c:1412-1430) */
+    vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 3, 2); vp8l_bw_put(bw, (uint32_t)(npal - 1), 8);
+    for (int i = npal - 1; i >= 1; --i) pix[i] = sub_pixels(palette[i], palette[i - 1]);
+    pix[0] = palette[0];
+    ok &= write_sub_image(bw, pix, npal);
+  } else {
+    if (!p->alpha && (emode & VP8L_MODE_SUBGREEN)) { vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 2, 2); }
+    if (emode & VP8L_MODE_SPATIAL) {
+      vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 0, 2); vp8l_bw_put(bw, (uint32_t)(tb - 2), 3);
+      for (int t = 0; t < ntt; ++t) pix[t] = 0xff000000u | ((uint32_t)modes[t] << 8);
+      ok &= write_sub_image(bw, pix, ntt);
+      vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 1, 2); vp8l_bw_put(bw, (uint32_t)(tb - 2), 3);
+      for (int t = 0; t < ntt; ++t) pix[t] = 0xff000000u | (mult[t] & 0xffffffu);
+      ok &= write_sub_image(bw, pix, ntt);
+    }
+  }
   vp8l_bw_put(bw, 0, 1);
-  if (p->cache_bits) {
-    vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, (uint32_t)p->cache_bits, 4);
+  if (cache_bits) {
+    vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, (uint32_t)cache_bits, 4);
   } else {
     vp8l_bw_put(bw, 0, 1);
   }

@@ -31,18 +31,31 @@ int vp8l_transform_bits(int method, int histo_bits);
 /* candidate distances and their codes (model: candidate_distances,
  * distance_code); alpha != 0: the ALPH-chunk form (model: alpha_plane) */
 void vp8l_setup_params(vp8l_params* p, int w, int h, int n, int method, int alpha);
+/* the colour-indexing engine for w x h pictures bundled by xbits */
+void vp8l_setup_palette_params(vp8l_params* p, int w, int h, int n, int method, int xbits);
+
+/* model: bits_entropy_fx / entropy_choice -- the entropy mode (0..4,
+ * VP8L_MODE_*) from the 13 AnalyzeEntropy histograms; npal = colours when
+ * they fit a palette, else 0; ntiles = transform tiles */
+int64_t vp8l_bits_entropy_fx(const uint32_t* h, int n);
+int vp8l_entropy_choice(const uint32_t* ehist, int npal, int ntiles);
+/* model: minimize_deltas -- palette sorted, then reordered in place */
+void vp8l_palette_order(uint32_t* pal, int n);
 
 /* nlogn table (4097 entries, round(n log2 n * 4096)) and the log2 fraction
  * table (1024 entries) uploaded to the device */
 const int32_t* vp8l_nlogn_table(void);
 const int32_t* vp8l_flog2_table(void);
 
-/* Per-frame header. Inputs from the device: predictor modes and colour
- * multipliers per transform tile, cluster histograms hc (KMAX x NS) and the
- * cluster of each histogram tile. Outputs: the header bits (bw), the code
- * table ctab (KMAX x NS: code | bits << 16) and the code group of each
- * histogram tile (gtile). Returns 0 on allocation failure. */
-int vp8l_build_header(const vp8l_params* p, int has_alpha, const uint8_t* modes,
+/* Per-frame header. Inputs: the entropy mode (transforms written), the
+ * frame's colour-cache bits, the palette in stored order (palette engine);
+ * from the device: predictor modes and colour multipliers per transform tile
+ * (spatial modes), cluster histograms hc (KMAX x NS) and the cluster of each
+ * histogram tile. Outputs: the header bits (bw), the code table ctab (KMAX x
+ * NS: code | bits << 16) and the code group of each histogram tile (gtile).
+ * Returns 0 on allocation failure. */
+int vp8l_build_header(const vp8l_params* p, int has_alpha, int emode, int cache_bits,
+                      const uint32_t* palette, int npal, const uint8_t* modes,
                       const uint32_t* mult, const uint32_t* hc, const uint8_t* assign,
                       vp8l_bw* bw, uint32_t* ctab, uint8_t* gtile);
 

@@ -9,8 +9,12 @@
  *                                        predictor and cross-colour (L1)
  *   modes     N x ntt  uint8             predictor mode per transform tile
  *   mult      N x ntt  uint32            g2r | g2b << 8 | r2b << 16
- *   hits      N x ceil(npix/64) uint64   colour-cache hit bit per pixel (L2)
+ *   ehist     N x 13 x 256 uint32        AnalyzeEntropy histograms (L0)
+ *   pal       N x VP8L_PAL_STRIDE uint32 colour count (257 = too many) + colours (L0)
+ *   minb      N x npix uint8             smallest cache size holding the pixel (L2)
  *   ops       N x npix uint32            parse: act | len << 2 | dist_code << 15 (L3)
+ *   prov      N x npix uint16            provisional parse: act | len << 2 (L3)
+ *   chist     N x VP8L_CHIST uint32      cache-size choice histograms (L3)
  *   feat      N x nht  int64             histogram-tile entropy feature (L4)
  *   tl / tn   N x nht x tile_cap uint32  sparse tile histograms: symbol | count << 12,
  *             N x nht uint32             and their lengths (L4)
@@ -33,15 +37,33 @@ extern "C" {
 #endif
 
 #define VP8L_KMAX 16               /* max code groups (clusters) per frame */
-#define VP8L_CACHE_BITS 8          /* colour cache size (fixed) */
+#define VP8L_MAX_CACHE_BITS 9      /* largest colour cache (the size is chosen per frame) */
+#define VP8L_NEVER_HIT (VP8L_MAX_CACHE_BITS + 1)
 #define VP8L_CLUSTER_ITERS 6
 #define VP8L_MIN_COPY 3
 #define VP8L_MAX_LENGTH 4096
 #define VP8L_NUM_CAND 4            /* candidate distances: up, left, up-left, up-right */
-#define VP8L_GS (256 + 24 + (1 << VP8L_CACHE_BITS))
+#define VP8L_GS (256 + 24 + (1 << VP8L_MAX_CACHE_BITS))
 #define VP8L_NS (VP8L_GS + 3 * 256 + 40)   /* G | R | B | A | D */
 #define VP8L_BLOCK 1024            /* pixels per bit-writer block */
 #define VP8L_MAX_HUFF_IMAGE 2600   /* MAX_HUFF_IMAGE_SIZE, src/enc/vp8l_enc.c */
+#define VP8L_EHIST (13 * 256)      /* AnalyzeEntropy histograms (HistoIx order) */
+#define VP8L_PAL_STRIDE 260        /* count + up to 256 colours (+ pad) */
+#define VP8L_MAX_PALETTE 256
+/* cache-size choice histograms per frame: literal channels G,R,B,A per
+ * class c = minb (1..NEVER_HIT), cache keys (9 bits) per class 1..9, length
+ * prefixes of the provisional copies */
+#define VP8L_CH_LIT 0
+#define VP8L_CH_KEY (VP8L_NEVER_HIT * 1024)
+#define VP8L_CH_LEN (VP8L_CH_KEY + VP8L_MAX_CACHE_BITS * 512)
+#define VP8L_CHIST (VP8L_CH_LEN + 24)
+/* entropy modes (src/enc/vp8l_enc.c:38-46): bit 0 predictor + cross colour,
+ * bit 1 subtract green; 4 = palette (colour indexing) */
+#define VP8L_MODE_DIRECT 0
+#define VP8L_MODE_SPATIAL 1
+#define VP8L_MODE_SUBGREEN 2
+#define VP8L_MODE_SPATIAL_SUBGREEN 3
+#define VP8L_MODE_PALETTE 4
 
 /* entries of one sparse tile histogram: at most NS symbols, at most 4 per
  * pixel of a (1 << hb)^2 tile */
@@ -57,27 +79,47 @@ typedef struct {
   int alpha;                       /* ALPH mode: input is an alpha plane (1 B/px,
                                       coded as green), bare stream (no image
                                       header), no subtract green, no colour cache */
-  int cache_bits;                  /* VP8L_CACHE_BITS, or 0 in ALPH mode */
+  int cache_bits;                  /* largest cache size tried (VP8L_MAX_CACHE_BITS),
+                                      0 = no colour cache (ALPH mode) */
+  int palette;                     /* colour-indexing engine: w = packed width */
+  int xbits;                       /* palette bundling (0..3) */
+  int ow;                          /* picture width (w is the coded width) */
 } vp8l_params;
 
-/* L1: subtract green + per-tile predictor + cross colour. rgba frames at
- * fstride bytes, rows at rstride bytes. alpha_flag[f] |= 1 if any alpha
- * != 255. */
+/* L0: per frame (rgba frames at fstride bytes, rows at rstride) the 13
+ * AnalyzeEntropy histograms into ehist (n x VP8L_EHIST, zeroed by the
+ * caller) and the colour set into pal (n x VP8L_PAL_STRIDE: count, 257 when
+ * it exceeds VP8L_MAX_PALETTE, then the colours in no particular order). */
+int vp8l_launch_scan(const uint8_t* rgba, size_t fstride, int rstride, int w, int h, int n,
+                     uint32_t* ehist, uint32_t* pal, void* stream);
+/* L1: per slot f the input frame fidx[f] (NULL: f); entropy mode fmode[f]
+ * (0..3): subtract green (mode & 2), per-tile predictor + cross colour
+ * (mode & 1). sg_mask: bit 0 some slot without subtract green, bit 1 some
+ * with. alpha_flag[f] |= 1 if any alpha != 255. */
 int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rstride,
-                          const vp8l_params* p,
+                          const vp8l_params* p, const int* fidx, const uint8_t* fmode,
+                          int sg_mask,
                           uint32_t* argb, uint8_t* modes, uint32_t* mult,
                           uint32_t* alpha_flag, void* stream);
-/* L2..L5: cache hits, row parse, tile features, clustering. flog2: DEVICE
- * table (1024 entries) of the fraction of log2 in 1/4096 bit. */
-int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
-                        const int32_t* flog2, uint64_t* hits, uint32_t* ops,
-                        int64_t* feat, uint32_t* tl, uint32_t* tn, uint32_t* hc,
-                        uint8_t* assign, void* stream);
+/* L1 (palette engine): colour indexing with bundling. sorted: per slot the
+ * palette sorted ascending (VP8L_MAX_PALETTE entries), sidx: the index each
+ * sorted colour has in the stored palette, npal: palette sizes. */
+int vp8l_launch_palette_apply(const uint8_t* rgba, size_t fstride, int rstride,
+                              const vp8l_params* p, const int* fidx, const uint32_t* sorted,
+                              const uint8_t* sidx, const int* npal, uint32_t* argb,
+                              uint32_t* alpha_flag, void* stream);
+/* L2..L5: cache sizes, provisional parse, cache-size choice (cbits[f]),
+ * row parse, tile features, clustering. tabs: DEVICE tables (nlogn 4097 |
+ * log2 fraction 1024, in 1/4096 bit). */
+int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p, const int32_t* tabs,
+                        uint8_t* minb, uint16_t* prov, uint32_t* chist, uint8_t* cbits,
+                        uint32_t* ops, int64_t* feat, uint32_t* tl, uint32_t* tn,
+                        uint32_t* hc, uint8_t* assign, void* stream);
 /* L6/L7: per-block bit counts, per-frame scan from start_bit[f], and the
  * bit writer into out (n x out_cap bytes, zeroed except the header words the
  * host placed at the start). end_bit[f] = total payload bits. */
 int vp8l_launch_write(const uint32_t* argb, const uint32_t* ops,
-                      const vp8l_params* p, const uint32_t* ctab,
+                      const vp8l_params* p, const uint8_t* cbits, const uint32_t* ctab,
                       const uint8_t* gtile, const uint64_t* start_bit,
                       uint32_t* bsum, uint64_t* boff, uint64_t* end_bit,
                       uint8_t* out, size_t out_cap, void* stream);

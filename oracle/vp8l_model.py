@@ -77,6 +77,15 @@ def histo_bits(method, w, h):
     return min(max(b, 2), 9)
 
 
+def histo_bits_palette(method, w, h):
+    """GetHistoBits with use_palette (src/enc/vp8l_enc.c:234-245): 9 - method,
+    on the picture's own size."""
+    b = 9 - method
+    while sub_sample(w, b) * sub_sample(h, b) > MAX_HUFF_IMAGE_SIZE:
+        b += 1
+    return min(max(b, 2), 9)
+
+
 def transform_bits(method, hb):
     """GetTransformBits (src/enc/vp8l_enc.c:247-253)."""
     mx = 6 if method < 4 else (4 if method > 4 else 5)
@@ -282,17 +291,26 @@ def choose_cross_color(res, tb, H, W):
     return mult, out
 
 
-def transform_image(rgba, tb, subgreen=True):
-    """Subtract green (unless `subgreen` is off) -> predictor (per-tile best
-    of 14 by the bitlen score) -> cross colour. Returns (modes (tiles,), mult
-    (tiles,3), residual ARGB uint32 (H, W))."""
+# entropy modes (src/enc/vp8l_enc.c:38-46 EntropyIx): bit 0 = predictor +
+# cross colour, bit 1 = subtract green; 4 = palette
+DIRECT, SPATIAL, SUBGREEN, SPATIAL_SUBGREEN, PALETTE = 0, 1, 2, 3, 4
+
+
+def transform_image(rgba, tb, mode=SPATIAL_SUBGREEN):
+    """Subtract green (mode & 2) -> predictor (per-tile best of 14 by the
+    bitlen score) -> cross colour (both mode & 1). Returns (modes (tiles,),
+    mult (tiles,3), residual ARGB uint32 (H, W)); modes/mult are None without
+    the spatial transforms."""
     H, W, _ = rgba.shape
     a = rgba[..., 3].astype(np.int64); r = rgba[..., 0].astype(np.int64)
     g = rgba[..., 1].astype(np.int64); b = rgba[..., 2].astype(np.int64)
-    if subgreen:
+    if mode & SUBGREEN:
         P = np.stack([a, (r - g) & 255, g, (b - g) & 255], axis=-1)
     else:
         P = np.stack([a, r, g, b], axis=-1)
+    if not mode & SPATIAL:
+        argb = (P[..., 0] << 24) | (P[..., 1] << 16) | (P[..., 2] << 8) | P[..., 3]
+        return None, None, argb.astype(np.uint32)
     L, T, TL, TR = neighbours(P)
     fixed = fixed_mode_mask(H, W)
     preds = [predict(m, L, T, TL, TR) for m in range(14)]
@@ -338,6 +356,21 @@ def cache_hits(argb_flat, bits):
     return held == argb_flat
 
 
+MAX_CACHE_BITS = 9     # largest colour cache the GPU layout holds (VP8L_MAX_CACHE_BITS)
+NEVER_HIT = MAX_CACHE_BITS + 1
+
+
+def cache_minb(argb_flat):
+    """Per pixel the smallest cache size (bits 1..9) whose cache holds it, or
+    NEVER_HIT. Keys of size b are the top b bits of one hash, so a hit at b is
+    a hit at every larger size (the slot's most recent same-key pixel at b is
+    also the most recent one at b + 1): one number per pixel describes all."""
+    out = np.full(len(argb_flat), NEVER_HIT, dtype=np.int64)
+    for b in range(MAX_CACHE_BITS, 0, -1):
+        out[cache_hits(argb_flat, b)] = b
+    return out
+
+
 def match_lengths(argb, dists):
     """len[k, y, x]: run of argb[p+i] == argb[p+i-d] for candidate k, within
     the row (copies never cross a row end), capped at MAX_LENGTH."""
@@ -356,16 +389,15 @@ def match_lengths(argb, dists):
     return out
 
 
-def parse(argb, bits, dists):
+def parse(argb, hit, dists, lens=None):
     """Greedy parse, each row on its own (one GPU thread per row). Per pixel:
     act 0 literal, 1 cache hit, 2 copy start, 3 inside a copy; clen/ccode =
     length and distance code of a copy start. Rule: copy when the best
     candidate run is >= MIN_COPY, or == 2 and the pixel is no cache hit;
-    else cache hit; else literal."""
+    else cache hit; else literal. hit: (H, W) bool."""
     H, W = argb.shape
-    flat = argb.ravel()
-    hit = cache_hits(flat, bits).reshape(H, W)
-    lens = match_lengths(argb, dists)
+    if lens is None:
+        lens = match_lengths(argb, dists)
     best = np.argmax(lens, axis=0)                  # first maximum
     blen = np.take_along_axis(lens, best[None], axis=0)[0]
     dcode = np.array([distance_code(W, d) for d in dists], dtype=np.int64)
@@ -387,6 +419,34 @@ def parse(argb, bits, dists):
                 x += 1
     ccode = np.where(act == 2, dcode[best], 0)
     return act, clen, ccode
+
+
+def choose_cache_bits(argb, act, clen, minb):
+    """Colour-cache size of a frame (the role of CalculateBestCacheSize,
+    src/enc/backward_references_enc.c:756-851): over the pixels the
+    provisional parse codes as literal or cache hit, the estimated bits of
+    the green (+ length prefix + cache) / red / blue / alpha codes with each
+    size 0..MAX_CACHE_BITS; smallest wins (first on ties)."""
+    a = argb.ravel().astype(np.int64)
+    act = act.ravel(); minb = minb.ravel()
+    lit = act <= 1
+    la, lm = a[lit], minb[lit]
+    key9 = (((la.astype(np.uint64) * HASH_MUL) & 0xFFFFFFFF) >> (32 - MAX_CACHE_BITS)).astype(np.int64)
+    lp, _, _ = prefix_arrays(clen.ravel()[act == 2])
+    hlen = np.bincount(lp, minlength=NUM_LENGTH)
+    best, best_b = None, 0
+    for b in range(0, MAX_CACHE_BITS + 1):
+        inc = lm <= b if b else np.zeros(len(lm), dtype=bool)
+        L = la[~inc]
+        g = np.concatenate([np.bincount((L >> 8) & 255, minlength=256), hlen,
+                            np.bincount(key9[inc] >> (MAX_CACHE_BITS - b), minlength=1 << b)
+                            if b else np.zeros(0, np.int64)])
+        e = (bits_entropy_fx(g) + bits_entropy_fx(np.bincount((L >> 16) & 255, minlength=256)) +
+             bits_entropy_fx(np.bincount(L & 255, minlength=256)) +
+             bits_entropy_fx(np.bincount((L >> 24) & 255, minlength=256)))
+        if best is None or e < best:
+            best, best_b = e, b
+    return best_b
 
 
 def prefix_arrays(v):
@@ -756,29 +816,244 @@ def pack_fields(v, b, start_bit):
 DEFAULT_CACHE_BITS = 8
 
 
-def encode(rgba, method=4, cache_bits=DEFAULT_CACHE_BITS, kmax=KMAX, return_parts=False,
-           alpha_plane=False):
+# ---------------------------------------------------------------- palette
+
+MAX_PALETTE = 256
+
+
+def to_argb(rgba):
+    """(H, W, 4) RGBA bytes -> (H, W) ARGB words (the WebPPicture argb layout)."""
+    r = rgba.astype(np.uint32)
+    return (r[..., 3] << 24) | (r[..., 0] << 16) | (r[..., 1] << 8) | r[..., 2]
+
+
+def sub_pixels_u32(a, b):
+    """VP8LSubPixels (src/dsp/lossless_common.h): per-channel (a - b) & 255."""
+    a = np.asarray(a, dtype=np.uint64); b = np.asarray(b, dtype=np.uint64)
+    ag = ((a | 0x00ff00ff) + 0x100000000 - (b & 0xff00ff00)) & 0xff00ff00
+    rb = ((a | 0xff00ff00) + 0x100000000 - (b & 0x00ff00ff)) & 0x00ff00ff
+    return (ag | rb).astype(np.uint32)
+
+
+def hash_pix(p):
+    """HashPix (src/enc/vp8l_enc.c:81-85): the 8-bit palette-entropy proxy."""
+    p = np.asarray(p, dtype=np.uint64)
+    return ((((p + (p >> 19)) * 0x39c5fba7) & 0xFFFFFFFF) >> 24).astype(np.int64)
+
+
+def slog2_fx(v):
+    """v * log2(v) in 1/4096 bit (0 for v <= 1), fixed point via flog2."""
+    v = np.asarray(v, dtype=np.int64)
+    return np.where(v > 1, v * flog2(np.maximum(v, 1)), 0)
+
+
+def bits_entropy_fx(h):
+    """VP8LBitsEntropy (src/enc/histogram_enc.c:233-270) restated in integer
+    fixed point (1/4096 bit; the refine mixes as rationals): the estimate the
+    palette decision compares. Own arithmetic, so the model and the host C
+    take the same decision bit for bit."""
+    h = np.asarray(h, dtype=np.int64)
+    nz = h[h > 0]
+    nonzeros = len(nz)
+    if nonzeros <= 1:
+        return 0
+    s = int(nz.sum())
+    ent = int(slog2_fx(s)) - int(slog2_fx(nz).sum())
+    if nonzeros == 2:
+        return (99 * s * 4096 + ent) // 100
+    mix = 950 if nonzeros == 3 else 700 if nonzeros == 4 else 627
+    min_limit = (2 * s - int(nz.max())) * 4096
+    min_limit = (mix * min_limit + (1000 - mix) * ent) // 1000
+    return max(ent, min_limit)
+
+
+FLOG2_14 = int(flog2(14))
+FLOG2_24 = int(flog2(24))
+
+
+def analyze_entropy(argb, npal, tb):
+    """AnalyzeEntropy (src/enc/vp8l_enc.c:87-232): the entropy mode with the
+    smallest estimate among direct / spatial / subtract-green / spatial +
+    subtract-green (/ palette when npal > 0, i.e. the colours fit one);
+    first minimum wins. <= 16 colours always take the palette (:96-101).
+    Estimates in integer fixed point (bits_entropy_fx)."""
+    if 0 < npal <= 16:
+        return PALETTE
+    H, W = argb.shape
+    flat = argb.ravel().astype(np.uint32)
+    prev = np.concatenate([flat[:1], flat[:-1]])
+    diff = sub_pixels_u32(flat, prev)
+    keep = diff != 0
+    above = np.zeros(H * W, dtype=bool)
+    above[W:] = flat[W:] == flat[:-W]
+    keep &= ~above
+    pix = flat[keep].astype(np.int64); dif = diff[keep].astype(np.int64)
+    hs = entropy_histograms(pix, dif)
+    return entropy_choice(hs, npal, sub_sample(W, tb) * sub_sample(H, tb))
+
+
+def entropy_histograms(pix, dif):
+    """The 13 histograms of AnalyzeEntropy (HistoIx order, vp8l_enc.c:48-63)
+    over the pixels it keeps, with its +1 on the predicted zeros (:151-156)."""
+    def hist(v):
+        return np.bincount(v & 255, minlength=256).astype(np.int64)
+    hs = [hist(pix >> 24), hist(dif >> 24), hist(pix >> 8), hist(dif >> 8),
+          hist(pix >> 16), hist(dif >> 16), hist(pix), hist(dif),
+          hist((pix >> 16) - (pix >> 8)), hist((dif >> 16) - (dif >> 8)),
+          hist(pix - (pix >> 8)), hist(dif - (dif >> 8)),
+          np.bincount(hash_pix(pix), minlength=256).astype(np.int64)]
+    for i in (9, 11, 5, 3, 7, 1):
+        hs[i][0] += 1
+    return hs
+
+
+def entropy_choice(hs, npal, ntiles):
+    """vp8l_enc.c:158-201 on the 13 histograms."""
+    e = [bits_entropy_fx(h) for h in hs]
+    ent = [e[0] + e[4] + e[2] + e[6],
+           e[1] + e[5] + e[3] + e[7] + ntiles * FLOG2_14,
+           e[0] + e[8] + e[2] + e[10],
+           e[1] + e[9] + e[3] + e[11] + ntiles * FLOG2_24,
+           e[12] + npal * 8 * 4096]
+    last = PALETTE if npal > 0 else SPATIAL_SUBGREEN
+    best = DIRECT
+    for k in range(DIRECT + 1, last + 1):
+        if ent[best] > ent[k]:
+            best = k
+    return best
+
+
+def minimize_deltas(pal):
+    """PaletteSortMinimizeDeltas (src/utils/palette.c:155-207) on the sorted
+    palette: greedy nearest colour to the previous entry, unless every channel
+    develops monotonically."""
+    pal = [int(c) for c in pal]
+
+    def sub(a, b):
+        return int(sub_pixels_u32(a, b))
+
+    pred, sign = 0, 0
+    for c in pal:
+        d = sub(c, pred)
+        for sh, lo, hi in ((16, 1, 2), (8, 8, 16), (0, 64, 128)):
+            v = (d >> sh) & 255
+            if v:
+                sign |= lo if v < 0x80 else hi
+        pred = c
+    if not (sign & (sign << 1)):
+        return pal
+
+    def cdist(v):
+        return v if v <= 128 else 256 - v
+
+    def dist(a, b):
+        d = sub(a, b)
+        s = cdist(d & 255) + cdist((d >> 8) & 255) + cdist((d >> 16) & 255)
+        return s * 9 + cdist((d >> 24) & 255)
+
+    pred = 0
+    for i in range(len(pal)):
+        best_ix, best = i, None
+        for k in range(i, len(pal)):
+            s = dist(pal[k], pred)
+            if best is None or best > s:
+                best, best_ix = s, k
+        pal[i], pal[best_ix] = pal[best_ix], pal[i]
+        pred = pal[i]
+    return pal
+
+
+def palette_xbits(npal):
+    """pixel bundling of the colour-indexing transform (src/dec/vp8l_dec.c
+    :1356-1361 ReadTransform)."""
+    return 3 if npal <= 2 else 2 if npal <= 4 else 1 if npal <= 16 else 0
+
+
+def bundle(idx, xbits):
+    """VP8LBundleColorMap_C (src/dsp/lossless_enc.c): 2^xbits indices per
+    packed pixel in green, alpha 0xff."""
+    H, W = idx.shape
+    pw = sub_sample(W, xbits)
+    out = np.full((H, pw), 0xff000000, dtype=np.uint64)
+    bd = 8 >> xbits
+    for j in range(1 << xbits):
+        cols = idx[:, j::1 << xbits].astype(np.uint64)
+        out[:, :cols.shape[1]] |= cols << np.uint64(8 + bd * j)
+    return out.astype(np.uint32)
+
+
+def entropy_plan(rgba, method):
+    """(entropy mode, palette in stored order or None) of one picture."""
+    H, W, _ = rgba.shape
+    argb = to_argb(rgba)
+    cols = np.unique(argb)
+    npal = len(cols) if len(cols) <= MAX_PALETTE else 0
+    tb = transform_bits(method, histo_bits(method, W, H))
+    mode = analyze_entropy(argb, npal, tb)
+    return mode, (minimize_deltas(cols) if mode == PALETTE else None)
+
+
+AUTO_CACHE = -1
+
+
+def encode(rgba, method=4, cache_bits=AUTO_CACHE, kmax=KMAX, return_parts=False,
+           alpha_plane=False, emode=None):
     """rgba: (H, W, 4) uint8 -> .webp bytes (VP8L).
 
     alpha_plane=True: the ALPH-chunk form (src/enc/alpha_enc.c:50-98 +
     src/dec/alpha_dec.c): rgba is the alpha plane (H, W) uint8, coded as the
     green channel of an image with R = B = A = 0, as a bare VP8L stream (no
-    RIFF, no 5-byte image header, no colour cache), no subtract-green."""
+    RIFF, no 5-byte image header, no colour cache), no subtract-green.
+
+    The entropy mode comes from analyze_entropy (the reference's one guessed
+    crunch config at -m 1..5 / q < 100, src/enc/vp8l_enc.c:352-367) unless
+    `emode` forces a non-palette one: direct, spatial, subtract green,
+    spatial + subtract green, or -- for <= 256 colours -- the colour-indexing
+    transform alone (palette ordered by minimize_deltas, indices bundled).
+    cache_bits AUTO_CACHE: the size from choose_cache_bits after a
+    provisional parse with every cache hit of the largest size."""
     if alpha_plane:
         a = np.asarray(rgba, dtype=np.uint8)
         rgba = np.zeros(a.shape + (4,), dtype=np.uint8)
         rgba[..., 1] = a
         cache_bits = 0
     H, W, _ = rgba.shape
-    hb = histo_bits(method, W, H)
-    tb = transform_bits(method, hb)
-    modes, mult, argb = transform_image(rgba, tb, subgreen=not alpha_plane)
-    act, clen, ccode = parse(argb, cache_bits, candidate_distances(W))
+    if alpha_plane:
+        mode, pal = SPATIAL, None
+    elif emode is not None:
+        mode, pal = emode, None
+    else:
+        mode, pal = entropy_plan(rgba, method)
+    if pal is not None:
+        xbits = palette_xbits(len(pal))
+        lut = {c: i for i, c in enumerate(pal)}
+        argb0 = to_argb(rgba)
+        u, inv = np.unique(argb0, return_inverse=True)
+        idx = np.array([lut[int(c)] for c in u], dtype=np.int64)[inv.reshape(H, W)]
+        argb = bundle(idx, xbits)
+        hb = histo_bits_palette(method, W, H)
+        tb = 0
+        modes = mult = None
+    else:
+        hb = histo_bits(method, W, H)
+        tb = transform_bits(method, hb)
+        modes, mult, argb = transform_image(rgba, tb, mode)
+    PW = argb.shape[1]
+    dists = candidate_distances(PW)
+    lens = match_lengths(argb, dists)
+    if cache_bits == AUTO_CACHE:
+        minb = cache_minb(argb.ravel()).reshape(H, PW)
+        act, clen, _ = parse(argb, minb <= MAX_CACHE_BITS, dists, lens)
+        cache_bits = choose_cache_bits(argb, act, clen, minb)
+        hit = minb <= cache_bits
+    else:
+        hit = cache_hits(argb.ravel(), cache_bits).reshape(H, PW)
+    act, clen, ccode = parse(argb, hit, dists, lens)
     al = Alphabets(cache_bits)
     S, X = pixel_symbols(argb, act, clen, ccode, cache_bits, al)
-    tw, th = sub_sample(W, hb), sub_sample(H, hb)
+    tw, th = sub_sample(PW, hb), sub_sample(H, hb)
     nt = tw * th
-    tile = (np.arange(H) >> hb)[:, None] * tw + (np.arange(W) >> hb)[None, :]
+    tile = (np.arange(H) >> hb)[:, None] * tw + (np.arange(PW) >> hb)[None, :]
     Ht = tile_histograms(S, tile, nt, al)
     npix = np.bincount(tile.ravel(), minlength=nt)
     K = min(kmax, nt)
@@ -814,13 +1089,22 @@ def encode(rgba, method=4, cache_bits=DEFAULT_CACHE_BITS, kmax=KMAX, return_part
     if not alpha_plane:
         bw.put(0x2F, 8); bw.put(W - 1, 14); bw.put(H - 1, 14)
         bw.put(int((rgba[..., 3] != 255).any()), 1); bw.put(0, 3)
-        # SUBTRACT_GREEN, PREDICTOR, CROSS_COLOR (applied in this order)
-        bw.put(1, 1); bw.put(2, 2)
-    bw.put(1, 1); bw.put(0, 2); bw.put(tb - 2, 3)
-    write_sub_image(bw, [0xFF000000 | (int(m) << 8) for m in modes])
-    bw.put(1, 1); bw.put(1, 2); bw.put(tb - 2, 3)
-    write_sub_image(bw, [0xFF000000 | ((int(c[2]) & 255) << 16) | ((int(c[1]) & 255) << 8)
-                         | (int(c[0]) & 255) for c in mult])
+    if pal is not None:
+        # COLOR_INDEXING: size, then the delta-coded palette as a 1-row
+        # sub-image (src/enc/vp8l_enc.c:1412-1430, decoder :1346-1366)
+        bw.put(1, 1); bw.put(3, 2); bw.put(len(pal) - 1, 8)
+        write_sub_image(bw, [pal[0]] + [int(sub_pixels_u32(pal[i], pal[i - 1]))
+                                        for i in range(1, len(pal))])
+    else:
+        if mode & SUBGREEN:
+            # SUBTRACT_GREEN, PREDICTOR, CROSS_COLOR (applied in this order)
+            bw.put(1, 1); bw.put(2, 2)
+        if mode & SPATIAL:
+            bw.put(1, 1); bw.put(0, 2); bw.put(tb - 2, 3)
+            write_sub_image(bw, [0xFF000000 | (int(m) << 8) for m in modes])
+            bw.put(1, 1); bw.put(1, 2); bw.put(tb - 2, 3)
+            write_sub_image(bw, [0xFF000000 | ((int(c[2]) & 255) << 16) |
+                                 ((int(c[1]) & 255) << 8) | (int(c[0]) & 255) for c in mult])
     bw.put(0, 1)   # no more transforms
     if cache_bits:
         bw.put(1, 1); bw.put(cache_bits, 4)
@@ -850,7 +1134,8 @@ def encode(rgba, method=4, cache_bits=DEFAULT_CACHE_BITS, kmax=KMAX, return_part
         return out, dict(modes=modes, mult=mult, argb=argb, act=act, clen=clen, ccode=ccode,
                          assign=assign, groups=len(groups), header_bits=header_bits, tb=tb,
                          hb=hb, Hc=Hc, assign_raw=assign_raw, hc_raw=hc_raw, header=header,
-                         code=code, nb=nb, k=K)
+                         code=code, nb=nb, k=K, palette=pal,
+                         mode=mode, cache_bits=cache_bits)
     return out
 
 

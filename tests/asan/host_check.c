@@ -156,25 +156,39 @@ static void lossy_host_paths(void) {
 }
 
 static void lossless_host_paths(void) {
-  for (int it = 0; it < 12; ++it) {
+  for (int it = 0; it < 24; ++it) {
     const int w = rnd_in(1, 200), h = rnd_in(1, 200);
+    const int pal_engine = (it % 3) == 2;
+    const int npal = rnd_in(1, VP8L_MAX_PALETTE);
+    const int xb = npal <= 2 ? 3 : npal <= 4 ? 2 : npal <= 16 ? 1 : 0;
     vp8l_params p;
-    vp8l_setup_params(&p, w, h, 1, rnd_in(0, 6), it & 1);
-    const int ntt = ((w + (1 << p.tb) - 1) >> p.tb) * ((h + (1 << p.tb) - 1) >> p.tb);
-    const int nht = ((w + (1 << p.hb) - 1) >> p.hb) * ((h + (1 << p.hb) - 1) >> p.hb);
+    if (pal_engine) vp8l_setup_palette_params(&p, w, h, 1, rnd_in(0, 6), xb);
+    else vp8l_setup_params(&p, w, h, 1, rnd_in(0, 6), it & 1);
+    const int ntt = ((p.w + (1 << p.tb) - 1) >> p.tb) * ((h + (1 << p.tb) - 1) >> p.tb);
+    const int nht = ((p.w + (1 << p.hb) - 1) >> p.hb) * ((h + (1 << p.hb) - 1) >> p.hb);
     uint8_t* modes = (uint8_t*)malloc((size_t)ntt);
     uint32_t* mult = (uint32_t*)malloc((size_t)ntt * 4);
     uint32_t* hc = (uint32_t*)calloc((size_t)VP8L_KMAX * VP8L_NS, 4);
     uint32_t* ctab = (uint32_t*)calloc((size_t)VP8L_KMAX * VP8L_NS, 4);
     uint8_t* assign = (uint8_t*)malloc((size_t)nht);
     uint8_t* gtile = (uint8_t*)malloc((size_t)nht);
+    uint32_t pal[VP8L_MAX_PALETTE];
+    uint32_t eh[VP8L_EHIST];
+    for (int i = 0; i < npal; ++i) pal[i] = rnd() ^ ((uint32_t)i << 24);
+    vp8l_palette_order(pal, npal);
+    for (int i = 0; i < VP8L_EHIST; ++i) eh[i] = (rnd() & 3) ? 0 : rnd() & 0xfffff;
+    const int emode = vp8l_entropy_choice(eh, (it & 4) ? npal : 0, ntt);
+    CHECK(emode >= 0 && emode <= VP8L_MODE_PALETTE);
     const int k = rnd_in(1, VP8L_KMAX);
+    const int cb = p.alpha ? 0 : rnd_in(0, VP8L_MAX_CACHE_BITS);
     for (int i = 0; i < ntt; ++i) { modes[i] = (uint8_t)rnd_in(0, 13); mult[i] = rnd() & 0xffffff; }
     for (int i = 0; i < nht; ++i) assign[i] = (uint8_t)rnd_in(0, k - 1);
     for (int i = 0; i < k * VP8L_NS; ++i) hc[i] = (rnd() & 7) ? 0 : rnd() & 0xffff;
     vp8l_bw bw;
     vp8l_bw_init(&bw, 1 << 12);
-    CHECK(vp8l_build_header(&p, it & 2, modes, mult, hc, assign, &bw, ctab, gtile));
+    CHECK(vp8l_build_header(&p, it & 2, pal_engine ? VP8L_MODE_PALETTE : rnd_in(0, 3), cb,
+                            pal_engine ? pal : NULL, pal_engine ? npal : 0, modes, mult, hc,
+                            assign, &bw, ctab, gtile));
     (void)vp8l_bw_finish(&bw);
     vp8l_bw_free(&bw);
     free(modes); free(mult); free(hc); free(ctab); free(assign); free(gtile);

@@ -1,0 +1,49 @@
+"""Regenerate tests/golden/lossless_kat.json with the reference build
+(oracle/_ref/libwebp_ref.so, compiled from /root/reference by oracle/Makefile).
+Dev container only:  python tests/golden/make_lossless_golden.py
+
+Per case: the size of the reference encoder's `-lossless -m 4 -q 75` output
+and the transforms / colour-cache bits / palette size it reported
+(WebPAuxStats), for the synthetic pictures of tests/test_vp8l.py (syn-v1,
+palettised graphics, quantised syn-v1). The lossless parity contract is
+decode-exact + size within a tolerance of these.
+"""
+import ctypes
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+from libwebp_amd import abi  # noqa: E402
+from test_vp8l import lossless_picture  # noqa: E402
+
+CASES = [
+    # kind, w, h, frame
+    ("syn", 512, 512, 0), ("syn", 333, 257, 5), ("syn", 1920, 1080, 0),
+    ("g2", 320, 240, 1), ("g4", 320, 240, 2), ("g16", 320, 240, 3), ("g200", 320, 240, 4),
+    ("g16", 1920, 1080, 5), ("q3", 320, 240, 0), ("q4", 512, 384, 1), ("q6", 256, 256, 1),
+    ("q7", 400, 300, 2), ("q16", 320, 240, 3),
+]
+
+
+def main():
+    lib = abi.bind_encoder_api(ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libwebp_ref.so")))
+    out = []
+    for kind, w, h, f in CASES:
+        img = lossless_picture(kind, w, h, f)
+        data, st = abi.encode_rgba(lib, img, 75.0, 4, stats=True, lossless=1, use_argb=True)
+        out.append(dict(kind=kind, w=w, h=h, frame=f, size=len(data),
+                        features=st.lossless_features, cache_bits=st.cache_bits,
+                        palette_size=st.palette_size))
+        print(out[-1])
+    json.dump({"generator": "tests/golden/make_lossless_golden.py",
+               "reference": "libwebp 1.3.2 (oracle/_ref), -lossless -m 4 -q 75",
+               "cases": out}, open(os.path.join(HERE, "lossless_kat.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

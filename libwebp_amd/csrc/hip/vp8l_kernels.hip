@@ -507,6 +507,53 @@ __global__ __launch_bounds__(256) void k_vp8l_palapply(const uint8_t* __restrict
   if (__any(a_any) && lane_id() == 0) atomicOr(&alpha_flag[f], 1u);
 }
 
+// Near-lossless preprocessing, one pass (NearLossless,
+// src/enc/near_lossless_enc.c:63-101): an interior pixel whose 4-neighbourhood
+// is not smooth (some channel differs by >= 2^bits) snaps each channel to the
+// closest multiple of 2^bits (FindClosestDiscretized :27-34); border rows and
+// columns stay. in: frame fidx[f] (NULL: f) at fstride / rstride; out: slot f,
+// packed RGBA. One thread per pixel: each pass reads only the previous one.
+__device__ __forceinline__ uint32_t nl_snap(uint32_t a, int bits) {
+  const uint32_t mask = (1u << bits) - 1;
+  const uint32_t b = a + (mask >> 1) + ((a >> bits) & 1);
+  return b > 255 ? 255 : (b & ~mask);
+}
+// apply: per slot, 0 = copy (model: near_lossless_applies)
+__global__ __launch_bounds__(256) void k_vp8l_nearlossless(const uint8_t* __restrict__ in,
+                                                           size_t fstride, int rstride,
+                                                           const int* __restrict__ fidx, int W,
+                                                           int H, int bits,
+                                                           const uint8_t* __restrict__ apply,
+                                                           uint8_t* __restrict__ out) {
+  const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+  if (x >= W) return;
+  const uint8_t* img = in + (size_t)(fidx ? fidx[f] : f) * fstride;
+  const uint32_t c = *reinterpret_cast<const uint32_t*>(img + (size_t)y * rstride + 4 * x);
+  uint32_t o = c;
+  if (apply[f] && x > 0 && x < W - 1 && y > 0 && y < H - 1) {
+    const uint32_t nb[4] = {
+        *reinterpret_cast<const uint32_t*>(img + (size_t)y * rstride + 4 * (x - 1)),
+        *reinterpret_cast<const uint32_t*>(img + (size_t)y * rstride + 4 * (x + 1)),
+        *reinterpret_cast<const uint32_t*>(img + (size_t)(y - 1) * rstride + 4 * x),
+        *reinterpret_cast<const uint32_t*>(img + (size_t)(y + 1) * rstride + 4 * x)};
+    const int limit = 1 << bits;
+    bool smooth = true;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int sh = 0; sh < 32; sh += 8) {
+        const int d = (int)((c >> sh) & 255) - (int)((nb[k] >> sh) & 255);
+        smooth &= d < limit && d > -limit;
+      }
+    if (!smooth) {
+      o = 0;
+#pragma unroll
+      for (int sh = 0; sh < 32; sh += 8) o |= nl_snap((c >> sh) & 255, bits) << sh;
+    }
+  }
+  *reinterpret_cast<uint32_t*>(out + ((size_t)f * H + y) * W * 4 + 4 * x) = o;
+}
+
 // ------------------------------------------------------------------ L2
 
 // One wave per frame walks the pixels in stream order, 64 at a time, keeping
@@ -1285,6 +1332,27 @@ extern "C" int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rs
     }
   }
 #undef L1
+  return check_launch();
+}
+
+extern "C" int vp8l_launch_near_lossless(const uint8_t* rgba, size_t fstride, int rstride,
+                                         const int* fidx, const uint8_t* apply, int w, int h,
+                                         int n, int bits, uint8_t* buf0, uint8_t* buf1,
+                                         const uint8_t** out, void* stream) {
+  if (w <= 0 || h <= 0 || n <= 0 || bits < 1 || bits > 5 || (rstride & 3) || (fstride & 3) ||
+      ((uintptr_t)rgba & 3))
+    return 0;   // the pass reads whole RGBA words
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((w + 255) / 256, h, n);
+  uint8_t* bufs[2] = {buf0, buf1};
+  hipLaunchKernelGGL(k_vp8l_nearlossless, grid, dim3(256), 0, st, rgba, fstride, rstride, fidx, w,
+                     h, bits, apply, bufs[0]);
+  int cur = 0;
+  for (int i = bits - 1; i >= 1; --i, cur ^= 1)
+    hipLaunchKernelGGL(k_vp8l_nearlossless, grid, dim3(256), 0, st, (const uint8_t*)bufs[cur],
+                       (size_t)w * h * 4, w * 4, (const int*)nullptr, w, h, i, apply,
+                       bufs[cur ^ 1]);
+  *out = bufs[cur];
   return check_launch();
 }
 

@@ -81,11 +81,6 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   if (!WebPValidateConfig(config)) return NULL;
   WebPGpuBatch* b = (WebPGpuBatch*)calloc(1, sizeof(*b));
   if (!b) return NULL;
-  /* near-lossless (near_lossless_enc.c, and its residual quantisation inside
-   * the reference's predictor search, predictor_enc.c) is tied to the
-   * reference's transform choices, which the GPU VP8L encoder does not make:
-   * refused rather than silently encoded lossless */
-  if (config->lossless && config->near_lossless < 100) { free(b); return NULL; }
   if (config->lossless) {   /* VP8L engine (host/vp8l_batch.c) */
     b->device = device;
     b->w = width; b->h = height;
@@ -97,6 +92,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
     for (int i = 0; i < 6; ++i) CHK(hipEventCreate(&b->ev[i]));
     b->l = vp8l_engine_new(width, height, max_frames, config->method, 0);
     if (!b->l) goto fail;
+    vp8l_engine_set_near_lossless(b->l, config->near_lossless);
     return b;
   }
   vp8h_frame probe;

@@ -46,6 +46,7 @@ void vp8l_engine_free(vp8l_engine* l) {
   hipHostFree(l->h_ehist); hipHostFree(l->h_scan); hipHostFree(l->h_fidx); hipHostFree(l->h_fmode);
   hipHostFree(l->h_cbits); hipHostFree(l->h_psort); hipHostFree(l->h_psidx); hipHostFree(l->h_npal);
   free(l->h_pal);
+  hipFree(l->d_nl[0]); hipFree(l->d_nl[1]); hipFree(l->d_nlapply); hipHostFree(l->h_nlapply);
   hipFree(l->d_tabs); hipFree(l->d_argb); hipFree(l->d_modes); hipFree(l->d_mult);
   hipFree(l->d_aflag); hipFree(l->d_ops); hipFree(l->d_feat); hipFree(l->d_tl); hipFree(l->d_tn);
   hipFree(l->d_hc); hipFree(l->d_assign); hipFree(l->d_ctab); hipFree(l->d_gtile);
@@ -91,6 +92,8 @@ static vp8l_engine* engine_alloc(const vp8l_params* p, int max_frames, int metho
   CHK(hipMalloc((void**)&l->d_cbits, N));
   CHK(hipMalloc((void**)&l->d_fidx, N * sizeof(int)));
   CHK(hipMalloc((void**)&l->d_fmode, N));
+  CHK(hipMalloc((void**)&l->d_nlapply, N));
+  CHK(hipHostMalloc((void**)&l->h_nlapply, N, 0));
   CHK(hipHostMalloc((void**)&l->h_fidx, N * sizeof(int), 0));
   CHK(hipHostMalloc((void**)&l->h_fmode, N, 0));
   CHK(hipHostMalloc((void**)&l->h_cbits, N, 0));
@@ -159,6 +162,12 @@ vp8l_engine* vp8l_engine_new(int w, int h, int max_frames, int method, int alpha
   vp8l_params p;
   vp8l_setup_params(&p, w, h, max_frames, method, alpha);
   return engine_alloc(&p, max_frames, method, 1);
+}
+
+void vp8l_engine_set_near_lossless(vp8l_engine* l, int quality) {
+  const int bits = quality >= 100 ? 0 : 5 - quality / 20;   /* VP8LNearLosslessBits */
+  /* VP8ApplyNearLossless leaves pictures under 64x64 or 3 rows as they are */
+  l->nl_bits = ((l->p.w < 64 && l->p.h < 64) || l->p.h < 3 || l->p.alpha) ? 0 : bits;
 }
 
 static void route(const vp8l_engine* l, int f, const vp8l_engine** e, int* s) {
@@ -244,6 +253,7 @@ static int pipeline(vp8l_engine* l, hipStream_t st, int threads, const uint8_t* 
   double t0 = now_us(), t1, t2, t3, t4, t5;
   vp8l_params p = l->p;
   p.n = n;
+  const int* fidx_in = identity ? NULL : l->d_fidx;
   for (int f = 0; f < n; ++f) l->err[f] = VP8_ENC_OK;
   CHK(hipMemsetAsync(l->d_aflag, 0, N * sizeof(uint32_t), st));
   if (!identity) {
@@ -256,15 +266,33 @@ static int pipeline(vp8l_engine* l, hipStream_t st, int threads, const uint8_t* 
     CHK(hipMemcpyAsync(l->d_psidx, l->h_psidx, N * VP8L_MAX_PALETTE, hipMemcpyHostToDevice, st));
     CHK(hipMemcpyAsync(l->d_npal, l->h_npal, N * sizeof(int), hipMemcpyHostToDevice, st));
   }
+  int nl_any = 0;   /* model: near_lossless_applies (spatial modes from 2 bits on) */
+  if (l->nl_bits && !p.palette && !identity)
+    for (int f = 0; f < n; ++f) {
+      l->h_nlapply[f] = !(l->h_fmode[f] & VP8L_MODE_SPATIAL) || l->nl_bits >= 2;
+      nl_any |= l->h_nlapply[f];
+    }
+  if (nl_any) {   /* near-lossless passes into slot-indexed buffers */
+    const size_t fb = l->npix * 4;
+    for (int i = 0; i < 2; ++i)
+      if (!l->d_nl[i]) CHK(hipMalloc((void**)&l->d_nl[i], (size_t)l->max_frames * fb));
+    CHK(hipMemcpyAsync(l->d_nlapply, l->h_nlapply, N, hipMemcpyHostToDevice, st));
+    const uint8_t* nl = NULL;
+    if (!vp8l_launch_near_lossless(rgba, fstride, rstride, l->d_fidx, l->d_nlapply, p.w, p.h, n,
+                                   l->nl_bits, l->d_nl[0], l->d_nl[1], &nl, st))
+      goto fail;
+    rgba = nl; fstride = fb; rstride = p.w * 4;
+    fidx_in = NULL;
+  }
   CHK(hipEventRecord(l->ev[0], st));
   if (p.palette) {
-    if (!vp8l_launch_palette_apply(rgba, fstride, rstride, &p, identity ? NULL : l->d_fidx,
+    if (!vp8l_launch_palette_apply(rgba, fstride, rstride, &p, fidx_in,
                                    l->d_psort, l->d_psidx, l->d_npal, l->d_argb, l->d_aflag, st))
       goto fail;
   } else {
     int sg_mask = 0;
     for (int f = 0; f < n; ++f) sg_mask |= identity ? 1 : 1 << ((l->h_fmode[f] >> 1) & 1);
-    if (!vp8l_launch_transform(rgba, fstride, rstride, &p, identity ? NULL : l->d_fidx,
+    if (!vp8l_launch_transform(rgba, fstride, rstride, &p, fidx_in,
                                identity ? NULL : l->d_fmode, sg_mask, l->d_argb, l->d_modes,
                                l->d_mult, l->d_aflag, st))
       goto fail;

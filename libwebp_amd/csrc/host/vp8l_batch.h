@@ -37,6 +37,10 @@ typedef struct vp8l_engine {
   uint32_t* d_psort;           /* palette engine: sorted palette per slot */
   uint8_t* d_psidx;            /*   stored index of each sorted colour */
   int* d_npal;
+  int nl_bits;                 /* near-lossless limit bits (0 = lossless) */
+  uint8_t* d_nl[2];            /* near-lossless passes (max_frames x w*h*4), on demand */
+  uint8_t* d_nlapply;          /* per slot: preprocess (1) or copy (0) */
+  uint8_t* h_nlapply;
   uint8_t* d_modes;
   uint32_t* d_mult;
   uint32_t* d_aflag;
@@ -114,6 +118,10 @@ typedef struct {
 } vp8l_frame_info;
 void vp8l_engine_frame_info(const vp8l_engine* l, int f, vp8l_frame_info* info);
 void vp8l_engine_free(vp8l_engine* l);
+/* config->near_lossless (0..100) for the next calls: frames coded without a
+ * palette are first passed through VP8ApplyNearLossless (own choice for the
+ * spatial modes, see oracle/vp8l_model.py:encode) */
+void vp8l_engine_set_near_lossless(vp8l_engine* l, int quality);
 int vp8l_engine_run(struct WebPGpuBatch* b, const uint8_t* rgba, size_t fstride, int rstride,
                     int n);
 /* one call on `stream` (hipStream_t) with `threads` host threads; stage

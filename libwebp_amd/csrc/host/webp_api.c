@@ -268,8 +268,6 @@ static double psnr(uint64_t err, uint64_t size) {
  * fully transparent pixels zeroed unless `exact`, then the VP8L engine
  * (host/vp8l_batch.c) on one frame. */
 static int encode_lossless(const WebPConfig* config, WebPPicture* pic) {
-  /* near-lossless is not implemented by the GPU VP8L encoder (gpu_batch.c) */
-  if (config->near_lossless < 100) return set_error(pic, VP8_ENC_ERROR_INVALID_CONFIGURATION);
   if (pic->argb == NULL && !WebPPictureYUVAToARGB(pic)) return 0;
   const int w = pic->width, h = pic->height;
   uint8_t* rgba = (uint8_t*)malloc((size_t)w * h * 4);
@@ -286,6 +284,7 @@ static int encode_lossless(const WebPConfig* config, WebPPicture* pic) {
   }
   if (!report(pic, 5)) { free(rgba); return 0; }
   WebPGpuBatch* e = pool_get(config, w, h, 1);
+  if (e) vp8l_engine_set_near_lossless(e->l, config->near_lossless);   /* per call */
   int ok = e != NULL && WebPGpuBatchEncodeRGBAHost(e, rgba, (size_t)w * h * 4, 4 * w, 1);
   free(rgba);
   const int err = ok ? WebPGpuBatchError(e, 0) : VP8_ENC_ERROR_OUT_OF_MEMORY;

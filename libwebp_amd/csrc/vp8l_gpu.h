@@ -101,6 +101,13 @@ int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rstride,
                           int sg_mask,
                           uint32_t* argb, uint8_t* modes, uint32_t* mult,
                           uint32_t* alpha_flag, void* stream);
+/* Near-lossless preprocessing (VP8ApplyNearLossless): passes at bits .. 1
+ * from frame fidx[f] of rgba into slot f of buf0 / buf1 (n x w*h*4 each,
+ * packed RGBA), slots with apply[f] == 0 copied; *out = the buffer holding
+ * the last pass. */
+int vp8l_launch_near_lossless(const uint8_t* rgba, size_t fstride, int rstride, const int* fidx,
+                              const uint8_t* apply, int w, int h, int n, int bits,
+                              uint8_t* buf0, uint8_t* buf1, const uint8_t** out, void* stream);
 /* L1 (palette engine): colour indexing with bundling. sorted: per slot the
  * palette sorted ascending (VP8L_MAX_PALETTE entries), sidx: the index each
  * sorted colour has in the stored palette, npal: palette sizes. */

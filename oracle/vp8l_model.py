@@ -963,6 +963,73 @@ def minimize_deltas(pal):
     return pal
 
 
+def near_lossless_bits(quality):
+    """VP8LNearLosslessBits (src/dsp/lossless_common.h:57-65)."""
+    return 5 - quality // 20
+
+
+def _closest_discretized(a, bits):
+    """FindClosestDiscretized (src/enc/near_lossless_enc.c:27-34), per byte."""
+    mask = (1 << bits) - 1
+    biased = a + (mask >> 1) + ((a >> bits) & 1)
+    return np.where(biased > 255, 255, biased & ~mask)
+
+
+def near_lossless_pass(argb, bits):
+    """NearLossless (near_lossless_enc.c:63-101): interior pixels whose
+    4-neighbourhood is not smooth (a channel differs by >= 2^bits) snap every
+    channel to the closest multiple of 2^bits; border rows and columns stay."""
+    a = argb.astype(np.int64)
+    H, W = a.shape
+    out = a.copy()
+    if H < 3 or W < 3:
+        return out.astype(np.uint32)
+    limit = 1 << bits
+    c = a[1:-1, 1:-1]
+    smooth = np.ones(c.shape, dtype=bool)
+    for nb in (a[1:-1, :-2], a[1:-1, 2:], a[:-2, 1:-1], a[2:, 1:-1]):
+        for sh in (0, 8, 16, 24):
+            d = ((c >> sh) & 255) - ((nb >> sh) & 255)
+            smooth &= (d < limit) & (d > -limit)
+    q = np.zeros_like(c)
+    for sh in (0, 8, 16, 24):
+        q |= _closest_discretized((c >> sh) & 255, bits) << sh
+    out[1:-1, 1:-1] = np.where(smooth, c, q)
+    return out.astype(np.uint32)
+
+
+def near_lossless(argb, quality):
+    """VP8ApplyNearLossless (near_lossless_enc.c:110-144): passes at
+    limit_bits, limit_bits - 1, .., 1, each on the previous one's output;
+    pictures under 64x64 or under 3 rows stay as they are."""
+    H, W = argb.shape
+    bits = near_lossless_bits(quality)
+    if bits <= 0 or (W < 64 and H < 64) or H < 3:
+        return argb.astype(np.uint32).copy()
+    out = near_lossless_pass(argb, bits)
+    for i in range(bits - 1, 0, -1):
+        out = near_lossless_pass(out, i)
+    return out
+
+
+def near_lossless_applies(mode, quality):
+    """The reference preprocesses the direct / subtract-green modes with
+    VP8ApplyNearLossless (vp8l_enc.c:1536-1547) and quantises predictor
+    residuals for the spatial ones (predictor_enc.c:473-...), which is a
+    pixel-serial reconstruction this encoder does not reproduce. Here the
+    spatial modes take the preprocessing too from 2 limit bits on (quality <
+    80); at 1 bit it costs more than it saves ahead of the predictors, and
+    those frames stay lossless (inside any error bound)."""
+    if mode == PALETTE:
+        return False
+    return not (mode & SPATIAL) or near_lossless_bits(quality) >= 2
+
+
+def argb_to_rgba(argb):
+    a = argb.astype(np.uint32)
+    return np.stack([(a >> 16) & 255, (a >> 8) & 255, a & 255, a >> 24], axis=-1).astype(np.uint8)
+
+
 def palette_xbits(npal):
     """pixel bundling of the colour-indexing transform (src/dec/vp8l_dec.c
     :1356-1361 ReadTransform)."""
@@ -997,7 +1064,7 @@ AUTO_CACHE = -1
 
 
 def encode(rgba, method=4, cache_bits=AUTO_CACHE, kmax=KMAX, return_parts=False,
-           alpha_plane=False, emode=None):
+           alpha_plane=False, emode=None, near_lossless_q=100):
     """rgba: (H, W, 4) uint8 -> .webp bytes (VP8L).
 
     alpha_plane=True: the ALPH-chunk form (src/enc/alpha_enc.c:50-98 +
@@ -1011,7 +1078,10 @@ def encode(rgba, method=4, cache_bits=AUTO_CACHE, kmax=KMAX, return_parts=False,
     spatial + subtract green, or -- for <= 256 colours -- the colour-indexing
     transform alone (palette ordered by minimize_deltas, indices bundled).
     cache_bits AUTO_CACHE: the size from choose_cache_bits after a
-    provisional parse with every cache hit of the largest size."""
+    provisional parse with every cache hit of the largest size.
+
+    near_lossless_q < 100: frames that take no palette are first passed
+    through near_lossless when near_lossless_applies (see there)."""
     if alpha_plane:
         a = np.asarray(rgba, dtype=np.uint8)
         rgba = np.zeros(a.shape + (4,), dtype=np.uint8)
@@ -1037,6 +1107,8 @@ def encode(rgba, method=4, cache_bits=AUTO_CACHE, kmax=KMAX, return_parts=False,
     else:
         hb = histo_bits(method, W, H)
         tb = transform_bits(method, hb)
+        if near_lossless_q < 100 and not alpha_plane and near_lossless_applies(mode, near_lossless_q):
+            rgba = argb_to_rgba(near_lossless(to_argb(rgba), near_lossless_q))
         modes, mult, argb = transform_image(rgba, tb, mode)
     PW = argb.shape[1]
     dists = candidate_distances(PW)

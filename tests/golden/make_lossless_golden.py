@@ -7,8 +7,13 @@ and the transforms / colour-cache bits / palette size it reported
 (WebPAuxStats), for the synthetic pictures of tests/test_vp8l.py (syn-v1,
 palettised graphics, quantised syn-v1). The lossless parity contract is
 decode-exact + size within a tolerance of these.
+
+Near-lossless cases: the SHA-256 of the reference's VP8ApplyNearLossless
+output (src/enc/near_lossless_enc.c, exported by the reference build) as
+little-endian ARGB words, and the size of its `-near_lossless q` encode.
 """
 import ctypes
+import hashlib
 import json
 import os
 import sys
@@ -30,6 +35,30 @@ CASES = [
 ]
 
 
+NL_CASES = [
+    # kind, w, h, frame, near_lossless quality
+    ("syn", 96, 80, 0, 60), ("syn", 200, 130, 2, 0), ("syn", 200, 130, 2, 99),
+    ("q7", 120, 90, 3, 40), ("syn", 64, 3, 1, 20), ("syn", 63, 63, 4, 0), ("syn", 320, 240, 5, 80),
+]
+
+
+def ref_near_lossless(lib, img, q):
+    import numpy as np
+    h, w = img.shape[:2]
+    lib.VP8ApplyNearLossless.argtypes = [ctypes.POINTER(abi.WebPPicture), ctypes.c_int,
+                                         ctypes.c_void_p]
+    lib.VP8ApplyNearLossless.restype = ctypes.c_int
+    pic = abi.WebPPicture()
+    lib.WebPPictureInitInternal(ctypes.byref(pic), abi.WEBP_ENCODER_ABI_VERSION)
+    pic.width, pic.height, pic.use_argb = w, h, 1
+    rgba = np.ascontiguousarray(img)
+    assert lib.WebPPictureImportRGBA(ctypes.byref(pic), rgba.ctypes.data, 4 * w)
+    out = np.zeros((h, w), np.uint32)
+    assert lib.VP8ApplyNearLossless(ctypes.byref(pic), q, out.ctypes.data)
+    lib.WebPPictureFree(ctypes.byref(pic))
+    return out
+
+
 def main():
     lib = abi.bind_encoder_api(ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libwebp_ref.so")))
     out = []
@@ -40,9 +69,19 @@ def main():
                         features=st.lossless_features, cache_bits=st.cache_bits,
                         palette_size=st.palette_size))
         print(out[-1])
+    nl = []
+    for kind, w, h, f, q in NL_CASES:
+        img = lossless_picture(kind, w, h, f)
+        pre = ref_near_lossless(lib, img, q)
+        data, _ = abi.encode_rgba(lib, img, 75.0, 4, lossless=1, use_argb=True, near_lossless=q)
+        nl.append(dict(kind=kind, w=w, h=h, frame=f, near_lossless=q,
+                       argb_sha256=hashlib.sha256(pre.astype("<u4").tobytes()).hexdigest(),
+                       size=len(data)))
+        print(nl[-1])
     json.dump({"generator": "tests/golden/make_lossless_golden.py",
                "reference": "libwebp 1.3.2 (oracle/_ref), -lossless -m 4 -q 75",
-               "cases": out}, open(os.path.join(HERE, "lossless_kat.json"), "w"), indent=1)
+               "cases": out, "near_lossless": nl},
+              open(os.path.join(HERE, "lossless_kat.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":

@@ -104,6 +104,22 @@ def test_model_entropy_mode_and_size_vs_reference():
         assert len(data) <= c["size"] * (1 + kind_tol(c["kind"])), (c, len(data))
 
 
+def test_model_near_lossless_matches_reference_preprocessing():
+    """near_lossless == the reference's VP8ApplyNearLossless (committed
+    SHA-256s of its output; tests/golden/make_lossless_golden.py)"""
+    import hashlib
+    import json
+    kat = json.load(open(os.path.join(ROOT, "tests", "golden", "lossless_kat.json")))
+    for c in kat["near_lossless"]:
+        img = lossless_picture(c["kind"], c["w"], c["h"], c["frame"])
+        pre = M.near_lossless(M.to_argb(img), c["near_lossless"])
+        assert hashlib.sha256(pre.astype("<u4").tobytes()).hexdigest() == c["argb_sha256"], c
+        data = M.encode(img, near_lossless_q=c["near_lossless"])
+        mode = M.entropy_plan(img, 4)[0]
+        want = M.argb_to_rgba(pre) if M.near_lossless_applies(mode, c["near_lossless"]) else img
+        assert np.array_equal(decode(data), want), c
+
+
 def test_prefix_and_distance_codes():
     for v in list(range(1, 70)) + [4095, 4096, 100000]:
         s, nb, e = M.prefix_encode(v)
@@ -410,15 +426,25 @@ def test_gpu_1080p_palette_and_direct_sizes(gpu):
 
 
 @pytest.mark.gpu
-def test_gpu_near_lossless_fails_loudly(gpu):
-    """near_lossless < 100 (near_lossless_enc.c and the residual quantisation
-    inside the reference's predictor search, predictor_enc.c) is refused, not
-    silently encoded lossless."""
-    img = syn_v1(64, 48, 0)
-    with pytest.raises(RuntimeError):
-        gpu.encode_rgba(img, quality=75.0, method=4, lossless=1, use_argb=True, near_lossless=60)
-    with pytest.raises(RuntimeError):
-        gpu.GpuBatch(64, 48, 1, lossless=1, near_lossless=60)
+@pytest.mark.parametrize("kind,w,h,f,q", [("syn", 96, 80, 0, 60), ("syn", 200, 130, 2, 0),
+                                          ("q7", 120, 90, 3, 40), ("syn", 64, 3, 1, 20),
+                                          ("syn", 63, 63, 4, 0), ("g16", 96, 64, 3, 40)])
+def test_gpu_near_lossless(gpu, kind, w, h, f, q):
+    """near_lossless < 100 (VP8ApplyNearLossless preprocessing on the GPU for
+    the frames that take no palette): bit-exact with the model, decodes to
+    the preprocessed picture; small pictures and palettes stay lossless"""
+    img = lossless_picture(kind, w, h, f)
+    enc = gpu.GpuBatch(w, h, 1, quality=75.0, method=4, lossless=1, near_lossless=q)
+    import torch
+    buf = torch.from_numpy(np.ascontiguousarray(img[None])).to("cuda:0")
+    torch.cuda.synchronize()
+    enc.encode_device(buf.data_ptr(), 1)
+    got = enc.output(0)
+    enc.close()
+    assert got == M.encode(img, near_lossless_q=q)
+    data = gpu.encode_rgba(img, quality=75.0, method=4, lossless=1, use_argb=True, exact=1,
+                           near_lossless=q)
+    assert data == got
 
 
 @pytest.mark.gpu

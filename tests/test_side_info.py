@@ -40,9 +40,18 @@ def test_gpu_lossless_stats(gpu):
     data, st = gpu.encode_rgba(img, quality=75.0, method=4, lossless=1, use_argb=True, stats=True)
     assert st.coded_size == st.lossless_size == len(data)
     assert list(st.PSNR) == [99.0] * 5
-    assert st.lossless_features == 7 and st.cache_bits == 8 and st.palette_size == 0
+    from oracle import vp8l_model as M
+    _, P = M.encode(img, return_parts=True)
+    assert st.lossless_features == 7 and st.cache_bits == P["cache_bits"] and st.palette_size == 0
     assert 2 <= st.histogram_bits <= 9 and 2 <= st.transform_bits <= 9
     assert abs(st.lossless_hdr_size + st.lossless_data_size - (len(data) - 20)) <= 2
     _, m = abi.encode_rgba_map(gpu.load(), img, 2, quality=75.0, method=4, lossless=1,
                                use_argb=True)
     assert set(m) == {0}
+    # a palette picture: colour indexing reported (feature 8) with its size
+    from test_vp8l import graphics
+    g = graphics(96, 64, 16, 3)
+    _, P = M.encode(g, return_parts=True)
+    _, st = gpu.encode_rgba(g, quality=75.0, method=4, lossless=1, use_argb=True, stats=True)
+    assert st.lossless_features == 8 and st.palette_size == len(P["palette"])
+    assert st.cache_bits == P["cache_bits"]

@@ -35,7 +35,7 @@
 namespace {
 
 __device__ __forceinline__ int renorm(int& r) {   // range_ in [0, 254] -> [127, 254]
-  const int sh = __clz(r + 1) - 24;
+  const int sh = __builtin_clz((unsigned)r + 1u) - 24;   // r + 1 > 0: no clz(0) clamp
   r = ((r + 1) << sh) - 1;
   return sh;
 }
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void k_emit_resolve(uint16_t* __restrict__ tok
 
 // One range-chain step: returns the renormalisation shift.
 __device__ __forceinline__ int chain_step(int& r, uint32_t pb) {
-  const int split = (r * (int)(pb & 0xff)) >> 8;
+  const int split = (int)(__umul24((unsigned)r, pb & 0xff) >> 8);   // full-rate 24-bit multiply
   r = (pb >> 8) ? r - split - 1 : split;
   return renorm(r);
 }
@@ -84,79 +84,126 @@ __device__ __forceinline__ int chain_step(int& r, uint32_t pb) {
 // (a handful: the chains merge quickly). Segment 0 starts at 254.
 #define EMIT_IMG 256
 #define EMIT_SLOTS 16
-__global__ __launch_bounds__(128) void k_emit_img(const uint16_t* __restrict__ tokens,
+#define IMG_GROUP 16   // segments per workgroup, two at a time (128 ranges each)
+__global__ __launch_bounds__(256) void k_emit_img(const uint16_t* __restrict__ tokens,
                                                   size_t tok_cap,
                                                   const vp8g_emit_meta* __restrict__ meta,
                                                   uint8_t* __restrict__ img) {
-  __shared__ __align__(16) uint16_t stage[EMIT_IMG];
-  __shared__ uint32_t seen[4];
-  const int f = blockIdx.y, s = blockIdx.x, t = threadIdx.x;
+  __shared__ __align__(16) uint16_t stage[2][EMIT_IMG];
+  __shared__ uint32_t seen[2][4];
+  const int f = blockIdx.y, t = threadIdx.x, half = t >> 7, r_id = t & 127;
   const vp8g_emit_meta M = meta[f];
-  if ((uint32_t)s >= M.nseg) return;
-  uint8_t* out = img + ((size_t)M.seg_base + s) * (EMIT_SLOTS + 1);
-  if (s == 0) {
-    if (t == 0) { out[0] = 1; out[1] = 254; }
-    return;
-  }
-  const uint16_t* tok = tokens + (size_t)f * tok_cap + (size_t)s * EMIT_SEG - EMIT_IMG;
-  if (t < EMIT_IMG / 8)
-    *reinterpret_cast<uint4*>(stage + 8 * t) = *reinterpret_cast<const uint4*>(tok + 8 * t);
-  if (t < 4) seen[t] = 0;
-  __syncthreads();
-  int r = 127 + t;
-  for (int i = 0; i < EMIT_IMG; i += 8) {
-    const uint4 q = *reinterpret_cast<const uint4*>(stage + i);
-    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+  const uint16_t* ftok = tokens + (size_t)f * tok_cap;
+  for (int g = 0; g < IMG_GROUP; g += 2) {
+    const uint32_t s0 = blockIdx.x * IMG_GROUP + g;   // this pair: s0, s0 + 1
+    if (s0 >= M.nseg) break;                           // uniform over the workgroup
+    __syncthreads();                                   // previous pair's LDS reads done
+    if (t < 2 * EMIT_IMG / 8) {                        // 64 x 16 B: both segments' tails
+      const int h = t >> 5, q = t & 31;
+      const uint32_t s = s0 + h;
+      if (s > 0 && s < M.nseg)
+        *reinterpret_cast<uint4*>(&stage[h][8 * q]) =
+            *reinterpret_cast<const uint4*>(ftok + (size_t)s * EMIT_SEG - EMIT_IMG + 8 * q);
+    }
+    if (t < 8) seen[t >> 2][t & 3] = 0;
+    __syncthreads();
+    const uint32_t s = s0 + half;
+    const bool run = s > 0 && s < M.nseg;
+    int r = 127 + r_id;
+    if (run) {
+      for (int i = 0; i < EMIT_IMG; i += 8) {
+        const uint4 q = *reinterpret_cast<const uint4*>(&stage[half][i]);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-    for (int k = 0; k < 8; ++k) chain_step(r, (w[k >> 1] >> (16 * (k & 1))) & 0xffff);
-  }
-  atomicOr(&seen[(r - 127) >> 5], 1u << ((r - 127) & 31));
-  __syncthreads();
-  if (t == 0) {
-    int cnt = 0;
-    for (int wv = 0; wv < 4; ++wv) cnt += __popc(seen[wv]);
-    if (cnt > EMIT_SLOTS) {
-      out[0] = 0xff;   // too many: the map kernel covers all 128 ranges
-    } else {
-      out[0] = (uint8_t)cnt;
-      int k = 1;
-      for (int wv = 0; wv < 4; ++wv)
-        for (uint32_t m = seen[wv]; m; m &= m - 1) out[k++] = (uint8_t)(127 + 32 * wv + __ffs(m) - 1);
+        for (int k = 0; k < 8; ++k) chain_step(r, (w[k >> 1] >> (16 * (k & 1))) & 0xffff);
+      }
+      atomicOr(&seen[half][(r - 127) >> 5], 1u << ((r - 127) & 31));
+    }
+    __syncthreads();
+    if (r_id == 0 && s < M.nseg) {
+      uint8_t* out = img + ((size_t)M.seg_base + s) * (EMIT_SLOTS + 1);
+      if (s == 0) {   // segment 0 starts at 254
+        out[0] = 1; out[1] = 254;
+      } else {
+        int cnt = 0;
+        for (int wv = 0; wv < 4; ++wv) cnt += __popc(seen[half][wv]);
+        if (cnt > EMIT_SLOTS) {
+          out[0] = 0xff;   // too many: the map kernel covers all 128 ranges
+        } else {
+          out[0] = (uint8_t)cnt;
+          int k = 1;
+          for (int wv = 0; wv < 4; ++wv)
+            for (uint32_t m = seen[half][wv]; m; m &= m - 1)
+              out[k++] = (uint8_t)(127 + 32 * wv + __ffs(m) - 1);
+        }
+      }
     }
   }
 }
 
 // E1b: per segment, the end range and shift count from each possible start
-// range: 4 segments per wavefront, 16 lanes (start ranges) each.
+// range: 4 segments per wavefront, 16 lanes (start ranges) each. The 4
+// segments' tokens go through LDS 256 at a time (every lane loads 2 x 16 B
+// of the chunk; the next chunk is loaded into registers while this one runs),
+// so the chains read LDS broadcasts instead of waiting on global loads.
+#define MAP_CH 256
 __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ tokens,
                                                   size_t tok_cap,
                                                   const vp8g_emit_meta* __restrict__ meta,
                                                   const uint8_t* __restrict__ img,
                                                   uint8_t* __restrict__ emap,
                                                   uint16_t* __restrict__ eshift) {
-  const int f = blockIdx.y, lane = threadIdx.x;
+  __shared__ __align__(16) uint16_t stage[4][MAP_CH];
+  const int f = blockIdx.y, lane = threadIdx.x, grp = lane >> 4;
   const vp8g_emit_meta M = meta[f];
-  const uint32_t s = blockIdx.x * 4 + (lane >> 4);
+  const uint32_t sbase = blockIdx.x * 4;
+  const uint32_t s = sbase + grp;
   const int slot = lane & 15;
   const bool valid = s < M.nseg;
   const uint32_t cnt = valid ? min((uint32_t)EMIT_SEG, M.ntok - s * EMIT_SEG) : 0u;
   const uint8_t* im = img + ((size_t)M.seg_base + (valid ? s : 0)) * (EMIT_SLOTS + 1);
   const int ni = valid ? im[0] : 0;
   const int rounds = ni == 0xff ? 128 / EMIT_SLOTS : 1;
-  const uint16_t* tok = tokens + (size_t)f * tok_cap + (size_t)(valid ? s : 0) * EMIT_SEG;
-  for (int rd = 0; rd < rounds; ++rd) {
-    const bool live = valid && (ni == 0xff || slot < ni);
+  int rmax = 0;   // wave-uniform round count
+  for (int o = 1; o < 64; o <<= 1) rmax = max(rmax, __shfl_xor(rounds, o));
+  rmax = max(rmax, rounds);
+  const uint16_t* ftok = tokens + (size_t)f * tok_cap;
+  // this lane's two 16-byte pieces of a chunk: segment lane >> 4, parts (lane & 15) and +16
+  const uint32_t ls = sbase + (lane >> 4);
+  auto load = [&](uint32_t c0, uint4& a, uint4& b) {
+    a = b = make_uint4(0, 0, 0, 0);
+    if (ls < M.nseg) {
+      const uint32_t i = ls * EMIT_SEG + c0 + 8 * (lane & 15);
+      if (i < M.ntok) a = *reinterpret_cast<const uint4*>(ftok + i);
+      if (i + 128 < M.ntok) b = *reinterpret_cast<const uint4*>(ftok + i + 128);
+    }
+  };
+  for (int rd = 0; rd < rmax; ++rd) {
+    const bool live = valid && rd < rounds && (ni == 0xff || slot < ni);
     const int r0 = ni == 0xff ? 127 + EMIT_SLOTS * rd + slot : (live ? im[1 + slot] : 127);
     int r = r0;
     uint32_t S = 0;
-    const uint32_t full = cnt & ~7u;   // segment starts are 16-byte aligned
-    for (uint32_t i = 0; i < full; i += 8) {
-      const uint4 q = *reinterpret_cast<const uint4*>(tok + i);
-      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+    uint4 na, nb;
+    load(0, na, nb);
+    for (uint32_t c0 = 0; c0 < EMIT_SEG; c0 += MAP_CH) {
+      __syncthreads();   // the previous chunk's reads are done
+      *reinterpret_cast<uint4*>(&stage[lane >> 4][8 * (lane & 15)]) = na;
+      *reinterpret_cast<uint4*>(&stage[lane >> 4][128 + 8 * (lane & 15)]) = nb;
+      __syncthreads();
+      if (c0 + MAP_CH < EMIT_SEG) load(c0 + MAP_CH, na, nb);   // in flight during the chain
+      const uint32_t n = cnt > c0 ? min((uint32_t)MAP_CH, cnt - c0) : 0u;
+      const uint16_t* st = stage[grp];
+      if (n == MAP_CH) {
+        for (int i = 0; i < MAP_CH; i += 8) {
+          const uint4 q = *reinterpret_cast<const uint4*>(st + i);
+          const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-      for (int k = 0; k < 8; ++k) S += chain_step(r, (w[k >> 1] >> (16 * (k & 1))) & 0xffff);
+          for (int k = 0; k < 8; ++k) S += chain_step(r, (w[k >> 1] >> (16 * (k & 1))) & 0xffff);
+        }
+      } else {
+        for (uint32_t i = 0; i < n; ++i) S += chain_step(r, st[i]);   // frame's last segment
+      }
     }
-    for (uint32_t i = full; i < cnt; ++i) S += chain_step(r, tok[i]);   // frame's last segment
     if (live) {
       const size_t o = ((size_t)M.seg_base + s) * 128 + (r0 - 127);
       emap[o] = (uint8_t)r;
@@ -268,7 +315,7 @@ __global__ __launch_bounds__(64) void k_emit_seg(uint16_t* __restrict__ tokens, 
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const uint32_t pb = (w >> (16 * h)) & 0xffff;
-        const int split = (r * (int)(pb & 0xff)) >> 8;
+        const int split = (int)(__umul24((unsigned)r, pb & 0xff) >> 8);   // full-rate 24-bit multiply
         const int bit = (pb >> 8) & 1;
         const int c = bit ? split + 1 : 0;
         int rr = bit ? r - split - 1 : split;
@@ -387,7 +434,8 @@ extern "C" int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
     if (!vp8g_launch_check("k_emit_resolve")) return 0;
   }
   if (max_seg) {
-    hipLaunchKernelGGL(k_emit_img, dim3(max_seg, n), dim3(128), 0, st, (const uint16_t*)tokens,
+    hipLaunchKernelGGL(k_emit_img, dim3((max_seg + IMG_GROUP - 1) / IMG_GROUP, n), dim3(256), 0, st,
+                       (const uint16_t*)tokens,
                        tok_cap, (const vp8g_emit_meta*)meta, img);
     if (!vp8g_launch_check("k_emit_img")) return 0;
     hipLaunchKernelGGL(k_emit_maps, dim3((max_seg + 3) / 4, n), dim3(64), 0, st,

@@ -247,14 +247,33 @@ void vp8l_palette_order(uint32_t* pal, int n) {
 
 /* ---------------------------------------------------------------- Huffman */
 
-typedef struct { uint64_t w; int s; } Leaf;
-
-static int leaf_cmp(const void* a, const void* b) {
-  const Leaf* x = (const Leaf*)a;
-  const Leaf* y = (const Leaf*)b;
-  if (x->w != y->w) return x->w < y->w ? -1 : 1;
-  return x->s - y->s;
+/* leaves sorted by (weight, symbol): LSD radix sort of packed 64-bit keys
+ * weight << 12 | symbol, one 8-bit digit per pass up to the largest weight
+ * (the headers build ~200 codes per frame; qsort and its comparator calls
+ * were most of the host header time) */
+static void sort_keys(uint64_t* k, uint64_t* tmp, int n) {
+  if (n <= 48) {   /* insertion sort: cheaper than 256-bucket passes here */
+    for (int i = 1; i < n; ++i) {
+      const uint64_t v = k[i];
+      int j = i - 1;
+      while (j >= 0 && k[j] > v) { k[j + 1] = k[j]; --j; }
+      k[j + 1] = v;
+    }
+    return;
+  }
+  uint64_t mx = 0;
+  for (int i = 0; i < n; ++i) mx |= k[i];
+  for (int sh = 0; sh < 64 && (mx >> sh); sh += 8) {
+    uint32_t cnt[257] = {0};
+    for (int i = 0; i < n; ++i) cnt[((k[i] >> sh) & 255) + 1]++;
+    if (cnt[((k[0] >> sh) & 255) + 1] == (uint32_t)n) continue;   /* one digit value: no-op */
+    for (int d = 0; d < 256; ++d) cnt[d + 1] += cnt[d];
+    for (int i = 0; i < n; ++i) tmp[cnt[(k[i] >> sh) & 255]++] = k[i];
+    memcpy(k, tmp, sizeof(uint64_t) * (size_t)n);
+  }
 }
+
+#define HUFF_MAX_SYMS (VP8L_GS > 280 ? VP8L_GS : 280)
 
 /* model: huffman_lengths -- two-queue Huffman on (max(count, count_min),
  * symbol)-sorted leaves, count_min doubling until the depth fits. */
@@ -265,24 +284,21 @@ static int huffman_lengths(const uint32_t* hist, int n, int limit, uint8_t* len)
     if (hist[s]) { ++nu; last = s; }
   if (nu == 0) return 1;
   if (nu == 1) { len[last] = 1; return 1; }
-  Leaf* lv = (Leaf*)malloc(sizeof(Leaf) * nu);
-  uint64_t* iw = (uint64_t*)malloc(sizeof(uint64_t) * nu);
-  int* lpar = (int*)malloc(sizeof(int) * nu);
-  int* ipar = (int*)malloc(sizeof(int) * nu);
-  int* idep = (int*)malloc(sizeof(int) * nu);
-  int ok = lv && iw && lpar && ipar && idep;
-  for (uint64_t cmin = 1; ok; cmin *= 2) {
+  if (n > HUFF_MAX_SYMS) return 0;
+  uint64_t lv[HUFF_MAX_SYMS], tmp[HUFF_MAX_SYMS], iw[HUFF_MAX_SYMS];
+  int lpar[HUFF_MAX_SYMS], ipar[HUFF_MAX_SYMS], idep[HUFF_MAX_SYMS];
+  for (uint64_t cmin = 1;; cmin *= 2) {
     int k = 0;
     for (int s = 0; s < n; ++s)
-      if (hist[s]) { lv[k].w = hist[s] > cmin ? hist[s] : cmin; lv[k].s = s; ++k; }
-    qsort(lv, (size_t)nu, sizeof(Leaf), leaf_cmp);
+      if (hist[s]) lv[k++] = ((hist[s] > cmin ? (uint64_t)hist[s] : cmin) << 12) | (uint64_t)s;
+    sort_keys(lv, tmp, nu);
     int i1 = 0, i2 = 0, n2 = 0;
     while ((nu - i1) + (n2 - i2) > 1) {
       int node[2];
       uint64_t wsum = 0;
       for (int t = 0; t < 2; ++t) {
-        if (i2 >= n2 || (i1 < nu && lv[i1].w <= iw[i2])) {
-          wsum += lv[i1].w; node[t] = i1++;
+        if (i2 >= n2 || (i1 < nu && (lv[i1] >> 12) <= iw[i2])) {
+          wsum += lv[i1] >> 12; node[t] = i1++;
         } else {
           wsum += iw[i2]; node[t] = -1 - i2++;
         }
@@ -298,17 +314,31 @@ static int huffman_lengths(const uint32_t* hist, int n, int limit, uint8_t* len)
     int mx = 0;
     for (int j = 0; j < nu; ++j) {
       const int d = idep[lpar[j]] + 1;
-      len[lv[j].s] = (uint8_t)d;
+      len[lv[j] & 4095] = (uint8_t)d;
       if (d > mx) mx = d;
     }
     if (mx <= limit) break;
   }
-  free(lv); free(iw); free(lpar); free(ipar); free(idep);
-  return ok;
+  return 1;
+}
+
+static const uint8_t* rev8_table(void) {
+  static uint8_t t[256];
+  static int done = 0;
+  if (!done) {   /* benign race: every thread writes the same bytes */
+    for (int i = 0; i < 256; ++i) {
+      int r = 0;
+      for (int b = 0; b < 8; ++b) r |= ((i >> b) & 1) << (7 - b);
+      t[i] = (uint8_t)r;
+    }
+    __atomic_store_n(&done, 1, __ATOMIC_RELEASE);
+  }
+  return t;
 }
 
 /* model: canonical_codes (deflate order, bit-reversed for LSB-first) */
 static void canonical_codes(const uint8_t* len, int n, uint16_t* codes) {
+  const uint8_t* rv = rev8_table();
   int bl[17] = {0}, next[17] = {0};
   for (int s = 0; s < n; ++s) bl[len[s]]++;
   bl[0] = 0;
@@ -320,10 +350,9 @@ static void canonical_codes(const uint8_t* len, int n, uint16_t* codes) {
   for (int s = 0; s < n; ++s) {
     codes[s] = 0;
     if (!len[s]) continue;
-    const int c = next[len[s]]++;
-    int r = 0;
-    for (int i = 0; i < len[s]; ++i) r |= ((c >> i) & 1) << (len[s] - 1 - i);
-    codes[s] = (uint16_t)r;
+    const uint32_t c = (uint32_t)next[len[s]]++;
+    const uint32_t r16 = ((uint32_t)rv[c & 255] << 8) | rv[(c >> 8) & 255];
+    codes[s] = (uint16_t)(r16 >> (16 - len[s]));
   }
 }
 

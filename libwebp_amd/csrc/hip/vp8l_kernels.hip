@@ -167,7 +167,7 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
   const uint8_t* img = rgba + (size_t)(fidx ? fidx[f] : f) * fstride;
   const int tiles_x = (W + T - 1) / T;
   const int tile = blockIdx.y * tiles_x + blockIdx.x;
-  const int emode = p.alpha ? VP8L_MODE_SPATIAL : (int)fmode[f];
+  const int emode = fmode ? (int)fmode[f] : VP8L_MODE_SPATIAL;
   constexpr bool subgreen = SG;
   if (((emode & VP8L_MODE_SUBGREEN) != 0) != SG) return;
 
@@ -176,12 +176,18 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     uint32_t* out = argb_out + (size_t)f * W * H;
     for (int i = tid; i < tw * th; i += 256) {
       const int ly = i / tw, lx = i - ly * tw;
-      const uint8_t* q = img + (size_t)(y0 + ly) * rstride + 4 * (x0 + lx);
-      const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
-      any_alpha |= a != 255;
-      out[(size_t)(y0 + ly) * W + x0 + lx] =
-          subgreen ? (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255)
-                   : (a << 24) | (r << 16) | (g << 8) | b;
+      uint32_t v;
+      if (p.alpha) {   // ALPH: the alpha plane as green
+        const uint32_t g = img[(size_t)(y0 + ly) * rstride + x0 + lx];
+        v = subgreen ? (((0u - g) & 255) << 16) | (g << 8) | ((0u - g) & 255) : g << 8;
+      } else {
+        const uint8_t* q = img + (size_t)(y0 + ly) * rstride + 4 * (x0 + lx);
+        const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
+        any_alpha |= a != 255;
+        v = subgreen ? (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255)
+                     : (a << 24) | (r << 16) | (g << 8) | b;
+      }
+      out[(size_t)(y0 + ly) * W + x0 + lx] = v;
     }
     if (__any(any_alpha) && lane_id() == 0) atomicOr(&alpha_flag[f], 1u);
     return;
@@ -194,8 +200,9 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     const int y = y0 - 1 + ly, x = x0 - 1 + lx;
     uint32_t v = 0;
     if (y >= 0 && x >= 0 && x < W) {
-      if (p.alpha) {   // ALPH: the alpha plane as green, no subtract green
-        v = (uint32_t)img[(size_t)y * rstride + x] << 8;
+      if (p.alpha) {   // ALPH: the alpha plane as green
+        const uint32_t g = img[(size_t)y * rstride + x];
+        v = subgreen ? (((0u - g) & 255) << 16) | (g << 8) | ((0u - g) & 255) : g << 8;
       } else {
         const uint8_t* q = img + (size_t)y * rstride + 4 * x;
         const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
@@ -210,7 +217,8 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     for (int i = tid; i < th; i += 256) {
       const uint8_t* q = img + (size_t)(y0 + i) * rstride;
       if (p.alpha) {
-        S.first[i] = (uint32_t)q[0] << 8;
+        const uint32_t g = q[0];
+        S.first[i] = subgreen ? (((0u - g) & 255) << 16) | (g << 8) | ((0u - g) & 255) : g << 8;
       } else {
         const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
         S.first[i] = subgreen ? (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255)
@@ -363,6 +371,11 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
 __device__ __forceinline__ uint32_t rgba_argb(const uint8_t* q) {
   return ((uint32_t)q[3] << 24) | ((uint32_t)q[0] << 16) | ((uint32_t)q[1] << 8) | q[2];
 }
+// pixel x of a row: RGBA bytes, or (plane) an ALPH alpha byte as green
+// (WebPDispatchAlphaToGreen, src/enc/alpha_enc.c:73)
+__device__ __forceinline__ uint32_t pix_at(const uint8_t* row, int x, bool plane) {
+  return plane ? (uint32_t)row[x] << 8 : rgba_argb(row + 4 * x);
+}
 
 // AnalyzeEntropy's histograms (src/enc/vp8l_enc.c:87-141, HistoIx order
 // A, A', G, G', R, R', B, B', R-G, (R-G)', B-G, (B-G)', palette hash) over
@@ -371,7 +384,7 @@ __device__ __forceinline__ uint32_t rgba_argb(const uint8_t* q) {
 #define ENTROPY_BANDS 16
 __global__ __launch_bounds__(256) void k_vp8l_entropy(const uint8_t* __restrict__ rgba,
                                                       size_t fstride, int rstride, int W, int H,
-                                                      uint32_t* __restrict__ ehist) {
+                                                      int plane, uint32_t* __restrict__ ehist) {
   __shared__ uint32_t h[VP8L_EHIST];
   const int tid = threadIdx.x, f = blockIdx.y;
   const uint8_t* img = rgba + (size_t)f * fstride;
@@ -383,12 +396,12 @@ __global__ __launch_bounds__(256) void k_vp8l_entropy(const uint8_t* __restrict_
   for (long long i = tid; i < n; i += 256) {
     const int y = y0 + (int)(i / W), x = (int)(i % W);
     const uint8_t* row = img + (size_t)y * rstride;
-    const uint32_t pix = rgba_argb(row + 4 * x);
-    const uint32_t prev = x > 0 ? rgba_argb(row + 4 * (x - 1))
-                        : y > 0 ? rgba_argb(row - rstride + 4 * (W - 1)) : pix;
+    const uint32_t pix = pix_at(row, x, plane);
+    const uint32_t prev = x > 0 ? pix_at(row, x - 1, plane)
+                        : y > 0 ? pix_at(row - rstride, W - 1, plane) : pix;
     const uint32_t d = sub_pixels(pix, prev);
     if (d == 0) continue;
-    if (y > 0 && rgba_argb(row - rstride + 4 * x) == pix) continue;
+    if (y > 0 && pix_at(row - rstride, x, plane) == pix) continue;
     const int g = (int)(pix >> 8), gd = (int)(d >> 8);
     atomicAdd(&h[0 * 256 + (pix >> 24)], 1u);
     atomicAdd(&h[1 * 256 + (d >> 24)], 1u);
@@ -417,7 +430,7 @@ __global__ __launch_bounds__(256) void k_vp8l_entropy(const uint8_t* __restrict_
 // out: count (VP8L_MAX_PALETTE + 1 = too many) then the colours unordered.
 __global__ __launch_bounds__(256) void k_vp8l_palscan(const uint8_t* __restrict__ rgba,
                                                       size_t fstride, int rstride, int W, int H,
-                                                      uint32_t* __restrict__ pal) {
+                                                      int plane, uint32_t* __restrict__ pal) {
   __shared__ uint32_t keys[1024];
   __shared__ uint32_t cnt, zero, over, outn;
   const int tid = threadIdx.x, f = blockIdx.x;
@@ -431,7 +444,7 @@ __global__ __launch_bounds__(256) void k_vp8l_palscan(const uint8_t* __restrict_
   for (long long i = tid; i < n; i += 256) {
     if (*(volatile uint32_t*)&over) break;
     const int y = (int)(i / W), x = (int)(i % W);
-    const uint32_t pix = rgba_argb(img + (size_t)y * rstride + 4 * x);
+    const uint32_t pix = pix_at(img + (size_t)y * rstride, x, plane);
     if (have_last && pix == last) continue;
     last = pix; have_last = true;
     if (pix == 0) {
@@ -494,8 +507,8 @@ __global__ __launch_bounds__(256) void k_vp8l_palapply(const uint8_t* __restrict
   for (int j = 0; j < (1 << xb); ++j) {
     const int sx = (x << xb) + j;
     if (sx >= p.ow) break;
-    const uint32_t c = rgba_argb(row + 4 * sx);
-    a_any |= (c >> 24) != 255;
+    const uint32_t c = pix_at(row, sx, p.alpha != 0);
+    a_any |= !p.alpha && (c >> 24) != 255;
     int lo = 0, hi = np;   // sp[lo] <= c < sp[hi]
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
@@ -1300,12 +1313,13 @@ __global__ __launch_bounds__(256) void k_vp8l_pack(const uint8_t* __restrict__ o
 static int check_launch() { return hipGetLastError() == hipSuccess; }
 
 extern "C" int vp8l_launch_scan(const uint8_t* rgba, size_t fstride, int rstride, int w, int h,
-                                int n, uint32_t* ehist, uint32_t* pal, void* stream) {
+                                int n, int plane, uint32_t* ehist, uint32_t* pal, void* stream) {
   if (w <= 0 || h <= 0 || n <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_vp8l_entropy, dim3(ENTROPY_BANDS, n), dim3(256), 0, st, rgba, fstride,
-                     rstride, w, h, ehist);
-  hipLaunchKernelGGL(k_vp8l_palscan, dim3(n), dim3(256), 0, st, rgba, fstride, rstride, w, h, pal);
+                     rstride, w, h, plane, ehist);
+  hipLaunchKernelGGL(k_vp8l_palscan, dim3(n), dim3(256), 0, st, rgba, fstride, rstride, w, h, plane,
+                     pal);
   return check_launch();
 }
 
@@ -1315,7 +1329,7 @@ extern "C" int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rs
                                      uint32_t* alpha_flag, void* stream) {
   if (p->tb < 2 || p->tb > 6 || p->w <= 0 || p->h <= 0 || p->n <= 0) return 0;
   if (!p->alpha && !fmode) return 0;
-  if (p->alpha) sg_mask = 1;
+  if (!fmode) sg_mask = 1;
   dim3 grid((p->w + (1 << p->tb) - 1) >> p->tb, (p->h + (1 << p->tb) - 1) >> p->tb, p->n);
   hipStream_t st = (hipStream_t)stream;
 #define L1(T, SG)                                                                             \

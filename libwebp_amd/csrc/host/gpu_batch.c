@@ -264,7 +264,7 @@ static void frame_finish(WebPGpuBatch* b, int f) {
     } else {
       alpha.header = 1;   /* ALPHA_LOSSLESS_COMPRESSION, no filter */
       alpha.data = vp8l_engine_output(b->la, f);
-      alpha.size = b->la->out_size[f];
+      alpha.size = vp8l_engine_out_size(b->la, f);
     }
     if (b->cfg.alpha_quality < 100) alpha.header |= 1 << 4;   /* ALPHA_PREPROCESSED_LEVELS */
     ap = &alpha;
@@ -354,7 +354,9 @@ static int encode_alpha(WebPGpuBatch* b, int n) {
   }
   for (int f = 0; f < n; ++f) {
     if (!b->h_aflags[f]) continue;
-    if (b->cfg.alpha_compression && !b->la->err[f] && b->la->out_size[f] <= plane) continue;
+    if (b->cfg.alpha_compression && !vp8l_engine_error(b->la, f) &&
+        vp8l_engine_out_size(b->la, f) <= plane)
+      continue;
     b->araw[f] = (uint8_t*)malloc(plane);
     if (!b->araw[f] ||
         hipMemcpy(b->araw[f], b->d_aplane + (size_t)f * plane, plane, hipMemcpyDeviceToHost) !=

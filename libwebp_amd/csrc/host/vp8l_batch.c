@@ -97,7 +97,7 @@ static vp8l_engine* engine_alloc(const vp8l_params* p, int max_frames, int metho
   CHK(hipHostMalloc((void**)&l->h_fidx, N * sizeof(int), 0));
   CHK(hipHostMalloc((void**)&l->h_fmode, N, 0));
   CHK(hipHostMalloc((void**)&l->h_cbits, N, 0));
-  if (root && !l->p.alpha) {
+  if (root) {
     CHK(hipMalloc((void**)&l->d_ehist, N * VP8L_EHIST * sizeof(uint32_t)));
     CHK(hipMalloc((void**)&l->d_scan, N * VP8L_PAL_STRIDE * sizeof(uint32_t)));
     CHK(hipHostMalloc((void**)&l->h_ehist, N * VP8L_EHIST * sizeof(uint32_t), 0));
@@ -187,7 +187,7 @@ static void frame_header(vp8l_engine* l, int f) {
   vp8l_bw bw;
   const vp8l_params* p = &l->p;
   vp8l_bw_init(&bw, 1 << 16);
-  const int emode = p->palette ? VP8L_MODE_PALETTE : p->alpha ? VP8L_MODE_SPATIAL : l->h_fmode[f];
+  const int emode = p->palette ? VP8L_MODE_PALETTE : l->h_fmode[f];
   const int ok = vp8l_build_header(p, l->h_aflag[f] != 0, emode, l->h_cbits[f],
                                    p->palette ? l->h_pal + (size_t)f * VP8L_MAX_PALETTE : NULL,
                                    p->palette ? l->h_npal[f] : 0,
@@ -450,10 +450,10 @@ int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t*
   hipStream_t st = (hipStream_t)stream;
   const size_t N = (size_t)n;
   for (int i = 0; i < 10; ++i) timings[i] = 0.;
-  if (l->p.alpha) return pipeline(l, st, threads, rgba, fstride, rstride, n, 1, timings);
   const double t0 = now_us();
   CHK(hipMemsetAsync(l->d_ehist, 0, N * VP8L_EHIST * sizeof(uint32_t), st));
-  if (!vp8l_launch_scan(rgba, fstride, rstride, l->p.w, l->p.h, n, l->d_ehist, l->d_scan, st))
+  if (!vp8l_launch_scan(rgba, fstride, rstride, l->p.w, l->p.h, n, l->p.alpha, l->d_ehist,
+                        l->d_scan, st))
     goto fail;
   CHK(hipMemcpyAsync(l->h_ehist, l->d_ehist, N * VP8L_EHIST * sizeof(uint32_t),
                      hipMemcpyDeviceToHost, st));
@@ -476,7 +476,7 @@ int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t*
       if (!cnt[xb] || (l->sub[xb] && l->sub[xb]->max_frames >= cnt[xb])) continue;
       vp8l_engine_free(l->sub[xb]);
       vp8l_params pp;
-      vp8l_setup_palette_params(&pp, l->p.w, l->p.h, cnt[xb], l->method, xb);
+      vp8l_setup_palette_params(&pp, l->p.w, l->p.h, cnt[xb], l->method, xb, l->p.alpha);
       l->sub[xb] = engine_alloc(&pp, cnt[xb], l->method, 0);
       if (!l->sub[xb]) { free(mode); goto fail; }
     }
@@ -551,7 +551,7 @@ void vp8l_engine_frame_info(const vp8l_engine* l, int f, vp8l_frame_info* info) 
   const vp8l_engine* e; int s;
   route(l, f, &e, &s);
   memset(info, 0, sizeof(*info));
-  const int mode = e->p.palette ? VP8L_MODE_PALETTE : e->p.alpha ? VP8L_MODE_SPATIAL : e->h_fmode[s];
+  const int mode = e->p.palette ? VP8L_MODE_PALETTE : e->h_fmode[s];
   /* transforms used (vp8l_enc.c:1628-1632): 1 predictor, 2 cross colour,
    * 4 subtract green, 8 palette */
   info->features = mode == VP8L_MODE_PALETTE ? 8 :

@@ -128,9 +128,10 @@ void vp8l_setup_params(vp8l_params* p, int w, int h, int n, int method, int alph
 
 /* the colour-indexing engine: coded width = bundled width, tile bits from
  * GetHistoBits with use_palette on the picture size (vp8l_enc.c:234-245) */
-void vp8l_setup_palette_params(vp8l_params* p, int w, int h, int n, int method, int xbits) {
+void vp8l_setup_palette_params(vp8l_params* p, int w, int h, int n, int method, int xbits,
+                               int alpha) {
   const int pw = sub_sample(w, xbits);
-  vp8l_setup_params(p, pw, h, n, method, 0);
+  vp8l_setup_params(p, pw, h, n, method, alpha);
   p->palette = 1;
   p->xbits = xbits;
   p->ow = w;
@@ -567,7 +568,7 @@ int vp8l_build_header(const vp8l_params* p, int has_alpha, int emode, int cache_
     pix[0] = palette[0];
     ok &= write_sub_image(bw, pix, npal);
   } else {
-    if (!p->alpha && (emode & VP8L_MODE_SUBGREEN)) { vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 2, 2); }
+    if (emode & VP8L_MODE_SUBGREEN) { vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 2, 2); }
     if (emode & VP8L_MODE_SPATIAL) {
       vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 0, 2); vp8l_bw_put(bw, (uint32_t)(tb - 2), 3);
       for (int t = 0; t < ntt; ++t) pix[t] = 0xff000000u | ((uint32_t)modes[t] << 8);

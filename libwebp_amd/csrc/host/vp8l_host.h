@@ -31,8 +31,10 @@ int vp8l_transform_bits(int method, int histo_bits);
 /* candidate distances and their codes (model: candidate_distances,
  * distance_code); alpha != 0: the ALPH-chunk form (model: alpha_plane) */
 void vp8l_setup_params(vp8l_params* p, int w, int h, int n, int method, int alpha);
-/* the colour-indexing engine for w x h pictures bundled by xbits */
-void vp8l_setup_palette_params(vp8l_params* p, int w, int h, int n, int method, int xbits);
+/* the colour-indexing engine for w x h pictures bundled by xbits (alpha:
+ * ALPH planes) */
+void vp8l_setup_palette_params(vp8l_params* p, int w, int h, int n, int method, int xbits,
+                               int alpha);
 
 /* model: bits_entropy_fx / entropy_choice -- the entropy mode (0..4,
  * VP8L_MODE_*) from the 13 AnalyzeEntropy histograms; npal = colours when

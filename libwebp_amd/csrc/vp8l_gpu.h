@@ -89,9 +89,10 @@ typedef struct {
 /* L0: per frame (rgba frames at fstride bytes, rows at rstride) the 13
  * AnalyzeEntropy histograms into ehist (n x VP8L_EHIST, zeroed by the
  * caller) and the colour set into pal (n x VP8L_PAL_STRIDE: count, 257 when
- * it exceeds VP8L_MAX_PALETTE, then the colours in no particular order). */
+ * it exceeds VP8L_MAX_PALETTE, then the colours in no particular order).
+ * plane: the input is ALPH alpha planes (1 byte per pixel, coded as green). */
 int vp8l_launch_scan(const uint8_t* rgba, size_t fstride, int rstride, int w, int h, int n,
-                     uint32_t* ehist, uint32_t* pal, void* stream);
+                     int plane, uint32_t* ehist, uint32_t* pal, void* stream);
 /* L1: per slot f the input frame fidx[f] (NULL: f); entropy mode fmode[f]
  * (0..3): subtract green (mode & 2), per-tile predictor + cross colour
  * (mode & 1). sg_mask: bit 0 some slot without subtract green, bit 1 some

@@ -1070,7 +1070,9 @@ def encode(rgba, method=4, cache_bits=AUTO_CACHE, kmax=KMAX, return_parts=False,
     alpha_plane=True: the ALPH-chunk form (src/enc/alpha_enc.c:50-98 +
     src/dec/alpha_dec.c): rgba is the alpha plane (H, W) uint8, coded as the
     green channel of an image with R = B = A = 0, as a bare VP8L stream (no
-    RIFF, no 5-byte image header, no colour cache), no subtract-green.
+    RIFF, no 5-byte image header, no colour cache) -- WebPDispatchAlphaToGreen
+    + VP8LEncodeStream(use_cache = 0), src/enc/alpha_enc.c:50-98; its entropy
+    mode / palette come from the same analysis as a picture's.
 
     The entropy mode comes from analyze_entropy (the reference's one guessed
     crunch config at -m 1..5 / q < 100, src/enc/vp8l_enc.c:352-367) unless
@@ -1088,9 +1090,7 @@ def encode(rgba, method=4, cache_bits=AUTO_CACHE, kmax=KMAX, return_parts=False,
         rgba[..., 1] = a
         cache_bits = 0
     H, W, _ = rgba.shape
-    if alpha_plane:
-        mode, pal = SPATIAL, None
-    elif emode is not None:
+    if emode is not None:
         mode, pal = emode, None
     else:
         mode, pal = entropy_plan(rgba, method)

@@ -162,7 +162,7 @@ static void lossless_host_paths(void) {
     const int npal = rnd_in(1, VP8L_MAX_PALETTE);
     const int xb = npal <= 2 ? 3 : npal <= 4 ? 2 : npal <= 16 ? 1 : 0;
     vp8l_params p;
-    if (pal_engine) vp8l_setup_palette_params(&p, w, h, 1, rnd_in(0, 6), xb);
+    if (pal_engine) vp8l_setup_palette_params(&p, w, h, 1, rnd_in(0, 6), xb, it & 1);
     else vp8l_setup_params(&p, w, h, 1, rnd_in(0, 6), it & 1);
     const int ntt = ((p.w + (1 << p.tb) - 1) >> p.tb) * ((h + (1 << p.tb) - 1) >> p.tb);
     const int nht = ((p.w + (1 << p.hb) - 1) >> p.hb) * ((h + (1 << p.hb) - 1) >> p.hb);
@@ -180,7 +180,7 @@ static void lossless_host_paths(void) {
     const int emode = vp8l_entropy_choice(eh, (it & 4) ? npal : 0, ntt);
     CHECK(emode >= 0 && emode <= VP8L_MODE_PALETTE);
     const int k = rnd_in(1, VP8L_KMAX);
-    const int cb = p.alpha ? 0 : rnd_in(0, VP8L_MAX_CACHE_BITS);
+    const int cb = p.alpha ? 0 : rnd_in(0, VP8L_MAX_CACHE_BITS);   /* ALPH: no cache */
     for (int i = 0; i < ntt; ++i) { modes[i] = (uint8_t)rnd_in(0, 13); mult[i] = rnd() & 0xffffff; }
     for (int i = 0; i < nht; ++i) assign[i] = (uint8_t)rnd_in(0, k - 1);
     for (int i = 0; i < k * VP8L_NS; ++i) hc[i] = (rnd() & 7) ? 0 : rnd() & 0xffff;

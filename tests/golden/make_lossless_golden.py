@@ -59,6 +59,12 @@ def ref_near_lossless(lib, img, q):
     return out
 
 
+ALPH_CASES = [
+    # kind, w, h, frame, our tolerance (size ratio allowed)
+    ("logo", 512, 384, 0, 2.40), ("frame", 512, 384, 1, 1.15),
+]
+
+
 def main():
     lib = abi.bind_encoder_api(ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libwebp_ref.so")))
     out = []
@@ -78,9 +84,18 @@ def main():
                        argb_sha256=hashlib.sha256(pre.astype("<u4").tobytes()).hexdigest(),
                        size=len(data)))
         print(nl[-1])
+    from test_alpha import alpha_frame, logo_frame
+    from oracle import vp8l_model as M
+    al = []
+    for kind, w, h, f, tol in ALPH_CASES:
+        img = (logo_frame if kind == "logo" else alpha_frame)(w, h, f)
+        data, _ = abi.encode_rgba(lib, img, 75.0, 4)
+        al.append(dict(kind=kind, w=w, h=h, frame=f, alph_size=len(dict(M.riff_chunks(data))[b"ALPH"]),
+                       tol=tol))
+        print(al[-1])
     json.dump({"generator": "tests/golden/make_lossless_golden.py",
                "reference": "libwebp 1.3.2 (oracle/_ref), -lossless -m 4 -q 75",
-               "cases": out, "near_lossless": nl},
+               "cases": out, "near_lossless": nl, "alph": al},
               open(os.path.join(HERE, "lossless_kat.json"), "w"), indent=1)
 
 

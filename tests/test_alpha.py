@@ -36,6 +36,19 @@ def alpha_frame(w, h, f):
     return img
 
 
+def logo_frame(w, h, f):
+    """syn-v1 RGB with a logo-like alpha plane of three levels: an opaque
+    disc, a transparent background, half-transparent diagonal blocks (the
+    reference codes such planes with a palette)."""
+    img = syn_v1(w, h, f)
+    yy, xx = np.mgrid[0:h, 0:w]
+    a = np.zeros((h, w), np.uint8)
+    a[(xx - w / 2) ** 2 + (yy - h / 2) ** 2 < (min(w, h) / 3) ** 2] = 255
+    a[(xx // 8 + yy // 8 + f) % 5 == 0] = 128
+    img[..., 3] = a
+    return img
+
+
 def kat():
     return json.load(open(os.path.join(ROOT, "tests", "golden", "alpha_kat.json")))
 
@@ -101,6 +114,30 @@ def test_gpu_api_alpha(gpu):
                                alpha_compression=case["alpha_compression"],
                                alpha_quality=case["alpha_quality"])
         check(data, img, case)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,w,h,f,m", [("logo", 512, 384, 0, 4), ("frame", 200, 130, 3, 4),
+                                          ("logo", 97, 61, 2, 6), ("frame", 333, 257, 5, 2)])
+def test_gpu_alph_matches_model(gpu, kind, w, h, f, m):
+    """the ALPH payload (VP8L engine in ALPH mode, its entropy mode / palette
+    chosen per frame) equals the model's alpha-plane stream"""
+    img = (logo_frame if kind == "logo" else alpha_frame)(w, h, f)
+    data = gpu.encode_rgba(img, quality=75.0, method=m, exact=1)
+    alph = chunks(data)[b"ALPH"]
+    assert alph[0] & 3 == 1
+    assert alph[1:] == M.encode(img[..., 3], method=m, alpha_plane=True)
+
+
+def test_model_alph_size_vs_reference():
+    """ALPH sizes against the reference's (committed, lossless_kat.json):
+    the logo plane takes a palette like the reference's"""
+    k = json.load(open(os.path.join(ROOT, "tests", "golden", "lossless_kat.json")))
+    for c in k["alph"]:
+        img = (logo_frame if c["kind"] == "logo" else alpha_frame)(c["w"], c["h"], c["frame"])
+        data, P = M.encode(img[..., 3], method=4, alpha_plane=True, return_parts=True)
+        assert (P["palette"] is not None) == (c["kind"] == "logo")
+        assert len(data) + 1 <= c["alph_size"] * c["tol"], (c, len(data) + 1)
 
 
 def test_quantize_levels_model_matches_reference():

@@ -165,7 +165,8 @@ def host_lib(tmp_path_factory):
                                       vp, vp, vp]
     lib.vp8l_entropy_choice.argtypes = [vp, C.c_int, C.c_int]
     lib.vp8l_palette_order.argtypes = [vp, C.c_int]
-    lib.vp8l_setup_palette_params.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
+    lib.vp8l_setup_palette_params.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                              C.c_int]
     lib.vp8l_bw_finish.restype = C.c_size_t
     lib.vp8l_bw_finish.argtypes = [vp]
     lib.vp8l_bw_init.argtypes = [vp, C.c_size_t]
@@ -266,12 +267,16 @@ def test_palette_helpers_match_model(host_lib):
     (1, 1, 0, False, 4, False, "syn"), (256, 192, 2, False, 4, False, "syn"),
     (200, 130, 6, True, 4, False, "syn"), (160, 96, 1, False, 6, False, "syn"),
     (97, 61, 2, False, 3, False, "syn"), (120, 77, 1, False, 4, True, "syn"),
-    (1, 1, 0, False, 4, True, "syn"), (96, 64, 1, False, 4, False, "g2"),
+    (1, 1, 0, False, 4, True, "syn"), (96, 64, 1, False, 4, True, "logo"),
+    (200, 130, 3, False, 4, True, "frame"), (96, 64, 1, False, 4, False, "g2"),
     (101, 67, 2, False, 4, False, "g4"), (90, 70, 3, False, 4, False, "g16"),
     (96, 64, 4, False, 4, False, "g200"), (80, 60, 0, False, 4, False, "q7"),
     (80, 60, 1, False, 4, False, "q4")])
 def test_host_header_matches_model(host_lib, w, h, f, alpha, method, plane, kind):
-    if plane:
+    if plane and kind in ("logo", "frame"):   # the ALPH planes of tests/test_alpha.py
+        from test_alpha import alpha_frame, logo_frame
+        img = (logo_frame if kind == "logo" else alpha_frame)(w, h, f)[..., 3]
+    elif plane:
         img = alpha_plane(w, h, f)
     elif kind == "syn":
         img = syn_v1(w, h, f)
@@ -285,7 +290,8 @@ def test_host_header_matches_model(host_lib, w, h, f, alpha, method, plane, kind
     p = Params()
     pal = P["palette"]
     if pal is not None:
-        host_lib.vp8l_setup_palette_params(C.byref(p), w, h, 1, method, M.palette_xbits(len(pal)))
+        host_lib.vp8l_setup_palette_params(C.byref(p), w, h, 1, method, M.palette_xbits(len(pal)),
+                                           int(plane))
         assert (p.hb, p.k, p.w) == (P["hb"], P["k"], P["argb"].shape[1])
     else:
         host_lib.vp8l_setup_params(C.byref(p), w, h, 1, method, int(plane))

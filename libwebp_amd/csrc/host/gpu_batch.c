@@ -432,20 +432,23 @@ static int lowmem_passes(WebPGpuBatch* b, int n) {
       return 0;
     CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
                        hipMemcpyDeviceToHost, st));
+    const int probe = nb < (int)nmb;   /* method 3: OneStatPass covers the first nb MBs */
+    if (probe)
+      CHK(hipMemcpyAsync(b->h_mbinfo, b->d_mbinfo, n * nmb * VP8G_MBINFO_BYTES,
+                         hipMemcpyDeviceToHost, st));
     CHK(hipStreamSynchronize(st));
     for (int f = 0; f < n; ++f) {
       if (!act[f]) continue;
       vp8h_frame* fr = &b->frames[f];
       const vp8g_frame_result* R = &b->h_results[f];
       if (R->error) { act[f] = 0; continue; }
-      const uint64_t size_p0 = R->size_p0 + (uint64_t)fr->seg_hdr_size;   /* all MBs */
-      if (b->cfg.method == 3 && size_p0 > VP8H_P0_LIMIT) {
-        /* the probe covers half the frame: its estimate is not K3's */
-        b->err[f] = VP8_ENC_ERROR_INVALID_CONFIGURATION;
-        act[f] = 0;
-        continue;
-      }
-      act[f] = vp8h_pass_finish(fr, size_p0) && vp8h_pass_start(fr);
+      /* size_p0 of the probe (frame_enc.c:596, 651-655): K3 sums every MB's
+       * info.H; the probe's sum comes from the MBs' modes */
+      const uint64_t hdr = probe ? vp8h_mode_header_bits(
+                                       b->h_mbinfo + (size_t)f * nmb * VP8G_MBINFO_BYTES,
+                                       fr->mbw, nb)
+                                 : R->size_p0;
+      act[f] = vp8h_pass_finish(fr, hdr + (uint64_t)fr->seg_hdr_size) && vp8h_pass_start(fr);
     }
   }
   /* FinalizeSkipProba + FinalizeTokenProbas + VP8CalculateLevelCosts */

@@ -180,6 +180,37 @@ double vp8h_pass_size_value(uint64_t finalize_cost, uint64_t token_bits, uint64_
   return (double)(size + HEADER_SIZE_ESTIMATE);
 }
 
+/* Sum of the per-MB header-bit estimates info.H (OneStatPass,
+ * frame_enc.c:588-596) of MBs 0..nb-1 from their coded modes: an intra-16
+ * MB's VP8FixedCostsI16[mode], an intra-4 MB's 211 plus each sub-block's
+ * VP8FixedCostsI4[top][left][mode] (contexts from the neighbour MBs' modes, 0
+ * outside the frame; an intra-16 MB lends its mode to all 16 contexts), plus
+ * VP8FixedCostsUV[uv mode] (quant_enc.c:1002-1217). */
+uint64_t vp8h_mode_header_bits(const uint8_t* mbinfo, int mbw, int nb) {
+  uint64_t sum = 0;
+  for (int mb = 0; mb < nb; ++mb) {
+    const uint8_t* in = mbinfo + (size_t)mb * VP8G_MBINFO_BYTES;
+    const uint8_t* m = in + 4;
+    const int x = mb % mbw;
+    uint32_t H;
+    if (in[0]) {
+      H = kVP8ModeCostI16[m[0]];
+    } else {
+      const uint8_t* top = mb >= mbw ? mbinfo + (size_t)(mb - mbw) * VP8G_MBINFO_BYTES + 4 : NULL;
+      const uint8_t* left = x > 0 ? mbinfo + (size_t)(mb - 1) * VP8G_MBINFO_BYTES + 4 : NULL;
+      H = 211;
+      for (int i = 0; i < 16; ++i) {
+        const int bx = i & 3, by = i >> 2;
+        const int t = by > 0 ? m[i - 4] : top ? top[12 + bx] : 0;
+        const int l = bx > 0 ? m[i - 1] : left ? left[4 * by + 3] : 0;
+        H += kVP8ModeCostI4[t][l][m[i]];
+      }
+    }
+    sum += H + kVP8ModeCostUV[in[1]];
+  }
+  return sum;
+}
+
 double vp8h_psnr(uint64_t mse, uint64_t count) {
   return (mse > 0 && count > 0) ? 10. * log10(255. * 255. * count / mse) : 99;
 }

@@ -91,6 +91,10 @@ int vp8h_finalize_probas(const uint32_t* stats, uint8_t* coeffs, int* dirty);
  * bit estimate (VP8EstimateTokenSize) and the header estimate */
 double vp8h_pass_size_value(uint64_t finalize_cost, uint64_t token_bits, uint64_t size_p0);
 double vp8h_psnr(uint64_t mse, uint64_t count);   /* GetPSNR, frame_enc.c:554-556 */
+/* sum of the header-bit estimates info.H of MBs 0..nb-1 from their modes
+ * (mbinfo rows of VP8G_MBINFO_BYTES): the probe's size_p0 before the
+ * segment header */
+uint64_t vp8h_mode_header_bits(const uint8_t* mbinfo, int mbw, int nb);
 
 /* Dithered import (preprocessing & 2): the amplitude WebPEncode derives from
  * the quality (webp_enc.c:357-365, 0 when off), and the rounding terms the

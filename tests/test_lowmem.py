@@ -34,6 +34,10 @@ CASES = [
     (240, 160, 6, {"quality": 70.0, "method": 4, "autofilter": 1, "sns_strength": 90}),
     (128, 96, 5, {"quality": 10.0, "method": 6, "filter_strength": 0}),
     (1920, 1080, 0, {"quality": 75.0, "method": 4}),
+    # method 3 checks partition 0 on its half-frame probe (frame_enc.c:614-655):
+    # the whole frame's header estimate is over PARTITION0_SIZE_LIMIT, the
+    # probe's is not, so the reference encodes it in one pass
+    (5120, 5120, 0, {"quality": 95.0, "method": 3}),
     # methods 0-2 already run VP8EncLoop: low_memory changes nothing there
     # (webp_enc.c:115-122), the bytes equal the encode without the flag
     (176, 144, 2, {"quality": 70.0, "method": 0}),

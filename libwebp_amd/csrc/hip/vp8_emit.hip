@@ -15,7 +15,8 @@
 //                      states of the previous segment's last 256 tokens run
 //                      from all 128 ranges; typically 4-10 survive)
 //      k_emit_maps     per segment, the end range and shift count from each
-//                      of those start ranges (16 lanes per segment)
+//                      of those start ranges (the group's (segment, start)
+//                      pairs packed densely onto the lanes)
 //   E2 k_emit_compose  per frame, chain the segment maps: every segment's true
 //                      start range and bit offset, pad bits, S and L
 //   E3 k_emit_seg      per segment (one lane each): forward pass with the true
@@ -142,63 +143,84 @@ __global__ __launch_bounds__(256) void k_emit_img(const uint16_t* __restrict__ t
 }
 
 // E1b: per segment, the end range and shift count from each possible start
-// range: 4 segments per wavefront, 16 lanes (start ranges) each. The 4
-// segments' tokens go through LDS 256 at a time (every lane loads 2 x 16 B
-// of the chunk; the next chunk is loaded into registers while this one runs),
-// so the chains read LDS broadcasts instead of waiting on global loads.
+// range. A wavefront takes MAP_G consecutive segments and packs their
+// (segment, start range) pairs densely onto its 64 lanes (a segment has ~4
+// start ranges, so a fixed 16 lanes per segment would leave most lanes idle);
+// more than 64 pairs take further rounds. The group's tokens go through LDS
+// MAP_CH per segment at a time (the next chunk is loaded into registers while
+// this one runs), so the chains read LDS broadcasts instead of global loads.
+#define MAP_G 16
 #define MAP_CH 256
+#define MAP_ROW (MAP_CH + 8)   // u16; +16 B per row: the 16 rows' b128 reads hit distinct banks
+#define MAP_PIECES (MAP_G * MAP_CH / 8 / 64)   // 16-byte pieces per lane per chunk
 __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ tokens,
                                                   size_t tok_cap,
                                                   const vp8g_emit_meta* __restrict__ meta,
                                                   const uint8_t* __restrict__ img,
                                                   uint8_t* __restrict__ emap,
                                                   uint16_t* __restrict__ eshift) {
-  __shared__ __align__(16) uint16_t stage[4][MAP_CH];
-  const int f = blockIdx.y, lane = threadIdx.x, grp = lane >> 4;
+  __shared__ __align__(16) uint16_t stage[MAP_G * MAP_ROW];
+  const int f = blockIdx.y, lane = threadIdx.x;
   const vp8g_emit_meta M = meta[f];
-  const uint32_t sbase = blockIdx.x * 4;
-  const uint32_t s = sbase + grp;
-  const int slot = lane & 15;
-  const bool valid = s < M.nseg;
-  const uint32_t cnt = valid ? min((uint32_t)EMIT_SEG, M.ntok - s * EMIT_SEG) : 0u;
-  const uint8_t* im = img + ((size_t)M.seg_base + (valid ? s : 0)) * (EMIT_SLOTS + 1);
-  const int ni = valid ? im[0] : 0;
-  const int rounds = ni == 0xff ? 128 / EMIT_SLOTS : 1;
-  int rmax = 0;   // wave-uniform round count
-  for (int o = 1; o < 64; o <<= 1) rmax = max(rmax, __shfl_xor(rounds, o));
-  rmax = max(rmax, rounds);
+  const uint32_t sbase = blockIdx.x * MAP_G;
+  if (sbase >= M.nseg) return;   // whole wave
+  // pair counts of the group's segments (lanes 0..MAP_G-1), inclusive scan
+  int nk = 0;
+  if (lane < MAP_G && sbase + lane < M.nseg) {
+    const int ni = img[((size_t)M.seg_base + sbase + lane) * (EMIT_SLOTS + 1)];
+    nk = ni == 0xff ? 128 : ni;
+  }
+  int incl = nk;
+  for (int o = 1; o < MAP_G; o <<= 1) {
+    const int v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  const int total = __shfl(incl, MAP_G - 1);
   const uint16_t* ftok = tokens + (size_t)f * tok_cap;
-  // this lane's two 16-byte pieces of a chunk: segment lane >> 4, parts (lane & 15) and +16
-  const uint32_t ls = sbase + (lane >> 4);
-  auto load = [&](uint32_t c0, uint4& a, uint4& b) {
-    a = b = make_uint4(0, 0, 0, 0);
-    if (ls < M.nseg) {
-      const uint32_t i = ls * EMIT_SEG + c0 + 8 * (lane & 15);
-      if (i < M.ntok) a = *reinterpret_cast<const uint4*>(ftok + i);
-      if (i + 128 < M.ntok) b = *reinterpret_cast<const uint4*>(ftok + i + 128);
+  auto load = [&](uint32_t c0, uint4* v) {
+#pragma unroll
+    for (int t = 0; t < MAP_PIECES; ++t) {
+      const int q = lane + 64 * t, sg = q / (MAP_CH / 8), part = q % (MAP_CH / 8);
+      const uint32_t i = (sbase + sg) * EMIT_SEG + c0 + 8 * part;
+      v[t] = make_uint4(0, 0, 0, 0);
+      if (sbase + sg < M.nseg && i < M.ntok) v[t] = *reinterpret_cast<const uint4*>(ftok + i);
     }
   };
-  for (int rd = 0; rd < rmax; ++rd) {
-    const bool live = valid && rd < rounds && (ni == 0xff || slot < ni);
-    const int r0 = ni == 0xff ? 127 + EMIT_SLOTS * rd + slot : (live ? im[1 + slot] : 127);
+  for (int p0 = 0; p0 < total; p0 += 64) {
+    const int p = p0 + lane;   // this lane's pair
+    int g = 0, excl = 0;
+#pragma unroll
+    for (int j = 0; j < MAP_G; ++j) {
+      const int ij = __shfl(incl, j);
+      if (p >= ij) { g = j + 1; excl = ij; }
+    }
+    const bool live = p < total;
+    const uint32_t s = sbase + (live ? g : 0);
+    const uint8_t* im = img + ((size_t)M.seg_base + s) * (EMIT_SLOTS + 1);
+    const int k = p - excl;
+    const int r0 = !live ? 127 : im[0] == 0xff ? 127 + k : im[1 + k];
+    const uint32_t cnt = live ? min((uint32_t)EMIT_SEG, M.ntok - s * EMIT_SEG) : 0u;
+    const uint16_t* st = stage + (live ? g : 0) * MAP_ROW;
     int r = r0;
     uint32_t S = 0;
-    uint4 na, nb;
-    load(0, na, nb);
+    uint4 nv[MAP_PIECES];
+    load(0, nv);
     for (uint32_t c0 = 0; c0 < EMIT_SEG; c0 += MAP_CH) {
       __syncthreads();   // the previous chunk's reads are done
-      *reinterpret_cast<uint4*>(&stage[lane >> 4][8 * (lane & 15)]) = na;
-      *reinterpret_cast<uint4*>(&stage[lane >> 4][128 + 8 * (lane & 15)]) = nb;
+#pragma unroll
+      for (int t = 0; t < MAP_PIECES; ++t) {
+        const int q = lane + 64 * t, sg = q / (MAP_CH / 8), part = q % (MAP_CH / 8);
+        *reinterpret_cast<uint4*>(&stage[sg * MAP_ROW + 8 * part]) = nv[t];
+      }
       __syncthreads();
-      if (c0 + MAP_CH < EMIT_SEG) load(c0 + MAP_CH, na, nb);   // in flight during the chain
+      if (c0 + MAP_CH < EMIT_SEG) load(c0 + MAP_CH, nv);   // in flight during the chain
       const uint32_t n = cnt > c0 ? min((uint32_t)MAP_CH, cnt - c0) : 0u;
-      const uint16_t* st = stage[grp];
       if (n == MAP_CH) {
         for (int i = 0; i < MAP_CH; i += 8) {
           const uint4 q = *reinterpret_cast<const uint4*>(st + i);
           const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-          for (int k = 0; k < 8; ++k) S += chain_step(r, (w[k >> 1] >> (16 * (k & 1))) & 0xffff);
+          for (int kk = 0; kk < 8; ++kk) S += chain_step(r, (w[kk >> 1] >> (16 * (kk & 1))) & 0xffff);
         }
       } else {
         for (uint32_t i = 0; i < n; ++i) S += chain_step(r, st[i]);   // frame's last segment
@@ -438,7 +460,7 @@ extern "C" int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
                        (const uint16_t*)tokens,
                        tok_cap, (const vp8g_emit_meta*)meta, img);
     if (!vp8g_launch_check("k_emit_img")) return 0;
-    hipLaunchKernelGGL(k_emit_maps, dim3((max_seg + 3) / 4, n), dim3(64), 0, st,
+    hipLaunchKernelGGL(k_emit_maps, dim3((max_seg + MAP_G - 1) / MAP_G, n), dim3(64), 0, st,
                        (const uint16_t*)tokens, tok_cap, (const vp8g_emit_meta*)meta,
                        (const uint8_t*)img, emap, eshift);
     if (!vp8g_launch_check("k_emit_maps")) return 0;

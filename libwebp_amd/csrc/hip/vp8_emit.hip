@@ -81,65 +81,101 @@ __device__ __forceinline__ int chain_step(int& r, uint32_t pb) {
 
 // E1a: the range a segment can start with is the end state of the previous
 // segment, whatever state that one was in EMIT_IMG tokens before its end:
-// run those last tokens from all 128 ranges and keep the distinct end states
-// (a handful: the chains merge quickly). Segment 0 starts at 254.
+// push the set of all 128 ranges through those last tokens and keep the end
+// set (a handful: the chains merge quickly). Only the set matters, so it is
+// carried as distinct values: a wavefront takes IMG_G segments, runs the
+// (segment, range) pairs of the current sets packed onto its lanes for one
+// phase of tokens, collects the images in per-segment 128-bit maps and
+// repacks the (by then far fewer) distinct ranges for the next phase.
+// Segment 0 starts at 254.
 #define EMIT_IMG 256
 #define EMIT_SLOTS 16
-#define IMG_GROUP 16   // segments per workgroup, two at a time (128 ranges each)
-__global__ __launch_bounds__(256) void k_emit_img(const uint16_t* __restrict__ tokens,
-                                                  size_t tok_cap,
-                                                  const vp8g_emit_meta* __restrict__ meta,
-                                                  uint8_t* __restrict__ img) {
-  __shared__ __align__(16) uint16_t stage[2][EMIT_IMG];
-  __shared__ uint32_t seen[2][4];
-  const int f = blockIdx.y, t = threadIdx.x, half = t >> 7, r_id = t & 127;
+#define IMG_G 16                     // segments per wavefront (4 lanes each for the maps)
+#define IMG_ROW (EMIT_IMG + 8)       // u16; +16 B per row: conflict-free b128 reads
+__global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ tokens,
+                                                 size_t tok_cap,
+                                                 const vp8g_emit_meta* __restrict__ meta,
+                                                 uint8_t* __restrict__ img) {
+  __shared__ __align__(16) uint16_t tk[IMG_G * IMG_ROW];
+  __shared__ uint32_t bm[IMG_G * 4];
+  __shared__ uint16_t pairs[IMG_G * 128];   // (segment << 7) | (range - 127)
+  const int f = blockIdx.y, lane = threadIdx.x;
   const vp8g_emit_meta M = meta[f];
+  const uint32_t sbase = blockIdx.x * IMG_G;
+  if (sbase >= M.nseg) return;   // whole wave
   const uint16_t* ftok = tokens + (size_t)f * tok_cap;
-  for (int g = 0; g < IMG_GROUP; g += 2) {
-    const uint32_t s0 = blockIdx.x * IMG_GROUP + g;   // this pair: s0, s0 + 1
-    if (s0 >= M.nseg) break;                           // uniform over the workgroup
-    __syncthreads();                                   // previous pair's LDS reads done
-    if (t < 2 * EMIT_IMG / 8) {                        // 64 x 16 B: both segments' tails
-      const int h = t >> 5, q = t & 31;
-      const uint32_t s = s0 + h;
-      if (s > 0 && s < M.nseg)
-        *reinterpret_cast<uint4*>(&stage[h][8 * q]) =
-            *reinterpret_cast<const uint4*>(ftok + (size_t)s * EMIT_SEG - EMIT_IMG + 8 * q);
-    }
-    if (t < 8) seen[t >> 2][t & 3] = 0;
-    __syncthreads();
-    const uint32_t s = s0 + half;
-    const bool run = s > 0 && s < M.nseg;
-    int r = 127 + r_id;
-    if (run) {
-      for (int i = 0; i < EMIT_IMG; i += 8) {
-        const uint4 q = *reinterpret_cast<const uint4*>(&stage[half][i]);
-        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-        for (int k = 0; k < 8; ++k) chain_step(r, (w[k >> 1] >> (16 * (k & 1))) & 0xffff);
-      }
-      atomicOr(&seen[half][(r - 127) >> 5], 1u << ((r - 127) & 31));
-    }
-    __syncthreads();
-    if (r_id == 0 && s < M.nseg) {
-      uint8_t* out = img + ((size_t)M.seg_base + s) * (EMIT_SLOTS + 1);
-      if (s == 0) {   // segment 0 starts at 254
-        out[0] = 1; out[1] = 254;
-      } else {
-        int cnt = 0;
-        for (int wv = 0; wv < 4; ++wv) cnt += __popc(seen[half][wv]);
-        if (cnt > EMIT_SLOTS) {
-          out[0] = 0xff;   // too many: the map kernel covers all 128 ranges
-        } else {
-          out[0] = (uint8_t)cnt;
-          int k = 1;
-          for (int wv = 0; wv < 4; ++wv)
-            for (uint32_t m = seen[half][wv]; m; m &= m - 1)
-              out[k++] = (uint8_t)(127 + 32 * wv + __ffs(m) - 1);
+  for (int t = 0; t < IMG_G * EMIT_IMG / 8 / 64; ++t) {   // every segment's last-tokens window
+    const int q = lane + 64 * t, sg = q / (EMIT_IMG / 8), part = q % (EMIT_IMG / 8);
+    const uint32_t s = sbase + sg;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (s > 0 && s < M.nseg)
+      v = *reinterpret_cast<const uint4*>(ftok + (size_t)s * EMIT_SEG - EMIT_IMG + 8 * part);
+    *reinterpret_cast<uint4*>(&tk[sg * IMG_ROW + 8 * part]) = v;
+  }
+  // this lane's piece of the maps: segment mg, word mw
+  const int mg = lane >> 2, mw = lane & 3;
+  const uint32_t ms = sbase + mg;
+  const bool mact = ms > 0 && ms < M.nseg;
+  int np = IMG_G * 128;   // phase 0: pair p = (segment p >> 7, range 127 + (p & 127))
+  int cnt = 0, wofs = 0;
+  for (int ph = 0, t0 = 0; t0 < EMIT_IMG; ++ph) {
+    const int t1 = ph == 0 ? 8 : 2 * t0;   // phases [0,8) [8,16) [16,32) ... [128,256)
+    bm[lane] = 0;
+    __syncthreads();   // tokens / pairs / cleared maps visible
+    for (int p0 = 0; p0 < np; p0 += 64) {
+      const int p = p0 + lane;
+      if (p < np) {
+        const int pr = ph == 0 ? p : pairs[p];
+        const int g = pr >> 7;
+        const uint32_t s = sbase + g;
+        if (s > 0 && s < M.nseg) {
+          int r = 127 + (pr & 127);
+          const uint16_t* row = tk + g * IMG_ROW;
+          for (int i = t0; i < t1; i += 8) {
+            const uint4 q = *reinterpret_cast<const uint4*>(row + i);
+            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) chain_step(r, (w[k >> 1] >> (16 * (k & 1))) & 0xffff);
+          }
+          atomicOr(&bm[g * 4 + ((r - 127) >> 5)], 1u << ((r - 127) & 31));
         }
       }
     }
+    __syncthreads();   // the maps are complete
+    // repack: this lane's map word -> pairs[offset of its segment + earlier words]
+    const uint32_t word = bm[lane];
+    const int pc = __popc(word);
+    int incl = pc;   // inclusive scan over all 64 words = segment-major order
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    np = __shfl(incl, 63);
+    const int gfirst = __shfl(incl - pc, lane & ~3);   // the segment's first pair
+    cnt = __shfl(incl, lane | 3) - gfirst;
+    wofs = incl - pc - gfirst;
+    t0 = t1;
+    if (t0 < EMIT_IMG) {
+      int k = incl - pc;
+      for (uint32_t m = word; m; m &= m - 1)
+        pairs[k++] = (uint16_t)((mg << 7) | (32 * mw + __ffs(m) - 1));
+    }
   }
+  // output: the end set of each segment (lanes of segment mg, word mw)
+  if (ms >= M.nseg) return;
+  uint8_t* out = img + ((size_t)M.seg_base + ms) * (EMIT_SLOTS + 1);
+  if (!mact) {   // segment 0
+    if (mw == 0) { out[0] = 1; out[1] = 254; }
+    return;
+  }
+  if (cnt > EMIT_SLOTS) {   // too many: the map kernel covers all 128 ranges
+    if (mw == 0) out[0] = 0xff;
+    return;
+  }
+  if (mw == 0) out[0] = (uint8_t)cnt;
+  int k = 1 + wofs;
+  for (uint32_t m = bm[lane]; m; m &= m - 1) out[k++] = (uint8_t)(127 + 32 * mw + __ffs(m) - 1);
 }
 
 // E1b: per segment, the end range and shift count from each possible start
@@ -234,41 +270,65 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
   }
 }
 
+// E2: one wavefront per frame. The segment maps are staged through LDS 64
+// segments at a time (coalesced 16-byte loads of the whole 128-entry maps),
+// so the serial walk along the true range chain reads LDS, not dependent
+// global loads; the walk's per-segment (rs, S, T) go out coalesced.
+#define CMP_SEGS 64
 __global__ __launch_bounds__(64) void k_emit_compose(vp8g_emit_meta* __restrict__ meta,
                                                      const uint8_t* __restrict__ emap,
                                                      const uint16_t* __restrict__ eshift,
                                                      vp8g_emit_seg* __restrict__ segs,
                                                      uint32_t* __restrict__ out_size) {
-  const int f = blockIdx.x;
-  if (threadIdx.x != 0) return;
+  __shared__ __align__(16) uint8_t lmap[CMP_SEGS * 128];
+  __shared__ __align__(16) uint16_t lsh[CMP_SEGS * 128];
+  __shared__ vp8g_emit_seg lseg[CMP_SEGS];
+  __shared__ uint32_t lS;
+  const int f = blockIdx.x, lane = threadIdx.x;
   vp8g_emit_meta M = meta[f];
-  int r = 254;
+  int r = 254;        // lane 0's walk state
   uint32_t cum = 0;
-  for (uint32_t s = 0; s < M.nseg; ++s) {
-    const size_t o = ((size_t)M.seg_base + s) * 128 + (r - 127);
-    const uint32_t Ss = eshift[o];
-    segs[M.seg_base + s].rs = (uint8_t)r;
-    segs[M.seg_base + s].S = Ss;
-    segs[M.seg_base + s].T = cum;   // provisional: shifts BEFORE the segment
-    cum += Ss;
-    r = emap[o];
+  for (uint32_t c = 0; c < M.nseg; c += CMP_SEGS) {
+    const uint32_t m = min((uint32_t)CMP_SEGS, M.nseg - c);
+    const uint4* gm = reinterpret_cast<const uint4*>(emap + ((size_t)M.seg_base + c) * 128);
+    const uint4* gs = reinterpret_cast<const uint4*>(eshift + ((size_t)M.seg_base + c) * 128);
+    __syncthreads();   // the previous chunk's LDS reads are done
+    for (uint32_t q = lane; q < m * 8; q += 64) reinterpret_cast<uint4*>(lmap)[q] = gm[q];
+    for (uint32_t q = lane; q < m * 16; q += 64) reinterpret_cast<uint4*>(lsh)[q] = gs[q];
+    __syncthreads();
+    if (lane == 0) {
+      for (uint32_t j = 0; j < m; ++j) {
+        const uint32_t o = j * 128 + (r - 127);
+        const uint32_t Ss = lsh[o];
+        lseg[j] = vp8g_emit_seg{cum, (uint16_t)Ss, (uint8_t)r, 0};   // T: shifts BEFORE the segment
+        cum += Ss;
+        r = lmap[o];
+      }
+    }
+    __syncthreads();
+    if ((uint32_t)lane < m) segs[M.seg_base + c + lane] = lseg[lane];
   }
-  // VP8BitWriterFinish pads 9 - nb_bits zero bits at probability 1/2, where
-  // nb_bits is what the flushes left after cum shifts from -8
-  const int t = (int)cum - 8;
-  const int nb = t <= 0 ? t : t - 8 * ((t + 7) / 8);
-  uint32_t spad = 0;
-  for (int k = 0; k < 9 - nb; ++k) {
-    r = (r * 128) >> 8;
-    spad += renorm(r);
+  if (lane == 0) {
+    // VP8BitWriterFinish pads 9 - nb_bits zero bits at probability 1/2, where
+    // nb_bits is what the flushes left after cum shifts from -8
+    const int t = (int)cum - 8;
+    const int nb = t <= 0 ? t : t - 8 * ((t + 7) / 8);
+    uint32_t spad = 0;
+    for (int k = 0; k < 9 - nb; ++k) {
+      r = (r * 128) >> 8;
+      spad += renorm(r);
+    }
+    M.S = cum + spad;
+    M.L = (M.S + 7) / 8;
+    meta[f] = M;
+    out_size[f] = M.L;
+    lS = M.S;
   }
-  M.S = cum + spad;
-  M.L = (M.S + 7) / 8;
-  meta[f] = M;
-  out_size[f] = M.L;
-  for (uint32_t s = 0; s < M.nseg; ++s) {   // T_s = bit offset of the segment's bottom in N
+  __syncthreads();
+  const uint32_t St = lS;
+  for (uint32_t s = lane; s < M.nseg; s += 64) {   // T_s = bit offset of the segment's bottom in N
     vp8g_emit_seg& g = segs[M.seg_base + s];
-    g.T = M.S - (g.T + g.S);
+    g.T = St - (g.T + g.S);
   }
 }
 
@@ -456,7 +516,7 @@ extern "C" int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
     if (!vp8g_launch_check("k_emit_resolve")) return 0;
   }
   if (max_seg) {
-    hipLaunchKernelGGL(k_emit_img, dim3((max_seg + IMG_GROUP - 1) / IMG_GROUP, n), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_emit_img, dim3((max_seg + IMG_G - 1) / IMG_G, n), dim3(64), 0, st,
                        (const uint16_t*)tokens,
                        tok_cap, (const vp8g_emit_meta*)meta, img);
     if (!vp8g_launch_check("k_emit_img")) return 0;

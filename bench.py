@@ -60,6 +60,9 @@ def parse_args(argv=None):
     ap.add_argument("--low-memory", action="store_true",
                     help="config->low_memory (cwebp -low_memory, VP8EncLoop); not the headline")
     ap.add_argument("--threads", type=int, default=0, help="host tail threads (0 = auto)")
+    ap.add_argument("--engines", type=int, default=2,
+                    help="encoder instances on their own streams and host threads; steps are "
+                         "dealt round-robin so one batch's host work overlaps another's kernels")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="CPU work per baseline leg (single thread, all cores)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -276,7 +279,8 @@ def lossless_line(args, world, B, W, H, elapsed, tails, total_bytes):
         "config": {"workload": "batch of %d %dx%d RGBA frames per GPU, -lossless -q %g -m %d" %
                                (B, W, H, args.quality, args.method),
                    "frames_per_gpu": B, "width": W, "height": H, "quality": args.quality,
-                   "method": args.method, "parallelism": "frames sharded %d ways" % world},
+                   "method": args.method, "parallelism": "frames sharded %d ways" % world,
+                   "engines_per_gpu": getattr(args, "engines_used", 1)},
         "roofline": {"bound": "hbm", "kernel": "k_vp8l_transform", "achieved": round(achieved, 3),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
@@ -377,8 +381,22 @@ def main(argv=None):
                                    use_sharp_yuv=int(args.sharp_yuv),
                                    lossless=int(args.lossless), low_memory=int(args.low_memory))
 
-    def step():
-        enc.encode_device(rgba.data_ptr() if rgba is not None else 0, B, stream=stream)
+    # more engines: each on its own HIP stream with its own host buffers; the
+    # timed steps are dealt round-robin to one host thread per engine (the
+    # ctypes calls release the GIL), so one batch's host stages (segment
+    # setup, partition 0, RIFF write) run while another batch's kernels do
+    E = 1 if args.stub else max(1, min(args.engines, args.steps))
+    args.engines_used = E
+    encs = [enc]
+    for _ in range(E - 1):
+        encs.append(libwebp_amd.GpuBatch(W, H, B, quality=args.quality, method=args.method,
+                                         device=local, threads=args.threads,
+                                         use_sharp_yuv=int(args.sharp_yuv),
+                                         lossless=int(args.lossless),
+                                         low_memory=int(args.low_memory)))
+
+    def step(e=0):
+        encs[e].encode_device(rgba.data_ptr() if rgba is not None else 0, B, stream=stream)
 
     def barrier():
         if world > 1:
@@ -386,14 +404,36 @@ def main(argv=None):
         if not args.stub:
             torch.cuda.synchronize(dev)
 
-    for _ in range(args.warmup):
-        step()
+    for e in range(E):
+        for _ in range(max(args.warmup, 1 if E > 1 else 0)):
+            step(e)
     barrier()
-    t0 = time.perf_counter()
     tails = []
-    for _ in range(args.steps):
-        step()
-        tails.append(enc.timings())
+    if E == 1:
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+            tails.append(enc.timings())
+    else:
+        import threading
+        errors = []
+
+        def worker(e):
+            try:
+                for _ in range(e, args.steps, E):
+                    step(e)
+                    tails.append(encs[e].timings())
+            except Exception as ex:   # re-raised below, after every thread ends
+                errors.append(ex)
+
+        th = [threading.Thread(target=worker, args=(e,)) for e in range(E)]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errors:
+            raise errors[0]
     barrier()
     elapsed = time.perf_counter() - t0
 
@@ -442,7 +482,8 @@ def main(argv=None):
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    enc.close()
+    for e in encs:
+        e.close()
     if failed:
         raise SystemExit("timed-batch frames differ from the reference known answers")
     return 0
@@ -482,7 +523,8 @@ def lossy_line(args, world, B, W, H, elapsed, tails, total_bytes, ntok):
                                 (" -low_memory" if args.low_memory else "")),
                    "frames_per_gpu": B, "width": W, "height": H,
                    "quality": args.quality, "method": args.method,
-                   "parallelism": "frames sharded %d ways" % world},
+                   "parallelism": "frames sharded %d ways" % world,
+                   "engines_per_gpu": getattr(args, "engines_used", 1)},
         "roofline": {"bound": "hbm", "kernel": "k_encode", "achieved": round(achieved, 3),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6),

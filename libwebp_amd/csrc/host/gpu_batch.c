@@ -155,6 +155,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   b->tok_off = (size_t*)calloc(N + 1, sizeof(size_t));
   b->p0 = (vp8h_bw*)calloc(N, sizeof(vp8h_bw));
   b->out = (uint8_t**)calloc(N, sizeof(uint8_t*));
+  b->out_cap = (size_t*)calloc(N, sizeof(size_t));
   b->out_size = (size_t*)calloc(N, sizeof(size_t));
   b->err = (int*)calloc(N, sizeof(int));
   b->hdr = (int*)calloc(2 * N, sizeof(int));
@@ -162,7 +163,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   b->fin_cost = (int*)calloc(N, sizeof(int));
   b->pass_act = (uint8_t*)calloc(N, 1);
   b->asse = (uint64_t*)calloc(N, sizeof(uint64_t));
-  if (!b->frames || !b->tok_off || !b->p0 || !b->out || !b->out_size || !b->err || !b->hdr ||
+  if (!b->frames || !b->tok_off || !b->p0 || !b->out || !b->out_cap || !b->out_size || !b->err || !b->hdr ||
       !b->araw || !b->fin_cost || !b->pass_act || !b->asse)
     goto fail;
   return b;
@@ -206,7 +207,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   if (b->stream) hipStreamDestroy(b->stream);
   if (b->out)
     for (int i = 0; i < b->max_frames; ++i) free(b->out[i]);
-  free(b->out); free(b->out_size); free(b->err); free(b->hdr);
+  free(b->out); free(b->out_cap); free(b->out_size); free(b->err); free(b->hdr);
   if (b->p0)
     for (int i = 0; i < b->max_frames; ++i) vp8h_bw_free(&b->p0[i]);
   free(b->frames); free(b->tok_off); free(b->p0);
@@ -219,7 +220,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
 
 typedef struct {
   WebPGpuBatch* b;
-  int n, phase;   /* phase 0: partition 0; phase 1: partition 1 + RIFF write */
+  int n, phase;   /* 0: partition 0; 1: partition 1 + RIFF write; 2: frame setup */
   atomic_int next;
   pthread_t th[TAIL_MAX_THREADS];
   int started;
@@ -229,9 +230,7 @@ typedef struct {
 static void frame_head(WebPGpuBatch* b, int f) {
   vp8h_frame* fr = &b->frames[f];
   const vp8g_frame_result* res = &b->h_results[f];
-  free(b->out[f]);
-  b->out[f] = NULL;
-  b->out_size[f] = 0;
+  b->out_size[f] = 0;   /* b->out[f] (capacity b->out_cap[f]) is reused */
   vp8h_bw_free(&b->p0[f]);
   if (b->err[f] != VP8_ENC_OK) return;
   if (res->error) { b->err[f] = VP8_ENC_ERROR_OUT_OF_MEMORY; return; }
@@ -269,9 +268,20 @@ static void frame_finish(WebPGpuBatch* b, int f) {
     if (b->cfg.alpha_quality < 100) alpha.header |= 1 << 4;   /* ALPHA_PREPROCESSED_LEVELS */
     ap = &alpha;
   }
-  b->out_size[f] = vp8h_write_riff(&b->frames[f], &b->p0[f], &part1, ap, &b->out[f], &err);
+  b->out_size[f] =
+      vp8h_write_riff(&b->frames[f], &b->p0[f], &part1, ap, &b->out[f], &b->out_cap[f], &err);
   b->err[f] = err;
   if (b->host_emit) vp8h_bw_free(&part1);
+}
+
+/* Frame header state and the segment map from K2's per-MB alphas
+ * (vp8h_analyze_segments: analysis_enc.c's k-means). */
+static void frame_setup(WebPGpuBatch* b, int f) {
+  if (b->err[f] != VP8_ENC_OK) return;
+  const size_t nmb = (size_t)b->nmb;
+  vp8h_frame_init(&b->frames[f], &b->cfg, b->w, b->h);
+  vp8h_analyze_segments(&b->frames[f], b->h_alpha + f * nmb, b->h_uva + f * nmb,
+                        b->h_segmap + f * nmb);
 }
 
 static void* tail_worker(void* arg) {
@@ -280,7 +290,8 @@ static void* tail_worker(void* arg) {
     const int f = atomic_fetch_add(&j->next, 1);
     if (f >= j->n) break;
     if (j->phase == 0) frame_head(j->b, f);
-    else frame_finish(j->b, f);
+    else if (j->phase == 1) frame_finish(j->b, f);
+    else frame_setup(j->b, f);
   }
   return NULL;
 }
@@ -694,12 +705,7 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   CHK(hipMemcpyAsync(b->h_uva, b->d_uva, n * nmb * sizeof(uint16_t), hipMemcpyDeviceToHost, st));
   CHK(hipStreamSynchronize(st));
   t1 = now_us();
-  for (int f = 0; f < n; ++f) {
-    if (b->err[f] != VP8_ENC_OK) continue;
-    vp8h_frame_init(&b->frames[f], &b->cfg, b->w, b->h);
-    vp8h_analyze_segments(&b->frames[f], b->h_alpha + f * nmb, b->h_uva + f * nmb,
-                          b->h_segmap + f * nmb);
-  }
+  run_tails(b, n, 2);   /* per-frame setup + segment k-means on the host threads */
   t2 = now_us();
   if (!run_passes(b, n)) return 0;
   if (!b->host_emit) {   /* K4 on the device, sized from the token counts */
@@ -809,8 +815,12 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   } else {
     run_tails(b, n, 0);
   }
+  const double t4b = now_us();
   run_tails(b, n, 1);
   const double t5 = now_us();
+  if (getenv("LIBWEBP_AMD_TAIL_TIMING"))
+    fprintf(stderr, "tail: head join %.0f us, finish %.0f us, threads %d\n", t4b - t4, t5 - t4b,
+            b->threads);
   float k3_ms = 0.f, k12_ms = 0.f, k4_ms = 0.f;
   CHK(hipEventElapsedTime(&k3_ms, b->ev[2], b->ev[3]));
   CHK(hipEventElapsedTime(&k12_ms, b->ev[0], b->ev[1]));

@@ -98,6 +98,7 @@ struct WebPGpuBatch {
   vp8h_frame* frames;
   /* outputs of the last call */
   uint8_t** out;
+  size_t* out_cap;     /* allocated bytes of out[f] (reused across batches) */
   size_t* out_size;
   int* err;
   int* hdr;

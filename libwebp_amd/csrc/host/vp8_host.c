@@ -705,27 +705,75 @@ void vp8h_emit_tokens(vp8h_bw* bw, const uint16_t* tok, size_t n, const uint8_t*
 /* Partition 0 (syntax_enc.c:187-310, tree_enc.c:270-347,485-504) and the
  * RIFF container (syntax_enc.c:37-185,320-389). */
 
+/* Partition-0 modes are coded in two steps per MB row: the row's decisions
+ * become (bit << 8 | probability) tokens through path tables (no branches on
+ * the modes), then one tight coder loop with a branch-free renormalisation
+ * codes them; both branch-heavy tree walks of the direct form mispredicted on
+ * nearly every decision. */
+#define P0_MB_TOKENS 128   /* >= 2 + 1 + 16 * 7 + 3, plus 7 slack for the path writes */
+
+/* intra4 mode tree (tree_enc.c:270-295): nodes visited and bits, per mode */
+static const uint8_t kI4PathLen[10] = {1, 2, 3, 5, 6, 6, 5, 6, 7, 7};
+static const uint8_t kI4PathNode[10][7] = {
+    {0}, {0, 1}, {0, 1, 2}, {0, 1, 2, 3, 4}, {0, 1, 2, 3, 4, 5}, {0, 1, 2, 3, 4, 5},
+    {0, 1, 2, 3, 6}, {0, 1, 2, 3, 6, 7}, {0, 1, 2, 3, 6, 7, 8}, {0, 1, 2, 3, 6, 7, 8}};
+static const uint8_t kI4PathBit[10][7] = {
+    {0}, {1, 0}, {1, 1, 0}, {1, 1, 1, 0, 0}, {1, 1, 1, 0, 1, 0}, {1, 1, 1, 0, 1, 1},
+    {1, 1, 1, 1, 0}, {1, 1, 1, 1, 1, 0}, {1, 1, 1, 1, 1, 1, 0}, {1, 1, 1, 1, 1, 1, 1}};
+
+static inline uint32_t p0_tok(int bit, int prob) { return ((uint32_t)bit << 8) | (uint32_t)prob; }
+
+static void p0_code(vp8h_bw* bw, const uint16_t* tok, size_t n) {
+  int32_t range = bw->range, value = bw->value;
+  int nb_bits = bw->nb_bits;
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t t = tok[i];
+    const int split = (range * (int)(t & 0xff)) >> 8;
+    const int bit = (int)(t >> 8);
+    value += bit ? split + 1 : 0;
+    range = bit ? range - split - 1 : split;
+    const int shift = __builtin_clz((unsigned)(range + 1)) - 24;   /* 0 when range >= 127 */
+    range = ((range + 1) << shift) - 1;
+    value <<= shift;
+    nb_bits += shift;
+    if (nb_bits > 0) {
+      bw->value = value; bw->nb_bits = nb_bits;
+      bw_flush(bw);
+      value = bw->value; nb_bits = bw->nb_bits;
+    }
+  }
+  bw->range = range; bw->value = value; bw->nb_bits = nb_bits;
+}
+
 static void code_intra_modes(vp8h_bw* bw, const vp8h_frame* fr, const uint8_t* mbinfo,
                              int use_skip, int skip_proba) {
   const int mbw = fr->mbw;
   uint8_t* top_modes = (uint8_t*)calloc(4 * (size_t)mbw, 1);   /* B_DC_PRED border */
-  if (!top_modes) { bw->error = 1; return; }
+  uint16_t* tok = (uint16_t*)malloc((size_t)mbw * P0_MB_TOKENS * sizeof(uint16_t));
+  if (!top_modes || !tok) { bw->error = 1; free(top_modes); free(tok); return; }
+  const int upd = fr->update_map;
+  const uint8_t* sp = fr->seg_probas;
   for (int y = 0; y < fr->mbh; ++y) {
     uint8_t left_modes[4] = {0, 0, 0, 0};
+    size_t n = 0;
     for (int x = 0; x < mbw; ++x) {
       const uint8_t* info = mbinfo + ((size_t)y * mbw + x) * VP8G_MBINFO_BYTES;
       const uint8_t* modes = info + 4;
-      if (fr->update_map) {
+      if (upd) {   /* segment id tree */
         const int s = info[2];
-        const uint8_t* p = fr->seg_probas;
-        if (bw_put(bw, s >= 2, p[0])) p += 1;
-        bw_put(bw, s & 1, p[1]);
+        tok[n] = (uint16_t)p0_tok(s >= 2, sp[0]);
+        tok[n + 1] = (uint16_t)p0_tok(s & 1, sp[1 + (s >= 2)]);
+        n += 2;
       }
-      if (use_skip) bw_put(bw, info[3], skip_proba);   /* tree_enc.c:323-325 */
-      if (bw_put(bw, info[0] != 0, 145)) {   /* intra16 */
+      if (use_skip) tok[n++] = (uint16_t)p0_tok(info[3] != 0, skip_proba);   /* tree_enc.c:323-325 */
+      const int i16 = info[0] != 0;
+      tok[n++] = (uint16_t)p0_tok(i16, 145);
+      if (i16) {
         const int m = modes[0];
-        if (bw_put(bw, m == 1 || m == 3, 156)) bw_put(bw, m == 1, 128);
-        else bw_put(bw, m == 2, 163);
+        const int b0 = m == 1 || m == 3;
+        tok[n] = (uint16_t)p0_tok(b0, 156);
+        tok[n + 1] = (uint16_t)(b0 ? p0_tok(m == 1, 128) : p0_tok(m == 2, 163));
+        n += 2;
       } else {
         for (int yy = 0; yy < 4; ++yy) {
           int left = left_modes[yy];
@@ -733,27 +781,27 @@ static void code_intra_modes(vp8h_bw* bw, const vp8h_frame* fr, const uint8_t* m
             const int top = yy == 0 ? top_modes[4 * x + xx] : modes[4 * (yy - 1) + xx];
             const uint8_t* pr = kVP8BModeProba[top][left];
             const int m = modes[4 * yy + xx];
-            if (bw_put(bw, m != 0, pr[0]) && bw_put(bw, m != 1, pr[1]) &&
-                bw_put(bw, m != 2, pr[2])) {
-              if (!bw_put(bw, m >= 6, pr[3])) {
-                if (bw_put(bw, m != 3, pr[4])) bw_put(bw, m != 4, pr[5]);
-              } else if (bw_put(bw, m != 6, pr[6])) {
-                if (bw_put(bw, m != 7, pr[7])) bw_put(bw, m != 8, pr[8]);
-              }
-            }
+            for (int k = 0; k < 7; ++k)   /* fixed trip count; the length advances n */
+              tok[n + k] = (uint16_t)p0_tok(kI4PathBit[m][k], pr[kI4PathNode[m][k]]);
+            n += kI4PathLen[m];
             left = m;
           }
         }
       }
-      const int uvm = info[1];
-      if (bw_put(bw, uvm != 0, 142) && bw_put(bw, uvm != 2, 114)) bw_put(bw, uvm != 3, 183);
+      const int uvm = info[1];   /* uv mode tree: DC, then V / H / TM */
+      tok[n] = (uint16_t)p0_tok(uvm != 0, 142);
+      tok[n + 1] = (uint16_t)p0_tok(uvm != 2, 114);
+      tok[n + 2] = (uint16_t)p0_tok(uvm != 3, 183);
+      n += uvm == 0 ? 1 : uvm == 2 ? 2 : 3;
       for (int k = 0; k < 4; ++k) {
         top_modes[4 * x + k] = modes[12 + k];
         left_modes[k] = modes[4 * k + 3];
       }
     }
+    p0_code(bw, tok, n);
   }
   free(top_modes);
+  free(tok);
 }
 
 static void put_le32(uint8_t* p, uint32_t v) {
@@ -821,7 +869,7 @@ int vp8h_build_p0(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* m
 }
 
 size_t vp8h_write_riff(const vp8h_frame* fr, vp8h_bw* p0, const vp8h_bw* part1,
-                       const vp8h_alpha* alpha, uint8_t** out, int* err) {
+                       const vp8h_alpha* alpha, uint8_t** out, size_t* cap, int* err) {
   /* VP8EncWrite + PutWebPHeaders (syntax_enc.c:149-185, 320-392): RIFF,
    * [VP8X + ALPH when the picture has alpha], 'VP8 ', frame header,
    * partition 0, partition 1, pad byte */
@@ -845,7 +893,7 @@ size_t vp8h_write_riff(const vp8h_frame* fr, vp8h_bw* p0, const vp8h_bw* part1,
     return 0;
   }
   const size_t total = 8 + riff_size;
-  uint8_t* o = (uint8_t*)malloc(total);
+  uint8_t* o = cap && *out && *cap >= total ? *out : (uint8_t*)malloc(total);
   if (!o) {
     vp8h_bw_free(&bw);
     *err = VP8_ENC_ERROR_OUT_OF_MEMORY;
@@ -883,7 +931,13 @@ size_t vp8h_write_riff(const vp8h_frame* fr, vp8h_bw* p0, const vp8h_bw* part1,
   if (size1) memcpy(fh + 10 + size0, part1->buf, size1);
   if (pad) fh[10 + size0 + size1] = 0;
   vp8h_bw_free(&bw);
-  *out = o;
+  if (o != *out) {
+    if (cap) {   /* the caller's buffer was too small: replace it */
+      free(*out);
+      *cap = total;
+    }
+    *out = o;
+  }
   *err = VP8_ENC_OK;
   return total;
 }
@@ -896,5 +950,5 @@ size_t vp8h_assemble(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t
     vp8h_bw_free(&p0);
     return 0;
   }
-  return vp8h_write_riff(fr, &p0, part1, NULL, out, err);
+  return vp8h_write_riff(fr, &p0, part1, NULL, out, NULL, err);
 }

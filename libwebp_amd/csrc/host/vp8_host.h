@@ -144,8 +144,10 @@ typedef struct {
   const uint8_t* data;
   size_t size;
 } vp8h_alpha;
+/* *out is reused when *cap (if cap != NULL) already holds the file, else
+ * replaced by a fresh allocation (*cap updated) */
 size_t vp8h_write_riff(const vp8h_frame* fr, vp8h_bw* p0, const vp8h_bw* part1,
-                       const vp8h_alpha* alpha, uint8_t** out, int* err);
+                       const vp8h_alpha* alpha, uint8_t** out, size_t* cap, int* err);
 size_t vp8h_assemble(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* mbinfo,
                      vp8h_bw* part1, uint8_t** out, int* err, int* hdr_bytes);
 

@@ -353,7 +353,10 @@ int WebPEncode(const WebPConfig* config, WebPPicture* pic) {
   int err = ok ? e->err[0] : VP8_ENC_ERROR_OUT_OF_MEMORY;
   uint8_t* out = ok ? e->out[0] : NULL;
   const size_t size = ok ? e->out_size[0] : 0;
-  if (ok) e->out[0] = NULL;   /* take ownership */
+  if (ok) {   /* take ownership */
+    e->out[0] = NULL;
+    e->out_cap[0] = 0;
+  }
   vp8h_frame fr;
   vp8g_frame_result res;
   memset(&fr, 0, sizeof(fr));

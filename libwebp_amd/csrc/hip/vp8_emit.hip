@@ -49,13 +49,15 @@ __global__ __launch_bounds__(256) void k_emit_resolve(uint16_t* __restrict__ tok
                                                       const vp8g_emit_meta* __restrict__ meta) {
   __shared__ uint8_t prob[VP8G_NUM_SLOTS];
   const int f = blockIdx.y;
-  const vp8g_frame_result* R = results + f;
+  const vp8g_emit_meta M = meta[f];
+  const uint32_t ntok = M.ntok;
+  if (blockIdx.x * 2048 >= ntok) return;   // whole workgroup
+  const vp8g_frame_result* R = results + M.frame;
   for (int s = threadIdx.x; s < VP8G_NUM_SLOTS; s += 256) prob[s] = R->probas[s];
   __syncthreads();
-  const uint32_t ntok = meta[f].ntok;
   const uint32_t i0 = (blockIdx.x * 256 + threadIdx.x) * 8;
   if (i0 >= ntok) return;
-  uint16_t* tok = tokens + (size_t)f * tok_cap + i0;
+  uint16_t* tok = tokens + M.tok_off + i0;
   uint4 w = *reinterpret_cast<const uint4*>(tok);
   uint32_t v[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
@@ -103,7 +105,7 @@ __global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ to
   const vp8g_emit_meta M = meta[f];
   const uint32_t sbase = blockIdx.x * IMG_G;
   if (sbase >= M.nseg) return;   // whole wave
-  const uint16_t* ftok = tokens + (size_t)f * tok_cap;
+  const uint16_t* ftok = tokens + M.tok_off;
 #pragma unroll
   for (int t = 0; t < IMG_G * EMIT_IMG / 8 / 64; ++t) {   // every segment's last-tokens window
     const int q = lane + 64 * t, sg = q / (EMIT_IMG / 8), part = q % (EMIT_IMG / 8);
@@ -212,7 +214,7 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
     if (lane >= o) incl += v;
   }
   const int total = __shfl(incl, MAP_G - 1);
-  const uint16_t* ftok = tokens + (size_t)f * tok_cap;
+  const uint16_t* ftok = tokens + M.tok_off;
   auto load = [&](uint32_t c0, uint4* v) {
 #pragma unroll
     for (int t = 0; t < MAP_PIECES; ++t) {
@@ -379,7 +381,7 @@ __global__ __launch_bounds__(64) void k_emit_seg(uint16_t* __restrict__ tokens, 
   vp8g_emit_seg g = valid ? segs[M.seg_base + s] : vp8g_emit_seg{0, 0, 254, 0};
   const uint32_t i0 = s * EMIT_SEG;
   const uint32_t cnt = valid ? min((uint32_t)EMIT_SEG, M.ntok - i0) : 0u;
-  uint16_t* base = tokens + (size_t)f * tok_cap;
+  uint16_t* base = tokens + M.tok_off;
   uint32_t* row = lds + lane * SEG_ROW;
   // the chunks this wave needs: up to its longest segment
   const uint32_t last_s = min(s0 + 64, M.nseg) - 1;
@@ -497,7 +499,7 @@ __global__ __launch_bounds__(256) void k_emit_bytes(uint16_t* __restrict__ token
   const uint32_t* W = nbuf + M.nb_base;
   const uint32_t b = 1 + 8 * (M.L - 1 - k);   // lowest bit of output byte k
   const uint64_t two = (uint64_t)W[b >> 5] | ((uint64_t)W[(b >> 5) + 1] << 32);
-  reinterpret_cast<uint8_t*>(tokens + (size_t)f * tok_cap)[k] = (uint8_t)(two >> (b & 31));
+  reinterpret_cast<uint8_t*>(tokens + M.tok_off)[k] = (uint8_t)(two >> (b & 31));
 }
 
 extern "C" int vp8g_launch_check(const char* what);
@@ -544,31 +546,137 @@ extern "C" int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
   return vp8g_launch_check("k_emit_bytes");
 }
 
-// Gather every frame's partition-1 bytes (at the head of its token slab) into
-// one packed buffer at 16-byte aligned offsets, so the host pulls the whole
-// batch back with a single DMA instead of one copy per frame.
-__global__ __launch_bounds__(256) void k_pack(const uint8_t* __restrict__ src, size_t pitch,
+// Gather every stream's bytes (at its token offset) into one packed buffer at
+// 16-byte aligned offsets, so the host pulls the whole batch back with a
+// single DMA instead of one copy per stream.
+__global__ __launch_bounds__(256) void k_pack(const uint16_t* __restrict__ tokens,
+                                              const vp8g_emit_meta* __restrict__ meta,
                                               const uint64_t* __restrict__ off,
                                               const uint32_t* __restrict__ size,
                                               uint8_t* __restrict__ dst) {
   const int f = blockIdx.y;
   const uint32_t n16 = (size[f] + 15) >> 4;
-  const uint4* s4 = reinterpret_cast<const uint4*>(src + (size_t)f * pitch);
+  const uint4* s4 = reinterpret_cast<const uint4*>(tokens + meta[f].tok_off);
   uint4* d4 = reinterpret_cast<uint4*>(dst + off[f]);
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) d4[i] = s4[i];
 }
 
-extern "C" int vp8g_launch_pack(const uint16_t* tokens, size_t tok_cap, int n,
+extern "C" int vp8g_launch_pack(const uint16_t* tokens, const vp8g_emit_meta* meta, int n,
                                 const uint64_t* off, const uint32_t* size, uint32_t max_size,
                                 uint8_t* dst, void* stream) {
   if (n <= 0 || max_size == 0) return 1;
-  if ((tok_cap * sizeof(uint16_t)) & 15) return 0;
   uint32_t gx = (max_size + 16 * 256 - 1) / (16 * 256);
   if (gx > 64) gx = 64;
-  hipLaunchKernelGGL(k_pack, dim3(gx, n), dim3(256), 0, (hipStream_t)stream,
-                     reinterpret_cast<const uint8_t*>(tokens), tok_cap * sizeof(uint16_t), off,
+  hipLaunchKernelGGL(k_pack, dim3(gx, n), dim3(256), 0, (hipStream_t)stream, tokens, meta, off,
                      size, dst);
   return vp8g_launch_check("k_pack");
+}
+
+// Token partitions (VP8EncLoop writes MB row y into parts_[y & (P - 1)],
+// iterator_enc.c:48): one workgroup per frame. Row token counts from the
+// per-MB counts, raster row starts in the compact stream, then each
+// partition's rows are copied, in order, to its own region in the upper half
+// of the frame's slab (disjoint from the compact stream in the lower half).
+// Each region holds at least the partition's coded bytes, so K4's output at a
+// region's head never reaches the next one.
+#define PART_MAX_ROWS 1024   // mbh <= 1024 (height <= 16383)
+__device__ __forceinline__ uint32_t part_region(uint32_t ntok) {
+  const uint32_t bytes = (7u * ntok + 48) / 8 + 2;   // K4's output bound
+  const uint32_t need = max(ntok, (bytes + 1) / 2);
+  return (need + 7u) & ~7u;
+}
+
+__global__ __launch_bounds__(256) void k_partition(uint16_t* __restrict__ tokens, size_t tok_cap,
+                                                   const uint32_t* __restrict__ mboff,
+                                                   const vp8g_frame_result* __restrict__ results,
+                                                   const uint8_t* __restrict__ mbinfo, int mbw,
+                                                   int mbh, int kind, int nparts,
+                                                   uint32_t* __restrict__ part) {
+  __shared__ uint32_t rowlen[PART_MAX_ROWS], rowsrc[PART_MAX_ROWS], rowdst[PART_MAX_ROWS];
+  __shared__ uint32_t poff[VP8G_MAX_PARTS], plen[VP8G_MAX_PARTS];
+  __shared__ uint32_t lastfix;
+  __shared__ int bad;
+  const int f = blockIdx.x, tid = threadIdx.x;
+  const int nmb = mbw * mbh;
+  const vp8g_frame_result& R = results[f];
+  uint32_t* P = part + 16 * (size_t)f;
+  if (R.error) {
+    if (tid < 16) P[tid] = 0;
+    return;
+  }
+  const uint32_t* cnt = mboff + (size_t)f * nmb;
+  const uint8_t* info = mbinfo + (size_t)f * nmb * VP8G_MBINFO_BYTES;
+  const bool drop = R.use_skip != 0;
+  const uint32_t ntok = R.ntokens;
+  auto mb_count = [&](int m) -> uint32_t {   // the last MB of kind 1 is fixed up below
+    if (drop && info[(size_t)m * VP8G_MBINFO_BYTES + 3]) return 0u;
+    if (kind == 0) return cnt[m];
+    return m + 1 < nmb ? cnt[m + 1] - cnt[m] : 0u;
+  };
+  for (int y = tid; y < mbh; y += 256) {
+    uint32_t sum = 0;
+    for (int x = 0; x < mbw; ++x) sum += mb_count(y * mbw + x);
+    rowlen[y] = sum;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (int y = 0; y < mbh; ++y) acc += rowlen[y];
+    lastfix = 0;
+    if (kind == 1 && !(drop && info[(size_t)(nmb - 1) * VP8G_MBINFO_BYTES + 3]))
+      lastfix = ntok - acc;   // the last MB ends at the frame's token count
+    rowlen[mbh - 1] += lastfix;
+    uint32_t src = 0;
+    for (int p = 0; p < VP8G_MAX_PARTS; ++p) plen[p] = 0;
+    for (int y = 0; y < mbh; ++y) {
+      rowsrc[y] = src;
+      src += rowlen[y];
+      plen[y & (nparts - 1)] += rowlen[y];
+    }
+    uint32_t o = (uint32_t)(((tok_cap / 2) + 7) & ~(size_t)7);
+    bad = src != ntok || (size_t)ntok > tok_cap / 2;
+    for (int p = 0; p < nparts; ++p) {
+      poff[p] = o;
+      o += part_region(plen[p]);
+    }
+    bad |= (size_t)o > tok_cap;
+    uint32_t at[VP8G_MAX_PARTS];
+    for (int p = 0; p < nparts; ++p) at[p] = poff[p];
+    for (int y = 0; y < mbh; ++y) {
+      rowdst[y] = at[y & (nparts - 1)];
+      at[y & (nparts - 1)] += rowlen[y];
+    }
+  }
+  __syncthreads();
+  if (bad) {
+    if (tid == 0) P[0] = 0xffffffffu;
+    return;
+  }
+  uint16_t* T = tokens + (size_t)f * tok_cap;
+  const int wv = tid >> 6, ln = tid & 63;
+  for (int y = wv; y < mbh; y += 4) {
+    const uint16_t* s = T + rowsrc[y];
+    uint16_t* d = T + rowdst[y];
+    for (uint32_t i = ln; i < rowlen[y]; i += 64) d[i] = s[i];
+  }
+  if (tid < nparts) {
+    P[tid] = poff[tid];
+    P[8 + tid] = plen[tid];
+  }
+}
+
+extern "C" int vp8g_launch_partition(uint16_t* tokens, size_t tok_cap, int n,
+                                     const uint32_t* mboff, const vp8g_frame_result* results,
+                                     const uint8_t* mbinfo, int mbw, int mbh, int kind,
+                                     int nparts, uint32_t* part, void* stream) {
+  if (n <= 0) return 1;
+  if (mbh > PART_MAX_ROWS || nparts < 1 || nparts > VP8G_MAX_PARTS || (nparts & (nparts - 1))) {
+    vp8g_set_error("k_partition", "unsupported frame height or partition count");
+    return 0;
+  }
+  hipLaunchKernelGGL(k_partition, dim3(n), dim3(256), 0, (hipStream_t)stream, tokens, tok_cap,
+                     mboff, results, mbinfo, mbw, mbh, kind, nparts, part);
+  return vp8g_launch_check("k_partition");
 }
 
 // VP8EstimateTokenSize (token_enc.c:226-247) between the passes of a size

@@ -115,6 +115,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
     const char* he = getenv("WEBP_AMD_HOST_EMIT");
     b->host_emit = he && he[0] == '1';
   }
+
   const size_t N = (size_t)max_frames, nmb = (size_t)b->nmb;
   CHK(hipSetDevice(device));
   CHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
@@ -138,8 +139,13 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   if (N <= VP8G_XSPLIT_MAX_FRAMES)   /* few frames: K3 splits each over several CUs */
     CHK(hipMalloc((void**)&b->d_xsync, N * vp8g_xsync_bytes(width, height)));
   CHK(hipMalloc((void**)&b->d_results, N * sizeof(vp8g_frame_result)));
-  CHK(hipMalloc((void**)&b->d_psize, N * sizeof(uint32_t)));
-  CHK(hipMalloc((void**)&b->d_emeta, N * sizeof(vp8g_emit_meta)));
+  /* K4 streams: one per token partition; the WebPEncode pool changes the
+   * config of an engine between calls, so room for the most partitions */
+  const size_t NS = N * VP8G_MAX_PARTS;
+  CHK(hipMalloc((void**)&b->d_psize, NS * sizeof(uint32_t)));
+  CHK(hipMalloc((void**)&b->d_emeta, NS * sizeof(vp8g_emit_meta)));
+  CHK(hipMalloc((void**)&b->d_pinfo, N * 16 * sizeof(uint32_t)));
+  CHK(hipHostMalloc((void**)&b->h_pinfo, N * 16 * sizeof(uint32_t), 0));
   CHK(hipHostMalloc((void**)&b->h_aflags, N * sizeof(uint32_t), 0));
   CHK(hipHostMalloc((void**)&b->h_alpha, N * nmb, 0));
   CHK(hipHostMalloc((void**)&b->h_uva, N * nmb * sizeof(uint16_t), 0));
@@ -147,10 +153,10 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   CHK(hipHostMalloc((void**)&b->h_params, N * sizeof(vp8g_frame_params), 0));
   CHK(hipHostMalloc((void**)&b->h_mbinfo, N * nmb * VP8G_MBINFO_BYTES, 0));
   CHK(hipHostMalloc((void**)&b->h_results, N * sizeof(vp8g_frame_result), 0));
-  CHK(hipHostMalloc((void**)&b->h_psize, N * sizeof(uint32_t), 0));
-  CHK(hipHostMalloc((void**)&b->h_poff, (N + 1) * sizeof(uint64_t), 0));
-  CHK(hipMalloc((void**)&b->d_poff, (N + 1) * sizeof(uint64_t)));
-  CHK(hipHostMalloc((void**)&b->h_emeta, N * sizeof(vp8g_emit_meta), 0));
+  CHK(hipHostMalloc((void**)&b->h_psize, NS * sizeof(uint32_t), 0));
+  CHK(hipHostMalloc((void**)&b->h_poff, (NS + 1) * sizeof(uint64_t), 0));
+  CHK(hipMalloc((void**)&b->d_poff, (NS + 1) * sizeof(uint64_t)));
+  CHK(hipHostMalloc((void**)&b->h_emeta, NS * sizeof(vp8g_emit_meta), 0));
   b->frames = (vp8h_frame*)calloc(N, sizeof(vp8h_frame));
   b->tok_off = (size_t*)calloc(N + 1, sizeof(size_t));
   b->p0 = (vp8h_bw*)calloc(N, sizeof(vp8h_bw));
@@ -179,7 +185,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipFree(b->d_g2l); hipFree(b->d_rgba); hipFree(b->d_yuv); hipFree(b->d_aflags); hipFree(b->d_alpha);
   hipFree(b->d_uva); hipFree(b->d_amode); hipFree(b->d_segmap); hipFree(b->d_params); hipFree(b->d_tokens);
   hipFree(b->d_mbinfo); hipFree(b->d_mboff); hipFree(b->d_rerun); hipFree(b->d_xsync); hipFree(b->d_results); hipFree(b->d_psize); hipFree(b->d_emeta);
-  hipFree(b->d_poff); hipFree(b->d_part);
+  hipFree(b->d_poff); hipFree(b->d_part); hipFree(b->d_pinfo);
   hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs); hipFree(b->d_nbuf);
   hipFree(b->d_eimg);
   hipFree(b->d_stabs); hipFree(b->d_sharp); hipFree(b->d_sstate);
@@ -194,7 +200,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipHostFree(b->h_aflags); hipHostFree(b->h_alpha); hipHostFree(b->h_uva);
   hipHostFree(b->h_segmap); hipHostFree(b->h_params); hipHostFree(b->h_mbinfo);
   hipHostFree(b->h_results); hipHostFree(b->h_tokens); hipHostFree(b->h_psize);
-  hipHostFree(b->h_part); hipHostFree(b->h_emeta); hipHostFree(b->h_poff);
+  hipHostFree(b->h_part); hipHostFree(b->h_emeta); hipHostFree(b->h_poff); hipHostFree(b->h_pinfo);
   vp8l_engine_free(b->l);
   vp8l_engine_free(b->la);
   hipFree(b->d_aplane);
@@ -243,15 +249,19 @@ static void frame_head(WebPGpuBatch* b, int f) {
 static void frame_finish(WebPGpuBatch* b, int f) {
   const vp8g_frame_result* res = &b->h_results[f];
   if (b->err[f] != VP8_ENC_OK) { vp8h_bw_free(&b->p0[f]); return; }
-  vp8h_bw part1;
+  vp8h_bw part1[VP8G_MAX_PARTS];
+  const int np = b->nparts;
   if (b->host_emit) {   /* boolean-code the tokens here (token_enc.c:200-223) */
-    vp8h_bw_init(&part1, (size_t)res->ntokens / 8 + 4096);
-    vp8h_emit_tokens(&part1, b->h_tokens + b->tok_off[f], res->ntokens, res->probas);
-    vp8h_bw_finish(&part1);
-  } else {              /* partition 1 already coded by K4 */
-    memset(&part1, 0, sizeof(part1));
-    part1.buf = b->h_part + b->h_poff[f];
-    part1.pos = b->h_psize[f];
+    vp8h_bw_init(&part1[0], (size_t)res->ntokens / 8 + 4096);
+    vp8h_emit_tokens(&part1[0], b->h_tokens + b->tok_off[f], res->ntokens, res->probas);
+    vp8h_bw_finish(&part1[0]);
+  } else {              /* the token partitions, already coded by K4 */
+    for (int p = 0; p < np; ++p) {
+      const size_t s = (size_t)f * np + p;
+      memset(&part1[p], 0, sizeof(part1[p]));
+      part1[p].buf = b->h_part + b->h_poff[s];
+      part1[p].pos = b->h_psize[s];
+    }
   }
   int err = VP8_ENC_OK;
   vp8h_alpha alpha, *ap = NULL;
@@ -268,10 +278,10 @@ static void frame_finish(WebPGpuBatch* b, int f) {
     if (b->cfg.alpha_quality < 100) alpha.header |= 1 << 4;   /* ALPHA_PREPROCESSED_LEVELS */
     ap = &alpha;
   }
-  b->out_size[f] =
-      vp8h_write_riff(&b->frames[f], &b->p0[f], &part1, ap, &b->out[f], &b->out_cap[f], &err);
+  b->out_size[f] = vp8h_write_riff(&b->frames[f], &b->p0[f], part1, b->host_emit ? 1 : np, ap,
+                                   &b->out[f], &b->out_cap[f], &err);
   b->err[f] = err;
-  if (b->host_emit) vp8h_bw_free(&part1);
+  if (b->host_emit) vp8h_bw_free(&part1[0]);
 }
 
 /* Frame header state and the segment map from K2's per-MB alphas
@@ -708,12 +718,36 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   run_tails(b, n, 2);   /* per-frame setup + segment k-means on the host threads */
   t2 = now_us();
   if (!run_passes(b, n)) return 0;
+  /* token partitions: VP8EncLoop only (vp8h_frame_init) */
+  const int np = (b->cfg.method < 3 || b->cfg.low_memory) ? 1 << b->cfg.partitions : 1;
+  const int ns = n * np;   /* K4 streams */
+  b->nparts = np;
+  if (np > 1 && b->host_emit) {
+    vp8g_set_error("WebPGpuBatch", "WEBP_AMD_HOST_EMIT codes a single token partition");
+    return 0;
+  }
+  if (!b->host_emit && np > 1) {   /* token partitions: rows regrouped per partition */
+    if (!vp8g_launch_partition(b->d_tokens, b->tok_cap, n, b->d_mboff, b->d_results, b->d_mbinfo,
+                               b->mbw, b->mbh, b->cfg.method < 3 ? 0 : 1, np, b->d_pinfo, st))
+      return 0;
+    CHK(hipMemcpyAsync(b->h_pinfo, b->d_pinfo, (size_t)n * 16 * sizeof(uint32_t),
+                       hipMemcpyDeviceToHost, st));
+    CHK(hipStreamSynchronize(st));
+  }
   if (!b->host_emit) {   /* K4 on the device, sized from the token counts */
     uint32_t max_ntok = 0, max_seg = 0;
     size_t segs = 0, words = 0;
-    for (int f = 0; f < n; ++f) {
-      vp8g_emit_meta* m = &b->h_emeta[f];
-      m->ntok = b->h_results[f].error ? 0 : b->h_results[f].ntokens;
+    for (int s = 0; s < ns; ++s) {
+      const int f = s / np, p = s % np;
+      vp8g_emit_meta* m = &b->h_emeta[s];
+      const uint32_t* pi = np > 1 ? b->h_pinfo + 16 * (size_t)f : NULL;
+      if (pi && pi[0] == 0xffffffffu && !b->h_results[f].error && b->err[f] == VP8_ENC_OK)
+        b->err[f] = VP8_ENC_ERROR_OUT_OF_MEMORY;   /* the partitions did not fit the slab */
+      const int ok = !b->h_results[f].error && !(pi && pi[0] == 0xffffffffu);
+      m->ntok = !ok ? 0 : pi ? pi[8 + p] : b->h_results[f].ntokens;
+      m->frame = (uint32_t)f;
+      m->reserved = 0;
+      m->tok_off = (uint64_t)f * b->tok_cap + (ok && pi ? pi[p] : 0);
       m->nseg = (m->ntok + VP8G_EMIT_SEG - 1) / VP8G_EMIT_SEG;
       m->seg_base = (uint32_t)segs;
       m->nb_base = (uint32_t)words;
@@ -743,14 +777,14 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
     }
     CHK(hipEventRecord(b->ev[5], st));
     CHK(hipMemsetAsync(b->d_nbuf, 0, words * sizeof(uint32_t), st));
-    CHK(hipMemcpyAsync(b->d_emeta, b->h_emeta, n * sizeof(vp8g_emit_meta),
+    CHK(hipMemcpyAsync(b->d_emeta, b->h_emeta, ns * sizeof(vp8g_emit_meta),
                        hipMemcpyHostToDevice, st));
-    if (!vp8g_launch_emit(b->d_tokens, b->tok_cap, n, b->d_results, b->d_emeta, max_ntok,
+    if (!vp8g_launch_emit(b->d_tokens, b->tok_cap, ns, b->d_results, b->d_emeta, max_ntok,
                           max_seg, b->d_emap, b->d_eshift, b->d_eimg, b->d_esegs, b->d_nbuf,
                           b->d_psize, st))
       return 0;
     CHK(hipEventRecord(b->ev[4], st));
-    CHK(hipMemcpyAsync(b->h_psize, b->d_psize, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    CHK(hipMemcpyAsync(b->h_psize, b->d_psize, ns * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     /* partition 0 on the host threads while K4 runs on the device */
     tail_spawn(&head, b, n, 0, b->threads - 1);
     head_running = 1;
@@ -774,14 +808,14 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
         CHK(hipMemcpyAsync(b->h_tokens + b->tok_off[f], b->d_tokens + (size_t)f * b->tok_cap,
                            b->h_results[f].ntokens * sizeof(uint16_t), hipMemcpyDeviceToHost, st));
   } else {
-    /* one packed D2H of every frame's partition 1 (k_pack) */
+    /* one packed D2H of every frame's token partitions (k_pack) */
     uint32_t max_size = 0;
     b->h_poff[0] = 0;
-    for (int f = 0; f < n; ++f) {
-      b->h_poff[f + 1] = b->h_poff[f] + ((b->h_psize[f] + 15u) & ~15u);
-      if (b->h_psize[f] > max_size) max_size = b->h_psize[f];
+    for (int s = 0; s < ns; ++s) {
+      b->h_poff[s + 1] = b->h_poff[s] + ((b->h_psize[s] + 15u) & ~15u);
+      if (b->h_psize[s] > max_size) max_size = b->h_psize[s];
     }
-    const size_t total = b->h_poff[n];
+    const size_t total = b->h_poff[ns];
     if (total > b->h_part_cap) {
       hipHostFree(b->h_part);
       b->h_part = NULL;
@@ -799,9 +833,9 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
       b->d_part_cap = cap;
     }
     if (total) {
-      CHK(hipMemcpyAsync(b->d_poff, b->h_poff, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
+      CHK(hipMemcpyAsync(b->d_poff, b->h_poff, (ns + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
                          st));
-      if (!vp8g_launch_pack(b->d_tokens, b->tok_cap, n, b->d_poff, b->d_psize, max_size, b->d_part,
+      if (!vp8g_launch_pack(b->d_tokens, b->d_emeta, ns, b->d_poff, b->d_psize, max_size, b->d_part,
                             st))
         goto fail;
       CHK(hipMemcpyAsync(b->h_part, b->d_part, total, hipMemcpyDeviceToHost, st));

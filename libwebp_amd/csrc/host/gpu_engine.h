@@ -61,7 +61,10 @@ struct WebPGpuBatch {
   uint8_t* pass_act;         /* frames with a pass to run */
   vp8g_frame_result* d_results;
   uint32_t* d_psize;         /* partition-1 bytes per frame (K4) */
-  vp8g_emit_meta* d_emeta;   /* K4 per-frame bookkeeping */
+  vp8g_emit_meta* d_emeta;   /* K4 per-stream bookkeeping (nparts streams per frame) */
+  int nparts;                /* token partitions per frame (1 << partitions for VP8EncLoop) */
+  uint32_t* d_pinfo;         /* k_partition: 16 words per frame (starts, counts) */
+  uint32_t* h_pinfo;
   vp8g_emit_meta* h_emeta;
   uint8_t* d_emap;           /* K4 scratch, grown on demand */
   uint16_t* d_eshift;

@@ -52,14 +52,15 @@ int vp8h_frame_init(vp8h_frame* fr, const WebPConfig* cfg, int w, int h) {
   memset(fr, 0, sizeof(*fr));
   if (cfg->method < 0 || cfg->method > 6) return 0;
   /* methods 0-2 run VP8EncLoop (RD_OPT_NONE): its size / PSNR search passes
-   * (StatLoop with RD_OPT_BASIC, frame_enc.c:614-674) and token partitions
-   * (one bit writer per MB row modulo 2^partitions) are not implemented */
-  if (cfg->method < 3 && (cfg->target_size > 0 || cfg->target_PSNR > 0 || cfg->partitions > 0))
-    return 0;
+   * (StatLoop with RD_OPT_BASIC, frame_enc.c:614-674) are not implemented */
+  if (cfg->method < 3 && (cfg->target_size > 0 || cfg->target_PSNR > 0)) return 0;
   /* low_memory runs VP8EncLoop for methods 3-6 too; its size / PSNR search
-   * and token partitions are not implemented */
-  if (cfg->low_memory && (cfg->target_size > 0 || cfg->target_PSNR > 0 || cfg->partitions > 0))
-    return 0;
+   * is not implemented */
+  if (cfg->low_memory && (cfg->target_size > 0 || cfg->target_PSNR > 0)) return 0;
+  /* token partitions: VP8EncLoop writes MB row y into partition
+   * y & (2^partitions - 1); the token loop (methods 3-6 without low_memory)
+   * keeps one (webp_enc.c:115-122, 209) */
+  fr->num_parts = (cfg->method < 3 || cfg->low_memory) ? 1 << cfg->partitions : 1;
   fr->w = w; fr->h = h;
   fr->mbw = (w + 15) >> 4; fr->mbh = (h + 15) >> 4;
   fr->method = cfg->method;
@@ -841,7 +842,8 @@ int vp8h_build_p0(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* m
   bw_put_bits(&bw, (uint32_t)fr->f_level, 6);
   bw_put_bits(&bw, (uint32_t)fr->f_sharpness, 3);
   bw_put_uniform(&bw, 0);          /* no loop-filter deltas */
-  bw_put_bits(&bw, 0, 2);          /* a single token partition */
+  bw_put_bits(&bw, fr->num_parts == 8 ? 3 : fr->num_parts == 4 ? 2 : fr->num_parts == 2 ? 1 : 0,
+              2);                  /* token partitions (syntax_enc.c:283-285) */
   bw_put_bits(&bw, (uint32_t)fr->base_quant, 7);
   bw_put_signed(&bw, 0, 4);        /* dq_y1_dc */
   bw_put_signed(&bw, 0, 4);        /* dq_y2_dc */
@@ -868,20 +870,30 @@ int vp8h_build_p0(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* m
   return VP8_ENC_OK;
 }
 
-size_t vp8h_write_riff(const vp8h_frame* fr, vp8h_bw* p0, const vp8h_bw* part1,
+size_t vp8h_write_riff(const vp8h_frame* fr, vp8h_bw* p0, const vp8h_bw* parts, int nparts,
                        const vp8h_alpha* alpha, uint8_t** out, size_t* cap, int* err) {
   /* VP8EncWrite + PutWebPHeaders (syntax_enc.c:149-185, 320-392): RIFF,
    * [VP8X + ALPH when the picture has alpha], 'VP8 ', frame header,
-   * partition 0, partition 1, pad byte */
+   * partition 0, the sizes of all token partitions but the last (3 bytes
+   * each, EmitPartitionsSize :248-265), the token partitions, pad byte */
   vp8h_bw bw = *p0;
   memset(p0, 0, sizeof(*p0));
-  if (part1->error) {
-    vp8h_bw_free(&bw);
-    *err = VP8_ENC_ERROR_OUT_OF_MEMORY;
-    return 0;
+  size_t size1 = 0;
+  for (int p = 0; p < nparts; ++p) {
+    if (parts[p].error) {
+      vp8h_bw_free(&bw);
+      *err = VP8_ENC_ERROR_OUT_OF_MEMORY;
+      return 0;
+    }
+    if (p < nparts - 1 && parts[p].pos >= (1u << 24)) {   /* VP8_MAX_PARTITION_SIZE */
+      vp8h_bw_free(&bw);
+      *err = VP8_ENC_ERROR_PARTITION_OVERFLOW;
+      return 0;
+    }
+    size1 += parts[p].pos;
   }
-  const size_t size0 = bw.pos, size1 = part1->pos;
-  size_t vp8_size = 10 + size0 + size1;
+  const size_t size0 = bw.pos, psz = 3 * (size_t)(nparts - 1);
+  size_t vp8_size = 10 + size0 + psz + size1;
   const size_t pad = vp8_size & 1;
   vp8_size += pad;
   size_t riff_size = 4 + 8 + vp8_size;
@@ -928,8 +940,17 @@ size_t vp8h_write_riff(const vp8h_frame* fr, vp8h_bw* p0, const vp8h_bw* part1,
   fh[6] = (uint8_t)(fr->w & 0xff); fh[7] = (uint8_t)(fr->w >> 8);
   fh[8] = (uint8_t)(fr->h & 0xff); fh[9] = (uint8_t)(fr->h >> 8);
   memcpy(fh + 10, bw.buf, size0);
-  if (size1) memcpy(fh + 10 + size0, part1->buf, size1);
-  if (pad) fh[10 + size0 + size1] = 0;
+  uint8_t* d = fh + 10 + size0;
+  for (int p = 0; p < nparts - 1; ++p) {
+    const size_t ps = parts[p].pos;
+    d[0] = (uint8_t)ps; d[1] = (uint8_t)(ps >> 8); d[2] = (uint8_t)(ps >> 16);
+    d += 3;
+  }
+  for (int p = 0; p < nparts; ++p) {
+    if (parts[p].pos) memcpy(d, parts[p].buf, parts[p].pos);
+    d += parts[p].pos;
+  }
+  if (pad) *d = 0;
   vp8h_bw_free(&bw);
   if (o != *out) {
     if (cap) {   /* the caller's buffer was too small: replace it */
@@ -950,5 +971,5 @@ size_t vp8h_assemble(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t
     vp8h_bw_free(&p0);
     return 0;
   }
-  return vp8h_write_riff(fr, &p0, part1, NULL, out, NULL, err);
+  return vp8h_write_riff(fr, &p0, part1, 1, NULL, out, NULL, err);
 }

@@ -28,6 +28,7 @@ typedef struct {
   int preprocessing, emulate_jpeg_size, cfg_segments;
   /* segment header + per-segment values */
   int num_segments, update_map, seg_hdr_size;
+  int num_parts;   /* token partitions (1, 2, 4 or 8) */
   uint8_t seg_probas[3];
   int alpha, uv_alpha, base_quant, dq_uv_dc, dq_uv_ac;
   int seg_alpha[4], seg_beta[4], seg_quant[4], seg_fstrength[4], seg_y2ac[4];
@@ -146,7 +147,7 @@ typedef struct {
 } vp8h_alpha;
 /* *out is reused when *cap (if cap != NULL) already holds the file, else
  * replaced by a fresh allocation (*cap updated) */
-size_t vp8h_write_riff(const vp8h_frame* fr, vp8h_bw* p0, const vp8h_bw* part1,
+size_t vp8h_write_riff(const vp8h_frame* fr, vp8h_bw* p0, const vp8h_bw* parts, int nparts,
                        const vp8h_alpha* alpha, uint8_t** out, size_t* cap, int* err);
 size_t vp8h_assemble(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* mbinfo,
                      vp8h_bw* part1, uint8_t** out, int* err, int* hdr_bytes);

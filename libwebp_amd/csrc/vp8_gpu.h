@@ -199,12 +199,18 @@ int vp8g_launch_token_cost(const uint16_t* tokens, size_t tok_cap, int n,
                            const vp8g_frame_result* results, const uint8_t* state,
                            const uint8_t* active, unsigned long long* bits, void* stream);
 
-/* K4: boolean coder for the token partition, parallel inside each frame
- * (hip/vp8_emit.hip). Per-frame bookkeeping: ntok, the segment count and the
- * first segment / first N-array word of the frame (host), S and L (device). */
+/* K4: boolean coder for the token partitions, parallel inside each stream
+ * (hip/vp8_emit.hip). A stream is one token partition of one frame: its
+ * tokens start at tokens + tok_off (a multiple of 8 tokens) and take their
+ * probabilities from results[frame]; the coded bytes replace them there.
+ * Per-stream bookkeeping: ntok, the segment count and the first segment /
+ * first N-array word of the stream (host), S and L (device). */
 typedef struct {
   uint32_t ntok, nseg, seg_base, nb_base, S, L;
+  uint32_t frame, reserved;
+  uint64_t tok_off;
 } vp8g_emit_meta;
+#define VP8G_MAX_PARTS 8   /* token partitions per frame (syntax_enc.c:283) */
 typedef struct {
   uint32_t T;      /* bit offset of the segment's part of N */
   uint16_t S;      /* renormalisation shifts inside the segment */
@@ -212,18 +218,31 @@ typedef struct {
   uint8_t H;       /* bits of the segment's partial sum above its region */
 } vp8g_emit_seg;
 #define VP8G_EMIT_SEG 2048
-/* partition-1 bytes replace the tokens at the start of each frame's token
- * buffer; out_size[f] = their count */
+/* n streams; out_size[s] = the byte count of stream s */
 int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
                      const vp8g_frame_result* results, vp8g_emit_meta* meta,
                      uint32_t max_ntok, uint32_t max_seg, uint8_t* emap, uint16_t* eshift,
                      uint8_t* img, vp8g_emit_seg* segs, uint32_t* nbuf, uint32_t* out_size,
                      void* stream);
 
-/* K4 tail: copy each frame's partition-1 bytes (size[f] bytes at the head of
- * its token slab) to dst + off[f]; off[f] must be 16-byte aligned. */
-int vp8g_launch_pack(const uint16_t* tokens, size_t tok_cap, int n, const uint64_t* off,
-                     const uint32_t* size, uint32_t max_size, uint8_t* dst, void* stream);
+/* K4 tail: copy each stream's bytes (size[s] bytes at tokens +
+ * meta[s].tok_off) to dst + off[s]; off[s] must be 16-byte aligned. */
+int vp8g_launch_pack(const uint16_t* tokens, const vp8g_emit_meta* meta, int n,
+                     const uint64_t* off, const uint32_t* size, uint32_t max_size, uint8_t* dst,
+                     void* stream);
+
+/* Token partitions (VP8EncLoop, iterator_enc.c:48; methods 0-2 and
+ * low_memory): per frame, gather the MB rows of the compact raster token
+ * stream into nparts streams, row y into partition y & (nparts - 1), placed
+ * from token round8(tok_cap / 2) of the frame's slab. Each MB's token count
+ * comes from mboff: kind 0 = the count itself (K3N), kind 1 = compact-stream
+ * offsets with the last MB ending at the frame's token count (K3 + k_lowmem);
+ * MBs with the skip flag of a use_skip frame count 0. part[16 f + p] = start
+ * of partition p (tokens from the frame slab), part[16 f + 8 + p] = its token
+ * count; part[16 f] = 0xffffffff when the stream does not fit. */
+int vp8g_launch_partition(uint16_t* tokens, size_t tok_cap, int n, const uint32_t* mboff,
+                          const vp8g_frame_result* results, const uint8_t* mbinfo, int mbw,
+                          int mbh, int kind, int nparts, uint32_t* part, void* stream);
 
 /* Sharp (iterative) RGB->YUV420 for n frames (hip/vp8_sharp.hip), the
  * use_sharp_yuv import (sharpyuv/sharpyuv.c). scratch holds

@@ -20,7 +20,7 @@ class Config(C.Structure):
                 ("emulate_jpeg_size", C.c_int), ("use_sharp_yuv", C.c_int),
                 ("pass_", C.c_int), ("target_size", C.c_int), ("target_PSNR", C.c_float),
                 ("qmin", C.c_int), ("qmax", C.c_int), ("autofilter", C.c_int),
-                ("low_memory", C.c_int)]
+                ("low_memory", C.c_int), ("partitions", C.c_int)]
 
 
 class MBTrace(C.Structure):

@@ -573,6 +573,11 @@ typedef struct {
   /* VP8EncLoop (m0-2): skip probability (frame_enc.c:99-127) */
   int nb_skip, use_skip, skip_proba;
   score_t mb_header_limit;
+  /* token partitions (webp_enc.c:115-122, 209; iterator_enc.c:48): row y's
+   * tokens go to partition y & (num_parts - 1); row_tok[y] = the row's first
+   * token in the final pass */
+  int num_parts;
+  size_t* row_tok;
 } Enc;
 
 typedef struct {
@@ -1887,7 +1892,7 @@ static void code_intra_modes(Enc* e, BW* bw) {
 
 static void put_le32(uint8_t* p, uint32_t v) { p[0] = v; p[1] = v >> 8; p[2] = v >> 16; p[3] = v >> 24; }
 
-static size_t write_stream(Enc* e, BW* part1, uint8_t** out) {
+static size_t write_stream(Enc* e, BW* parts, int nparts, uint8_t** out) {
   BW bw;
   bw_init(&bw);
   bw_put_uniform(&bw, 0);   /* colorspace */
@@ -1906,7 +1911,7 @@ static size_t write_stream(Enc* e, BW* part1, uint8_t** out) {
   bw_put_bits(&bw, e->f_level, 6);
   bw_put_bits(&bw, e->f_sharpness, 3);
   bw_put_uniform(&bw, 0);       /* no lf delta */
-  bw_put_bits(&bw, 0, 2);       /* one token partition */
+  bw_put_bits(&bw, nparts == 8 ? 3 : nparts == 4 ? 2 : nparts == 2 ? 1 : 0, 2);
   bw_put_bits(&bw, e->base_quant, 7);
   bw_put_signed(&bw, 0, 4);
   bw_put_signed(&bw, 0, 4);
@@ -1925,9 +1930,17 @@ static size_t write_stream(Enc* e, BW* part1, uint8_t** out) {
   if (bw_put_uniform(&bw, e->use_skip)) bw_put_bits(&bw, e->skip_proba, 8);   /* tree_enc.c:500-502 */
   code_intra_modes(e, &bw);
   bw_finish(&bw);
-  if (bw.error || part1->error || bw.pos >= (1u << 19)) { free(bw.buf); return 0; }
-  const size_t size0 = bw.pos, size1 = part1->pos;
-  size_t vp8_size = 10 + size0 + size1;
+  if (bw.error || bw.pos >= (1u << 19)) { free(bw.buf); return 0; }
+  size_t size1 = 0;   /* the token partitions, EmitPartitionsSize (syntax_enc.c:248-265) */
+  for (int p = 0; p < nparts; ++p) {
+    if (parts[p].error || (p < nparts - 1 && parts[p].pos >= (1u << 24))) {
+      free(bw.buf);
+      return 0;
+    }
+    size1 += parts[p].pos;
+  }
+  const size_t size0 = bw.pos;
+  size_t vp8_size = 10 + size0 + 3 * (size_t)(nparts - 1) + size1;
   const size_t pad = vp8_size & 1;
   vp8_size += pad;
   const size_t riff_size = 4 + 8 + vp8_size;
@@ -1944,8 +1957,17 @@ static size_t write_stream(Enc* e, BW* part1, uint8_t** out) {
   f[3] = 0x9d; f[4] = 0x01; f[5] = 0x2a;
   f[6] = e->w & 0xff; f[7] = e->w >> 8; f[8] = e->h & 0xff; f[9] = e->h >> 8;
   memcpy(o + 30, bw.buf, size0);
-  if (size1) memcpy(o + 30 + size0, part1->buf, size1);
-  if (pad) o[30 + size0 + size1] = 0;
+  uint8_t* d = o + 30 + size0;
+  for (int p = 0; p < nparts - 1; ++p) {
+    d[0] = (uint8_t)parts[p].pos; d[1] = (uint8_t)(parts[p].pos >> 8);
+    d[2] = (uint8_t)(parts[p].pos >> 16);
+    d += 3;
+  }
+  for (int p = 0; p < nparts; ++p) {
+    if (parts[p].pos) memcpy(d, parts[p].buf, parts[p].pos);
+    d += parts[p].pos;
+  }
+  if (pad) *d = 0;
   free(bw.buf);
   *out = o;
   return total;
@@ -2230,6 +2252,7 @@ static void enc_loop(Enc* e, const vp8o_config* cfg, vp8o_mb_trace* trace, doubl
   it_reset(&it, e);
   do {
     Score rd;
+    if (it.x == 0 && e->row_tok) e->row_tok[it.y] = e->ntok;
     it_import(&it, e);
     const int skip = decimate(&it, e, &rd);
     e->no_tokens = skip && e->use_skip;   /* ResetAfterSkip == the nz of coding zeros */
@@ -2297,8 +2320,10 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
 
   analyze(e);
 
-  BW part1;
-  bw_init(&part1);
+  BW part1[8];
+  e->num_parts = (e->rd_opt == 0 || cfg->low_memory) ? 1 << cfg->partitions : 1;
+  for (int p = 0; p < e->num_parts; ++p) bw_init(&part1[p]);
+  if (e->num_parts > 1) e->row_tok = (size_t*)calloc((size_t)e->mbh + 1, sizeof(size_t));
   It it;
   double (*lf)[64] = cfg->autofilter ? (double (*)[64])calloc(4 * 64, sizeof(double)) : NULL;
   if (e->rd_opt == 0 || cfg->low_memory) {   /* VP8EncLoop: webp_enc.c:115-122 */
@@ -2379,12 +2404,17 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
   if (e->tok_err) goto done;
   if (e->rd_opt > 0 && !cfg->low_memory)   /* enc_loop has settled its probabilities */
     finalize_token_probas(e);
-  for (size_t k = 0; k < e->ntok; ++k) {
-    const uint16_t t = e->tok[k];
-    const int bit = t >> 15;
-    bw_put(&part1, bit, (t & (1u << 14)) ? (t & 0xff) : ((const uint8_t*)e->coeffs)[t & 0x3fff]);
+  if (e->row_tok) e->row_tok[e->mbh] = e->ntok;
+  for (int y = 0; y < (e->row_tok ? e->mbh : 1); ++y) {   /* VP8EmitTokens per partition */
+    BW* pb = &part1[y & (e->num_parts - 1)];
+    const size_t k0 = e->row_tok ? e->row_tok[y] : 0, k1 = e->row_tok ? e->row_tok[y + 1] : e->ntok;
+    for (size_t k = k0; k < k1; ++k) {
+      const uint16_t t = e->tok[k];
+      const int bit = t >> 15;
+      bw_put(pb, bit, (t & (1u << 14)) ? (t & 0xff) : ((const uint8_t*)e->coeffs)[t & 0x3fff]);
+    }
   }
-  bw_finish(&part1);
+  for (int p = 0; p < e->num_parts; ++p) bw_finish(&part1[p]);
   if (lf) {   /* VP8AdjustFilterStrength with -af (filter_enc.c:197-212) */
     for (int sg = 0; sg < 4; ++sg) {
       int best_level = 0;
@@ -2404,10 +2434,11 @@ size_t vp8o_encode_yuv(const uint8_t* Y, const uint8_t* U, const uint8_t* V,
     }
     e->f_level = max_level;
   }
-  result = write_stream(e, &part1, out);
+  result = write_stream(e, part1, e->num_parts, out);
 done:
   free(lf);
-  free(part1.buf);
+  for (int p = 0; p < e->num_parts; ++p) free(part1[p].buf);
+  free(e->row_tok);
   free(e->tok); free(e->mb_type); free(e->mb_uv); free(e->mb_skip); free(e->mb_seg);
   free(e->mb_alpha); free(e->preds_mem); free(e->nz_mem); free(e->y_top); free(e->top_derr);
   free(e);

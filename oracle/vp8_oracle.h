@@ -31,6 +31,7 @@ typedef struct {
   int qmin, qmax;         /* 0..100 */
   int autofilter;         /* 0/1: SSIM-driven per-segment filter levels */
   int low_memory;         /* 0/1: VP8EncLoop for methods 3-6 too */
+  int partitions;         /* 0..3: 2^partitions token partitions (VP8EncLoop only) */
 } vp8o_config;
 
 /* per-macroblock decisions, for stage-by-stage comparison with the GPU */

@@ -14,6 +14,7 @@ Y PSNR / segment levels the reference reports in WebPAuxStats.
   methods012  config->method 0-2 (VP8EncLoop, src/enc/frame_enc.c:614-775)
   dither      config->preprocessing & 2 on ARGB input (src/enc/webp_enc.c:357-365)
   lowmem      config->low_memory with methods 3-6 (VP8EncLoop, frame_enc.c:614-775)
+  partitions  config->partitions with VP8EncLoop (iterator_enc.c:48, syntax_enc.c:248-285)
 """
 import ctypes
 import hashlib
@@ -29,7 +30,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 from libwebp_amd import abi  # noqa: E402
 from libwebp_amd.synth import syn_v1  # noqa: E402
 
-MODULES = ["multipass", "autofilter", "methods012", "dither", "lowmem"]
+MODULES = ["multipass", "autofilter", "methods012", "dither", "lowmem", "partitions"]
 
 
 def main():

@@ -306,24 +306,44 @@ def measured_traffic(kernel, B, W, H, quality, method):
     return (int(k["bytes_per_launch"]) if k else None), d["source"]
 
 
-def host_input_rate(enc, rgba, B, W, H, steps, dev):
+def host_input_rate(encs, rgba, B, W, H, steps, dev):
     """SURVEY.md 8(d) MP/s: RGBA in (pinned) host memory -> .webp bytes in host
-    memory, upload included. Two device buffers, one copy stream each: the
-    upload of step i+1 overlaps the encode of step i."""
+    memory, upload included. Per encoder instance (one host thread each, steps
+    dealt round-robin): two device buffers, one copy stream each, the upload
+    of its step i+1 overlapping its encode of step i (and the other
+    instances' work)."""
+    import threading
     import torch
     pinned = torch.empty(rgba.numel(), dtype=torch.uint8, pin_memory=True)
     pinned.copy_(rgba)
-    bufs = [torch.empty_like(rgba), torch.empty_like(rgba)]
-    cs = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    E = len(encs)
+    bufs = [[torch.empty_like(rgba), torch.empty_like(rgba)] for _ in range(E)]
+    cs = [[torch.cuda.Stream(dev), torch.cuda.Stream(dev)] for _ in range(E)]
+    errors = []
+
+    def worker(e):   # this instance's steps, double-buffered uploads
+        try:
+            mine = list(range(e, steps, E))
+            with torch.cuda.stream(cs[e][0]):
+                bufs[e][0].copy_(pinned, non_blocking=True)
+            for i in range(len(mine)):
+                if i + 1 < len(mine):
+                    with torch.cuda.stream(cs[e][(i + 1) & 1]):
+                        bufs[e][(i + 1) & 1].copy_(pinned, non_blocking=True)
+                encs[e].encode_device(bufs[e][i & 1].data_ptr(), B,
+                                      stream=cs[e][i & 1].cuda_stream)
+        except Exception as ex:   # re-raised below, after every thread ends
+            errors.append(ex)
+
+    th = [threading.Thread(target=worker, args=(e,)) for e in range(E)]
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    with torch.cuda.stream(cs[0]):
-        bufs[0].copy_(pinned, non_blocking=True)
-    for i in range(steps):
-        if i + 1 < steps:
-            with torch.cuda.stream(cs[(i + 1) & 1]):
-                bufs[(i + 1) & 1].copy_(pinned, non_blocking=True)
-        enc.encode_device(bufs[i & 1].data_ptr(), B, stream=cs[i & 1].cuda_stream)
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errors:
+        raise errors[0]
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     del bufs, pinned
@@ -456,7 +476,7 @@ def main(argv=None):
 
     host_rate = None
     if rank == 0 and world == 1 and not args.stub and not args.no_host_input:
-        host_rate = host_input_rate(enc, rgba, B, W, H, max(2, min(args.steps, 4)), dev)
+        host_rate = host_input_rate(encs, rgba, B, W, H, max(3 * E, min(args.steps, 4)), dev)
 
     line = None
     if rank == 0:
@@ -473,7 +493,9 @@ def main(argv=None):
         if host_rate is not None:
             line["host_input_mps"] = round(host_rate, 3)
             line["host_input_note"] = ("RGBA in pinned host memory -> .webp in host memory, "
-                                       "H2D upload of step i+1 overlapped with step i")
+                                       "H2D upload included; %d encoder instance(s), each "
+                                       "uploading step i+1 during its step i"
+                                       % len(encs))
         if cb:
             line["cpu_baseline"] = cb
         if args.stub:

@@ -42,6 +42,7 @@ struct alignas(16) K3G {
   int32_t max_edge[4];
   struct {
     unsigned long long size_p0, sse[3], dist;
+    unsigned long long size_rh;    // sum of the per-MB R + H (OneStatPass, frame_enc.c:593)
     int32_t nb[3];
   } fs;                            // per-frame side statistics (frame_enc.c:480-489, :839)
   int32_t dirty;                   // FinalizeTokenProbas result
@@ -95,6 +96,8 @@ struct K3S {
   int32_t flag_ldc;                // left DC nz flag hand-off from wave 0
   int32_t mdist;                   // VP8ModeScore D of the MB (thread 0 only)
   int32_t d4acc;                   // intra4 D of the blocks chosen so far (thread 0 only)
+  int32_t r4acc;                   // intra4 R of the blocks chosen so far (thread 0 only)
+  int32_t ry16;                    // R of the best intra16 mode
   uint32_t mark_any;
   uint8_t yl_mem[17], ul_mem[9], vl_mem[9];
   uint8_t predleft[4];
@@ -693,7 +696,7 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
   int total_hdr = 0;
   I4Result res;
   res.ok = 1;
-  if (tid == 0) { L.best4[0] = ~0ull; L.d4acc = 0; }
+  if (tid == 0) { L.best4[0] = ~0ull; L.d4acc = 0; L.r4acc = 0; }
   WB();
   for (int i4 = 0; i4 < 16; ++i4) {
     const int bx = i4 & 3, by = i4 >> 2;
@@ -767,6 +770,7 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
         L.sm4[m] = (score_t)(R0 + Rc + H) * S.lambda_mode + dist;
         L.r4[m][0] = H;
         L.r4[m][1] = nzb;
+        L.r4[m][2] = R0 + Rc;   // (the !search pass uses slot 2 for nz instead)
         L.r4[m][3] = D;
       }
     }
@@ -775,7 +779,11 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
     int bm;
     if (search) {
       bm = (int)(L.best4[i4 & 1] & 15);   // argmin, ties to the lower mode
-      if (tid == 0) { L.best4[(i4 + 1) & 1] = ~0ull; L.d4acc += L.r4[bm][3]; }
+      if (tid == 0) {
+        L.best4[(i4 + 1) & 1] = ~0ull;
+        L.d4acc += L.r4[bm][3];
+        L.r4acc += L.r4[bm][2];
+      }
       const int H = L.r4[bm][0], bnzv = L.r4[bm][1];
       accH += H;
       acc_score += L.sm4[bm];
@@ -1010,10 +1018,11 @@ struct XHdr {
   int32_t fold_ptr, epoch, abort, lcver;
   uint32_t ntok;
   int32_t tok_err, pad[2];
-  unsigned long long size_p0, sse[3], dist;
+  unsigned long long size_p0, sse[3], dist, size_rh;
   int32_t nb[3], max_edge[4], pad2;
 };
 #define XS_HDR 128
+static_assert(sizeof(XHdr) <= XS_HDR, "XHdr outgrew its slot");
 #define XS_STATS XS_HDR
 #define XS_COEFFS (XS_STATS + 4 * NSLOT)
 #define XS_LCOEFFS (XS_COEFFS + NSLOT)
@@ -1372,6 +1381,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   if (gt < 4) G.max_edge[gt] = 0;
   if (gt == 0) {
     G.fs.size_p0 = 0; G.fs.sse[0] = G.fs.sse[1] = G.fs.sse[2] = 0; G.fs.dist = 0;
+    G.fs.size_rh = 0;
     G.fs.nb[0] = G.fs.nb[1] = G.fs.nb[2] = 0;
     G.fold_ptr = 0; G.ntok = 0; G.tok_err = 0; G.epoch = 0; G.abort = 0;
   }
@@ -1603,7 +1613,10 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
       score_t rdH = H16;
       uint32_t rd_nz = nz16;
       int is_i16 = 1;
-      if (tid < 64) L.mdist = (int32_t)D16;   // whole wave 0: a lone-lane store here spills
+      if (tid < 64) {   // whole wave 0: a lone-lane store here spills
+        L.mdist = (int32_t)D16;
+        L.ry16 = (int32_t)R16;
+      }
       if ((rd_nz & 0x100ffff) == 0x1000000 && D16 > S.min_disto) {   // StoreMaxDelta
         int mv = iabs_(L.lvdc[best16][1]);
         mv = max(mv, iabs_(L.lvdc[best16][2]));
@@ -1711,6 +1724,11 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
         atomicAdd(&G.fs.nb[is_i16 ? 1 : 0], 1);
         if (skip) atomicAdd(&G.fs.nb[2], 1);
         atomicAdd(&G.fs.size_p0, (unsigned long long)rdH);
+        {   // R of the chosen luma modes + the chosen UV mode's R with its flatness penalty
+          const int ruv = L.mres[bu][1] + ((bu > 0 && L.mres[bu][2] <= 2) ? 140 * 8 : 0);
+          atomicAdd(&G.fs.size_rh,
+                    (unsigned long long)(rdH + (is_i16 ? L.ry16 : L.r4acc) + ruv));
+        }
         atomicAdd(&G.fs.dist, (unsigned long long)L.mdist);
       }
       if (tid < 16) mbinfo[(size_t)mb * VP8G_MBINFO_BYTES + 4 + tid] = L.modes[tid];
@@ -1911,6 +1929,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
   if constexpr (X) {   // this workgroup's share of the side statistics; k_encode_xtail finishes
     if (gt == 0) {
       atomicAdd(&XH->size_p0, G.fs.size_p0);
+      atomicAdd(&XH->size_rh, G.fs.size_rh);
       for (int c = 0; c < 3; ++c) {
         atomicAdd(&XH->sse[c], G.fs.sse[c]);
         atomicAdd(&XH->nb[c], G.fs.nb[c]);
@@ -1937,6 +1956,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
       R->error = G.abort ? 2 : G.tok_err;
       for (int s = 0; s < 4; ++s) R->max_edge[s] = G.max_edge[s];
       R->size_p0 = G.fs.size_p0;
+      R->size_rh = G.fs.size_rh;
       R->sse[0] = G.fs.sse[0]; R->sse[1] = G.fs.sse[1]; R->sse[2] = G.fs.sse[2];
       R->distortion = G.fs.dist;
       R->use_skip = 0;     // the token loop never uses the skip flag (frame_enc.c:805)
@@ -2004,6 +2024,7 @@ __global__ __launch_bounds__(K3T) void k_encode_xtail(K3Args a) {
     R->error = err;
     for (int s = 0; s < 4; ++s) R->max_edge[s] = XH->max_edge[s];
     R->size_p0 = XH->size_p0;
+    R->size_rh = XH->size_rh;
     R->sse[0] = XH->sse[0]; R->sse[1] = XH->sse[1]; R->sse[2] = XH->sse[2];
     R->distortion = XH->dist;
     R->use_skip = 0;

@@ -965,7 +965,7 @@ __global__ __launch_bounds__(64) void k_encode_w1(K3ArgsW1 a) {
           if (sc < best_uv) { bu = mm; best_uv = sc; }
         }
       } else {
-        bu = am & 1;   // method 0 keeps the analysis' UV mode
+        bu = (am & 1) | ((am >> 1) & 2);   // method 0 keeps the preset UV mode (bits 0, 2)
       }
       // ReconstructUV: the DC error diffusion reads errors that RD_OPT_NONE
       // never stores (StoreDiffusionErrors is PickBestUV's), i.e. zeros
@@ -1564,7 +1564,7 @@ __global__ __launch_bounds__(NW * 64) void k_encode_none(K3ArgsW1 a) {
           if (sc < best_uv) { bu = mm; best_uv = sc; }
         }
       } else {
-        bu = am & 1;   // method 0 keeps the analysis' UV mode
+        bu = (am & 1) | ((am >> 1) & 2);   // method 0 keeps the preset UV mode (bits 0, 2)
       }
       // ReconstructUV: the DC error diffusion reads errors that RD_OPT_NONE
       // never stores (StoreDiffusionErrors is PickBestUV's), i.e. zeros
@@ -1768,7 +1768,8 @@ __global__ __launch_bounds__(NW * 64) void k_encode_none(K3ArgsW1 a) {
     // its header estimate is 0 (frame_enc.c:645-646): default probabilities
     if (P->none_finalize) {
       finalize_probas(L0, lane);
-      skip_proba = (int)((uint64_t)(nmb - G.nb[3]) * 255 / nmb);   // CalcSkipProba
+      const int nsk = P->skip_count >= 0 ? P->skip_count : G.nb[3];
+      skip_proba = (int)((uint64_t)(nmb - nsk) * 255 / nmb);   // CalcSkipProba
       use_skip = skip_proba < 250;
     }
     if (lane == 0) { G.use_skip = use_skip; G.skip_proba = skip_proba; }

@@ -390,6 +390,19 @@ fail:
   return 0;
 }
 
+/* VP8AdjustFilterStrength reads dqm->max_edge_, which StoreMaxDelta raises in
+ * every RD_OPT_BASIC decision since the last SetupMatrices: the last StatLoop
+ * pass and the final pass share one set of segment parameters, so the final
+ * maxima include the last StatLoop pass's (lm_max_edge). */
+static void merge_stat_max_edge(WebPGpuBatch* b, int n) {
+  for (int f = 0; f < n; ++f) {
+    vp8g_frame_result* R = &b->h_results[f];
+    if (b->err[f] != VP8_ENC_OK || R->error) continue;
+    for (int sg = 0; sg < 4; ++sg)
+      if (b->frames[f].lm_max_edge[sg] > R->max_edge[sg]) R->max_edge[sg] = b->frames[f].lm_max_edge[sg];
+  }
+}
+
 /* low_memory with methods 3-6: VP8EncLoop (frame_enc.c:614-775). StatLoop
  * passes run K3 at RD_OPT_BASIC with the default probabilities and no cost
  * refreshes; k_lowmem replays the statistics of the probe MBs (method 3: half
@@ -419,6 +432,7 @@ static int lowmem_passes(WebPGpuBatch* b, int n) {
   CHK(hipMemsetAsync(b->d_lmstats, 0, n * VP8G_NUM_SLOTS * sizeof(uint32_t), st));
   for (int f = 0; f < n; ++f) {
     h_nb[f] = nb;
+    memset(b->frames[f].lm_max_edge, 0, sizeof(b->frames[f].lm_max_edge));
     act[f] = b->err[f] == VP8_ENC_OK && vp8h_pass_start(&b->frames[f]);
   }
   CHK(hipMemcpyAsync(b->d_lmi, b->h_lmi, 2 * n * sizeof(int32_t), hipMemcpyHostToDevice, st));
@@ -463,6 +477,8 @@ static int lowmem_passes(WebPGpuBatch* b, int n) {
       vp8h_frame* fr = &b->frames[f];
       const vp8g_frame_result* R = &b->h_results[f];
       if (R->error) { act[f] = 0; continue; }
+      if (!probe)   /* K3's maxima span the whole frame, a probe pass only its MBs */
+        for (int sg = 0; sg < 4; ++sg) fr->lm_max_edge[sg] = R->max_edge[sg];
       /* size_p0 of the probe (frame_enc.c:596, 651-655): K3 sums every MB's
        * info.H; the probe's sum comes from the MBs' modes */
       const uint64_t hdr = probe ? vp8h_mode_header_bits(
@@ -531,6 +547,216 @@ static int lowmem_passes(WebPGpuBatch* b, int n) {
   CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
                      hipMemcpyDeviceToHost, st));
   CHK(hipStreamSynchronize(st));
+  merge_stat_max_edge(b, n);
+  return 1;
+fail:
+  return 0;
+}
+
+/* VP8EncLoop with a size / PSNR search (methods 0-2, or low_memory;
+ * frame_enc.c:574-672, 739-774): StatLoop's passes decide at RD_OPT_BASIC
+ * over every MB (no fast probe while searching) -> K3 with the level costs of
+ * the current probabilities and no refreshes (intra-4 only from method 2,
+ * quant_enc.c:1375-1377), k_lowmem adds every MB's token statistics (kept
+ * across passes, ResetTokenStats runs once) and counts the skips. A size
+ * search finalises the skip flag and the probabilities after each pass
+ * (OneStatPass, :602-607; the next pass's costs follow them when they
+ * changed) and values the pass at (sum R + H + both finalize costs + header
+ * estimate) in bytes; a PSNR search values it by its distortion and
+ * finalises once at the end. The final pass keeps the last pass's segment
+ * parameters: K3 at the method's RD level (low_memory) then k_lowmem's skip
+ * drop, or K3N (methods 0-2) with the StatLoop statistics and skip count. */
+static int statloop_search(WebPGpuBatch* b, int n) {
+  const size_t nmb = (size_t)b->nmb, N = (size_t)b->max_frames;
+  hipStream_t st = b->stream;
+  uint8_t* act = b->pass_act;
+  const int m012 = b->cfg.method < 3;
+  if (!b->d_lmstats) {
+    CHK(hipMalloc((void**)&b->d_lmstats, N * VP8G_NUM_SLOTS * sizeof(uint32_t)));
+    CHK(hipMalloc((void**)&b->d_lmi, 2 * N * sizeof(int32_t)));
+    CHK(hipHostMalloc((void**)&b->h_lmstats, N * VP8G_NUM_SLOTS * sizeof(uint32_t), 0));
+    CHK(hipHostMalloc((void**)&b->h_lmi, 2 * N * sizeof(int32_t), 0));
+  }
+  if (!b->h_active) {
+    CHK(hipHostMalloc((void**)&b->h_active, N, 0));
+    CHK(hipMalloc((void**)&b->d_active, N));
+  }
+  if (!b->h_state)
+    CHK(hipHostMalloc((void**)&b->h_state, N * VP8G_RERUN_STATE_BYTES, 0));
+  int32_t* h_nb = b->h_lmi;          /* statistics MBs per frame: all of them */
+  int32_t* h_nskip = b->h_lmi + N;   /* their skips */
+  CHK(hipMemsetAsync(b->d_lmstats, 0, n * VP8G_NUM_SLOTS * sizeof(uint32_t), st));
+  for (int f = 0; f < n; ++f) {
+    h_nb[f] = (int32_t)nmb;
+    uint8_t* S = b->h_state + (size_t)f * VP8G_RERUN_STATE_BYTES;
+    vp8h_default_probas(S);                        /* the probabilities of the level costs */
+    vp8h_default_probas(S + VP8G_STATE_COEFFS);    /* the current probabilities */
+    b->frames[f].npass = 0;
+    b->frames[f].lm_nskip = 0;
+    b->frames[f].lm_skip_proba = 255;
+    memset(b->frames[f].lm_max_edge, 0, sizeof(b->frames[f].lm_max_edge));
+    act[f] = b->err[f] == VP8_ENC_OK && vp8h_pass_start(&b->frames[f]);
+  }
+  CHK(hipMemcpyAsync(b->d_lmi, b->h_lmi, 2 * n * sizeof(int32_t), hipMemcpyHostToDevice, st));
+  int first = 1;
+  for (;;) {
+    int nact = 0;
+    for (int f = 0; f < n; ++f) {
+      vp8g_frame_params* P = &b->h_params[f];
+      b->h_active[f] = act[f];
+      if (!act[f]) { P->pass_mode = 2; continue; }
+      vp8h_frame* fr = &b->frames[f];
+      vp8h_set_loop_params(fr, fr->ps_q, b->h_segmap + f * nmb, P);
+      P->rd_opt = 1;                /* RD_OPT_BASIC */
+      P->max_count = 0x7fffffff;    /* no refreshes inside a pass */
+      P->pass_mode = fr->npass == 0 ? 0 : 1;   /* later passes: the costs of S */
+      P->max_i4_header_bits = fr->method >= 2 ? fr->max_i4_header_bits : 0;
+      P->recon_addr = 0;
+      ++fr->npass;
+      ++nact;
+    }
+    if (!nact) break;
+    CHK(hipMemcpyAsync(b->d_segmap, b->h_segmap, n * nmb, hipMemcpyHostToDevice, st));
+    CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
+                       hipMemcpyHostToDevice, st));
+    CHK(hipMemcpyAsync(b->d_active, b->h_active, n, hipMemcpyHostToDevice, st));
+    CHK(hipMemcpyAsync(b->d_rerun, b->h_state, n * VP8G_RERUN_STATE_BYTES, hipMemcpyHostToDevice,
+                       st));
+    if (first) CHK(hipEventRecord(b->ev[2], st));
+    first = 0;
+    if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params,
+                            b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5,
+                            b->d_results, b->d_rerun, NULL, b->d_xsync, st))
+      return 0;
+    if (!vp8g_launch_lowmem(b->d_tokens, b->tok_cap, b->d_mboff, b->d_results, b->d_mbinfo,
+                            (int)nmb, n, b->d_lmi, b->d_active, 0, b->d_lmstats, b->d_lmi + N, st))
+      return 0;
+    CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
+                       hipMemcpyDeviceToHost, st));
+    CHK(hipMemcpyAsync(b->h_lmstats, b->d_lmstats, n * VP8G_NUM_SLOTS * sizeof(uint32_t),
+                       hipMemcpyDeviceToHost, st));
+    CHK(hipMemcpyAsync(h_nskip, b->d_lmi + N, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    CHK(hipStreamSynchronize(st));
+    for (int f = 0; f < n; ++f) {
+      if (!act[f]) continue;
+      vp8h_frame* fr = &b->frames[f];
+      const vp8g_frame_result* R = &b->h_results[f];
+      if (R->error) { act[f] = 0; continue; }
+      fr->lm_nskip = h_nskip[f];
+      for (int sg = 0; sg < 4; ++sg) fr->lm_max_edge[sg] = R->max_edge[sg];
+      const uint64_t size_p0 = R->size_p0 + (uint64_t)fr->seg_hdr_size;
+      if (fr->do_size_search) {   /* OneStatPass, :602-607 */
+        uint8_t* S = b->h_state + (size_t)f * VP8G_RERUN_STATE_BYTES;
+        int use_skip = 0, dirty = 0;
+        uint64_t size = R->size_rh;
+        size += (uint64_t)vp8h_finalize_skip(h_nskip[f], (int)nmb, &fr->lm_skip_proba, &use_skip);
+        size += (uint64_t)vp8h_finalize_probas(b->h_lmstats + (size_t)f * VP8G_NUM_SLOTS,
+                                               S + VP8G_STATE_COEFFS, &dirty);
+        if (dirty) memcpy(S, S + VP8G_STATE_COEFFS, VP8G_NUM_SLOTS);   /* VP8CalculateLevelCosts */
+        fr->ps_value = (double)(((size + size_p0 + 1024) >> 11) + (12 + 8 + 10));
+      } else {
+        fr->ps_value = vp8h_psnr(R->distortion, (uint64_t)nmb * 384);
+      }
+      act[f] = vp8h_statloop_finish(fr, size_p0) && vp8h_pass_start(fr);
+    }
+  }
+  /* the final pass */
+  int nfinal = 0;
+  for (int f = 0; f < n; ++f) {
+    vp8g_frame_params* P = &b->h_params[f];
+    vp8h_frame* fr = &b->frames[f];
+    b->h_active[f] = 0;
+    if (b->err[f] != VP8_ENC_OK || b->h_results[f].error) { P->pass_mode = 2; continue; }
+    uint8_t* S = b->h_state + (size_t)f * VP8G_RERUN_STATE_BYTES;
+    const uint32_t* stats = b->h_lmstats + (size_t)f * VP8G_NUM_SLOTS;
+    if (!fr->do_size_search) {   /* StatLoop's own finalisation, :665-669 */
+      int use_skip = 0, dirty = 0;
+      vp8h_finalize_skip(fr->lm_nskip, (int)nmb, &fr->lm_skip_proba, &use_skip);
+      vp8h_finalize_probas(stats, S + VP8G_STATE_COEFFS, &dirty);
+      if (dirty) memcpy(S, S + VP8G_STATE_COEFFS, VP8G_NUM_SLOTS);
+    }
+    /* the segment parameters stay those of the last pass (P as set then) */
+    P->max_i4_header_bits = fr->max_i4_header_bits;
+    P->recon_addr = b->cfg.autofilter ? (uint64_t)(uintptr_t)(b->d_recon + (size_t)f * nmb * 512) : 0;
+    if (m012) {   /* K3N with StatLoop's statistics and skip count */
+      P->rd_opt = 0;
+      P->max_count = 0x7fffffff;
+      P->pass_mode = 3;
+      P->nb_stat = 0;
+      P->none_finalize = 1;
+      P->skip_count = fr->lm_nskip;
+      memcpy(S + VP8G_STATE_STATS, stats, VP8G_NUM_SLOTS * sizeof(uint32_t));
+    } else {      /* K3 at the method's RD level with the costs frozen */
+      b->h_active[f] = fr->lm_skip_proba < 250;   /* use_skip_proba */
+      P->rd_opt = fr->rd_opt;
+      P->max_count = 0x7fffffff;
+      P->pass_mode = 1;
+    }
+    ++nfinal;
+  }
+  if (!nfinal) {
+    CHK(hipEventRecord(b->ev[3], st));
+    return 1;
+  }
+  if (m012 && b->cfg.method < 2) {
+    /* RefineUsingDistortion's presets for methods 0-1 are the MB type and UV
+     * mode the last StatLoop pass chose (PickBestIntra16/4/UV set them in
+     * the MB info, quant_enc.c:1058,1161,1215): K3N's mode byte, bit 1 =
+     * intra-4, bits 0 and 2 = the UV mode */
+    CHK(hipMemcpyAsync(b->h_mbinfo, b->d_mbinfo, n * nmb * VP8G_MBINFO_BYTES,
+                       hipMemcpyDeviceToHost, st));
+    CHK(hipStreamSynchronize(st));
+    uint8_t* am = (uint8_t*)malloc(n * nmb);
+    if (!am) return 0;
+    for (size_t k = 0; k < n * nmb; ++k) {
+      const uint8_t* in = b->h_mbinfo + k * VP8G_MBINFO_BYTES;
+      am[k] = (uint8_t)((in[1] & 1) | ((in[0] == 0) << 1) | ((in[1] >> 1) << 2));
+    }
+    const hipError_t e1 = hipMemcpy(b->d_amode, am, n * nmb, hipMemcpyHostToDevice);
+    free(am);
+    CHK(e1);
+  }
+  CHK(hipMemcpyAsync(b->d_rerun, b->h_state, n * VP8G_RERUN_STATE_BYTES, hipMemcpyHostToDevice, st));
+  CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
+                     hipMemcpyHostToDevice, st));
+  if (m012) {
+    if (!vp8g_launch_encode_none(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_amode,
+                                 b->d_params, b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff,
+                                 b->d_results, b->d_rerun, st))
+      return 0;
+    CHK(hipEventRecord(b->ev[3], st));
+    CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
+                       hipMemcpyDeviceToHost, st));
+    CHK(hipStreamSynchronize(st));
+    merge_stat_max_edge(b, n);
+    return 1;
+  }
+  if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
+                          b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5, b->d_results,
+                          b->d_rerun, b->cfg.autofilter ? b->d_recon : NULL, b->d_xsync, st))
+    return 0;
+  CHK(hipEventRecord(b->ev[3], st));
+  CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
+                     hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  for (int f = 0; f < n; ++f) {   /* the emitted probabilities are StatLoop's */
+    if (b->h_params[f].pass_mode != 1 || b->h_results[f].error) continue;
+    vp8g_frame_result* R = &b->h_results[f];
+    memcpy(R->probas, b->h_state + (size_t)f * VP8G_RERUN_STATE_BYTES + VP8G_STATE_COEFFS,
+           VP8G_NUM_SLOTS);
+    R->use_skip = (int16_t)b->h_active[f];
+    R->skip_proba = (int16_t)b->frames[f].lm_skip_proba;
+  }
+  CHK(hipMemcpyAsync(b->d_results, b->h_results, n * sizeof(vp8g_frame_result),
+                     hipMemcpyHostToDevice, st));
+  CHK(hipMemcpyAsync(b->d_active, b->h_active, n, hipMemcpyHostToDevice, st));
+  if (!vp8g_launch_lowmem(b->d_tokens, b->tok_cap, b->d_mboff, b->d_results, b->d_mbinfo,
+                          (int)nmb, n, b->d_lmi, b->d_active, 1, b->d_lmstats, b->d_lmi + N, st))
+    return 0;
+  CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
+                     hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  merge_stat_max_edge(b, n);
   return 1;
 fail:
   return 0;
@@ -568,12 +794,18 @@ static int run_passes(WebPGpuBatch* b, int n) {
    * webp_enc.c:115-122); methods 0-2 already run VP8EncLoop and encode exactly
    * as without the flag */
   const int lowmem = b->cfg.low_memory && b->cfg.method >= 3;
-  if (lowmem) {
+  /* a size / PSNR search under VP8EncLoop (methods 0-2 or low_memory) */
+  const int search = (b->cfg.method < 3 || b->cfg.low_memory) &&
+                     (b->cfg.target_size > 0 || b->cfg.target_PSNR > 0);
+  if (search) {
+    if (!statloop_search(b, n)) return 0;
+    round = 1;
+  } else if (lowmem) {
     if (!lowmem_passes(b, n)) return 0;
     round = 1;
   }
   for (int f = 0; f < n; ++f)
-    act[f] = !lowmem && b->err[f] == VP8_ENC_OK && vp8h_pass_start(&b->frames[f]);
+    act[f] = !lowmem && !search && b->err[f] == VP8_ENC_OK && vp8h_pass_start(&b->frames[f]);
   for (;;) {
     int nact = 0, nsize = 0;
     for (int f = 0; f < n; ++f) {

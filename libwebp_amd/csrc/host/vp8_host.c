@@ -51,12 +51,6 @@ int vp8h_use_sharp(const WebPConfig* cfg, int w, int h) {
 int vp8h_frame_init(vp8h_frame* fr, const WebPConfig* cfg, int w, int h) {
   memset(fr, 0, sizeof(*fr));
   if (cfg->method < 0 || cfg->method > 6) return 0;
-  /* methods 0-2 run VP8EncLoop (RD_OPT_NONE): its size / PSNR search passes
-   * (StatLoop with RD_OPT_BASIC, frame_enc.c:614-674) are not implemented */
-  if (cfg->method < 3 && (cfg->target_size > 0 || cfg->target_PSNR > 0)) return 0;
-  /* low_memory runs VP8EncLoop for methods 3-6 too; its size / PSNR search
-   * is not implemented */
-  if (cfg->low_memory && (cfg->target_size > 0 || cfg->target_PSNR > 0)) return 0;
   /* token partitions: VP8EncLoop writes MB row y into partition
    * y & (2^partitions - 1); the token loop (methods 3-6 without low_memory)
    * keeps one (webp_enc.c:115-122, 209) */
@@ -132,6 +126,35 @@ static void compute_next_q(vp8h_frame* s) {   /* ComputeNextQ, :60-80 */
   s->ps_last_q = s->ps_q;
   s->ps_last_value = s->ps_value;
   s->ps_q = clampf(s->ps_q + s->ps_dq, s->ps_qmin, s->ps_qmax);
+}
+
+/* StatLoop's pass control (frame_enc.c:640-664): like the token loop's, but a
+ * search step that lands within DQ_LIMIT ends the loop at once (the new q is
+ * never run: the final pass keeps the last pass's segment parameters) */
+int vp8h_statloop_finish(vp8h_frame* fr, uint64_t size_p0) {
+  if (size_p0 == 0) return 0;   /* :646 */
+  if (fr->max_i4_header_bits > 0 && size_p0 > VP8H_P0_LIMIT) {
+    ++fr->pass_left;
+    fr->max_i4_header_bits >>= 1;
+    return 1;
+  }
+  if (fr->is_last_pass) return 0;
+  if (fr->do_search) {
+    compute_next_q(fr);
+    if (fabs(fr->ps_dq) <= DQ_LIMIT) return 0;
+  }
+  return fr->pass_left > 0;
+}
+
+/* FinalizeSkipProba (frame_enc.c:111-127): the skip probability from the
+ * pass's skip count, whether it pays, and its header cost (1/256 bit) */
+int vp8h_finalize_skip(int nb_skip, int nmb, int* skip_proba, int* use_skip) {
+  const int p = nmb ? (int)((uint64_t)(nmb - nb_skip) * 255 / nmb) : 255;   /* CalcSkipProba */
+  *skip_proba = p;
+  *use_skip = p < 250;
+  int size = 256;
+  if (*use_skip) size += nb_skip * bit_cost(1, p) + (nmb - nb_skip) * bit_cost(0, p) + 8 * 256;
+  return size;
 }
 
 int vp8h_pass_finish(vp8h_frame* fr, uint64_t size_p0) {
@@ -474,6 +497,7 @@ void vp8h_set_loop_params(vp8h_frame* fr, float quality, uint8_t* segmap, vp8g_f
   P->mb_header_limit = (int32_t)((int64_t)256 * 510 * 8 * 1024 / nmb);
   P->nb_stat = fr->method == 0 ? ((nmb > 200) ? nmb >> 2 : 50) : nmb;
   P->none_finalize = fr->seg_hdr_size != 0;
+  P->skip_count = -1;
   if (fr->rd_opt == 0) P->max_count = 0x7fffffff;
 }
 

@@ -40,6 +40,9 @@ typedef struct {
   int f_simple, f_level, f_sharpness;
   /* multi-pass convergence (PassStats, frame_enc.c:38-80) */
   int lm_skip_proba;   /* low_memory: StatLoop's skip probability */
+  int lm_nskip;        /* StatLoop search: the last pass's skip count */
+  int lm_max_edge[4];  /* StatLoop at RD_OPT_BASIC: the last pass's StoreMaxDelta maxima
+                          (SetupMatrices resets them per pass, quant_enc.c:283) */
   int autofilter;   /* segment filter levels from the GPU SSIM search (filter_enc.c:156-212) */
   int cfg_pass, pass_left, is_last_pass, npass, do_search, do_size_search, ps_is_first;
   float ps_dq, ps_q, ps_last_q, ps_qmin, ps_qmax;
@@ -83,6 +86,12 @@ void vp8h_set_loop_params(vp8h_frame* fr, float q, uint8_t* segmap, vp8g_frame_p
  * (ComputeNextQ, :60-80). */
 int vp8h_pass_start(vp8h_frame* fr);
 int vp8h_pass_finish(vp8h_frame* fr, uint64_t size_p0);
+/* StatLoop's pass loop (VP8EncLoop with a size / PSNR search, frame_enc.c:
+ * 614-672) with the same vp8h_pass_start; returns 1 when another pass
+ * follows */
+int vp8h_statloop_finish(vp8h_frame* fr, uint64_t size_p0);
+/* FinalizeSkipProba (frame_enc.c:111-127): returns the size term */
+int vp8h_finalize_skip(int nb_skip, int nmb, int* skip_proba, int* use_skip);
 /* FinalizeTokenProbas (frame_enc.c:146-180) from the token statistics:
  * writes the probabilities, returns the proba-update header cost (1/256
  * bit); *dirty = some probability differs from the default table */

@@ -63,7 +63,8 @@ typedef struct {
   int32_t mb_header_limit;  /* webp_enc.c:109-110 */
   int32_t nb_stat;          /* MBs of the statistics pass (StatLoop's fast probe) */
   int32_t none_finalize;    /* the statistics pass finalises the probabilities */
-  int32_t pad1;
+  int32_t skip_count;       /* >= 0: FinalizeSkipProba's skip count, StatLoop having run as
+                               K3 passes (a size / PSNR search); -1: the probe's own */
 } vp8g_frame_params;
 
 /* per-frame cost state K3 leaves for the next pass: the probabilities the
@@ -82,6 +83,8 @@ typedef struct {
   uint64_t size_p0;      /* sum of per-MB header-bit estimates (frame_enc.c:839) */
   uint64_t sse[3];
   uint64_t distortion;   /* sum of the per-MB VP8ModeScore D (frame_enc.c:840) */
+  uint64_t size_rh;      /* sum of the per-MB R + H (OneStatPass's size, frame_enc.c:593);
+                            K3 only */
   int32_t block_count[3];
   int16_t use_skip, skip_proba;   /* RD_OPT_NONE: FinalizeSkipProba (frame_enc.c:111-127) */
   uint64_t stamps[8];    /* per-stage shader-clock cycles summed over MBs (profiling) */

@@ -15,6 +15,7 @@ Y PSNR / segment levels the reference reports in WebPAuxStats.
   dither      config->preprocessing & 2 on ARGB input (src/enc/webp_enc.c:357-365)
   lowmem      config->low_memory with methods 3-6 (VP8EncLoop, frame_enc.c:614-775)
   partitions  config->partitions with VP8EncLoop (iterator_enc.c:48, syntax_enc.c:248-285)
+  statloop_search  target_size / target_PSNR under VP8EncLoop (frame_enc.c:574-672)
 """
 import ctypes
 import hashlib
@@ -30,7 +31,8 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 from libwebp_amd import abi  # noqa: E402
 from libwebp_amd.synth import syn_v1  # noqa: E402
 
-MODULES = ["multipass", "autofilter", "methods012", "dither", "lowmem", "partitions"]
+MODULES = ["multipass", "autofilter", "methods012", "dither", "lowmem", "partitions",
+           "statloop_search"]
 
 
 def main():

@@ -93,11 +93,3 @@ def test_gpu_batch_lowmem(gpu):
         for f in range(n):
             assert enc.output(f) == oracle.encode_rgba(frames[f], **kw), (m, f)
         enc.close()
-
-
-@pytest.mark.gpu
-def test_gpu_lowmem_unsupported_fail_loudly(gpu):
-    img = syn_v1(64, 48, 0)
-    for kw in ({"method": 4, "target_size": 2000, "pass": 4}, {"method": 5, "target_PSNR": 40.0}):
-        with pytest.raises(RuntimeError):
-            gpu.encode_rgba(img, quality=75.0, low_memory=1, **kw)

@@ -477,7 +477,9 @@ static int lowmem_passes(WebPGpuBatch* b, int n) {
       vp8h_frame* fr = &b->frames[f];
       const vp8g_frame_result* R = &b->h_results[f];
       if (R->error) { act[f] = 0; continue; }
-      if (!probe)   /* K3's maxima span the whole frame, a probe pass only its MBs */
+      /* K3's maxima span the whole frame: merged only when the pass covers
+       * every MB (a method-3 probe's own maxima are not available) */
+      if (!probe)
         for (int sg = 0; sg < 4; ++sg) fr->lm_max_edge[sg] = R->max_edge[sg];
       /* size_p0 of the probe (frame_enc.c:596, 651-655): K3 sums every MB's
        * info.H; the probe's sum comes from the MBs' modes */

@@ -1724,7 +1724,8 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
         atomicAdd(&G.fs.nb[is_i16 ? 1 : 0], 1);
         if (skip) atomicAdd(&G.fs.nb[2], 1);
         atomicAdd(&G.fs.size_p0, (unsigned long long)rdH);
-        {   // R of the chosen luma modes + the chosen UV mode's R with its flatness penalty
+        if constexpr (!TR) {   // R of the chosen luma modes + the chosen UV mode's R
+          // with its flatness penalty (StatLoop passes run RD_OPT_BASIC, never TR)
           const int ruv = L.mres[bu][1] + ((bu > 0 && L.mres[bu][2] <= 2) ? 140 * 8 : 0);
           atomicAdd(&G.fs.size_rh,
                     (unsigned long long)(rdH + (is_i16 ? L.ry16 : L.r4acc) + ruv));

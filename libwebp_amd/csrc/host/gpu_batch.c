@@ -626,8 +626,9 @@ static int statloop_search(WebPGpuBatch* b, int n) {
                        st));
     if (first) CHK(hipEventRecord(b->ev[2], st));
     first = 0;
+    /* RD_OPT_BASIC: the instantiation without trellis paths (it sums R + H) */
     if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params,
-                            b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5,
+                            b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff, 0,
                             b->d_results, b->d_rerun, NULL, b->d_xsync, st))
       return 0;
     if (!vp8g_launch_lowmem(b->d_tokens, b->tok_cap, b->d_mboff, b->d_results, b->d_mbinfo,

@@ -115,6 +115,29 @@ __device__ __forceinline__ void fdct4(const uint8_t* src, int ss, const uint8_t*
   }
 }
 
+// the same transform of a residual block d (row-major 4x4)
+__device__ __forceinline__ void fdct4_res(const int d[16], int out[16]) {
+  int t[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int d0 = d[4 * i], d1 = d[4 * i + 1], d2 = d[4 * i + 2], d3 = d[4 * i + 3];
+    const int a0 = d0 + d3, a1 = d1 + d2, a2 = d1 - d2, a3 = d0 - d3;
+    t[4 * i + 0] = (a0 + a1) * 8;
+    t[4 * i + 1] = (a2 * 2217 + a3 * 5352 + 1812) >> 9;
+    t[4 * i + 2] = (a0 - a1) * 8;
+    t[4 * i + 3] = (a3 * 2217 - a2 * 5352 + 937) >> 9;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int a0 = t[i] + t[12 + i], a1 = t[4 + i] + t[8 + i];
+    const int a2 = t[4 + i] - t[8 + i], a3 = t[i] - t[12 + i];
+    out[i] = (int16_t)((a0 + a1 + 7) >> 4);
+    out[4 + i] = (int16_t)(((a2 * 2217 + a3 * 5352 + 12000) >> 16) + (a3 != 0));
+    out[8 + i] = (int16_t)((a0 - a1 + 7) >> 4);
+    out[12 + i] = (int16_t)((a3 * 2217 - a2 * 5352 + 51000) >> 16);
+  }
+}
+
 #define IMUL(a, b) (((a) * (b)) >> 16)
 __device__ __forceinline__ void idct4(const uint8_t* ref, int rs, const int in[16], uint8_t* dst,
                                       int ds) {

@@ -202,16 +202,20 @@ __global__ __launch_bounds__(256) void k_cleanup_alpha(uint8_t* __restrict__ yuv
 
 // ---------------------------------------------------------------------------
 // K2: analysis (analysis_enc.c:230-333, iterator_enc.c:147-173; histogram
-// dsp/enc.c:46-81). One wavefront per MB, 4 MBs per 256-thread workgroup.
+// dsp/enc.c:46-81). A 256-thread workgroup takes a strip of K2_STRIP MBs of
+// one MB row: the strip's Y/U/V pixels plus the row above and the column to
+// the left are staged in LDS with coalesced loads (edge replication by
+// clamping to the picture, which is iterator_enc.c's import), then each
+// wavefront analyses K2_STRIP / 4 of the MBs from LDS.
+
+#define K2_STRIP 8
+#define K2_YW (16 * K2_STRIP + 4)   // Y tile row: column -1 .. 16*K2_STRIP-1 (+pad)
+#define K2_CW (8 * K2_STRIP + 4)    // U/V tile row: column -1 .. 8*K2_STRIP-1 (+pad)
 
 struct K2Wave {
-  uint8_t yin[16 * BPS];
-  uint8_t p16[2][256];
-  uint8_t puv[2][128];
   uint8_t yl[17], ul[9], vl[9];
   uint8_t top[32];
   int hist[4][32];
-  uint32_t dc[16];
 };
 
 __global__ __launch_bounds__(256) void k_analyze(const uint8_t* __restrict__ yuv, size_t yfb,
@@ -219,135 +223,164 @@ __global__ __launch_bounds__(256) void k_analyze(const uint8_t* __restrict__ yuv
                                                  uint8_t* __restrict__ mb_alpha,
                                                  uint16_t* __restrict__ mb_uva, int fast_q,
                                                  uint8_t* __restrict__ mb_amode) {
+  __shared__ uint8_t ty[17 * K2_YW];       // row 0 = the row above the strip
+  __shared__ uint8_t tu[9 * K2_CW], tv[9 * K2_CW];
   __shared__ K2Wave S[4];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int mb = blockIdx.x * 4 + wave;
-  const int f = blockIdx.y;
-  if (mb >= nmb) return;
-  K2Wave& L = S[wave];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tid = threadIdx.x;
+  const int f = blockIdx.z, y = blockIdx.y, x0 = blockIdx.x * K2_STRIP;
   const int mbw = (w + 15) >> 4;
-  const int x = mb % mbw, y = mb / mbw;
   const int uvw = (w + 1) >> 1, uvh = (h + 1) >> 1;
   const uint8_t* Yp = yuv + f * yfb;
   const uint8_t* Up = Yp + (size_t)w * h;
   const uint8_t* Vp = Up + (size_t)uvw * uvh;
-  load_mb(Yp, Up, Vp, w, h, x, y, L.yin, lane, 64);
-  const int bw = min(w - 16 * x, 16), bh = min(h - 16 * y, 16);
-  const int cw = (bw + 1) >> 1, ch = (bh + 1) >> 1;
-  uint8_t* yl = L.yl + 1;
-  uint8_t* ul = L.ul + 1;
-  uint8_t* vl = L.vl + 1;
-  // source boundary
-  if (lane < 32) {
-    const int i = lane;
-    if (x == 0) {
-      if (i < 16) yl[i] = 129;
-      if (i < 8) { ul[i] = 129; vl[i] = 129; }
-      if (i == 0) yl[-1] = ul[-1] = vl[-1] = (y > 0) ? 129 : 127;
-    } else {
-      if (i < 16) yl[i] = Yp[(size_t)(16 * y + min(i, bh - 1)) * w + 16 * x - 1];
-      if (i < 8) {
-        ul[i] = Up[(size_t)(8 * y + min(i, ch - 1)) * uvw + 8 * x - 1];
-        vl[i] = Vp[(size_t)(8 * y + min(i, ch - 1)) * uvw + 8 * x - 1];
-      }
-      if (i == 0) {
-        if (y == 0) {
-          yl[-1] = ul[-1] = vl[-1] = 127;
-        } else {
-          yl[-1] = Yp[(size_t)(16 * y - 1) * w + 16 * x - 1];
-          ul[-1] = Up[(size_t)(8 * y - 1) * uvw + 8 * x - 1];
-          vl[-1] = Vp[(size_t)(8 * y - 1) * uvw + 8 * x - 1];
+  // ---- strip tiles: tile (r, c) = picture (16y - 1 + r, 16x0 - 1 + c), clamped
+  for (int k = tid; k < 17 * (16 * K2_STRIP + 1); k += 256) {
+    const int r = k / (16 * K2_STRIP + 1), c = k % (16 * K2_STRIP + 1);
+    const int gy = min(max(16 * y - 1 + r, 0), h - 1), gx = min(max(16 * x0 - 1 + c, 0), w - 1);
+    ty[r * K2_YW + c] = Yp[(size_t)gy * w + gx];
+  }
+  for (int k = tid; k < 2 * 9 * (8 * K2_STRIP + 1); k += 256) {
+    const int pl = k / (9 * (8 * K2_STRIP + 1)), kk = k % (9 * (8 * K2_STRIP + 1));
+    const int r = kk / (8 * K2_STRIP + 1), c = kk % (8 * K2_STRIP + 1);
+    const int gy = min(max(8 * y - 1 + r, 0), uvh - 1), gx = min(max(8 * x0 - 1 + c, 0), uvw - 1);
+    (pl ? tv : tu)[r * K2_CW + c] = (pl ? Vp : Up)[(size_t)gy * uvw + gx];
+  }
+  __syncthreads();
+  K2Wave& L = S[wave];
+  for (int it = 0; it < K2_STRIP / 4; ++it) {   // uniform trip count: the barriers below
+    const int xl = wave + 4 * it, x = x0 + xl;
+    const bool valid = x < mbw;
+    const int mb = y * mbw + x;
+    // this MB's pixels in the tiles: Y at (1, 1 + 16 xl), U/V at (1, 1 + 8 xl)
+    const uint8_t* yin = ty + K2_YW + 1 + 16 * xl;
+    const uint8_t* uin = tu + K2_CW + 1 + 8 * xl;
+    const uint8_t* vin = tv + K2_CW + 1 + 8 * xl;
+    uint8_t* yl = L.yl + 1;
+    uint8_t* ul = L.ul + 1;
+    uint8_t* vl = L.vl + 1;
+    if (lane < 32) {   // source boundary (iterator_enc.c:147-173)
+      const int i = lane;
+      if (x == 0) {
+        if (i < 16) yl[i] = 129;
+        if (i < 8) { ul[i] = 129; vl[i] = 129; }
+        if (i == 0) yl[-1] = ul[-1] = vl[-1] = (y > 0) ? 129 : 127;
+      } else {
+        if (i < 16) yl[i] = yin[i * K2_YW - 1];
+        if (i < 8) { ul[i] = uin[i * K2_CW - 1]; vl[i] = vin[i * K2_CW - 1]; }
+        if (i == 0) {
+          if (y == 0) {
+            yl[-1] = ul[-1] = vl[-1] = 127;
+          } else {
+            yl[-1] = yin[-K2_YW - 1]; ul[-1] = uin[-K2_CW - 1]; vl[-1] = vin[-K2_CW - 1];
+          }
         }
       }
+      if (y == 0) L.top[i] = 127;
+      else if (i < 16) L.top[i] = yin[i - K2_YW];
+      else L.top[i] = (i < 24 ? uin : vin)[(i & 7) - K2_CW];
     }
-    if (y == 0) {
-      L.top[i] = 127;
-    } else if (i < 16) {
-      L.top[i] = Yp[(size_t)(16 * y - 1) * w + 16 * x + min(i, bw - 1)];
-    } else {
-      const int k = i & 7;
-      const uint8_t* P = (i < 24) ? Up : Vp;
-      L.top[i] = P[(size_t)(8 * y - 1) * uvw + 8 * x + min(k, cw - 1)];
-    }
-  }
-  for (int k = lane; k < 4 * 32; k += 64) (&L.hist[0][0])[k] = 0;
-  __syncthreads();
-  const bool hl = x > 0, ht = y > 0;
-  {
-    const int dcy = dc_value(yl, L.top, hl, ht, 16, 5);
-    for (int k = lane; k < 512; k += 64) {
-      const int m = k >> 8, p = k & 255;
-      L.p16[m][p] = pred_sample(m, 16, p & 15, p >> 4, yl, L.top, hl, ht, dcy);
-    }
-    const int dcu = dc_value(ul, L.top + 16, hl, ht, 8, 4);
-    const int dcv = dc_value(vl, L.top + 24, hl, ht, 8, 4);
-    for (int k = lane; k < 256; k += 64) {
-      const int m = k >> 7, p = k & 127, px = p & 15, py = p >> 4;
-      const int c = px >> 3;
-      L.puv[m][p] = pred_sample(m, 8, px & 7, py, c ? vl : ul, L.top + 16 + 8 * c, hl, ht,
-                                c ? dcv : dcu);
-    }
-  }
-  __syncthreads();
-  if (lane < 48) {
-    int coeffs[16], hsel;
-    if (lane < 32) {
-      const int m = lane >> 4, b = lane & 15;
-      fdct4(L.yin + (b >> 2) * 4 * BPS + (b & 3) * 4, BPS, L.p16[m] + (b >> 2) * 64 + (b & 3) * 4,
-            16, coeffs);
-      hsel = m;
-    } else {
-      const int m = (lane - 32) >> 3, b = lane & 7, c = b >> 2, k = b & 3;
-      fdct4(L.yin + 16 + 8 * c + (k >> 1) * 4 * BPS + (k & 1) * 4, BPS,
-            L.puv[m] + 8 * c + (k >> 1) * 64 + (k & 1) * 4, 16, coeffs);
-      hsel = 2 + m;
-    }
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int v = min(iabs_(coeffs[k]) >> 3, 31);
-      atomicAdd(&L.hist[hsel][v], 1);
-    }
-  }
-  if (fast_q >= 0 && lane < 16) {   // VP8Mean16x4 block sums (dsp/enc.c:594-608)
-    uint32_t dc = 0;
-    for (int k = 0; k < 16; ++k) dc += L.yin[(4 * (lane >> 2) + (k >> 2)) * BPS + 4 * (lane & 3) + (k & 3)];
-    L.dc[lane] = dc;
-  }
-  __syncthreads();
-  if (lane == 0) {
-    int alpha[4];
-    for (int hh = 0; hh < 4; ++hh) {
-      int maxv = 0, last = 1;
-      for (int k = 0; k < 32; ++k) {
-        const int v = L.hist[hh][k];
-        if (v > 0) { if (v > maxv) maxv = v; last = k; }
+    for (int k = lane; k < 4 * 32; k += 64) (&L.hist[0][0])[k] = 0;
+    __syncthreads();
+    const bool hl = x > 0, ht = y > 0;
+    if (lane < 48) {   // DC / TM residual of one 4x4 block, predicted on the fly
+      int coeffs[16], hsel, d[16];
+      const uint8_t* src;
+      int ss, m, px0, py0, n;
+      const uint8_t *left, *top;
+      if (lane < 32) {
+        m = lane >> 4;
+        const int b = lane & 15;
+        px0 = (b & 3) * 4; py0 = (b >> 2) * 4;
+        src = yin + py0 * K2_YW + px0; ss = K2_YW;
+        left = yl; top = L.top; n = 16;
+        hsel = m;
+      } else {
+        m = (lane - 32) >> 3;
+        const int b = lane & 7, c = b >> 2, k = b & 3;
+        px0 = (k & 1) * 4; py0 = (k >> 1) * 4;
+        src = (c ? vin : uin) + py0 * K2_CW + px0; ss = K2_CW;
+        left = c ? vl : ul; top = L.top + 16 + 8 * c; n = 8;
+        hsel = 2 + m;
       }
-      alpha[hh] = maxv > 1 ? 510 * last / maxv : 0;
+      const int dcv = m == 0 ? dc_value(left, top, hl, ht, n, n == 16 ? 5 : 4) : 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        d[i] = src[(i >> 2) * ss + (i & 3)] -
+               pred_sample(m, n, px0 + (i & 3), py0 + (i >> 2), left, top, hl, ht, dcv);
+      fdct4_res(d, coeffs);
+      // bins 0..7 counted in 16-bit fields of two registers, summed over the
+      // block group's lanes (16 for Y, 8 for U/V) with shuffles; the rarer
+      // bins 8..31 by LDS atomics
+      uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int v = min(iabs_(coeffs[k]) >> 3, 31);
+        const uint64_t one = 1ull << (16 * (v & 3));
+        c0 += v < 4 ? one : 0ull;
+        c1 += (v >= 4 && v < 8) ? one : 0ull;
+        if (v >= 8) atomicAdd(&L.hist[hsel][v], 1);
+      }
+      const int gsz = lane < 32 ? 16 : 8;
+      for (int o = 1; o < gsz; o <<= 1) {
+        c0 += __shfl_xor(c0, o);
+        c1 += __shfl_xor(c1, o);
+      }
+      if ((lane & (gsz - 1)) < 8) {   // 8 lanes per group store the 8 bins
+        const int bin = lane & 7;
+        const uint64_t c = bin < 4 ? c0 : c1;
+        L.hist[hsel][bin] = (int)((c >> (16 * (bin & 3))) & 0xffff);
+      }
     }
-    int best = -1;
-    if (alpha[0] > best) best = alpha[0];
-    if (alpha[1] > best) best = alpha[1];
-    int best_uv = -1;
-    if (alpha[2] > best_uv) best_uv = alpha[2];
-    if (alpha[3] > best_uv) best_uv = alpha[3];
-    // analysis modes for the RD_OPT_NONE encoder (methods 0-2): the UV mode
-    // of smallest alpha (analysis_enc.c:278-305) and, for methods 0-1,
-    // FastMBAnalyze's intra-16 / intra-4 pick with susceptibility 0 (:255-276)
-    int i4 = 0;
-    if (fast_q >= 0) {
-      const uint32_t thr = 8 + (17 - 8) * fast_q / 100;
-      uint32_t m = 0, m2 = 0;
-      for (int k = 0; k < 16; ++k) { m += L.dc[k]; m2 += L.dc[k] * L.dc[k]; }
-      i4 = !(thr * m2 < m * m);
-      best = 0;
+    uint32_t dcs = 0;   // VP8Mean16x4 block sums (dsp/enc.c:594-608), lanes 0..15
+    if (fast_q >= 0 && lane < 16)
+      for (int k = 0; k < 16; ++k)
+        dcs += yin[(4 * (lane >> 2) + (k >> 2)) * K2_YW + 4 * (lane & 3) + (k & 3)];
+    __syncthreads();
+    // alpha of each histogram (dsp/enc.c:46-81): max count and last non-empty
+    // bin, one bin per lane, half a wave per histogram, two rounds
+    int alpha[4];
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const int hh = (lane >> 5) + 2 * pass;
+      const int v = L.hist[hh][lane & 31];
+      int mx = v;
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+      const uint64_t nz = __ballot(v > 0);
+      const uint32_t half = (uint32_t)(nz >> (lane & 32));
+      const int last = half ? 31 - __builtin_clz(half) : 1;
+      const int al = mx > 1 ? 510 * last / mx : 0;
+      alpha[2 * pass] = __shfl(al, 0);
+      alpha[2 * pass + 1] = __shfl(al, 32);
     }
-    if (mb_amode != nullptr)
-      mb_amode[(size_t)f * nmb + mb] = (uint8_t)((alpha[3] < alpha[2] ? 1 : 0) | (i4 << 1));
-    int a = (3 * best + best_uv + 2) >> 2;
-    a = 255 - a;
-    a = a < 0 ? 0 : a > 255 ? 255 : a;
-    mb_alpha[(size_t)f * nmb + mb] = (uint8_t)a;
-    mb_uva[(size_t)f * nmb + mb] = (uint16_t)best_uv;
+    uint32_t dsum = dcs, dsq = dcs * dcs;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) { dsum += __shfl_xor(dsum, o); dsq += __shfl_xor(dsq, o); }
+    if (lane == 0 && valid) {
+      int best = -1;
+      if (alpha[0] > best) best = alpha[0];
+      if (alpha[1] > best) best = alpha[1];
+      int best_uv = -1;
+      if (alpha[2] > best_uv) best_uv = alpha[2];
+      if (alpha[3] > best_uv) best_uv = alpha[3];
+      // analysis modes for the RD_OPT_NONE encoder (methods 0-2): the UV mode
+      // of smallest alpha (analysis_enc.c:278-305) and, for methods 0-1,
+      // FastMBAnalyze's intra-16 / intra-4 pick with susceptibility 0 (:255-276)
+      int i4 = 0;
+      if (fast_q >= 0) {
+        const uint32_t thr = 8 + (17 - 8) * fast_q / 100;
+        i4 = !(thr * dsq < dsum * dsum);
+        best = 0;
+      }
+      if (mb_amode != nullptr)
+        mb_amode[(size_t)f * nmb + mb] = (uint8_t)((alpha[3] < alpha[2] ? 1 : 0) | (i4 << 1));
+      int a = (3 * best + best_uv + 2) >> 2;
+      a = 255 - a;
+      a = a < 0 ? 0 : a > 255 ? 255 : a;
+      mb_alpha[(size_t)f * nmb + mb] = (uint8_t)a;
+      mb_uva[(size_t)f * nmb + mb] = (uint16_t)best_uv;
+    }
+    __syncthreads();   // this wave's LDS is reused by its next MB
   }
 }
 
@@ -1923,8 +1956,8 @@ int vp8g_launch_alpha_remap(uint8_t* aplane, size_t plane, const uint32_t* aflag
 
 int vp8g_launch_analysis(const uint8_t* yuv, size_t yfb, int w, int h, int n, uint8_t* mb_alpha,
                          uint16_t* mb_uva, int fast_q, uint8_t* mb_amode, void* stream) {
-  const int nmb = ((w + 15) >> 4) * ((h + 15) >> 4);
-  dim3 grid((nmb + 3) / 4, n);
+  const int mbw = (w + 15) >> 4, mbh = (h + 15) >> 4, nmb = mbw * mbh;
+  dim3 grid((mbw + K2_STRIP - 1) / K2_STRIP, mbh, n);
   hipLaunchKernelGGL(k_analyze, grid, dim3(256), 0, (hipStream_t)stream, yuv, yfb, w, h, nmb,
                      mb_alpha, mb_uva, fast_q, mb_amode);
   return launch_check("k_analyze");

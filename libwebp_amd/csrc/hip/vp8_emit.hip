@@ -10,7 +10,8 @@
 // end of the stream including the finishing pad bits, and S the total shift
 // count. (Checked against the reference coder; tests/test_emit_model.py.)
 // So a frame's tokens are cut into segments and:
-//   E0 k_emit_resolve  token -> (bit, probability) in place, all tokens
+//   (tokens are resolved to (bit, probability) under the frame's final
+//   probabilities by each kernel below as it stages them in LDS)
 //   E1 k_emit_img      per segment, the few ranges it can start with (the end
 //                      states of the previous segment's last 256 tokens run
 //                      from all 128 ranges; typically 4-10 survive)
@@ -43,42 +44,31 @@ __device__ __forceinline__ int renorm(int& r) {   // range_ in [0, 254] -> [127,
 
 }  // namespace
 
-__global__ __launch_bounds__(256) void k_emit_resolve(uint16_t* __restrict__ tokens,
-                                                      size_t tok_cap,
-                                                      const vp8g_frame_result* __restrict__ results,
-                                                      const vp8g_emit_meta* __restrict__ meta) {
-  __shared__ uint8_t prob[VP8G_NUM_SLOTS];
-  const int f = blockIdx.y;
-  const vp8g_emit_meta M = meta[f];
-  const uint32_t ntok = M.ntok;
-  if (blockIdx.x * 2048 >= ntok) return;   // whole workgroup
-  const vp8g_frame_result* R = results + M.frame;
-  for (int s = threadIdx.x; s < VP8G_NUM_SLOTS; s += 256) prob[s] = R->probas[s];
-  __syncthreads();
-  const uint32_t i0 = (blockIdx.x * 256 + threadIdx.x) * 8;
-  if (i0 >= ntok) return;
-  uint16_t* tok = tokens + M.tok_off + i0;
-  uint4 w = *reinterpret_cast<const uint4*>(tok);
-  uint32_t v[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    uint32_t r = 0;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t t = (v[k] >> (16 * h)) & 0xffff;
-      const uint32_t p = (t & 0x4000) ? (t & 0xff) : prob[t & 0x3fff & 2047];
-      r |= (((t >> 15) << 8) | p) << (16 * h);
-    }
-    v[k] = r;
-  }
-  *reinterpret_cast<uint4*>(tok) = make_uint4(v[0], v[1], v[2], v[3]);
-}
-
 // One range-chain step: returns the renormalisation shift.
 __device__ __forceinline__ int chain_step(int& r, uint32_t pb) {
   const int split = (int)(__umul24((unsigned)r, pb & 0xff) >> 8);   // full-rate 24-bit multiply
   r = (pb >> 8) ? r - split - 1 : split;
   return renorm(r);
+}
+
+// A recorded token (bit << 15 | fixed << 14 | probability or slot) as
+// (bit << 8 | probability) under the frame's final probabilities (prob in
+// LDS): the consumers resolve tokens as they stage them.
+__device__ __forceinline__ uint32_t resolve_tok(uint32_t t, const uint8_t* prob) {
+  const uint32_t p = (t & 0x4000) ? (t & 0xff) : prob[t & 0x3fff & 2047];
+  return ((t >> 15) << 8) | p;
+}
+__device__ __forceinline__ uint32_t resolve_pair(uint32_t w, const uint8_t* prob) {
+  return resolve_tok(w & 0xffff, prob) | (resolve_tok(w >> 16, prob) << 16);
+}
+__device__ __forceinline__ uint4 resolve_quad(uint4 q, const uint8_t* prob) {
+  return make_uint4(resolve_pair(q.x, prob), resolve_pair(q.y, prob), resolve_pair(q.z, prob),
+                    resolve_pair(q.w, prob));
+}
+__device__ __forceinline__ void load_probas(uint8_t* prob, const vp8g_frame_result* results,
+                                            const vp8g_emit_meta& M, int t, int nt) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(results[M.frame].probas);
+  for (int k = t; k < VP8G_NUM_SLOTS / 4; k += nt) reinterpret_cast<uint32_t*>(prob)[k] = src[k];
 }
 
 // E1a: the range a segment can start with is the end state of the previous
@@ -96,9 +86,11 @@ __device__ __forceinline__ int chain_step(int& r, uint32_t pb) {
 #define IMG_ROW (EMIT_IMG + 8)       // u16; +16 B per row: conflict-free b128 reads
 __global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ tokens,
                                                  size_t tok_cap,
+                                                 const vp8g_frame_result* __restrict__ results,
                                                  const vp8g_emit_meta* __restrict__ meta,
                                                  uint8_t* __restrict__ img) {
   __shared__ __align__(16) uint16_t tk[IMG_G * IMG_ROW];
+  __shared__ __align__(4) uint8_t prob[VP8G_NUM_SLOTS];
   __shared__ uint32_t bm[IMG_G * 4];
   __shared__ uint16_t pairs[IMG_G * 128];   // (segment << 7) | (range - 127)
   const int f = blockIdx.y, lane = threadIdx.x;
@@ -106,13 +98,16 @@ __global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ to
   const uint32_t sbase = blockIdx.x * IMG_G;
   if (sbase >= M.nseg) return;   // whole wave
   const uint16_t* ftok = tokens + M.tok_off;
+  load_probas(prob, results, M, lane, 64);
+  __syncthreads();
 #pragma unroll
   for (int t = 0; t < IMG_G * EMIT_IMG / 8 / 64; ++t) {   // every segment's last-tokens window
     const int q = lane + 64 * t, sg = q / (EMIT_IMG / 8), part = q % (EMIT_IMG / 8);
     const uint32_t s = sbase + sg;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (s > 0 && s < M.nseg)
-      v = *reinterpret_cast<const uint4*>(ftok + (size_t)s * EMIT_SEG - EMIT_IMG + 8 * part);
+      v = resolve_quad(
+          *reinterpret_cast<const uint4*>(ftok + (size_t)s * EMIT_SEG - EMIT_IMG + 8 * part), prob);
     *reinterpret_cast<uint4*>(&tk[sg * IMG_ROW + 8 * part]) = v;
   }
   // this lane's piece of the maps: segment mg, word mw
@@ -193,11 +188,13 @@ __global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ to
 #define MAP_PIECES (MAP_G * MAP_CH / 8 / 64)   // 16-byte pieces per lane per chunk
 __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ tokens,
                                                   size_t tok_cap,
+                                                  const vp8g_frame_result* __restrict__ results,
                                                   const vp8g_emit_meta* __restrict__ meta,
                                                   const uint8_t* __restrict__ img,
                                                   uint8_t* __restrict__ emap,
                                                   uint16_t* __restrict__ eshift) {
   __shared__ __align__(16) uint16_t stage[MAP_G * MAP_ROW];
+  __shared__ __align__(4) uint8_t prob[VP8G_NUM_SLOTS];
   const int f = blockIdx.y, lane = threadIdx.x;
   const vp8g_emit_meta M = meta[f];
   const uint32_t sbase = blockIdx.x * MAP_G;
@@ -215,6 +212,8 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
   }
   const int total = __shfl(incl, MAP_G - 1);
   const uint16_t* ftok = tokens + M.tok_off;
+  load_probas(prob, results, M, lane, 64);
+  __syncthreads();
   auto load = [&](uint32_t c0, uint4* v) {
 #pragma unroll
     for (int t = 0; t < MAP_PIECES; ++t) {
@@ -248,7 +247,7 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
 #pragma unroll
       for (int t = 0; t < MAP_PIECES; ++t) {
         const int q = lane + 64 * t, sg = q / (MAP_CH / 8), part = q % (MAP_CH / 8);
-        *reinterpret_cast<uint4*>(&stage[sg * MAP_ROW + 8 * part]) = nv[t];
+        *reinterpret_cast<uint4*>(&stage[sg * MAP_ROW + 8 * part]) = resolve_quad(nv[t], prob);
       }
       __syncthreads();
       if (c0 + MAP_CH < EMIT_SEG) load(c0 + MAP_CH, nv);   // in flight during the chain
@@ -369,10 +368,12 @@ __device__ __forceinline__ void seg_chunk_store(const uint32_t* lds, uint16_t* b
 }
 
 __global__ __launch_bounds__(64) void k_emit_seg(uint16_t* __restrict__ tokens, size_t tok_cap,
+                                                 const vp8g_frame_result* __restrict__ results,
                                                  const vp8g_emit_meta* __restrict__ meta,
                                                  vp8g_emit_seg* __restrict__ segs,
                                                  uint32_t* __restrict__ nbuf) {
   __shared__ uint32_t lds[64 * SEG_ROW];
+  __shared__ __align__(4) uint8_t prob[VP8G_NUM_SLOTS];
   const int f = blockIdx.y, lane = threadIdx.x;
   const uint32_t s0 = blockIdx.x * 64, s = s0 + lane;
   const vp8g_emit_meta M = meta[f];
@@ -389,13 +390,14 @@ __global__ __launch_bounds__(64) void k_emit_seg(uint16_t* __restrict__ tokens, 
                             ? (uint32_t)EMIT_SEG
                             : M.ntok - last_s * EMIT_SEG;
   // forward: true range chain -> (c, shift) packed in place
+  load_probas(prob, results, M, lane, 64);
   int r = g.rs;
   for (uint32_t c0 = 0; c0 < span; c0 += SEG_CH) {
     seg_chunk_load(lds, base, s0, M.nseg, M.ntok, c0, lane);
     __syncthreads();
 #pragma unroll 4
     for (int k = 0; k < SEG_CH / 2; ++k) {
-      uint32_t w = row[k];
+      uint32_t w = resolve_pair(row[k], prob);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const uint32_t pb = (w >> (16 * h)) & 0xffff;
@@ -511,19 +513,14 @@ extern "C" int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
                                 uint32_t* nbuf, uint32_t* out_size, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (n <= 0) return 1;
-  const uint32_t rb = (max_ntok + 2047) / 2048;
-  if (rb) {
-    hipLaunchKernelGGL(k_emit_resolve, dim3(rb, n), dim3(256), 0, st, tokens, tok_cap, results,
-                       (const vp8g_emit_meta*)meta);
-    if (!vp8g_launch_check("k_emit_resolve")) return 0;
-  }
+  (void)max_ntok;   // the token consumers resolve the probabilities themselves
   if (max_seg) {
     hipLaunchKernelGGL(k_emit_img, dim3((max_seg + IMG_G - 1) / IMG_G, n), dim3(64), 0, st,
-                       (const uint16_t*)tokens,
-                       tok_cap, (const vp8g_emit_meta*)meta, img);
+                       (const uint16_t*)tokens, tok_cap, results, (const vp8g_emit_meta*)meta,
+                       img);
     if (!vp8g_launch_check("k_emit_img")) return 0;
     hipLaunchKernelGGL(k_emit_maps, dim3((max_seg + MAP_G - 1) / MAP_G, n), dim3(64), 0, st,
-                       (const uint16_t*)tokens, tok_cap, (const vp8g_emit_meta*)meta,
+                       (const uint16_t*)tokens, tok_cap, results, (const vp8g_emit_meta*)meta,
                        (const uint8_t*)img, emap, eshift);
     if (!vp8g_launch_check("k_emit_maps")) return 0;
   }
@@ -532,7 +529,7 @@ extern "C" int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
   if (!vp8g_launch_check("k_emit_compose")) return 0;
   const uint32_t sb = (max_seg + 63) / 64;
   if (sb) {
-    hipLaunchKernelGGL(k_emit_seg, dim3(sb, n), dim3(64), 0, st, tokens, tok_cap,
+    hipLaunchKernelGGL(k_emit_seg, dim3(sb, n), dim3(64), 0, st, tokens, tok_cap, results,
                        (const vp8g_emit_meta*)meta, segs, nbuf);
     if (!vp8g_launch_check("k_emit_seg")) return 0;
     hipLaunchKernelGGL(k_emit_carry, dim3(sb, n), dim3(64), 0, st, (const vp8g_emit_meta*)meta,

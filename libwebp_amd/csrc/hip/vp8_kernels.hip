@@ -69,23 +69,40 @@ __global__ __launch_bounds__(256) void k_import(const uint8_t* __restrict__ rgba
   const uint8_t* r0 = src + (size_t)y0 * rstride + 4 * x0;
   const uint8_t* r1 = two_rows ? r0 + rstride : r0;
   uint8_t p[2][2][4];
+  if (two_cols && ((rstride | (int)((uintptr_t)src & 7)) & 7) == 0) {   // 8-byte loads
+    const uint2 a = *reinterpret_cast<const uint2*>(r0);
+    const uint2 b = *reinterpret_cast<const uint2*>(r1);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    p[0][0][k] = r0[k];
-    p[1][0][k] = r1[k];
-    p[0][1][k] = two_cols ? r0[4 + k] : 0;
-    p[1][1][k] = two_cols ? r1[4 + k] : 0;
+    for (int k = 0; k < 4; ++k) {
+      p[0][0][k] = (uint8_t)(a.x >> (8 * k)); p[0][1][k] = (uint8_t)(a.y >> (8 * k));
+      p[1][0][k] = (uint8_t)(b.x >> (8 * k)); p[1][1][k] = (uint8_t)(b.y >> (8 * k));
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      p[0][0][k] = r0[k];
+      p[1][0][k] = r1[k];
+      p[0][1][k] = two_cols ? r0[4 + k] : 0;
+      p[1][1][k] = two_cols ? r1[4 + k] : 0;
+    }
   }
+  const bool pair16 = two_cols && !(w & 1);   // 16-bit stores of the pixel pairs
   uint32_t alpha_bad = (p[0][0][3] != 0xff) | (p[1][0][3] != 0xff);
   if (two_cols) alpha_bad |= (p[0][1][3] != 0xff) | (p[1][1][3] != 0xff);
   if (alpha_bad) atomicOr(aflags + f, 1u);
   {   // the WebPPicture alpha plane (WebPExtractAlpha), stride w
     uint8_t* arow = aplane + (size_t)f * w * h + (size_t)y0 * w + x0;
-    arow[0] = p[0][0][3];
-    if (two_cols) arow[1] = p[0][1][3];
-    if (two_rows) {
-      arow[w] = p[1][0][3];
-      if (two_cols) arow[w + 1] = p[1][1][3];
+    if (pair16) {
+      *reinterpret_cast<uint16_t*>(arow) = (uint16_t)(p[0][0][3] | (p[0][1][3] << 8));
+      if (two_rows)
+        *reinterpret_cast<uint16_t*>(arow + w) = (uint16_t)(p[1][0][3] | (p[1][1][3] << 8));
+    } else {
+      arow[0] = p[0][0][3];
+      if (two_cols) arow[1] = p[0][1][3];
+      if (two_rows) {
+        arow[w] = p[1][0][3];
+        if (two_cols) arow[w + 1] = p[1][1][3];
+      }
     }
   }
   uint8_t* yrow = Y + (size_t)y0 * w + x0;
@@ -94,11 +111,22 @@ __global__ __launch_bounds__(256) void k_import(const uint8_t* __restrict__ rgba
   const int ry01 = rnd_y && two_cols ? rnd_y[yo + 1] : 1 << 15;
   const int ry10 = rnd_y && two_rows ? rnd_y[yo + w] : 1 << 15;
   const int ry11 = rnd_y && two_rows && two_cols ? rnd_y[yo + w + 1] : 1 << 15;
-  yrow[0] = rgb_to_y(p[0][0][0], p[0][0][1], p[0][0][2], ry00);
-  if (two_cols) yrow[1] = rgb_to_y(p[0][1][0], p[0][1][1], p[0][1][2], ry01);
-  if (two_rows) {
-    yrow[w] = rgb_to_y(p[1][0][0], p[1][0][1], p[1][0][2], ry10);
-    if (two_cols) yrow[w + 1] = rgb_to_y(p[1][1][0], p[1][1][1], p[1][1][2], ry11);
+  {
+    const int y00 = rgb_to_y(p[0][0][0], p[0][0][1], p[0][0][2], ry00);
+    const int y01 = rgb_to_y(p[0][1][0], p[0][1][1], p[0][1][2], ry01);
+    const int y10 = rgb_to_y(p[1][0][0], p[1][0][1], p[1][0][2], ry10);
+    const int y11 = rgb_to_y(p[1][1][0], p[1][1][1], p[1][1][2], ry11);
+    if (pair16) {
+      *reinterpret_cast<uint16_t*>(yrow) = (uint16_t)(y00 | (y01 << 8));
+      if (two_rows) *reinterpret_cast<uint16_t*>(yrow + w) = (uint16_t)(y10 | (y11 << 8));
+    } else {
+      yrow[0] = (uint8_t)y00;
+      if (two_cols) yrow[1] = (uint8_t)y01;
+      if (two_rows) {
+        yrow[w] = (uint8_t)y10;
+        if (two_cols) yrow[w + 1] = (uint8_t)y11;
+      }
+    }
   }
   // AccumulateRGBA (picture_csp_enc.c:388-424): 2x2 blocks with partial
   // alpha average in linear light weighted by alpha, divided through

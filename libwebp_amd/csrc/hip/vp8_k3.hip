@@ -1141,10 +1141,18 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
      for (uint32_t i = i0; i < i1; ++i) {
       const uint32_t n = L.rowcnt[i - row0];
       const uint16_t* tk = tok_base + (size_t)i * VP8G_MAX_TOKENS_PER_MB;
-      uint32_t nxt = ln < n ? tk[ln] : 0x4000u;
-      for (uint32_t k0 = 0; k0 < n; k0 += 64) {
-        const uint32_t t = nxt;
-        nxt = (k0 + 64 + ln < n) ? tk[k0 + 64 + ln] : 0x4000u;
+      // 4 chunks of 64 tokens loaded together (one memory latency per 256
+      // tokens), then applied in order
+      for (uint32_t k4 = 0; k4 < n; k4 += 256) {
+       uint32_t tq[4];
+#pragma unroll
+       for (int q = 0; q < 4; ++q) {
+         const uint32_t k = k4 + 64 * q + ln;
+         tq[q] = k < n ? tk[k] : 0x4000u;
+       }
+#pragma unroll
+       for (int q = 0; q < 4; ++q) {
+        const uint32_t t = tq[q];
         const int sl = (t & 0x4000) ? 0 : tok_stat_slot(t);
         const bool pend = !(t & 0x4000) && ((G.mark[sl >> 5] >> (sl & 31)) & 1u);
         uint64_t pm = __ballot(pend);
@@ -1167,6 +1175,7 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
           }
           pm &= ~mm;
         }
+       }
       }
      }
     }

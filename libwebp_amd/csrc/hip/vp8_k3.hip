@@ -1124,60 +1124,68 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
       const uint32_t p = G.stats[s];
       if ((p >> 16) + (dlt >> 16) < 0xffffu) {
         G.stats[s] = p + dlt;
-      } else {
+        L.rdelta[s] = 0;
+      } else {   // the delta stays for the replay below
         atomicOr(&G.mark[s >> 5], 1u << (s & 31));
         L.mark_any = 1;
       }
-      L.rdelta[s] = 0;
     }
   }
   wbar(L);
   if (L.mark_any) {
-    // exact in-order replay of the marked counters by wave 0, MB by MB from
-    // the per-MB token slots, 64 tokens at a time; the tokens of one marked
-    // counter in a group are applied at once unless the group reaches the
-    // halving point, then one by one
+    // exact in-order replay of each marked counter by wave 0: its tokens only
+    // matter up to the points where the counter halves, so the row's tokens
+    // are scanned (four 64-token chunks per load step) with the counter's
+    // count / ones of each chunk taken by ballots, the chunk holding a halving
+    // point applied token by token, and everything after the last halving
+    // point added at once from the row's delta
     if (tid < 64) {
-     for (uint32_t i = i0; i < i1; ++i) {
-      const uint32_t n = L.rowcnt[i - row0];
-      const uint16_t* tk = tok_base + (size_t)i * VP8G_MAX_TOKENS_PER_MB;
-      // 4 chunks of 64 tokens loaded together (one memory latency per 256
-      // tokens), then applied in order
-      for (uint32_t k4 = 0; k4 < n; k4 += 256) {
-       uint32_t tq[4];
+      for (int wd = 0; wd < 33; ++wd) {
+        uint32_t bits = G.mark[wd];
+        while (bits) {
+          const int ss = wd * 32 + __builtin_ctz(bits);
+          bits &= bits - 1;
+          uint32_t p = G.stats[ss];
+          const uint32_t dlt = L.rdelta[ss];
+          uint32_t n = dlt >> 16, k = dlt & 0xffffu;   // the row's tokens of ss not applied yet
+          for (uint32_t i = i0; i < i1 && n; ++i) {
+            const uint32_t nt = L.rowcnt[i - row0];
+            const uint16_t* tk = tok_base + (size_t)i * VP8G_MAX_TOKENS_PER_MB;
+            for (uint32_t k4 = 0; k4 < nt && n; k4 += 256) {
+              if ((p >> 16) + n < 0xfffeu) break;   // no halving left in the row
+              uint32_t tq[4];
 #pragma unroll
-       for (int q = 0; q < 4; ++q) {
-         const uint32_t k = k4 + 64 * q + ln;
-         tq[q] = k < n ? tk[k] : 0x4000u;
-       }
+              for (int q = 0; q < 4; ++q) {
+                const uint32_t kk = k4 + 64 * q + ln;
+                tq[q] = kk < nt ? tk[kk] : 0x4000u;
+              }
 #pragma unroll
-       for (int q = 0; q < 4; ++q) {
-        const uint32_t t = tq[q];
-        const int sl = (t & 0x4000) ? 0 : tok_stat_slot(t);
-        const bool pend = !(t & 0x4000) && ((G.mark[sl >> 5] >> (sl & 31)) & 1u);
-        uint64_t pm = __ballot(pend);
-        while (pm) {
-          const int ss = __builtin_amdgcn_readlane(sl, (int)__builtin_ctzll(pm));
-          const uint64_t mm = __ballot(pend && sl == ss);
-          const uint64_t ones = __ballot(pend && sl == ss && (t >> 15));
-          if (ln == 0) {
-            uint32_t p = G.stats[ss];
-            const uint32_t cnt = (uint32_t)__popcll(mm);
-            if ((p >> 16) + cnt < 0xffffu) {
-              p += (cnt << 16) + (uint32_t)__popcll(ones);
-            } else {
-              for (uint64_t b = mm; b; b &= b - 1) {
-                if (p >= 0xfffe0000u) p = ((p + 1u) >> 1) & 0x7fff7fffu;
-                p += 0x00010000u + (uint32_t)((ones >> __builtin_ctzll(b)) & 1u);
+              for (int q = 0; q < 4; ++q) {
+                const uint32_t t = tq[q];
+                const bool mine = !(t & 0x4000) && tok_stat_slot(t) == ss;
+                const uint64_t mm = __ballot(mine);
+                const uint64_t ones = __ballot(mine && (t >> 15));
+                const uint32_t cnt = (uint32_t)__popcll(mm);
+                if ((p >> 16) + cnt < 0xfffeu) {
+                  p += (cnt << 16) + (uint32_t)__popcll(ones);
+                } else {
+                  for (uint64_t bm = mm; bm; bm &= bm - 1) {
+                    if (p >= 0xfffe0000u) p = ((p + 1u) >> 1) & 0x7fff7fffu;
+                    p += 0x00010000u + (uint32_t)((ones >> __builtin_ctzll(bm)) & 1u);
+                  }
+                }
+                n -= cnt;
+                k -= (uint32_t)__popcll(ones);
               }
             }
-            G.stats[ss] = p;
           }
-          pm &= ~mm;
+          p += (n << 16) + k;   // the rest of the row: no halving point left
+          if (ln == 0) {
+            G.stats[ss] = p;
+            L.rdelta[ss] = 0;
+          }
         }
-       }
       }
-     }
     }
     wbar(L);
     for (int k = tid; k < 33; k += K3T) G.mark[k] = 0;

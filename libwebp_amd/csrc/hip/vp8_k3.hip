@@ -90,6 +90,7 @@ struct K3S {
   int32_t blast[32];               // last non-zero zigzag position per token block
   int32_t wsum[2][4];              // per-wave token-count totals (scan)
   int32_t redw[4];                 // per-wave reduction slots
+  uint32_t fold_total;             // tokens of the MBs being folded
   uint32_t trnz[4];
   uint32_t bar;                    // worker barrier counter
   int32_t myabort;
@@ -1105,17 +1106,24 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
   // Called once every earlier MB is folded (G.fold_ptr == i0).
   const uint32_t base = G.ntok;
   const uint32_t ln = (uint32_t)tid & 63;
-  uint32_t total = 0;
-  for (uint32_t i = i0; i < i1; ++i) total += L.rowcnt[i - row0];
-  if (tid == 0) {
+  if (tid < 64) {   // compact-stream offsets: a wave scan over the MBs, 64 at a time
     uint32_t off = base;
-    for (uint32_t i = i0; i < i1; ++i) {
-      mboff[i] = off;
-      off += L.rowcnt[i - row0];
+    for (uint32_t c = i0; c < i1; c += 64) {
+      const uint32_t i = c + ln;
+      const uint32_t v = i < i1 ? L.rowcnt[i - row0] : 0u;
+      uint32_t incl = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o);
+        if (ln >= (uint32_t)o) incl += u;
+      }
+      if (i < i1) mboff[i] = off + incl - v;
+      off += __shfl(incl, 63);
     }
+    if (ln == 0) { L.fold_total = off - base; L.mark_any = 0; }
   }
-  if (tid == 0) L.mark_any = 0;
   wbar(L);
+  const uint32_t total = L.fold_total;
   // statistics: one add per counter unless it would reach the halving point
   // (VP8RecordStats, cost_enc.h:50-57), then an in-order replay of that counter
   for (int s = tid; s < NSLOT; s += K3T) {

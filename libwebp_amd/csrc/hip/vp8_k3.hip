@@ -1141,18 +1141,21 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
   }
   wbar(L);
   if (L.mark_any) {
-    // exact in-order replay of each marked counter by wave 0: its tokens only
+    // exact in-order replay of each marked counter by one wave: its tokens only
     // matter up to the points where the counter halves, so the row's tokens
     // are scanned (four 64-token chunks per load step) with the counter's
     // count / ones of each chunk taken by ballots, the chunk holding a halving
     // point applied token by token, and everything after the last halving
     // point added at once from the row's delta
-    if (tid < 64) {
+    {   // the marked counters are independent: dealt round-robin to the 4 waves
+      const int wv = tid >> 6;
+      int j = 0;
       for (int wd = 0; wd < 33; ++wd) {
         uint32_t bits = G.mark[wd];
         while (bits) {
           const int ss = wd * 32 + __builtin_ctz(bits);
           bits &= bits - 1;
+          if ((j++ & 3) != wv) continue;
           uint32_t p = G.stats[ss];
           const uint32_t dlt = L.rdelta[ss];
           uint32_t n = dlt >> 16, k = dlt & 0xffffu;   // the row's tokens of ss not applied yet

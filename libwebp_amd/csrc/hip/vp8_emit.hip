@@ -182,7 +182,7 @@ __global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ to
 // more than 64 pairs take further rounds. The group's tokens go through LDS
 // MAP_CH per segment at a time (the next chunk is loaded into registers while
 // this one runs), so the chains read LDS broadcasts instead of global loads.
-#define MAP_G 16
+#define MAP_G 8
 #define MAP_CH 256
 #define MAP_ROW (MAP_CH + 8)   // u16; +16 B per row: the 16 rows' b128 reads hit distinct banks
 #define MAP_PIECES (MAP_G * MAP_CH / 8 / 64)   // 16-byte pieces per lane per chunk

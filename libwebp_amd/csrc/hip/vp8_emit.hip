@@ -340,17 +340,25 @@ __global__ __launch_bounds__(64) void k_emit_compose(vp8g_emit_meta* __restrict_
 #define SEG_CH 64                   // tokens per segment per chunk
 #define SEG_ROW (SEG_CH / 2 + 1)    // LDS row in dwords, +1: conflict-free rows
 
-__device__ __forceinline__ void seg_chunk_load(uint32_t* lds, const uint16_t* base, uint32_t s0,
-                                               uint32_t nseg, uint32_t ntok, uint32_t c0,
-                                               int lane) {
+// a chunk of 64 segments x SEG_CH tokens in two steps: global -> registers (issued early, so the
+// loads fly while the previous chunk is processed), registers -> LDS
+__device__ __forceinline__ void seg_chunk_fetch(uint4 v[8], const uint16_t* base, uint32_t s0,
+                                                uint32_t nseg, uint32_t ntok, uint32_t c0,
+                                                int lane) {
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
     const int q = lane + 64 * t, sg = q >> 3, part = q & 7;
-    const uint32_t i = (s0 + sg) * EMIT_SEG + c0 + 8 * part;   // frame token index
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (s0 + sg < nseg && i < ntok) v = *reinterpret_cast<const uint4*>(base + i);
+    const uint32_t i = (s0 + sg) * EMIT_SEG + c0 + 8 * part;
+    v[t] = make_uint4(0, 0, 0, 0);
+    if (s0 + sg < nseg && i < ntok) v[t] = *reinterpret_cast<const uint4*>(base + i);
+  }
+}
+__device__ __forceinline__ void seg_chunk_put(uint32_t* lds, const uint4 v[8], int lane) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int q = lane + 64 * t, sg = q >> 3, part = q & 7;
     uint32_t* d = lds + sg * SEG_ROW + 4 * part;
-    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    d[0] = v[t].x; d[1] = v[t].y; d[2] = v[t].z; d[3] = v[t].w;
   }
 }
 
@@ -392,9 +400,12 @@ __global__ __launch_bounds__(64) void k_emit_seg(uint16_t* __restrict__ tokens, 
   // forward: true range chain -> (c, shift) packed in place
   load_probas(prob, results, M, lane, 64);
   int r = g.rs;
+  uint4 nv[8];
+  seg_chunk_fetch(nv, base, s0, M.nseg, M.ntok, 0, lane);
   for (uint32_t c0 = 0; c0 < span; c0 += SEG_CH) {
-    seg_chunk_load(lds, base, s0, M.nseg, M.ntok, c0, lane);
+    seg_chunk_put(lds, nv, lane);
     __syncthreads();
+    if (c0 + SEG_CH < span) seg_chunk_fetch(nv, base, s0, M.nseg, M.ntok, c0 + SEG_CH, lane);
 #pragma unroll 4
     for (int k = 0; k < SEG_CH / 2; ++k) {
       uint32_t w = resolve_pair(row[k], prob);
@@ -424,10 +435,12 @@ __global__ __launch_bounds__(64) void k_emit_seg(uint16_t* __restrict__ tokens, 
   uint64_t acc = 0;
   uint32_t E = 0;
   const uint32_t nch = (span + SEG_CH - 1) / SEG_CH;
+  seg_chunk_fetch(nv, base, s0, M.nseg, M.ntok, (nch - 1) * SEG_CH, lane);
   for (uint32_t ch = nch; ch > 0; --ch) {
     const uint32_t c0 = (ch - 1) * SEG_CH;
-    seg_chunk_load(lds, base, s0, M.nseg, M.ntok, c0, lane);   // (c, shift); 0 past the end
+    seg_chunk_put(lds, nv, lane);   // (c, shift); 0 past the end
     __syncthreads();
+    if (ch > 1) seg_chunk_fetch(nv, base, s0, M.nseg, M.ntok, c0 - SEG_CH, lane);
     for (int k = SEG_CH / 2 - 1; k >= 0; --k) {
       const uint32_t w = row[k];
 #pragma unroll

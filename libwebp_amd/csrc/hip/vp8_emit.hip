@@ -509,12 +509,21 @@ __global__ __launch_bounds__(256) void k_emit_bytes(uint16_t* __restrict__ token
                                                     const uint32_t* __restrict__ nbuf) {
   const int f = blockIdx.y;
   const vp8g_emit_meta M = meta[f];
-  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= M.L) return;
+  const uint32_t k0 = 4 * (blockIdx.x * 256 + threadIdx.x);   // output bytes k0 .. k0 + 3
+  if (k0 >= M.L) return;
   const uint32_t* W = nbuf + M.nb_base;
-  const uint32_t b = 1 + 8 * (M.L - 1 - k);   // lowest bit of output byte k
-  const uint64_t two = (uint64_t)W[b >> 5] | ((uint64_t)W[(b >> 5) + 1] << 32);
-  reinterpret_cast<uint8_t*>(tokens + M.tok_off)[k] = (uint8_t)(two >> (b & 31));
+  uint8_t* out = reinterpret_cast<uint8_t*>(tokens + M.tok_off);
+  if (k0 + 3 < M.L) {   // bits [b, b + 32) of N, byte k0 the most significant
+    const uint32_t b = 1 + 8 * (M.L - 1 - (k0 + 3));
+    const uint64_t two = (uint64_t)W[b >> 5] | ((uint64_t)W[(b >> 5) + 1] << 32);
+    *reinterpret_cast<uint32_t*>(out + k0) = __builtin_bswap32((uint32_t)(two >> (b & 31)));
+  } else {
+    for (uint32_t k = k0; k < M.L; ++k) {
+      const uint32_t b = 1 + 8 * (M.L - 1 - k);   // lowest bit of output byte k
+      const uint64_t two = (uint64_t)W[b >> 5] | ((uint64_t)W[(b >> 5) + 1] << 32);
+      out[k] = (uint8_t)(two >> (b & 31));
+    }
+  }
 }
 
 extern "C" int vp8g_launch_check(const char* what);
@@ -551,7 +560,7 @@ extern "C" int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
   }
   // output bytes: at most (7 * ntok + 40) / 8 + 1 per frame
   const uint32_t maxL = (7u * max_ntok + 48) / 8 + 2;
-  hipLaunchKernelGGL(k_emit_bytes, dim3((maxL + 255) / 256, n), dim3(256), 0, st, tokens, tok_cap,
+  hipLaunchKernelGGL(k_emit_bytes, dim3((maxL + 1023) / 1024, n), dim3(256), 0, st, tokens, tok_cap,
                      (const vp8g_emit_meta*)meta, (const uint32_t*)nbuf);
   return vp8g_launch_check("k_emit_bytes");
 }

@@ -243,6 +243,7 @@ __global__ __launch_bounds__(256) void k_cleanup_alpha(uint8_t* __restrict__ yuv
 struct K2Wave {
   uint8_t yl[17], ul[9], vl[9];
   uint8_t top[32];
+  int dc3[3];   // the DC predictions of Y, U, V
   int hist[4][32];
 };
 
@@ -307,6 +308,24 @@ __global__ __launch_bounds__(256) void k_analyze(const uint8_t* __restrict__ yuv
       else if (i < 16) L.top[i] = yin[i - K2_YW];
       else L.top[i] = (i < 24 ? uin : vin)[(i & 7) - K2_CW];
     }
+    if (lane >= 32 && lane < 35) {   // DC predictions straight from the tiles (dc_value)
+      const int c = lane - 32, n = c ? 8 : 16, stride = c ? K2_CW : K2_YW;
+      const uint8_t* in = c == 0 ? yin : c == 1 ? uin : vin;
+      int dc = 0;
+      if (y > 0) {
+        for (int jj = 0; jj < n; ++jj) dc += in[jj - stride];
+        if (x > 0) { for (int jj = 0; jj < n; ++jj) dc += in[jj * stride - 1]; }
+        else dc += dc;
+        dc = (dc + n) >> (c ? 4 : 5);
+      } else if (x > 0) {
+        for (int jj = 0; jj < n; ++jj) dc += in[jj * stride - 1];
+        dc += dc;
+        dc = (dc + n) >> (c ? 4 : 5);
+      } else {
+        dc = 0x80;
+      }
+      L.dc3[c] = dc;
+    }
     for (int k = lane; k < 4 * 32; k += 64) (&L.hist[0][0])[k] = 0;
     __syncthreads();
     const bool hl = x > 0, ht = y > 0;
@@ -330,7 +349,7 @@ __global__ __launch_bounds__(256) void k_analyze(const uint8_t* __restrict__ yuv
         left = c ? vl : ul; top = L.top + 16 + 8 * c; n = 8;
         hsel = 2 + m;
       }
-      const int dcv = m == 0 ? dc_value(left, top, hl, ht, n, n == 16 ? 5 : 4) : 0;
+      const int dcv = m == 0 ? L.dc3[lane < 32 ? 0 : 1 + ((lane & 7) >> 2)] : 0;
 #pragma unroll
       for (int i = 0; i < 16; ++i)
         d[i] = src[(i >> 2) * ss + (i & 3)] -

@@ -2098,6 +2098,15 @@ static int launch_k3_t(const K3Args& a, int n, bool trellis, void* stream) {
   }
   hipLaunchKernelGGL((k_encode<NW, TR, AF>), dim3(n), dim3(NW * K3T), lds, (hipStream_t)stream,
                      a);
+  static int sync_each = -1;   // WEBP_AMD_SYNC_K3=1: wait for K3 (fault localisation)
+  if (sync_each < 0) sync_each = getenv("WEBP_AMD_SYNC_K3") != nullptr;
+  if (sync_each) {
+    const hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+    if (e != hipSuccess) {
+      vp8g_set_error("k_encode (synchronised)", hipGetErrorString(e));
+      return 0;
+    }
+  }
   return vp8g_launch_check("k_encode");
 }
 

@@ -989,13 +989,13 @@ __device__ __forceinline__ int tok_stat_slot(uint32_t t) {
 #define K3_WAIT_TICKS (30ull * 100000000ull)
 
 // worker-uniform wait until *p >= v (another worker of this workgroup publishes *p)
-__device__ bool wait_ge(K3G& G, K3S& L, const int32_t* p, int32_t v) {
+__device__ bool wait_ge(K3G& G, K3S& L, const int32_t* p, int32_t v, int site) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) {
     if (__hip_atomic_load(&G.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
         __builtin_amdgcn_s_memrealtime() - t0 > K3_WAIT_TICKS) {
       L.myabort = 1;
-      G.abort = 1;
+      if (!G.abort) G.abort = site;   // the wait that gave up (in the result's error)
       break;
     }
     __builtin_amdgcn_s_sleep(2);
@@ -1318,8 +1318,8 @@ struct K3Args {
 // AF: also store each MB's reconstruction for the autofilter
 // X: K3X, the frame's rows are dealt to a.nwg workgroups (blocks of NW rows
 // round-robin); k_encode_xtail finishes the frame
-template <int NW, bool TR, bool AF = false, bool X = false>
-__global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
+template <int NW, bool TR, bool AF = false, bool X = false, int WPE = 1>
+__global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode(K3Args a) {
   extern __shared__ __align__(16) uint8_t smem[];
   const int mbw = a.mbw, mbh = a.mbh, nmb = mbw * mbh;
   K3G& G = *reinterpret_cast<K3G*>(smem);
@@ -1476,7 +1476,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
             if (tid == 0) atomicMax(&XL.claim, ep);
             if (!wait_gx(G, L, &XH->fold_ptr, (int32_t)fold_from, XH)) break;
           } else {
-            if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from)) break;
+            if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from, 1)) break;
           }
           fold_rows<X>(G, L, tid, fold_from, mb, (uint32_t)y * mbw, tok_base, mboff, xs);
           fold_from = mb;
@@ -1538,10 +1538,10 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
             wbar(L);
             if (tid == 0) publish(&G.epoch, ep);
           } else {
-            if (!wait_ge(G, L, &G.epoch, ep)) break;
+            if (!wait_ge(G, L, &G.epoch, ep, 2)) break;
           }
         } else {
-          if (!wait_ge(G, L, &G.epoch, ep)) break;
+          if (!wait_ge(G, L, &G.epoch, ep, 2)) break;
         }
       }
       // ---- wavefront dependency: MB x+1 of the row above (top-right) is done
@@ -1561,7 +1561,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
             else if (k == 10) reinterpret_cast<uint32_t*>(xtopderr + 4 * c)[0] = v;
           }
         }
-      } else if (y > 0 && !wait_ge(G, L, &rowdone[y - 1], min(x + 2, mbw))) {
+      } else if (y > 0 && !wait_ge(G, L, &rowdone[y - 1], min(x + 2, mbw), 3)) {
         break;
       }
       K3_STAMP(0);
@@ -1945,7 +1945,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
     if constexpr (X) {
       if (!wait_gx(G, L, &XH->fold_ptr, (int32_t)fold_from, XH)) break;
     } else {
-      if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from)) break;
+      if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from, 4)) break;
     }
     fold_rows<X>(G, L, tid, fold_from, (uint32_t)(y + 1) * mbw, (uint32_t)y * mbw, tok_base,
                  mboff, xs);
@@ -1982,7 +1982,7 @@ __global__ __launch_bounds__(NW * K3T) void k_encode(K3Args a) {
     for (int s = tid; s < NSLOT; s += K3T) R->probas[s] = G.coeffs[s];
     if (tid == 0) {
       R->ntokens = G.ntok;
-      R->error = G.abort ? 2 : G.tok_err;
+      R->error = G.abort ? 2 | (G.abort << 4) : G.tok_err;
       for (int s = 0; s < 4; ++s) R->max_edge[s] = G.max_edge[s];
       R->size_p0 = G.fs.size_p0;
       R->size_rh = G.fs.size_rh;
@@ -2077,7 +2077,7 @@ extern "C" int vp8g_launch_encode_w1(const uint8_t* yuv, size_t yfb, int w, int 
                                      vp8g_frame_result* results, void* stream);
 extern "C" int vp8g_launch_check(const char* what);
 
-template <int NW, bool TR, bool AF = false>
+template <int NW, bool TR, bool AF = false, int WPE = 1>
 static int launch_k3_t(const K3Args& a, int n, bool trellis, void* stream) {
   const size_t lds = k3_lds_bytes<NW>(a.mbw, a.mbh, trellis);
   if (lds > 160 * 1024) {
@@ -2088,7 +2088,8 @@ static int launch_k3_t(const K3Args& a, int n, bool trellis, void* stream) {
     static size_t attr_bytes = 0;
     if (lds > attr_bytes) {
       const hipError_t e = hipFuncSetAttribute(
-          (const void*)k_encode<NW, TR, AF>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+          (const void*)k_encode<NW, TR, AF, false, WPE>,
+          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) {
         vp8g_set_error("k_encode dynamic LDS opt-in", hipGetErrorString(e));
         return 0;
@@ -2096,8 +2097,8 @@ static int launch_k3_t(const K3Args& a, int n, bool trellis, void* stream) {
       attr_bytes = lds;
     }
   }
-  hipLaunchKernelGGL((k_encode<NW, TR, AF>), dim3(n), dim3(NW * K3T), lds, (hipStream_t)stream,
-                     a);
+  hipLaunchKernelGGL((k_encode<NW, TR, AF, false, WPE>), dim3(n), dim3(NW * K3T), lds,
+                     (hipStream_t)stream, a);
   static int sync_each = -1;   // WEBP_AMD_SYNC_K3=1: wait for K3 (fault localisation)
   if (sync_each < 0) sync_each = getenv("WEBP_AMD_SYNC_K3") != nullptr;
   if (sync_each) {
@@ -2231,9 +2232,10 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
                                   void* stream) {
   static int variant = -1;
   if (variant < 0) {   // WEBP_AMD_K3: 1 = single-wavefront reference kernel, 2/3/5/4 =
-                       // 1/2/3/4 MB workers per frame, unset = default above
+                       // 1/2/3/4 MB workers per frame, 6 = 3 workers held to 128
+                       // VGPRs (spills to scratch; diagnostic), unset = default above
     const char* v = getenv("WEBP_AMD_K3");
-    variant = (v && v[0] >= '1' && v[0] <= '5') ? v[0] - '0' : 0;
+    variant = (v && v[0] >= '1' && v[0] <= '6') ? v[0] - '0' : 0;
   }
   // recon != NULL selects the autofilter instantiation; each frame's buffer
   // address travels in vp8g_frame_params::recon_addr
@@ -2260,5 +2262,6 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   if (variant == 3) return launch_k3<2>(a, n, trellis != 0, stream);
   if (variant == 4) return launch_k3<4>(a, n, trellis != 0, stream);
   if (variant == 5) return launch_k3<3>(a, n, trellis != 0, stream);
+  if (variant == 6 && !trellis) return launch_k3_t<3, false, false, 4>(a, n, false, stream);
   return launch_k3_default(a, n, trellis != 0, recon != nullptr, stream);
 }

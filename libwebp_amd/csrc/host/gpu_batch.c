@@ -239,7 +239,12 @@ static void frame_head(WebPGpuBatch* b, int f) {
   b->out_size[f] = 0;   /* b->out[f] (capacity b->out_cap[f]) is reused */
   vp8h_bw_free(&b->p0[f]);
   if (b->err[f] != VP8_ENC_OK) return;
-  if (res->error) { b->err[f] = VP8_ENC_ERROR_OUT_OF_MEMORY; return; }
+  if (res->error) {
+    if (getenv("WEBP_AMD_SYNC_K3"))   /* fault localisation: K3's raw error (wait site << 4) */
+      fprintf(stderr, "frame %d: K3 error 0x%x\n", f, (unsigned)res->error);
+    b->err[f] = VP8_ENC_ERROR_OUT_OF_MEMORY;
+    return;
+  }
   b->err[f] = vp8h_build_p0(fr, res, b->h_mbinfo + (size_t)f * b->nmb * VP8G_MBINFO_BYTES,
                             &b->p0[f], b->hdr + 2 * f);
 }

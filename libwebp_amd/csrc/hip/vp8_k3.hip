@@ -1318,7 +1318,7 @@ struct K3Args {
 // AF: also store each MB's reconstruction for the autofilter
 // X: K3X, the frame's rows are dealt to a.nwg workgroups (blocks of NW rows
 // round-robin); k_encode_xtail finishes the frame
-template <int NW, bool TR, bool AF = false, bool X = false, int WPE = 1>
+template <int NW, bool TR, bool AF = false, bool X = false, int WPE = 1, int PAD = 0>
 __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode(K3Args a) {
   extern __shared__ __align__(16) uint8_t smem[];
   const int mbw = a.mbw, mbh = a.mbh, nmb = mbw * mbh;
@@ -1326,8 +1326,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
   const int wk = threadIdx.x / K3T;        // worker
   const int tid_k = threadIdx.x % K3T;     // thread within the worker
   const int tid = tid_k;
-  K3S& L = reinterpret_cast<K3S*>(smem + sizeof(K3G))[wk];
-  uint8_t* ytop = smem + sizeof(K3G) + NW * sizeof(K3S);   // 16*mbw + 16
+  K3S& L = reinterpret_cast<K3S*>(smem + sizeof(K3G) + PAD)[wk];
+  uint8_t* ytop = smem + sizeof(K3G) + PAD + NW * sizeof(K3S);   // 16*mbw + 16
   uint8_t* uvtop = ytop + 16 * mbw + 16;                      // 16*mbw
   uint32_t* nzw = reinterpret_cast<uint32_t*>(uvtop + 16 * mbw) + 1;   // [-1..mbw-1]
   uint8_t* predtop = reinterpret_cast<uint8_t*>(nzw + mbw);           // 4*mbw
@@ -2066,8 +2066,8 @@ __global__ __launch_bounds__(K3T) void k_encode_xtail(K3Args a) {
 // ---------------------------------------------------------------------------
 
 template <int NW>
-static size_t k3_lds_bytes(int mbw, int mbh, bool trellis) {
-  return sizeof(K3G) + NW * sizeof(K3S) + (16 * mbw + 16) + 16 * mbw + 4 * (mbw + 1) + 4 * mbw +
+static size_t k3_lds_bytes(int mbw, int mbh, bool trellis, size_t pad = 0) {
+  return sizeof(K3G) + pad + NW * sizeof(K3S) + (16 * mbw + 16) + 16 * mbw + 4 * (mbw + 1) + 4 * mbw +
          4 * mbw + 4 * mbh + (trellis ? (size_t)NW * 64 * 32 * 4 : 0) + 16;
 }
 
@@ -2077,9 +2077,9 @@ extern "C" int vp8g_launch_encode_w1(const uint8_t* yuv, size_t yfb, int w, int 
                                      vp8g_frame_result* results, void* stream);
 extern "C" int vp8g_launch_check(const char* what);
 
-template <int NW, bool TR, bool AF = false, int WPE = 1>
+template <int NW, bool TR, bool AF = false, int WPE = 1, int PAD = 0>
 static int launch_k3_t(const K3Args& a, int n, bool trellis, void* stream) {
-  const size_t lds = k3_lds_bytes<NW>(a.mbw, a.mbh, trellis);
+  const size_t lds = k3_lds_bytes<NW>(a.mbw, a.mbh, trellis, PAD);
   if (lds > 160 * 1024) {
     vp8g_set_error("k_encode", "frame too wide for the LDS budget");
     return 0;
@@ -2088,7 +2088,7 @@ static int launch_k3_t(const K3Args& a, int n, bool trellis, void* stream) {
     static size_t attr_bytes = 0;
     if (lds > attr_bytes) {
       const hipError_t e = hipFuncSetAttribute(
-          (const void*)k_encode<NW, TR, AF, false, WPE>,
+          (const void*)k_encode<NW, TR, AF, false, WPE, PAD>,
           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) {
         vp8g_set_error("k_encode dynamic LDS opt-in", hipGetErrorString(e));
@@ -2097,7 +2097,7 @@ static int launch_k3_t(const K3Args& a, int n, bool trellis, void* stream) {
       attr_bytes = lds;
     }
   }
-  hipLaunchKernelGGL((k_encode<NW, TR, AF, false, WPE>), dim3(n), dim3(NW * K3T), lds,
+  hipLaunchKernelGGL((k_encode<NW, TR, AF, false, WPE, PAD>), dim3(n), dim3(NW * K3T), lds,
                      (hipStream_t)stream, a);
   static int sync_each = -1;   // WEBP_AMD_SYNC_K3=1: wait for K3 (fault localisation)
   if (sync_each < 0) sync_each = getenv("WEBP_AMD_SYNC_K3") != nullptr;
@@ -2233,9 +2233,12 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   static int variant = -1;
   if (variant < 0) {   // WEBP_AMD_K3: 1 = single-wavefront reference kernel, 2/3/5/4 =
                        // 1/2/3/4 MB workers per frame, 6 = 3 workers held to 128
-                       // VGPRs (spills to scratch; diagnostic), unset = default above
+                       // VGPRs (spills to scratch; diagnostic), 7 / 8 = 3 / 2 workers
+                       // with their state moved 40 KB / 64 KB up the LDS (diagnostic:
+                       // the 4-worker stall vs worker state at high LDS addresses),
+                       // unset = default above
     const char* v = getenv("WEBP_AMD_K3");
-    variant = (v && v[0] >= '1' && v[0] <= '6') ? v[0] - '0' : 0;
+    variant = (v && v[0] >= '1' && v[0] <= '8') ? v[0] - '0' : 0;
   }
   // recon != NULL selects the autofilter instantiation; each frame's buffer
   // address travels in vp8g_frame_params::recon_addr
@@ -2263,5 +2266,7 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   if (variant == 4) return launch_k3<4>(a, n, trellis != 0, stream);
   if (variant == 5) return launch_k3<3>(a, n, trellis != 0, stream);
   if (variant == 6 && !trellis) return launch_k3_t<3, false, false, 4>(a, n, false, stream);
+  if (variant == 7 && !trellis) return launch_k3_t<3, false, false, 1, 40960>(a, n, false, stream);
+  if (variant == 8 && !trellis) return launch_k3_t<2, false, false, 1, 65536>(a, n, false, stream);
   return launch_k3_default(a, n, trellis != 0, recon != nullptr, stream);
 }

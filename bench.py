@@ -70,6 +70,11 @@ def parse_args(argv=None):
                     help="skip the PCIe-inclusive host-input measurement")
     ap.add_argument("--stub", action="store_true",
                     help="CPU test double instead of the GPU encoder (gloo; tests only)")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default=None,
+                    help="collective backend (default nccl = RCCL on the GPUs; gloo lets "
+                         "tests run several real-encoder ranks on one GPU)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on device 0 (tests on a one-GPU box only)")
     return ap.parse_args(argv)
 
 
@@ -373,19 +378,30 @@ def main(argv=None):
 
     import torch
     import torch.distributed as dist
+    gpu_dev = 0 if args.same_device else local
     if args.stub:
         dev = torch.device("cpu")
         backend = "gloo"
     else:
-        torch.cuda.set_device(local)
-        dev = torch.device("cuda", local)
-        backend = "nccl"
+        torch.cuda.set_device(gpu_dev)
+        dev = torch.device("cuda", gpu_dev)
+        backend = args.dist_backend or "nccl"
+    # the collectives' tensors: on the GPU for RCCL, in host memory for gloo
+    cdev = dev if backend == "nccl" else torch.device("cpu")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if args.stub:
-            dist.init_process_group(backend, rank=rank, world_size=world)
-        else:
+        if backend == "nccl":
             dist.init_process_group(backend, rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
+    cpus = []
+    if not args.stub:
+        # this rank's host threads on its GPU's NUMA node; the
+        # engines pin their own worker threads to the same CPUs
+        import libwebp_amd
+        cpus = libwebp_amd.host_cpus(gpu_dev)
+        if cpus:
+            os.sched_setaffinity(0, cpus)
 
     first, _ = shard(rank, B)
     if args.stub:
@@ -397,7 +413,7 @@ def main(argv=None):
         libwebp_amd.synth_device(rgba.data_ptr(), W, H, first, B, seed=1, stream=stream)
         torch.cuda.synchronize(dev)
         enc = libwebp_amd.GpuBatch(W, H, B, quality=args.quality, method=args.method,
-                                   device=local, threads=args.threads,
+                                   device=gpu_dev, threads=args.threads,
                                    use_sharp_yuv=int(args.sharp_yuv),
                                    lossless=int(args.lossless), low_memory=int(args.low_memory))
 
@@ -410,7 +426,7 @@ def main(argv=None):
     encs = [enc]
     for _ in range(E - 1):
         encs.append(libwebp_amd.GpuBatch(W, H, B, quality=args.quality, method=args.method,
-                                         device=local, threads=args.threads,
+                                         device=gpu_dev, threads=args.threads,
                                          use_sharp_yuv=int(args.sharp_yuv),
                                          lossless=int(args.lossless),
                                          low_memory=int(args.low_memory)))
@@ -467,11 +483,11 @@ def main(argv=None):
         if first <= g < first + B:
             checked += 1
             failed += hashlib.sha256(enc.output(g - first)).hexdigest() != want
-    sizes = torch.tensor([enc.output_size(f) for f in range(B)], dtype=torch.int64, device=dev)
+    sizes = torch.tensor([enc.output_size(f) for f in range(B)], dtype=torch.int64, device=cdev)
     ntok = sum(enc.token_count(f) for f in range(B))
     allsizes = gather_sizes(sizes, world)
-    elapsed = max_over_ranks(elapsed, world, dev)
-    checked, failed = sum_over_ranks([checked, failed], world, dev)
+    elapsed = max_over_ranks(elapsed, world, cdev)
+    checked, failed = sum_over_ranks([checked, failed], world, cdev)
     total_bytes = int(sum(int(s.sum().item()) for s in allsizes))
 
     host_rate = None
@@ -498,6 +514,8 @@ def main(argv=None):
                                        % len(encs))
         if cb:
             line["cpu_baseline"] = cb
+        if not args.stub:
+            line["host_cpus_per_rank"] = len(cpus) if cpus else "unpinned"
         if args.stub:
             line["data"] = "stub encoder (CPU test double, no GPU)"
         print(json.dumps(line), flush=True)

@@ -118,11 +118,11 @@ typedef enum WebPPreset {
 WEBP_EXTERN int WebPConfigInitInternal(WebPConfig*, WebPPreset, float, int);
 
 /* ref encode.h:173-186 */
-WEBP_INLINE int WebPConfigInit(WebPConfig* config) {
+static WEBP_INLINE int WebPConfigInit(WebPConfig* config) {
   return WebPConfigInitInternal(config, WEBP_PRESET_DEFAULT, 75.f,
                                 WEBP_ENCODER_ABI_VERSION);
 }
-WEBP_INLINE int WebPConfigPreset(WebPConfig* config, WebPPreset preset,
+static WEBP_INLINE int WebPConfigPreset(WebPConfig* config, WebPPreset preset,
                                  float quality) {
   return WebPConfigInitInternal(config, preset, quality,
                                 WEBP_ENCODER_ABI_VERSION);
@@ -232,7 +232,7 @@ struct WebPPicture {
 
 /* ref encode.h:367-375 */
 WEBP_EXTERN int WebPPictureInitInternal(WebPPicture*, int);
-WEBP_INLINE int WebPPictureInit(WebPPicture* picture) {
+static WEBP_INLINE int WebPPictureInit(WebPPicture* picture) {
   return WebPPictureInitInternal(picture, WEBP_ENCODER_ABI_VERSION);
 }
 

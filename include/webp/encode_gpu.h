@@ -98,6 +98,13 @@ WEBP_EXTERN int WebPGpuSynthRGBA(void* rgba_dev, size_t frame_stride, int width,
 /* Text of the first HIP/runtime error seen by this thread ("" if none). */
 WEBP_EXTERN const char* WebPGpuLastError(void);
 
+/* The host CPUs this process's engines on `device` run their threads on:
+ * the device's NUMA node (sysfs), within the process affinity, split evenly
+ * between the LOCAL_WORLD_SIZE ranks sharing the node (rank r on device r).
+ * Writes up to max_cpus CPU ids into cpus and returns how many there are
+ * (0 when the node is unknown: threads are then not pinned). */
+WEBP_EXTERN int WebPGpuHostCpus(int device, int* cpus, int max_cpus);
+
 /* Number of HIP devices visible (0 when no GPU / no driver). */
 WEBP_EXTERN int WebPGpuDeviceCount(void);
 

@@ -8,8 +8,16 @@
 #include <stddef.h>
 #include <stdint.h>
 
+/* like the reference (src/webp/types.h:19-37): the headers write
+ * `static WEBP_INLINE`, and so do callers that define their own helpers
+ * (cwebp's stopwatch.h, the decoder and mux headers) */
 #ifndef WEBP_INLINE
-#define WEBP_INLINE static inline
+#if defined(__cplusplus) || !defined(__STRICT_ANSI__) || \
+    (defined(__STDC_VERSION__) && __STDC_VERSION__ >= 199901L)
+#define WEBP_INLINE inline
+#else
+#define WEBP_INLINE
+#endif
 #endif
 
 #ifndef WEBP_EXTERN

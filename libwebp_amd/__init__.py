@@ -12,7 +12,7 @@ import os
 
 from . import abi
 
-__all__ = ["load", "GpuBatch", "encode_rgba", "device_count", "lib_path", "abi"]
+__all__ = ["load", "GpuBatch", "encode_rgba", "device_count", "host_cpus", "lib_path", "abi"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
@@ -61,6 +61,7 @@ def load():
         "WebPGpuBatchGetTokens": (i, [vp, i, vp, sz]),
         "WebPGpuSynthRGBA": (i, [vp, sz, i, i, i, i, i, vp]),
         "WebPGpuDeviceCount": (i, []),
+        "WebPGpuHostCpus": (i, [i, C.POINTER(C.c_int), i]),
         "WebPGpuLastError": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
@@ -181,6 +182,15 @@ class GpuBatch:
         if not self._lib.WebPGpuBatchGetMBInfo(self._h, f, buf.ctypes.data):
             raise RuntimeError("GetMBInfo failed")
         return buf
+
+
+def host_cpus(device):
+    """CPU ids the engines on `device` pin their host threads to ([] = unpinned)."""
+    lib = load()
+    n = lib.WebPGpuHostCpus(device, None, 0)
+    buf = (C.c_int * max(n, 1))()
+    n = lib.WebPGpuHostCpus(device, buf, n)
+    return list(buf[:n])
 
 
 def synth_device(ptr, width, height, first, n, seed=1, frame_stride=None, stream=None):

@@ -23,6 +23,7 @@
 #include <stdio.h>
 
 #include <atomic>
+#include <mutex>
 
 #define K3T 256
 
@@ -109,18 +110,35 @@ struct K3S {
   uint16_t rowcnt[1024];           // mbw <= 1024 (width <= 16383)
 };
 
+// a cross-worker wait that has not been satisfied after this long (100 MHz
+// s_memrealtime ticks, 30 s) is a bug: the frame is aborted with an error
+// instead of hanging the GPU
+#define K3_WAIT_TICKS (30ull * 100000000ull)
+
 // Barrier over the 4 wavefronts of one worker (s_barrier would stop the whole
 // workgroup, i.e. every worker). Arrivals count up an LDS word; a wave
 // waits for the next multiple of 4. Called in worker-uniform control flow.
+// Bounded like every other cross-wave wait: a wave that has waited
+// K3_WAIT_TICKS sets the worker's abort flag, after which every barrier of
+// the worker falls through, the worker leaves its row loop and the frame
+// reports an error (no barrier can hang the GPU).
 __device__ __forceinline__ void wbar(K3S& L) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   uint32_t target = 0;
   if ((threadIdx.x & 63) == 0) target = (atomicAdd(&L.bar, 1u) & ~3u) + 4u;
   target = __builtin_amdgcn_readfirstlane(target);
-  while (__hip_atomic_load(&L.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+  // ~2^30 polls of >= 64 clocks each: well beyond K3_WAIT_TICKS
+  for (uint32_t spin = 0;
+       __hip_atomic_load(&L.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target; ++spin) {
+    if (spin >> 30) {
+      L.myabort = 1;
+      break;
+    }
     __builtin_amdgcn_s_sleep(1);
+  }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
+
 #define WB() wbar(L)
 
 // all-threads AND over the worker
@@ -982,11 +1000,6 @@ __device__ __forceinline__ int tok_stat_slot(uint32_t t) {
   const int id = (int)(t & 0x3fff);
   return (id % 11 == 10) ? id - 1 : id;
 }
-
-// a cross-worker wait that has not been satisfied after this long (100 MHz
-// s_memrealtime ticks, 30 s) is a bug: the frame is aborted with an error
-// instead of hanging the GPU
-#define K3_WAIT_TICKS (30ull * 100000000ull)
 
 // worker-uniform wait until *p >= v (another worker of this workgroup publishes *p)
 __device__ bool wait_ge(K3G& G, K3S& L, const int32_t* p, int32_t v, int site) {
@@ -1940,7 +1953,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       }
       K3_STAMP(6);
     }
-    if (L.myabort) break;
+    if (L.myabort) {   // a timed-out wait or barrier: the other workers stop waiting too
+      if (tid == 0 && !G.abort) G.abort = 5;
+      break;
+    }
     // row end: fold this row's remaining MBs once the rows above are folded
     if constexpr (X) {
       if (!wait_gx(G, L, &XH->fold_ptr, (int32_t)fold_from, XH)) break;
@@ -1954,6 +1970,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
   }
 
   // ---- frame epilogue: final probabilities and side results
+  // a worker barrier that timed out (wbar) aborts the frame (wait site 5)
+  if (tid == 0 && L.myabort && !G.abort) G.abort = 5;
   __syncthreads();
   if constexpr (X) {   // this workgroup's share of the side statistics; k_encode_xtail finishes
     if (gt == 0) {
@@ -2085,22 +2103,24 @@ static int launch_k3_t(const K3Args& a, int n, bool trellis, void* stream) {
     return 0;
   }
   if (lds > 64 * 1024) {   // beyond the default dynamic-LDS limit: opt in
-    static size_t attr_bytes = 0;
-    if (lds > attr_bytes) {
-      const hipError_t e = hipFuncSetAttribute(
-          (const void*)k_encode<NW, TR, AF, false, WPE, PAD>,
-          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (e != hipSuccess) {
-        vp8g_set_error("k_encode dynamic LDS opt-in", hipGetErrorString(e));
-        return 0;
-      }
-      attr_bytes = lds;
+    // once, to the whole 160 KB: engines on other host threads launch this
+    // kernel concurrently, and a smaller opt-in landing after a larger one
+    // would lower the limit under the other launch
+    static std::once_flag once;
+    static hipError_t attr_err = hipSuccess;
+    std::call_once(once, [] {
+      attr_err = hipFuncSetAttribute((const void*)k_encode<NW, TR, AF, false, WPE, PAD>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    });
+    if (attr_err != hipSuccess) {
+      vp8g_set_error("k_encode dynamic LDS opt-in", hipGetErrorString(attr_err));
+      return 0;
     }
   }
   hipLaunchKernelGGL((k_encode<NW, TR, AF, false, WPE, PAD>), dim3(n), dim3(NW * K3T), lds,
                      (hipStream_t)stream, a);
-  static int sync_each = -1;   // WEBP_AMD_SYNC_K3=1: wait for K3 (fault localisation)
-  if (sync_each < 0) sync_each = getenv("WEBP_AMD_SYNC_K3") != nullptr;
+  // WEBP_AMD_SYNC_K3=1: wait for K3 (fault localisation)
+  static const bool sync_each = getenv("WEBP_AMD_SYNC_K3") != nullptr;
   if (sync_each) {
     const hipError_t e = hipStreamSynchronize((hipStream_t)stream);
     if (e != hipSuccess) {
@@ -2134,26 +2154,21 @@ static int launch_k3x(K3Args a, int n, int nwg, void* stream) {
     vp8g_set_error("k_encode (K3X)", "frame too wide for the LDS budget");
     return 0;
   }
-  static size_t attr_bytes = 0, attr_tail = 0;
-  if (lds > 64 * 1024 && lds > attr_bytes) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k_encode<NW, TR, false, true>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) {
-      vp8g_set_error("k_encode (K3X) dynamic LDS opt-in", hipGetErrorString(e));
-      return 0;
-    }
-    attr_bytes = lds;
+  // one opt-in to the whole 160 KB per kernel (see launch_k3_t)
+  static std::once_flag once;
+  static hipError_t attr_err = hipSuccess;
+  std::call_once(once, [] {
+    attr_err = hipFuncSetAttribute((const void*)k_encode<NW, TR, false, true>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (attr_err == hipSuccess)
+      attr_err = hipFuncSetAttribute((const void*)k_encode_xtail,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  });
+  if (attr_err != hipSuccess) {
+    vp8g_set_error("k_encode (K3X) dynamic LDS opt-in", hipGetErrorString(attr_err));
+    return 0;
   }
-  if (lds_tail > 64 * 1024 && attr_tail == 0) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k_encode_xtail,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)lds_tail);
-    if (e != hipSuccess) {
-      vp8g_set_error("k_encode_xtail dynamic LDS opt-in", hipGetErrorString(e));
-      return 0;
-    }
-    attr_tail = lds_tail;
-  }
+  (void)lds_tail;
   a.nwg = nwg;
   if (hipMemsetAsync(a.xs, 0, (size_t)n * a.xs_fb, (hipStream_t)stream) != hipSuccess) {
     vp8g_set_error("k_encode (K3X)", "xsync reset failed");
@@ -2188,11 +2203,10 @@ static int launch_k3x_budget(const K3Args& a, int n, int nwg, void* stream) {
 // workgroups per frame for K3X: fill the free CUs with the frames' MB rows
 // (NW rows per workgroup), taken from the budget; 1 = the one-workgroup kernel
 static int k3x_take(int n, int mbh, int nw) {
-  static int mode = -1;
-  if (mode < 0) {   // WEBP_AMD_K3X=0 turns the split off (A/B)
+  static const int mode = [] {   // WEBP_AMD_K3X=0 turns the split off (A/B)
     const char* v = getenv("WEBP_AMD_K3X");
-    mode = (v && v[0] == '0') ? 0 : 1;
-  }
+    return (v && v[0] == '0') ? 0 : 1;
+  }();
   if (!mode || n > VP8G_XSPLIT_MAX_FRAMES) return 1;
   int cur = g_x_free.load();
   if (cur < 0) {   // first use: one workgroup per CU of the device
@@ -2230,16 +2244,15 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
                                   uint32_t* mboff, int trellis, vp8g_frame_result* results,
                                   uint8_t* rerun_state, uint8_t* recon, uint8_t* xsync,
                                   void* stream) {
-  static int variant = -1;
-  if (variant < 0) {   // WEBP_AMD_K3: 1 = single-wavefront reference kernel, 2/3/5/4 =
-                       // 1/2/3/4 MB workers per frame, 6 = 3 workers held to 128
-                       // VGPRs (spills to scratch; diagnostic), 7 / 8 = 3 / 2 workers
-                       // with their state moved 40 KB / 64 KB up the LDS (diagnostic:
-                       // the 4-worker stall vs worker state at high LDS addresses),
-                       // unset = default above
+  // WEBP_AMD_K3: 1 = single-wavefront reference kernel, 2/3/5 = 1/2/3 MB
+  // workers per frame (4 = the refused 4-worker build), 6 = 3 workers held to
+  // 128 VGPRs (spills to scratch; diagnostic), 7 / 8 = 3 / 2 workers with
+  // their state moved 40 KB / 64 KB up the LDS (diagnostic: the 4-worker
+  // stall vs worker state at high LDS addresses), unset = default above
+  static const int variant = [] {
     const char* v = getenv("WEBP_AMD_K3");
-    variant = (v && v[0] >= '1' && v[0] <= '8') ? v[0] - '0' : 0;
-  }
+    return (v && v[0] >= '1' && v[0] <= '8') ? v[0] - '0' : 0;
+  }();
   // recon != NULL selects the autofilter instantiation; each frame's buffer
   // address travels in vp8g_frame_params::recon_addr
   if (recon != nullptr && variant != 0) {
@@ -2263,7 +2276,10 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   }
   if (variant == 2) return launch_k3<1>(a, n, trellis != 0, stream);
   if (variant == 3) return launch_k3<2>(a, n, trellis != 0, stream);
-  if (variant == 4) return launch_k3<4>(a, n, trellis != 0, stream);
+  if (variant == 4) {   // stalls in its wavefront wait: refused
+    vp8g_set_error("k_encode", "the 4-worker K3 variant is disabled (known stall)");
+    return 0;
+  }
   if (variant == 5) return launch_k3<3>(a, n, trellis != 0, stream);
   if (variant == 6 && !trellis) return launch_k3_t<3, false, false, 4>(a, n, false, stream);
   if (variant == 7 && !trellis) return launch_k3_t<3, false, false, 1, 40960>(a, n, false, stream);

@@ -46,10 +46,14 @@ int WebPGpuDeviceCount(void) {
   return n;
 }
 
-static int default_threads(void) {
+/* host threads of an engine: WEBP_AMD_THREADS, else at most 16, and no more
+ * than the CPUs of this rank's share of its GPU's NUMA node (host_cpus.c) */
+static int default_threads(int device) {
   const char* e = getenv("WEBP_AMD_THREADS");
   if (e && atoi(e) > 0) return atoi(e);
   long n = sysconf(_SC_NPROCESSORS_ONLN);
+  const int pinned = vp8g_device_ncpu(device);
+  if (pinned > 0 && pinned < n) n = pinned;
   if (n < 1) n = 1;
   return n > 16 ? 16 : (int)n;
 }
@@ -86,7 +90,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
     b->w = width; b->h = height;
     b->max_frames = max_frames;
     b->cfg = *config;
-    b->threads = host_threads > 0 ? host_threads : default_threads();
+    b->threads = host_threads > 0 ? host_threads : default_threads(device);
     CHK(hipSetDevice(device));
     CHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
     for (int i = 0; i < 6; ++i) CHK(hipEventCreate(&b->ev[i]));
@@ -110,7 +114,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   b->tok_cap = (size_t)b->nmb * VP8G_MAX_TOKENS_PER_MB;
   b->sharp = vp8h_use_sharp(config, width, height);
   b->dither = b->sharp ? 0.f : vp8h_import_dithering(config);
-  b->threads = host_threads > 0 ? host_threads : default_threads();
+  b->threads = host_threads > 0 ? host_threads : default_threads(device);
   {   /* WEBP_AMD_HOST_EMIT=1: boolean-code partition 1 on the host threads */
     const char* he = getenv("WEBP_AMD_HOST_EMIT");
     b->host_emit = he && he[0] == '1';
@@ -318,7 +322,7 @@ static void tail_spawn(TailJob* j, WebPGpuBatch* b, int n, int phase, int extra)
   if (extra > n) extra = n;
   if (extra > TAIL_MAX_THREADS) extra = TAIL_MAX_THREADS;
   for (int i = 0; i < extra; ++i)
-    if (pthread_create(&j->th[j->started], NULL, tail_worker, j) == 0) ++j->started;
+    if (vp8g_thread_create(&j->th[j->started], tail_worker, j, b->device) == 0) ++j->started;
 }
 
 static void tail_join(TailJob* j) {
@@ -373,6 +377,12 @@ static int encode_alpha(WebPGpuBatch* b, int n) {
     CHK(hipStreamSynchronize(b->stream));
   }
   if (b->cfg.alpha_compression) {
+    /* the ALPH effort follows config->method on every call (alpha_enc.c:76,
+     * 379); the WebPEncode pool hands an engine configs of other methods */
+    if (b->la && b->la->method != b->cfg.method) {
+      vp8l_engine_free(b->la);
+      b->la = NULL;
+    }
     if (!b->la) b->la = vp8l_engine_new(b->w, b->h, b->max_frames, b->cfg.method, 1);
     if (!b->la) return 0;
     if (!vp8l_engine_encode(b->la, b->stream, b->threads, b->d_aplane, plane, b->w, n, t))

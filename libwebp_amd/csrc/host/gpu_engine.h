@@ -2,12 +2,18 @@
 #ifndef LIBWEBP_AMD_GPU_ENGINE_H_
 #define LIBWEBP_AMD_GPU_ENGINE_H_
 
+#include <pthread.h>
+
 #include <hip/hip_runtime_api.h>
 
 #include "../vp8_gpu.h"
 #include "vp8_host.h"
 #include "vp8l_batch.h"
 #include "webp/encode.h"
+
+/* host-thread placement on the GPU's NUMA node (host_cpus.c) */
+int vp8g_thread_create(pthread_t* th, void* (*fn)(void*), void* arg, int device);
+int vp8g_device_ncpu(int device);   /* CPUs of the device's share (0: not pinned) */
 
 struct WebPGpuBatch {
   int device, w, h, max_frames, mbw, mbh, nmb, uvw, uvh, threads, last_n;

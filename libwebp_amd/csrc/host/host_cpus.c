@@ -1,0 +1,153 @@
+/* Host-thread placement ("each GPU runs its own batch
+ * pipeline and host-tail pool; pin host threads to the GPU's NUMA node").
+ *
+ * The CPUs an engine's host threads may use: the NUMA node of its GPU (from
+ * the device's PCI address in sysfs), intersected with this process's
+ * affinity mask, split evenly between the ranks that share the node. Ranks
+ * are one process per GPU with local rank r on device r (torchrun's
+ * LOCAL_WORLD_SIZE ranks over the visible devices); a single process (no
+ * LOCAL_WORLD_SIZE) keeps the whole node. When the node is unknown (no sysfs
+ * entry, a node with none of our CPUs) nothing is pinned.
+ * WEBP_AMD_NO_PIN=1 turns placement off. */
+#define _GNU_SOURCE
+#include <ctype.h>
+#include <pthread.h>
+#include <sched.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "gpu_engine.h"
+#include "webp/encode_gpu.h"
+
+#define MAX_DEV 64
+
+typedef struct {
+  int done, ncpu;
+  cpu_set_t set;
+} DevCpus;
+
+static DevCpus g_dev[MAX_DEV];
+static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
+
+static int device_numa_node(int device) {
+  char bus[64], path[160];
+  if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus), device) != hipSuccess) return -1;
+  for (char* p = bus; *p; ++p) *p = (char)tolower((unsigned char)*p);
+  snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus);
+  FILE* f = fopen(path, "r");
+  if (!f) return -1;
+  int node = -1;
+  if (fscanf(f, "%d", &node) != 1) node = -1;
+  fclose(f);
+  return node;
+}
+
+/* "0-23,48-71" -> set; returns the number of CPUs read */
+static int read_cpulist(int node, cpu_set_t* set) {
+  char path[96], buf[4096];
+  snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+  FILE* f = fopen(path, "r");
+  if (!f) return 0;
+  const size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+  fclose(f);
+  buf[n] = 0;
+  CPU_ZERO(set);
+  int count = 0;
+  for (char* p = buf; *p;) {
+    if (!isdigit((unsigned char)*p)) { ++p; continue; }
+    char* end;
+    const long a = strtol(p, &end, 10);
+    long b = a;
+    if (*end == '-') b = strtol(end + 1, &end, 10);
+    for (long c = a; c <= b && c < CPU_SETSIZE; ++c) {
+      if (!CPU_ISSET((int)c, set)) ++count;
+      CPU_SET((int)c, set);
+    }
+    p = end;
+  }
+  return count;
+}
+
+static void compute(int device, DevCpus* d) {
+  d->ncpu = 0;
+  const char* off = getenv("WEBP_AMD_NO_PIN");
+  if (off && off[0] == '1') return;
+  const int node = device_numa_node(device);
+  if (node < 0) return;
+  cpu_set_t nodeset, mine;
+  if (read_cpulist(node, &nodeset) <= 0) return;
+  if (sched_getaffinity(0, sizeof(mine), &mine) != 0) return;
+  int cpus[CPU_SETSIZE], n = 0;
+  for (int c = 0; c < CPU_SETSIZE; ++c)
+    if (CPU_ISSET(c, &nodeset) && CPU_ISSET(c, &mine)) cpus[n++] = c;
+  if (n == 0) return;
+  /* ranks on this node: devices 0 .. local_world-1 in use, one rank each */
+  int ndev = 0, ranks = 1, idx = 0;
+  const char* lw = getenv("LOCAL_WORLD_SIZE");
+  const int local_world = lw ? atoi(lw) : 1;
+  if (local_world > 1 && hipGetDeviceCount(&ndev) == hipSuccess) {
+    ranks = 0;
+    for (int k = 0; k < ndev && k < local_world; ++k) {
+      if (device_numa_node(k) != node) continue;
+      if (k < device) ++idx;
+      ++ranks;
+    }
+    if (ranks < 1) ranks = 1;
+    if (idx >= ranks) idx = ranks - 1;
+  }
+  int share = n / ranks;
+  if (share < 1) share = 1;
+  const int lo = (idx * share) % n;
+  CPU_ZERO(&d->set);
+  for (int k = 0; k < share; ++k) CPU_SET(cpus[(lo + k) % n], &d->set);
+  d->ncpu = share;
+}
+
+/* The CPU set of `device`'s host threads (NULL: no placement); *ncpu its size. */
+const cpu_set_t* vp8g_device_cpus(int device, int* ncpu) {
+  *ncpu = 0;
+  if (device < 0 || device >= MAX_DEV) return NULL;
+  pthread_mutex_lock(&g_lock);
+  DevCpus* d = &g_dev[device];
+  if (!d->done) {
+    compute(device, d);
+    d->done = 1;
+  }
+  pthread_mutex_unlock(&g_lock);
+  *ncpu = d->ncpu;
+  return d->ncpu > 0 ? &d->set : NULL;
+}
+
+/* pthread_create with the device's CPU set (plain create without one) */
+int vp8g_thread_create(pthread_t* th, void* (*fn)(void*), void* arg, int device) {
+  int ncpu = 0;
+  const cpu_set_t* set = vp8g_device_cpus(device, &ncpu);
+  if (!set) return pthread_create(th, NULL, fn, arg);
+  pthread_attr_t attr;
+  if (pthread_attr_init(&attr) != 0) return pthread_create(th, NULL, fn, arg);
+  int rc = pthread_attr_setaffinity_np(&attr, sizeof(cpu_set_t), set);
+  rc = rc == 0 ? pthread_create(th, &attr, fn, arg) : pthread_create(th, NULL, fn, arg);
+  pthread_attr_destroy(&attr);
+  return rc;
+}
+
+int WebPGpuHostCpus(int device, int* cpus, int max_cpus) {
+  int ncpu = 0, k = 0;
+  const cpu_set_t* set = vp8g_device_cpus(device, &ncpu);
+  if (!set) return 0;
+  for (int c = 0; c < CPU_SETSIZE && k < ncpu; ++c)
+    if (CPU_ISSET(c, set)) {
+      if (cpus && k < max_cpus) cpus[k] = c;
+      ++k;
+    }
+  return k;
+}
+
+int vp8g_device_ncpu(int device) {
+  int ncpu = 0;
+  (void)vp8g_device_cpus(device, &ncpu);
+  return ncpu;
+}

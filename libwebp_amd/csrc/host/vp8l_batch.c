@@ -230,8 +230,10 @@ static void run_headers(vp8l_engine* l, int n, int threads) {
   pthread_t th[64];
   int started = 0;
   if (threads > 64) threads = 64;
-  for (int i = 0; i < threads - 1 && i < n - 1; ++i)
-    if (pthread_create(&th[started], NULL, hdr_worker, &job) == 0) ++started;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  for (int i = 0; i < threads - 1 && i < n - 1; ++i)   /* on the GPU's NUMA node */
+    if (vp8g_thread_create(&th[started], hdr_worker, &job, dev) == 0) ++started;
   hdr_worker(&job);
   for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
 }

@@ -129,6 +129,17 @@ def test_gpu_alph_matches_model(gpu, kind, w, h, f, m):
     assert alph[1:] == M.encode(img[..., 3], method=m, alpha_plane=True)
 
 
+@pytest.mark.gpu
+def test_gpu_alph_effort_follows_method(gpu):
+    """WebPEncode calls of one picture size share a pooled engine: the ALPH
+    effort must follow each call's method (alpha_enc.c:76,379), not the
+    method of the call that created the engine"""
+    img = alpha_frame(160, 96, 1)   # its ALPH stream differs for m0 / m2 / m6
+    for m in (6, 2, 6, 0):
+        data = gpu.encode_rgba(img, quality=75.0, method=m, exact=1)
+        assert chunks(data)[b"ALPH"][1:] == M.encode(img[..., 3], method=m, alpha_plane=True), m
+
+
 def test_model_alph_size_vs_reference():
     """ALPH sizes against the reference's (committed, lossless_kat.json):
     the logo plane takes a palette like the reference's"""

@@ -27,6 +27,11 @@
 
 #define K3T 256
 
+// a cross-worker wait that has not been satisfied after this long (100 MHz
+// s_memrealtime ticks, 30 s) is a bug: the frame is aborted with an error
+// instead of hanging the GPU
+#define K3_WAIT_TICKS (30ull * 100000000ull)
+
 // LDS shared by all of a frame's workers: cost tables of the current epoch,
 // token statistics, quantiser/segment parameters and frame-level counters.
 struct alignas(16) K3G {
@@ -110,35 +115,27 @@ struct K3S {
   uint16_t rowcnt[1024];           // mbw <= 1024 (width <= 16383)
 };
 
-// a cross-worker wait that has not been satisfied after this long (100 MHz
-// s_memrealtime ticks, 30 s) is a bug: the frame is aborted with an error
-// instead of hanging the GPU
-#define K3_WAIT_TICKS (30ull * 100000000ull)
-
 // Barrier over the 4 wavefronts of one worker (s_barrier would stop the whole
 // workgroup, i.e. every worker). Arrivals count up an LDS word; a wave
 // waits for the next multiple of 4. Called in worker-uniform control flow.
-// Bounded like every other cross-wave wait: a wave that has waited
-// K3_WAIT_TICKS sets the worker's abort flag, after which every barrier of
-// the worker falls through, the worker leaves its row loop and the frame
-// reports an error (no barrier can hang the GPU).
+// The poll loop is deliberately bare: ~40 of these barriers sit on each MB's
+// dependent chain, and every variant with a time or iteration bound inside
+// the loop measured 3-7% slower K3 launches. A worker
+// barrier can only wait forever if a wave of the worker never arrives: all
+// waves of a worker take the same path, and every cross-worker wait that can
+// fail (wait_ge / wait_gx, bounded by K3_WAIT_TICKS) releases its worker's
+// waiting waves by setting bit 31 of the counter (WBAR_RELEASE), so they
+// fall through, the worker leaves its row loop and the frame reports an error.
+#define WBAR_RELEASE 0x80000000u
 __device__ __forceinline__ void wbar(K3S& L) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   uint32_t target = 0;
   if ((threadIdx.x & 63) == 0) target = (atomicAdd(&L.bar, 1u) & ~3u) + 4u;
   target = __builtin_amdgcn_readfirstlane(target);
-  // ~2^30 polls of >= 64 clocks each: well beyond K3_WAIT_TICKS
-  for (uint32_t spin = 0;
-       __hip_atomic_load(&L.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target; ++spin) {
-    if (spin >> 30) {
-      L.myabort = 1;
-      break;
-    }
+  while (__hip_atomic_load(&L.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
     __builtin_amdgcn_s_sleep(1);
-  }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
-
 #define WB() wbar(L)
 
 // all-threads AND over the worker
@@ -1008,7 +1005,8 @@ __device__ bool wait_ge(K3G& G, K3S& L, const int32_t* p, int32_t v, int site) {
     if (__hip_atomic_load(&G.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
         __builtin_amdgcn_s_memrealtime() - t0 > K3_WAIT_TICKS) {
       L.myabort = 1;
-      if (!G.abort) G.abort = site;   // the wait that gave up (in the result's error)
+      atomicOr(&L.bar, WBAR_RELEASE);   // no wave of this worker waits at a barrier now
+      if (!G.abort) G.abort = site;     // the wait that gave up (in the result's error)
       break;
     }
     __builtin_amdgcn_s_sleep(2);
@@ -1083,6 +1081,7 @@ __device__ bool wait_gx(K3G& G, K3S& L, const int32_t* p, int32_t v, XHdr* XH) {
     if (__hip_atomic_load(&G.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
         ld_sc1(&XH->abort) || __builtin_amdgcn_s_memrealtime() - t0 > K3_WAIT_TICKS) {
       L.myabort = 1;
+      atomicOr(&L.bar, WBAR_RELEASE);
       G.abort = 1;
       st_sc1(&XH->abort, 1);
       break;
@@ -1953,10 +1952,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       }
       K3_STAMP(6);
     }
-    if (L.myabort) {   // a timed-out wait or barrier: the other workers stop waiting too
-      if (tid == 0 && !G.abort) G.abort = 5;
-      break;
-    }
+    if (L.myabort) break;
     // row end: fold this row's remaining MBs once the rows above are folded
     if constexpr (X) {
       if (!wait_gx(G, L, &XH->fold_ptr, (int32_t)fold_from, XH)) break;
@@ -1970,8 +1966,6 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
   }
 
   // ---- frame epilogue: final probabilities and side results
-  // a worker barrier that timed out (wbar) aborts the frame (wait site 5)
-  if (tid == 0 && L.myabort && !G.abort) G.abort = 5;
   __syncthreads();
   if constexpr (X) {   // this workgroup's share of the side statistics; k_encode_xtail finishes
     if (gt == 0) {

@@ -7,10 +7,11 @@
 //                        LDS histograms, one global add per bin)
 //      k_vp8l_palscan    one workgroup per frame: the colour set in an LDS hash
 //                        table, out as soon as it exceeds 256 colours
-//   L1 k_vp8l_transform  one workgroup per transform tile: subtract green,
-//                        best of 14 predictors by a bit-length cost,
-//                        cross-colour multipliers (least squares + 6
-//                        candidates), residual ARGB to HBM -- or the plain
+//   L1 k_vp8l_transform  one workgroup per L1_TILES transform tiles: subtract
+//                        green, best of 14 predictors and the cross-colour
+//                        multipliers (a descent over parallel candidate
+//                        steps), all scored by entropy against the frame's
+//                        L0 histograms; residual ARGB to HBM -- or the plain
 //                        (sub-green) pixels for the non-spatial modes
 //      k_vp8l_palapply   colour indexing: binary search in the sorted palette,
 //                        2^xbits indices bundled per packed pixel
@@ -103,20 +104,14 @@ __device__ __forceinline__ uint32_t sub_pixels(uint32_t a, uint32_t b) {
   return (ag & 0xff00ff00u) | (rb & 0x00ff00ffu);
 }
 
-__device__ __forceinline__ int s8(int v) { return (int)(int8_t)(uint8_t)v; }
-__device__ __forceinline__ int ctd(int t, int c) { return (t * s8(c)) >> 5; }
-
-// round(32 * sxy / sxx) half away from zero, clamped to int8 (model: ls_multiplier)
-__device__ int ls_multiplier(long long sxy, long long sxx) {
-  if (sxx == 0) return 0;
-  const long long num = 32 * sxy;
-  const long long an = num < 0 ? -num : num;
-  long long q = (2 * an + sxx) / (2 * sxx);
-  q = num >= 0 ? q : -q;
-  return (int)(q < -128 ? -128 : q > 127 ? 127 : q);
+// (A, R-G, G, B-G) of a pixel (subtract green, src/dsp/lossless_enc.c)
+__device__ __forceinline__ uint32_t sub_green(uint32_t v) {
+  const uint32_t g = (v >> 8) & 255;
+  return (v & 0xff00ff00u) | ((((v >> 16) - g) & 255) << 16) | (((v & 255) - g) & 255);
 }
 
-__device__ __forceinline__ int clamp8(int v) { return v < -128 ? -128 : v > 127 ? 127 : v; }
+__device__ __forceinline__ int s8(int v) { return (int)(int8_t)(uint8_t)v; }
+__device__ __forceinline__ int ctd(int t, int c) { return (t * s8(c)) >> 5; }
 
 // block-wide sums through LDS atomics (T threads, wave reductions first)
 template <typename V>
@@ -129,31 +124,120 @@ __device__ __forceinline__ V wave_sum(V v) {
 
 // ------------------------------------------------------------------ L1
 
-// bits of |v| for the signed 8-bit view of each residual byte, summed over
-// the bytes of a pixel (model: bitlen) -- the search cost, pure VALU
-__device__ __forceinline__ int bitlen8(int b) { return 32 - __clz(abs(s8(b))); }
-__device__ __forceinline__ int pixel_bits(uint32_t r) {
-  return bitlen8(ch(r, 0)) + bitlen8(ch(r, 8)) + bitlen8(ch(r, 16)) + bitlen8(ch(r, 24));
+// Entropy-scored transform search (model: choose_predictors /
+// choose_cross_color, oracle/vp8l_model.py): every candidate is scored by
+//   cost = 16 * sum_i t_i SP[i] - sum_{i: t_i > 0} [slog(t_i) + slog(t_i + G_i) - slog(G_i)]
+// (1/4096 bit) over the tile's residual histograms t against the frame's
+// accumulated histograms G (L0's residuals against the raster predecessor).
+// SP: PredictionCostSpatial (src/enc/predictor_enc.c:35-46) per value.
+__constant__ int8_t kSpPred[16] = {-26, -24, -14, -9, -5, -3, -2, -1, -1, 0, 0, 0, 0, 0, 0, 0};
+__constant__ int8_t kSpCC[16] = {-77, -61, -37, -22, -13, -8, -5, -3, -2, -1, -1, 0, 0, 0, 0, 0};
+__device__ __forceinline__ int sp_of(const int8_t* tab, int v) {
+  const int k = v < 128 ? v : 256 - v;   // symmetric in +-k
+  return k < 16 ? tab[k] : 0;
 }
+
+#define CC_ZERO_BONUS (3ll << 12)
+#define L1_TILES 4   // transform tiles per workgroup (the per-frame setup is shared)
 
 template <int T>
 struct TransformSmem {
   uint32_t src[(T + 1) * (T + 2)];   // rows y0-1.., cols x0-1..x0+tw
   uint32_t first[T];                 // P(0, y) for the right-edge TR wrap
-  uint32_t res[T * T];
-  int score[16];
-  long long sums[4];
+  union {
+    uint32_t h14[14 * 4 * 128];      // predictor search: 14 modes x 4 channels, u16 counts
+    struct {
+      uint32_t res[T * T];           // the chosen predictor's residuals
+      uint32_t h9[9 * 128];          // colour search: up to 9 candidates, u16 counts
+    } cc;
+  } u;
+  long long slogg[4][256];           // slog(G) per channel and value
+  uint32_t g[4][256];                // the frame's accumulated histograms (A, R, G, B)
+  int32_t frac[1024];                // log2 fraction table (model: FLOG2_FRAC)
+  long long cost[16];
   int best;
 };
 
+// v * log2(v) in 1/4096 bit, 0 for v <= 1 (model: slog2_fx)
+__device__ __forceinline__ long long slog_fx(const int32_t* frac, uint32_t v) {
+  if (v <= 1) return 0;
+  const int e = 31 - __clz((int)v);
+  const uint32_t m = (e >= 10 ? (v >> (e - 10)) : (v << (10 - e))) & 1023;
+  return (long long)v * (((long long)e << 12) + frac[m]);
+}
+
+// block-wide sums of K int64 values into S.cost[0..K) (zeroed by the caller)
+template <int K, int T>
+__device__ __forceinline__ void reduce_costs(TransformSmem<T>& S, const long long (&v)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const long long w = wave_sum(v[k]);
+    if (lane_id() == 0) atomicAdd((unsigned long long*)&S.cost[k], (unsigned long long)w);
+  }
+}
+
+// The bin side of one candidate evaluation: thread b owns value b of each of
+// the K histograms (u16 pairs in h) against channel c of G.
+template <int K, int T>
+__device__ __forceinline__ void bin_costs(TransformSmem<T>& S, const uint32_t* h, int c,
+                                          const int8_t* sp, long long (&acc)[K]) {
+  const int b = threadIdx.x;   // 256 threads = 256 values
+  const uint32_t gv = S.g[c][b];
+  const long long sg = S.slogg[c][b];
+  const int spv = sp_of(sp, b);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const uint32_t t = (h[k * 128 + (b >> 1)] >> ((b & 1) * 16)) & 0xffffu;
+    if (t) acc[k] += 16ll * (long long)t * spv - (slog_fx(S.frac, t) + slog_fx(S.frac, t + gv) - sg);
+  }
+}
+
+__device__ __forceinline__ void hist_add(uint32_t* h, int v) {
+  atomicAdd(&h[v >> 1], 1u << ((v & 1) * 16));
+}
+
+// one colour-search step: the cost of each of K multiplier candidates;
+// blue = false: green-to-red (r - ctd(c0, g)); true: blue (b - ctd(c0, g) - ctd(c1, r))
+template <int K, int T, bool BLUE>
+__device__ void cc_eval(TransformSmem<T>& S, int np, const int (&c0)[K], const int (&c1)[K],
+                        long long (&out)[K]) {
+  const int tid = threadIdx.x;
+  for (int i = tid; i < K * 128; i += 256) S.u.cc.h9[i] = 0;
+  if (tid < K) S.cost[tid] = 0;
+  __syncthreads();
+  for (int i = tid; i < np; i += 256) {
+    const uint32_t r = S.u.cc.res[i];
+    const int g = ch(r, 8), rr = ch(r, 16), bb = ch(r, 0);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int v = BLUE ? (bb - ctd(c0[k], g) - ctd(c1[k], rr)) & 255 : (rr - ctd(c0[k], g)) & 255;
+      hist_add(S.u.cc.h9 + k * 128, v);
+    }
+  }
+  __syncthreads();
+  long long acc[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc[k] = 0;
+  bin_costs<K>(S, S.u.cc.h9, BLUE ? 3 : 1, kSpCC, acc);
+  reduce_costs<K>(S, acc);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    out[k] = S.cost[k] - CC_ZERO_BONUS * ((c0[k] == 0) + (BLUE && c1[k] == 0));
+  __syncthreads();   // S.cost is reused by the next step
+}
+
 // SG: the subtract-green instantiation; a launch of each covers every slot,
 // the blocks of slots with the other flag leave at once (a runtime flag
-// costs the spatial search 40 VGPRs and half its occupancy)
+// costs the spatial search registers and occupancy)
 template <int T, bool SG>
 __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restrict__ rgba,
                                                         size_t fstride, int rstride, vp8l_params p,
                                                         const int* __restrict__ fidx,
+                                                        const int* __restrict__ efidx,
                                                         const uint8_t* __restrict__ fmode,
+                                                        const uint32_t* __restrict__ ehist,
+                                                        const int32_t* __restrict__ frac_tab,
                                                         uint32_t* __restrict__ argb_out,
                                                         uint8_t* __restrict__ modes,
                                                         uint32_t* __restrict__ mult,
@@ -161,208 +245,226 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
   __shared__ TransformSmem<T> S;
   const int tid = threadIdx.x, f = blockIdx.z;
   const int W = p.w, H = p.h;
-  const int x0 = blockIdx.x * T, y0 = blockIdx.y * T;
-  const int tw = min(T, W - x0), th = min(T, H - y0);
-  const int sw = tw + 2;   // LDS source row width (cols x0-1 .. x0+tw)
   const uint8_t* img = rgba + (size_t)(fidx ? fidx[f] : f) * fstride;
-  const int tiles_x = (W + T - 1) / T;
-  const int tile = blockIdx.y * tiles_x + blockIdx.x;
+  const int tiles_x = (W + T - 1) / T, tiles_y = (H + T - 1) / T, ntt = tiles_x * tiles_y;
   const int emode = fmode ? (int)fmode[f] : VP8L_MODE_SPATIAL;
   constexpr bool subgreen = SG;
   if (((emode & VP8L_MODE_SUBGREEN) != 0) != SG) return;
+  const int tile0 = blockIdx.x * L1_TILES;
 
   if (!(emode & VP8L_MODE_SPATIAL)) {   // direct / subtract green only: no predictor
     bool any_alpha = false;
     uint32_t* out = argb_out + (size_t)f * W * H;
-    for (int i = tid; i < tw * th; i += 256) {
-      const int ly = i / tw, lx = i - ly * tw;
-      uint32_t v;
-      if (p.alpha) {   // ALPH: the alpha plane as green
-        const uint32_t g = img[(size_t)(y0 + ly) * rstride + x0 + lx];
-        v = subgreen ? (((0u - g) & 255) << 16) | (g << 8) | ((0u - g) & 255) : g << 8;
-      } else {
-        const uint8_t* q = img + (size_t)(y0 + ly) * rstride + 4 * (x0 + lx);
-        const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
-        any_alpha |= a != 255;
-        v = subgreen ? (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255)
-                     : (a << 24) | (r << 16) | (g << 8) | b;
+    for (int tile = tile0; tile < min(tile0 + L1_TILES, ntt); ++tile) {
+      const int x0 = (tile % tiles_x) * T, y0 = (tile / tiles_x) * T;
+      const int tw = min(T, W - x0), th = min(T, H - y0);
+      for (int i = tid; i < tw * th; i += 256) {
+        const int ly = i / tw, lx = i - ly * tw;
+        uint32_t v;
+        if (p.alpha) {   // ALPH: the alpha plane as green
+          const uint32_t g = img[(size_t)(y0 + ly) * rstride + x0 + lx];
+          v = subgreen ? (((0u - g) & 255) << 16) | (g << 8) | ((0u - g) & 255) : g << 8;
+        } else {
+          const uint8_t* q = img + (size_t)(y0 + ly) * rstride + 4 * (x0 + lx);
+          const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
+          any_alpha |= a != 255;
+          v = subgreen ? (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255)
+                       : (a << 24) | (r << 16) | (g << 8) | b;
+        }
+        out[(size_t)(y0 + ly) * W + x0 + lx] = v;
       }
-      out[(size_t)(y0 + ly) * W + x0 + lx] = v;
     }
     if (__any(any_alpha) && lane_id() == 0) atomicOr(&alpha_flag[f], 1u);
     return;
   }
 
-  // load sub-green pixels (A, R-G, G, B-G) with a 1-pixel border
-  bool tile_alpha = false;
-  for (int i = tid; i < (th + 1) * sw; i += 256) {
-    const int ly = i / sw, lx = i - ly * sw;
-    const int y = y0 - 1 + ly, x = x0 - 1 + lx;
-    uint32_t v = 0;
-    if (y >= 0 && x >= 0 && x < W) {
-      if (p.alpha) {   // ALPH: the alpha plane as green
-        const uint32_t g = img[(size_t)y * rstride + x];
-        v = subgreen ? (((0u - g) & 255) << 16) | (g << 8) | ((0u - g) & 255) : g << 8;
-      } else {
-        const uint8_t* q = img + (size_t)y * rstride + 4 * x;
-        const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
-        v = subgreen ? (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255)
-                     : (a << 24) | (r << 16) | (g << 8) | b;
-        if (a != 255 && ly > 0 && lx > 0 && lx <= tw) tile_alpha = true;
-      }
-    }
-    S.src[i] = v;
-  }
-  if (x0 + tw == W) {
-    for (int i = tid; i < th; i += 256) {
-      const uint8_t* q = img + (size_t)(y0 + i) * rstride;
-      if (p.alpha) {
-        const uint32_t g = q[0];
-        S.first[i] = subgreen ? (((0u - g) & 255) << 16) | (g << 8) | ((0u - g) & 255) : g << 8;
-      } else {
-        const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
-        S.first[i] = subgreen ? (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255)
-                              : (a << 24) | (r << 16) | (g << 8) | b;
-      }
-    }
-  }
-  if (__any(tile_alpha) && lane_id() == 0) atomicOr(&alpha_flag[f], 1u);
-  if (tid < 16) S.score[tid] = 0;
-  __syncthreads();
-
-  auto at = [&](int lx, int ly) -> uint32_t { return S.src[(ly + 1) * sw + lx + 1]; };
-  auto tr = [&](int lx, int ly) -> uint32_t {   // (y-1)*W + x + 1, linear
-    return (x0 + lx + 1 < W) ? at(lx + 1, ly - 1) : S.first[ly];
-  };
-  const int np = tw * th;
-  // fixed predictors: (0,0) black, row 0 left, column 0 top (lossless.c:219-239)
-  auto fixed_mode = [&](int x, int y) -> int { return y == 0 ? (x == 0 ? 0 : 1) : (x == 0 ? 2 : -1); };
-
-  // cost of each of the 14 predictors over the tile (smallest wins, first on ties)
+  // per-frame setup: the accumulated histograms (L0's predictor-12 residual
+  // histograms of the input frame, plain or sub-green) and their slog, the
+  // log2 fraction table
   {
-    int sc[14];
+    const uint32_t* eh = ehist + (size_t)(efidx ? efidx[f] : f) * VP8L_EHIST;
+    const int hix[4] = {VP8L_EH_ACC + 0, VP8L_EH_ACC + (SG ? 4 : 1), VP8L_EH_ACC + 2,
+                        VP8L_EH_ACC + (SG ? 5 : 3)};
+    for (int i = tid; i < 1024; i += 256) S.frac[i] = frac_tab[i];
+    __syncthreads();
 #pragma unroll
-    for (int m = 0; m < 14; ++m) sc[m] = 0;
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t v = eh[hix[c] * 256 + tid];
+      S.g[c][tid] = v;
+      S.slogg[c][tid] = slog_fx(S.frac, v);
+    }
+  }
+
+  for (int tile = tile0; tile < min(tile0 + L1_TILES, ntt); ++tile) {
+    const int x0 = (tile % tiles_x) * T, y0 = (tile / tiles_x) * T;
+    const int tw = min(T, W - x0), th = min(T, H - y0);
+    const int sw = tw + 2;   // LDS source row width (cols x0-1 .. x0+tw)
+    __syncthreads();         // the previous tile is done with S
+    // load sub-green pixels (A, R-G, G, B-G) with a 1-pixel border
+    bool tile_alpha = false;
+    for (int i = tid; i < (th + 1) * sw; i += 256) {
+      const int ly = i / sw, lx = i - ly * sw;
+      const int y = y0 - 1 + ly, x = x0 - 1 + lx;
+      uint32_t v = 0;
+      if (y >= 0 && x >= 0 && x < W) {
+        if (p.alpha) {   // ALPH: the alpha plane as green
+          const uint32_t g = img[(size_t)y * rstride + x];
+          v = subgreen ? (((0u - g) & 255) << 16) | (g << 8) | ((0u - g) & 255) : g << 8;
+        } else {
+          const uint8_t* q = img + (size_t)y * rstride + 4 * x;
+          const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
+          v = subgreen ? (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255)
+                       : (a << 24) | (r << 16) | (g << 8) | b;
+          if (a != 255 && ly > 0 && lx > 0 && lx <= tw) tile_alpha = true;
+        }
+      }
+      S.src[i] = v;
+    }
+    if (x0 + tw == W) {
+      for (int i = tid; i < th; i += 256) {
+        const uint8_t* q = img + (size_t)(y0 + i) * rstride;
+        if (p.alpha) {
+          const uint32_t g = q[0];
+          S.first[i] = subgreen ? (((0u - g) & 255) << 16) | (g << 8) | ((0u - g) & 255) : g << 8;
+        } else {
+          const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
+          S.first[i] = subgreen ? (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255)
+                                : (a << 24) | (r << 16) | (g << 8) | b;
+        }
+      }
+    }
+    if (__any(tile_alpha) && lane_id() == 0) atomicOr(&alpha_flag[f], 1u);
+    for (int i = tid; i < 14 * 4 * 128; i += 256) S.u.h14[i] = 0;
+    if (tid < 16) S.cost[tid] = 0;
+    __syncthreads();
+
+    auto at = [&](int lx, int ly) -> uint32_t { return S.src[(ly + 1) * sw + lx + 1]; };
+    auto tr = [&](int lx, int ly) -> uint32_t {   // (y-1)*W + x + 1, linear
+      return (x0 + lx + 1 < W) ? at(lx + 1, ly - 1) : S.first[ly];
+    };
+    const int np = tw * th;
+    // fixed predictors: (0,0) black, row 0 left, column 0 top (lossless.c:219-239)
+    auto fixed_mode = [&](int x, int y) -> int { return y == 0 ? (x == 0 ? 0 : 1) : (x == 0 ? 2 : -1); };
+
+    // predictor search (model: choose_predictors): the tile's residual
+    // histograms of all 14 modes at once, then one value per thread
     for (int i = tid; i < np; i += 256) {
       const int ly = i / tw, lx = i - ly * tw;
       const uint32_t P = at(lx, ly), L = at(lx - 1, ly), T_ = at(lx, ly - 1), TL = at(lx - 1, ly - 1);
       const uint32_t TR = tr(lx, ly);
       const int fm = fixed_mode(x0 + lx, y0 + ly);
 #pragma unroll
-      for (int m = 0; m < 14; ++m)
-        sc[m] += pixel_bits(sub_pixels(P, predict(fm >= 0 ? fm : m, L, T_, TL, TR)));
+      for (int m = 0; m < 14; ++m) {
+        const uint32_t r = sub_pixels(P, predict(fm >= 0 ? fm : m, L, T_, TL, TR));
+        uint32_t* h = S.u.h14 + m * 4 * 128;
+        hist_add(h + 0 * 128, (int)(r >> 24));
+        hist_add(h + 1 * 128, ch(r, 16));
+        hist_add(h + 2 * 128, ch(r, 8));
+        hist_add(h + 3 * 128, ch(r, 0));
+      }
     }
+    __syncthreads();
+    {
+      long long acc[14];
 #pragma unroll
-    for (int m = 0; m < 14; ++m) {
-      const int v = wave_sum(sc[m]);
-      if (lane_id() == 0) atomicAdd(&S.score[m], v);
+      for (int m = 0; m < 14; ++m) acc[m] = 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int b = tid;
+        const uint32_t gv = S.g[c][b];
+        const long long sg = S.slogg[c][b];
+        const int spv = sp_of(kSpPred, b);
+#pragma unroll
+        for (int m = 0; m < 14; ++m) {
+          const uint32_t t = (S.u.h14[(m * 4 + c) * 128 + (b >> 1)] >> ((b & 1) * 16)) & 0xffffu;
+          if (t) acc[m] += 16ll * (long long)t * spv - (slog_fx(S.frac, t) + slog_fx(S.frac, t + gv) - sg);
+        }
+      }
+      reduce_costs<14>(S, acc);
     }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    int best = 0;
-    for (int m = 1; m < 14; ++m)
-      if (S.score[m] < S.score[best]) best = m;
-    S.best = best;
-    S.sums[0] = S.sums[1] = S.sums[2] = S.sums[3] = 0;
-  }
-  __syncthreads();
-  const int best = S.best;
-  long long sgg = 0, sgr = 0, sgb = 0;
-  for (int i = tid; i < np; i += 256) {
-    const int ly = i / tw, lx = i - ly * tw;
-    const int fm = fixed_mode(x0 + lx, y0 + ly);
-    const uint32_t r = sub_pixels(at(lx, ly), predict(fm >= 0 ? fm : best, at(lx - 1, ly),
-                                                      at(lx, ly - 1), at(lx - 1, ly - 1), tr(lx, ly)));
-    S.res[i] = r;
-    const int g = s8(ch(r, 8)), rr = s8(ch(r, 16)), bb = s8(ch(r, 0));
-    sgg += g * g; sgr += g * rr; sgb += g * bb;
-  }
-  sgg = wave_sum(sgg); sgr = wave_sum(sgr); sgb = wave_sum(sgb);
-  if (lane_id() == 0) {
-    atomicAdd((unsigned long long*)&S.sums[0], (unsigned long long)sgg);
-    atomicAdd((unsigned long long*)&S.sums[1], (unsigned long long)sgr);
-    atomicAdd((unsigned long long*)&S.sums[2], (unsigned long long)sgb);
-  }
-  __syncthreads();
-  // cross colour (model: choose_cross_color): three rounds, each the best of
-  // 6 candidates {0, ls-2 .. ls+2} by the bitlen cost
-  int g2r = 0, g2b = 0, r2b = 0;
-  for (int round = 0; round < 3; ++round) {
-    long long sxy, sxx;
-    if (round == 0) { sxy = S.sums[1]; sxx = S.sums[0]; }
-    else if (round == 1) { sxy = S.sums[2]; sxx = S.sums[0]; }
-    else { sxy = S.sums[3]; sxx = S.sums[2]; }   // r2b sums, computed in round 1
-    const int ls = ls_multiplier(sxy, sxx);
-    int cand[6];
-    cand[0] = 0;
-#pragma unroll
-    for (int c = 1; c < 6; ++c) cand[c] = clamp8(ls + c - 3);
-    int cs[6] = {0, 0, 0, 0, 0, 0};
+    __syncthreads();
+    if (tid == 0) {
+      int best = 0;
+      for (int m = 1; m < 14; ++m)
+        if (S.cost[m] < S.cost[best]) best = m;
+      S.best = best;
+    }
+    __syncthreads();
+    const int best = S.best;
     for (int i = tid; i < np; i += 256) {
-      const uint32_t r = S.res[i];
+      const int ly = i / tw, lx = i - ly * tw;
+      const int fm = fixed_mode(x0 + lx, y0 + ly);
+      S.u.cc.res[i] = sub_pixels(at(lx, ly), predict(fm >= 0 ? fm : best, at(lx - 1, ly),
+                                                     at(lx, ly - 1), at(lx - 1, ly - 1), tr(lx, ly)));
+    }
+    // colour search (model: choose_cross_color)
+    int g2r = 0, g2b = 0, r2b = 0;
+    {
+      long long bestc;
+      {   // start (0) and the first +-32 step in one evaluation
+        const int c0[3] = {0, -32, 32}, c1[3] = {0, 0, 0};
+        long long v[3];
+        cc_eval<3, T, false>(S, np, c0, c1, v);
+        bestc = v[0];
+        const int k = v[2] < v[1] ? 2 : 1;
+        if (v[k] < bestc) { bestc = v[k]; g2r = c0[k]; }
+      }
+      for (int d = 16; d >= 1; d >>= 1) {
+        const int c0[2] = {g2r - d, g2r + d}, c1[2] = {0, 0};
+        long long v[2];
+        cc_eval<2, T, false>(S, np, c0, c1, v);
+        const int k = v[1] < v[0] ? 1 : 0;
+        if (v[k] < bestc) { bestc = v[k]; g2r = c0[k]; }
+      }
+    }
+    {
+      const int ax0[8] = {0, 0, -1, 1, -1, -1, 1, 1}, ax1[8] = {-1, 1, 0, 0, -1, 1, -1, 1};
+      const int deltas[7] = {16, 16, 8, 4, 2, 2, 2};
+      long long bestc;
+      {   // start (0, 0) and the first delta-16 step in one evaluation
+        int c0[9], c1[9];
+        c0[0] = 0; c1[0] = 0;
+#pragma unroll
+        for (int a = 0; a < 8; ++a) { c0[a + 1] = ax0[a] * 16; c1[a + 1] = ax1[a] * 16; }
+        long long v[9];
+        cc_eval<9, T, true>(S, np, c0, c1, v);
+        bestc = v[0];
+        int k = 1;
+#pragma unroll
+        for (int a = 2; a < 9; ++a)
+          if (v[a] < v[k]) k = a;
+        if (v[k] < bestc) { bestc = v[k]; g2b = c0[k]; r2b = c1[k]; }
+      }
+      for (int it = 1; it < 7; ++it) {
+        const int d = deltas[it];
+        int c0[8], c1[8];
+#pragma unroll
+        for (int a = 0; a < 8; ++a) { c0[a] = g2b + ax0[a] * d; c1[a] = r2b + ax1[a] * d; }
+        long long v[8];
+        cc_eval<8, T, true>(S, np, c0, c1, v);
+        int k = 0;
+#pragma unroll
+        for (int a = 1; a < 8; ++a)
+          if (v[a] < v[k]) k = a;
+        if (v[k] < bestc) { bestc = v[k]; g2b = c0[k]; r2b = c1[k]; }
+        if (d == 2 && g2b == 0 && r2b == 0) break;
+      }
+    }
+    // final residuals
+    uint32_t* out = argb_out + (size_t)f * W * H;
+    for (int i = tid; i < np; i += 256) {
+      const int ly = i / tw, lx = i - ly * tw;
+      const uint32_t r = S.u.cc.res[i];
       const int g = ch(r, 8), rr = ch(r, 16), bb = ch(r, 0);
-#pragma unroll
-      for (int c = 0; c < 6; ++c) {
-        int v;
-        if (round == 0) v = rr - ctd(cand[c], g);
-        else if (round == 1) v = bb - ctd(cand[c], g);
-        else v = (bb - ctd(g2b, g)) - ctd(cand[c], rr);
-        cs[c] += bitlen8(v & 255);
-      }
+      const int nr = (rr - ctd(g2r, g)) & 255;
+      const int nb = (bb - ctd(g2b, g) - ctd(r2b, rr)) & 255;
+      out[(size_t)(y0 + ly) * W + x0 + lx] = (r & 0xff00ff00u) | ((uint32_t)nr << 16) | (uint32_t)nb;
     }
-    __syncthreads();   // everyone has read S.score / S.sums of the previous step
-    if (tid < 6) S.score[tid] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < 6; ++c) {
-      const int v = wave_sum(cs[c]);
-      if (lane_id() == 0) atomicAdd(&S.score[c], v);
+    if (tid == 0) {
+      modes[(size_t)f * ntt + tile] = (uint8_t)best;
+      mult[(size_t)f * ntt + tile] =
+          (uint32_t)(g2r & 255) | ((uint32_t)(g2b & 255) << 8) | ((uint32_t)(r2b & 255) << 16);
     }
-    __syncthreads();
-    int bc = 0;
-    for (int c = 1; c < 6; ++c)
-      if (S.score[c] < S.score[bc]) bc = c;
-    const int chosen = cand[bc];
-    if (round == 0) g2r = chosen;
-    else if (round == 1) {
-      g2b = chosen;
-      // sums for r2b: srr = sum r^2, srb = sum r * s8(b - ctd(g2b, g))
-      long long srr = 0, srb = 0;
-      for (int i = tid; i < np; i += 256) {
-        const uint32_t r = S.res[i];
-        const int rr = s8(ch(r, 16));
-        const int bq = s8((ch(r, 0) - ctd(g2b, ch(r, 8))) & 255);
-        srr += rr * rr; srb += rr * bq;
-      }
-      srr = wave_sum(srr); srb = wave_sum(srb);
-      __syncthreads();
-      if (tid == 0) { S.sums[2] = 0; S.sums[3] = 0; }
-      __syncthreads();
-      if (lane_id() == 0) {
-        atomicAdd((unsigned long long*)&S.sums[2], (unsigned long long)srr);
-        atomicAdd((unsigned long long*)&S.sums[3], (unsigned long long)srb);
-      }
-    } else {
-      r2b = chosen;
-    }
-    __syncthreads();
-  }
-  // final residuals
-  uint32_t* out = argb_out + (size_t)f * W * H;
-  for (int i = tid; i < np; i += 256) {
-    const int ly = i / tw, lx = i - ly * tw;
-    const uint32_t r = S.res[i];
-    const int g = ch(r, 8), rr = ch(r, 16), bb = ch(r, 0);
-    const int nr = (rr - ctd(g2r, g)) & 255;
-    const int nb = (bb - ctd(g2b, g) - ctd(r2b, rr)) & 255;
-    out[(size_t)(y0 + ly) * W + x0 + lx] = (r & 0xff00ff00u) | ((uint32_t)nr << 16) | (uint32_t)nb;
-  }
-  if (tid == 0) {
-    const int ntt = tiles_x * ((H + T - 1) / T);
-    modes[(size_t)f * ntt + tile] = (uint8_t)best;
-    mult[(size_t)f * ntt + tile] =
-        (uint32_t)(g2r & 255) | ((uint32_t)(g2b & 255) << 8) | ((uint32_t)(r2b & 255) << 16);
   }
 }
 
@@ -417,6 +519,22 @@ __global__ __launch_bounds__(256) void k_vp8l_entropy(const uint8_t* __restrict_
     atomicAdd(&h[11 * 256 + (((int)d - gd) & 255)], 1u);
     const uint64_t hp = ((uint64_t)pix + (pix >> 19)) * 0x39c5fba7ull;   // HashPix :81-85
     atomicAdd(&h[12 * 256 + (uint32_t)((hp & 0xffffffffull) >> 24)], 1u);
+    // the transform search's accumulated histograms (model:
+    // accumulated_histograms): residuals of predictor 12, or of the fixed
+    // modes on row 0 (left) and column 0 (top), plain and sub-green
+    const uint32_t T_ = y > 0 ? pix_at(row - rstride, x, plane) : 0u;
+    const uint32_t L = x > 0 ? pix_at(row, x - 1, plane) : 0u;
+    const uint32_t TL = (x > 0 && y > 0) ? pix_at(row - rstride, x - 1, plane) : 0u;
+    const int fm = y == 0 ? 1 : (x == 0 ? 2 : 12);
+    const uint32_t r = sub_pixels(pix, predict(fm, L, T_, TL, 0u));
+    const uint32_t rs = sub_pixels(sub_green(pix), predict(fm, sub_green(L), sub_green(T_),
+                                                          sub_green(TL), 0u));
+    atomicAdd(&h[(VP8L_EH_ACC + 0) * 256 + (r >> 24)], 1u);
+    atomicAdd(&h[(VP8L_EH_ACC + 1) * 256 + ((r >> 16) & 255)], 1u);
+    atomicAdd(&h[(VP8L_EH_ACC + 2) * 256 + ((r >> 8) & 255)], 1u);
+    atomicAdd(&h[(VP8L_EH_ACC + 3) * 256 + (r & 255)], 1u);
+    atomicAdd(&h[(VP8L_EH_ACC + 4) * 256 + ((rs >> 16) & 255)], 1u);
+    atomicAdd(&h[(VP8L_EH_ACC + 5) * 256 + (rs & 255)], 1u);
   }
   __syncthreads();
   uint32_t* out = ehist + (size_t)f * VP8L_EHIST;
@@ -729,7 +847,7 @@ __global__ __launch_bounds__(64) void k_vp8l_parse(vp8l_params p, uint32_t* __re
         const int bn = (int)(m & 0x1fff), bk = (int)((m >> 13) & 3);
         const bool hit = cb > 0 && (m >> 15) <= cb;
         if (bn >= VP8L_MIN_COPY || (bn == 2 && !hit)) {
-          tile[ln][i] = final_pass ? 2u | ((uint32_t)bn << 2) | ((uint32_t)p.dcode[bk] << 15)
+          tile[ln][i] = final_pass ? 2u | ((uint32_t)(bn - 1) << 2) | ((uint32_t)p.dcode[bk] << 14)
                                    : 2u | ((uint32_t)(bn - 1) << 2);
           const int e = min(x + bn, cx + cw);
           for (int j = i + 1; j < e - cx; ++j) tile[ln][j] = 3u;
@@ -785,9 +903,9 @@ __device__ __forceinline__ void pix_symbols(uint32_t op, uint32_t a, int cb, Pix
     o.s[0] = 280 + (int)((a * HASH_MUL) >> (32 - cb));
   } else if (act == 2) {
     int sym, nb; uint32_t ex;
-    prefix_enc((op >> 2) & 0x1fff, sym, nb, ex);
+    prefix_enc(((op >> 2) & 0xfff) + 1, sym, nb, ex);
     o.s[0] = 256 + sym; o.xv[0] = ex; o.xb[0] = nb;
-    prefix_enc(op >> 15, sym, nb, ex);
+    prefix_enc(op >> 14, sym, nb, ex);
     o.s[1] = VP8L_GS + 768 + sym; o.xv[1] = ex; o.xb[1] = nb;
   }
 }
@@ -815,6 +933,331 @@ __device__ __forceinline__ long long flog2_fx64(const int32_t* frac, unsigned lo
 }
 
 }  // namespace
+
+// ------------------------------------------------------------------ L3p
+// Colour-indexed frames: the cost-model parse over long-range matches
+// (model: palette_parse and the lz_* functions, oracle/vp8l_model.py; the
+// reference's VP8LHashChainFill, backward_references_enc.c:259-452, and
+// TraceBackwards, backward_references_cost_enc.c:569-795).
+
+#define LZ_SEG 4096
+#define LZ_MAX_LENGTH 4095
+#define LZ_HASH_SIZE (1 << 18)
+#define LZ_ITER_MAX (8 + (75 * 75) / 128)
+#define LZ_WINDOW_CAP ((1 << 18) - 121)
+#define LZ_NCOST (280 + 3 * 256 + 40)   // G+length | R | B | A | D
+#define LZ_INF 0x7fffffff
+
+__device__ __forceinline__ uint32_t lz_hash(uint32_t a, uint32_t b) {
+  return (b * 0xc6a4a793u + a * 0x5bd1e996u) >> (32 - 18);
+}
+
+// R[q] = equal pixels starting at q, capped at LZ_MAX_LENGTH + 3 (model:
+// lz_runs): one wave per frame, 64-pixel chunks from the end, a run reaching
+// a chunk's end continues with the next chunk's first run.
+__global__ __launch_bounds__(64) void k_lz_runs(const uint32_t* __restrict__ argb, int npix,
+                                                uint16_t* __restrict__ runs) {
+  const int f = blockIdx.x, ln = lane_id();
+  const uint32_t* E = argb + (size_t)f * npix;
+  uint16_t* R = runs + (size_t)f * npix;
+  int carry = 0;   // run at the first position of the chunk after this one
+  for (int c = (npix - 1) >> 6; c >= 0; --c) {
+    const int q = (c << 6) + ln;
+    const bool valid = q < npix;
+    const bool eq = valid && q + 1 < npix && E[q] == E[q + 1];
+    const uint64_t mask = __ballot(eq);
+    const uint64_t miss = ~(mask >> ln);
+    int run = (miss ? (int)__builtin_ctzll(miss) : 64) + 1;   // this pixel + equal followers
+    if (run == 65 - ln) run += carry - 1 >= 0 ? carry - 1 : 0;
+    if (run > LZ_MAX_LENGTH + 3) run = LZ_MAX_LENGTH + 3;
+    if (valid) R[q] = (uint16_t)run;
+    carry = __shfl(run, 0);
+  }
+}
+
+// The hash chain (model: lz_hash_chain): one wave per frame walks the
+// positions 64 at a time; the lanes sharing a hash come from 18 ballots, a
+// lane's link is its nearest lower inserting lane of the same hash, else the
+// table entry, and the highest inserting lane of each hash updates the table
+// (n x 2^18 words in HBM, -1 filled by the caller).
+__global__ __launch_bounds__(64) void k_lz_chain(const uint32_t* __restrict__ argb, int npix,
+                                                 const uint16_t* __restrict__ runs,
+                                                 int32_t* __restrict__ htab,
+                                                 int32_t* __restrict__ chain) {
+  const int f = blockIdx.x, ln = lane_id();
+  const uint32_t* E = argb + (size_t)f * npix;
+  const uint16_t* R = runs + (size_t)f * npix;
+  int32_t* T = htab + (size_t)f * LZ_HASH_SIZE;
+  int32_t* C = chain + (size_t)f * npix;
+  const uint64_t below = (1ull << ln) - 1ull;
+  for (int c = 0; c < (npix + 63) >> 6; ++c) {
+    const int q = (c << 6) + ln;
+    const bool look0 = q <= npix - 2 && npix > 2;
+    uint32_t key = 0;
+    bool skip = false;
+    if (look0) {
+      const int r = R[q];
+      if (r >= 3) {
+        skip = r - 2 > LZ_MAX_LENGTH;
+        key = lz_hash(E[q], (uint32_t)(r - 2));
+      } else {
+        key = lz_hash(E[q], E[q + 1]);
+      }
+    }
+    const bool look = look0 && !skip;
+    const bool ins = look && q <= npix - 3;
+    uint64_t acc = __ballot(ins);
+#pragma unroll
+    for (int b = 17; b >= 0; --b) {
+      const bool bit = (key >> b) & 1;
+      const uint64_t bv = __ballot(ins && bit);
+      acc &= bit ? bv : ~bv;
+    }
+    const uint64_t lower = acc & below;
+    int32_t link = -1;
+    if (look)
+      link = lower ? (c << 6) + (63 - __clzll((long long)lower))
+                   : __hip_atomic_load(&T[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (q < npix) C[q] = look ? link : -1;
+    // every lane has read the table above before the writes below (one wave,
+    // program order; the loads are waited for by the link store); table
+    // reads and writes go to L2 (agent scope), so the next chunk's reads see
+    // this chunk's writes
+    if (ins && (acc >> ln) == 1ull)
+      __hip_atomic_store(&T[key], (int32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Per position the chain's best match (model: lz_hash_search): one thread
+// per position.
+__global__ __launch_bounds__(256) void k_lz_search(const uint32_t* __restrict__ argb, int W,
+                                                   int npix, const int32_t* __restrict__ chain,
+                                                   uint32_t* __restrict__ hoff,
+                                                   uint16_t* __restrict__ hlen) {
+  const int f = blockIdx.y;
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= npix) return;
+  const uint32_t* E = argb + (size_t)f * npix;
+  const int32_t* C = chain + (size_t)f * npix;
+  uint32_t bd = 0;
+  int bl = 0;
+  if (p >= 1 && p <= npix - 2) {
+    const int seg_end = (p / LZ_SEG + 1) * LZ_SEG;
+    const int max_len = min(min(npix - 1 - p, LZ_MAX_LENGTH), seg_end - p);
+    auto mlen = [&](int a) {
+      int k = 0;
+      while (k < max_len && E[a + k] == E[p + k]) ++k;
+      return k;
+    };
+    const int window = min(W << 8, LZ_WINDOW_CAP);
+    const int min_pos = max(p - window, 0);
+    const int length_max = min(max_len, 256);
+    int it = LZ_ITER_MAX;
+    int q = C[p];
+    if (p >= W) {
+      const int c = mlen(p - W);
+      if (c > bl) { bl = c; bd = (uint32_t)W; }
+      --it;
+    }
+    {
+      const int c = mlen(p - 1);
+      if (c > bl) { bl = c; bd = 1; }
+      --it;
+    }
+    if (bl == LZ_MAX_LENGTH) q = min_pos - 1;
+    while (q >= min_pos) {
+      if (--it == 0) break;
+      if (E[q + bl] == E[p + bl]) {
+        const int c = mlen(q);
+        if (c > bl) {
+          bl = c; bd = (uint32_t)(p - q);
+          if (bl >= length_max) break;
+        }
+      }
+      q = C[q];
+    }
+  }
+  hoff[(size_t)f * npix + p] = bd;
+  hlen[(size_t)f * npix + p] = (uint16_t)bl;
+}
+
+// Per position the longest run against the 4 candidate distances within its
+// segment (model: lz_local): one wave per segment, 64-pixel chunks from the
+// segment end, ballots as in k_vp8l_match.
+__global__ __launch_bounds__(64) void k_lz_local(const uint32_t* __restrict__ argb, vp8l_params p,
+                                                 uint32_t* __restrict__ loff,
+                                                 uint16_t* __restrict__ llen) {
+  const int f = blockIdx.y, ln = lane_id();
+  const int npix = p.w * p.h;
+  const int s = blockIdx.x * LZ_SEG, e = min(npix, s + LZ_SEG);
+  const uint32_t* E = argb + (size_t)f * npix;
+  int carry[VP8L_NUM_CAND] = {0, 0, 0, 0};
+  const int nch = (e - s + 63) >> 6;
+  for (int c = nch - 1; c >= 0; --c) {
+    const int q = s + (c << 6) + ln;
+    const bool valid = q < e;
+    const uint32_t v = valid ? E[q] : 0u;
+    int bn = 0, bk = 0;
+#pragma unroll
+    for (int k = 0; k < VP8L_NUM_CAND; ++k) {
+      const int d = p.dist[k];
+      const bool ok = valid && d > 0 && d <= q && E[q - d] == v;
+      const uint64_t mask = __ballot(ok);
+      const uint64_t miss = ~(mask >> ln);
+      int run = miss ? (int)__builtin_ctzll(miss) : 64;
+      if (run == 64 - ln) run += carry[k];
+      carry[k] = __shfl(run, 0);
+      const int n = min(run, LZ_MAX_LENGTH);
+      if (n > bn) { bn = n; bk = k; }
+    }
+    if (valid) {
+      loff[(size_t)f * npix + q] = bn ? (uint32_t)p.dist[bk] : 0u;
+      llen[(size_t)f * npix + q] = (uint16_t)bn;
+    }
+  }
+}
+
+// Symbol costs of a frame's parse (model: lz_costs / lz_pop_costs): one
+// workgroup per frame, histograms in LDS, 1/256 bit per symbol.
+__global__ __launch_bounds__(1024) void k_lz_costs(const uint32_t* __restrict__ argb,
+                                                   const uint32_t* __restrict__ ops, int npix,
+                                                   const int32_t* __restrict__ frac,
+                                                   int32_t* __restrict__ costs) {
+  __shared__ uint32_t h[LZ_NCOST];
+  __shared__ uint32_t tot[5], nz[5];
+  const int f = blockIdx.x, tid = threadIdx.x;
+  const uint32_t* E = argb + (size_t)f * npix;
+  const uint32_t* O = ops + (size_t)f * npix;
+  for (int i = tid; i < LZ_NCOST; i += 1024) h[i] = 0;
+  if (tid < 5) { tot[tid] = 0; nz[tid] = 0; }
+  __syncthreads();
+  for (int q = tid; q < npix; q += 1024) {
+    const uint32_t op = O[q], act = op & 3;
+    if (act == 0) {
+      const uint32_t a = E[q];
+      atomicAdd(&h[(a >> 8) & 255], 1u);
+      atomicAdd(&h[280 + ((a >> 16) & 255)], 1u);
+      atomicAdd(&h[536 + (a & 255)], 1u);
+      atomicAdd(&h[792 + (a >> 24)], 1u);
+    } else if (act == 2) {
+      int sym, nb; uint32_t ex;
+      prefix_enc(((op >> 2) & 0xfff) + 1, sym, nb, ex);
+      atomicAdd(&h[256 + sym], 1u);
+      prefix_enc(op >> 14, sym, nb, ex);
+      atomicAdd(&h[1048 + sym], 1u);
+    }
+  }
+  __syncthreads();
+  auto alph = [](int i) { return i < 280 ? 0 : i < 536 ? 1 : i < 792 ? 2 : i < 1048 ? 3 : 4; };
+  for (int i = tid; i < LZ_NCOST; i += 1024)
+    if (h[i]) { atomicAdd(&tot[alph(i)], h[i]); atomicAdd(&nz[alph(i)], 1u); }
+  __syncthreads();
+  int32_t* out = costs + (size_t)f * LZ_NCOST;
+  for (int i = tid; i < LZ_NCOST; i += 1024) {
+    const int a = alph(i);
+    int32_t c = 0;
+    if (nz[a] > 1)
+      c = (flog2_fx(frac, tot[a]) - (h[i] ? flog2_fx(frac, h[i]) : 0)) >> 4;
+    out[i] = c;
+  }
+}
+
+// VP8L distance code of a distance (model: distance_code): the plane code
+// table of the frame width for short distances (dcodes[d], 0 = none), else
+// d + 120
+__device__ __forceinline__ uint32_t lz_dcode(const uint8_t* dcodes, int nd, uint32_t d) {
+  const uint32_t c = d < (uint32_t)nd ? dcodes[d] : 0u;
+  return c ? c : d + 120;
+}
+
+// The cost-model parse of one segment (model: lz_dp): one wave per segment,
+// the path costs / choices in LDS; per position the literal (lane 0), then
+// the chain match and then the local match, each with one lane per length of
+// LZ_LENGTHS (and one for the match's own length). Lanes of one match write
+// distinct targets; the matches run one after the other (one wave: LDS ops
+// in program order). Then lane 0 walks the choices back and the wave writes
+// the segment's ops.
+__constant__ int16_t kLzLengths[32] = {2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17,
+                                       32, 33, 64, 65, 128, 129, 256, 257, 512, 513, 1024,
+                                       1025, 2048, 2049, 0, 0};
+#define LZ_NLEN 30
+struct LzSmem {
+  int32_t cost[LZ_SEG + 1];
+  uint16_t ch[LZ_SEG + 1];
+  uint32_t dd[LZ_SEG + 1];
+  int32_t tab[LZ_NCOST];
+};
+__global__ __launch_bounds__(64) void k_lz_dp(const uint32_t* __restrict__ argb, int W, int npix,
+                                              const int32_t* __restrict__ costs,
+                                              const uint32_t* __restrict__ hoff,
+                                              const uint16_t* __restrict__ hlen,
+                                              const uint32_t* __restrict__ loff,
+                                              const uint16_t* __restrict__ llen,
+                                              const uint8_t* __restrict__ dcodes, int nd,
+                                              uint32_t* __restrict__ ops) {
+  __shared__ LzSmem S;
+  const int f = blockIdx.y, ln = lane_id();
+  const int s = blockIdx.x * LZ_SEG, e = min(npix, s + LZ_SEG), m = e - s;
+  const uint32_t* E = argb + (size_t)f * npix;
+  const size_t base = (size_t)f * npix;
+  for (int i = ln; i < LZ_NCOST; i += 64) S.tab[i] = costs[(size_t)f * LZ_NCOST + i];
+  for (int i = ln; i <= m; i += 64) { S.cost[i] = i ? LZ_INF : 0; S.ch[i] = 0; S.dd[i] = 0; }
+  __syncthreads();
+  const int32_t* cG = S.tab;
+  const int32_t* cR = S.tab + 280;
+  const int32_t* cB = S.tab + 536;
+  const int32_t* cA = S.tab + 792;
+  const int32_t* cD = S.tab + 1048;
+  const int myk = ln < LZ_NLEN ? kLzLengths[ln] : 0;
+  for (int j = 0; j < m; ++j) {
+    const int i = s + j;
+    const int c = S.cost[j];
+    if (ln == 0) {
+      const uint32_t a = E[i];
+      const int v = c + ((cA[a >> 24] + cR[(a >> 16) & 255] + cG[(a >> 8) & 255] + cB[a & 255]) *
+                         82) / 100;
+      if (v < S.cost[j + 1]) { S.cost[j + 1] = v; S.ch[j + 1] = 1; }
+    }
+#pragma unroll
+    for (int mk = 0; mk < 2; ++mk) {
+      const uint32_t d = mk == 0 ? hoff[base + i] : loff[base + i];
+      const int L = min((int)(mk == 0 ? hlen[base + i] : llen[base + i]), e - i);
+      if (L < 2) continue;   // wave-uniform
+      int sym, nb; uint32_t ex;
+      prefix_enc(lz_dcode(dcodes, nd, d), sym, nb, ex);
+      const int dc = c + cD[sym] + 256 * nb;
+      // lane LZ_NLEN takes the match's own length when it is not in the list
+      bool own_listed = false;
+#pragma unroll
+      for (int t = 0; t < LZ_NLEN; ++t) own_listed |= kLzLengths[t] == L;
+      const int k = ln < LZ_NLEN ? myk : (ln == LZ_NLEN && !own_listed ? L : 0);
+      if (k >= 2 && k <= L) {
+        prefix_enc((uint32_t)k, sym, nb, ex);
+        const int v = dc + cG[256 + sym] + 256 * nb;
+        if (v < S.cost[j + k]) { S.cost[j + k] = v; S.ch[j + k] = (uint16_t)k; S.dd[j + k] = d; }
+      }
+    }
+  }
+  __syncthreads();
+  // trace back: mark copy starts (ch value at the start position: 2 | k << 2
+  // with the code), the rest literal or inside
+  if (ln == 0) {
+    int j = m;
+    while (j > 0) {
+      const int k = S.ch[j];
+      const int st = j - k;
+      if (k >= 2) {
+        S.cost[st] = (int32_t)(2u | ((uint32_t)(k - 1) << 2) | (lz_dcode(dcodes, nd, S.dd[j]) << 14));
+        for (int t = st + 1; t < j; ++t) S.cost[t] = 3;
+      } else {
+        S.cost[st] = 0;
+      }
+      j = st;
+    }
+  }
+  __syncthreads();
+  for (int i = ln; i < m; i += 64) ops[base + s + i] = (uint32_t)S.cost[i];
+}
 
 // ------------------------------------------------------------------ L3b
 
@@ -1324,17 +1767,21 @@ extern "C" int vp8l_launch_scan(const uint8_t* rgba, size_t fstride, int rstride
 }
 
 extern "C" int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rstride,
-                                     const vp8l_params* p, const int* fidx, const uint8_t* fmode,
-                                     int sg_mask, uint32_t* argb, uint8_t* modes, uint32_t* mult,
-                                     uint32_t* alpha_flag, void* stream) {
+                                     const vp8l_params* p, const int* fidx, const int* efidx,
+                                     const uint8_t* fmode, const uint32_t* ehist,
+                                     const int32_t* tabs, int sg_mask, uint32_t* argb,
+                                     uint8_t* modes, uint32_t* mult, uint32_t* alpha_flag,
+                                     void* stream) {
   if (p->tb < 2 || p->tb > 6 || p->w <= 0 || p->h <= 0 || p->n <= 0) return 0;
   if (!p->alpha && !fmode) return 0;
   if (!fmode) sg_mask = 1;
-  dim3 grid((p->w + (1 << p->tb) - 1) >> p->tb, (p->h + (1 << p->tb) - 1) >> p->tb, p->n);
+  const int ntt = ((p->w + (1 << p->tb) - 1) >> p->tb) * ((p->h + (1 << p->tb) - 1) >> p->tb);
+  dim3 grid((ntt + L1_TILES - 1) / L1_TILES, 1, p->n);
   hipStream_t st = (hipStream_t)stream;
+  const int32_t* frac = tabs + 4097;
 #define L1(T, SG)                                                                             \
   hipLaunchKernelGGL((k_vp8l_transform<T, SG>), grid, dim3(256), 0, st, rgba, fstride, rstride, \
-                     *p, fidx, fmode, argb, modes, mult, alpha_flag)
+                     *p, fidx, efidx, fmode, ehist, frac, argb, modes, mult, alpha_flag)
   for (int sg = 0; sg < 2; ++sg) {
     if (!((sg_mask >> sg) & 1)) continue;
     switch (p->tb) {
@@ -1388,31 +1835,58 @@ extern "C" int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
                                    const int32_t* tabs, uint8_t* minb, uint16_t* prov,
                                    uint32_t* chist, uint8_t* cbits, uint32_t* ops, int64_t* feat,
                                    uint32_t* tl, uint32_t* tn, uint32_t* hc, uint8_t* assign,
-                                   void* stream) {
+                                   const vp8l_lz* lz, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int npix = p->w * p->h;
   const int32_t* flog2 = tabs + 4097;
   const int tx_n = (p->w + (1 << p->hb) - 1) >> p->hb, ty_n = (p->h + (1 << p->hb) - 1) >> p->hb;
   if (tx_n * ty_n > VP8L_MAX_HUFF_IMAGE || p->k < 1 || p->k > VP8L_KMAX) return 0;
   if (p->cache_bits < 0 || p->cache_bits > VP8L_MAX_CACHE_BITS) return 0;
-  if (p->cache_bits) {
-    hipLaunchKernelGGL(k_vp8l_cache, dim3(p->n), dim3(64), 0, st, argb, npix, minb);
-  } else if (hipMemsetAsync(minb, VP8L_NEVER_HIT, (size_t)p->n * npix, st) != hipSuccess) {
-    return 0;
-  }
-  hipLaunchKernelGGL(k_vp8l_match, dim3(p->h, p->n), dim3(64), 0, st, argb, minb, *p, ops);
-  if (p->cache_bits) {
+  if (lz) {   // colour-indexed: cost-model parse (model: palette_parse), no cache
+    if (hipMemsetAsync(minb, VP8L_NEVER_HIT, (size_t)p->n * npix, st) != hipSuccess ||
+        hipMemsetAsync(cbits, 0, (size_t)p->n, st) != hipSuccess ||
+        hipMemsetAsync(lz->htab, 0xff, (size_t)p->n * LZ_HASH_SIZE * sizeof(int32_t), st) !=
+            hipSuccess)
+      return 0;
+    const int nseg = (npix + LZ_SEG - 1) / LZ_SEG;
+    hipLaunchKernelGGL(k_vp8l_match, dim3(p->h, p->n), dim3(64), 0, st, argb, minb, *p, ops);
     hipLaunchKernelGGL(k_vp8l_parse, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, *p, ops, prov,
-                       (const uint8_t*)nullptr);   // provisional
-    hipLaunchKernelGGL(k_vp8l_cachehist, dim3(p->n), dim3(1024), VP8L_CHIST * sizeof(uint32_t), st,
-                       argb, (const uint32_t*)ops, prov, npix, chist);
-    hipLaunchKernelGGL(k_vp8l_cachechoose, dim3(p->n), dim3(256), 0, st, chist, flog2,
-                       p->cache_bits, cbits);
-  } else if (hipMemsetAsync(cbits, 0, (size_t)p->n, st) != hipSuccess) {
-    return 0;
+                       (const uint8_t*)cbits);   // the greedy parse: first costs
+    hipLaunchKernelGGL(k_lz_runs, dim3(p->n), dim3(64), 0, st, argb, npix, lz->runs);
+    hipLaunchKernelGGL(k_lz_chain, dim3(p->n), dim3(64), 0, st, argb, npix,
+                       (const uint16_t*)lz->runs, lz->htab, lz->chain);
+    hipLaunchKernelGGL(k_lz_search, dim3((npix + 255) / 256, p->n), dim3(256), 0, st, argb, p->w,
+                       npix, (const int32_t*)lz->chain, lz->hoff, lz->hlen);
+    hipLaunchKernelGGL(k_lz_local, dim3(nseg, p->n), dim3(64), 0, st, argb, *p, lz->loff,
+                       lz->llen);
+    for (int round = 0; round < 2; ++round) {
+      hipLaunchKernelGGL(k_lz_costs, dim3(p->n), dim3(1024), 0, st, argb, (const uint32_t*)ops,
+                         npix, flog2, lz->costs);
+      hipLaunchKernelGGL(k_lz_dp, dim3(nseg, p->n), dim3(64), 0, st, argb, p->w, npix,
+                         (const int32_t*)lz->costs, (const uint32_t*)lz->hoff,
+                         (const uint16_t*)lz->hlen, (const uint32_t*)lz->loff,
+                         (const uint16_t*)lz->llen, lz->dcodes, lz->nd, ops);
+    }
+  } else {
+    if (p->cache_bits) {
+      hipLaunchKernelGGL(k_vp8l_cache, dim3(p->n), dim3(64), 0, st, argb, npix, minb);
+    } else if (hipMemsetAsync(minb, VP8L_NEVER_HIT, (size_t)p->n * npix, st) != hipSuccess) {
+      return 0;
+    }
+    hipLaunchKernelGGL(k_vp8l_match, dim3(p->h, p->n), dim3(64), 0, st, argb, minb, *p, ops);
+    if (p->cache_bits) {
+      hipLaunchKernelGGL(k_vp8l_parse, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, *p, ops,
+                         prov, (const uint8_t*)nullptr);   // provisional
+      hipLaunchKernelGGL(k_vp8l_cachehist, dim3(p->n), dim3(1024), VP8L_CHIST * sizeof(uint32_t),
+                         st, argb, (const uint32_t*)ops, prov, npix, chist);
+      hipLaunchKernelGGL(k_vp8l_cachechoose, dim3(p->n), dim3(256), 0, st, chist, flog2,
+                         p->cache_bits, cbits);
+    } else if (hipMemsetAsync(cbits, 0, (size_t)p->n, st) != hipSuccess) {
+      return 0;
+    }
+    hipLaunchKernelGGL(k_vp8l_parse, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, *p, ops, prov,
+                       (const uint8_t*)cbits);
   }
-  hipLaunchKernelGGL(k_vp8l_parse, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, *p, ops, prov,
-                     (const uint8_t*)cbits);
   hipLaunchKernelGGL(k_vp8l_tilefeat, dim3(tx_n * ty_n, p->n), dim3(256), 0, st, argb, ops, *p,
                      (const uint8_t*)cbits, flog2, feat, tl, tn);
   static int attr = 0;

@@ -58,6 +58,9 @@ void vp8l_engine_free(vp8l_engine* l) {
   hipHostFree(l->h_start); hipHostFree(l->h_end); hipHostFree(l->h_hdr); hipHostFree(l->h_out);
   hipHostFree(l->h_poff); hipHostFree(l->h_hpack); hipHostFree(l->h_hoff); hipHostFree(l->h_hwords);
   free(l->hdr_bytes); free(l->out_off); free(l->out_size); free(l->err);
+  hipFree(l->lz.runs); hipFree(l->lz.htab); hipFree(l->lz.chain); hipFree(l->lz.hoff);
+  hipFree(l->lz.hlen); hipFree(l->lz.loff); hipFree(l->lz.llen); hipFree(l->lz.costs);
+  hipFree(l->d_dcodes);
   for (int i = 0; i < 5; ++i)
     if (l->ev[i]) hipEventDestroy(l->ev[i]);
   free(l);
@@ -106,7 +109,28 @@ static vp8l_engine* engine_alloc(const vp8l_params* p, int max_frames, int metho
     l->route_slot = (int*)calloc(N, sizeof(int));
     if (!l->route_eng || !l->route_slot) goto fail;
   }
-  if (l->p.palette) {
+  if (l->p.palette) {   /* the cost-model parse (vp8l_launch_analyze with lz) */
+    CHK(hipMalloc((void**)&l->lz.runs, N * np * sizeof(uint16_t)));
+    CHK(hipMalloc((void**)&l->lz.htab, N * VP8L_LZ_HASH_SIZE * sizeof(int32_t)));
+    CHK(hipMalloc((void**)&l->lz.chain, N * np * sizeof(int32_t)));
+    CHK(hipMalloc((void**)&l->lz.hoff, N * np * sizeof(uint32_t)));
+    CHK(hipMalloc((void**)&l->lz.hlen, N * np * sizeof(uint16_t)));
+    CHK(hipMalloc((void**)&l->lz.loff, N * np * sizeof(uint32_t)));
+    CHK(hipMalloc((void**)&l->lz.llen, N * np * sizeof(uint16_t)));
+    CHK(hipMalloc((void**)&l->lz.costs, N * VP8L_LZ_NCOST * sizeof(int32_t)));
+    {
+      const int nd = vp8l_plane_dcodes(w, NULL);
+      uint8_t* tab = (uint8_t*)malloc((size_t)nd);
+      if (!tab) goto fail;
+      vp8l_plane_dcodes(w, tab);
+      const hipError_t e1 = hipMalloc((void**)&l->d_dcodes, (size_t)nd);
+      const hipError_t e2 = e1 == hipSuccess ? hipMemcpy(l->d_dcodes, tab, (size_t)nd,
+                                                         hipMemcpyHostToDevice) : e1;
+      free(tab);
+      CHK(e2);
+      l->lz.dcodes = l->d_dcodes;
+      l->lz.nd = nd;
+    }
     CHK(hipMalloc((void**)&l->d_psort, N * VP8L_MAX_PALETTE * sizeof(uint32_t)));
     CHK(hipMalloc((void**)&l->d_psidx, N * VP8L_MAX_PALETTE));
     CHK(hipMalloc((void**)&l->d_npal, N * sizeof(int)));
@@ -294,15 +318,16 @@ static int pipeline(vp8l_engine* l, hipStream_t st, int threads, const uint8_t* 
   } else {
     int sg_mask = 0;
     for (int f = 0; f < n; ++f) sg_mask |= identity ? 1 : 1 << ((l->h_fmode[f] >> 1) & 1);
-    if (!vp8l_launch_transform(rgba, fstride, rstride, &p, fidx_in,
-                               identity ? NULL : l->d_fmode, sg_mask, l->d_argb, l->d_modes,
-                               l->d_mult, l->d_aflag, st))
+    /* the transform search scores against the input frame's L0 histograms */
+    if (!vp8l_launch_transform(rgba, fstride, rstride, &p, fidx_in, identity ? NULL : l->d_fidx,
+                               identity ? NULL : l->d_fmode, l->d_ehist, l->d_tabs, sg_mask,
+                               l->d_argb, l->d_modes, l->d_mult, l->d_aflag, st))
       goto fail;
   }
   CHK(hipEventRecord(l->ev[1], st));
   if (!vp8l_launch_analyze(l->d_argb, &p, l->d_tabs, l->d_minb, l->d_prov, l->d_chist,
                            l->d_cbits, l->d_ops, l->d_feat, l->d_tl, l->d_tn, l->d_hc,
-                           l->d_assign, st))
+                           l->d_assign, p.palette ? &l->lz : NULL, st))
     goto fail;
   CHK(hipEventRecord(l->ev[2], st));
   {   /* debugging aid: LIBWEBP_AMD_VP8L_DUMP=<prefix> writes slot 0's

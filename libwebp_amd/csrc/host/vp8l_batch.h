@@ -94,6 +94,9 @@ typedef struct vp8l_engine {
   size_t* out_off;
   size_t* out_size;
   int* err;
+  /* colour-indexed engines: the cost-model parse's buffers (vp8l_gpu.h) */
+  vp8l_lz lz;
+  uint8_t* d_dcodes;
 } vp8l_engine;
 
 #ifdef __cplusplus

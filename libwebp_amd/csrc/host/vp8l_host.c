@@ -126,6 +126,23 @@ void vp8l_setup_params(vp8l_params* p, int w, int h, int n, int method, int alph
   }
 }
 
+/* distance -> smallest plane code for every distance a plane code reaches
+ * (model: distance_code); returns the table size (largest such distance + 1) */
+int vp8l_plane_dcodes(int w, uint8_t* tab) {
+  int nd = 0;
+  for (int c = 1; c <= 120; ++c) {
+    const int d = plane_code_to_distance(w, c);
+    if (d + 1 > nd) nd = d + 1;
+  }
+  if (!tab) return nd;
+  memset(tab, 0, (size_t)nd);
+  for (int c = 1; c <= 120; ++c) {
+    const int d = plane_code_to_distance(w, c);
+    if (!tab[d]) tab[d] = (uint8_t)c;
+  }
+  return nd;
+}
+
 /* the colour-indexing engine: coded width = bundled width, tile bits from
  * GetHistoBits with use_palette on the picture size (vp8l_enc.c:234-245) */
 void vp8l_setup_palette_params(vp8l_params* p, int w, int h, int n, int method, int xbits,

@@ -61,6 +61,9 @@ int vp8l_build_header(const vp8l_params* p, int has_alpha, int emode, int cache_
                       const uint32_t* mult, const uint32_t* hc, const uint8_t* assign,
                       vp8l_bw* bw, uint32_t* ctab, uint8_t* gtile);
 
+/* distance -> smallest plane code table for width w (NULL: size only) */
+int vp8l_plane_dcodes(int w, uint8_t* tab);
+
 /* RIFF + "VP8L" chunk header for a payload of `size` bytes (20 bytes) */
 void vp8l_riff_header(uint8_t out[20], size_t size);
 

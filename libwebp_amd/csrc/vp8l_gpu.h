@@ -12,7 +12,7 @@
  *   ehist     N x 13 x 256 uint32        AnalyzeEntropy histograms (L0)
  *   pal       N x VP8L_PAL_STRIDE uint32 colour count (257 = too many) + colours (L0)
  *   minb      N x npix uint8             smallest cache size holding the pixel (L2)
- *   ops       N x npix uint32            parse: act | len << 2 | dist_code << 15 (L3)
+ *   ops       N x npix uint32            parse: act | (len - 1) << 2 | dist_code << 14 (L3)
  *   prov      N x npix uint16            provisional parse: act | len << 2 (L3)
  *   chist     N x VP8L_CHIST uint32      cache-size choice histograms (L3)
  *   feat      N x nht  int64             histogram-tile entropy feature (L4)
@@ -47,7 +47,11 @@ extern "C" {
 #define VP8L_NS (VP8L_GS + 3 * 256 + 40)   /* G | R | B | A | D */
 #define VP8L_BLOCK 1024            /* pixels per bit-writer block */
 #define VP8L_MAX_HUFF_IMAGE 2600   /* MAX_HUFF_IMAGE_SIZE, src/enc/vp8l_enc.c */
-#define VP8L_EHIST (13 * 256)      /* AnalyzeEntropy histograms (HistoIx order) */
+/* per frame: AnalyzeEntropy's 13 histograms (HistoIx order), then the
+ * transform search's accumulated histograms: predictor-12 residuals of A, R,
+ * G, B and of the sub-green R-G, B-G (VP8L_EH_ACC + 0..5) */
+#define VP8L_EH_ACC 13
+#define VP8L_EHIST (19 * 256)
 #define VP8L_PAL_STRIDE 260        /* count + up to 256 colours (+ pad) */
 #define VP8L_MAX_PALETTE 256
 /* cache-size choice histograms per frame: literal channels G,R,B,A per
@@ -95,12 +99,14 @@ int vp8l_launch_scan(const uint8_t* rgba, size_t fstride, int rstride, int w, in
                      int plane, uint32_t* ehist, uint32_t* pal, void* stream);
 /* L1: per slot f the input frame fidx[f] (NULL: f); entropy mode fmode[f]
  * (0..3): subtract green (mode & 2), per-tile predictor + cross colour
- * (mode & 1). sg_mask: bit 0 some slot without subtract green, bit 1 some
- * with. alpha_flag[f] |= 1 if any alpha != 255. */
+ * (mode & 1), scored against the L0 histograms ehist of input frame
+ * efidx[f] (NULL: f); tabs: the engine's nlogn | log2-fraction tables.
+ * sg_mask: bit 0 some slot without subtract green, bit 1 some with.
+ * alpha_flag[f] |= 1 if any alpha != 255. */
 int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rstride,
-                          const vp8l_params* p, const int* fidx, const uint8_t* fmode,
-                          int sg_mask,
-                          uint32_t* argb, uint8_t* modes, uint32_t* mult,
+                          const vp8l_params* p, const int* fidx, const int* efidx,
+                          const uint8_t* fmode, const uint32_t* ehist, const int32_t* tabs,
+                          int sg_mask, uint32_t* argb, uint8_t* modes, uint32_t* mult,
                           uint32_t* alpha_flag, void* stream);
 /* Near-lossless preprocessing (VP8ApplyNearLossless): passes at bits .. 1
  * from frame fidx[f] of rgba into slot f of buf0 / buf1 (n x w*h*4 each,
@@ -119,10 +125,29 @@ int vp8l_launch_palette_apply(const uint8_t* rgba, size_t fstride, int rstride,
 /* L2..L5: cache sizes, provisional parse, cache-size choice (cbits[f]),
  * row parse, tile features, clustering. tabs: DEVICE tables (nlogn 4097 |
  * log2 fraction 1024, in 1/4096 bit). */
+/* Colour-indexed frames: buffers of the cost-model parse (L3p kernels) */
+#define VP8L_LZ_NCOST (280 + 3 * 256 + 40)
+#define VP8L_LZ_HASH_SIZE (1 << 18)
+typedef struct {
+  uint16_t* runs;              /* n x npix: equal pixels from each position */
+  int32_t* htab;               /* n x VP8L_LZ_HASH_SIZE: hash -> last position */
+  int32_t* chain;              /* n x npix */
+  uint32_t* hoff;              /* n x npix: the chain's best match */
+  uint16_t* hlen;
+  uint32_t* loff;              /* n x npix: the best of the 4 candidate distances */
+  uint16_t* llen;
+  int32_t* costs;              /* n x VP8L_LZ_NCOST symbol costs (1/256 bit) */
+  const uint8_t* dcodes;       /* distance -> plane code for distances < nd (0: none) */
+  int nd;
+} vp8l_lz;
+
+/* lz != NULL (colour-indexed engines): no colour cache, the greedy parse
+ * feeds two rounds of the cost-model parse over the hash chain's and the
+ * candidate distances' matches */
 int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p, const int32_t* tabs,
                         uint8_t* minb, uint16_t* prov, uint32_t* chist, uint8_t* cbits,
                         uint32_t* ops, int64_t* feat, uint32_t* tl, uint32_t* tn,
-                        uint32_t* hc, uint8_t* assign, void* stream);
+                        uint32_t* hc, uint8_t* assign, const vp8l_lz* lz, void* stream);
 /* L6/L7: per-block bit counts, per-frame scan from start_bit[f], and the
  * bit writer into out (n x out_cap bytes, zeroed except the header words the
  * host placed at the start). end_bit[f] = total payload bits. */

@@ -204,24 +204,6 @@ def fixed_mode_mask(H, W):
     return m
 
 
-def bitlen(v):
-    """Bits of |v| for the signed 8-bit view of residual bytes (0 for 0):
-    the per-value cost of the predictor and cross-colour searches (a
-    Laplacian-like proxy for the coded size that needs no histogram)."""
-    return np.frexp(np.abs(to_s8(v)).astype(np.float64))[1].astype(np.int64)
-
-
-def tile_sums(values, tb, H, W):
-    """Score per tile (larger is better): minus the sum of bitlen over all
-    pixels and channels. values: (H, W, C) int64 in 0..255."""
-    tw, th = sub_sample(W, tb), sub_sample(H, tb)
-    ty = (np.arange(H) >> tb)[:, None]
-    tx = (np.arange(W) >> tb)[None, :]
-    tile = (ty * tw + tx)
-    return -np.bincount(tile.ravel(), weights=bitlen(values).sum(axis=-1).ravel(),
-                        minlength=tw * th).astype(np.int64)
-
-
 def to_s8(v):
     v = np.asarray(v, dtype=np.int64) & 255
     return np.where(v >= 128, v - 256, v)
@@ -232,60 +214,157 @@ def ctd(t, c):
     return (np.asarray(t, dtype=np.int64) * to_s8(c)) >> 5
 
 
-def ls_multiplier(sxy, sxx):
-    """round(32 * sxy / sxx) half away from zero, clamped to int8."""
-    if sxx == 0:
-        return 0
-    num = 32 * sxy
-    q = (2 * abs(num) + sxx) // (2 * sxx)
-    q = q if num >= 0 else -q
-    return int(max(-128, min(127, q)))
+# ---- entropy-scored transform search
+#
+# The reference picks each tile's predictor and colour-transform multipliers
+# by Shannon estimates of the tile's residual histograms against histograms
+# accumulated over the tiles before it (GetBestPredictorForTile,
+# src/enc/predictor_enc.c:299-409; PredictionCostSpatialHistogram :48-58;
+# GetBestGreenToRed / GetBestGreenRedToBlue :573-681 with
+# PredictionCostCrossColor :541-547). Raster-order accumulation makes every
+# tile wait for all earlier ones; here every tile is scored against one
+# histogram set per frame instead -- the residuals of the gradient predictor
+# (mode 12, ClampedAddSubtractFull) over the pixels AnalyzeEntropy keeps
+# (repeats of the raster predecessor or of the pixel above skipped, the role
+# of the reference's "repeated pixels are handled by backward references",
+# :776-786), collected by L0 k_vp8l_entropy next to AnalyzeEntropy's own
+# histograms -- so all tiles choose at once.
+# Costs are integers in 1/4096 bit:
+#   E(t, a)   = sum_{i: t_i > 0} [slog(t_i) + slog(t_i + a_i) - slog(a_i)]
+#               (minus CombinedShannonEntropy(t, a), lossless_enc.c:403-422,
+#               less the terms that are equal for every candidate)
+#   cost(t)   = -E + 16 * sum_i t_i * SP[i]
+# SP is PredictionCostSpatial (:35-46) as a per-value table: -0.1 w0 for 0,
+# -0.1 e 0.6^(k-1) for +-k, k < 16, rounded to 1/256 bit; the predictor
+# search uses (w0, e) = (1, 0.94), the colour search (3, 2.4).
+SP_PRED = np.zeros(256, dtype=np.int64)
+SP_PRED[[0, 1, 2, 3, 4, 5, 6, 7, 8]] = [-26, -24, -14, -9, -5, -3, -2, -1, -1]
+SP_PRED[[255, 254, 253, 252, 251, 250, 249, 248]] = [-24, -14, -9, -5, -3, -2, -1, -1]
+SP_CC = np.zeros(256, dtype=np.int64)
+SP_CC[list(range(11))] = [-77, -61, -37, -22, -13, -8, -5, -3, -2, -1, -1]
+SP_CC[[256 - k for k in range(1, 11)]] = [-61, -37, -22, -13, -8, -5, -3, -2, -1, -1]
+CC_ZERO_BONUS = 3 << 12     # "-3 bits" for a zero multiplier (:565-567, :613-618)
+CC_RED_DELTAS = [32, 16, 8, 4, 2, 1]          # kMaxIters 6 at quality 75 (:577)
+CC_BLUE_DELTAS = [16, 16, 8, 4, 2, 2, 2]      # delta_lut (:640)
+CC_BLUE_AXES = [(0, -1), (0, 1), (-1, 0), (1, 0), (-1, -1), (-1, 1), (1, -1), (1, 1)]
 
 
-def candidates(ls):
-    out = [0]
-    for c in (ls - 2, ls - 1, ls, ls + 1, ls + 2):
-        out.append(max(-128, min(127, c)))
-    return out
+def spatial_table(w0, e):
+    """The SP tables above from their definition (checked by the tests)."""
+    t = [0.0] * 256
+    t[0] = -0.1 * w0
+    for k in range(1, 16):
+        t[k] = t[256 - k] = -0.1 * e
+        e *= 0.6
+    return np.array([int(math.floor(v * 256 + 0.5)) for v in t], dtype=np.int64)
 
 
-def choose_cross_color(res, tb, H, W):
-    """res: (H, W, 4) predictor residuals (A,R,G,B). Per tile choose
-    (g2r, g2b, r2b) -- least squares start, then the best of 6 candidates
-    (0 and ls-2..ls+2) by the bitlen score. Returns (tiles, 3) int and the
-    transformed residual image."""
+def tile_cost(hists, acc, slog_acc, sp):
+    """cost of (..., 256) histograms against acc (256,) with slog(acc)."""
+    t = np.asarray(hists, dtype=np.int64)
+    nz = t > 0
+    e = np.where(nz, slog2_fx(t) + slog2_fx(t + acc) - slog_acc, 0).sum(axis=-1)
+    return 16 * (t * sp).sum(axis=-1) - e
+
+
+def accumulated_histograms(argb):
+    """Per channel A, R, G, B the histogram (4, 256) of the residuals of
+    predictor 12 (fixed modes on row 0 / column 0) over the pixels
+    AnalyzeEntropy keeps. argb: the (sub-green) pixels the spatial transform
+    predicts."""
+    H, W = argb.shape
+    flat = argb.ravel().astype(np.uint32)
+    prev = np.concatenate([flat[:1], flat[:-1]])
+    keep = flat != prev
+    keep[W:] &= flat[W:] != flat[:-W]
+    a = argb.astype(np.int64)
+    P = np.stack([(a >> 24) & 255, (a >> 16) & 255, (a >> 8) & 255, a & 255], axis=-1)
+    L, T, TL, TR = neighbours(P)
+    pr = predict(12, L, T, TL, TR)
+    fixed = fixed_mode_mask(H, W)
+    for m in (0, 1, 2):
+        sel = fixed == m
+        pr[sel] = predict(m, L, T, TL, TR)[sel]
+    res = ((P - pr) & 255).reshape(-1, 4)[keep]
+    return np.stack([np.bincount(res[:, c], minlength=256) for c in range(4)])
+
+
+def tile_index(H, W, tb):
+    tw = sub_sample(W, tb)
+    return (np.arange(H) >> tb)[:, None] * tw + (np.arange(W) >> tb)[None, :]
+
+
+def choose_predictors(P, preds_res, tb, G):
+    """Per tile the predictor with the smallest cost summed over the four
+    channels (first minimum on ties). preds_res[m]: (H, W, 4) residuals of
+    mode m (fixed modes already in place on row 0 / column 0)."""
+    H, W, _ = P.shape
+    nt = sub_sample(W, tb) * sub_sample(H, tb)
+    tile = tile_index(H, W, tb).ravel()
+    slog_g = slog2_fx(G)
+    costs = []
+    for rm in preds_res:
+        e = 0
+        sp = 0
+        for c in range(4):
+            t = np.bincount(tile * 256 + rm[..., c].ravel(), minlength=nt * 256).reshape(nt, 256)
+            nz = t > 0
+            e = e + np.where(nz, slog2_fx(t) + slog2_fx(t + G[c]) - slog_g[c], 0).sum(axis=-1)
+            sp = sp + (t * SP_PRED).sum(axis=-1)
+        costs.append(16 * sp - e)
+    return np.argmin(np.stack(costs), axis=0)
+
+
+def choose_cross_color(res, tb, H, W, G):
+    """res: (H, W, 4) predictor residuals (A,R,G,B). Per tile (g2r, g2b, r2b):
+    green-to-red by a descent over CC_RED_DELTAS (both +-delta around the
+    current best scored together, the better one taken if it beats the best),
+    then (green-to-blue, red-to-blue) over CC_BLUE_AXES x CC_BLUE_DELTAS the
+    same way, stopping when a delta-2 step leaves both at 0 (the shape of
+    GetBestGreenToRed / GetBestGreenRedToBlue, predictor_enc.c:573-681, with
+    each step's candidates scored from the same start so a step is one
+    parallel evaluation). Returns (tiles, 3) and the transformed image."""
     tw, th = sub_sample(W, tb), sub_sample(H, tb)
+    accR, accB = G[1], G[3]
+    sR, sB = slog2_fx(accR), slog2_fx(accB)
     out = res.copy()
     mult = np.zeros((th * tw, 3), dtype=np.int64)
     for ty in range(th):
         for tx in range(tw):
             blk = res[ty << tb:(ty + 1) << tb, tx << tb:(tx + 1) << tb].reshape(-1, 4)
-            g = to_s8(blk[:, 2]); r = to_s8(blk[:, 1]); b = blk[:, 3]
-            sgg = int((g * g).sum())
-            best = None
-            for t in candidates(ls_multiplier(int((g * r).sum()), sgg)):
-                s = -int(bitlen((blk[:, 1] - ctd(t, g)) & 255).sum())
-                if best is None or s > best[0]:
-                    best = (s, t)
-            g2r = best[1]
-            best = None
-            for t in candidates(ls_multiplier(int((g * to_s8(b)).sum()), sgg)):
-                s = -int(bitlen((b - ctd(t, g)) & 255).sum())
-                if best is None or s > best[0]:
-                    best = (s, t)
-            g2b = best[1]
-            bb = (b - ctd(g2b, g)) & 255
-            srr = int((r * r).sum())
-            best = None
-            for t in candidates(ls_multiplier(int((r * to_s8(bb)).sum()), srr)):
-                s = -int(bitlen((bb - ctd(t, r)) & 255).sum())
-                if best is None or s > best[0]:
-                    best = (s, t)
-            r2b = best[1]
-            k = ty * tw + tx
-            mult[k] = (g2r, g2b, r2b)
+            g = blk[:, 2]; r = blk[:, 1]; b = blk[:, 3]
+
+            def cost_r(cands):
+                h = np.stack([np.bincount((r - ctd(t, g)) & 255, minlength=256) for t in cands])
+                return tile_cost(h, accR, sR, SP_CC) - CC_ZERO_BONUS * (np.array(cands) == 0)
+
+            def cost_b(cands):
+                h = np.stack([np.bincount((b - ctd(t1, g) - ctd(t2, r)) & 255, minlength=256)
+                              for t1, t2 in cands])
+                z = np.array([(t1 == 0) + (t2 == 0) for t1, t2 in cands])
+                return tile_cost(h, accB, sB, SP_CC) - CC_ZERO_BONUS * z
+
+            g2r = 0
+            best = int(cost_r([0])[0])
+            for d in CC_RED_DELTAS:
+                cands = [g2r - d, g2r + d]
+                v = cost_r(cands)
+                k = int(np.argmin(v))
+                if v[k] < best:
+                    best, g2r = int(v[k]), cands[k]
+            g2b = r2b = 0
+            best = int(cost_b([(0, 0)])[0])
+            for d in CC_BLUE_DELTAS:
+                cands = [(g2b + a0 * d, r2b + a1 * d) for a0, a1 in CC_BLUE_AXES]
+                v = cost_b(cands)
+                k = int(np.argmin(v))
+                if v[k] < best:
+                    best, (g2b, r2b) = int(v[k]), cands[k]
+                if d == 2 and g2b == 0 and r2b == 0:
+                    break
+            mult[ty * tw + tx] = (g2r, g2b, r2b)
             o = out[ty << tb:(ty + 1) << tb, tx << tb:(tx + 1) << tb]
-            og = to_s8(o[..., 2]); orr = to_s8(o[..., 1])
+            og = o[..., 2]; orr = o[..., 1]
             o[..., 3] = (o[..., 3] - ctd(g2b, og) - ctd(r2b, orr)) & 255
             o[..., 1] = (o[..., 1] - ctd(g2r, og)) & 255
     return mult, out
@@ -296,21 +375,33 @@ def choose_cross_color(res, tb, H, W):
 DIRECT, SPATIAL, SUBGREEN, SPATIAL_SUBGREEN, PALETTE = 0, 1, 2, 3, 4
 
 
-def transform_image(rgba, tb, mode=SPATIAL_SUBGREEN):
-    """Subtract green (mode & 2) -> predictor (per-tile best of 14 by the
-    bitlen score) -> cross colour (both mode & 1). Returns (modes (tiles,),
-    mult (tiles,3), residual ARGB uint32 (H, W)); modes/mult are None without
-    the spatial transforms."""
-    H, W, _ = rgba.shape
+def sub_green_planes(rgba, mode):
+    """(H, W, 4) int64 channels A, R, G, B -- after subtract green when the
+    mode has it (the image the spatial transform predicts)."""
     a = rgba[..., 3].astype(np.int64); r = rgba[..., 0].astype(np.int64)
     g = rgba[..., 1].astype(np.int64); b = rgba[..., 2].astype(np.int64)
     if mode & SUBGREEN:
-        P = np.stack([a, (r - g) & 255, g, (b - g) & 255], axis=-1)
-    else:
-        P = np.stack([a, r, g, b], axis=-1)
+        return np.stack([a, (r - g) & 255, g, (b - g) & 255], axis=-1)
+    return np.stack([a, r, g, b], axis=-1)
+
+
+def planes_argb(P):
+    return ((P[..., 0] << 24) | (P[..., 1] << 16) | (P[..., 2] << 8) | P[..., 3]).astype(np.uint32)
+
+
+def transform_image(rgba, tb, mode=SPATIAL_SUBGREEN, G=None):
+    """Subtract green (mode & 2) -> predictor (per tile the best of 14,
+    choose_predictors) -> cross colour (choose_cross_color), both mode & 1.
+    G: the frame's accumulated histograms (accumulated_histograms of the
+    sub-green input; computed here when not given). Returns (modes (tiles,),
+    mult (tiles,3), residual ARGB uint32 (H, W)); modes/mult are None
+    without the spatial transforms."""
+    H, W, _ = rgba.shape
+    P = sub_green_planes(rgba, mode)
     if not mode & SPATIAL:
-        argb = (P[..., 0] << 24) | (P[..., 1] << 16) | (P[..., 2] << 8) | P[..., 3]
-        return None, None, argb.astype(np.uint32)
+        return None, None, planes_argb(P)
+    if G is None:
+        G = accumulated_histograms(planes_argb(P))
     L, T, TL, TR = neighbours(P)
     fixed = fixed_mode_mask(H, W)
     preds = [predict(m, L, T, TL, TR) for m in range(14)]
@@ -318,21 +409,15 @@ def transform_image(rgba, tb, mode=SPATIAL_SUBGREEN):
     for m in (0, 1, 2):
         sel = fixed == m
         fres[sel] = (P[sel] - preds[m][sel]) & 255
-    scores = []
-    for m in range(14):
-        rm = np.where((fixed >= 0)[..., None], fres, (P - preds[m]) & 255)
-        scores.append(tile_sums(rm, tb, H, W))
-    scores = np.stack(scores)               # (14, tiles)
-    modes = np.argmax(scores, axis=0)       # first maximum = lowest mode on ties
-    tw = sub_sample(W, tb)
-    tmode = modes[((np.arange(H) >> tb)[:, None] * tw + (np.arange(W) >> tb)[None, :])]
+    rms = [np.where((fixed >= 0)[..., None], fres, (P - preds[m]) & 255) for m in range(14)]
+    modes = choose_predictors(P, rms, tb, G)
+    tmode = modes[tile_index(H, W, tb)]
     res = fres.copy()
     for m in range(14):
         sel = (tmode == m) & (fixed < 0)
-        res[sel] = (P[sel] - preds[m][sel]) & 255
-    mult, res = choose_cross_color(res, tb, H, W)
-    argb = (res[..., 0] << 24) | (res[..., 1] << 16) | (res[..., 2] << 8) | res[..., 3]
-    return modes, mult, argb.astype(np.uint32)
+        res[sel] = rms[m][sel]
+    mult, res = choose_cross_color(res, tb, H, W, G)
+    return modes, mult, planes_argb(res)
 
 
 # ---------------------------------------------------------------- LZ77 / cache
@@ -419,6 +504,261 @@ def parse(argb, hit, dists, lens=None):
                 x += 1
     ccode = np.where(act == 2, dcode[best], 0)
     return act, clen, ccode
+
+
+# ---------------------------------------------------------------- palette LZ77
+#
+# Colour-indexed frames (graphics: few colours, long repeats) take a
+# cost-model parse over long-range matches -- the reference's
+# VP8LHashChainFill (src/enc/backward_references_enc.c:259-452) and
+# TraceBackwards (backward_references_cost_enc.c:569-795), restated for the
+# GPU:
+#   * the hash chain exactly as the reference builds it: a 2-pixel hash,
+#     runs of >= 3 equal pixels hashed as (colour, remaining run); chain[q] =
+#     the previous position with the same hash (lz_hash_chain);
+#   * every position searches that chain on its own (GetMaxItersForQuality
+#     (75) = 51 steps, the up / left heuristics first, stop at 256) -- no
+#     left extension of a neighbour's match, so all positions search at once
+#     (lz_hash_search);
+#   * besides the chain's longest match, the longest run against the 4
+#     cheap candidate distances (up, left, up-left, up-right) (lz_local);
+#   * a shortest-path parse in integer bits over those two matches per
+#     position (the reference keeps one and spreads its cost over every
+#     length with cost intervals; here each match offers the lengths
+#     LZ_LENGTHS <= its length and itself), on independent LZ_SEG-pixel
+#     segments of the frame (lz_dp), with per-symbol costs from a first parse:
+#     the greedy parse, then the first cost-model parse (two rounds);
+#   * no colour cache (a palette index costs about what a cache index does;
+#     measured smaller on the fixtures).
+LZ_SEG = 4096
+LZ_MAX_LENGTH = 4095                      # MAX_LENGTH (backward_references_enc.h:117)
+LZ_HASH_SHIFT = 32 - 18                   # HASH_BITS 18
+LZ_ITER_MAX = 8 + (75 * 75) // 128        # GetMaxItersForQuality(75) (:242-244)
+LZ_WINDOW_CAP = (1 << 18) - 121           # distance code + 120 fits the 18-bit ops field
+LZ_LENGTHS = sorted(set(range(2, 17)) | {v for j in range(2, 13) for v in (1 << j, (1 << j) + 1)
+                                         if v <= LZ_MAX_LENGTH})
+LZ_INF = (1 << 31) - 1
+
+
+def lz_pair_hash(a, b):
+    """GetPixPairHash64 (backward_references_enc.c:231-238)."""
+    return (((b * 0xc6a4a793) + (a * 0x5bd1e996)) & 0xFFFFFFFF) >> LZ_HASH_SHIFT
+
+
+def lz_runs(flat):
+    """R[q]: equal pixels starting at q (>= 1)."""
+    n = len(flat)
+    R = np.ones(n, dtype=np.int64)
+    for q in range(n - 2, -1, -1):
+        if flat[q] == flat[q + 1]:
+            R[q] = R[q + 1] + 1
+    return R
+
+
+def lz_hash_chain(flat):
+    """chain[q]: the previous position with q's hash, -1 if none (the
+    reference's chain, :283-345). q is hashed as (colour, R[q] - 2) when
+    R[q] >= 3 (skipped -- no link, not inserted -- when R[q] - 2 exceeds
+    MAX_LENGTH), else as the pixel pair; positions up to n - 3 are inserted,
+    n - 2 only looks up."""
+    n = len(flat)
+    chain = np.full(n, -1, dtype=np.int64)
+    if n <= 2:
+        return chain
+    R = lz_runs(flat)
+    first = {}
+    for q in range(n - 1):
+        if R[q] >= 3:
+            if R[q] - 2 > LZ_MAX_LENGTH:
+                continue
+            key = lz_pair_hash(int(flat[q]), int(R[q] - 2))
+        else:
+            key = lz_pair_hash(int(flat[q]), int(flat[q + 1]))
+        chain[q] = first.get(key, -1)
+        if q <= n - 3:
+            first[key] = q
+    return chain
+
+
+def lz_hash_search(flat, W):
+    """(distance, length) per position: the reference's per-position search
+    (:359-411) over lz_hash_chain with lengths capped at the position's
+    segment end, no left extension."""
+    flat = [int(v) for v in flat]
+    n = len(flat)
+    off = np.zeros(n, dtype=np.int64)
+    ln = np.zeros(n, dtype=np.int64)
+    if n <= 2:
+        return off, ln
+    chain = lz_hash_chain(flat)
+    window = min(W << 8, LZ_WINDOW_CAP)
+    for p in range(1, n - 1):
+        max_len = min(n - 1 - p, LZ_MAX_LENGTH, (p // LZ_SEG + 1) * LZ_SEG - p)
+
+        def mlen(a):
+            k = 0
+            while k < max_len and flat[a + k] == flat[p + k]:
+                k += 1
+            return k
+        it = LZ_ITER_MAX
+        bl = bd = 0
+        min_pos = max(p - window, 0)
+        length_max = min(max_len, 256)
+        q = int(chain[p])
+        if p >= W:
+            c = mlen(p - W)
+            if c > bl:
+                bl, bd = c, W
+            it -= 1
+        c = mlen(p - 1)
+        if c > bl:
+            bl, bd = c, 1
+        it -= 1
+        if bl == LZ_MAX_LENGTH:
+            q = min_pos - 1
+        while q >= min_pos:
+            it -= 1
+            if it == 0:
+                break
+            if flat[q + bl] == flat[p + bl]:
+                c = mlen(q)
+                if c > bl:
+                    bl, bd = c, p - q
+                    if bl >= length_max:
+                        break
+            q = int(chain[q])
+        off[p], ln[p] = bd, bl
+    return off, ln
+
+
+def lz_local(flat, W):
+    """(distance, length) per position: the longest run against the 4
+    candidate distances (first on ties) within the position's segment."""
+    n = len(flat)
+    off = np.zeros(n, dtype=np.int64)
+    ln = np.zeros(n, dtype=np.int64)
+    last = (np.arange(n) + 1) % LZ_SEG == 0
+    last[-1] = True
+    for d in candidate_distances(W):
+        eq = np.zeros(n, dtype=bool)
+        eq[d:] = flat[d:] == flat[:-d]
+        run = np.zeros(n, dtype=np.int64)
+        nxt = 0
+        for i in range(n - 1, -1, -1):
+            nxt = (1 + (0 if last[i] else nxt)) if eq[i] else 0
+            run[i] = nxt
+        r = np.minimum(run, LZ_MAX_LENGTH)
+        better = r > ln
+        off[better] = d
+        ln[better] = r[better]
+    return off, ln
+
+
+def lz_pop_costs(h):
+    """1/256 bit per symbol: log2(total) - log2(count) (log2 0 := 0), all 0
+    for fewer than two used symbols (ConvertPopulationCountTableToBitEstimates,
+    backward_references_cost_enc.c:41-60)."""
+    h = np.asarray(h, dtype=np.int64)
+    if (h > 0).sum() <= 1:
+        return np.zeros(len(h), dtype=np.int64)
+    return (int(flog2(int(h.sum()))) - np.where(h > 0, flog2(np.maximum(h, 1)), 0)) >> 4
+
+
+def lz_costs(flat, act, clen, ccode, W):
+    """Symbol costs of a parse (cache-free): G+length (280), R, B, A, D (40)."""
+    a = np.asarray(flat, dtype=np.int64)
+    lit = act == 0
+    cp = act == 2
+    la = a[lit]
+    ls, _, _ = prefix_arrays(clen[cp])
+    ds, _, _ = prefix_arrays(ccode[cp])
+    g = np.bincount(np.concatenate([(la >> 8) & 255, 256 + ls]), minlength=280)
+    return (lz_pop_costs(g), lz_pop_costs(np.bincount((la >> 16) & 255, minlength=256)),
+            lz_pop_costs(np.bincount(la & 255, minlength=256)),
+            lz_pop_costs(np.bincount((la >> 24) & 255, minlength=256)),
+            lz_pop_costs(np.bincount(ds, minlength=NUM_DIST)))
+
+
+def lz_dp(flat, W, costs, cands):
+    """Shortest-path parse per LZ_SEG segment. Per position, in order: the
+    literal, then each (distance, length) of cands at the lengths
+    LZ_LENGTHS <= length and the length itself; a target keeps the first
+    cheapest path. Literal = 82% of its four symbols (mul1, :134), copy =
+    distance + length symbols and their extra bits. Returns act, clen, ccode."""
+    cG, cR, cB, cA, cD = [c.tolist() for c in costs]
+    a = [int(v) for v in flat]
+    n = len(a)
+    lit = [((cA[v >> 24] + cR[(v >> 16) & 255] + cG[(v >> 8) & 255] + cB[v & 255]) * 82) // 100
+           for v in a]
+    dcache, lcache = {}, {}
+
+    def dcost(d):
+        if d not in dcache:
+            code = distance_code(W, d)
+            sy, nb, _ = prefix_encode(code)
+            dcache[d] = (cD[sy] + 256 * nb, code)
+        return dcache[d]
+
+    def lcost(k):
+        if k not in lcache:
+            sy, nb, _ = prefix_encode(k)
+            lcache[k] = cG[256 + sy] + 256 * nb
+        return lcache[k]
+    cands = [([int(v) for v in o], [int(v) for v in l]) for o, l in cands]
+    act = np.zeros(n, dtype=np.int64)
+    clen = np.zeros(n, dtype=np.int64)
+    ccode = np.zeros(n, dtype=np.int64)
+    for s in range(0, n, LZ_SEG):
+        e = min(n, s + LZ_SEG)
+        m = e - s
+        cost = [LZ_INF] * (m + 1)
+        cost[0] = 0
+        ch = [0] * (m + 1)
+        dd = [0] * (m + 1)
+        for j in range(m):
+            i = s + j
+            c = cost[j]
+            v = c + lit[i]
+            if v < cost[j + 1]:
+                cost[j + 1] = v
+                ch[j + 1] = 1
+            for off, ln in cands:
+                L = min(ln[i], e - i)
+                if L < 2:
+                    continue
+                base = c + dcost(off[i])[0]
+                for k in LZ_LENGTHS + ([L] if L not in LZ_LENGTHS else []):
+                    if k > L:
+                        continue
+                    v = base + lcost(k)
+                    if v < cost[j + k]:
+                        cost[j + k] = v
+                        ch[j + k] = k
+                        dd[j + k] = off[i]
+        j = m
+        while j > 0:
+            k = ch[j]
+            st = s + j - k
+            if k >= 2:
+                act[st] = 2
+                act[st + 1:s + j] = 3
+                clen[st] = k
+                ccode[st] = dcost(dd[j])[1]
+            j -= k
+    return act, clen, ccode
+
+
+def palette_parse(argb, dists, lens):
+    """The parse of a colour-indexed frame (see above): greedy parse without
+    cache -> costs -> cost-model parse -> its costs -> cost-model parse."""
+    H, W = argb.shape
+    flat = argb.ravel().astype(np.int64)
+    act, clen, ccode = parse(argb, np.zeros((H, W), dtype=bool), dists, lens)
+    cands = [lz_hash_search(flat, W), lz_local(flat, W)]
+    act, clen, ccode = act.ravel(), clen.ravel(), ccode.ravel()
+    for _ in range(2):
+        act, clen, ccode = lz_dp(flat, W, lz_costs(flat, act, clen, ccode, W), cands)
+    return act.reshape(H, W), clen.reshape(H, W), ccode.reshape(H, W)
 
 
 def choose_cache_bits(argb, act, clen, minb):
@@ -1107,20 +1447,27 @@ def encode(rgba, method=4, cache_bits=AUTO_CACHE, kmax=KMAX, return_parts=False,
     else:
         hb = histo_bits(method, W, H)
         tb = transform_bits(method, hb)
+        # the transform search's histograms: L0's, i.e. of the input picture
+        G = accumulated_histograms(planes_argb(sub_green_planes(rgba, mode)))
         if near_lossless_q < 100 and not alpha_plane and near_lossless_applies(mode, near_lossless_q):
             rgba = argb_to_rgba(near_lossless(to_argb(rgba), near_lossless_q))
-        modes, mult, argb = transform_image(rgba, tb, mode)
+        modes, mult, argb = transform_image(rgba, tb, mode, G)
     PW = argb.shape[1]
     dists = candidate_distances(PW)
     lens = match_lengths(argb, dists)
-    if cache_bits == AUTO_CACHE:
+    if pal is not None:   # colour-indexed: the cost-model parse, no colour cache
+        cache_bits = 0
+        hit = np.zeros((H, PW), dtype=bool)
+        act, clen, ccode = palette_parse(argb, dists, lens)
+    elif cache_bits == AUTO_CACHE:
         minb = cache_minb(argb.ravel()).reshape(H, PW)
         act, clen, _ = parse(argb, minb <= MAX_CACHE_BITS, dists, lens)
         cache_bits = choose_cache_bits(argb, act, clen, minb)
         hit = minb <= cache_bits
     else:
         hit = cache_hits(argb.ravel(), cache_bits).reshape(H, PW)
-    act, clen, ccode = parse(argb, hit, dists, lens)
+    if pal is None:
+        act, clen, ccode = parse(argb, hit, dists, lens)
     al = Alphabets(cache_bits)
     S, X = pixel_symbols(argb, act, clen, ccode, cache_bits, al)
     tw, th = sub_sample(PW, hb), sub_sample(H, hb)

@@ -2,7 +2,7 @@
 # One GPU-box session: GPU tests, bench line, K3 stage split, rocprofv3 kernel
 # stats, PMC passes (HBM bytes, SQ issue counters) and the PMC calibration.
 # Usage (on the box): bash tools/gpu_session.sh <tag> [steps...]
-#   steps: tests bench stages prof pmc sq calib (default: all)
+#   steps: tests bench lossless lprof stages prof pmc sq calib (default: all but lossless/lprof)
 set -o pipefail
 TAG=${1:-s}; shift
 STEPS=${*:-tests bench stages prof pmc sq calib}
@@ -17,6 +17,15 @@ if has tests; then
 fi
 if has bench; then
   run timeout -k 10 400 python3 bench.py --steps 5 --warmup 2 > $O/bench.json 2> $O/bench.err || exit 1
+fi
+if has lossless; then
+  run timeout -k 10 400 python3 bench.py --lossless --steps 3 --warmup 1 > $O/bench_lossless.json \
+    2> $O/bench_lossless.err || exit 1
+fi
+if has lprof; then
+  (cd /tmp && TMPDIR=/tmp run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+    -d $O/lstats -o run -- python3 $R/bench.py --lossless --no-cpu --no-host-input --steps 2 \
+    --warmup 1 > $O/lprof.log 2>&1) || exit 1
 fi
 if has stages; then
   for B in 256 1; do

@@ -158,12 +158,15 @@ def encode_rgba_map(lib, rgba, info_type, quality=75.0, method=4, **kw):
 
 
 def encode_rgba(lib, rgba, quality=75.0, method=4, stats=False, use_argb=None, _extra_info=None,
-                **kw):
+                progress=None, **kw):
     """Encode an (H, W, 4) uint8 array through `lib`'s WebPEncode().
 
     use_argb: import into the ARGB container first (what cwebp does for
     -sharp_yuv, examples/cwebp.c); defaults to on when use_sharp_yuv is set,
     since WebPEncode only re-converts an ARGB picture.
+
+    progress: callable(percent) -> bool, installed as picture.progress_hook
+    (a False return aborts the encode: VP8_ENC_ERROR_USER_ABORT).
 
     Returns (bytes, WebPAuxStats or None). Raises on encoder error.
     """
@@ -185,6 +188,10 @@ def encode_rgba(lib, rgba, quality=75.0, method=4, stats=False, use_argb=None, _
     st = WebPAuxStats() if stats else None
     if st is not None:
         pic.stats = C.pointer(st)
+    hook = None
+    if progress is not None:
+        hook = WebPProgressHook(lambda pct, _pic: 1 if progress(pct) else 0)
+        pic.progress_hook = C.cast(hook, C.c_void_p)
     if _extra_info is not None:
         pic.extra_info_type = _extra_info[0]
         pic.extra_info = C.cast(_extra_info[1], C.POINTER(C.c_uint8))

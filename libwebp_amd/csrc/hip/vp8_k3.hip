@@ -719,8 +719,14 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
     const int left_m = bx == 0 ? L.predleft[by] : L.modes[i4 - 1];
     const int top_m = by == 0 ? predtop[4 * x0 + bx] : L.modes[i4 - 4];
     const int ctx4 = (int)((tnz >> bx) & 1) + (int)((lnz >> by) & 1);
+    // the worker's 4th wave (rtid 192..255) holds no mode: without trellis
+    // (whose per-mode steps carry barriers) it skips straight to the
+    // barrier, leaving its SIMD's issue slots to the other workers
+    const bool busy = TRELLIS || (tid >> 6) != 3;   // wave-uniform
     const int src = L.yin[(4 * by + y) * BPS + 4 * bx + x];
-    int pr;
+    int pr = 0, rec = 0, nzb = 0;
+    int level = 0, dq = 0;
+    if (busy) {
     {
       const int ea = cv[edge_off(pl.ia, bx, by)];
       const int eb = cv[edge_off(pl.ib, bx, by)];
@@ -736,7 +742,6 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
     SUBST(0);
     const int c = fdct_lane(src - pr, make_tlane(opaque(j)));
     SUBST(1);
-    int level = 0, dq = 0;
     if constexpr (TRELLIS) {
       if (act) L.co4[m][j] = (int16_t)c;
       WB();
@@ -762,10 +767,10 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
       dq = (int16_t)__mul24(level, q_q);
     }
     SUBST(2);
-    const int rec = idct_lane(dq, pr, make_tlane(opaque(j)));
+    rec = idct_lane(dq, pr, make_tlane(opaque(j)));
     const uint64_t bnz = __ballot(act && level != 0);
     const uint64_t bac = __ballot(act && level != 0 && j != 0);
-    const int nzb = ((bnz >> g) & 0xffff) != 0;
+    nzb = ((bnz >> g) & 0xffff) != 0;
     SUBST(3);
     if (search) {
       const int D = sum16((src - rec) * (src - rec));
@@ -790,6 +795,7 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
         L.r4[m][3] = D;
       }
     }
+    }   // busy
     SUBST(5);
     WB();
     int bm;
@@ -1029,7 +1035,7 @@ __device__ bool wait_ge(K3G& G, K3S& L, const int32_t* p, int32_t v, int site) {
 struct XHdr {
   int32_t fold_ptr, epoch, abort, lcver;
   uint32_t ntok;
-  int32_t tok_err, pad[2];
+  int32_t tok_err, uabort, pad;   // uabort: the progress hook asked to stop
   unsigned long long size_p0, sse[3], dist, size_rh;
   int32_t nb[3], max_edge[4], pad2;
 };
@@ -1217,6 +1223,24 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
   if (tid == 0) {
     G.ntok = base + total;
     publish((int32_t*)&G.fold_ptr, (int32_t)i1);
+  }
+}
+
+// WebPEncode progress: MB rows folded (folds run in raster order, so the
+// stored value only grows), a system-scope store to the host-mapped word; the
+// word after it is the hook's stop request, taken up here as an abort the
+// other workers see at their next wait (the worker's loop ends on myabort)
+template <bool X>
+__device__ __forceinline__ void report_rows(K3G& G, K3S& L, const vp8g_frame_params* P, int tid,
+                                            uint32_t i1, int mbw, XHdr* XH) {
+  if (P->progress_addr && tid == 0) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(P->progress_addr);
+    __hip_atomic_store(w, i1 / (uint32_t)mbw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (__hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+      L.myabort = 1;
+      G.abort = 6;
+      if constexpr (X) { st_sc1(&XH->uabort, 1); st_sc1(&XH->abort, 1); }
+    }
   }
 }
 
@@ -1961,6 +1985,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     }
     fold_rows<X>(G, L, tid, fold_from, (uint32_t)(y + 1) * mbw, (uint32_t)y * mbw, tok_base,
                  mboff, xs);
+    report_rows<X>(G, L, P, tid, (uint32_t)(y + 1) * mbw, mbw, XH);
     wbar(L);
     K3_STAMP(7);
   }
@@ -2049,7 +2074,7 @@ __global__ __launch_bounds__(K3T) void k_encode_xtail(K3Args a) {
     G.mark[0] = 0;
   }
   __syncthreads();
-  const int err = XH->abort ? 2 : XH->tok_err;
+  const int err = XH->uabort ? 2 | (6 << 4) : XH->abort ? 2 : XH->tok_err;
   if (!err) compact_tokens(G, tok_base, mboff, nmb);
   __syncthreads();
   for (int s = tid; s < NSLOT; s += K3T) {

@@ -7,12 +7,16 @@
 //                        LDS histograms, one global add per bin)
 //      k_vp8l_palscan    one workgroup per frame: the colour set in an LDS hash
 //                        table, out as soon as it exceeds 256 colours
+//   L1a k_vp8l_predsel   one workgroup per frame: the reference's predictor
+//                        choice exactly (serial over tiles, float entropy)
+//      k_vp8l_resid_serial  one wave per frame: residuals where near-lossless
+//                        / alpha-0 clean-up update the picture (wavefront)
 //   L1 k_vp8l_transform  one workgroup per L1_TILES transform tiles: subtract
-//                        green, best of 14 predictors and the cross-colour
-//                        multipliers (a descent over parallel candidate
-//                        steps), all scored by entropy against the frame's
-//                        L0 histograms; residual ARGB to HBM -- or the plain
-//                        (sub-green) pixels for the non-spatial modes
+//                        green, the chosen predictor's residuals and the
+//                        cross-colour multipliers (a descent over parallel
+//                        candidate steps) scored by entropy against the
+//                        frame's L0 histograms; residual ARGB to HBM -- or the
+//                        plain (sub-green) pixels for the non-spatial modes
 //      k_vp8l_palapply   colour indexing: binary search in the sorted palette,
 //                        2^xbits indices bundled per packed pixel
 //   L2 k_vp8l_cache      one wave per frame, 64 pixels per step: per pixel the
@@ -124,13 +128,13 @@ __device__ __forceinline__ V wave_sum(V v) {
 
 // ------------------------------------------------------------------ L1
 
-// Entropy-scored transform search (model: choose_predictors /
-// choose_cross_color, oracle/vp8l_model.py): every candidate is scored by
+// The tile's residuals under the predictor L1a chose, then the cross-colour
+// search (model: choose_cross_color, oracle/vp8l_model.py): every candidate
+// is scored by
 //   cost = 16 * sum_i t_i SP[i] - sum_{i: t_i > 0} [slog(t_i) + slog(t_i + G_i) - slog(G_i)]
 // (1/4096 bit) over the tile's residual histograms t against the frame's
 // accumulated histograms G (L0's residuals against the raster predecessor).
 // SP: PredictionCostSpatial (src/enc/predictor_enc.c:35-46) per value.
-__constant__ int8_t kSpPred[16] = {-26, -24, -14, -9, -5, -3, -2, -1, -1, 0, 0, 0, 0, 0, 0, 0};
 __constant__ int8_t kSpCC[16] = {-77, -61, -37, -22, -13, -8, -5, -3, -2, -1, -1, 0, 0, 0, 0, 0};
 __device__ __forceinline__ int sp_of(const int8_t* tab, int v) {
   const int k = v < 128 ? v : 256 - v;   // symmetric in +-k
@@ -144,13 +148,10 @@ template <int T>
 struct TransformSmem {
   uint32_t src[(T + 1) * (T + 2)];   // rows y0-1.., cols x0-1..x0+tw
   uint32_t first[T];                 // P(0, y) for the right-edge TR wrap
-  union {
-    uint32_t h14[14 * 4 * 128];      // predictor search: 14 modes x 4 channels, u16 counts
-    struct {
-      uint32_t res[T * T];           // the chosen predictor's residuals
-      uint32_t h9[9 * 128];          // colour search: up to 9 candidates, u16 counts
-    } cc;
-  } u;
+  struct {
+    uint32_t res[T * T];             // the chosen predictor's residuals
+    uint32_t h9[9 * 128];            // colour search: up to 9 candidates, u16 counts
+  } cc;
   long long slogg[4][256];           // slog(G) per channel and value
   uint32_t g[4][256];                // the frame's accumulated histograms (A, R, G, B)
   int32_t frac[1024];                // log2 fraction table (model: FLOG2_FRAC)
@@ -202,23 +203,23 @@ template <int K, int T, bool BLUE>
 __device__ void cc_eval(TransformSmem<T>& S, int np, const int (&c0)[K], const int (&c1)[K],
                         long long (&out)[K]) {
   const int tid = threadIdx.x;
-  for (int i = tid; i < K * 128; i += 256) S.u.cc.h9[i] = 0;
+  for (int i = tid; i < K * 128; i += 256) S.cc.h9[i] = 0;
   if (tid < K) S.cost[tid] = 0;
   __syncthreads();
   for (int i = tid; i < np; i += 256) {
-    const uint32_t r = S.u.cc.res[i];
+    const uint32_t r = S.cc.res[i];
     const int g = ch(r, 8), rr = ch(r, 16), bb = ch(r, 0);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int v = BLUE ? (bb - ctd(c0[k], g) - ctd(c1[k], rr)) & 255 : (rr - ctd(c0[k], g)) & 255;
-      hist_add(S.u.cc.h9 + k * 128, v);
+      hist_add(S.cc.h9 + k * 128, v);
     }
   }
   __syncthreads();
   long long acc[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) acc[k] = 0;
-  bin_costs<K>(S, S.u.cc.h9, BLUE ? 3 : 1, kSpCC, acc);
+  bin_costs<K>(S, S.cc.h9, BLUE ? 3 : 1, kSpCC, acc);
   reduce_costs<K>(S, acc);
   __syncthreads();
 #pragma unroll
@@ -238,8 +239,9 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
                                                         const uint8_t* __restrict__ fmode,
                                                         const uint32_t* __restrict__ ehist,
                                                         const int32_t* __restrict__ frac_tab,
+                                                        const uint8_t* __restrict__ modes,
+                                                        const uint32_t* __restrict__ pflag,
                                                         uint32_t* __restrict__ argb_out,
-                                                        uint8_t* __restrict__ modes,
                                                         uint32_t* __restrict__ mult,
                                                         uint32_t* __restrict__ alpha_flag) {
   __shared__ TransformSmem<T> S;
@@ -334,8 +336,6 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
       }
     }
     if (__any(tile_alpha) && lane_id() == 0) atomicOr(&alpha_flag[f], 1u);
-    for (int i = tid; i < 14 * 4 * 128; i += 256) S.u.h14[i] = 0;
-    if (tid < 16) S.cost[tid] = 0;
     __syncthreads();
 
     auto at = [&](int lx, int ly) -> uint32_t { return S.src[(ly + 1) * sw + lx + 1]; };
@@ -345,60 +345,27 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     const int np = tw * th;
     // fixed predictors: (0,0) black, row 0 left, column 0 top (lossless.c:219-239)
     auto fixed_mode = [&](int x, int y) -> int { return y == 0 ? (x == 0 ? 0 : 1) : (x == 0 ? 2 : -1); };
-
-    // predictor search (model: choose_predictors): the tile's residual
-    // histograms of all 14 modes at once, then one value per thread
-    for (int i = tid; i < np; i += 256) {
-      const int ly = i / tw, lx = i - ly * tw;
-      const uint32_t P = at(lx, ly), L = at(lx - 1, ly), T_ = at(lx, ly - 1), TL = at(lx - 1, ly - 1);
-      const uint32_t TR = tr(lx, ly);
-      const int fm = fixed_mode(x0 + lx, y0 + ly);
-#pragma unroll
-      for (int m = 0; m < 14; ++m) {
-        const uint32_t r = sub_pixels(P, predict(fm >= 0 ? fm : m, L, T_, TL, TR));
-        uint32_t* h = S.u.h14 + m * 4 * 128;
-        hist_add(h + 0 * 128, (int)(r >> 24));
-        hist_add(h + 1 * 128, ch(r, 16));
-        hist_add(h + 2 * 128, ch(r, 8));
-        hist_add(h + 3 * 128, ch(r, 0));
+    // the tile's predictor (L1a, the reference's choice) and its residuals:
+    // computed here, or, where GetResidual updated the picture (pflag), the
+    // serial pass's
+    const int best = modes[(size_t)f * ntt + tile];
+    uint32_t* out = argb_out + (size_t)f * W * H;
+    if (pflag[f]) {
+      for (int i = tid; i < np; i += 256) {
+        const int ly = i / tw, lx = i - ly * tw;
+        S.cc.res[i] = out[(size_t)(y0 + ly) * W + x0 + lx];
+      }
+    } else {
+      for (int i = tid; i < np; i += 256) {
+        const int ly = i / tw, lx = i - ly * tw;
+        const int fm = fixed_mode(x0 + lx, y0 + ly);
+        S.cc.res[i] = sub_pixels(at(lx, ly), predict(fm >= 0 ? fm : best, at(lx - 1, ly),
+                                                       at(lx, ly - 1), at(lx - 1, ly - 1), tr(lx, ly)));
       }
     }
-    __syncthreads();
-    {
-      long long acc[14];
-#pragma unroll
-      for (int m = 0; m < 14; ++m) acc[m] = 0;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int b = tid;
-        const uint32_t gv = S.g[c][b];
-        const long long sg = S.slogg[c][b];
-        const int spv = sp_of(kSpPred, b);
-#pragma unroll
-        for (int m = 0; m < 14; ++m) {
-          const uint32_t t = (S.u.h14[(m * 4 + c) * 128 + (b >> 1)] >> ((b & 1) * 16)) & 0xffffu;
-          if (t) acc[m] += 16ll * (long long)t * spv - (slog_fx(S.frac, t) + slog_fx(S.frac, t + gv) - sg);
-        }
-      }
-      reduce_costs<14>(S, acc);
-    }
-    __syncthreads();
-    if (tid == 0) {
-      int best = 0;
-      for (int m = 1; m < 14; ++m)
-        if (S.cost[m] < S.cost[best]) best = m;
-      S.best = best;
-    }
-    __syncthreads();
-    const int best = S.best;
-    for (int i = tid; i < np; i += 256) {
-      const int ly = i / tw, lx = i - ly * tw;
-      const int fm = fixed_mode(x0 + lx, y0 + ly);
-      S.u.cc.res[i] = sub_pixels(at(lx, ly), predict(fm >= 0 ? fm : best, at(lx - 1, ly),
-                                                     at(lx, ly - 1), at(lx - 1, ly - 1), tr(lx, ly)));
-    }
-    // colour search (model: choose_cross_color)
+    // colour search (model: choose_cross_color); none at method 0 (vp8l_enc.c:1525-1526)
     int g2r = 0, g2b = 0, r2b = 0;
+    if (!p.low_effort) {
     {
       long long bestc;
       {   // start (0) and the first +-32 step in one evaluation
@@ -450,21 +417,482 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
         if (d == 2 && g2b == 0 && r2b == 0) break;
       }
     }
+    }   // !low_effort
     // final residuals
-    uint32_t* out = argb_out + (size_t)f * W * H;
+    __syncthreads();   // every residual of the tile read before any is overwritten
     for (int i = tid; i < np; i += 256) {
       const int ly = i / tw, lx = i - ly * tw;
-      const uint32_t r = S.u.cc.res[i];
+      const uint32_t r = S.cc.res[i];
       const int g = ch(r, 8), rr = ch(r, 16), bb = ch(r, 0);
       const int nr = (rr - ctd(g2r, g)) & 255;
       const int nb = (bb - ctd(g2b, g) - ctd(r2b, rr)) & 255;
       out[(size_t)(y0 + ly) * W + x0 + lx] = (r & 0xff00ff00u) | ((uint32_t)nr << 16) | (uint32_t)nb;
     }
     if (tid == 0) {
-      modes[(size_t)f * ntt + tile] = (uint8_t)best;
       mult[(size_t)f * ntt + tile] =
           (uint32_t)(g2r & 255) | ((uint32_t)(g2b & 255) << 8) | ((uint32_t)(r2b & 255) << 16);
     }
+  }
+}
+
+// ------------------------------------------------------------------ L1a
+// VP8LResidualImage's predictor choice, exactly (model: residual_image;
+// src/enc/predictor_enc.c:299-409,476-516). Serial over the frame's tiles in
+// raster order -- each tile is scored against the histograms of the
+// residuals its predecessors chose -- so one workgroup per frame:
+//   1. the tile (+ border) into LDS; near-lossless max diffs (:121-146);
+//   2. the 14 modes' residual histograms: all pixels at once, or, where
+//      GetResidual updates the picture as it goes (near-lossless
+//      quantisation, alpha-0 clean-up; :234-292), a wavefront per mode with
+//      one lane per tile row (row r at column s - 2r in step s; the row
+//      above comes in by a lane shuffle, one column ahead);
+//   3. PredictionCostSpatialHistogram (:47-57) per mode: the subtrahends of
+//      CombinedShannonEntropy (src/dsp/lossless_enc.c:403-422) computed in
+//      parallel, then one lane per (mode, channel) subtracts them in the
+//      reference's order -- float32 with no contraction, so the sums are the
+//      reference's bit for bit; the first minimum wins.
+// The float tables (VP8LFastSLog2 0..255, log2 0..255: tabs + 5121, + 5377)
+// are the host's (float)(v log2 v), (float)log2 v, equal to the reference's
+// literals (tests/test_vp8l.py checks them against its source).
+#define PS_THREADS 1024
+#define PS_MAXT 64
+#define LOG_2_RECIPROCAL_D 1.44269504088896338700465094007086
+
+struct PredSelSmem {
+  uint32_t src[(PS_MAXT + 2) * (PS_MAXT + 2)];   // rows y0-1..y1, cols x0-1..x1 (original)
+  uint32_t first[PS_MAXT + 1];                   // P(0, y) for y0-1 .. y1-1 (TR wrap)
+  uint8_t maxd[PS_MAXT * PS_MAXT];
+  uint32_t hist[14 * 4 * 128];                   // u16 pairs: [mode][channel][value]
+  int32_t acc[4][256];
+  float sacc[4][256];                            // FastSLog2(acc)
+  float terms[2][14][256][2];                    // one channel pair's subtrahends, in order
+  float slog[256], log2t[256];
+  float pcs[14][4], cse[14][4];
+  int accsum[4];
+  int best, serial, any_t;
+};
+
+__device__ __forceinline__ float ps_slog2(uint32_t v, const float* slog, const float* log2t) {
+  if (v < 256) return slog[v];
+  if (v < 65536) {   // FastSLog2Slow_C (src/dsp/lossless_enc.c:329-359)
+    const int log_cnt = (31 - __clz((int)v)) - 7;
+    const uint32_t y = 1u << log_cnt;
+    const int corr = (int)((23 * (v & (y - 1))) >> 4);
+    return __fadd_rn(__fmul_rn((float)v, __fadd_rn(log2t[v >> log_cnt], (float)log_cnt)),
+                     (float)corr);
+  }
+  return (float)__dmul_rn(__dmul_rn(LOG_2_RECIPROCAL_D, (double)v), log((double)v));
+}
+
+__device__ __forceinline__ uint32_t add_pixels(uint32_t a, uint32_t b) {
+  const uint32_t ag = (a & 0xff00ff00u) + (b & 0xff00ff00u);
+  const uint32_t rb = (a & 0x00ff00ffu) + (b & 0x00ff00ffu);
+  return (ag & 0xff00ff00u) | (rb & 0x00ff00ffu);
+}
+
+// NearLosslessComponent (src/enc/predictor_enc.c:151-179)
+__device__ __forceinline__ int nl_component(int value, int pred, int boundary, int q) {
+  const int residual = (value - pred) & 0xff;
+  const int boundary_residual = (boundary - pred) & 0xff;
+  const int lower = residual & ~(q - 1);
+  const int upper = lower + q;
+  const int bias = ((boundary - value) & 0xff) < boundary_residual;
+  if (residual - lower < upper - residual + bias) {
+    if (residual > boundary_residual && lower <= boundary_residual) return lower + (q >> 1);
+    return lower;
+  }
+  if (residual <= boundary_residual && upper > boundary_residual) return lower + (q >> 1);
+  return upper & 0xff;
+}
+
+// NearLossless (:190-227)
+__device__ uint32_t nl_residual(uint32_t value, uint32_t pred, int max_q, int max_diff, bool sg) {
+  if (max_diff <= 2) return sub_pixels(value, pred);
+  int q = max_q;
+  while (q >= max_diff) q >>= 1;
+  const int va = (int)(value >> 24);
+  const int a = (va == 0 || va == 0xff) ? (va - (int)(pred >> 24)) & 0xff
+                                        : nl_component(va, (int)(pred >> 24), 0xff, q);
+  const int g = nl_component(ch(value, 8), ch(pred, 8), 0xff, q);
+  int new_green = 0, green_diff = 0;
+  if (sg) {
+    new_green = (ch(pred, 8) + g) & 0xff;
+    green_diff = (new_green - ch(value, 8)) & 0xff;
+  }
+  const int r = nl_component((ch(value, 16) - green_diff) & 0xff, ch(pred, 16), 0xff - new_green, q);
+  const int b = nl_component((ch(value, 0) - green_diff) & 0xff, ch(pred, 0), 0xff - new_green, q);
+  return ((uint32_t)a << 24) | ((uint32_t)r << 16) | ((uint32_t)g << 8) | (uint32_t)b;
+}
+
+__device__ __forceinline__ uint32_t add_green(uint32_t v) {   // AddGreenToBlueAndRed (:113-119)
+  const uint32_t g = (v >> 8) & 0xff;
+  return (v & 0xff00ff00u) | (((v & 0x00ff00ffu) + ((g << 16) | g)) & 0x00ff00ffu);
+}
+__device__ __forceinline__ int max_diff_px(uint32_t a, uint32_t b) {
+  int m = 0;
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) m = max(m, abs(ch(a, k) - ch(b, k)));
+  return m;
+}
+
+// one pixel of GetResidual's non-exact branch (:243-290): the residual, and
+// the (possibly updated) pixel the later predictions read
+__device__ __forceinline__ uint32_t resid_px(uint32_t cur, uint32_t pred, bool quant, int max_q,
+                                             int md, bool sg, uint32_t& rec) {
+  uint32_t res;
+  if (!quant) {
+    res = sub_pixels(cur, pred);
+  } else {
+    res = nl_residual(cur, pred, max_q, md, sg);
+    cur = add_pixels(pred, res);
+  }
+  rec = cur;
+  if ((cur >> 24) == 0) {
+    res &= 0xff000000u;
+    rec = pred & 0x00ffffffu;
+  }
+  return res;
+}
+
+// residual histogram counts with the five most frequent values per channel
+// (0, +-1, +-2) kept in registers: same-bin LDS atomics within a wave
+// serialise, and those values are most of a good predictor's residuals
+__device__ __forceinline__ void count_res(uint32_t res, uint32_t (&hot)[20], uint32_t* h) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int v = ch(res, 24 - 8 * c);
+    const int k = (v + 2) & 255;   // 254, 255, 0, 1, 2 -> 0..4
+#pragma unroll
+    for (int j = 0; j < 5; ++j) hot[c * 5 + j] += (k == j);
+    if (k >= 5) hist_add(h + c * 128, v);
+  }
+}
+__device__ __forceinline__ void flush_hot_lane(const uint32_t (&hot)[20], uint32_t* h) {
+#pragma unroll
+  for (int i = 0; i < 20; ++i) {
+    const int v = (i % 5 + 254) & 255;
+    if (hot[i]) atomicAdd(&h[(i / 5) * 128 + (v >> 1)], hot[i] << ((v & 1) * 16));
+  }
+}
+
+// pixel of the input frame as the transform sees it (sub-green when SG)
+template <bool SG>
+__device__ __forceinline__ uint32_t in_px(const uint8_t* img, int rstride, bool plane, int x, int y) {
+  if (plane) {
+    const uint32_t g = img[(size_t)y * rstride + x];
+    return SG ? (((0u - g) & 255) << 16) | (g << 8) | ((0u - g) & 255) : g << 8;
+  }
+  const uint8_t* q = img + (size_t)y * rstride + 4 * x;
+  const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
+  return SG ? (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255)
+            : (a << 24) | (r << 16) | (g << 8) | b;
+}
+
+template <int T, bool SG>
+__global__ __launch_bounds__(PS_THREADS) void k_vp8l_predsel(const uint8_t* __restrict__ rgba,
+                                                             size_t fstride, int rstride,
+                                                             vp8l_params p,
+                                                             const int* __restrict__ fidx,
+                                                             const uint8_t* __restrict__ fmode,
+                                                             const float* __restrict__ ftabs,
+                                                             uint8_t* __restrict__ modes,
+                                                             uint32_t* __restrict__ pflag) {
+  extern __shared__ __align__(16) uint8_t ps_smem[];
+  PredSelSmem& S = *reinterpret_cast<PredSelSmem*>(ps_smem);
+  const int tid = threadIdx.x, f = blockIdx.x;
+  const int W = p.w, H = p.h;
+  const int emode = fmode ? (int)fmode[f] : VP8L_MODE_SPATIAL;
+  if (!(emode & VP8L_MODE_SPATIAL) || ((emode & VP8L_MODE_SUBGREEN) != 0) != SG) return;
+  const uint8_t* img = rgba + (size_t)(fidx ? fidx[f] : f) * fstride;
+  const int tiles_x = (W + T - 1) / T, tiles_y = (H + T - 1) / T, ntt = tiles_x * tiles_y;
+  uint8_t* fm = modes + (size_t)f * ntt;
+  const bool plane = p.alpha != 0;
+  if (p.low_effort) {   // kPredLowEffort everywhere (:488-492), plain residuals
+    for (int t = tid; t < ntt; t += PS_THREADS) fm[t] = 11;
+    if (tid == 0) pflag[f] = 0;
+    return;
+  }
+  const int max_q = 1 << p.nlq_bits;
+  for (int i = tid; i < 256; i += PS_THREADS) { S.slog[i] = ftabs[i]; S.log2t[i] = ftabs[256 + i]; }
+  for (int i = tid; i < 1024; i += PS_THREADS) {
+    (&S.acc[0][0])[i] = 0;
+    (&S.sacc[0][0])[i] = 0.f;
+  }
+  if (tid < 4) S.accsum[tid] = 0;
+  if (tid == 0) S.any_t = 0;
+  const float kBias = 15.f;   // kSpatialPredictorBias (:24)
+
+  for (int tile = 0; tile < ntt; ++tile) {
+    const int tx = tile % tiles_x, ty = tile / tiles_x;
+    const int x0 = tx * T, y0 = ty * T;
+    const int tw = min(T, W - x0), th = min(T, H - y0);
+    const int sw = tw + 2, np = tw * th;
+    __syncthreads();   // the previous tile is done with S
+    bool tr_alpha = false;
+    for (int i = tid; i < (th + 2) * sw; i += PS_THREADS) {
+      const int ly = i / sw, lx = i - ly * sw;
+      const int y = y0 - 1 + ly, x = x0 - 1 + lx;
+      uint32_t v = 0;
+      if (y >= 0 && y < H && x >= 0 && x < W) v = in_px<SG>(img, rstride, plane, x, y);
+      S.src[i] = v;
+      if (ly >= 1 && ly <= th && lx >= 1 && lx <= tw && (v >> 24) == 0) tr_alpha = true;
+    }
+    for (int i = tid; i <= th; i += PS_THREADS) {
+      const int y = y0 - 1 + i;
+      S.first[i] = y >= 0 ? in_px<SG>(img, rstride, plane, 0, y) : 0u;
+    }
+    for (int i = tid; i < 14 * 4 * 128; i += PS_THREADS) S.hist[i] = 0;
+    if (tid == 0) S.serial = 0;
+    __syncthreads();
+    if (!p.exact && __any(tr_alpha) && lane_id() == 0) { S.serial = 1; S.any_t = 1; }
+    if (!p.exact && max_q > 1) {
+      if (tid == 0) S.serial = 1;
+      for (int i = tid; i < np; i += PS_THREADS) {   // MaxDiffsForRow over the original
+        const int ly = i / tw, lx = i - ly * tw;
+        const int x = x0 + lx, y = y0 + ly;
+        int md = 0;
+        if (x >= 1 && x < W - 1 && y >= 1 && y < H - 1) {
+          auto at = [&](int ax, int ay) -> uint32_t {
+            const uint32_t v = S.src[(ay + 1) * sw + ax + 1];
+            return SG ? add_green(v) : v;
+          };
+          const uint32_t c = at(lx, ly);
+          md = max(max(max_diff_px(c, at(lx, ly - 1)), max_diff_px(c, at(lx, ly + 1))),
+                   max(max_diff_px(c, at(lx - 1, ly)), max_diff_px(c, at(lx + 1, ly))));
+        }
+        S.maxd[i] = (uint8_t)min(md, 255);
+      }
+    }
+    __syncthreads();
+    auto at = [&](int lx, int ly) -> uint32_t { return S.src[(ly + 1) * sw + lx + 1]; };
+    if (!S.serial) {
+      // plain residuals: one wave per mode over the tile's pixels (fixed
+      // modes on row 0 / column 0)
+      const int m = tid >> 6;
+      if (m < 14) {
+        uint32_t hot[20];
+#pragma unroll
+        for (int i = 0; i < 20; ++i) hot[i] = 0;
+        uint32_t* h = S.hist + m * 4 * 128;
+        for (int k = lane_id(); k < np; k += 64) {
+          const int ly = k / tw, lx = k - ly * tw;
+          const int x = x0 + lx, y = y0 + ly;
+          uint32_t pred;
+          if (y == 0) pred = x == 0 ? 0xff000000u : at(lx - 1, ly);
+          else if (x == 0) pred = at(lx, ly - 1);
+          else pred = predict(m, at(lx - 1, ly), at(lx, ly - 1), at(lx - 1, ly - 1),
+                              x + 1 < W ? at(lx + 1, ly - 1) : S.first[ly + 1]);
+          count_res(sub_pixels(at(lx, ly), pred), hot, h);
+        }
+#pragma unroll
+        for (int i = 0; i < 20; ++i) {
+          const uint32_t t = wave_sum(hot[i]);
+          const int v = (i % 5 + 254) & 255;
+          if (lane_id() == 0 && t) atomicAdd(&h[(i / 5) * 128 + (v >> 1)], t << ((v & 1) * 16));
+        }
+      }
+    } else {
+      // wavefront: lane (m, r) takes tile row r; T lanes per mode, 64 / T modes per wave
+      const int m = tid / T, r = tid - m * T;
+      const bool live = m < 14 && r < th;
+      const int y = y0 + r;
+      const bool quant_row = max_q > 1 && m != 0 && y != 0 && y != H - 1;
+      uint32_t out = live ? at(-1, r) : 0u;   // what the row below reads next: left context first
+      uint32_t a = 0, b = 0, c = 0;           // the row above at x-1, x, x+1 (r > 0)
+      uint32_t L = out, first_rec = 0;
+      uint32_t hot[20];
+#pragma unroll
+      for (int i = 0; i < 20; ++i) hot[i] = 0;
+      uint32_t* h = S.hist + (m < 14 ? m : 0) * 4 * 128;
+      const int nsteps = tw + 2 * (th - 1);
+      for (int s = 0; s < nsteps; ++s) {
+        const uint32_t up = __shfl_up(out, 1);   // row r-1's newest pixel
+        a = b; b = c; c = up;
+        const int lx = s - 2 * r, x = x0 + lx;
+        if (live && lx >= 0 && lx < tw) {
+          uint32_t T_, TL, TR;
+          if (r == 0) {
+            T_ = at(lx, -1); TL = at(lx - 1, -1);
+            TR = x + 1 < W ? at(lx + 1, -1) : S.first[1];
+          } else {
+            T_ = b; TL = a;
+            TR = lx + 1 < tw ? c : (x + 1 < W ? at(lx + 1, r - 1) : 0u);
+          }
+          if (x + 1 >= W) TR = (x0 == 0) ? first_rec : S.first[r + 1];   // P(0, y), this row
+          uint32_t pred;
+          if (y == 0) pred = x == 0 ? 0xff000000u : L;
+          else if (x == 0) pred = T_;
+          else pred = predict(m, L, T_, TL, TR);
+          const bool q = quant_row && x != 0 && x != W - 1;
+          uint32_t rec;
+          const uint32_t res = resid_px(at(lx, r), pred, q, max_q, q ? S.maxd[r * tw + lx] : 0,
+                                        SG, rec);
+          count_res(res, hot, h);
+          if (lx == 0) first_rec = rec;
+          L = rec;
+          out = rec;
+        } else if (live && lx == tw) {
+          out = x < W ? at(lx, r) : 0u;   // the right context, for the row below's last TR
+        }
+      }
+      if (live) flush_hot_lane(hot, h);
+    }
+    __syncthreads();
+    // costs, one channel pair at a time
+    for (int cp = 0; cp < 2; ++cp) {
+      for (int i = tid; i < 2 * 14 * 256; i += PS_THREADS) {
+        const int cc = i / (14 * 256), rem = i - cc * 14 * 256;
+        const int m = rem >> 8, v = rem & 255, c = 2 * cp + cc;
+        const uint32_t x = (S.hist[(m * 4 + c) * 128 + (v >> 1)] >> ((v & 1) * 16)) & 0xffffu;
+        const uint32_t y = (uint32_t)S.acc[c][v];
+        float t1, t2 = 0.f;
+        if (x) {
+          t1 = ps_slog2(x, S.slog, S.log2t);
+          t2 = ps_slog2(x + y, S.slog, S.log2t);
+        } else {
+          t1 = S.sacc[c][v];   // 0 when y == 0
+        }
+        S.terms[cc][m][v][0] = t1;
+        S.terms[cc][m][v][1] = t2;
+      }
+      __syncthreads();
+      if (tid < 28) {
+        const int cc = tid / 14, m = tid - cc * 14, c = 2 * cp + cc;
+        float rr = 0.f;
+        const float2* tv = reinterpret_cast<const float2*>(&S.terms[cc][m][0][0]);
+        for (int v = 0; v < 256; ++v) {
+          const float2 t = tv[v];
+          rr = __fsub_rn(rr, t.x);
+          rr = __fsub_rn(rr, t.y);
+        }
+        const float sxy = __fadd_rn(ps_slog2((uint32_t)np, S.slog, S.log2t),
+                                    ps_slog2((uint32_t)(np + S.accsum[c]), S.slog, S.log2t));
+        S.cse[m][c] = __fadd_rn(rr, sxy);
+        // PredictionCostSpatial(counts, 1, 0.94f) (:34-45)
+        auto cnt = [&](int v) -> int {
+          return (int)((S.hist[(m * 4 + c) * 128 + (v >> 1)] >> ((v & 1) * 16)) & 0xffffu);
+        };
+        float bits = __fmul_rn(1.f, (float)cnt(0));
+        float e = 0.94f;
+        for (int i = 1; i < 16; ++i) {
+          bits = __fadd_rn(bits, __fmul_rn(e, (float)(cnt(i) + cnt(256 - i))));
+          e = __fmul_rn(e, 0.6f);
+        }
+        S.pcs[m][c] = (float)__dmul_rn(-0.1, (double)bits);
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      const int left = tx > 0 ? fm[tile - 1] : 0xff, above = ty > 0 ? fm[tile - tiles_x] : 0xff;
+      float best_diff = 1e30f;
+      int best = 0;
+      for (int m = 0; m < 14; ++m) {
+        float cst = 0.f;
+        for (int c = 0; c < 4; ++c) {
+          cst = __fadd_rn(cst, S.pcs[m][c]);
+          cst = __fadd_rn(cst, S.cse[m][c]);
+        }
+        if (m == left) cst = __fsub_rn(cst, kBias);
+        if (m == above) cst = __fsub_rn(cst, kBias);
+        if (cst < best_diff) { best_diff = cst; best = m; }
+      }
+      S.best = best;
+      fm[tile] = (uint8_t)best;
+    }
+    __syncthreads();
+    {   // accumulate the chosen histograms (:401-405)
+      const int best = S.best;
+      for (int i = tid; i < 1024; i += PS_THREADS) {
+        const int c = i >> 8, v = i & 255;
+        const uint32_t x = (S.hist[(best * 4 + c) * 128 + (v >> 1)] >> ((v & 1) * 16)) & 0xffffu;
+        if (x) {
+          const int nv = S.acc[c][v] + (int)x;
+          S.acc[c][v] = nv;
+          S.sacc[c][v] = ps_slog2((uint32_t)nv, S.slog, S.log2t);
+        }
+      }
+      if (tid < 4) S.accsum[tid] += np;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) pflag[f] = (!p.exact && (max_q > 1 || S.any_t)) ? 1u : 0u;
+}
+
+// CopyImageWithPrediction (:414-470) where GetResidual updates the picture
+// (pflag[f]): one wave per frame, the rows in bands of 64 (one lane each),
+// row r of a band at column s - 2r in step s; the row above comes from the
+// lane above by a shuffle or, for the band's first row, from the previous
+// band's last row (LDS, read before it is overwritten: lane 63 stores column
+// x only at step x + 126). Residuals to argb (before the colour transform).
+template <bool SG>
+__global__ __launch_bounds__(64) void k_vp8l_resid_serial(const uint8_t* __restrict__ rgba,
+                                                          size_t fstride, int rstride,
+                                                          vp8l_params p,
+                                                          const int* __restrict__ fidx,
+                                                          const uint8_t* __restrict__ fmode,
+                                                          const uint8_t* __restrict__ modes,
+                                                          const uint32_t* __restrict__ pflag,
+                                                          uint32_t* __restrict__ argb_out) {
+  extern __shared__ __align__(16) uint32_t prev_row[];   // W pixels of the band above
+  const int f = blockIdx.x, lane = threadIdx.x;
+  const int emode = fmode ? (int)fmode[f] : VP8L_MODE_SPATIAL;
+  if (!(emode & VP8L_MODE_SPATIAL) || ((emode & VP8L_MODE_SUBGREEN) != 0) != SG || !pflag[f]) return;
+  const int W = p.w, H = p.h, tb = p.tb;
+  const int tiles_x = (W + (1 << tb) - 1) >> tb;
+  const uint8_t* img = rgba + (size_t)(fidx ? fidx[f] : f) * fstride;
+  const uint8_t* fm = modes + (size_t)f * tiles_x * ((H + (1 << tb) - 1) >> tb);
+  uint32_t* out = argb_out + (size_t)f * W * H;
+  const bool plane = p.alpha != 0;
+  const int max_q = 1 << p.nlq_bits;
+  auto src = [&](int x, int y) -> uint32_t { return in_px<SG>(img, rstride, plane, x, y); };
+  auto orig_g = [&](int x, int y) -> uint32_t {   // for the max diffs: sub-green undone
+    const uint32_t v = src(x, y);
+    return SG ? add_green(v) : v;
+  };
+  for (int yb = 0; yb < H; yb += 64) {
+    const int r = lane, y = yb + r;
+    const bool live = y < H;
+    const bool quant_row = max_q > 1 && y != 0 && y != H - 1;
+    uint32_t outv = 0, a = 0, b = 0, c = 0, L = 0, first_rec = 0;
+    const int nrows = min(64, H - yb);
+    const int nsteps = W + 2 * (nrows - 1);
+    for (int s = 0; s < nsteps; ++s) {
+      const uint32_t up = __shfl_up(outv, 1);
+      a = b; b = c; c = up;
+      const int x = s - 2 * r;
+      if (live && x >= 0 && x < W) {
+        uint32_t T_ = 0, TL = 0, TR = 0;
+        if (y > 0) {
+          if (r == 0) {
+            T_ = prev_row[x];
+            TL = x > 0 ? prev_row[x - 1] : 0u;
+            TR = x + 1 < W ? prev_row[x + 1] : 0u;
+          } else {
+            T_ = b; TL = a; TR = c;
+          }
+        }
+        if (x + 1 >= W) TR = first_rec;   // P(0, y), reconstructed
+        const int m = fm[(y >> tb) * tiles_x + (x >> tb)];
+        uint32_t pred;
+        if (y == 0) pred = x == 0 ? 0xff000000u : L;
+        else if (x == 0) pred = T_;
+        else pred = predict(m, L, T_, TL, TR);
+        const bool q = quant_row && m != 0 && x != 0 && x != W - 1;
+        int md = 0;
+        if (q) {
+          const uint32_t cg = orig_g(x, y);
+          md = max(max(max_diff_px(cg, orig_g(x, y - 1)), max_diff_px(cg, orig_g(x, y + 1))),
+                   max(max_diff_px(cg, orig_g(x - 1, y)), max_diff_px(cg, orig_g(x + 1, y))));
+        }
+        uint32_t rec;
+        out[(size_t)y * W + x] = resid_px(src(x, y), pred, q, max_q, md, SG, rec);
+        if (x == 0) first_rec = rec;
+        L = rec;
+        outv = rec;
+        if (r == 63 || y == H - 1) prev_row[x] = rec;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -1754,6 +2182,10 @@ __global__ __launch_bounds__(256) void k_vp8l_pack(const uint8_t* __restrict__ o
 // ------------------------------------------------------------------ launchers
 
 static int check_launch() { return hipGetLastError() == hipSuccess; }
+#define CHK_LAUNCH(x) \
+  do {                \
+    if ((x) != hipSuccess) return 0; \
+  } while (0)
 
 extern "C" int vp8l_launch_scan(const uint8_t* rgba, size_t fstride, int rstride, int w, int h,
                                 int n, int plane, uint32_t* ehist, uint32_t* pal, void* stream) {
@@ -1766,12 +2198,36 @@ extern "C" int vp8l_launch_scan(const uint8_t* rgba, size_t fstride, int rstride
   return check_launch();
 }
 
+template <int T, bool SG>
+static int launch_predsel(const uint8_t* rgba, size_t fstride, int rstride, const vp8l_params* p,
+                          const int* fidx, const uint8_t* fmode, const float* ftabs,
+                          uint8_t* modes, uint32_t* pflag, uint32_t* argb, hipStream_t st) {
+  static bool lds_ok = [] {
+    return hipFuncSetAttribute((const void*)k_vp8l_predsel<T, SG>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)sizeof(PredSelSmem)) == hipSuccess;
+  }();
+  if (!lds_ok) return 0;
+  hipLaunchKernelGGL((k_vp8l_predsel<T, SG>), dim3(p->n), dim3(PS_THREADS), sizeof(PredSelSmem),
+                     st, rgba, fstride, rstride, *p, fidx, fmode, ftabs, modes, pflag);
+  if (!check_launch()) return 0;
+  const size_t row_lds = (size_t)p->w * sizeof(uint32_t);
+  static bool lds2_ok = [] {
+    return hipFuncSetAttribute((const void*)k_vp8l_resid_serial<SG>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  }();
+  if (!lds2_ok || row_lds > 160 * 1024) return 0;
+  hipLaunchKernelGGL((k_vp8l_resid_serial<SG>), dim3(p->n), dim3(64), row_lds, st, rgba, fstride,
+                     rstride, *p, fidx, fmode, (const uint8_t*)modes, (const uint32_t*)pflag, argb);
+  return check_launch();
+}
+
 extern "C" int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rstride,
                                      const vp8l_params* p, const int* fidx, const int* efidx,
                                      const uint8_t* fmode, const uint32_t* ehist,
                                      const int32_t* tabs, int sg_mask, uint32_t* argb,
-                                     uint8_t* modes, uint32_t* mult, uint32_t* alpha_flag,
-                                     void* stream) {
+                                     uint8_t* modes, uint32_t* pflag, uint32_t* mult,
+                                     uint32_t* alpha_flag, void* stream) {
   if (p->tb < 2 || p->tb > 6 || p->w <= 0 || p->h <= 0 || p->n <= 0) return 0;
   if (!p->alpha && !fmode) return 0;
   if (!fmode) sg_mask = 1;
@@ -1779,9 +2235,26 @@ extern "C" int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rs
   dim3 grid((ntt + L1_TILES - 1) / L1_TILES, 1, p->n);
   hipStream_t st = (hipStream_t)stream;
   const int32_t* frac = tabs + 4097;
+  const float* ftabs = reinterpret_cast<const float*>(tabs + VP8L_TAB_FSLOG);
+  // L1a: the predictor of every tile (and the serial residuals where needed)
+  CHK_LAUNCH(hipMemsetAsync(pflag, 0, (size_t)p->n * sizeof(uint32_t), st));
+#define L1A(T, SG) \
+  if (!launch_predsel<T, SG>(rgba, fstride, rstride, p, fidx, fmode, ftabs, modes, pflag, argb, st)) return 0
+  for (int sg = 0; sg < 2; ++sg) {
+    if (!((sg_mask >> sg) & 1)) continue;
+    switch (p->tb) {
+      case 2: if (sg) { L1A(4, true); } else { L1A(4, false); } break;
+      case 3: if (sg) { L1A(8, true); } else { L1A(8, false); } break;
+      case 4: if (sg) { L1A(16, true); } else { L1A(16, false); } break;
+      case 5: if (sg) { L1A(32, true); } else { L1A(32, false); } break;
+      default: if (sg) { L1A(64, true); } else { L1A(64, false); } break;
+    }
+  }
+#undef L1A
 #define L1(T, SG)                                                                             \
   hipLaunchKernelGGL((k_vp8l_transform<T, SG>), grid, dim3(256), 0, st, rgba, fstride, rstride, \
-                     *p, fidx, efidx, fmode, ehist, frac, argb, modes, mult, alpha_flag)
+                     *p, fidx, efidx, fmode, ehist, frac, (const uint8_t*)modes,                \
+                     (const uint32_t*)pflag, argb, mult, alpha_flag)
   for (int sg = 0; sg < 2; ++sg) {
     if (!((sg_mask >> sg) & 1)) continue;
     switch (p->tb) {

@@ -97,6 +97,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
     b->l = vp8l_engine_new(width, height, max_frames, config->method, 0);
     if (!b->l) goto fail;
     vp8l_engine_set_near_lossless(b->l, config->near_lossless);
+    vp8l_engine_set_exact(b->l, config->exact);
     return b;
   }
   vp8h_frame probe;
@@ -201,6 +202,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipFree(b->d_recon); hipFree(b->d_mbval); hipFree(b->d_afp); hipFree(b->d_aflevel);
   hipHostFree(b->h_afp); hipHostFree(b->h_aflevel);
   hipHostFree(b->h_state); hipHostFree(b->h_active); hipHostFree(b->h_tbits);
+  hipHostFree(b->h_prog);
   hipHostFree(b->h_aflags); hipHostFree(b->h_alpha); hipHostFree(b->h_uva);
   hipHostFree(b->h_segmap); hipHostFree(b->h_params); hipHostFree(b->h_mbinfo);
   hipHostFree(b->h_results); hipHostFree(b->h_tokens); hipHostFree(b->h_psize);
@@ -246,7 +248,8 @@ static void frame_head(WebPGpuBatch* b, int f) {
   if (res->error) {
     if (getenv("WEBP_AMD_SYNC_K3"))   /* fault localisation: K3's raw error (wait site << 4) */
       fprintf(stderr, "frame %d: K3 error 0x%x\n", f, (unsigned)res->error);
-    b->err[f] = VP8_ENC_ERROR_OUT_OF_MEMORY;
+    /* wait site 6: the progress hook asked to stop (WebPEncode) */
+    b->err[f] = (res->error >> 4) == 6 ? VP8_ENC_ERROR_USER_ABORT : VP8_ENC_ERROR_OUT_OF_MEMORY;
     return;
   }
   b->err[f] = vp8h_build_p0(fr, res, b->h_mbinfo + (size_t)f * b->nmb * VP8G_MBINFO_BYTES,
@@ -338,6 +341,47 @@ static void run_tails(WebPGpuBatch* b, int n, int phase) {
 }
 
 /* ---- pipeline ---- */
+
+/* frame 0's progress words into the parameters of the next K3 launch
+ * (WebPEncode with a progress hook), every other frame none */
+static int stamp_progress(WebPGpuBatch* b, int n) {
+  if (b->progress && !b->h_prog) {
+    void* dp = NULL;
+    if (hipHostMalloc((void**)&b->h_prog, 2 * sizeof(uint32_t), hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer(&dp, b->h_prog, 0) != hipSuccess) {
+      vp8g_set_error("stamp_progress", "host-mapped progress words");
+      return 0;
+    }
+    b->d_prog = (uint64_t)(uintptr_t)dp;
+  }
+  if (b->progress) {
+    __atomic_store_n(&b->h_prog[0], 0u, __ATOMIC_RELAXED);
+    __atomic_store_n(&b->h_prog[1], 0u, __ATOMIC_RELAXED);
+  }
+  for (int f = 0; f < n; ++f) b->h_params[f].progress_addr = (f == 0 && b->progress) ? b->d_prog : 0;
+  return 1;
+}
+
+/* wait for the stream; with a progress hook, poll the rows K3 has folded
+ * and pass them on (WebPReportProgress per MB row, iterator_enc.c:89-99); a
+ * hook returning 0 raises the abort word K3 checks after each row it folds,
+ * and the hook is not called again */
+static hipError_t engine_wait(WebPGpuBatch* b, hipStream_t st) {
+  if (!b->progress || !b->h_prog) return hipStreamSynchronize(st);
+  int last = -1;
+  for (;;) {
+    const hipError_t e = hipStreamQuery(st);
+    if (e != hipErrorNotReady) return e;
+    const int rows = (int)__atomic_load_n(&b->h_prog[0], __ATOMIC_RELAXED);
+    if (rows != last && !__atomic_load_n(&b->h_prog[1], __ATOMIC_RELAXED)) {
+      last = rows;
+      if (!b->progress(b->progress_ctx, rows, b->mbh))
+        __atomic_store_n(&b->h_prog[1], 1u, __ATOMIC_RELAXED);
+    }
+    usleep(200);
+  }
+}
 
 /* ALPH chunks of the frames with alpha (h_aflags): the alpha planes in
  * d_aplane through the VP8L engine in ALPH mode (alpha_enc.c:50-98), or raw
@@ -467,6 +511,7 @@ static int lowmem_passes(WebPGpuBatch* b, int n) {
       ++nact;
     }
     if (!nact) break;
+    if (!stamp_progress(b, n)) return 0;
     CHK(hipMemcpyAsync(b->d_segmap, b->h_segmap, n * nmb, hipMemcpyHostToDevice, st));
     CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
                        hipMemcpyHostToDevice, st));
@@ -536,6 +581,7 @@ static int lowmem_passes(WebPGpuBatch* b, int n) {
     return 1;
   }
   CHK(hipMemcpyAsync(b->d_rerun, b->h_state, n * VP8G_RERUN_STATE_BYTES, hipMemcpyHostToDevice, st));
+  if (!stamp_progress(b, n)) return 0;
   CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
                      hipMemcpyHostToDevice, st));
   if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
@@ -633,6 +679,7 @@ static int statloop_search(WebPGpuBatch* b, int n) {
       ++nact;
     }
     if (!nact) break;
+    if (!stamp_progress(b, n)) return 0;
     CHK(hipMemcpyAsync(b->d_segmap, b->h_segmap, n * nmb, hipMemcpyHostToDevice, st));
     CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
                        hipMemcpyHostToDevice, st));
@@ -735,6 +782,7 @@ static int statloop_search(WebPGpuBatch* b, int n) {
     CHK(e1);
   }
   CHK(hipMemcpyAsync(b->d_rerun, b->h_state, n * VP8G_RERUN_STATE_BYTES, hipMemcpyHostToDevice, st));
+  if (!stamp_progress(b, n)) return 0;
   CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
                      hipMemcpyHostToDevice, st));
   if (m012) {
@@ -839,6 +887,7 @@ static int run_passes(WebPGpuBatch* b, int n) {
       nsize += fr->do_size_search && !fr->is_last_pass;
     }
     if (!nact) break;
+    if (!stamp_progress(b, n)) return 0;
     CHK(hipMemcpyAsync(b->d_segmap, b->h_segmap, n * nmb, hipMemcpyHostToDevice, st));
     CHK(hipMemcpyAsync(b->d_params, b->h_params, n * sizeof(vp8g_frame_params),
                        hipMemcpyHostToDevice, st));
@@ -872,7 +921,7 @@ static int run_passes(WebPGpuBatch* b, int n) {
       CHK(hipMemcpyAsync(b->h_state, b->d_rerun, (size_t)n * VP8G_RERUN_STATE_BYTES,
                          hipMemcpyDeviceToHost, st));
     }
-    CHK(hipStreamSynchronize(st));
+    CHK(engine_wait(b, st));
     if (nsize) {   /* FinalizeTokenProbas, then VP8EstimateTokenSize on the device */
       for (int f = 0; f < n; ++f) {
         vp8h_frame* fr = &b->frames[f];

@@ -17,6 +17,13 @@ int vp8g_device_ncpu(int device);   /* CPUs of the device's share (0: not pinned
 
 struct WebPGpuBatch {
   int device, w, h, max_frames, mbw, mbh, nmb, uvw, uvh, threads, last_n;
+  /* WebPEncode's per-MB-row progress / abort (vp8g_frame_params::progress_addr):
+     progress(ctx, rows_done, mbh) is polled while K3 runs on frame 0; a 0
+     return stops K3 after its next row fold (VP8_ENC_ERROR_USER_ABORT) */
+  int (*progress)(void* ctx, int rows_done, int rows_total);
+  void* progress_ctx;
+  uint32_t* h_prog;          /* 2 host-mapped words: rows done, abort */
+  uint64_t d_prog;           /* their device address */
   WebPConfig cfg;
   size_t yfb, tok_cap, d_rgba_cap, h_tok_cap;
   hipStream_t stream;

@@ -38,7 +38,7 @@ static int sub_sample(int size, int bits) { return (size + (1 << bits) - 1) >> b
 
 void vp8l_engine_free(vp8l_engine* l) {
   if (!l) return;
-  for (int i = 0; i < 4; ++i) vp8l_engine_free(l->sub[i]);
+  for (int i = 0; i < 5; ++i) vp8l_engine_free(l->sub[i]);
   free(l->route_eng); free(l->route_slot);
   hipFree(l->d_minb); hipFree(l->d_prov); hipFree(l->d_chist); hipFree(l->d_cbits);
   hipFree(l->d_ehist); hipFree(l->d_scan); hipFree(l->d_fidx); hipFree(l->d_fmode);
@@ -48,7 +48,7 @@ void vp8l_engine_free(vp8l_engine* l) {
   free(l->h_pal);
   hipFree(l->d_nl[0]); hipFree(l->d_nl[1]); hipFree(l->d_nlapply); hipHostFree(l->h_nlapply);
   hipFree(l->d_tabs); hipFree(l->d_argb); hipFree(l->d_modes); hipFree(l->d_mult);
-  hipFree(l->d_aflag); hipFree(l->d_ops); hipFree(l->d_feat); hipFree(l->d_tl); hipFree(l->d_tn);
+  hipFree(l->d_aflag); hipFree(l->d_pflag); hipFree(l->d_ops); hipFree(l->d_feat); hipFree(l->d_tl); hipFree(l->d_tn);
   hipFree(l->d_hc); hipFree(l->d_assign); hipFree(l->d_ctab); hipFree(l->d_gtile);
   hipFree(l->d_start); hipFree(l->d_bsum); hipFree(l->d_boff); hipFree(l->d_end); hipFree(l->d_out);
   hipFree(l->d_packed); hipFree(l->d_poff); hipFree(l->d_hpack); hipFree(l->d_hoff);
@@ -81,7 +81,9 @@ static vp8l_engine* engine_alloc(const vp8l_params* p, int max_frames, int metho
   l->out_cap = (l->npix * 5 + l->hdr_cap + 255) & ~(size_t)255;
   const size_t N = (size_t)max_frames, np = l->npix;
   for (int i = 0; i < 5; ++i) CHK(hipEventCreate(&l->ev[i]));
-  CHK(hipMalloc((void**)&l->d_tabs, (4097 + 1024) * sizeof(int32_t)));
+  CHK(hipMalloc((void**)&l->d_tabs, VP8L_TAB_WORDS * sizeof(int32_t)));
+  CHK(hipMemcpy(l->d_tabs + VP8L_TAB_FSLOG, vp8l_float_tables(), 512 * sizeof(float),
+                hipMemcpyHostToDevice));
   CHK(hipMemcpy(l->d_tabs, vp8l_nlogn_table(), 4097 * sizeof(int32_t), hipMemcpyHostToDevice));
   CHK(hipMemcpy(l->d_tabs + 4097, vp8l_flog2_table(), 1024 * sizeof(int32_t),
                 hipMemcpyHostToDevice));
@@ -143,6 +145,7 @@ static vp8l_engine* engine_alloc(const vp8l_params* p, int max_frames, int metho
   CHK(hipMalloc((void**)&l->d_modes, N * l->ntt));
   CHK(hipMalloc((void**)&l->d_mult, N * l->ntt * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&l->d_aflag, N * sizeof(uint32_t)));
+  CHK(hipMalloc((void**)&l->d_pflag, N * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&l->d_feat, N * l->nht * sizeof(int64_t)));
   CHK(hipMalloc((void**)&l->d_tl, N * l->nht * VP8L_TILE_CAP(l->p.hb) * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&l->d_tn, N * l->nht * sizeof(uint32_t)));
@@ -190,8 +193,14 @@ vp8l_engine* vp8l_engine_new(int w, int h, int max_frames, int method, int alpha
 
 void vp8l_engine_set_near_lossless(vp8l_engine* l, int quality) {
   const int bits = quality >= 100 ? 0 : 5 - quality / 20;   /* VP8LNearLosslessBits */
-  /* VP8ApplyNearLossless leaves pictures under 64x64 or 3 rows as they are */
+  /* VP8ApplyNearLossless leaves pictures under 64x64 or 3 rows as they are;
+   * the predictor's quantisation (spatial modes) has no such exception */
   l->nl_bits = ((l->p.w < 64 && l->p.h < 64) || l->p.h < 3 || l->p.alpha) ? 0 : bits;
+  l->p.nlq_bits = l->p.alpha ? 0 : bits;
+}
+
+void vp8l_engine_set_exact(vp8l_engine* l, int exact) {
+  if (!l->p.alpha) l->p.exact = exact != 0;
 }
 
 static void route(const vp8l_engine* l, int f, const vp8l_engine** e, int* s) {
@@ -274,7 +283,8 @@ int vp8l_engine_run(struct WebPGpuBatch* b, const uint8_t* rgba, size_t fstride,
 /* One engine's stages over its n slots. identity: slot f = frame f (the
  * ALPH engine); else h_fidx / h_fmode (and the palettes) were filled. */
 static int pipeline(vp8l_engine* l, hipStream_t st, int threads, const uint8_t* rgba,
-                    size_t fstride, int rstride, int n, int identity, double timings[10]) {
+                    size_t fstride, int rstride, int n, int identity, const uint32_t* ehist,
+                    double timings[10]) {
   const size_t N = (size_t)n;
   double t0 = now_us(), t1, t2, t3, t4, t5;
   vp8l_params p = l->p;
@@ -292,10 +302,11 @@ static int pipeline(vp8l_engine* l, hipStream_t st, int threads, const uint8_t* 
     CHK(hipMemcpyAsync(l->d_psidx, l->h_psidx, N * VP8L_MAX_PALETTE, hipMemcpyHostToDevice, st));
     CHK(hipMemcpyAsync(l->d_npal, l->h_npal, N * sizeof(int), hipMemcpyHostToDevice, st));
   }
-  int nl_any = 0;   /* model: near_lossless_applies (spatial modes from 2 bits on) */
+  int nl_any = 0;   /* VP8ApplyNearLossless: direct / subtract-green frames only
+                       (vp8l_enc.c:1537-1538; the spatial ones quantise in L1a) */
   if (l->nl_bits && !p.palette && !identity)
     for (int f = 0; f < n; ++f) {
-      l->h_nlapply[f] = !(l->h_fmode[f] & VP8L_MODE_SPATIAL) || l->nl_bits >= 2;
+      l->h_nlapply[f] = !(l->h_fmode[f] & VP8L_MODE_SPATIAL);
       nl_any |= l->h_nlapply[f];
     }
   if (nl_any) {   /* near-lossless passes into slot-indexed buffers */
@@ -320,8 +331,8 @@ static int pipeline(vp8l_engine* l, hipStream_t st, int threads, const uint8_t* 
     for (int f = 0; f < n; ++f) sg_mask |= identity ? 1 : 1 << ((l->h_fmode[f] >> 1) & 1);
     /* the transform search scores against the input frame's L0 histograms */
     if (!vp8l_launch_transform(rgba, fstride, rstride, &p, fidx_in, identity ? NULL : l->d_fidx,
-                               identity ? NULL : l->d_fmode, l->d_ehist, l->d_tabs, sg_mask,
-                               l->d_argb, l->d_modes, l->d_mult, l->d_aflag, st))
+                               identity ? NULL : l->d_fmode, ehist, l->d_tabs, sg_mask,
+                               l->d_argb, l->d_modes, l->d_pflag, l->d_mult, l->d_aflag, st))
       goto fail;
   }
   CHK(hipEventRecord(l->ev[1], st));
@@ -488,16 +499,38 @@ int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t*
                      hipMemcpyDeviceToHost, st));
   CHK(hipStreamSynchronize(st));
   {
-    const int ntiles = l->ntt;
-    int cnt[5] = {0, 0, 0, 0, 0};   /* [0..3] palette engines by xbits, [4] root */
+    /* [0..3] palette engines by xbits, [4] root, [5] sub[4]: non-palette
+       frames whose colours fit a palette take the palette histogram bits */
+    int cnt[6] = {0, 0, 0, 0, 0, 0};
+    const int ntt_pal = sub_sample(l->p.w, vp8l_transform_bits(l->method,
+                                   vp8l_histo_bits_palette(l->method, l->p.w, l->p.h)));
+    const int ntiles_pal = ntt_pal * sub_sample(l->p.h, vp8l_transform_bits(l->method,
+                                   vp8l_histo_bits_palette(l->method, l->p.w, l->p.h)));
     uint8_t* mode = (uint8_t*)malloc(N);
     if (!mode) goto fail;
     for (int f = 0; f < n; ++f) {
       const uint32_t* sc = l->h_scan + (size_t)f * VP8L_PAL_STRIDE;
       const int npal = sc[0] <= VP8L_MAX_PALETTE ? (int)sc[0] : 0;
-      mode[f] = (uint8_t)vp8l_entropy_choice(l->h_ehist + (size_t)f * VP8L_EHIST, npal, ntiles);
+      const int ntiles = npal ? ntiles_pal : l->ntt;
+      /* method 0 skips AnalyzeEntropy: palette or spatial + subtract green (vp8l_enc.c:302-308) */
+      mode[f] = l->p.low_effort ? (uint8_t)(npal ? VP8L_MODE_PALETTE : VP8L_MODE_SPATIAL_SUBGREEN)
+                                : (uint8_t)vp8l_entropy_choice(l->h_ehist + (size_t)f * VP8L_EHIST,
+                                                               npal, ntiles);
       if (mode[f] == VP8L_MODE_PALETTE) cnt[xbits_of(npal)]++;
-      else cnt[4]++;
+      else cnt[npal ? 5 : 4]++;
+    }
+    if (cnt[5] && !(l->sub[4] && l->sub[4]->max_frames >= cnt[5])) {
+      vp8l_engine_free(l->sub[4]);
+      vp8l_params pp;
+      vp8l_setup_params_palette_hb(&pp, l->p.w, l->p.h, cnt[5], l->method, l->p.alpha);
+      l->sub[4] = engine_alloc(&pp, cnt[5], l->method, 0);
+      if (!l->sub[4]) { free(mode); goto fail; }
+    }
+    if (l->sub[4]) {   /* the root's per-call settings */
+      l->sub[4]->nl_bits = l->nl_bits;
+      l->sub[4]->p.nlq_bits = l->p.nlq_bits;
+      l->sub[4]->p.exact = l->p.exact;
+      l->sub[4]->p.low_effort = l->p.low_effort;
     }
     for (int xb = 0; xb < 4; ++xb) {
       if (!cnt[xb] || (l->sub[xb] && l->sub[xb]->max_frames >= cnt[xb])) continue;
@@ -507,17 +540,18 @@ int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t*
       l->sub[xb] = engine_alloc(&pp, cnt[xb], l->method, 0);
       if (!l->sub[xb]) { free(mode); goto fail; }
     }
-    int used[5] = {0, 0, 0, 0, 0};
+    int used[6] = {0, 0, 0, 0, 0, 0};
     for (int f = 0; f < n; ++f) {
+      const uint32_t* sc = l->h_scan + (size_t)f * VP8L_PAL_STRIDE;
       if (mode[f] != VP8L_MODE_PALETTE) {
-        const int s = used[4]++;
-        l->h_fidx[s] = f;
-        l->h_fmode[s] = mode[f];
-        l->route_eng[f] = l;
+        vp8l_engine* e = sc[0] <= VP8L_MAX_PALETTE ? l->sub[4] : l;
+        const int s = used[e == l ? 4 : 5]++;
+        e->h_fidx[s] = f;
+        e->h_fmode[s] = mode[f];
+        l->route_eng[f] = e;
         l->route_slot[f] = s;
         continue;
       }
-      const uint32_t* sc = l->h_scan + (size_t)f * VP8L_PAL_STRIDE;
       const int npal = (int)sc[0], xb = xbits_of(npal);
       vp8l_engine* e = l->sub[xb];
       const int s = used[xb]++;
@@ -543,11 +577,16 @@ int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t*
     }
     free(mode);
     timings[9] = now_us() - t0;   /* L0 analysis + decision */
-    if (used[4] && !pipeline(l, st, threads, rgba, fstride, rstride, used[4], 0, timings))
+    if (used[4] && !pipeline(l, st, threads, rgba, fstride, rstride, used[4], 0, l->d_ehist,
+                             timings))
+      goto fail;
+    if (used[5] && !pipeline(l->sub[4], st, threads, rgba, fstride, rstride, used[5], 0,
+                             l->d_ehist, timings))
       goto fail;
     for (int xb = 0; xb < 4; ++xb)
       if (used[xb] &&
-          !pipeline(l->sub[xb], st, threads, rgba, fstride, rstride, used[xb], 0, timings))
+          !pipeline(l->sub[xb], st, threads, rgba, fstride, rstride, used[xb], 0, l->d_ehist,
+                    timings))
         goto fail;
   }
   return 1;

@@ -19,7 +19,8 @@ typedef struct vp8l_engine {
   /* the root engine decides per frame: its own slots take the spatial /
    * direct / subtract-green frames, palette engines (one per bundling,
    * created on demand) the colour-indexed ones; route_* map frame -> slot */
-  struct vp8l_engine* sub[4];
+  struct vp8l_engine* sub[5];   /* [0..3] palette by bundling, [4] spatial / direct frames
+                                   whose colours fit a palette (palette histogram bits) */
   struct vp8l_engine** route_eng;
   int* route_slot;
   /* device (HBM) */
@@ -44,6 +45,7 @@ typedef struct vp8l_engine {
   uint8_t* d_modes;
   uint32_t* d_mult;
   uint32_t* d_aflag;
+  uint32_t* d_pflag;           /* per slot: residuals from the serial pass (L1a) */
   int64_t* d_feat;
   uint32_t* d_tl;
   uint32_t* d_tn;
@@ -125,6 +127,8 @@ void vp8l_engine_free(vp8l_engine* l);
  * palette are first passed through VP8ApplyNearLossless (own choice for the
  * spatial modes, see oracle/vp8l_model.py:encode) */
 void vp8l_engine_set_near_lossless(vp8l_engine* l, int quality);
+/* WebPConfig::exact for the predictor's residuals (ALPH engines stay exact) */
+void vp8l_engine_set_exact(vp8l_engine* l, int exact);
 int vp8l_engine_run(struct WebPGpuBatch* b, const uint8_t* rgba, size_t fstride, int rstride,
                     int n);
 /* one call on `stream` (hipStream_t) with `threads` host threads; stage

@@ -107,6 +107,8 @@ void vp8l_setup_params(vp8l_params* p, int w, int h, int n, int method, int alph
   memset(p, 0, sizeof(*p));
   p->w = w; p->h = h; p->n = n;
   p->alpha = alpha != 0;
+  p->exact = alpha != 0;   /* the ALPH encoder sets exact (alpha_enc.c:66-72) */
+  p->low_effort = method == 0 && !alpha;
   p->cache_bits = alpha ? 0 : VP8L_MAX_CACHE_BITS;
   p->ow = w;
   p->hb = vp8l_histo_bits(method, w, h);
@@ -145,6 +147,24 @@ int vp8l_plane_dcodes(int w, uint8_t* tab) {
 
 /* the colour-indexing engine: coded width = bundled width, tile bits from
  * GetHistoBits with use_palette on the picture size (vp8l_enc.c:234-245) */
+/* histogram bits of a picture whose colours fit a palette (GetHistoBits
+ * with use_palette, src/enc/vp8l_enc.c:234-245): EncoderAnalyze sets them
+ * (:295-300) whatever entropy mode the frame then takes */
+int vp8l_histo_bits_palette(int method, int w, int h) {
+  int b = 9 - method;
+  while (sub_sample(w, b) * sub_sample(h, b) > VP8L_MAX_HUFF_IMAGE) ++b;
+  return b < 2 ? 2 : b > 9 ? 9 : b;
+}
+
+/* the spatial / direct engine for frames whose colours fit a palette */
+void vp8l_setup_params_palette_hb(vp8l_params* p, int w, int h, int n, int method, int alpha) {
+  vp8l_setup_params(p, w, h, n, method, alpha);
+  p->hb = vp8l_histo_bits_palette(method, w, h);
+  p->tb = vp8l_transform_bits(method, p->hb);
+  const int nht = sub_sample(w, p->hb) * sub_sample(h, p->hb);
+  p->k = nht < VP8L_KMAX ? nht : VP8L_KMAX;
+}
+
 void vp8l_setup_palette_params(vp8l_params* p, int w, int h, int n, int method, int xbits,
                                int alpha) {
   const int pw = sub_sample(w, xbits);
@@ -152,9 +172,7 @@ void vp8l_setup_palette_params(vp8l_params* p, int w, int h, int n, int method, 
   p->palette = 1;
   p->xbits = xbits;
   p->ow = w;
-  int b = 9 - method;
-  while (sub_sample(w, b) * sub_sample(h, b) > VP8L_MAX_HUFF_IMAGE) ++b;
-  p->hb = b < 2 ? 2 : b > 9 ? 9 : b;
+  p->hb = vp8l_histo_bits_palette(method, w, h);
   p->tb = 2;   /* unused: no predictor */
   const int nht = sub_sample(pw, p->hb) * sub_sample(h, p->hb);
   p->k = nht < VP8L_KMAX ? nht : VP8L_KMAX;
@@ -162,14 +180,22 @@ void vp8l_setup_palette_params(vp8l_params* p, int w, int h, int n, int method, 
 
 static int32_t g_nlogn[4097];
 static int32_t g_flog2[1024];
+static float g_ftabs[512];   /* VP8LFastSLog2 / log2 of 0..255 as the reference's float tables */
 static pthread_once_t g_tab_once = PTHREAD_ONCE_INIT;
 static void tables_init(void) {
+  /* kSLog2Table / kLog2Table (src/dsp/lossless_enc.c:28-224) are the float
+   * roundings of v log2 v and log2 v (tests/test_vp8l.py checks all 512) */
+  for (int v = 0; v < 256; ++v) {
+    g_ftabs[v] = v < 2 ? 0.f : (float)(v * log2((double)v));
+    g_ftabs[256 + v] = v < 2 ? 0.f : (float)log2((double)v);
+  }
   g_nlogn[0] = g_nlogn[1] = 0;
   for (int n = 2; n <= 4096; ++n) g_nlogn[n] = (int32_t)floor(n * log2((double)n) * 4096 + 0.5);
   for (int m = 0; m < 1024; ++m) g_flog2[m] = (int32_t)floor(4096 * log2(1 + m / 1024.0) + 0.5);
 }
 const int32_t* vp8l_nlogn_table(void) { pthread_once(&g_tab_once, tables_init); return g_nlogn; }
 const int32_t* vp8l_flog2_table(void) { pthread_once(&g_tab_once, tables_init); return g_flog2; }
+const float* vp8l_float_tables(void) { pthread_once(&g_tab_once, tables_init); return g_ftabs; }
 
 /* ---------------------------------------------------------------- analysis */
 
@@ -590,9 +616,11 @@ int vp8l_build_header(const vp8l_params* p, int has_alpha, int emode, int cache_
       vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 0, 2); vp8l_bw_put(bw, (uint32_t)(tb - 2), 3);
       for (int t = 0; t < ntt; ++t) pix[t] = 0xff000000u | ((uint32_t)modes[t] << 8);
       ok &= write_sub_image(bw, pix, ntt);
-      vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 1, 2); vp8l_bw_put(bw, (uint32_t)(tb - 2), 3);
-      for (int t = 0; t < ntt; ++t) pix[t] = 0xff000000u | (mult[t] & 0xffffffu);
-      ok &= write_sub_image(bw, pix, ntt);
+      if (!p->low_effort) {   /* no cross colour at method 0 (vp8l_enc.c:1525-1526) */
+        vp8l_bw_put(bw, 1, 1); vp8l_bw_put(bw, 1, 2); vp8l_bw_put(bw, (uint32_t)(tb - 2), 3);
+        for (int t = 0; t < ntt; ++t) pix[t] = 0xff000000u | (mult[t] & 0xffffffu);
+        ok &= write_sub_image(bw, pix, ntt);
+      }
     }
   }
   vp8l_bw_put(bw, 0, 1);

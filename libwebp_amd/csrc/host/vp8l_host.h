@@ -28,6 +28,8 @@ size_t vp8l_bw_finish(vp8l_bw* bw);
 /* GetHistoBits / GetTransformBits (src/enc/vp8l_enc.c:234-253), no palette */
 int vp8l_histo_bits(int method, int w, int h);
 int vp8l_transform_bits(int method, int histo_bits);
+int vp8l_histo_bits_palette(int method, int w, int h);
+void vp8l_setup_params_palette_hb(vp8l_params* p, int w, int h, int n, int method, int alpha);
 /* candidate distances and their codes (model: candidate_distances,
  * distance_code); alpha != 0: the ALPH-chunk form (model: alpha_plane) */
 void vp8l_setup_params(vp8l_params* p, int w, int h, int n, int method, int alpha);
@@ -48,6 +50,7 @@ void vp8l_palette_order(uint32_t* pal, int n);
  * table (1024 entries) uploaded to the device */
 const int32_t* vp8l_nlogn_table(void);
 const int32_t* vp8l_flog2_table(void);
+const float* vp8l_float_tables(void);   /* 512 floats: VP8LFastSLog2, log2 of 0..255 */
 
 /* Per-frame header. Inputs: the entropy mode (transforms written), the
  * frame's colour-cache bits, the palette in stored order (palette engine);

@@ -260,6 +260,22 @@ static int report(const WebPPicture* pic, int percent) {
   return 1;
 }
 
+/* the token loop's progress, one call per MB row folded (VP8IteratorProgress,
+ * iterator_enc.c:89-99, between WebPEncode's 20 and 90), deduplicated like
+ * WebPReportProgress (webp_enc.c:317-327) and kept monotone over the passes
+ * of a size / PSNR search (each K3 pass folds the rows from the top again) */
+typedef struct {
+  const WebPPicture* pic;
+  int last;
+} ProgressCtx;
+static int progress_rows(void* ctx, int rows, int total) {
+  ProgressCtx* c = (ProgressCtx*)ctx;
+  const int pct = 20 + (69 * rows) / (total > 0 ? total : 1);   /* 90 follows */
+  if (pct <= c->last) return 1;
+  c->last = pct;
+  return report(c->pic, pct);
+}
+
 static double psnr(uint64_t err, uint64_t size) {
   return (err > 0 && size > 0) ? 10. * log10(255. * 255. * size / err) : 99.;
 }
@@ -284,7 +300,10 @@ static int encode_lossless(const WebPConfig* config, WebPPicture* pic) {
   }
   if (!report(pic, 5)) { free(rgba); return 0; }
   WebPGpuBatch* e = pool_get(config, w, h, 1);
-  if (e) vp8l_engine_set_near_lossless(e->l, config->near_lossless);   /* per call */
+  if (e) {   /* per call */
+    vp8l_engine_set_near_lossless(e->l, config->near_lossless);
+    vp8l_engine_set_exact(e->l, config->exact);
+  }
   int ok = e != NULL && WebPGpuBatchEncodeRGBAHost(e, rgba, (size_t)w * h * 4, 4 * w, 1);
   free(rgba);
   const int err = ok ? WebPGpuBatchError(e, 0) : VP8_ENC_ERROR_OUT_OF_MEMORY;
@@ -347,9 +366,14 @@ int WebPEncode(const WebPConfig* config, WebPPicture* pic) {
   WebPGpuBatch* e = pool_get(config, pic->width, pic->height, 0);
   int ok = e != NULL;
   if (!ok) return set_error(pic, VP8_ENC_ERROR_OUT_OF_MEMORY);
+  ProgressCtx pc = {pic, 20};
+  e->progress = pic->progress_hook ? progress_rows : NULL;
+  e->progress_ctx = &pc;
   ok = vp8g_engine_upload_yuv(e, 0, pic->y, pic->y_stride, pic->u, pic->v, pic->uv_stride,
                               has_alpha ? pic->a : NULL, pic->a_stride) &&
        report(pic, 20) && vp8g_engine_run_yuv(e, 1);
+  e->progress = NULL;
+  e->progress_ctx = NULL;
   int err = ok ? e->err[0] : VP8_ENC_ERROR_OUT_OF_MEMORY;
   uint8_t* out = ok ? e->out[0] : NULL;
   const size_t size = ok ? e->out_size[0] : 0;

@@ -65,6 +65,11 @@ typedef struct {
   int32_t none_finalize;    /* the statistics pass finalises the probabilities */
   int32_t skip_count;       /* >= 0: FinalizeSkipProba's skip count, StatLoop having run as
                                K3 passes (a size / PSNR search); -1: the probe's own */
+  /* WebPEncode progress / abort (iterator_enc.c:89-99): device address of two
+     host-mapped words, or 0: [0] MB rows folded so far (K3 stores it in
+     raster order), [1] non-zero = abort (the host sets it when the progress
+     hook returns 0; K3 stops after the row it folds next, error site 6) */
+  uint64_t progress_addr;
 } vp8g_frame_params;
 
 /* per-frame cost state K3 leaves for the next pass: the probabilities the

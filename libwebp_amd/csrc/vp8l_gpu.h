@@ -88,7 +88,17 @@ typedef struct {
   int palette;                     /* colour-indexing engine: w = packed width */
   int xbits;                       /* palette bundling (0..3) */
   int ow;                          /* picture width (w is the coded width) */
+  int exact;                       /* WebPConfig::exact: no alpha-0 clean-up in the
+                                      predictor's residuals */
+  int nlq_bits;                    /* predictor near-lossless quantisation
+                                      (VP8LNearLosslessBits; 0 = off) */
+  int low_effort;                  /* method 0: predictor 11 everywhere, no cross colour */
 } vp8l_params;
+
+/* the engine's table block (tabs): nlogn 0..4096 (int, 1/4096 bit) | log2
+ * fractions (1024 int) | VP8LFastSLog2 0..255 (float) | log2 0..255 (float) */
+#define VP8L_TAB_FSLOG (4097 + 1024)
+#define VP8L_TAB_WORDS (VP8L_TAB_FSLOG + 512)
 
 /* L0: per frame (rgba frames at fstride bytes, rows at rstride) the 13
  * AnalyzeEntropy histograms into ehist (n x VP8L_EHIST, zeroed by the
@@ -98,16 +108,18 @@ typedef struct {
 int vp8l_launch_scan(const uint8_t* rgba, size_t fstride, int rstride, int w, int h, int n,
                      int plane, uint32_t* ehist, uint32_t* pal, void* stream);
 /* L1: per slot f the input frame fidx[f] (NULL: f); entropy mode fmode[f]
- * (0..3): subtract green (mode & 2), per-tile predictor + cross colour
- * (mode & 1), scored against the L0 histograms ehist of input frame
- * efidx[f] (NULL: f); tabs: the engine's nlogn | log2-fraction tables.
- * sg_mask: bit 0 some slot without subtract green, bit 1 some with.
+ * (0..3): subtract green (mode & 2), per-tile predictor (the reference's
+ * choice, L1a) + cross colour (mode & 1), the latter scored against the L0
+ * histograms ehist of input frame efidx[f] (NULL: f); tabs: the engine's
+ * table block (VP8L_TAB_WORDS). sg_mask: bit 0 some slot without subtract
+ * green, bit 1 some with. pflag (n words): per slot 1 when the residuals
+ * came from the serial pass (near-lossless / alpha-0 clean-up).
  * alpha_flag[f] |= 1 if any alpha != 255. */
 int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rstride,
                           const vp8l_params* p, const int* fidx, const int* efidx,
                           const uint8_t* fmode, const uint32_t* ehist, const int32_t* tabs,
-                          int sg_mask, uint32_t* argb, uint8_t* modes, uint32_t* mult,
-                          uint32_t* alpha_flag, void* stream);
+                          int sg_mask, uint32_t* argb, uint8_t* modes, uint32_t* pflag,
+                          uint32_t* mult, uint32_t* alpha_flag, void* stream);
 /* Near-lossless preprocessing (VP8ApplyNearLossless): passes at bits .. 1
  * from frame fidx[f] of rgba into slot f of buf0 / buf1 (n x w*h*4 each,
  * packed RGBA), slots with apply[f] == 0 copied; *out = the buffer holding

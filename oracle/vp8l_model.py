@@ -214,32 +214,29 @@ def ctd(t, c):
     return (np.asarray(t, dtype=np.int64) * to_s8(c)) >> 5
 
 
-# ---- entropy-scored transform search
+# ---- entropy-scored colour-transform search
 #
-# The reference picks each tile's predictor and colour-transform multipliers
-# by Shannon estimates of the tile's residual histograms against histograms
-# accumulated over the tiles before it (GetBestPredictorForTile,
-# src/enc/predictor_enc.c:299-409; PredictionCostSpatialHistogram :48-58;
-# GetBestGreenToRed / GetBestGreenRedToBlue :573-681 with
-# PredictionCostCrossColor :541-547). Raster-order accumulation makes every
-# tile wait for all earlier ones; here every tile is scored against one
-# histogram set per frame instead -- the residuals of the gradient predictor
-# (mode 12, ClampedAddSubtractFull) over the pixels AnalyzeEntropy keeps
-# (repeats of the raster predecessor or of the pixel above skipped, the role
-# of the reference's "repeated pixels are handled by backward references",
-# :776-786), collected by L0 k_vp8l_entropy next to AnalyzeEntropy's own
-# histograms -- so all tiles choose at once.
+# The reference picks each tile's colour-transform multipliers by Shannon
+# estimates of the tile's histograms against histograms accumulated over the
+# tiles before it (GetBestGreenToRed / GetBestGreenRedToBlue,
+# src/enc/predictor_enc.c:573-681, PredictionCostCrossColor :541-547).
+# Raster-order accumulation makes every tile wait for all earlier ones (and
+# its ~50 dependent candidate evaluations per tile); here every tile is scored
+# against one histogram set per frame instead -- the residuals of the
+# gradient predictor (mode 12, ClampedAddSubtractFull) over the pixels
+# AnalyzeEntropy keeps (repeats of the raster predecessor or of the pixel
+# above skipped, the role of the reference's "repeated pixels are handled by
+# backward references", :776-786), collected by L0 k_vp8l_entropy next to
+# AnalyzeEntropy's own histograms -- so all tiles choose at once. (The
+# predictor itself is the reference's exact choice: residual_image.)
 # Costs are integers in 1/4096 bit:
 #   E(t, a)   = sum_{i: t_i > 0} [slog(t_i) + slog(t_i + a_i) - slog(a_i)]
 #               (minus CombinedShannonEntropy(t, a), lossless_enc.c:403-422,
 #               less the terms that are equal for every candidate)
 #   cost(t)   = -E + 16 * sum_i t_i * SP[i]
 # SP is PredictionCostSpatial (:35-46) as a per-value table: -0.1 w0 for 0,
-# -0.1 e 0.6^(k-1) for +-k, k < 16, rounded to 1/256 bit; the predictor
-# search uses (w0, e) = (1, 0.94), the colour search (3, 2.4).
-SP_PRED = np.zeros(256, dtype=np.int64)
-SP_PRED[[0, 1, 2, 3, 4, 5, 6, 7, 8]] = [-26, -24, -14, -9, -5, -3, -2, -1, -1]
-SP_PRED[[255, 254, 253, 252, 251, 250, 249, 248]] = [-24, -14, -9, -5, -3, -2, -1, -1]
+# -0.1 e 0.6^(k-1) for +-k, k < 16, rounded to 1/256 bit, with (w0, e) =
+# (3, 2.4) for the colour search.
 SP_CC = np.zeros(256, dtype=np.int64)
 SP_CC[list(range(11))] = [-77, -61, -37, -22, -13, -8, -5, -3, -2, -1, -1]
 SP_CC[[256 - k for k in range(1, 11)]] = [-61, -37, -22, -13, -8, -5, -3, -2, -1, -1]
@@ -292,27 +289,6 @@ def accumulated_histograms(argb):
 def tile_index(H, W, tb):
     tw = sub_sample(W, tb)
     return (np.arange(H) >> tb)[:, None] * tw + (np.arange(W) >> tb)[None, :]
-
-
-def choose_predictors(P, preds_res, tb, G):
-    """Per tile the predictor with the smallest cost summed over the four
-    channels (first minimum on ties). preds_res[m]: (H, W, 4) residuals of
-    mode m (fixed modes already in place on row 0 / column 0)."""
-    H, W, _ = P.shape
-    nt = sub_sample(W, tb) * sub_sample(H, tb)
-    tile = tile_index(H, W, tb).ravel()
-    slog_g = slog2_fx(G)
-    costs = []
-    for rm in preds_res:
-        e = 0
-        sp = 0
-        for c in range(4):
-            t = np.bincount(tile * 256 + rm[..., c].ravel(), minlength=nt * 256).reshape(nt, 256)
-            nz = t > 0
-            e = e + np.where(nz, slog2_fx(t) + slog2_fx(t + G[c]) - slog_g[c], 0).sum(axis=-1)
-            sp = sp + (t * SP_PRED).sum(axis=-1)
-        costs.append(16 * sp - e)
-    return np.argmin(np.stack(costs), axis=0)
 
 
 def choose_cross_color(res, tb, H, W, G):
@@ -370,6 +346,291 @@ def choose_cross_color(res, tb, H, W, G):
     return mult, out
 
 
+# ---- the reference's own predictor choice, restated exactly
+#
+# VP8LResidualImage (src/enc/predictor_enc.c:476-516): the tiles in raster
+# order, each taking the first of the 14 predictors with the smallest
+# PredictionCostSpatialHistogram (:47-57) of its residual histograms against
+# the histograms accumulated over the tiles before it (:401-405 adds the
+# chosen predictor's), less kSpatialPredictorBias (15, :24) when it equals
+# the left / above tile's predictor (:388-390); then CopyImageWithPrediction
+# (:414-470) writes the residuals. The costs are float32 sums in the
+# reference's order (numpy float32 rounds after every operation, as the C
+# code built without contraction does), so the choice is the reference's bit
+# for bit. Unless `exact`, GetResidual (:234-292) quantises residuals for
+# near-lossless (NearLossless :190-227, where the 4-neighbourhood of the
+# original is not smooth) and keeps only the alpha residual under alpha 0,
+# each time updating the picture it predicts from: a serial dependency along
+# rows, within a tile for the search and over the frame for the copy. At
+# method 0 every tile takes predictor 11 (kPredLowEffort :25, :488-492) and
+# the plain residuals (PredictBatch :69-91).
+LOG2_F32 = np.array([0.0, 0.0] + [math.log2(v) for v in range(2, 256)], dtype=np.float32)
+SLOG2_F32 = np.array([0.0, 0.0] + [v * math.log2(v) for v in range(2, 256)], dtype=np.float32)
+LOG_2_RECIPROCAL = 1.44269504088896338700465094007086
+SPATIAL_PREDICTOR_BIAS = np.float32(15.0)
+PRED_LOW_EFFORT = 11
+F32 = np.float32
+
+
+def fast_slog2_f32(v):
+    """VP8LFastSLog2 (src/dsp/lossless_common.h:89-91; FastSLog2Slow_C,
+    src/dsp/lossless_enc.c:329-363) as float32, elementwise."""
+    v = np.asarray(v, dtype=np.int64)
+    out = np.zeros(v.shape, dtype=np.float32)
+    small = v < 256
+    out[small] = SLOG2_F32[v[small]]
+    mid = (v >= 256) & (v < 65536)
+    if mid.any():
+        vm = v[mid]
+        log_cnt = np.frexp(vm.astype(np.float64))[1].astype(np.int64) - 1 - 7
+        corr = (23 * (vm & ((1 << log_cnt) - 1))) >> 4
+        t = LOG2_F32[vm >> log_cnt] + log_cnt.astype(np.float32)
+        out[mid] = vm.astype(np.float32) * t + corr.astype(np.float32)
+    big = v >= 65536
+    if big.any():   # libm log, one value at a time (numpy's own log may differ in an ulp)
+        out[big] = np.array([LOG_2_RECIPROCAL * float(x) * math.log(float(x)) for x in v[big]],
+                            dtype=np.float64).astype(np.float32)
+    return out
+
+
+def combined_shannon_f32(X, Y):
+    """VP8LCombinedShannonEntropy (CombinedShannonEntropy_C, src/dsp/
+    lossless_enc.c:403-422; the SSE2 variant adds the same terms in the same
+    order) of each row of X (K, 256) against Y (256,), float32."""
+    X = np.asarray(X, dtype=np.int64)
+    Y = np.asarray(Y, dtype=np.int64)
+    K = X.shape[0]
+    nz = X != 0
+    xy = X + Y[None, :]
+    # the terms subtracted in order: per bin S(x), S(x + y) -- or S(y), 0
+    t = np.zeros((K, 256, 2), dtype=np.float32)
+    t[..., 0] = np.where(nz, fast_slog2_f32(X), fast_slog2_f32(np.broadcast_to(Y, X.shape)))
+    t[..., 1] = np.where(nz, fast_slog2_f32(xy), 0)
+    seq = np.concatenate([np.zeros((K, 1), dtype=np.float32), t.reshape(K, 512)], axis=1)
+    r = np.subtract.accumulate(seq, axis=1, dtype=np.float32)[:, -1]
+    sx = np.where(nz, X, 0).sum(axis=1)
+    sxy = np.where(nz, xy, np.broadcast_to(Y, X.shape)).sum(axis=1)
+    return r + (fast_slog2_f32(sx) + fast_slog2_f32(sxy))
+
+
+def prediction_cost_spatial_f32(counts, weight_0, exp_val):
+    """PredictionCostSpatial (src/enc/predictor_enc.c:34-45), rows of counts (K, 256)."""
+    c = np.asarray(counts, dtype=np.int64)
+    bits = F32(weight_0) * c[:, 0].astype(np.float32)
+    e = F32(exp_val)
+    for i in range(1, 16):
+        bits = bits + e * (c[:, i] + c[:, 256 - i]).astype(np.float32)
+        e = e * F32(0.6)
+    return (-0.1 * bits.astype(np.float64)).astype(np.float32)
+
+
+def prediction_cost_spatial_histogram_f32(acc, tile):
+    """PredictionCostSpatialHistogram (:47-57): acc (4, 256), tile (K, 4, 256)."""
+    tile = np.asarray(tile, dtype=np.int64)
+    r = np.zeros(tile.shape[0], dtype=np.float32)
+    for c in range(4):
+        r = r + prediction_cost_spatial_f32(tile[:, c], 1, 0.94)
+        r = r + combined_shannon_f32(tile[:, c], acc[c])
+    return r
+
+
+def _px_sub(a, b):
+    return (((a | 0x00ff00ff) - (b & 0xff00ff00)) & 0xff00ff00) | \
+           (((a | 0xff00ff00) - (b & 0x00ff00ff)) & 0x00ff00ff)
+
+
+def _px_add(a, b):
+    return (((a & 0xff00ff00) + (b & 0xff00ff00)) & 0xff00ff00) | \
+           (((a & 0x00ff00ff) + (b & 0x00ff00ff)) & 0x00ff00ff)
+
+
+def _px_avg2(a, b):
+    return (((a ^ b) & 0xfefefefe) >> 1) + (a & b)
+
+
+def predict_px(m, L, T, TL, TR):
+    """predict() on packed ARGB ints (src/dsp/lossless.c:103-180)."""
+    if m == 0:
+        return 0xff000000
+    if m <= 4:
+        return (L, T, TR, TL)[m - 1]
+    if m == 5:
+        return _px_avg2(_px_avg2(L, TR), T)
+    if m <= 9:
+        return _px_avg2(*{6: (L, TL), 7: (L, T), 8: (TL, T), 9: (T, TR)}[m])
+    if m == 10:
+        return _px_avg2(_px_avg2(L, TL), _px_avg2(T, TR))
+    cs = [(v >> 24 & 255, v >> 16 & 255, v >> 8 & 255, v & 255) for v in (L, T, TL)]
+    if m == 11:
+        s = sum(abs(l - tl) - abs(t - tl) for l, t, tl in zip(*cs))
+        return T if s <= 0 else L
+    if m == 12:
+        o = [min(max(l + t - tl, 0), 255) for l, t, tl in zip(*cs)]
+    else:
+        a = _px_avg2(L, T)
+        o = []
+        for k, tl in zip((24, 16, 8, 0), cs[2]):
+            ak = a >> k & 255
+            x = ak - tl
+            o.append(min(max(ak + int(x / 2), 0), 255))
+    return (o[0] << 24) | (o[1] << 16) | (o[2] << 8) | o[3]
+
+
+def _nl_component(value, pred, boundary, q):
+    """NearLosslessComponent (src/enc/predictor_enc.c:151-179)."""
+    residual = (value - pred) & 0xff
+    boundary_residual = (boundary - pred) & 0xff
+    lower = residual & ~(q - 1)
+    upper = lower + q
+    bias = int(((boundary - value) & 0xff) < boundary_residual)
+    if residual - lower < upper - residual + bias:
+        if residual > boundary_residual and lower <= boundary_residual:
+            return lower + (q >> 1)
+        return lower
+    if residual <= boundary_residual and upper > boundary_residual:
+        return lower + (q >> 1)
+    return upper & 0xff
+
+
+def near_lossless_residual(value, pred, max_q, max_diff, sg):
+    """NearLossless (src/enc/predictor_enc.c:190-227) on packed ARGB ints."""
+    if max_diff <= 2:
+        return _px_sub(value, pred)
+    q = max_q
+    while q >= max_diff:
+        q >>= 1
+    va = value >> 24
+    if va == 0 or va == 0xff:
+        a = (va - (pred >> 24)) & 0xff
+    else:
+        a = _nl_component(va, pred >> 24, 0xff, q)
+    g = _nl_component((value >> 8) & 0xff, (pred >> 8) & 0xff, 0xff, q)
+    new_green = green_diff = 0
+    if sg:
+        new_green = ((pred >> 8) + g) & 0xff
+        green_diff = (new_green - ((value >> 8) & 0xff)) & 0xff
+    r = _nl_component((((value >> 16) & 0xff) - green_diff) & 0xff, (pred >> 16) & 0xff,
+                      0xff - new_green, q)
+    b = _nl_component(((value & 0xff) - green_diff) & 0xff, pred & 0xff, 0xff - new_green, q)
+    return (a << 24) | (r << 16) | (g << 8) | b
+
+
+def _add_green(v):
+    """AddGreenToBlueAndRed (:113-119) on packed ints / arrays."""
+    g = (v >> 8) & 0xff
+    rb = ((v & 0x00ff00ff) + ((g << 16) | g)) & 0x00ff00ff
+    return (v & 0xff00ff00) | rb
+
+
+def near_lossless_max_diffs(argb, sg):
+    """MaxDiffsForRow (:121-146) for every pixel: the largest channel
+    difference to the 4-neighbours in the original (sub-green undone); 0 on
+    the border, where it is never used."""
+    a = argb.astype(np.int64)
+    if sg:
+        a = _add_green(a)
+    H, W = a.shape
+    md = np.zeros((H, W), dtype=np.int64)
+    if H < 3 or W < 3:
+        return md
+    c = a[1:-1, 1:-1]
+    m = np.zeros(c.shape, dtype=np.int64)
+    for nb in (a[:-2, 1:-1], a[2:, 1:-1], a[1:-1, :-2], a[1:-1, 2:]):
+        for sh in (0, 8, 16, 24):
+            m = np.maximum(m, np.abs(((c >> sh) & 255) - ((nb >> sh) & 255)))
+    md[1:-1, 1:-1] = m
+    return md
+
+
+def _residual_serial(rec, x, y, W, H, mode, max_q, md, sg):
+    """GetResidual's non-exact branch (:243-290) for one pixel of `rec` (a
+    flat list of packed pixels, updated in place); returns the residual."""
+    cur = rec[y * W + x]
+    if y == 0:
+        pred = 0xff000000 if x == 0 else rec[y * W + x - 1]
+    elif x == 0:
+        pred = rec[(y - 1) * W]
+    else:
+        pred = predict_px(mode, rec[y * W + x - 1], rec[(y - 1) * W + x],
+                          rec[(y - 1) * W + x - 1], rec[(y - 1) * W + x + 1])
+    if max_q == 1 or mode == 0 or y == 0 or y == H - 1 or x == 0 or x == W - 1:
+        res = _px_sub(cur, pred)
+    else:
+        res = near_lossless_residual(cur, pred, max_q, int(md[y, x]), sg)
+        cur = _px_add(pred, res)
+        rec[y * W + x] = cur
+    if (cur >> 24) == 0:
+        res &= 0xff000000
+        rec[y * W + x] = pred & 0x00ffffff
+    return res
+
+
+def _plain_residuals(P, H, W, modes_of_px):
+    """residuals of the packed (H, W) image under a per-pixel predictor
+    (fixed modes on row 0 / column 0 applied here)."""
+    Pc = np.stack([(P >> 24) & 255, (P >> 16) & 255, (P >> 8) & 255, P & 255], axis=-1)
+    L, T, TL, TR = neighbours(Pc)
+    fixed = fixed_mode_mask(H, W)
+    mp = np.where(fixed >= 0, fixed, modes_of_px)
+    pr = np.zeros_like(Pc)
+    for m in np.unique(mp):
+        sel = mp == m
+        pr[sel] = predict(int(m), L, T, TL, TR)[sel]
+    return planes_argb((Pc - pr) & 255)
+
+
+def residual_image(argb, tb, low_effort=False, near_q=100, exact=False, sg=False):
+    """VP8LResidualImage (src/enc/predictor_enc.c:476-516): argb (H, W) uint32
+    after subtract green (sg) -> (modes (tiles,), residuals (H, W) uint32)."""
+    argb = np.asarray(argb, dtype=np.uint32)
+    H, W = argb.shape
+    tw, th = sub_sample(W, tb), sub_sample(H, tb)
+    if low_effort:
+        modes = np.full(tw * th, PRED_LOW_EFFORT, dtype=np.int64)
+        return modes, _plain_residuals(argb.astype(np.int64), H, W, PRED_LOW_EFFORT)
+    max_q = 1 << near_lossless_bits(near_q)
+    md = near_lossless_max_diffs(argb, sg) if max_q > 1 else None
+    P = argb.astype(np.int64)
+    transparent = (P >> 24) == 0
+    flat = [int(v) for v in P.ravel()]
+    acc = np.zeros((4, 256), dtype=np.int64)
+    modes = np.zeros(tw * th, dtype=np.int64)
+    pres = [_plain_residuals(P, H, W, m) for m in range(14)]   # the plain case, all tiles
+    for ty in range(th):
+        for tx in range(tw):
+            x0, y0 = tx << tb, ty << tb
+            x1, y1 = min(x0 + (1 << tb), W), min(y0 + (1 << tb), H)
+            serial = not exact and (max_q > 1 or transparent[y0:y1, x0:x1].any())
+            hist = np.zeros((14, 4, 256), dtype=np.int64)
+            for m in range(14):
+                if serial:
+                    rec = list(flat)
+                    res = np.array([_residual_serial(rec, x, y, W, H, m, max_q, md, sg)
+                                    for y in range(y0, y1) for x in range(x0, x1)], dtype=np.int64)
+                else:
+                    res = pres[m][y0:y1, x0:x1].astype(np.int64).ravel()
+                for c, sh in enumerate((24, 16, 8, 0)):
+                    hist[m, c] = np.bincount((res >> sh) & 255, minlength=256)
+            cost = prediction_cost_spatial_histogram_f32(acc, hist)
+            left = modes[ty * tw + tx - 1] if tx > 0 else 0xff
+            above = modes[(ty - 1) * tw + tx] if ty > 0 else 0xff
+            for m in range(14):
+                if m == left:
+                    cost[m] = cost[m] - SPATIAL_PREDICTOR_BIAS
+                if m == above:
+                    cost[m] = cost[m] - SPATIAL_PREDICTOR_BIAS
+            best = int(np.argmin(cost))
+            modes[ty * tw + tx] = best
+            acc += hist[best]
+    tmode = modes[tile_index(H, W, tb)]
+    if exact or (max_q == 1 and not transparent.any()):
+        return modes, _plain_residuals(P, H, W, tmode)
+    rec = list(flat)
+    res = np.array([_residual_serial(rec, x, y, W, H, int(tmode[y, x]), max_q, md, sg)
+                    for y in range(H) for x in range(W)], dtype=np.int64)
+    return modes, res.reshape(H, W).astype(np.uint32)
+
+
 # entropy modes (src/enc/vp8l_enc.c:38-46 EntropyIx): bit 0 = predictor +
 # cross colour, bit 1 = subtract green; 4 = palette
 DIRECT, SPATIAL, SUBGREEN, SPATIAL_SUBGREEN, PALETTE = 0, 1, 2, 3, 4
@@ -389,33 +650,27 @@ def planes_argb(P):
     return ((P[..., 0] << 24) | (P[..., 1] << 16) | (P[..., 2] << 8) | P[..., 3]).astype(np.uint32)
 
 
-def transform_image(rgba, tb, mode=SPATIAL_SUBGREEN, G=None):
-    """Subtract green (mode & 2) -> predictor (per tile the best of 14,
-    choose_predictors) -> cross colour (choose_cross_color), both mode & 1.
-    G: the frame's accumulated histograms (accumulated_histograms of the
-    sub-green input; computed here when not given). Returns (modes (tiles,),
-    mult (tiles,3), residual ARGB uint32 (H, W)); modes/mult are None
-    without the spatial transforms."""
+def transform_image(rgba, tb, mode=SPATIAL_SUBGREEN, G=None, near_q=100, exact=False,
+                    low_effort=False):
+    """Subtract green (mode & 2) -> predictor (the reference's own choice,
+    residual_image, with its near-lossless quantisation below near_q 100 and
+    alpha-0 clean-up unless exact) -> cross colour (choose_cross_color; none
+    at low effort), both mode & 1. G: the frame's accumulated histograms for
+    the colour search (accumulated_histograms of the sub-green input;
+    computed here when not given). Returns (modes (tiles,), mult (tiles,3),
+    residual ARGB uint32 (H, W)); modes/mult are None without the spatial
+    transforms."""
     H, W, _ = rgba.shape
     P = sub_green_planes(rgba, mode)
     if not mode & SPATIAL:
         return None, None, planes_argb(P)
     if G is None:
         G = accumulated_histograms(planes_argb(P))
-    L, T, TL, TR = neighbours(P)
-    fixed = fixed_mode_mask(H, W)
-    preds = [predict(m, L, T, TL, TR) for m in range(14)]
-    fres = np.zeros_like(P)
-    for m in (0, 1, 2):
-        sel = fixed == m
-        fres[sel] = (P[sel] - preds[m][sel]) & 255
-    rms = [np.where((fixed >= 0)[..., None], fres, (P - preds[m]) & 255) for m in range(14)]
-    modes = choose_predictors(P, rms, tb, G)
-    tmode = modes[tile_index(H, W, tb)]
-    res = fres.copy()
-    for m in range(14):
-        sel = (tmode == m) & (fixed < 0)
-        res[sel] = rms[m][sel]
+    modes, r = residual_image(planes_argb(P), tb, low_effort, near_q, exact, bool(mode & SUBGREEN))
+    r = r.astype(np.int64)
+    res = np.stack([(r >> 24) & 255, (r >> 16) & 255, (r >> 8) & 255, r & 255], axis=-1)
+    if low_effort:
+        return modes, np.zeros((len(modes), 3), dtype=np.int64), planes_argb(res)
     mult, res = choose_cross_color(res, tb, H, W, G)
     return modes, mult, planes_argb(res)
 
@@ -1353,16 +1608,10 @@ def near_lossless(argb, quality):
 
 
 def near_lossless_applies(mode, quality):
-    """The reference preprocesses the direct / subtract-green modes with
-    VP8ApplyNearLossless (vp8l_enc.c:1536-1547) and quantises predictor
-    residuals for the spatial ones (predictor_enc.c:473-...), which is a
-    pixel-serial reconstruction this encoder does not reproduce. Here the
-    spatial modes take the preprocessing too from 2 limit bits on (quality <
-    80); at 1 bit it costs more than it saves ahead of the predictors, and
-    those frames stay lossless (inside any error bound)."""
-    if mode == PALETTE:
-        return False
-    return not (mode & SPATIAL) or near_lossless_bits(quality) >= 2
+    """VP8ApplyNearLossless preprocesses the direct / subtract-green modes
+    only (vp8l_enc.c:1536-1547); the spatial ones quantise their residuals
+    inside the predictor (residual_image)."""
+    return mode != PALETTE and not (mode & SPATIAL)
 
 
 def argb_to_rgba(argb):
@@ -1389,14 +1638,26 @@ def bundle(idx, xbits):
     return out.astype(np.uint32)
 
 
+def frame_histo_bits(method, w, h, npal):
+    """EncoderAnalyze's histogram bits (src/enc/vp8l_enc.c:295-300): the
+    palette form whenever the colours fit a palette, whatever entropy mode
+    the frame then takes -- the transform bits follow from them."""
+    return histo_bits_palette(method, w, h) if npal else histo_bits(method, w, h)
+
+
 def entropy_plan(rgba, method):
-    """(entropy mode, palette in stored order or None) of one picture."""
+    """(entropy mode, palette in stored order or None) of one picture; method
+    0 takes the palette when the colours fit one, else spatial + subtract
+    green, without AnalyzeEntropy (vp8l_enc.c:302-308)."""
     H, W, _ = rgba.shape
     argb = to_argb(rgba)
     cols = np.unique(argb)
     npal = len(cols) if len(cols) <= MAX_PALETTE else 0
-    tb = transform_bits(method, histo_bits(method, W, H))
-    mode = analyze_entropy(argb, npal, tb)
+    tb = transform_bits(method, frame_histo_bits(method, W, H, npal))
+    if method == 0:
+        mode = PALETTE if npal else SPATIAL_SUBGREEN
+    else:
+        mode = analyze_entropy(argb, npal, tb)
     return mode, (minimize_deltas(cols) if mode == PALETTE else None)
 
 
@@ -1404,7 +1665,7 @@ AUTO_CACHE = -1
 
 
 def encode(rgba, method=4, cache_bits=AUTO_CACHE, kmax=KMAX, return_parts=False,
-           alpha_plane=False, emode=None, near_lossless_q=100):
+           alpha_plane=False, emode=None, near_lossless_q=100, exact=False):
     """rgba: (H, W, 4) uint8 -> .webp bytes (VP8L).
 
     alpha_plane=True: the ALPH-chunk form (src/enc/alpha_enc.c:50-98 +
@@ -1422,8 +1683,10 @@ def encode(rgba, method=4, cache_bits=AUTO_CACHE, kmax=KMAX, return_parts=False,
     cache_bits AUTO_CACHE: the size from choose_cache_bits after a
     provisional parse with every cache hit of the largest size.
 
-    near_lossless_q < 100: frames that take no palette are first passed
-    through near_lossless when near_lossless_applies (see there)."""
+    near_lossless_q < 100: direct / subtract-green frames are first passed
+    through near_lossless, spatial ones quantise inside the predictor.
+    exact: no alpha-0 clean-up in the predictor (the ALPH form is exact).
+    Method 0 (low effort): predictor 11 everywhere and no cross colour."""
     if alpha_plane:
         a = np.asarray(rgba, dtype=np.uint8)
         rgba = np.zeros(a.shape + (4,), dtype=np.uint8)
@@ -1445,13 +1708,17 @@ def encode(rgba, method=4, cache_bits=AUTO_CACHE, kmax=KMAX, return_parts=False,
         tb = 0
         modes = mult = None
     else:
-        hb = histo_bits(method, W, H)
+        ncol = len(np.unique(to_argb(rgba)))
+        hb = frame_histo_bits(method, W, H, ncol if ncol <= MAX_PALETTE else 0)
         tb = transform_bits(method, hb)
         # the transform search's histograms: L0's, i.e. of the input picture
         G = accumulated_histograms(planes_argb(sub_green_planes(rgba, mode)))
         if near_lossless_q < 100 and not alpha_plane and near_lossless_applies(mode, near_lossless_q):
             rgba = argb_to_rgba(near_lossless(to_argb(rgba), near_lossless_q))
-        modes, mult, argb = transform_image(rgba, tb, mode, G)
+        low_effort = method == 0 and not alpha_plane
+        modes, mult, argb = transform_image(rgba, tb, mode, G,
+                                            100 if alpha_plane else near_lossless_q,
+                                            exact or alpha_plane, low_effort)
     PW = argb.shape[1]
     dists = candidate_distances(PW)
     lens = match_lengths(argb, dists)
@@ -1521,9 +1788,10 @@ def encode(rgba, method=4, cache_bits=AUTO_CACHE, kmax=KMAX, return_parts=False,
         if mode & SPATIAL:
             bw.put(1, 1); bw.put(0, 2); bw.put(tb - 2, 3)
             write_sub_image(bw, [0xFF000000 | (int(m) << 8) for m in modes])
-            bw.put(1, 1); bw.put(1, 2); bw.put(tb - 2, 3)
-            write_sub_image(bw, [0xFF000000 | ((int(c[2]) & 255) << 16) |
-                                 ((int(c[1]) & 255) << 8) | (int(c[0]) & 255) for c in mult])
+            if not (method == 0 and not alpha_plane):   # no cross colour at method 0
+                bw.put(1, 1); bw.put(1, 2); bw.put(tb - 2, 3)
+                write_sub_image(bw, [0xFF000000 | ((int(c[2]) & 255) << 16) |
+                                     ((int(c[1]) & 255) << 8) | (int(c[0]) & 255) for c in mult])
     bw.put(0, 1)   # no more transforms
     if cache_bits:
         bw.put(1, 1); bw.put(cache_bits, 4)
@@ -1587,6 +1855,22 @@ def riff_chunks(data):
         n = struct.unpack("<I", data[pos + 4:pos + 8])[0]
         out.append((tag, data[pos + 8:pos + 8 + n]))
         pos += 8 + n + (n & 1)
+    return out
+
+
+def vp8l_transforms(data):
+    """The transform types a VP8L stream opens with (src/dec/vp8l_dec.c
+    :1330-1380: 0 predictor, 1 cross colour, 2 subtract green, 3 colour
+    indexing), read up to the first one that carries data."""
+    payload = dict(riff_chunks(data))[b"VP8L"]
+    bits = int.from_bytes(payload[5:16], "little")
+    pos, out = 0, []
+    while (bits >> pos) & 1:
+        t = (bits >> (pos + 1)) & 3
+        out.append(t)
+        pos += 3
+        if t != 2:
+            break
     return out
 
 

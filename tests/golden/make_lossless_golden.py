@@ -10,7 +10,11 @@ decode-exact + size within a tolerance of these.
 
 Near-lossless cases: the SHA-256 of the reference's VP8ApplyNearLossless
 output (src/enc/near_lossless_enc.c, exported by the reference build) as
-little-endian ARGB words, and the size of its `-near_lossless q` encode.
+little-endian ARGB words, the size of its `-near_lossless q` encode, the
+SHA-256 of that stream decoded (RGBA) and the transforms it carries.
+Residual-image cases: VP8LResidualImage (the predictor choice and the
+residuals, near-lossless quantisation and alpha-0 clean-up included) on
+sub-green / plain ARGB: the chosen predictors and the residuals' SHA-256.
 """
 import ctypes
 import hashlib
@@ -39,7 +43,35 @@ NL_CASES = [
     # kind, w, h, frame, near_lossless quality
     ("syn", 96, 80, 0, 60), ("syn", 200, 130, 2, 0), ("syn", 200, 130, 2, 99),
     ("q7", 120, 90, 3, 40), ("syn", 64, 3, 1, 20), ("syn", 63, 63, 4, 0), ("syn", 320, 240, 5, 80),
+    ("q16", 160, 120, 3, 40), ("syn", 256, 192, 6, 20), ("synt", 128, 96, 1, 60),
 ]
+
+# VP8LResidualImage (src/enc/predictor_enc.c:476-516) called directly:
+# (kind, w, h, frame, transform bits, near_lossless, exact, subtract green)
+RESID_CASES = [
+    ("syn", 96, 80, 0, 5, 100, 0, 1), ("syn", 130, 70, 3, 4, 100, 0, 0),
+    ("syn", 160, 128, 2, 5, 60, 0, 1), ("syn", 66, 45, 2, 3, 40, 0, 0),
+    ("synt", 64, 64, 1, 4, 100, 0, 1), ("synt", 64, 64, 1, 4, 100, 1, 1),
+    ("synt", 70, 50, 5, 5, 0, 0, 1), ("syn", 200, 40, 4, 6, 80, 0, 1),
+]
+
+
+def ref_residual_image(lib, argb, tb, near_q, exact, sg):
+    import numpy as np
+    h, w = argb.shape
+    a = np.ascontiguousarray(argb, dtype=np.uint32).copy()
+    scratch = np.zeros(4 * w + 64, dtype=np.uint32)
+    tw, th = (w + (1 << tb) - 1) >> tb, (h + (1 << tb) - 1) >> tb
+    img = np.zeros(tw * th, dtype=np.uint32)
+    pic = abi.WebPPicture()   # progress reporting only: no hook
+    pct = ctypes.c_int(0)
+    lib.VP8LDspInit()
+    lib.VP8LEncDspInit()
+    assert lib.VP8LResidualImage(w, h, tb, 0, a.ctypes.data_as(ctypes.c_void_p),
+                                 scratch.ctypes.data_as(ctypes.c_void_p),
+                                 img.ctypes.data_as(ctypes.c_void_p), near_q, exact, sg,
+                                 ctypes.byref(pic), 0, ctypes.byref(pct))
+    return [int(m) for m in (img >> 8) & 255], a
 
 
 def ref_near_lossless(lib, img, q):
@@ -75,17 +107,28 @@ def main():
                         features=st.lossless_features, cache_bits=st.cache_bits,
                         palette_size=st.palette_size))
         print(out[-1])
+    from oracle import vp8l_model as M
     nl = []
     for kind, w, h, f, q in NL_CASES:
         img = lossless_picture(kind, w, h, f)
         pre = ref_near_lossless(lib, img, q)
         data, _ = abi.encode_rgba(lib, img, 75.0, 4, lossless=1, use_argb=True, near_lossless=q)
+        dec = M.ref_decode(lib, data)
         nl.append(dict(kind=kind, w=w, h=h, frame=f, near_lossless=q,
                        argb_sha256=hashlib.sha256(pre.astype("<u4").tobytes()).hexdigest(),
-                       size=len(data)))
+                       decoded_sha256=hashlib.sha256(dec.tobytes()).hexdigest(),
+                       transforms=M.vp8l_transforms(data), size=len(data)))
         print(nl[-1])
+    rs = []
+    for kind, w, h, f, tb, q, ex, sg in RESID_CASES:
+        img = lossless_picture(kind, w, h, f)
+        argb = M.planes_argb(M.sub_green_planes(img, M.SUBGREEN if sg else M.DIRECT))
+        modes, res = ref_residual_image(lib, argb, tb, q, ex, sg)
+        rs.append(dict(kind=kind, w=w, h=h, frame=f, tb=tb, near_lossless=q, exact=ex,
+                       subtract_green=sg, modes=modes,
+                       residual_sha256=hashlib.sha256(res.astype("<u4").tobytes()).hexdigest()))
+        print({k: v for k, v in rs[-1].items() if k != "modes"})
     from test_alpha import alpha_frame, logo_frame
-    from oracle import vp8l_model as M
     al = []
     for kind, w, h, f, tol in ALPH_CASES:
         img = (logo_frame if kind == "logo" else alpha_frame)(w, h, f)
@@ -95,7 +138,7 @@ def main():
         print(al[-1])
     json.dump({"generator": "tests/golden/make_lossless_golden.py",
                "reference": "libwebp 1.3.2 (oracle/_ref), -lossless -m 4 -q 75",
-               "cases": out, "near_lossless": nl, "alph": al},
+               "cases": out, "near_lossless": nl, "residual_image": rs, "alph": al},
               open(os.path.join(HERE, "lossless_kat.json"), "w"), indent=1)
 
 

@@ -1,0 +1,63 @@
+"""WebPEncode's progress hook and user abort (reference
+src/enc/webp_enc.c:317-327 WebPReportProgress, iterator_enc.c:89-99 per MB
+row, webp_enc.c:330-410 the 5/20/90/100 milestones).
+
+The GPU engine publishes the MB rows K3 has folded in a host-mapped word the
+calling thread polls; a hook returning 0 raises the abort word K3 checks
+after each row fold, the call fails with VP8_ENC_ERROR_USER_ABORT and the
+engine stays usable (the next call's output is bit-exact)."""
+import hashlib
+
+import pytest
+
+from libwebp_amd.synth import syn_v1
+
+pytestmark = pytest.mark.gpu
+
+
+def _kat(kat, w, f):
+    return next(c["sha256"] for c in kat["survey"] if c["w"] == w and c["frame"] == f)
+
+
+def test_progress_monotone_and_output_unchanged(gpu, kat):
+    img = syn_v1(1920, 1080, 0)
+    seen = []
+    out = gpu.encode_rgba(img, quality=75.0, method=4, progress=lambda p: seen.append(p) or True)
+    assert hashlib.sha256(out).hexdigest() == _kat(kat, 1920, 0)
+    assert seen[-1] == 100 and 20 in seen and 90 in seen
+    assert seen == sorted(seen) and len(seen) == len(set(seen)), seen
+    assert all(0 <= p <= 100 for p in seen)
+
+
+def test_progress_rows_reported(gpu):
+    """a 4K frame runs long enough for row progress between 20 and 90"""
+    img = syn_v1(3840, 2160, 3)
+    seen = []
+    gpu.encode_rgba(img, quality=75.0, method=4, progress=lambda p: seen.append(p) or True)
+    mid = [p for p in seen if 20 < p < 90]
+    assert mid, seen
+    assert seen == sorted(seen), seen
+
+
+@pytest.mark.parametrize("stop_at", [20, 21, 90])
+def test_user_abort_then_reuse(gpu, kat, stop_at):
+    img = syn_v1(1920, 1080, 1)
+    calls = []
+
+    def hook(p):
+        calls.append(p)
+        return p < stop_at
+
+    with pytest.raises(RuntimeError, match="USER_ABORT"):
+        gpu.encode_rgba(img, quality=75.0, method=4, progress=hook)
+    assert calls[-1] >= stop_at and all(p < stop_at for p in calls[:-1]), calls
+    assert 100 not in calls
+    # the pooled engine encodes the next picture bit-exactly
+    out = gpu.encode_rgba(syn_v1(1920, 1080, 0), quality=75.0, method=4)
+    assert hashlib.sha256(out).hexdigest() == _kat(kat, 1920, 0)
+
+
+def test_user_abort_lossless(gpu):
+    img = syn_v1(512, 512, 0)
+    with pytest.raises(RuntimeError, match="USER_ABORT"):
+        gpu.encode_rgba(img, quality=75.0, method=4, lossless=1, progress=lambda p: False)

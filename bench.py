@@ -268,6 +268,10 @@ def lossless_line(args, world, B, W, H, elapsed, tails, total_bytes):
     l1_bytes = B * (8 * W * H + 5 * ntt)
     l1_s = avg(7) / 1e6
     achieved = l1_bytes / l1_s / 1e9 if l1_s > 0 else 0.0
+    # PMC bytes of one k_vp8l_transform launch of this workload (each of the
+    # two instances encodes half the batch per launch)
+    l1_traffic, l1_tsrc = measured_traffic("k_vp8l_transform", B // max(1, getattr(
+        args, "engines_used", 1)), W, H, args.quality, args.method, lossless=True)
     return {
         "metric": "megapixels/sec encoded (cwebp -lossless -m 4, 1920x1080 batch)",
         "value": round(mp_ / elapsed, 3),
@@ -288,8 +292,15 @@ def lossless_line(args, world, B, W, H, elapsed, tails, total_bytes):
                    "engines_per_gpu": getattr(args, "engines_used", 1)},
         "roofline": {"bound": "hbm", "kernel": "k_vp8l_transform", "achieved": round(achieved, 3),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
-                     "k_ms": round(1e3 * l1_s, 3), "algorithmic_bytes_per_launch": l1_bytes},
+                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": l1_traffic,
+                     "traffic_source": l1_tsrc,
+                     "k_ms": round(1e3 * l1_s, 3), "algorithmic_bytes_per_launch": l1_bytes,
+                     # the per-frame-serial kernels (one wave / one workgroup per
+                     # frame): their share is k_cache_parse_cluster_events below
+                     "per_frame_serial_kernels": ["k_vp8l_cache (one wave per frame)",
+                                                  "k_vp8l_cluster (one workgroup per frame)",
+                                                  "k_vp8l_predsel (one workgroup per frame, "
+                                                  "near-lossless / transparent frames only)"]},
         "stage_ms": {k: round(avg(i) / 1e3, 3) for k, i in
                      (("transform_analysis", 0), ("host_headers", 1), ("bit_writer", 2),
                       ("d2h", 3), ("riff", 4), ("total", 5), ("k_transform_events", 7),
@@ -298,13 +309,15 @@ def lossless_line(args, world, B, W, H, elapsed, tails, total_bytes):
     }
 
 
-def measured_traffic(kernel, B, W, H, quality, method):
+def measured_traffic(kernel, B, W, H, quality, method, lossless=False):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (profiles/hbm_traffic.json: FETCH_SIZE and WRITE_SIZE of one launch of this
-    same default workload, gfx950 corrections applied as documented there), or
-    None for another workload."""
-    path = os.path.join(HERE, "profiles", "hbm_traffic.json")
-    if not os.path.exists(path) or (B, W, H, quality, method) != (256, 1920, 1080, 75.0, 4):
+    (profiles/hbm_traffic.json, profiles/hbm_traffic_lossless.json: FETCH_SIZE
+    and WRITE_SIZE of one launch of this same default workload, gfx950
+    corrections applied as documented there), or None for another workload."""
+    path = os.path.join(HERE, "profiles",
+                        "hbm_traffic_lossless.json" if lossless else "hbm_traffic.json")
+    want = (512 if lossless else 256, 1920, 1080, 75.0, 4)
+    if not os.path.exists(path) or (B, W, H, quality, method) != want:
         return None, None
     d = json.load(open(path))
     k = d["kernels"].get(kernel)

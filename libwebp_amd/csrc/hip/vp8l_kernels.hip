@@ -126,6 +126,27 @@ __device__ __forceinline__ V wave_sum(V v) {
 
 }  // namespace
 
+// Phase cycle accounting only in the diagnostic build (-DVP8L_PS_PROF,
+// libwebp_amd_prof.so; vp8l_prof_phase_cycles): workgroup thread 0 adds the
+// shader-clock delta of each phase to a device-global counter.
+#ifdef VP8L_PS_PROF
+__device__ unsigned long long g_vp8l_prof[16];
+#define PS_STAMP(i)                                                          \
+  do {                                                                      \
+    if (threadIdx.x == 0) {                                                 \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();           \
+      atomicAdd(&g_vp8l_prof[i], t_ - ps_t);                                \
+      ps_t = t_;                                                            \
+    }                                                                       \
+  } while (0)
+#define PS_STAMP_INIT unsigned long long ps_t = __builtin_amdgcn_s_memtime()
+#else
+#define PS_STAMP(i) \
+  do {              \
+  } while (0)
+#define PS_STAMP_INIT
+#endif
+
 // ------------------------------------------------------------------ L1
 
 // The tile's residuals under the predictor L1a chose, then the cross-colour
@@ -150,14 +171,24 @@ struct TransformSmem {
   uint32_t first[T];                 // P(0, y) for the right-edge TR wrap
   struct {
     uint32_t res[T * T];             // the chosen predictor's residuals
-    uint32_t h9[9 * 128];            // colour search: up to 9 candidates, u16 counts
+    uint32_t h9[8 * 128];            // colour search: up to 8 candidates, u16 counts
   } cc;
   long long slogg[4][256];           // slog(G) per channel and value
   uint32_t g[4][256];                // the frame's accumulated histograms (A, R, G, B)
   int32_t frac[1024];                // log2 fraction table (model: FLOG2_FRAC)
   long long cost[16];
+  int32_t ct[4][256];                // cross-entropy cost per channel and residual (model: ce_tables)
+  int32_t pcost[16];                 // the tile's cross-entropy cost per predictor
+  uint32_t nsum[4];
   int best;
 };
+
+// log2(v) in 1/4096 bit for v >= 1 (model: flog2)
+__device__ __forceinline__ int flog2_fx(const int32_t* frac, uint32_t v) {
+  const int e = 31 - __clz((int)v);
+  const uint32_t m = (e >= 10 ? (v >> (e - 10)) : (v << (10 - e))) & 1023;
+  return (e << 12) + frac[m];
+}
 
 // v * log2(v) in 1/4096 bit, 0 for v <= 1 (model: slog2_fx)
 __device__ __forceinline__ long long slog_fx(const int32_t* frac, uint32_t v) {
@@ -197,34 +228,85 @@ __device__ __forceinline__ void hist_add(uint32_t* h, int v) {
   atomicAdd(&h[v >> 1], 1u << ((v & 1) * 16));
 }
 
-// one colour-search step: the cost of each of K multiplier candidates;
-// blue = false: green-to-red (r - ctd(c0, g)); true: blue (b - ctd(c0, g) - ctd(c1, r))
-template <int K, int T, bool BLUE>
-__device__ void cc_eval(TransformSmem<T>& S, int np, const int (&c0)[K], const int (&c1)[K],
-                        long long (&out)[K]) {
+// register fields of the histogram counts (count_res below): five 11-bit
+// fields (values -2..2) up to 32 x 32 tiles, four 13-bit ones (-1..2) for
+// 64 x 64 -- wide enough for a whole wave's sum over a tile of one value
+template <int T>
+struct Hot {
+  static constexpr int NH = T >= 64 ? 4 : 5, FB = T >= 64 ? 13 : 11, OFF = T >= 64 ? 1 : 2;
+  static constexpr uint32_t MASK = (1u << FB) - 1;
+  __device__ static int slot(int v) { return (v + OFF) & 255; }   // < NH: a register field
+  __device__ static int value(int j) { return (j - OFF) & 255; }
+};
+
+// one colour-search step: the costs of KR green-to-red candidates r0[] and
+// KB (green-to-blue, red-to-blue) candidates (b0[], b1[]) -- the two
+// descents are independent (the blue one reads the untransformed red), so
+// their steps share an evaluation
+template <int KR, int KB, int T>
+__device__ void cc_eval(TransformSmem<T>& S, int np, const int (&r0)[KR > 0 ? KR : 1],
+                        const int (&b0)[KB > 0 ? KB : 1], const int (&b1)[KB > 0 ? KB : 1],
+                        long long (&outR)[KR > 0 ? KR : 1], long long (&outB)[KB > 0 ? KB : 1]) {
+  constexpr int K = KR + KB;
   const int tid = threadIdx.x;
   for (int i = tid; i < K * 128; i += 256) S.cc.h9[i] = 0;
   if (tid < K) S.cost[tid] = 0;
   __syncthreads();
-  for (int i = tid; i < np; i += 256) {
-    const uint32_t r = S.cc.res[i];
-    const int g = ch(r, 8), rr = ch(r, 16), bb = ch(r, 0);
+  // one wave per candidate (k = wave, wave + 4, ..) over the tile's pixels:
+  // the five values next to 0 -- most of a good multiplier's residuals --
+  // counted in registers and summed over the wave once, the rest by LDS
+  // atomics (same-bin atomics of a wave serialise)
+  const int wv = tid >> 6;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int v = BLUE ? (bb - ctd(c0[k], g) - ctd(c1[k], rr)) & 255 : (rr - ctd(c0[k], g)) & 255;
-      hist_add(S.cc.h9 + k * 128, v);
+  for (int k = 0; k < K; ++k) {
+    if ((k & 3) != wv) continue;   // wave-uniform
+    uint64_t hot = 0;
+    uint32_t* h = S.cc.h9 + k * 128;
+    for (int i = lane_id(); i < np; i += 64) {
+      const uint32_t r = S.cc.res[i];
+      const int g = ch(r, 8), rr = ch(r, 16), bb = ch(r, 0);
+      const int v = k >= KR ? (bb - ctd(b0[k - KR], g) - ctd(b1[k - KR], rr)) & 255
+                            : (rr - ctd(r0[k], g)) & 255;
+      const int q = Hot<T>::slot(v);
+      hot += q < Hot<T>::NH ? (1ull << (Hot<T>::FB * q)) : 0ull;
+      if (q >= Hot<T>::NH) hist_add(h, v);
     }
+    hot = wave_sum(hot);
+    if (lane_id() == 0)
+#pragma unroll
+      for (int j = 0; j < Hot<T>::NH; ++j) {
+        const uint32_t t = (uint32_t)(hot >> (Hot<T>::FB * j)) & Hot<T>::MASK;
+        const int v = Hot<T>::value(j);
+        if (t) atomicAdd(&h[v >> 1], t << ((v & 1) * 16));
+      }
   }
   __syncthreads();
   long long acc[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) acc[k] = 0;
-  bin_costs<K>(S, S.cc.h9, BLUE ? 3 : 1, kSpCC, acc);
+  if constexpr (KR > 0) {
+    long long a[KR];
+#pragma unroll
+    for (int k = 0; k < KR; ++k) a[k] = 0;
+    bin_costs<KR>(S, S.cc.h9, 1, kSpCC, a);
+#pragma unroll
+    for (int k = 0; k < KR; ++k) acc[k] = a[k];
+  }
+  if constexpr (KB > 0) {
+    long long a[KB];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) a[k] = 0;
+    bin_costs<KB>(S, S.cc.h9 + KR * 128, 3, kSpCC, a);
+#pragma unroll
+    for (int k = 0; k < KB; ++k) acc[KR + k] = a[k];
+  }
   reduce_costs<K>(S, acc);
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < K; ++k)
-    out[k] = S.cost[k] - CC_ZERO_BONUS * ((c0[k] == 0) + (BLUE && c1[k] == 0));
+  for (int k = 0; k < KR; ++k) outR[k] = S.cost[k] - CC_ZERO_BONUS * (r0[k] == 0);
+#pragma unroll
+  for (int k = 0; k < KB; ++k)
+    outB[k] = S.cost[KR + k] - CC_ZERO_BONUS * ((b0[k] == 0) + (b1[k] == 0));
   __syncthreads();   // S.cost is reused by the next step
 }
 
@@ -239,8 +321,9 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
                                                         const uint8_t* __restrict__ fmode,
                                                         const uint32_t* __restrict__ ehist,
                                                         const int32_t* __restrict__ frac_tab,
-                                                        const uint8_t* __restrict__ modes,
+                                                        uint8_t* __restrict__ modes,
                                                         const uint32_t* __restrict__ pflag,
+                                                        const uint8_t* __restrict__ pexact,
                                                         uint32_t* __restrict__ argb_out,
                                                         uint32_t* __restrict__ mult,
                                                         uint32_t* __restrict__ alpha_flag) {
@@ -289,14 +372,24 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
                         VP8L_EH_ACC + (SG ? 5 : 3)};
     for (int i = tid; i < 1024; i += 256) S.frac[i] = frac_tab[i];
     __syncthreads();
+    if (tid < 4) S.nsum[tid] = 0;
+    __syncthreads();
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const uint32_t v = eh[hix[c] * 256 + tid];
       S.g[c][tid] = v;
       S.slogg[c][tid] = slog_fx(S.frac, v);
+      const uint32_t t = wave_sum(v);
+      if (lane_id() == 0) atomicAdd(&S.nsum[c], t);
     }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; ++c)   // model: ce_tables
+      S.ct[c][tid] = flog2_fx(S.frac, 2 * S.nsum[c] + 256) - flog2_fx(S.frac, 2 * S.g[c][tid] + 1);
   }
+  const bool own_pred = !p.low_effort && !(pexact && pexact[f]);   // else L1a's choice
 
+  PS_STAMP_INIT;
   for (int tile = tile0; tile < min(tile0 + L1_TILES, ntt); ++tile) {
     const int x0 = (tile % tiles_x) * T, y0 = (tile / tiles_x) * T;
     const int tw = min(T, W - x0), th = min(T, H - y0);
@@ -348,7 +441,40 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     // the tile's predictor (L1a, the reference's choice) and its residuals:
     // computed here, or, where GetResidual updated the picture (pflag), the
     // serial pass's
-    const int best = modes[(size_t)f * ntt + tile];
+    int best;
+    if (own_pred) {
+      // the cross-entropy choice (model: choose_predictors_ce): every thread
+      // sums the 14 predictors' costs over its pixels, then wave sums
+      if (tid < 16) S.pcost[tid] = 0;
+      int32_t pc[14];
+#pragma unroll
+      for (int m = 0; m < 14; ++m) pc[m] = 0;
+      for (int i = tid; i < np; i += 256) {
+        const int ly = i / tw, lx = i - ly * tw;
+        const int fm = fixed_mode(x0 + lx, y0 + ly);
+        const uint32_t P = at(lx, ly), L = at(lx - 1, ly), T_ = at(lx, ly - 1), TL = at(lx - 1, ly - 1);
+        const uint32_t TR = tr(lx, ly);
+#pragma unroll
+        for (int m = 0; m < 14; ++m) {
+          const uint32_t r = sub_pixels(P, predict(fm >= 0 ? fm : m, L, T_, TL, TR));
+          pc[m] += S.ct[0][r >> 24] + S.ct[1][ch(r, 16)] + S.ct[2][ch(r, 8)] + S.ct[3][ch(r, 0)];
+        }
+      }
+      __syncthreads();   // pcost zeroed
+#pragma unroll
+      for (int m = 0; m < 14; ++m) {
+        const int32_t t = wave_sum(pc[m]);
+        if (lane_id() == 0) atomicAdd(&S.pcost[m], t);
+      }
+      __syncthreads();
+      best = 0;
+#pragma unroll
+      for (int m = 1; m < 14; ++m)
+        if (S.pcost[m] < S.pcost[best]) best = m;
+      if (tid == 0) modes[(size_t)f * ntt + tile] = (uint8_t)best;
+    } else {
+      best = modes[(size_t)f * ntt + tile];
+    }
     uint32_t* out = argb_out + (size_t)f * W * H;
     if (pflag[f]) {
       for (int i = tid; i < np; i += 256) {
@@ -363,61 +489,71 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
                                                        at(lx, ly - 1), at(lx - 1, ly - 1), tr(lx, ly)));
       }
     }
+    PS_STAMP(8);
     // colour search (model: choose_cross_color); none at method 0 (vp8l_enc.c:1525-1526)
     int g2r = 0, g2b = 0, r2b = 0;
     if (!p.low_effort) {
-    {
-      long long bestc;
-      {   // start (0) and the first +-32 step in one evaluation
-        const int c0[3] = {0, -32, 32}, c1[3] = {0, 0, 0};
-        long long v[3];
-        cc_eval<3, T, false>(S, np, c0, c1, v);
-        bestc = v[0];
-        const int k = v[2] < v[1] ? 2 : 1;
-        if (v[k] < bestc) { bestc = v[k]; g2r = c0[k]; }
-      }
-      for (int d = 16; d >= 1; d >>= 1) {
-        const int c0[2] = {g2r - d, g2r + d}, c1[2] = {0, 0};
-        long long v[2];
-        cc_eval<2, T, false>(S, np, c0, c1, v);
-        const int k = v[1] < v[0] ? 1 : 0;
-        if (v[k] < bestc) { bestc = v[k]; g2r = c0[k]; }
-      }
-    }
-    {
-      const int ax0[8] = {0, 0, -1, 1, -1, -1, 1, 1}, ax1[8] = {-1, 1, 0, 0, -1, 1, -1, 1};
-      const int deltas[7] = {16, 16, 8, 4, 2, 2, 2};
-      long long bestc;
-      {   // start (0, 0) and the first delta-16 step in one evaluation
-        int c0[9], c1[9];
-        c0[0] = 0; c1[0] = 0;
+      // green-to-red: start 0, then +-32, 16, .., 1 around the best;
+      // (green-to-blue, red-to-blue): start (0, 0), then the 4 axis steps at
+      // deltas 16, 16, 8, 4, 2, 2, 2 (stopping once a delta-2 step leaves
+      // both at 0); step i of both in one evaluation
+      const int ax0[4] = {0, 0, -1, 1}, ax1[4] = {-1, 1, 0, 0};
+      const int bdel[7] = {16, 16, 8, 4, 2, 2, 2};
+      long long bestr, bestb;
+      {   // the starts and the first steps
+        const int r0[3] = {0, -32, 32};
+        int b0[5], b1[5];
+        b0[0] = 0; b1[0] = 0;
 #pragma unroll
-        for (int a = 0; a < 8; ++a) { c0[a + 1] = ax0[a] * 16; c1[a + 1] = ax1[a] * 16; }
-        long long v[9];
-        cc_eval<9, T, true>(S, np, c0, c1, v);
-        bestc = v[0];
-        int k = 1;
+        for (int a2 = 0; a2 < 4; ++a2) { b0[a2 + 1] = ax0[a2] * 16; b1[a2 + 1] = ax1[a2] * 16; }
+        long long vr[3], vb[5];
+        cc_eval<3, 5, T>(S, np, r0, b0, b1, vr, vb);
+        bestr = vr[0];
+        int k = vr[2] < vr[1] ? 2 : 1;
+        if (vr[k] < bestr) { bestr = vr[k]; g2r = r0[k]; }
+        bestb = vb[0];
+        k = 1;
 #pragma unroll
-        for (int a = 2; a < 9; ++a)
-          if (v[a] < v[k]) k = a;
-        if (v[k] < bestc) { bestc = v[k]; g2b = c0[k]; r2b = c1[k]; }
+        for (int a2 = 2; a2 < 5; ++a2)
+          if (vb[a2] < vb[k]) k = a2;
+        if (vb[k] < bestb) { bestb = vb[k]; g2b = b0[k]; r2b = b1[k]; }
       }
+      bool blue_on = true;
       for (int it = 1; it < 7; ++it) {
-        const int d = deltas[it];
-        int c0[8], c1[8];
+        const int d = bdel[it], dr = 32 >> it;   // red deltas 16, 8, 4, 2, 1, then none
+        int b0[4], b1[4];
 #pragma unroll
-        for (int a = 0; a < 8; ++a) { c0[a] = g2b + ax0[a] * d; c1[a] = r2b + ax1[a] * d; }
-        long long v[8];
-        cc_eval<8, T, true>(S, np, c0, c1, v);
+        for (int a2 = 0; a2 < 4; ++a2) { b0[a2] = g2b + ax0[a2] * d; b1[a2] = r2b + ax1[a2] * d; }
+        long long vb[4];
+        if (dr > 0 && blue_on) {
+          const int r0[2] = {g2r - dr, g2r + dr};
+          long long vr[2];
+          cc_eval<2, 4, T>(S, np, r0, b0, b1, vr, vb);
+          const int k = vr[1] < vr[0] ? 1 : 0;
+          if (vr[k] < bestr) { bestr = vr[k]; g2r = r0[k]; }
+        } else if (dr > 0) {
+          const int r0[2] = {g2r - dr, g2r + dr}, z[1] = {0};
+          long long vr[2], vz[1];
+          cc_eval<2, 0, T>(S, np, r0, z, z, vr, vz);
+          const int k = vr[1] < vr[0] ? 1 : 0;
+          if (vr[k] < bestr) { bestr = vr[k]; g2r = r0[k]; }
+          continue;
+        } else if (blue_on) {
+          const int z[1] = {0};
+          long long vz[1];
+          cc_eval<0, 4, T>(S, np, z, b0, b1, vz, vb);
+        } else {
+          break;
+        }
         int k = 0;
 #pragma unroll
-        for (int a = 1; a < 8; ++a)
-          if (v[a] < v[k]) k = a;
-        if (v[k] < bestc) { bestc = v[k]; g2b = c0[k]; r2b = c1[k]; }
-        if (d == 2 && g2b == 0 && r2b == 0) break;
+        for (int a2 = 1; a2 < 4; ++a2)
+          if (vb[a2] < vb[k]) k = a2;
+        if (vb[k] < bestb) { bestb = vb[k]; g2b = b0[k]; r2b = b1[k]; }
+        if (d == 2 && g2b == 0 && r2b == 0) blue_on = false;
       }
-    }
     }   // !low_effort
+    PS_STAMP(9);
     // final residuals
     __syncthreads();   // every residual of the tile read before any is overwritten
     for (int i = tid; i < np; i += 256) {
@@ -455,17 +591,25 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
 // are the host's (float)(v log2 v), (float)log2 v, equal to the reference's
 // literals (tests/test_vp8l.py checks them against its source).
 #define PS_THREADS 1024
-#define PS_MAXT 64
 #define LOG_2_RECIPROCAL_D 1.44269504088896338700465094007086
 
+
+// histogram / term rows padded by one word / one float4: the cost chains'
+// lanes walk one row each, and unpadded rows would all start in one LDS bank
+#define PS_HS 129
+#define PS_TS 129
+// T: tile size; NCH channels' cost terms at a time (all four up to T = 32,
+// two at T = 64 where the tile itself takes more LDS)
+template <int T>
 struct PredSelSmem {
-  uint32_t src[(PS_MAXT + 2) * (PS_MAXT + 2)];   // rows y0-1..y1, cols x0-1..x1 (original)
-  uint32_t first[PS_MAXT + 1];                   // P(0, y) for y0-1 .. y1-1 (TR wrap)
-  uint8_t maxd[PS_MAXT * PS_MAXT];
-  uint32_t hist[14 * 4 * 128];                   // u16 pairs: [mode][channel][value]
+  static constexpr int NCH = T >= 64 ? 2 : 4;
+  uint32_t src[(T + 2) * (T + 2)];   // rows y0-1..y1, cols x0-1..x1 (original)
+  uint32_t first[T + 1];             // P(0, y) for y0-1 .. y1-1 (TR wrap)
+  uint8_t maxd[T * T];
+  uint32_t hist[14 * 4 * PS_HS];     // u16 pairs: [mode][channel][value], padded rows
   int32_t acc[4][256];
-  float sacc[4][256];                            // FastSLog2(acc)
-  float terms[2][14][256][2];                    // one channel pair's subtrahends, in order
+  float sacc[4][256];                // FastSLog2(acc)
+  float4 terms[NCH][14][PS_TS];      // subtrahends in bin order: (t1, t2) of two bins
   float slog[256], log2t[256];
   float pcs[14][4], cse[14][4];
   int accsum[4];
@@ -554,25 +698,32 @@ __device__ __forceinline__ uint32_t resid_px(uint32_t cur, uint32_t pred, bool q
   return res;
 }
 
-// residual histogram counts with the five most frequent values per channel
-// (0, +-1, +-2) kept in registers: same-bin LDS atomics within a wave
-// serialise, and those values are most of a good predictor's residuals
-__device__ __forceinline__ void count_res(uint32_t res, uint32_t (&hot)[20], uint32_t* h) {
+// residual histogram counts with the most frequent values per channel (0 and
+// its neighbours) kept in registers -- same-bin LDS atomics within a wave
+// serialise, and those values are most of a good predictor's residuals --
+// packed per channel into the fields of a u64: five 11-bit fields (values
+// -2..2) up to 32 x 32 tiles, four 13-bit ones (-1..2) for 64 x 64, wide
+// enough for a whole wave's sum over a tile of one value
+template <int T>
+__device__ __forceinline__ void count_res(uint32_t res, uint64_t (&hot)[4], uint32_t* h) {
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int v = ch(res, 24 - 8 * c);
-    const int k = (v + 2) & 255;   // 254, 255, 0, 1, 2 -> 0..4
-#pragma unroll
-    for (int j = 0; j < 5; ++j) hot[c * 5 + j] += (k == j);
-    if (k >= 5) hist_add(h + c * 128, v);
+    const int k = Hot<T>::slot(v);
+    hot[c] += k < Hot<T>::NH ? (1ull << (Hot<T>::FB * k)) : 0ull;
+    if (k >= Hot<T>::NH) hist_add(h + c * PS_HS, v);
   }
 }
-__device__ __forceinline__ void flush_hot_lane(const uint32_t (&hot)[20], uint32_t* h) {
+template <int T>
+__device__ __forceinline__ void flush_hot(const uint64_t (&hot)[4], uint32_t* h) {
 #pragma unroll
-  for (int i = 0; i < 20; ++i) {
-    const int v = (i % 5 + 254) & 255;
-    if (hot[i]) atomicAdd(&h[(i / 5) * 128 + (v >> 1)], hot[i] << ((v & 1) * 16));
-  }
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int j = 0; j < Hot<T>::NH; ++j) {
+      const uint32_t t = (uint32_t)(hot[c] >> (Hot<T>::FB * j)) & Hot<T>::MASK;
+      const int v = Hot<T>::value(j);
+      if (t) atomicAdd(&h[c * PS_HS + (v >> 1)], t << ((v & 1) * 16));
+    }
 }
 
 // pixel of the input frame as the transform sees it (sub-green when SG)
@@ -582,8 +733,8 @@ __device__ __forceinline__ uint32_t in_px(const uint8_t* img, int rstride, bool 
     const uint32_t g = img[(size_t)y * rstride + x];
     return SG ? (((0u - g) & 255) << 16) | (g << 8) | ((0u - g) & 255) : g << 8;
   }
-  const uint8_t* q = img + (size_t)y * rstride + 4 * x;
-  const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
+  const uint32_t q = *reinterpret_cast<const uint32_t*>(img + (size_t)y * rstride + 4 * x);
+  const uint32_t r = q & 255, g = (q >> 8) & 255, b = (q >> 16) & 255, a = q >> 24;
   return SG ? (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255)
             : (a << 24) | (r << 16) | (g << 8) | b;
 }
@@ -594,11 +745,13 @@ __global__ __launch_bounds__(PS_THREADS) void k_vp8l_predsel(const uint8_t* __re
                                                              vp8l_params p,
                                                              const int* __restrict__ fidx,
                                                              const uint8_t* __restrict__ fmode,
+                                                             const uint8_t* __restrict__ pexact,
                                                              const float* __restrict__ ftabs,
                                                              uint8_t* __restrict__ modes,
                                                              uint32_t* __restrict__ pflag) {
   extern __shared__ __align__(16) uint8_t ps_smem[];
-  PredSelSmem& S = *reinterpret_cast<PredSelSmem*>(ps_smem);
+  using Smem = PredSelSmem<T>;
+  Smem& S = *reinterpret_cast<Smem*>(ps_smem);
   const int tid = threadIdx.x, f = blockIdx.x;
   const int W = p.w, H = p.h;
   const int emode = fmode ? (int)fmode[f] : VP8L_MODE_SPATIAL;
@@ -612,6 +765,7 @@ __global__ __launch_bounds__(PS_THREADS) void k_vp8l_predsel(const uint8_t* __re
     if (tid == 0) pflag[f] = 0;
     return;
   }
+  if (!(pexact && pexact[f])) return;   // L1's cross-entropy choice
   const int max_q = 1 << p.nlq_bits;
   for (int i = tid; i < 256; i += PS_THREADS) { S.slog[i] = ftabs[i]; S.log2t[i] = ftabs[256 + i]; }
   for (int i = tid; i < 1024; i += PS_THREADS) {
@@ -621,6 +775,7 @@ __global__ __launch_bounds__(PS_THREADS) void k_vp8l_predsel(const uint8_t* __re
   if (tid < 4) S.accsum[tid] = 0;
   if (tid == 0) S.any_t = 0;
   const float kBias = 15.f;   // kSpatialPredictorBias (:24)
+  PS_STAMP_INIT;
 
   for (int tile = 0; tile < ntt; ++tile) {
     const int tx = tile % tiles_x, ty = tile / tiles_x;
@@ -641,9 +796,10 @@ __global__ __launch_bounds__(PS_THREADS) void k_vp8l_predsel(const uint8_t* __re
       const int y = y0 - 1 + i;
       S.first[i] = y >= 0 ? in_px<SG>(img, rstride, plane, 0, y) : 0u;
     }
-    for (int i = tid; i < 14 * 4 * 128; i += PS_THREADS) S.hist[i] = 0;
+    for (int i = tid; i < 14 * 4 * PS_HS; i += PS_THREADS) S.hist[i] = 0;
     if (tid == 0) S.serial = 0;
     __syncthreads();
+    PS_STAMP(0);
     if (!p.exact && __any(tr_alpha) && lane_id() == 0) { S.serial = 1; S.any_t = 1; }
     if (!p.exact && max_q > 1) {
       if (tid == 0) S.serial = 1;
@@ -664,16 +820,15 @@ __global__ __launch_bounds__(PS_THREADS) void k_vp8l_predsel(const uint8_t* __re
       }
     }
     __syncthreads();
+    PS_STAMP(1);
     auto at = [&](int lx, int ly) -> uint32_t { return S.src[(ly + 1) * sw + lx + 1]; };
     if (!S.serial) {
       // plain residuals: one wave per mode over the tile's pixels (fixed
       // modes on row 0 / column 0)
       const int m = tid >> 6;
       if (m < 14) {
-        uint32_t hot[20];
-#pragma unroll
-        for (int i = 0; i < 20; ++i) hot[i] = 0;
-        uint32_t* h = S.hist + m * 4 * 128;
+        uint64_t hot[4] = {0, 0, 0, 0};
+        uint32_t* h = S.hist + m * 4 * PS_HS;
         for (int k = lane_id(); k < np; k += 64) {
           const int ly = k / tw, lx = k - ly * tw;
           const int x = x0 + lx, y = y0 + ly;
@@ -682,14 +837,11 @@ __global__ __launch_bounds__(PS_THREADS) void k_vp8l_predsel(const uint8_t* __re
           else if (x == 0) pred = at(lx, ly - 1);
           else pred = predict(m, at(lx - 1, ly), at(lx, ly - 1), at(lx - 1, ly - 1),
                               x + 1 < W ? at(lx + 1, ly - 1) : S.first[ly + 1]);
-          count_res(sub_pixels(at(lx, ly), pred), hot, h);
+          count_res<T>(sub_pixels(at(lx, ly), pred), hot, h);
         }
 #pragma unroll
-        for (int i = 0; i < 20; ++i) {
-          const uint32_t t = wave_sum(hot[i]);
-          const int v = (i % 5 + 254) & 255;
-          if (lane_id() == 0 && t) atomicAdd(&h[(i / 5) * 128 + (v >> 1)], t << ((v & 1) * 16));
-        }
+        for (int c = 0; c < 4; ++c) hot[c] = wave_sum(hot[c]);
+        if (lane_id() == 0) flush_hot<T>(hot, h);
       }
     } else {
       // wavefront: lane (m, r) takes tile row r; T lanes per mode, 64 / T modes per wave
@@ -700,10 +852,8 @@ __global__ __launch_bounds__(PS_THREADS) void k_vp8l_predsel(const uint8_t* __re
       uint32_t out = live ? at(-1, r) : 0u;   // what the row below reads next: left context first
       uint32_t a = 0, b = 0, c = 0;           // the row above at x-1, x, x+1 (r > 0)
       uint32_t L = out, first_rec = 0;
-      uint32_t hot[20];
-#pragma unroll
-      for (int i = 0; i < 20; ++i) hot[i] = 0;
-      uint32_t* h = S.hist + (m < 14 ? m : 0) * 4 * 128;
+      uint64_t hot[4] = {0, 0, 0, 0};
+      uint32_t* h = S.hist + (m < 14 ? m : 0) * 4 * PS_HS;
       const int nsteps = tw + 2 * (th - 1);
       for (int s = 0; s < nsteps; ++s) {
         const uint32_t up = __shfl_up(out, 1);   // row r-1's newest pixel
@@ -727,7 +877,7 @@ __global__ __launch_bounds__(PS_THREADS) void k_vp8l_predsel(const uint8_t* __re
           uint32_t rec;
           const uint32_t res = resid_px(at(lx, r), pred, q, max_q, q ? S.maxd[r * tw + lx] : 0,
                                         SG, rec);
-          count_res(res, hot, h);
+          count_res<T>(res, hot, h);
           if (lx == 0) first_rec = rec;
           L = rec;
           out = rec;
@@ -735,45 +885,55 @@ __global__ __launch_bounds__(PS_THREADS) void k_vp8l_predsel(const uint8_t* __re
           out = x < W ? at(lx, r) : 0u;   // the right context, for the row below's last TR
         }
       }
-      if (live) flush_hot_lane(hot, h);
+      if (live) flush_hot<T>(hot, h);
     }
     __syncthreads();
-    // costs, one channel pair at a time
-    for (int cp = 0; cp < 2; ++cp) {
-      for (int i = tid; i < 2 * 14 * 256; i += PS_THREADS) {
-        const int cc = i / (14 * 256), rem = i - cc * 14 * 256;
-        const int m = rem >> 8, v = rem & 255, c = 2 * cp + cc;
-        const uint32_t x = (S.hist[(m * 4 + c) * 128 + (v >> 1)] >> ((v & 1) * 16)) & 0xffffu;
-        const uint32_t y = (uint32_t)S.acc[c][v];
-        float t1, t2 = 0.f;
-        if (x) {
-          t1 = ps_slog2(x, S.slog, S.log2t);
-          t2 = ps_slog2(x + y, S.slog, S.log2t);
-        } else {
-          t1 = S.sacc[c][v];   // 0 when y == 0
+    PS_STAMP(2);
+    // costs, NCH channels at a time: the subtrahends in parallel, then one
+    // lane per (mode, channel) subtracts them in bin order
+    constexpr int NCH = Smem::NCH;
+    for (int c0 = 0; c0 < 4; c0 += NCH) {
+      for (int i = tid; i < NCH * 14 * 128; i += PS_THREADS) {
+        const int cc = i / (14 * 128), rem = i - cc * 14 * 128;
+        const int m = rem >> 7, v2 = rem & 127, c = c0 + cc;
+        const uint32_t xx = S.hist[(m * 4 + c) * PS_HS + v2];   // bins 2 v2, 2 v2 + 1
+        float4 t;
+        {
+          const uint32_t x = xx & 0xffffu, y = (uint32_t)S.acc[c][2 * v2];
+          t.x = x ? ps_slog2(x, S.slog, S.log2t) : S.sacc[c][2 * v2];   // 0 when y == 0
+          t.y = x ? ps_slog2(x + y, S.slog, S.log2t) : 0.f;
         }
-        S.terms[cc][m][v][0] = t1;
-        S.terms[cc][m][v][1] = t2;
+        {
+          const uint32_t x = xx >> 16, y = (uint32_t)S.acc[c][2 * v2 + 1];
+          t.z = x ? ps_slog2(x, S.slog, S.log2t) : S.sacc[c][2 * v2 + 1];
+          t.w = x ? ps_slog2(x + y, S.slog, S.log2t) : 0.f;
+        }
+        S.terms[cc][m][v2] = t;
       }
       __syncthreads();
-      if (tid < 28) {
-        const int cc = tid / 14, m = tid - cc * 14, c = 2 * cp + cc;
+      PS_STAMP(3);
+      if (tid < NCH * 14) {
+        const int cc = tid / 14, m = tid - cc * 14, c = c0 + cc;
         float rr = 0.f;
-        const float2* tv = reinterpret_cast<const float2*>(&S.terms[cc][m][0][0]);
-        for (int v = 0; v < 256; ++v) {
-          const float2 t = tv[v];
+        const float4* tv = S.terms[cc][m];
+#pragma unroll 16
+        for (int v2 = 0; v2 < 128; ++v2) {
+          const float4 t = tv[v2];
           rr = __fsub_rn(rr, t.x);
           rr = __fsub_rn(rr, t.y);
+          rr = __fsub_rn(rr, t.z);
+          rr = __fsub_rn(rr, t.w);
         }
         const float sxy = __fadd_rn(ps_slog2((uint32_t)np, S.slog, S.log2t),
                                     ps_slog2((uint32_t)(np + S.accsum[c]), S.slog, S.log2t));
         S.cse[m][c] = __fadd_rn(rr, sxy);
         // PredictionCostSpatial(counts, 1, 0.94f) (:34-45)
         auto cnt = [&](int v) -> int {
-          return (int)((S.hist[(m * 4 + c) * 128 + (v >> 1)] >> ((v & 1) * 16)) & 0xffffu);
+          return (int)((S.hist[(m * 4 + c) * PS_HS + (v >> 1)] >> ((v & 1) * 16)) & 0xffffu);
         };
         float bits = __fmul_rn(1.f, (float)cnt(0));
         float e = 0.94f;
+#pragma unroll
         for (int i = 1; i < 16; ++i) {
           bits = __fadd_rn(bits, __fmul_rn(e, (float)(cnt(i) + cnt(256 - i))));
           e = __fmul_rn(e, 0.6f);
@@ -781,6 +941,7 @@ __global__ __launch_bounds__(PS_THREADS) void k_vp8l_predsel(const uint8_t* __re
         S.pcs[m][c] = (float)__dmul_rn(-0.1, (double)bits);
       }
       __syncthreads();
+      PS_STAMP(4);
     }
     if (tid == 0) {
       const int left = tx > 0 ? fm[tile - 1] : 0xff, above = ty > 0 ? fm[tile - tiles_x] : 0xff;
@@ -804,7 +965,7 @@ __global__ __launch_bounds__(PS_THREADS) void k_vp8l_predsel(const uint8_t* __re
       const int best = S.best;
       for (int i = tid; i < 1024; i += PS_THREADS) {
         const int c = i >> 8, v = i & 255;
-        const uint32_t x = (S.hist[(best * 4 + c) * 128 + (v >> 1)] >> ((v & 1) * 16)) & 0xffffu;
+        const uint32_t x = (S.hist[(best * 4 + c) * PS_HS + (v >> 1)] >> ((v & 1) * 16)) & 0xffffu;
         if (x) {
           const int nv = S.acc[c][v] + (int)x;
           S.acc[c][v] = nv;
@@ -813,6 +974,7 @@ __global__ __launch_bounds__(PS_THREADS) void k_vp8l_predsel(const uint8_t* __re
       }
       if (tid < 4) S.accsum[tid] += np;
     }
+    PS_STAMP(5);
   }
   __syncthreads();
   if (tid == 0) pflag[f] = (!p.exact && (max_q > 1 || S.any_t)) ? 1u : 0u;
@@ -1348,12 +1510,6 @@ __device__ __forceinline__ int alph_size(int a, int cb) {
   return a == 0 ? 280 + (cb ? 1 << cb : 0) : a == 4 ? 40 : 256;
 }
 
-__device__ __forceinline__ int flog2_fx(const int32_t* frac, uint32_t v) {
-  // log2(v) in 1/4096 bit, v >= 1 (model: flog2)
-  const int e = 31 - __clz((int)v);
-  const uint32_t m = (e >= 10 ? (v >> (e - 10)) : (v << (10 - e))) & 1023;
-  return (e << 12) + frac[m];
-}
 __device__ __forceinline__ long long flog2_fx64(const int32_t* frac, unsigned long long v) {
   const int e = 63 - __clzll((long long)v);
   const unsigned long long m = (e >= 10 ? (v >> (e - 10)) : (v << (10 - e))) & 1023;
@@ -2200,16 +2356,17 @@ extern "C" int vp8l_launch_scan(const uint8_t* rgba, size_t fstride, int rstride
 
 template <int T, bool SG>
 static int launch_predsel(const uint8_t* rgba, size_t fstride, int rstride, const vp8l_params* p,
-                          const int* fidx, const uint8_t* fmode, const float* ftabs,
-                          uint8_t* modes, uint32_t* pflag, uint32_t* argb, hipStream_t st) {
+                          const int* fidx, const uint8_t* fmode, const uint8_t* pexact,
+                          const float* ftabs, uint8_t* modes, uint32_t* pflag, uint32_t* argb,
+                          hipStream_t st) {
   static bool lds_ok = [] {
     return hipFuncSetAttribute((const void*)k_vp8l_predsel<T, SG>,
                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)sizeof(PredSelSmem)) == hipSuccess;
+                               (int)sizeof(PredSelSmem<T>)) == hipSuccess;
   }();
   if (!lds_ok) return 0;
-  hipLaunchKernelGGL((k_vp8l_predsel<T, SG>), dim3(p->n), dim3(PS_THREADS), sizeof(PredSelSmem),
-                     st, rgba, fstride, rstride, *p, fidx, fmode, ftabs, modes, pflag);
+  hipLaunchKernelGGL((k_vp8l_predsel<T, SG>), dim3(p->n), dim3(PS_THREADS), sizeof(PredSelSmem<T>),
+                     st, rgba, fstride, rstride, *p, fidx, fmode, pexact, ftabs, modes, pflag);
   if (!check_launch()) return 0;
   const size_t row_lds = (size_t)p->w * sizeof(uint32_t);
   static bool lds2_ok = [] {
@@ -2226,8 +2383,9 @@ extern "C" int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rs
                                      const vp8l_params* p, const int* fidx, const int* efidx,
                                      const uint8_t* fmode, const uint32_t* ehist,
                                      const int32_t* tabs, int sg_mask, uint32_t* argb,
-                                     uint8_t* modes, uint32_t* pflag, uint32_t* mult,
-                                     uint32_t* alpha_flag, void* stream) {
+                                     uint8_t* modes, const uint8_t* pexact, int any_exact,
+                                     uint32_t* pflag, uint32_t* mult, uint32_t* alpha_flag,
+                                     void* stream) {
   if (p->tb < 2 || p->tb > 6 || p->w <= 0 || p->h <= 0 || p->n <= 0) return 0;
   if (!p->alpha && !fmode) return 0;
   if (!fmode) sg_mask = 1;
@@ -2236,12 +2394,15 @@ extern "C" int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rs
   hipStream_t st = (hipStream_t)stream;
   const int32_t* frac = tabs + 4097;
   const float* ftabs = reinterpret_cast<const float*>(tabs + VP8L_TAB_FSLOG);
-  // L1a: the predictor of every tile (and the serial residuals where needed)
+  // L1a: the reference's predictor choice for the frames that need it
+  // (pexact, or every frame at method 0), with the serial residuals
   CHK_LAUNCH(hipMemsetAsync(pflag, 0, (size_t)p->n * sizeof(uint32_t), st));
-#define L1A(T, SG) \
-  if (!launch_predsel<T, SG>(rgba, fstride, rstride, p, fidx, fmode, ftabs, modes, pflag, argb, st)) return 0
+#define L1A(T, SG)                                                                                \
+  if (!launch_predsel<T, SG>(rgba, fstride, rstride, p, fidx, fmode, pexact, ftabs, modes, pflag, \
+                             argb, st))                                                           \
+  return 0
   for (int sg = 0; sg < 2; ++sg) {
-    if (!((sg_mask >> sg) & 1)) continue;
+    if (!((sg_mask >> sg) & 1) || !(any_exact || p->low_effort)) continue;
     switch (p->tb) {
       case 2: if (sg) { L1A(4, true); } else { L1A(4, false); } break;
       case 3: if (sg) { L1A(8, true); } else { L1A(8, false); } break;
@@ -2253,8 +2414,8 @@ extern "C" int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rs
 #undef L1A
 #define L1(T, SG)                                                                             \
   hipLaunchKernelGGL((k_vp8l_transform<T, SG>), grid, dim3(256), 0, st, rgba, fstride, rstride, \
-                     *p, fidx, efidx, fmode, ehist, frac, (const uint8_t*)modes,                \
-                     (const uint32_t*)pflag, argb, mult, alpha_flag)
+                     *p, fidx, efidx, fmode, ehist, frac, modes, (const uint32_t*)pflag, pexact, \
+                     argb, mult, alpha_flag)
   for (int sg = 0; sg < 2; ++sg) {
     if (!((sg_mask >> sg) & 1)) continue;
     switch (p->tb) {
@@ -2406,3 +2567,16 @@ extern "C" int vp8l_launch_pack(const uint8_t* out, size_t out_cap, const uint64
                      poff, end_bit, packed);
   return check_launch();
 }
+
+#ifdef VP8L_PS_PROF
+// diagnostic build only: the phase cycle counters (L1a phases 0-5, L1 8-9)
+extern "C" __attribute__((visibility("default"))) int vp8l_prof_phase_cycles(
+    unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vp8l_prof), sizeof(g_vp8l_prof)) != hipSuccess) return 0;
+  if (reset) {
+    static const unsigned long long zero[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_vp8l_prof), zero, sizeof(zero)) != hipSuccess) return 0;
+  }
+  return 1;
+}
+#endif

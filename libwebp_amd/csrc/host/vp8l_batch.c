@@ -48,7 +48,8 @@ void vp8l_engine_free(vp8l_engine* l) {
   free(l->h_pal);
   hipFree(l->d_nl[0]); hipFree(l->d_nl[1]); hipFree(l->d_nlapply); hipHostFree(l->h_nlapply);
   hipFree(l->d_tabs); hipFree(l->d_argb); hipFree(l->d_modes); hipFree(l->d_mult);
-  hipFree(l->d_aflag); hipFree(l->d_pflag); hipFree(l->d_ops); hipFree(l->d_feat); hipFree(l->d_tl); hipFree(l->d_tn);
+  hipFree(l->d_aflag); hipFree(l->d_pflag); hipFree(l->d_pexact); hipHostFree(l->h_pexact);
+  hipFree(l->d_ops); hipFree(l->d_feat); hipFree(l->d_tl); hipFree(l->d_tn);
   hipFree(l->d_hc); hipFree(l->d_assign); hipFree(l->d_ctab); hipFree(l->d_gtile);
   hipFree(l->d_start); hipFree(l->d_bsum); hipFree(l->d_boff); hipFree(l->d_end); hipFree(l->d_out);
   hipFree(l->d_packed); hipFree(l->d_poff); hipFree(l->d_hpack); hipFree(l->d_hoff);
@@ -146,6 +147,8 @@ static vp8l_engine* engine_alloc(const vp8l_params* p, int max_frames, int metho
   CHK(hipMalloc((void**)&l->d_mult, N * l->ntt * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&l->d_aflag, N * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&l->d_pflag, N * sizeof(uint32_t)));
+  CHK(hipMalloc((void**)&l->d_pexact, N));
+  CHK(hipHostMalloc((void**)&l->h_pexact, N, 0));
   CHK(hipMalloc((void**)&l->d_feat, N * l->nht * sizeof(int64_t)));
   CHK(hipMalloc((void**)&l->d_tl, N * l->nht * VP8L_TILE_CAP(l->p.hb) * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&l->d_tn, N * l->nht * sizeof(uint32_t)));
@@ -292,9 +295,12 @@ static int pipeline(vp8l_engine* l, hipStream_t st, int threads, const uint8_t* 
   const int* fidx_in = identity ? NULL : l->d_fidx;
   for (int f = 0; f < n; ++f) l->err[f] = VP8_ENC_OK;
   CHK(hipMemsetAsync(l->d_aflag, 0, N * sizeof(uint32_t), st));
+  int any_exact = 0;
   if (!identity) {
     CHK(hipMemcpyAsync(l->d_fidx, l->h_fidx, N * sizeof(int), hipMemcpyHostToDevice, st));
     CHK(hipMemcpyAsync(l->d_fmode, l->h_fmode, N, hipMemcpyHostToDevice, st));
+    for (int f = 0; f < n; ++f) any_exact |= l->h_pexact[f];
+    CHK(hipMemcpyAsync(l->d_pexact, l->h_pexact, N, hipMemcpyHostToDevice, st));
   }
   if (p.palette) {
     CHK(hipMemcpyAsync(l->d_psort, l->h_psort, N * VP8L_MAX_PALETTE * sizeof(uint32_t),
@@ -332,7 +338,8 @@ static int pipeline(vp8l_engine* l, hipStream_t st, int threads, const uint8_t* 
     /* the transform search scores against the input frame's L0 histograms */
     if (!vp8l_launch_transform(rgba, fstride, rstride, &p, fidx_in, identity ? NULL : l->d_fidx,
                                identity ? NULL : l->d_fmode, ehist, l->d_tabs, sg_mask,
-                               l->d_argb, l->d_modes, l->d_pflag, l->d_mult, l->d_aflag, st))
+                               l->d_argb, l->d_modes, identity ? NULL : l->d_pexact, any_exact,
+                               l->d_pflag, l->d_mult, l->d_aflag, st))
       goto fail;
   }
   CHK(hipEventRecord(l->ev[1], st));
@@ -345,12 +352,18 @@ static int pipeline(vp8l_engine* l, hipStream_t st, int threads, const uint8_t* 
        * coded image, cache sizes, parse ops and cache bits */
     const char* dump = getenv("LIBWEBP_AMD_VP8L_DUMP");
     if (dump) {
+      fprintf(stderr, "vp8l dump: n %d palette %d tb %d hb %d exact %d nlq_bits %d low_effort %d "
+              "nl_bits %d\n", n, p.palette, p.tb, p.hb, p.exact, p.nlq_bits, p.low_effort,
+              l->nl_bits);
       const size_t np = l->npix;
       uint8_t* buf = (uint8_t*)malloc(np * 4 + 1);
       char path[512];
       const struct { const void* d; size_t bytes; const char* tag; } parts[] = {
-          {l->d_argb, np * 4, "argb"}, {l->d_ops, np * 4, "ops"}, {l->d_cbits, 1, "cbits"}};
-      for (int i = 0; buf && i < 3; ++i) {
+          {l->d_argb, np * 4, "argb"}, {l->d_ops, np * 4, "ops"}, {l->d_cbits, 1, "cbits"},
+          {l->d_modes, (size_t)l->ntt, "modes"}, {l->d_mult, (size_t)l->ntt * 4, "mult"},
+          {l->d_pflag, 4, "pflag"}};
+      for (int i = 0; buf && i < 6; ++i) {
+        if (p.palette && i >= 3) break;
         CHK(hipStreamSynchronize(st));
         CHK(hipMemcpy(buf, parts[i].d, parts[i].bytes, hipMemcpyDeviceToHost));
         snprintf(path, sizeof(path), "%s.%s", dump, parts[i].tag);
@@ -548,6 +561,11 @@ int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t*
         const int s = used[e == l ? 4 : 5]++;
         e->h_fidx[s] = f;
         e->h_fmode[s] = mode[f];
+        /* the reference's own predictor choice where GetResidual updates the
+           picture (model: needs_exact_predictor): near-lossless, or a
+           transparent pixel L0 kept (its alpha histogram at 0) without exact */
+        e->h_pexact[s] = !l->p.exact &&
+                         (l->p.nlq_bits > 0 || l->h_ehist[(size_t)f * VP8L_EHIST + 0] > 0);
         l->route_eng[f] = e;
         l->route_slot[f] = s;
         continue;

@@ -46,6 +46,8 @@ typedef struct vp8l_engine {
   uint32_t* d_mult;
   uint32_t* d_aflag;
   uint32_t* d_pflag;           /* per slot: residuals from the serial pass (L1a) */
+  uint8_t* d_pexact;           /* per slot: the reference's predictor choice (L1a) */
+  uint8_t* h_pexact;
   int64_t* d_feat;
   uint32_t* d_tl;
   uint32_t* d_tn;

@@ -108,7 +108,7 @@ void vp8l_setup_params(vp8l_params* p, int w, int h, int n, int method, int alph
   p->w = w; p->h = h; p->n = n;
   p->alpha = alpha != 0;
   p->exact = alpha != 0;   /* the ALPH encoder sets exact (alpha_enc.c:66-72) */
-  p->low_effort = method == 0 && !alpha;
+  p->low_effort = method == 0;   /* the ALPH encoder passes its effort as the method (alpha_enc.c:76) */
   p->cache_bits = alpha ? 0 : VP8L_MAX_CACHE_BITS;
   p->ow = w;
   p->hb = vp8l_histo_bits(method, w, h);

@@ -108,18 +108,21 @@ typedef struct {
 int vp8l_launch_scan(const uint8_t* rgba, size_t fstride, int rstride, int w, int h, int n,
                      int plane, uint32_t* ehist, uint32_t* pal, void* stream);
 /* L1: per slot f the input frame fidx[f] (NULL: f); entropy mode fmode[f]
- * (0..3): subtract green (mode & 2), per-tile predictor (the reference's
- * choice, L1a) + cross colour (mode & 1), the latter scored against the L0
- * histograms ehist of input frame efidx[f] (NULL: f); tabs: the engine's
- * table block (VP8L_TAB_WORDS). sg_mask: bit 0 some slot without subtract
- * green, bit 1 some with. pflag (n words): per slot 1 when the residuals
- * came from the serial pass (near-lossless / alpha-0 clean-up).
- * alpha_flag[f] |= 1 if any alpha != 255. */
+ * (0..3): subtract green (mode & 2), per-tile predictor + cross colour
+ * (mode & 1). The predictor: the reference's own choice (L1a) for slots with
+ * pexact[f] (their residuals update the picture: near-lossless, alpha-0
+ * clean-up) and at method 0, else the cross-entropy choice against the L0
+ * histograms ehist of input frame efidx[f] (NULL: f), which also score the
+ * cross colour; any_exact: some slot has pexact. tabs: the engine's table
+ * block (VP8L_TAB_WORDS). sg_mask: bit 0 some slot without subtract green,
+ * bit 1 some with. pflag (n words): per slot 1 when the residuals came from
+ * the serial pass. alpha_flag[f] |= 1 if any alpha != 255. */
 int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rstride,
                           const vp8l_params* p, const int* fidx, const int* efidx,
                           const uint8_t* fmode, const uint32_t* ehist, const int32_t* tabs,
-                          int sg_mask, uint32_t* argb, uint8_t* modes, uint32_t* pflag,
-                          uint32_t* mult, uint32_t* alpha_flag, void* stream);
+                          int sg_mask, uint32_t* argb, uint8_t* modes, const uint8_t* pexact,
+                          int any_exact, uint32_t* pflag, uint32_t* mult, uint32_t* alpha_flag,
+                          void* stream);
 /* Near-lossless preprocessing (VP8ApplyNearLossless): passes at bits .. 1
  * from frame fidx[f] of rgba into slot f of buf0 / buf1 (n x w*h*4 each,
  * packed RGBA), slots with apply[f] == 0 copied; *out = the buffer holding

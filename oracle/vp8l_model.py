@@ -243,7 +243,10 @@ SP_CC[[256 - k for k in range(1, 11)]] = [-61, -37, -22, -13, -8, -5, -3, -2, -1
 CC_ZERO_BONUS = 3 << 12     # "-3 bits" for a zero multiplier (:565-567, :613-618)
 CC_RED_DELTAS = [32, 16, 8, 4, 2, 1]          # kMaxIters 6 at quality 75 (:577)
 CC_BLUE_DELTAS = [16, 16, 8, 4, 2, 2, 2]      # delta_lut (:640)
-CC_BLUE_AXES = [(0, -1), (0, 1), (-1, 0), (1, 0), (-1, -1), (-1, 1), (1, -1), (1, 1)]
+# axis-aligned steps only (the reference's own low-quality variant,
+# :670-673): the same sizes here as all 8 directions for 4
+# candidates per step instead of 8
+CC_BLUE_AXES = [(0, -1), (0, 1), (-1, 0), (1, 0)]
 
 
 def spatial_table(w0, e):
@@ -631,6 +634,45 @@ def residual_image(argb, tb, low_effort=False, near_q=100, exact=False, sg=False
     return modes, res.reshape(H, W).astype(np.uint32)
 
 
+def needs_exact_predictor(argb_in, near_q, exact):
+    """Frames whose predictor residuals update the picture as GetResidual
+    goes (predictor_enc.c:234-292): near-lossless below 100, or -- without
+    `exact` -- a transparent pixel among those L0 keeps (its alpha histogram
+    at 0). They take the reference's own predictor choice (residual_image);
+    the others the cross-entropy choice (choose_predictors_ce). argb_in: the
+    input picture's ARGB."""
+    if exact:
+        return False
+    return near_lossless_bits(near_q) > 0 or int(l0_histograms(argb_in)[0][0]) > 0
+
+
+def ce_tables(G):
+    """Per channel the cost (1/4096 bit) of each residual value under the
+    frame's accumulated histograms G (L0's predictor-12 residuals, counts
+    + 1/2): flog2(2 N + 256) - flog2(2 G + 1)."""
+    G = np.asarray(G, dtype=np.int64)
+    N = G.sum(axis=1, keepdims=True)
+    return flog2(2 * N + 256) - flog2(2 * G + 1)
+
+
+def choose_predictors_ce(P, tb, G):
+    """Per tile the first of the 14 predictors with the smallest sum over its
+    pixels and channels of ce_tables(G)[channel][residual] -- the residuals'
+    cross entropy against the frame's histograms: tile-parallel, no
+    histograms (the exact search, residual_image, accumulates them tile
+    after tile). P: (H, W) packed ARGB (sub-green applied)."""
+    H, W = P.shape
+    CT = ce_tables(G)
+    tile = tile_index(H, W, tb).ravel()
+    nt = sub_sample(W, tb) * sub_sample(H, tb)
+    costs = []
+    for m in range(14):
+        r = _plain_residuals(P, H, W, m).astype(np.int64).ravel()
+        c = CT[0][r >> 24] + CT[1][(r >> 16) & 255] + CT[2][(r >> 8) & 255] + CT[3][r & 255]
+        costs.append(np.bincount(tile, weights=c, minlength=nt).astype(np.int64))
+    return np.argmin(np.stack(costs), axis=0)
+
+
 # entropy modes (src/enc/vp8l_enc.c:38-46 EntropyIx): bit 0 = predictor +
 # cross colour, bit 1 = subtract green; 4 = palette
 DIRECT, SPATIAL, SUBGREEN, SPATIAL_SUBGREEN, PALETTE = 0, 1, 2, 3, 4
@@ -653,9 +695,10 @@ def planes_argb(P):
 def transform_image(rgba, tb, mode=SPATIAL_SUBGREEN, G=None, near_q=100, exact=False,
                     low_effort=False):
     """Subtract green (mode & 2) -> predictor (the reference's own choice,
-    residual_image, with its near-lossless quantisation below near_q 100 and
-    alpha-0 clean-up unless exact) -> cross colour (choose_cross_color; none
-    at low effort), both mode & 1. G: the frame's accumulated histograms for
+    residual_image, where the residuals update the picture -- near-lossless
+    below near_q 100, alpha-0 clean-up unless exact: needs_exact_predictor --
+    else choose_predictors_ce) -> cross colour (choose_cross_color; none at
+    low effort), both mode & 1. G: the frame's accumulated histograms for
     the colour search (accumulated_histograms of the sub-green input;
     computed here when not given). Returns (modes (tiles,), mult (tiles,3),
     residual ARGB uint32 (H, W)); modes/mult are None without the spatial
@@ -666,7 +709,12 @@ def transform_image(rgba, tb, mode=SPATIAL_SUBGREEN, G=None, near_q=100, exact=F
         return None, None, planes_argb(P)
     if G is None:
         G = accumulated_histograms(planes_argb(P))
-    modes, r = residual_image(planes_argb(P), tb, low_effort, near_q, exact, bool(mode & SUBGREEN))
+    argb = planes_argb(P)
+    if low_effort or needs_exact_predictor(to_argb(rgba), near_q, exact):
+        modes, r = residual_image(argb, tb, low_effort, near_q, exact, bool(mode & SUBGREEN))
+    else:
+        modes = choose_predictors_ce(argb.astype(np.int64), tb, G)
+        r = _plain_residuals(argb.astype(np.int64), H, W, modes[tile_index(H, W, tb)])
     r = r.astype(np.int64)
     res = np.stack([(r >> 24) & 255, (r >> 16) & 255, (r >> 8) & 255, r & 255], axis=-1)
     if low_effort:
@@ -1475,6 +1523,14 @@ def analyze_entropy(argb, npal, tb):
     if 0 < npal <= 16:
         return PALETTE
     H, W = argb.shape
+    return entropy_choice(l0_histograms(argb), npal, sub_sample(W, tb) * sub_sample(H, tb))
+
+
+def l0_histograms(argb):
+    """AnalyzeEntropy's 13 histograms over the pixels it keeps (those that
+    differ from their raster predecessor and from the pixel above): L0
+    k_vp8l_entropy."""
+    H, W = argb.shape
     flat = argb.ravel().astype(np.uint32)
     prev = np.concatenate([flat[:1], flat[:-1]])
     diff = sub_pixels_u32(flat, prev)
@@ -1483,8 +1539,7 @@ def analyze_entropy(argb, npal, tb):
     above[W:] = flat[W:] == flat[:-W]
     keep &= ~above
     pix = flat[keep].astype(np.int64); dif = diff[keep].astype(np.int64)
-    hs = entropy_histograms(pix, dif)
-    return entropy_choice(hs, npal, sub_sample(W, tb) * sub_sample(H, tb))
+    return entropy_histograms(pix, dif)
 
 
 def entropy_histograms(pix, dif):
@@ -1715,7 +1770,7 @@ def encode(rgba, method=4, cache_bits=AUTO_CACHE, kmax=KMAX, return_parts=False,
         G = accumulated_histograms(planes_argb(sub_green_planes(rgba, mode)))
         if near_lossless_q < 100 and not alpha_plane and near_lossless_applies(mode, near_lossless_q):
             rgba = argb_to_rgba(near_lossless(to_argb(rgba), near_lossless_q))
-        low_effort = method == 0 and not alpha_plane
+        low_effort = method == 0
         modes, mult, argb = transform_image(rgba, tb, mode, G,
                                             100 if alpha_plane else near_lossless_q,
                                             exact or alpha_plane, low_effort)
@@ -1788,7 +1843,7 @@ def encode(rgba, method=4, cache_bits=AUTO_CACHE, kmax=KMAX, return_parts=False,
         if mode & SPATIAL:
             bw.put(1, 1); bw.put(0, 2); bw.put(tb - 2, 3)
             write_sub_image(bw, [0xFF000000 | (int(m) << 8) for m in modes])
-            if not (method == 0 and not alpha_plane):   # no cross colour at method 0
+            if method != 0:   # no cross colour at method 0
                 bw.put(1, 1); bw.put(1, 2); bw.put(tb - 2, 3)
                 write_sub_image(bw, [0xFF000000 | ((int(c[2]) & 255) << 16) |
                                      ((int(c[1]) & 255) << 8) | (int(c[0]) & 255) for c in mult])

@@ -366,7 +366,7 @@ def test_host_header_matches_model(host_lib, w, h, f, alpha, method, plane, kind
         setup = host_lib.vp8l_setup_params_palette_hb if fits else host_lib.vp8l_setup_params
         setup(C.byref(p), w, h, 1, method, int(plane))
         assert (p.tb, p.hb, p.k) == (P["tb"], P["hb"], P["k"])
-        assert p.low_effort == (method == 0 and not plane)
+        assert p.low_effort == (method == 0)
     pw = P["argb"].shape[1]
     dists = M.candidate_distances(pw)
     assert list(p.dist)[:len(dists)] == dists
@@ -507,9 +507,9 @@ def test_gpu_1080p_palette_and_direct_sizes(gpu):
                                           ("q7", 120, 90, 3, 40), ("syn", 64, 3, 1, 20),
                                           ("syn", 63, 63, 4, 0), ("g16", 96, 64, 3, 40)])
 def test_gpu_near_lossless(gpu, kind, w, h, f, q):
-    """near_lossless < 100 (VP8ApplyNearLossless preprocessing on the GPU for
-    the frames that take no palette): bit-exact with the model, decodes to
-    the preprocessed picture; small pictures and palettes stay lossless"""
+    """near_lossless < 100 (VP8ApplyNearLossless preprocessing of direct /
+    subtract-green frames, quantisation inside the predictor for spatial
+    ones; palettes stay lossless): bit-exact with the model"""
     img = lossless_picture(kind, w, h, f)
     enc = gpu.GpuBatch(w, h, 1, quality=75.0, method=4, lossless=1, near_lossless=q)
     import torch
@@ -519,9 +519,13 @@ def test_gpu_near_lossless(gpu, kind, w, h, f, q):
     got = enc.output(0)
     enc.close()
     assert got == M.encode(img, near_lossless_q=q)
+    data = gpu.encode_rgba(img, quality=75.0, method=4, lossless=1, use_argb=True, near_lossless=q)
+    assert data == got   # opaque pictures: WebPEncode's transparent-pixel zeroing is a no-op
+    # `exact` keeps the predictor's residuals plain, near-lossless included
+    # (GetResidual's exact branch, predictor_enc.c:239-241)
     data = gpu.encode_rgba(img, quality=75.0, method=4, lossless=1, use_argb=True, exact=1,
                            near_lossless=q)
-    assert data == got
+    assert data == M.encode(img, near_lossless_q=q, exact=True)
 
 
 @pytest.mark.gpu

@@ -2,7 +2,7 @@
 # One GPU-box session: GPU tests, bench line, K3 stage split, rocprofv3 kernel
 # stats, PMC passes (HBM bytes, SQ issue counters) and the PMC calibration.
 # Usage (on the box): bash tools/gpu_session.sh <tag> [steps...]
-#   steps: tests bench lossless lprof stages prof pmc sq calib (default: all but lossless/lprof)
+#   steps: tests bench lossless lprof lpmc stages prof pmc sq calib (default: all but the lossless ones)
 set -o pipefail
 TAG=${1:-s}; shift
 STEPS=${*:-tests bench stages prof pmc sq calib}
@@ -51,6 +51,13 @@ if has sq; then
   run timeout -s KILL 200 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS \
     SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_WAVES --output-format csv -d $O/sq2 -o run \
     -- $BENCH --steps 1 --warmup 0 > $O/sq2.log 2>&1 || exit 1
+fi
+if has lpmc; then   # HBM bytes of the lossless kernels (bench.py --lossless, one step)
+  for C in FETCH_SIZE WRITE_SIZE; do
+    run timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d $O/lpmc/pmc_$C -o run \
+      -- python3 $R/bench.py --lossless --no-cpu --no-host-input --steps 1 --warmup 0 \
+      > $O/lpmc_$C.log 2>&1 || exit 1
+  done
 fi
 if has calib; then
   for C in FETCH_SIZE WRITE_SIZE; do

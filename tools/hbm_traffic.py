@@ -5,7 +5,7 @@ correction (profiles/r2/calib_*: a 1 GiB stream of dword / dwordx4 loads
 reads back as 0.5 GiB of FETCH_SIZE, 1 GiB of stores as 1 GiB of
 WRITE_SIZE): FETCH_SIZE x 2, WRITE_SIZE as is.
 
-usage: python tools/hbm_traffic.py gpurun_out/<tag> > profiles/hbm_traffic.json"""
+usage: python tools/hbm_traffic.py gpurun_out/<tag> [workload text] > profiles/hbm_traffic.json"""
 import collections
 import csv
 import json
@@ -23,6 +23,7 @@ def load(path):
 
 def main():
     d = sys.argv[1]
+    workload = sys.argv[2] if len(sys.argv) > 2 else "256 x 1920x1080 q75 m4"
     fetch = load(os.path.join(d, "pmc_FETCH_SIZE", "run_counter_collection.csv"))
     write = load(os.path.join(d, "pmc_WRITE_SIZE", "run_counter_collection.csv"))
     kernels = {}
@@ -36,8 +37,8 @@ def main():
             "fetch_bytes_raw": int(f), "fetch_bytes": int(2 * f), "write_bytes": int(w),
             "bytes_per_launch": int(2 * f + w)}
     json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
-                         "bench.py --steps 1 --warmup 0 (256 x 1920x1080 q75 m4), "
-                         "FETCH_SIZE x2 (gfx950 calibration profiles/r2/calib_*)",
+                         "bench.py --steps 1 --warmup 0 (%s), "
+                         "FETCH_SIZE x2 (gfx950 calibration profiles/r2/calib_*)" % workload,
                "session": os.path.basename(os.path.normpath(d)),
                "kernels": kernels}, sys.stdout, indent=1)
 

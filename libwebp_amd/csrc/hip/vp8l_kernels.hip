@@ -178,6 +178,7 @@ struct TransformSmem {
   int32_t frac[1024];                // log2 fraction table (model: FLOG2_FRAC)
   long long cost[16];
   int32_t ct[4][256];                // cross-entropy cost per channel and residual (model: ce_tables)
+  int32_t slogt[T * T + 1];          // slog(t) for the counts a tile can have
   int32_t pcost[16];                 // the tile's cross-entropy cost per predictor
   uint32_t nsum[4];
   int best;
@@ -200,19 +201,21 @@ __device__ __forceinline__ long long slog_fx(const int32_t* frac, uint32_t v) {
 
 // block-wide sums of K int64 values into S.cost[0..K) (zeroed by the caller)
 template <int K, int T>
-__device__ __forceinline__ void reduce_costs(TransformSmem<T>& S, const long long (&v)[K]) {
+__device__ __forceinline__ void reduce_costs(TransformSmem<T>& S, const int32_t (&v)[K]) {
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const long long w = wave_sum(v[k]);
-    if (lane_id() == 0) atomicAdd((unsigned long long*)&S.cost[k], (unsigned long long)w);
+    const int32_t w = wave_sum(v[k]);
+    if (lane_id() == 0) atomicAdd((unsigned long long*)&S.cost[k], (unsigned long long)(long long)w);
   }
 }
 
 // The bin side of one candidate evaluation: thread b owns value b of each of
-// the K histograms (u16 pairs in h) against channel c of G.
+// the K histograms (u16 pairs in h) against channel c of G. Every term fits
+// 32 bits (t <= 4096: slog(t) < 2^28, slog(t + g) - slog(g) ~ t log2(t + g)),
+// and so does a candidate's sum over the bins (< 2^29 at 4096 pixels).
 template <int K, int T>
 __device__ __forceinline__ void bin_costs(TransformSmem<T>& S, const uint32_t* h, int c,
-                                          const int8_t* sp, long long (&acc)[K]) {
+                                          const int8_t* sp, int32_t (&acc)[K]) {
   const int b = threadIdx.x;   // 256 threads = 256 values
   const uint32_t gv = S.g[c][b];
   const long long sg = S.slogg[c][b];
@@ -220,7 +223,8 @@ __device__ __forceinline__ void bin_costs(TransformSmem<T>& S, const uint32_t* h
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const uint32_t t = (h[k * 128 + (b >> 1)] >> ((b & 1) * 16)) & 0xffffu;
-    if (t) acc[k] += 16ll * (long long)t * spv - (slog_fx(S.frac, t) + slog_fx(S.frac, t + gv) - sg);
+    if (t)
+      acc[k] += 16 * (int32_t)t * spv - (S.slogt[t] + (int32_t)(slog_fx(S.frac, t + gv) - sg));
   }
 }
 
@@ -281,11 +285,11 @@ __device__ void cc_eval(TransformSmem<T>& S, int np, const int (&r0)[KR > 0 ? KR
       }
   }
   __syncthreads();
-  long long acc[K];
+  int32_t acc[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) acc[k] = 0;
   if constexpr (KR > 0) {
-    long long a[KR];
+    int32_t a[KR];
 #pragma unroll
     for (int k = 0; k < KR; ++k) a[k] = 0;
     bin_costs<KR>(S, S.cc.h9, 1, kSpCC, a);
@@ -293,7 +297,7 @@ __device__ void cc_eval(TransformSmem<T>& S, int np, const int (&r0)[KR > 0 ? KR
     for (int k = 0; k < KR; ++k) acc[k] = a[k];
   }
   if constexpr (KB > 0) {
-    long long a[KB];
+    int32_t a[KB];
 #pragma unroll
     for (int k = 0; k < KB; ++k) a[k] = 0;
     bin_costs<KB>(S, S.cc.h9 + KR * 128, 3, kSpCC, a);
@@ -372,6 +376,7 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
                         VP8L_EH_ACC + (SG ? 5 : 3)};
     for (int i = tid; i < 1024; i += 256) S.frac[i] = frac_tab[i];
     __syncthreads();
+    for (int i = tid; i <= T * T; i += 256) S.slogt[i] = (int32_t)slog_fx(S.frac, (uint32_t)i);
     if (tid < 4) S.nsum[tid] = 0;
     __syncthreads();
 #pragma unroll
@@ -446,25 +451,27 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
       // the cross-entropy choice (model: choose_predictors_ce): every thread
       // sums the 14 predictors' costs over its pixels, then wave sums
       if (tid < 16) S.pcost[tid] = 0;
-      int32_t pc[14];
-#pragma unroll
-      for (int m = 0; m < 14; ++m) pc[m] = 0;
-      for (int i = tid; i < np; i += 256) {
-        const int ly = i / tw, lx = i - ly * tw;
-        const int fm = fixed_mode(x0 + lx, y0 + ly);
-        const uint32_t P = at(lx, ly), L = at(lx - 1, ly), T_ = at(lx, ly - 1), TL = at(lx - 1, ly - 1);
-        const uint32_t TR = tr(lx, ly);
-#pragma unroll
-        for (int m = 0; m < 14; ++m) {
-          const uint32_t r = sub_pixels(P, predict(fm >= 0 ? fm : m, L, T_, TL, TR));
-          pc[m] += S.ct[0][r >> 24] + S.ct[1][ch(r, 16)] + S.ct[2][ch(r, 8)] + S.ct[3][ch(r, 0)];
-        }
-      }
       __syncthreads();   // pcost zeroed
+      for (int m0 = 0; m0 < 14; m0 += 7) {   // 7 modes at a time: registers
+        int32_t pc[7];
 #pragma unroll
-      for (int m = 0; m < 14; ++m) {
-        const int32_t t = wave_sum(pc[m]);
-        if (lane_id() == 0) atomicAdd(&S.pcost[m], t);
+        for (int m = 0; m < 7; ++m) pc[m] = 0;
+        for (int i = tid; i < np; i += 256) {
+          const int ly = i / tw, lx = i - ly * tw;
+          const int fm = fixed_mode(x0 + lx, y0 + ly);
+          const uint32_t P = at(lx, ly), L = at(lx - 1, ly), T_ = at(lx, ly - 1);
+          const uint32_t TL = at(lx - 1, ly - 1), TR = tr(lx, ly);
+#pragma unroll
+          for (int m = 0; m < 7; ++m) {
+            const uint32_t r = sub_pixels(P, predict(fm >= 0 ? fm : m0 + m, L, T_, TL, TR));
+            pc[m] += S.ct[0][r >> 24] + S.ct[1][ch(r, 16)] + S.ct[2][ch(r, 8)] + S.ct[3][ch(r, 0)];
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < 7; ++m) {
+          const int32_t t = wave_sum(pc[m]);
+          if (lane_id() == 0) atomicAdd(&S.pcost[m0 + m], t);
+        }
       }
       __syncthreads();
       best = 0;

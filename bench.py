@@ -60,9 +60,10 @@ def parse_args(argv=None):
     ap.add_argument("--low-memory", action="store_true",
                     help="config->low_memory (cwebp -low_memory, VP8EncLoop); not the headline")
     ap.add_argument("--threads", type=int, default=0, help="host tail threads (0 = auto)")
-    ap.add_argument("--engines", type=int, default=2,
+    ap.add_argument("--engines", type=int, default=0,
                     help="encoder instances on their own streams and host threads; steps are "
-                         "dealt round-robin so one batch's host work overlaps another's kernels")
+                         "dealt round-robin so one batch's host work overlaps another's kernels "
+                         "(0: 3 lossy, 2 lossless -- profiles/r3/ab5_*.json)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="CPU work per baseline leg (single thread, all cores)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -436,7 +437,8 @@ def main(argv=None):
     # timed steps are dealt round-robin to one host thread per engine (the
     # ctypes calls release the GIL), so one batch's host stages (segment
     # setup, partition 0, RIFF write) run while another batch's kernels do
-    E = 1 if args.stub else max(1, min(args.engines, args.steps))
+    engines = args.engines or (2 if args.lossless else 3)
+    E = 1 if args.stub else max(1, min(engines, args.steps))
     args.engines_used = E
     encs = [enc]
     for _ in range(E - 1):

@@ -256,33 +256,39 @@ __device__ void cc_eval(TransformSmem<T>& S, int np, const int (&r0)[KR > 0 ? KR
   for (int i = tid; i < K * 128; i += 256) S.cc.h9[i] = 0;
   if (tid < K) S.cost[tid] = 0;
   __syncthreads();
-  // one wave per candidate (k = wave, wave + 4, ..) over the tile's pixels:
-  // the five values next to 0 -- most of a good multiplier's residuals --
-  // counted in registers and summed over the wave once, the rest by LDS
-  // atomics (same-bin atomics of a wave serialise)
-  const int wv = tid >> 6;
+  // every thread takes every 256th pixel of the tile for all K candidates:
+  // the values next to 0 -- most of a good multiplier's residuals -- counted
+  // in packed register fields and summed over the wave once (lane k * NH + j
+  // adds field j of candidate k), the rest by LDS atomics (same-bin atomics
+  // of a wave serialise)
+  uint64_t hot[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    if ((k & 3) != wv) continue;   // wave-uniform
-    uint64_t hot = 0;
-    uint32_t* h = S.cc.h9 + k * 128;
-    for (int i = lane_id(); i < np; i += 64) {
-      const uint32_t r = S.cc.res[i];
-      const int g = ch(r, 8), rr = ch(r, 16), bb = ch(r, 0);
+  for (int k = 0; k < K; ++k) hot[k] = 0;
+  for (int i = tid; i < np; i += 256) {
+    const uint32_t r = S.cc.res[i];
+    const int g = ch(r, 8), rr = ch(r, 16), bb = ch(r, 0);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
       const int v = k >= KR ? (bb - ctd(b0[k - KR], g) - ctd(b1[k - KR], rr)) & 255
                             : (rr - ctd(r0[k], g)) & 255;
       const int q = Hot<T>::slot(v);
-      hot += q < Hot<T>::NH ? (1ull << (Hot<T>::FB * q)) : 0ull;
-      if (q >= Hot<T>::NH) hist_add(h, v);
+      hot[k] += q < Hot<T>::NH ? (1ull << (Hot<T>::FB * q)) : 0ull;
+      if (q >= Hot<T>::NH) hist_add(S.cc.h9 + k * 128, v);
     }
-    hot = wave_sum(hot);
-    if (lane_id() == 0)
+  }
+  {
+    const int lane = lane_id(), kk = lane / Hot<T>::NH, j = lane - kk * Hot<T>::NH;
+    uint64_t mine = 0;
 #pragma unroll
-      for (int j = 0; j < Hot<T>::NH; ++j) {
-        const uint32_t t = (uint32_t)(hot >> (Hot<T>::FB * j)) & Hot<T>::MASK;
-        const int v = Hot<T>::value(j);
-        if (t) atomicAdd(&h[v >> 1], t << ((v & 1) * 16));
-      }
+    for (int k = 0; k < K; ++k) {
+      const uint64_t t = wave_sum(hot[k]);
+      if (k == kk) mine = t;
+    }
+    if (kk < K) {
+      const uint32_t t = (uint32_t)(mine >> (Hot<T>::FB * j)) & Hot<T>::MASK;
+      const int v = Hot<T>::value(j);
+      if (t) atomicAdd(&S.cc.h9[kk * 128 + (v >> 1)], t << ((v & 1) * 16));
+    }
   }
   __syncthreads();
   int32_t acc[K];
@@ -1068,7 +1074,9 @@ __global__ __launch_bounds__(64) void k_vp8l_resid_serial(const uint8_t* __restr
 // ------------------------------------------------------------------ L0
 
 __device__ __forceinline__ uint32_t rgba_argb(const uint8_t* q) {
-  return ((uint32_t)q[3] << 24) | ((uint32_t)q[0] << 16) | ((uint32_t)q[1] << 8) | q[2];
+  // one dword load: R | G << 8 | B << 16 | A << 24 (RGBA rows are 4-byte aligned)
+  const uint32_t v = *reinterpret_cast<const uint32_t*>(q);
+  return (v & 0xff00ff00u) | ((v >> 16) & 0xffu) | ((v & 0xffu) << 16);
 }
 // pixel x of a row: RGBA bytes, or (plane) an ALPH alpha byte as green
 // (WebPDispatchAlphaToGreen, src/enc/alpha_enc.c:73)

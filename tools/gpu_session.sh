@@ -59,6 +59,10 @@ if has lpmc; then   # HBM bytes of the lossless kernels (bench.py --lossless, on
       > $O/lpmc_$C.log 2>&1 || exit 1
   done
 fi
+if has sq3; then   # VALU lane utilisation (thread-cycles per VALU cycle); last: a counter
+  run timeout -s KILL 120 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU \
+    --output-format csv -d $O/sq3 -o run -- $BENCH --steps 1 --warmup 0 > $O/sq3.log 2>&1 || exit 1
+fi
 if has calib; then
   for C in FETCH_SIZE WRITE_SIZE; do
     run timeout -s KILL 60 rocprofv3 --pmc $C --output-format csv -d $O/calib_$C -o run \

@@ -19,9 +19,10 @@
 //                        plain (sub-green) pixels for the non-spatial modes
 //      k_vp8l_palapply   colour indexing: binary search in the sorted palette,
 //                        2^xbits indices bundled per packed pixel
-//   L2 k_vp8l_cache      one wave per frame, 64 pixels per step: per pixel the
-//                        smallest cache size (1..9 bits) holding it; same-key
-//                        lanes found with one ballot per key bit, MSB first
+//   L2 k_vp8l_cache      one wave per frame segment, 64 pixels per step: per
+//                        pixel the smallest cache size (1..9 bits) holding it;
+//                        same-key lanes found with one ballot per key bit, MSB
+//                        first; k_vp8l_cache_start chains the segments
 //   L3 k_vp8l_match      one wave per row: best candidate run per pixel (ballots)
 //      k_vp8l_parse      one thread per row: greedy copy / cache / literal
 //                        (once with every hit of the largest cache, then with
@@ -36,6 +37,8 @@
 //                        interior words stored, the two edge words OR-ed
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 #include "../vp8l_gpu.h"
 
@@ -65,7 +68,7 @@ __device__ __forceinline__ int clip255(int v) { return v < 0 ? 0 : v > 255 ? 255
 __device__ __forceinline__ int ch(uint32_t v, int s) { return (int)((v >> s) & 255); }
 
 // src/dsp/lossless.c:103-180
-__device__ uint32_t predict(int m, uint32_t L, uint32_t T, uint32_t TL, uint32_t TR) {
+__device__ __forceinline__ uint32_t predict(int m, uint32_t L, uint32_t T, uint32_t TL, uint32_t TR) {
   switch (m) {
     case 0: return 0xff000000u;
     case 1: return L;
@@ -407,7 +410,7 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     const int sw = tw + 2;   // LDS source row width (cols x0-1 .. x0+tw)
     __syncthreads();         // the previous tile is done with S
     // load sub-green pixels (A, R-G, G, B-G) with a 1-pixel border
-    bool tile_alpha = false;
+    bool tile_alpha = false, opaque = true;   // opaque: every real pixel loaded has A 255
     for (int i = tid; i < (th + 1) * sw; i += 256) {
       const int ly = i / sw, lx = i - ly * sw;
       const int y = y0 - 1 + ly, x = x0 - 1 + lx;
@@ -422,8 +425,10 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
           v = subgreen ? (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255)
                        : (a << 24) | (r << 16) | (g << 8) | b;
           if (a != 255 && ly > 0 && lx > 0 && lx <= tw) tile_alpha = true;
+          opaque &= a == 255;
         }
       }
+      if (p.alpha) opaque = false;
       S.src[i] = v;
     }
     if (x0 + tw == W) {
@@ -436,11 +441,13 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
           const uint32_t r = q[0], g = q[1], b = q[2], a = q[3];
           S.first[i] = subgreen ? (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255)
                                 : (a << 24) | (r << 16) | (g << 8) | b;
+          opaque &= a == 255;
         }
       }
     }
     if (__any(tile_alpha) && lane_id() == 0) atomicOr(&alpha_flag[f], 1u);
-    __syncthreads();
+    opaque = __syncthreads_and(opaque);
+    PS_STAMP(6);
 
     auto at = [&](int lx, int ly) -> uint32_t { return S.src[(ly + 1) * sw + lx + 1]; };
     auto tr = [&](int lx, int ly) -> uint32_t {   // (y-1)*W + x + 1, linear
@@ -455,29 +462,35 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     int best;
     if (own_pred) {
       // the cross-entropy choice (model: choose_predictors_ce): every thread
-      // sums the 14 predictors' costs over its pixels, then wave sums
+      // sums the 14 predictors' costs over its pixels, then wave sums. The
+      // fixed-predictor pixels (frame row 0 / column 0) add one cost to every
+      // mode, which leaves the first minimum where it is: skipped. Where every
+      // pixel is opaque, every residual alpha is 0: skipped likewise.
       if (tid < 16) S.pcost[tid] = 0;
       __syncthreads();   // pcost zeroed
-      for (int m0 = 0; m0 < 14; m0 += 7) {   // 7 modes at a time: registers
-        int32_t pc[7];
+      int32_t pc[14];
 #pragma unroll
-        for (int m = 0; m < 7; ++m) pc[m] = 0;
+      for (int m = 0; m < 14; ++m) pc[m] = 0;
+      auto ce_sum = [&](auto opq) {
         for (int i = tid; i < np; i += 256) {
           const int ly = i / tw, lx = i - ly * tw;
-          const int fm = fixed_mode(x0 + lx, y0 + ly);
+          if (fixed_mode(x0 + lx, y0 + ly) >= 0) continue;
           const uint32_t P = at(lx, ly), L = at(lx - 1, ly), T_ = at(lx, ly - 1);
           const uint32_t TL = at(lx - 1, ly - 1), TR = tr(lx, ly);
 #pragma unroll
-          for (int m = 0; m < 7; ++m) {
-            const uint32_t r = sub_pixels(P, predict(fm >= 0 ? fm : m0 + m, L, T_, TL, TR));
-            pc[m] += S.ct[0][r >> 24] + S.ct[1][ch(r, 16)] + S.ct[2][ch(r, 8)] + S.ct[3][ch(r, 0)];
+          for (int m = 0; m < 14; ++m) {
+            const uint32_t r = sub_pixels(P, predict(m, L, T_, TL, TR));
+            pc[m] += (decltype(opq)::value ? 0 : S.ct[0][r >> 24]) + S.ct[1][ch(r, 16)] +
+                     S.ct[2][ch(r, 8)] + S.ct[3][ch(r, 0)];
           }
         }
+      };
+      if (opaque) ce_sum(std::true_type{});
+      else ce_sum(std::false_type{});
 #pragma unroll
-        for (int m = 0; m < 7; ++m) {
-          const int32_t t = wave_sum(pc[m]);
-          if (lane_id() == 0) atomicAdd(&S.pcost[m0 + m], t);
-        }
+      for (int m = 0; m < 14; ++m) {
+        const int32_t t = wave_sum(pc[m]);
+        if (lane_id() == 0) atomicAdd(&S.pcost[m], t);
       }
       __syncthreads();
       best = 0;
@@ -488,6 +501,7 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     } else {
       best = modes[(size_t)f * ntt + tile];
     }
+    PS_STAMP(7);
     uint32_t* out = argb_out + (size_t)f * W * H;
     if (pflag[f]) {
       for (int i = tid; i < np; i += 256) {
@@ -581,6 +595,7 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
       mult[(size_t)f * ntt + tile] =
           (uint32_t)(g2r & 255) | ((uint32_t)(g2b & 255) << 8) | ((uint32_t)(r2b & 255) << 16);
     }
+    PS_STAMP(10);
   }
 }
 
@@ -1110,8 +1125,9 @@ __global__ __launch_bounds__(256) void k_vp8l_entropy(const uint8_t* __restrict_
     if (d == 0) continue;
     if (y > 0 && pix_at(row - rstride, x, plane) == pix) continue;
     const int g = (int)(pix >> 8), gd = (int)(d >> 8);
-    atomicAdd(&h[0 * 256 + (pix >> 24)], 1u);
-    atomicAdd(&h[1 * 256 + (d >> 24)], 1u);
+    // alpha is one value over most waves: the wave-uniform fast path
+    hadd(h, 0 * 256 + (pix >> 24));
+    hadd(h, 1 * 256 + (d >> 24));
     atomicAdd(&h[2 * 256 + (g & 255)], 1u);
     atomicAdd(&h[3 * 256 + (gd & 255)], 1u);
     atomicAdd(&h[4 * 256 + ((pix >> 16) & 255)], 1u);
@@ -1134,7 +1150,7 @@ __global__ __launch_bounds__(256) void k_vp8l_entropy(const uint8_t* __restrict_
     const uint32_t r = sub_pixels(pix, predict(fm, L, T_, TL, 0u));
     const uint32_t rs = sub_pixels(sub_green(pix), predict(fm, sub_green(L), sub_green(T_),
                                                           sub_green(TL), 0u));
-    atomicAdd(&h[(VP8L_EH_ACC + 0) * 256 + (r >> 24)], 1u);
+    hadd(h, (VP8L_EH_ACC + 0) * 256 + (r >> 24));
     atomicAdd(&h[(VP8L_EH_ACC + 1) * 256 + ((r >> 16) & 255)], 1u);
     atomicAdd(&h[(VP8L_EH_ACC + 2) * 256 + ((r >> 8) & 255)], 1u);
     atomicAdd(&h[(VP8L_EH_ACC + 3) * 256 + (r & 255)], 1u);
@@ -1292,51 +1308,69 @@ __global__ __launch_bounds__(256) void k_vp8l_nearlossless(const uint8_t* __rest
 
 // ------------------------------------------------------------------ L2
 
-// One wave per frame walks the pixels in stream order, 64 at a time, keeping
-// the decoder's colour caches of every size b = 1..9 in LDS (zero-initialised
-// like VP8LColorCacheInit; 2 + 4 + ... + 512 entries). The keys of size b are
-// the top b bits of one 9-bit key, so the lanes sharing a key of every size
-// come from 9 ballots (most significant bit first, AND-ed). A lane's cache
-// content is the value of its nearest lower same-key lane, else the table
-// entry; the highest lane of each key group updates the table. The nine
-// sizes are independent: all lane exchanges, then all table reads, then all
-// table writes, so their latencies overlap. Out: per pixel the smallest size
-// whose cache holds it (hits are monotone in the size: the most recent
-// same-key pixel at b is also the most recent one at b + 1), one coalesced
-// byte store per 64 pixels.
+// A frame's pixels in stream order are cut into S segments of whole 64-pixel
+// chunks, one wave each, walked at once. A wave keeps the decoder's colour
+// caches of every size b = 1..9 in LDS (2 + 4 + ... + 512 entries). The keys
+// of size b are the top b bits of one 9-bit key, so the lanes sharing a key
+// of every size come from 9 ballots (most significant bit first, AND-ed). A
+// lane's cache content is the value of its nearest lower same-key lane, else
+// the table entry; the highest lane of each key group updates the table (the
+// other lanes write a slot of their own, no branch). The nine sizes are
+// independent: all lane exchanges, then all table reads, then all table
+// writes, so their latencies overlap. Out: per pixel the smallest size whose
+// cache holds it (hits are monotone in the size: the most recent same-key
+// pixel at b is also the most recent one at b + 1), one byte store per lane.
+//
+// Segment 0 starts from the zeroed caches (VP8LColorCacheInit); a later
+// segment does not know its start, so an entry it has not written yet is
+// unknown. Unknown at b means no earlier same-key pixel in the segment, so
+// it is unknown at b + 1 too: a pixel whose smallest known hit is not below
+// its first unknown size u leaves VP8L_CACHE_PARTIAL | u, and the segment's
+// final tables go to cseg. k_vp8l_cache_start turns those into each
+// segment's start contents; k_vp8l_match settles the partial pixels there.
 #define CACHE_BATCH 8
+__device__ __forceinline__ int cache_seg_begin(int s, int S, int nchunk) {
+  return (int)((long long)nchunk * s / S);
+}
+__device__ __forceinline__ int cache_seg_of(int c, int S, int nchunk) {   // begin(s) <= c < begin(s+1)
+  return (int)(((long long)(c + 1) * S - 1) / nchunk);
+}
+
 __global__ __launch_bounds__(64) void k_vp8l_cache(const uint32_t* __restrict__ argb, int npix,
-                                                   uint8_t* __restrict__ minb) {
-  __shared__ uint32_t tab[(2 << VP8L_MAX_CACHE_BITS) - 2];
-  const int f = blockIdx.x, ln = lane_id();
+                                                   int S, uint8_t* __restrict__ minb,
+                                                   uint2* __restrict__ cseg) {
+  __shared__ uint2 tab[VP8L_CACHE_TAB + 64];   // (value, written); + one dump slot per lane
+  const int s = blockIdx.x, f = blockIdx.y, ln = lane_id();
   const uint32_t* E = argb + (size_t)f * npix;
   const int nchunk = (npix + 63) >> 6;
+  const int cb = cache_seg_begin(s, S, nchunk), ce = cache_seg_begin(s + 1, S, nchunk);
   uint8_t* out = minb + (size_t)f * npix;
-  for (int i = ln; i < (2 << VP8L_MAX_CACHE_BITS) - 2; i += 64) tab[i] = 0;
+  for (int i = ln; i < VP8L_CACHE_TAB; i += 64) tab[i] = make_uint2(0u, s == 0 ? 1u : 0u);
   __syncthreads();
   const uint64_t below = (1ull << ln) - 1ull;
   uint32_t cur[CACHE_BATCH], nxt[CACHE_BATCH];
 #pragma unroll
   for (int k = 0; k < CACHE_BATCH; ++k) {
-    const int q = (k << 6) + ln;
-    cur[k] = q < npix ? E[q] : 0;
+    const int q = ((cb + k) << 6) + ln;
+    cur[k] = (cb + k < ce && q < npix) ? E[q] : 0;
   }
-  for (int c0 = 0; c0 < nchunk; c0 += CACHE_BATCH) {
+  for (int c0 = cb; c0 < ce; c0 += CACHE_BATCH) {
 #pragma unroll
     for (int k = 0; k < CACHE_BATCH; ++k) {
-      const int q = ((c0 + CACHE_BATCH + k) << 6) + ln;
-      nxt[k] = q < npix ? E[q] : 0;
+      const int c = c0 + CACHE_BATCH + k, q = (c << 6) + ln;
+      nxt[k] = (c < ce && q < npix) ? E[q] : 0;
     }
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CACHE_BATCH; ++k) {
       const int c = c0 + k;
-      if (c >= nchunk) break;
+      if (c >= ce) break;
       const int q = (c << 6) + ln;
       const bool valid = q < npix;
       const uint32_t v = cur[k];
       const uint32_t key9 = (v * HASH_MUL) >> (32 - VP8L_MAX_CACHE_BITS);
       uint64_t m[VP8L_MAX_CACHE_BITS];
-      uint32_t pv[VP8L_MAX_CACHE_BITS], tv[VP8L_MAX_CACHE_BITS];
+      uint32_t pv[VP8L_MAX_CACHE_BITS];
+      uint2 tv[VP8L_MAX_CACHE_BITS];
       uint64_t acc = __ballot(valid);
 #pragma unroll
       for (int b = 1; b <= VP8L_MAX_CACHE_BITS; ++b) {
@@ -1351,22 +1385,57 @@ __global__ __launch_bounds__(64) void k_vp8l_cache(const uint32_t* __restrict__ 
         pv[b - 1] = __shfl(v, lower ? 63 - __clzll((long long)lower) : ln);
         tv[b - 1] = tab[(1 << b) - 2 + (key9 >> (VP8L_MAX_CACHE_BITS - b))];
       }
-      uint32_t mb = VP8L_NEVER_HIT;
+      uint32_t mb = VP8L_NEVER_HIT, u = VP8L_NEVER_HIT;
 #pragma unroll
       for (int b = VP8L_MAX_CACHE_BITS; b >= 1; --b) {
-        const uint32_t held = (m[b - 1] & below) ? pv[b - 1] : tv[b - 1];
-        if (held == v) mb = b;
+        const bool low = (m[b - 1] & below) != 0;
+        const uint32_t held = low ? pv[b - 1] : tv[b - 1].x;
+        if (!low && !tv[b - 1].y) u = b;
+        else if (held == v) mb = b;
       }
+      if (mb == VP8L_NEVER_HIT && u < VP8L_NEVER_HIT) mb = VP8L_CACHE_PARTIAL | u;
       if (valid) out[q] = (uint8_t)mb;
       // LDS ops of a wave stay in order: every read above precedes these writes
 #pragma unroll
-      for (int b = 1; b <= VP8L_MAX_CACHE_BITS; ++b)
-        if (valid && (m[b - 1] >> ln) == 1ull)
-          tab[(1 << b) - 2 + (key9 >> (VP8L_MAX_CACHE_BITS - b))] = v;
+      for (int b = 1; b <= VP8L_MAX_CACHE_BITS; ++b) {
+        const bool top = valid && (m[b - 1] >> ln) == 1ull;
+        tab[top ? (1 << b) - 2 + (key9 >> (VP8L_MAX_CACHE_BITS - b)) : VP8L_CACHE_TAB + ln] =
+            make_uint2(v, 1u);
+      }
     }
 #pragma unroll
     for (int k = 0; k < CACHE_BATCH; ++k) cur[k] = nxt[k];
   }
+  if (s + 1 < S) {
+    __syncthreads();
+    uint2* o = cseg + ((size_t)f * S + s) * VP8L_CACHE_TAB;
+    for (int i = ln; i < VP8L_CACHE_TAB; i += 64) o[i] = tab[i];
+  }
+}
+
+// per frame and cache entry, the segments' start contents in place: the
+// value of the latest earlier segment that wrote the entry, else 0
+__global__ __launch_bounds__(1024) void k_vp8l_cache_start(int S, uint2* __restrict__ cseg) {
+  const int e = threadIdx.x, f = blockIdx.x;
+  if (e >= VP8L_CACHE_TAB) return;
+  uint2* t = cseg + (size_t)f * S * VP8L_CACHE_TAB + e;
+  uint32_t cur = 0;
+  for (int s = 0; s < S; ++s) {
+    const uint2 w = s + 1 < S ? t[(size_t)s * VP8L_CACHE_TAB] : make_uint2(0u, 0u);
+    t[(size_t)s * VP8L_CACHE_TAB] = make_uint2(cur, 1u);
+    if (w.y) cur = w.x;
+  }
+}
+
+// a partial pixel of L2: its sizes from u up hold the segment's start contents
+__device__ __forceinline__ uint32_t cache_settle(uint32_t mb, uint32_t v, size_t q, int npix, int S,
+                                                 const uint2* __restrict__ cstart) {
+  const int nchunk = (npix + 63) >> 6;
+  const uint2* t = cstart + (size_t)cache_seg_of((int)(q >> 6), S, nchunk) * VP8L_CACHE_TAB;
+  const uint32_t key9 = (v * HASH_MUL) >> (32 - VP8L_MAX_CACHE_BITS);
+  for (int b = (int)(mb & 15); b <= VP8L_MAX_CACHE_BITS; ++b)
+    if (t[(1 << b) - 2 + (key9 >> (VP8L_MAX_CACHE_BITS - b))].x == v) return (uint32_t)b;
+  return VP8L_NEVER_HIT;
 }
 
 // ------------------------------------------------------------------ L3
@@ -1375,11 +1444,13 @@ __global__ __launch_bounds__(64) void k_vp8l_cache(const uint32_t* __restrict__ 
 // distance the run of equal pixels starting at every x (ballot of the 64
 // comparisons; count trailing ones; a run reaching the chunk end continues
 // with the run at the next chunk's start), the longest (first on ties,
-// capped at MAX_LENGTH) and the smallest cache size holding the pixel,
-// packed per pixel as len | cand << 13 | minb << 15 for the parse.
+// capped at MAX_LENGTH) and the smallest cache size holding the pixel (L2's,
+// settled here where L2 left it partial), packed per pixel as
+// len | cand << 13 | minb << 15 for the parse.
 __global__ __launch_bounds__(64) void k_vp8l_match(const uint32_t* __restrict__ argb,
-                                                   const uint8_t* __restrict__ minb, vp8l_params p,
-                                                   uint32_t* __restrict__ bm) {
+                                                   const uint8_t* __restrict__ minb,
+                                                   const uint2* __restrict__ cstart, int S,
+                                                   vp8l_params p, uint32_t* __restrict__ bm) {
   const int f = blockIdx.y, y = blockIdx.x, ln = lane_id();
   const int W = p.w;
   const size_t npix = (size_t)W * p.h;
@@ -1406,7 +1477,12 @@ __global__ __launch_bounds__(64) void k_vp8l_match(const uint32_t* __restrict__ 
       const int n = min(run, VP8L_MAX_LENGTH);
       if (n > bn) { bn = n; bk = k; }
     }
-    if (valid) O[q] = (uint32_t)bn | ((uint32_t)bk << 13) | ((uint32_t)MB[q] << 15);
+    if (valid) {
+      uint32_t mb = MB[q];
+      if (mb & VP8L_CACHE_PARTIAL)
+        mb = cache_settle(mb, e, q, (int)npix, S, cstart + (size_t)f * S * VP8L_CACHE_TAB);
+      O[q] = (uint32_t)bn | ((uint32_t)bk << 13) | (mb << 15);
+    }
   }
 }
 
@@ -2060,12 +2136,76 @@ __global__ __launch_bounds__(256) void k_vp8l_tilefeat(const uint32_t* __restric
 struct ClusterSmem {
   uint32_t hc[VP8L_KMAX * VP8L_NS];
   union {
-    uint16_t lc[VP8L_KMAX * VP8L_NS];
+    uint16_t lc[VP8L_NS * VP8L_KMAX];   // per symbol the cost under each cluster (1/256 bit)
     long long feat[VP8L_MAX_HUFF_IMAGE];
   } u;
   uint8_t assign[VP8L_MAX_HUFF_IMAGE];
   uint32_t nsum[VP8L_KMAX * 5];
 };
+
+// The cluster of each tile: the cheapest under the per-symbol costs lc
+// (symbol-major, 16 x u16). Narrow tiles (counts < 2^16, sums < 2^32): every
+// pair of clusters is two dot2 steps of one cost word (v_dot2_u32_u16);
+// wider ones sum in 64 bits, 8 clusters per pass over the tile's list.
+__device__ __forceinline__ void reassign_tiles(ClusterSmem& S, const uint32_t* __restrict__ TL,
+                                               const uint32_t* __restrict__ TN, size_t cap, int nt,
+                                               int K, bool narrow, int wv, int ln) {
+  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+  for (int t = wv; t < nt; t += 16) {
+    const uint32_t* e = TL + (size_t)t * cap;
+    const int m = (int)TN[t];
+    int bc = 0;
+    if (narrow) {
+      uint32_t cost[VP8L_KMAX];
+#pragma unroll
+      for (int c = 0; c < VP8L_KMAX; ++c) cost[c] = 0;
+      for (int i = ln; i < m; i += 64) {
+        const uint32_t v = e[i];
+        const uint32_t cnt = v >> 12;
+        const uint4* row = reinterpret_cast<const uint4*>(S.u.lc + (v & 4095) * VP8L_KMAX);
+        const uint4 w0 = row[0], w1 = row[1];
+        const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        const us2 lo = {(unsigned short)cnt, 0}, hi = {0, (unsigned short)cnt};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const us2 pr = __builtin_bit_cast(us2, w[j]);
+          cost[2 * j] = __builtin_amdgcn_udot2(pr, lo, cost[2 * j], false);
+          cost[2 * j + 1] = __builtin_amdgcn_udot2(pr, hi, cost[2 * j + 1], false);
+        }
+      }
+      uint32_t bv = ~0u;
+#pragma unroll
+      for (int c = 0; c < VP8L_KMAX; ++c) {
+        const uint32_t v = wave_sum(cost[c]);
+        if (c < K && v < bv) { bv = v; bc = c; }
+      }
+    } else {
+      unsigned long long bv = ~0ull;
+      for (int h = 0; h < 2; ++h) {
+        unsigned long long cost[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) cost[c] = 0;
+        for (int i = ln; i < m; i += 64) {
+          const uint32_t v = e[i];
+          const unsigned long long cnt = v >> 12;
+          const uint4 w = reinterpret_cast<const uint4*>(S.u.lc + (v & 4095) * VP8L_KMAX)[h];
+          const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            cost[2 * j] += cnt * (ww[j] & 0xffffu);
+            cost[2 * j + 1] += cnt * (ww[j] >> 16);
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const unsigned long long v = wave_sum(cost[c]);
+          if (8 * h + c < K && v < bv) { bv = v; bc = 8 * h + c; }
+        }
+      }
+    }
+    if (ln == 0) S.assign[t] = (uint8_t)bc;
+  }
+}
 
 // One workgroup per frame (16 waves): k-means of the histogram tiles over
 // their sparse histograms (model: cluster_tiles). A wave owns a tile at a
@@ -2088,6 +2228,8 @@ __global__ __launch_bounds__(1024) void k_vp8l_cluster(vp8l_params p,
   const size_t cap = VP8L_TILE_CAP(hb);
   const uint32_t* TL = tl + (size_t)f * nt * cap;
   const uint32_t* TN = tn + (size_t)f * nt;
+  // a tile's counts fit 16 bits and its costs 32 (count sum <= 4 px, cost < 2^16)
+  const bool narrow = (1 << (2 * hb)) <= 16384;
 
   // init: rank by (feature, tile), K quantiles
   for (int t = tid; t < nt; t += 1024) S.u.feat[t] = feat[(size_t)f * nt + t];
@@ -2130,38 +2272,18 @@ __global__ __launch_bounds__(1024) void k_vp8l_cluster(vp8l_params p,
       }
     }
     __syncthreads();
-    for (int i = tid; i < K * VP8L_NS; i += 1024) {
-      const int c = i / VP8L_NS, s = i - c * VP8L_NS, a = alph_of(s);
-      const uint32_t N = S.nsum[c * 5 + a];
-      const int v = flog2_fx(frac, 10u * N + (uint32_t)alph_size(a, cb)) -
-                    flog2_fx(frac, 10u * S.hc[i] + 1u);
+    // symbol-major, all 16 slots of a symbol in 32 bytes (unused clusters 0)
+    for (int i = tid; i < VP8L_KMAX * VP8L_NS; i += 1024) {
+      const int s = i >> 4, c = i & 15, a = alph_of(s);
+      int v = 0;
+      if (c < K)
+        v = flog2_fx(frac, 10u * S.nsum[c * 5 + a] + (uint32_t)alph_size(a, cb)) -
+            flog2_fx(frac, 10u * S.hc[c * VP8L_NS + s] + 1u);
       S.u.lc[i] = (uint16_t)(v >> 4);
     }
     __syncthreads();
     // reassign: one wave per tile
-    for (int t = wv; t < nt; t += 16) {
-      const uint32_t* e = TL + (size_t)t * cap;
-      const int m = (int)TN[t];
-      unsigned long long cost[VP8L_KMAX];
-#pragma unroll
-      for (int c = 0; c < VP8L_KMAX; ++c) cost[c] = 0;
-      for (int i = ln; i < m; i += 64) {
-        const uint32_t v = e[i];
-        const int sym = (int)(v & 4095);
-        const uint32_t cnt = v >> 12;
-#pragma unroll
-        for (int c = 0; c < VP8L_KMAX; ++c)
-          if (c < K) cost[c] += (unsigned long long)cnt * S.u.lc[c * VP8L_NS + sym];
-      }
-      int bc = 0;
-      unsigned long long bv = ~0ull;
-#pragma unroll
-      for (int c = 0; c < VP8L_KMAX; ++c) {
-        const unsigned long long v = wave_sum(cost[c]);
-        if (c < K && v < bv) { bv = v; bc = c; }
-      }
-      if (ln == 0) S.assign[t] = (uint8_t)bc;
-    }
+    reassign_tiles(S, TL, TN, cap, nt, K, narrow, wv, ln);
     __syncthreads();
   }
   uint32_t* ho = hc_out + (size_t)f * VP8L_KMAX * VP8L_NS;
@@ -2481,7 +2603,8 @@ extern "C" int vp8l_launch_palette_apply(const uint8_t* rgba, size_t fstride, in
 }
 
 extern "C" int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
-                                   const int32_t* tabs, uint8_t* minb, uint16_t* prov,
+                                   const int32_t* tabs, uint8_t* minb, uint32_t* cseg,
+                                   uint16_t* prov,
                                    uint32_t* chist, uint8_t* cbits, uint32_t* ops, int64_t* feat,
                                    uint32_t* tl, uint32_t* tn, uint32_t* hc, uint8_t* assign,
                                    const vp8l_lz* lz, void* stream) {
@@ -2498,7 +2621,8 @@ extern "C" int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
             hipSuccess)
       return 0;
     const int nseg = (npix + LZ_SEG - 1) / LZ_SEG;
-    hipLaunchKernelGGL(k_vp8l_match, dim3(p->h, p->n), dim3(64), 0, st, argb, minb, *p, ops);
+    hipLaunchKernelGGL(k_vp8l_match, dim3(p->h, p->n), dim3(64), 0, st, argb, minb,
+                       (const uint2*)nullptr, 1, *p, ops);
     hipLaunchKernelGGL(k_vp8l_parse, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, *p, ops, prov,
                        (const uint8_t*)cbits);   // the greedy parse: first costs
     hipLaunchKernelGGL(k_lz_runs, dim3(p->n), dim3(64), 0, st, argb, npix, lz->runs);
@@ -2517,12 +2641,19 @@ extern "C" int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
                          (const uint16_t*)lz->llen, lz->dcodes, lz->nd, ops);
     }
   } else {
+    // L2 segments: >= 256 chunks each, so few pixels are left partial
+    const int S = p->cache_bits ? max(1, min(VP8L_CACHE_SEGS, ((npix + 63) >> 6) / 256)) : 1;
     if (p->cache_bits) {
-      hipLaunchKernelGGL(k_vp8l_cache, dim3(p->n), dim3(64), 0, st, argb, npix, minb);
+      if (!cseg) return 0;
+      hipLaunchKernelGGL(k_vp8l_cache, dim3(S, p->n), dim3(64), 0, st, argb, npix, S, minb,
+                         (uint2*)cseg);
+      if (S > 1)
+        hipLaunchKernelGGL(k_vp8l_cache_start, dim3(p->n), dim3(1024), 0, st, S, (uint2*)cseg);
     } else if (hipMemsetAsync(minb, VP8L_NEVER_HIT, (size_t)p->n * npix, st) != hipSuccess) {
       return 0;
     }
-    hipLaunchKernelGGL(k_vp8l_match, dim3(p->h, p->n), dim3(64), 0, st, argb, minb, *p, ops);
+    hipLaunchKernelGGL(k_vp8l_match, dim3(p->h, p->n), dim3(64), 0, st, argb, minb,
+                       (const uint2*)cseg, S, *p, ops);
     if (p->cache_bits) {
       hipLaunchKernelGGL(k_vp8l_parse, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, *p, ops,
                          prov, (const uint8_t*)nullptr);   // provisional

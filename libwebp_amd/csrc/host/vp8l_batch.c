@@ -40,7 +40,7 @@ void vp8l_engine_free(vp8l_engine* l) {
   if (!l) return;
   for (int i = 0; i < 5; ++i) vp8l_engine_free(l->sub[i]);
   free(l->route_eng); free(l->route_slot);
-  hipFree(l->d_minb); hipFree(l->d_prov); hipFree(l->d_chist); hipFree(l->d_cbits);
+  hipFree(l->d_minb); hipFree(l->d_cseg); hipFree(l->d_prov); hipFree(l->d_chist); hipFree(l->d_cbits);
   hipFree(l->d_ehist); hipFree(l->d_scan); hipFree(l->d_fidx); hipFree(l->d_fmode);
   hipFree(l->d_psort); hipFree(l->d_psidx); hipFree(l->d_npal);
   hipHostFree(l->h_ehist); hipHostFree(l->h_scan); hipHostFree(l->h_fidx); hipHostFree(l->h_fmode);
@@ -94,6 +94,7 @@ static vp8l_engine* engine_alloc(const vp8l_params* p, int max_frames, int metho
   if (l->p.cache_bits) {
     CHK(hipMalloc((void**)&l->d_prov, N * np * sizeof(uint16_t)));
     CHK(hipMalloc((void**)&l->d_chist, N * VP8L_CHIST * sizeof(uint32_t)));
+    CHK(hipMalloc((void**)&l->d_cseg, N * VP8L_CACHE_SEGS * VP8L_CACHE_TAB * 2 * sizeof(uint32_t)));
   }
   CHK(hipMalloc((void**)&l->d_cbits, N));
   CHK(hipMalloc((void**)&l->d_fidx, N * sizeof(int)));
@@ -343,7 +344,7 @@ static int pipeline(vp8l_engine* l, hipStream_t st, int threads, const uint8_t* 
       goto fail;
   }
   CHK(hipEventRecord(l->ev[1], st));
-  if (!vp8l_launch_analyze(l->d_argb, &p, l->d_tabs, l->d_minb, l->d_prov, l->d_chist,
+  if (!vp8l_launch_analyze(l->d_argb, &p, l->d_tabs, l->d_minb, l->d_cseg, l->d_prov, l->d_chist,
                            l->d_cbits, l->d_ops, l->d_feat, l->d_tl, l->d_tn, l->d_hc,
                            l->d_assign, p.palette ? &l->lz : NULL, st))
     goto fail;

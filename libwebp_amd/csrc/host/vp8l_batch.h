@@ -28,6 +28,7 @@ typedef struct vp8l_engine {
   uint32_t* d_argb;
   uint32_t* d_ops;
   uint8_t* d_minb;             /* smallest cache size holding each pixel */
+  uint32_t* d_cseg;            /* L2 segment cache tables (vp8l_gpu.h) */
   uint16_t* d_prov;            /* provisional parse */
   uint32_t* d_chist;           /* cache-size choice histograms */
   uint8_t* d_cbits;            /* chosen cache bits per slot */

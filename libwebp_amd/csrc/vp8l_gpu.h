@@ -12,6 +12,8 @@
  *   ehist     N x 13 x 256 uint32        AnalyzeEntropy histograms (L0)
  *   pal       N x VP8L_PAL_STRIDE uint32 colour count (257 = too many) + colours (L0)
  *   minb      N x npix uint8             smallest cache size holding the pixel (L2)
+ *   cseg      N x CACHE_SEGS x CACHE_TAB uint32 pairs   per L2 segment: its last
+ *                                        cache contents, then the contents at its start
  *   ops       N x npix uint32            parse: act | (len - 1) << 2 | dist_code << 14 (L3)
  *   prov      N x npix uint16            provisional parse: act | len << 2 (L3)
  *   chist     N x VP8L_CHIST uint32      cache-size choice histograms (L3)
@@ -39,6 +41,9 @@ extern "C" {
 #define VP8L_KMAX 16               /* max code groups (clusters) per frame */
 #define VP8L_MAX_CACHE_BITS 9      /* largest colour cache (the size is chosen per frame) */
 #define VP8L_NEVER_HIT (VP8L_MAX_CACHE_BITS + 1)
+#define VP8L_CACHE_TAB ((2 << VP8L_MAX_CACHE_BITS) - 2)   /* entries of all 9 cache sizes */
+#define VP8L_CACHE_SEGS 16         /* L2 walks a frame in up to this many segments at once */
+#define VP8L_CACHE_PARTIAL 0x80    /* minb from L2: not settled below the size in bits 0-3 */
 #define VP8L_CLUSTER_ITERS 6
 #define VP8L_MIN_COPY 3
 #define VP8L_MAX_LENGTH 4096
@@ -160,7 +165,8 @@ typedef struct {
  * feeds two rounds of the cost-model parse over the hash chain's and the
  * candidate distances' matches */
 int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p, const int32_t* tabs,
-                        uint8_t* minb, uint16_t* prov, uint32_t* chist, uint8_t* cbits,
+                        uint8_t* minb, uint32_t* cseg, uint16_t* prov, uint32_t* chist,
+                        uint8_t* cbits,
                         uint32_t* ops, int64_t* feat, uint32_t* tl, uint32_t* tn,
                         uint32_t* hc, uint8_t* assign, const vp8l_lz* lz, void* stream);
 /* L6/L7: per-block bit counts, per-frame scan from start_bit[f], and the

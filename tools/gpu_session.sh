@@ -2,7 +2,7 @@
 # One GPU-box session: GPU tests, bench line, K3 stage split, rocprofv3 kernel
 # stats, PMC passes (HBM bytes, SQ issue counters) and the PMC calibration.
 # Usage (on the box): bash tools/gpu_session.sh <tag> [steps...]
-#   steps: tests bench lossless lprof lpmc stages prof pmc sq calib (default: all but the lossless ones)
+#   steps: tests ltests bench lossless lphases lprof lpmc stages prof pmc sq calib (default: all but the lossless ones)
 set -o pipefail
 TAG=${1:-s}; shift
 STEPS=${*:-tests bench stages prof pmc sq calib}
@@ -15,6 +15,10 @@ if has tests; then
   run timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
     > $O/gpu_tests.log 2>&1 || exit 1
 fi
+if has ltests; then   # the lossless GPU tests only
+  run timeout -k 10 400 python -u -m pytest tests/test_vp8l.py -m gpu -x -v --timeout 120 \
+    --timeout-method thread > $O/gpu_ltests.log 2>&1 || exit 1
+fi
 if has bench; then
   run timeout -k 10 400 python3 bench.py --steps 5 --warmup 2 > $O/bench.json 2> $O/bench.err || exit 1
 fi
@@ -26,6 +30,10 @@ if has lprof; then
   (cd /tmp && TMPDIR=/tmp run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
     -d $O/lstats -o run -- python3 $R/bench.py --lossless --no-cpu --no-host-input --steps 2 \
     --warmup 1 > $O/lprof.log 2>&1) || exit 1
+fi
+if has lphases; then   # L1a / L1 phase cycles (diagnostic build)
+  WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_prof.so run timeout -k 10 150 \
+    python3 tools/vp8l_phases.py 1920 1080 256 4 > $O/vp8l_phases.log 2>&1 || exit 1
 fi
 if has stages; then
   for B in 256 1; do

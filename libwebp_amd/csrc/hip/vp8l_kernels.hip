@@ -143,7 +143,11 @@ __device__ unsigned long long g_vp8l_prof[16];
     }                                                                       \
   } while (0)
 #define PS_STAMP_INIT unsigned long long ps_t = __builtin_amdgcn_s_memtime()
+#define PS_PARAM , unsigned long long& ps_t
+#define PS_ARG , ps_t
 #else
+#define PS_PARAM
+#define PS_ARG
 #define PS_STAMP(i) \
   do {              \
   } while (0)
@@ -170,16 +174,14 @@ __device__ __forceinline__ int sp_of(const int8_t* tab, int v) {
 
 template <int T>
 struct TransformSmem {
-  uint32_t src[(T + 1) * (T + 2)];   // rows y0-1.., cols x0-1..x0+tw
+  union {
+    uint32_t src[(T + 1) * (T + 2)];   // rows y0-1.., cols x0-1..x0+tw (until the residuals)
+    uint32_t h9[8 * 128];              // colour search: up to 8 candidates, u16 counts
+  } u;
   uint32_t first[T];                 // P(0, y) for the right-edge TR wrap
-  struct {
-    uint32_t res[T * T];             // the chosen predictor's residuals
-    uint32_t h9[8 * 128];            // colour search: up to 8 candidates, u16 counts
-  } cc;
-  long long slogg[4][256];           // slog(G) per channel and value
-  uint32_t g[4][256];                // the frame's accumulated histograms (A, R, G, B)
+  uint32_t res[T * T];               // the chosen predictor's residuals
   int32_t frac[1024];                // log2 fraction table (model: FLOG2_FRAC)
-  long long cost[16];
+  int32_t cost[2][8];                // colour-search step sums, alternate steps alternate rows
   int32_t ct[4][256];                // cross-entropy cost per channel and residual (model: ce_tables)
   int32_t slogt[T * T + 1];          // slog(t) for the counts a tile can have
   int32_t pcost[16];                 // the tile's cross-entropy cost per predictor
@@ -202,32 +204,47 @@ __device__ __forceinline__ long long slog_fx(const int32_t* frac, uint32_t v) {
   return (long long)v * (((long long)e << 12) + frac[m]);
 }
 
-// block-wide sums of K int64 values into S.cost[0..K) (zeroed by the caller)
-template <int K, int T>
-__device__ __forceinline__ void reduce_costs(TransformSmem<T>& S, const int32_t (&v)[K]) {
+// block-wide sums of K values into cost[0..K) (zeroed beforehand)
+template <int K>
+__device__ __forceinline__ void reduce_costs(int32_t* cost, const int32_t (&v)[K]) {
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int32_t w = wave_sum(v[k]);
-    if (lane_id() == 0) atomicAdd((unsigned long long*)&S.cost[k], (unsigned long long)(long long)w);
+    if (lane_id() == 0) atomicAdd(&cost[k], w);
   }
 }
 
+// what thread b = value b brings to every candidate evaluation: the frame's
+// R and B counts G, slog(G) and PredictionCostSpatial of the value
+struct CcBin {
+  uint32_t g[2];
+  long long sg[2];
+  int spv;
+};
+
 // The bin side of one candidate evaluation: thread b owns value b of each of
-// the K histograms (u16 pairs in h) against channel c of G. Every term fits
-// 32 bits (t <= 4096: slog(t) < 2^28, slog(t + g) - slog(g) ~ t log2(t + g)),
-// and so does a candidate's sum over the bins (< 2^29 at 4096 pixels).
+// the K histograms (u16 pairs in h) against channel ch (0: R, 1: B) of G, and
+// zeroes the words it read for the next step (their other reader is the
+// neighbouring lane of the same wave, whose reads are issued with these).
+// Every term fits 32 bits (t <= 4096: slog(t) < 2^28, slog(t + g) - slog(g) ~
+// t log2(t + g)), and so does a candidate's sum over the bins (< 2^29 at 4096
+// pixels).
 template <int K, int T>
-__device__ __forceinline__ void bin_costs(TransformSmem<T>& S, const uint32_t* h, int c,
-                                          const int8_t* sp, int32_t (&acc)[K]) {
+__device__ __forceinline__ void bin_costs(TransformSmem<T>& S, uint32_t* h, int chn,
+                                          const CcBin& cb, int32_t (&acc)[K]) {
   const int b = threadIdx.x;   // 256 threads = 256 values
-  const uint32_t gv = S.g[c][b];
-  const long long sg = S.slogg[c][b];
-  const int spv = sp_of(sp, b);
+  const uint32_t gv = cb.g[chn];
+  const long long sg = cb.sg[chn];
+  uint32_t w[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) w[k] = h[k * 128 + (b >> 1)];
+#pragma unroll
+  for (int k = 0; k < K; ++k) h[k * 128 + (b >> 1)] = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const uint32_t t = (h[k * 128 + (b >> 1)] >> ((b & 1) * 16)) & 0xffffu;
+    const uint32_t t = (w[k] >> ((b & 1) * 16)) & 0xffffu;
     if (t)
-      acc[k] += 16 * (int32_t)t * spv - (S.slogt[t] + (int32_t)(slog_fx(S.frac, t + gv) - sg));
+      acc[k] += 16 * (int32_t)t * cb.spv - (S.slogt[t] + (int32_t)(slog_fx(S.frac, t + gv) - sg));
   }
 }
 
@@ -250,15 +267,17 @@ struct Hot {
 // KB (green-to-blue, red-to-blue) candidates (b0[], b1[]) -- the two
 // descents are independent (the blue one reads the untransformed red), so
 // their steps share an evaluation
+// Entry: S.u.h9 all zero, S.cost[par] zero; exit: the same for the next step
+// (par ^ 1), after two block barriers.
 template <int KR, int KB, int T>
-__device__ void cc_eval(TransformSmem<T>& S, int np, const int (&r0)[KR > 0 ? KR : 1],
+__device__ void cc_eval(TransformSmem<T>& S, int np, const CcBin& cb, int& par,
+                        const int (&r0)[KR > 0 ? KR : 1],
                         const int (&b0)[KB > 0 ? KB : 1], const int (&b1)[KB > 0 ? KB : 1],
-                        long long (&outR)[KR > 0 ? KR : 1], long long (&outB)[KB > 0 ? KB : 1]) {
+                        long long (&outR)[KR > 0 ? KR : 1], long long (&outB)[KB > 0 ? KB : 1]
+                        PS_PARAM) {
   constexpr int K = KR + KB;
   const int tid = threadIdx.x;
-  for (int i = tid; i < K * 128; i += 256) S.cc.h9[i] = 0;
-  if (tid < K) S.cost[tid] = 0;
-  __syncthreads();
+  PS_STAMP(11);
   // every thread takes every 256th pixel of the tile for all K candidates:
   // the values next to 0 -- most of a good multiplier's residuals -- counted
   // in packed register fields and summed over the wave once (lane k * NH + j
@@ -268,7 +287,7 @@ __device__ void cc_eval(TransformSmem<T>& S, int np, const int (&r0)[KR > 0 ? KR
 #pragma unroll
   for (int k = 0; k < K; ++k) hot[k] = 0;
   for (int i = tid; i < np; i += 256) {
-    const uint32_t r = S.cc.res[i];
+    const uint32_t r = S.res[i];
     const int g = ch(r, 8), rr = ch(r, 16), bb = ch(r, 0);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -276,7 +295,7 @@ __device__ void cc_eval(TransformSmem<T>& S, int np, const int (&r0)[KR > 0 ? KR
                             : (rr - ctd(r0[k], g)) & 255;
       const int q = Hot<T>::slot(v);
       hot[k] += q < Hot<T>::NH ? (1ull << (Hot<T>::FB * q)) : 0ull;
-      if (q >= Hot<T>::NH) hist_add(S.cc.h9 + k * 128, v);
+      if (q >= Hot<T>::NH) hist_add(S.u.h9 + k * 128, v);
     }
   }
   {
@@ -290,10 +309,13 @@ __device__ void cc_eval(TransformSmem<T>& S, int np, const int (&r0)[KR > 0 ? KR
     if (kk < K) {
       const uint32_t t = (uint32_t)(mine >> (Hot<T>::FB * j)) & Hot<T>::MASK;
       const int v = Hot<T>::value(j);
-      if (t) atomicAdd(&S.cc.h9[kk * 128 + (v >> 1)], t << ((v & 1) * 16));
+      if (t) atomicAdd(&S.u.h9[kk * 128 + (v >> 1)], t << ((v & 1) * 16));
     }
   }
   __syncthreads();
+  PS_STAMP(12);
+  // the previous step's sums were read before the barrier above
+  if (tid < 8) S.cost[par ^ 1][tid] = 0;
   int32_t acc[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) acc[k] = 0;
@@ -301,7 +323,7 @@ __device__ void cc_eval(TransformSmem<T>& S, int np, const int (&r0)[KR > 0 ? KR
     int32_t a[KR];
 #pragma unroll
     for (int k = 0; k < KR; ++k) a[k] = 0;
-    bin_costs<KR>(S, S.cc.h9, 1, kSpCC, a);
+    bin_costs<KR>(S, S.u.h9, 0, cb, a);
 #pragma unroll
     for (int k = 0; k < KR; ++k) acc[k] = a[k];
   }
@@ -309,18 +331,19 @@ __device__ void cc_eval(TransformSmem<T>& S, int np, const int (&r0)[KR > 0 ? KR
     int32_t a[KB];
 #pragma unroll
     for (int k = 0; k < KB; ++k) a[k] = 0;
-    bin_costs<KB>(S, S.cc.h9 + KR * 128, 3, kSpCC, a);
+    bin_costs<KB>(S, S.u.h9 + KR * 128, 1, cb, a);
 #pragma unroll
     for (int k = 0; k < KB; ++k) acc[KR + k] = a[k];
   }
-  reduce_costs<K>(S, acc);
+  reduce_costs<K>(S.cost[par], acc);
   __syncthreads();
+  PS_STAMP(13);
 #pragma unroll
-  for (int k = 0; k < KR; ++k) outR[k] = S.cost[k] - CC_ZERO_BONUS * (r0[k] == 0);
+  for (int k = 0; k < KR; ++k) outR[k] = (long long)S.cost[par][k] - CC_ZERO_BONUS * (r0[k] == 0);
 #pragma unroll
   for (int k = 0; k < KB; ++k)
-    outB[k] = S.cost[KR + k] - CC_ZERO_BONUS * ((b0[k] == 0) + (b1[k] == 0));
-  __syncthreads();   // S.cost is reused by the next step
+    outB[k] = (long long)S.cost[par][KR + k] - CC_ZERO_BONUS * ((b0[k] == 0) + (b1[k] == 0));
+  par ^= 1;
 }
 
 // SG: the subtract-green instantiation; a launch of each covers every slot,
@@ -376,6 +399,7 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     return;
   }
 
+  CcBin cb;   // thread tid = value tid of the colour search's histograms
   // per-frame setup: the accumulated histograms (L0's predictor-12 residual
   // histograms of the input frame, plain or sub-green) and their slog, the
   // log2 fraction table
@@ -388,20 +412,24 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     for (int i = tid; i <= T * T; i += 256) S.slogt[i] = (int32_t)slog_fx(S.frac, (uint32_t)i);
     if (tid < 4) S.nsum[tid] = 0;
     __syncthreads();
+    uint32_t gv[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const uint32_t v = eh[hix[c] * 256 + tid];
-      S.g[c][tid] = v;
-      S.slogg[c][tid] = slog_fx(S.frac, v);
-      const uint32_t t = wave_sum(v);
+      gv[c] = eh[hix[c] * 256 + tid];
+      if (c & 1) {
+        cb.g[c >> 1] = gv[c];
+        cb.sg[c >> 1] = slog_fx(S.frac, gv[c]);
+      }
+      const uint32_t t = wave_sum(gv[c]);
       if (lane_id() == 0) atomicAdd(&S.nsum[c], t);
     }
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < 4; ++c)   // model: ce_tables
-      S.ct[c][tid] = flog2_fx(S.frac, 2 * S.nsum[c] + 256) - flog2_fx(S.frac, 2 * S.g[c][tid] + 1);
+      S.ct[c][tid] = flog2_fx(S.frac, 2 * S.nsum[c] + 256) - flog2_fx(S.frac, 2 * gv[c] + 1);
   }
   const bool own_pred = !p.low_effort && !(pexact && pexact[f]);   // else L1a's choice
+  cb.spv = sp_of(kSpCC, tid);
 
   PS_STAMP_INIT;
   for (int tile = tile0; tile < min(tile0 + L1_TILES, ntt); ++tile) {
@@ -429,7 +457,7 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
         }
       }
       if (p.alpha) opaque = false;
-      S.src[i] = v;
+      S.u.src[i] = v;
     }
     if (x0 + tw == W) {
       for (int i = tid; i < th; i += 256) {
@@ -449,7 +477,7 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     opaque = __syncthreads_and(opaque);
     PS_STAMP(6);
 
-    auto at = [&](int lx, int ly) -> uint32_t { return S.src[(ly + 1) * sw + lx + 1]; };
+    auto at = [&](int lx, int ly) -> uint32_t { return S.u.src[(ly + 1) * sw + lx + 1]; };
     auto tr = [&](int lx, int ly) -> uint32_t {   // (y-1)*W + x + 1, linear
       return (x0 + lx + 1 < W) ? at(lx + 1, ly - 1) : S.first[ly];
     };
@@ -506,17 +534,24 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     if (pflag[f]) {
       for (int i = tid; i < np; i += 256) {
         const int ly = i / tw, lx = i - ly * tw;
-        S.cc.res[i] = out[(size_t)(y0 + ly) * W + x0 + lx];
+        S.res[i] = out[(size_t)(y0 + ly) * W + x0 + lx];
       }
     } else {
       for (int i = tid; i < np; i += 256) {
         const int ly = i / tw, lx = i - ly * tw;
         const int fm = fixed_mode(x0 + lx, y0 + ly);
-        S.cc.res[i] = sub_pixels(at(lx, ly), predict(fm >= 0 ? fm : best, at(lx - 1, ly),
+        S.res[i] = sub_pixels(at(lx, ly), predict(fm >= 0 ? fm : best, at(lx - 1, ly),
                                                        at(lx, ly - 1), at(lx - 1, ly - 1), tr(lx, ly)));
       }
     }
+    __syncthreads();   // every source pixel read before the colour search reuses its LDS
     PS_STAMP(8);
+    int par = 0;
+    if (!p.low_effort) {
+      for (int i = tid; i < 8 * 128; i += 256) S.u.h9[i] = 0;
+      if (tid < 8) S.cost[0][tid] = 0;
+      __syncthreads();
+    }
     // colour search (model: choose_cross_color); none at method 0 (vp8l_enc.c:1525-1526)
     int g2r = 0, g2b = 0, r2b = 0;
     if (!p.low_effort) {
@@ -534,7 +569,7 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
 #pragma unroll
         for (int a2 = 0; a2 < 4; ++a2) { b0[a2 + 1] = ax0[a2] * 16; b1[a2 + 1] = ax1[a2] * 16; }
         long long vr[3], vb[5];
-        cc_eval<3, 5, T>(S, np, r0, b0, b1, vr, vb);
+        cc_eval<3, 5, T>(S, np, cb, par, r0, b0, b1, vr, vb PS_ARG);
         bestr = vr[0];
         int k = vr[2] < vr[1] ? 2 : 1;
         if (vr[k] < bestr) { bestr = vr[k]; g2r = r0[k]; }
@@ -555,20 +590,20 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
         if (dr > 0 && blue_on) {
           const int r0[2] = {g2r - dr, g2r + dr};
           long long vr[2];
-          cc_eval<2, 4, T>(S, np, r0, b0, b1, vr, vb);
+          cc_eval<2, 4, T>(S, np, cb, par, r0, b0, b1, vr, vb PS_ARG);
           const int k = vr[1] < vr[0] ? 1 : 0;
           if (vr[k] < bestr) { bestr = vr[k]; g2r = r0[k]; }
         } else if (dr > 0) {
           const int r0[2] = {g2r - dr, g2r + dr}, z[1] = {0};
           long long vr[2], vz[1];
-          cc_eval<2, 0, T>(S, np, r0, z, z, vr, vz);
+          cc_eval<2, 0, T>(S, np, cb, par, r0, z, z, vr, vz PS_ARG);
           const int k = vr[1] < vr[0] ? 1 : 0;
           if (vr[k] < bestr) { bestr = vr[k]; g2r = r0[k]; }
           continue;
         } else if (blue_on) {
           const int z[1] = {0};
           long long vz[1];
-          cc_eval<0, 4, T>(S, np, z, b0, b1, vz, vb);
+          cc_eval<0, 4, T>(S, np, cb, par, z, b0, b1, vz, vb PS_ARG);
         } else {
           break;
         }
@@ -585,7 +620,7 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
     __syncthreads();   // every residual of the tile read before any is overwritten
     for (int i = tid; i < np; i += 256) {
       const int ly = i / tw, lx = i - ly * tw;
-      const uint32_t r = S.cc.res[i];
+      const uint32_t r = S.res[i];
       const int g = ch(r, 8), rr = ch(r, 16), bb = ch(r, 0);
       const int nr = (rr - ctd(g2r, g)) & 255;
       const int nb = (bb - ctd(g2b, g) - ctd(r2b, rr)) & 255;

@@ -28,6 +28,7 @@ tb = 5 if method in (2, 3, 4) else (4 if method > 4 else 6)
 ntt = ((W + (1 << tb) - 1) >> tb) * ((H + (1 << tb) - 1) >> tb)
 names = {0: "L1a load", 1: "L1a maxd/flags", 2: "L1a histograms", 3: "L1a terms",
          4: "L1a chains", 5: "L1a select+acc", 6: "L1 load", 7: "L1 predictor choice",
-         8: "L1 residuals", 9: "L1 colour search", 10: "L1 final residuals"}
+         8: "L1 residuals", 9: "L1 colour search (rest)", 10: "L1 final residuals",
+         11: "  cc zero", 12: "  cc pixels", 13: "  cc bins"}
 for i, n in names.items():
     print("%-18s %12.0f clk per tile" % (n, out[i] / (B * ntt)))

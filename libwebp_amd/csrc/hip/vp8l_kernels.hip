@@ -634,6 +634,369 @@ __global__ __launch_bounds__(256) void k_vp8l_transform(const uint8_t* __restric
   }
 }
 
+// ------------------------------------------------------------------ L1 (wave tiles)
+// The same transform search with one wave per tile (T = 8, 16, 32): a
+// workgroup's four waves share the frame's tables and each walks its own
+// tiles, so no block barrier sits in the search. A lane owns the tile's
+// pixels ln, ln + 64, .. (PX of them) and keeps their residuals in
+// registers; every sum over the tile is a wave butterfly, which leaves the
+// total in every lane. Same arithmetic and order of choices as
+// k_vp8l_transform (model: choose_predictors_ce, choose_cross_color).
+#define L1W_TPW 2   // tiles per wave
+template <int T>
+struct WaveTile {
+  union {
+    uint32_t src[(T + 1) * (T + 2)];   // rows y0-1.., cols x0-1..x0+tw (until the residuals)
+    uint32_t h9[8 * 128];              // colour search: up to 8 candidates, u16 counts
+  } u;
+  uint32_t first[T];
+};
+template <int T>
+struct TransformWSmem {
+  int32_t frac[1024];
+  int32_t ct[4][256];
+  uint32_t g[2][256];                // the frame's accumulated R and B histograms
+  long long slogg[2][256];           // and their slog
+  uint32_t nsum[4];
+  WaveTile<T> w[4];
+};
+
+// LDS written by some lanes of a wave, then read by others
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// v log2 v in 1/4096 bit for the counts of a tile (v <= 4096: 32 bits)
+__device__ __forceinline__ int32_t slog_small(const int32_t* frac, uint32_t v) {
+  if (v <= 1) return 0;
+  const int e = 31 - __clz((int)v);
+  const uint32_t m = (e >= 10 ? (v >> (e - 10)) : (v << (10 - e))) & 1023;
+  return (int32_t)v * ((e << 12) + frac[m]);
+}
+
+__device__ __forceinline__ uint32_t load_px(const uint8_t* img, int rstride, bool plane, int x,
+                                            int y, bool sg, bool& opaque) {
+  if (plane) {   // ALPH: the alpha plane as green
+    const uint32_t g = img[(size_t)y * rstride + x];
+    opaque = false;
+    return sg ? (((0u - g) & 255) << 16) | (g << 8) | ((0u - g) & 255) : g << 8;
+  }
+  const uint32_t v = *reinterpret_cast<const uint32_t*>(img + (size_t)y * rstride + 4 * x);
+  const uint32_t r = v & 255, g = (v >> 8) & 255, b = (v >> 16) & 255, a = v >> 24;
+  opaque &= a == 255;
+  return sg ? (a << 24) | (((r - g) & 255) << 16) | (g << 8) | ((b - g) & 255)
+            : (a << 24) | (r << 16) | (g << 8) | b;
+}
+
+// one colour-search step of a wave's tile (cc_eval's arithmetic): h9 zero on
+// entry and on exit
+template <int KR, int KB, int T, int PX>
+__device__ __forceinline__ void cc_eval_w(TransformWSmem<T>& S, uint32_t* h9, const uint32_t (&res)[PX], int np,
+                          const int (&spv)[2], const int (&r0)[KR > 0 ? KR : 1],
+                          const int (&b0)[KB > 0 ? KB : 1], const int (&b1)[KB > 0 ? KB : 1],
+                          long long (&outR)[KR > 0 ? KR : 1], long long (&outB)[KB > 0 ? KB : 1]) {
+  constexpr int K = KR + KB;
+  const int ln = lane_id();
+  uint64_t hot[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) hot[k] = 0;
+#pragma unroll
+  for (int j = 0; j < PX; ++j) {
+    if (ln + 64 * j >= np) break;
+    uint32_t r = res[j];
+    asm volatile("" : "+v"(r));   // no channel values kept live across the steps: registers
+    const int g = ch(r, 8), rr = ch(r, 16), bb = ch(r, 0);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int v = k >= KR ? (bb - ctd(b0[k - KR], g) - ctd(b1[k - KR], rr)) & 255
+                            : (rr - ctd(r0[k], g)) & 255;
+      const int q = Hot<T>::slot(v);
+      hot[k] += q < Hot<T>::NH ? (1ull << (Hot<T>::FB * q)) : 0ull;
+      if (q >= Hot<T>::NH) hist_add(h9 + k * 128, v);
+    }
+  }
+  {
+    const int kk = ln / Hot<T>::NH, j = ln - kk * Hot<T>::NH;
+    uint64_t mine = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint64_t t = wave_sum(hot[k]);
+      if (k == kk) mine = t;
+    }
+    if (kk < K) {
+      const uint32_t t = (uint32_t)(mine >> (Hot<T>::FB * j)) & Hot<T>::MASK;
+      const int v = Hot<T>::value(j);
+      if (t) atomicAdd(&h9[kk * 128 + (v >> 1)], t << ((v & 1) * 16));
+    }
+  }
+  wave_sync();
+  // bins: lane ln owns values ln + 64 i; the words it reads are zeroed by
+  // their two readers (neighbouring lanes) after the reads
+  int32_t acc[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int b = ln + 64 * i;
+    uint32_t w[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) w[k] = h9[k * 128 + (b >> 1)];
+#pragma unroll
+    for (int k = 0; k < K; ++k) h9[k * 128 + (b >> 1)] = 0;
+    const int sp = i == 0 ? spv[0] : i == 3 ? spv[1] : 0;   // |value| >= 64 in between: 0
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint32_t t = (w[k] >> ((b & 1) * 16)) & 0xffffu;
+      if (t) {
+        const int c = k < KR ? 0 : 1;   // R or B
+        acc[k] += 16 * (int32_t)t * sp -
+                  (slog_small(S.frac, t) + (int32_t)(slog_fx(S.frac, t + S.g[c][b]) - S.slogg[c][b]));
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < KR; ++k) outR[k] = (long long)wave_sum(acc[k]) - CC_ZERO_BONUS * (r0[k] == 0);
+#pragma unroll
+  for (int k = 0; k < KB; ++k)
+    outB[k] = (long long)wave_sum(acc[KR + k]) - CC_ZERO_BONUS * ((b0[k] == 0) + (b1[k] == 0));
+  wave_sync();
+}
+
+template <int T, bool SG>
+__global__ __launch_bounds__(256) void k_vp8l_transform_w(const uint8_t* __restrict__ rgba,
+                                                          size_t fstride, int rstride, vp8l_params p,
+                                                          const int* __restrict__ fidx,
+                                                          const int* __restrict__ efidx,
+                                                          const uint8_t* __restrict__ fmode,
+                                                          const uint32_t* __restrict__ ehist,
+                                                          const int32_t* __restrict__ frac_tab,
+                                                          uint8_t* __restrict__ modes,
+                                                          const uint32_t* __restrict__ pflag,
+                                                          const uint8_t* __restrict__ pexact,
+                                                          uint32_t* __restrict__ argb_out,
+                                                          uint32_t* __restrict__ mult,
+                                                          uint32_t* __restrict__ alpha_flag) {
+  constexpr int PX = T * T / 64;
+  static_assert(PX >= 1, "one wave per tile needs >= 64 pixels");
+  __shared__ TransformWSmem<T> S;
+  const int tid = threadIdx.x, ln = lane_id(), wv = tid >> 6, f = blockIdx.z;
+  const int W = p.w, H = p.h;
+  const uint8_t* img = rgba + (size_t)(fidx ? fidx[f] : f) * fstride;
+  const int tiles_x = (W + T - 1) / T, tiles_y = (H + T - 1) / T, ntt = tiles_x * tiles_y;
+  const int emode = fmode ? (int)fmode[f] : VP8L_MODE_SPATIAL;
+  if (((emode & VP8L_MODE_SUBGREEN) != 0) != SG) return;
+  const int tile0 = blockIdx.x * 4 * L1W_TPW, tile1 = min(tile0 + 4 * L1W_TPW, ntt);
+  const bool plane = p.alpha != 0;
+  uint32_t* out = argb_out + (size_t)f * W * H;
+
+  if (!(emode & VP8L_MODE_SPATIAL)) {   // direct / subtract green only: no predictor
+    bool opaque = true;
+    for (int tile = tile0 + wv; tile < tile1; tile += 4) {
+      const int x0 = (tile % tiles_x) * T, y0 = (tile / tiles_x) * T;
+      const int tw = min(T, W - x0), th = min(T, H - y0);
+      for (int i = ln; i < tw * th; i += 64) {
+        const int ly = i / tw, lx = i - ly * tw;
+        out[(size_t)(y0 + ly) * W + x0 + lx] = load_px(img, rstride, plane, x0 + lx, y0 + ly, SG, opaque);
+      }
+    }
+    if (!plane && !__all(opaque) && ln == 0) atomicOr(&alpha_flag[f], 1u);
+    return;
+  }
+
+  // per-frame setup (as k_vp8l_transform)
+  {
+    const uint32_t* eh = ehist + (size_t)(efidx ? efidx[f] : f) * VP8L_EHIST;
+    const int hix[4] = {VP8L_EH_ACC + 0, VP8L_EH_ACC + (SG ? 4 : 1), VP8L_EH_ACC + 2,
+                        VP8L_EH_ACC + (SG ? 5 : 3)};
+    for (int i = tid; i < 1024; i += 256) S.frac[i] = frac_tab[i];
+    if (tid < 4) S.nsum[tid] = 0;
+    __syncthreads();
+    uint32_t gv[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      gv[c] = eh[hix[c] * 256 + tid];
+      if (c & 1) {
+        S.g[c >> 1][tid] = gv[c];
+        S.slogg[c >> 1][tid] = slog_fx(S.frac, gv[c]);
+      }
+      const uint32_t t = wave_sum(gv[c]);
+      if (ln == 0) atomicAdd(&S.nsum[c], t);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; ++c)   // model: ce_tables
+      S.ct[c][tid] = flog2_fx(S.frac, 2 * S.nsum[c] + 256) - flog2_fx(S.frac, 2 * gv[c] + 1);
+    __syncthreads();
+  }
+  const bool own_pred = !p.low_effort && !(pexact && pexact[f]);   // else L1a's choice
+  const int spv[2] = {sp_of(kSpCC, ln), sp_of(kSpCC, ln + 192)};
+  WaveTile<T>& Wt = S.w[wv];
+  bool any_alpha = false;
+
+  for (int tile = tile0 + wv; tile < tile1; tile += 4) {
+    const int x0 = (tile % tiles_x) * T, y0 = (tile / tiles_x) * T;
+    const int tw = min(T, W - x0), th = min(T, H - y0);
+    const int sw = tw + 2, np = tw * th;
+    // the tile (+ the row above and the column left) into LDS
+    bool opaque = true;
+    for (int i = ln; i < (th + 1) * sw; i += 64) {
+      const int ly = i / sw, lx = i - ly * sw;
+      const int y = y0 - 1 + ly, x = x0 - 1 + lx;
+      uint32_t v = 0;
+      if (y >= 0 && x >= 0 && x < W) {
+        bool o = true;
+        v = load_px(img, rstride, plane, x, y, SG, o);
+        opaque &= o;
+        if (!o && !plane && ly > 0 && lx > 0 && lx <= tw) any_alpha = true;
+      }
+      Wt.u.src[i] = v;
+    }
+    if (x0 + tw == W)
+      for (int i = ln; i < th; i += 64) Wt.first[i] = load_px(img, rstride, plane, 0, y0 + i, SG, opaque);
+    opaque = !plane && __all(opaque);
+    wave_sync();
+
+    auto at = [&](int lx, int ly) -> uint32_t { return Wt.u.src[(ly + 1) * sw + lx + 1]; };
+    auto tr = [&](int lx, int ly) -> uint32_t {   // (y-1)*W + x + 1, linear
+      return (x0 + lx + 1 < W) ? at(lx + 1, ly - 1) : Wt.first[ly];
+    };
+    auto fixed_mode = [&](int x, int y) -> int { return y == 0 ? (x == 0 ? 0 : 1) : (x == 0 ? 2 : -1); };
+    int best;
+    if (own_pred) {   // model: choose_predictors_ce (fixed-predictor pixels: one cost for all)
+      int32_t pc[14];
+#pragma unroll
+      for (int m = 0; m < 14; ++m) pc[m] = 0;
+      auto ce_sum = [&](auto opq) {
+#pragma unroll
+        for (int j = 0; j < PX; ++j) {
+          const int i = ln + 64 * j;
+          if (i >= np) break;
+          const int ly = i / tw, lx = i - ly * tw;
+          if (fixed_mode(x0 + lx, y0 + ly) >= 0) continue;
+          const uint32_t P = at(lx, ly), L = at(lx - 1, ly), T_ = at(lx, ly - 1);
+          const uint32_t TL = at(lx - 1, ly - 1), TR = tr(lx, ly);
+#pragma unroll
+          for (int m = 0; m < 14; ++m) {
+            const uint32_t r = sub_pixels(P, predict(m, L, T_, TL, TR));
+            pc[m] += (decltype(opq)::value ? 0 : S.ct[0][r >> 24]) + S.ct[1][ch(r, 16)] +
+                     S.ct[2][ch(r, 8)] + S.ct[3][ch(r, 0)];
+          }
+        }
+      };
+      if (opaque) ce_sum(std::true_type{});
+      else ce_sum(std::false_type{});
+      best = 0;
+      int32_t bv = wave_sum(pc[0]);
+#pragma unroll
+      for (int m = 1; m < 14; ++m) {
+        const int32_t v = wave_sum(pc[m]);
+        if (v < bv) { bv = v; best = m; }
+      }
+      if (ln == 0) modes[(size_t)f * ntt + tile] = (uint8_t)best;
+    } else {
+      best = modes[(size_t)f * ntt + tile];
+    }
+    // the chosen predictor's residuals (or the serial pass's, pflag), in registers
+    uint32_t res[PX];
+#pragma unroll
+    for (int j = 0; j < PX; ++j) {
+      const int i = ln + 64 * j;
+      res[j] = 0;
+      if (i < np) {
+        const int ly = i / tw, lx = i - ly * tw;
+        if (pflag[f]) {
+          res[j] = out[(size_t)(y0 + ly) * W + x0 + lx];
+        } else {
+          const int fm = fixed_mode(x0 + lx, y0 + ly);
+          res[j] = sub_pixels(at(lx, ly), predict(fm >= 0 ? fm : best, at(lx - 1, ly), at(lx, ly - 1),
+                                                  at(lx - 1, ly - 1), tr(lx, ly)));
+        }
+      }
+    }
+    wave_sync();   // every source pixel read before h9 reuses the LDS
+    int g2r = 0, g2b = 0, r2b = 0;
+    if (!p.low_effort) {   // model: choose_cross_color; none at method 0
+      uint32_t* h9 = Wt.u.h9;
+      for (int i = ln; i < 8 * 128; i += 64) h9[i] = 0;
+      wave_sync();
+      const int ax0[4] = {0, 0, -1, 1}, ax1[4] = {-1, 1, 0, 0};
+      const int bdel[7] = {16, 16, 8, 4, 2, 2, 2};
+      long long bestr, bestb;
+      {
+        const int r0[3] = {0, -32, 32};
+        int b0[5], b1[5];
+        b0[0] = 0; b1[0] = 0;
+#pragma unroll
+        for (int a2 = 0; a2 < 4; ++a2) { b0[a2 + 1] = ax0[a2] * 16; b1[a2 + 1] = ax1[a2] * 16; }
+        long long vr[3], vb[5];
+        cc_eval_w<3, 5, T, PX>(S, h9, res, np, spv, r0, b0, b1, vr, vb);
+        bestr = vr[0];
+        int k = vr[2] < vr[1] ? 2 : 1;
+        if (vr[k] < bestr) { bestr = vr[k]; g2r = r0[k]; }
+        bestb = vb[0];
+        k = 1;
+#pragma unroll
+        for (int a2 = 2; a2 < 5; ++a2)
+          if (vb[a2] < vb[k]) k = a2;
+        if (vb[k] < bestb) { bestb = vb[k]; g2b = b0[k]; r2b = b1[k]; }
+      }
+      bool blue_on = true;
+      for (int it = 1; it < 7; ++it) {
+        const int d = bdel[it], dr = 32 >> it;
+        int b0[4], b1[4];
+#pragma unroll
+        for (int a2 = 0; a2 < 4; ++a2) { b0[a2] = g2b + ax0[a2] * d; b1[a2] = r2b + ax1[a2] * d; }
+        long long vb[4];
+        if (dr > 0 && blue_on) {
+          const int r0[2] = {g2r - dr, g2r + dr};
+          long long vr[2];
+          cc_eval_w<2, 4, T, PX>(S, h9, res, np, spv, r0, b0, b1, vr, vb);
+          const int k = vr[1] < vr[0] ? 1 : 0;
+          if (vr[k] < bestr) { bestr = vr[k]; g2r = r0[k]; }
+        } else if (dr > 0) {
+          const int r0[2] = {g2r - dr, g2r + dr}, z[1] = {0};
+          long long vr[2], vz[1];
+          cc_eval_w<2, 0, T, PX>(S, h9, res, np, spv, r0, z, z, vr, vz);
+          const int k = vr[1] < vr[0] ? 1 : 0;
+          if (vr[k] < bestr) { bestr = vr[k]; g2r = r0[k]; }
+          continue;
+        } else if (blue_on) {
+          const int z[1] = {0};
+          long long vz[1];
+          cc_eval_w<0, 4, T, PX>(S, h9, res, np, spv, z, b0, b1, vz, vb);
+        } else {
+          break;
+        }
+        int k = 0;
+#pragma unroll
+        for (int a2 = 1; a2 < 4; ++a2)
+          if (vb[a2] < vb[k]) k = a2;
+        if (vb[k] < bestb) { bestb = vb[k]; g2b = b0[k]; r2b = b1[k]; }
+        if (d == 2 && g2b == 0 && r2b == 0) blue_on = false;
+      }
+    }
+    // final residuals
+#pragma unroll
+    for (int j = 0; j < PX; ++j) {
+      const int i = ln + 64 * j;
+      if (i >= np) break;
+      const int ly = i / tw, lx = i - ly * tw;
+      const uint32_t r = res[j];
+      const int g = ch(r, 8), rr = ch(r, 16), bb = ch(r, 0);
+      const int nr = (rr - ctd(g2r, g)) & 255;
+      const int nb = (bb - ctd(g2b, g) - ctd(r2b, rr)) & 255;
+      out[(size_t)(y0 + ly) * W + x0 + lx] = (r & 0xff00ff00u) | ((uint32_t)nr << 16) | (uint32_t)nb;
+    }
+    if (ln == 0)
+      mult[(size_t)f * ntt + tile] =
+          (uint32_t)(g2r & 255) | ((uint32_t)(g2b & 255) << 8) | ((uint32_t)(r2b & 255) << 16);
+    wave_sync();   // the next tile's load reuses the LDS
+  }
+  if (__any(any_alpha) && ln == 0) atomicOr(&alpha_flag[f], 1u);
+}
+
 // ------------------------------------------------------------------ L1a
 // VP8LResidualImage's predictor choice, exactly (model: residual_image;
 // src/enc/predictor_enc.c:299-409,476-516). Serial over the frame's tiles in
@@ -2194,18 +2557,24 @@ __device__ __forceinline__ void reassign_tiles(ClusterSmem& S, const uint32_t* _
       uint32_t cost[VP8L_KMAX];
 #pragma unroll
       for (int c = 0; c < VP8L_KMAX; ++c) cost[c] = 0;
-      for (int i = ln; i < m; i += 64) {
-        const uint32_t v = e[i];
-        const uint32_t cnt = v >> 12;
-        const uint4* row = reinterpret_cast<const uint4*>(S.u.lc + (v & 4095) * VP8L_KMAX);
-        const uint4 w0 = row[0], w1 = row[1];
-        const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-        const us2 lo = {(unsigned short)cnt, 0}, hi = {0, (unsigned short)cnt};
+      for (int i0 = ln; i0 < m; i0 += 256) {   // 4 loads in flight per lane
+        uint32_t ev[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const us2 pr = __builtin_bit_cast(us2, w[j]);
-          cost[2 * j] = __builtin_amdgcn_udot2(pr, lo, cost[2 * j], false);
-          cost[2 * j + 1] = __builtin_amdgcn_udot2(pr, hi, cost[2 * j + 1], false);
+        for (int u = 0; u < 4; ++u) ev[u] = i0 + 64 * u < m ? e[i0 + 64 * u] : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t v = ev[u];   // 0: past the list (count 0 adds nothing)
+          const uint32_t cnt = v >> 12;
+          const uint4* row = reinterpret_cast<const uint4*>(S.u.lc + (v & 4095) * VP8L_KMAX);
+          const uint4 w0 = row[0], w1 = row[1];
+          const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+          const us2 lo = {(unsigned short)cnt, 0}, hi = {0, (unsigned short)cnt};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const us2 pr = __builtin_bit_cast(us2, w[j]);
+            cost[2 * j] = __builtin_amdgcn_udot2(pr, lo, cost[2 * j], false);
+            cost[2 * j + 1] = __builtin_amdgcn_udot2(pr, hi, cost[2 * j + 1], false);
+          }
         }
       }
       uint32_t bv = ~0u;
@@ -2288,9 +2657,13 @@ __global__ __launch_bounds__(1024) void k_vp8l_cluster(vp8l_params p,
       uint32_t* hcc = S.hc + S.assign[t] * VP8L_NS;
       const uint32_t* e = TL + (size_t)t * cap;
       const int m = (int)TN[t];
-      for (int i = ln; i < m; i += 64) {
-        const uint32_t v = e[i];
-        atomicAdd(&hcc[v & 4095], v >> 12);
+      for (int i0 = ln; i0 < m; i0 += 256) {   // 4 loads in flight per lane
+        uint32_t v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = i0 + 64 * j < m ? e[i0 + 64 * j] : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (v[j]) atomicAdd(&hcc[v[j] & 4095], v[j] >> 12);
       }
     }
     __syncthreads();
@@ -2335,6 +2708,19 @@ __device__ __forceinline__ int pix_bits(const PixSym& s, const uint32_t* ct) {
     if (s.s[k] >= 0) b += (int)(ct[s.s[k]] >> 16);
   return b;
 }
+static_assert(VP8L_BLOCK == 4 * 256, "bit writer: 4 pixels per thread");
+// words q0..q0+3 of a frame's array (one 16-byte load when all are inside
+// and aligned: frames of npix % 4 == 0)
+__device__ __forceinline__ void load4(const uint32_t* __restrict__ a, size_t q0, size_t npix,
+                                      uint32_t (&o)[4]) {
+  if (q0 + 4 <= npix && ((reinterpret_cast<uintptr_t>(a + q0) & 15) == 0)) {
+    const uint4 v = *reinterpret_cast<const uint4*>(a + q0);
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = q0 + k < npix ? a[q0 + k] : 0u;
+  }
+}
 __device__ __forceinline__ const uint32_t* pixel_codes(const vp8l_params& p, const uint32_t* ctab,
                                                        const uint8_t* gtile, int f, size_t q) {
   const int W = p.w, hb = p.hb;
@@ -2359,11 +2745,17 @@ __global__ __launch_bounds__(256) void k_vp8l_bitcount(const uint32_t* __restric
   if (tid == 0) tot = 0;
   __syncthreads();
   uint32_t b = 0;
+  const size_t q0 = (size_t)blk * VP8L_BLOCK + tid * (VP8L_BLOCK / 256);
+  const int cb = cbits[f];
+  uint32_t op4[4], px4[4];
+  load4(ops + f * npix, q0, npix, op4);
+  load4(argb + f * npix, q0, npix, px4);
+#pragma unroll
   for (int k = 0; k < VP8L_BLOCK / 256; ++k) {
-    const size_t q = (size_t)blk * VP8L_BLOCK + tid * (VP8L_BLOCK / 256) + k;
+    const size_t q = q0 + k;
     if (q >= npix) break;
     PixSym s;
-    pix_symbols(ops[f * npix + q], argb[f * npix + q], cbits[f], s);
+    pix_symbols(op4[k], px4[k], cb, s);
     b += pix_bits(s, pixel_codes(p, ctab, gtile, f, q));
   }
   b = wave_sum(b);
@@ -2422,11 +2814,16 @@ __global__ __launch_bounds__(256) void k_vp8l_write(const uint32_t* __restrict__
   PixSym s[VP8L_BLOCK / 256];
   const uint32_t* ct[VP8L_BLOCK / 256];
   uint32_t mine = 0;
+  const size_t q0 = (size_t)blk * VP8L_BLOCK + tid * (VP8L_BLOCK / 256);
+  const int cb = cbits[f];
+  uint32_t op4[4], px4[4];
+  load4(ops + f * npix, q0, npix, op4);
+  load4(argb + f * npix, q0, npix, px4);
 #pragma unroll
   for (int k = 0; k < VP8L_BLOCK / 256; ++k) {
-    const size_t q = (size_t)blk * VP8L_BLOCK + tid * (VP8L_BLOCK / 256) + k;
+    const size_t q = q0 + k;
     if (q < npix) {
-      pix_symbols(ops[f * npix + q], argb[f * npix + q], cbits[f], s[k]);
+      pix_symbols(op4[k], px4[k], cb, s[k]);
       ct[k] = pixel_codes(p, ctab, gtile, f, q);
       mine += pix_bits(s[k], ct[k]);
     } else {
@@ -2563,6 +2960,7 @@ extern "C" int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rs
   if (!fmode) sg_mask = 1;
   const int ntt = ((p->w + (1 << p->tb) - 1) >> p->tb) * ((p->h + (1 << p->tb) - 1) >> p->tb);
   dim3 grid((ntt + L1_TILES - 1) / L1_TILES, 1, p->n);
+  dim3 gridw((ntt + 4 * L1W_TPW - 1) / (4 * L1W_TPW), 1, p->n);
   hipStream_t st = (hipStream_t)stream;
   const int32_t* frac = tabs + 4097;
   const float* ftabs = reinterpret_cast<const float*>(tabs + VP8L_TAB_FSLOG);
@@ -2588,17 +2986,22 @@ extern "C" int vp8l_launch_transform(const uint8_t* rgba, size_t fstride, int rs
   hipLaunchKernelGGL((k_vp8l_transform<T, SG>), grid, dim3(256), 0, st, rgba, fstride, rstride, \
                      *p, fidx, efidx, fmode, ehist, frac, modes, (const uint32_t*)pflag, pexact, \
                      argb, mult, alpha_flag)
+#define L1W(T, SG)                                                                               \
+  hipLaunchKernelGGL((k_vp8l_transform_w<T, SG>), gridw, dim3(256), 0, st, rgba, fstride,         \
+                     rstride, *p, fidx, efidx, fmode, ehist, frac, modes, (const uint32_t*)pflag, \
+                     pexact, argb, mult, alpha_flag)
   for (int sg = 0; sg < 2; ++sg) {
     if (!((sg_mask >> sg) & 1)) continue;
     switch (p->tb) {
       case 2: if (sg) L1(4, true); else L1(4, false); break;
-      case 3: if (sg) L1(8, true); else L1(8, false); break;
-      case 4: if (sg) L1(16, true); else L1(16, false); break;
-      case 5: if (sg) L1(32, true); else L1(32, false); break;
+      case 3: if (sg) L1W(8, true); else L1W(8, false); break;
+      case 4: if (sg) L1W(16, true); else L1W(16, false); break;
+      case 5: if (sg) L1W(32, true); else L1W(32, false); break;
       default: if (sg) L1(64, true); else L1(64, false); break;
     }
   }
 #undef L1
+#undef L1W
   return check_launch();
 }
 

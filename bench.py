@@ -259,8 +259,10 @@ class StubBatch:
 
 def lossless_line(args, world, B, W, H, elapsed, tails, total_bytes, solo=None):
     """configs[4] line: VP8L encode. Dominant kernel: the L1 transform tile
-    kernel (k_vp8l_transform); algorithmic bytes per launch = RGBA read
-    (4 B/px) + residual ARGB written (4 B/px) + per-tile modes/multipliers."""
+    kernel (k_vp8l_transform_w: one wave per 8..32-pixel tile, or
+    k_vp8l_transform for 4- and 64-pixel tiles); algorithmic bytes per launch
+    = RGBA read (4 B/px) + residual ARGB written (4 B/px) + per-tile
+    modes/multipliers."""
     mp_ = world * B * W * H * args.steps / 1e6
     steps = len(tails)
     avg = lambda i: sum(t[i] for t in tails) / steps
@@ -272,7 +274,8 @@ def lossless_line(args, world, B, W, H, elapsed, tails, total_bytes, solo=None):
     achieved = l1_bytes / l1_solo / 1e9 if l1_solo > 0 else 0.0
     # PMC bytes of one k_vp8l_transform launch of this workload (a step is one
     # instance's call on the whole batch)
-    l1_traffic, l1_tsrc = measured_traffic("k_vp8l_transform", B, W, H, args.quality,
+    l1_kernel = "k_vp8l_transform_w" if 3 <= tb <= 5 else "k_vp8l_transform"
+    l1_traffic, l1_tsrc = measured_traffic(l1_kernel, B, W, H, args.quality,
                                            args.method, lossless=True)
     return {
         "metric": "megapixels/sec encoded (cwebp -lossless -m 4, 1920x1080 batch)",
@@ -292,7 +295,7 @@ def lossless_line(args, world, B, W, H, elapsed, tails, total_bytes, solo=None):
                    "frames_per_gpu": B, "width": W, "height": H, "quality": args.quality,
                    "method": args.method, "parallelism": "frames sharded %d ways" % world,
                    "engines_per_gpu": getattr(args, "engines_used", 1)},
-        "roofline": {"bound": "hbm", "kernel": "k_vp8l_transform", "achieved": round(achieved, 3),
+        "roofline": {"bound": "hbm", "kernel": l1_kernel, "achieved": round(achieved, 3),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": l1_traffic,
                      "traffic_source": l1_tsrc,
@@ -300,7 +303,8 @@ def lossless_line(args, world, B, W, H, elapsed, tails, total_bytes, solo=None):
                      "algorithmic_bytes_per_launch": l1_bytes,
                      # the per-frame-serial kernels (one wave / one workgroup per
                      # frame): their share is k_cache_parse_cluster_events below
-                     "per_frame_serial_kernels": ["k_vp8l_cache (one wave per frame)",
+                     "per_frame_serial_kernels": ["k_vp8l_cache (one wave per frame segment, "
+                                                  "up to 16 segments)",
                                                   "k_vp8l_cluster (one workgroup per frame)",
                                                   "k_vp8l_predsel (one workgroup per frame, "
                                                   "near-lossless / transparent frames only)"]},

@@ -63,7 +63,7 @@ def parse_args(argv=None):
     ap.add_argument("--engines", type=int, default=0,
                     help="encoder instances on their own streams and host threads; steps are "
                          "dealt round-robin so one batch's host work overlaps another's kernels "
-                         "(0: 3 lossy, 2 lossless -- profiles/r3/ab5_*.json)")
+                         "(0: 3 -- profiles/r3/ab5_*.json, lab_*.json)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="CPU work per baseline leg (single thread, all cores)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -441,7 +441,7 @@ def main(argv=None):
     # timed steps are dealt round-robin to one host thread per engine (the
     # ctypes calls release the GIL), so one batch's host stages (segment
     # setup, partition 0, RIFF write) run while another batch's kernels do
-    engines = args.engines or (2 if args.lossless else 3)
+    engines = args.engines or 3
     E = 1 if args.stub else max(1, min(engines, args.steps))
     args.engines_used = E
     encs = [enc]

@@ -2,7 +2,7 @@
 # One GPU-box session: GPU tests, bench line, K3 stage split, rocprofv3 kernel
 # stats, PMC passes (HBM bytes, SQ issue counters) and the PMC calibration.
 # Usage (on the box): bash tools/gpu_session.sh <tag> [steps...]
-#   steps: tests ltests bench lossless lphases lprof lpmc stages prof pmc sq calib (default: all but the lossless ones)
+#   steps: tests ltests bench lossless lab cfg4 lphases lprof lpmc stages prof pmc sq calib (default: all but the lossless ones)
 set -o pipefail
 TAG=${1:-s}; shift
 STEPS=${*:-tests bench stages prof pmc sq calib}
@@ -23,8 +23,23 @@ if has bench; then
   run timeout -k 10 400 python3 bench.py --steps 5 --warmup 2 > $O/bench.json 2> $O/bench.err || exit 1
 fi
 if has lossless; then
-  run timeout -k 10 400 python3 bench.py --lossless --steps 3 --warmup 1 > $O/bench_lossless.json \
+  run timeout -k 10 400 python3 bench.py --lossless --steps 6 --warmup 1 > $O/bench_lossless.json \
     2> $O/bench_lossless.err || exit 1
+fi
+if has lab; then   # lossless encoder instances: 2 vs 3 (balanced step counts)
+  for i in 1 2; do
+    run timeout -k 10 300 $BENCH --lossless --engines 2 --steps 4 --warmup 1 > $O/lab_e2_$i.json \
+      2> $O/lab_e2_$i.err || exit 1
+    run timeout -k 10 300 $BENCH --lossless --engines 3 --steps 6 --warmup 1 > $O/lab_e3_$i.json \
+      2> $O/lab_e3_$i.err || exit 1
+  done
+fi
+if has cfg4; then   # config 4 (one 4096^2 q90 m6 frame, K3X) and one 1080p frame
+  run timeout -k 10 300 python3 bench.py --batch 1 --width 4096 --height 4096 --quality 90 --method 6 \
+    --steps 2 --warmup 1 --no-host-input --cpu-seconds 10 --engines 1 > $O/bench_cfg4.json \
+    2> $O/bench_cfg4.err || exit 1
+  run timeout -k 10 300 python3 bench.py --batch 1 --steps 10 --warmup 2 --no-host-input --no-cpu \
+    --engines 1 > $O/bench_1080p_single.json 2> $O/bench_1080p_single.err || exit 1
 fi
 if has lprof; then
   (cd /tmp && TMPDIR=/tmp run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \

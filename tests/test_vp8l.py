@@ -436,6 +436,17 @@ def test_gpu_alpha_methods_match_model(gpu):
 
 
 @pytest.mark.gpu
+def test_gpu_low_methods_match_model(gpu):
+    # methods 0-2: 64-pixel transform tiles (k_vp8l_transform with its
+    # block-wide colour search; method 0: the reference's predictor choice, no
+    # colour search), and 32-pixel ones at method 2 (k_vp8l_transform_w)
+    for img in (with_alpha(syn_v1(200, 130, 6), 6), syn_v1(150, 100, 2)):
+        for method in (0, 1, 2):
+            assert gpu_encode(gpu, img[None], method=method)[0] == M.encode(img, method=method), \
+                "method %d" % method
+
+
+@pytest.mark.gpu
 def test_gpu_batch_frames_match_model(gpu):
     frames = np.stack([syn_v1(160, 96, f) for f in range(5)])
     got = gpu_encode(gpu, frames)

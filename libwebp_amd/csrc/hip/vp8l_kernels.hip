@@ -2506,11 +2506,17 @@ __global__ __launch_bounds__(256) void k_vp8l_tilefeat(const uint32_t* __restric
   unsigned long long hl = 0;
   const size_t cap = VP8L_TILE_CAP(hb);
   uint32_t* out = tl + ((size_t)f * tiles + t) * cap;
-  for (int i = tid; i < VP8L_NS; i += 256) {
-    const uint32_t c = h[i];
-    n[alph_of(i)] += c;
+  for (int i0 = 0; i0 < VP8L_NS; i0 += 256) {
+    const int i = i0 + tid;
+    const uint32_t c = i < VP8L_NS ? h[i] : 0u;
+    if (i < VP8L_NS) n[alph_of(i)] += c;
     if (c > 1) hl += (unsigned long long)c * (unsigned long long)flog2_fx(frac, c);
-    if (c) out[atomicAdd(&nnz, 1u)] = (uint32_t)i | (c << 12);
+    // the non-zero bins' slots: one LDS atomic per wave, a ballot prefix inside
+    const uint64_t nzm = __ballot(c != 0);
+    uint32_t base = 0;
+    if (lane_id() == 0 && nzm) base = atomicAdd(&nnz, (uint32_t)__popcll(nzm));
+    base = __shfl(base, 0);
+    if (c) out[base + __popcll(nzm & ((1ull << lane_id()) - 1ull))] = (uint32_t)i | (c << 12);
   }
   for (int a = 0; a < 5; ++a) n[a] = wave_sum(n[a]);
   hl = wave_sum(hl);

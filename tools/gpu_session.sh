@@ -50,6 +50,16 @@ if has lphases; then   # L1a / L1 phase cycles (diagnostic build)
   WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_prof.so run timeout -k 10 150 \
     python3 tools/vp8l_phases.py 1920 1080 256 4 > $O/vp8l_phases.log 2>&1 || exit 1
 fi
+if has lprof1; then   # the lossless kernels one instance at a time (solo durations)
+  (cd /tmp && TMPDIR=/tmp run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+    -d $O/lstats1 -o run -- python3 $R/bench.py --lossless --no-cpu --no-host-input --steps 2 \
+    --warmup 1 --engines 1 > $O/lprof1.log 2>&1) || exit 1
+fi
+if has prof1; then   # the lossy kernels one instance at a time
+  (cd /tmp && TMPDIR=/tmp run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+    -d $O/stats1 -o run -- python3 $R/bench.py --no-cpu --no-host-input --steps 2 \
+    --warmup 1 --engines 1 > $O/prof1.log 2>&1) || exit 1
+fi
 if has stages; then
   for B in 256 1; do
     WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_prof.so run timeout -k 10 150 \

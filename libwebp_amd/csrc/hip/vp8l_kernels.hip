@@ -1512,16 +1512,26 @@ __global__ __launch_bounds__(256) void k_vp8l_entropy(const uint8_t* __restrict_
   __syncthreads();
   const int y0 = (int)((long long)H * blockIdx.x / ENTROPY_BANDS);
   const int y1 = (int)((long long)H * (blockIdx.x + 1) / ENTROPY_BANDS);
-  const long long n = (long long)(y1 - y0) * W;
-  for (long long i = tid; i < n; i += 256) {
-    const int y = y0 + (int)(i / W), x = (int)(i % W);
+  const int n = (y1 - y0) * W;   // <= 2^31: a band of rows
+  // a pixel, its raster predecessor, the pixels above and above-left, loaded
+  // one iteration ahead of their use
+  auto load = [&](int i, uint32_t (&o)[4]) {
+    const int yy = i / W, x = i - yy * W, y = y0 + yy;
     const uint8_t* row = img + (size_t)y * rstride;
-    const uint32_t pix = pix_at(row, x, plane);
-    const uint32_t prev = x > 0 ? pix_at(row, x - 1, plane)
-                        : y > 0 ? pix_at(row - rstride, W - 1, plane) : pix;
+    o[0] = pix_at(row, x, plane);
+    o[1] = x > 0 ? pix_at(row, x - 1, plane) : y > 0 ? pix_at(row - rstride, W - 1, plane) : o[0];
+    o[2] = y > 0 ? pix_at(row - rstride, x, plane) : 0u;
+    o[3] = (x > 0 && y > 0) ? pix_at(row - rstride, x - 1, plane) : 0u;
+  };
+  uint32_t nx[4] = {0, 0, 0, 0};
+  if (tid < n) load(tid, nx);
+  for (int i = tid; i < n; i += 256) {
+    const uint32_t pix = nx[0], prev = nx[1], up = nx[2], ul = nx[3];
+    if (i + 256 < n) load(i + 256, nx);
+    const int yy = i / W, x = i - yy * W, y = y0 + yy;
     const uint32_t d = sub_pixels(pix, prev);
     if (d == 0) continue;
-    if (y > 0 && pix_at(row - rstride, x, plane) == pix) continue;
+    if (y > 0 && up == pix) continue;
     const int g = (int)(pix >> 8), gd = (int)(d >> 8);
     // alpha is one value over most waves: the wave-uniform fast path
     hadd(h, 0 * 256 + (pix >> 24));
@@ -1541,9 +1551,9 @@ __global__ __launch_bounds__(256) void k_vp8l_entropy(const uint8_t* __restrict_
     // the transform search's accumulated histograms (model:
     // accumulated_histograms): residuals of predictor 12, or of the fixed
     // modes on row 0 (left) and column 0 (top), plain and sub-green
-    const uint32_t T_ = y > 0 ? pix_at(row - rstride, x, plane) : 0u;
-    const uint32_t L = x > 0 ? pix_at(row, x - 1, plane) : 0u;
-    const uint32_t TL = (x > 0 && y > 0) ? pix_at(row - rstride, x - 1, plane) : 0u;
+    const uint32_t T_ = up;
+    const uint32_t L = x > 0 ? prev : 0u;
+    const uint32_t TL = ul;
     const int fm = y == 0 ? 1 : (x == 0 ? 2 : 12);
     const uint32_t r = sub_pixels(pix, predict(fm, L, T_, TL, 0u));
     const uint32_t rs = sub_pixels(sub_green(pix), predict(fm, sub_green(L), sub_green(T_),
@@ -1857,16 +1867,33 @@ __global__ __launch_bounds__(64) void k_vp8l_match(const uint32_t* __restrict__ 
   uint32_t* O = bm + f * npix;
   const size_t row = (size_t)y * W;
   int carry[VP8L_NUM_CAND] = {0, 0, 0, 0};
-  for (int c = (W - 1) >> 6; c >= 0; --c) {
+  // chunk c's pixel, its 4 candidates and its cache size, loaded one chunk
+  // ahead of their use (the walk is serial over the row's chunks)
+  struct Ld { uint32_t e, cv[VP8L_NUM_CAND], mb; };
+  auto load = [&](int c, Ld& o) {
     const int x = (c << 6) + ln;
-    const bool valid = x < W;
-    const size_t q = row + (size_t)x;
-    const uint32_t e = valid ? E[q] : 0u;
-    int bn = 0, bk = 0;
+    const bool valid = c >= 0 && x < W;
+    const size_t q = row + (size_t)(valid ? x : 0);
+    o.e = valid ? E[q] : 0u;
 #pragma unroll
     for (int k = 0; k < VP8L_NUM_CAND; ++k) {
       const int d = p.dist[k];
-      const bool ok = valid && d > 0 && (size_t)d <= q && E[q - d] == e;
+      o.cv[k] = (valid && d > 0 && (size_t)d <= q) ? E[q - d] : ~o.e;   // ~e: never equal
+    }
+    o.mb = valid ? MB[q] : 0u;
+  };
+  Ld cur, nxt;
+  load((W - 1) >> 6, cur);
+  for (int c = (W - 1) >> 6; c >= 0; --c) {
+    load(c - 1, nxt);
+    const int x = (c << 6) + ln;
+    const bool valid = x < W;
+    const size_t q = row + (size_t)x;
+    const uint32_t e = cur.e;
+    int bn = 0, bk = 0;
+#pragma unroll
+    for (int k = 0; k < VP8L_NUM_CAND; ++k) {
+      const bool ok = valid && cur.cv[k] == e;
       const uint64_t mask = __ballot(ok);
       const uint64_t miss = ~(mask >> ln);   // zero when all 64 lanes from lane 0 match:
       int run = miss ? (int)__builtin_ctzll(miss) : 64;   // ctz(0) is undefined (gives 31)
@@ -1876,11 +1903,12 @@ __global__ __launch_bounds__(64) void k_vp8l_match(const uint32_t* __restrict__ 
       if (n > bn) { bn = n; bk = k; }
     }
     if (valid) {
-      uint32_t mb = MB[q];
+      uint32_t mb = cur.mb;
       if (mb & VP8L_CACHE_PARTIAL)
         mb = cache_settle(mb, e, q, (int)npix, S, cstart + (size_t)f * S * VP8L_CACHE_TAB);
       O[q] = (uint32_t)bn | ((uint32_t)bk << 13) | (mb << 15);
     }
+    cur = nxt;
   }
 }
 
@@ -1912,11 +1940,17 @@ __global__ __launch_bounds__(64) void k_vp8l_parse(vp8l_params p, uint32_t* __re
   for (int cx = 0; cx < W; cx += 64) {
     const int cw = min(64, W - cx);
     __syncthreads();
-    for (int r = 0; r < nrows; ++r) {
-      if (ln < cw) {
-        const int xp = cx + ln;
-        tile[r][ln] = xp < xs[r] ? 0xffffffffu : O[(size_t)r * W + xp];   // covered: marker
-      }
+    // 16 rows' loads in flight at a time (a load behind the covered test
+    // would wait for each row in turn)
+    for (int r0 = 0; r0 < nrows; r0 += 16) {
+      uint32_t v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        v[k] = (r0 + k < nrows && ln < cw) ? O[(size_t)(r0 + k) * W + cx + ln] : 0u;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (r0 + k < nrows && ln < cw)
+          tile[r0 + k][ln] = cx + ln < xs[r0 + k] ? 0xffffffffu : v[k];   // covered: marker
     }
     __syncthreads();
     if (ln < nrows) {
@@ -2349,8 +2383,14 @@ __global__ __launch_bounds__(1024) void k_vp8l_cachehist(const uint32_t* __restr
   for (int i = tid; i < VP8L_CHIST; i += 1024) h[i] = 0;
   __syncthreads();
   const size_t base = (size_t)f * npix;
+  // the three words of a pixel loaded one iteration ahead of their use
+  uint32_t op_n = 0, v_n = 0, m_n = 0;
+  if (tid < npix) { op_n = prov[base + tid]; v_n = argb[base + tid]; m_n = match[base + tid]; }
   for (int q = tid; q < npix; q += 1024) {
-    const uint32_t op = prov[base + q];
+    const uint32_t op = op_n, v = v_n, mw = m_n;
+    if (q + 1024 < npix) {
+      op_n = prov[base + q + 1024]; v_n = argb[base + q + 1024]; m_n = match[base + q + 1024];
+    }
     const uint32_t act = op & 3;
     if (act == 3) continue;
     if (act == 2) {
@@ -2359,8 +2399,7 @@ __global__ __launch_bounds__(1024) void k_vp8l_cachehist(const uint32_t* __restr
       atomicAdd(&h[VP8L_CH_LEN + sym], 1u);
       continue;
     }
-    const uint32_t v = argb[base + q];
-    const int c = (int)(match[base + q] >> 15);   // smallest cache size holding it
+    const int c = (int)(mw >> 15);   // smallest cache size holding it
     const uint32_t L = VP8L_CH_LIT + (uint32_t)(c - 1) * 1024;   // lanes differ in class:
     hadd(h, L + ((v >> 8) & 255));                               // full index for hadd
     hadd(h, L + 256 + ((v >> 16) & 255));
@@ -2492,13 +2531,27 @@ __global__ __launch_bounds__(256) void k_vp8l_tilefeat(const uint32_t* __restric
   if (tid < 6) acc[tid] = 0;
   if (tid == 0) nnz = 0;
   __syncthreads();
-  for (int i = tid; i < tw * th; i += 256) {
-    const int ly = i / tw, lx = i - ly * tw;
-    const size_t q = f * npix + (size_t)(y0 + ly) * W + x0 + lx;
-    PixSym s;
-    pix_symbols(ops[q], argb[q], cb, s);
-    for (int k = 0; k < 4; ++k)
-      if (s.s[k] >= 0) hadd(h, (uint32_t)s.s[k]);
+  for (int i0 = tid; i0 < tw * th; i0 += 4 * 256) {   // 4 pixels' loads in flight
+    uint32_t o4[4], a4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + 256 * u;
+      o4[u] = a4[u] = 0;
+      if (i < tw * th) {
+        const int ly = i / tw, lx = i - ly * tw;
+        const size_t q = f * npix + (size_t)(y0 + ly) * W + x0 + lx;
+        o4[u] = ops[q];
+        a4[u] = argb[q];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (i0 + 256 * u >= tw * th) break;
+      PixSym s;
+      pix_symbols(o4[u], a4[u], cb, s);
+      for (int k = 0; k < 4; ++k)
+        if (s.s[k] >= 0) hadd(h, (uint32_t)s.s[k]);
+    }
   }
   __syncthreads();
   // per alphabet: N, then own = sum_a N_a log N_a - sum h log h

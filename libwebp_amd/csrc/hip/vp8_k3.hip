@@ -670,15 +670,12 @@ __device__ __forceinline__ P4Lane p4_lane(const P4Op& op, int x, int y) {
   }
   return r;
 }
-// canvas byte offset of edge k of sub-block (bx, by): rows of 24 bytes,
-// row 0 = the row above the MB, column 0 = the column left of it
-__device__ __forceinline__ int edge_off(int k, int bx, int by) {
-  const int r = 4 * by, cc = 4 * bx;
-  const bool tr = k >= 9 && by > 0 && bx == 3;   // top-right from the MB above
-  const int row = k < 4 ? r + 4 - k : (tr ? 0 : r);
-  const int col = k < 4 ? cc : (tr ? k + 8 : cc + k - 4);
-  return row * 24 + col;
-}
+// canvas byte offset of edge k (L K J I X A B C D E F G H) from the base of
+// its sub-block (row 4 by, column 4 bx): rows of 24 bytes, row 0 = the row
+// above the MB, column 0 = the column left of it. Left edges are the column
+// before the sub-block, the others the row above it (incl. the top-right
+// samples, which run_i4 places beside rows 4 / 8 / 12 for bx = 3).
+__device__ __forceinline__ int edge_off0(int k) { return k < 4 ? (4 - k) * 24 : k - 4; }
 
 template <bool TRELLIS>
 __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_seg& S,
@@ -697,10 +694,18 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
     L.canvas[0][k] = v;
   }
   if (tid < 16) L.canvas[1 + tid][0] = yl[tid];
+  // the top-right samples of the right column's sub-blocks (bx = 3, by > 0)
+  // are the MB above-right's (row 0, columns 17..20): copied to rows 4, 8,
+  // 12 so that every edge sample sits at sub-block base + a fixed offset
+  if (tid >= 64 && tid < 76) {
+    const int k = tid - 64;
+    L.canvas[4 * (1 + (k >> 2))][17 + (k & 3)] = (x0 < mbw - 1) ? yt[16 + (k & 3)] : yt[15];
+  }
   const int m = tid >> 4, j = tid & 15, g = (tid & 63) & 48, x = j & 3, y = j >> 2;
   const bool act = tid < 160;
   const int wj = G.wy[j];
   const P4Lane pl = p4_lane(G.p4[act ? tid : 0], x, y);
+  const int offa = edge_off0(pl.ia), offb = edge_off0(pl.ib), offc = edge_off0(pl.ic);
   // this lane's y1 quantiser entries, once per MB
   const vp8g_mtx& M = S.y1;
   const uint32_t q_sh = M.sharpen[j], q_zt = M.zthresh[j], q_iq = M.iq[j], q_bias = M.bias[j];
@@ -728,14 +733,15 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
     int level = 0, dq = 0;
     if (busy) {
     {
-      const int ea = cv[edge_off(pl.ia, bx, by)];
-      const int eb = cv[edge_off(pl.ib, bx, by)];
-      const int ec = cv[edge_off(pl.ic, bx, by)];
+      const uint8_t* cb = cv + 96 * by + 4 * bx;   // sub-block base (worker-uniform)
+      const int ea = cb[offa];
+      const int eb = cb[offb];
+      const int ec = cb[offc];
       pr = clip8((pl.wa * ea + pl.wb * eb + pl.wc * ec + pl.rnd) >> pl.sh);
       if (pl.dc) {
         int s4 = 4;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) s4 += cv[edge_off(k, bx, by)] + cv[edge_off(5 + k, bx, by)];
+        for (int k = 0; k < 4; ++k) s4 += cb[edge_off0(k)] + cb[edge_off0(5 + k)];
         pr = s4 >> 3;
       }
     }

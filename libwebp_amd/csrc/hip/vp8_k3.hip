@@ -194,7 +194,6 @@ struct TLane {
   int fc[4], fcr, fy1;     // FTransform column pass: (sum fc*u + fcr) >> 16 (+ b3 != 0 on row 1)
   int ia[4], ib[4], ig[4]; // ITransform vertical: sum ia*u + ib*MUL(u, ig)
   int is2, ig1, is1, ig3, is3;   // ITransform horizontal
-  int hr[4], hc[4];        // TTransform row / column signs
 };
 
 // An optimisation barrier on a per-lane value: constants derived from it are
@@ -243,12 +242,6 @@ __device__ __forceinline__ TLane make_tlane(int j) {
   const int HG1[4] = {kC1, kC2, kC2, kC1}, HS1[4] = {1, 1, -1, -1};
   const int HG3[4] = {kC2, kC1, kC1, kC2}, HS3[4] = {1, -1, 1, -1};
   T.is2 = HS2[x]; T.ig1 = HG1[x]; T.is1 = HS1[x]; T.ig3 = HG3[x]; T.is3 = HS3[x];
-  // TTransform (:590-622): both passes are +-1 sums
-  const int TS[4][4] = {{1, 1, 1, 1}, {1, 1, -1, -1}, {1, -1, -1, 1}, {1, -1, 1, -1}};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) T.hr[k] = TS[x][k];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) T.hc[s] = TS[y][(y - s) & 3];
   return T;
 }
 
@@ -284,16 +277,29 @@ __device__ __forceinline__ int idct_lane(int c, int pr, const TLane& T) {
 }
 
 // One lane's term of TTransform (src/dsp/enc.c:590-622): weighted |Hadamard
-// coefficient j| of the 4x4 samples p.
-__device__ __forceinline__ int ttrans_lane(int p, const TLane& T, int wj) {
+// coefficient j| of the 4x4 samples p, as butterflies without per-lane
+// constants. Only |coefficient| is used, so each lane may compute its
+// coefficient up to a sign: a sign that depends on the lane's column x
+// alone flips all four row-pass values a column-pass lane combines, and the
+// column pass is free to flip its own result. With those freedoms the row
+// pass of column x is a0 + a1 | a3 + a2 | a3 - a2 | a0 - a1 (x = 0..3) over
+// a0 = i0 + i2, a1 = i1 + i3, a2 = i1 - i3, a3 = i0 - i2, and the column
+// pass over the rotated rows u_s (colrot) is (u0 + u1) + (u2 + u3) (y = 0),
+// (u0 + u1) - (u2 + u3) (y = 1, 2), (u0 - u1) + (u2 - u3) (y = 3).
+__device__ __forceinline__ int ttrans_lane(int p, int j, int wj) {
+  const int x = j & 3, y = j >> 2;
   int i0, i1, i2, i3;
   row4(p, i0, i1, i2, i3);
-  const int t = __mul24(T.hr[0], i0) + __mul24(T.hr[1], i1) + __mul24(T.hr[2], i2) +
-                __mul24(T.hr[3], i3);
+  const int a0 = i0 + i2, a1 = i1 + i3, a2 = i1 - i3, a3 = i0 - i2;
+  const bool xo = ((x + 1) & 2) == 0;   // x = 0 or 3
+  const int pu = xo ? a0 : a3, pv = xo ? a1 : a2;
+  const int t = x < 2 ? pu + pv : pu - pv;
   int u0, u1, u2, u3;
   colrot(t, u0, u1, u2, u3);
-  const int o = __mul24(T.hc[0], u0) + __mul24(T.hc[1], u1) + __mul24(T.hc[2], u2) +
-                __mul24(T.hc[3], u3);
+  const bool y3 = y == 3;
+  const int A = y3 ? u0 - u1 : u0 + u1;
+  const int B = y3 ? u2 - u3 : u2 + u3;
+  const int o = (y == 1 || y == 2) ? A - B : A + B;
   return __mul24(wj, iabs_(o));
 }
 
@@ -491,7 +497,7 @@ __device__ void eval_i16(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_se
     const int rec = idct_lane(dq[p], pr, T);
     L.rec16[m][py * 16 + px] = (uint8_t)rec;
     sse += (src - rec) * (src - rec);
-    const int td = sum16(ttrans_lane(rec, T, wj)) - L.hsrc[b];
+    const int td = sum16(ttrans_lane(rec, j, wj)) - L.hsrc[b];
     if (j == 0) tds += iabs_(td) >> 5;
   }
   sse = sum64(sse);
@@ -782,7 +788,7 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
       const int D = sum16((src - rec) * (src - rec));
       int SD = 0;
       if (S.tlambda) {
-        const int td = sum16(ttrans_lane(rec, make_tlane(opaque(j)), wj)) - L.hsrc[i4];
+        const int td = sum16(ttrans_lane(rec, j, wj)) - L.hsrc[i4];
         SD = (S.tlambda * (iabs_(td) >> 5) + 128) >> 8;
       }
       SUBST(4);
@@ -1637,7 +1643,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         // intra16 and intra4 distortions (VP8TDisto4x4 / 16x16)
         const int b = tid >> 4, j = tid & 15;
         const int src = L.yin[(4 * (b >> 2) + (j >> 2)) * BPS + 4 * (b & 3) + (j & 3)];
-        const int hs = sum16(ttrans_lane(src, make_tlane(opaque(j)), G.wy[j]));
+        const int hs = sum16(ttrans_lane(src, j, G.wy[j]));
         if (j == 0) L.hsrc[b] = hs;
       }
       wbar(L);

@@ -184,15 +184,12 @@ __device__ __forceinline__ void colrot(int v, int& u0, int& u1, int& u2, int& u3
   u3 = dpp<DPP_ROR(12)>(v);
 }
 
-// Per-lane constants that turn the 4x4 butterflies into straight-line
-// multiply-adds (no data-dependent selects or branches): lane j = 4y + x.
-// Column passes see their inputs rotated by the lane's row y (colrot), so
-// their constants are rotated the same way once, here.
+// Per-lane constants of the ITransform horizontal pass, the one transform
+// pass still written as a dot product (lane j = 4y + x): its inputs come
+// from row4 in natural order, and its constants load from one small table
+// with a scalar base. The other passes are butterflies below (no tables).
 struct TLane {
   int x, y;
-  int fr[4], frr;          // FTransform row pass: t = (sum fr*d + frr) >> 9
-  int fc[4], fcr, fy1;     // FTransform column pass: (sum fc*u + fcr) >> 16 (+ b3 != 0 on row 1)
-  int ia[4], ib[4], ig[4]; // ITransform vertical: sum ia*u + ib*MUL(u, ig)
   int is2, ig1, is1, ig3, is3;   // ITransform horizontal
 };
 
@@ -204,71 +201,74 @@ __device__ __forceinline__ int opaque(int v) {
   return v;
 }
 
+#define K_C1 (20091 + (1 << 16))
+#define K_C2 35468
+
 __device__ __forceinline__ TLane make_tlane(int j) {
   TLane T;
   const int x = j & 3, y = j >> 2;
   T.x = x; T.y = y;
-  const int kC1 = 20091 + (1 << 16), kC2 = 35468;
-  // FTransform_C (src/dsp/enc.c:157-191) row-pass outputs as dot products
-  // with (d0, d1, d2, d3), scaled to a common >> 9
-  const int FR[4][5] = {{4096, 4096, 4096, 4096, 0},
-                        {5352, 2217, -2217, -5352, 1812},
-                        {4096, -4096, -4096, 4096, 0},
-                        {2217, -5352, 5352, -2217, 937}};
-  // column-pass outputs as dot products with (t0, t1, t2, t3), common >> 16
-  const int FC[4][5] = {{4096, 4096, 4096, 4096, 7 * 4096},
-                        {5352, 2217, -2217, -5352, 12000},
-                        {4096, -4096, -4096, 4096, 7 * 4096},
-                        {2217, -5352, 5352, -2217, 51000}};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) T.fr[k] = FR[x][k];
-  T.frr = FR[x][4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) T.fc[s] = FC[y][(y - s) & 3];
-  T.fcr = FC[y][4];
-  T.fy1 = y == 1;
-  // ITransformOne vertical pass (src/dsp/enc.c:116-133): output index y of
-  // column x is +-in0 +-in2 +-MUL(in1, c) +-MUL(in3, c')
-  const int VA[4][4] = {{1, 0, 1, 0}, {1, 0, -1, 0}, {1, 0, -1, 0}, {1, 0, 1, 0}};
-  const int VB[4][4] = {{0, 1, 0, 1}, {0, 1, 0, -1}, {0, -1, 0, 1}, {0, -1, 0, -1}};
-  const int VG[4][4] = {{0, kC1, 0, kC2}, {0, kC2, 0, kC1}, {0, kC2, 0, kC1}, {0, kC1, 0, kC2}};
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int k = (y - s) & 3;
-    T.ia[s] = VA[y][k]; T.ib[s] = VB[y][k]; T.ig[s] = VG[y][k];
-  }
-  // horizontal pass (:134-146): dc + 4 +-t2 +-MUL(t1, c) +-MUL(t3, c')
+  // ITransformOne horizontal pass (src/dsp/enc.c:134-146):
+  // dc + 4 +-t2 +-MUL(t1, c) +-MUL(t3, c')
   const int HS2[4] = {1, -1, -1, 1};
-  const int HG1[4] = {kC1, kC2, kC2, kC1}, HS1[4] = {1, 1, -1, -1};
-  const int HG3[4] = {kC2, kC1, kC1, kC2}, HS3[4] = {1, -1, 1, -1};
+  const int HG1[4] = {K_C1, K_C2, K_C2, K_C1}, HS1[4] = {1, 1, -1, -1};
+  const int HG3[4] = {K_C2, K_C1, K_C1, K_C2}, HS3[4] = {1, -1, 1, -1};
   T.is2 = HS2[x]; T.ig1 = HG1[x]; T.is1 = HS1[x]; T.ig3 = HG3[x]; T.is3 = HS3[x];
   return T;
 }
 
 // FTransform_C (src/dsp/enc.c:157-191): lane holds the residual of pixel
 // (x, y); returns output coefficient j (int16 like the reference's out[]).
-__device__ __forceinline__ int fdct_lane(int d, const TLane& T) {
+// Row pass over the lane's row in natural order (row4), column pass over the
+// column rotated by the lane's row (colrot: u_s = row (y - s) & 3), both as
+// the reference's butterflies with the lane picking its output:
+//   row    x = 0, 2: (a0 +- a1) * 8        x = 1, 3: (a2 2217 + a3 5352 + 1812) >> 9,
+//                                                    (a3 2217 - a2 5352 +  937) >> 9
+//   column y = 0, 2: (a0 +- a1 + 7) >> 4   y = 1, 3: the same pair with 12000 / 51000,
+//                                                    >> 16, + (a3 != 0) on row 1
+// where in the rotated column a0 + a1 = u0 + u1 + u2 + u3 (y = 0),
+// a0 - a1 = u2 + u3 - u0 - u1 (y = 2), (a2, a3) = (u0 - u3, u1 - u2) (y = 1)
+// and (u2 - u1, u3 - u0) (y = 3).
+__device__ __forceinline__ int fdct_lane(int d, int j) {
+  const int x = j & 3, y = j >> 2;
   int d0, d1, d2, d3;
   row4(d, d0, d1, d2, d3);
-  const int t = (__mul24(T.fr[0], d0) + __mul24(T.fr[1], d1) + __mul24(T.fr[2], d2) +
-                 __mul24(T.fr[3], d3) + T.frr) >> 9;
+  const int a0 = d0 + d3, a1 = d1 + d2, a2 = d1 - d2, a3 = d0 - d3;
+  const bool x1 = x == 1;
+  const int P = x1 ? a2 : a3, Q = x1 ? a3 : -a2;
+  const int todd = (__mul24(P, 2217) + __mul24(Q, 5352) + (x1 ? 1812 : 937)) >> 9;
+  const int tev = (x == 0 ? a0 + a1 : a0 - a1) * 8;
+  const int t = (x & 1) ? todd : tev;
   int u0, u1, u2, u3;
   colrot(t, u0, u1, u2, u3);
-  const int o = ((__mul24(T.fc[0], u0) + __mul24(T.fc[1], u1) + __mul24(T.fc[2], u2) +
-                  __mul24(T.fc[3], u3) + T.fcr) >> 16) +
-                (T.fy1 & (u1 != u2));   // row 1: + (a3 != 0), a3 = t0 - t3 = u1 - u2
-  return (int16_t)o;
+  const int S = u0 + u1, T = u2 + u3;
+  const int oev = ((y == 0 ? S + T : T - S) + 7) >> 4;
+  const bool y1 = y == 1;
+  const int b2 = y1 ? u0 - u3 : u2 - u1, b3 = y1 ? u1 - u2 : u3 - u0;
+  const int P2 = y1 ? b2 : b3, Q2 = y1 ? b3 : -b2;
+  const int oodd = ((__mul24(P2, 2217) + __mul24(Q2, 5352) + (y1 ? 12000 : 51000)) >> 16) +
+                   (y1 && b3 != 0);
+  return (int16_t)((y & 1) ? oodd : oev);
 }
 
 // ITransformOne (src/dsp/enc.c:116-147): lane holds dequantised coefficient
 // j and the prediction sample of pixel (x, y); returns the reconstruction.
-__device__ __forceinline__ int idct_lane(int c, int pr, const TLane& T) {
+// Vertical pass (output y of column x) over the rotated column u_s:
+// with (p, q, r, s) = (u0, u2, MUL(u1, kC2), MUL(u3, kC1)) for even y and
+// (u1, u3, MUL(u0, kC2), MUL(u2, kC1)) for odd y, the reference's a + d,
+// b + c, b - c, a - d are (p + q) + (r + s), (p - q) + (r - s),
+// -((p - q) + (r - s)), (p + q) - (r + s) for y = 0..3.
+__device__ __forceinline__ int idct_lane(int c, int pr, int j, const TLane& T) {
+  const int y = j >> 2;
   int u0, u1, u2, u3;
   colrot(c, u0, u1, u2, u3);
-  const int t = __mul24(T.ia[0], u0) + __mul24(T.ib[0], IMUL24(u0, T.ig[0])) +
-                __mul24(T.ia[1], u1) + __mul24(T.ib[1], IMUL24(u1, T.ig[1])) +
-                __mul24(T.ia[2], u2) + __mul24(T.ib[2], IMUL24(u2, T.ig[2])) +
-                __mul24(T.ia[3], u3) + __mul24(T.ib[3], IMUL24(u3, T.ig[3]));   // tmp[4x + y]
+  const bool yo = y & 1;
+  const int p = yo ? u1 : u0, q = yo ? u3 : u2, mA = yo ? u0 : u1, mB = yo ? u2 : u3;
+  const int r = IMUL24(mA, K_C2), s = IMUL24(mB, K_C1);
+  const bool e = ((y + 1) & 2) == 0;   // y = 0 or 3
+  const int A = e ? p + q : p - q, B = e ? r + s : r - s;
+  int t = y == 3 ? A - B : A + B;   // tmp[4x + y]
+  t = y == 2 ? -t : t;
   int t0, t1, t2, t3;
   row4(t, t0, t1, t2, t3);
   const int v = t0 + 4 + __mul24(T.is2, t2) + __mul24(T.is1, IMUL24(t1, T.ig1)) +
@@ -387,7 +387,7 @@ __device__ void eval_i16(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_se
   for (int p = 0; p < 4; ++p) {
     const int b = 4 * p + bsub, px = 4 * (b & 3) + x, py = 4 * (b >> 2) + y;
     const int d = L.yin[py * BPS + px] - L.p16[m][py * 16 + px];
-    co[p] = fdct_lane(d, T);
+    co[p] = fdct_lane(d, j);
     if (j == 0) L.dcs[m][b] = (int16_t)co[p];
     if (TRELLIS) L.co16[m][b][j] = (int16_t)co[p];
   }
@@ -494,7 +494,7 @@ __device__ void eval_i16(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_se
     const int b = 4 * p + bsub, px = 4 * (b & 3) + x, py = 4 * (b >> 2) + y;
     const int pr = L.p16[m][py * 16 + px];
     const int src = L.yin[py * BPS + px];
-    const int rec = idct_lane(dq[p], pr, T);
+    const int rec = idct_lane(dq[p], pr, j, T);
     L.rec16[m][py * 16 + px] = (uint8_t)rec;
     sse += (src - rec) * (src - rec);
     const int td = sum16(ttrans_lane(rec, j, wj)) - L.hsrc[b];
@@ -533,7 +533,7 @@ __device__ void eval_uv(const K3G& G, K3S& L, const vp8g_seg& S, const MBCtx& ct
     const int b = 4 * p + bsub, ch = b >> 2, k4 = b & 3;
     const int px = 8 * ch + 4 * (k4 & 1) + x, py = 4 * (k4 >> 1) + y;
     const int d = L.yin[py * BPS + 16 + px] - L.puv[m][py * 16 + px];
-    co[p] = fdct_lane(d, T);
+    co[p] = fdct_lane(d, j);
     if (j == 0) L.uvdc[m][b] = (int16_t)co[p];
   }
   WB();
@@ -599,7 +599,7 @@ __device__ void eval_uv(const K3G& G, K3S& L, const vp8g_seg& S, const MBCtx& ct
     const int px = 8 * ch + 4 * bx + x, py = 4 * by + y;
     const int pr = L.puv[m][py * 16 + px];
     const int src = L.yin[py * BPS + 16 + px];
-    const int rec = idct_lane(dq[p], pr, T);
+    const int rec = idct_lane(dq[p], pr, j, T);
     L.recuv[m][py * 16 + px] = (uint8_t)rec;
     sse += (src - rec) * (src - rec);
   }
@@ -752,7 +752,7 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
       }
     }
     SUBST(0);
-    const int c = fdct_lane(src - pr, make_tlane(opaque(j)));
+    const int c = fdct_lane(src - pr, j);
     SUBST(1);
     if constexpr (TRELLIS) {
       if (act) L.co4[m][j] = (int16_t)c;
@@ -779,7 +779,7 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
       dq = (int16_t)__mul24(level, q_q);
     }
     SUBST(2);
-    rec = idct_lane(dq, pr, make_tlane(opaque(j)));
+    rec = idct_lane(dq, pr, j, make_tlane(opaque(j)));
     const uint64_t bnz = __ballot(act && level != 0);
     const uint64_t bac = __ballot(act && level != 0 && j != 0);
     nzb = ((bnz >> g) & 0xffff) != 0;

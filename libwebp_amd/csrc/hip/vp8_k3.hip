@@ -184,15 +184,6 @@ __device__ __forceinline__ void colrot(int v, int& u0, int& u1, int& u2, int& u3
   u3 = dpp<DPP_ROR(12)>(v);
 }
 
-// Per-lane constants of the ITransform horizontal pass, the one transform
-// pass still written as a dot product (lane j = 4y + x): its inputs come
-// from row4 in natural order, and its constants load from one small table
-// with a scalar base. The other passes are butterflies below (no tables).
-struct TLane {
-  int x, y;
-  int is2, ig1, is1, ig3, is3;   // ITransform horizontal
-};
-
 // An optimisation barrier on a per-lane value: constants derived from it are
 // rebuilt where they are used instead of being hoisted out of the MB loop and
 // held in registers (and spilled) across the whole kernel.
@@ -203,19 +194,6 @@ __device__ __forceinline__ int opaque(int v) {
 
 #define K_C1 (20091 + (1 << 16))
 #define K_C2 35468
-
-__device__ __forceinline__ TLane make_tlane(int j) {
-  TLane T;
-  const int x = j & 3, y = j >> 2;
-  T.x = x; T.y = y;
-  // ITransformOne horizontal pass (src/dsp/enc.c:134-146):
-  // dc + 4 +-t2 +-MUL(t1, c) +-MUL(t3, c')
-  const int HS2[4] = {1, -1, -1, 1};
-  const int HG1[4] = {K_C1, K_C2, K_C2, K_C1}, HS1[4] = {1, 1, -1, -1};
-  const int HG3[4] = {K_C2, K_C1, K_C1, K_C2}, HS3[4] = {1, -1, 1, -1};
-  T.is2 = HS2[x]; T.ig1 = HG1[x]; T.is1 = HS1[x]; T.ig3 = HG3[x]; T.is3 = HS3[x];
-  return T;
-}
 
 // FTransform_C (src/dsp/enc.c:157-191): lane holds the residual of pixel
 // (x, y); returns output coefficient j (int16 like the reference's out[]).
@@ -258,7 +236,7 @@ __device__ __forceinline__ int fdct_lane(int d, int j) {
 // (u1, u3, MUL(u0, kC2), MUL(u2, kC1)) for odd y, the reference's a + d,
 // b + c, b - c, a - d are (p + q) + (r + s), (p - q) + (r - s),
 // -((p - q) + (r - s)), (p + q) - (r + s) for y = 0..3.
-__device__ __forceinline__ int idct_lane(int c, int pr, int j, const TLane& T) {
+__device__ __forceinline__ int idct_lane(int c, int pr, int j) {
   const int y = j >> 2;
   int u0, u1, u2, u3;
   colrot(c, u0, u1, u2, u3);
@@ -271,8 +249,15 @@ __device__ __forceinline__ int idct_lane(int c, int pr, int j, const TLane& T) {
   t = y == 2 ? -t : t;
   int t0, t1, t2, t3;
   row4(t, t0, t1, t2, t3);
-  const int v = t0 + 4 + __mul24(T.is2, t2) + __mul24(T.is1, IMUL24(t1, T.ig1)) +
-                __mul24(T.is3, IMUL24(t3, T.ig3));
+  // horizontal pass (:134-146): a = dc + t2, b = dc - t2 (dc = t0 + 4),
+  // d = MUL(t1, kC1) + MUL(t3, kC2), c = MUL(t1, kC2) - MUL(t3, kC1);
+  // x = 0..3 takes a + d, b + c, b - c, a - d
+  const int x = j & 3;
+  const bool xo = ((x + 1) & 2) == 0;   // x = 0 or 3
+  const int P = t0 + 4 + (xo ? t2 : -t2);
+  const int m1 = IMUL24(t1, xo ? K_C1 : K_C2), m3 = IMUL24(t3, xo ? K_C2 : K_C1);
+  const int Q = xo ? m1 + m3 : m1 - m3;
+  const int v = x < 2 ? P + Q : P - Q;
   return clip8(pr + (v >> 3));
 }
 
@@ -381,7 +366,6 @@ __device__ void eval_i16(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_se
                          const MBCtx& ctx, int tid) {
   const int m = tid >> 6, lane = tid & 63, g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
   const int bsub = lane >> 4;
-  const TLane T = make_tlane(opaque(j));
   int co[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
@@ -494,7 +478,7 @@ __device__ void eval_i16(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_se
     const int b = 4 * p + bsub, px = 4 * (b & 3) + x, py = 4 * (b >> 2) + y;
     const int pr = L.p16[m][py * 16 + px];
     const int src = L.yin[py * BPS + px];
-    const int rec = idct_lane(dq[p], pr, j, T);
+    const int rec = idct_lane(dq[p], pr, j);
     L.rec16[m][py * 16 + px] = (uint8_t)rec;
     sse += (src - rec) * (src - rec);
     const int td = sum16(ttrans_lane(rec, j, wj)) - L.hsrc[b];
@@ -526,7 +510,6 @@ __device__ void eval_uv(const K3G& G, K3S& L, const vp8g_seg& S, const MBCtx& ct
                         const int8_t* topderr, int use_derr) {
   const int m = tid >> 6, lane = tid & 63, g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
   const int bsub = lane >> 4;
-  const TLane T = make_tlane(opaque(j));
   int co[2];
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
@@ -599,7 +582,7 @@ __device__ void eval_uv(const K3G& G, K3S& L, const vp8g_seg& S, const MBCtx& ct
     const int px = 8 * ch + 4 * bx + x, py = 4 * by + y;
     const int pr = L.puv[m][py * 16 + px];
     const int src = L.yin[py * BPS + 16 + px];
-    const int rec = idct_lane(dq[p], pr, j, T);
+    const int rec = idct_lane(dq[p], pr, j);
     L.recuv[m][py * 16 + px] = (uint8_t)rec;
     sse += (src - rec) * (src - rec);
   }
@@ -779,7 +762,7 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
       dq = (int16_t)__mul24(level, q_q);
     }
     SUBST(2);
-    rec = idct_lane(dq, pr, j, make_tlane(opaque(j)));
+    rec = idct_lane(dq, pr, j);
     const uint64_t bnz = __ballot(act && level != 0);
     const uint64_t bac = __ballot(act && level != 0 && j != 0);
     nzb = ((bnz >> g) & 0xffff) != 0;

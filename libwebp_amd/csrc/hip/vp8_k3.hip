@@ -451,13 +451,13 @@ __device__ void eval_i16(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_se
     if (j == 0) rate += r;
   }
   WB();   // whtq complete
-  // inverse WHT: the DC of each block (dec.c:137-162)
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    if (j == 0) {
-      const int b = 4 * p + bsub;
+  // inverse WHT (dec.c:137-162): lane b < 16 of the mode's wave computes the
+  // DC of block b once; each block's coefficient-0 lane takes it by a shuffle
+  {
+    int dcv = 0;
+    if (lane < 16) {
       const int16_t* q = L.whtq[m];
-      const int r = b >> 2, col = b & 3;
+      const int b = lane, r = b >> 2, col = b & 3;
       int t[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -467,7 +467,12 @@ __device__ void eval_i16(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_se
       }
       const int dd = t[0] + 3;
       const int a0 = dd + t[3], a1 = t[1] + t[2], a2 = t[1] - t[2], a3 = dd - t[3];
-      dq[p] = (int16_t)((col == 0 ? a0 + a1 : col == 1 ? a3 + a2 : col == 2 ? a0 - a1 : a3 - a2) >> 3);
+      dcv = (int16_t)((col == 0 ? a0 + a1 : col == 1 ? a3 + a2 : col == 2 ? a0 - a1 : a3 - a2) >> 3);
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int v = __shfl(dcv, 4 * p + bsub);
+      if (j == 0) dq[p] = v;
     }
   }
   // reconstruction, SSE, texture distortion

@@ -127,13 +127,16 @@ struct K3S {
 // waiting waves by setting bit 31 of the counter (WBAR_RELEASE), so they
 // fall through, the worker leaves its row loop and the frame reports an error.
 #define WBAR_RELEASE 0x80000000u
+#ifndef K3_WBAR_SLEEP
+#define K3_WBAR_SLEEP 0   // s_sleep units between polls (0 / 1 / 2: 124.0 / 124.3 / 124.9 ms, profiles/r3/ab13_*)
+#endif
 __device__ __forceinline__ void wbar(K3S& L) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   uint32_t target = 0;
   if ((threadIdx.x & 63) == 0) target = (atomicAdd(&L.bar, 1u) & ~3u) + 4u;
   target = __builtin_amdgcn_readfirstlane(target);
   while (__hip_atomic_load(&L.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(K3_WBAR_SLEEP);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 #define WB() wbar(L)

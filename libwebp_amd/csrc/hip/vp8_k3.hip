@@ -1603,6 +1603,24 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       } else if (y > 0 && !wait_ge(G, L, &rowdone[y - 1], min(x + 2, mbw), 3)) {
         break;
       }
+#ifdef K3_WAVE_PRIO   // A/B
+      if constexpr (!X) {
+        // issue priority by place in the row wavefront: a worker whose row
+        // above is finished leads and gates the others (they wait on its
+        // progress), so its waves win the SIMDs' issue arbitration
+        int lead = 0;
+        if (y == 0 || __hip_atomic_load(&rowdone[y - 1], __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_WORKGROUP) >= mbw)
+          lead = 2;
+        else if (y == 1 || __hip_atomic_load(&rowdone[y - 2], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP) >= mbw)
+          lead = 1;
+        lead = __builtin_amdgcn_readfirstlane(lead);
+        if (lead == 2) __builtin_amdgcn_s_setprio(2);
+        else if (lead == 1) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
+#endif
       K3_STAMP(0);
 
       load_mb(Yp, Up, Vp, w, h, x, y, L.yin, tid, K3T);

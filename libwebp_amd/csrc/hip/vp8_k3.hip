@@ -1603,7 +1603,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       } else if (y > 0 && !wait_ge(G, L, &rowdone[y - 1], min(x + 2, mbw), 3)) {
         break;
       }
-#ifdef K3_WAVE_PRIO   // A/B
+#ifndef K3_NO_PRIO   // K3 124.5 -> 118.1 ms (profiles/r3/ab16_*)
       if constexpr (!X) {
         // issue priority by place in the row wavefront: a worker whose row
         // above is finished leads and gates the others (they wait on its
@@ -1616,7 +1616,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
                                              __HIP_MEMORY_SCOPE_WORKGROUP) >= mbw)
           lead = 1;
         lead = __builtin_amdgcn_readfirstlane(lead);
-        if (lead == 2) __builtin_amdgcn_s_setprio(2);
+#ifndef K3_PRIO_LEAD
+#define K3_PRIO_LEAD 2
+#endif
+        if (lead == 2) __builtin_amdgcn_s_setprio(K3_PRIO_LEAD);
         else if (lead == 1) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
       }

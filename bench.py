@@ -2,16 +2,14 @@
 """Benchmark: batched WebP lossy encode (cwebp -q 75 -m 4) of 1920x1080 RGBA
 frames on MI355X, BASELINE.json configs[1] (1 GPU) / configs[2] (8 GPUs).
 
-One "step" = one WebPGpuBatchEncodeRGBA call over the rank's batch of
-HBM-resident syn-v1 frames: K1 import, K2 analysis, host
-segment setup, K3 RD search + tokens, K4 boolean coder on the device (host
-codes partition 0 meanwhile), one D2H of the packed partitions and the RIFF
-write, ending with every .webp in host memory. Frames are synthesised on the
-device before timing starts, so `value` is the throughput with the input
-resident in HBM. SURVEY.md 8(d)'s own MP/s definition (RGBA in host memory,
-upload included) is reported beside it as `host_input_mps`: the same frames
-from pinned host memory, the upload of step i+1 overlapping the encode of
-step i (two device buffers, one copy stream each).
+One "step" = one batch of the rank's syn-v1 frames taken from
+RGBA in pinned host memory to .webp byte strings in host memory: the H2D
+upload, K1 import, K2 analysis, host segment setup, K3 RD search + tokens, K4
+boolean coder on the device (host codes partition 0 meanwhile), one D2H of
+the packed partitions and the RIFF write. `value` is that rate, SURVEY.md
+8(d)'s own MP/s definition (upload included): each encoder instance uploads
+its step i+1 on a copy stream while its step i encodes. The same frames
+already resident in HBM (no upload) are timed after it as `hbm_resident_mps`.
 
 Multi-GPU (configs[2]): one process per GPU. `--gpus N` without a torchrun
 environment starts `torch.distributed.run` with N ranks itself (a child
@@ -38,7 +36,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
-BOX_CORE_SHARE = 16     # host cores a one-GPU box gives a job (gpurun notes)
+BOX_CORE_SHARE = 16     # host cores the GPU pool grants a one-GPU job (its operator notes)
 
 
 def parse_args(argv=None):
@@ -67,8 +65,13 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="CPU work per baseline leg (single thread, all cores)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-host-input", action="store_true",
-                    help="skip the PCIe-inclusive host-input measurement")
+    ap.add_argument("--input", choices=("host", "hbm"), default="host",
+                    help="timed steps take RGBA from pinned host memory (upload included, "
+                         "SURVEY.md 8(d), the default) or already resident in HBM")
+    ap.add_argument("--no-host-input", dest="input", action="store_const", const="hbm",
+                    help="same as --input hbm")
+    ap.add_argument("--no-other-input", action="store_true",
+                    help="skip timing the other input mode after the line's steps")
     ap.add_argument("--stub", action="store_true",
                     help="CPU test double instead of the GPU encoder (gloo; tests only)")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default=None,
@@ -139,6 +142,45 @@ def _cpu_leg_worker(a):
     return _cpu_leg(*a)
 
 
+def cgroup_cpu_quota():
+    """CPUs granted by the cgroup CPU quota (v2 cpu.max, v1 cfs_quota), or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return q / per
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_share():
+    """(processes for the all-cores CPU leg, why that many): the cgroup CPU
+    quota when one is set, else the process's affinity set, in both cases at
+    most the pool's per-GPU core share (BOX_CORE_SHARE)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = cgroup_cpu_quota()
+    if quota is not None:
+        n = max(1, min(aff, int(quota + 0.5)))
+        why = "cgroup CPU quota %.1f CPUs, affinity set %d CPUs" % (quota, aff)
+    else:
+        n = aff
+        why = "no cgroup CPU quota, affinity set %d CPUs" % aff
+    if n > BOX_CORE_SHARE:
+        why += "; capped at the pool's per-GPU share of %d cores" % BOX_CORE_SHARE
+        n = BOX_CORE_SHARE
+    return n, why
+
+
 def cpu_baseline(width, height, quality, method, seconds, lossless=False):
     """WebPPictureImportRGBA + WebPEncode into a memory writer,
     single thread (the 40x denominator) and one process per host core
@@ -149,11 +191,7 @@ def cpu_baseline(width, height, quality, method, seconds, lossless=False):
     if kind is None:
         return None
     px = width * height
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, BOX_CORE_SHARE))
+    cores, share_note = cpu_share()
     with mp.get_context("fork").Pool(cores) as pool:
         legs = pool.map(_cpu_leg_worker, [(width, height, quality, method, lossless, seconds,
                                            1 + 2 * k) for k in range(cores)])
@@ -165,7 +203,7 @@ def cpu_baseline(width, height, quality, method, seconds, lossless=False):
             "sample": "%d syn-v1 %dx%d frames, q%d m%d%s, WebPPictureImportRGBA+WebPEncode, "
                       "single thread, %.1f s" % (frames, width, height, quality, method, mode, el),
             "all_cores": {"value": round(all_frames * px / all_wall / 1e6, 3), "unit": "MP/s",
-                          "cores": cores,
+                          "cores": cores, "cores_basis": share_note,
                           "sample": "%d processes x %.1f s, %d frames in all, independent "
                                     "frames per process" % (cores, all_wall, all_frames)}}
 
@@ -289,7 +327,7 @@ def lossless_line(args, world, B, W, H, elapsed, tails, total_bytes, solo=None):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8/u32",
-        "data": "synthetic syn-v1 RGBA frames generated in HBM (SURVEY.md 8(d))",
+        "data": "synthetic syn-v1 RGBA frames (SURVEY.md 8(d)), generated on the device",
         "config": {"workload": "batch of %d %dx%d RGBA frames per GPU, -lossless -q %g -m %d" %
                                (B, W, H, args.quality, args.method),
                    "frames_per_gpu": B, "width": W, "height": H, "quality": args.quality,
@@ -316,6 +354,27 @@ def lossless_line(args, world, B, W, H, elapsed, tails, total_bytes, solo=None):
     }
 
 
+def issue_roofline(B, W, H, quality, method, k3_seconds):
+    """K3's vector-issue fraction: SQ_INSTS_VALU per launch and the effective
+    clock from the committed SQ passes of this same workload
+    (profiles/k3_issue.json, tools/k3_issue.py) over 1024 SIMDs x 0.5 wave64
+    VALU instructions per cycle x this run's solo K3 time; None for another
+    workload."""
+    path = os.path.join(HERE, "profiles", "k3_issue.json")
+    if not os.path.exists(path) or (B, W, H, quality, method) != (256, 1920, 1080, 75.0, 4) \
+            or k3_seconds <= 0:
+        return None
+    d = json.load(open(path))
+    peak = 1024 * 0.5 * d["effective_clock_hz"]
+    return {"achieved": round(d["valu_per_launch"] / k3_seconds / 1e12, 4),
+            "peak": round(peak / 1e12, 4), "unit": "T wave64 VALU instructions/s",
+            "frac": round(d["valu_per_launch"] / (peak * k3_seconds), 4),
+            "frac_profiled": round(d["issue_frac_profiled"], 4),
+            "lane_utilisation": round(d["lane_utilisation"], 4),
+            "valu_per_launch": d["valu_per_launch"],
+            "effective_clock_hz": round(d["effective_clock_hz"]), "source": d["source"]}
+
+
 def measured_traffic(kernel, B, W, H, quality, method, lossless=False):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (profiles/hbm_traffic.json, profiles/hbm_traffic_lossless.json: FETCH_SIZE
@@ -329,50 +388,6 @@ def measured_traffic(kernel, B, W, H, quality, method, lossless=False):
     d = json.load(open(path))
     k = d["kernels"].get(kernel)
     return (int(k["bytes_per_launch"]) if k else None), d["source"]
-
-
-def host_input_rate(encs, rgba, B, W, H, steps, dev):
-    """SURVEY.md 8(d) MP/s: RGBA in (pinned) host memory -> .webp bytes in host
-    memory, upload included. Per encoder instance (one host thread each, steps
-    dealt round-robin): two device buffers, one copy stream each, the upload
-    of its step i+1 overlapping its encode of step i (and the other
-    instances' work)."""
-    import threading
-    import torch
-    pinned = torch.empty(rgba.numel(), dtype=torch.uint8, pin_memory=True)
-    pinned.copy_(rgba)
-    E = len(encs)
-    bufs = [[torch.empty_like(rgba), torch.empty_like(rgba)] for _ in range(E)]
-    cs = [[torch.cuda.Stream(dev), torch.cuda.Stream(dev)] for _ in range(E)]
-    errors = []
-
-    def worker(e):   # this instance's steps, double-buffered uploads
-        try:
-            mine = list(range(e, steps, E))
-            with torch.cuda.stream(cs[e][0]):
-                bufs[e][0].copy_(pinned, non_blocking=True)
-            for i in range(len(mine)):
-                if i + 1 < len(mine):
-                    with torch.cuda.stream(cs[e][(i + 1) & 1]):
-                        bufs[e][(i + 1) & 1].copy_(pinned, non_blocking=True)
-                encs[e].encode_device(bufs[e][i & 1].data_ptr(), B,
-                                      stream=cs[e][i & 1].cuda_stream)
-        except Exception as ex:   # re-raised below, after every thread ends
-            errors.append(ex)
-
-    th = [threading.Thread(target=worker, args=(e,)) for e in range(E)]
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    if errors:
-        raise errors[0]
-    torch.cuda.synchronize(dev)
-    el = time.perf_counter() - t0
-    del bufs, pinned
-    return steps * B * W * H / el / 1e6
 
 
 def main(argv=None):
@@ -452,8 +467,40 @@ def main(argv=None):
                                          lossless=int(args.lossless),
                                          low_memory=int(args.low_memory)))
 
-    def step(e=0):
-        encs[e].encode_device(rgba.data_ptr() if rgba is not None else 0, B, stream=stream)
+    # input of a step: "host" = RGBA in pinned host memory, uploaded by the
+    # step itself; "hbm" = the frames already in HBM. With
+    # host input every instance has two device buffers and two copy streams:
+    # the upload of its step i+1 runs while its step i encodes (encode_device
+    # returns once the batch's .webp bytes are in host memory, so the buffer
+    # of step i is free for step i+2 when the call returns)
+    host_in = args.input == "host" and not args.stub
+    pinned, bufs, cstreams = None, None, None
+    if host_in:
+        pinned = torch.empty(rgba.numel(), dtype=torch.uint8, pin_memory=True)
+        pinned.copy_(rgba)
+        bufs = [[torch.empty_like(rgba), torch.empty_like(rgba)] for _ in range(E)]
+        cstreams = [[torch.cuda.Stream(dev), torch.cuda.Stream(dev)] for _ in range(E)]
+
+    def upload(e, slot):
+        with torch.cuda.stream(cstreams[e][slot]):
+            bufs[e][slot].copy_(pinned, non_blocking=True)
+
+    def engine_steps(e, n, host, tails):
+        """Engine e's share of n steps (dealt round-robin over the engines)."""
+        mine = len(range(e, n, E))
+        if host and mine:
+            upload(e, 0)
+        for i in range(mine):
+            if host:
+                if i + 1 < mine:
+                    upload(e, (i + 1) & 1)
+                encs[e].encode_device(bufs[e][i & 1].data_ptr(), B,
+                                      stream=cstreams[e][i & 1].cuda_stream)
+            else:
+                encs[e].encode_device(rgba.data_ptr() if rgba is not None else 0, B,
+                                      stream=stream)
+            if tails is not None:
+                tails.append(encs[e].timings())
 
     def barrier():
         if world > 1:
@@ -461,38 +508,37 @@ def main(argv=None):
         if not args.stub:
             torch.cuda.synchronize(dev)
 
-    for e in range(E):
-        for _ in range(max(args.warmup, 1 if E > 1 else 0)):
-            step(e)
-    barrier()
+    def run(n, host, tails=None):
+        """n steps over the E engines (one host thread each when E > 1; the
+        ctypes calls release the GIL), bracketed by barrier + synchronize;
+        returns the wall time."""
+        barrier()
+        t0 = time.perf_counter()
+        if E == 1:
+            engine_steps(0, n, host, tails)
+        else:
+            import threading
+            errors = []
+
+            def worker(e):
+                try:
+                    engine_steps(e, n, host, tails)
+                except Exception as ex:   # re-raised below, after every thread ends
+                    errors.append(ex)
+
+            th = [threading.Thread(target=worker, args=(e,)) for e in range(E)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            if errors:
+                raise errors[0]
+        barrier()
+        return time.perf_counter() - t0
+
+    run(E * max(args.warmup, 1 if E > 1 else 0), host_in)
     tails = []
-    if E == 1:
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-            tails.append(enc.timings())
-    else:
-        import threading
-        errors = []
-
-        def worker(e):
-            try:
-                for _ in range(e, args.steps, E):
-                    step(e)
-                    tails.append(encs[e].timings())
-            except Exception as ex:   # re-raised below, after every thread ends
-                errors.append(ex)
-
-        th = [threading.Thread(target=worker, args=(e,)) for e in range(E)]
-        t0 = time.perf_counter()
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        if errors:
-            raise errors[0]
-    barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = run(args.steps, host_in, tails)
 
     errs = [enc.error(f) for f in range(B)]
     if any(errs):
@@ -512,18 +558,28 @@ def main(argv=None):
     total_bytes = int(sum(int(s.sum().item()) for s in allsizes))
 
     # the dominant kernel's time without the other instances' kernels beside
-    # it: one more (untimed) step on instance 0 alone -- with two instances
-    # the HIP events of the timed steps include waiting for CUs the other
-    # instance's kernels hold
+    # it: one more (untimed) HBM-input step on instance 0 alone -- with several
+    # instances the HIP events of the timed steps include waiting for CUs the
+    # other instances' kernels hold
     solo = None
     if not args.stub:
         barrier()
-        step(0)
+        engine_steps(0, 1, False, None)
         barrier()
         solo = enc.timings()
-    host_rate = None
-    if rank == 0 and world == 1 and not args.stub and not args.no_host_input:
-        host_rate = host_input_rate(encs, rgba, B, W, H, max(3 * E, min(args.steps, 4)), dev)
+    # the other input mode, reported beside the line (HBM-resident input when
+    # the timed steps uploaded from host memory, and vice versa)
+    other_rate = None
+    if not args.stub and not args.no_other_input:
+        n_other = max(3 * E, min(args.steps, 4))
+        if not host_in:
+            pinned = torch.empty(rgba.numel(), dtype=torch.uint8, pin_memory=True)
+            pinned.copy_(rgba)
+            bufs = [[torch.empty_like(rgba), torch.empty_like(rgba)] for _ in range(E)]
+            cstreams = [[torch.cuda.Stream(dev), torch.cuda.Stream(dev)] for _ in range(E)]
+        el = max_over_ranks(run(n_other, not host_in), world, cdev)
+        other_rate = world * n_other * B * W * H / el / 1e6
+    del bufs, pinned
 
     line = None
     if rank == 0:
@@ -537,12 +593,15 @@ def main(argv=None):
         elif kats:
             line["kat_check"] = "ok: %d timed-batch frames on %d rank(s) equal " \
                                 "tests/golden/shard_kat.json" % (checked, world)
-        if host_rate is not None:
-            line["host_input_mps"] = round(host_rate, 3)
-            line["host_input_note"] = ("RGBA in pinned host memory -> .webp in host memory, "
-                                       "H2D upload included; %d encoder instance(s), each "
-                                       "uploading step i+1 during its step i"
-                                       % len(encs))
+        line["config"]["input"] = "host" if host_in else "hbm"
+        line["input"] = ("host: RGBA in pinned host memory -> .webp in host memory, H2D "
+                         "upload inside every step (SURVEY.md 8(d)); each of the %d encoder "
+                         "instances uploads its step i+1 during its step i" % len(encs)
+                         if host_in else
+                         "hbm: RGBA frames already resident in HBM (no upload)")
+        if other_rate is not None:
+            key = "hbm_resident_mps" if host_in else "host_input_mps"
+            line[key] = round(other_rate, 3)
         if cb:
             line["cpu_baseline"] = cb
         if not args.stub:
@@ -574,8 +633,10 @@ def lossy_line(args, world, B, W, H, elapsed, tails, total_bytes, ntok, solo=Non
     k3_solo = solo[6] / 1e6 if solo else k3_s   # the roofline uses the uncontended time
     achieved = k3_bytes / k3_solo / 1e9 if k3_solo > 0 else 0.0
     traffic, tsrc = (None, None)
+    issue = None
     if not (args.sharp_yuv or args.low_memory or args.stub):
         traffic, tsrc = measured_traffic("k_encode", B, W, H, args.quality, args.method)
+        issue = issue_roofline(B, W, H, args.quality, args.method, k3_solo)
     return {
         "metric": "megapixels/sec encoded (cwebp -q 75, 1920x1080 batch)",
         "value": round(mp_ / elapsed, 3),
@@ -588,7 +649,7 @@ def lossy_line(args, world, B, W, H, elapsed, tails, total_bytes, ntok, solo=Non
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8/int32",
-        "data": "synthetic syn-v1 RGBA frames generated in HBM (SURVEY.md 8(d))",
+        "data": "synthetic syn-v1 RGBA frames (SURVEY.md 8(d)), generated on the device",
         "config": {"workload": "batch of %d %dx%d RGBA frames per GPU, -q %g -m %d%s" %
                                (B, W, H, args.quality, args.method,
                                 (" -sharp_yuv" if args.sharp_yuv else "") +
@@ -608,7 +669,9 @@ def lossy_line(args, world, B, W, H, elapsed, tails, total_bytes, ntok, solo=Non
                                          "k_encode_solo_ms: one step on one instance alone, "
                                          "the time `achieved` uses (≈ rocprof's average, "
                                          "profiles/r3/kernel_stats_*.csv)",
-                     "algorithmic_bytes_per_launch": k3_bytes},
+                     "algorithmic_bytes_per_launch": k3_bytes,
+                     # the roof that binds K3: vector issue
+                     "issue": issue},
         "stage_ms": {k: round(avg(i) / 1e3, 3) for k, i in
                      (("import_analysis", 0), ("host_setup", 1), ("rd_tokens", 2),
                       ("d2h", 3), ("host_tail", 4), ("total", 5),

@@ -113,6 +113,9 @@ struct K3S {
   // written), and the token count of each MB of its current row
   uint32_t rdelta[NSLOT];
   uint16_t rowcnt[1024];           // mbw <= 1024 (width <= 16383)
+#ifdef K3_TRACE
+  unsigned long long trace[16];    // diagnostic build: per-worker cycle / event counts (K3TR_*)
+#endif
 };
 
 // Barrier over the 4 wavefronts of one worker (s_barrier would stop the whole
@@ -966,6 +969,48 @@ __device__ __forceinline__ void refresh_hc(K3G& G, int tid) {
   } while (0)
 #endif
 
+// Wait / stage accounting per worker (-DK3_TRACE, diagnostic build only; the
+// product kernel has none of it): shader-clock cycles and event counts kept
+// by each worker's thread 0 in LDS and written to g_k3trace at frame end
+// (vp8g_k3_trace reads them back)
+enum {
+  K3TR_REFR_WAIT = 0,   // the refresher waiting for every earlier MB folded (site 1)
+  K3TR_EPOCH_WAIT,      // other workers waiting for the epoch (site 2)
+  K3TR_ROW_WAIT,        // the top-right wavefront wait (site 3)
+  K3TR_FOLD_WAIT,       // row end: waiting for the rows above folded (site 4)
+  K3TR_FOLD,            // fold_rows (row ends and epoch refreshes)
+  K3TR_REPLAY,          // of which the in-order replay of marked counters
+  K3TR_NREPLAY,         // marked counters replayed
+  K3TR_REFRESH,         // FinalizeTokenProbas + level costs + header costs
+  K3TR_MB,              // MB work (after the waits, to the MB's publish)
+  K3TR_I4,              // intra-4 search
+  K3TR_I16,             // intra-16 candidates
+  K3TR_NMB,             // MBs
+  K3TR_TOTAL,           // the worker's whole lifetime
+  K3TR_NROWWAIT,        // wavefront waits that found the row above behind
+  K3TR_TOK,             // per-MB info, SSE and tokens
+  K3TR_UV,              // chroma candidates (+ the m5 re-quantisation)
+  K3TR_N
+};
+#ifdef K3_TRACE
+#define K3TR_MAXB 1024
+__device__ unsigned long long g_k3trace[K3TR_MAXB][4][K3TR_N];
+#define TR_NOW() __builtin_amdgcn_s_memtime()
+#define TR_ADD(slot, v)                           \
+  do {                                            \
+    if (threadIdx.x % K3T == 0) L.trace[slot] += (v); \
+  } while (0)
+#define TR_SINCE(slot, t0) TR_ADD(slot, TR_NOW() - (t0))
+#else
+#define TR_NOW() 0ull
+#define TR_ADD(slot, v) \
+  do {                  \
+  } while (0)
+#define TR_SINCE(slot, t0) \
+  do {                     \
+  } while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // Frame-level machinery: several workers encode MBs of different rows at the
 // same time (a wavefront: row y may encode MB x once row y-1 has finished
@@ -1162,6 +1207,14 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
   }
   wbar(L);
   if (L.mark_any) {
+#ifdef K3_TRACE
+    const uint64_t tr_rp = TR_NOW();
+    if (tid == 0) {
+      int nm = 0;
+      for (int wd = 0; wd < 33; ++wd) nm += __popc(G.mark[wd]);
+      L.trace[K3TR_NREPLAY] += nm;
+    }
+#endif
     // exact in-order replay of each marked counter by one wave: its tokens only
     // matter up to the points where the counter halves, so the row's tokens
     // are scanned (four 64-token chunks per load step) with the counter's
@@ -1222,6 +1275,7 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
     wbar(L);
     for (int k = tid; k < 33; k += K3T) G.mark[k] = 0;
     wbar(L);
+    TR_SINCE(K3TR_REPLAY, tr_rp);
   }
   if (tid == 0) {
     G.ntok = base + total;
@@ -1483,6 +1537,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
   uint8_t* yl = L.yl_mem + 1;
   uint8_t* ul = L.ul_mem + 1;
   uint8_t* vl = L.vl_mem + 1;
+#ifdef K3_TRACE
+  if (tid < K3TR_N) L.trace[tid] = 0;
+  const uint64_t tr_start = TR_NOW();
+#endif
 
   for (int y = blk * NW + wk; y < mbh && !L.myabort; y += NW * nwg) {
     // InitLeft (iterator_enc.c:22-32)
@@ -1511,15 +1569,20 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         if (refresher) {
           // everything before this MB: rows above folded by their owners,
           // this row's earlier MBs folded here
+          const uint64_t tr_w = TR_NOW();
           if constexpr (X) {
             if (tid == 0) atomicMax(&XL.claim, ep);
             if (!wait_gx(G, L, &XH->fold_ptr, (int32_t)fold_from, XH)) break;
           } else {
             if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from, 1)) break;
           }
+          const uint64_t tr_f = TR_NOW();
+          TR_ADD(K3TR_REFR_WAIT, tr_f - tr_w);
           fold_rows<X>(G, L, tid, fold_from, mb, (uint32_t)y * mbw, tok_base, mboff, xs);
           fold_from = mb;
           wbar(L);
+          const uint64_t tr_r = TR_NOW();
+          TR_ADD(K3TR_FOLD, tr_r - tr_f);
           const int dirty = finalize_probas_wg(G, L, tid);
           if constexpr (X) {
             // level costs: recomputed when dirty, else those of the frame's
@@ -1554,6 +1617,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
             }
           }
           if (tid == 0) publish(&G.epoch, ep);
+          TR_SINCE(K3TR_REFRESH, tr_r);
         } else if (X) {
           // the frame's refresher published epoch ep; the first worker of this
           // workgroup to need it copies the probabilities (and, if they
@@ -1580,7 +1644,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
             if (!wait_ge(G, L, &G.epoch, ep, 2)) break;
           }
         } else {
+          const uint64_t tr_w = TR_NOW();
           if (!wait_ge(G, L, &G.epoch, ep, 2)) break;
+          TR_SINCE(K3TR_EPOCH_WAIT, tr_w);
         }
       }
       // ---- wavefront dependency: MB x+1 of the row above (top-right) is done
@@ -1600,8 +1666,15 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
             else if (k == 10) reinterpret_cast<uint32_t*>(xtopderr + 4 * c)[0] = v;
           }
         }
-      } else if (y > 0 && !wait_ge(G, L, &rowdone[y - 1], min(x + 2, mbw), 3)) {
-        break;
+      } else if (y > 0) {
+#ifdef K3_TRACE
+        const uint64_t tr_w = TR_NOW();
+        if (__hip_atomic_load(&rowdone[y - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
+            min(x + 2, mbw))
+          TR_ADD(K3TR_NROWWAIT, 1);
+#endif
+        if (!wait_ge(G, L, &rowdone[y - 1], min(x + 2, mbw), 3)) break;
+        TR_SINCE(K3TR_ROW_WAIT, tr_w);
       }
 #ifndef K3_NO_PRIO   // K3 124.5 -> 118.1 ms (profiles/r3/ab16_*)
       if constexpr (!X) {
@@ -1625,6 +1698,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       }
 #endif
       K3_STAMP(0);
+      const uint64_t tr_mb = TR_NOW();
+      TR_ADD(K3TR_NMB, 1);
 
       load_mb(Yp, Up, Vp, w, h, x, y, L.yin, tid, K3T);
       wbar(L);
@@ -1662,12 +1737,14 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       K3_STAMP(1);
 
       // ---- Intra16 (quant_enc.c:1002-1058)
+      const uint64_t tr_i16 = TR_NOW();
       if constexpr (TR) {
         if (trellis_all) eval_i16<true>(G, L, tn, S, ctx, tid);
         else eval_i16<false>(G, L, tn, S, ctx, tid);
       } else {
         eval_i16<false>(G, L, tn, S, ctx, tid);
       }
+      TR_SINCE(K3TR_I16, tr_i16);
       int best16 = 0;
       uint32_t nz16 = 0;
       score_t D16 = 0, SD16 = 0, H16 = 0, R16 = 0;
@@ -1715,6 +1792,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       K3_STAMP(2);
 
       // ---- Intra4 (quant_enc.c:1072-1165)
+      const uint64_t tr_i4 = TR_NOW();
       if (max_i4_bits > 0) {
         I4Result r4;
         if constexpr (TR) {
@@ -1740,6 +1818,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         wbar(L);
       }
       K3_STAMP(3);
+      const uint64_t tr_uv = TR_NOW();
+      TR_ADD(K3TR_I4, tr_uv - tr_i4);
 
       // ---- UV (quant_enc.c:1169-1217)
       int bu = 0;
@@ -1803,6 +1883,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       }
       (void)rd_score;
       K3_STAMP(4);
+      const uint64_t tr_tok = TR_NOW();
+      TR_ADD(K3TR_UV, tr_tok - tr_uv);
 
       // ---- per-MB info + side statistics
       const int skip = rd_nz == 0;
@@ -1934,6 +2016,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         if (rtid == 0) L.rowcnt[x] = (uint16_t)(tot0 + tot1);
       }
       K3_STAMP(5);
+      TR_SINCE(K3TR_TOK, tr_tok);
       // update nz context (iterator_enc.c:267-283) and the left DC flag
       if (rtid == 0) {
         int tn9[9], ln[9];
@@ -1999,22 +2082,31 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         }
       }
       K3_STAMP(6);
+      TR_SINCE(K3TR_MB, tr_mb);
     }
     if (L.myabort) break;
     // row end: fold this row's remaining MBs once the rows above are folded
+    const uint64_t tr_fw = TR_NOW();
     if constexpr (X) {
       if (!wait_gx(G, L, &XH->fold_ptr, (int32_t)fold_from, XH)) break;
     } else {
       if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from, 4)) break;
     }
+    const uint64_t tr_ff = TR_NOW();
+    TR_ADD(K3TR_FOLD_WAIT, tr_ff - tr_fw);
     fold_rows<X>(G, L, tid, fold_from, (uint32_t)(y + 1) * mbw, (uint32_t)y * mbw, tok_base,
                  mboff, xs);
+    TR_SINCE(K3TR_FOLD, tr_ff);
     report_rows<X>(G, L, P, tid, (uint32_t)(y + 1) * mbw, mbw, XH);
     wbar(L);
     K3_STAMP(7);
   }
 
   // ---- frame epilogue: final probabilities and side results
+#ifdef K3_TRACE
+  TR_SINCE(K3TR_TOTAL, tr_start);
+  if (tid < K3TR_N && blockIdx.x < K3TR_MAXB) g_k3trace[blockIdx.x][wk & 3][tid] = L.trace[tid];
+#endif
   __syncthreads();
   if constexpr (X) {   // this workgroup's share of the side statistics; k_encode_xtail finishes
     if (gt == 0) {
@@ -2132,10 +2224,12 @@ static size_t k3_lds_bytes(int mbw, int mbh, bool trellis, size_t pad = 0) {
          4 * mbw + 4 * mbh + (trellis ? (size_t)NW * 64 * 32 * 4 : 0) + 16;
 }
 
+#ifdef WEBP_AMD_DIAG
 extern "C" int vp8g_launch_encode_w1(const uint8_t* yuv, size_t yfb, int w, int h, int n,
                                      const uint8_t* segmap, const vp8g_frame_params* params,
                                      uint16_t* tokens, size_t tok_cap, uint8_t* mbinfo,
                                      vp8g_frame_result* results, void* stream);
+#endif
 extern "C" int vp8g_launch_check(const char* what);
 
 template <int NW, bool TR, bool AF = false, int WPE = 1, int PAD = 0>
@@ -2174,11 +2268,13 @@ static int launch_k3_t(const K3Args& a, int n, bool trellis, void* stream) {
   return vp8g_launch_check("k_encode");
 }
 
+#ifdef WEBP_AMD_DIAG
 template <int NW>
 static int launch_k3(const K3Args& a, int n, bool trellis, void* stream) {
   return trellis ? launch_k3_t<NW, true>(a, n, true, stream)
                  : launch_k3_t<NW, false>(a, n, false, stream);
 }
+#endif
 
 static std::atomic<int> g_x_free{-1};   // K3X workgroup budget (k3x_take)
 
@@ -2281,30 +2377,50 @@ static int launch_k3_default(const K3Args& a, int n, bool trellis, bool af, void
                  : launch_k3_t<3, false>(a, n, false, stream);
 }
 
+#ifdef K3_TRACE
+// diagnostic build: the per-worker K3TR_* counters of the last launch,
+// out[block][worker][slot] for the first nblocks workgroups
+extern "C" __attribute__((visibility("default"))) int vp8g_k3_trace(unsigned long long* out,
+                                                                    int nblocks) {
+  if (nblocks > K3TR_MAXB) nblocks = K3TR_MAXB;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k3trace),
+                             (size_t)nblocks * 4 * K3TR_N * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess
+             ? nblocks
+             : 0;
+}
+#endif
+
 extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, int n,
                                   const uint8_t* segmap, const vp8g_frame_params* params,
                                   uint16_t* tokens, size_t tok_cap, uint8_t* mbinfo,
                                   uint32_t* mboff, int trellis, vp8g_frame_result* results,
                                   uint8_t* rerun_state, uint8_t* recon, uint8_t* xsync,
                                   void* stream) {
-  // WEBP_AMD_K3: 1 = single-wavefront reference kernel, 2/3/5 = 1/2/3 MB
-  // workers per frame (4 = the refused 4-worker build), 6 = 3 workers held to
-  // 128 VGPRs (spills to scratch; diagnostic), 7 / 8 = 3 / 2 workers with
-  // their state moved 40 KB / 64 KB up the LDS (diagnostic: the 4-worker
-  // stall vs worker state at high LDS addresses), unset = default above
+#ifdef WEBP_AMD_DIAG
+  // diagnostic build only (make diag -> libwebp_amd_diag.so; the product
+  // library has no switch): WEBP_AMD_K3 = 1 single-wavefront twin,
+  // 2/3/5 = 1/2/3 MB workers per frame, 4 = the 4-worker build, 6 = 3 workers
+  // held to 128 VGPRs, 7 / 8 = 3 / 2 workers with their state moved 40 KB /
+  // 64 KB up the LDS
   static const int variant = [] {
     const char* v = getenv("WEBP_AMD_K3");
     return (v && v[0] >= '1' && v[0] <= '8') ? v[0] - '0' : 0;
   }();
+#else
+  constexpr int variant = 0;
+#endif
   // recon != NULL selects the autofilter instantiation; each frame's buffer
   // address travels in vp8g_frame_params::recon_addr
   if (recon != nullptr && variant != 0) {
     vp8g_set_error("k_encode", "the autofilter runs on the default K3 variant only");
     return 0;
   }
+#ifdef WEBP_AMD_DIAG
   if (variant == 1)
     return vp8g_launch_encode_w1(yuv, yfb, w, h, n, segmap, params, tokens, tok_cap, mbinfo,
                                  results, stream);
+#endif
   K3Args a;
   a.yuv = yuv; a.yfb = yfb; a.w = w; a.h = h;
   a.mbw = (w + 15) >> 4; a.mbh = (h + 15) >> 4;
@@ -2317,15 +2433,14 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
       return trellis ? launch_k3x_budget<2, true>(a, n, nwg, stream)
                      : launch_k3x_budget<2, false>(a, n, nwg, stream);
   }
+#ifdef WEBP_AMD_DIAG
   if (variant == 2) return launch_k3<1>(a, n, trellis != 0, stream);
   if (variant == 3) return launch_k3<2>(a, n, trellis != 0, stream);
-  if (variant == 4) {   // stalls in its wavefront wait: refused
-    vp8g_set_error("k_encode", "the 4-worker K3 variant is disabled (known stall)");
-    return 0;
-  }
+  if (variant == 4) return launch_k3<4>(a, n, trellis != 0, stream);
   if (variant == 5) return launch_k3<3>(a, n, trellis != 0, stream);
   if (variant == 6 && !trellis) return launch_k3_t<3, false, false, 4>(a, n, false, stream);
   if (variant == 7 && !trellis) return launch_k3_t<3, false, false, 1, 40960>(a, n, false, stream);
   if (variant == 8 && !trellis) return launch_k3_t<2, false, false, 1, 65536>(a, n, false, stream);
+#endif
   return launch_k3_default(a, n, trellis != 0, recon != nullptr, stream);
 }

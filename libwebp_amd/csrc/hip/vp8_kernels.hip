@@ -2010,6 +2010,7 @@ int vp8g_launch_analysis(const uint8_t* yuv, size_t yfb, int w, int h, int n, ui
   return launch_check("k_analyze");
 }
 
+#ifdef WEBP_AMD_DIAG   // the single-wavefront twin of K3 (WEBP_AMD_K3=1, libwebp_amd_diag.so)
 int vp8g_launch_encode_w1(const uint8_t* yuv, size_t yfb, int w, int h, int n,
                        const uint8_t* segmap, const vp8g_frame_params* params, uint16_t* tokens,
                        size_t tok_cap, uint8_t* mbinfo, vp8g_frame_result* results,
@@ -2034,6 +2035,8 @@ int vp8g_launch_encode_w1(const uint8_t* yuv, size_t yfb, int w, int h, int n,
   hipLaunchKernelGGL(k_encode_w1<false>, dim3(n), dim3(64), lds, (hipStream_t)stream, a);
   return launch_check("k_encode_w1");
 }
+
+#endif
 
 int vp8g_launch_encode_none(const uint8_t* yuv, size_t yfb, int w, int h, int n,
                             const uint8_t* segmap, const uint8_t* amode,

@@ -1529,6 +1529,11 @@ __global__ __launch_bounds__(256) void k_vp8l_entropy(const uint8_t* __restrict_
     const uint32_t pix = nx[0], prev = nx[1], up = nx[2], ul = nx[3];
     if (i + 256 < n) load(i + 256, nx);
     const int yy = i / W, x = i - yy * W, y = y0 + yy;
+    {   // transparent pixels, none skipped (VP8L_EH_TRANSP): one add per wave
+      const uint64_t tr = __ballot(!plane && (pix >> 24) == 0);
+      if (tr && (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)))
+        atomicAdd(&h[VP8L_EH_TRANSP], (uint32_t)__popcll(tr));
+    }
     const uint32_t d = sub_pixels(pix, prev);
     if (d == 0) continue;
     if (y > 0 && up == pix) continue;

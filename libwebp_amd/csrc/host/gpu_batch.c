@@ -116,10 +116,14 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   b->sharp = vp8h_use_sharp(config, width, height);
   b->dither = b->sharp ? 0.f : vp8h_import_dithering(config);
   b->threads = host_threads > 0 ? host_threads : default_threads(device);
-  {   /* WEBP_AMD_HOST_EMIT=1: boolean-code partition 1 on the host threads */
+  b->host_emit = 0;
+#ifdef WEBP_AMD_DIAG
+  {   /* diagnostic build only: WEBP_AMD_HOST_EMIT=1 boolean-codes partition 1
+         on the host threads (A/B of K4; libwebp_amd_diag.so) */
     const char* he = getenv("WEBP_AMD_HOST_EMIT");
     b->host_emit = he && he[0] == '1';
   }
+#endif
 
   const size_t N = (size_t)max_frames, nmb = (size_t)b->nmb;
   CHK(hipSetDevice(device));

@@ -563,10 +563,11 @@ int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t*
         e->h_fidx[s] = f;
         e->h_fmode[s] = mode[f];
         /* the reference's own predictor choice where GetResidual updates the
-           picture (model: needs_exact_predictor): near-lossless, or a
-           transparent pixel L0 kept (its alpha histogram at 0) without exact */
-        e->h_pexact[s] = !l->p.exact &&
-                         (l->p.nlq_bits > 0 || l->h_ehist[(size_t)f * VP8L_EHIST + 0] > 0);
+           picture (model: needs_exact_predictor): near-lossless, or -- without
+           exact -- any transparent pixel (predictor_enc.c:273-288), counted by
+           L0 over every pixel */
+        e->h_pexact[s] = !l->p.exact && (l->p.nlq_bits > 0 ||
+                                         l->h_ehist[(size_t)f * VP8L_EHIST + VP8L_EH_TRANSP] > 0);
         l->route_eng[f] = e;
         l->route_slot[f] = s;
         continue;

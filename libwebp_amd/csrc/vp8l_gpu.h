@@ -54,9 +54,13 @@ extern "C" {
 #define VP8L_MAX_HUFF_IMAGE 2600   /* MAX_HUFF_IMAGE_SIZE, src/enc/vp8l_enc.c */
 /* per frame: AnalyzeEntropy's 13 histograms (HistoIx order), then the
  * transform search's accumulated histograms: predictor-12 residuals of A, R,
- * G, B and of the sub-green R-G, B-G (VP8L_EH_ACC + 0..5) */
+ * G, B and of the sub-green R-G, B-G (VP8L_EH_ACC + 0..5), then the count of
+ * fully transparent pixels over the whole picture (VP8L_EH_TRANSP: the
+ * histograms skip pixels equal to their left or upper neighbour, so a
+ * transparent area leaves no trace in them) */
 #define VP8L_EH_ACC 13
-#define VP8L_EHIST (19 * 256)
+#define VP8L_EH_TRANSP (19 * 256)
+#define VP8L_EHIST (19 * 256 + 4)
 #define VP8L_PAL_STRIDE 260        /* count + up to 256 colours (+ pad) */
 #define VP8L_MAX_PALETTE 256
 /* cache-size choice histograms per frame: literal channels G,R,B,A per

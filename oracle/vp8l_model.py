@@ -637,13 +637,14 @@ def residual_image(argb, tb, low_effort=False, near_q=100, exact=False, sg=False
 def needs_exact_predictor(argb_in, near_q, exact):
     """Frames whose predictor residuals update the picture as GetResidual
     goes (predictor_enc.c:234-292): near-lossless below 100, or -- without
-    `exact` -- a transparent pixel among those L0 keeps (its alpha histogram
-    at 0). They take the reference's own predictor choice (residual_image);
-    the others the cross-entropy choice (choose_predictors_ce). argb_in: the
-    input picture's ARGB."""
+    `exact` -- any fully transparent pixel (GetResidual's alpha-0 clean-up,
+    :273-288; counted over every pixel, not L0's de-duplicated ones). They
+    take the reference's own predictor choice (residual_image); the others
+    the cross-entropy choice (choose_predictors_ce). argb_in: the input
+    picture's ARGB."""
     if exact:
         return False
-    return near_lossless_bits(near_q) > 0 or int(l0_histograms(argb_in)[0][0]) > 0
+    return near_lossless_bits(near_q) > 0 or bool(((np.asarray(argb_in) >> 24) == 0).any())
 
 
 def ce_tables(G):

@@ -12,6 +12,8 @@ Near-lossless cases: the SHA-256 of the reference's VP8ApplyNearLossless
 output (src/enc/near_lossless_enc.c, exported by the reference build) as
 little-endian ARGB words, the size of its `-near_lossless q` encode, the
 SHA-256 of that stream decoded (RGBA) and the transforms it carries.
+Transparent cases (no `exact`): the size of the reference's output and the
+SHA-256 of that stream decoded (RGBA).
 Residual-image cases: VP8LResidualImage (the predictor choice and the
 residuals, near-lossless quantisation and alpha-0 clean-up included) on
 sub-green / plain ARGB: the chosen predictors and the residuals' SHA-256.
@@ -36,6 +38,18 @@ CASES = [
     ("g2", 320, 240, 1), ("g4", 320, 240, 2), ("g16", 320, 240, 3), ("g200", 320, 240, 4),
     ("g16", 1920, 1080, 5), ("q3", 320, 240, 0), ("q4", 512, 384, 1), ("q6", 256, 256, 1),
     ("q7", 400, 300, 2), ("q16", 320, 240, 3),
+    # > 256 colours with long-range repeats (round 4)
+    ("tile", 512, 384, 0), ("tile", 1920, 1080, 1), ("text", 640, 360, 0), ("text", 1920, 1080, 2),
+]
+
+# transparent areas without `exact` (webp_enc.c:402-403 zeroes them, then
+# GetResidual keeps only the alpha residual, predictor_enc.c:273-288): the
+# decoded pixels depend on the predictor of every tile, so the stream
+# decoded must equal the reference's stream decoded
+TRANSP_CASES = [
+    # kind, w, h, frame
+    ("border", 200, 150, 0), ("border", 333, 257, 3), ("sprite", 256, 192, 1),
+    ("sprite", 127, 95, 2),
 ]
 
 
@@ -128,6 +142,15 @@ def main():
                        subtract_green=sg, modes=modes,
                        residual_sha256=hashlib.sha256(res.astype("<u4").tobytes()).hexdigest()))
         print({k: v for k, v in rs[-1].items() if k != "modes"})
+    tr = []
+    for kind, w, h, f in TRANSP_CASES:
+        img = lossless_picture(kind, w, h, f)
+        data, _ = abi.encode_rgba(lib, img, 75.0, 4, lossless=1, use_argb=True)
+        dec = M.ref_decode(lib, data)
+        tr.append(dict(kind=kind, w=w, h=h, frame=f, size=len(data),
+                       decoded_sha256=hashlib.sha256(dec.tobytes()).hexdigest(),
+                       transforms=M.vp8l_transforms(data)))
+        print(tr[-1])
     from test_alpha import alpha_frame, logo_frame
     al = []
     for kind, w, h, f, tol in ALPH_CASES:
@@ -138,7 +161,8 @@ def main():
         print(al[-1])
     json.dump({"generator": "tests/golden/make_lossless_golden.py",
                "reference": "libwebp 1.3.2 (oracle/_ref), -lossless -m 4 -q 75",
-               "cases": out, "near_lossless": nl, "residual_image": rs, "alph": al},
+               "cases": out, "near_lossless": nl, "residual_image": rs, "alph": al,
+               "transparent": tr},
               open(os.path.join(HERE, "lossless_kat.json"), "w"), indent=1)
 
 

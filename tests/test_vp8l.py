@@ -28,7 +28,9 @@ VP8L_SIZE_TOL = 0.02
 # direct mode on quantised syn-v1 within 3.5%, palettised graphics (glyph
 # rows, rectangles; the hash-chain + cost-model parse) within 5% (1080p g16:
 # 1.042)
-KIND_TOL = {"syn": 0.02, "g": 0.05, "q": 0.035, "q16": 0.02}
+# tiled syn-v1 / text over a gradient (more than 256 colours, long-range
+# repeats: tests/golden/make_lossless_golden.py)
+KIND_TOL = {"syn": 0.02, "g": 0.05, "q": 0.035, "q16": 0.02, "tile": 0.20, "text": 0.05}
 
 
 def kind_tol(kind):
@@ -113,6 +115,37 @@ def test_model_entropy_mode_and_size_vs_reference():
             assert len(P["palette"]) == c["palette_size"], c
         assert np.array_equal(decode(data), img), c
         assert len(data) <= c["size"] * (1 + kind_tol(c["kind"])), (c, len(data))
+
+
+def transparent_cases():
+    import json
+    kat = json.load(open(os.path.join(ROOT, "tests", "golden", "lossless_kat.json")))
+    return kat["transparent"]
+
+
+def zero_transparent(img):
+    """WebPEncode's WebPReplaceTransparentPixels(pic, 0) without `exact`
+    (src/enc/webp_enc.c:402-403)"""
+    out = img.copy()
+    out[out[..., 3] == 0] = 0
+    return out
+
+
+def test_model_transparent_matches_reference():
+    """transparent areas without `exact`, incl. a border through pixel (0, 0)
+    that AnalyzeEntropy's de-duplicated histograms never see: the alpha-0
+    clean-up makes the decoded RGB depend on every tile's predictor, so the
+    model takes the reference's own predictor search and its stream decodes
+    to the reference encoder's pixels (committed SHA-256s of the reference's
+    output decoded, tests/golden/make_lossless_golden.py)"""
+    import hashlib
+    for c in transparent_cases():
+        img = zero_transparent(lossless_picture(c["kind"], c["w"], c["h"], c["frame"]))
+        assert M.needs_exact_predictor(M.to_argb(img), 100, False), c
+        data = M.encode(img)
+        assert M.vp8l_transforms(data) == c["transforms"], c
+        assert hashlib.sha256(decode(data).tobytes()).hexdigest() == c["decoded_sha256"], c
+        assert len(data) <= c["size"] * 1.10, (c, len(data))
 
 
 def test_model_near_lossless_matches_reference():
@@ -285,11 +318,88 @@ def quantized(w, h, levels, f):
     return img.astype(np.uint8)
 
 
+def tiled(w, h, f):
+    """syn-v1 (thousands of colours) with long-range repeats: 64x64 tiles of
+    the picture copied to other places, most of them rows away (the content
+    only a hash-chain LZ77 search finds; backward_references_enc.c:259)."""
+    img = syn_v1(w, h, f).copy()
+    rng = np.random.default_rng(100 + f)
+    T = 64
+    srcs = [(int(rng.integers(0, max(1, h - T))), int(rng.integers(0, max(1, w - T))))
+            for _ in range(4)]
+    for ty in range(0, h - T + 1, T):
+        for tx in range(0, w - T + 1, T):
+            if (tx // T + 2 * (ty // T) + f) % 3 == 0:
+                sy, sx = srcs[int(rng.integers(0, len(srcs)))]
+                img[ty:ty + T, tx:tx + T] = img[sy:sy + T, sx:sx + T]
+    return img
+
+
+def text_on_gradient(w, h, f):
+    """Anti-aliased 'text' over a colour gradient: a few hundred distinct
+    8x12 glyphs set in lines (the same glyph repeats far apart), blended
+    over a smooth background -- more than 256 colours, long-range repeats."""
+    rng = np.random.default_rng(200 + f)
+    yy, xx = np.mgrid[0:h, 0:w]
+    bg = np.stack([(xx * 255) // max(1, w - 1), (yy * 255) // max(1, h - 1),
+                   ((xx + yy) * 127) // max(1, w + h - 2) + 64], axis=-1).astype(np.int64)
+    glyphs = rng.integers(0, 5, size=(40, 12, 8)) * 64   # coverage 0..256 in 5 steps
+    glyphs = np.minimum(glyphs, 256)
+    cov = np.zeros((h, w), dtype=np.int64)
+    for r in range(4, h - 12, 16):
+        x = 4
+        while x + 8 < w:
+            if rng.random() < 0.15:   # word gap
+                x += 8
+                continue
+            cov[r:r + 12, x:x + 8] = glyphs[int(rng.integers(0, 40))]
+            x += 9
+    ink = np.array([20, 20, 40], dtype=np.int64)
+    rgb = (bg * (256 - cov[..., None]) + ink * cov[..., None]) >> 8
+    img = np.empty((h, w, 4), dtype=np.uint8)
+    img[..., :3] = rgb
+    img[..., 3] = 255
+    return img
+
+
+def transparent_border(w, h, f):
+    """syn-v1 inside a fully transparent border that includes pixel (0, 0)
+    (icons, sprites): every transparent pixel equals its left or upper
+    neighbour, so AnalyzeEntropy's histograms never see one."""
+    img = syn_v1(w, h, f).copy()
+    b = 6 + f % 4
+    img[:b, :, 3] = 0
+    img[-b:, :, 3] = 0
+    img[:, :b, 3] = 0
+    img[:, -b:, 3] = 0
+    return img
+
+
+def transparent_sprite(w, h, f):
+    """an opaque disc of syn-v1 on a transparent background (whose RGB is
+    not zero: WebPEncode zeroes it unless `exact`)"""
+    img = syn_v1(w, h, f).copy()
+    yy, xx = np.mgrid[0:h, 0:w]
+    r2 = (xx - w / 2) ** 2 + (yy - h / 2) ** 2
+    img[..., 3] = np.where(r2 < (min(w, h) * 0.4) ** 2, 255, 0).astype(np.uint8)
+    return img
+
+
 def lossless_picture(kind, w, h, f):
-    """syn-v1 ("syn"), palettised graphics ("g<colours>") or syn-v1 cut to
-    <levels> values per channel ("q<levels>")"""
+    """syn-v1 ("syn"), palettised graphics ("g<colours>"), syn-v1 cut to
+    <levels> values per channel ("q<levels>"), syn-v1 with repeated tiles
+    ("tile"), text over a gradient ("text"), syn-v1 in a transparent border
+    ("border") or a transparent-background sprite ("sprite")"""
     if kind == "syn":
         return syn_v1(w, h, f)
+    if kind == "tile":
+        return tiled(w, h, f)
+    if kind == "text":
+        return text_on_gradient(w, h, f)
+    if kind == "border":
+        return transparent_border(w, h, f)
+    if kind == "sprite":
+        return transparent_sprite(w, h, f)
     if kind == "synt":   # syn-v1 with transparent (zeroed, as WebPEncode leaves them) and soft alpha
         img = syn_v1(w, h, f).copy()
         yy, xx = np.mgrid[0:h, 0:w]
@@ -555,6 +665,21 @@ def test_gpu_near_lossless_decodes_like_reference(gpu):
         assert M.vp8l_transforms(data) == c["transforms"], c
         assert hashlib.sha256(decode(data).tobytes()).hexdigest() == c["decoded_sha256"], c
         assert data == M.encode(img, near_lossless_q=c["near_lossless"]), c
+
+
+@pytest.mark.gpu
+def test_gpu_transparent_no_exact(gpu):
+    """WebPEncode -lossless without `exact` on pictures with transparent
+    areas (a border through pixel (0, 0), a sprite on a transparent
+    background): the engine's L0 counts transparent pixels over the whole
+    picture and routes the frame to the reference's predictor search, so the
+    stream equals the model's and decodes to the reference encoder's pixels"""
+    import hashlib
+    for c in transparent_cases():
+        img = lossless_picture(c["kind"], c["w"], c["h"], c["frame"])
+        data = gpu.encode_rgba(img, quality=75.0, method=4, lossless=1, use_argb=True)
+        assert data == M.encode(zero_transparent(img)), c
+        assert hashlib.sha256(decode(data).tobytes()).hexdigest() == c["decoded_sha256"], c
 
 
 @pytest.mark.gpu

@@ -11,6 +11,24 @@ cd $R
 has() { [[ " $STEPS " == *" $1 "* ]]; }
 run() { echo "== $*" >> $O/steps.log; "$@"; local rc=$?; echo "   rc=$rc" >> $O/steps.log; return $rc; }
 BENCH="python3 $R/bench.py --no-cpu --no-host-input"
+if has boxinfo; then   # CPU share, affinity and clocks of this box
+  { echo "cpu.max: $(cat /sys/fs/cgroup/cpu.max 2>/dev/null)"; echo "nproc: $(nproc)";
+    python3 -c 'import os; print("affinity:", len(os.sched_getaffinity(0)))';
+    rocm-smi --showclocks 2>&1; rocm-smi --showproductname 2>&1 | head -20; } > $O/boxinfo.log 2>&1
+fi
+if has h2d; then   # H2D / D2H copy rates from pinned host memory (host-input leg)
+  run timeout -k 10 120 python3 tools/h2d_probe.py 256 > $O/h2d.json 2> $O/h2d.err || exit 1
+  HSA_ENABLE_SDMA=0 run timeout -k 10 120 python3 tools/h2d_probe.py 256 > $O/h2d_nosdma.json \
+    2> $O/h2d_nosdma.err || exit 1
+fi
+if has trace; then   # K3 per-worker wait / stage accounting (diagnostic build)
+  WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_trace.so run timeout -k 10 150 \
+    python3 tools/k3_trace.py 1920 1080 256 4 75 $O/k3_trace_256.json > $O/k3_trace_256.log 2>&1 || exit 1
+fi
+if has trace4; then   # the same for config 4 (one 4096^2 q90 m6 frame, K3X)
+  WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_trace.so run timeout -k 10 150 \
+    python3 tools/k3_trace.py 4096 4096 1 6 90 $O/k3_trace_cfg4.json > $O/k3_trace_cfg4.log 2>&1 || exit 1
+fi
 if has tests; then
   run timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
     > $O/gpu_tests.log 2>&1 || exit 1

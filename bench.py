@@ -79,6 +79,9 @@ def parse_args(argv=None):
                          "tests run several real-encoder ranks on one GPU)")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on device 0 (tests on a one-GPU box only)")
+    ap.add_argument("--force-pg", action="store_true",
+                    help="create the process group (and run the size all-gather / timing "
+                         "reductions through it) even with one rank (tests of the RCCL path)")
     return ap.parse_args(argv)
 
 
@@ -221,7 +224,7 @@ def gather_sizes(sizes, world):
     data-path collective)."""
     import torch
     import torch.distributed as dist
-    if world == 1:
+    if not dist.is_initialized():
         return [sizes]
     out = [torch.empty_like(sizes) for _ in range(world)]
     dist.all_gather(out, sizes)
@@ -231,7 +234,7 @@ def gather_sizes(sizes, world):
 def max_over_ranks(seconds, world, device):
     import torch
     import torch.distributed as dist
-    if world == 1:
+    if not dist.is_initialized():
         return seconds
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -242,7 +245,7 @@ def sum_over_ranks(values, world, device):
     import torch
     import torch.distributed as dist
     t = torch.tensor(values, dtype=torch.int64, device=device)
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [int(v) for v in t.tolist()]
 
@@ -423,8 +426,14 @@ def main(argv=None):
         backend = args.dist_backend or "nccl"
     # the collectives' tensors: on the GPU for RCCL, in host memory for gloo
     cdev = dev if backend == "nccl" else torch.device("cpu")
-    if world > 1:
+    if world > 1 or args.force_pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:   # a one-rank group outside torchrun
+            import socket
+            sk = socket.socket()
+            sk.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            sk.close()
         if backend == "nccl":
             dist.init_process_group(backend, rank=rank, world_size=world, device_id=dev)
         else:
@@ -468,34 +477,26 @@ def main(argv=None):
                                          low_memory=int(args.low_memory)))
 
     # input of a step: "host" = RGBA in pinned host memory, uploaded by the
-    # step itself; "hbm" = the frames already in HBM. With
-    # host input every instance has two device buffers and two copy streams:
-    # the upload of its step i+1 runs while its step i encodes (encode_device
-    # returns once the batch's .webp bytes are in host memory, so the buffer
-    # of step i is free for step i+2 when the call returns)
+    # step itself: WebPGpuBatchEncodeRGBAHost puts the DMA
+    # copy on the encoder instance's own stream ahead of its K1, so it runs
+    # while the other instances' kernels occupy the CUs; "hbm" = the frames
+    # already in HBM
     host_in = args.input == "host" and not args.stub
-    pinned, bufs, cstreams = None, None, None
-    if host_in:
-        pinned = torch.empty(rgba.numel(), dtype=torch.uint8, pin_memory=True)
-        pinned.copy_(rgba)
-        bufs = [[torch.empty_like(rgba), torch.empty_like(rgba)] for _ in range(E)]
-        cstreams = [[torch.cuda.Stream(dev), torch.cuda.Stream(dev)] for _ in range(E)]
+    pinned = None
 
-    def upload(e, slot):
-        with torch.cuda.stream(cstreams[e][slot]):
-            bufs[e][slot].copy_(pinned, non_blocking=True)
+    def make_pinned():
+        p = torch.empty(rgba.numel(), dtype=torch.uint8, pin_memory=True)
+        p.copy_(rgba)
+        return p
+
+    if host_in:
+        pinned = make_pinned()
 
     def engine_steps(e, n, host, tails):
         """Engine e's share of n steps (dealt round-robin over the engines)."""
-        mine = len(range(e, n, E))
-        if host and mine:
-            upload(e, 0)
-        for i in range(mine):
+        for _ in range(e, n, E):
             if host:
-                if i + 1 < mine:
-                    upload(e, (i + 1) & 1)
-                encs[e].encode_device(bufs[e][i & 1].data_ptr(), B,
-                                      stream=cstreams[e][i & 1].cuda_stream)
+                encs[e].encode_host_ptr(pinned.data_ptr(), B)
             else:
                 encs[e].encode_device(rgba.data_ptr() if rgba is not None else 0, B,
                                       stream=stream)
@@ -503,7 +504,7 @@ def main(argv=None):
                 tails.append(encs[e].timings())
 
     def barrier():
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
         if not args.stub:
             torch.cuda.synchronize(dev)
@@ -573,13 +574,10 @@ def main(argv=None):
     if not args.stub and not args.no_other_input:
         n_other = max(3 * E, min(args.steps, 4))
         if not host_in:
-            pinned = torch.empty(rgba.numel(), dtype=torch.uint8, pin_memory=True)
-            pinned.copy_(rgba)
-            bufs = [[torch.empty_like(rgba), torch.empty_like(rgba)] for _ in range(E)]
-            cstreams = [[torch.cuda.Stream(dev), torch.cuda.Stream(dev)] for _ in range(E)]
+            pinned = make_pinned()
         el = max_over_ranks(run(n_other, not host_in), world, cdev)
         other_rate = world * n_other * B * W * H / el / 1e6
-    del bufs, pinned
+    del pinned
 
     line = None
     if rank == 0:
@@ -595,8 +593,9 @@ def main(argv=None):
                                 "tests/golden/shard_kat.json" % (checked, world)
         line["config"]["input"] = "host" if host_in else "hbm"
         line["input"] = ("host: RGBA in pinned host memory -> .webp in host memory, H2D "
-                         "upload inside every step (SURVEY.md 8(d)); each of the %d encoder "
-                         "instances uploads its step i+1 during its step i" % len(encs)
+                         "upload inside every step (SURVEY.md 8(d)): one DMA copy on the "
+                         "encoder instance's stream ahead of its kernels, beside the other "
+                         "%d instance(s)' kernels" % (len(encs) - 1)
                          if host_in else
                          "hbm: RGBA frames already resident in HBM (no upload)")
         if other_rate is not None:
@@ -608,8 +607,11 @@ def main(argv=None):
             line["host_cpus_per_rank"] = len(cpus) if cpus else "unpinned"
         if args.stub:
             line["data"] = "stub encoder (CPU test double, no GPU)"
+        if dist.is_initialized():
+            line["collectives"] = "%s, %d rank(s): all-gather of the encoded sizes, " \
+                                  "max / sum reductions" % (dist.get_backend(), world)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
     for e in encs:

@@ -121,6 +121,17 @@ class GpuBatch:
         self.n = n
         return self
 
+    def encode_host_ptr(self, ptr, n, frame_stride=None, row_stride=None):
+        """Encode n RGBA frames at host address ptr. Page-locked memory
+        (hipHostMalloc, torch pin_memory) is uploaded by one DMA copy on the
+        encoder's own stream ahead of its kernels; pageable memory is copied
+        synchronously first."""
+        row_stride = row_stride or 4 * self.width
+        frame_stride = frame_stride or row_stride * self.height
+        ok = self._lib.WebPGpuBatchEncodeRGBAHost(self._h, ptr, frame_stride, row_stride, n)
+        if not ok:
+            raise RuntimeError("WebPGpuBatchEncodeRGBAHost failed: %s" % last_error())
+
     def encode_host(self, frames):
         """frames: (N, H, W, 4) uint8 numpy array in host memory."""
         import numpy as np

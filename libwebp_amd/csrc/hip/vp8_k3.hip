@@ -72,7 +72,6 @@ struct K3S {
   uint8_t recuv[4][128];
   alignas(16) int16_t lv16[4][16][16];   // zigzag levels per mode/block
   alignas(16) int16_t lvdc[4][16];
-  alignas(16) int16_t co16[4][16][16];   // coefficients (trellis hand-off)
   int16_t whtq[4][16];
   int16_t dcs[4][16];
   alignas(16) int16_t lvuv[4][8][16];
@@ -83,11 +82,12 @@ struct K3S {
   alignas(16) int16_t fin_uv[8][16];
   uint8_t modes[16];
   uint8_t canvas[17][24];
-  alignas(16) int16_t lv4[10][16];
-  alignas(16) int16_t co4[10][16];
-  alignas(8) unsigned long long best4[2];   // intra4 argmin key (score << 4 | mode), 2 buffers
-  alignas(8) score_t sm4[10];      // intra4 candidate scores with lambda_mode
-  int32_t r4[10][4];               // H, nz
+  alignas(8) unsigned long long best4[3];   // intra4 argmin key (score << 4 | mode), 3 buffers
+  alignas(8) score_t sm4[2][10];   // intra4 candidate scores with lambda_mode (by sub-block parity)
+  int32_t r4[2][10][4];            // H, nz, R, D (by sub-block parity)
+  uint8_t rec4[2][10][16];         // every candidate's reconstruction (by sub-block parity)
+  int32_t nzsel;                   // the m5 pass: nz of the sub-block's given mode
+  int32_t lead;                    // the worker's place in the row wavefront (issue priority)
   int32_t hsrc[16];                // sum_j w_j |Hadamard(src block)_j| per luma block
   alignas(16) int16_t acc_ac[16][16];
   uint8_t acc_out[256];
@@ -97,7 +97,6 @@ struct K3S {
   int32_t wsum[2][4];              // per-wave token-count totals (scan)
   int32_t redw[4];                 // per-wave reduction slots
   uint32_t fold_total;             // tokens of the MBs being folded
-  uint32_t trnz[4];
   uint32_t bar;                    // worker barrier counter
   int32_t myabort;
   int32_t flag_ldc;                // left DC nz flag hand-off from wave 0
@@ -113,6 +112,10 @@ struct K3S {
   // written), and the token count of each MB of its current row
   uint32_t rdelta[NSLOT];
   uint16_t rowcnt[1024];           // mbw <= 1024 (width <= 16383)
+  // token arena (K3Args::arena): this worker's current chunk [cpos, cend),
+  // and where each MB of its current row put its tokens
+  uint32_t cpos, cend;
+  uint32_t rowpos[1024];
 #ifdef K3_TRACE
   unsigned long long trace[16];    // diagnostic build: per-worker cycle / event counts (K3TR_*)
 #endif
@@ -166,6 +169,18 @@ __device__ __forceinline__ int zz_rt(int n) {   // kZigzag[n] for a runtime n
 template <int C>
 __device__ __forceinline__ int dpp(int v) {
   return __builtin_amdgcn_mov_dpp(v, C, 0xf, 0xf, false);
+}
+// DPP reads for the trellis whose result is pinned where it is written: a
+// DPP whose value feeds only one arm of a select may otherwise be sunk into
+// a branch, where the lanes of the other arm are masked off and the source
+// lanes among them hand over stale registers (seen on gfx950: lane first + 1
+// read its own initial value instead of lane first's score). `old` is what a
+// lane with no source lane in its row (row_shr at lane 0, row_shl at 15) gets.
+template <int C>
+__device__ __forceinline__ int dpp_pin(int old, int v) {
+  int r = __builtin_amdgcn_update_dpp(old, v, C, 0xf, 0xf, false);
+  asm volatile("" : "+v"(r));
+  return r;
 }
 #define DPP_QB(k) ((k) | ((k) << 2) | ((k) << 4) | ((k) << 6))
 #define DPP_ROR(n) (0x120 + (n))   // lane i reads lane (i - n) mod 16
@@ -334,10 +349,10 @@ __device__ __forceinline__ int quant_lane(int cv, int j, const vp8g_mtx& M, int&
 // 16-lane block: natural index j reads j-1, j-3, j-4 or j+3 (DPP row shifts,
 // no LDS round trip). Lane j = 0 (zigzag 0) has no predecessor.
 __device__ __forceinline__ int zz_prev(int v, int j) {
-  const int m1 = dpp<0x111>(v);   // row_shr:1
-  const int m3 = dpp<0x113>(v);   // row_shr:3
-  const int m4 = dpp<0x114>(v);   // row_shr:4
-  const int p3 = dpp<0x103>(v);   // row_shl:3
+  const int m1 = dpp_pin<0x111>(0, v);   // row_shr:1
+  const int m3 = dpp_pin<0x113>(0, v);   // row_shr:3
+  const int m4 = dpp_pin<0x114>(0, v);   // row_shr:4
+  const int p3 = dpp_pin<0x103>(0, v);   // row_shl:3
   const uint32_t bit = 1u << j;
   return (bit & 0xA00Au) ? m1 : (bit & 0x5250u) ? m3 : (bit & 0x0900u) ? m4 : p3;
 }
@@ -363,12 +378,158 @@ __device__ __forceinline__ int rate_lane(const K3G& G, int level, int j, int g, 
 }
 
 // ---------------------------------------------------------------------------
+// Lane-parallel TrellisQuantizeBlock (quant_enc.c:593-763) on the 16-lane
+// groups of a wave, one block per group (group-uniform `act`, `ctx0`).
+//
+// The reference walks zigzag positions n = first..last keeping two nodes
+// (level0 and level0 + 1) with their best score. Everything but the scores
+// is known up front: a node's level, its distortion change and the cost row
+// of each predecessor (that row depends only on the predecessor's level,
+// level0(n - 1) + p, not on the path). So lane n of the group (zigzag
+// order; the coefficients arrive by one bpermute) computes its levels,
+// distortion terms and the four transition costs in parallel, and only the
+// min-plus recursion over n stays sequential: round r hands every lane its
+// predecessor's two scores by DPP row_shr:1, and lane n holds its final
+// scores after n - first + 1 rounds -- the same int64 additions and the same
+// comparisons (predecessor 0 first, 1 only if strictly smaller) as the
+// reference, so the result is bit-exact. The best terminal node (first
+// minimum over (n, m) in the reference's order, against the skip score) is a
+// 16-lane minimum plus a ballot; the path is unwound by row_shl:1 rounds.
+// Rounds run to the wave's longest group only.
+struct Trellis16 {
+  int level;   // quantised level of this lane's coefficient (natural index j)
+  int dq;      // level * q[j] (reconstruction input)
+  int lvz;     // the level at zigzag position lane & 15
+  int nz;      // the group's block has a non-zero level (group-uniform)
+};
+
+template <int C>
+__device__ __forceinline__ long long dpp64(long long old, long long v) {
+  const int lo = dpp_pin<C>((int)(old & 0xffffffff), (int)(v & 0xffffffff));
+  const int hi = dpp_pin<C>((int)(old >> 32), (int)(v >> 32));
+  return (long long)(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__device__ __forceinline__ int wtrellis(int j) {   // kWeightTrellis[j] (quant_enc.c)
+  const unsigned long long t = j < 8 ? 0x0a11181b0b131b1eull : 0x06080a0b080c1113ull;
+  return (int)((t >> (8 * (j & 7))) & 0xff);
+}
+
+template <bool DBG = false>
+__device__ Trellis16 trellis16(const K3G& G, int c, bool act, int ctx0, int type,
+                               const vp8g_mtx& M, int lambda, long long* dbg = nullptr) {
+  const int lane = threadIdx.x & 63, g = lane & 48, n = lane & 15;
+  const int first = type == 0 ? 1 : 0;
+  const int jn = zz_rt(n);   // natural index of zigzag position n
+  const int cin = __shfl(c, g + jn);
+  // the last position worth inspecting (+1)
+  const int thresh2 = (int)M.q[1] * (int)M.q[1] / 4;
+  int last = max16((n >= first && cin * cin > thresh2) ? n : first - 1);
+  if (last < 15) ++last;
+  // this position's two nodes
+  const uint32_t Q = M.q[jn], iQ = M.iq[jn];
+  const int sign = cin < 0;
+  const uint32_t coeff0 = (uint32_t)(sign ? -cin : cin) + M.sharpen[jn];
+  const int level0 = min((int)((coeff0 * iQ) >> QFIX), MAX_LEVEL);
+  const int thr = min((int)((coeff0 * iQ + (0x80u << (QFIX - 8))) >> QFIX), MAX_LEVEL);
+  const int wt = wtrellis(jn);
+  const int e0 = (int)coeff0 - level0 * (int)Q, e1 = e0 - (int)Q;
+  const int cc = (int)(coeff0 * coeff0);
+  // delta_error in the reference's uint32 arithmetic, then as int
+  const score_t base0 = (score_t)256 * (int)((uint32_t)wt * ((uint32_t)(e0 * e0) - (uint32_t)cc));
+  const score_t base1 = (score_t)256 * (int)((uint32_t)wt * ((uint32_t)(e1 * e1) - (uint32_t)cc));
+  const bool live1 = level0 + 1 <= thr;   // level0 itself never exceeds thr
+  // cost rows of the two predecessors (position n - 1's nodes)
+  const int lp0 = dpp_pin<0x111>(0, level0);   // row_shr:1: level0 of position n - 1
+  const int rfirst = type * 24 + first * 3 + ctx0;
+  const int rb = type * 24 + band_of(n) * 3;
+  const int row0 = n == first ? rfirst : rb + min(lp0, 2);
+  const int row1 = n == first ? rfirst : rb + min(lp0 + 1, 2);
+  const score_t t00 = (score_t)level_cost(G.lcost[row0], level0) * lambda;
+  const score_t t01 = (score_t)level_cost(G.lcost[row1], level0) * lambda;
+  const int l1 = min(level0 + 1, MAX_LEVEL);   // (a node beyond MAX_LEVEL is dead anyway)
+  const score_t t10 = (score_t)level_cost(G.lcost[row0], l1) * lambda;
+  const score_t t11 = (score_t)level_cost(G.lcost[row1], l1) * lambda;
+  // the source node and the skip score
+  const int lastp = G.coeffs[((type * 8 + first) * 3 + ctx0) * 11];
+  const score_t s_init = (score_t)(ctx0 == 0 ? bit_cost(G.ecost, 1, lastp) : 0) * lambda;
+  const score_t skip = (score_t)bit_cost(G.ecost, 0, lastp) * lambda;
+  // min-plus recursion: R rounds, R = the longest group of the wave
+  const int span = act ? last - first + 1 : 0;
+  int R = span;
+#pragma unroll
+  for (int o = 16; o < 64; o <<= 1) R = max(R, __shfl_xor(R, o));
+  R = __builtin_amdgcn_readfirstlane(R);
+  // the source node reaches position `first` as its predecessor: through the
+  // DPP's `old` at lane 0 (first = 0), from lane 0 held at s_init (first = 1)
+  const bool src = n < first;
+  score_t S0 = src ? s_init : MAX_COST, S1 = S0;
+  int pv = 0;   // best predecessor of node 0 (bit 0) and node 1 (bit 1)
+  for (int r = 0; r < R; ++r) {
+    const score_t p0 = dpp64<0x111>(s_init, S0);
+    const score_t p1 = dpp64<0x111>(s_init, S1);
+    const score_t a0 = p0 + t00, b0 = p1 + t01;
+    const score_t a1 = p0 + t10, b1 = p1 + t11;
+    const bool q0 = b0 < a0, q1 = b1 < a1;
+    const score_t n0 = (q0 ? b0 : a0) + base0;
+    const score_t n1 = live1 ? (q1 ? b1 : a1) + base1 : MAX_COST;
+    S0 = src ? s_init : n0;
+    S1 = src ? s_init : n1;
+    pv = (int)q0 | ((int)q1 << 1);
+  }
+  // best terminal node: sc = S + last-position cost, first minimum in (n, m)
+  const bool in = act && n >= first && n <= last;
+  const int ctx1 = min(level0 + 1, 2);
+  const int bnext = type * 8 + band_of(n + 1);
+  const int lpc0 = n < 15 ? bit_cost(G.ecost, 0, G.coeffs[(bnext * 3 + min(level0, 2)) * 11]) : 0;
+  const int lpc1 = n < 15 ? bit_cost(G.ecost, 0, G.coeffs[(bnext * 3 + ctx1) * 11]) : 0;
+  const bool v0 = in && level0 != 0, v1 = in && live1;
+  const score_t sc0 = S0 + (score_t)lpc0 * lambda, sc1 = S1 + (score_t)lpc1 * lambda;
+  const bool take1 = v1 && (!v0 || sc1 < sc0);
+  const score_t NONE = 0x7fffffffffffffffLL;
+  const score_t cand = take1 ? sc1 : v0 ? sc0 : NONE;
+  score_t mn = cand;
+  mn = min(mn, dpp64<DPP_ROR(8)>(mn, mn));
+  mn = min(mn, dpp64<DPP_ROR(4)>(mn, mn));
+  mn = min(mn, dpp64<DPP_ROR(2)>(mn, mn));
+  mn = min(mn, dpp64<DPP_ROR(1)>(mn, mn));
+  const bool path = mn < skip;   // group-uniform
+  const uint64_t hit = __ballot(cand == mn && (v0 || v1));
+  const int nstar = path ? __builtin_ctzll((hit >> g) & 0xffff) : -1;
+  const int mstar = __shfl((int)take1, g + max(nstar, 0));
+  // unwind the path: node(n) = predecessor bit of node(n + 1) at n + 1
+  int B = path && act ? nstar - first + 1 : 0;
+#pragma unroll
+  for (int o = 16; o < 64; o <<= 1) B = max(B, __shfl_xor(B, o));
+  B = __builtin_amdgcn_readfirstlane(B);
+  int nd = mstar;
+  for (int r = 0; r < B; ++r) {
+    const int t = dpp_pin<0x101>(0, (pv >> nd) & 1);   // row_shl:1: lane n + 1's predecessor bit
+    nd = n == nstar ? mstar : t;
+  }
+  if constexpr (DBG) {
+    long long* d = dbg + 16 * lane;
+    d[0] = S0; d[1] = S1; d[2] = pv; d[3] = level0; d[4] = live1; d[5] = t00; d[6] = t01;
+    d[7] = t10; d[8] = t11; d[9] = base0; d[10] = base1; d[11] = nstar; d[12] = mstar;
+    d[13] = nd; d[14] = cand; d[15] = ((long long)R << 32) | (uint32_t)B;
+  }
+  Trellis16 res;
+  const int lvl = level0 + nd;
+  res.lvz = (path && act && n >= first && n <= nstar) ? (sign ? -lvl : lvl) : 0;
+  res.nz = ((__ballot(res.lvz != 0) >> g) & 0xffff) != 0;
+  const int j = lane & 15;
+  res.level = __shfl(res.lvz, g + zz_inv(j));
+  res.dq = (int16_t)(res.level * (int)M.q[j]);   // in[j] = out[n] * q_[j] (int16_t)
+  return res;
+}
+
+// ---------------------------------------------------------------------------
 // Intra16 candidates (quant_enc.c:772-822 ReconstructIntra16, cost_enc.c:232-256
 // VP8GetCostLuma16). Wave m = mode m. Fills rec16/lv16/lvdc and
 // mres[m] = {SSE, texture distortion, rate, nz (ac bits | dc << 24)}.
 
 template <bool TRELLIS>
-__device__ void eval_i16(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_seg& S,
+__device__ void eval_i16(const K3G& G, K3S& L, const vp8g_seg& S,
                          const MBCtx& ctx, int tid) {
   const int m = tid >> 6, lane = tid & 63, g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
   const int bsub = lane >> 4;
@@ -379,10 +540,8 @@ __device__ void eval_i16(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_se
     const int d = L.yin[py * BPS + px] - L.p16[m][py * 16 + px];
     co[p] = fdct_lane(d, j);
     if (j == 0) L.dcs[m][b] = (int16_t)co[p];
-    if (TRELLIS) L.co16[m][b][j] = (int16_t)co[p];
   }
-  if (lane < 4) L.trnz[lane] = 0;
-  WB();
+  wsync();   // the DC terms of this mode: written and read by its own wave
   if (lane < 16) {   // FTransformWHT + y2 quantisation, coefficient b = lane
     const int16_t* d = L.dcs[m];
     const int b = lane, r = b >> 2, col = b & 3;
@@ -402,32 +561,32 @@ __device__ void eval_i16(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_se
     L.whtq[m][b] = (int16_t)dq;
   }
   int lv[4], dq[4];
-  if constexpr (TRELLIS) {   // quant_enc.c:790-803, anti-diagonal order
+  if constexpr (TRELLIS) {
+    // quant_enc.c:790-803: the 16 blocks in anti-diagonal order, each
+    // block's context from the trellis results of the blocks above and to
+    // its left. Step st: group bx (= bsub) takes block (bx, st - bx) -- up to
+    // four blocks at once, one per 16-lane group of the mode's wave; the nz
+    // bits stay in a wave-uniform mask (no worker barrier)
+    uint32_t tnz = 0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) { lv[p] = 0; dq[p] = 0; }
     for (int st = 0; st < 7; ++st) {
-      if (lane < 16) {
-        const int b = lane, bx = b & 3, by = b >> 2;
-        if (bx + by == st) {
-          const uint32_t tm = L.trnz[m];
-          const int tc = by == 0 ? ctx.top(bx) : (int)((tm >> (b - 4)) & 1);
-          const int lc = bx == 0 ? ctx.left(by) : (int)((tm >> (b - 1)) & 1);
-          int c[16];
+      const int bx = bsub, by = st - bsub;
+      const bool on = by >= 0 && by < 4;
+      const int byc = on ? by : 0;
+      const int cst = byc == 0 ? co[0] : byc == 1 ? co[1] : byc == 2 ? co[2] : co[3];
+      const int tc = byc == 0 ? ctx.top(bx) : (int)((tnz >> (4 * (byc - 1) + bx)) & 1);
+      const int lc = bx == 0 ? ctx.left(byc) : (int)((tnz >> (4 * byc + bx - 1)) & 1);
+      const Trellis16 t = trellis16(G, j == 0 ? 0 : cst, on, tc + lc, 0, S.y1,
+                                    S.lambda_trellis_i16);
+      const uint64_t bal = __ballot(on && t.nz && j == 0);
 #pragma unroll
-          for (int k = 0; k < 16; ++k) c[k] = L.co16[m][b][k];
-          const int nz = trellis_quant(G, tn[m * 16 + b], c, L.lv16[m][b], tc + lc, 0, &S.y1,
-                                       S.lambda_trellis_i16);
-          L.lv16[m][b][0] = 0;
+      for (int q = 0; q < 4; ++q)
+        if ((bal >> (16 * q)) & 1) tnz |= 1u << (4 * (st - q) + q);
+      if (on) L.lv16[m][4 * byc + bx][j] = (int16_t)t.lvz;   // zigzag order (lane & 15 = n)
 #pragma unroll
-          for (int k = 1; k < 16; ++k) L.co16[m][b][k] = (int16_t)c[k];
-          if (nz) atomicOr(&L.trnz[m], 1u << b);
-        }
-      }
-      WB();
-    }
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int b = 4 * p + bsub;
-      lv[p] = j == 0 ? 0 : L.lv16[m][b][zz_inv(j)];
-      dq[p] = j == 0 ? 0 : L.co16[m][b][j];
+      for (int p = 0; p < 4; ++p)
+        if (on && byc == p) { lv[p] = j == 0 ? 0 : t.level; dq[p] = j == 0 ? 0 : t.dq; }
     }
   } else {   // quant_enc.c:805-812: DC position zeroed before QuantizeBlock
 #pragma unroll
@@ -456,7 +615,7 @@ __device__ void eval_i16(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_se
     const int r = rate_lane(G, lv[p], j, g, tctx + lctx, 0, 1);
     if (j == 0) rate += r;
   }
-  WB();   // whtq complete
+  wsync();   // whtq complete (this mode's wave only)
   // inverse WHT (dec.c:137-162): lane b < 16 of the mode's wave computes the
   // DC of block b once; each block's coefficient-0 lane takes it by a shuffle
   {
@@ -530,7 +689,7 @@ __device__ void eval_uv(const K3G& G, K3S& L, const vp8g_seg& S, const MBCtx& ct
     co[p] = fdct_lane(d, j);
     if (j == 0) L.uvdc[m][b] = (int16_t)co[p];
   }
-  WB();
+  wsync();   // uvdc of this mode: its own wave
   if (use_derr && lane < 2) {   // CorrectDCValues (quant_enc.c:875-906)
     const int cch = lane;
     const vp8g_mtx& M = S.uv;
@@ -562,7 +721,7 @@ __device__ void eval_uv(const K3G& G, K3S& L, const vp8g_seg& S, const MBCtx& ct
     L.uvderr[m][cch][1] = (int8_t)err[2];
     L.uvderr[m][cch][2] = (int8_t)err[3];
   }
-  WB();
+  wsync();   // CorrectDCValues results: this mode's wave
   int lv[2], dq[2];
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
@@ -678,7 +837,7 @@ __device__ __forceinline__ P4Lane p4_lane(const P4Op& op, int x, int y) {
 __device__ __forceinline__ int edge_off0(int k) { return k < 4 ? (4 - k) * 24 : k - 4; }
 
 template <bool TRELLIS>
-__device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_seg& S,
+__device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
                            const MBCtx& ctx, int tid, int x0,
                            int mbw, const uint8_t* predtop, const uint8_t* yl,
                            const uint8_t* yt, bool search, score_t rd_score, int max_bits,
@@ -706,6 +865,13 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
   const int wj = G.wy[j];
   const P4Lane pl = p4_lane(G.p4[act ? tid : 0], x, y);
   const int offa = edge_off0(pl.ia), offb = edge_off0(pl.ib), offc = edge_off0(pl.ic);
+  // left-edge samples (L K J I = column 3 of the sub-block to the left, rows
+  // 3..0): during the search they come from the winning candidate's row of
+  // rec4 -- the sub-block to the left was decided by the barrier just passed,
+  // its winner's commit to the canvas is not ordered before this read
+  const int la = pl.ia < 4 ? 4 * (3 - pl.ia) + 3 : -1;
+  const int lb = pl.ib < 4 ? 4 * (3 - pl.ib) + 3 : -1;
+  const int lc = pl.ic < 4 ? 4 * (3 - pl.ic) + 3 : -1;
   // this lane's y1 quantiser entries, once per MB
   const vp8g_mtx& M = S.y1;
   const uint32_t q_sh = M.sharpen[j], q_zt = M.zthresh[j], q_iq = M.iq[j], q_bias = M.bias[j];
@@ -717,53 +883,44 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
   int total_hdr = 0;
   I4Result res;
   res.ok = 1;
-  if (tid == 0) { L.best4[0] = ~0ull; L.d4acc = 0; L.r4acc = 0; }
+  if (tid == 0) { L.best4[0] = ~0ull; L.best4[1] = ~0ull; L.d4acc = 0; L.r4acc = 0; }
   WB();
+  int prev_bm = 0;   // the mode chosen for the previous sub-block (worker-uniform)
   for (int i4 = 0; i4 < 16; ++i4) {
-    const int bx = i4 & 3, by = i4 >> 2;
-    const int left_m = bx == 0 ? L.predleft[by] : L.modes[i4 - 1];
+    const int bx = i4 & 3, by = i4 >> 2, par = i4 & 1;
+    const int left_m = bx == 0 ? L.predleft[by] : search ? prev_bm : L.modes[i4 - 1];
     const int top_m = by == 0 ? predtop[4 * x0 + bx] : L.modes[i4 - 4];
     const int ctx4 = (int)((tnz >> bx) & 1) + (int)((lnz >> by) & 1);
-    // the worker's 4th wave (rtid 192..255) holds no mode: without trellis
-    // (whose per-mode steps carry barriers) it skips straight to the
-    // barrier, leaving its SIMD's issue slots to the other workers
-    const bool busy = TRELLIS || (tid >> 6) != 3;   // wave-uniform
+    // the worker's 4th wave (rtid 192..255) holds no mode: it skips straight
+    // to the barrier, leaving its SIMD's issue slots to the other workers
+    const bool busy = (tid >> 6) != 3;   // wave-uniform
     const int src = L.yin[(4 * by + y) * BPS + 4 * bx + x];
     int pr = 0, rec = 0, nzb = 0;
     int level = 0, dq = 0;
     if (busy) {
     {
       const uint8_t* cb = cv + 96 * by + 4 * bx;   // sub-block base (worker-uniform)
-      const int ea = cb[offa];
-      const int eb = cb[offb];
-      const int ec = cb[offc];
+      const bool lft = search && bx > 0;          // worker-uniform
+      const uint8_t* rl = &L.rec4[par ^ 1][prev_bm][0];
+      const int ea = *(lft && la >= 0 ? rl + la : cb + offa);
+      const int eb = *(lft && lb >= 0 ? rl + lb : cb + offb);
+      const int ec = *(lft && lc >= 0 ? rl + lc : cb + offc);
       pr = clip8((pl.wa * ea + pl.wb * eb + pl.wc * ec + pl.rnd) >> pl.sh);
       if (pl.dc) {
         int s4 = 4;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) s4 += cb[edge_off0(k)] + cb[edge_off0(5 + k)];
+        for (int k = 0; k < 4; ++k)
+          s4 += *(lft ? rl + 4 * (3 - k) + 3 : cb + edge_off0(k)) + cb[edge_off0(5 + k)];
         pr = s4 >> 3;
       }
     }
     SUBST(0);
     const int c = fdct_lane(src - pr, j);
     SUBST(1);
-    if constexpr (TRELLIS) {
-      if (act) L.co4[m][j] = (int16_t)c;
-      WB();
-      if (act && j == 0) {
-        int cc[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) cc[k] = L.co4[m][k];
-        trellis_quant(G, tn[m], cc, L.lv4[m], ctx4, 3, &S.y1, S.lambda_trellis_i4);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) L.co4[m][k] = (int16_t)cc[k];
-      }
-      WB();
-      if (act) {
-        level = L.lv4[m][zz_inv(j)];
-        dq = L.co4[m][j];
-      }
+    if constexpr (TRELLIS) {   // one mode per 16-lane group, no worker barrier
+      const Trellis16 t = trellis16(G, c, act, ctx4, 3, S.y1, S.lambda_trellis_i4);
+      level = t.level;
+      dq = t.dq;
     } else {   // QuantizeBlock_C (src/dsp/enc.c:653-677)
       const int neg = c < 0;
       const uint32_t coeff = (uint32_t)(neg ? -c : c) + q_sh;
@@ -789,16 +946,17 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
       const int cntnz = __popcll((bac >> g) & 0xffff);
       const int R0 = (m > 0 && cntnz <= 3) ? 140 : 0;
       const int Rc = rate_lane(G, level, j, g, ctx4, 3, 0);
+      if (act) L.rec4[par][m][j] = (uint8_t)rec;
       if (act && j == 0) {
         const int H = G.mcost4[(top_m * 10 + left_m) * 10 + m];
         const score_t dist = 256 * (score_t)(D + SD);
         const score_t sc = (score_t)(R0 + Rc + H) * S.lambda_i4 + dist;
-        atomicMin(&L.best4[i4 & 1], ((unsigned long long)sc << 4) | (unsigned)m);
-        L.sm4[m] = (score_t)(R0 + Rc + H) * S.lambda_mode + dist;
-        L.r4[m][0] = H;
-        L.r4[m][1] = nzb;
-        L.r4[m][2] = R0 + Rc;   // (the !search pass uses slot 2 for nz instead)
-        L.r4[m][3] = D;
+        atomicMin(&L.best4[i4 % 3], ((unsigned long long)sc << 4) | (unsigned)m);
+        L.sm4[par][m] = (score_t)(R0 + Rc + H) * S.lambda_mode + dist;
+        L.r4[par][m][0] = H;
+        L.r4[par][m][1] = nzb;
+        L.r4[par][m][2] = R0 + Rc;
+        L.r4[par][m][3] = D;
       }
     }
     }   // busy
@@ -806,15 +964,18 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
     WB();
     int bm;
     if (search) {
-      bm = (int)(L.best4[i4 & 1] & 15);   // argmin, ties to the lower mode
+      // argmin, ties to the lower mode. The slot read here was last written
+      // before this barrier; the one reset here (used two sub-blocks on) was
+      // last read before it (three slots, so no second barrier is needed)
+      bm = (int)(L.best4[i4 % 3] & 15);
       if (tid == 0) {
-        L.best4[(i4 + 1) & 1] = ~0ull;
-        L.d4acc += L.r4[bm][3];
-        L.r4acc += L.r4[bm][2];
+        L.best4[(i4 + 2) % 3] = ~0ull;
+        L.d4acc += L.r4[par][bm][3];
+        L.r4acc += L.r4[par][bm][2];
       }
-      const int H = L.r4[bm][0], bnzv = L.r4[bm][1];
+      const int H = L.r4[par][bm][0], bnzv = L.r4[par][bm][1];
       accH += H;
-      acc_score += L.sm4[bm];
+      acc_score += L.sm4[par][bm];
       acc_nz |= (uint32_t)bnzv << i4;
       if (acc_score >= rd_score) { res.ok = 0; break; }
       total_hdr += H;
@@ -829,11 +990,17 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, uint32_t (*tn)[32], const vp8g_
       L.canvas[4 * by + 1 + y][4 * bx + 1 + x] = (uint8_t)rec;
       L.acc_out[(4 * by + y) * 16 + 4 * bx + x] = (uint8_t)rec;
       L.acc_ac[i4][zz_inv(j)] = (int16_t)level;
-      if (!search && j == 0) L.r4[0][2] = nzb;
+      if (!search && j == 0) L.nzsel = nzb;
     }
     if (search && tid == 0) L.modes[i4] = (uint8_t)bm;
-    WB();
-    if (!search) acc_nz |= (uint32_t)L.r4[0][2] << i4;
+    prev_bm = bm;
+    // the search needs no second barrier: the next sub-block reads its left
+    // edge from rec4 (above), every other canvas sample it reads was committed
+    // before an earlier barrier, and L.modes[i4] is read 4 sub-blocks on
+    if (!search) {
+      WB();
+      acc_nz |= (uint32_t)L.nzsel << i4;
+    }
     SUBST(7);
   }
   WB();
@@ -1165,7 +1332,7 @@ __device__ __forceinline__ void publish(int32_t* p, int32_t v) {
 // accumulate; counters that would cross the halving threshold inside the MB
 // are replayed token by token (VP8RecordStats, cost_enc.h:45-56).
 __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t row0,
-                         uint16_t* tok_base, uint32_t* mboff) {
+                         uint16_t* tok_base, uint32_t* mboff, const uint16_t* arena) {
   // MBs [i0, i1) of this worker's row (first MB row0): record where their
   // tokens go in the frame's compact stream (moved there at frame end, see
   // compact_tokens), then add their statistics in one step.
@@ -1235,7 +1402,8 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
           uint32_t n = dlt >> 16, k = dlt & 0xffffu;   // the row's tokens of ss not applied yet
           for (uint32_t i = i0; i < i1 && n; ++i) {
             const uint32_t nt = L.rowcnt[i - row0];
-            const uint16_t* tk = tok_base + (size_t)i * VP8G_MAX_TOKENS_PER_MB;
+            const uint16_t* tk = arena ? arena + L.rowpos[i - row0]
+                                       : tok_base + (size_t)i * VP8G_MAX_TOKENS_PER_MB;
             for (uint32_t k4 = 0; k4 < nt && n; k4 += 256) {
               if ((p >> 16) + n < 0xfffeu) break;   // no halving left in the row
               uint32_t tq[4];
@@ -1307,7 +1475,8 @@ __device__ __forceinline__ void report_rows(K3G& G, K3S& L, const vp8g_frame_par
 // raster order by fold_ptr, so one worker of the frame folds at a time)
 template <bool X>
 __device__ void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t row0,
-                          uint16_t* tok_base, uint32_t* mboff, uint8_t* xs) {
+                          uint16_t* tok_base, uint32_t* mboff, uint8_t* xs,
+                          const uint16_t* arena) {
   if constexpr (X) {
     XHdr* XH = reinterpret_cast<XHdr*>(xs);
     uint32_t* xstats = reinterpret_cast<uint32_t*>(xs + XS_STATS);
@@ -1316,7 +1485,7 @@ __device__ void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uin
       if (tid == 0) G.ntok = ld_sc1(&XH->ntok);
       wbar(L);
     }
-    fold_mbs(G, L, tid, i0, i1, row0, tok_base, mboff);
+    fold_mbs(G, L, tid, i0, i1, row0, tok_base, mboff, arena);
     wbar(L);
     for (int s = tid; s < NSLOT; s += K3T) st_sc1(xstats + s, G.stats[s]);
     if (tid == 0) st_sc1(&XH->ntok, G.ntok);
@@ -1324,7 +1493,7 @@ __device__ void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uin
     wbar(L);
     if (tid == 0) st_sc1(&XH->fold_ptr, (int32_t)i1);
   } else {
-    fold_mbs(G, L, tid, i0, i1, row0, tok_base, mboff);
+    fold_mbs(G, L, tid, i0, i1, row0, tok_base, mboff, arena);
   }
 }
 
@@ -1404,7 +1573,32 @@ struct K3Args {
   uint8_t* xs;      // K3X: n x xs_fb bytes of cross-workgroup frame state
   size_t xs_fb;
   int nwg;          // K3X: workgroups per frame
+  // token arena (NULL: the per-MB slot layout, compacted at frame end). Each
+  // worker takes VP8G_ARENA_CHUNK-token chunks from *arena_top and writes
+  // every MB's tokens once, contiguously, at the chunk's next free position
+  // (mbpos, n x nmb); k_gather_tokens lays the frames' streams out later.
+  // Past arena_cap the tokens go to the sink chunk behind it and the frame
+  // reports VP8G_ERR_ARENA.
+  uint16_t* arena;
+  uint32_t arena_cap;
+  uint32_t* arena_top;
+  uint32_t* mbpos;
 };
+
+// a new chunk for this worker once fewer than one MB's worst case is left
+// (one lane; the caller orders it before the chunk's readers)
+__device__ __forceinline__ void arena_refill(K3S& L, K3G& G, const K3Args& a) {
+  if (L.cend - L.cpos >= (uint32_t)VP8G_MAX_TOKENS_PER_MB) return;
+  const uint32_t p = atomicAdd(a.arena_top, (uint32_t)VP8G_ARENA_CHUNK);
+  if (p <= a.arena_cap - (uint32_t)VP8G_ARENA_CHUNK && p < a.arena_cap) {
+    L.cpos = p;
+    L.cend = p + VP8G_ARENA_CHUNK;
+  } else {   // exhausted: the sink (its contents are never read)
+    L.cpos = a.arena_cap;
+    L.cend = a.arena_cap + VP8G_MAX_TOKENS_PER_MB;
+    atomicOr(&G.tok_err, VP8G_ERR_ARENA);
+  }
+}
 
 // TR: the method >= 5 instantiation carries the trellis paths; m3/m4 frames
 // run a kernel without them (smaller register footprint).
@@ -1426,12 +1620,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
   uint8_t* predtop = reinterpret_cast<uint8_t*>(nzw + mbw);           // 4*mbw
   int8_t* topderr = reinterpret_cast<int8_t*>(predtop + 4 * mbw);     // 4*mbw
   int32_t* rowdone = reinterpret_cast<int32_t*>(topderr + 4 * mbw);   // mbh
-  uint32_t (*tnall)[32] = reinterpret_cast<uint32_t (*)[32]>(rowdone + mbh);   // NW*64 (trellis)
-  uint32_t (*tn)[32] = tnall + 64 * wk;
   // K3X: the row above worker 0 comes from another workgroup, pulled into
   // these copies of the boundary arrays (same layout); every worker still
   // writes its own row's boundary into the shared arrays
-  uint8_t* xbase = reinterpret_cast<uint8_t*>(tnall) + (TR ? (size_t)NW * 64 * 32 * 4 : 0);
+  uint8_t* xbase = reinterpret_cast<uint8_t*>(((uintptr_t)(rowdone + mbh) + 15) & ~(uintptr_t)15);
   K3XL& XL = *reinterpret_cast<K3XL*>(xbase);
   uint8_t* xytop = xbase + ((sizeof(K3XL) + 15) & ~(size_t)15);
   uint8_t* xuvtop = xytop + 16 * mbw + 16;
@@ -1506,8 +1698,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     G.fs.nb[0] = G.fs.nb[1] = G.fs.nb[2] = 0;
     G.fold_ptr = 0; G.ntok = 0; G.tok_err = 0; G.epoch = 0; G.abort = 0;
   }
-  if (tid == 0) { L.bar = 0; L.myabort = 0; }
+  if (tid == 0) { L.bar = 0; L.myabort = 0; L.cpos = 0; L.cend = 0; }
   __syncthreads();
+  if (a.arena && tid == 0) arena_refill(L, G, a);
   if (wk == 0) level_costs_w(G, G.coeffs, tid);
   __syncthreads();
   if (rerun) {   // the level costs came from rstate[0..]; the probabilities are the loop-end ones
@@ -1578,7 +1771,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           }
           const uint64_t tr_f = TR_NOW();
           TR_ADD(K3TR_REFR_WAIT, tr_f - tr_w);
-          fold_rows<X>(G, L, tid, fold_from, mb, (uint32_t)y * mbw, tok_base, mboff, xs);
+          fold_rows<X>(G, L, tid, fold_from, mb, (uint32_t)y * mbw, tok_base, mboff, xs, a.arena);
           fold_from = mb;
           wbar(L);
           const uint64_t tr_r = TR_NOW();
@@ -1650,6 +1843,23 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         }
       }
       // ---- wavefront dependency: MB x+1 of the row above (top-right) is done
+#ifndef K3_NO_PRIO
+      // place in the row wavefront (issue priority below), taken by one lane
+      // before the wait so the wait's barrier hands every wave the same value
+      if constexpr (!X) {
+        if (tid == 0) {
+          int ld = 0;
+          if (y == 0 || __hip_atomic_load(&rowdone[y - 1], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP) >= mbw)
+            ld = 2;
+          else if (y == 1 || __hip_atomic_load(&rowdone[y - 2], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP) >= mbw)
+            ld = 1;
+          L.lead = ld;
+        }
+        if (y == 0) wbar(L);   // (rows > 0 pass the wait's barrier)
+      }
+#endif
       if (xr) {
         if (y > 0) {
           if (!wait_gx(G, L, &xrowdone[y - 1], min(x + 2, mbw), XH)) break;
@@ -1681,14 +1891,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         // issue priority by place in the row wavefront: a worker whose row
         // above is finished leads and gates the others (they wait on its
         // progress), so its waves win the SIMDs' issue arbitration
-        int lead = 0;
-        if (y == 0 || __hip_atomic_load(&rowdone[y - 1], __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_WORKGROUP) >= mbw)
-          lead = 2;
-        else if (y == 1 || __hip_atomic_load(&rowdone[y - 2], __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_WORKGROUP) >= mbw)
-          lead = 1;
-        lead = __builtin_amdgcn_readfirstlane(lead);
+        const int lead = __builtin_amdgcn_readfirstlane(L.lead);
 #ifndef K3_PRIO_LEAD
 #define K3_PRIO_LEAD 2
 #endif
@@ -1739,19 +1942,25 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       // ---- Intra16 (quant_enc.c:1002-1058)
       const uint64_t tr_i16 = TR_NOW();
       if constexpr (TR) {
-        if (trellis_all) eval_i16<true>(G, L, tn, S, ctx, tid);
-        else eval_i16<false>(G, L, tn, S, ctx, tid);
+        if (trellis_all) eval_i16<true>(G, L, S, ctx, tid);
+        else eval_i16<false>(G, L, S, ctx, tid);
       } else {
-        eval_i16<false>(G, L, tn, S, ctx, tid);
+        eval_i16<false>(G, L, S, ctx, tid);
       }
       TR_SINCE(K3TR_I16, tr_i16);
       int best16 = 0;
       uint32_t nz16 = 0;
       score_t D16 = 0, SD16 = 0, H16 = 0, R16 = 0;
       {
+        // IsFlatSource16 per wave (each lane checks 4 of the 256 samples): no barrier
         const int v0 = L.yin[0];
-        const int same = L.yin[(tid >> 4) * BPS + (tid & 15)] == v0;
-        int flat = wbar_and(L, same);
+        int same = 1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int p = lane + 64 * q;
+          same &= L.yin[(p >> 4) * BPS + (p & 15)] == v0;
+        }
+        int flat = __all(same);
         score_t best16_score = 0;
         for (int mm = 0; mm < 4; ++mm) {
           score_t Dm = L.mres[mm][0];
@@ -1788,7 +1997,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         mv = max(mv, iabs_(L.lvdc[best16][4]));
         if (tid == 0) atomicMax(&G.max_edge[segid], mv);
       }
-      wbar(L);
+      // the intra-4 search opens with a worker barrier, which orders the
+      // commit above before anything reads it
+      if (max_i4_bits <= 0) wbar(L);
       K3_STAMP(2);
 
       // ---- Intra4 (quant_enc.c:1072-1165)
@@ -1796,12 +2007,12 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       if (max_i4_bits > 0) {
         I4Result r4;
         if constexpr (TR) {
-          r4 = trellis_all ? run_i4<true>(G, L, tn, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
+          r4 = trellis_all ? run_i4<true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
                                           rd_score, max_i4_bits, substamps)
-                           : run_i4<false>(G, L, tn, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
+                           : run_i4<false>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
                                            rd_score, max_i4_bits, substamps);
         } else {
-          r4 = run_i4<false>(G, L, tn, S, ctx, rtid, x, mbw, predrd, yl, yt, true, rd_score,
+          r4 = run_i4<false>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true, rd_score,
                              max_i4_bits, substamps);
         }
         if (r4.ok) {
@@ -1815,7 +2026,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         } else {
           if (tid < 16) L.modes[tid] = best16;   // the aborted search wrote some
         }
-        wbar(L);
+        // (no barrier: the chroma search reads none of this, and its own
+        // barriers order it before the readers -- info, SSE, tokens)
       }
       K3_STAMP(3);
       const uint64_t tr_uv = TR_NOW();
@@ -1860,13 +2072,13 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         uint32_t nzq = 0;
         if constexpr (!TR) {
         } else if (is_i16) {
-          eval_i16<true>(G, L, tn, S, ctx, tid);
+          eval_i16<true>(G, L, S, ctx, tid);
           L.yout[(tid >> 4) * BPS + (tid & 15)] = L.rec16[best16][tid];
           (&L.fin_ac[0][0])[tid] = (&L.lv16[best16][0][0])[tid];
           if (tid < 16) L.fin_dc[tid] = L.lvdc[best16][tid];
           nzq = (uint32_t)L.mres[best16][3];
         } else {
-          I4Result r4 = run_i4<true>(G, L, tn, S, ctx, rtid, x, mbw, predrd, yl, yt, false, 0, 0,
+          I4Result r4 = run_i4<true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, false, 0, 0,
                                      substamps);
           L.yout[(tid >> 4) * BPS + (tid & 15)] = L.acc_out[tid];
           (&L.fin_ac[0][0])[tid] = (&L.acc_ac[0][0])[tid];
@@ -1933,6 +2145,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       // ---- tokens (token_enc.c:113-193) into this MB's slot; one (block,
       // zigzag position) item per thread, counts + scan + writes in parallel
       const int first_blk = is_i16 ? 0 : 1;
+      // this MB's place in the arena: read before the scan barrier below,
+      // after which thread 0 of wave 0 moves the chunk position on
+      const uint32_t tpos = a.arena ? L.cpos : 0u;
       uint64_t nzb = 0;
       int lvi[2], lvp[2];
 #pragma unroll
@@ -1950,39 +2165,29 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         if (n == 0 && k < 32) L.blast[k] = last;
       }
       wbar(L);
-      if (w0) {
-        const int k = lane;
-        const bool active = k >= first_blk && k < 25;
-        nzb = __ballot(active && L.blast[k] >= 0);
-        if (active) {
-          int my_type, my_first, my_ctx;
-          if (k == 0) {
-            my_type = 1; my_first = 0; my_ctx = ctx.top(8) + ctx.left(8);
-          } else if (k <= 16) {
-            const int b = k - 1, bx = b & 3, by = b >> 2;
-            my_type = is_i16 ? 0 : 3; my_first = is_i16 ? 1 : 0;
-            const int t = by == 0 ? ctx.top(bx) : (int)((nzb >> (k - 4)) & 1);
-            const int l = bx == 0 ? ctx.left(by) : (int)((nzb >> (k - 1)) & 1);
-            my_ctx = t + l;
-          } else {
-            const int b = k - 17, ch = b >> 2, k4 = b & 3, bx = k4 & 1, by = k4 >> 1;
-            my_type = 2; my_first = 0;
-            const int t = by == 0 ? ctx.top(4 + 2 * ch + bx) : (int)((nzb >> (k - 2)) & 1);
-            const int l = bx == 0 ? ctx.left(4 + 2 * ch + by) : (int)((nzb >> (k - 1)) & 1);
-            my_ctx = t + l;
-          }
-          L.blkinfo[k] = my_type | (my_first << 4) | (my_ctx << 8);
-        } else if (k < 32) {
-          L.blkinfo[k] = -1;
+      // every wave derives the blocks' nz bits and its items' block
+      // parameters itself (no second barrier): type | first << 4 | ctx << 8
+      nzb = __ballot(lane >= first_blk && lane < 25 && L.blast[lane] >= 0);
+      auto blk_param = [&](int k) -> int {
+        if (k < first_blk || k >= 25) return -1;
+        if (k == 0) return 1 | ((ctx.top(8) + ctx.left(8)) << 8);
+        if (k <= 16) {
+          const int b = k - 1, bx = b & 3, by = b >> 2;
+          const int t = by == 0 ? ctx.top(bx) : (int)((nzb >> (k - 4)) & 1);
+          const int l = bx == 0 ? ctx.left(by) : (int)((nzb >> (k - 1)) & 1);
+          return (is_i16 ? 0 | (1 << 4) : 3) | ((t + l) << 8);
         }
-      }
-      wbar(L);
+        const int b = k - 17, ch = b >> 2, k4 = b & 3, bx = k4 & 1, by = k4 >> 1;
+        const int t = by == 0 ? ctx.top(4 + 2 * ch + bx) : (int)((nzb >> (k - 2)) & 1);
+        const int l = bx == 0 ? ctx.left(4 + 2 * ch + by) : (int)((nzb >> (k - 1)) & 1);
+        return 2 | ((t + l) << 8);
+      };
       {
         int cnt[2], bi[2], last[2];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           const int item = rtid + K3T * q, k = item >> 4, n = item & 15;
-          bi[q] = k < 25 ? L.blkinfo[k] : -1;
+          bi[q] = blk_param(k);
           last[q] = k < 25 ? L.blast[k] : -1;
           cnt[q] = bi[q] < 0 ? 0
                              : pos_tokens<false>(bi[q] & 15, (bi[q] >> 4) & 15, bi[q] >> 8, n,
@@ -2004,7 +2209,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           if (w2 < wv) { pre0 += s0; pre1 += s1; }
           tot0 += s0; tot1 += s1;
         }
-        uint16_t* slot = tok_base + (size_t)mb * VP8G_MAX_TOKENS_PER_MB;
+        uint16_t* slot = a.arena ? a.arena + tpos : tok_base + (size_t)mb * VP8G_MAX_TOKENS_PER_MB;
         const int off0 = pre0 + inc0 - cnt[0];
         const int off1 = tot0 + pre1 + inc1 - cnt[1];
         if (cnt[0])
@@ -2013,7 +2218,15 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         if (cnt[1])
           pos_tokens<true>(bi[1] & 15, (bi[1] >> 4) & 15, bi[1] >> 8, rtid & 15, lvi[1], lvp[1],
                            last[1], slot + off1, L.rdelta);
-        if (rtid == 0) L.rowcnt[x] = (uint16_t)(tot0 + tot1);
+        if (rtid == 0) {
+          L.rowcnt[x] = (uint16_t)(tot0 + tot1);
+          if (a.arena) {
+            L.rowpos[x] = tpos;
+            a.mbpos[(size_t)f * nmb + mb] = tpos;
+            L.cpos = tpos + (uint32_t)(tot0 + tot1);
+            arena_refill(L, G, a);   // read by the next MB after the boundary barrier
+          }
+        }
       }
       K3_STAMP(5);
       TR_SINCE(K3TR_TOK, tr_tok);
@@ -2042,16 +2255,17 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         nzw[x] = word;
         L.flag_ldc = ln[8];
       }
-      wbar(L);
-      left_dc = L.flag_ldc;
 
-      // ---- boundary save (iterator_enc.c:290-313) + mode context
+      // ---- boundary save (iterator_enc.c:290-313) + mode context, in the
+      // same phase as the nz words: the left corners (yl[-1], ul[-1], vl[-1]
+      // = the row above's samples at columns 15 / 7 / 15 of this MB) are read
+      // by the threads that then overwrite those samples in ytop / uvtop
       if (x < mbw - 1) {
         if (tid < 16) yl[tid] = L.yout[15 + tid * BPS];
         if (tid < 8) { ul[tid] = L.yout[16 + 7 + tid * BPS]; vl[tid] = L.yout[24 + 7 + tid * BPS]; }
-        if (tid == 0) { yl[-1] = yt[15]; ul[-1] = uvt[7]; vl[-1] = uvt[15]; }
+        if (tid == 15) { yl[-1] = yt[15]; vl[-1] = uvt[15]; }
+        if (tid == 7) ul[-1] = uvt[7];
       }
-      wbar(L);
       if (y < mbh - 1) {
         if (tid < 16) {
           ytop[16 * x + tid] = L.yout[15 * BPS + tid];
@@ -2063,6 +2277,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         L.predleft[tid] = L.modes[4 * tid + 3];
       }
       wbar(L);
+      left_dc = L.flag_ldc;
       if (tid == 0) publish(&rowdone[y], x + 1);
       if constexpr (X) {
         // the last worker's row feeds worker 0 of the next workgroup: its
@@ -2095,7 +2310,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     const uint64_t tr_ff = TR_NOW();
     TR_ADD(K3TR_FOLD_WAIT, tr_ff - tr_fw);
     fold_rows<X>(G, L, tid, fold_from, (uint32_t)(y + 1) * mbw, (uint32_t)y * mbw, tok_base,
-                 mboff, xs);
+                 mboff, xs, a.arena);
     TR_SINCE(K3TR_FOLD, tr_ff);
     report_rows<X>(G, L, P, tid, (uint32_t)(y + 1) * mbw, mbw, XH);
     wbar(L);
@@ -2123,10 +2338,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     }
     return;
   }
-  if (!G.abort && !G.tok_err) compact_tokens(G, tok_base, mboff, nmb);
+  if (!a.arena && !G.abort && !G.tok_err) compact_tokens(G, tok_base, mboff, nmb);
   __syncthreads();
   if (wk == 0) {
-    for (int s = tid; s < NSLOT; s += K3T) {
+    for (int s = tid; s < NSLOT && !(G.tok_err & VP8G_ERR_ARENA); s += K3T) {
       rstate[NSLOT + s] = G.coeffs[s];
       rstats[s] = G.stats[s];
     }
@@ -2191,9 +2406,9 @@ __global__ __launch_bounds__(K3T) void k_encode_xtail(K3Args a) {
   }
   __syncthreads();
   const int err = XH->uabort ? 2 | (6 << 4) : XH->abort ? 2 : XH->tok_err;
-  if (!err) compact_tokens(G, tok_base, mboff, nmb);
+  if (!err && !a.arena) compact_tokens(G, tok_base, mboff, nmb);
   __syncthreads();
-  for (int s = tid; s < NSLOT; s += K3T) {
+  for (int s = tid; s < NSLOT && !(XH->tok_err & VP8G_ERR_ARENA); s += K3T) {
     if (lcver > 0) rstate[s] = xs[XS_LCOEFFS + s];   // the level costs' probabilities
     rstate[NSLOT + s] = G.coeffs[s];
     rstats[s] = G.stats[s];
@@ -2220,8 +2435,9 @@ __global__ __launch_bounds__(K3T) void k_encode_xtail(K3Args a) {
 
 template <int NW>
 static size_t k3_lds_bytes(int mbw, int mbh, bool trellis, size_t pad = 0) {
+  (void)trellis;   // (the trellis keeps its nodes in registers: no LDS of its own)
   return sizeof(K3G) + pad + NW * sizeof(K3S) + (16 * mbw + 16) + 16 * mbw + 4 * (mbw + 1) + 4 * mbw +
-         4 * mbw + 4 * mbh + (trellis ? (size_t)NW * 64 * 32 * 4 : 0) + 16;
+         4 * mbw + 4 * mbh + 16;
 }
 
 #ifdef WEBP_AMD_DIAG
@@ -2377,7 +2593,139 @@ static int launch_k3_default(const K3Args& a, int n, bool trellis, bool af, void
                  : launch_k3_t<3, false>(a, n, false, stream);
 }
 
+// The frames' compact token streams from the arena (K3Args::arena): frame f's
+// stream at tokens + f * tok_cap in raster MB order, each MB's run of tokens
+// moved by one wave from arena + mbpos to its compact offset (mboff, the
+// frame's statistics fold computed it); the last MB ends at the frame's
+// token count. Frames that were not encoded by the launch (pass_mode 2),
+// failed, or do not fit tok_cap are left alone (the host checks the counts).
+__global__ __launch_bounds__(256) void k_gather_tokens(uint16_t* __restrict__ tokens,
+                                                       size_t tok_cap,
+                                                       const uint16_t* __restrict__ arena,
+                                                       const uint32_t* __restrict__ mbpos,
+                                                       const uint32_t* __restrict__ mboff, int nmb,
+                                                       const vp8g_frame_params* __restrict__ params,
+                                                       const vp8g_frame_result* __restrict__ results) {
+  const int f = blockIdx.y, ln = threadIdx.x & 63;
+  const int mb = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (mb >= nmb || params[f].pass_mode == 2) return;
+  const vp8g_frame_result* R = results + f;
+  const uint32_t ntok = R->ntokens;
+  if (R->error || ntok > tok_cap) return;
+  const size_t fm = (size_t)f * nmb;
+  const uint32_t d = mboff[fm + mb];
+  const uint32_t e = mb + 1 < nmb ? mboff[fm + mb + 1] : ntok;
+  const uint16_t* src = arena + mbpos[fm + mb];
+  uint16_t* dst = tokens + (size_t)f * tok_cap + d;
+  const uint32_t n = e - d;
+  uint32_t c = ln;
+  for (; c + 192 < n; c += 256) {   // four loads in flight per lane
+    const uint16_t t0 = src[c], t1 = src[c + 64], t2 = src[c + 128], t3 = src[c + 192];
+    dst[c] = t0; dst[c + 64] = t1; dst[c + 128] = t2; dst[c + 192] = t3;
+  }
+  for (; c < n; c += 64) dst[c] = src[c];
+}
+
+extern "C" int vp8g_launch_gather(uint16_t* tokens, size_t tok_cap, const uint16_t* arena,
+                                  const uint32_t* mbpos, const uint32_t* mboff, int w, int h, int n,
+                                  const vp8g_frame_params* params,
+                                  const vp8g_frame_result* results, void* stream) {
+  const int nmb = ((w + 15) >> 4) * ((h + 15) >> 4);
+  hipLaunchKernelGGL(k_gather_tokens, dim3((nmb + 3) / 4, n), dim3(256), 0, (hipStream_t)stream,
+                     tokens, tok_cap, arena, mbpos, mboff, nmb, params, results);
+  return vp8g_launch_check("k_gather_tokens");
+}
+
 #ifdef K3_TRACE
+// diagnostic build: trellis16 against the serial trellis_quant on random
+// blocks (one wave; its 4 groups take 4 blocks per iteration) with random
+// cost tables. out[0] = mismatching blocks, out[1] = blocks, out[2..] = the
+// first mismatch (type, ctx0, lambda, coefficients, both level vectors).
+__global__ __launch_bounds__(64) void k_trellis_selftest(int iters, uint32_t seed, int* out) {
+  __shared__ K3G G;
+  __shared__ uint32_t nodes[4][32];
+  __shared__ int16_t lvs[4][16];
+  __shared__ int cs[4][16];
+  __shared__ long long dbg[64 * 16];
+  const int lane = threadIdx.x, g = lane & 48, j = lane & 15, grp = lane >> 4;
+  auto rnd = [](uint32_t& st) {
+    st ^= st << 13; st ^= st >> 17; st ^= st << 5;
+    return st;
+  };
+  uint32_t st = seed * 747796405u + lane * 2891336453u + 1u;
+  for (int k = lane; k < 256; k += 64) G.ecost[k] = kVP8EntropyCost[k];
+  for (int it = 0; it < iters; ++it) {
+    // fresh tables every 64 iterations: level costs, probabilities, matrix
+    if ((it & 63) == 0) {
+      for (int k = lane; k < 96 * (MAX_VLEVEL + 1); k += 64)
+        (&G.lcost[0][0])[k] = (uint16_t)(rnd(st) % 3000);
+      for (int k = lane; k < NSLOT; k += 64) G.coeffs[k] = (uint8_t)(1 + rnd(st) % 255);
+      if (lane < 16) {
+        const int q = 4 + (int)(rnd(st) % 120);
+        G.seg[0].y1.q[lane] = (uint16_t)q;
+        G.seg[0].y1.iq[lane] = (uint16_t)((1 << QFIX) / q);
+        G.seg[0].y1.sharpen[lane] = (uint16_t)(rnd(st) % 16);
+      }
+      __syncthreads();
+    }
+    const vp8g_mtx& M = G.seg[0].y1;
+    const uint32_t ru = __shfl(rnd(st), g);
+    const int type = (int)((ru >> 3) & 3), ctx0 = (int)(ru % 3);
+    const int lambda = 1 + (int)((ru >> 8) % 4000);
+    const int mag = 1 << (2 + (ru >> 20) % 10);
+    const uint32_t r2 = rnd(st);
+    int c = (r2 & 1) ? (int)(r2 % (2 * mag)) - mag : 0;
+    c = max(-2048, min(2047, c));
+    cs[grp][j] = c;
+    __syncthreads();
+    const Trellis16 t = trellis16<true>(G, c, true, ctx0, type, M, lambda, dbg);
+    int ref_lv = 0;
+    if (j == 0) {
+      int cc[16];
+      for (int k = 0; k < 16; ++k) cc[k] = cs[grp][k];
+      trellis_quant(G, nodes[grp], cc, lvs[grp], ctx0, type, &M, lambda);
+    }
+    __syncthreads();
+    ref_lv = lvs[grp][j];
+    if (type == 0 && j == 0) ref_lv = 0;   // position 0 is left to the caller
+    const uint64_t bad = __ballot(ref_lv != t.lvz);
+    __shared__ int first_bad;
+    if (lane == 0) {
+      first_bad = -1;
+      for (int q = 0; q < 4; ++q) {
+        atomicAdd(&out[1], 1);
+        if ((bad >> (16 * q)) & 0xffff) {
+          if (atomicAdd(&out[0], 1) == 0) {
+            out[2] = q; out[3] = type; out[4] = ctx0; out[5] = lambda; out[6] = it;
+            first_bad = q;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (grp == first_bad) {
+      out[8 + j] = c; out[24 + j] = ref_lv; out[40 + j] = t.lvz;
+      out[56 + j] = G.seg[0].y1.q[j]; out[72 + j] = G.seg[0].y1.sharpen[j];
+      for (int k = 0; k < 32; k += 1) out[96 + 32 * 0 + k] = (int)nodes[grp][k];   // same for all lanes
+      long long* o = (long long*)(out + 128);
+      for (int k = 0; k < 16; ++k) o[16 * j + k] = dbg[16 * lane + k];
+    }
+    __syncthreads();
+  }
+}
+
+extern "C" __attribute__((visibility("default"))) int vp8g_trellis_selftest(int iters,
+                                                                            unsigned seed,
+                                                                            int* host_out) {
+  int* d = nullptr;
+  if (hipMalloc(&d, 1024 * sizeof(int)) != hipSuccess) return 0;
+  (void)hipMemset(d, 0, 1024 * sizeof(int));
+  hipLaunchKernelGGL(k_trellis_selftest, dim3(1), dim3(64), 0, 0, iters, seed, d);
+  const int ok = hipMemcpy(host_out, d, 1024 * sizeof(int), hipMemcpyDeviceToHost) == hipSuccess;
+  (void)hipFree(d);
+  return ok;
+}
+
 // diagnostic build: the per-worker K3TR_* counters of the last launch,
 // out[block][worker][slot] for the first nblocks workgroups
 extern "C" __attribute__((visibility("default"))) int vp8g_k3_trace(unsigned long long* out,
@@ -2396,7 +2744,7 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
                                   uint16_t* tokens, size_t tok_cap, uint8_t* mbinfo,
                                   uint32_t* mboff, int trellis, vp8g_frame_result* results,
                                   uint8_t* rerun_state, uint8_t* recon, uint8_t* xsync,
-                                  void* stream) {
+                                  const vp8g_arena* arena, void* stream) {
 #ifdef WEBP_AMD_DIAG
   // diagnostic build only (make diag -> libwebp_amd_diag.so; the product
   // library has no switch): WEBP_AMD_K3 = 1 single-wavefront twin,
@@ -2427,6 +2775,17 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   a.segmap = segmap; a.params = params; a.tokens = tokens; a.tok_cap = tok_cap;
   a.mbinfo = mbinfo; a.mboff = mboff; a.results = results; a.rerun = rerun_state;
   a.xs = xsync; a.xs_fb = vp8g_xsync_bytes(w, h); a.nwg = 1;
+  a.arena = nullptr; a.arena_cap = 0; a.arena_top = nullptr; a.mbpos = nullptr;
+  if (arena) {   // one arena per launch: the bump pointer starts at 0
+    a.arena = arena->tokens;
+    a.arena_cap = arena->cap;
+    a.arena_top = arena->top;
+    a.mbpos = arena->mbpos;
+    if (hipMemsetAsync(arena->top, 0, sizeof(uint32_t), (hipStream_t)stream) != hipSuccess) {
+      vp8g_set_error("k_encode", "arena reset failed");
+      return 0;
+    }
+  }
   if (xsync != nullptr && recon == nullptr && variant == 0) {
     const int nwg = k3x_take(n, a.mbh, 2);
     if (nwg > 1)

@@ -112,7 +112,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   b->uvw = (width + 1) >> 1; b->uvh = (height + 1) >> 1;
   b->yfb = (size_t)width * height + 2 * (size_t)b->uvw * b->uvh;
   b->yfb = (b->yfb + 255) & ~(size_t)255;
-  b->tok_cap = (size_t)b->nmb * VP8G_MAX_TOKENS_PER_MB;
+  b->tok_cap = 0;   /* d_tokens: sized per run (tokens_for_run) */
   b->sharp = vp8h_use_sharp(config, width, height);
   b->dither = b->sharp ? 0.f : vp8h_import_dithering(config);
   b->threads = host_threads > 0 ? host_threads : default_threads(device);
@@ -141,7 +141,6 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   CHK(hipMalloc((void**)&b->d_amode, N * nmb));
   CHK(hipMalloc((void**)&b->d_segmap, N * nmb));
   CHK(hipMalloc((void**)&b->d_params, N * sizeof(vp8g_frame_params)));
-  CHK(hipMalloc((void**)&b->d_tokens, N * b->tok_cap * sizeof(uint16_t)));
   CHK(hipMalloc((void**)&b->d_mbinfo, N * nmb * VP8G_MBINFO_BYTES));
   CHK(hipMalloc((void**)&b->d_mboff, N * nmb * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&b->d_rerun, N * VP8G_RERUN_STATE_BYTES));
@@ -193,6 +192,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   if (b->stream) hipStreamSynchronize(b->stream);
   hipFree(b->d_g2l); hipFree(b->d_rgba); hipFree(b->d_yuv); hipFree(b->d_aflags); hipFree(b->d_alpha);
   hipFree(b->d_uva); hipFree(b->d_amode); hipFree(b->d_segmap); hipFree(b->d_params); hipFree(b->d_tokens);
+  hipFree(b->d_arena); hipFree(b->d_arena_top); hipFree(b->d_mbpos); hipFree(b->d_rerun_snap);
   hipFree(b->d_mbinfo); hipFree(b->d_mboff); hipFree(b->d_rerun); hipFree(b->d_xsync); hipFree(b->d_results); hipFree(b->d_psize); hipFree(b->d_emeta);
   hipFree(b->d_poff); hipFree(b->d_part); hipFree(b->d_pinfo);
   hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs); hipFree(b->d_nbuf);
@@ -453,6 +453,137 @@ fail:
   return 0;
 }
 
+/* ---- token buffers ----------------------------------------------------
+ * The token loop (methods 3-6 without low_memory) runs K3 with an arena:
+ * every MB's tokens are written once, k_gather_tokens lays out each frame's
+ * compact stream at d_tokens + f * tok_cap, and tok_cap follows the largest
+ * stream seen. The other paths (methods 0-2, low_memory, VP8EncLoop's
+ * searches) keep per-MB slots of the worst case VP8G_MAX_TOKENS_PER_MB. */
+static int arena_mode(const WebPGpuBatch* b) {
+  return b->cfg.method >= 3 && !b->cfg.low_memory;
+}
+
+/* d_tokens with a stride of at least cap tokens per frame (grows only) */
+static int ensure_tok_cap(WebPGpuBatch* b, size_t cap) {
+  cap = (cap + 255) & ~(size_t)255;
+  if (b->d_tokens && b->tok_cap >= cap) return 1;
+  hipFree(b->d_tokens);
+  b->d_tokens = NULL;
+  b->tok_cap = 0;
+  CHK(hipMalloc((void**)&b->d_tokens, (size_t)b->max_frames * cap * sizeof(uint16_t)));
+  b->tok_cap = cap;
+  return 1;
+fail:
+  return 0;
+}
+
+/* the arena with at least cap tokens (grows only; u32 positions) */
+static int ensure_arena(WebPGpuBatch* b, size_t cap) {
+  const size_t lim = 0xfff00000u - VP8G_MAX_TOKENS_PER_MB;
+  if (cap > lim) cap = lim;
+  if (b->d_arena && b->arena_cap >= cap) return 1;
+  hipFree(b->d_arena);
+  b->d_arena = NULL;
+  b->arena_cap = 0;
+  CHK(hipMalloc((void**)&b->d_arena, (cap + VP8G_MAX_TOKENS_PER_MB) * sizeof(uint16_t)));
+  b->arena_cap = cap;
+  if (!b->d_arena_top) {
+    const size_t N = (size_t)b->max_frames;
+    CHK(hipMalloc((void**)&b->d_arena_top, sizeof(uint32_t)));
+    CHK(hipMalloc((void**)&b->d_mbpos, N * b->nmb * sizeof(uint32_t)));
+    CHK(hipMalloc((void**)&b->d_rerun_snap, N * VP8G_RERUN_STATE_BYTES));
+  }
+  return 1;
+fail:
+  return 0;
+}
+
+/* the token buffers of this run's path (before K3's first launch) */
+static int tokens_for_run(WebPGpuBatch* b) {
+  const size_t nmb = (size_t)b->nmb;
+  if (!arena_mode(b)) return ensure_tok_cap(b, nmb * VP8G_MAX_TOKENS_PER_MB);
+  /* ~1.2x the tokens of a -q 75 frame of natural content per MB to start
+   * with, and room for every worker's partly used last chunk */
+  return ensure_tok_cap(b, nmb * 1536 + 4096) &&
+         ensure_arena(b, (size_t)b->max_frames * nmb * 1024 + 768 * (size_t)VP8G_ARENA_CHUNK);
+}
+
+/* K3 over the frames of h_params (already on the device), then the gather in
+ * arena mode. The caller copies the results back and calls k3_settle. */
+static int launch_k3(WebPGpuBatch* b, int n, uint8_t* recon) {
+  hipStream_t st = b->stream;
+  vp8g_arena A, *ap = NULL;
+  if (arena_mode(b)) {
+    int reread = 0;   /* a pass that starts from d_rerun: keep a copy for a re-run */
+    for (int f = 0; f < n; ++f)
+      reread |= b->h_params[f].pass_mode == 1 || b->h_params[f].pass_mode == 3;
+    if (reread)
+      CHK(hipMemcpyAsync(b->d_rerun_snap, b->d_rerun, (size_t)n * VP8G_RERUN_STATE_BYTES,
+                         hipMemcpyDeviceToDevice, st));
+    A.tokens = b->d_arena;
+    A.cap = (uint32_t)b->arena_cap;
+    A.top = b->d_arena_top;
+    A.mbpos = b->d_mbpos;
+    ap = &A;
+  }
+  if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
+                          b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5, b->d_results,
+                          b->d_rerun, recon, b->d_xsync, ap, st))
+    return 0;
+  if (ap && !vp8g_launch_gather(b->d_tokens, b->tok_cap, b->d_arena, b->d_mbpos, b->d_mboff, b->w,
+                                b->h, n, b->d_params, b->d_results, st))
+    return 0;
+  return 1;
+fail:
+  return 0;
+}
+
+/* after launch_k3 and the results' copy to h_results (stream drained): a
+ * launch whose arena ran out runs again with twice the arena (from the
+ * saved d_rerun); streams longer than tok_cap are gathered again into a
+ * wider d_tokens. Returns 2 when K3 ran again (d_rerun changed), 1 else. */
+static int k3_settle(WebPGpuBatch* b, int n, uint8_t* recon) {
+  if (!arena_mode(b)) return 1;
+  hipStream_t st = b->stream;
+  int rerun = 0;
+  for (int tries = 0;; ++tries) {
+    int over = 0;
+    size_t longest = 0;
+    for (int f = 0; f < n; ++f) {
+      const vp8g_frame_result* R = &b->h_results[f];
+      if (b->h_params[f].pass_mode == 2) continue;
+      if (R->error & VP8G_ERR_ARENA) over = 1;
+      else if (!R->error && R->ntokens > longest) longest = R->ntokens;
+    }
+    if (over) {
+      if (tries > 6 || !ensure_arena(b, 2 * b->arena_cap)) {
+        vp8g_set_error("k_encode", "token arena cannot grow");
+        return 0;
+      }
+      int reread = 0;
+      for (int f = 0; f < n; ++f)
+        reread |= b->h_params[f].pass_mode == 1 || b->h_params[f].pass_mode == 3;
+      if (reread)
+        CHK(hipMemcpyAsync(b->d_rerun, b->d_rerun_snap, (size_t)n * VP8G_RERUN_STATE_BYTES,
+                           hipMemcpyDeviceToDevice, st));
+      if (!launch_k3(b, n, recon)) return 0;
+      rerun = 1;
+    } else if (longest + 64 > b->tok_cap) {
+      if (!ensure_tok_cap(b, longest + longest / 4 + 64) ||
+          !vp8g_launch_gather(b->d_tokens, b->tok_cap, b->d_arena, b->d_mbpos, b->d_mboff, b->w,
+                              b->h, n, b->d_params, b->d_results, st))
+        return 0;
+    } else {
+      return rerun ? 2 : 1;
+    }
+    CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
+                       hipMemcpyDeviceToHost, st));
+    CHK(hipStreamSynchronize(st));
+  }
+fail:
+  return 0;
+}
+
 /* VP8AdjustFilterStrength reads dqm->max_edge_, which StoreMaxDelta raises in
  * every RD_OPT_BASIC decision since the last SetupMatrices: the last StatLoop
  * pass and the final pass share one set of segment parameters, so the final
@@ -524,7 +655,7 @@ static int lowmem_passes(WebPGpuBatch* b, int n) {
     first = 0;
     if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params,
                             b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5,
-                            b->d_results, b->d_rerun, NULL, b->d_xsync, st))
+                            b->d_results, b->d_rerun, NULL, b->d_xsync, NULL, st))
       return 0;
     if (!vp8g_launch_lowmem(b->d_tokens, b->tok_cap, b->d_mboff, b->d_results, b->d_mbinfo,
                             (int)nmb, n, b->d_lmi, b->d_active, 0, b->d_lmstats, b->d_lmi + N, st))
@@ -535,7 +666,7 @@ static int lowmem_passes(WebPGpuBatch* b, int n) {
     if (probe)
       CHK(hipMemcpyAsync(b->h_mbinfo, b->d_mbinfo, n * nmb * VP8G_MBINFO_BYTES,
                          hipMemcpyDeviceToHost, st));
-    CHK(hipStreamSynchronize(st));
+    CHK(engine_wait(b, st));   /* per-row progress and the hook's abort */
     for (int f = 0; f < n; ++f) {
       if (!act[f]) continue;
       vp8h_frame* fr = &b->frames[f];
@@ -590,12 +721,12 @@ static int lowmem_passes(WebPGpuBatch* b, int n) {
                      hipMemcpyHostToDevice, st));
   if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
                           b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5, b->d_results,
-                          b->d_rerun, b->cfg.autofilter ? b->d_recon : NULL, b->d_xsync, st))
+                          b->d_rerun, b->cfg.autofilter ? b->d_recon : NULL, b->d_xsync, NULL, st))
     return 0;
   CHK(hipEventRecord(b->ev[3], st));
   CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
                      hipMemcpyDeviceToHost, st));
-  CHK(hipStreamSynchronize(st));
+  CHK(engine_wait(b, st));   /* per-row progress and the hook's abort */
   /* the emitted probabilities are StatLoop's, not the final pass's */
   for (int f = 0; f < n; ++f) {
     if (b->h_params[f].pass_mode != 1 || b->h_results[f].error) continue;
@@ -695,7 +826,7 @@ static int statloop_search(WebPGpuBatch* b, int n) {
     /* RD_OPT_BASIC: the instantiation without trellis paths (it sums R + H) */
     if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params,
                             b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff, 0,
-                            b->d_results, b->d_rerun, NULL, b->d_xsync, st))
+                            b->d_results, b->d_rerun, NULL, b->d_xsync, NULL, st))
       return 0;
     if (!vp8g_launch_lowmem(b->d_tokens, b->tok_cap, b->d_mboff, b->d_results, b->d_mbinfo,
                             (int)nmb, n, b->d_lmi, b->d_active, 0, b->d_lmstats, b->d_lmi + N, st))
@@ -705,7 +836,7 @@ static int statloop_search(WebPGpuBatch* b, int n) {
     CHK(hipMemcpyAsync(b->h_lmstats, b->d_lmstats, n * VP8G_NUM_SLOTS * sizeof(uint32_t),
                        hipMemcpyDeviceToHost, st));
     CHK(hipMemcpyAsync(h_nskip, b->d_lmi + N, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    CHK(hipStreamSynchronize(st));
+    CHK(engine_wait(b, st));   /* per-row progress and the hook's abort */
     for (int f = 0; f < n; ++f) {
       if (!act[f]) continue;
       vp8h_frame* fr = &b->frames[f];
@@ -803,12 +934,12 @@ static int statloop_search(WebPGpuBatch* b, int n) {
   }
   if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
                           b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5, b->d_results,
-                          b->d_rerun, b->cfg.autofilter ? b->d_recon : NULL, b->d_xsync, st))
+                          b->d_rerun, b->cfg.autofilter ? b->d_recon : NULL, b->d_xsync, NULL, st))
     return 0;
   CHK(hipEventRecord(b->ev[3], st));
   CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
                      hipMemcpyDeviceToHost, st));
-  CHK(hipStreamSynchronize(st));
+  CHK(engine_wait(b, st));   /* per-row progress and the hook's abort */
   for (int f = 0; f < n; ++f) {   /* the emitted probabilities are StatLoop's */
     if (b->h_params[f].pass_mode != 1 || b->h_results[f].error) continue;
     vp8g_frame_result* R = &b->h_results[f];
@@ -901,10 +1032,7 @@ static int run_passes(WebPGpuBatch* b, int n) {
                                    b->d_params, b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff,
                                    b->d_results, b->d_rerun, st))
         return 0;
-    } else if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params,
-                                   b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff,
-                                   b->cfg.method >= 5, b->d_results, b->d_rerun,
-                                   af ? b->d_recon : NULL, b->d_xsync, st)) {
+    } else if (!launch_k3(b, n, af ? b->d_recon : NULL)) {   /* the token loop */
       return 0;
     }
     CHK(hipEventRecord(b->ev[3], st));
@@ -926,6 +1054,13 @@ static int run_passes(WebPGpuBatch* b, int n) {
                          hipMemcpyDeviceToHost, st));
     }
     CHK(engine_wait(b, st));
+    if (b->cfg.method >= 3) {
+      const int rc = k3_settle(b, n, af ? b->d_recon : NULL);
+      if (!rc) return 0;
+      if (rc == 2 && nsize)   /* K3 ran again: the state the size search reads */
+        CHK(hipMemcpy(b->h_state, b->d_rerun, (size_t)n * VP8G_RERUN_STATE_BYTES,
+                      hipMemcpyDeviceToHost));
+    }
     if (nsize) {   /* FinalizeTokenProbas, then VP8EstimateTokenSize on the device */
       for (int f = 0; f < n; ++f) {
         vp8h_frame* fr = &b->frames[f];
@@ -1007,6 +1142,7 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   TailJob head;
   int head_running = 0;
   b->timings[9] = 0;
+  if (!tokens_for_run(b)) return 0;
   if (!encode_alpha(b, n)) return 0;
   if (!b->ev0_recorded) CHK(hipEventRecord(b->ev[0], st));
   b->ev0_recorded = 0;
@@ -1278,6 +1414,16 @@ int WebPGpuBatchEncodeRGBA(WebPGpuBatch* b, const void* rgba_dev, size_t fstride
   return run_rgba(b, rgba_dev, fstride, rstride, n, stream);
 }
 
+/* host memory the DMA engines can read directly (page-locked by HIP) */
+static int host_is_pinned(const void* p) {
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();   /* an unregistered pointer reports an error: clear it */
+    return 0;
+  }
+  return at.type == hipMemoryTypeHost;
+}
+
 int WebPGpuBatchEncodeRGBAHost(WebPGpuBatch* b, const uint8_t* rgba, size_t fstride, int rstride,
                                int n) {
   if (!b || !rgba || n <= 0 || n > b->max_frames || rstride < 4 * b->w) return 0;
@@ -1291,11 +1437,19 @@ int WebPGpuBatchEncodeRGBAHost(WebPGpuBatch* b, const uint8_t* rgba, size_t fstr
     CHK(hipMalloc((void**)&b->d_rgba, need));
     b->d_rgba_cap = need;
   }
-  /* the caller's buffer is pageable: an async copy of it on our
-   * non-blocking stream is not safe on this platform (the runtime may read
-   * it from the GPU directly), so drain the stream and copy synchronously */
-  CHK(hipStreamSynchronize(b->stream));
-  CHK(hipMemcpy(b->d_rgba, rgba, need, hipMemcpyHostToDevice));
+  if (host_is_pinned(rgba)) {
+    /* page-locked (hipHostMalloc / hipHostRegister): the upload is one DMA
+       copy on the engine's own stream, ahead of K1 in stream order -- it runs
+       beside the other engines' kernels, and no second stream has to share a
+       hardware queue with a running K3 (whose queue would hold it back) */
+    CHK(hipMemcpyAsync(b->d_rgba, rgba, need, hipMemcpyHostToDevice, b->stream));
+  } else {
+    /* pageable: an async copy of it on our non-blocking stream is not safe
+       on this platform (the runtime may read it from the GPU directly), so
+       drain the stream and copy synchronously */
+    CHK(hipStreamSynchronize(b->stream));
+    CHK(hipMemcpy(b->d_rgba, rgba, need, hipMemcpyHostToDevice));
+  }
   return run_rgba(b, b->d_rgba, fstride, rstride, n, NULL);
 fail:
   return 0;

@@ -48,7 +48,15 @@ struct WebPGpuBatch {
   uint16_t* d_uva;
   uint8_t* d_segmap;
   vp8g_frame_params* d_params;
-  uint16_t* d_tokens;
+  uint16_t* d_tokens;         /* per-frame compact streams, stride tok_cap tokens */
+  /* token arena of the token loop (methods 3-6 without low_memory): K3
+   * writes each MB's tokens once into it and k_gather_tokens lays out the
+   * streams (allocated on first use, grown when a launch runs out) */
+  uint16_t* d_arena;
+  size_t arena_cap;          /* tokens (a sink of VP8G_MAX_TOKENS_PER_MB follows) */
+  uint32_t* d_arena_top;
+  uint32_t* d_mbpos;
+  uint8_t* d_rerun_snap;     /* d_rerun before a pass that re-reads it (arena re-runs) */
   uint8_t* d_mbinfo;
   uint32_t* d_mboff;         /* K3 scratch: compact-stream offset per MB */
   uint8_t* d_rerun;          /* K3 cost state carried from pass to pass */

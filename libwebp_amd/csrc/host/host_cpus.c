@@ -84,15 +84,20 @@ static void compute(int device, DevCpus* d) {
   for (int c = 0; c < CPU_SETSIZE; ++c)
     if (CPU_ISSET(c, &nodeset) && CPU_ISSET(c, &mine)) cpus[n++] = c;
   if (n == 0) return;
-  /* ranks on this node: devices 0 .. local_world-1 in use, one rank each */
+  /* ranks on this node: local rank k drives device k mod the device count
+   * (one rank per GPU, or every rank on one GPU in a one-GPU test); this
+   * process's slot comes from LOCAL_RANK when the launcher sets it, else
+   * from the device index */
   int ndev = 0, ranks = 1, idx = 0;
   const char* lw = getenv("LOCAL_WORLD_SIZE");
+  const char* lr = getenv("LOCAL_RANK");
   const int local_world = lw ? atoi(lw) : 1;
-  if (local_world > 1 && hipGetDeviceCount(&ndev) == hipSuccess) {
+  const int local_rank = lr ? atoi(lr) : device;
+  if (local_world > 1 && hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0) {
     ranks = 0;
-    for (int k = 0; k < ndev && k < local_world; ++k) {
-      if (device_numa_node(k) != node) continue;
-      if (k < device) ++idx;
+    for (int k = 0; k < local_world; ++k) {
+      if (device_numa_node(k % ndev) != node) continue;
+      if (k < local_rank) ++idx;
       ++ranks;
     }
     if (ranks < 1) ranks = 1;

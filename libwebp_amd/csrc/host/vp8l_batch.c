@@ -73,6 +73,7 @@ static vp8l_engine* engine_alloc(const vp8l_params* p, int max_frames, int metho
   l->p = *p;
   const int w = p->w, h = p->h;
   l->method = method;
+  if (hipGetDevice(&l->device) != hipSuccess) l->device = 0;
   l->max_frames = max_frames;
   l->npix = (size_t)w * h;
   l->ntt = sub_sample(w, l->p.tb) * sub_sample(h, l->p.tb);
@@ -267,10 +268,8 @@ static void run_headers(vp8l_engine* l, int n, int threads) {
   pthread_t th[64];
   int started = 0;
   if (threads > 64) threads = 64;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-  for (int i = 0; i < threads - 1 && i < n - 1; ++i)   /* on the GPU's NUMA node */
-    if (vp8g_thread_create(&th[started], hdr_worker, &job, dev) == 0) ++started;
+  for (int i = 0; i < threads - 1 && i < n - 1; ++i)   /* on the engine GPU's NUMA node */
+    if (vp8g_thread_create(&th[started], hdr_worker, &job, l->device) == 0) ++started;
   hdr_worker(&job);
   for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
 }

@@ -102,6 +102,7 @@ typedef struct vp8l_engine {
   /* colour-indexed engines: the cost-model parse's buffers (vp8l_gpu.h) */
   vp8l_lz lz;
   uint8_t* d_dcodes;
+  int device;   /* the HIP device current at creation (host threads' NUMA node) */
 } vp8l_engine;
 
 #ifdef __cplusplus

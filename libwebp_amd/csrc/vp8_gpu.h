@@ -27,6 +27,11 @@ extern "C" {
 #define VP8G_NUM_SLOTS 1056        /* 4 types x 8 bands x 3 ctx x 11 probas */
 #define VP8G_MBINFO_BYTES 20       /* type, uv_mode, segment, skip, modes[16] */
 #define VP8G_MAX_TOKENS_PER_MB 7680 /* 25 blocks x 16 coeffs x 19 tokens + EOBs */
+/* token arena (K3 with an arena): tokens per chunk a worker takes at a time,
+ * and the frame error bit of a launch whose arena ran out (the host grows the
+ * arena and runs the pass again) */
+#define VP8G_ARENA_CHUNK (128 * 1024)
+#define VP8G_ERR_ARENA 0x100
 
 /* one quantiser matrix, src/enc/vp8i_enc.h:181-187 */
 typedef struct {
@@ -143,12 +148,32 @@ int vp8g_launch_analysis(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int 
  * each MB's reconstruction in the 32-byte-stride layout of the reference's
  * yuv_out_ (Y | U | V side by side, src/enc/vp8i_enc.h:72-78) for the
  * autofilter. */
+/* the token arena of a K3 launch (see vp8g_launch_encode): cap tokens plus
+ * a sink of VP8G_MAX_TOKENS_PER_MB behind them, the bump pointer (reset by
+ * the launch) and n x nmb MB positions */
+typedef struct {
+  uint16_t* tokens;
+  uint32_t cap;
+  uint32_t* top;
+  uint32_t* mbpos;
+} vp8g_arena;
+
 int vp8g_launch_encode(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h,
                        int n, const uint8_t* segmap,
                        const vp8g_frame_params* params, uint16_t* tokens,
                        size_t tok_cap, uint8_t* mbinfo, uint32_t* mboff, int trellis,
                        vp8g_frame_result* results, uint8_t* rerun_state, uint8_t* recon,
-                       uint8_t* xsync, void* stream);
+                       uint8_t* xsync, const vp8g_arena* arena, void* stream);
+
+/* With an arena, K3 writes every MB's tokens once into the arena and the
+ * frames' compact streams are laid out by this gather (frame f at tokens +
+ * f * tok_cap; frames with ntokens > tok_cap, errors or pass_mode 2 are
+ * skipped). Without one, K3 writes per-MB slots of VP8G_MAX_TOKENS_PER_MB and
+ * compacts each frame's stream itself. */
+int vp8g_launch_gather(uint16_t* tokens, size_t tok_cap, const uint16_t* arena,
+                       const uint32_t* mbpos, const uint32_t* mboff, int w, int h, int n,
+                       const vp8g_frame_params* params, const vp8g_frame_result* results,
+                       void* stream);
 
 /* K3X: when a launch has few frames (n <= VP8G_XSPLIT_MAX_FRAMES) and xsync
  * is not NULL, each frame's MB rows are split over several workgroups (CUs)

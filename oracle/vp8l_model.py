@@ -1721,7 +1721,7 @@ AUTO_CACHE = -1
 
 
 def encode(rgba, method=4, cache_bits=AUTO_CACHE, kmax=KMAX, return_parts=False,
-           alpha_plane=False, emode=None, near_lossless_q=100, exact=False):
+           alpha_plane=False, emode=None, near_lossless_q=100, exact=False, lz_parse=None):
     """rgba: (H, W, 4) uint8 -> .webp bytes (VP8L).
 
     alpha_plane=True: the ALPH-chunk form (src/enc/alpha_enc.c:50-98 +
@@ -1778,7 +1778,9 @@ def encode(rgba, method=4, cache_bits=AUTO_CACHE, kmax=KMAX, return_parts=False,
     PW = argb.shape[1]
     dists = candidate_distances(PW)
     lens = match_lengths(argb, dists)
-    if pal is not None:   # colour-indexed: the cost-model parse, no colour cache
+    if lz_parse is None:
+        lz_parse = pal is not None
+    if lz_parse:   # colour-indexed (or repeat-heavy): the cost-model parse, no colour cache
         cache_bits = 0
         hit = np.zeros((H, PW), dtype=bool)
         act, clen, ccode = palette_parse(argb, dists, lens)
@@ -1789,7 +1791,7 @@ def encode(rgba, method=4, cache_bits=AUTO_CACHE, kmax=KMAX, return_parts=False,
         hit = minb <= cache_bits
     else:
         hit = cache_hits(argb.ravel(), cache_bits).reshape(H, PW)
-    if pal is None:
+    if not lz_parse:
         act, clen, ccode = parse(argb, hit, dists, lens)
     al = Alphabets(cache_bits)
     S, X = pixel_symbols(argb, act, clen, ccode, cache_bits, al)

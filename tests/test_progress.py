@@ -61,3 +61,28 @@ def test_user_abort_lossless(gpu):
     img = syn_v1(512, 512, 0)
     with pytest.raises(RuntimeError, match="USER_ABORT"):
         gpu.encode_rgba(img, quality=75.0, method=4, lossless=1, progress=lambda p: False)
+
+
+@pytest.mark.parametrize("cfg", [dict(low_memory=1), dict(method=2, target_size=60000)],
+                         ids=["low_memory", "target_size"])
+def test_progress_rows_and_abort_vp8encloop(gpu, cfg):
+    """VP8EncLoop's passes (low_memory's StatLoop + final pass, a size
+    search's passes) report rows between 20 and 90 like the token loop, and a
+    hook returning 0 there stops the call with USER_ABORT"""
+    img = syn_v1(3840, 2160, 2)
+    kw = dict(quality=75.0, method=4)
+    kw.update(cfg)
+    seen = []
+    gpu.encode_rgba(img, progress=lambda p: seen.append(p) or True, **kw)
+    mid = [p for p in seen if 20 < p < 90]
+    assert mid and seen[-1] == 100, seen
+    assert seen == sorted(seen), seen
+    calls = []
+
+    def hook(p):
+        calls.append(p)
+        return p <= 20
+
+    with pytest.raises(RuntimeError, match="USER_ABORT"):
+        gpu.encode_rgba(img, progress=hook, **kw)
+    assert 20 < calls[-1] < 90 and 100 not in calls, calls

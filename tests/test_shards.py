@@ -88,6 +88,31 @@ def test_two_real_ranks_on_one_gpu(gpu):
 
 
 @pytest.mark.gpu
+def test_rccl_rank_path_one_gpu(gpu):
+    """configs[2]'s collective over RCCL itself: bench.py as one rank with its
+    process group created on the nccl backend (RCCL on ROCm) -- the real
+    encoder's timed batch, the all-gather of the encoded sizes and the max /
+    sum reductions of the timing and the known-answer counts all go through
+    RCCL on the GPU (two ranks cannot share one GPU under RCCL; the 8-GPU
+    run is the driver's)"""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
+              "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--force-pg",
+                        "--dist-backend", "nccl", "--engines", "1", "--steps", "1",
+                        "--warmup", "0", "--no-cpu", "--no-other-input", "--input", "hbm"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["collectives"].startswith("nccl, 1 rank(s)"), line
+    assert line["kat_check"].startswith("ok: 10 timed-batch frames on 1 rank(s)"), line
+    assert line["output_bytes_per_frame"] > 0
+
+
+@pytest.mark.gpu
 def test_host_cpus_on_numa_node(gpu):
     """the engines' CPU share: inside this process's affinity and on the GPU's
     NUMA node when sysfs names one (else unpinned)"""

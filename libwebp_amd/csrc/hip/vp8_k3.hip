@@ -97,6 +97,8 @@ struct K3S {
   int32_t wsum[2][4];              // per-wave token-count totals (scan)
   int32_t redw[4];                 // per-wave reduction slots
   uint32_t fold_total;             // tokens of the MBs being folded
+  uint32_t fold_base;              // their first compact-stream offset
+  int32_t epseen;                  // G.epoch as one lane read it before the last worker barrier
   uint32_t bar;                    // worker barrier counter
   int32_t myabort;
   int32_t flag_ldc;                // left DC nz flag hand-off from wave 0
@@ -1353,7 +1355,7 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
       if (i < i1) mboff[i] = off + incl - v;
       off += __shfl(incl, 63);
     }
-    if (ln == 0) { L.fold_total = off - base; L.mark_any = 0; }
+    if (ln == 0) { L.fold_total = off - base; L.fold_base = base; L.mark_any = 0; }
   }
   wbar(L);
   const uint32_t total = L.fold_total;
@@ -1494,6 +1496,44 @@ __device__ void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uin
     if (tid == 0) st_sc1(&XH->fold_ptr, (int32_t)i1);
   } else {
     fold_mbs(G, L, tid, i0, i1, row0, tok_base, mboff, arena);
+  }
+}
+
+// Arena mode: once MBs [i0, i1) of the worker's row are folded (their
+// compact offsets fixed from `base` = L.fold_base of that fold), their tokens
+// move from the worker's arena chunk to the frame's compact stream, one MB per
+// wave at a time, off the fold chain (fold_ptr / the epoch are published
+// first). An MB that would end beyond tok_cap is left out: the frame's count
+// then exceeds tok_cap and the host gathers it again into a wider buffer.
+__device__ void copy_folded(K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t row0,
+                            uint32_t base, uint16_t* tok_base, size_t tok_cap,
+                            const uint16_t* arena) {
+  const uint32_t ln = (uint32_t)tid & 63, wv = (uint32_t)tid >> 6;
+  uint32_t off = base;
+  for (uint32_t c = i0; c < i1; c += 64) {
+    const uint32_t i = c + ln;
+    const uint32_t v = i < i1 ? L.rowcnt[i - row0] : 0u;
+    uint32_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(incl, o);
+      if (ln >= (uint32_t)o) incl += u;
+    }
+    const uint32_t excl = off + incl - v;
+    const uint32_t nc = min(64u, i1 - c);
+    for (uint32_t k = wv; k < nc; k += 4) {
+      const uint32_t d = __shfl(excl, (int)k), n = __shfl(v, (int)k);
+      if ((size_t)d + n > tok_cap) continue;   // wave-uniform
+      const uint16_t* src = arena + L.rowpos[c + k - row0];
+      uint16_t* dst = tok_base + d;
+      uint32_t q = ln;
+      for (; q + 192 < n; q += 256) {   // four loads in flight per lane
+        const uint16_t t0 = src[q], t1 = src[q + 64], t2 = src[q + 128], t3 = src[q + 192];
+        dst[q] = t0; dst[q + 64] = t1; dst[q + 128] = t2; dst[q + 192] = t3;
+      }
+      for (; q < n; q += 64) dst[q] = src[q];
+    }
+    off += __shfl(incl, 63);
   }
 }
 
@@ -1744,6 +1784,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       L.lderr[0][0] = L.lderr[0][1] = L.lderr[1][0] = L.lderr[1][1] = 0;
     }
     if (tid < 4) L.predleft[tid] = 0;
+    if (tid == 0)
+      L.epseen = __hip_atomic_load(&G.epoch, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
     int left_dc = 0;
     uint32_t fold_from = (uint32_t)y * mbw;   // first MB of this row not folded yet
     wbar(L);
@@ -1757,7 +1799,15 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       // ---- cost-table epoch (frame_enc.c:828-832): refresh before MB k with
       // k = max_count + e * (max_count + 1)
       const int ep = (int)mb < max_count ? 0 : ((int)mb - max_count) / (max_count + 1) + 1;
-      if (ep > __hip_atomic_load(&G.epoch, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+      // The decision is the worker's, from one lane's read of G.epoch taken
+      // before the barrier that ended the previous MB (L.epseen): every wave
+      // of the worker takes the same branch and so the same barriers. (Each
+      // wave reading G.epoch itself let the waves of a waiting worker split
+      // when the refresher published between their reads: some entered the
+      // wait with its barrier, some skipped it, and the worker's barrier
+      // generations went out of step -- a hang at the frame's end.) A stale
+      // value only sends the worker through a wait that returns at once.
+      if (ep > L.epseen) {
         const bool refresher = (int)mb == max_count + (ep - 1) * (max_count + 1);
         if (refresher) {
           // everything before this MB: rows above folded by their owners,
@@ -1772,8 +1822,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           const uint64_t tr_f = TR_NOW();
           TR_ADD(K3TR_REFR_WAIT, tr_f - tr_w);
           fold_rows<X>(G, L, tid, fold_from, mb, (uint32_t)y * mbw, tok_base, mboff, xs, a.arena);
+          const uint32_t cp_from = fold_from;
           fold_from = mb;
           wbar(L);
+          const uint32_t cp_base = L.fold_base;
           const uint64_t tr_r = TR_NOW();
           TR_ADD(K3TR_FOLD, tr_r - tr_f);
           const int dirty = finalize_probas_wg(G, L, tid);
@@ -1811,6 +1863,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           }
           if (tid == 0) publish(&G.epoch, ep);
           TR_SINCE(K3TR_REFRESH, tr_r);
+          if (a.arena)
+            copy_folded(L, tid, cp_from, mb, (uint32_t)y * mbw, cp_base, tok_base, a.tok_cap, a.arena);
         } else if (X) {
           // the frame's refresher published epoch ep; the first worker of this
           // workgroup to need it copies the probabilities (and, if they
@@ -2276,6 +2330,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         predtop[4 * x + tid] = L.modes[12 + tid];
         L.predleft[tid] = L.modes[4 * tid + 3];
       }
+      if (tid == 0)
+        L.epseen = __hip_atomic_load(&G.epoch, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
       wbar(L);
       left_dc = L.flag_ldc;
       if (tid == 0) publish(&rowdone[y], x + 1);
@@ -2314,6 +2370,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     TR_SINCE(K3TR_FOLD, tr_ff);
     report_rows<X>(G, L, P, tid, (uint32_t)(y + 1) * mbw, mbw, XH);
     wbar(L);
+    if (a.arena)
+      copy_folded(L, tid, fold_from, (uint32_t)(y + 1) * mbw, (uint32_t)y * mbw, L.fold_base,
+                  tok_base, a.tok_cap, a.arena);
     K3_STAMP(7);
   }
 
@@ -2582,15 +2641,17 @@ static int k3x_take(int n, int mbh, int nw) {
   }
 }
 
-// default: 3 MB workers for m3/m4 frames (4 spill registers to scratch and
-// are no faster: the CU's vector issue is already saturated), 2 when the
-// trellis paths (and their registers and LDS) are in the kernel
+// default: 4 MB workers for m3/m4 frames (a 1,024-thread workgroup held to
+// 128 VGPRs, 120 B/lane of scratch: 16 waves per CU hide more of each MB's
+// dependency latency than 12 waves with 168 VGPRs -- K3 116.9 -> 105.4 ms,
+// profiles/r4/nw4a_*), 2 when the trellis paths are in the kernel, 3 for the
+// autofilter instantiation
 static int launch_k3_default(const K3Args& a, int n, bool trellis, bool af, void* stream) {
   if (af)
     return trellis ? launch_k3_t<2, true, true>(a, n, true, stream)
                    : launch_k3_t<3, false, true>(a, n, false, stream);
   return trellis ? launch_k3_t<2, true>(a, n, true, stream)
-                 : launch_k3_t<3, false>(a, n, false, stream);
+                 : launch_k3_t<4, false>(a, n, false, stream);
 }
 
 // The frames' compact token streams from the arena (K3Args::arena): frame f's

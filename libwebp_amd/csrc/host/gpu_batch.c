@@ -455,9 +455,10 @@ fail:
 
 /* ---- token buffers ----------------------------------------------------
  * The token loop (methods 3-6 without low_memory) runs K3 with an arena:
- * every MB's tokens are written once, k_gather_tokens lays out each frame's
- * compact stream at d_tokens + f * tok_cap, and tok_cap follows the largest
- * stream seen. The other paths (methods 0-2, low_memory, VP8EncLoop's
+ * every MB's tokens are written once into a worker's arena chunk and moved
+ * by K3 to the frame's compact stream at d_tokens + f * tok_cap once their
+ * row is folded; tok_cap follows the largest stream seen (k_gather_tokens
+ * redoes a stream that did not fit). The other paths (methods 0-2, low_memory, VP8EncLoop's
  * searches) keep per-MB slots of the worst case VP8G_MAX_TOKENS_PER_MB. */
 static int arena_mode(const WebPGpuBatch* b) {
   return b->cfg.method >= 3 && !b->cfg.low_memory;
@@ -508,8 +509,8 @@ static int tokens_for_run(WebPGpuBatch* b) {
          ensure_arena(b, (size_t)b->max_frames * nmb * 1024 + 768 * (size_t)VP8G_ARENA_CHUNK);
 }
 
-/* K3 over the frames of h_params (already on the device), then the gather in
- * arena mode. The caller copies the results back and calls k3_settle. */
+/* K3 over the frames of h_params (already on the device). The caller copies
+ * the results back and calls k3_settle. */
 static int launch_k3(WebPGpuBatch* b, int n, uint8_t* recon) {
   hipStream_t st = b->stream;
   vp8g_arena A, *ap = NULL;
@@ -526,12 +527,12 @@ static int launch_k3(WebPGpuBatch* b, int n, uint8_t* recon) {
     A.mbpos = b->d_mbpos;
     ap = &A;
   }
+  /* in arena mode K3 itself moves each folded row's tokens to the compact
+     stream (copy_folded); k_gather_tokens only redoes it for a stream that
+     outgrew tok_cap (k3_settle) */
   if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
                           b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5, b->d_results,
                           b->d_rerun, recon, b->d_xsync, ap, st))
-    return 0;
-  if (ap && !vp8g_launch_gather(b->d_tokens, b->tok_cap, b->d_arena, b->d_mbpos, b->d_mboff, b->w,
-                                b->h, n, b->d_params, b->d_results, st))
     return 0;
   return 1;
 fail:

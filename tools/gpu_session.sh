@@ -2,7 +2,7 @@
 # One GPU-box session: GPU tests, bench line, K3 stage split, rocprofv3 kernel
 # stats, PMC passes (HBM bytes, SQ issue counters) and the PMC calibration.
 # Usage (on the box): bash tools/gpu_session.sh <tag> [steps...]
-#   steps: tests ltests bench lossless lab cfg4 lphases lprof lpmc stages prof pmc sq calib (default: all but the lossless ones)
+#   steps: tests ltests bench lowmem lossless lab cfg4 lphases lprof lpmc stages prof pmc sq calib (default: all but the lossless ones)
 set -o pipefail
 TAG=${1:-s}; shift
 STEPS=${*:-tests bench stages prof pmc sq calib}
@@ -39,6 +39,10 @@ if has ltests; then   # the lossless GPU tests only
 fi
 if has bench; then
   run timeout -k 10 400 python3 bench.py --steps 5 --warmup 2 > $O/bench.json 2> $O/bench.err || exit 1
+fi
+if has lowmem; then   # low_memory (K3 once per pass, tokens re-derived)
+  run timeout -k 10 400 python3 bench.py --low-memory --steps 3 --warmup 1 --no-cpu > $O/bench_lowmem.json \
+    2> $O/bench_lowmem.err || exit 1
 fi
 if has lossless; then
   run timeout -k 10 400 python3 bench.py --lossless --steps 6 --warmup 1 > $O/bench_lossless.json \
@@ -88,6 +92,10 @@ cd /tmp && export TMPDIR=/tmp
 if has prof; then
   run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run \
     -- $BENCH --steps 2 --warmup 1 > $O/prof.log 2>&1 || exit 1
+fi
+if has copytrace; then   # host-input bench: kernels and memory copies (SDMA or blit kernel)
+  run timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
+    -d $O/ctrace -o run -- python3 $R/bench.py --no-cpu --steps 2 --warmup 1 > $O/ctrace.log 2>&1 || exit 1
 fi
 if has pmc; then
   for C in FETCH_SIZE WRITE_SIZE; do

@@ -123,14 +123,15 @@ class GpuBatch:
 
     def encode_host_ptr(self, ptr, n, frame_stride=None, row_stride=None):
         """Encode n RGBA frames at host address ptr. Page-locked memory
-        (hipHostMalloc, torch pin_memory) is uploaded by one DMA copy on the
-        encoder's own stream ahead of its kernels; pageable memory is copied
-        synchronously first."""
+        (hipHostMalloc, torch pin_memory) is uploaded by one copy on an SDMA
+        engine (host/h2d_sdma.c) ahead of the encoder's kernels; pageable
+        memory is copied synchronously first."""
         row_stride = row_stride or 4 * self.width
         frame_stride = frame_stride or row_stride * self.height
         ok = self._lib.WebPGpuBatchEncodeRGBAHost(self._h, ptr, frame_stride, row_stride, n)
         if not ok:
             raise RuntimeError("WebPGpuBatchEncodeRGBAHost failed: %s" % last_error())
+        self.n = n
 
     def encode_host(self, frames):
         """frames: (N, H, W, 4) uint8 numpy array in host memory."""

@@ -1903,12 +1903,24 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       if constexpr (!X) {
         if (tid == 0) {
           int ld = 0;
+#ifdef K3_PRIO4   // A/B: one level per row above still running (3 = leads)
+          if (y == 0 || __hip_atomic_load(&rowdone[y - 1], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP) >= mbw)
+            ld = 3;
+          else if (y == 1 || __hip_atomic_load(&rowdone[y - 2], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP) >= mbw)
+            ld = 2;
+          else if (y == 2 || __hip_atomic_load(&rowdone[y - 3], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP) >= mbw)
+            ld = 1;
+#else
           if (y == 0 || __hip_atomic_load(&rowdone[y - 1], __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WORKGROUP) >= mbw)
             ld = 2;
           else if (y == 1 || __hip_atomic_load(&rowdone[y - 2], __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP) >= mbw)
             ld = 1;
+#endif
           L.lead = ld;
         }
         if (y == 0) wbar(L);   // (rows > 0 pass the wait's barrier)
@@ -1949,9 +1961,16 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
 #ifndef K3_PRIO_LEAD
 #define K3_PRIO_LEAD 2
 #endif
+#ifdef K3_PRIO4
+        if (lead == 3) __builtin_amdgcn_s_setprio(3);
+        else if (lead == 2) __builtin_amdgcn_s_setprio(2);
+        else if (lead == 1) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+#else
         if (lead == 2) __builtin_amdgcn_s_setprio(K3_PRIO_LEAD);
         else if (lead == 1) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
+#endif
       }
 #endif
       K3_STAMP(0);

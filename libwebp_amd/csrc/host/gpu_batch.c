@@ -1,6 +1,7 @@
 /* Batched GPU engine: device buffers, the K1 -> K2 -> host setup -> K3
  * pipeline, and the host thread pool that runs the boolean-coder tail.
  * Host C over the HIP runtime C API; kernels live in hip/vp8_kernels.hip. */
+#include "h2d_sdma.h"
 #include <math.h>
 #include <stdio.h>
 #include <pthread.h>
@@ -1439,11 +1440,12 @@ int WebPGpuBatchEncodeRGBAHost(WebPGpuBatch* b, const uint8_t* rgba, size_t fstr
     b->d_rgba_cap = need;
   }
   if (host_is_pinned(rgba)) {
-    /* page-locked (hipHostMalloc / hipHostRegister): the upload is one DMA
-       copy on the engine's own stream, ahead of K1 in stream order -- it runs
-       beside the other engines' kernels, and no second stream has to share a
-       hardware queue with a running K3 (whose queue would hold it back) */
-    CHK(hipMemcpyAsync(b->d_rgba, rgba, need, hipMemcpyHostToDevice, b->stream));
+    /* page-locked (hipHostMalloc / hipHostRegister): one copy on an SDMA
+       engine (host/h2d_sdma.c) -- it runs beside the other engines' kernels,
+       where the runtime's copy kernel would wait for CUs a running K3 holds */
+    CHK(hipStreamSynchronize(b->stream));   /* (idle between batch calls) */
+    if (!h2d_sdma_upload(b->device, b->d_rgba, rgba, need))   /* an SDMA engine, no CU */
+      CHK(hipMemcpyAsync(b->d_rgba, rgba, need, hipMemcpyHostToDevice, b->stream));
   } else {
     /* pageable: an async copy of it on our non-blocking stream is not safe
        on this platform (the runtime may read it from the GPU directly), so

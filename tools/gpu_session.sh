@@ -93,6 +93,10 @@ if has prof; then
   run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run \
     -- $BENCH --steps 2 --warmup 1 > $O/prof.log 2>&1 || exit 1
 fi
+if has hprof; then   # host-input bench (SDMA upload): kernel timeline
+  run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/hstats -o run \
+    -- python3 $R/bench.py --no-cpu --steps 3 --warmup 1 > $O/hprof.log 2>&1 || exit 1
+fi
 if has copytrace; then   # host-input bench: kernels and memory copies (SDMA or blit kernel)
   run timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
     -d $O/ctrace -o run -- python3 $R/bench.py --no-cpu --steps 2 --warmup 1 > $O/ctrace.log 2>&1 || exit 1

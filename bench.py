@@ -43,7 +43,9 @@ def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
                     help="ranks; without a torchrun environment bench.py launches them itself")
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=9,
+                    help="timed steps (default 9: three per encoder instance, so the "
+                         "line is not dominated by filling and draining the pipeline)")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=0,
                     help="frames per GPU per step (0: 256 lossy, 1024 lossless)")
@@ -579,6 +581,12 @@ def main(argv=None):
         other_rate = world * n_other * B * W * H / el / 1e6
     del pinned
 
+    # device memory in use with every instance's buffers allocated and run
+    # (the whole device: a box runs one job)
+    hbm_used = None
+    if not args.stub:
+        free_b, total_b = torch.cuda.mem_get_info(dev)
+        hbm_used = round((total_b - free_b) / 1e9, 2)
     line = None
     if rank == 0:
         if args.lossless:
@@ -593,8 +601,8 @@ def main(argv=None):
                                 "tests/golden/shard_kat.json" % (checked, world)
         line["config"]["input"] = "host" if host_in else "hbm"
         line["input"] = ("host: RGBA in pinned host memory -> .webp in host memory, H2D "
-                         "upload inside every step (SURVEY.md 8(d)): one DMA copy on the "
-                         "encoder instance's stream ahead of its kernels, beside the other "
+                         "upload inside every step (SURVEY.md 8(d)): one copy on an SDMA "
+                         "engine ahead of the instance's kernels, beside the other "
                          "%d instance(s)' kernels" % (len(encs) - 1)
                          if host_in else
                          "hbm: RGBA frames already resident in HBM (no upload)")
@@ -605,6 +613,8 @@ def main(argv=None):
             line["cpu_baseline"] = cb
         if not args.stub:
             line["host_cpus_per_rank"] = len(cpus) if cpus else "unpinned"
+            if hbm_used is not None:
+                line["hbm_used_gb"] = hbm_used
         if args.stub:
             line["data"] = "stub encoder (CPU test double, no GPU)"
         if dist.is_initialized():

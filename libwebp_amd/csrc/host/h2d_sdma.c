@@ -24,6 +24,7 @@
 typedef struct {
   int ok;              /* 1 usable, -1 unusable, 0 not looked up yet */
   hsa_agent_t gpu, cpu;
+  pthread_mutex_t up;  /* one upload at a time per device (see below) */
 } dev_agents;
 
 static dev_agents g_dev[MAX_DEV];
@@ -70,6 +71,7 @@ static int lookup(int device) {
       hsa_iterate_agents(find_agent, &c);
     }
     g_dev[device].ok = (c.found_gpu && c.found_cpu) ? 1 : -1;
+    pthread_mutex_init(&g_dev[device].up, NULL);
     g_dev[device].gpu = c.gpu;
     g_dev[device].cpu = c.cpu;
   }
@@ -85,8 +87,16 @@ int h2d_sdma_upload(int device, void* dst, const void* src, size_t bytes) {
     mode = (v && v[0] == 'h') ? 0 : 1;
   }
   if (!mode || !lookup(device)) return 0;
+  /* Uploads to one device go one after another: they share the PCIe link
+     anyway, and in turn the first engine's frames are on the device after one
+     transfer time instead of all engines' after three (its kernels start
+     while the next engine uploads). */
+  pthread_mutex_lock(&g_dev[device].up);
   hsa_signal_t sig;
-  if (hsa_signal_create(1, 0, NULL, &sig) != HSA_STATUS_SUCCESS) return 0;
+  if (hsa_signal_create(1, 0, NULL, &sig) != HSA_STATUS_SUCCESS) {
+    pthread_mutex_unlock(&g_dev[device].up);
+    return 0;
+  }
   const hsa_status_t st = hsa_amd_memory_async_copy(dst, g_dev[device].gpu, src, g_dev[device].cpu,
                                                     bytes, 0, NULL, sig);
   int ok = 0;
@@ -97,5 +107,6 @@ int h2d_sdma_upload(int device, void* dst, const void* src, size_t bytes) {
     ok = 1;
   }
   hsa_signal_destroy(sig);
+  pthread_mutex_unlock(&g_dev[device].up);
   return ok;
 }

@@ -22,7 +22,7 @@ enc.encode_device(buf.data_ptr(), B)
 t = enc.timings()
 nmb = ((W + 15) // 16) * ((H + 15) // 16)
 # the stamps are worker 0's: it encodes rows 0, NW, 2NW, ...
-NW = {"2": 1, "3": 2, "4": 4, "5": 3}.get(os.environ.get("WEBP_AMD_K3", ""), 2 if method >= 5 else 3)
+NW = {"2": 1, "3": 2, "4": 4, "5": 3}.get(os.environ.get("WEBP_AMD_K3", ""), 2 if method >= 5 else 4)
 mbh = (H + 15) // 16
 wmb = ((mbh + NW - 1) // NW) * ((W + 15) // 16)
 c = enc.stage_cycles(0)

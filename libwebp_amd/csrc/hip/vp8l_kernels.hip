@@ -1861,14 +1861,14 @@ __device__ __forceinline__ uint32_t cache_settle(uint32_t mb, uint32_t v, size_t
 // settled here where L2 left it partial), packed per pixel as
 // len | cand << 13 | minb << 15 for the parse.
 __global__ __launch_bounds__(64) void k_vp8l_match(const uint32_t* __restrict__ argb,
-                                                   const uint8_t* __restrict__ minb,
+                                                   uint8_t* __restrict__ minb,
                                                    const uint2* __restrict__ cstart, int S,
                                                    vp8l_params p, uint32_t* __restrict__ bm) {
   const int f = blockIdx.y, y = blockIdx.x, ln = lane_id();
   const int W = p.w;
   const size_t npix = (size_t)W * p.h;
   const uint32_t* E = argb + f * npix;
-  const uint8_t* MB = minb + (size_t)f * npix;
+  uint8_t* MB = minb + (size_t)f * npix;
   uint32_t* O = bm + f * npix;
   const size_t row = (size_t)y * W;
   int carry[VP8L_NUM_CAND] = {0, 0, 0, 0};
@@ -1909,8 +1909,10 @@ __global__ __launch_bounds__(64) void k_vp8l_match(const uint32_t* __restrict__ 
     }
     if (valid) {
       uint32_t mb = cur.mb;
-      if (mb & VP8L_CACHE_PARTIAL)
+      if (mb & VP8L_CACHE_PARTIAL) {   // settled here, and kept for the shortest-path parse
         mb = cache_settle(mb, e, q, (int)npix, S, cstart + (size_t)f * S * VP8L_CACHE_TAB);
+        MB[q] = (uint8_t)mb;
+      }
       O[q] = (uint32_t)bn | ((uint32_t)bk << 13) | (mb << 15);
     }
     cur = nxt;
@@ -3104,12 +3106,269 @@ extern "C" int vp8l_launch_palette_apply(const uint8_t* rgba, size_t fstride, in
   return check_launch();
 }
 
+// ------------------------------------------------------------------ L3d
+// Frames without a predictor (direct / subtract green): the shortest-path
+// parse (model: dp_parse, oracle/vp8l_dp.c) over the first VP8L_DP_NC plane-
+// code distances with the colour cache in the cost model, two rounds of
+// symbol costs (k_vp8l_dpcost) -> backward DP per row (k_vp8l_dp) -> the
+// forward walk into parse ops (k_vp8l_dpwalk). Reference idea:
+// TraceBackwards, backward_references_cost_enc.c:569-795.
+
+__device__ __forceinline__ bool dp_frame(const uint8_t* fmode, int f) {
+  if (!fmode) return false;
+  const int m = fmode[f];
+  return m != VP8L_MODE_PALETTE && !(m & VP8L_MODE_SPATIAL);
+}
+
+// Symbol costs of a frame's parse with its colour cache (model: dp_costs):
+// one workgroup per frame, histograms in LDS, 1/256 bit per symbol.
+__global__ __launch_bounds__(1024) void k_vp8l_dpcost(const uint32_t* __restrict__ argb,
+                                                      const uint32_t* __restrict__ ops, int npix,
+                                                      const uint8_t* __restrict__ fmode,
+                                                      const uint8_t* __restrict__ cbits,
+                                                      const int32_t* __restrict__ frac,
+                                                      int32_t* __restrict__ costs) {
+  __shared__ uint32_t h[VP8L_DP_NCOST];
+  __shared__ uint32_t tot[5], nz[5];
+  const int f = blockIdx.x, tid = threadIdx.x;
+  if (!dp_frame(fmode, f)) return;
+  const uint32_t* E = argb + (size_t)f * npix;
+  const uint32_t* O = ops + (size_t)f * npix;
+  const int cb = cbits[f];
+  const int oR = VP8L_DP_NG, oB = oR + 256, oA = oB + 256, oD = oA + 256;
+  for (int i = tid; i < VP8L_DP_NCOST; i += 1024) h[i] = 0;
+  if (tid < 5) { tot[tid] = 0; nz[tid] = 0; }
+  __syncthreads();
+  for (int q = tid; q < npix; q += 1024) {
+    const uint32_t op = O[q], act = op & 3;
+    if (act == 0) {
+      const uint32_t a = E[q];
+      atomicAdd(&h[(a >> 8) & 255], 1u);
+      atomicAdd(&h[oR + ((a >> 16) & 255)], 1u);
+      atomicAdd(&h[oB + (a & 255)], 1u);
+      atomicAdd(&h[oA + (a >> 24)], 1u);
+    } else if (act == 1) {
+      atomicAdd(&h[280 + ((E[q] * HASH_MUL) >> (32 - cb))], 1u);
+    } else if (act == 2) {
+      int sym, nb; uint32_t ex;
+      prefix_enc(((op >> 2) & 0xfff) + 1, sym, nb, ex);
+      atomicAdd(&h[256 + sym], 1u);
+      prefix_enc(op >> 14, sym, nb, ex);
+      atomicAdd(&h[oD + sym], 1u);
+    }
+  }
+  __syncthreads();
+  auto alph = [&](int i) { return i < oR ? 0 : i < oB ? 1 : i < oA ? 2 : i < oD ? 3 : 4; };
+  for (int i = tid; i < VP8L_DP_NCOST; i += 1024)
+    if (h[i]) { atomicAdd(&tot[alph(i)], h[i]); atomicAdd(&nz[alph(i)], 1u); }
+  __syncthreads();
+  int32_t* out = costs + (size_t)f * VP8L_DP_NCOST;
+  for (int i = tid; i < VP8L_DP_NCOST; i += 1024) {
+    const int a = alph(i);
+    int32_t c = 0;
+    if (nz[a] > 1) c = (flog2_fx(frac, tot[a]) - (h[i] ? flog2_fx(frac, h[i]) : 0)) >> 4;
+    out[i] = c;
+  }
+}
+
+#define DP_XM 8                        // columns either side of a chunk in the tile
+#define DP_MAXDY 8                     // rows above the block in the tile (+1 for a wrap)
+#define DP_TR (64 + DP_MAXDY + 1)
+#define DP_TW (64 + 2 * DP_XM)
+#define DP_RING (VP8L_DP_MAXK + 1)
+struct DpSmem {
+  uint32_t tile[DP_TR][DP_TW];         // the block's rows (and DP_MAXDY + 1 above), chunk +- DP_XM
+  int32_t ring[64][DP_RING + 1];       // per row: cost to the row end of the next 64 positions
+  uint8_t runs[VP8L_DP_NC][64];        // per row: each candidate's run from the position on (<= 64)
+  uint16_t ch[64][66];                 // the chunk's choices, row-major (k | candidate << 7)
+  uint8_t mb[64][68];                  // the chunk's smallest cache sizes
+  int32_t cost[VP8L_DP_NCOST];
+  int32_t lcost[VP8L_DP_MAXK + 1];
+  int32_t dcost[VP8L_DP_NC], ord[VP8L_DP_NC], cdy[VP8L_DP_NC], cdx[VP8L_DP_NC];
+};
+
+// Backward DP per row (model / oracle vp8l_dp_parse): one wave per 64 rows of
+// a frame, one row per lane, the row walked right to left in 64-pixel chunks
+// staged in LDS with the rows above the source candidates reach (a source
+// outside the tile -- a wrap across a row end, or a far row -- is read from
+// HBM). Per position: every candidate's run updated from the one to its
+// right, then the literal / cache hit against copies of 2..min(run, 64) in
+// increasing length, each length by the cheapest candidate covering it
+// (candidates walked in (distance cost, index) order), strictly better only.
+__global__ __launch_bounds__(64) void k_vp8l_dp(const uint32_t* __restrict__ argb,
+                                                const uint8_t* __restrict__ minb, vp8l_params p,
+                                                const uint8_t* __restrict__ fmode,
+                                                const uint8_t* __restrict__ cbits,
+                                                const int32_t* __restrict__ costs,
+                                                const int4* __restrict__ cand, int ncand,
+                                                uint16_t* __restrict__ choice) {
+  __shared__ DpSmem S;
+  const int f = blockIdx.y, ln = lane_id();
+  if (!dp_frame(fmode, f)) return;   // whole wave
+  const int W = p.w, H = p.h, r0 = blockIdx.x * 64, r = r0 + ln;
+  const bool valid = r < H;
+  const size_t npix = (size_t)W * H;
+  const uint32_t* E = argb + (size_t)f * npix;
+  const uint8_t* MB = minb + (size_t)f * npix;
+  uint16_t* CH = choice + (size_t)f * npix;
+  const int cb = cbits[f];
+  const int oR = VP8L_DP_NG, oB = oR + 256, oA = oB + 256, oD = oA + 256;
+  for (int i = ln; i < VP8L_DP_NCOST; i += 64) S.cost[i] = costs[(size_t)f * VP8L_DP_NCOST + i];
+  __syncthreads();
+  if (ln >= 1 && ln <= VP8L_DP_MAXK) {
+    int sym, nb; uint32_t ex;
+    prefix_enc((uint32_t)ln, sym, nb, ex);
+    S.lcost[ln] = S.cost[256 + sym] + 256 * nb;
+  }
+  int4 cv = make_int4(0, 0, 0, 0);
+  if (ln < ncand) {
+    cv = cand[ln];
+    int sym, nb; uint32_t ex;
+    prefix_enc((uint32_t)cv.w, sym, nb, ex);
+    S.dcost[ln] = S.cost[oD + sym] + 256 * nb;
+    S.cdy[ln] = cv.y;
+    S.cdx[ln] = cv.z;
+  }
+  __syncthreads();
+  if (ln < ncand) {   // rank by (distance cost, index)
+    int rank = 0;
+    for (int c = 0; c < ncand; ++c)
+      rank += S.dcost[c] < S.dcost[ln] || (S.dcost[c] == S.dcost[ln] && c < ln);
+    S.ord[rank] = ln;
+  }
+  for (int c = 0; c < ncand; ++c) S.runs[c][ln] = 0;
+  S.ring[ln][W % DP_RING] = 0;
+  __syncthreads();
+  const int trow0 = r0 - DP_MAXDY - 1;   // the tile's first row
+  for (int c0 = ((W - 1) >> 6) << 6; c0 >= 0; c0 -= 64) {
+    const int tcol0 = c0 - DP_XM;
+    __syncthreads();
+    for (int i = ln; i < DP_TR * DP_TW; i += 64) {
+      const int tr = i / DP_TW, tc = i - tr * DP_TW;
+      const int rr = trow0 + tr, cc = tcol0 + tc;
+      S.tile[tr][tc] = (rr >= 0 && rr < H && cc >= 0 && cc < W) ? E[(size_t)rr * W + cc] : 0u;
+    }
+    for (int rr = 0; rr < 64; ++rr)
+      if (r0 + rr < H && c0 + ln < W) S.mb[rr][ln] = MB[(size_t)(r0 + rr) * W + c0 + ln];
+    __syncthreads();
+    const int jt = min(63, W - 1 - c0);
+    for (int jj = jt; jj >= 0; --jj) {
+      const int j = c0 + jj;
+      if (valid) {
+        const uint32_t e = S.tile[ln + DP_MAXDY + 1][jj + DP_XM];
+        for (int c = 0; c < ncand; ++c) {
+          int sc = j - S.cdx[c], sr = r - S.cdy[c];
+          if (sc < 0) { sc += W; sr -= 1; }
+          else if (sc >= W) { sc -= W; sr += 1; }
+          bool eq = false;
+          if (sr >= 0) {
+            const int tr = sr - trow0, tc = sc - tcol0;
+            eq = (tr >= 0 && tc >= 0 && tc < DP_TW) ? S.tile[tr][tc] == e
+                                                    : E[(size_t)sr * W + sc] == e;
+          }
+          const int run = eq ? min((int)S.runs[c][ln] + 1, VP8L_DP_MAXK) : 0;
+          S.runs[c][ln] = (uint8_t)run;
+        }
+        const int m = S.mb[ln][jj];
+        int lit;
+        if (cb > 0 && m <= cb)
+          lit = S.cost[280 + (int)((e * HASH_MUL) >> (32 - cb))] * 68 / 100;
+        else
+          lit = (S.cost[(e >> 8) & 255] + S.cost[oR + ((e >> 16) & 255)] + S.cost[oB + (e & 255)] +
+                 S.cost[oA + (e >> 24)]) * 82 / 100;
+        int best = S.ring[ln][(j + 1) % DP_RING] + lit, bk = 1, bc = 0;
+        const int kmax = min(VP8L_DP_MAXK, W - j);
+        int maxl = 1;
+        for (int i = 0; i < ncand; ++i) {
+          const int c = S.ord[i];
+          const int L = min((int)S.runs[c][ln], kmax);
+          if (L <= maxl) continue;
+          const int dc = S.dcost[c];
+          for (int k = maxl + 1; k <= L; ++k) {
+            const int v = S.ring[ln][(j + k) % DP_RING] + dc + S.lcost[k];
+            if (v < best) { best = v; bk = k; bc = c; }
+          }
+          maxl = L;
+        }
+        S.ring[ln][j % DP_RING] = best;
+        S.ch[ln][jj] = (uint16_t)(bk | (bc << 7));
+      }
+    }
+    __syncthreads();
+    for (int rr = 0; rr < 64; ++rr)
+      if (r0 + rr < H && c0 + ln < W) CH[(size_t)(r0 + rr) * W + c0 + ln] = S.ch[rr][ln];
+  }
+}
+
+// The forward walk of the DP choices into parse ops (the structure of
+// k_vp8l_parse: a wave owns 64 rows, 64-pixel chunks staged through LDS,
+// positions a copy from an earlier chunk covers marked on load).
+__global__ __launch_bounds__(64) void k_vp8l_dpwalk(vp8l_params p, const uint8_t* __restrict__ fmode,
+                                                    const uint16_t* __restrict__ choice,
+                                                    const uint8_t* __restrict__ minb,
+                                                    const uint8_t* __restrict__ cbits,
+                                                    const int4* __restrict__ cand,
+                                                    uint32_t* __restrict__ ops) {
+  __shared__ uint32_t tile[64][65];
+  __shared__ int xs[64];
+  __shared__ int dcode[VP8L_DP_NC];
+  const int f = blockIdx.y, ln = lane_id();
+  if (!dp_frame(fmode, f)) return;
+  const int W = p.w, H = p.h, y0 = blockIdx.x * 64;
+  const int nrows = min(64, H - y0);
+  const size_t npix = (size_t)W * H;
+  uint32_t* O = ops + (size_t)f * npix + (size_t)y0 * W;
+  const uint16_t* C = choice + (size_t)f * npix + (size_t)y0 * W;
+  const uint8_t* MB = minb + (size_t)f * npix + (size_t)y0 * W;
+  const int cb = cbits[f];
+  if (ln < VP8L_DP_NC) dcode[ln] = cand[ln].w;
+  int x = 0;
+  xs[ln] = 0;
+  for (int cx = 0; cx < W; cx += 64) {
+    const int cw = min(64, W - cx);
+    __syncthreads();
+    for (int r = 0; r < nrows; ++r) {
+      if (ln < cw) {
+        const size_t q = (size_t)r * W + cx + ln;
+        const uint32_t hit = cb > 0 && MB[q] <= cb;
+        tile[r][ln] = cx + ln < xs[r] ? 0xffffffffu : ((uint32_t)C[q] | (hit << 16));
+      }
+    }
+    __syncthreads();
+    if (ln < nrows) {
+      while (x < cx + cw) {
+        const int i = x - cx;
+        const uint32_t w = tile[ln][i];
+        const int k = (int)(w & 127);
+        if (k >= 2) {
+          tile[ln][i] = 2u | ((uint32_t)(k - 1) << 2) | ((uint32_t)dcode[(w >> 7) & 31] << 14);
+          const int e = min(x + k, cx + cw);
+          for (int t = i + 1; t < e - cx; ++t) tile[ln][t] = 3u;
+          x += k;
+        } else {
+          tile[ln][i] = (w >> 16) & 1u;
+          ++x;
+        }
+      }
+      xs[ln] = x;
+    }
+    __syncthreads();
+    for (int r = 0; r < nrows; ++r) {
+      if (ln < cw) {
+        uint32_t v = tile[r][ln];
+        if (v == 0xffffffffu) v = 3u;
+        O[(size_t)r * W + cx + ln] = v;
+      }
+    }
+  }
+}
+
 extern "C" int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
                                    const int32_t* tabs, uint8_t* minb, uint32_t* cseg,
                                    uint16_t* prov,
                                    uint32_t* chist, uint8_t* cbits, uint32_t* ops, int64_t* feat,
                                    uint32_t* tl, uint32_t* tn, uint32_t* hc, uint8_t* assign,
-                                   const vp8l_lz* lz, void* stream) {
+                                   const vp8l_lz* lz, const vp8l_dp* dp, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int npix = p->w * p->h;
   const int32_t* flog2 = tabs + 4097;
@@ -3168,6 +3427,18 @@ extern "C" int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
     }
     hipLaunchKernelGGL(k_vp8l_parse, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, *p, ops, prov,
                        (const uint8_t*)cbits);
+    if (dp && dp->fmode && dp->ncand > 0 && prov) {   // frames without a predictor
+      for (int round = 0; round < 2; ++round) {
+        hipLaunchKernelGGL(k_vp8l_dpcost, dim3(p->n), dim3(1024), 0, st, argb, (const uint32_t*)ops,
+                           npix, dp->fmode, (const uint8_t*)cbits, flog2, dp->costs);
+        hipLaunchKernelGGL(k_vp8l_dp, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, argb,
+                           (const uint8_t*)minb, *p, dp->fmode, (const uint8_t*)cbits,
+                           (const int32_t*)dp->costs, (const int4*)dp->cand, dp->ncand, prov);
+        hipLaunchKernelGGL(k_vp8l_dpwalk, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, *p,
+                           dp->fmode, (const uint16_t*)prov, (const uint8_t*)minb,
+                           (const uint8_t*)cbits, (const int4*)dp->cand, ops);
+      }
+    }
   }
   hipLaunchKernelGGL(k_vp8l_tilefeat, dim3(tx_n * ty_n, p->n), dim3(256), 0, st, argb, ops, *p,
                      (const uint8_t*)cbits, flog2, feat, tl, tn);

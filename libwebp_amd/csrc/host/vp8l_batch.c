@@ -62,6 +62,7 @@ void vp8l_engine_free(vp8l_engine* l) {
   hipFree(l->lz.runs); hipFree(l->lz.htab); hipFree(l->lz.chain); hipFree(l->lz.hoff);
   hipFree(l->lz.hlen); hipFree(l->lz.loff); hipFree(l->lz.llen); hipFree(l->lz.costs);
   hipFree(l->d_dcodes);
+  hipFree(l->d_dpcand); hipFree(l->d_dpcost);
   for (int i = 0; i < 5; ++i)
     if (l->ev[i]) hipEventDestroy(l->ev[i]);
   free(l);
@@ -144,6 +145,14 @@ static vp8l_engine* engine_alloc(const vp8l_params* p, int max_frames, int metho
     CHK(hipHostMalloc((void**)&l->h_npal, N * sizeof(int), 0));
     l->h_pal = (uint32_t*)calloc(N * VP8L_MAX_PALETTE, sizeof(uint32_t));
     if (!l->h_pal) goto fail;
+  }
+  if (!l->p.palette && !l->p.alpha) {   /* the shortest-path parse (frames without a predictor) */
+    int32_t cand[VP8L_DP_NC * 4];
+    memset(cand, 0, sizeof(cand));
+    l->dp_ncand = vp8l_dp_candidates(w, cand);
+    CHK(hipMalloc((void**)&l->d_dpcand, sizeof(cand)));
+    CHK(hipMemcpy(l->d_dpcand, cand, sizeof(cand), hipMemcpyHostToDevice));
+    CHK(hipMalloc((void**)&l->d_dpcost, N * VP8L_DP_NCOST * sizeof(int32_t)));
   }
   CHK(hipMalloc((void**)&l->d_modes, N * l->ntt));
   CHK(hipMalloc((void**)&l->d_mult, N * l->ntt * sizeof(uint32_t)));
@@ -343,9 +352,16 @@ static int pipeline(vp8l_engine* l, hipStream_t st, int threads, const uint8_t* 
       goto fail;
   }
   CHK(hipEventRecord(l->ev[1], st));
+  vp8l_dp dp = {NULL, NULL, 0, NULL};
+  if (VP8L_DP_ENABLED && !identity && l->d_dpcand && !p.low_effort) {   /* model: dp_parse's frames */
+    dp.fmode = l->d_fmode;
+    dp.cand = l->d_dpcand;
+    dp.ncand = l->dp_ncand;
+    dp.costs = l->d_dpcost;
+  }
   if (!vp8l_launch_analyze(l->d_argb, &p, l->d_tabs, l->d_minb, l->d_cseg, l->d_prov, l->d_chist,
                            l->d_cbits, l->d_ops, l->d_feat, l->d_tl, l->d_tn, l->d_hc,
-                           l->d_assign, p.palette ? &l->lz : NULL, st))
+                           l->d_assign, p.palette ? &l->lz : NULL, &dp, st))
     goto fail;
   CHK(hipEventRecord(l->ev[2], st));
   {   /* debugging aid: LIBWEBP_AMD_VP8L_DUMP=<prefix> writes slot 0's

@@ -102,6 +102,9 @@ typedef struct vp8l_engine {
   /* colour-indexed engines: the cost-model parse's buffers (vp8l_gpu.h) */
   vp8l_lz lz;
   uint8_t* d_dcodes;
+  int32_t* d_dpcand;   /* shortest-path parse: VP8L_DP_NC x 4 candidate words */
+  int dp_ncand;
+  int32_t* d_dpcost;   /* max_frames x VP8L_DP_NCOST */
   int device;   /* the HIP device current at creation (host threads' NUMA node) */
 } vp8l_engine;
 

@@ -145,6 +145,29 @@ int vp8l_plane_dcodes(int w, uint8_t* tab) {
   return nd;
 }
 
+/* the shortest-path parse's candidate distances (model: dp_candidates): the
+ * first VP8L_DP_NC distinct plane-code distances >= 1 for width w, each as
+ * {distance, rows up, columns left, distance code} with the distance =
+ * rows * w + columns and |columns| <= w / 2 (the kernel's source pixel is
+ * the flat index p - distance, wrapping across a row end at most once).
+ * Returns the count. */
+int vp8l_dp_candidates(int w, int32_t* out) {
+  int n = 0;
+  for (int code = 1; code <= 120 && n < VP8L_DP_NC; ++code) {
+    const int d = plane_code_to_distance(w, code);
+    int dup = d < 1;
+    for (int i = 0; i < n; ++i) dup |= out[4 * i] == d;
+    if (dup) continue;
+    const int dy = (d + w / 2) / w;
+    out[4 * n + 0] = d;
+    out[4 * n + 1] = dy;
+    out[4 * n + 2] = d - dy * w;
+    out[4 * n + 3] = distance_code(w, d);
+    ++n;
+  }
+  return n;
+}
+
 /* the colour-indexing engine: coded width = bundled width, tile bits from
  * GetHistoBits with use_palette on the picture size (vp8l_enc.c:234-245) */
 /* histogram bits of a picture whose colours fit a palette (GetHistoBits

@@ -66,6 +66,7 @@ int vp8l_build_header(const vp8l_params* p, int has_alpha, int emode, int cache_
 
 /* distance -> smallest plane code table for width w (NULL: size only) */
 int vp8l_plane_dcodes(int w, uint8_t* tab);
+int vp8l_dp_candidates(int w, int32_t* out);   /* VP8L_DP_NC x {d, dy, dx, dcode} */
 
 /* RIFF + "VP8L" chunk header for a payload of `size` bytes (20 bytes) */
 void vp8l_riff_header(uint8_t out[20], size_t size);

@@ -77,6 +77,14 @@ extern "C" {
 #define VP8L_MODE_SUBGREEN 2
 #define VP8L_MODE_SPATIAL_SUBGREEN 3
 #define VP8L_MODE_PALETTE 4
+/* the shortest-path parse of frames without a predictor (direct / subtract
+ * green; model: dp_parse): candidate distances, longest copy, cost table
+ * (G with 2^MAX_CACHE_BITS cache symbols | R | B | A | D) per frame */
+#define VP8L_DP_ENABLED 1   /* oracle/vp8l_model.py: DP_ENABLED */
+#define VP8L_DP_NC 32
+#define VP8L_DP_MAXK 64
+#define VP8L_DP_NG (280 + (1 << VP8L_MAX_CACHE_BITS))
+#define VP8L_DP_NCOST (VP8L_DP_NG + 3 * 256 + 40)
 
 /* entries of one sparse tile histogram: at most NS symbols, at most 4 per
  * pixel of a (1 << hb)^2 tile */
@@ -168,11 +176,22 @@ typedef struct {
 /* lz != NULL (colour-indexed engines): no colour cache, the greedy parse
  * feeds two rounds of the cost-model parse over the hash chain's and the
  * candidate distances' matches */
+/* the shortest-path parse of frames without a predictor (k_vp8l_dp*): the
+ * slots' entropy modes (NULL: none of them), VP8L_DP_NC x {distance, rows,
+ * columns, code} candidates (host vp8l_dp_candidates) and n x VP8L_DP_NCOST
+ * symbol costs of scratch */
+typedef struct {
+  const uint8_t* fmode;
+  const int32_t* cand;
+  int ncand;
+  int32_t* costs;
+} vp8l_dp;
 int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p, const int32_t* tabs,
                         uint8_t* minb, uint32_t* cseg, uint16_t* prov, uint32_t* chist,
                         uint8_t* cbits,
                         uint32_t* ops, int64_t* feat, uint32_t* tl, uint32_t* tn,
-                        uint32_t* hc, uint8_t* assign, const vp8l_lz* lz, void* stream);
+                        uint32_t* hc, uint8_t* assign, const vp8l_lz* lz, const vp8l_dp* dp,
+                        void* stream);
 /* L6/L7: per-block bit counts, per-frame scan from start_bit[f], and the
  * bit writer into out (n x out_cap bytes, zeroed except the header words the
  * host placed at the start). end_bit[f] = total payload bits. */

@@ -731,3 +731,95 @@ def test_gpu_webpencode_lossless_api(gpu):
     L.WebPFree(out)
     assert np.array_equal(decode(got), a)
     assert got == M.encode(a, method=4)
+
+
+def _dp_parse_py(argb, hit, bits, act, clen, ccode):
+    """Pure-Python restatement of oracle/vp8l_dp.c (small pictures only)."""
+    H, W = argb.shape
+    dd = M.dp_candidates(W)
+    dcodes = [M.distance_code(W, d) for d in dd]
+    runs = M.match_lengths(argb, dd).reshape(len(dd), -1)
+    px = argb.ravel().astype(np.int64)
+    hv = hit.ravel() if bits else np.zeros(H * W, bool)
+    for _ in range(2):
+        (G, R, B, A, D), keys = M.dp_costs(argb, act, clen, ccode, bits)
+        dcost = []
+        for c in dcodes:
+            s, nb, _ = M.prefix_encode(c)
+            dcost.append(int(D[s]) + 256 * nb)
+        lcost = [0] * 65
+        for k in range(1, 65):
+            s, nb, _ = M.prefix_encode(k)
+            lcost[k] = int(G[256 + s]) + 256 * nb
+        a2 = np.zeros(H * W, np.int64); c2 = np.zeros(H * W, np.int64); d2 = np.zeros(H * W, np.int64)
+        for y in range(H):
+            cost = [0] * (W + 1); chk = [1] * W; chc = [0] * W
+            for j in range(W - 1, -1, -1):
+                q = y * W + j
+                a = int(px[q])
+                if hv[q]:
+                    best = cost[j + 1] + int(G[280 + keys[q]]) * 68 // 100
+                else:
+                    best = cost[j + 1] + (int(G[(a >> 8) & 255]) + int(R[(a >> 16) & 255]) +
+                                          int(B[a & 255]) + int(A[a >> 24])) * 82 // 100
+                bk, bc = 1, 0
+                for k in range(2, 65):
+                    if j + k > W:
+                        break
+                    cov = [(dcost[c], c) for c in range(len(dd)) if runs[c][q] >= k]
+                    if not cov:
+                        break
+                    dc, cc = min(cov)
+                    v = cost[j + k] + dc + lcost[k]
+                    if v < best:
+                        best, bk, bc = v, k, cc
+                cost[j] = best; chk[j] = bk; chc[j] = bc
+            j = 0
+            while j < W:
+                q = y * W + j
+                if chk[j] >= 2:
+                    a2[q] = 2; c2[q] = chk[j]; d2[q] = dcodes[chc[j]]
+                    a2[q + 1:q + chk[j]] = 3
+                    j += chk[j]
+                else:
+                    a2[q] = 1 if hv[q] else 0
+                    j += 1
+        act, clen, ccode = a2.reshape(H, W), c2.reshape(H, W), d2.reshape(H, W)
+    return act, clen, ccode
+
+
+@pytest.mark.parametrize("w,h,f,bits", [(24, 9, 0, 4), (17, 12, 1, 0), (5, 30, 2, 2), (1, 11, 3, 3)])
+def test_dp_parse_c_matches_python(w, h, f, bits):
+    """the shortest-path parse's C walk (oracle/vp8l_dp.c) equals its plain
+    restatement, on pictures with repeats at small 2-D offsets"""
+    rng = np.random.default_rng(f)
+    base = rng.integers(0, 5, size=(h, w)).astype(np.uint32)
+    img = np.zeros((h, w, 4), np.uint8)
+    img[..., 1] = (base * 40).astype(np.uint8)
+    img[..., 0] = ((base * 7) % 3 * 60).astype(np.uint8)
+    img[..., 3] = 255
+    img[h // 2:, : w // 2] = img[: h - h // 2, : w // 2]   # a repeat rows away
+    argb = M.to_argb(img)
+    flat = argb.ravel()
+    minb = M.cache_minb(flat).reshape(h, w)
+    hit = minb <= bits if bits else np.zeros((h, w), bool)
+    dists = M.candidate_distances(w)
+    act, clen, ccode = M.parse(argb, hit, dists)
+    got = M.dp_parse(argb, hit, bits, act, clen, ccode)
+    want = _dp_parse_py(argb, hit, bits, act, clen, ccode)
+    for g, w_ in zip(got, want):
+        assert np.array_equal(g, w_)
+
+
+def test_dp_parse_text_size_vs_reference():
+    """the direct-mode 1080p text fixture through the model with the
+    shortest-path parse: within 5% of the reference's size (was 1.31x with
+    the greedy parse)"""
+    import json
+    if not M.DP_ENABLED:
+        pytest.skip("shortest-path parse switched off (DP_ENABLED)")
+    c = [c for c in json.load(open(os.path.join(ROOT, "tests", "golden", "lossless_kat.json")))["cases"]
+         if c["kind"] == "text" and c["w"] == 1920][0]
+    img = lossless_picture(c["kind"], c["w"], c["h"], c["frame"])
+    got = M.encode(img)
+    assert len(got) <= c["size"] * 1.05, (len(got), c["size"])

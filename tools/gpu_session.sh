@@ -72,6 +72,10 @@ if has lphases; then   # L1a / L1 phase cycles (diagnostic build)
   WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_prof.so run timeout -k 10 150 \
     python3 tools/vp8l_phases.py 1920 1080 256 4 > $O/vp8l_phases.log 2>&1 || exit 1
 fi
+if has dptime; then   # lossless text frames (the shortest-path parse on every frame)
+  (cd /tmp && TMPDIR=/tmp run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+    -d $O/dpstats -o run -- python3 $R/tools/dp_time.py 64 > $O/dptime.json 2> $O/dptime.err) || exit 1
+fi
 if has lprof1; then   # the lossless kernels one instance at a time (solo durations)
   (cd /tmp && TMPDIR=/tmp run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
     -d $O/lstats1 -o run -- python3 $R/bench.py --lossless --no-cpu --no-host-input --steps 2 \

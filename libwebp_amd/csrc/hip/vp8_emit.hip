@@ -20,16 +20,18 @@
 //                      pairs packed densely onto the lanes)
 //   E2 k_emit_compose  per frame, chain the segment maps: every segment's true
 //                      start range and bit offset, pad bits, S and L
-//   E3 k_emit_seg      per segment (one lane each): forward pass with the true
-//                      start range -> (c_i, shift_i); reverse pass accumulating
-//                      the segment's part of N least-significant word first;
-//                      its low S_s bits tile N exactly (plain stores inside,
-//                      atomicOr on the two shared boundary words), the <= 8
-//                      bits above go to H_s
+//   E3 k_emit_seg      per segment (one lane each): one forward pass with the
+//                      true start range places every c_i at bit E_i of N, most
+//                      significant first (a 64-bit window sliding down a word
+//                      at a time); its low S_s bits tile N exactly (plain
+//                      stores inside, atomicOr on the two shared boundary
+//                      words), the <= 8 bits above go to H_s
 //   E4 k_emit_carry    adds every H_s at its segment's top with atomicAdd and
 //                      ripple carry (additions commute, so order is free)
 //   E5 k_emit_bytes    output byte k = bits [1 + 8(L-1-k), +8) of N, written
 //                      over the frame's (consumed) token buffer
+#include <stdlib.h>
+
 #include "vp8_dev.h"
 
 #define EMIT_SEG VP8G_EMIT_SEG   // tokens per segment
@@ -362,42 +364,88 @@ __device__ __forceinline__ void seg_chunk_put(uint32_t* lds, const uint4 v[8], i
   }
 }
 
-__device__ __forceinline__ void seg_chunk_store(const uint32_t* lds, uint16_t* base, uint32_t s0,
-                                                uint32_t nseg, uint32_t ntok, uint32_t c0,
-                                                int lane) {
-#pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const int q = lane + 64 * t, sg = q >> 3, part = q & 7;
-    const uint32_t i = (s0 + sg) * EMIT_SEG + c0 + 8 * part;
-    const uint32_t* d = lds + sg * SEG_ROW + 4 * part;
-    if (s0 + sg < nseg && i < ntok)
-      *reinterpret_cast<uint4*>(base + i) = make_uint4(d[0], d[1], d[2], d[3]);
+// The segment's bits of N, most significant first. Token i's c_i lands at
+// bit E_i = top - P_i (P_i: the segment's shifts before token i), so with the
+// true start range one forward pass places every c: the lane keeps the bits
+// [B, B + 64) of the sum in a 64-bit window and, once every later c lies below
+// B + 32 (p + 8 <= B + 32, p the current position), the window's upper word
+// can only change by a carry out of the lower one, so it is staged (LDS, one
+// column per lane) and the window slides down 32 bits. A carry out of the
+// window needs its upper word all ones (about 2^-32 per word); it ripples into
+// the words already written. Bits at or above top go to H_s, the word that
+// straddles top is kept in a register until the end (the segment above ORs its
+// low bits into the same word), the word that straddles T is ORed.
+struct seg_sink {
+  uint32_t* W;
+  int T, top;
+  uint32_t topw, H;
+};
+__device__ __forceinline__ void seg_put(seg_sink& o, int wp, uint32_t v) {
+  if (!v) return;   // the words start zeroed
+  if (wp + 32 <= o.top) {
+    if (wp >= o.T) o.W[wp >> 5] = v;
+    else atomicOr(o.W + (wp >> 5), v);   // the bottom word, shared with the segment below
+  } else if (wp < o.top) {
+    const int k = o.top - wp;
+    o.topw += v & ((1u << k) - 1u);
+    o.H += v >> k;
+  } else if (wp - o.top < 32) {
+    o.H += v << (wp - o.top);
   }
 }
+__device__ __noinline__ void seg_carry(seg_sink& o, int q) {   // +1 at bit q (> T)
+  __threadfence();   // the words this lane stored before
+  for (;;) {
+    const int wp = q & ~31;
+    if (q >= o.top) { o.H += 1u << (q - o.top); return; }
+    if (wp + 32 > o.top) {
+      const int k = o.top - wp;
+      o.topw += 1u << (q - wp);
+      if (o.topw >> k) { o.topw -= 1u << k; o.H += 1; }
+      return;
+    }
+    const uint32_t add = 1u << (q & 31);
+    const uint32_t old = atomicAdd(o.W + (wp >> 5), add);
+    if (old + add >= old) return;
+    q = wp + 32;
+  }
+}
+#define SEG_STG 16   // staged words per lane: a chunk shifts at most 7 * SEG_CH bits
+__device__ __forceinline__ void seg_unstage(seg_sink& o, const uint32_t* stg, int& nst, int B,
+                                            int lane) {
+  // staged word i sits at B + 64 + 32 (nst - 1 - i)
+  for (int i = 0; i < nst; ++i) seg_put(o, B + 64 + 32 * (nst - 1 - i), stg[i * 64 + lane]);
+  nst = 0;
+}
 
-__global__ __launch_bounds__(64) void k_emit_seg(uint16_t* __restrict__ tokens, size_t tok_cap,
+__global__ __launch_bounds__(64) void k_emit_seg(const uint16_t* __restrict__ tokens, size_t tok_cap,
                                                  const vp8g_frame_result* __restrict__ results,
                                                  const vp8g_emit_meta* __restrict__ meta,
                                                  vp8g_emit_seg* __restrict__ segs,
                                                  uint32_t* __restrict__ nbuf) {
   __shared__ uint32_t lds[64 * SEG_ROW];
+  __shared__ uint32_t stg[SEG_STG * 64];
   __shared__ __align__(4) uint8_t prob[VP8G_NUM_SLOTS];
   const int f = blockIdx.y, lane = threadIdx.x;
   const uint32_t s0 = blockIdx.x * 64, s = s0 + lane;
   const vp8g_emit_meta M = meta[f];
   if (s0 >= M.nseg) return;   // whole wave
   const bool valid = s < M.nseg;
-  vp8g_emit_seg g = valid ? segs[M.seg_base + s] : vp8g_emit_seg{0, 0, 254, 0};
+  const vp8g_emit_seg g = valid ? segs[M.seg_base + s] : vp8g_emit_seg{0, 0, 254, 0};
   const uint32_t i0 = s * EMIT_SEG;
   const uint32_t cnt = valid ? min((uint32_t)EMIT_SEG, M.ntok - i0) : 0u;
-  uint16_t* base = tokens + M.tok_off;
-  uint32_t* row = lds + lane * SEG_ROW;
+  const uint16_t* base = tokens + M.tok_off;
+  const uint32_t* row = lds + lane * SEG_ROW;
   // the chunks this wave needs: up to its longest segment
   const uint32_t last_s = min(s0 + 64, M.nseg) - 1;
   const uint32_t span = min((uint32_t)EMIT_SEG, M.ntok - last_s * EMIT_SEG) == EMIT_SEG || last_s > s0
                             ? (uint32_t)EMIT_SEG
                             : M.ntok - last_s * EMIT_SEG;
-  // forward: true range chain -> (c, shift) packed in place
+  seg_sink o{nbuf + M.nb_base, (int)g.T, (int)(g.T + g.S), 0u, 0u};
+  int p = o.top;                 // the bit the next c lands on
+  int B = (o.top - 24) & ~31;    // window [B, B + 64); top - B in [24, 55]
+  uint64_t acc = 0;
+  int nst = 0;
   load_probas(prob, results, M, lane, 64);
   int r = g.rs;
   uint4 nv[8];
@@ -406,75 +454,43 @@ __global__ __launch_bounds__(64) void k_emit_seg(uint16_t* __restrict__ tokens, 
     seg_chunk_put(lds, nv, lane);
     __syncthreads();
     if (c0 + SEG_CH < span) seg_chunk_fetch(nv, base, s0, M.nseg, M.ntok, c0 + SEG_CH, lane);
-#pragma unroll 4
+#pragma unroll 2
     for (int k = 0; k < SEG_CH / 2; ++k) {
-      uint32_t w = resolve_pair(row[k], prob);
+      const uint32_t w = resolve_pair(row[k], prob);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const uint32_t pb = (w >> (16 * h)) & 0xffff;
         const int split = (int)(__umul24((unsigned)r, pb & 0xff) >> 8);   // full-rate 24-bit multiply
         const int bit = (pb >> 8) & 1;
-        const int c = bit ? split + 1 : 0;
+        const uint32_t c = bit ? (uint32_t)split + 1u : 0u;
         int rr = bit ? r - split - 1 : split;
         const int sh = renorm(rr);
-        const bool live = c0 + 2 * k + h < cnt;
-        r = live ? rr : r;
-        const uint32_t pk = live ? (uint32_t)(c | (sh << 8)) : 0u;
-        w = (w & ~(0xffffu << (16 * h))) | (pk << (16 * h));
-      }
-      row[k] = w;
-    }
-    __syncthreads();
-    seg_chunk_store(lds, base, s0, M.nseg, M.ntok, c0, lane);
-    __syncthreads();
-  }
-  // reverse: least-significant first; bits below the current position are final
-  uint32_t* W = nbuf + M.nb_base;
-  const uint32_t T = g.T, top = T + g.S;
-  uint32_t wb = T & ~31u;      // global bit index of acc's bit 0
-  uint64_t acc = 0;
-  uint32_t E = 0;
-  const uint32_t nch = (span + SEG_CH - 1) / SEG_CH;
-  seg_chunk_fetch(nv, base, s0, M.nseg, M.ntok, (nch - 1) * SEG_CH, lane);
-  for (uint32_t ch = nch; ch > 0; --ch) {
-    const uint32_t c0 = (ch - 1) * SEG_CH;
-    seg_chunk_put(lds, nv, lane);   // (c, shift); 0 past the end
-    __syncthreads();
-    if (ch > 1) seg_chunk_fetch(nv, base, s0, M.nseg, M.ntok, c0 - SEG_CH, lane);
-    for (int k = SEG_CH / 2 - 1; k >= 0; --k) {
-      const uint32_t w = row[k];
-#pragma unroll
-      for (int h = 1; h >= 0; --h) {
-        const uint32_t pk = c0 + 2 * k + h < cnt ? (w >> (16 * h)) & 0xffff : 0u;
-        E += pk >> 8;
-        const uint32_t G = T + E;
-        while (G >= wb + 32) {   // word [wb, wb+32) is final
-          const uint32_t lo = (uint32_t)acc;
-          const uint32_t mlo = wb < T ? (~0u << (T - wb)) : ~0u;
-          if (mlo != ~0u) atomicOr(W + (wb >> 5), lo & mlo);
-          else W[wb >> 5] = lo;
-          acc >>= 32;
-          wb += 32;
+        if (c0 + 2 * k + h < cnt) {
+          r = rr;
+          const uint64_t na = acc + ((uint64_t)c << (p - B));   // p - B in [17, 56]
+          if (na < acc) {   // carry out of the window
+            seg_unstage(o, stg, nst, B, lane);
+            seg_carry(o, B + 64);
+          }
+          acc = na;
+          p -= sh;
+          if (p - B <= 24) {   // the upper word is final but for carries
+            stg[nst * 64 + lane] = (uint32_t)(acc >> 32);
+            ++nst;
+            acc <<= 32;
+            B -= 32;
+          }
         }
-        acc += (uint64_t)(pk & 0xff) << (G - wb);
       }
     }
+    if (nst) seg_unstage(o, stg, nst, B, lane);
     __syncthreads();
   }
   if (!valid) return;
-  // remaining words up to the region top; bits above it are H_s
-  while (wb < top) {
-    const uint32_t lo = (uint32_t)acc;
-    uint32_t m = ~0u;
-    if (wb < T) m &= ~0u << (T - wb);
-    if (top < wb + 32) m &= (1u << (top - wb)) - 1u;
-    if (m != ~0u) atomicOr(W + (wb >> 5), lo & m);
-    else W[wb >> 5] = lo;
-    if (top < wb + 32) break;
-    acc >>= 32;
-    wb += 32;
-  }
-  segs[M.seg_base + s].H = (uint8_t)((acc >> (top - wb)) & 0xff);
+  seg_put(o, B + 32, (uint32_t)(acc >> 32));
+  seg_put(o, B, (uint32_t)acc);
+  if ((o.top & 31) && o.topw) atomicOr(o.W + (o.top >> 5), o.topw);
+  segs[M.seg_base + s].H = (uint8_t)o.H;
 }
 
 // big-number add of h at bit b (h < 256) with ripple carry, via atomics
@@ -563,6 +579,73 @@ extern "C" int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
   hipLaunchKernelGGL(k_emit_bytes, dim3((maxL + 1023) / 1024, n), dim3(256), 0, st, tokens, tok_cap,
                      (const vp8g_emit_meta*)meta, (const uint32_t*)nbuf);
   return vp8g_launch_check("k_emit_bytes");
+}
+
+// K4 on caller-given token streams (fixed-probability tokens: bit << 15 |
+// 1 << 14 | probability), for tests that drive the coder with streams the
+// encoder rarely makes (long all-ones runs: the carry paths). Streams are
+// concatenated in host_tokens; stream s's bytes go to host_out + s * out_stride,
+// its size to out_size[s]. Returns 0 on any HIP error or a too small stride.
+extern "C" __attribute__((visibility("default"))) int vp8g_emit_streams(
+    const uint16_t* host_tokens, const uint32_t* ntok, int n, uint8_t* host_out,
+    uint32_t out_stride, uint32_t* out_size) {
+  if (n <= 0) return 1;
+  vp8g_emit_meta* meta = (vp8g_emit_meta*)calloc((size_t)n, sizeof(vp8g_emit_meta));
+  if (!meta) return 0;
+  size_t off = 0, segs = 0, words = 0, src = 0;
+  uint32_t max_ntok = 0, max_seg = 0;
+  for (int s = 0; s < n; ++s) {
+    vp8g_emit_meta& m = meta[s];
+    m.ntok = ntok[s];
+    m.frame = (uint32_t)s;
+    m.tok_off = off;
+    m.nseg = (m.ntok + EMIT_SEG - 1) / EMIT_SEG;
+    m.seg_base = (uint32_t)segs;
+    m.nb_base = (uint32_t)words;
+    segs += m.nseg;
+    words += (7 * (size_t)m.ntok + 17 + 8 + 63) / 32 + 4;
+    off += ((size_t)m.ntok + 64 + 7) & ~(size_t)7;   // room for the bytes of a short stream
+    max_ntok = m.ntok > max_ntok ? m.ntok : max_ntok;
+    max_seg = m.nseg > max_seg ? m.nseg : max_seg;
+    if ((7ull * m.ntok + 48) / 8 + 2 > out_stride) { free(meta); return 0; }
+  }
+  uint16_t* d_tok = nullptr; vp8g_frame_result* d_res = nullptr; vp8g_emit_meta* d_meta = nullptr;
+  uint8_t *d_emap = nullptr, *d_img = nullptr; uint16_t* d_eshift = nullptr;
+  vp8g_emit_seg* d_segs = nullptr; uint32_t *d_nbuf = nullptr, *d_size = nullptr;
+  const size_t cs = segs + 1;
+  bool ok = hipMalloc((void**)&d_tok, off * 2) == hipSuccess &&
+            hipMalloc((void**)&d_res, (size_t)n * sizeof(vp8g_frame_result)) == hipSuccess &&
+            hipMalloc((void**)&d_meta, (size_t)n * sizeof(vp8g_emit_meta)) == hipSuccess &&
+            hipMalloc((void**)&d_emap, cs * 128) == hipSuccess &&
+            hipMalloc((void**)&d_eshift, cs * 128 * sizeof(uint16_t)) == hipSuccess &&
+            hipMalloc((void**)&d_img, cs * 17) == hipSuccess &&
+            hipMalloc((void**)&d_segs, cs * sizeof(vp8g_emit_seg)) == hipSuccess &&
+            hipMalloc((void**)&d_nbuf, (words + 1) * sizeof(uint32_t)) == hipSuccess &&
+            hipMalloc((void**)&d_size, (size_t)n * sizeof(uint32_t)) == hipSuccess;
+  ok = ok && hipMemset(d_res, 0, (size_t)n * sizeof(vp8g_frame_result)) == hipSuccess &&
+       hipMemset(d_nbuf, 0, (words + 1) * sizeof(uint32_t)) == hipSuccess &&
+       hipMemset(d_tok, 0, off * 2) == hipSuccess &&
+       hipMemcpy(d_meta, meta, (size_t)n * sizeof(vp8g_emit_meta), hipMemcpyHostToDevice) == hipSuccess;
+  for (int s = 0; ok && s < n; ++s) {
+    if (meta[s].ntok)
+      ok = hipMemcpy(d_tok + meta[s].tok_off, host_tokens + src, meta[s].ntok * 2,
+                     hipMemcpyHostToDevice) == hipSuccess;
+    src += meta[s].ntok;
+  }
+  ok = ok && vp8g_launch_emit(d_tok, off, n, d_res, d_meta, max_ntok, max_seg, d_emap, d_eshift,
+                              d_img, d_segs, d_nbuf, d_size, 0);
+  ok = ok && hipDeviceSynchronize() == hipSuccess &&
+       hipMemcpy(out_size, d_size, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost) == hipSuccess;
+  for (int s = 0; ok && s < n; ++s) {
+    if (out_size[s] > out_stride) { ok = false; break; }
+    if (out_size[s])
+      ok = hipMemcpy(host_out + (size_t)s * out_stride, d_tok + meta[s].tok_off, out_size[s],
+                     hipMemcpyDeviceToHost) == hipSuccess;
+  }
+  void* bufs[] = {d_tok, d_res, d_meta, d_emap, d_eshift, d_img, d_segs, d_nbuf, d_size};
+  for (void* b : bufs) (void)hipFree(b);
+  free(meta);
+  return ok ? 1 : 0;
 }
 
 // Gather every stream's bytes (at its token offset) into one packed buffer at

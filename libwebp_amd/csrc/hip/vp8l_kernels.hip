@@ -3215,10 +3215,11 @@ __global__ __launch_bounds__(64) void k_vp8l_dp(const uint32_t* __restrict__ arg
   const int oR = VP8L_DP_NG, oB = oR + 256, oA = oB + 256, oD = oA + 256;
   for (int i = ln; i < VP8L_DP_NCOST; i += 64) S.cost[i] = costs[(size_t)f * VP8L_DP_NCOST + i];
   __syncthreads();
-  if (ln >= 1 && ln <= VP8L_DP_MAXK) {
+  static_assert(VP8L_DP_MAXK <= 64, "one lane per copy length");
+  if (ln < VP8L_DP_MAXK) {   // lengths 1..64 on lanes 0..63
     int sym, nb; uint32_t ex;
-    prefix_enc((uint32_t)ln, sym, nb, ex);
-    S.lcost[ln] = S.cost[256 + sym] + 256 * nb;
+    prefix_enc((uint32_t)ln + 1u, sym, nb, ex);
+    S.lcost[ln + 1] = S.cost[256 + sym] + 256 * nb;
   }
   int4 cv = make_int4(0, 0, 0, 0);
   if (ln < ncand) {

@@ -1129,9 +1129,12 @@ static int run_passes(WebPGpuBatch* b, int n) {
       if (b->h_active[f])
         for (int s = 0; s < 4; ++s) b->frames[f].seg_fstrength[s] = b->h_aflevel[4 * f + s];
   }
-  CHK(hipMemcpyAsync(b->h_mbinfo, b->d_mbinfo, n * nmb * VP8G_MBINFO_BYTES,
-                     hipMemcpyDeviceToHost, st));
   CHK(hipStreamSynchronize(st));
+  if (!d2h_sdma_download(b->device, b->h_mbinfo, b->d_mbinfo, n * nmb * VP8G_MBINFO_BYTES)) {
+    CHK(hipMemcpyAsync(b->h_mbinfo, b->d_mbinfo, n * nmb * VP8G_MBINFO_BYTES,
+                       hipMemcpyDeviceToHost, st));
+    CHK(hipStreamSynchronize(st));
+  }
   return 1;
 fail:
   return 0;
@@ -1279,7 +1282,9 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
       if (!vp8g_launch_pack(b->d_tokens, b->d_emeta, ns, b->d_poff, b->d_psize, max_size, b->d_part,
                             st))
         goto fail;
-      CHK(hipMemcpyAsync(b->h_part, b->d_part, total, hipMemcpyDeviceToHost, st));
+      CHK(hipStreamSynchronize(st));   /* then the bytes come back on a copy engine */
+      if (!d2h_sdma_download(b->device, b->h_part, b->d_part, total))
+        CHK(hipMemcpyAsync(b->h_part, b->d_part, total, hipMemcpyDeviceToHost, st));
     }
   }
   CHK(hipStreamSynchronize(st));

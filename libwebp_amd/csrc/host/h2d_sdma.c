@@ -1,4 +1,4 @@
-/* Host -> device uploads of pinned frames on a copy (SDMA) engine.
+/* Host <-> device copies of pinned buffers on a copy (SDMA) engine.
  *
  * With hipMemcpyAsync the host-input bench line sat ≈ 32 ms per 256 × 1080p
  * batch below the HBM-resident one -- about the upload's PCIe time
@@ -7,7 +7,9 @@
  * K3 holds every CU (its VGPRs fill the register file) a blit kernel waits
  * for it and then holds CU slots for the whole transfer.
  * hsa_amd_memory_async_copy puts the transfer on an SDMA engine, which needs
- * no CU. The calling engine thread waits for the copy's signal
+ * no CU. The batch's big downloads (the packed .webp partitions, the MB
+ * info) go the same way: as blit kernels they waited behind the other
+ * instances' K3 (up to 100 ms in kernel_stats_r4z.csv). The calling engine thread waits for the copy's signal
  * (its own stream is idle at that point: every batch call drains it before
  * returning). */
 #include "h2d_sdma.h"
@@ -25,6 +27,7 @@ typedef struct {
   int ok;              /* 1 usable, -1 unusable, 0 not looked up yet */
   hsa_agent_t gpu, cpu;
   pthread_mutex_t up;  /* one upload at a time per device (see below) */
+  pthread_mutex_t down;
 } dev_agents;
 
 static dev_agents g_dev[MAX_DEV];
@@ -72,6 +75,7 @@ static int lookup(int device) {
     }
     g_dev[device].ok = (c.found_gpu && c.found_cpu) ? 1 : -1;
     pthread_mutex_init(&g_dev[device].up, NULL);
+    pthread_mutex_init(&g_dev[device].down, NULL);
     g_dev[device].gpu = c.gpu;
     g_dev[device].cpu = c.cpu;
   }
@@ -80,25 +84,24 @@ static int lookup(int device) {
   return ok;
 }
 
-int h2d_sdma_upload(int device, void* dst, const void* src, size_t bytes) {
-  static int mode = -1;   /* LIBWEBP_AMD_H2D=hip keeps the runtime's copy (A/B) */
+static int sdma_mode(void) {   /* LIBWEBP_AMD_H2D=hip keeps the runtime's copies (A/B) */
+  static int mode = -1;
   if (mode < 0) {
     const char* v = getenv("LIBWEBP_AMD_H2D");
     mode = (v && v[0] == 'h') ? 0 : 1;
   }
-  if (!mode || !lookup(device)) return 0;
-  /* Uploads to one device go one after another: they share the PCIe link
-     anyway, and in turn the first engine's frames are on the device after one
-     transfer time instead of all engines' after three (its kernels start
-     while the next engine uploads). */
-  pthread_mutex_lock(&g_dev[device].up);
+  return mode;
+}
+
+static int sdma_copy(pthread_mutex_t* mu, void* dst, hsa_agent_t dst_agent, const void* src,
+                     hsa_agent_t src_agent, size_t bytes) {
+  pthread_mutex_lock(mu);
   hsa_signal_t sig;
   if (hsa_signal_create(1, 0, NULL, &sig) != HSA_STATUS_SUCCESS) {
-    pthread_mutex_unlock(&g_dev[device].up);
+    pthread_mutex_unlock(mu);
     return 0;
   }
-  const hsa_status_t st = hsa_amd_memory_async_copy(dst, g_dev[device].gpu, src, g_dev[device].cpu,
-                                                    bytes, 0, NULL, sig);
+  const hsa_status_t st = hsa_amd_memory_async_copy(dst, dst_agent, src, src_agent, bytes, 0, NULL, sig);
   int ok = 0;
   if (st == HSA_STATUS_SUCCESS) {
     while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
@@ -107,6 +110,23 @@ int h2d_sdma_upload(int device, void* dst, const void* src, size_t bytes) {
     ok = 1;
   }
   hsa_signal_destroy(sig);
-  pthread_mutex_unlock(&g_dev[device].up);
+  pthread_mutex_unlock(mu);
   return ok;
+}
+
+int h2d_sdma_upload(int device, void* dst, const void* src, size_t bytes) {
+  if (!sdma_mode() || !lookup(device)) return 0;
+  /* Uploads to one device go one after another: they share the PCIe link
+     anyway, and in turn the first engine's frames are on the device after one
+     transfer time instead of all engines' after three (its kernels start
+     while the next engine uploads). */
+  dev_agents* d = &g_dev[device];
+  return sdma_copy(&d->up, dst, d->gpu, src, d->cpu, bytes);
+}
+
+int d2h_sdma_download(int device, void* dst, const void* src, size_t bytes) {
+  if (!bytes) return 1;
+  if (!sdma_mode() || !lookup(device)) return 0;
+  dev_agents* d = &g_dev[device];
+  return sdma_copy(&d->down, dst, d->cpu, src, d->gpu, bytes);
 }

@@ -8,4 +8,8 @@
  * hipMemcpy). */
 int h2d_sdma_upload(int device, void* dst, const void* src, size_t bytes);
 
+/* The other direction: device memory of `device` to pinned host memory.
+ * The caller has drained the stream that produced `src`. */
+int d2h_sdma_download(int device, void* dst, const void* src, size_t bytes);
+
 #endif

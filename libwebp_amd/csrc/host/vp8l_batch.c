@@ -13,6 +13,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include "h2d_sdma.h"
 #include "gpu_engine.h"
 #include "vp8l_batch.h"
 #include "vp8l_host.h"
@@ -467,9 +468,14 @@ static int pipeline(vp8l_engine* l, hipStream_t st, int threads, const uint8_t* 
   for (int f = 0; f <= n; ++f) l->h_poff[f] = l->out_off[f];
   CHK(hipMemcpyAsync(l->d_poff, l->h_poff, (N + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
   if (!vp8l_launch_pack(l->d_out, l->out_cap, l->d_poff, l->d_end, n, l->d_packed, st)) goto fail;
-  CHK(hipMemcpyAsync(l->h_out, l->d_packed, l->out_off[n] + 16 <= l->d_packed_cap ?
-                     l->out_off[n] + 16 : l->out_off[n], hipMemcpyDeviceToHost, st));
-  CHK(hipStreamSynchronize(st));
+  {
+    const size_t down = l->out_off[n] + 16 <= l->d_packed_cap ? l->out_off[n] + 16 : l->out_off[n];
+    CHK(hipStreamSynchronize(st));   /* the bytes come back on a copy engine (h2d_sdma.c) */
+    if (!d2h_sdma_download(l->device, l->h_out, l->d_packed, down)) {
+      CHK(hipMemcpyAsync(l->h_out, l->d_packed, down, hipMemcpyDeviceToHost, st));
+      CHK(hipStreamSynchronize(st));
+    }
+  }
   t4 = now_us();
   for (int f = 0; f < n; ++f) {
     if (!l->out_size[f]) continue;

@@ -258,6 +258,11 @@ int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
                      uint8_t* img, vp8g_emit_seg* segs, uint32_t* nbuf, uint32_t* out_size,
                      void* stream);
 
+/* K4 alone on caller-given fixed-probability token streams (host memory in
+ * and out; test hook, see hip/vp8_emit.hip) */
+int vp8g_emit_streams(const uint16_t* host_tokens, const uint32_t* ntok, int n, uint8_t* host_out,
+                      uint32_t out_stride, uint32_t* out_size);
+
 /* K4 tail: copy each stream's bytes (size[s] bytes at tokens +
  * meta[s].tok_off) to dst + off[s]; off[s] must be 16-byte aligned. */
 int vp8g_launch_pack(const uint16_t* tokens, const vp8g_emit_meta* meta, int n,

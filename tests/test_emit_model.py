@@ -118,3 +118,151 @@ def test_segmented_model_matches_reference_coder():
             toks.append((b, p))
         seg = rng.choice([1, 3, 64, 200, 2048])
         assert seg_coder(toks, seg) == ref_coder(toks)
+
+
+def window_coder(toks, seg, wd=32, stats=None):
+    """E1-E5 with E3 as k_emit_seg runs it: one forward pass per segment that
+    places c_i most significant first through a 2*wd-bit window sliding down
+    wd bits at a time, staged words, carries out of the window rippling into
+    the words already written, the top-straddling word held back and the bits
+    above the segment's top in H (added by E4). wd=32 is the kernel; a smaller
+    wd makes the carry path frequent."""
+    n = len(toks)
+    nseg = (n + seg - 1) // seg
+    mask = (1 << wd) - 1
+    thr = wd - 8                      # rebase once p - B <= thr
+    assert thr >= 7
+    r, cum, starts = 254, 0, []
+    for s in range(nseg):             # E1/E2: true start ranges and shift counts
+        starts.append((r, cum))
+        for b, p in toks[s * seg:(s + 1) * seg]:
+            r, _, k = _step(r, b, p)
+            cum += k
+    t = cum - 8
+    nb = t if t <= 0 else t - 8 * ((t + 7) // 8)
+    spad = 0
+    for _ in range(9 - nb):
+        r, _, k = _step(r, 0, 128)
+        spad += k
+    S = cum + spad
+    L = (S + 7) // 8
+    W = {}
+    Hs = []
+    for s in range(nseg):
+        r, before = starts[s]
+        part = toks[s * seg:(s + 1) * seg]
+        segS = sum(_step_chain(r, part))
+        top = S - before
+        T = top - segS
+        o = {"topw": 0, "H": 0}
+
+        def put(wp, v):
+            if not v:
+                return
+            assert wp >= 0
+            if wp + wd <= top:
+                if wp >= T:
+                    assert W.get(wp // wd, 0) == 0
+                    W[wp // wd] = v
+                else:
+                    W[wp // wd] = W.get(wp // wd, 0) | v
+            elif wp < top:
+                k = top - wp
+                o["topw"] += v & ((1 << k) - 1)
+                o["H"] += v >> k
+            else:
+                o["H"] += v << (wp - top)
+
+        def carry(q):
+            if stats is not None:
+                stats["carries"] = stats.get("carries", 0) + 1
+            while True:
+                wp = q - q % wd
+                if q >= top:
+                    o["H"] += 1 << (q - top)
+                    return
+                if wp + wd > top:
+                    k = top - wp
+                    o["topw"] += 1 << (q - wp)
+                    if o["topw"] >> k:
+                        o["topw"] -= 1 << k
+                        o["H"] += 1
+                    return
+                old = W.get(wp // wd, 0)
+                W[wp // wd] = (old + (1 << (q - wp))) & mask
+                if old + (1 << (q - wp)) <= mask:
+                    return
+                q = wp + wd
+
+        p = top
+        B = (top - thr) - (top - thr) % wd
+        acc, stg = 0, []
+        for b, pr in part:
+            r, c, k = _step(r, b, pr)
+            assert thr - 7 <= p - B <= 2 * wd - 8
+            na = acc + (c << (p - B))
+            if na >> (2 * wd):
+                for i, v in enumerate(stg):
+                    put(B + 2 * wd + wd * (len(stg) - 1 - i), v)
+                stg = []
+                carry(B + 2 * wd)
+                na &= (1 << (2 * wd)) - 1
+            acc = na
+            p -= k
+            if p - B <= thr:
+                stg.append(acc >> wd)
+                acc = (acc & mask) << wd
+                B -= wd
+        assert p == T
+        for i, v in enumerate(stg):
+            put(B + 2 * wd + wd * (len(stg) - 1 - i), v)
+        put(B + wd, acc >> wd)
+        put(B, acc & mask)
+        if top % wd and o["topw"]:
+            W[top // wd] = W.get(top // wd, 0) | o["topw"]
+        assert o["H"] < 256
+        Hs.append((top, o["H"]))
+    N = sum(v << (wd * i) for i, v in W.items())
+    for top, h in Hs:                 # E4: H_s added at the segment's top
+        N += h << top
+    return (N >> 1).to_bytes(L, "big") if L else b""
+
+
+def _step_chain(r, part):
+    for b, p in part:
+        r, _, k = _step(r, b, p)
+        yield k
+
+
+def _carry_heavy(rng, n):
+    """Long runs of 1 bits push the coder's low end towards the top of its
+    interval: all-ones words, then carries."""
+    toks = []
+    while len(toks) < n:
+        if rng.random() < 0.5:
+            p = rng.choice([128, 200, 250, 16])
+            toks.extend([(1, p)] * rng.randint(5, 120))
+        else:
+            for _ in range(rng.randint(1, 20)):
+                p = rng.randint(1, 255)
+                toks.append((rng.randint(0, 1), p))
+    return toks[:n]
+
+
+def test_window_pass_matches_reference_coder():
+    rng = random.Random(11)
+    st16, st32 = {}, {}
+    for it in range(120):
+        n = rng.randint(0, 3000)
+        if it % 2:
+            toks = _carry_heavy(rng, n)
+        else:
+            toks = []
+            for _ in range(n):
+                p = rng.randint(1, 255)
+                toks.append((1 if rng.random() * 256 >= p else 0, p))
+        seg = rng.choice([1, 3, 64, 200, 2048])
+        want = ref_coder(toks)
+        assert window_coder(toks, seg, 32, st32) == want
+        assert window_coder(toks, seg, 15, st16) == want
+    assert st16.get("carries", 0) > 20   # the carry path ran

@@ -18,9 +18,6 @@
 //      k_emit_maps     per segment, the end range and shift count from each
 //                      of those start ranges (the group's (segment, start)
 //                      pairs packed densely onto the lanes)
-//      k_emit_suffix   the segments whose chains all met within the first
-//                      MAP_CH tokens (most): k_emit_maps stops there and one
-//                      lane per segment runs the single chain to the end
 //   E2 k_emit_compose  per frame, chain the segment maps: every segment's true
 //                      start range and bit offset, pad bits, S and L
 //   E3 k_emit_seg      per segment (one lane each): one forward pass with the
@@ -87,7 +84,6 @@ __device__ __forceinline__ void load_probas(uint8_t* prob, const vp8g_frame_resu
 // Segment 0 starts at 254.
 #define EMIT_IMG 256
 #define EMIT_SLOTS 16
-#define IMG_STRIDE VP8G_EMIT_IMG_BYTES   // count, EMIT_SLOTS ranges, suffix flag
 #define IMG_G 16                     // segments per wavefront (4 lanes each for the maps)
 #define IMG_ROW (EMIT_IMG + 8)       // u16; +16 B per row: conflict-free b128 reads
 __global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ tokens,
@@ -167,7 +163,7 @@ __global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ to
   }
   // output: the end set of each segment (lanes of segment mg, word mw)
   if (ms >= M.nseg) return;
-  uint8_t* out = img + ((size_t)M.seg_base + ms) * IMG_STRIDE;
+  uint8_t* out = img + ((size_t)M.seg_base + ms) * (EMIT_SLOTS + 1);
   if (!mact) {   // segment 0
     if (mw == 0) { out[0] = 1; out[1] = 254; }
     return;
@@ -188,11 +184,6 @@ __global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ to
 // more than 64 pairs take further rounds. The group's tokens go through LDS
 // MAP_CH per segment at a time (the next chunk is loaded into registers while
 // this one runs), so the chains read LDS broadcasts instead of global loads.
-// The chains of one segment merge fast (two equal ranges stay equal): when
-// after the first MAP_CH tokens every segment of the group is down to one
-// range, the group stops there -- each pair's shift count so far and the
-// common range go out, the segment's suffix flag holds the range -- and
-// k_emit_suffix carries the one chain on, one lane per segment.
 #define MAP_G 8
 #define MAP_CH 256
 #define MAP_ROW (MAP_CH + 8)   // u16; +16 B per row: the 16 rows' b128 reads hit distinct banks
@@ -201,7 +192,7 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
                                                   size_t tok_cap,
                                                   const vp8g_frame_result* __restrict__ results,
                                                   const vp8g_emit_meta* __restrict__ meta,
-                                                  uint8_t* __restrict__ img,
+                                                  const uint8_t* __restrict__ img,
                                                   uint8_t* __restrict__ emap,
                                                   uint16_t* __restrict__ eshift) {
   __shared__ __align__(16) uint16_t stage[MAP_G * MAP_ROW];
@@ -213,7 +204,7 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
   // pair counts of the group's segments (lanes 0..MAP_G-1), inclusive scan
   int nk = 0;
   if (lane < MAP_G && sbase + lane < M.nseg) {
-    const int ni = img[((size_t)M.seg_base + sbase + lane) * IMG_STRIDE];
+    const int ni = img[((size_t)M.seg_base + sbase + lane) * (EMIT_SLOTS + 1)];
     nk = ni == 0xff ? 128 : ni;
   }
   int incl = nk;
@@ -234,7 +225,6 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
       if (sbase + sg < M.nseg && i < M.ntok) v[t] = *reinterpret_cast<const uint4*>(ftok + i);
     }
   };
-  const bool may_merge = total <= 64;   // one round: the group's pairs all on this wave
   for (int p0 = 0; p0 < total; p0 += 64) {
     const int p = p0 + lane;   // this lane's pair
     int g = 0, excl = 0;
@@ -245,7 +235,7 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
     }
     const bool live = p < total;
     const uint32_t s = sbase + (live ? g : 0);
-    const uint8_t* im = img + ((size_t)M.seg_base + s) * IMG_STRIDE;
+    const uint8_t* im = img + ((size_t)M.seg_base + s) * (EMIT_SLOTS + 1);
     const int k = p - excl;
     const int r0 = !live ? 127 : im[0] == 0xff ? 127 + k : im[1 + k];
     const uint32_t cnt = live ? min((uint32_t)EMIT_SEG, M.ntok - s * EMIT_SEG) : 0u;
@@ -274,27 +264,11 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
       } else {
         for (uint32_t i = 0; i < n; ++i) S += chain_step(r, st[i]);   // frame's last segment
       }
-      if (c0 == 0 && may_merge) {
-        const int rf = __shfl(r, excl);   // the segment's first pair
-        // (segments that end inside the chunk are complete whatever their chains did)
-        if (!__ballot(live && cnt > MAP_CH && r != rf)) {   // merged: k_emit_suffix goes on
-          if (live) {
-            const size_t o = ((size_t)M.seg_base + s) * 128 + (r0 - 127);
-            emap[o] = (uint8_t)r;
-            eshift[o] = (uint16_t)S;
-            if (p == excl)
-              img[((size_t)M.seg_base + s) * IMG_STRIDE + IMG_STRIDE - 1] =
-                  cnt > MAP_CH ? (uint8_t)r : 0;
-          }
-          return;
-        }
-      }
     }
     if (live) {
       const size_t o = ((size_t)M.seg_base + s) * 128 + (r0 - 127);
       emap[o] = (uint8_t)r;
       eshift[o] = (uint16_t)S;
-      if (p == excl) img[((size_t)M.seg_base + s) * IMG_STRIDE + IMG_STRIDE - 1] = 0;   // complete
     }
   }
 }
@@ -390,66 +364,6 @@ __device__ __forceinline__ void seg_chunk_put(uint32_t* lds, const uint4 v[8], i
   }
 }
 
-// E1c: the merged segments (suffix flag = the one range their chains reached
-// after MAP_CH tokens), one lane each, 64 segments per wave, tokens staged
-// like k_emit_seg's: the rest of the chain, then every start range's map
-// entry gets the end range and its shift count grows by the suffix's.
-__global__ __launch_bounds__(64) void k_emit_suffix(const uint16_t* __restrict__ tokens,
-                                                    const vp8g_frame_result* __restrict__ results,
-                                                    const vp8g_emit_meta* __restrict__ meta,
-                                                    const uint8_t* __restrict__ img,
-                                                    uint8_t* __restrict__ emap,
-                                                    uint16_t* __restrict__ eshift) {
-  __shared__ uint32_t lds[64 * SEG_ROW];
-  __shared__ __align__(4) uint8_t prob[VP8G_NUM_SLOTS];
-  const int f = blockIdx.y, lane = threadIdx.x;
-  const uint32_t s0 = blockIdx.x * 64, s = s0 + lane;
-  const vp8g_emit_meta M = meta[f];
-  if (s0 >= M.nseg) return;   // whole wave
-  const uint8_t* im = img + ((size_t)M.seg_base + s) * IMG_STRIDE;
-  const int flag = s < M.nseg ? im[IMG_STRIDE - 1] : 0;
-  if (!__ballot(flag != 0)) return;   // whole wave: nothing merged here
-  const uint32_t cnt = flag ? min((uint32_t)EMIT_SEG, M.ntok - s * EMIT_SEG) : 0u;
-  uint32_t span = cnt;   // the chunks this wave needs
-  for (int o = 32; o > 0; o >>= 1) span = max(span, (uint32_t)__shfl_xor((int)span, o));
-  const uint16_t* base = tokens + M.tok_off;
-  const uint32_t* row = lds + lane * SEG_ROW;
-  load_probas(prob, results, M, lane, 64);
-  int r = flag;
-  uint32_t S = 0;
-  uint4 nv[8];
-  seg_chunk_fetch(nv, base, s0, M.nseg, M.ntok, MAP_CH, lane);
-  for (uint32_t c0 = MAP_CH; c0 < span; c0 += SEG_CH) {
-    __syncthreads();   // the previous chunk's reads are done
-    seg_chunk_put(lds, nv, lane);
-    __syncthreads();
-    if (c0 + SEG_CH < span) seg_chunk_fetch(nv, base, s0, M.nseg, M.ntok, c0 + SEG_CH, lane);
-    if (c0 + SEG_CH <= cnt) {
-#pragma unroll 4
-      for (int k = 0; k < SEG_CH / 2; ++k) {
-        const uint32_t w = resolve_pair(row[k], prob);
-        S += chain_step(r, w & 0xffff);
-        S += chain_step(r, w >> 16);
-      }
-    } else if (c0 < cnt) {   // the frame's last segment
-      for (uint32_t i = 0; c0 + i < cnt; ++i) {
-        const uint32_t w = resolve_tok((row[i >> 1] >> (16 * (i & 1))) & 0xffff, prob);
-        S += chain_step(r, w);
-      }
-    }
-  }
-  if (!flag) return;
-  // every start range of the segment (img: the count and list, 0xff = all 128)
-  const int ni = im[0];
-  const int nk = ni == 0xff ? 128 : ni;
-  for (int k = 0; k < nk; ++k) {
-    const int r0 = ni == 0xff ? 127 + k : im[1 + k];
-    const size_t o = ((size_t)M.seg_base + s) * 128 + (r0 - 127);
-    emap[o] = (uint8_t)r;
-    eshift[o] = (uint16_t)(eshift[o] + S);
-  }
-}
-
 // The segment's bits of N, most significant first. Token i's c_i lands at
 // bit E_i = top - P_i (P_i: the segment's shifts before token i), so with the
 // true start range one forward pass places every c: the lane keeps the bits
@@ -479,7 +393,7 @@ __device__ __forceinline__ void seg_put(seg_sink& o, int wp, uint32_t v) {
     o.H += v << (wp - o.top);
   }
 }
-__device__ __forceinline__ void seg_carry(seg_sink& o, int q) {   // +1 at bit q (> T)
+__device__ __noinline__ void seg_carry(seg_sink& o, int q) {   // +1 at bit q (> T)
   __threadfence();   // the words this lane stored before
   for (;;) {
     const int wp = q & ~31;
@@ -645,12 +559,8 @@ extern "C" int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
     if (!vp8g_launch_check("k_emit_img")) return 0;
     hipLaunchKernelGGL(k_emit_maps, dim3((max_seg + MAP_G - 1) / MAP_G, n), dim3(64), 0, st,
                        (const uint16_t*)tokens, tok_cap, results, (const vp8g_emit_meta*)meta,
-                       img, emap, eshift);
-    if (!vp8g_launch_check("k_emit_maps")) return 0;
-    hipLaunchKernelGGL(k_emit_suffix, dim3((max_seg + 63) / 64, n), dim3(64), 0, st,
-                       (const uint16_t*)tokens, results, (const vp8g_emit_meta*)meta,
                        (const uint8_t*)img, emap, eshift);
-    if (!vp8g_launch_check("k_emit_suffix")) return 0;
+    if (!vp8g_launch_check("k_emit_maps")) return 0;
   }
   hipLaunchKernelGGL(k_emit_compose, dim3(n), dim3(64), 0, st, meta, (const uint8_t*)emap,
                      (const uint16_t*)eshift, segs, out_size);
@@ -708,7 +618,7 @@ extern "C" __attribute__((visibility("default"))) int vp8g_emit_streams(
             hipMalloc((void**)&d_meta, (size_t)n * sizeof(vp8g_emit_meta)) == hipSuccess &&
             hipMalloc((void**)&d_emap, cs * 128) == hipSuccess &&
             hipMalloc((void**)&d_eshift, cs * 128 * sizeof(uint16_t)) == hipSuccess &&
-            hipMalloc((void**)&d_img, cs * IMG_STRIDE) == hipSuccess &&
+            hipMalloc((void**)&d_img, cs * 17) == hipSuccess &&
             hipMalloc((void**)&d_segs, cs * sizeof(vp8g_emit_seg)) == hipSuccess &&
             hipMalloc((void**)&d_nbuf, (words + 1) * sizeof(uint32_t)) == hipSuccess &&
             hipMalloc((void**)&d_size, (size_t)n * sizeof(uint32_t)) == hipSuccess;

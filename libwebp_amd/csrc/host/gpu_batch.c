@@ -1209,7 +1209,7 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
       CHK(hipMalloc((void**)&b->d_emap, cap * 128));
       CHK(hipMalloc((void**)&b->d_eshift, cap * 128 * sizeof(uint16_t)));
       CHK(hipMalloc((void**)&b->d_esegs, cap * sizeof(vp8g_emit_seg)));
-      CHK(hipMalloc((void**)&b->d_eimg, cap * VP8G_EMIT_IMG_BYTES));
+      CHK(hipMalloc((void**)&b->d_eimg, cap * 17));
       b->emit_seg_cap = cap;
     }
     if (words > b->emit_word_cap) {

@@ -251,7 +251,6 @@ typedef struct {
   uint8_t H;       /* bits of the segment's partial sum above its region */
 } vp8g_emit_seg;
 #define VP8G_EMIT_SEG 2048
-#define VP8G_EMIT_IMG_BYTES 18   /* per segment: start-range count, 16 ranges, suffix flag */
 /* n streams; out_size[s] = the byte count of stream s */
 int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
                      const vp8g_frame_result* results, vp8g_emit_meta* meta,

@@ -40,6 +40,14 @@ fi
 if has bench; then
   run timeout -k 10 400 python3 bench.py --steps 5 --warmup 2 > $O/bench.json 2> $O/bench.err || exit 1
 fi
+if has k3res; then   # K3 CU reserve A/B (LIBWEBP_AMD_K3_RESERVE, gpu_batch.c), host-input line
+  for i in 1 2; do
+    for R in 0 8 16; do
+      LIBWEBP_AMD_K3_RESERVE=$R run timeout -k 10 300 python3 bench.py --no-cpu --steps 5 --warmup 1 \
+        > $O/k3res_${R}_$i.json 2> $O/k3res_${R}_$i.err || exit 1
+    done
+  done
+fi
 if has lowmem; then   # low_memory (K3 once per pass, tokens re-derived)
   run timeout -k 10 400 python3 bench.py --low-memory --steps 3 --warmup 1 --no-cpu > $O/bench_lowmem.json \
     2> $O/bench_lowmem.err || exit 1

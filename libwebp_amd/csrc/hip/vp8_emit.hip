@@ -367,12 +367,14 @@ __device__ __forceinline__ void seg_chunk_put(uint32_t* lds, const uint4 v[8], i
 // The segment's bits of N, most significant first. Token i's c_i lands at
 // bit E_i = top - P_i (P_i: the segment's shifts before token i), so with the
 // true start range one forward pass places every c: the lane keeps the bits
-// [B, B + 64) of the sum in a 64-bit window and, once every later c lies below
-// B + 32 (p + 8 <= B + 32, p the current position), the window's upper word
-// can only change by a carry out of the lower one, so it is staged (LDS, one
-// column per lane) and the window slides down 32 bits. A carry out of the
-// window needs its upper word all ones (about 2^-32 per word); it ripples into
-// the words already written. Bits at or above top go to H_s, the word that
+// [B, B + 64) of the sum in a 64-bit window with p - B in [0, 39] (p the bit
+// the next c lands on). Once p - B <= 7 every later c lies below B + 15, so
+// the window's upper word can only change by a carry out of the lower one: it
+// is staged (LDS, one column per lane) and the window slides down 32 bits.
+// A carry out of the window needs the >= 17 bits between the current byte and
+// the window top all ones (the coder's carries themselves are frequent: with
+// no headroom above p + 8 this kernel ran 60x slower); it ripples into the
+// words already written. Bits at or above top go to H_s, the word that
 // straddles top is kept in a register until the end (the segment above ORs its
 // low bits into the same word), the word that straddles T is ORed.
 struct seg_sink {
@@ -443,7 +445,7 @@ __global__ __launch_bounds__(64) void k_emit_seg(const uint16_t* __restrict__ to
                             : M.ntok - last_s * EMIT_SEG;
   seg_sink o{nbuf + M.nb_base, (int)g.T, (int)(g.T + g.S), 0u, 0u};
   int p = o.top;                 // the bit the next c lands on
-  int B = (o.top - 24) & ~31;    // window [B, B + 64); top - B in [24, 55]
+  int B = (o.top - 7) & ~31;     // window [B, B + 64); top - B in [7, 38]
   uint64_t acc = 0;
   int nst = 0;
   load_probas(prob, results, M, lane, 64);
@@ -467,14 +469,14 @@ __global__ __launch_bounds__(64) void k_emit_seg(const uint16_t* __restrict__ to
         const int sh = renorm(rr);
         if (c0 + 2 * k + h < cnt) {
           r = rr;
-          const uint64_t na = acc + ((uint64_t)c << (p - B));   // p - B in [17, 56]
+          const uint64_t na = acc + ((uint64_t)c << (p - B));   // p - B in [0, 39]
           if (na < acc) {   // carry out of the window
             seg_unstage(o, stg, nst, B, lane);
             seg_carry(o, B + 64);
           }
           acc = na;
           p -= sh;
-          if (p - B <= 24) {   // the upper word is final but for carries
+          if (p - B <= 7) {   // the upper word is final but for carries
             stg[nst * 64 + lane] = (uint32_t)(acc >> 32);
             ++nst;
             acc <<= 32;

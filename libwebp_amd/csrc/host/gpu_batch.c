@@ -523,7 +523,7 @@ static int tokens_for_run(WebPGpuBatch* b) {
  * the host-input kernel trace shows the GPU idle ~20% of the time between
  * K3 launches). With two or more lossy engines on a device, batches of more
  * than VP8G_XSPLIT_MAX_FRAMES frames run K3 on a stream whose CU mask leaves
- * LIBWEBP_AMD_K3_RESERVE CUs (default 8) to everything else; the K3
+ * LIBWEBP_AMD_K3_RESERVE CUs (default 0: off) to everything else; the K3
  * workgroups of the engines' batches keep the other CUs busy. A lone engine
  * keeps every CU (its 256th frame would otherwise wait a whole frame time). */
 static atomic_int g_lossy_engines[64];
@@ -532,7 +532,7 @@ static int k3_reserve(void) {
   static int r = -1;
   if (r < 0) {
     const char* v = getenv("LIBWEBP_AMD_K3_RESERVE");
-    r = v ? atoi(v) : 8;
+    r = v ? atoi(v) : 0;
     if (r < 0) r = 0;
   }
   return r;

@@ -1,6 +1,8 @@
 """K4 (hip/vp8_emit.hip) alone on token streams built to stress it: random
-streams and streams with long runs of 1 bits (all-ones words, so carries out
-of k_emit_seg's 64-bit window and through the words it already wrote), cut
+streams, streams with long runs of 1 bits, and streams that drive the
+coder's low end up to a point and across it (long runs of 1 bits in N, then
+a carry through them: out of k_emit_seg's 64-bit window and into the words
+it already wrote), cut
 at and around the 2048-token segment size. Each stream's bytes must equal
 libwebp's boolean coder on the same (bit, probability) sequence
 (tests/test_emit_model.py: ref_coder, a restatement of
@@ -13,7 +15,7 @@ import numpy as np
 import pytest
 
 import libwebp_amd
-from test_emit_model import _carry_heavy, ref_coder, window_coder
+from test_emit_model import _carry_forcing, _carry_heavy, ref_coder, window_coder
 
 pytestmark = pytest.mark.gpu
 
@@ -28,6 +30,8 @@ def _streams():
             toks.append((1 if rng.random() * 256 >= p else 0, p))
         out.append(toks)
         out.append(_carry_heavy(rng, n))
+        if 0 < n <= 20000:
+            out.append(_carry_forcing(rng, n))
     return out
 
 

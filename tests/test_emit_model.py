@@ -120,18 +120,19 @@ def test_segmented_model_matches_reference_coder():
         assert seg_coder(toks, seg) == ref_coder(toks)
 
 
-def window_coder(toks, seg, wd=32, stats=None):
+def window_coder(toks, seg, wd=32, stats=None, thr=7):
     """E1-E5 with E3 as k_emit_seg runs it: one forward pass per segment that
     places c_i most significant first through a 2*wd-bit window sliding down
     wd bits at a time, staged words, carries out of the window rippling into
     the words already written, the top-straddling word held back and the bits
-    above the segment's top in H (added by E4). wd=32 is the kernel; a smaller
-    wd makes the carry path frequent."""
+    above the segment's top in H (added by E4). The upper word is staged once
+    p - B <= thr (the kernel: wd=32, thr=7, so >= 17 bits of headroom above
+    the current byte); a small wd or a large thr makes the carry path
+    frequent."""
     n = len(toks)
     nseg = (n + seg - 1) // seg
     mask = (1 << wd) - 1
-    thr = wd - 8                      # rebase once p - B <= thr
-    assert thr >= 7
+    assert 7 <= thr <= wd - 8         # p stays >= B; the upper word gets no direct adds
     r, cum, starts = 254, 0, []
     for s in range(nseg):             # E1/E2: true start ranges and shift counts
         starts.append((r, cum))
@@ -195,11 +196,11 @@ def window_coder(toks, seg, wd=32, stats=None):
                 q = wp + wd
 
         p = top
-        B = (top - thr) - (top - thr) % wd
+        B = (top - thr) - (top - thr) % wd   # top - B in [thr, thr + wd)
         acc, stg = 0, []
         for b, pr in part:
             r, c, k = _step(r, b, pr)
-            assert thr - 7 <= p - B <= 2 * wd - 8
+            assert 0 <= p - B <= thr + wd
             na = acc + (c << (p - B))
             if na >> (2 * wd):
                 for i, v in enumerate(stg):
@@ -249,6 +250,48 @@ def _carry_heavy(rng, n):
     return toks[:n]
 
 
+def _carry_forcing(rng, n):
+    """Streams that make the coder's low end run up to a point from below (a
+    long run of 1 bits in N) and then cross it (a carry through the whole
+    run): each episode takes the midpoint of the current interval and codes
+    the bits whose subintervals hold a point just below it, then just above
+    it; random tokens in between. Exact interval arithmetic (A / 2^M)."""
+    M = 8 * n + 64
+    st = {"A": 0, "r": 254, "P": 0}
+    toks = []
+
+    def put(b, p):
+        r = st["r"]
+        split = (r * p) >> 8
+        if b:
+            st["A"] += (split + 1) << (M - st["P"])
+            r = r - split - 1
+        else:
+            r = split
+        sh = 0
+        while ((r + 1) << sh) < 128:
+            sh += 1
+        st["r"] = ((r + 1) << sh) - 1
+        st["P"] += sh
+        toks.append((b, p))
+
+    while len(toks) < n:
+        if rng.random() < 0.3:
+            for _ in range(rng.randint(1, 30)):
+                put(rng.randint(0, 1), rng.randint(1, 255))
+            continue
+        mid = st["A"] + ((st["r"] + 1) << (M - st["P"] - 1))
+        eps = 1 << max(0, M - st["P"] - 90)
+        for target, k in ((mid - eps, rng.randint(30, 80)), (mid + eps, rng.randint(20, 80))):
+            for _ in range(k):
+                if len(toks) >= n or st["P"] + 8 >= M - 64:
+                    break
+                p = rng.choice([128, 100, 160, 200, 60])
+                bound = st["A"] + ((((st["r"] * p) >> 8) + 1) << (M - st["P"]))
+                put(0 if target < bound else 1, p)
+    return toks[:n]
+
+
 def test_window_pass_matches_reference_coder():
     rng = random.Random(11)
     st16, st32 = {}, {}
@@ -264,5 +307,11 @@ def test_window_pass_matches_reference_coder():
         seg = rng.choice([1, 3, 64, 200, 2048])
         want = ref_coder(toks)
         assert window_coder(toks, seg, 32, st32) == want
+        assert window_coder(toks, seg, 32, None, 24) == want
         assert window_coder(toks, seg, 15, st16) == want
     assert st16.get("carries", 0) > 20   # the carry path ran
+    st = {}
+    for _ in range(4):   # and with the kernel's own window
+        toks = _carry_forcing(rng, 5000)
+        assert window_coder(toks, rng.choice([64, 2048]), 32, st) == ref_coder(toks)
+    assert st.get("carries", 0) > 20

@@ -42,11 +42,17 @@ if has bench; then
 fi
 if has k3res; then   # K3 CU reserve A/B (LIBWEBP_AMD_K3_RESERVE, gpu_batch.c), host-input line
   for i in 1 2; do
-    for R in 0 8 16; do
-      LIBWEBP_AMD_K3_RESERVE=$R run timeout -k 10 300 python3 bench.py --no-cpu --steps 5 --warmup 1 \
-        > $O/k3res_${R}_$i.json 2> $O/k3res_${R}_$i.err || exit 1
+    for KR in 0 8 16 32; do
+      LIBWEBP_AMD_K3_RESERVE=$KR run timeout -k 10 300 python3 bench.py --no-cpu --steps 5 --warmup 1 \
+        > $O/k3res_${KR}_$i.json 2> $O/k3res_${KR}_$i.err || exit 1
     done
   done
+fi
+if has h2dab; then   # runtime copies vs SDMA (LIBWEBP_AMD_H2D=hip), one and three engines
+  LIBWEBP_AMD_H2D=hip run timeout -k 10 300 python3 bench.py --no-cpu --steps 3 --warmup 1 \
+    > $O/h2dab_hip.json 2> $O/h2dab_hip.err || exit 1
+  run timeout -k 10 300 python3 bench.py --no-cpu --steps 3 --warmup 1 --engines 1 \
+    > $O/h2dab_e1.json 2> $O/h2dab_e1.err || exit 1
 fi
 if has lowmem; then   # low_memory (K3 once per pass, tokens re-derived)
   run timeout -k 10 400 python3 bench.py --low-memory --steps 3 --warmup 1 --no-cpu > $O/bench_lowmem.json \

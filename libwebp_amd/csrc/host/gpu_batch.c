@@ -17,9 +17,6 @@
 #include "vp8_host.h"
 #include "webp/encode_gpu.h"
 
-static int k3_stream_init(WebPGpuBatch* b);
-static void k3_stream_free(WebPGpuBatch* b);
-
 static double now_us(void) {
   struct timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -133,7 +130,6 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   CHK(hipSetDevice(device));
   CHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
   for (int i = 0; i < 6; ++i) CHK(hipEventCreate(&b->ev[i]));
-  if (!k3_stream_init(b)) goto fail;
   CHK(hipMalloc((void**)&b->d_g2l, 256 * sizeof(uint16_t) + 33 * sizeof(int32_t)));
   b->d_l2g = (int32_t*)(b->d_g2l + 256);
   CHK(hipMemcpy(b->d_g2l, g_g2l, 256 * sizeof(uint16_t), hipMemcpyHostToDevice));
@@ -226,7 +222,6 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   for (int i = 0; i < 6; ++i)
     if (b->ev[i]) hipEventDestroy(b->ev[i]);
   if (b->stream) hipStreamDestroy(b->stream);
-  k3_stream_free(b);
   if (b->out)
     for (int i = 0; i < b->max_frames; ++i) free(b->out[i]);
   free(b->out); free(b->out_cap); free(b->out_size); free(b->err); free(b->hdr);
@@ -515,79 +510,6 @@ static int tokens_for_run(WebPGpuBatch* b) {
          ensure_arena(b, (size_t)b->max_frames * nmb * 1024 + 768 * (size_t)VP8G_ARENA_CHUNK);
 }
 
-/* ---- K3's stream ----
- * A K3 workgroup encodes a whole frame (~100 ms for 1080p), and a 256-frame
- * batch puts one on every CU, so while one engine's K3 runs, the other
- * engines' K1/K2/K4 kernels and blit copies on the same device wait for it
- * to finish (profiles/r4/kernel_stats_r4z.csv: copies queued up to 102 ms;
- * the host-input kernel trace shows the GPU idle ~20% of the time between
- * K3 launches). With two or more lossy engines on a device, batches of more
- * than VP8G_XSPLIT_MAX_FRAMES frames run K3 on a stream whose CU mask leaves
- * LIBWEBP_AMD_K3_RESERVE CUs (default 0: off) to everything else; the K3
- * workgroups of the engines' batches keep the other CUs busy. A lone engine
- * keeps every CU (its 256th frame would otherwise wait a whole frame time). */
-static atomic_int g_lossy_engines[64];
-
-static int k3_reserve(void) {
-  static int r = -1;
-  if (r < 0) {
-    const char* v = getenv("LIBWEBP_AMD_K3_RESERVE");
-    r = v ? atoi(v) : 0;
-    if (r < 0) r = 0;
-  }
-  return r;
-}
-
-static int k3_stream_init(WebPGpuBatch* b) {
-  if (b->device >= 0 && b->device < 64) {
-    atomic_fetch_add(&g_lossy_engines[b->device], 1);
-    b->counted = 1;
-  }
-  const int r = k3_reserve();
-  int cus = 0;
-  if (!r || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, b->device) !=
-                hipSuccess || cus < 4 * r || cus > 32 * 32)
-    return 1;   /* no reserve: K3 stays on the engine's stream */
-  uint32_t mask[32] = {0};
-  for (int c = r; c < cus; ++c) mask[c >> 5] |= 1u << (c & 31);
-  if (hipExtStreamCreateWithCUMask(&b->k3stream, (uint32_t)((cus + 31) / 32), mask) != hipSuccess) {
-    b->k3stream = NULL;
-    return 1;
-  }
-  return hipEventCreateWithFlags(&b->evk[0], hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&b->evk[1], hipEventDisableTiming) == hipSuccess;
-}
-
-static void k3_stream_free(WebPGpuBatch* b) {
-  if (b->counted) atomic_fetch_sub(&g_lossy_engines[b->device], 1);
-  b->counted = 0;
-  for (int i = 0; i < 2; ++i)
-    if (b->evk[i]) hipEventDestroy(b->evk[i]);
-  if (b->k3stream) hipStreamDestroy(b->k3stream);
-}
-
-/* the stream the next K3 launch goes on (ordered after the engine stream's
- * work); k3_end orders the engine stream after it again */
-static hipStream_t k3_begin(WebPGpuBatch* b, int n) {
-  if (!b->k3stream || n <= VP8G_XSPLIT_MAX_FRAMES ||
-      atomic_load(&g_lossy_engines[b->device]) < 2)
-    return b->stream;
-  if (hipEventRecord(b->evk[0], b->stream) != hipSuccess ||
-      hipStreamWaitEvent(b->k3stream, b->evk[0], 0) != hipSuccess)
-    return b->stream;
-  return b->k3stream;
-}
-
-static int k3_end(WebPGpuBatch* b, hipStream_t s) {
-  if (s == b->stream) return 1;
-  if (hipEventRecord(b->evk[1], s) != hipSuccess ||
-      hipStreamWaitEvent(b->stream, b->evk[1], 0) != hipSuccess) {
-    vp8g_set_error("k3_end", "stream order after K3");
-    return 0;
-  }
-  return 1;
-}
-
 /* K3 over the frames of h_params (already on the device). The caller copies
  * the results back and calls k3_settle. */
 static int launch_k3(WebPGpuBatch* b, int n, uint8_t* recon) {
@@ -609,14 +531,11 @@ static int launch_k3(WebPGpuBatch* b, int n, uint8_t* recon) {
   /* in arena mode K3 itself moves each folded row's tokens to the compact
      stream (copy_folded); k_gather_tokens only redoes it for a stream that
      outgrew tok_cap (k3_settle) */
-  const hipStream_t ks = k3_begin(b, n);
   if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
                           b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5, b->d_results,
-                          b->d_rerun, recon, b->d_xsync, ap, ks)) {
-    (void)k3_end(b, ks);
+                          b->d_rerun, recon, b->d_xsync, ap, st))
     return 0;
-  }
-  return k3_end(b, ks);
+  return 1;
 fail:
   return 0;
 }

@@ -28,12 +28,6 @@ struct WebPGpuBatch {
   size_t yfb, tok_cap, d_rgba_cap, h_tok_cap;
   hipStream_t stream;
   hipEvent_t ev[6];          /* K1 start, K2 end, K3 start, K3 end, K4 start, K4 end */
-  /* K3 of big batches on its own stream that leaves a few CUs out, so the
-   * other engines' short kernels (K1/K2/K4, copies) on this device are not
-   * held behind K3 workgroups that run a whole frame each (gpu_batch.c) */
-  hipStream_t k3stream;
-  hipEvent_t evk[2];
-  int counted;               /* counted in the device's lossy-engine total */
   int ev0_recorded;
   /* device (HBM) */
   uint8_t* d_rgba;

@@ -40,14 +40,6 @@ fi
 if has bench; then
   run timeout -k 10 400 python3 bench.py --steps 5 --warmup 2 > $O/bench.json 2> $O/bench.err || exit 1
 fi
-if has k3res; then   # K3 CU reserve A/B (LIBWEBP_AMD_K3_RESERVE, gpu_batch.c), host-input line
-  for i in 1 2; do
-    for KR in 0 8 16 32; do
-      LIBWEBP_AMD_K3_RESERVE=$KR run timeout -k 10 300 python3 bench.py --no-cpu --steps 5 --warmup 1 \
-        > $O/k3res_${KR}_$i.json 2> $O/k3res_${KR}_$i.err || exit 1
-    done
-  done
-fi
 if has h2dab; then   # runtime copies vs SDMA (LIBWEBP_AMD_H2D=hip), one and three engines
   LIBWEBP_AMD_H2D=hip run timeout -k 10 300 python3 bench.py --no-cpu --steps 3 --warmup 1 \
     > $O/h2dab_hip.json 2> $O/h2dab_hip.err || exit 1

@@ -23,55 +23,6 @@ static double now_us(void) {
   return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
 }
 
-/* ---- the K3 gate ----
- * A K3 workgroup encodes a whole frame (~100 ms at 1080p) and a big batch
- * puts one on every CU, so whatever another engine queues on the device
- * while a K3 runs waits for it. Left alone, the engines drifted into
- * launching K3 in pairs (each then took twice as long) and leaving K1/K2/K4
- * and their host phases to the gaps, with the GPU idle ~20% of the time
- * (host-input kernel trace, r4k). With two or more lossy engines on a device,
- * a batch of more than VP8G_XSPLIT_MAX_FRAMES frames holds the device's gate
- * from its K3 launch to the end of its K4: one K3 at a time, each followed
- * by the short kernels queued meanwhile, while the other engines do their
- * host work and uploads. LIBWEBP_AMD_K3_GATE=0 turns it off (A/B). */
-#define GATE_DEV 64
-static pthread_mutex_t g_k3gate[GATE_DEV];
-static atomic_int g_lossy_engines[GATE_DEV];
-static pthread_once_t g_gate_once = PTHREAD_ONCE_INIT;
-static void gate_init(void) {
-  for (int i = 0; i < GATE_DEV; ++i) pthread_mutex_init(&g_k3gate[i], NULL);
-}
-
-static void k3_gate_count(WebPGpuBatch* b, int add) {
-  if (add && !b->counted && b->device >= 0 && b->device < GATE_DEV) {
-    atomic_fetch_add(&g_lossy_engines[b->device], 1);
-    b->counted = 1;
-  } else if (!add && b->counted) {
-    atomic_fetch_sub(&g_lossy_engines[b->device], 1);
-    b->counted = 0;
-  }
-}
-
-static void k3_gate_enter(WebPGpuBatch* b, int n) {
-  static int mode = -1;
-  if (mode < 0) {
-    const char* v = getenv("LIBWEBP_AMD_K3_GATE");
-    mode = (v && v[0] == '0') ? 0 : 1;
-  }
-  if (!mode || !b->counted || b->gate_held || n <= VP8G_XSPLIT_MAX_FRAMES ||
-      atomic_load(&g_lossy_engines[b->device]) < 2)
-    return;
-  pthread_once(&g_gate_once, gate_init);
-  pthread_mutex_lock(&g_k3gate[b->device]);
-  b->gate_held = 1;
-}
-
-static void k3_gate_leave(WebPGpuBatch* b) {
-  if (!b->gate_held) return;
-  b->gate_held = 0;
-  pthread_mutex_unlock(&g_k3gate[b->device]);
-}
-
 /* gamma tables for the RGB->YUV import (picture_csp_enc.c:103-117) */
 static uint16_t g_g2l[256];
 static int32_t g_l2g[33];
@@ -179,7 +130,6 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   CHK(hipSetDevice(device));
   CHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
   for (int i = 0; i < 6; ++i) CHK(hipEventCreate(&b->ev[i]));
-  k3_gate_count(b, 1);
   CHK(hipMalloc((void**)&b->d_g2l, 256 * sizeof(uint16_t) + 33 * sizeof(int32_t)));
   b->d_l2g = (int32_t*)(b->d_g2l + 256);
   CHK(hipMemcpy(b->d_g2l, g_g2l, 256 * sizeof(uint16_t), hipMemcpyHostToDevice));
@@ -272,8 +222,6 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   for (int i = 0; i < 6; ++i)
     if (b->ev[i]) hipEventDestroy(b->ev[i]);
   if (b->stream) hipStreamDestroy(b->stream);
-  k3_gate_leave(b);
-  k3_gate_count(b, 0);
   if (b->out)
     for (int i = 0; i < b->max_frames; ++i) free(b->out[i]);
   free(b->out); free(b->out_cap); free(b->out_size); free(b->err); free(b->hdr);
@@ -1192,7 +1140,7 @@ fail:
   return 0;
 }
 
-static int engine_run_yuv(WebPGpuBatch* b, int n) {
+int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   const size_t nmb = (size_t)b->nmb;
   double t0 = now_us(), t1, t2, t3, t4;
   hipStream_t st = b->stream;
@@ -1213,7 +1161,6 @@ static int engine_run_yuv(WebPGpuBatch* b, int n) {
   t1 = now_us();
   run_tails(b, n, 2);   /* per-frame setup + segment k-means on the host threads */
   t2 = now_us();
-  k3_gate_enter(b, n);
   if (!run_passes(b, n)) return 0;
   /* token partitions: VP8EncLoop only (vp8h_frame_init) */
   const int np = (b->cfg.method < 3 || b->cfg.low_memory) ? 1 << b->cfg.partitions : 1;
@@ -1287,7 +1234,6 @@ static int engine_run_yuv(WebPGpuBatch* b, int n) {
     head_running = 1;
     CHK(hipStreamSynchronize(st));
   }
-  k3_gate_leave(b);
   t3 = now_us();
   if (b->host_emit) {
     b->tok_off[0] = 0;
@@ -1372,12 +1318,6 @@ static int engine_run_yuv(WebPGpuBatch* b, int n) {
 fail:
   if (head_running) tail_join(&head);
   return 0;
-}
-
-int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
-  const int ok = engine_run_yuv(b, n);
-  k3_gate_leave(b);   /* the error paths */
-  return ok;
 }
 
 /* RGBA -> YUV420 of n frames on the engine stream: K1, or the sharp-YUV

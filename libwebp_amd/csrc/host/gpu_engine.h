@@ -28,8 +28,6 @@ struct WebPGpuBatch {
   size_t yfb, tok_cap, d_rgba_cap, h_tok_cap;
   hipStream_t stream;
   hipEvent_t ev[6];          /* K1 start, K2 end, K3 start, K3 end, K4 start, K4 end */
-  int counted;               /* counted in its device's lossy-engine total (K3 gate) */
-  int gate_held;             /* holds its device's K3 gate (gpu_batch.c) */
   int ev0_recorded;
   /* device (HBM) */
   uint8_t* d_rgba;

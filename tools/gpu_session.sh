@@ -40,14 +40,6 @@ fi
 if has bench; then
   run timeout -k 10 400 python3 bench.py --steps 5 --warmup 2 > $O/bench.json 2> $O/bench.err || exit 1
 fi
-if has gateab; then   # per-device K3 gate (gpu_batch.c) on / off, host-input line
-  for i in 1 2; do
-    for G in 1 0; do
-      LIBWEBP_AMD_K3_GATE=$G run timeout -k 10 300 python3 bench.py --no-cpu --steps 5 --warmup 1 \
-        > $O/gate_${G}_$i.json 2> $O/gate_${G}_$i.err || exit 1
-    done
-  done
-fi
 if has h2dab; then   # runtime copies vs SDMA (LIBWEBP_AMD_H2D=hip), one and three engines
   LIBWEBP_AMD_H2D=hip run timeout -k 10 300 python3 bench.py --no-cpu --steps 3 --warmup 1 \
     > $O/h2dab_hip.json 2> $O/h2dab_hip.err || exit 1

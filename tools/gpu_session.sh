@@ -40,6 +40,21 @@ fi
 if has bench; then
   run timeout -k 10 400 python3 bench.py --steps 5 --warmup 2 > $O/bench.json 2> $O/bench.err || exit 1
 fi
+if has engab; then   # encoder instances per GPU: 3 (9 steps) vs 4 (12 steps), host-input line
+  for i in 1 2; do
+    run timeout -k 10 300 python3 bench.py --no-cpu --steps 9 --warmup 2 --engines 3 \
+      > $O/eng3_$i.json 2> $O/eng3_$i.err || exit 1
+    run timeout -k 10 300 python3 bench.py --no-cpu --steps 12 --warmup 2 --engines 4 \
+      > $O/eng4_$i.json 2> $O/eng4_$i.err || exit 1
+  done
+fi
+if has mapsab; then   # k_emit_maps group shapes (LIBWEBP_AMD_MAPS), solo kernel stats
+  for MS in 0 1 2; do
+    (cd /tmp && TMPDIR=/tmp LIBWEBP_AMD_MAPS=$MS run timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+      --output-format csv -d $O/maps$MS -o run -- python3 $R/bench.py --no-cpu --no-host-input \
+      --steps 2 --warmup 1 --engines 1 > $O/maps$MS.log 2>&1) || exit 1
+  done
+fi
 if has h2dab; then   # runtime copies vs SDMA (LIBWEBP_AMD_H2D=hip), one and three engines
   LIBWEBP_AMD_H2D=hip run timeout -k 10 300 python3 bench.py --no-cpu --steps 3 --warmup 1 \
     > $O/h2dab_hip.json 2> $O/h2dab_hip.err || exit 1

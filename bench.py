@@ -43,9 +43,9 @@ def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
                     help="ranks; without a torchrun environment bench.py launches them itself")
-    ap.add_argument("--steps", type=int, default=9,
-                    help="timed steps (default 9: three per encoder instance, so the "
-                         "line is not dominated by filling and draining the pipeline)")
+    ap.add_argument("--steps", type=int, default=0,
+                    help="timed steps (0: three per encoder instance, 12 lossy / 9 lossless, so "
+                         "the line is not dominated by filling and draining the pipeline)")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=0,
                     help="frames per GPU per step (0: 256 lossy, 1024 lossless)")
@@ -63,7 +63,8 @@ def parse_args(argv=None):
     ap.add_argument("--engines", type=int, default=0,
                     help="encoder instances on their own streams and host threads; steps are "
                          "dealt round-robin so one batch's host work overlaps another's kernels "
-                         "(0: 3 -- profiles/r3/ab5_*.json, lab_*.json)")
+                         "(0: 4 lossy -- profiles/r4/eng{3,4}_r4t.json: 4069-4146 MP/s with 3, "
+                         "4271-4272 with 4; 3 lossless -- profiles/r3/lab_*.json)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="CPU work per baseline leg (single thread, all cores)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -409,6 +410,10 @@ def main(argv=None):
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     W, H = args.width, args.height
     B = args.batch or (1024 if args.lossless else 256)
+    if not args.engines:
+        args.engines = 3 if args.lossless else 4
+    if not args.steps:
+        args.steps = 3 * (1 if args.stub else args.engines)
 
     # the CPU baseline first: before this process initialises the GPU
     cb = None
@@ -467,8 +472,7 @@ def main(argv=None):
     # timed steps are dealt round-robin to one host thread per engine (the
     # ctypes calls release the GIL), so one batch's host stages (segment
     # setup, partition 0, RIFF write) run while another batch's kernels do
-    engines = args.engines or 3
-    E = 1 if args.stub else max(1, min(engines, args.steps))
+    E = 1 if args.stub else max(1, min(args.engines, args.steps))
     args.engines_used = E
     encs = [enc]
     for _ in range(E - 1):

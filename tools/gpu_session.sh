@@ -61,6 +61,9 @@ if has h2dab; then   # runtime copies vs SDMA (LIBWEBP_AMD_H2D=hip), one and thr
   run timeout -k 10 300 python3 bench.py --no-cpu --steps 3 --warmup 1 --engines 1 \
     > $O/h2dab_e1.json 2> $O/h2dab_e1.err || exit 1
 fi
+if has bench0; then   # the line exactly as the driver's default run makes it
+  run timeout -k 10 400 python3 bench.py > $O/bench0.json 2> $O/bench0.err || exit 1
+fi
 if has lowmem; then   # low_memory (K3 once per pass, tokens re-derived)
   run timeout -k 10 400 python3 bench.py --low-memory --steps 3 --warmup 1 --no-cpu > $O/bench_lowmem.json \
     2> $O/bench_lowmem.err || exit 1

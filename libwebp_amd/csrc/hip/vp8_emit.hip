@@ -179,15 +179,15 @@ __global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ to
 
 // E1b: per segment, the end range and shift count from each possible start
 // range. A wavefront takes MAP_G consecutive segments and packs their
-// (segment, start range) pairs densely onto its lanes, MAP_C pairs per lane
-// (a segment has ~5 start ranges, so a fixed 16 lanes per segment would leave
-// most lanes idle); a lane's chains are independent, so their steps
-// interleave and hide each other's latency. More than 64 * MAP_C pairs take
-// further rounds. The group's tokens go through LDS MAP_CH per segment at a
-// time (the next chunk is loaded into registers while this one runs), so the
-// chains read LDS broadcasts instead of global loads.
-// MAP_G segments per wave, MAP_C chains per lane, MAP_CH tokens per chunk
-template <int MAP_G, int MAP_C, int MAP_CH>
+// (segment, start range) pairs densely onto its 64 lanes (a segment has ~4
+// start ranges, so a fixed 16 lanes per segment would leave most lanes idle);
+// more than 64 pairs take further rounds. The group's tokens go through LDS
+// MAP_CH per segment at a time (the next chunk is loaded into registers while
+// this one runs), so the chains read LDS broadcasts instead of global loads.
+#define MAP_G 8
+#define MAP_CH 256
+#define MAP_ROW (MAP_CH + 8)   // u16; +16 B per row: the 16 rows' b128 reads hit distinct banks
+#define MAP_PIECES (MAP_G * MAP_CH / 8 / 64)   // 16-byte pieces per lane per chunk
 __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ tokens,
                                                   size_t tok_cap,
                                                   const vp8g_frame_result* __restrict__ results,
@@ -195,8 +195,6 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
                                                   const uint8_t* __restrict__ img,
                                                   uint8_t* __restrict__ emap,
                                                   uint16_t* __restrict__ eshift) {
-  constexpr int MAP_ROW = MAP_CH + 8;   // u16; +16 B per row: the rows' b128 reads hit distinct banks
-  constexpr int MAP_PIECES = MAP_G * MAP_CH / 8 / 64;   // 16-byte pieces per lane per chunk
   __shared__ __align__(16) uint16_t stage[MAP_G * MAP_ROW];
   __shared__ __align__(4) uint8_t prob[VP8G_NUM_SLOTS];
   const int f = blockIdx.y, lane = threadIdx.x;
@@ -227,31 +225,23 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
       if (sbase + sg < M.nseg && i < M.ntok) v[t] = *reinterpret_cast<const uint4*>(ftok + i);
     }
   };
-  for (int p0 = 0; p0 < total; p0 += 64 * MAP_C) {
-    int r[MAP_C], r0[MAP_C];
-    uint32_t S[MAP_C], cnt[MAP_C], seg[MAP_C];
-    bool live[MAP_C];
-    const uint16_t* st[MAP_C];
+  for (int p0 = 0; p0 < total; p0 += 64) {
+    const int p = p0 + lane;   // this lane's pair
+    int g = 0, excl = 0;
 #pragma unroll
-    for (int c = 0; c < MAP_C; ++c) {
-      const int p = p0 + 64 * c + lane;   // this chain's pair
-      int g = 0, excl = 0;
-#pragma unroll
-      for (int j = 0; j < MAP_G; ++j) {
-        const int ij = __shfl(incl, j);
-        if (p >= ij) { g = j + 1; excl = ij; }
-      }
-      live[c] = p < total;
-      seg[c] = sbase + (live[c] ? g : 0);
-      const uint8_t* im = img + ((size_t)M.seg_base + seg[c]) * (EMIT_SLOTS + 1);
-      const int k = p - excl;
-      r0[c] = !live[c] ? 127 : im[0] == 0xff ? 127 + k : im[1 + k];
-      // a dead chain runs a full segment's dummy steps beside the live one
-      cnt[c] = live[c] ? min((uint32_t)EMIT_SEG, M.ntok - seg[c] * EMIT_SEG) : (uint32_t)EMIT_SEG;
-      st[c] = stage + (live[c] ? g : 0) * MAP_ROW;
-      r[c] = r0[c];
-      S[c] = 0;
+    for (int j = 0; j < MAP_G; ++j) {
+      const int ij = __shfl(incl, j);
+      if (p >= ij) { g = j + 1; excl = ij; }
     }
+    const bool live = p < total;
+    const uint32_t s = sbase + (live ? g : 0);
+    const uint8_t* im = img + ((size_t)M.seg_base + s) * (EMIT_SLOTS + 1);
+    const int k = p - excl;
+    const int r0 = !live ? 127 : im[0] == 0xff ? 127 + k : im[1 + k];
+    const uint32_t cnt = live ? min((uint32_t)EMIT_SEG, M.ntok - s * EMIT_SEG) : 0u;
+    const uint16_t* st = stage + (live ? g : 0) * MAP_ROW;
+    int r = r0;
+    uint32_t S = 0;
     uint4 nv[MAP_PIECES];
     load(0, nv);
     for (uint32_t c0 = 0; c0 < EMIT_SEG; c0 += MAP_CH) {
@@ -262,41 +252,24 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
         *reinterpret_cast<uint4*>(&stage[sg * MAP_ROW + 8 * part]) = resolve_quad(nv[t], prob);
       }
       __syncthreads();
-      if (c0 + MAP_CH < EMIT_SEG) load(c0 + MAP_CH, nv);   // in flight during the chains
-      bool full = true;
-      uint32_t n[MAP_C];
-#pragma unroll
-      for (int c = 0; c < MAP_C; ++c) {
-        n[c] = cnt[c] > c0 ? min((uint32_t)MAP_CH, cnt[c] - c0) : 0u;
-        full = full && n[c] == MAP_CH;
-      }
-      if (full) {
+      if (c0 + MAP_CH < EMIT_SEG) load(c0 + MAP_CH, nv);   // in flight during the chain
+      const uint32_t n = cnt > c0 ? min((uint32_t)MAP_CH, cnt - c0) : 0u;
+      if (n == MAP_CH) {
         for (int i = 0; i < MAP_CH; i += 8) {
-          uint32_t w[MAP_C][4];
+          const uint4 q = *reinterpret_cast<const uint4*>(st + i);
+          const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-          for (int c = 0; c < MAP_C; ++c) {
-            const uint4 q = *reinterpret_cast<const uint4*>(st[c] + i);
-            w[c][0] = q.x; w[c][1] = q.y; w[c][2] = q.z; w[c][3] = q.w;
-          }
-#pragma unroll
-          for (int kk = 0; kk < 8; ++kk)
-#pragma unroll
-            for (int c = 0; c < MAP_C; ++c)
-              S[c] += chain_step(r[c], (w[c][kk >> 1] >> (16 * (kk & 1))) & 0xffff);
+          for (int kk = 0; kk < 8; ++kk) S += chain_step(r, (w[kk >> 1] >> (16 * (kk & 1))) & 0xffff);
         }
-      } else {   // the frame's last segment
-#pragma unroll
-        for (int c = 0; c < MAP_C; ++c)
-          for (uint32_t i = 0; i < n[c]; ++i) S[c] += chain_step(r[c], st[c][i]);
+      } else {
+        for (uint32_t i = 0; i < n; ++i) S += chain_step(r, st[i]);   // frame's last segment
       }
     }
-#pragma unroll
-    for (int c = 0; c < MAP_C; ++c)
-      if (live[c]) {
-        const size_t o = ((size_t)M.seg_base + seg[c]) * 128 + (r0[c] - 127);
-        emap[o] = (uint8_t)r[c];
-        eshift[o] = (uint16_t)S[c];
-      }
+    if (live) {
+      const size_t o = ((size_t)M.seg_base + s) * 128 + (r0 - 127);
+      emap[o] = (uint8_t)r;
+      eshift[o] = (uint16_t)S;
+    }
   }
 }
 
@@ -586,25 +559,9 @@ extern "C" int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
                        (const uint16_t*)tokens, tok_cap, results, (const vp8g_emit_meta*)meta,
                        img);
     if (!vp8g_launch_check("k_emit_img")) return 0;
-    // group shape (A/B: LIBWEBP_AMD_MAPS=0 8 segments x 1 chain, 1 16 x 2, 2 16 x 2 with
-    // 128-token chunks)
-    static int shape = -1;
-    if (shape < 0) {
-      const char* v = getenv("LIBWEBP_AMD_MAPS");
-      shape = v ? atoi(v) : 0;
-    }
-    if (shape == 1)
-      hipLaunchKernelGGL((k_emit_maps<16, 2, 256>), dim3((max_seg + 15) / 16, n), dim3(64), 0, st,
-                         (const uint16_t*)tokens, tok_cap, results, (const vp8g_emit_meta*)meta,
-                         (const uint8_t*)img, emap, eshift);
-    else if (shape == 2)
-      hipLaunchKernelGGL((k_emit_maps<16, 2, 128>), dim3((max_seg + 15) / 16, n), dim3(64), 0, st,
-                         (const uint16_t*)tokens, tok_cap, results, (const vp8g_emit_meta*)meta,
-                         (const uint8_t*)img, emap, eshift);
-    else
-      hipLaunchKernelGGL((k_emit_maps<8, 1, 256>), dim3((max_seg + 7) / 8, n), dim3(64), 0, st,
-                         (const uint16_t*)tokens, tok_cap, results, (const vp8g_emit_meta*)meta,
-                         (const uint8_t*)img, emap, eshift);
+    hipLaunchKernelGGL(k_emit_maps, dim3((max_seg + MAP_G - 1) / MAP_G, n), dim3(64), 0, st,
+                       (const uint16_t*)tokens, tok_cap, results, (const vp8g_emit_meta*)meta,
+                       (const uint8_t*)img, emap, eshift);
     if (!vp8g_launch_check("k_emit_maps")) return 0;
   }
   hipLaunchKernelGGL(k_emit_compose, dim3(n), dim3(64), 0, st, meta, (const uint8_t*)emap,

@@ -48,13 +48,6 @@ if has engab; then   # encoder instances per GPU: 3 (9 steps) vs 4 (12 steps), h
       > $O/eng4_$i.json 2> $O/eng4_$i.err || exit 1
   done
 fi
-if has mapsab; then   # k_emit_maps group shapes (LIBWEBP_AMD_MAPS), solo kernel stats
-  for MS in 0 1 2; do
-    (cd /tmp && TMPDIR=/tmp LIBWEBP_AMD_MAPS=$MS run timeout -k 10 300 rocprofv3 --kernel-trace --stats \
-      --output-format csv -d $O/maps$MS -o run -- python3 $R/bench.py --no-cpu --no-host-input \
-      --steps 2 --warmup 1 --engines 1 > $O/maps$MS.log 2>&1) || exit 1
-  done
-fi
 if has h2dab; then   # runtime copies vs SDMA (LIBWEBP_AMD_H2D=hip), one and three engines
   LIBWEBP_AMD_H2D=hip run timeout -k 10 300 python3 bench.py --no-cpu --steps 3 --warmup 1 \
     > $O/h2dab_hip.json 2> $O/h2dab_hip.err || exit 1

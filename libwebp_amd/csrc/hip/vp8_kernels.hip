@@ -253,7 +253,9 @@ __global__ __launch_bounds__(256) void k_analyze(const uint8_t* __restrict__ yuv
                                                  uint16_t* __restrict__ mb_uva, int fast_q,
                                                  uint8_t* __restrict__ mb_amode) {
   __shared__ uint8_t ty[17 * K2_YW];       // row 0 = the row above the strip
-  __shared__ uint8_t tu[9 * K2_CW], tv[9 * K2_CW];
+  __shared__ uint8_t tuv[2 * 9 * K2_CW];   // U tile, then V tile
+  uint8_t* const tu = tuv;
+  uint8_t* const tv = tuv + 9 * K2_CW;
   __shared__ K2Wave S[4];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tid = threadIdx.x;
   const int f = blockIdx.z, y = blockIdx.y, x0 = blockIdx.x * K2_STRIP;
@@ -262,18 +264,37 @@ __global__ __launch_bounds__(256) void k_analyze(const uint8_t* __restrict__ yuv
   const uint8_t* Yp = yuv + f * yfb;
   const uint8_t* Up = Yp + (size_t)w * h;
   const uint8_t* Vp = Up + (size_t)uvw * uvh;
-  // ---- strip tiles: tile (r, c) = picture (16y - 1 + r, 16x0 - 1 + c), clamped
-  for (int k = tid; k < 17 * (16 * K2_STRIP + 1); k += 256) {
+  // ---- strip tiles: tile (r, c) = picture (16y - 1 + r, 16x0 - 1 + c), clamped.
+  // Every byte a thread loads is fetched before any goes to LDS, so the
+  // loads are in flight together (a load / wait / store loop made the strip
+  // 14 HBM round trips long: K2 4.5 ms per 256 x 1080p batch).
+  constexpr int NY = 17 * (16 * K2_STRIP + 1), NYI = (NY + 255) / 256;
+  constexpr int NC = 2 * 9 * (8 * K2_STRIP + 1), NCI = (NC + 255) / 256;
+  uint8_t vy[NYI], vc[NCI];
+  int oy[NYI], oc[NCI];
+#pragma unroll
+  for (int i = 0; i < NYI; ++i) {   // no branches here: a thread past the tile reloads its last byte
+    const int k0 = tid + 256 * i, k = min(k0, NY - 1);
     const int r = k / (16 * K2_STRIP + 1), c = k % (16 * K2_STRIP + 1);
     const int gy = min(max(16 * y - 1 + r, 0), h - 1), gx = min(max(16 * x0 - 1 + c, 0), w - 1);
-    ty[r * K2_YW + c] = Yp[(size_t)gy * w + gx];
+    vy[i] = Yp[(size_t)gy * w + gx];
+    oy[i] = k0 < NY ? r * K2_YW + c : -1;
   }
-  for (int k = tid; k < 2 * 9 * (8 * K2_STRIP + 1); k += 256) {
+#pragma unroll
+  for (int i = 0; i < NCI; ++i) {
+    const int k0 = tid + 256 * i, k = min(k0, NC - 1);
     const int pl = k / (9 * (8 * K2_STRIP + 1)), kk = k % (9 * (8 * K2_STRIP + 1));
     const int r = kk / (8 * K2_STRIP + 1), c = kk % (8 * K2_STRIP + 1);
     const int gy = min(max(8 * y - 1 + r, 0), uvh - 1), gx = min(max(8 * x0 - 1 + c, 0), uvw - 1);
-    (pl ? tv : tu)[r * K2_CW + c] = (pl ? Vp : Up)[(size_t)gy * uvw + gx];
+    vc[i] = (pl ? Vp : Up)[(size_t)gy * uvw + gx];
+    oc[i] = k0 < NC ? pl * (9 * K2_CW) + r * K2_CW + c : -1;   // tu and tv back to back
   }
+#pragma unroll
+  for (int i = 0; i < NYI; ++i)
+    if (oy[i] >= 0) ty[oy[i]] = vy[i];
+#pragma unroll
+  for (int i = 0; i < NCI; ++i)
+    if (oc[i] >= 0) tuv[oc[i]] = vc[i];
   __syncthreads();
   K2Wave& L = S[wave];
   for (int it = 0; it < K2_STRIP / 4; ++it) {   // uniform trip count: the barriers below

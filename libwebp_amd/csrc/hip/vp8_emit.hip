@@ -82,7 +82,9 @@ __device__ __forceinline__ void load_probas(uint8_t* prob, const vp8g_frame_resu
 // phase of tokens, collects the images in per-segment 128-bit maps and
 // repacks the (by then far fewer) distinct ranges for the next phase.
 // Segment 0 starts at 254.
+#ifndef EMIT_IMG   // (overridable for the K4 A/B builds, tools/emit_ab.sh)
 #define EMIT_IMG 256
+#endif
 #define EMIT_SLOTS 16
 #define IMG_G 16                     // segments per wavefront (4 lanes each for the maps)
 #define IMG_ROW (EMIT_IMG + 8)       // u16; +16 B per row: conflict-free b128 reads
@@ -184,7 +186,9 @@ __global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ to
 // more than 64 pairs take further rounds. The group's tokens go through LDS
 // MAP_CH per segment at a time (the next chunk is loaded into registers while
 // this one runs), so the chains read LDS broadcasts instead of global loads.
+#ifndef MAP_G
 #define MAP_G 8
+#endif
 #define MAP_CH 256
 #define MAP_ROW (MAP_CH + 8)   // u16; +16 B per row: the 16 rows' b128 reads hit distinct banks
 #define MAP_PIECES (MAP_G * MAP_CH / 8 / 64)   // 16-byte pieces per lane per chunk

@@ -73,6 +73,9 @@ def parse_args(argv=None):
                          "SURVEY.md 8(d), the default) or already resident in HBM")
     ap.add_argument("--no-host-input", dest="input", action="store_const", const="hbm",
                     help="same as --input hbm")
+    ap.add_argument("--no-prefetch", dest="prefetch", action="store_false",
+                    help="host input: upload each batch inside its own call only (no "
+                         "upload of an engine's next batch while its current one encodes)")
     ap.add_argument("--no-other-input", action="store_true",
                     help="skip timing the other input mode after the line's steps")
     ap.add_argument("--stub", action="store_true",
@@ -500,9 +503,15 @@ def main(argv=None):
 
     def engine_steps(e, n, host, tails):
         """Engine e's share of n steps (dealt round-robin over the engines)."""
-        for _ in range(e, n, E):
+        mine = range(e, n, E)
+        for k, _ in enumerate(mine):
             if host:
-                encs[e].encode_host_ptr(pinned.data_ptr(), B)
+                # double-buffered upload: while this batch encodes, the engine's
+                # next batch of the same run goes up on a copy engine. Every
+                # batch of the timed run is uploaded inside it: its first call
+                # uploads its own frames and its last starts no upload.
+                nxt = pinned.data_ptr() if args.prefetch and k + 1 < len(mine) else None
+                encs[e].encode_host_ptr(pinned.data_ptr(), B, next_ptr=nxt)
             else:
                 encs[e].encode_device(rgba.data_ptr() if rgba is not None else 0, B,
                                       stream=stream)
@@ -605,9 +614,13 @@ def main(argv=None):
                                 "tests/golden/shard_kat.json" % (checked, world)
         line["config"]["input"] = "host" if host_in else "hbm"
         line["input"] = ("host: RGBA in pinned host memory -> .webp in host memory, H2D "
-                         "upload inside every step (SURVEY.md 8(d)): one copy on an SDMA "
-                         "engine ahead of the instance's kernels, beside the other "
-                         "%d instance(s)' kernels" % (len(encs) - 1)
+                         "upload of every step inside the timed run (SURVEY.md 8(d)): one "
+                         "copy on an SDMA engine, beside the other %d instance(s)' kernels; "
+                         "%s" % (len(encs) - 1,
+                                 "double-buffered: an instance's next batch goes up while its "
+                                 "current one encodes (the run's first batch per instance "
+                                 "uploads in its own call, its last starts no upload)"
+                                 if args.prefetch else "each batch uploaded in its own call")
                          if host_in else
                          "hbm: RGBA frames already resident in HBM (no upload)")
         if other_rate is not None:

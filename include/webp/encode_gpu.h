@@ -49,6 +49,19 @@ WEBP_EXTERN int WebPGpuBatchEncodeRGBAHost(WebPGpuBatch* batch,
                                            size_t frame_stride, int row_stride,
                                            int num_frames);
 
+/* Same, and while this batch encodes, upload the next one: rgba_next
+ * (page-locked host memory, same frame count and strides) goes to the
+ * device on a copy engine, and the next call whose rgba_host is rgba_next
+ * (same geometry) encodes from that copy instead of uploading. rgba_next
+ * must not change until then; a call for other frames discards it.
+ * rgba_next NULL (or pageable): WebPGpuBatchEncodeRGBAHost. */
+WEBP_EXTERN int WebPGpuBatchEncodeRGBAHostPrefetch(WebPGpuBatch* batch,
+                                                   const uint8_t* rgba_host,
+                                                   const uint8_t* rgba_next,
+                                                   size_t frame_stride,
+                                                   int row_stride,
+                                                   int num_frames);
+
 /* Results of the last encode call. */
 WEBP_EXTERN size_t WebPGpuBatchOutputSize(const WebPGpuBatch* batch, int frame);
 WEBP_EXTERN const uint8_t* WebPGpuBatchOutput(const WebPGpuBatch* batch,

@@ -50,6 +50,7 @@ def load():
         "WebPGpuBatchDelete": (None, [vp]),
         "WebPGpuBatchEncodeRGBA": (i, [vp, vp, sz, i, i, vp]),
         "WebPGpuBatchEncodeRGBAHost": (i, [vp, vp, sz, i, i]),
+        "WebPGpuBatchEncodeRGBAHostPrefetch": (i, [vp, vp, vp, sz, i, i]),
         "WebPGpuBatchOutputSize": (sz, [vp, i]),
         "WebPGpuBatchOutput": (vp, [vp, i]),
         "WebPGpuBatchError": (i, [vp, i]),
@@ -121,14 +122,21 @@ class GpuBatch:
         self.n = n
         return self
 
-    def encode_host_ptr(self, ptr, n, frame_stride=None, row_stride=None):
+    def encode_host_ptr(self, ptr, n, frame_stride=None, row_stride=None, next_ptr=None):
         """Encode n RGBA frames at host address ptr. Page-locked memory
         (hipHostMalloc, torch pin_memory) is uploaded by one copy on an SDMA
         engine (host/h2d_sdma.c) ahead of the encoder's kernels; pageable
-        memory is copied synchronously first."""
+        memory is copied synchronously first. next_ptr (page-locked, same
+        geometry): the next batch, uploaded while this one encodes
+        (WebPGpuBatchEncodeRGBAHostPrefetch); the next call with ptr ==
+        next_ptr encodes from that copy."""
         row_stride = row_stride or 4 * self.width
         frame_stride = frame_stride or row_stride * self.height
-        ok = self._lib.WebPGpuBatchEncodeRGBAHost(self._h, ptr, frame_stride, row_stride, n)
+        if next_ptr is not None:
+            ok = self._lib.WebPGpuBatchEncodeRGBAHostPrefetch(self._h, ptr, next_ptr, frame_stride,
+                                                             row_stride, n)
+        else:
+            ok = self._lib.WebPGpuBatchEncodeRGBAHost(self._h, ptr, frame_stride, row_stride, n)
         if not ok:
             raise RuntimeError("WebPGpuBatchEncodeRGBAHost failed: %s" % last_error())
         self.n = n

@@ -191,6 +191,8 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   if (!b) return;
   hipSetDevice(b->device);
   if (b->stream) hipStreamSynchronize(b->stream);
+  if (b->pf_busy) h2d_sdma_finish(b->pf_sig);
+  hipFree(b->d_rgba2);
   hipFree(b->d_g2l); hipFree(b->d_rgba); hipFree(b->d_yuv); hipFree(b->d_aflags); hipFree(b->d_alpha);
   hipFree(b->d_uva); hipFree(b->d_amode); hipFree(b->d_segmap); hipFree(b->d_params); hipFree(b->d_tokens);
   hipFree(b->d_arena); hipFree(b->d_arena_top); hipFree(b->d_mbpos); hipFree(b->d_rerun_snap);
@@ -1431,36 +1433,86 @@ static int host_is_pinned(const void* p) {
   return at.type == hipMemoryTypeHost;
 }
 
-int WebPGpuBatchEncodeRGBAHost(WebPGpuBatch* b, const uint8_t* rgba, size_t fstride, int rstride,
-                               int n) {
+/* Encode n frames from host memory; with `next` (pinned, same geometry),
+ * also start uploading the next batch into the spare buffer while this one
+ * encodes: a later call for `next` then finds its frames on the device. */
+static int encode_host(WebPGpuBatch* b, const uint8_t* rgba, const uint8_t* next, size_t fstride,
+                       int rstride, int n) {
   if (!b || !rgba || n <= 0 || n > b->max_frames || rstride < 4 * b->w) return 0;
   if (n > 1 && fstride < (size_t)rstride * b->h) return 0;
   CHK(hipSetDevice(b->device));
   const size_t need = (size_t)(n - 1) * fstride + (size_t)rstride * b->h;
-  if (need > b->d_rgba_cap) {
-    hipFree(b->d_rgba);
-    b->d_rgba = NULL;
-    b->d_rgba_cap = 0;
-    CHK(hipMalloc((void**)&b->d_rgba, need));
-    b->d_rgba_cap = need;
+  int have = 0;   /* this batch's frames already uploaded by the previous call */
+  if (b->pf_busy) {
+    h2d_sdma_finish(b->pf_sig);
+    b->pf_busy = 0;
+    if (b->pf_src == rgba && b->pf_need == need && b->pf_fstride == fstride &&
+        b->pf_rstride == rstride && b->pf_n == n) {
+      uint8_t* t = b->d_rgba;
+      const size_t tc = b->d_rgba_cap;
+      b->d_rgba = b->d_rgba2;
+      b->d_rgba_cap = b->d_rgba2_cap;
+      b->d_rgba2 = t;
+      b->d_rgba2_cap = tc;
+      have = 1;
+    }
   }
-  if (host_is_pinned(rgba)) {
-    /* page-locked (hipHostMalloc / hipHostRegister): one copy on an SDMA
-       engine (host/h2d_sdma.c) -- it runs beside the other engines' kernels,
-       where the runtime's copy kernel would wait for CUs a running K3 holds */
-    CHK(hipStreamSynchronize(b->stream));   /* (idle between batch calls) */
-    if (!h2d_sdma_upload(b->device, b->d_rgba, rgba, need))   /* an SDMA engine, no CU */
-      CHK(hipMemcpyAsync(b->d_rgba, rgba, need, hipMemcpyHostToDevice, b->stream));
-  } else {
-    /* pageable: an async copy of it on our non-blocking stream is not safe
-       on this platform (the runtime may read it from the GPU directly), so
-       drain the stream and copy synchronously */
-    CHK(hipStreamSynchronize(b->stream));
-    CHK(hipMemcpy(b->d_rgba, rgba, need, hipMemcpyHostToDevice));
+  if (!have) {
+    if (need > b->d_rgba_cap) {
+      hipFree(b->d_rgba);
+      b->d_rgba = NULL;
+      b->d_rgba_cap = 0;
+      CHK(hipMalloc((void**)&b->d_rgba, need));
+      b->d_rgba_cap = need;
+    }
+    if (host_is_pinned(rgba)) {
+      /* page-locked (hipHostMalloc / hipHostRegister): one copy on an SDMA
+         engine (host/h2d_sdma.c) -- it runs beside the other engines' kernels,
+         where the runtime's copy kernel would wait for CUs a running K3 holds */
+      CHK(hipStreamSynchronize(b->stream));   /* (idle between batch calls) */
+      if (!h2d_sdma_upload(b->device, b->d_rgba, rgba, need))   /* an SDMA engine, no CU */
+        CHK(hipMemcpyAsync(b->d_rgba, rgba, need, hipMemcpyHostToDevice, b->stream));
+    } else {
+      /* pageable: an async copy of it on our non-blocking stream is not safe
+         on this platform (the runtime may read it from the GPU directly), so
+         drain the stream and copy synchronously */
+      CHK(hipStreamSynchronize(b->stream));
+      CHK(hipMemcpy(b->d_rgba, rgba, need, hipMemcpyHostToDevice));
+    }
+  }
+  if (next && host_is_pinned(next)) {
+    /* the spare buffer was last read by the previous call's kernels, which
+       that call drained before returning */
+    if (need > b->d_rgba2_cap) {
+      hipFree(b->d_rgba2);
+      b->d_rgba2 = NULL;
+      b->d_rgba2_cap = 0;
+      CHK(hipMalloc((void**)&b->d_rgba2, need));
+      b->d_rgba2_cap = need;
+    }
+    if (h2d_sdma_upload_start(b->device, b->d_rgba2, next, need, &b->pf_sig)) {
+      b->pf_busy = 1;
+      b->pf_src = next;
+      b->pf_need = need;
+      b->pf_fstride = fstride;
+      b->pf_rstride = rstride;
+      b->pf_n = n;
+    }
   }
   return run_rgba(b, b->d_rgba, fstride, rstride, n, NULL);
 fail:
   return 0;
+}
+
+int WebPGpuBatchEncodeRGBAHost(WebPGpuBatch* b, const uint8_t* rgba, size_t fstride, int rstride,
+                               int n) {
+  return encode_host(b, rgba, NULL, fstride, rstride, n);
+}
+
+int WebPGpuBatchEncodeRGBAHostPrefetch(WebPGpuBatch* b, const uint8_t* rgba,
+                                       const uint8_t* rgba_next, size_t fstride, int rstride,
+                                       int n) {
+  return encode_host(b, rgba, rgba_next, fstride, rstride, n);
 }
 
 size_t WebPGpuBatchOutputSize(const WebPGpuBatch* b, int f) {

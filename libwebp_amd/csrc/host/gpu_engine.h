@@ -31,6 +31,15 @@ struct WebPGpuBatch {
   int ev0_recorded;
   /* device (HBM) */
   uint8_t* d_rgba;
+  /* the next batch's frames, uploaded while this one encodes
+     (WebPGpuBatchEncodeRGBAHostPrefetch): a second RGBA buffer and the
+     copy in flight into it */
+  uint8_t* d_rgba2;
+  size_t d_rgba2_cap;
+  const uint8_t* pf_src;
+  size_t pf_need, pf_fstride;
+  int pf_rstride, pf_n, pf_busy;
+  uint64_t pf_sig;
   uint16_t* d_g2l;   /* gamma tables: 256 x u16 then 33 x i32 */
   int32_t* d_l2g;
   uint8_t* d_yuv;

@@ -124,6 +124,30 @@ int h2d_sdma_upload(int device, void* dst, const void* src, size_t bytes) {
   return sdma_copy(&d->up, dst, d->gpu, src, d->cpu, bytes);
 }
 
+int h2d_sdma_upload_start(int device, void* dst, const void* src, size_t bytes, uint64_t* handle) {
+  if (!sdma_mode() || !lookup(device)) return 0;
+  /* no per-device lock: it runs while this engine's batch encodes, beside
+     the other engines' (blocking) uploads, which share the link with it */
+  dev_agents* d = &g_dev[device];
+  hsa_signal_t sig;
+  if (hsa_signal_create(1, 0, NULL, &sig) != HSA_STATUS_SUCCESS) return 0;
+  if (hsa_amd_memory_async_copy(dst, d->gpu, src, d->cpu, bytes, 0, NULL, sig) != HSA_STATUS_SUCCESS) {
+    hsa_signal_destroy(sig);
+    return 0;
+  }
+  *handle = sig.handle;
+  return 1;
+}
+
+void h2d_sdma_finish(uint64_t handle) {
+  hsa_signal_t sig;
+  sig.handle = handle;
+  while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                   HSA_WAIT_STATE_BLOCKED) >= 1) {
+  }
+  hsa_signal_destroy(sig);
+}
+
 int d2h_sdma_download(int device, void* dst, const void* src, size_t bytes) {
   if (!bytes) return 1;
   if (!sdma_mode() || !lookup(device)) return 0;

@@ -63,8 +63,9 @@ def parse_args(argv=None):
     ap.add_argument("--engines", type=int, default=0,
                     help="encoder instances on their own streams and host threads; steps are "
                          "dealt round-robin so one batch's host work overlaps another's kernels "
-                         "(0: 4 lossy -- profiles/r4/eng{3,4}_r4t.json: 4069-4146 MP/s with 3, "
-                         "4271-4272 with 4; 3 lossless -- profiles/r3/lab_*.json)")
+                         "(0: 6 lossy -- with the double-buffered upload 4321-4435 MP/s with 4, "
+                         "4446-4465 with 5, 4494-4497 with 6, profiles/r4/pf2; 3 lossless -- "
+                         "profiles/r3/lab_*.json)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="CPU work per baseline leg (single thread, all cores)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -414,7 +415,9 @@ def main(argv=None):
     W, H = args.width, args.height
     B = args.batch or (1024 if args.lossless else 256)
     if not args.engines:
-        args.engines = 3 if args.lossless else 4
+        # lossy: 6 instances with the double-buffered upload (4494-4497 MP/s
+        # against 4446-4465 with 5 and 4321-4435 with 4, profiles/r4/pf2)
+        args.engines = 3 if args.lossless else 6
     if not args.steps:
         args.steps = 3 * (1 if args.stub else args.engines)
 

@@ -386,7 +386,9 @@ __global__ __launch_bounds__(256) void k_analyze(const uint8_t* __restrict__ yuv
         const uint64_t one = 1ull << (16 * (v & 3));
         c0 += v < 4 ? one : 0ull;
         c1 += (v >= 4 && v < 8) ? one : 0ull;
+#ifndef K2_NO_ATOMIC   // (timing A/B only: drops bins 8..31)
         if (v >= 8) atomicAdd(&L.hist[hsel][v], 1);
+#endif
       }
       const int gsz = lane < 32 ? 16 : 8;
       for (int o = 1; o < gsz; o <<= 1) {

@@ -2978,6 +2978,69 @@ static int check_launch() { return hipGetLastError() == hipSuccess; }
     if ((x) != hipSuccess) return 0; \
   } while (0)
 
+// L0b: the repeat test of a frame (oracle/vp8l_model.py: repeat_stats). One
+// workgroup per frame: every sampled 8-pixel window (columns 0, 16, ..., rows
+// 0, ystep, ...) that is busy (no pixel equal to its left neighbour) goes
+// into an LDS hash set of its 32-bit key by linear probing; out[2f] = busy
+// windows, out[2f + 1] = those whose key was already in the set. The set
+// holds 2 x VP8L_REP_MAX_SAMPLES keys, so it never fills.
+#define REP_SLOTS (2 * VP8L_REP_MAX_SAMPLES)
+__global__ __launch_bounds__(1024) void k_vp8l_repeat(const uint8_t* __restrict__ rgba,
+                                                      size_t fstride, int rstride, int w, int h,
+                                                      int ystep, uint32_t* __restrict__ out) {
+  extern __shared__ uint32_t rset[];   // REP_SLOTS keys, 0 = empty
+  __shared__ uint32_t cnt[2];
+  const int f = blockIdx.x, t = threadIdx.x;
+  for (int i = t; i < REP_SLOTS; i += 1024) rset[i] = 0;
+  if (t < 2) cnt[t] = 0;
+  __syncthreads();
+  const int nx = (w - 8) / 16 + 1, ny = (h + ystep - 1) / ystep;
+  const uint8_t* F = rgba + (size_t)f * fstride;
+  uint32_t nb = 0, nr = 0;
+  for (int i = t; i < nx * ny; i += 1024) {
+    const int y = (i / nx) * ystep, x = (i % nx) * 16;
+    const uint8_t* q = F + (size_t)y * rstride + 4 * (size_t)x;
+    uint32_t key = 0, prev = 0;
+    bool busy = true;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t px = ((uint32_t)q[4 * k + 3] << 24) | ((uint32_t)q[4 * k] << 16) |
+                          ((uint32_t)q[4 * k + 1] << 8) | q[4 * k + 2];
+      if (k && px == prev) busy = false;
+      prev = px;
+      key = key * 0x9E3779B1u + px;
+    }
+    if (!busy) continue;
+    ++nb;
+    if (key == 0) key = 1;
+    uint32_t slot = (key * 0x85EBCA6Bu) % REP_SLOTS;
+    for (;;) {
+      const uint32_t old = atomicCAS(&rset[slot], 0u, key);
+      if (old == 0u) break;
+      if (old == key) { ++nr; break; }
+      slot = slot + 1 == REP_SLOTS ? 0 : slot + 1;
+    }
+  }
+  atomicAdd(&cnt[0], nb);
+  atomicAdd(&cnt[1], nr);
+  __syncthreads();
+  if (t < 2) out[2 * f + t] = cnt[t];
+}
+
+extern "C" int vp8l_launch_repeat(const uint8_t* rgba, size_t fstride, int rstride, int w, int h,
+                                  int n, int ystep, uint32_t* out, void* stream) {
+  if (w < 8 || h <= 0 || n <= 0 || ystep <= 0) return 0;
+  if ((size_t)((w - 8) / 16 + 1) * (size_t)((h + ystep - 1) / ystep) > VP8L_REP_MAX_SAMPLES) return 0;
+  static bool lds_ok = [] {
+    return hipFuncSetAttribute((const void*)k_vp8l_repeat, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(REP_SLOTS * sizeof(uint32_t))) == hipSuccess;
+  }();
+  if (!lds_ok) return 0;
+  hipLaunchKernelGGL(k_vp8l_repeat, dim3(n), dim3(1024), REP_SLOTS * sizeof(uint32_t),
+                     (hipStream_t)stream, rgba, fstride, rstride, w, h, ystep, out);
+  return check_launch();
+}
+
 extern "C" int vp8l_launch_scan(const uint8_t* rgba, size_t fstride, int rstride, int w, int h,
                                 int n, int plane, uint32_t* ehist, uint32_t* pal, void* stream) {
   if (w <= 0 || h <= 0 || n <= 0) return 0;

@@ -39,7 +39,8 @@ static int sub_sample(int size, int bits) { return (size + (1 << bits) - 1) >> b
 
 void vp8l_engine_free(vp8l_engine* l) {
   if (!l) return;
-  for (int i = 0; i < 5; ++i) vp8l_engine_free(l->sub[i]);
+  for (int i = 0; i < 6; ++i) vp8l_engine_free(l->sub[i]);
+  hipFree(l->d_rep); hipHostFree(l->h_rep);
   free(l->route_eng); free(l->route_slot);
   hipFree(l->d_minb); hipFree(l->d_cseg); hipFree(l->d_prov); hipFree(l->d_chist); hipFree(l->d_cbits);
   hipFree(l->d_ehist); hipFree(l->d_scan); hipFree(l->d_fidx); hipFree(l->d_fmode);
@@ -112,11 +113,13 @@ static vp8l_engine* engine_alloc(const vp8l_params* p, int max_frames, int metho
     CHK(hipMalloc((void**)&l->d_scan, N * VP8L_PAL_STRIDE * sizeof(uint32_t)));
     CHK(hipHostMalloc((void**)&l->h_ehist, N * VP8L_EHIST * sizeof(uint32_t), 0));
     CHK(hipHostMalloc((void**)&l->h_scan, N * VP8L_PAL_STRIDE * sizeof(uint32_t), 0));
+    CHK(hipMalloc((void**)&l->d_rep, N * 2 * sizeof(uint32_t)));
+    CHK(hipHostMalloc((void**)&l->h_rep, N * 2 * sizeof(uint32_t), 0));
     l->route_eng = (vp8l_engine**)calloc(N, sizeof(*l->route_eng));
     l->route_slot = (int*)calloc(N, sizeof(int));
     if (!l->route_eng || !l->route_slot) goto fail;
   }
-  if (l->p.palette) {   /* the cost-model parse (vp8l_launch_analyze with lz) */
+  if (l->p.palette || l->p.lz) {   /* the cost-model parse (vp8l_launch_analyze with lz) */
     CHK(hipMalloc((void**)&l->lz.runs, N * np * sizeof(uint16_t)));
     CHK(hipMalloc((void**)&l->lz.htab, N * VP8L_LZ_HASH_SIZE * sizeof(int32_t)));
     CHK(hipMalloc((void**)&l->lz.chain, N * np * sizeof(int32_t)));
@@ -138,6 +141,8 @@ static vp8l_engine* engine_alloc(const vp8l_params* p, int max_frames, int metho
       l->lz.dcodes = l->d_dcodes;
       l->lz.nd = nd;
     }
+  }
+  if (l->p.palette) {
     CHK(hipMalloc((void**)&l->d_psort, N * VP8L_MAX_PALETTE * sizeof(uint32_t)));
     CHK(hipMalloc((void**)&l->d_psidx, N * VP8L_MAX_PALETTE));
     CHK(hipMalloc((void**)&l->d_npal, N * sizeof(int)));
@@ -362,7 +367,7 @@ static int pipeline(vp8l_engine* l, hipStream_t st, int threads, const uint8_t* 
   }
   if (!vp8l_launch_analyze(l->d_argb, &p, l->d_tabs, l->d_minb, l->d_cseg, l->d_prov, l->d_chist,
                            l->d_cbits, l->d_ops, l->d_feat, l->d_tl, l->d_tn, l->d_hc,
-                           l->d_assign, p.palette ? &l->lz : NULL, &dp, st))
+                           l->d_assign, (p.palette || p.lz) ? &l->lz : NULL, &dp, st))
     goto fail;
   CHK(hipEventRecord(l->ev[2], st));
   {   /* debugging aid: LIBWEBP_AMD_VP8L_DUMP=<prefix> writes slot 0's
@@ -532,11 +537,20 @@ int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t*
                      hipMemcpyDeviceToHost, st));
   CHK(hipMemcpyAsync(l->h_scan, l->d_scan, N * VP8L_PAL_STRIDE * sizeof(uint32_t),
                      hipMemcpyDeviceToHost, st));
+  /* repeat-heavy frames (oracle/vp8l_model.py: repeat_heavy) take the hash
+     chain; not for ALPH planes nor method 0 */
+  const int rep_on = !l->p.alpha && !l->p.low_effort && l->p.w >= 8;
+  if (rep_on) {
+    if (!vp8l_launch_repeat(rgba, fstride, rstride, l->p.w, l->p.h, n,
+                            vp8l_repeat_ystep(l->p.w, l->p.h), l->d_rep, st))
+      goto fail;
+    CHK(hipMemcpyAsync(l->h_rep, l->d_rep, N * 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  }
   CHK(hipStreamSynchronize(st));
   {
     /* [0..3] palette engines by xbits, [4] root, [5] sub[4]: non-palette
        frames whose colours fit a palette take the palette histogram bits */
-    int cnt[6] = {0, 0, 0, 0, 0, 0};
+    int cnt[7] = {0, 0, 0, 0, 0, 0, 0};   /* [6] sub[5] */
     const int ntt_pal = sub_sample(l->p.w, vp8l_transform_bits(l->method,
                                    vp8l_histo_bits_palette(l->method, l->p.w, l->p.h)));
     const int ntiles_pal = ntt_pal * sub_sample(l->p.h, vp8l_transform_bits(l->method,
@@ -552,6 +566,7 @@ int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t*
                                 : (uint8_t)vp8l_entropy_choice(l->h_ehist + (size_t)f * VP8L_EHIST,
                                                                npal, ntiles);
       if (mode[f] == VP8L_MODE_PALETTE) cnt[xbits_of(npal)]++;
+      else if (!npal && rep_on && vp8l_repeat_heavy(l->h_rep + 2 * (size_t)f)) cnt[6]++;
       else cnt[npal ? 5 : 4]++;
     }
     if (cnt[5] && !(l->sub[4] && l->sub[4]->max_frames >= cnt[5])) {
@@ -560,6 +575,19 @@ int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t*
       vp8l_setup_params_palette_hb(&pp, l->p.w, l->p.h, cnt[5], l->method, l->p.alpha);
       l->sub[4] = engine_alloc(&pp, cnt[5], l->method, 0);
       if (!l->sub[4]) { free(mode); goto fail; }
+    }
+    if (cnt[6] && !(l->sub[5] && l->sub[5]->max_frames >= cnt[6])) {
+      vp8l_engine_free(l->sub[5]);
+      vp8l_params pp = l->p;
+      pp.lz = 1;
+      l->sub[5] = engine_alloc(&pp, cnt[6], l->method, 0);
+      if (!l->sub[5]) { free(mode); goto fail; }
+    }
+    if (l->sub[5]) {
+      l->sub[5]->nl_bits = l->nl_bits;
+      l->sub[5]->p.nlq_bits = l->p.nlq_bits;
+      l->sub[5]->p.exact = l->p.exact;
+      l->sub[5]->p.low_effort = l->p.low_effort;
     }
     if (l->sub[4]) {   /* the root's per-call settings */
       l->sub[4]->nl_bits = l->nl_bits;
@@ -575,12 +603,14 @@ int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t*
       l->sub[xb] = engine_alloc(&pp, cnt[xb], l->method, 0);
       if (!l->sub[xb]) { free(mode); goto fail; }
     }
-    int used[6] = {0, 0, 0, 0, 0, 0};
+    int used[7] = {0, 0, 0, 0, 0, 0, 0};
     for (int f = 0; f < n; ++f) {
       const uint32_t* sc = l->h_scan + (size_t)f * VP8L_PAL_STRIDE;
       if (mode[f] != VP8L_MODE_PALETTE) {
-        vp8l_engine* e = sc[0] <= VP8L_MAX_PALETTE ? l->sub[4] : l;
-        const int s = used[e == l ? 4 : 5]++;
+        const int lzf = sc[0] > VP8L_MAX_PALETTE && rep_on &&
+                        vp8l_repeat_heavy(l->h_rep + 2 * (size_t)f);
+        vp8l_engine* e = lzf ? l->sub[5] : sc[0] <= VP8L_MAX_PALETTE ? l->sub[4] : l;
+        const int s = used[lzf ? 6 : e == l ? 4 : 5]++;
         e->h_fidx[s] = f;
         e->h_fmode[s] = mode[f];
         /* the reference's own predictor choice where GetResidual updates the
@@ -622,6 +652,9 @@ int vp8l_engine_encode(vp8l_engine* l, void* stream, int threads, const uint8_t*
                              timings))
       goto fail;
     if (used[5] && !pipeline(l->sub[4], st, threads, rgba, fstride, rstride, used[5], 0,
+                             l->d_ehist, timings))
+      goto fail;
+    if (used[6] && !pipeline(l->sub[5], st, threads, rgba, fstride, rstride, used[6], 0,
                              l->d_ehist, timings))
       goto fail;
     for (int xb = 0; xb < 4; ++xb)

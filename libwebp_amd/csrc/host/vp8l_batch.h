@@ -19,8 +19,9 @@ typedef struct vp8l_engine {
   /* the root engine decides per frame: its own slots take the spatial /
    * direct / subtract-green frames, palette engines (one per bundling,
    * created on demand) the colour-indexed ones; route_* map frame -> slot */
-  struct vp8l_engine* sub[5];   /* [0..3] palette by bundling, [4] spatial / direct frames
-                                   whose colours fit a palette (palette histogram bits) */
+  struct vp8l_engine* sub[6];   /* [0..3] palette by bundling, [4] spatial / direct frames
+                                   whose colours fit a palette (palette histogram bits),
+                                   [5] repeat-heavy frames of more colours (p.lz) */
   struct vp8l_engine** route_eng;
   int* route_slot;
   /* device (HBM) */
@@ -34,6 +35,8 @@ typedef struct vp8l_engine {
   uint8_t* d_cbits;            /* chosen cache bits per slot */
   uint32_t* d_ehist;           /* L0 entropy histograms (root engine) */
   uint32_t* d_scan;            /* L0 colour sets (root engine) */
+  uint32_t* d_rep;             /* L0b repeat test, 2 words per frame (root engine) */
+  uint32_t* h_rep;
   int* d_fidx;                 /* input frame of each slot */
   uint8_t* d_fmode;            /* entropy mode of each slot */
   uint32_t* d_psort;           /* palette engine: sorted palette per slot */

@@ -110,6 +110,8 @@ typedef struct {
   int nlq_bits;                    /* predictor near-lossless quantisation
                                       (VP8LNearLosslessBits; 0 = off) */
   int low_effort;                  /* method 0: predictor 11 everywhere, no cross colour */
+  int lz;                          /* non-palette engine of repeat-heavy frames: the
+                                      cost-model parse over the hash chain, no cache */
 } vp8l_params;
 
 /* the engine's table block (tabs): nlogn 0..4096 (int, 1/4096 bit) | log2
@@ -124,6 +126,25 @@ typedef struct {
  * plane: the input is ALPH alpha planes (1 byte per pixel, coded as green). */
 int vp8l_launch_scan(const uint8_t* rgba, size_t fstride, int rstride, int w, int h, int n,
                      int plane, uint32_t* ehist, uint32_t* pal, void* stream);
+/* L0b: the repeat test (oracle/vp8l_model.py: repeat_stats) of n RGBA
+ * frames: out[2f] busy sampled windows, out[2f + 1] repeats among them;
+ * ystep from vp8l_repeat_ystep. Frames with more than 256 colours that pass
+ * it (vp8l_repeat_heavy) take the cost-model parse over the hash chain
+ * (vp8l_params::lz). */
+#define VP8L_REP_MAX_SAMPLES 16384
+#define VP8L_REP_MIN_BUSY 64
+#define VP8L_REP_FRAC_DEN 10
+int vp8l_launch_repeat(const uint8_t* rgba, size_t fstride, int rstride, int w, int h, int n,
+                       int ystep, uint32_t* out, void* stream);
+static inline int vp8l_repeat_ystep(int w, int h) {
+  const long nx = w >= 8 ? (w - 8) / 16 + 1 : 0;
+  int k = 1;
+  while (nx * ((h + 4L * k - 1) / (4L * k)) > VP8L_REP_MAX_SAMPLES) ++k;
+  return 4 * k;
+}
+static inline int vp8l_repeat_heavy(const uint32_t* rep) {
+  return rep[0] >= VP8L_REP_MIN_BUSY && (uint64_t)VP8L_REP_FRAC_DEN * rep[1] >= rep[0];
+}
 /* L1: per slot f the input frame fidx[f] (NULL: f); entropy mode fmode[f]
  * (0..3): subtract green (mode & 2), per-tile predictor + cross colour
  * (mode & 1). The predictor: the reference's own choice (L1a) for slots with

@@ -30,7 +30,7 @@ VP8L_SIZE_TOL = 0.02
 # 1.042)
 # tiled syn-v1 / text over a gradient (more than 256 colours, long-range
 # repeats: tests/golden/make_lossless_golden.py)
-KIND_TOL = {"syn": 0.02, "g": 0.05, "q": 0.035, "q16": 0.02, "tile": 0.20, "text": 0.05}
+KIND_TOL = {"syn": 0.02, "g": 0.05, "q": 0.035, "q16": 0.02, "tile": 0.02, "text": 0.05}
 
 
 def kind_tol(kind):
@@ -590,6 +590,32 @@ def test_gpu_mixed_modes_batch(gpu):
         assert got[f] == M.encode(frames[f]), "frame %d" % f
 
 
+def test_repeat_test_separates_fixtures():
+    """the repeat test (model: repeat_stats) sends the copied-tile pictures,
+    and none of the other fixture kinds, to the hash-chain parse"""
+    seen = set()
+    for c in lossless_cases(1 << 30):
+        k = (c["kind"], c["w"], c["h"], c["frame"])
+        if k in seen or c["kind"][0] == "g":
+            continue
+        seen.add(k)
+        img = lossless_picture(*k)
+        assert M.repeat_heavy(img) == (c["kind"] == "tile"), (k, M.repeat_stats(img))
+
+
+@pytest.mark.gpu
+def test_gpu_repeat_routing_batch(gpu):
+    """repeat-heavy frames (the lz sub-engine) beside spatial and palette
+    frames in one batch: routed back to their frame, bit-exact with the model"""
+    w, h = 320, 192
+    frames = np.stack([tiled(w, h, 0), syn_v1(w, h, 1), graphics(w, h, 16, 2), tiled(w, h, 5),
+                       tiled(w, h, 3)])   # (the last one has too few repeats: the local parse)
+    assert [M.repeat_heavy(f) for f in frames] == [True, False, False, True, False]
+    got = gpu_encode(gpu, frames)
+    for f in range(len(frames)):
+        assert got[f] == M.encode(frames[f]), "frame %d" % f
+
+
 @pytest.mark.gpu
 def test_gpu_1080p_decodes_exact_and_size(gpu):
     import json
@@ -626,14 +652,11 @@ def test_gpu_1080p_palette_and_direct_sizes(gpu):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", [
-    pytest.param("tile", marks=pytest.mark.xfail(
-        reason="repeated tiles rows away need the hash-chain parse on non-palette frames "
-               "(open gap: 1.29x the reference, DESIGN.md section 9)", strict=False)),
+    "tile",    # repeat-heavy: the hash-chain parse (model 0.964x the reference; 1.29x before)
     "text"])   # direct-mode text over a gradient: 1.31x with the greedy parse, 1.037x with
                # the shortest-path parse over 32 plane codes + the colour cache (L3d)
 def test_gpu_1080p_repeat_sizes(gpu, kind):
-    """decode-exact always; size within the kind's tolerance of the reference
-    (tile: the open gap)"""
+    """decode-exact always; size within the kind's tolerance of the reference"""
     c = [c for c in lossless_cases(1 << 30) if c["kind"] == kind and c["w"] == 1920][0]
     img = lossless_picture(c["kind"], c["w"], c["h"], c["frame"])
     got = gpu_encode(gpu, img[None])[0]

@@ -2323,32 +2323,83 @@ __global__ __launch_bounds__(64) void k_lz_dp(const uint32_t* __restrict__ argb,
   const int32_t* cA = S.tab + 792;
   const int32_t* cD = S.tab + 1048;
   const int myk = ln < LZ_NLEN ? kLzLengths[ln] : 0;
-  for (int j = 0; j < m; ++j) {
-    const int i = s + j;
-    const int c = S.cost[j];
-    if (ln == 0) {
-      const uint32_t a = E[i];
-      const int v = c + ((cA[a >> 24] + cR[(a >> 16) & 255] + cG[(a >> 8) & 255] + cB[a & 255]) *
-                         82) / 100;
-      if (v < S.cost[j + 1]) { S.cost[j + 1] = v; S.ch[j + 1] = 1; }
+  int lcost_my = 0;   // this lane's listed length: its prefix cost (per frame)
+  if (myk) {
+    int sym, nb; uint32_t ex;
+    prefix_enc((uint32_t)myk, sym, nb, ex);
+    lcost_my = cG[256 + sym] + 256 * nb;
+  }
+  // Everything a position needs that does not depend on the path costs --
+  // its literal cost, and per match the length L, the distance's cost, the
+  // own-length lane's length and cost -- is worked out 64 positions at a
+  // time, one position per lane, and read back with readlane in the serial
+  // walk; the chunk's inputs are loaded a chunk ahead. (With the loads and
+  // the distance-code lookup on the walk's path it waited ~1 us per
+  // position: 175 ms per launch on 64 copied-tile 1080p frames,
+  // profiles/r4/lzprof.)
+  uint32_t pa = 0, ph = 0, pl = 0, phl = 0, pll = 0;
+  auto fetch = [&](int j0) {
+    const int q = j0 + ln;
+    pa = ph = pl = phl = pll = 0;
+    if (q < m) {
+      const size_t i = base + s + q;
+      pa = E[s + q]; ph = hoff[i]; pl = loff[i]; phl = hlen[i]; pll = llen[i];
     }
+  };
+  fetch(0);
+  for (int j0 = 0; j0 < m; j0 += 64) {
+    const uint32_t ca = pa, cd[2] = {ph, pl}, cl[2] = {phl, pll};
+    if (j0 + 64 < m) fetch(j0 + 64);   // in flight during this chunk
+    const int jn = min(64, m - j0);
+    const int q = j0 + ln, rem = e - (s + q);   // positions left in the segment from q
+    const int litc = ((cA[ca >> 24] + cR[(ca >> 16) & 255] + cG[(ca >> 8) & 255] + cB[ca & 255]) *
+                      82) / 100;
+    int mL[2], mdc[2], mok[2], mol[2];
 #pragma unroll
     for (int mk = 0; mk < 2; ++mk) {
-      const uint32_t d = mk == 0 ? hoff[base + i] : loff[base + i];
-      const int L = min((int)(mk == 0 ? hlen[base + i] : llen[base + i]), e - i);
-      if (L < 2) continue;   // wave-uniform
-      int sym, nb; uint32_t ex;
-      prefix_enc(lz_dcode(dcodes, nd, d), sym, nb, ex);
-      const int dc = c + cD[sym] + 256 * nb;
-      // lane LZ_NLEN takes the match's own length when it is not in the list
-      bool own_listed = false;
+      const int L = q < m ? min((int)cl[mk], rem) : 0;
+      mL[mk] = L;
+      mdc[mk] = mok[mk] = mol[mk] = 0;
+      if (L >= 2) {
+        int sym, nb; uint32_t ex;
+        prefix_enc(lz_dcode(dcodes, nd, cd[mk]), sym, nb, ex);
+        mdc[mk] = cD[sym] + 256 * nb;
+        bool own_listed = false;
 #pragma unroll
-      for (int t = 0; t < LZ_NLEN; ++t) own_listed |= kLzLengths[t] == L;
-      const int k = ln < LZ_NLEN ? myk : (ln == LZ_NLEN && !own_listed ? L : 0);
-      if (k >= 2 && k <= L) {
-        prefix_enc((uint32_t)k, sym, nb, ex);
-        const int v = dc + cG[256 + sym] + 256 * nb;
-        if (v < S.cost[j + k]) { S.cost[j + k] = v; S.ch[j + k] = (uint16_t)k; S.dd[j + k] = d; }
+        for (int t = 0; t < LZ_NLEN; ++t) own_listed |= kLzLengths[t] == L;
+        if (!own_listed) {
+          prefix_enc((uint32_t)L, sym, nb, ex);
+          mok[mk] = L;
+          mol[mk] = cG[256 + sym] + 256 * nb;
+        }
+      }
+    }
+    for (int jj = 0; jj < jn; ++jj) {
+      const int j = j0 + jj;
+      const int c = S.cost[j];
+      if (ln == 0) {
+        const int v = c + __builtin_amdgcn_readlane(litc, jj);
+        if (v < S.cost[j + 1]) { S.cost[j + 1] = v; S.ch[j + 1] = 1; }
+      }
+#pragma unroll
+      for (int mk = 0; mk < 2; ++mk) {
+        const int L = __builtin_amdgcn_readlane(mL[mk], jj);
+        if (L < 2) continue;   // wave-uniform
+        const int dc = c + __builtin_amdgcn_readlane(mdc[mk], jj);
+        // lane LZ_NLEN takes the match's own length when it is not in the list
+        int k = myk, lc = lcost_my;
+        if (ln == LZ_NLEN) {
+          k = __builtin_amdgcn_readlane(mok[mk], jj);
+          lc = __builtin_amdgcn_readlane(mol[mk], jj);
+        }
+        if (k >= 2 && k <= L) {
+          const int v = dc + lc;
+          if (v < S.cost[j + k]) {
+            S.cost[j + k] = v;
+            S.ch[j + k] = (uint16_t)k;
+            S.dd[j + k] = (uint32_t)__builtin_amdgcn_readlane((int)cd[mk], jj);
+          }
+        }
       }
     }
   }

@@ -2069,13 +2069,26 @@ __device__ __forceinline__ uint32_t lz_hash(uint32_t a, uint32_t b) {
 // R[q] = equal pixels starting at q, capped at LZ_MAX_LENGTH + 3 (model:
 // lz_runs): one wave per frame, 64-pixel chunks from the end, a run reaching
 // a chunk's end continues with the next chunk's first run.
+// Runs of equal pixels (capped at LZ_MAX_LENGTH + 3), one wave per piece of
+// LZ_RUN_PIECE positions: the walk goes backwards 64 positions at a time and
+// starts LZ_RUN_LOOK positions past the piece with no carry. The run it has
+// at the piece's last position is then the capped run of the whole-frame
+// walk (a run reaching the walk's start is at least LZ_RUN_LOOK long there,
+// past the cap), so every piece matches one backward walk over the frame.
+#define LZ_RUN_PIECE 16384
+#define LZ_RUN_LOOK 4160
+static_assert(LZ_RUN_LOOK >= LZ_MAX_LENGTH + 4 && LZ_RUN_LOOK % 64 == 0 && LZ_RUN_PIECE % 64 == 0,
+              "the look-ahead must cover the run cap");
 __global__ __launch_bounds__(64) void k_lz_runs(const uint32_t* __restrict__ argb, int npix,
                                                 uint16_t* __restrict__ runs) {
-  const int f = blockIdx.x, ln = lane_id();
+  const int f = blockIdx.y, ln = lane_id();
+  const int p0 = blockIdx.x * LZ_RUN_PIECE;
+  if (p0 >= npix) return;   // whole wave
+  const int p1 = min(npix, p0 + LZ_RUN_PIECE), top = min(npix, p1 + LZ_RUN_LOOK);
   const uint32_t* E = argb + (size_t)f * npix;
   uint16_t* R = runs + (size_t)f * npix;
   int carry = 0;   // run at the first position of the chunk after this one
-  for (int c = (npix - 1) >> 6; c >= 0; --c) {
+  for (int c = (top - 1) >> 6; c >= (p0 >> 6); --c) {
     const int q = (c << 6) + ln;
     const bool valid = q < npix;
     const bool eq = valid && q + 1 < npix && E[q] == E[q + 1];
@@ -2084,7 +2097,7 @@ __global__ __launch_bounds__(64) void k_lz_runs(const uint32_t* __restrict__ arg
     int run = (miss ? (int)__builtin_ctzll(miss) : 64) + 1;   // this pixel + equal followers
     if (run == 65 - ln) run += carry - 1 >= 0 ? carry - 1 : 0;
     if (run > LZ_MAX_LENGTH + 3) run = LZ_MAX_LENGTH + 3;
-    if (valid) R[q] = (uint16_t)run;
+    if (valid && q < p1) R[q] = (uint16_t)run;
     carry = __shfl(run, 0);
   }
 }
@@ -3501,7 +3514,8 @@ extern "C" int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
                        (const uint2*)nullptr, 1, *p, ops);
     hipLaunchKernelGGL(k_vp8l_parse, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, *p, ops, prov,
                        (const uint8_t*)cbits);   // the greedy parse: first costs
-    hipLaunchKernelGGL(k_lz_runs, dim3(p->n), dim3(64), 0, st, argb, npix, lz->runs);
+    hipLaunchKernelGGL(k_lz_runs, dim3((npix + LZ_RUN_PIECE - 1) / LZ_RUN_PIECE, p->n), dim3(64), 0,
+                       st, argb, npix, lz->runs);
     hipLaunchKernelGGL(k_lz_chain, dim3(p->n), dim3(64), 0, st, argb, npix,
                        (const uint16_t*)lz->runs, lz->htab, lz->chain);
     hipLaunchKernelGGL(k_lz_search, dim3((npix + 255) / 256, p->n), dim3(256), 0, st, argb, p->w,

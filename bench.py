@@ -64,7 +64,9 @@ def parse_args(argv=None):
                     help="encoder instances on their own streams and host threads; steps are "
                          "dealt round-robin so one batch's host work overlaps another's kernels "
                          "(0: 6 lossy -- with the double-buffered upload 4321-4435 MP/s with 4, "
-                         "4446-4465 with 5, 4494-4497 with 6, profiles/r4/pf2; 3 lossless -- "
+                         "4446-4465 with 5, 4494-4497 with 6, profiles/r4/pf2; 8 gave 4535-4546 "
+                         "against 4409-4533 for 6 on one box, profiles/r4/eng68: kept at 6 for "
+                         "the host threads of 8 ranks on one node; 3 lossless -- "
                          "profiles/r3/lab_*.json)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="CPU work per baseline leg (single thread, all cores)")

@@ -2310,10 +2310,11 @@ __constant__ int16_t kLzLengths[32] = {2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 1
 #define LZ_NLEN 30
 struct LzSmem {
   int32_t cost[LZ_SEG + 1];
-  uint16_t ch[LZ_SEG + 1];
-  uint32_t dd[LZ_SEG + 1];
+  uint32_t cd[LZ_SEG + 1];   // choice ending here: length k (12 bits) | distance << 12 (18 bits)
   int32_t tab[LZ_NCOST];
 };
+static_assert(LZ_MAX_LENGTH < (1 << 12) && LZ_WINDOW_CAP < (1 << 18) && 16384 + 1 < (1 << 18),
+              "LzSmem::cd packs a length and a distance (window, or a local one <= width + 1)");
 __global__ __launch_bounds__(64) void k_lz_dp(const uint32_t* __restrict__ argb, int W, int npix,
                                               const int32_t* __restrict__ costs,
                                               const uint32_t* __restrict__ hoff,
@@ -2328,7 +2329,7 @@ __global__ __launch_bounds__(64) void k_lz_dp(const uint32_t* __restrict__ argb,
   const uint32_t* E = argb + (size_t)f * npix;
   const size_t base = (size_t)f * npix;
   for (int i = ln; i < LZ_NCOST; i += 64) S.tab[i] = costs[(size_t)f * LZ_NCOST + i];
-  for (int i = ln; i <= m; i += 64) { S.cost[i] = i ? LZ_INF : 0; S.ch[i] = 0; S.dd[i] = 0; }
+  for (int i = ln; i <= m; i += 64) { S.cost[i] = i ? LZ_INF : 0; S.cd[i] = 0; }
   __syncthreads();
   const int32_t* cG = S.tab;
   const int32_t* cR = S.tab + 280;
@@ -2392,7 +2393,7 @@ __global__ __launch_bounds__(64) void k_lz_dp(const uint32_t* __restrict__ argb,
       const int c = S.cost[j];
       if (ln == 0) {
         const int v = c + __builtin_amdgcn_readlane(litc, jj);
-        if (v < S.cost[j + 1]) { S.cost[j + 1] = v; S.ch[j + 1] = 1; }
+        if (v < S.cost[j + 1]) { S.cost[j + 1] = v; S.cd[j + 1] = 1; }
       }
 #pragma unroll
       for (int mk = 0; mk < 2; ++mk) {
@@ -2409,8 +2410,7 @@ __global__ __launch_bounds__(64) void k_lz_dp(const uint32_t* __restrict__ argb,
           const int v = dc + lc;
           if (v < S.cost[j + k]) {
             S.cost[j + k] = v;
-            S.ch[j + k] = (uint16_t)k;
-            S.dd[j + k] = (uint32_t)__builtin_amdgcn_readlane((int)cd[mk], jj);
+            S.cd[j + k] = (uint32_t)k | ((uint32_t)__builtin_amdgcn_readlane((int)cd[mk], jj) << 12);
           }
         }
       }
@@ -2422,10 +2422,11 @@ __global__ __launch_bounds__(64) void k_lz_dp(const uint32_t* __restrict__ argb,
   if (ln == 0) {
     int j = m;
     while (j > 0) {
-      const int k = S.ch[j];
+      const uint32_t cdj = S.cd[j];
+      const int k = (int)(cdj & 4095u);
       const int st = j - k;
       if (k >= 2) {
-        S.cost[st] = (int32_t)(2u | ((uint32_t)(k - 1) << 2) | (lz_dcode(dcodes, nd, S.dd[j]) << 14));
+        S.cost[st] = (int32_t)(2u | ((uint32_t)(k - 1) << 2) | (lz_dcode(dcodes, nd, cdj >> 12) << 14));
         for (int t = st + 1; t < j; ++t) S.cost[t] = 3;
       } else {
         S.cost[st] = 0;

@@ -491,10 +491,12 @@ def main(argv=None):
                                          low_memory=int(args.low_memory)))
 
     # input of a step: "host" = RGBA in pinned host memory, uploaded by the
-    # step itself: WebPGpuBatchEncodeRGBAHost puts the DMA
-    # copy on the encoder instance's own stream ahead of its K1, so it runs
-    # while the other instances' kernels occupy the CUs; "hbm" = the frames
-    # already in HBM
+    # step itself: WebPGpuBatchEncodeRGBAHostPrefetch copies
+    # the batch with a blocking HSA SDMA transfer under a per-device mutex
+    # (host/h2d_sdma.c: a copy engine, no CU) unless the previous call already
+    # prefetched it, and starts the next batch's SDMA copy into the engine's
+    # spare buffer, which then overlaps the current batch's kernels and host
+    # stages; "hbm" = the frames already in HBM
     host_in = args.input == "host" and not args.stub
     pinned = None
 
@@ -635,6 +637,12 @@ def main(argv=None):
             line["cpu_baseline"] = cb
         if not args.stub:
             line["host_cpus_per_rank"] = len(cpus) if cpus else "unpinned"
+            line["host_threads_per_rank"] = {
+                "budget": libwebp_amd.host_thread_budget(gpu_dev)[0],
+                "engines": len(encs),
+                "note": "every engine of the rank draws its host-phase helper threads from "
+                        "one pool of `budget` threads (cgroup quota / LOCAL_WORLD_SIZE, "
+                        "pinned CPUs; host/host_cpus.c)"}
             if hbm_used is not None:
                 line["hbm_used_gb"] = hbm_used
         if args.stub:
@@ -702,7 +710,7 @@ def lossy_line(args, world, B, W, H, elapsed, tails, total_bytes, ntok, solo=Non
                                          "the other instance's kernels beside it); "
                                          "k_encode_solo_ms: one step on one instance alone, "
                                          "the time `achieved` uses (≈ rocprof's average, "
-                                         "profiles/r4/kernel_stats_solo_r4z.csv)",
+                                         "profiles/r5/kernel_stats_solo_r6a.csv)",
                      "algorithmic_bytes_per_launch": k3_bytes,
                      # the roof that binds K3: vector issue
                      "issue": issue},

@@ -25,7 +25,8 @@ typedef struct WebPGpuBatch WebPGpuBatch;
 
 /* Create an encoder for up to max_frames frames of width x height, on HIP
  * device `device`, with `config` (lossy, method 3..6). host_threads <= 0
- * picks a default (env WEBP_AMD_THREADS, else min(16, online CPUs)).
+ * picks a default (env WEBP_AMD_THREADS, else min(16, the rank's host-thread
+ * budget, WebPGpuHostThreadBudget)).
  * Returns NULL on error (no GPU, bad config, out of memory). */
 WEBP_EXTERN WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height,
                                           int max_frames,
@@ -117,6 +118,13 @@ WEBP_EXTERN const char* WebPGpuLastError(void);
  * Writes up to max_cpus CPU ids into cpus and returns how many there are
  * (0 when the node is unknown: threads are then not pinned). */
 WEBP_EXTERN int WebPGpuHostCpus(int device, int* cpus, int max_cpus);
+
+/* Host-thread budget of this rank on `device`: the cgroup CPU quota (or
+ * WEBP_AMD_CPU_QUOTA) over LOCAL_WORLD_SIZE, capped by the pinned CPUs above
+ * and the online CPUs. All engines of the process draw the helper threads of
+ * their host phases from one pool of this size; *busy (may be NULL) receives
+ * the threads inside host phases right now. */
+WEBP_EXTERN int WebPGpuHostThreadBudget(int device, int* busy);
 
 /* Number of HIP devices visible (0 when no GPU / no driver). */
 WEBP_EXTERN int WebPGpuDeviceCount(void);

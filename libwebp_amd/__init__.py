@@ -63,6 +63,7 @@ def load():
         "WebPGpuSynthRGBA": (i, [vp, sz, i, i, i, i, i, vp]),
         "WebPGpuDeviceCount": (i, []),
         "WebPGpuHostCpus": (i, [i, C.POINTER(C.c_int), i]),
+        "WebPGpuHostThreadBudget": (i, [i, C.POINTER(C.c_int)]),
         "WebPGpuLastError": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
@@ -211,6 +212,14 @@ def host_cpus(device):
     buf = (C.c_int * max(n, 1))()
     n = lib.WebPGpuHostCpus(device, buf, n)
     return list(buf[:n])
+
+
+def host_thread_budget(device):
+    """(budget, busy): the rank's host-thread pool size on `device` (cgroup
+    quota over LOCAL_WORLD_SIZE, pinned CPUs) and the threads in host phases."""
+    busy = C.c_int(0)
+    n = load().WebPGpuHostThreadBudget(device, C.byref(busy))
+    return n, busy.value
 
 
 def synth_device(ptr, width, height, first, n, seed=1, frame_stride=None, stream=None):

@@ -121,7 +121,40 @@ struct K3S {
 #ifdef K3_TRACE
   unsigned long long trace[16];    // diagnostic build: per-worker cycle / event counts (K3TR_*)
 #endif
+#ifdef K3_CHECK
+  uint32_t ck_nmb, ck_cap;         // check build: the frame's MBs, the arena's end (+ sink)
+#endif
 };
+
+// Index checks (-DK3_CHECK, diagnostic build libwebp_amd_check.so): every
+// global address k_encode computes from LDS state (arena chunk positions,
+// per-MB token counts and positions, compact-stream offsets, MB indices) is
+// checked before the access; a failing check records the first failure
+// (site, workgroup, worker, MB, value, bound) and counts the rest, and the
+// access is skipped, so a bad index shows up as a record instead of a GPU
+// fault. vp8g_k3_check reads the record back (tools/k3_trace.py).
+#ifdef K3_CHECK
+__device__ unsigned long long g_k3check[8];
+__device__ __noinline__ void k3ck_fail(int site, unsigned long long v, unsigned long long bound,
+                                       unsigned mb) {
+  if (atomicAdd(&g_k3check[0], 1ull) == 0) {
+    g_k3check[1] = (unsigned long long)site;
+    g_k3check[2] = blockIdx.x;
+    g_k3check[3] = threadIdx.x;
+    g_k3check[4] = mb;
+    g_k3check[5] = v;
+    g_k3check[6] = bound;
+  }
+}
+#define K3CK(cond, site, v, bound, mb) \
+  ((cond) ? true : (k3ck_fail((site), (unsigned long long)(v), (unsigned long long)(bound), (mb)), false))
+#define CK_NMB(L, dflt) (L).ck_nmb
+#define CK_CAP(L, dflt) (unsigned long long)(L).ck_cap
+#else
+#define K3CK(cond, site, v, bound, mb) true
+#define CK_NMB(L, dflt) (dflt)
+#define CK_CAP(L, dflt) (dflt)
+#endif
 
 // Barrier over the 4 wavefronts of one worker (s_barrier would stop the whole
 // workgroup, i.e. every worker). Arrivals count up an LDS word; a wave
@@ -1352,7 +1385,7 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
         const uint32_t u = __shfl_up(incl, o);
         if (ln >= (uint32_t)o) incl += u;
       }
-      if (i < i1) mboff[i] = off + incl - v;
+      if (i < i1 && K3CK(i < CK_NMB(L, i + 1), 10, i, 0, i)) mboff[i] = off + incl - v;
       off += __shfl(incl, 63);
     }
     if (ln == 0) { L.fold_total = off - base; L.fold_base = base; L.mark_any = 0; }
@@ -1406,6 +1439,9 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
             const uint32_t nt = L.rowcnt[i - row0];
             const uint16_t* tk = arena ? arena + L.rowpos[i - row0]
                                        : tok_base + (size_t)i * VP8G_MAX_TOKENS_PER_MB;
+            if (arena && !K3CK((unsigned long long)L.rowpos[i - row0] + nt <= CK_CAP(L, ~0u), 11,
+                               L.rowpos[i - row0], nt, i))
+              break;
             for (uint32_t k4 = 0; k4 < nt && n; k4 += 256) {
               if ((p >> 16) + n < 0xfffeu) break;   // no halving left in the row
               uint32_t tq[4];
@@ -1524,6 +1560,9 @@ __device__ void copy_folded(K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t 
     for (uint32_t k = wv; k < nc; k += 4) {
       const uint32_t d = __shfl(excl, (int)k), n = __shfl(v, (int)k);
       if ((size_t)d + n > tok_cap) continue;   // wave-uniform
+      if (!K3CK((unsigned long long)L.rowpos[c + k - row0] + n <= CK_CAP(L, ~0u), 12,
+                L.rowpos[c + k - row0], n, c + k))
+        continue;
       const uint16_t* src = arena + L.rowpos[c + k - row0];
       uint16_t* dst = tok_base + d;
       uint32_t q = ln;
@@ -1621,18 +1660,23 @@ struct K3Args {
   // reports VP8G_ERR_ARENA.
   uint16_t* arena;
   uint32_t arena_cap;
-  uint32_t* arena_top;
+  unsigned long long* arena_top;
   uint32_t* mbpos;
 };
 
 // a new chunk for this worker once fewer than one MB's worst case is left
-// (one lane; the caller orders it before the chunk's readers)
+// (one lane; the caller orders it before the chunk's readers). Once the
+// arena is exhausted nothing bumps the pointer any more (a worker that sees
+// it at or past the end stays on the sink), and the pointer is 64-bit, so
+// it can never wrap back into live chunks of other frames.
 __device__ __forceinline__ void arena_refill(K3S& L, K3G& G, const K3Args& a) {
   if (L.cend - L.cpos >= (uint32_t)VP8G_MAX_TOKENS_PER_MB) return;
-  const uint32_t p = atomicAdd(a.arena_top, (uint32_t)VP8G_ARENA_CHUNK);
-  if (p <= a.arena_cap - (uint32_t)VP8G_ARENA_CHUNK && p < a.arena_cap) {
-    L.cpos = p;
-    L.cend = p + VP8G_ARENA_CHUNK;
+  const unsigned long long cap = a.arena_cap;
+  unsigned long long p = __hip_atomic_load(a.arena_top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (p + VP8G_ARENA_CHUNK <= cap) p = atomicAdd(a.arena_top, (unsigned long long)VP8G_ARENA_CHUNK);
+  if (p + VP8G_ARENA_CHUNK <= cap) {
+    L.cpos = (uint32_t)p;
+    L.cend = (uint32_t)p + VP8G_ARENA_CHUNK;
   } else {   // exhausted: the sink (its contents are never read)
     L.cpos = a.arena_cap;
     L.cend = a.arena_cap + VP8G_MAX_TOKENS_PER_MB;
@@ -1739,6 +1783,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     G.fold_ptr = 0; G.ntok = 0; G.tok_err = 0; G.epoch = 0; G.abort = 0;
   }
   if (tid == 0) { L.bar = 0; L.myabort = 0; L.cpos = 0; L.cend = 0; }
+#ifdef K3_CHECK
+  if (tid == 0) { L.ck_nmb = (uint32_t)nmb; L.ck_cap = a.arena_cap + VP8G_MAX_TOKENS_PER_MB; }
+#endif
   __syncthreads();
   if (a.arena && tid == 0) arena_refill(L, G, a);
   if (wk == 0) level_costs_w(G, G.coeffs, tid);
@@ -1979,7 +2026,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
 
       load_mb(Yp, Up, Vp, w, h, x, y, L.yin, tid, K3T);
       wbar(L);
-      const int segid = segmap[mb];
+      int segid = segmap[mb];
+      if (!K3CK(segid >= 0 && segid < 4, 13, segid, 4, mb)) segid = 0;
       const vp8g_seg& S = G.seg[segid];
       const bool hl = x > 0, ht = y > 0;
       const uint8_t* yt = (xr ? xytop : ytop) + 16 * x;
@@ -2174,6 +2222,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       // ---- per-MB info + side statistics
       const int skip = rd_nz == 0;
       if (tid == 0) {
+        (void)K3CK(mb < (uint32_t)nmb, 14, mb, nmb, mb);
         uint8_t* info = mbinfo + (size_t)mb * VP8G_MBINFO_BYTES;
         info[0] = is_i16; info[1] = bu; info[2] = segid; info[3] = skip;
         atomicAdd(&G.fs.nb[is_i16 ? 1 : 0], 1);
@@ -2285,6 +2334,15 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         uint16_t* slot = a.arena ? a.arena + tpos : tok_base + (size_t)mb * VP8G_MAX_TOKENS_PER_MB;
         const int off0 = pre0 + inc0 - cnt[0];
         const int off1 = tot0 + pre1 + inc1 - cnt[1];
+#ifdef K3_CHECK
+        if (a.arena) {
+          const unsigned long long top = (unsigned long long)tpos + tot0 + tot1;
+          if (!K3CK(top <= CK_CAP(L, ~0u) && tot0 + tot1 <= VP8G_MAX_TOKENS_PER_MB, 15, tpos,
+                    tot0 + tot1, mb)) {
+            cnt[0] = 0; cnt[1] = 0;
+          }
+        }
+#endif
         if (cnt[0])
           pos_tokens<true>(bi[0] & 15, (bi[0] >> 4) & 15, bi[0] >> 8, rtid & 15, lvi[0], lvp[0],
                            last[0], slot + off0, L.rdelta);
@@ -2295,7 +2353,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           L.rowcnt[x] = (uint16_t)(tot0 + tot1);
           if (a.arena) {
             L.rowpos[x] = tpos;
-            a.mbpos[(size_t)f * nmb + mb] = tpos;
+            if (K3CK(mb < (uint32_t)nmb, 16, mb, nmb, mb)) a.mbpos[(size_t)f * nmb + mb] = tpos;
             L.cpos = tpos + (uint32_t)(tot0 + tot1);
             arena_refill(L, G, a);   // read by the next MB after the boundary barrier
           }
@@ -2716,6 +2774,19 @@ extern "C" int vp8g_launch_gather(uint16_t* tokens, size_t tok_cap, const uint16
   return vp8g_launch_check("k_gather_tokens");
 }
 
+#ifdef K3_CHECK
+// check build: the index-check record (count, site, workgroup, thread, MB,
+// value, bound) since the last call, then cleared
+extern "C" __attribute__((visibility("default"))) int vp8g_k3_check(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k3check), 7 * sizeof(unsigned long long), 0,
+                          hipMemcpyDeviceToHost) != hipSuccess)
+    return 0;
+  unsigned long long z[8] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_k3check), z, sizeof(z), 0, hipMemcpyHostToDevice) ==
+         hipSuccess;
+}
+#endif
+
 #ifdef K3_TRACE
 // diagnostic build: trellis16 against the serial trellis_quant on random
 // blocks (one wave; its 4 groups take 4 blocks per iteration) with random
@@ -2806,6 +2877,7 @@ extern "C" __attribute__((visibility("default"))) int vp8g_trellis_selftest(int 
   return ok;
 }
 
+
 // diagnostic build: the per-worker K3TR_* counters of the last launch,
 // out[block][worker][slot] for the first nblocks workgroups
 extern "C" __attribute__((visibility("default"))) int vp8g_k3_trace(unsigned long long* out,
@@ -2861,7 +2933,7 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
     a.arena_cap = arena->cap;
     a.arena_top = arena->top;
     a.mbpos = arena->mbpos;
-    if (hipMemsetAsync(arena->top, 0, sizeof(uint32_t), (hipStream_t)stream) != hipSuccess) {
+    if (hipMemsetAsync(arena->top, 0, sizeof(unsigned long long), (hipStream_t)stream) != hipSuccess) {
       vp8g_set_error("k_encode", "arena reset failed");
       return 0;
     }

@@ -47,16 +47,16 @@ int WebPGpuDeviceCount(void) {
   return n;
 }
 
-/* host threads of an engine: WEBP_AMD_THREADS, else at most 16, and no more
- * than the CPUs of this rank's share of its GPU's NUMA node (host_cpus.c) */
+/* host threads of an engine: WEBP_AMD_THREADS, else at most 16 and no more
+ * than the rank's host-thread budget (cgroup quota over the node's ranks, the
+ * rank's share of its GPU's NUMA node; host_cpus.c). The helpers of each
+ * host phase are drawn from the process-wide pool of that budget, so several
+ * engines per rank do not multiply it. */
 static int default_threads(int device) {
   const char* e = getenv("WEBP_AMD_THREADS");
   if (e && atoi(e) > 0) return atoi(e);
-  long n = sysconf(_SC_NPROCESSORS_ONLN);
-  const int pinned = vp8g_device_ncpu(device);
-  if (pinned > 0 && pinned < n) n = pinned;
-  if (n < 1) n = 1;
-  return n > 16 ? 16 : (int)n;
+  const int n = vp8g_rank_threads(device);
+  return n > 16 ? 16 : n;
 }
 
 static __thread char g_last_error[256];
@@ -118,6 +118,12 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   b->dither = b->sharp ? 0.f : vp8h_import_dithering(config);
   b->threads = host_threads > 0 ? host_threads : default_threads(device);
   b->host_emit = 0;
+  {   /* test knob: start with a one-chunk arena and 4096-token streams, so
+         the first call re-runs K3 with a grown arena and gathers the streams
+         again (k3_settle's two fallbacks) */
+    const char* tt = getenv("WEBP_AMD_TEST_TINY_TOKENS");
+    b->tiny_tokens = tt && tt[0] == '1';
+  }
 #ifdef WEBP_AMD_DIAG
   {   /* diagnostic build only: WEBP_AMD_HOST_EMIT=1 boolean-codes partition 1
          on the host threads (A/B of K4; libwebp_amd_diag.so) */
@@ -242,7 +248,7 @@ typedef struct {
   int n, phase;   /* 0: partition 0; 1: partition 1 + RIFF write; 2: frame setup */
   atomic_int next;
   pthread_t th[TAIL_MAX_THREADS];
-  int started;
+  int started, grant;
 } TailJob;
 
 /* Partition 0 of frame f: needs only K3's results and modes. */
@@ -329,8 +335,10 @@ static void* tail_worker(void* arg) {
 static void tail_spawn(TailJob* j, WebPGpuBatch* b, int n, int phase, int extra) {
   j->b = b; j->n = n; j->phase = phase; j->started = 0;
   atomic_init(&j->next, 0);
-  if (extra > n) extra = n;
+  if (extra > n - 1) extra = n - 1;
   if (extra > TAIL_MAX_THREADS) extra = TAIL_MAX_THREADS;
+  if (extra < 0) extra = 0;
+  extra = j->grant = vp8g_helpers_take(b->device, extra);
   for (int i = 0; i < extra; ++i)
     if (vp8g_thread_create(&j->th[j->started], tail_worker, j, b->device) == 0) ++j->started;
 }
@@ -339,6 +347,8 @@ static void tail_join(TailJob* j) {
   tail_worker(j);   /* the caller takes frames too until none are left */
   for (int i = 0; i < j->started; ++i) pthread_join(j->th[i], NULL);
   j->started = 0;
+  vp8g_helpers_give(j->grant);
+  j->grant = 0;
 }
 
 static void run_tails(WebPGpuBatch* b, int n, int phase) {
@@ -493,7 +503,7 @@ static int ensure_arena(WebPGpuBatch* b, size_t cap) {
   b->arena_cap = cap;
   if (!b->d_arena_top) {
     const size_t N = (size_t)b->max_frames;
-    CHK(hipMalloc((void**)&b->d_arena_top, sizeof(uint32_t)));
+    CHK(hipMalloc((void**)&b->d_arena_top, sizeof(unsigned long long)));
     CHK(hipMalloc((void**)&b->d_mbpos, N * b->nmb * sizeof(uint32_t)));
     CHK(hipMalloc((void**)&b->d_rerun_snap, N * VP8G_RERUN_STATE_BYTES));
   }
@@ -506,6 +516,8 @@ fail:
 static int tokens_for_run(WebPGpuBatch* b) {
   const size_t nmb = (size_t)b->nmb;
   if (!arena_mode(b)) return ensure_tok_cap(b, nmb * VP8G_MAX_TOKENS_PER_MB);
+  if (b->tiny_tokens)   /* test knob: both fallbacks of k3_settle run on the first call */
+    return ensure_tok_cap(b, 4096) && ensure_arena(b, (size_t)VP8G_ARENA_CHUNK);
   /* ~1.2x the tokens of a -q 75 frame of natural content per MB to start
    * with, and room for every worker's partly used last chunk */
   return ensure_tok_cap(b, nmb * 1536 + 4096) &&
@@ -552,15 +564,21 @@ static int k3_settle(WebPGpuBatch* b, int n, uint8_t* recon) {
   int rerun = 0;
   for (int tries = 0;; ++tries) {
     int over = 0;
-    size_t longest = 0;
+    size_t longest = 0, total = 0;
     for (int f = 0; f < n; ++f) {
       const vp8g_frame_result* R = &b->h_results[f];
       if (b->h_params[f].pass_mode == 2) continue;
+      total += R->ntokens;   /* counted by the fold even for tokens that went to the sink */
       if (R->error & VP8G_ERR_ARENA) over = 1;
       else if (!R->error && R->ntokens > longest) longest = R->ntokens;
     }
     if (over) {
-      if (tries > 6 || !ensure_arena(b, 2 * b->arena_cap)) {
+      /* the tokens this launch needs (+ a partly used last chunk per worker
+       * and 1/8 headroom), at least twice the old arena */
+      size_t want = total + total / 8 + 1024 * (size_t)VP8G_ARENA_CHUNK;
+      if (want < 2 * (size_t)b->arena_cap) want = 2 * (size_t)b->arena_cap;
+      if (tries > 6 || b->arena_cap >= 0xfff00000u - VP8G_MAX_TOKENS_PER_MB ||
+          !ensure_arena(b, want)) {
         vp8g_set_error("k_encode", "token arena cannot grow");
         return 0;
       }
@@ -1424,13 +1442,24 @@ int WebPGpuBatchEncodeRGBA(WebPGpuBatch* b, const void* rgba_dev, size_t fstride
 }
 
 /* host memory the DMA engines can read directly (page-locked by HIP) */
-static int host_is_pinned(const void* p) {
+static int byte_is_pinned(const void* p) {
   hipPointerAttribute_t at;
   if (hipPointerGetAttributes(&at, p) != hipSuccess) {
     (void)hipGetLastError();   /* an unregistered pointer reports an error: clear it */
     return 0;
   }
   return at.type == hipMemoryTypeHost;
+}
+
+/* the whole range [p, p + n) page-locked: its first and last byte and one
+ * byte every 64 MB between (a caller may have hipHostRegister-ed only part
+ * of a buffer; the SDMA engine must not read pageable pages) */
+static int host_is_pinned(const void* p, size_t n) {
+  const uint8_t* c = (const uint8_t*)p;
+  if (n == 0) return byte_is_pinned(c);
+  for (size_t o = 0; o < n; o += (size_t)64 << 20)
+    if (!byte_is_pinned(c + o)) return 0;
+  return byte_is_pinned(c + n - 1);
 }
 
 /* Encode n frames from host memory; with `next` (pinned, same geometry),
@@ -1465,7 +1494,7 @@ static int encode_host(WebPGpuBatch* b, const uint8_t* rgba, const uint8_t* next
       CHK(hipMalloc((void**)&b->d_rgba, need));
       b->d_rgba_cap = need;
     }
-    if (host_is_pinned(rgba)) {
+    if (host_is_pinned(rgba, need)) {
       /* page-locked (hipHostMalloc / hipHostRegister): one copy on an SDMA
          engine (host/h2d_sdma.c) -- it runs beside the other engines' kernels,
          where the runtime's copy kernel would wait for CUs a running K3 holds */
@@ -1480,7 +1509,7 @@ static int encode_host(WebPGpuBatch* b, const uint8_t* rgba, const uint8_t* next
       CHK(hipMemcpy(b->d_rgba, rgba, need, hipMemcpyHostToDevice));
     }
   }
-  if (next && host_is_pinned(next)) {
+  if (next && host_is_pinned(next, need)) {
     /* the spare buffer was last read by the previous call's kernels, which
        that call drained before returning */
     if (need > b->d_rgba2_cap) {

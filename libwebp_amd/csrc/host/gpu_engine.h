@@ -14,6 +14,11 @@
 /* host-thread placement on the GPU's NUMA node (host_cpus.c) */
 int vp8g_thread_create(pthread_t* th, void* (*fn)(void*), void* arg, int device);
 int vp8g_device_ncpu(int device);   /* CPUs of the device's share (0: not pinned) */
+int vp8g_rank_threads(int device);  /* the rank's host-thread budget (quota / ranks, pinned CPUs) */
+/* helpers for a host phase from the process-wide pool (the caller counts as
+ * one busy thread); returns how many of `want` may start; give back after */
+int vp8g_helpers_take(int device, int want);
+void vp8g_helpers_give(int grant);
 
 struct WebPGpuBatch {
   int device, w, h, max_frames, mbw, mbh, nmb, uvw, uvh, threads, last_n;
@@ -63,7 +68,8 @@ struct WebPGpuBatch {
    * streams (allocated on first use, grown when a launch runs out) */
   uint16_t* d_arena;
   size_t arena_cap;          /* tokens (a sink of VP8G_MAX_TOKENS_PER_MB follows) */
-  uint32_t* d_arena_top;
+  unsigned long long* d_arena_top;
+  int tiny_tokens;   /* WEBP_AMD_TEST_TINY_TOKENS=1 (tests): tiny initial token buffers */
   uint32_t* d_mbpos;
   uint8_t* d_rerun_snap;     /* d_rerun before a pass that re-reads it (arena re-runs) */
   uint8_t* d_mbinfo;

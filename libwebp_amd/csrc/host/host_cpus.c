@@ -16,6 +16,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <hip/hip_runtime_api.h>
 
@@ -155,4 +156,90 @@ int vp8g_device_ncpu(int device) {
   int ncpu = 0;
   (void)vp8g_device_cpus(device, &ncpu);
   return ncpu;
+}
+
+/* ---- host-thread budget of a rank ---------------------------------------
+ * A rank's host threads share its CPU quota: the cgroup CPU quota (v2
+ * cpu.max, v1 cfs_quota_us; WEBP_AMD_CPU_QUOTA overrides it, tests use that)
+ * divided by the ranks of the node (LOCAL_WORLD_SIZE), capped by the pinned
+ * NUMA share above and by the online CPUs. Every engine of the process
+ * draws the helper threads of its host phases from one pool of that size,
+ * so six engines per rank and eight ranks per node together stay at about
+ * one busy host thread per quota CPU (the calling thread of a phase counts
+ * against the pool too; it always works, so only helpers can be refused). */
+
+/* CPUs granted by the cgroup CPU quota, 0 when there is none */
+static double cgroup_quota(void) {
+  const char* o = getenv("WEBP_AMD_CPU_QUOTA");
+  if (o && atof(o) > 0) return atof(o);
+  FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r");
+  if (f) {
+    char q[32] = {0};
+    long per = 0;
+    const int got = fscanf(f, "%31s %ld", q, &per);
+    fclose(f);
+    if (got == 2 && strcmp(q, "max") != 0 && per > 0) return atof(q) / (double)per;
+  }
+  long q = 0, per = 0;
+  f = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r");
+  if (f) {
+    if (fscanf(f, "%ld", &q) != 1) q = 0;
+    fclose(f);
+  }
+  f = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r");
+  if (f) {
+    if (fscanf(f, "%ld", &per) != 1) per = 0;
+    fclose(f);
+  }
+  return (q > 0 && per > 0) ? (double)q / (double)per : 0.0;
+}
+
+int vp8g_rank_threads(int device) {
+  long n = sysconf(_SC_NPROCESSORS_ONLN);
+  const int pinned = vp8g_device_ncpu(device);
+  if (pinned > 0 && pinned < n) n = pinned;
+  const double quota = cgroup_quota();
+  if (quota > 0) {
+    const char* lw = getenv("LOCAL_WORLD_SIZE");
+    const int ranks = (lw && atoi(lw) > 0) ? atoi(lw) : 1;
+    long q = (long)(quota / ranks + 0.5);
+    if (q < 1) q = 1;
+    if (q < n) n = q;
+  }
+  return n < 1 ? 1 : (int)n;
+}
+
+static pthread_mutex_t g_pool_lock = PTHREAD_MUTEX_INITIALIZER;
+static int g_pool_busy = 0;   /* callers + helpers inside host phases */
+static int g_pool_size = 0;
+
+int vp8g_helpers_take(int device, int want) {
+  pthread_mutex_lock(&g_pool_lock);
+  if (g_pool_size == 0) {
+    const char* e = getenv("WEBP_AMD_THREADS");   /* explicit override: per engine, as before */
+    g_pool_size = vp8g_rank_threads(device);
+    if (e && atoi(e) > 0) g_pool_size = 0x7fffffff;
+  }
+  int grant = g_pool_size - g_pool_busy - 1;
+  if (grant > want) grant = want;
+  if (grant < 0) grant = 0;
+  g_pool_busy += grant + 1;
+  pthread_mutex_unlock(&g_pool_lock);
+  return grant;
+}
+
+void vp8g_helpers_give(int grant) {
+  pthread_mutex_lock(&g_pool_lock);
+  g_pool_busy -= grant + 1;
+  pthread_mutex_unlock(&g_pool_lock);
+}
+
+int WebPGpuHostThreadBudget(int device, int* busy) {
+  const int n = vp8g_rank_threads(device);
+  if (busy) {
+    pthread_mutex_lock(&g_pool_lock);
+    *busy = g_pool_busy;
+    pthread_mutex_unlock(&g_pool_lock);
+  }
+  return n;
 }

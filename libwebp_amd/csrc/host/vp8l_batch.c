@@ -283,10 +283,14 @@ static void run_headers(vp8l_engine* l, int n, int threads) {
   pthread_t th[64];
   int started = 0;
   if (threads > 64) threads = 64;
-  for (int i = 0; i < threads - 1 && i < n - 1; ++i)   /* on the engine GPU's NUMA node */
+  int want = threads - 1 < n - 1 ? threads - 1 : n - 1;
+  if (want < 0) want = 0;
+  const int grant = vp8g_helpers_take(l->device, want);   /* the rank's pool (host_cpus.c) */
+  for (int i = 0; i < grant; ++i)   /* on the engine GPU's NUMA node */
     if (vp8g_thread_create(&th[started], hdr_worker, &job, l->device) == 0) ++started;
   hdr_worker(&job);
   for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
+  vp8g_helpers_give(grant);
 }
 
 /* ---- pipeline ---- */

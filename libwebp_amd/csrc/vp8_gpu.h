@@ -154,7 +154,7 @@ int vp8g_launch_analysis(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int 
 typedef struct {
   uint16_t* tokens;
   uint32_t cap;
-  uint32_t* top;
+  unsigned long long* top;   /* 64-bit bump pointer: cannot wrap past cap */
   uint32_t* mbpos;
 } vp8g_arena;
 

@@ -27,6 +27,17 @@ enc.encode_device(buf.data_ptr(), B)
 enc.encode_device(buf.data_ptr(), B)
 t = enc.timings()
 lib = libwebp_amd.load()
+if hasattr(lib, "vp8g_k3_check"):   # check build: the index-check record of both calls
+    ck = (C.c_ulonglong * 8)()
+    lib.vp8g_k3_check.restype = C.c_int
+    assert lib.vp8g_k3_check(ck)
+    rec = {"failed_checks": int(ck[0])}
+    if ck[0]:
+        rec.update(site=int(ck[1]), workgroup=int(ck[2]), thread=int(ck[3]), mb=int(ck[4]),
+                   value=int(ck[5]), bound=int(ck[6]))
+    print("K3_CHECK", json.dumps(rec), flush=True)
+    if not hasattr(lib, "vp8g_k3_trace"):
+        sys.exit(0)
 fn = lib.vp8g_k3_trace
 fn.restype = C.c_int
 fn.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]

@@ -123,6 +123,8 @@ struct K3S {
 #endif
 #ifdef K3_CHECK
   uint32_t ck_nmb, ck_cap;         // check build: the frame's MBs, the arena's end (+ sink)
+  int32_t ck_y, ck_x;              // the MB the worker is at (the hang record)
+  uint32_t ck_rowdone;             // LDS offset of rowdone[0]
 #endif
 };
 
@@ -148,6 +150,10 @@ __device__ __noinline__ void k3ck_fail(int site, unsigned long long v, unsigned 
 }
 #define K3CK(cond, site, v, bound, mb) \
   ((cond) ? true : (k3ck_fail((site), (unsigned long long)(v), (unsigned long long)(bound), (mb)), false))
+// a cross-worker wait that gives up (timeout or another worker's abort)
+// records, per workgroup and worker: site, the waited word's LDS offset, the
+// value waited for, the value seen, the worker's MB (y, x), its barrier count
+__device__ uint32_t g_k3hang[1024][4][10];
 #define CK_NMB(L, dflt) (L).ck_nmb
 #define CK_CAP(L, dflt) (unsigned long long)(L).ck_cap
 #else
@@ -1260,6 +1266,22 @@ __device__ bool wait_ge(K3G& G, K3S& L, const int32_t* p, int32_t v, int site) {
   while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) {
     if (__hip_atomic_load(&G.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
         __builtin_amdgcn_s_memrealtime() - t0 > K3_WAIT_TICKS) {
+#ifdef K3_CHECK
+      if ((threadIdx.x & 255) == 0 && blockIdx.x < 1024) {
+        uint32_t* hr = g_k3hang[blockIdx.x][(threadIdx.x >> 8) & 3];
+        extern __shared__ __align__(16) uint8_t smem[];
+        hr[0] = (uint32_t)site;
+        hr[1] = (uint32_t)((uintptr_t)p - (uintptr_t)smem);
+        hr[2] = (uint32_t)v;
+        hr[3] = (uint32_t)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        hr[4] = (uint32_t)L.ck_y;
+        hr[5] = (uint32_t)L.ck_x;
+        hr[6] = L.bar;
+        hr[7] = 0x80000000u | (uint32_t)G.abort;
+        hr[8] = L.ck_rowdone;
+        hr[9] = (uint32_t)((uintptr_t)&G.fold_ptr - (uintptr_t)smem);
+      }
+#endif
       L.myabort = 1;
       atomicOr(&L.bar, WBAR_RELEASE);   // no wave of this worker waits at a barrier now
       if (!G.abort) G.abort = site;     // the wait that gave up (in the result's error)
@@ -1784,7 +1806,11 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
   }
   if (tid == 0) { L.bar = 0; L.myabort = 0; L.cpos = 0; L.cend = 0; }
 #ifdef K3_CHECK
-  if (tid == 0) { L.ck_nmb = (uint32_t)nmb; L.ck_cap = a.arena_cap + VP8G_MAX_TOKENS_PER_MB; }
+  if (tid == 0) {
+    L.ck_nmb = (uint32_t)nmb; L.ck_cap = a.arena_cap + VP8G_MAX_TOKENS_PER_MB;
+    L.ck_rowdone = (uint32_t)((uintptr_t)rowdone - (uintptr_t)smem);
+    L.ck_y = -1; L.ck_x = 0;
+  }
 #endif
   __syncthreads();
   if (a.arena && tid == 0) arena_refill(L, G, a);
@@ -1843,6 +1869,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       const int tid = opaque(tid_k), rtid = opaque(rtid_k), lane = tid & 63;
       const bool w0 = rtid < 64;
       const uint32_t mb = (uint32_t)y * mbw + x;
+#ifdef K3_CHECK
+      if (tid == 0) { L.ck_y = y; L.ck_x = -1 - x; }   // (negative: before the MB's waits)
+#endif
       // ---- cost-table epoch (frame_enc.c:828-832): refresh before MB k with
       // k = max_count + e * (max_count + 1)
       const int ep = (int)mb < max_count ? 0 : ((int)mb - max_count) / (max_count + 1) + 1;
@@ -2021,6 +2050,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       }
 #endif
       K3_STAMP(0);
+#ifdef K3_CHECK
+      if (tid == 0) { L.ck_y = y; L.ck_x = x; }
+#endif
       const uint64_t tr_mb = TR_NOW();
       TR_ADD(K3TR_NMB, 1);
 
@@ -2784,6 +2816,13 @@ extern "C" __attribute__((visibility("default"))) int vp8g_k3_check(unsigned lon
   unsigned long long z[8] = {0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_k3check), z, sizeof(z), 0, hipMemcpyHostToDevice) ==
          hipSuccess;
+}
+// check build: the hang records [1024][4][8] (see g_k3hang), then cleared
+extern "C" __attribute__((visibility("default"))) int vp8g_k3_hang(uint32_t* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k3hang), sizeof(g_k3hang), 0,
+                          hipMemcpyDeviceToHost) != hipSuccess)
+    return 0;
+  return 1;
 }
 #endif
 

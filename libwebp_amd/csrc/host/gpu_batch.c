@@ -239,16 +239,12 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   free(b);
 }
 
-/* ---- host thread pool for the per-frame tail ---- */
-
-#define TAIL_MAX_THREADS 64
+/* ---- the per-frame host phases, on the rank's thread pool (host_cpus.c) ---- */
 
 typedef struct {
   WebPGpuBatch* b;
-  int n, phase;   /* 0: partition 0; 1: partition 1 + RIFF write; 2: frame setup */
-  atomic_int next;
-  pthread_t th[TAIL_MAX_THREADS];
-  int started, grant;
+  int phase;   /* 0: partition 0; 1: partition 1 + RIFF write; 2: frame setup */
+  vp8g_job job;
 } TailJob;
 
 /* Partition 0 of frame f: needs only K3's results and modes. */
@@ -319,37 +315,22 @@ static void frame_setup(WebPGpuBatch* b, int f) {
                         b->h_segmap + f * nmb);
 }
 
-static void* tail_worker(void* arg) {
+static void tail_item(void* arg, int f) {
   TailJob* j = (TailJob*)arg;
-  for (;;) {
-    const int f = atomic_fetch_add(&j->next, 1);
-    if (f >= j->n) break;
-    if (j->phase == 0) frame_head(j->b, f);
-    else if (j->phase == 1) frame_finish(j->b, f);
-    else frame_setup(j->b, f);
-  }
-  return NULL;
+  if (j->phase == 0) frame_head(j->b, f);
+  else if (j->phase == 1) frame_finish(j->b, f);
+  else frame_setup(j->b, f);
 }
 
-/* start up to `extra` helper threads on the job; the caller joins in later */
+/* queue the phase's frames on the pool (at most b->threads - 1 pool threads
+ * on it at once); the caller joins in later */
 static void tail_spawn(TailJob* j, WebPGpuBatch* b, int n, int phase, int extra) {
-  j->b = b; j->n = n; j->phase = phase; j->started = 0;
-  atomic_init(&j->next, 0);
-  if (extra > n - 1) extra = n - 1;
-  if (extra > TAIL_MAX_THREADS) extra = TAIL_MAX_THREADS;
-  if (extra < 0) extra = 0;
-  extra = j->grant = vp8g_helpers_take(b->device, extra);
-  for (int i = 0; i < extra; ++i)
-    if (vp8g_thread_create(&j->th[j->started], tail_worker, j, b->device) == 0) ++j->started;
+  j->b = b;
+  j->phase = phase;
+  vp8g_job_submit(b->device, &j->job, tail_item, j, n, extra);
 }
 
-static void tail_join(TailJob* j) {
-  tail_worker(j);   /* the caller takes frames too until none are left */
-  for (int i = 0; i < j->started; ++i) pthread_join(j->th[i], NULL);
-  j->started = 0;
-  vp8g_helpers_give(j->grant);
-  j->grant = 0;
-}
+static void tail_join(TailJob* j) { vp8g_job_join(&j->job); }
 
 static void run_tails(WebPGpuBatch* b, int n, int phase) {
   TailJob job;

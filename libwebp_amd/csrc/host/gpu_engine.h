@@ -3,6 +3,7 @@
 #define LIBWEBP_AMD_GPU_ENGINE_H_
 
 #include <pthread.h>
+#include <stdatomic.h>
 
 #include <hip/hip_runtime_api.h>
 
@@ -15,10 +16,19 @@
 int vp8g_thread_create(pthread_t* th, void* (*fn)(void*), void* arg, int device);
 int vp8g_device_ncpu(int device);   /* CPUs of the device's share (0: not pinned) */
 int vp8g_rank_threads(int device);  /* the rank's host-thread budget (quota / ranks, pinned CPUs) */
-/* helpers for a host phase from the process-wide pool (the caller counts as
- * one busy thread); returns how many of `want` may start; give back after */
-int vp8g_helpers_take(int device, int want);
-void vp8g_helpers_give(int grant);
+/* a host phase's n per-frame items on the rank's persistent thread pool
+ * (host_cpus.c): submit queues the job (at most `width` pool threads on it at
+ * once), join has the caller take items too and returns when all are done */
+typedef struct vp8g_job {
+  void (*fn)(void* ctx, int i);
+  void* ctx;
+  int n, width, active;
+  atomic_int next, done;
+  struct vp8g_job* link;
+  void* pool;
+} vp8g_job;
+void vp8g_job_submit(int device, vp8g_job* j, void (*fn)(void*, int), void* ctx, int n, int width);
+void vp8g_job_join(vp8g_job* j);
 
 struct WebPGpuBatch {
   int device, w, h, max_frames, mbw, mbh, nmb, uvw, uvh, threads, last_n;

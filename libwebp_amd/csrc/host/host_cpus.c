@@ -162,11 +162,10 @@ int vp8g_device_ncpu(int device) {
  * A rank's host threads share its CPU quota: the cgroup CPU quota (v2
  * cpu.max, v1 cfs_quota_us; WEBP_AMD_CPU_QUOTA overrides it, tests use that)
  * divided by the ranks of the node (LOCAL_WORLD_SIZE), capped by the pinned
- * NUMA share above and by the online CPUs. Every engine of the process
- * draws the helper threads of its host phases from one pool of that size,
- * so six engines per rank and eight ranks per node together stay at about
- * one busy host thread per quota CPU (the calling thread of a phase counts
- * against the pool too; it always works, so only helpers can be refused). */
+ * NUMA share above and by the online CPUs. Every engine of the process runs
+ * the per-frame items of its host phases on one persistent pool of budget - 1
+ * threads (below) plus its own calling thread, so six engines per rank and
+ * eight ranks per node stay at about one busy host thread per quota CPU. */
 
 /* CPUs granted by the cgroup CPU quota, 0 when there is none */
 static double cgroup_quota(void) {
@@ -209,37 +208,126 @@ int vp8g_rank_threads(int device) {
   return n < 1 ? 1 : (int)n;
 }
 
-static pthread_mutex_t g_pool_lock = PTHREAD_MUTEX_INITIALIZER;
-static int g_pool_busy = 0;   /* callers + helpers inside host phases */
-static int g_pool_size = 0;
+/* One persistent pool of host threads per device (so per rank): budget - 1
+ * threads pinned like vp8g_thread_create, fed from a queue of jobs. A job
+ * is n independent items (one frame each); any idle pool thread takes items
+ * of the oldest job that still has some, up to the job's width at once, and
+ * the submitting thread takes items too when it joins. The pool is
+ * work-conserving (one engine alone gets every thread, several share them)
+ * and never holds more threads than the budget, however many engines. */
+typedef struct {
+  pthread_mutex_t lock;
+  pthread_cond_t work, done;
+  vp8g_job* head;
+  int started, nthreads, busy;
+} DevPool;
 
-int vp8g_helpers_take(int device, int want) {
-  pthread_mutex_lock(&g_pool_lock);
-  if (g_pool_size == 0) {
-    const char* e = getenv("WEBP_AMD_THREADS");   /* explicit override: per engine, as before */
-    g_pool_size = vp8g_rank_threads(device);
-    if (e && atoi(e) > 0) g_pool_size = 0x7fffffff;
-  }
-  int grant = g_pool_size - g_pool_busy - 1;
-  if (grant > want) grant = want;
-  if (grant < 0) grant = 0;
-  g_pool_busy += grant + 1;
-  pthread_mutex_unlock(&g_pool_lock);
-  return grant;
+static DevPool g_pool[MAX_DEV];
+static pthread_mutex_t g_pools_lock = PTHREAD_MUTEX_INITIALIZER;
+
+static int pool_size(int device) {
+  const char* e = getenv("WEBP_AMD_THREADS");   /* explicit override of the budget */
+  if (e && atoi(e) > 0) return atoi(e);
+  return vp8g_rank_threads(device);
 }
 
-void vp8g_helpers_give(int grant) {
-  pthread_mutex_lock(&g_pool_lock);
-  g_pool_busy -= grant + 1;
-  pthread_mutex_unlock(&g_pool_lock);
+static void* pool_thread(void* arg) {
+  DevPool* P = (DevPool*)arg;
+  pthread_mutex_lock(&P->lock);
+  for (;;) {
+    vp8g_job* j = P->head;
+    while (j && (atomic_load(&j->next) >= j->n || j->active >= j->width)) j = j->link;
+    if (!j) {
+      pthread_cond_wait(&P->work, &P->lock);
+      continue;
+    }
+    ++j->active;
+    ++P->busy;
+    pthread_mutex_unlock(&P->lock);
+    for (;;) {
+      const int i = atomic_fetch_add(&j->next, 1);
+      if (i >= j->n) break;
+      j->fn(j->ctx, i);
+      atomic_fetch_add(&j->done, 1);
+    }
+    pthread_mutex_lock(&P->lock);
+    --P->busy;
+    if (--j->active == 0) pthread_cond_broadcast(&P->done);
+  }
+  return NULL;
+}
+
+static DevPool* pool_get(int device) {
+  if (device < 0 || device >= MAX_DEV) device = 0;
+  DevPool* P = &g_pool[device];
+  pthread_mutex_lock(&g_pools_lock);
+  if (!P->started) {
+    pthread_mutex_init(&P->lock, NULL);
+    pthread_cond_init(&P->work, NULL);
+    pthread_cond_init(&P->done, NULL);
+    P->head = NULL;
+    P->started = 1;
+    const int want = pool_size(device) - 1;
+    for (int k = 0; k < want; ++k) {
+      pthread_t th;
+      if (vp8g_thread_create(&th, pool_thread, P, device) != 0) break;
+      pthread_detach(th);
+      ++P->nthreads;
+    }
+  }
+  pthread_mutex_unlock(&g_pools_lock);
+  return P;
+}
+
+void vp8g_job_submit(int device, vp8g_job* j, void (*fn)(void*, int), void* ctx, int n, int width) {
+  j->fn = fn;
+  j->ctx = ctx;
+  j->n = n > 0 ? n : 0;
+  j->width = width;
+  atomic_init(&j->next, 0);
+  atomic_init(&j->done, 0);
+  j->active = 0;
+  j->link = NULL;
+  j->pool = NULL;
+  if (j->n <= 1 || width <= 0) return;   /* the caller does it alone in vp8g_job_join */
+  DevPool* P = pool_get(device);
+  if (P->nthreads == 0) return;
+  j->pool = P;
+  pthread_mutex_lock(&P->lock);
+  vp8g_job** q = &P->head;
+  while (*q) q = &(*q)->link;
+  *q = j;
+  pthread_cond_broadcast(&P->work);
+  pthread_mutex_unlock(&P->lock);
+}
+
+void vp8g_job_join(vp8g_job* j) {
+  for (;;) {   /* the caller takes items too */
+    const int i = atomic_fetch_add(&j->next, 1);
+    if (i >= j->n) break;
+    j->fn(j->ctx, i);
+    atomic_fetch_add(&j->done, 1);
+  }
+  DevPool* P = (DevPool*)j->pool;
+  if (!P) return;
+  pthread_mutex_lock(&P->lock);
+  vp8g_job** q = &P->head;   /* off the queue: no thread starts on it any more */
+  while (*q && *q != j) q = &(*q)->link;
+  if (*q) *q = j->link;
+  while (j->active > 0 || atomic_load(&j->done) < j->n) pthread_cond_wait(&P->done, &P->lock);
+  pthread_mutex_unlock(&P->lock);
+  j->pool = NULL;
 }
 
 int WebPGpuHostThreadBudget(int device, int* busy) {
-  const int n = vp8g_rank_threads(device);
+  const int n = pool_size(device);
   if (busy) {
-    pthread_mutex_lock(&g_pool_lock);
-    *busy = g_pool_busy;
-    pthread_mutex_unlock(&g_pool_lock);
+    *busy = 0;
+    if (device >= 0 && device < MAX_DEV && g_pool[device].started) {
+      pthread_mutex_lock(&g_pool[device].lock);
+      *busy = g_pool[device].busy;
+      pthread_mutex_unlock(&g_pool[device].lock);
+    }
   }
   return n;
 }

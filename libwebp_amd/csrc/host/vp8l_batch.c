@@ -266,31 +266,16 @@ static void frame_header(vp8l_engine* l, int f) {
   vp8l_bw_free(&bw);
 }
 
-static void* hdr_worker(void* arg) {
-  HdrJob* j = (HdrJob*)arg;
-  for (;;) {
-    const int f = atomic_fetch_add(&j->next, 1);
-    if (f >= j->n) break;
-    frame_header(j->l, f);
-  }
-  return NULL;
-}
+static void hdr_item(void* arg, int f) { frame_header(((HdrJob*)arg)->l, f); }
 
+/* the frames' headers on the rank's thread pool (host_cpus.c), at most
+ * threads - 1 pool threads at once, the caller taking frames too */
 static void run_headers(vp8l_engine* l, int n, int threads) {
   HdrJob job;
   job.l = l; job.n = n;
-  atomic_init(&job.next, 0);
-  pthread_t th[64];
-  int started = 0;
-  if (threads > 64) threads = 64;
-  int want = threads - 1 < n - 1 ? threads - 1 : n - 1;
-  if (want < 0) want = 0;
-  const int grant = vp8g_helpers_take(l->device, want);   /* the rank's pool (host_cpus.c) */
-  for (int i = 0; i < grant; ++i)   /* on the engine GPU's NUMA node */
-    if (vp8g_thread_create(&th[started], hdr_worker, &job, l->device) == 0) ++started;
-  hdr_worker(&job);
-  for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
-  vp8g_helpers_give(grant);
+  vp8g_job pj;
+  vp8g_job_submit(l->device, &pj, hdr_item, &job, n, threads - 1);
+  vp8g_job_join(&pj);
 }
 
 /* ---- pipeline ---- */

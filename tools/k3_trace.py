@@ -36,6 +36,27 @@ if hasattr(lib, "vp8g_k3_check"):   # check build: the index-check record of bot
         rec.update(site=int(ck[1]), workgroup=int(ck[2]), thread=int(ck[3]), mb=int(ck[4]),
                    value=int(ck[5]), bound=int(ck[6]))
     print("K3_CHECK", json.dumps(rec), flush=True)
+    hang = (C.c_uint32 * (1024 * 4 * 10))()
+    lib.vp8g_k3_hang.restype = C.c_int
+    if lib.vp8g_k3_hang(hang):
+        import collections
+        import numpy as np  # noqa: E402
+        hr = np.ctypeslib.as_array(hang).reshape(1024, 4, 10)
+        recs = collections.Counter()
+        for b in range(min(B, 1024)):
+            for w in range(4):
+                r = hr[b, w]
+                if r[7] & 0x80000000:
+                    site = int(r[0])
+                    poff = int(r[1])
+                    what = ("rowdone[%d]" % ((poff - int(r[8])) // 4)) if site == 3 else \
+                           ("fold_ptr" if poff == int(r[9]) else "off %d" % poff)
+                    recs[(w, site, what, int(r[2]), int(r[3]), int(r[4]), int(np.int32(r[5])),
+                          int(r[6]) & 3, int(r[7]) & 0xffff)] += 1
+        print("K3_HANG (worker, site, word, waited-for, seen, y, x (neg: before waits), "
+              "bar%4, G.abort): count")
+        for k, v in recs.most_common(24):
+            print("K3_HANG", k, v)
     if not hasattr(lib, "vp8g_k3_trace"):
         sys.exit(0)
 fn = lib.vp8g_k3_trace

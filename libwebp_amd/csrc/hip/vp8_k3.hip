@@ -82,10 +82,9 @@ struct K3S {
   alignas(16) int16_t fin_uv[8][16];
   uint8_t modes[16];
   uint8_t canvas[17][24];
-  alignas(8) unsigned long long best4[3];   // intra4 argmin key (score << 4 | mode), 3 buffers
-  alignas(8) score_t sm4[2][10];   // intra4 candidate scores with lambda_mode (by sub-block parity)
-  int32_t r4[2][10][4];            // H, nz, R, D (by sub-block parity)
-  uint8_t rec4[2][10][16];         // every candidate's reconstruction (by sub-block parity)
+  // intra-4 search: each of the three searching waves' best candidate of a
+  // sub-block (by sub-block parity), see I4Rec
+  alignas(16) uint32_t i4rec[2][3][8];
   int32_t nzsel;                   // the m5 pass: nz of the sub-block's given mode
   int32_t lead;                    // the worker's place in the row wavefront (issue priority)
   int32_t hsrc[16];                // sum_j w_j |Hadamard(src block)_j| per luma block
@@ -100,6 +99,19 @@ struct K3S {
   uint32_t fold_base;              // their first compact-stream offset
   int32_t epseen;                  // G.epoch as one lane read it before the last worker barrier
   uint32_t bar;                    // worker barrier counter
+  uint32_t bar3;                   // barrier of the worker's three intra-4 waves (wbar3)
+  // results handed across the intra-4 / chroma fork (k_encode): the intra-4
+  // search on waves 0-2 (rtid < 192), the chroma search on wave 3
+  int32_t i4ok;
+  uint32_t i4nz;
+  alignas(8) score_t i4H, i4score;
+  int32_t uvsel;                   // chosen chroma mode
+  int32_t i16best;                 // the intra-16 choice (wave 3) and its terms
+  uint32_t i16nz;
+  alignas(8) score_t i16D, i16SD, i16H, i16R;
+  score_t rd16pub;                 // its lambda_mode score, MAX_SCORE until known
+  score_t rd16snap[2];             // rd16pub as the intra-4 waves saw it (by parity)
+  int32_t mresuv[4][4];            // chroma candidates {SSE, rate, AC non-zeros, nz bits}
   int32_t myabort;
   int32_t flag_ldc;                // left DC nz flag hand-off from wave 0
   int32_t mdist;                   // VP8ModeScore D of the MB (thread 0 only)
@@ -177,16 +189,36 @@ __device__ uint32_t g_k3hang[1024][4][10];
 #ifndef K3_WBAR_SLEEP
 #define K3_WBAR_SLEEP 0   // s_sleep units between polls (0 / 1 / 2: 124.0 / 124.3 / 124.9 ms, profiles/r3/ab13_*)
 #endif
+// The last wave to arrive (its add returned 3 mod 4) does not poll: the
+// count it completed is the release, and it goes on one LDS round trip
+// sooner (it is the wave the others waited for).
 __device__ __forceinline__ void wbar(K3S& L) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  uint32_t target = 0;
-  if ((threadIdx.x & 63) == 0) target = (atomicAdd(&L.bar, 1u) & ~3u) + 4u;
-  target = __builtin_amdgcn_readfirstlane(target);
-  while (__hip_atomic_load(&L.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-    __builtin_amdgcn_s_sleep(K3_WBAR_SLEEP);
+  uint32_t old = 0;
+  if ((threadIdx.x & 63) == 0) old = atomicAdd(&L.bar, 1u);
+  old = __builtin_amdgcn_readfirstlane(old);
+  const uint32_t target = (old & ~3u) + 4u;
+  if ((old & 3u) != 3u)
+    while (__hip_atomic_load(&L.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+      __builtin_amdgcn_s_sleep(K3_WBAR_SLEEP);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 #define WB() wbar(L)
+
+// Barrier over the three waves of a worker that run the intra-4 search
+// (rtid < 192) while the fourth runs the chroma search: the same counting
+// scheme on its own counter, in generations of 3 arrivals.
+__device__ __forceinline__ void wbar3(K3S& L) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  uint32_t old = 0;
+  if ((threadIdx.x & 63) == 0) old = atomicAdd(&L.bar3, 1u);
+  old = __builtin_amdgcn_readfirstlane(old);
+  const uint32_t target = old - old % 3u + 3u;
+  if (old % 3u != 2u)   // (the last arrival does not poll)
+    while (__hip_atomic_load(&L.bar3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+      __builtin_amdgcn_s_sleep(K3_WBAR_SLEEP);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
 
 // all-threads AND over the worker
 __device__ __forceinline__ int wbar_and(K3S& L, int v) {
@@ -569,10 +601,11 @@ __device__ Trellis16 trellis16(const K3G& G, int c, bool act, int ctx0, int type
 // VP8GetCostLuma16). Wave m = mode m. Fills rec16/lv16/lvdc and
 // mres[m] = {SSE, texture distortion, rate, nz (ac bits | dc << 24)}.
 
+// one mode's candidates on one wave (no barrier at the end: the caller's)
 template <bool TRELLIS>
-__device__ void eval_i16(const K3G& G, K3S& L, const vp8g_seg& S,
-                         const MBCtx& ctx, int tid) {
-  const int m = tid >> 6, lane = tid & 63, g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
+__device__ __forceinline__ void eval_i16_mode(const K3G& G, K3S& L, const vp8g_seg& S,
+                                              const MBCtx& ctx, int m, int lane) {
+  const int g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
   const int bsub = lane >> 4;
   int co[4];
 #pragma unroll
@@ -709,6 +742,12 @@ __device__ void eval_i16(const K3G& G, K3S& L, const vp8g_seg& S,
     L.mres[m][2] = rate + rdc;
     L.mres[m][3] = (int)(nzm | (dcnz ? (1u << 24) : 0u));
   }
+}
+
+// wave m = mode m over the worker, then the worker barrier
+template <bool TRELLIS>
+__device__ void eval_i16(const K3G& G, K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid) {
+  eval_i16_mode<TRELLIS>(G, L, S, ctx, tid >> 6, tid & 63);
   WB();
 }
 
@@ -717,9 +756,12 @@ __device__ void eval_i16(const K3G& G, K3S& L, const vp8g_seg& S,
 // cost_enc.c:258-278 VP8GetCostUV). Wave m = mode m, 8 blocks in 2 passes.
 // mres[m] = {SSE, rate, non-zero AC count, nz bits}.
 
-__device__ void eval_uv(const K3G& G, K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, int x0,
-                        const int8_t* topderr, int use_derr) {
-  const int m = tid >> 6, lane = tid & 63, g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
+// one mode's candidates on one wave (no barrier at the end: the caller's)
+__device__ __forceinline__ void eval_uv_mode(const K3G& G, K3S& L, const vp8g_seg& S,
+                                             const MBCtx& ctx, int m, int lane, int x0,
+                                             const int8_t* topderr, int use_derr,
+                                             int32_t (*mres)[4]) {
+  const int g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
   const int bsub = lane >> 4;
   int co[2];
 #pragma unroll
@@ -800,11 +842,17 @@ __device__ void eval_uv(const K3G& G, K3S& L, const vp8g_seg& S, const MBCtx& ct
   sse = sum64(sse);
   rate = sum64(rate);
   if (lane == 0) {
-    L.mres[m][0] = sse;
-    L.mres[m][1] = rate;
-    L.mres[m][2] = flatc;
-    L.mres[m][3] = (int)nzm;
+    mres[m][0] = sse;
+    mres[m][1] = rate;
+    mres[m][2] = flatc;
+    mres[m][3] = (int)nzm;
   }
+}
+
+// wave m = mode m over the worker, then the worker barrier
+__device__ void eval_uv(const K3G& G, K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, int x0,
+                        const int8_t* topderr, int use_derr) {
+  eval_uv_mode(G, L, S, ctx, tid >> 6, tid & 63, x0, topderr, use_derr, L.mres);
   WB();
 }
 
@@ -877,7 +925,9 @@ __device__ __forceinline__ P4Lane p4_lane(const P4Op& op, int x, int y) {
 // samples, which run_i4 places beside rows 4 / 8 / 12 for bx = 3).
 __device__ __forceinline__ int edge_off0(int k) { return k < 4 ? (4 - k) * 24 : k - 4; }
 
-template <bool TRELLIS>
+// W3S: the fourth wave runs the chroma search meanwhile; the three intra-4
+// waves synchronise among themselves (wbar3)
+template <bool TRELLIS, bool W3S = false>
 __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
                            const MBCtx& ctx, int tid, int x0,
                            int mbw, const uint8_t* predtop, const uint8_t* yl,
@@ -907,12 +957,11 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
   const P4Lane pl = p4_lane(G.p4[act ? tid : 0], x, y);
   const int offa = edge_off0(pl.ia), offb = edge_off0(pl.ib), offc = edge_off0(pl.ic);
   // left-edge samples (L K J I = column 3 of the sub-block to the left, rows
-  // 3..0): during the search they come from the winning candidate's row of
-  // rec4 -- the sub-block to the left was decided by the barrier just passed,
-  // its winner's commit to the canvas is not ordered before this read
-  const int la = pl.ia < 4 ? 4 * (3 - pl.ia) + 3 : -1;
-  const int lb = pl.ib < 4 ? 4 * (3 - pl.ib) + 3 : -1;
-  const int lc = pl.ic < 4 ? 4 * (3 - pl.ic) + 3 : -1;
+  // 3..0): during the search they come from the winning candidate's record
+  // (its right column packed L | K << 8 | J << 16 | I << 24) -- the
+  // sub-block to the left was decided by the barrier just passed, its
+  // winner's commit to the canvas is not ordered before this read
+  const bool la = pl.ia < 4, lb = pl.ib < 4, lc = pl.ic < 4;
   // this lane's y1 quantiser entries, once per MB
   const vp8g_mtx& M = S.y1;
   const uint32_t q_sh = M.sharpen[j], q_zt = M.zthresh[j], q_iq = M.iq[j], q_bias = M.bias[j];
@@ -924,9 +973,16 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
   int total_hdr = 0;
   I4Result res;
   res.ok = 1;
-  if (tid == 0) { L.best4[0] = ~0ull; L.best4[1] = ~0ull; L.d4acc = 0; L.r4acc = 0; }
-  WB();
-  int prev_bm = 0;   // the mode chosen for the previous sub-block (worker-uniform)
+#define I4B()                      \
+  do {                             \
+    if constexpr (W3S) wbar3(L);   \
+    else wbar(L);                  \
+  } while (0)
+  int d4acc = 0, r4acc = 0;   // D and R of the blocks chosen so far (search)
+  if (!search && tid == 0) { L.d4acc = 0; L.r4acc = 0; }
+  I4B();
+  int prev_bm = 0;          // the mode chosen for the previous sub-block (worker-uniform)
+  uint32_t prev_col = 0;    // its right column (search)
   for (int i4 = 0; i4 < 16; ++i4) {
     const int bx = i4 & 3, by = i4 >> 2, par = i4 & 1;
     const int left_m = bx == 0 ? L.predleft[by] : search ? prev_bm : L.modes[i4 - 1];
@@ -942,16 +998,15 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
     {
       const uint8_t* cb = cv + 96 * by + 4 * bx;   // sub-block base (worker-uniform)
       const bool lft = search && bx > 0;          // worker-uniform
-      const uint8_t* rl = &L.rec4[par ^ 1][prev_bm][0];
-      const int ea = *(lft && la >= 0 ? rl + la : cb + offa);
-      const int eb = *(lft && lb >= 0 ? rl + lb : cb + offb);
-      const int ec = *(lft && lc >= 0 ? rl + lc : cb + offc);
+      const int ea = lft && la ? (int)((prev_col >> (8 * pl.ia)) & 255) : cb[offa];
+      const int eb = lft && lb ? (int)((prev_col >> (8 * pl.ib)) & 255) : cb[offb];
+      const int ec = lft && lc ? (int)((prev_col >> (8 * pl.ic)) & 255) : cb[offc];
       pr = clip8((pl.wa * ea + pl.wb * eb + pl.wc * ec + pl.rnd) >> pl.sh);
       if (pl.dc) {
         int s4 = 4;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-          s4 += *(lft ? rl + 4 * (3 - k) + 3 : cb + edge_off0(k)) + cb[edge_off0(5 + k)];
+          s4 += (lft ? (int)((prev_col >> (8 * k)) & 255) : cb[edge_off0(k)]) + cb[edge_off0(5 + k)];
         pr = s4 >> 3;
       }
     }
@@ -987,38 +1042,82 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
       const int cntnz = __popcll((bac >> g) & 0xffff);
       const int R0 = (m > 0 && cntnz <= 3) ? 140 : 0;
       const int Rc = rate_lane(G, level, j, g, ctx4, 3, 0);
-      if (act) L.rec4[par][m][j] = (uint8_t)rec;
-      if (act && j == 0) {
-        const int H = G.mcost4[(top_m * 10 + left_m) * 10 + m];
-        const score_t dist = 256 * (score_t)(D + SD);
-        const score_t sc = (score_t)(R0 + Rc + H) * S.lambda_i4 + dist;
-        atomicMin(&L.best4[i4 % 3], ((unsigned long long)sc << 4) | (unsigned)m);
-        L.sm4[par][m] = (score_t)(R0 + Rc + H) * S.lambda_mode + dist;
-        L.r4[par][m][0] = H;
-        L.r4[par][m][1] = nzb;
-        L.r4[par][m][2] = R0 + Rc;
-        L.r4[par][m][3] = D;
+      // the candidate's right column on its group's lane 0: L = row 3 (lane
+      // 15), K (11), J (7), I (3); row_ror:n reads lane (i - n) mod 16
+      // (pinned DPP reads: only lane 0 uses them, inside the branch below,
+      // and a DPP sunk there would read masked-off source lanes)
+      const uint32_t col = (uint32_t)dpp_pin<DPP_ROR(1)>(0, rec) |
+                           ((uint32_t)dpp_pin<DPP_ROR(5)>(0, rec) << 8) |
+                           ((uint32_t)dpp_pin<DPP_ROR(9)>(0, rec) << 16) |
+                           ((uint32_t)dpp_pin<DPP_ROR(13)>(0, rec) << 24);
+      // the wave's best candidate (argmin of score << 4 | mode: ties to the
+      // lower mode) from its four groups' lane 0, without LDS
+      const int H = G.mcost4[(top_m * 10 + left_m) * 10 + (act ? m : 0)];
+      const score_t dist = 256 * (score_t)(D + SD);
+      const score_t sc = (score_t)(R0 + Rc + H) * S.lambda_i4 + dist;
+      const unsigned long long key = act ? ((unsigned long long)sc << 4) | (unsigned)m : ~0ull;
+      unsigned long long wmin = ~0ull;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const unsigned long long kq =
+            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(key >> 32), 16 * q) << 32) |
+            (uint32_t)__builtin_amdgcn_readlane((int)key, 16 * q);
+        wmin = kq < wmin ? kq : wmin;
+      }
+      if (W3S && tid == 0)   // the intra-16 score so far (wave 3 publishes it once known)
+        L.rd16snap[par] = __hip_atomic_load(&L.rd16pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (j == 0 && key == wmin) {   // one lane per wave: its record
+        // key, H | nz << 16, R, D, right column (the lambda_mode score is
+        // the key's score with R + H re-weighted, after the barrier)
+        uint32_t* r = L.i4rec[par][tid >> 6];
+        *reinterpret_cast<uint4*>(r) = make_uint4((uint32_t)key, (uint32_t)(key >> 32),
+                                                  (uint32_t)H | ((uint32_t)nzb << 16),
+                                                  (uint32_t)(R0 + Rc));
+        *reinterpret_cast<uint2*>(r + 4) = make_uint2((uint32_t)D, col);
       }
     }
     }   // busy
     SUBST(5);
-    WB();
+    I4B();
     int bm;
     if (search) {
-      // argmin, ties to the lower mode. The slot read here was last written
-      // before this barrier; the one reset here (used two sub-blocks on) was
-      // last read before it (three slots, so no second barrier is needed)
-      bm = (int)(L.best4[i4 % 3] & 15);
-      if (tid == 0) {
-        L.best4[(i4 + 2) % 3] = ~0ull;
-        L.d4acc += L.r4[par][bm][3];
-        L.r4acc += L.r4[par][bm][2];
-      }
-      const int H = L.r4[par][bm][0], bnzv = L.r4[par][bm][1];
+      // argmin over the three waves' records (one LDS round trip for all of
+      // them). The records of this parity were written before this barrier;
+      // they are written again two sub-blocks on, after the next barrier,
+      // which every wave passes only once it has read them here.
+      const uint32_t* R0p = L.i4rec[par][0];
+      const uint32_t* R1p = L.i4rec[par][1];
+      const uint32_t* R2p = L.i4rec[par][2];
+      const uint4 a0 = *reinterpret_cast<const uint4*>(R0p);
+      const uint4 a1 = *reinterpret_cast<const uint4*>(R1p);
+      const uint4 a2 = *reinterpret_cast<const uint4*>(R2p);
+      const uint2 b0 = *reinterpret_cast<const uint2*>(R0p + 4);
+      const uint2 b1 = *reinterpret_cast<const uint2*>(R1p + 4);
+      const uint2 b2 = *reinterpret_cast<const uint2*>(R2p + 4);
+      const unsigned long long k0 = ((unsigned long long)a0.y << 32) | a0.x;
+      const unsigned long long k1 = ((unsigned long long)a1.y << 32) | a1.x;
+      const unsigned long long k2 = ((unsigned long long)a2.y << 32) | a2.x;
+      const bool w1 = k1 < k0;
+      const unsigned long long k01 = w1 ? k1 : k0;
+      const bool w2 = k2 < k01;
+      const unsigned long long kb = w2 ? k2 : k01;
+      const uint32_t hz = w2 ? a2.z : (w1 ? a1.z : a0.z);
+      const int Rb = (int)(w2 ? a2.w : (w1 ? a1.w : a0.w));
+      const uint2 Bv = w2 ? b2 : (w1 ? b1 : b0);
+      bm = (int)(kb & 15);
+      const int H = (int)(hz & 0xffff), bnzv = (int)(hz >> 16);
+      d4acc += (int)Bv.x;
+      r4acc += Rb;
+      prev_col = Bv.y;
       accH += H;
-      acc_score += L.sm4[par][bm];
+      // (R + H) lambda_mode + 256 (D + SD) = score - (R + H)(lambda_i4 - lambda_mode)
+      acc_score += (score_t)(kb >> 4) - (score_t)(Rb + H) * (S.lambda_i4 - S.lambda_mode);
       acc_nz |= (uint32_t)bnzv << i4;
-      if (acc_score >= rd_score) { res.ok = 0; break; }
+      // the early exit against the intra-16 score: with W3S the score may not
+      // be known yet (then the snapshot is the maximum, and the final
+      // comparison is made at the join); both scores only grow, so the
+      // outcome is the same
+      if (acc_score >= (W3S ? L.rd16snap[par] : rd_score)) { res.ok = 0; break; }
       total_hdr += H;
       if (total_hdr > max_bits) { res.ok = 0; break; }
       tnz = (tnz & ~(1u << bx)) | ((uint32_t)bnzv << bx);
@@ -1035,16 +1134,19 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
     }
     if (search && tid == 0) L.modes[i4] = (uint8_t)bm;
     prev_bm = bm;
-    // the search needs no second barrier: the next sub-block reads its left
-    // edge from rec4 (above), every other canvas sample it reads was committed
-    // before an earlier barrier, and L.modes[i4] is read 4 sub-blocks on
+    // the search needs no second barrier: the next sub-block takes its left
+    // edge from the winner's record (above), every other canvas sample it
+    // reads was committed before an earlier barrier, and L.modes[i4] is read
+    // 4 sub-blocks on
     if (!search) {
-      WB();
+      I4B();
       acc_nz |= (uint32_t)L.nzsel << i4;
     }
     SUBST(7);
   }
-  WB();
+  if (search && tid == 0) { L.d4acc = d4acc; L.r4acc = r4acc; }
+  I4B();
+#undef I4B
   res.H = accH;
   res.score = acc_score;
   res.nz = acc_nz;
@@ -1804,7 +1906,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     G.fs.nb[0] = G.fs.nb[1] = G.fs.nb[2] = 0;
     G.fold_ptr = 0; G.ntok = 0; G.tok_err = 0; G.epoch = 0; G.abort = 0;
   }
-  if (tid == 0) { L.bar = 0; L.myabort = 0; L.cpos = 0; L.cend = 0; }
+  if (tid == 0) { L.bar = 0; L.bar3 = 0; L.myabort = 0; L.cpos = 0; L.cend = 0; }
 #ifdef K3_CHECK
   if (tid == 0) {
     L.ck_nmb = (uint32_t)nmb; L.ck_cap = a.arena_cap + VP8G_MAX_TOKENS_PER_MB;
@@ -2150,63 +2252,109 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         mv = max(mv, iabs_(L.lvdc[best16][4]));
         if (tid == 0) atomicMax(&G.max_edge[segid], mv);
       }
-      // the intra-4 search opens with a worker barrier, which orders the
-      // commit above before anything reads it
-      if (max_i4_bits <= 0) wbar(L);
+      // The intra-4 search and the chroma search run side by side: intra-4
+      // on the worker's waves with rtid < 192 (its 160 lanes; barriers among
+      // those three waves, wbar3), chroma on the fourth wave, all four modes
+      // in turn. Neither reads what the other writes (chroma: the MB's source,
+      // its U/V predictions, the DC error state; intra-4: the luma canvas),
+      // and the chroma choice does not depend on the luma one
+      // (quant_enc.c:1169-1217). The barrier below orders the intra-16 commit
+      // above before either side, the one after the searches joins them.
+      const bool fork = max_i4_bits > 0;
+      wbar(L);
       K3_STAMP(2);
 
-      // ---- Intra4 (quant_enc.c:1072-1165)
+      // ---- Intra4 (quant_enc.c:1072-1165) || UV (quant_enc.c:1169-1217)
       const uint64_t tr_i4 = TR_NOW();
-      if (max_i4_bits > 0) {
-        I4Result r4;
-        if constexpr (TR) {
-          r4 = trellis_all ? run_i4<true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
-                                          rd_score, max_i4_bits, substamps)
-                           : run_i4<false>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
-                                           rd_score, max_i4_bits, substamps);
-        } else {
-          r4 = run_i4<false>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true, rd_score,
-                             max_i4_bits, substamps);
+      if (fork) {
+        if (rtid < 192) {
+          I4Result r4;
+          if constexpr (TR) {
+            r4 = trellis_all ? run_i4<true, true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
+                                                  rd_score, max_i4_bits, substamps)
+                             : run_i4<false, true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
+                                                   rd_score, max_i4_bits, substamps);
+          } else {
+            r4 = run_i4<false, true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true, rd_score,
+                                     max_i4_bits, substamps);
+          }
+          if (rtid == 0) {
+            L.i4ok = r4.ok;
+            L.i4H = r4.H;
+            L.i4score = r4.score;
+            L.i4nz = r4.nz;
+          }
+        } else {   // the chroma search on one wave, then its choice
+          for (int mm = 0; mm < 4; ++mm) {
+            eval_uv_mode(G, L, S, ctx, mm, lane, x, derrrd, use_derr, L.mresuv);
+            wsync();
+          }
+          int b = 0;
+          score_t bsc = 0;
+          for (int mm = 0; mm < 4; ++mm) {
+            const score_t Dm = L.mresuv[mm][0], Hm = kVP8ModeCostUV[mm];
+            score_t Rm = L.mresuv[mm][1];
+            if (mm > 0 && L.mresuv[mm][2] <= 2) Rm += 140 * 8;
+            const score_t sc = (Rm + Hm) * S.lambda_uv + 256 * Dm;
+            if (mm == 0 || sc < bsc) { bsc = sc; b = mm; }
+          }
+          if (lane == 0) L.uvsel = b;
+          if (use_derr && lane < 2) {   // StoreDiffusionErrors (quant_enc.c:909-920)
+            const int cch = lane;
+            int8_t* top = topderr + 4 * x + 2 * cch;
+            int8_t* left = L.lderr[cch];
+            const int8_t* e = L.uvderr[b][cch];
+            left[0] = e[0];
+            left[1] = (int8_t)(3 * e[2] >> 2);
+            top[0] = e[1];
+            top[1] = (int8_t)(e[2] - left[1]);
+          }
         }
-        if (r4.ok) {
+        wbar(L);   // join
+        if (L.i4ok) {
           is_i16 = 0;
           if (tid == 0) L.mdist = L.d4acc;
-          rdH = r4.H;
-          rd_score = r4.score;
-          rd_nz = r4.nz;
+          rdH = L.i4H;
+          rd_score = L.i4score;
+          rd_nz = L.i4nz;
           L.yout[(tid >> 4) * BPS + (tid & 15)] = L.acc_out[tid];
           (&L.fin_ac[0][0])[tid] = (&L.acc_ac[0][0])[tid];
         } else {
           if (tid < 16) L.modes[tid] = best16;   // the aborted search wrote some
         }
-        // (no barrier: the chroma search reads none of this, and its own
-        // barriers order it before the readers -- info, SSE, tokens)
+      } else {
+        eval_uv(G, L, S, ctx, tid, x, derrrd, use_derr);
       }
       K3_STAMP(3);
       const uint64_t tr_uv = TR_NOW();
       TR_ADD(K3TR_I4, tr_uv - tr_i4);
 
-      // ---- UV (quant_enc.c:1169-1217)
+      // ---- the chroma choice (quant_enc.c:1169-1217)
       int bu = 0;
+      const int32_t(*mr)[4] = fork ? L.mresuv : L.mres;   // the chroma candidates
       {
-        eval_uv(G, L, S, ctx, tid, x, derrrd, use_derr);
         score_t bsc = 0, bH = 0;
-        for (int mm = 0; mm < 4; ++mm) {
-          const score_t Dm = L.mres[mm][0], Hm = kVP8ModeCostUV[mm];
-          score_t Rm = L.mres[mm][1];
-          if (mm > 0 && L.mres[mm][2] <= 2) Rm += 140 * 8;
-          const score_t sc = (Rm + Hm) * S.lambda_uv + 256 * Dm;
-          if (mm == 0 || sc < bsc) { bsc = sc; bu = mm; bH = Hm; }
+        if (fork) {
+          bu = L.uvsel;
+          bH = kVP8ModeCostUV[bu];
+        } else {
+          for (int mm = 0; mm < 4; ++mm) {
+            const score_t Dm = mr[mm][0], Hm = kVP8ModeCostUV[mm];
+            score_t Rm = mr[mm][1];
+            if (mm > 0 && mr[mm][2] <= 2) Rm += 140 * 8;
+            const score_t sc = (Rm + Hm) * S.lambda_uv + 256 * Dm;
+            if (mm == 0 || sc < bsc) { bsc = sc; bu = mm; bH = Hm; }
+          }
         }
         rdH += bH;
         rd_score += bsc;
-        if (tid == 0) L.mdist += L.mres[bu][0];
-        rd_nz |= (uint32_t)L.mres[bu][3] << 16;
+        if (tid == 0) L.mdist += mr[bu][0];
+        rd_nz |= (uint32_t)mr[bu][3] << 16;
         if (tid < 128) {
           L.yout[(tid >> 4) * BPS + 16 + (tid & 15)] = L.recuv[bu][tid];
           (&L.fin_uv[0][0])[tid] = (&L.lvuv[bu][0][0])[tid];
         }
-        if (use_derr && tid < 2) {   // StoreDiffusionErrors (quant_enc.c:909-920)
+        if (!fork && use_derr && tid < 2) {   // StoreDiffusionErrors (quant_enc.c:909-920)
           const int cch = tid;
           int8_t* top = topderr + 4 * x + 2 * cch;
           int8_t* left = L.lderr[cch];
@@ -2262,7 +2410,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         atomicAdd(&G.fs.size_p0, (unsigned long long)rdH);
         if constexpr (!TR) {   // R of the chosen luma modes + the chosen UV mode's R
           // with its flatness penalty (StatLoop passes run RD_OPT_BASIC, never TR)
-          const int ruv = L.mres[bu][1] + ((bu > 0 && L.mres[bu][2] <= 2) ? 140 * 8 : 0);
+          const int ruv = mr[bu][1] + ((bu > 0 && mr[bu][2] <= 2) ? 140 * 8 : 0);
           atomicAdd(&G.fs.size_rh,
                     (unsigned long long)(rdH + (is_i16 ? L.ry16 : L.r4acc) + ruv));
         }

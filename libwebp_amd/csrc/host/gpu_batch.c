@@ -1353,7 +1353,8 @@ static int launch_import(WebPGpuBatch* b, const uint8_t* rgba, size_t fstride, i
                               b->d_aflags, b->d_aplane, b->d_g2l, b->d_l2g,
                               dith ? b->d_rnd_y : NULL, dith ? b->d_rnd_uv : NULL, b->stream);
   }
-  if (!vp8g_launch_extract_alpha(rgba, fstride, rstride, b->w, b->h, n, b->d_aplane, b->stream))
+  if (!vp8g_launch_extract_alpha(rgba, fstride, rstride, b->w, b->h, n, NULL, b->d_aplane,
+                                 b->stream))
     return 0;
   if (!b->d_sharp) {   /* first sharp call: scratch for max_frames frames */
     const uint32_t *g2l, *l2g;
@@ -1402,6 +1403,11 @@ static int run_rgba(WebPGpuBatch* b, const void* rgba_dev, size_t fstride, int r
     for (int f = 0; f < n; ++f) {
       any |= b->h_aflags[f] != 0;
     }
+    /* the alpha planes of the frames K1 found not opaque (K1 writes none) */
+    if (any && !b->sharp &&
+        !vp8g_launch_extract_alpha((const uint8_t*)rgba_dev, fstride, rstride, b->w, b->h, n,
+                                   b->d_aflags, b->d_aplane, b->stream))
+      return 0;
     /* webp_enc.c:369-371: smooth/flatten the fully transparent areas */
     if (any && !b->cfg.exact &&
         !vp8g_launch_cleanup_alpha(b->d_yuv, b->yfb, b->d_aplane, b->d_aflags, b->w, b->h, n,

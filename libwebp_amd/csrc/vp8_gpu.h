@@ -116,9 +116,11 @@ int vp8g_launch_import(const uint8_t* rgba, size_t frame_stride, int row_stride,
                        void* stream);
 /* (rnd_y, rnd_uv: DEVICE rounding terms of the dithered import, W*H and
  * 2 x uvw*uvh with U, V interleaved, from vp8h_dither_rounders; NULL = plain) */
-/* alpha planes (n x w*h, stride w) of RGBA frames (sharp-YUV path) */
+/* alpha planes (n x w*h, stride w) of RGBA frames: all of them (aflags
+ * NULL, the sharp-YUV path) or those with aflags[f] != 0 (after K1) */
 int vp8g_launch_extract_alpha(const uint8_t* rgba, size_t frame_stride, int row_stride, int w,
-                              int h, int n, uint8_t* alpha_plane, void* stream);
+                              int h, int n, const uint32_t* aflags, uint8_t* alpha_plane,
+                              void* stream);
 /* WebPCleanupTransparentArea on the YUV planes of the frames whose
  * alpha_flags are set (config->exact == 0) */
 int vp8g_launch_cleanup_alpha(uint8_t* yuv, size_t yuv_frame_bytes, const uint8_t* alpha_plane,

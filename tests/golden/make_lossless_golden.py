@@ -40,6 +40,11 @@ CASES = [
     ("q7", 400, 300, 2), ("q16", 320, 240, 3),
     # > 256 colours with long-range repeats (round 4)
     ("tile", 512, 384, 0), ("tile", 1920, 1080, 1), ("text", 640, 360, 0), ("text", 1920, 1080, 2),
+    # moderate repeats (round 5): tiles copied less often, or to unaligned
+    # places the repeat test (L0b) does not sample, so the frame keeps the
+    # local parse
+    ("tile", 512, 384, 3), ("tile", 1024, 576, 3), ("mrep8", 512, 384, 0), ("mrep20", 512, 384, 1),
+    ("mrep40", 640, 360, 2), ("mrep12", 1920, 1080, 3),
 ]
 
 # transparent areas without `exact` (webp_enc.c:402-403 zeroes them, then

@@ -30,10 +30,13 @@ VP8L_SIZE_TOL = 0.02
 # 1.042)
 # tiled syn-v1 / text over a gradient (more than 256 colours, long-range
 # repeats: tests/golden/make_lossless_golden.py)
-KIND_TOL = {"syn": 0.02, "g": 0.05, "q": 0.035, "q16": 0.02, "tile": 0.02, "text": 0.05}
+KIND_TOL = {"syn": 0.02, "g": 0.05, "q": 0.035, "q16": 0.02, "tile": 0.02, "text": 0.05,
+            "mrep": 0.05}
 
 
 def kind_tol(kind):
+    if kind.startswith("mrep"):
+        return KIND_TOL["mrep"]
     return KIND_TOL.get(kind, KIND_TOL.get(kind[0], KIND_TOL["syn"]))
 
 CASES = [(64, 48, 0), (33, 17, 3), (1, 1, 0), (7, 5, 1), (2, 130, 4), (130, 3, 2)]
@@ -335,6 +338,21 @@ def tiled(w, h, f):
     return img
 
 
+def moderate_repeats(w, h, f, every):
+    """syn-v1 where about one 32x32 tile in `every` is a copy of a block at
+    a random (unaligned) place: moderate long-range repeats that L0b's
+    aligned window sampling does not see (the frame keeps the local parse)"""
+    img = syn_v1(w, h, f).copy()
+    rng = np.random.default_rng(300 + f)
+    T = 32
+    for ty in range(0, h - T + 1, T):
+        for tx in range(0, w - T + 1, T):
+            if rng.integers(0, every) == 0:
+                sy, sx = int(rng.integers(0, h - T)), int(rng.integers(0, w - T))
+                img[ty:ty + T, tx:tx + T] = img[sy:sy + T, sx:sx + T]
+    return img
+
+
 def text_on_gradient(w, h, f):
     """Anti-aliased 'text' over a colour gradient: a few hundred distinct
     8x12 glyphs set in lines (the same glyph repeats far apart), blended
@@ -389,11 +407,14 @@ def lossless_picture(kind, w, h, f):
     """syn-v1 ("syn"), palettised graphics ("g<colours>"), syn-v1 cut to
     <levels> values per channel ("q<levels>"), syn-v1 with repeated tiles
     ("tile"), text over a gradient ("text"), syn-v1 in a transparent border
-    ("border") or a transparent-background sprite ("sprite")"""
+    ("border"), a transparent-background sprite ("sprite") or syn-v1 with one
+    unaligned copied tile in <every> ("mrep<every>")"""
     if kind == "syn":
         return syn_v1(w, h, f)
     if kind == "tile":
         return tiled(w, h, f)
+    if kind.startswith("mrep"):
+        return moderate_repeats(w, h, f, int(kind[4:]))
     if kind == "text":
         return text_on_gradient(w, h, f)
     if kind == "border":

@@ -61,6 +61,7 @@ struct alignas(16) K3G {
 };
 
 static_assert(offsetof(K3G, coeffs) % 4 == 0, "K3X moves the probabilities as words");
+static_assert(offsetof(K3G, hc) % 4 == 0, "rate_lane reads an hc row as one word");
 
 // LDS private to one worker (4 wavefronts) and the MB it is encoding.
 struct K3S {
@@ -186,39 +187,80 @@ __device__ uint32_t g_k3hang[1024][4][10];
 // waiting waves by setting bit 31 of the counter (WBAR_RELEASE), so they
 // fall through, the worker leaves its row loop and the frame reports an error.
 #define WBAR_RELEASE 0x80000000u
+// -DK3_BARCHECK (diagnostic, with K3_CHECK): the barrier polls are bounded
+// too; a wave that gives up records, per workgroup / worker / wave, the source
+// line of its barrier, its arrival count, the target and the count it saw,
+// the worker's MB, then releases its worker (vp8g_k3_bar, tools/k3_hang.py)
+#ifdef K3_BARCHECK
+#ifndef K3_CHECK
+#error "K3_BARCHECK needs K3_CHECK (its global index checks keep a released worker in bounds)"
+#endif
+#define K3_BAR_TICKS (10ull * 100000000ull)
+__device__ uint32_t g_k3bar[1024][4][4][8];
+__device__ __noinline__ bool k3bar_giveup(K3S& L, uint32_t* bar, uint64_t t0, int line, uint32_t old,
+                                          uint32_t target) {
+  if (__builtin_amdgcn_s_memrealtime() - t0 <= K3_BAR_TICKS) return false;
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) {
+    uint32_t* r = g_k3bar[blockIdx.x][(threadIdx.x >> 8) & 3][(threadIdx.x >> 6) & 3];
+    r[0] = (uint32_t)line;
+    r[1] = old;
+    r[2] = target;
+    r[3] = __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    r[4] = (uint32_t)L.ck_y;
+    r[5] = (uint32_t)L.ck_x;
+    r[6] = (uint32_t)(bar == &L.bar3);
+    r[7] = 0x80000000u;
+  }
+  L.myabort = 1;
+  atomicOr(&L.bar, WBAR_RELEASE);
+  atomicOr(&L.bar3, WBAR_RELEASE);
+  return true;
+}
+#define K3_BARPOLL(word, line)                                                         \
+  do {                                                                                 \
+    const uint64_t t0_ = __builtin_amdgcn_s_memrealtime();                             \
+    while (__hip_atomic_load(&(word), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < \
+           target)                                                                     \
+      if (k3bar_giveup(L, &(word), t0_, line, old, target)) break;                     \
+  } while (0)
+#else
+#define K3_BARPOLL(word, line)                                                                  \
+  while (__hip_atomic_load(&(word), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) \
+  __builtin_amdgcn_s_sleep(K3_WBAR_SLEEP)
+#endif
 #ifndef K3_WBAR_SLEEP
 #define K3_WBAR_SLEEP 0   // s_sleep units between polls (0 / 1 / 2: 124.0 / 124.3 / 124.9 ms, profiles/r3/ab13_*)
 #endif
 // The last wave to arrive (its add returned 3 mod 4) does not poll: the
 // count it completed is the release, and it goes on one LDS round trip
 // sooner (it is the wave the others waited for).
-__device__ __forceinline__ void wbar(K3S& L) {
+__device__ __forceinline__ void wbar_at(K3S& L, int line) {
+  (void)line;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   uint32_t old = 0;
   if ((threadIdx.x & 63) == 0) old = atomicAdd(&L.bar, 1u);
   old = __builtin_amdgcn_readfirstlane(old);
   const uint32_t target = (old & ~3u) + 4u;
-  if ((old & 3u) != 3u)
-    while (__hip_atomic_load(&L.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-      __builtin_amdgcn_s_sleep(K3_WBAR_SLEEP);
+  if ((old & 3u) != 3u) K3_BARPOLL(L.bar, line);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
+#define wbar(L_) wbar_at(L_, __LINE__)
 #define WB() wbar(L)
 
 // Barrier over the three waves of a worker that run the intra-4 search
 // (rtid < 192) while the fourth runs the chroma search: the same counting
 // scheme on its own counter, in generations of 3 arrivals.
-__device__ __forceinline__ void wbar3(K3S& L) {
+__device__ __forceinline__ void wbar3_at(K3S& L, int line) {
+  (void)line;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   uint32_t old = 0;
   if ((threadIdx.x & 63) == 0) old = atomicAdd(&L.bar3, 1u);
   old = __builtin_amdgcn_readfirstlane(old);
   const uint32_t target = old - old % 3u + 3u;
-  if (old % 3u != 2u)   // (the last arrival does not poll)
-    while (__hip_atomic_load(&L.bar3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-      __builtin_amdgcn_s_sleep(K3_WBAR_SLEEP);
+  if (old % 3u != 2u) K3_BARPOLL(L.bar3, line);   // (the last arrival does not poll)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
+#define wbar3(L_) wbar3_at(L_, __LINE__)
 
 // all-threads AND over the worker
 __device__ __forceinline__ int wbar_and(K3S& L, int v) {
@@ -440,13 +482,16 @@ __device__ __forceinline__ int rate_lane(const K3G& G, int level, int j, int g, 
   int cost = G.lcost[type * 24 + band_of(n) * 3 + ctxp][min(v, MAX_VLEVEL)];
   if (v > MAX_VLEVEL)   // rare: beyond the LDS rows
     cost += kVP8LevelFixedCost[v] - kVP8LevelFixedCost[MAX_VLEVEL];
+  // (the table words are read unconditionally and picked by masks: a select
+  // around a load becomes a branch that waits on every LDS access in flight)
   const int eob = G.hc[type * 24 + band_of(n + 1) * 3 + min(v, 2)][0];
-  cost += (n == last && n < 15) ? eob : 0;
-  cost = (n >= first && n <= last) ? cost : 0;
+  cost += eob & -(int)(n == last && n < 15);
+  cost &= -(int)(n >= first && n <= last);
   const int t0 = type * 24 + first * 3 + ctx0;   // band(first) == first
-  const int h0 = G.hc[t0][0], h1 = G.hc[t0][1];
-  const int hdr = last < 0 ? h0 : (ctx0 == 0 ? h1 : 0);
-  cost += j == 0 ? hdr : 0;
+  const uint32_t hh = *reinterpret_cast<const uint32_t*>(G.hc[t0]);   // hc[t0][0], hc[t0][1]
+  const int h0 = (int)(hh & 0xffff), h1 = (int)(hh >> 16);
+  const int hdr = (h0 & -(int)(last < 0)) | (h1 & -(int)(last >= 0 && ctx0 == 0));
+  cost += hdr & -(int)(j == 0);
   return sum16(cost);
 }
 
@@ -967,8 +1012,13 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
   const uint32_t q_sh = M.sharpen[j], q_zt = M.zthresh[j], q_iq = M.iq[j], q_bias = M.bias[j];
   const int q_q = M.q[j];
   const uint8_t* cv = &L.canvas[0][0];
+  // the segment's lambdas in registers for the whole search (read from LDS
+  // inside the loop they would be reloaded after every barrier)
+  const int tlambda = __builtin_amdgcn_readfirstlane(S.tlambda);
+  const int lam_i4 = __builtin_amdgcn_readfirstlane(S.lambda_i4);
+  const int lam_mode = __builtin_amdgcn_readfirstlane(S.lambda_mode);
   uint32_t tnz = ctx.t & 0xf, lnz = ctx.l & 0xf;
-  score_t acc_score = (score_t)211 * S.lambda_mode, accH = 211;
+  score_t acc_score = (score_t)211 * lam_mode, accH = 211;
   uint32_t acc_nz = 0;
   int total_hdr = 0;
   I4Result res;
@@ -994,19 +1044,33 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
     const int src = L.yin[(4 * by + y) * BPS + 4 * bx + x];
     int pr = 0, rec = 0, nzb = 0;
     int level = 0, dq = 0;
+    // the intra-16 score so far (wave 3 publishes it once known), read at the
+    // top so the load is long done when the snapshot is stored
+    score_t snap = 0;
+    if constexpr (W3S) {
+      if (tid == 0) snap = __hip_atomic_load(&L.rd16pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     if (busy) {
     {
       const uint8_t* cb = cv + 96 * by + 4 * bx;   // sub-block base (worker-uniform)
       const bool lft = search && bx > 0;          // worker-uniform
-      const int ea = lft && la ? (int)((prev_col >> (8 * pl.ia)) & 255) : cb[offa];
-      const int eb = lft && lb ? (int)((prev_col >> (8 * pl.ib)) & 255) : cb[offb];
-      const int ec = lft && lc ? (int)((prev_col >> (8 * pl.ic)) & 255) : cb[offc];
+      // branch-free: every canvas sample is loaded and the left ones are
+      // replaced arithmetically (a select the compiler turns into a branch
+      // around the load serialises the loads with a wait on each)
+      const int mlft = lft ? -1 : 0;
+      int ea = cb[offa], eb = cb[offb], ec = cb[offc];
+      ea += ((int)((prev_col >> (8 * pl.ia)) & 255) - ea) & (la ? mlft : 0);
+      eb += ((int)((prev_col >> (8 * pl.ib)) & 255) - eb) & (lb ? mlft : 0);
+      ec += ((int)((prev_col >> (8 * pl.ic)) & 255) - ec) & (lc ? mlft : 0);
       pr = clip8((pl.wa * ea + pl.wb * eb + pl.wc * ec + pl.rnd) >> pl.sh);
       if (pl.dc) {
         int s4 = 4;
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          s4 += (lft ? (int)((prev_col >> (8 * k)) & 255) : cb[edge_off0(k)]) + cb[edge_off0(5 + k)];
+        for (int k = 0; k < 4; ++k) {
+          int lv = cb[edge_off0(k)];
+          lv += ((int)((prev_col >> (8 * k)) & 255) - lv) & mlft;
+          s4 += lv + cb[edge_off0(5 + k)];
+        }
         pr = s4 >> 3;
       }
     }
@@ -1034,9 +1098,9 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
     if (search) {
       const int D = sum16((src - rec) * (src - rec));
       int SD = 0;
-      if (S.tlambda) {
+      if (tlambda) {
         const int td = sum16(ttrans_lane(rec, j, wj)) - L.hsrc[i4];
-        SD = (S.tlambda * (iabs_(td) >> 5) + 128) >> 8;
+        SD = (tlambda * (iabs_(td) >> 5) + 128) >> 8;
       }
       SUBST(4);
       const int cntnz = __popcll((bac >> g) & 0xffff);
@@ -1054,7 +1118,7 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
       // lower mode) from its four groups' lane 0, without LDS
       const int H = G.mcost4[(top_m * 10 + left_m) * 10 + (act ? m : 0)];
       const score_t dist = 256 * (score_t)(D + SD);
-      const score_t sc = (score_t)(R0 + Rc + H) * S.lambda_i4 + dist;
+      const score_t sc = (score_t)(R0 + Rc + H) * lam_i4 + dist;
       const unsigned long long key = act ? ((unsigned long long)sc << 4) | (unsigned)m : ~0ull;
       unsigned long long wmin = ~0ull;
 #pragma unroll
@@ -1064,8 +1128,7 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
             (uint32_t)__builtin_amdgcn_readlane((int)key, 16 * q);
         wmin = kq < wmin ? kq : wmin;
       }
-      if (W3S && tid == 0)   // the intra-16 score so far (wave 3 publishes it once known)
-        L.rd16snap[par] = __hip_atomic_load(&L.rd16pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (W3S && tid == 0) L.rd16snap[par] = snap;
       if (j == 0 && key == wmin) {   // one lane per wave: its record
         // key, H | nz << 16, R, D, right column (the lambda_mode score is
         // the key's score with R + H re-weighted, after the barrier)
@@ -1097,13 +1160,19 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
       const unsigned long long k0 = ((unsigned long long)a0.y << 32) | a0.x;
       const unsigned long long k1 = ((unsigned long long)a1.y << 32) | a1.x;
       const unsigned long long k2 = ((unsigned long long)a2.y << 32) | a2.x;
-      const bool w1 = k1 < k0;
-      const unsigned long long k01 = w1 ? k1 : k0;
-      const bool w2 = k2 < k01;
-      const unsigned long long kb = w2 ? k2 : k01;
-      const uint32_t hz = w2 ? a2.z : (w1 ? a1.z : a0.z);
-      const int Rb = (int)(w2 ? a2.w : (w1 ? a1.w : a0.w));
-      const uint2 Bv = w2 ? b2 : (w1 ? b1 : b0);
+      // (picked by masks, so every record word is loaded up front: a select
+      // the compiler turns into a branch around a load waits on all LDS ops)
+      const uint32_t m1 = 0u - (uint32_t)(k1 < k0);
+      const unsigned long long k01 = k0 ^ ((k0 ^ k1) & ((unsigned long long)m1 << 32 | m1));
+      const uint32_t m2 = 0u - (uint32_t)(k2 < k01);
+      const unsigned long long kb = k01 ^ ((k01 ^ k2) & ((unsigned long long)m2 << 32 | m2));
+      auto pick = [&](uint32_t v0, uint32_t v1, uint32_t v2) {
+        const uint32_t v01 = v0 ^ ((v0 ^ v1) & m1);
+        return v01 ^ ((v01 ^ v2) & m2);
+      };
+      const uint32_t hz = pick(a0.z, a1.z, a2.z);
+      const int Rb = (int)pick(a0.w, a1.w, a2.w);
+      const uint2 Bv = make_uint2(pick(b0.x, b1.x, b2.x), pick(b0.y, b1.y, b2.y));
       bm = (int)(kb & 15);
       const int H = (int)(hz & 0xffff), bnzv = (int)(hz >> 16);
       d4acc += (int)Bv.x;
@@ -1111,7 +1180,7 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
       prev_col = Bv.y;
       accH += H;
       // (R + H) lambda_mode + 256 (D + SD) = score - (R + H)(lambda_i4 - lambda_mode)
-      acc_score += (score_t)(kb >> 4) - (score_t)(Rb + H) * (S.lambda_i4 - S.lambda_mode);
+      acc_score += (score_t)(kb >> 4) - (score_t)(Rb + H) * (lam_i4 - lam_mode);
       acc_nz |= (uint32_t)bnzv << i4;
       // the early exit against the intra-16 score: with W3S the score may not
       // be known yet (then the snapshot is the maximum, and the final
@@ -1173,7 +1242,9 @@ __device__ __forceinline__ int pos_tokens(int type, int first, int ctx0, int n, 
   auto dyn = [&](int bit, int pid, int sid) -> int {
     if (EMIT) {
       out[count] = (uint16_t)((bit << 15) | pid);
+#ifndef K3_AB_NO_TOKSTAT   // (timing A/B only: wrong statistics)
       atomicAdd(&delta[sid], 0x10000u + (uint32_t)bit);   // folded in raster order later
+#endif
     }
     ++count;
     return bit;
@@ -1963,6 +2034,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       L.epseen = __hip_atomic_load(&G.epoch, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
     int left_dc = 0;
     uint32_t fold_from = (uint32_t)y * mbw;   // first MB of this row not folded yet
+    // the row's first MB's source; each MB fetches the next one's during its
+    // token stage, so the global loads never sit on an MB's critical path
+    uint32_t pf = fetch_mb256(Yp, Up, Vp, w, h, 0, y, tid);
     wbar(L);
     for (int x = 0; x < mbw; ++x) {
       // per-lane ids re-derived every MB (opaque): values computed from them
@@ -1973,6 +2047,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       const uint32_t mb = (uint32_t)y * mbw + x;
 #ifdef K3_CHECK
       if (tid == 0) { L.ck_y = y; L.ck_x = -1 - x; }   // (negative: before the MB's waits)
+#endif
+#ifdef K3_BARCHECK
+      if (L.myabort) break;   // (a barrier of this worker gave up)
 #endif
       // ---- cost-table epoch (frame_enc.c:828-832): refresh before MB k with
       // k = max_count + e * (max_count + 1)
@@ -2158,7 +2235,12 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       const uint64_t tr_mb = TR_NOW();
       TR_ADD(K3TR_NMB, 1);
 
+#ifdef K3_AB_NO_PREFETCH   // (timing A/B: the MB's source loaded at its start)
       load_mb(Yp, Up, Vp, w, h, x, y, L.yin, tid, K3T);
+      (void)pf;
+#else
+      put_mb256(pf, L.yin, tid);
+#endif
       wbar(L);
       int segid = segmap[mb];
       if (!K3CK(segid >= 0 && segid < 4, 13, segid, 4, mb)) segid = 0;
@@ -2194,20 +2276,30 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       wbar(L);
       K3_STAMP(1);
 
-      // ---- Intra16 (quant_enc.c:1002-1058)
-      const uint64_t tr_i16 = TR_NOW();
-      if constexpr (TR) {
-        if (trellis_all) eval_i16<true>(G, L, S, ctx, tid);
-        else eval_i16<false>(G, L, S, ctx, tid);
-      } else {
-        eval_i16<false>(G, L, S, ctx, tid);
-      }
-      TR_SINCE(K3TR_I16, tr_i16);
+      // Three searches per MB (quant_enc.c:1002-1217). With intra-4 on
+      // (max_i4_header_bits > 0) they run side by side: intra-4 on the
+      // worker's waves with rtid < 192 (its 160 lanes, barriers among those
+      // three waves, wbar3), intra-16 and then chroma on the fourth wave, all
+      // four modes of each in turn. None reads what another writes (intra-16:
+      // p16, its candidates' levels and reconstructions; chroma: the U/V
+      // predictions, the DC error state; intra-4: the luma canvas and its
+      // records) and the chroma choice depends on neither luma choice. The
+      // intra-4 loop's exit against the intra-16 score (quant_enc.c:1153)
+      // takes the score once the fourth wave has published it, and the final
+      // comparison is made at the join: both scores only grow, so the
+      // outcome is the reference's. Without intra-4 the worker runs intra-16
+      // and chroma one after the other, wave m = mode m.
+      const bool fork = max_i4_bits > 0;
+#ifndef K3_FORK16
+#define K3_FORK16 0   // intra-16 on the fourth wave too (A/B: slower)
+#endif
+      const bool fork16 = fork && K3_FORK16;
       int best16 = 0;
       uint32_t nz16 = 0;
       score_t D16 = 0, SD16 = 0, H16 = 0, R16 = 0;
-      {
-        // IsFlatSource16 per wave (each lane checks 4 of the 256 samples): no barrier
+      // the intra-16 choice from the candidates in L.mres (quant_enc.c:1040-1057;
+      // IsFlatSource16 per wave, each lane checks 4 of the 256 samples)
+      auto pick_i16 = [&]() {
         const int v0 = L.yin[0];
         int same = 1;
 #pragma unroll
@@ -2233,49 +2325,48 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
             nz16 = (uint32_t)L.mres[mm][3];
           }
         }
+      };
+      // StoreMaxDelta (quant_enc.c:1045-1050), whatever the MB's final choice
+      auto max_delta = [&](bool lane0) {
+        if ((nz16 & 0x100ffff) == 0x1000000 && D16 > S.min_disto) {
+          int mv = iabs_(L.lvdc[best16][1]);
+          mv = max(mv, iabs_(L.lvdc[best16][2]));
+          mv = max(mv, iabs_(L.lvdc[best16][4]));
+          if (lane0) atomicMax(&G.max_edge[segid], mv);
+        }
+      };
+      if (tid == 0) L.rd16pub = 0x7fffffffffffffffLL;
+      const uint64_t tr_i16 = TR_NOW();
+      if (!fork16) {
+        if constexpr (TR) {
+          if (trellis_all) eval_i16<true>(G, L, S, ctx, tid);
+          else eval_i16<false>(G, L, S, ctx, tid);
+        } else {
+          eval_i16<false>(G, L, S, ctx, tid);
+        }
+        pick_i16();
+        max_delta(tid == 0);
+        if (fork && tid == 0) L.rd16pub = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
       }
-      // commit I16 as current best
-      L.yout[(tid >> 4) * BPS + (tid & 15)] = L.rec16[best16][tid];
-      (&L.fin_ac[0][0])[tid] = (&L.lv16[best16][0][0])[tid];
-      if (tid < 16) { L.fin_dc[tid] = L.lvdc[best16][tid]; L.modes[tid] = best16; }
-      score_t rd_score = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
-      score_t rdH = H16;
-      uint32_t rd_nz = nz16;
-      int is_i16 = 1;
-      if (tid < 64) {   // whole wave 0: a lone-lane store here spills
-        L.mdist = (int32_t)D16;
-        L.ry16 = (int32_t)R16;
-      }
-      if ((rd_nz & 0x100ffff) == 0x1000000 && D16 > S.min_disto) {   // StoreMaxDelta
-        int mv = iabs_(L.lvdc[best16][1]);
-        mv = max(mv, iabs_(L.lvdc[best16][2]));
-        mv = max(mv, iabs_(L.lvdc[best16][4]));
-        if (tid == 0) atomicMax(&G.max_edge[segid], mv);
-      }
-      // The intra-4 search and the chroma search run side by side: intra-4
-      // on the worker's waves with rtid < 192 (its 160 lanes; barriers among
-      // those three waves, wbar3), chroma on the fourth wave, all four modes
-      // in turn. Neither reads what the other writes (chroma: the MB's source,
-      // its U/V predictions, the DC error state; intra-4: the luma canvas),
-      // and the chroma choice does not depend on the luma one
-      // (quant_enc.c:1169-1217). The barrier below orders the intra-16 commit
-      // above before either side, the one after the searches joins them.
-      const bool fork = max_i4_bits > 0;
-      wbar(L);
+      TR_SINCE(K3TR_I16, tr_i16);
       K3_STAMP(2);
+      wbar(L);   // (fork: the rd16pub reset above before either side)
 
-      // ---- Intra4 (quant_enc.c:1072-1165) || UV (quant_enc.c:1169-1217)
+      // ---- Intra4 (quant_enc.c:1072-1165) || Intra16 + UV
       const uint64_t tr_i4 = TR_NOW();
+      score_t rd_score = 0, rdH = 0;
+      uint32_t rd_nz = 0;
+      int is_i16 = 1;
       if (fork) {
         if (rtid < 192) {
           I4Result r4;
           if constexpr (TR) {
             r4 = trellis_all ? run_i4<true, true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
-                                                  rd_score, max_i4_bits, substamps)
+                                                  0, max_i4_bits, substamps)
                              : run_i4<false, true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
-                                                   rd_score, max_i4_bits, substamps);
+                                                   0, max_i4_bits, substamps);
           } else {
-            r4 = run_i4<false, true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true, rd_score,
+            r4 = run_i4<false, true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true, 0,
                                      max_i4_bits, substamps);
           }
           if (rtid == 0) {
@@ -2284,7 +2375,27 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
             L.i4score = r4.score;
             L.i4nz = r4.nz;
           }
-        } else {   // the chroma search on one wave, then its choice
+        } else {   // intra-16 (fork16), then chroma, on one wave
+          if (fork16) {
+            for (int mm = 0; mm < 4; ++mm) {
+              if constexpr (TR) {
+                if (trellis_all) eval_i16_mode<true>(G, L, S, ctx, mm, lane);
+                else eval_i16_mode<false>(G, L, S, ctx, mm, lane);
+              } else {
+                eval_i16_mode<false>(G, L, S, ctx, mm, lane);
+              }
+              wsync();
+            }
+            pick_i16();
+            max_delta(lane == 0);
+            if (lane == 0) {
+              L.i16best = best16;
+              L.i16nz = nz16;
+              L.i16D = D16; L.i16SD = SD16; L.i16H = H16; L.i16R = R16;
+              __hip_atomic_store(&L.rd16pub, (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+          }
           for (int mm = 0; mm < 4; ++mm) {
             eval_uv_mode(G, L, S, ctx, mm, lane, x, derrrd, use_derr, L.mresuv);
             wsync();
@@ -2311,20 +2422,34 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           }
         }
         wbar(L);   // join
-        if (L.i4ok) {
-          is_i16 = 0;
-          if (tid == 0) L.mdist = L.d4acc;
-          rdH = L.i4H;
-          rd_score = L.i4score;
-          rd_nz = L.i4nz;
-          L.yout[(tid >> 4) * BPS + (tid & 15)] = L.acc_out[tid];
-          (&L.fin_ac[0][0])[tid] = (&L.acc_ac[0][0])[tid];
-        } else {
-          if (tid < 16) L.modes[tid] = best16;   // the aborted search wrote some
+        if (fork16) {
+          best16 = L.i16best;
+          nz16 = L.i16nz;
+          D16 = L.i16D; SD16 = L.i16SD; H16 = L.i16H; R16 = L.i16R;
         }
-      } else {
-        eval_uv(G, L, S, ctx, tid, x, derrrd, use_derr);
       }
+      // the intra-16 candidate as the MB's score so far (quant_enc.c:1368-1372)
+      rd_score = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
+      rdH = H16;
+      rd_nz = nz16;
+      if (tid < 64) {   // whole wave 0: a lone-lane store here spills
+        L.mdist = (int32_t)D16;
+        L.ry16 = (int32_t)R16;
+      }
+      if (fork && L.i4ok && L.i4score < rd_score) {   // intra-4 wins (quant_enc.c:1375-1382)
+        is_i16 = 0;
+        if (tid == 0) L.mdist = L.d4acc;
+        rdH = L.i4H;
+        rd_score = L.i4score;
+        rd_nz = L.i4nz;
+        L.yout[(tid >> 4) * BPS + (tid & 15)] = L.acc_out[tid];
+        (&L.fin_ac[0][0])[tid] = (&L.acc_ac[0][0])[tid];
+      } else {   // intra-16 (the aborted or beaten intra-4 search wrote some modes)
+        L.yout[(tid >> 4) * BPS + (tid & 15)] = L.rec16[best16][tid];
+        (&L.fin_ac[0][0])[tid] = (&L.lv16[best16][0][0])[tid];
+        if (tid < 16) { L.fin_dc[tid] = L.lvdc[best16][tid]; L.modes[tid] = best16; }
+      }
+      if (!fork) eval_uv(G, L, S, ctx, tid, x, derrrd, use_derr);
       K3_STAMP(3);
       const uint64_t tr_uv = TR_NOW();
       TR_ADD(K3TR_I4, tr_uv - tr_i4);
@@ -2444,6 +2569,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         }
       }
 
+#ifndef K3_AB_NO_PREFETCH
+      if (x + 1 < mbw) pf = fetch_mb256(Yp, Up, Vp, w, h, x + 1, y, tid);
+#endif
       // ---- tokens (token_enc.c:113-193) into this MB's slot; one (block,
       // zigzag position) item per thread, counts + scan + writes in parallel
       const int first_blk = is_i16 ? 0 : 1;
@@ -2972,6 +3100,13 @@ extern "C" __attribute__((visibility("default"))) int vp8g_k3_hang(uint32_t* out
     return 0;
   return 1;
 }
+#ifdef K3_BARCHECK
+// barrier-check build: the barrier records [1024][4][4][8] (see g_k3bar)
+extern "C" __attribute__((visibility("default"))) int vp8g_k3_bar(uint32_t* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k3bar), sizeof(g_k3bar), 0, hipMemcpyDeviceToHost) ==
+         hipSuccess;
+}
+#endif
 #endif
 
 #ifdef K3_TRACE

@@ -52,6 +52,21 @@ int WebPGpuDeviceCount(void) {
  * rank's share of its GPU's NUMA node; host_cpus.c). The helpers of each
  * host phase are drawn from the process-wide pool of that budget, so several
  * engines per rank do not multiply it. */
+/* WEBP_AMD_WATCH=1 (diagnostics): frame 0's progress word is polled during
+ * every K3 launch of the batch API too, and each change is printed with the
+ * time since the launch -- how far a stalled launch got, without touching
+ * the kernel's code */
+static double watch_t0;
+static int watch_rows(void* ctx, int rows, int total) {
+  (void)ctx;
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  const double t = ts.tv_sec + 1e-9 * ts.tv_nsec;
+  if (rows <= 0) watch_t0 = t;
+  fprintf(stderr, "[watch] frame 0: %d / %d rows folded at %.3f s\n", rows, total, t - watch_t0);
+  return 1;
+}
+
 static int default_threads(int device) {
   const char* e = getenv("WEBP_AMD_THREADS");
   if (e && atoi(e) > 0) return atoi(e);
@@ -187,6 +202,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   if (!b->frames || !b->tok_off || !b->p0 || !b->out || !b->out_cap || !b->out_size || !b->err || !b->hdr ||
       !b->araw || !b->fin_cost || !b->pass_act || !b->asse)
     goto fail;
+  if (getenv("WEBP_AMD_WATCH")) b->progress = watch_rows;
   return b;
 fail:
   WebPGpuBatchDelete(b);
@@ -370,7 +386,10 @@ static hipError_t engine_wait(WebPGpuBatch* b, hipStream_t st) {
   int last = -1;
   for (;;) {
     const hipError_t e = hipStreamQuery(st);
-    if (e != hipErrorNotReady) return e;
+    if (e != hipErrorNotReady) {
+      if (b->progress == watch_rows) fprintf(stderr, "[watch] K3 launch done (status %d)\n", (int)e);
+      return e;
+    }
     const int rows = (int)__atomic_load_n(&b->h_prog[0], __ATOMIC_RELAXED);
     if (rows != last && !__atomic_load_n(&b->h_prog[1], __ATOMIC_RELAXED)) {
       last = rows;

@@ -187,6 +187,41 @@ __device__ uint32_t g_k3hang[1024][4][10];
 // waiting waves by setting bit 31 of the counter (WBAR_RELEASE), so they
 // fall through, the worker leaves its row loop and the frame reports an error.
 #define WBAR_RELEASE 0x80000000u
+
+// The synchronisation words are handled without any compiler-visible
+// lane-masked region: the code generator placed
+// register copies of wave-wide values (the row index, the row-wavefront
+// word's address) inside such regions -- after a poll loop's exit, where the
+// wave runs with no lanes enabled, and inside the lane-0 branch of a barrier
+// arrival -- so 63 or all 64 lanes kept stale registers, and in two builds a
+// worker polled or published the wrong LDS word and stalled.
+// (tools/isa_lane0_check.py checks every shipped code object for both
+// patterns.) Hence: the arrival is one asm statement that switches to lane 0
+// and back itself, and every poll loop tests a wave-uniform (readfirstlane)
+// value, i.e. is a scalar loop that never touches the exec mask.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ uint32_t lane0_add(uint32_t* p, uint32_t v) {
+  uint32_t old;
+  uint64_t saved;
+  asm volatile(
+      "s_mov_b64 %1, exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "ds_add_rtn_u32 %0, %2, %3\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b64 exec, %1"
+      : "=&v"(old), "=&s"(saved)
+      : "v"(lds_addr(p)), "v"(v)
+      : "memory");
+  return (uint32_t)__builtin_amdgcn_readlane((int)old, 0);
+}
+template <typename T>
+__device__ __forceinline__ T ld_uni(const T* p, int order = __ATOMIC_RELAXED) {
+  const T v = order == __ATOMIC_ACQUIRE ? __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)
+                                        : __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return (T)__builtin_amdgcn_readfirstlane((int)v);
+}
 // -DK3_BARCHECK (diagnostic, with K3_CHECK): the barrier polls are bounded
 // too; a wave that gives up records, per workgroup / worker / wave, the source
 // line of its barrier, its arrival count, the target and the count it saw,
@@ -219,14 +254,12 @@ __device__ __noinline__ bool k3bar_giveup(K3S& L, uint32_t* bar, uint64_t t0, in
 #define K3_BARPOLL(word, line)                                                         \
   do {                                                                                 \
     const uint64_t t0_ = __builtin_amdgcn_s_memrealtime();                             \
-    while (__hip_atomic_load(&(word), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < \
-           target)                                                                     \
+    while (ld_uni(&(word)) < target)                                                   \
       if (k3bar_giveup(L, &(word), t0_, line, old, target)) break;                     \
   } while (0)
 #else
-#define K3_BARPOLL(word, line)                                                                  \
-  while (__hip_atomic_load(&(word), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) \
-  __builtin_amdgcn_s_sleep(K3_WBAR_SLEEP)
+#define K3_BARPOLL(word, line) \
+  while (ld_uni(&(word)) < target) __builtin_amdgcn_s_sleep(K3_WBAR_SLEEP)
 #endif
 #ifndef K3_WBAR_SLEEP
 #define K3_WBAR_SLEEP 0   // s_sleep units between polls (0 / 1 / 2: 124.0 / 124.3 / 124.9 ms, profiles/r3/ab13_*)
@@ -237,9 +270,7 @@ __device__ __noinline__ bool k3bar_giveup(K3S& L, uint32_t* bar, uint64_t t0, in
 __device__ __forceinline__ void wbar_at(K3S& L, int line) {
   (void)line;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  uint32_t old = 0;
-  if ((threadIdx.x & 63) == 0) old = atomicAdd(&L.bar, 1u);
-  old = __builtin_amdgcn_readfirstlane(old);
+  const uint32_t old = lane0_add(&L.bar, 1u);
   const uint32_t target = (old & ~3u) + 4u;
   if ((old & 3u) != 3u) K3_BARPOLL(L.bar, line);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -253,9 +284,7 @@ __device__ __forceinline__ void wbar_at(K3S& L, int line) {
 __device__ __forceinline__ void wbar3_at(K3S& L, int line) {
   (void)line;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  uint32_t old = 0;
-  if ((threadIdx.x & 63) == 0) old = atomicAdd(&L.bar3, 1u);
-  old = __builtin_amdgcn_readfirstlane(old);
+  const uint32_t old = lane0_add(&L.bar3, 1u);
   const uint32_t target = old - old % 3u + 3u;
   if (old % 3u != 2u) K3_BARPOLL(L.bar3, line);   // (the last arrival does not poll)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -1436,8 +1465,8 @@ __device__ __forceinline__ int tok_stat_slot(uint32_t t) {
 // worker-uniform wait until *p >= v (another worker of this workgroup publishes *p)
 __device__ bool wait_ge(K3G& G, K3S& L, const int32_t* p, int32_t v, int site) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) {
-    if (__hip_atomic_load(&G.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
+  while (ld_uni(p, __ATOMIC_ACQUIRE) < v) {
+    if (ld_uni(&G.abort) ||
         __builtin_amdgcn_s_memrealtime() - t0 > K3_WAIT_TICKS) {
 #ifdef K3_CHECK
       if ((threadIdx.x & 255) == 0 && blockIdx.x < 1024) {
@@ -1528,9 +1557,9 @@ __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" :
 // itself, so each wave's later sc1 loads follow its own matching poll
 __device__ bool wait_gx(K3G& G, K3S& L, const int32_t* p, int32_t v, XHdr* XH) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (ld_sc1(p) < v) {
-    if (__hip_atomic_load(&G.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
-        ld_sc1(&XH->abort) || __builtin_amdgcn_s_memrealtime() - t0 > K3_WAIT_TICKS) {
+  while (__builtin_amdgcn_readfirstlane(ld_sc1(p)) < v) {
+    if (ld_uni(&G.abort) || __builtin_amdgcn_readfirstlane(ld_sc1(&XH->abort)) ||
+        __builtin_amdgcn_s_memrealtime() - t0 > K3_WAIT_TICKS) {
       L.myabort = 1;
       atomicOr(&L.bar, WBAR_RELEASE);
       G.abort = 1;

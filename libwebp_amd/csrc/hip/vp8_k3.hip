@@ -189,20 +189,27 @@ __device__ uint32_t g_k3hang[1024][4][10];
 #define WBAR_RELEASE 0x80000000u
 
 // The synchronisation words are handled without any compiler-visible
-// lane-masked region: the code generator placed
-// register copies of wave-wide values (the row index, the row-wavefront
-// word's address) inside such regions -- after a poll loop's exit, where the
-// wave runs with no lanes enabled, and inside the lane-0 branch of a barrier
-// arrival -- so 63 or all 64 lanes kept stale registers, and in two builds a
-// worker polled or published the wrong LDS word and stalled.
-// (tools/isa_lane0_check.py checks every shipped code object for both
-// patterns.) Hence: the arrival is one asm statement that switches to lane 0
-// and back itself, and every poll loop tests a wave-uniform (readfirstlane)
-// value, i.e. is a scalar loop that never touches the exec mask.
+// lane-masked region: this compiler's register
+// allocator places live-range-split copies and spill stores of wave-wide
+// values at the end of a divergent region, BEFORE the instruction that
+// restores the exec mask -- after a poll loop's exit (no lanes enabled),
+// inside the lane-0 branch of a barrier arrival, in the else arm of an
+// if / else -- so some or all lanes keep stale registers (the row index, the
+// row-wavefront word's address, the thread id). Four diagnostic builds
+// stalled, faulted or leaked arena chunks that way; tools/isa_lane0_check.py
+// finds the pattern in every one of them and checks every shipped code
+// object (build() fails on it). Hence: the arrival is one asm statement that
+// switches to lane 0 and back itself, and every poll loop tests a
+// wave-uniform (readfirstlane) value, i.e. is a scalar loop.
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 __device__ __forceinline__ uint32_t lane0_add(uint32_t* p, uint32_t v) {
+#ifdef K3_VPOLL   // (timing A/B only: the compiler's lane-0 branch)
+  uint32_t o = 0;
+  if ((threadIdx.x & 63) == 0) o = atomicAdd(p, v);
+  return __builtin_amdgcn_readfirstlane(o);
+#endif
   uint32_t old;
   uint64_t saved;
   asm volatile(
@@ -258,8 +265,14 @@ __device__ __noinline__ bool k3bar_giveup(K3S& L, uint32_t* bar, uint64_t t0, in
       if (k3bar_giveup(L, &(word), t0_, line, old, target)) break;                     \
   } while (0)
 #else
+#ifdef K3_VPOLL
+#define K3_BARPOLL(word, line)                                                                  \
+  while (__hip_atomic_load(&(word), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) \
+  __builtin_amdgcn_s_sleep(K3_WBAR_SLEEP)
+#else
 #define K3_BARPOLL(word, line) \
   while (ld_uni(&(word)) < target) __builtin_amdgcn_s_sleep(K3_WBAR_SLEEP)
+#endif
 #endif
 #ifndef K3_WBAR_SLEEP
 #define K3_WBAR_SLEEP 0   // s_sleep units between polls (0 / 1 / 2: 124.0 / 124.3 / 124.9 ms, profiles/r3/ab13_*)
@@ -997,7 +1010,12 @@ __device__ __forceinline__ P4Lane p4_lane(const P4Op& op, int x, int y) {
 // above the MB, column 0 = the column left of it. Left edges are the column
 // before the sub-block, the others the row above it (incl. the top-right
 // samples, which run_i4 places beside rows 4 / 8 / 12 for bx = 3).
-__device__ __forceinline__ int edge_off0(int k) { return k < 4 ? (4 - k) * 24 : k - 4; }
+__device__ __forceinline__ int edge_off0(int k) {
+  // arithmetic select: as a ternary the compiler emitted a divergent if / else
+  // per call, a place where it then parked register copies
+  const int m = -(int)(k < 4);
+  return (((4 - k) * 24) & m) | ((k - 4) & ~m);
+}
 
 // W3S: the fourth wave runs the chroma search meanwhile; the three intra-4
 // waves synchronise among themselves (wbar3)
@@ -1406,9 +1424,11 @@ enum {
 #define K3TR_MAXB 1024
 __device__ unsigned long long g_k3trace[K3TR_MAXB][4][K3TR_N];
 #define TR_NOW() __builtin_amdgcn_s_memtime()
-#define TR_ADD(slot, v)                           \
-  do {                                            \
-    if (threadIdx.x % K3T == 0) L.trace[slot] += (v); \
+// (the worker's first wave adds, every lane the same value: a wave-uniform
+// branch, no lane-masked region -- DESIGN.md section 9)
+#define TR_ADD(slot, v)                                                          \
+  do {                                                                           \
+    if ((__builtin_amdgcn_readfirstlane(threadIdx.x) % K3T) < 64) L.trace[slot] += (v); \
   } while (0)
 #define TR_SINCE(slot, t0) TR_ADD(slot, TR_NOW() - (t0))
 #else
@@ -2241,7 +2261,16 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         // issue priority by place in the row wavefront: a worker whose row
         // above is finished leads and gates the others (they wait on its
         // progress), so its waves win the SIMDs' issue arbitration
-        const int lead = __builtin_amdgcn_readfirstlane(L.lead);
+        int lead = __builtin_amdgcn_readfirstlane(L.lead);
+#ifdef K3_EPRIO   // A/B: before a cost-epoch boundary K the rows above K's row must
+                  // finish first; the one with the most left (right above) leads
+        {
+          const int K = max_count + ep * (max_count + 1);
+          const int d = __builtin_amdgcn_readfirstlane(K / mbw - y);
+          if (d >= 1 && d <= 2) lead = 3 - d;   // row K-1: 2, row K-2: 1
+          else if (d == 3 || d == 0) lead = 0;
+        }
+#endif
 #ifndef K3_PRIO_LEAD
 #define K3_PRIO_LEAD 2
 #endif
@@ -2318,7 +2347,11 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       // comparison is made at the join: both scores only grow, so the
       // outcome is the reference's. Without intra-4 the worker runs intra-16
       // and chroma one after the other, wave m = mode m.
-      const bool fork = max_i4_bits > 0;
+#ifndef K3_FORK
+#define K3_FORK 1
+#endif
+      const bool i4on = max_i4_bits > 0;   // (quant_enc.c:1375: intra-4 only then)
+      const bool fork = K3_FORK && i4on;
 #ifndef K3_FORK16
 #define K3_FORK16 0   // intra-16 on the fourth wave too (A/B: slower)
 #endif
@@ -2386,6 +2419,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       score_t rd_score = 0, rdH = 0;
       uint32_t rd_nz = 0;
       int is_i16 = 1;
+      int i4ok = 0;
+      score_t i4score = 0, i4H = 0;
+      uint32_t i4nz = 0;
       if (fork) {
         if (rtid < 192) {
           I4Result r4;
@@ -2456,6 +2492,28 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           nz16 = L.i16nz;
           D16 = L.i16D; SD16 = L.i16SD; H16 = L.i16H; R16 = L.i16R;
         }
+        i4ok = L.i4ok;
+        i4score = L.i4score;
+        i4H = L.i4H;
+        i4nz = L.i4nz;
+      } else if (i4on) {
+        // sequential: intra-4 on the worker's waves (the fourth holds no mode)
+        // with the intra-16 score known, then chroma on all four
+        const score_t rd16 = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
+        I4Result r4;
+        if constexpr (TR) {
+          r4 = trellis_all ? run_i4<true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true, rd16,
+                                          max_i4_bits, substamps)
+                           : run_i4<false>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true, rd16,
+                                           max_i4_bits, substamps);
+        } else {
+          r4 = run_i4<false>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true, rd16, max_i4_bits,
+                             substamps);
+        }
+        i4ok = r4.ok;
+        i4score = r4.score;
+        i4H = r4.H;
+        i4nz = r4.nz;
       }
       // the intra-16 candidate as the MB's score so far (quant_enc.c:1368-1372)
       rd_score = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
@@ -2465,12 +2523,12 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         L.mdist = (int32_t)D16;
         L.ry16 = (int32_t)R16;
       }
-      if (fork && L.i4ok && L.i4score < rd_score) {   // intra-4 wins (quant_enc.c:1375-1382)
+      if (i4on && i4ok && i4score < rd_score) {   // intra-4 wins (quant_enc.c:1375-1382)
         is_i16 = 0;
         if (tid == 0) L.mdist = L.d4acc;
-        rdH = L.i4H;
-        rd_score = L.i4score;
-        rd_nz = L.i4nz;
+        rdH = i4H;
+        rd_score = i4score;
+        rd_nz = i4nz;
         L.yout[(tid >> 4) * BPS + (tid & 15)] = L.acc_out[tid];
         (&L.fin_ac[0][0])[tid] = (&L.acc_ac[0][0])[tid];
       } else {   // intra-16 (the aborted or beaten intra-4 search wrote some modes)

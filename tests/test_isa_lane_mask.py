@@ -44,6 +44,32 @@ P1_CASE = """_Zk:
 \tv_mov_b32_e32 v91, v61
 .Lfunc_end0:
 """
+# the epoch-priority object: a live-range split inside an else arm, undone
+# after the join's exec restore
+P3_CASE = """_Zk:
+\tv_cmp_eq_u32_e32 vcc, 3, v9
+\ts_and_saveexec_b64 s[2:3], vcc
+\ts_xor_b64 s[0:1], exec, s[2:3]
+\tv_mov_b32_e32 v74, 1
+\ts_andn2_saveexec_b64 s[0:1], s[0:1]
+\tv_mov_b32_e32 v74, 2
+\tv_mov_b32_e32 v87, v73
+\ts_or_b64 exec, exec, s[0:1]
+\tv_mov_b32_e32 v73, 0
+\tv_mov_b32_e32 v73, v87
+.Lfunc_end0:
+"""
+# a phi written in both arms is not a split
+PHI = """_Zk:
+\ts_and_saveexec_b64 s[8:9], s[62:63]
+\ts_xor_b64 s[42:43], exec, s[8:9]
+\tv_cndmask_b32_e64 v48, v14, v46, s[62:63]
+\ts_andn2_saveexec_b64 s[42:43], s[42:43]
+\tv_mov_b32_e32 v48, v14
+\ts_or_b64 exec, exec, s[42:43]
+\tv_mov_b32_e32 v14, v48
+.Lfunc_end0:
+"""
 CLEAN = """_Zk:
 \ts_mov_b64 s[0:1], exec
 \ts_and_b64 s[2:3], s[0:1], s[2:3]
@@ -58,6 +84,8 @@ CLEAN = """_Zk:
 def test_checker_finds_both_patterns():
     assert chk.check_text(P2_CASE, "p2") == 1
     assert chk.check_text(P1_CASE, "p1") == 1
+    assert chk.check_text(P3_CASE, "p3") == 1
+    assert chk.check_text(PHI, "phi") == 0
     assert chk.check_text(CLEAN, "clean") == 0
 
 

@@ -11,7 +11,13 @@ lanes, or none, enabled:
       hoisted lane mask, `s_mov_b64 exec, s[..]` ... `s_or_b64 exec, exec,
       s[..]`: the code of `if (tid == 0) ...`) whose destination is read with
       the full mask afterwards, so 63 lanes read a stale register (the
-      round-5 stage-split object lost the row index that way).
+      round-5 stage-split object lost the row index that way);
+  P3  the register allocator's live-range split done inside any divergent
+      region (an if / else arm up to its exec restore): `v_mov vA, vB` (or a
+      spill store) with exec narrowed, undone by `v_mov vB, vA` (or a reload
+      of the same slot) after exec is widened again -- the lanes outside the
+      region get vA's stale contents back (the round-5 epoch-priority object
+      corrupted its per-lane thread id that way and leaked arena chunks).
 
 usage: python tools/isa_lane0_check.py <device .s | .so | .o> [...]
        python tools/isa_lane0_check.py --build [-D...]   (compiles vp8_k3.hip for gfx950)
@@ -96,6 +102,72 @@ def check_loop_exits(L):
     return bad
 
 
+NARROW = re.compile(r"s_(and|andn2|or|xor)_saveexec_b64 |s_mov_b64 exec, s\[|s_xor_b64 exec, exec|"
+                    r"s_andn2_b64 exec, exec|s_and_b64 exec, exec")
+
+
+def _other_arm_writes(L, k, regs):
+    """for an else arm starting at k (`s_andn2_saveexec_b64 sX, sX` / `s_or_saveexec_b64
+    sX, sX`): does the matching if arm write any of regs?"""
+    m = re.match(r"s_(andn2|or)_saveexec_b64 (s\[\d+:\d+\]), (s\[\d+:\d+\])$", L[k])
+    if not m or m.group(2) != m.group(3):
+        return False
+    sx = re.escape(m.group(2))
+    for t in range(k - 1, max(-1, k - 4000), -1):
+        if re.match(r"s_(and_saveexec_b64 %s,|xor_b64 %s, exec, )" % (sx, sx), L[t]):
+            for u in range(t + 1, k):
+                d, _ = _dst_src(L[u])
+                if d & regs:
+                    return True
+            return False
+    return False
+
+
+def check_split_copies(L):
+    """P3: split copies made with exec narrowed and undone with it widened"""
+    bad = []
+    n = len(L)
+    k = 0
+    while k < n:
+        if not NARROW.match(L[k]):
+            k += 1
+            continue
+        j = k + 1
+        while j < n and not ("exec" in L[j] or L[j].startswith(ENDS)):
+            j += 1
+        if j >= n or not RESTORE.match(L[j]):
+            k = j if j > k else k + 1
+            continue
+        for i in range(k + 1, j):
+            c = L[i]
+            m = re.match(r"v_mov_b(32|64)_e32 (v\S+), (v\S+)$", c)
+            sp = re.match(r"scratch_store_\S+ off, (v\S+), off offset:(\d+)", c)
+            if m:
+                a, b = m.group(2), m.group(3)
+                if _other_arm_writes(L, k, _regs(a)):
+                    continue   # a phi: the if-arm writes the register too
+                undo = re.compile(r"v_mov_b%s_e32 %s, %s$" % (m.group(1), re.escape(b), re.escape(a)))
+                for t in range(j + 1, min(n, j + 12000)):
+                    if undo.match(L[t]):
+                        bad.append((i + 1, c, "split under a narrowed exec (region %d-%d), undone at %d"
+                                    % (k + 1, j + 1, t + 1)))
+                        break
+                    d, _ = _dst_src(L[t])
+                    if d & _regs(a):
+                        break
+            elif sp:
+                slot = sp.group(2)
+                for t in range(j + 1, min(n, j + 12000)):
+                    if re.match(r"scratch_load_\S+ \S+, off, off offset:%s\b" % slot, L[t]):
+                        bad.append((i + 1, c, "spilled under a narrowed exec (region %d-%d), reloaded at %d"
+                                    % (k + 1, j + 1, t + 1)))
+                        break
+                    if re.match(r"scratch_store_\S+ off, \S+, off offset:%s\b" % slot, L[t]):
+                        break
+        k = j
+    return bad
+
+
 def check_function(lines):
     L = [ln.split(";")[0].split("//")[0].strip() for ln in lines]
     spans = _masked_spans(L)
@@ -128,7 +200,8 @@ def check_function(lines):
                             break
             d, _ = _dst_src(c)
             written |= d
-    return bad + check_loop_exits(L)
+    seen = {b[0] for b in bad}
+    return bad + check_loop_exits(L) + [b for b in check_split_copies(L) if b[0] not in seen]
 
 
 def functions(text):
@@ -154,15 +227,28 @@ LLVM = "/opt/rocm/lib/llvm/bin/"
 
 
 def disassemble(path):
-    """gfx950 disassembly of the device code bundled in a host .so / .o"""
+    """gfx950 disassembly of the device code bundled in a host .so / .o (a
+    linked library's .hip_fatbin holds one offload bundle per object file)"""
     d = tempfile.mkdtemp()
-    fb, co = os.path.join(d, "fb"), os.path.join(d, "co")
+    fb = os.path.join(d, "fb")
     subprocess.run([LLVM + "llvm-objcopy", "--dump-section=.hip_fatbin=" + fb, path, os.path.join(d, "x")],
                    check=True, stderr=subprocess.DEVNULL)
-    subprocess.run([LLVM + "clang-offload-bundler", "--unbundle", "--type=o", "--input=" + fb,
-                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co], check=True)
-    return subprocess.run([LLVM + "llvm-objdump", "-d", "--mcpu=gfx950", co], check=True,
-                          capture_output=True, text=True).stdout
+    data = open(fb, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = [m.start() for m in re.finditer(re.escape(magic), data)]
+    out = []
+    for i, st in enumerate(starts):
+        piece, co = os.path.join(d, "b%d" % i), os.path.join(d, "co%d" % i)
+        open(piece, "wb").write(data[st:starts[i + 1] if i + 1 < len(starts) else len(data)])
+        r = subprocess.run([LLVM + "clang-offload-bundler", "--unbundle", "--type=o", "--input=" + piece,
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co],
+                           stderr=subprocess.DEVNULL)
+        if r.returncode == 0 and os.path.getsize(co):
+            out.append(subprocess.run([LLVM + "llvm-objdump", "-d", "--mcpu=gfx950", co], check=True,
+                                      capture_output=True, text=True).stdout)
+    if not out:
+        raise RuntimeError("no gfx950 code object in " + path)
+    return "\n".join(out)
 
 
 def check_text(text, label):
@@ -179,7 +265,8 @@ def check_text(text, label):
 def build_asm(flags):
     src = os.path.join(ROOT, "libwebp_amd", "csrc", "hip", "vp8_k3.hip")
     out = os.path.join(tempfile.mkdtemp(), "k3.s")
-    cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--offload-device-only",
+    cmd = ["/opt/rocm/bin/hipcc", "-O3", "-fPIC", "-fvisibility=hidden", "-std=c++17", "--offload-arch=gfx950",
+           "--offload-device-only",
            "-Wno-unused-result", "-I" + os.path.join(ROOT, "include"),
            "-I" + os.path.join(ROOT, "libwebp_amd", "csrc"), "-S", src, "-o", out] + flags
     subprocess.run(cmd, check=True, stderr=subprocess.DEVNULL)

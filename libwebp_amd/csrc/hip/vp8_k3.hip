@@ -61,7 +61,6 @@ struct alignas(16) K3G {
 };
 
 static_assert(offsetof(K3G, coeffs) % 4 == 0, "K3X moves the probabilities as words");
-static_assert(offsetof(K3G, hc) % 4 == 0, "rate_lane reads an hc row as one word");
 
 // LDS private to one worker (4 wavefronts) and the MB it is encoding.
 struct K3S {
@@ -83,9 +82,10 @@ struct K3S {
   alignas(16) int16_t fin_uv[8][16];
   uint8_t modes[16];
   uint8_t canvas[17][24];
-  // intra-4 search: each of the three searching waves' best candidate of a
-  // sub-block (by sub-block parity), see I4Rec
-  alignas(16) uint32_t i4rec[2][3][8];
+  alignas(8) unsigned long long best4[3];   // intra4 argmin key (score << 4 | mode), 3 buffers
+  alignas(8) score_t sm4[2][10];   // intra4 candidate scores with lambda_mode (by sub-block parity)
+  int32_t r4[2][10][4];            // H, nz, R, D (by sub-block parity)
+  uint8_t rec4[2][10][16];         // every candidate's reconstruction (by sub-block parity)
   int32_t nzsel;                   // the m5 pass: nz of the sub-block's given mode
   int32_t lead;                    // the worker's place in the row wavefront (issue priority)
   int32_t hsrc[16];                // sum_j w_j |Hadamard(src block)_j| per luma block
@@ -100,19 +100,6 @@ struct K3S {
   uint32_t fold_base;              // their first compact-stream offset
   int32_t epseen;                  // G.epoch as one lane read it before the last worker barrier
   uint32_t bar;                    // worker barrier counter
-  uint32_t bar3;                   // barrier of the worker's three intra-4 waves (wbar3)
-  // results handed across the intra-4 / chroma fork (k_encode): the intra-4
-  // search on waves 0-2 (rtid < 192), the chroma search on wave 3
-  int32_t i4ok;
-  uint32_t i4nz;
-  alignas(8) score_t i4H, i4score;
-  int32_t uvsel;                   // chosen chroma mode
-  int32_t i16best;                 // the intra-16 choice (wave 3) and its terms
-  uint32_t i16nz;
-  alignas(8) score_t i16D, i16SD, i16H, i16R;
-  score_t rd16pub;                 // its lambda_mode score, MAX_SCORE until known
-  score_t rd16snap[2];             // rd16pub as the intra-4 waves saw it (by parity)
-  int32_t mresuv[4][4];            // chroma candidates {SSE, rate, AC non-zeros, nz bits}
   int32_t myabort;
   int32_t flag_ldc;                // left DC nz flag hand-off from wave 0
   int32_t mdist;                   // VP8ModeScore D of the MB (thread 0 only)
@@ -187,7 +174,9 @@ __device__ uint32_t g_k3hang[1024][4][10];
 // waiting waves by setting bit 31 of the counter (WBAR_RELEASE), so they
 // fall through, the worker leaves its row loop and the frame reports an error.
 #define WBAR_RELEASE 0x80000000u
-
+#ifndef K3_WBAR_SLEEP
+#define K3_WBAR_SLEEP 0   // s_sleep units between polls (0 / 1 / 2: 124.0 / 124.3 / 124.9 ms, profiles/r3/ab13_*)
+#endif
 // The synchronisation words are handled without any compiler-visible
 // lane-masked region: this compiler's register
 // allocator places live-range-split copies and spill stores of wave-wide
@@ -200,16 +189,13 @@ __device__ uint32_t g_k3hang[1024][4][10];
 // finds the pattern in every one of them and checks every shipped code
 // object (build() fails on it). Hence: the arrival is one asm statement that
 // switches to lane 0 and back itself, and every poll loop tests a
-// wave-uniform (readfirstlane) value, i.e. is a scalar loop.
+// wave-uniform (readfirstlane) value, i.e. is a scalar loop. The last wave to
+// arrive (its add returned 3 mod 4) does not poll: the count it completed is
+// the release.
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 __device__ __forceinline__ uint32_t lane0_add(uint32_t* p, uint32_t v) {
-#ifdef K3_VPOLL   // (timing A/B only: the compiler's lane-0 branch)
-  uint32_t o = 0;
-  if ((threadIdx.x & 63) == 0) o = atomicAdd(p, v);
-  return __builtin_amdgcn_readfirstlane(o);
-#endif
   uint32_t old;
   uint64_t saved;
   asm volatile(
@@ -229,80 +215,17 @@ __device__ __forceinline__ T ld_uni(const T* p, int order = __ATOMIC_RELAXED) {
                                         : __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   return (T)__builtin_amdgcn_readfirstlane((int)v);
 }
-// -DK3_BARCHECK (diagnostic, with K3_CHECK): the barrier polls are bounded
-// too; a wave that gives up records, per workgroup / worker / wave, the source
-// line of its barrier, its arrival count, the target and the count it saw,
-// the worker's MB, then releases its worker (vp8g_k3_bar, tools/k3_hang.py)
-#ifdef K3_BARCHECK
-#ifndef K3_CHECK
-#error "K3_BARCHECK needs K3_CHECK (its global index checks keep a released worker in bounds)"
-#endif
-#define K3_BAR_TICKS (10ull * 100000000ull)
-__device__ uint32_t g_k3bar[1024][4][4][8];
-__device__ __noinline__ bool k3bar_giveup(K3S& L, uint32_t* bar, uint64_t t0, int line, uint32_t old,
-                                          uint32_t target) {
-  if (__builtin_amdgcn_s_memrealtime() - t0 <= K3_BAR_TICKS) return false;
-  if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) {
-    uint32_t* r = g_k3bar[blockIdx.x][(threadIdx.x >> 8) & 3][(threadIdx.x >> 6) & 3];
-    r[0] = (uint32_t)line;
-    r[1] = old;
-    r[2] = target;
-    r[3] = __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    r[4] = (uint32_t)L.ck_y;
-    r[5] = (uint32_t)L.ck_x;
-    r[6] = (uint32_t)(bar == &L.bar3);
-    r[7] = 0x80000000u;
-  }
-  L.myabort = 1;
-  atomicOr(&L.bar, WBAR_RELEASE);
-  atomicOr(&L.bar3, WBAR_RELEASE);
-  return true;
-}
-#define K3_BARPOLL(word, line)                                                         \
-  do {                                                                                 \
-    const uint64_t t0_ = __builtin_amdgcn_s_memrealtime();                             \
-    while (ld_uni(&(word)) < target)                                                   \
-      if (k3bar_giveup(L, &(word), t0_, line, old, target)) break;                     \
-  } while (0)
-#else
-#ifdef K3_VPOLL
-#define K3_BARPOLL(word, line)                                                                  \
-  while (__hip_atomic_load(&(word), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) \
-  __builtin_amdgcn_s_sleep(K3_WBAR_SLEEP)
-#else
-#define K3_BARPOLL(word, line) \
-  while (ld_uni(&(word)) < target) __builtin_amdgcn_s_sleep(K3_WBAR_SLEEP)
-#endif
-#endif
-#ifndef K3_WBAR_SLEEP
-#define K3_WBAR_SLEEP 0   // s_sleep units between polls (0 / 1 / 2: 124.0 / 124.3 / 124.9 ms, profiles/r3/ab13_*)
-#endif
-// The last wave to arrive (its add returned 3 mod 4) does not poll: the
-// count it completed is the release, and it goes on one LDS round trip
-// sooner (it is the wave the others waited for).
-__device__ __forceinline__ void wbar_at(K3S& L, int line) {
-  (void)line;
+__device__ __forceinline__ void wbar(K3S& L) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   const uint32_t old = lane0_add(&L.bar, 1u);
   const uint32_t target = (old & ~3u) + 4u;
-  if ((old & 3u) != 3u) K3_BARPOLL(L.bar, line);
+#ifndef K3_NOSKIP
+  if ((old & 3u) != 3u)
+#endif
+    while (ld_uni(&L.bar) < target) __builtin_amdgcn_s_sleep(K3_WBAR_SLEEP);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
-#define wbar(L_) wbar_at(L_, __LINE__)
 #define WB() wbar(L)
-
-// Barrier over the three waves of a worker that run the intra-4 search
-// (rtid < 192) while the fourth runs the chroma search: the same counting
-// scheme on its own counter, in generations of 3 arrivals.
-__device__ __forceinline__ void wbar3_at(K3S& L, int line) {
-  (void)line;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  const uint32_t old = lane0_add(&L.bar3, 1u);
-  const uint32_t target = old - old % 3u + 3u;
-  if (old % 3u != 2u) K3_BARPOLL(L.bar3, line);   // (the last arrival does not poll)
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-#define wbar3(L_) wbar3_at(L_, __LINE__)
 
 // all-threads AND over the worker
 __device__ __forceinline__ int wbar_and(K3S& L, int v) {
@@ -524,16 +447,13 @@ __device__ __forceinline__ int rate_lane(const K3G& G, int level, int j, int g, 
   int cost = G.lcost[type * 24 + band_of(n) * 3 + ctxp][min(v, MAX_VLEVEL)];
   if (v > MAX_VLEVEL)   // rare: beyond the LDS rows
     cost += kVP8LevelFixedCost[v] - kVP8LevelFixedCost[MAX_VLEVEL];
-  // (the table words are read unconditionally and picked by masks: a select
-  // around a load becomes a branch that waits on every LDS access in flight)
   const int eob = G.hc[type * 24 + band_of(n + 1) * 3 + min(v, 2)][0];
-  cost += eob & -(int)(n == last && n < 15);
-  cost &= -(int)(n >= first && n <= last);
+  cost += (n == last && n < 15) ? eob : 0;
+  cost = (n >= first && n <= last) ? cost : 0;
   const int t0 = type * 24 + first * 3 + ctx0;   // band(first) == first
-  const uint32_t hh = *reinterpret_cast<const uint32_t*>(G.hc[t0]);   // hc[t0][0], hc[t0][1]
-  const int h0 = (int)(hh & 0xffff), h1 = (int)(hh >> 16);
-  const int hdr = (h0 & -(int)(last < 0)) | (h1 & -(int)(last >= 0 && ctx0 == 0));
-  cost += hdr & -(int)(j == 0);
+  const int h0 = G.hc[t0][0], h1 = G.hc[t0][1];
+  const int hdr = last < 0 ? h0 : (ctx0 == 0 ? h1 : 0);
+  cost += j == 0 ? hdr : 0;
   return sum16(cost);
 }
 
@@ -688,11 +608,10 @@ __device__ Trellis16 trellis16(const K3G& G, int c, bool act, int ctx0, int type
 // VP8GetCostLuma16). Wave m = mode m. Fills rec16/lv16/lvdc and
 // mres[m] = {SSE, texture distortion, rate, nz (ac bits | dc << 24)}.
 
-// one mode's candidates on one wave (no barrier at the end: the caller's)
 template <bool TRELLIS>
-__device__ __forceinline__ void eval_i16_mode(const K3G& G, K3S& L, const vp8g_seg& S,
-                                              const MBCtx& ctx, int m, int lane) {
-  const int g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
+__device__ void eval_i16(const K3G& G, K3S& L, const vp8g_seg& S,
+                         const MBCtx& ctx, int tid) {
+  const int m = tid >> 6, lane = tid & 63, g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
   const int bsub = lane >> 4;
   int co[4];
 #pragma unroll
@@ -829,12 +748,6 @@ __device__ __forceinline__ void eval_i16_mode(const K3G& G, K3S& L, const vp8g_s
     L.mres[m][2] = rate + rdc;
     L.mres[m][3] = (int)(nzm | (dcnz ? (1u << 24) : 0u));
   }
-}
-
-// wave m = mode m over the worker, then the worker barrier
-template <bool TRELLIS>
-__device__ void eval_i16(const K3G& G, K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid) {
-  eval_i16_mode<TRELLIS>(G, L, S, ctx, tid >> 6, tid & 63);
   WB();
 }
 
@@ -843,12 +756,9 @@ __device__ void eval_i16(const K3G& G, K3S& L, const vp8g_seg& S, const MBCtx& c
 // cost_enc.c:258-278 VP8GetCostUV). Wave m = mode m, 8 blocks in 2 passes.
 // mres[m] = {SSE, rate, non-zero AC count, nz bits}.
 
-// one mode's candidates on one wave (no barrier at the end: the caller's)
-__device__ __forceinline__ void eval_uv_mode(const K3G& G, K3S& L, const vp8g_seg& S,
-                                             const MBCtx& ctx, int m, int lane, int x0,
-                                             const int8_t* topderr, int use_derr,
-                                             int32_t (*mres)[4]) {
-  const int g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
+__device__ void eval_uv(const K3G& G, K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, int x0,
+                        const int8_t* topderr, int use_derr) {
+  const int m = tid >> 6, lane = tid & 63, g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
   const int bsub = lane >> 4;
   int co[2];
 #pragma unroll
@@ -929,17 +839,11 @@ __device__ __forceinline__ void eval_uv_mode(const K3G& G, K3S& L, const vp8g_se
   sse = sum64(sse);
   rate = sum64(rate);
   if (lane == 0) {
-    mres[m][0] = sse;
-    mres[m][1] = rate;
-    mres[m][2] = flatc;
-    mres[m][3] = (int)nzm;
+    L.mres[m][0] = sse;
+    L.mres[m][1] = rate;
+    L.mres[m][2] = flatc;
+    L.mres[m][3] = (int)nzm;
   }
-}
-
-// wave m = mode m over the worker, then the worker barrier
-__device__ void eval_uv(const K3G& G, K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, int x0,
-                        const int8_t* topderr, int use_derr) {
-  eval_uv_mode(G, L, S, ctx, tid >> 6, tid & 63, x0, topderr, use_derr, L.mres);
   WB();
 }
 
@@ -1017,9 +921,7 @@ __device__ __forceinline__ int edge_off0(int k) {
   return (((4 - k) * 24) & m) | ((k - 4) & ~m);
 }
 
-// W3S: the fourth wave runs the chroma search meanwhile; the three intra-4
-// waves synchronise among themselves (wbar3)
-template <bool TRELLIS, bool W3S = false>
+template <bool TRELLIS>
 __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
                            const MBCtx& ctx, int tid, int x0,
                            int mbw, const uint8_t* predtop, const uint8_t* yl,
@@ -1049,37 +951,26 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
   const P4Lane pl = p4_lane(G.p4[act ? tid : 0], x, y);
   const int offa = edge_off0(pl.ia), offb = edge_off0(pl.ib), offc = edge_off0(pl.ic);
   // left-edge samples (L K J I = column 3 of the sub-block to the left, rows
-  // 3..0): during the search they come from the winning candidate's record
-  // (its right column packed L | K << 8 | J << 16 | I << 24) -- the
-  // sub-block to the left was decided by the barrier just passed, its
-  // winner's commit to the canvas is not ordered before this read
-  const bool la = pl.ia < 4, lb = pl.ib < 4, lc = pl.ic < 4;
+  // 3..0): during the search they come from the winning candidate's row of
+  // rec4 -- the sub-block to the left was decided by the barrier just passed,
+  // its winner's commit to the canvas is not ordered before this read
+  const int la = pl.ia < 4 ? 4 * (3 - pl.ia) + 3 : -1;
+  const int lb = pl.ib < 4 ? 4 * (3 - pl.ib) + 3 : -1;
+  const int lc = pl.ic < 4 ? 4 * (3 - pl.ic) + 3 : -1;
   // this lane's y1 quantiser entries, once per MB
   const vp8g_mtx& M = S.y1;
   const uint32_t q_sh = M.sharpen[j], q_zt = M.zthresh[j], q_iq = M.iq[j], q_bias = M.bias[j];
   const int q_q = M.q[j];
   const uint8_t* cv = &L.canvas[0][0];
-  // the segment's lambdas in registers for the whole search (read from LDS
-  // inside the loop they would be reloaded after every barrier)
-  const int tlambda = __builtin_amdgcn_readfirstlane(S.tlambda);
-  const int lam_i4 = __builtin_amdgcn_readfirstlane(S.lambda_i4);
-  const int lam_mode = __builtin_amdgcn_readfirstlane(S.lambda_mode);
   uint32_t tnz = ctx.t & 0xf, lnz = ctx.l & 0xf;
-  score_t acc_score = (score_t)211 * lam_mode, accH = 211;
+  score_t acc_score = (score_t)211 * S.lambda_mode, accH = 211;
   uint32_t acc_nz = 0;
   int total_hdr = 0;
   I4Result res;
   res.ok = 1;
-#define I4B()                      \
-  do {                             \
-    if constexpr (W3S) wbar3(L);   \
-    else wbar(L);                  \
-  } while (0)
-  int d4acc = 0, r4acc = 0;   // D and R of the blocks chosen so far (search)
-  if (!search && tid == 0) { L.d4acc = 0; L.r4acc = 0; }
-  I4B();
-  int prev_bm = 0;          // the mode chosen for the previous sub-block (worker-uniform)
-  uint32_t prev_col = 0;    // its right column (search)
+  if (tid == 0) { L.best4[0] = ~0ull; L.best4[1] = ~0ull; L.d4acc = 0; L.r4acc = 0; }
+  WB();
+  int prev_bm = 0;   // the mode chosen for the previous sub-block (worker-uniform)
   for (int i4 = 0; i4 < 16; ++i4) {
     const int bx = i4 & 3, by = i4 >> 2, par = i4 & 1;
     const int left_m = bx == 0 ? L.predleft[by] : search ? prev_bm : L.modes[i4 - 1];
@@ -1091,33 +982,20 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
     const int src = L.yin[(4 * by + y) * BPS + 4 * bx + x];
     int pr = 0, rec = 0, nzb = 0;
     int level = 0, dq = 0;
-    // the intra-16 score so far (wave 3 publishes it once known), read at the
-    // top so the load is long done when the snapshot is stored
-    score_t snap = 0;
-    if constexpr (W3S) {
-      if (tid == 0) snap = __hip_atomic_load(&L.rd16pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
     if (busy) {
     {
       const uint8_t* cb = cv + 96 * by + 4 * bx;   // sub-block base (worker-uniform)
       const bool lft = search && bx > 0;          // worker-uniform
-      // branch-free: every canvas sample is loaded and the left ones are
-      // replaced arithmetically (a select the compiler turns into a branch
-      // around the load serialises the loads with a wait on each)
-      const int mlft = lft ? -1 : 0;
-      int ea = cb[offa], eb = cb[offb], ec = cb[offc];
-      ea += ((int)((prev_col >> (8 * pl.ia)) & 255) - ea) & (la ? mlft : 0);
-      eb += ((int)((prev_col >> (8 * pl.ib)) & 255) - eb) & (lb ? mlft : 0);
-      ec += ((int)((prev_col >> (8 * pl.ic)) & 255) - ec) & (lc ? mlft : 0);
+      const uint8_t* rl = &L.rec4[par ^ 1][prev_bm][0];
+      const int ea = *(lft && la >= 0 ? rl + la : cb + offa);
+      const int eb = *(lft && lb >= 0 ? rl + lb : cb + offb);
+      const int ec = *(lft && lc >= 0 ? rl + lc : cb + offc);
       pr = clip8((pl.wa * ea + pl.wb * eb + pl.wc * ec + pl.rnd) >> pl.sh);
       if (pl.dc) {
         int s4 = 4;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          int lv = cb[edge_off0(k)];
-          lv += ((int)((prev_col >> (8 * k)) & 255) - lv) & mlft;
-          s4 += lv + cb[edge_off0(5 + k)];
-        }
+        for (int k = 0; k < 4; ++k)
+          s4 += *(lft ? rl + 4 * (3 - k) + 3 : cb + edge_off0(k)) + cb[edge_off0(5 + k)];
         pr = s4 >> 3;
       }
     }
@@ -1145,95 +1023,46 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
     if (search) {
       const int D = sum16((src - rec) * (src - rec));
       int SD = 0;
-      if (tlambda) {
+      if (S.tlambda) {
         const int td = sum16(ttrans_lane(rec, j, wj)) - L.hsrc[i4];
-        SD = (tlambda * (iabs_(td) >> 5) + 128) >> 8;
+        SD = (S.tlambda * (iabs_(td) >> 5) + 128) >> 8;
       }
       SUBST(4);
       const int cntnz = __popcll((bac >> g) & 0xffff);
       const int R0 = (m > 0 && cntnz <= 3) ? 140 : 0;
       const int Rc = rate_lane(G, level, j, g, ctx4, 3, 0);
-      // the candidate's right column on its group's lane 0: L = row 3 (lane
-      // 15), K (11), J (7), I (3); row_ror:n reads lane (i - n) mod 16
-      // (pinned DPP reads: only lane 0 uses them, inside the branch below,
-      // and a DPP sunk there would read masked-off source lanes)
-      const uint32_t col = (uint32_t)dpp_pin<DPP_ROR(1)>(0, rec) |
-                           ((uint32_t)dpp_pin<DPP_ROR(5)>(0, rec) << 8) |
-                           ((uint32_t)dpp_pin<DPP_ROR(9)>(0, rec) << 16) |
-                           ((uint32_t)dpp_pin<DPP_ROR(13)>(0, rec) << 24);
-      // the wave's best candidate (argmin of score << 4 | mode: ties to the
-      // lower mode) from its four groups' lane 0, without LDS
-      const int H = G.mcost4[(top_m * 10 + left_m) * 10 + (act ? m : 0)];
-      const score_t dist = 256 * (score_t)(D + SD);
-      const score_t sc = (score_t)(R0 + Rc + H) * lam_i4 + dist;
-      const unsigned long long key = act ? ((unsigned long long)sc << 4) | (unsigned)m : ~0ull;
-      unsigned long long wmin = ~0ull;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const unsigned long long kq =
-            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(key >> 32), 16 * q) << 32) |
-            (uint32_t)__builtin_amdgcn_readlane((int)key, 16 * q);
-        wmin = kq < wmin ? kq : wmin;
-      }
-      if (W3S && tid == 0) L.rd16snap[par] = snap;
-      if (j == 0 && key == wmin) {   // one lane per wave: its record
-        // key, H | nz << 16, R, D, right column (the lambda_mode score is
-        // the key's score with R + H re-weighted, after the barrier)
-        uint32_t* r = L.i4rec[par][tid >> 6];
-        *reinterpret_cast<uint4*>(r) = make_uint4((uint32_t)key, (uint32_t)(key >> 32),
-                                                  (uint32_t)H | ((uint32_t)nzb << 16),
-                                                  (uint32_t)(R0 + Rc));
-        *reinterpret_cast<uint2*>(r + 4) = make_uint2((uint32_t)D, col);
+      if (act) L.rec4[par][m][j] = (uint8_t)rec;
+      if (act && j == 0) {
+        const int H = G.mcost4[(top_m * 10 + left_m) * 10 + m];
+        const score_t dist = 256 * (score_t)(D + SD);
+        const score_t sc = (score_t)(R0 + Rc + H) * S.lambda_i4 + dist;
+        atomicMin(&L.best4[i4 % 3], ((unsigned long long)sc << 4) | (unsigned)m);
+        L.sm4[par][m] = (score_t)(R0 + Rc + H) * S.lambda_mode + dist;
+        L.r4[par][m][0] = H;
+        L.r4[par][m][1] = nzb;
+        L.r4[par][m][2] = R0 + Rc;
+        L.r4[par][m][3] = D;
       }
     }
     }   // busy
     SUBST(5);
-    I4B();
+    WB();
     int bm;
     if (search) {
-      // argmin over the three waves' records (one LDS round trip for all of
-      // them). The records of this parity were written before this barrier;
-      // they are written again two sub-blocks on, after the next barrier,
-      // which every wave passes only once it has read them here.
-      const uint32_t* R0p = L.i4rec[par][0];
-      const uint32_t* R1p = L.i4rec[par][1];
-      const uint32_t* R2p = L.i4rec[par][2];
-      const uint4 a0 = *reinterpret_cast<const uint4*>(R0p);
-      const uint4 a1 = *reinterpret_cast<const uint4*>(R1p);
-      const uint4 a2 = *reinterpret_cast<const uint4*>(R2p);
-      const uint2 b0 = *reinterpret_cast<const uint2*>(R0p + 4);
-      const uint2 b1 = *reinterpret_cast<const uint2*>(R1p + 4);
-      const uint2 b2 = *reinterpret_cast<const uint2*>(R2p + 4);
-      const unsigned long long k0 = ((unsigned long long)a0.y << 32) | a0.x;
-      const unsigned long long k1 = ((unsigned long long)a1.y << 32) | a1.x;
-      const unsigned long long k2 = ((unsigned long long)a2.y << 32) | a2.x;
-      // (picked by masks, so every record word is loaded up front: a select
-      // the compiler turns into a branch around a load waits on all LDS ops)
-      const uint32_t m1 = 0u - (uint32_t)(k1 < k0);
-      const unsigned long long k01 = k0 ^ ((k0 ^ k1) & ((unsigned long long)m1 << 32 | m1));
-      const uint32_t m2 = 0u - (uint32_t)(k2 < k01);
-      const unsigned long long kb = k01 ^ ((k01 ^ k2) & ((unsigned long long)m2 << 32 | m2));
-      auto pick = [&](uint32_t v0, uint32_t v1, uint32_t v2) {
-        const uint32_t v01 = v0 ^ ((v0 ^ v1) & m1);
-        return v01 ^ ((v01 ^ v2) & m2);
-      };
-      const uint32_t hz = pick(a0.z, a1.z, a2.z);
-      const int Rb = (int)pick(a0.w, a1.w, a2.w);
-      const uint2 Bv = make_uint2(pick(b0.x, b1.x, b2.x), pick(b0.y, b1.y, b2.y));
-      bm = (int)(kb & 15);
-      const int H = (int)(hz & 0xffff), bnzv = (int)(hz >> 16);
-      d4acc += (int)Bv.x;
-      r4acc += Rb;
-      prev_col = Bv.y;
+      // argmin, ties to the lower mode. The slot read here was last written
+      // before this barrier; the one reset here (used two sub-blocks on) was
+      // last read before it (three slots, so no second barrier is needed)
+      bm = (int)(L.best4[i4 % 3] & 15);
+      if (tid == 0) {
+        L.best4[(i4 + 2) % 3] = ~0ull;
+        L.d4acc += L.r4[par][bm][3];
+        L.r4acc += L.r4[par][bm][2];
+      }
+      const int H = L.r4[par][bm][0], bnzv = L.r4[par][bm][1];
       accH += H;
-      // (R + H) lambda_mode + 256 (D + SD) = score - (R + H)(lambda_i4 - lambda_mode)
-      acc_score += (score_t)(kb >> 4) - (score_t)(Rb + H) * (lam_i4 - lam_mode);
+      acc_score += L.sm4[par][bm];
       acc_nz |= (uint32_t)bnzv << i4;
-      // the early exit against the intra-16 score: with W3S the score may not
-      // be known yet (then the snapshot is the maximum, and the final
-      // comparison is made at the join); both scores only grow, so the
-      // outcome is the same
-      if (acc_score >= (W3S ? L.rd16snap[par] : rd_score)) { res.ok = 0; break; }
+      if (acc_score >= rd_score) { res.ok = 0; break; }
       total_hdr += H;
       if (total_hdr > max_bits) { res.ok = 0; break; }
       tnz = (tnz & ~(1u << bx)) | ((uint32_t)bnzv << bx);
@@ -1250,19 +1079,16 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
     }
     if (search && tid == 0) L.modes[i4] = (uint8_t)bm;
     prev_bm = bm;
-    // the search needs no second barrier: the next sub-block takes its left
-    // edge from the winner's record (above), every other canvas sample it
-    // reads was committed before an earlier barrier, and L.modes[i4] is read
-    // 4 sub-blocks on
+    // the search needs no second barrier: the next sub-block reads its left
+    // edge from rec4 (above), every other canvas sample it reads was committed
+    // before an earlier barrier, and L.modes[i4] is read 4 sub-blocks on
     if (!search) {
-      I4B();
+      WB();
       acc_nz |= (uint32_t)L.nzsel << i4;
     }
     SUBST(7);
   }
-  if (search && tid == 0) { L.d4acc = d4acc; L.r4acc = r4acc; }
-  I4B();
-#undef I4B
+  WB();
   res.H = accH;
   res.score = acc_score;
   res.nz = acc_nz;
@@ -1289,9 +1115,7 @@ __device__ __forceinline__ int pos_tokens(int type, int first, int ctx0, int n, 
   auto dyn = [&](int bit, int pid, int sid) -> int {
     if (EMIT) {
       out[count] = (uint16_t)((bit << 15) | pid);
-#ifndef K3_AB_NO_TOKSTAT   // (timing A/B only: wrong statistics)
       atomicAdd(&delta[sid], 0x10000u + (uint32_t)bit);   // folded in raster order later
-#endif
     }
     ++count;
     return bit;
@@ -2026,7 +1850,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     G.fs.nb[0] = G.fs.nb[1] = G.fs.nb[2] = 0;
     G.fold_ptr = 0; G.ntok = 0; G.tok_err = 0; G.epoch = 0; G.abort = 0;
   }
-  if (tid == 0) { L.bar = 0; L.bar3 = 0; L.myabort = 0; L.cpos = 0; L.cend = 0; }
+  if (tid == 0) { L.bar = 0; L.myabort = 0; L.cpos = 0; L.cend = 0; }
 #ifdef K3_CHECK
   if (tid == 0) {
     L.ck_nmb = (uint32_t)nmb; L.ck_cap = a.arena_cap + VP8G_MAX_TOKENS_PER_MB;
@@ -2083,9 +1907,6 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       L.epseen = __hip_atomic_load(&G.epoch, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
     int left_dc = 0;
     uint32_t fold_from = (uint32_t)y * mbw;   // first MB of this row not folded yet
-    // the row's first MB's source; each MB fetches the next one's during its
-    // token stage, so the global loads never sit on an MB's critical path
-    uint32_t pf = fetch_mb256(Yp, Up, Vp, w, h, 0, y, tid);
     wbar(L);
     for (int x = 0; x < mbw; ++x) {
       // per-lane ids re-derived every MB (opaque): values computed from them
@@ -2096,9 +1917,6 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       const uint32_t mb = (uint32_t)y * mbw + x;
 #ifdef K3_CHECK
       if (tid == 0) { L.ck_y = y; L.ck_x = -1 - x; }   // (negative: before the MB's waits)
-#endif
-#ifdef K3_BARCHECK
-      if (L.myabort) break;   // (a barrier of this worker gave up)
 #endif
       // ---- cost-table epoch (frame_enc.c:828-832): refresh before MB k with
       // k = max_count + e * (max_count + 1)
@@ -2261,16 +2079,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         // issue priority by place in the row wavefront: a worker whose row
         // above is finished leads and gates the others (they wait on its
         // progress), so its waves win the SIMDs' issue arbitration
-        int lead = __builtin_amdgcn_readfirstlane(L.lead);
-#ifdef K3_EPRIO   // A/B: before a cost-epoch boundary K the rows above K's row must
-                  // finish first; the one with the most left (right above) leads
-        {
-          const int K = max_count + ep * (max_count + 1);
-          const int d = __builtin_amdgcn_readfirstlane(K / mbw - y);
-          if (d >= 1 && d <= 2) lead = 3 - d;   // row K-1: 2, row K-2: 1
-          else if (d == 3 || d == 0) lead = 0;
-        }
-#endif
+        const int lead = __builtin_amdgcn_readfirstlane(L.lead);
 #ifndef K3_PRIO_LEAD
 #define K3_PRIO_LEAD 2
 #endif
@@ -2293,12 +2102,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       const uint64_t tr_mb = TR_NOW();
       TR_ADD(K3TR_NMB, 1);
 
-#ifdef K3_AB_NO_PREFETCH   // (timing A/B: the MB's source loaded at its start)
       load_mb(Yp, Up, Vp, w, h, x, y, L.yin, tid, K3T);
-      (void)pf;
-#else
-      put_mb256(pf, L.yin, tid);
-#endif
       wbar(L);
       int segid = segmap[mb];
       if (!K3CK(segid >= 0 && segid < 4, 13, segid, 4, mb)) segid = 0;
@@ -2334,34 +2138,20 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       wbar(L);
       K3_STAMP(1);
 
-      // Three searches per MB (quant_enc.c:1002-1217). With intra-4 on
-      // (max_i4_header_bits > 0) they run side by side: intra-4 on the
-      // worker's waves with rtid < 192 (its 160 lanes, barriers among those
-      // three waves, wbar3), intra-16 and then chroma on the fourth wave, all
-      // four modes of each in turn. None reads what another writes (intra-16:
-      // p16, its candidates' levels and reconstructions; chroma: the U/V
-      // predictions, the DC error state; intra-4: the luma canvas and its
-      // records) and the chroma choice depends on neither luma choice. The
-      // intra-4 loop's exit against the intra-16 score (quant_enc.c:1153)
-      // takes the score once the fourth wave has published it, and the final
-      // comparison is made at the join: both scores only grow, so the
-      // outcome is the reference's. Without intra-4 the worker runs intra-16
-      // and chroma one after the other, wave m = mode m.
-#ifndef K3_FORK
-#define K3_FORK 1
-#endif
-      const bool i4on = max_i4_bits > 0;   // (quant_enc.c:1375: intra-4 only then)
-      const bool fork = K3_FORK && i4on;
-#ifndef K3_FORK16
-#define K3_FORK16 0   // intra-16 on the fourth wave too (A/B: slower)
-#endif
-      const bool fork16 = fork && K3_FORK16;
+      // ---- Intra16 (quant_enc.c:1002-1058)
+      const uint64_t tr_i16 = TR_NOW();
+      if constexpr (TR) {
+        if (trellis_all) eval_i16<true>(G, L, S, ctx, tid);
+        else eval_i16<false>(G, L, S, ctx, tid);
+      } else {
+        eval_i16<false>(G, L, S, ctx, tid);
+      }
+      TR_SINCE(K3TR_I16, tr_i16);
       int best16 = 0;
       uint32_t nz16 = 0;
       score_t D16 = 0, SD16 = 0, H16 = 0, R16 = 0;
-      // the intra-16 choice from the candidates in L.mres (quant_enc.c:1040-1057;
-      // IsFlatSource16 per wave, each lane checks 4 of the 256 samples)
-      auto pick_i16 = [&]() {
+      {
+        // IsFlatSource16 per wave (each lane checks 4 of the 256 samples): no barrier
         const int v0 = L.yin[0];
         int same = 1;
 #pragma unroll
@@ -2387,186 +2177,82 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
             nz16 = (uint32_t)L.mres[mm][3];
           }
         }
-      };
-      // StoreMaxDelta (quant_enc.c:1045-1050), whatever the MB's final choice
-      auto max_delta = [&](bool lane0) {
-        if ((nz16 & 0x100ffff) == 0x1000000 && D16 > S.min_disto) {
-          int mv = iabs_(L.lvdc[best16][1]);
-          mv = max(mv, iabs_(L.lvdc[best16][2]));
-          mv = max(mv, iabs_(L.lvdc[best16][4]));
-          if (lane0) atomicMax(&G.max_edge[segid], mv);
-        }
-      };
-      if (tid == 0) L.rd16pub = 0x7fffffffffffffffLL;
-      const uint64_t tr_i16 = TR_NOW();
-      if (!fork16) {
-        if constexpr (TR) {
-          if (trellis_all) eval_i16<true>(G, L, S, ctx, tid);
-          else eval_i16<false>(G, L, S, ctx, tid);
-        } else {
-          eval_i16<false>(G, L, S, ctx, tid);
-        }
-        pick_i16();
-        max_delta(tid == 0);
-        if (fork && tid == 0) L.rd16pub = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
       }
-      TR_SINCE(K3TR_I16, tr_i16);
-      K3_STAMP(2);
-      wbar(L);   // (fork: the rd16pub reset above before either side)
-
-      // ---- Intra4 (quant_enc.c:1072-1165) || Intra16 + UV
-      const uint64_t tr_i4 = TR_NOW();
-      score_t rd_score = 0, rdH = 0;
-      uint32_t rd_nz = 0;
+      // commit I16 as current best
+      L.yout[(tid >> 4) * BPS + (tid & 15)] = L.rec16[best16][tid];
+      (&L.fin_ac[0][0])[tid] = (&L.lv16[best16][0][0])[tid];
+      if (tid < 16) { L.fin_dc[tid] = L.lvdc[best16][tid]; L.modes[tid] = best16; }
+      score_t rd_score = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
+      score_t rdH = H16;
+      uint32_t rd_nz = nz16;
       int is_i16 = 1;
-      int i4ok = 0;
-      score_t i4score = 0, i4H = 0;
-      uint32_t i4nz = 0;
-      if (fork) {
-        if (rtid < 192) {
-          I4Result r4;
-          if constexpr (TR) {
-            r4 = trellis_all ? run_i4<true, true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
-                                                  0, max_i4_bits, substamps)
-                             : run_i4<false, true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
-                                                   0, max_i4_bits, substamps);
-          } else {
-            r4 = run_i4<false, true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true, 0,
-                                     max_i4_bits, substamps);
-          }
-          if (rtid == 0) {
-            L.i4ok = r4.ok;
-            L.i4H = r4.H;
-            L.i4score = r4.score;
-            L.i4nz = r4.nz;
-          }
-        } else {   // intra-16 (fork16), then chroma, on one wave
-          if (fork16) {
-            for (int mm = 0; mm < 4; ++mm) {
-              if constexpr (TR) {
-                if (trellis_all) eval_i16_mode<true>(G, L, S, ctx, mm, lane);
-                else eval_i16_mode<false>(G, L, S, ctx, mm, lane);
-              } else {
-                eval_i16_mode<false>(G, L, S, ctx, mm, lane);
-              }
-              wsync();
-            }
-            pick_i16();
-            max_delta(lane == 0);
-            if (lane == 0) {
-              L.i16best = best16;
-              L.i16nz = nz16;
-              L.i16D = D16; L.i16SD = SD16; L.i16H = H16; L.i16R = R16;
-              __hip_atomic_store(&L.rd16pub, (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16),
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-          }
-          for (int mm = 0; mm < 4; ++mm) {
-            eval_uv_mode(G, L, S, ctx, mm, lane, x, derrrd, use_derr, L.mresuv);
-            wsync();
-          }
-          int b = 0;
-          score_t bsc = 0;
-          for (int mm = 0; mm < 4; ++mm) {
-            const score_t Dm = L.mresuv[mm][0], Hm = kVP8ModeCostUV[mm];
-            score_t Rm = L.mresuv[mm][1];
-            if (mm > 0 && L.mresuv[mm][2] <= 2) Rm += 140 * 8;
-            const score_t sc = (Rm + Hm) * S.lambda_uv + 256 * Dm;
-            if (mm == 0 || sc < bsc) { bsc = sc; b = mm; }
-          }
-          if (lane == 0) L.uvsel = b;
-          if (use_derr && lane < 2) {   // StoreDiffusionErrors (quant_enc.c:909-920)
-            const int cch = lane;
-            int8_t* top = topderr + 4 * x + 2 * cch;
-            int8_t* left = L.lderr[cch];
-            const int8_t* e = L.uvderr[b][cch];
-            left[0] = e[0];
-            left[1] = (int8_t)(3 * e[2] >> 2);
-            top[0] = e[1];
-            top[1] = (int8_t)(e[2] - left[1]);
-          }
-        }
-        wbar(L);   // join
-        if (fork16) {
-          best16 = L.i16best;
-          nz16 = L.i16nz;
-          D16 = L.i16D; SD16 = L.i16SD; H16 = L.i16H; R16 = L.i16R;
-        }
-        i4ok = L.i4ok;
-        i4score = L.i4score;
-        i4H = L.i4H;
-        i4nz = L.i4nz;
-      } else if (i4on) {
-        // sequential: intra-4 on the worker's waves (the fourth holds no mode)
-        // with the intra-16 score known, then chroma on all four
-        const score_t rd16 = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
-        I4Result r4;
-        if constexpr (TR) {
-          r4 = trellis_all ? run_i4<true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true, rd16,
-                                          max_i4_bits, substamps)
-                           : run_i4<false>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true, rd16,
-                                           max_i4_bits, substamps);
-        } else {
-          r4 = run_i4<false>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true, rd16, max_i4_bits,
-                             substamps);
-        }
-        i4ok = r4.ok;
-        i4score = r4.score;
-        i4H = r4.H;
-        i4nz = r4.nz;
-      }
-      // the intra-16 candidate as the MB's score so far (quant_enc.c:1368-1372)
-      rd_score = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
-      rdH = H16;
-      rd_nz = nz16;
       if (tid < 64) {   // whole wave 0: a lone-lane store here spills
         L.mdist = (int32_t)D16;
         L.ry16 = (int32_t)R16;
       }
-      if (i4on && i4ok && i4score < rd_score) {   // intra-4 wins (quant_enc.c:1375-1382)
-        is_i16 = 0;
-        if (tid == 0) L.mdist = L.d4acc;
-        rdH = i4H;
-        rd_score = i4score;
-        rd_nz = i4nz;
-        L.yout[(tid >> 4) * BPS + (tid & 15)] = L.acc_out[tid];
-        (&L.fin_ac[0][0])[tid] = (&L.acc_ac[0][0])[tid];
-      } else {   // intra-16 (the aborted or beaten intra-4 search wrote some modes)
-        L.yout[(tid >> 4) * BPS + (tid & 15)] = L.rec16[best16][tid];
-        (&L.fin_ac[0][0])[tid] = (&L.lv16[best16][0][0])[tid];
-        if (tid < 16) { L.fin_dc[tid] = L.lvdc[best16][tid]; L.modes[tid] = best16; }
+      if ((rd_nz & 0x100ffff) == 0x1000000 && D16 > S.min_disto) {   // StoreMaxDelta
+        int mv = iabs_(L.lvdc[best16][1]);
+        mv = max(mv, iabs_(L.lvdc[best16][2]));
+        mv = max(mv, iabs_(L.lvdc[best16][4]));
+        if (tid == 0) atomicMax(&G.max_edge[segid], mv);
       }
-      if (!fork) eval_uv(G, L, S, ctx, tid, x, derrrd, use_derr);
+      // the intra-4 search opens with a worker barrier, which orders the
+      // commit above before anything reads it
+      if (max_i4_bits <= 0) wbar(L);
+      K3_STAMP(2);
+
+      // ---- Intra4 (quant_enc.c:1072-1165)
+      const uint64_t tr_i4 = TR_NOW();
+      if (max_i4_bits > 0) {
+        I4Result r4;
+        if constexpr (TR) {
+          r4 = trellis_all ? run_i4<true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
+                                          rd_score, max_i4_bits, substamps)
+                           : run_i4<false>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
+                                           rd_score, max_i4_bits, substamps);
+        } else {
+          r4 = run_i4<false>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true, rd_score,
+                             max_i4_bits, substamps);
+        }
+        if (r4.ok) {
+          is_i16 = 0;
+          if (tid == 0) L.mdist = L.d4acc;
+          rdH = r4.H;
+          rd_score = r4.score;
+          rd_nz = r4.nz;
+          L.yout[(tid >> 4) * BPS + (tid & 15)] = L.acc_out[tid];
+          (&L.fin_ac[0][0])[tid] = (&L.acc_ac[0][0])[tid];
+        } else {
+          if (tid < 16) L.modes[tid] = best16;   // the aborted search wrote some
+        }
+        // (no barrier: the chroma search reads none of this, and its own
+        // barriers order it before the readers -- info, SSE, tokens)
+      }
       K3_STAMP(3);
       const uint64_t tr_uv = TR_NOW();
       TR_ADD(K3TR_I4, tr_uv - tr_i4);
 
-      // ---- the chroma choice (quant_enc.c:1169-1217)
+      // ---- UV (quant_enc.c:1169-1217)
       int bu = 0;
-      const int32_t(*mr)[4] = fork ? L.mresuv : L.mres;   // the chroma candidates
       {
+        eval_uv(G, L, S, ctx, tid, x, derrrd, use_derr);
         score_t bsc = 0, bH = 0;
-        if (fork) {
-          bu = L.uvsel;
-          bH = kVP8ModeCostUV[bu];
-        } else {
-          for (int mm = 0; mm < 4; ++mm) {
-            const score_t Dm = mr[mm][0], Hm = kVP8ModeCostUV[mm];
-            score_t Rm = mr[mm][1];
-            if (mm > 0 && mr[mm][2] <= 2) Rm += 140 * 8;
-            const score_t sc = (Rm + Hm) * S.lambda_uv + 256 * Dm;
-            if (mm == 0 || sc < bsc) { bsc = sc; bu = mm; bH = Hm; }
-          }
+        for (int mm = 0; mm < 4; ++mm) {
+          const score_t Dm = L.mres[mm][0], Hm = kVP8ModeCostUV[mm];
+          score_t Rm = L.mres[mm][1];
+          if (mm > 0 && L.mres[mm][2] <= 2) Rm += 140 * 8;
+          const score_t sc = (Rm + Hm) * S.lambda_uv + 256 * Dm;
+          if (mm == 0 || sc < bsc) { bsc = sc; bu = mm; bH = Hm; }
         }
         rdH += bH;
         rd_score += bsc;
-        if (tid == 0) L.mdist += mr[bu][0];
-        rd_nz |= (uint32_t)mr[bu][3] << 16;
+        if (tid == 0) L.mdist += L.mres[bu][0];
+        rd_nz |= (uint32_t)L.mres[bu][3] << 16;
         if (tid < 128) {
           L.yout[(tid >> 4) * BPS + 16 + (tid & 15)] = L.recuv[bu][tid];
           (&L.fin_uv[0][0])[tid] = (&L.lvuv[bu][0][0])[tid];
         }
-        if (!fork && use_derr && tid < 2) {   // StoreDiffusionErrors (quant_enc.c:909-920)
+        if (use_derr && tid < 2) {   // StoreDiffusionErrors (quant_enc.c:909-920)
           const int cch = tid;
           int8_t* top = topderr + 4 * x + 2 * cch;
           int8_t* left = L.lderr[cch];
@@ -2622,7 +2308,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         atomicAdd(&G.fs.size_p0, (unsigned long long)rdH);
         if constexpr (!TR) {   // R of the chosen luma modes + the chosen UV mode's R
           // with its flatness penalty (StatLoop passes run RD_OPT_BASIC, never TR)
-          const int ruv = mr[bu][1] + ((bu > 0 && mr[bu][2] <= 2) ? 140 * 8 : 0);
+          const int ruv = L.mres[bu][1] + ((bu > 0 && L.mres[bu][2] <= 2) ? 140 * 8 : 0);
           atomicAdd(&G.fs.size_rh,
                     (unsigned long long)(rdH + (is_i16 ? L.ry16 : L.r4acc) + ruv));
         }
@@ -2656,9 +2342,6 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         }
       }
 
-#ifndef K3_AB_NO_PREFETCH
-      if (x + 1 < mbw) pf = fetch_mb256(Yp, Up, Vp, w, h, x + 1, y, tid);
-#endif
       // ---- tokens (token_enc.c:113-193) into this MB's slot; one (block,
       // zigzag position) item per thread, counts + scan + writes in parallel
       const int first_blk = is_i16 ? 0 : 1;
@@ -3187,13 +2870,6 @@ extern "C" __attribute__((visibility("default"))) int vp8g_k3_hang(uint32_t* out
     return 0;
   return 1;
 }
-#ifdef K3_BARCHECK
-// barrier-check build: the barrier records [1024][4][4][8] (see g_k3bar)
-extern "C" __attribute__((visibility("default"))) int vp8g_k3_bar(uint32_t* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k3bar), sizeof(g_k3bar), 0, hipMemcpyDeviceToHost) ==
-         hipSuccess;
-}
-#endif
 #endif
 
 #ifdef K3_TRACE

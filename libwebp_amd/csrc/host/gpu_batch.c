@@ -1638,6 +1638,14 @@ int vp8g_engine_import(WebPGpuBatch* b, const uint8_t* rgba, int stride, uint8_t
   uint32_t flag = 0;
   if (hipMemcpy(&flag, b->d_aflags, 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
   *has_alpha = flag != 0;
+  /* K1 writes no alpha plane (the sharp-YUV import extracts its own): the
+   * plane of a frame with alpha comes from the RGBA here */
+  const int sharp_used = sharp && b->w >= 4 && b->h >= 4;
+  if (a && flag && !sharp_used &&
+      (!vp8g_launch_extract_alpha(b->d_rgba, need, stride, b->w, b->h, 1, NULL, b->d_aplane,
+                                  b->stream) ||
+       hipStreamSynchronize(b->stream) != hipSuccess))
+    return 0;
   const uint8_t* src = b->d_yuv;
   if (hipMemcpy(y, src, (size_t)b->w * b->h, hipMemcpyDeviceToHost) != hipSuccess) return 0;
   src += (size_t)b->w * b->h;

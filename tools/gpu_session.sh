@@ -2,7 +2,7 @@
 # One GPU-box session: GPU tests, bench line, K3 stage split, rocprofv3 kernel
 # stats, PMC passes (HBM bytes, SQ issue counters) and the PMC calibration.
 # Usage (on the box): bash tools/gpu_session.sh <tag> [steps...]
-#   steps: tests ltests bench lowmem lossless lab cfg4 lphases lprof lpmc stages prof pmc sq calib (default: all but the lossless ones)
+#   steps: tests ltests bench lowmem lossless lab cfg4 lphases lprof lpmc stages stages6 prof pmc sq sq3 calib (default: all but the lossless ones)
 set -o pipefail
 TAG=${1:-s}; shift
 STEPS=${*:-tests bench stages prof pmc sq calib}
@@ -108,6 +108,12 @@ if has stages; then
     WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_prof.so run timeout -k 10 150 \
       python3 tools/k3_stages.py 1920 1080 $B 4 > $O/stages_$B.log 2>&1 || exit 1
   done
+fi
+if has stages6; then   # m6 (config 4's method) stage split at 1080p, and the intra-4 sub-stages
+  WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_prof.so run timeout -k 10 200 \
+    python3 tools/k3_stages.py 1920 1080 256 6 > $O/stages6_256.log 2>&1 || exit 1
+  WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_sub.so run timeout -k 10 200 \
+    python3 tools/k3_stages.py 1920 1080 256 6 > $O/sub6_256.log 2>&1 || exit 1
 fi
 cd /tmp && export TMPDIR=/tmp
 if has prof; then

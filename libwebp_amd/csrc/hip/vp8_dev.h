@@ -245,6 +245,36 @@ __device__ __forceinline__ void load_mb(const uint8_t* Yp, const uint8_t* Up, co
   }
 }
 
+// load_mb for a 256-thread worker in two steps, so the global loads of the
+// next MB can be in flight while the current one finishes: fetch_mb256 puts
+// MB (x, y)'s Y byte of this thread (and a U or V byte for threads < 128)
+// into one register (Y in bits 0-7, U or V in bits 8-15), put_mb256 stores
+// them into the cache.
+__device__ __forceinline__ uint32_t fetch_mb256(const uint8_t* Yp, const uint8_t* Up,
+                                                const uint8_t* Vp, int w, int h, int x, int y,
+                                                int t) {
+  const int uvw = (w + 1) >> 1;
+  const int bw = min(w - 16 * x, 16), bh = min(h - 16 * y, 16);
+  const int cw = (bw + 1) >> 1, ch = (bh + 1) >> 1;
+  uint32_t v;
+  {
+    const int r = t >> 4, c = t & 15;
+    const int rr = min(r, bh - 1), cc = min(c, bw - 1);
+    v = Yp[(size_t)(16 * y + rr) * w + 16 * x + cc];
+  }
+  if (t < 128) {
+    const int pl = t >> 6, r = (t >> 3) & 7, c = t & 7;
+    const int rr = min(r, ch - 1), cc = min(c, cw - 1);
+    const uint8_t* P = pl ? Vp : Up;
+    v |= (uint32_t)P[(size_t)(8 * y + rr) * uvw + 8 * x + cc] << 8;
+  }
+  return v;
+}
+__device__ __forceinline__ void put_mb256(uint32_t v, uint8_t* cache, int t) {
+  cache[(t >> 4) * BPS + (t & 15)] = (uint8_t)v;
+  if (t < 128) cache[((t >> 3) & 7) * BPS + 16 + 8 * (t >> 6) + (t & 7)] = (uint8_t)(v >> 8);
+}
+
 // 16x16 / 8x8 predictor sample (src/dsp/enc.c:238-342). left/top arrays with
 // index -1 = corner; has_left/has_top select the 127/129 fall-backs.
 __device__ __forceinline__ int pred_sample(int mode, int n, int px, int py, const uint8_t* left,

@@ -1165,6 +1165,23 @@ __device__ __forceinline__ int pos_tokens(int type, int first, int ctx0, int n, 
   return count;
 }
 
+// pos_tokens' token count without its branches (selects only): the header
+// token (first position or after a non-zero level; alone when n > last), the
+// zero check, and for a non-zero level the v > 1 check, the value tokens of
+// its range (2..4: 2 + (v != 2); 5..10: 3 + (v <= 6 ? 1 : 2); 11+: 4 + the
+// category's extra bits 3 / 4 / 5 / 11) and the sign
+__device__ __forceinline__ int pos_count(int first, int n, int c, int cprev, int last) {
+  const int vprev = iabs_(cprev), v = iabs_(c);
+  const int none = (n < first) | ((n > first) & (vprev == 0) & (n > last));
+  const int hdr = (n == first) | (vprev != 0);
+  const int res = v - 3;
+  const int nextra = res < 16 ? 3 : res < 32 ? 4 : res < 64 ? 5 : 11;
+  const int big = v <= 4 ? 2 + (v != 2) : v <= 10 ? 3 + 1 + (v > 6) : 4 + nextra;
+  const int body = 1 + (v != 0 ? 2 + (v > 1 ? big : 0) : 0);
+  const int cnt = (hdr & (n > last)) ? 1 : hdr + body;
+  return none ? 0 : cnt;
+}
+
 // FinalizeTokenProbas (frame_enc.c:146-180) over the workgroup; returns the
 // reference's "dirty" flag (some probability differs from the default).
 __device__ int finalize_probas_wg(K3G& G, K3S& L, int tid) {
@@ -1907,6 +1924,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       L.epseen = __hip_atomic_load(&G.epoch, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
     int left_dc = 0;
     uint32_t fold_from = (uint32_t)y * mbw;   // first MB of this row not folded yet
+#ifdef K3_PF   // (A/B) each MB fetches the next one's source during its token stage
+    uint32_t pf = K3T == 256 ? fetch_mb256(Yp, Up, Vp, w, h, 0, y, tid) : 0u;
+#endif
     wbar(L);
     for (int x = 0; x < mbw; ++x) {
       // per-lane ids re-derived every MB (opaque): values computed from them
@@ -2079,7 +2099,22 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         // issue priority by place in the row wavefront: a worker whose row
         // above is finished leads and gates the others (they wait on its
         // progress), so its waves win the SIMDs' issue arbitration
-        const int lead = __builtin_amdgcn_readfirstlane(L.lead);
+        int lead = __builtin_amdgcn_readfirstlane(L.lead);
+#ifndef K3_NO_EPRIO   // before a cost-epoch boundary K every row above K's row
+                      // must finish first: the row right above leads, the
+                      // rows below wait anyway (K3 105.8 -> 102.7 ms, r5s19)
+        {
+          const int K = max_count + ep * (max_count + 1);
+          const int d = __builtin_amdgcn_readfirstlane(K / mbw - y);
+#ifdef K3_EPRIO2   // (A/B) three levels above the boundary row, over the usual lead
+          if (d >= 1 && d <= 3) lead = 4 - d;
+          else if (d == 0) lead = 0;
+#else
+          if (d >= 1 && d <= 2) lead = 3 - d;
+          else if (d == 3 || d == 0) lead = 0;
+#endif
+        }
+#endif
 #ifndef K3_PRIO_LEAD
 #define K3_PRIO_LEAD 2
 #endif
@@ -2089,7 +2124,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         else if (lead == 1) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
 #else
-        if (lead == 2) __builtin_amdgcn_s_setprio(K3_PRIO_LEAD);
+        if (lead == 3) __builtin_amdgcn_s_setprio(3);
+        else if (lead == 2) __builtin_amdgcn_s_setprio(K3_PRIO_LEAD);
         else if (lead == 1) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
 #endif
@@ -2102,7 +2138,11 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       const uint64_t tr_mb = TR_NOW();
       TR_ADD(K3TR_NMB, 1);
 
+#ifdef K3_PF
+      put_mb256(pf, L.yin, tid);
+#else
       load_mb(Yp, Up, Vp, w, h, x, y, L.yin, tid, K3T);
+#endif
       wbar(L);
       int segid = segmap[mb];
       if (!K3CK(segid >= 0 && segid < 4, 13, segid, 4, mb)) segid = 0;
@@ -2342,6 +2382,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         }
       }
 
+#ifdef K3_PF
+      if (x + 1 < mbw) pf = fetch_mb256(Yp, Up, Vp, w, h, x + 1, y, tid);
+#endif
       // ---- tokens (token_enc.c:113-193) into this MB's slot; one (block,
       // zigzag position) item per thread, counts + scan + writes in parallel
       const int first_blk = is_i16 ? 0 : 1;
@@ -2389,9 +2432,13 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           const int item = rtid + K3T * q, k = item >> 4, n = item & 15;
           bi[q] = blk_param(k);
           last[q] = k < 25 ? L.blast[k] : -1;
+#ifndef K3_NO_CNT   // (branch-free count: 105.8 -> 105.1 ms, r5s19)
+          cnt[q] = bi[q] < 0 ? 0 : pos_count((bi[q] >> 4) & 15, n, lvi[q], lvp[q], last[q]);
+#else
           cnt[q] = bi[q] < 0 ? 0
                              : pos_tokens<false>(bi[q] & 15, (bi[q] >> 4) & 15, bi[q] >> 8, n,
                                                  lvi[q], lvp[q], last[q], nullptr, nullptr);
+#endif
         }
         int inc0 = cnt[0], inc1 = cnt[1];
 #pragma unroll

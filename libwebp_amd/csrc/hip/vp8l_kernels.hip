@@ -2675,7 +2675,11 @@ struct ClusterSmem {
 // The cluster of each tile: the cheapest under the per-symbol costs lc
 // (symbol-major, 16 x u16). Narrow tiles (counts < 2^16, sums < 2^32): every
 // pair of clusters is two dot2 steps of one cost word (v_dot2_u32_u16);
-// wider ones sum in 64 bits, 8 clusters per pass over the tile's list.
+// wider ones sum in 64 bits, 8 clusters per pass over the tile's list. The
+// tile's histogram then goes into its new cluster's (S.hc, zeroed by the
+// caller once lc was built): the next iteration's accumulation done in the
+// same pass over the lists, whose second read of the tile hits the cache
+// (one pass over every frame's tile lists per iteration instead of two).
 __device__ __forceinline__ void reassign_tiles(ClusterSmem& S, const uint32_t* __restrict__ TL,
                                                const uint32_t* __restrict__ TN, size_t cap, int nt,
                                                int K, bool narrow, int wv, int ln) {
@@ -2739,6 +2743,11 @@ __device__ __forceinline__ void reassign_tiles(ClusterSmem& S, const uint32_t* _
       }
     }
     if (ln == 0) S.assign[t] = (uint8_t)bc;
+    uint32_t* hcc = S.hc + bc * VP8L_NS;
+    for (int i = ln; i < m; i += 64) {
+      const uint32_t v = e[i];
+      if (v) atomicAdd(&hcc[v & 4095], v >> 12);
+    }
   }
 }
 
@@ -2780,25 +2789,25 @@ __global__ __launch_bounds__(1024) void k_vp8l_cluster(vp8l_params p,
   }
   __syncthreads();
 
-  for (int it = 0; it <= VP8L_CLUSTER_ITERS; ++it) {
-    // accumulate cluster histograms
-    for (int i = tid; i < K * VP8L_NS; i += 1024) S.hc[i] = 0;
-    __syncthreads();
-    for (int t = wv; t < nt; t += 16) {
-      uint32_t* hcc = S.hc + S.assign[t] * VP8L_NS;
-      const uint32_t* e = TL + (size_t)t * cap;
-      const int m = (int)TN[t];
-      for (int i0 = ln; i0 < m; i0 += 256) {   // 4 loads in flight per lane
-        uint32_t v[4];
+  // accumulate the initial clusters' histograms; every iteration then
+  // rebuilds them inside its reassignment pass
+  for (int i = tid; i < K * VP8L_NS; i += 1024) S.hc[i] = 0;
+  __syncthreads();
+  for (int t = wv; t < nt; t += 16) {
+    uint32_t* hcc = S.hc + S.assign[t] * VP8L_NS;
+    const uint32_t* e = TL + (size_t)t * cap;
+    const int m = (int)TN[t];
+    for (int i0 = ln; i0 < m; i0 += 256) {   // 4 loads in flight per lane
+      uint32_t v[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = i0 + 64 * j < m ? e[i0 + 64 * j] : 0u;
+      for (int j = 0; j < 4; ++j) v[j] = i0 + 64 * j < m ? e[i0 + 64 * j] : 0u;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (v[j]) atomicAdd(&hcc[v[j] & 4095], v[j] >> 12);
-      }
+      for (int j = 0; j < 4; ++j)
+        if (v[j]) atomicAdd(&hcc[v[j] & 4095], v[j] >> 12);
     }
-    __syncthreads();
-    if (it == VP8L_CLUSTER_ITERS) break;
+  }
+  __syncthreads();
+  for (int it = 0; it < VP8L_CLUSTER_ITERS; ++it) {
     // per-symbol costs (1/256 bit): log2((10 N + A) / (10 n + 1))
     for (int i = tid; i < K * 5; i += 1024) S.nsum[i] = 0;
     __syncthreads();
@@ -2821,7 +2830,9 @@ __global__ __launch_bounds__(1024) void k_vp8l_cluster(vp8l_params p,
       S.u.lc[i] = (uint16_t)(v >> 4);
     }
     __syncthreads();
-    // reassign: one wave per tile
+    for (int i = tid; i < K * VP8L_NS; i += 1024) S.hc[i] = 0;
+    __syncthreads();
+    // reassign (one wave per tile) + the new clusters' histograms
     reassign_tiles(S, TL, TN, cap, nt, K, narrow, wv, ln);
     __syncthreads();
   }

@@ -2106,9 +2106,16 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         {
           const int K = max_count + ep * (max_count + 1);
           const int d = __builtin_amdgcn_readfirstlane(K / mbw - y);
-#ifdef K3_EPRIO2   // (A/B) three levels above the boundary row, over the usual lead
+#if defined(K3_EPRIO2)   // (A/B) three levels above the boundary row, over the usual lead
           if (d >= 1 && d <= 3) lead = 4 - d;
           else if (d == 0) lead = 0;
+#elif defined(K3_EPRIO3)   // (A/B) both rows right above lead
+          if (d >= 1 && d <= 2) lead = 2;
+          else if (d == 3) lead = 1;
+          else if (d == 0) lead = 0;
+#elif defined(K3_EPRIO4)   // (A/B) the refresher's row also gives way to the usual lead
+          if (d >= 1 && d <= 2) lead = 3 - d;
+          else if (d == 3) lead = 0;
 #else
           if (d >= 1 && d <= 2) lead = 3 - d;
           else if (d == 3 || d == 0) lead = 0;

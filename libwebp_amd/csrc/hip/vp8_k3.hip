@@ -1451,6 +1451,9 @@ __device__ __forceinline__ void publish(int32_t* p, int32_t v) {
 // move from its slot to the compact stream while their statistics deltas
 // accumulate; counters that would cross the halving threshold inside the MB
 // are replayed token by token (VP8RecordStats, cost_enc.h:45-56).
+// RD: 64-token chunks per replay step (K3X: 16, the batch kernels: 4, where
+// deeper steps cost registers in the MB loop and the replay is ~2% anyway)
+template <int RD>
 __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t row0,
                          uint16_t* tok_base, uint32_t* mboff, const uint16_t* arena) {
   // MBs [i0, i1) of this worker's row (first MB row0): record where their
@@ -1520,6 +1523,9 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
           uint32_t p = G.stats[ss];
           const uint32_t dlt = L.rdelta[ss];
           uint32_t n = dlt >> 16, k = dlt & 0xffffu;   // the row's tokens of ss not applied yet
+          // the token ids counted in slot ss (tok_stat_slot: id, and id + 1
+          // when that is the 11th, cat-bit token of its (type, band, ctx))
+          const uint32_t alt = (ss % 11 == 9) ? (uint32_t)ss + 1u : 0xffffu;
           for (uint32_t i = i0; i < i1 && n; ++i) {
             const uint32_t nt = L.rowcnt[i - row0];
             const uint16_t* tk = arena ? arena + L.rowpos[i - row0]
@@ -1527,18 +1533,39 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
             if (arena && !K3CK((unsigned long long)L.rowpos[i - row0] + nt <= CK_CAP(L, ~0u), 11,
                                L.rowpos[i - row0], nt, i))
               break;
-            for (uint32_t k4 = 0; k4 < nt && n; k4 += 256) {
+            // RD 64-token chunks per step, all loads issued before the first
+            // ballot, and the step's count / ones of ss taken first from
+            // independent ballots: only the step holding the halving point
+            // goes chunk by chunk (K3X's row fold at q90 m6, ~750 K tokens
+            // per 4096-wide row, was 99% replay, a serial chain per chunk)
+            for (uint32_t k4 = 0; k4 < nt && n; k4 += 64 * RD) {
               if ((p >> 16) + n < 0xfffeu) break;   // no halving left in the row
-              uint32_t tq[4];
+              uint32_t tq[RD];
 #pragma unroll
-              for (int q = 0; q < 4; ++q) {
+              for (int q = 0; q < RD; ++q) {
                 const uint32_t kk = k4 + 64 * q + ln;
                 tq[q] = kk < nt ? tk[kk] : 0x4000u;
               }
+              uint32_t scnt = 0, sone = 0;
 #pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const uint32_t t = tq[q];
-                const bool mine = !(t & 0x4000) && tok_stat_slot(t) == ss;
+              for (int q = 0; q < RD; ++q) {
+                // (bit 14, the fixed-probability flag, keeps fixed tokens and
+                // the padding off ss / alt, both < 0x4000)
+                const uint32_t id = tq[q] & 0x7fffu;
+                const bool mine = id == (uint32_t)ss || id == alt;
+                scnt += (uint32_t)__popcll(__ballot(mine));
+                sone += (uint32_t)__popcll(__ballot(mine && (tq[q] >> 15)));
+              }
+              if ((p >> 16) + scnt < 0xfffeu) {   // no halving point in this step
+                p += (scnt << 16) + sone;
+                n -= scnt;
+                k -= sone;
+                continue;
+              }
+#pragma unroll
+              for (int q = 0; q < RD; ++q) {
+                const uint32_t t = tq[q], id = t & 0x7fffu;
+                const bool mine = id == (uint32_t)ss || id == alt;
                 const uint64_t mm = __ballot(mine);
                 const uint64_t ones = __ballot(mine && (t >> 15));
                 const uint32_t cnt = (uint32_t)__popcll(mm);
@@ -1608,7 +1635,7 @@ __device__ void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uin
       if (tid == 0) G.ntok = ld_sc1(&XH->ntok);
       wbar(L);
     }
-    fold_mbs(G, L, tid, i0, i1, row0, tok_base, mboff, arena);
+    fold_mbs<16>(G, L, tid, i0, i1, row0, tok_base, mboff, arena);
     wbar(L);
     for (int s = tid; s < NSLOT; s += K3T) st_sc1(xstats + s, G.stats[s]);
     if (tid == 0) st_sc1(&XH->ntok, G.ntok);
@@ -1616,7 +1643,7 @@ __device__ void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uin
     wbar(L);
     if (tid == 0) st_sc1(&XH->fold_ptr, (int32_t)i1);
   } else {
-    fold_mbs(G, L, tid, i0, i1, row0, tok_base, mboff, arena);
+    fold_mbs<4>(G, L, tid, i0, i1, row0, tok_base, mboff, arena);
   }
 }
 

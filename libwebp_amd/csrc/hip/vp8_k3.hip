@@ -1453,6 +1453,12 @@ __device__ __forceinline__ void publish(int32_t* p, int32_t v) {
 // are replayed token by token (VP8RecordStats, cost_enc.h:45-56).
 // RD: 64-token chunks per replay step (K3X: 16, the batch kernels: 4, where
 // deeper steps cost registers in the MB loop and the replay is ~2% anyway)
+#ifndef K3_RD_X
+#define K3_RD_X 8    // (config 4: 8 404 ms, 16 406, 32 518; r5s26)
+#endif
+#ifndef K3_RD_BATCH
+#define K3_RD_BATCH 8   // (batch K3: 4 99.05 ms, 8 98.4; r5s26)
+#endif
 template <int RD>
 __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t row0,
                          uint16_t* tok_base, uint32_t* mboff, const uint16_t* arena) {
@@ -1635,7 +1641,7 @@ __device__ void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uin
       if (tid == 0) G.ntok = ld_sc1(&XH->ntok);
       wbar(L);
     }
-    fold_mbs<16>(G, L, tid, i0, i1, row0, tok_base, mboff, arena);
+    fold_mbs<K3_RD_X>(G, L, tid, i0, i1, row0, tok_base, mboff, arena);
     wbar(L);
     for (int s = tid; s < NSLOT; s += K3T) st_sc1(xstats + s, G.stats[s]);
     if (tid == 0) st_sc1(&XH->ntok, G.ntok);
@@ -1643,7 +1649,7 @@ __device__ void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uin
     wbar(L);
     if (tid == 0) st_sc1(&XH->fold_ptr, (int32_t)i1);
   } else {
-    fold_mbs<4>(G, L, tid, i0, i1, row0, tok_base, mboff, arena);
+    fold_mbs<K3_RD_BATCH>(G, L, tid, i0, i1, row0, tok_base, mboff, arena);
   }
 }
 

@@ -1387,9 +1387,23 @@ static_assert(NSLOT % 4 == 0, "probabilities move as words");
 __host__ __device__ inline size_t xs_rec_off(int mbh) {
   return ((size_t)XS_ROWDONE + 4 * (size_t)mbh + 15) & ~(size_t)15;
 }
+// per row, every XS_SNAP_MBS MBs: the worker's pending statistics deltas
+// (count << 16 | ones per slot, cumulative since the row's last fold point),
+// so that a fold's replay finds the block holding a counter's halving point
+// without scanning the row's tokens up to it
+#define XS_SNAP_MBS 16
+__host__ __device__ inline int xs_snaps_per_row(int mbw) { return (mbw + XS_SNAP_MBS - 1) / XS_SNAP_MBS; }
+__host__ __device__ inline size_t xs_snap_off(int mbw, int mbh) {
+  return (xs_rec_off(mbh) + 4 * XS_REC_WORDS * (size_t)mbw * mbh + 255) & ~(size_t)255;
+}
+__device__ __forceinline__ uint32_t* xs_snap_row(uint8_t* xs, int mbw, int mbh, int y) {
+  return reinterpret_cast<uint32_t*>(xs + xs_snap_off(mbw, mbh)) +
+         (size_t)y * xs_snaps_per_row(mbw) * NSLOT;
+}
 extern "C" size_t vp8g_xsync_bytes(int w, int h) {
   const int mbw = (w + 15) >> 4, mbh = (h + 15) >> 4;
-  return (xs_rec_off(mbh) + 4 * XS_REC_WORDS * (size_t)mbw * mbh + 255) & ~(size_t)255;
+  return (xs_snap_off(mbw, mbh) + 4 * (size_t)NSLOT * xs_snaps_per_row(mbw) * mbh + 255) &
+         ~(size_t)255;
 }
 
 // LDS of one K3X workgroup beyond the K3 layout: the boundary of the row
@@ -1461,7 +1475,8 @@ __device__ __forceinline__ void publish(int32_t* p, int32_t v) {
 #endif
 template <int RD>
 __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t row0,
-                         uint16_t* tok_base, uint32_t* mboff, const uint16_t* arena) {
+                         uint16_t* tok_base, uint32_t* mboff, const uint16_t* arena,
+                         const uint32_t* snap = nullptr) {
   // MBs [i0, i1) of this worker's row (first MB row0): record where their
   // tokens go in the frame's compact stream (moved there at frame end, see
   // compact_tokens), then add their statistics in one step.
@@ -1532,7 +1547,29 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
           // the token ids counted in slot ss (tok_stat_slot: id, and id + 1
           // when that is the 11th, cat-bit token of its (type, band, ctx))
           const uint32_t alt = (ss % 11 == 9) ? (uint32_t)ss + 1u : 0xffffu;
-          for (uint32_t i = i0; i < i1 && n; ++i) {
+          uint32_t istart = i0;
+          if (snap) {
+            // the row's snapshots at MB boundaries b in (i0, i1) hold the
+            // counts since i0 (i0 is a fold point); counts only grow, so the
+            // boundaries reached before the halving point are a prefix of
+            // the lanes: their last one is added at once and the walk starts
+            // there
+            const uint32_t c0 = i0 - row0, c1 = i1 - row0;
+            const uint32_t b = (c0 / XS_SNAP_MBS + 1 + ln) * XS_SNAP_MBS;
+            const bool valid = b < c1;
+            const uint32_t v = valid ? ld_sc1(reinterpret_cast<const int32_t*>(snap) +
+                                              (size_t)(b / XS_SNAP_MBS - 1) * NSLOT + ss)
+                                     : 0u;
+            const int nok = __popcll(__ballot(valid && (p >> 16) + (v >> 16) < 0xfffeu));
+            if (nok > 0) {
+              const uint32_t vb = (uint32_t)__builtin_amdgcn_readlane((int)v, nok - 1);
+              p += vb;
+              n -= vb >> 16;
+              k -= vb & 0xffffu;
+              istart = row0 + (c0 / XS_SNAP_MBS + (uint32_t)nok) * XS_SNAP_MBS;
+            }
+          }
+          for (uint32_t i = istart; i < i1 && n; ++i) {
             const uint32_t nt = L.rowcnt[i - row0];
             const uint16_t* tk = arena ? arena + L.rowpos[i - row0]
                                        : tok_base + (size_t)i * VP8G_MAX_TOKENS_PER_MB;
@@ -1632,7 +1669,7 @@ __device__ __forceinline__ void report_rows(K3G& G, K3S& L, const vp8g_frame_par
 template <bool X>
 __device__ void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t row0,
                           uint16_t* tok_base, uint32_t* mboff, uint8_t* xs,
-                          const uint16_t* arena) {
+                          const uint16_t* arena, const uint32_t* snap = nullptr) {
   if constexpr (X) {
     XHdr* XH = reinterpret_cast<XHdr*>(xs);
     uint32_t* xstats = reinterpret_cast<uint32_t*>(xs + XS_STATS);
@@ -1641,7 +1678,10 @@ __device__ void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uin
       if (tid == 0) G.ntok = ld_sc1(&XH->ntok);
       wbar(L);
     }
-    fold_mbs<K3_RD_X>(G, L, tid, i0, i1, row0, tok_base, mboff, arena);
+#ifdef K3_NO_SNAP
+    snap = nullptr;
+#endif
+    fold_mbs<K3_RD_X>(G, L, tid, i0, i1, row0, tok_base, mboff, arena, snap);
     wbar(L);
     for (int s = tid; s < NSLOT; s += K3T) st_sc1(xstats + s, G.stats[s]);
     if (tid == 0) st_sc1(&XH->ntok, G.ntok);
@@ -1996,7 +2036,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           }
           const uint64_t tr_f = TR_NOW();
           TR_ADD(K3TR_REFR_WAIT, tr_f - tr_w);
-          fold_rows<X>(G, L, tid, fold_from, mb, (uint32_t)y * mbw, tok_base, mboff, xs, a.arena);
+          fold_rows<X>(G, L, tid, fold_from, mb, (uint32_t)y * mbw, tok_base, mboff, xs, a.arena,
+                       X ? xs_snap_row(xs, mbw, mbh, y) : nullptr);
           const uint32_t cp_from = fold_from;
           fold_from = mb;
           wbar(L);
@@ -2593,6 +2634,14 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           vm_drain();
           if (tid == 0) st_sc1(&xrowdone[y], x + 1);
         }
+#ifndef K3_NO_SNAP
+        // statistics snapshot at every XS_SNAP_MBS-th column (see fold_mbs)
+        if ((x + 1) % XS_SNAP_MBS == 0 && x + 1 < mbw) {
+          uint32_t* sr = xs_snap_row(xs, mbw, mbh, y) + (size_t)((x + 1) / XS_SNAP_MBS - 1) * NSLOT;
+          for (int s = tid; s < NSLOT; s += K3T) st_sc1(sr + s, L.rdelta[s]);
+          vm_drain();
+        }
+#endif
       }
       K3_STAMP(6);
       TR_SINCE(K3TR_MB, tr_mb);
@@ -2608,7 +2657,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     const uint64_t tr_ff = TR_NOW();
     TR_ADD(K3TR_FOLD_WAIT, tr_ff - tr_fw);
     fold_rows<X>(G, L, tid, fold_from, (uint32_t)(y + 1) * mbw, (uint32_t)y * mbw, tok_base,
-                 mboff, xs, a.arena);
+                 mboff, xs, a.arena, X ? xs_snap_row(xs, mbw, mbh, y) : nullptr);
     TR_SINCE(K3TR_FOLD, tr_ff);
     report_rows<X>(G, L, P, tid, (uint32_t)(y + 1) * mbw, mbw, XH);
     wbar(L);

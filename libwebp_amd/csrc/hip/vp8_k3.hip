@@ -1400,6 +1400,10 @@ __device__ __forceinline__ uint32_t* xs_snap_row(uint8_t* xs, int mbw, int mbh, 
   return reinterpret_cast<uint32_t*>(xs + xs_snap_off(mbw, mbh)) +
          (size_t)y * xs_snaps_per_row(mbw) * NSLOT;
 }
+extern "C" size_t vp8g_wsnap_bytes(int w, int h) {
+  (void)h;   // one row's snapshots per MB worker (at most 4 per frame)
+  return 4 * 4 * (size_t)NSLOT * xs_snaps_per_row((w + 15) >> 4);
+}
 extern "C" size_t vp8g_xsync_bytes(int w, int h) {
   const int mbw = (w + 15) >> 4, mbh = (h + 15) >> 4;
   return (xs_snap_off(mbw, mbh) + 4 * (size_t)NSLOT * xs_snaps_per_row(mbw) * mbh + 255) &
@@ -1670,6 +1674,9 @@ template <bool X>
 __device__ void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t row0,
                           uint16_t* tok_base, uint32_t* mboff, uint8_t* xs,
                           const uint16_t* arena, const uint32_t* snap = nullptr) {
+#ifdef K3_NO_SNAP
+  snap = nullptr;
+#endif
   if constexpr (X) {
     XHdr* XH = reinterpret_cast<XHdr*>(xs);
     uint32_t* xstats = reinterpret_cast<uint32_t*>(xs + XS_STATS);
@@ -1678,9 +1685,6 @@ __device__ void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uin
       if (tid == 0) G.ntok = ld_sc1(&XH->ntok);
       wbar(L);
     }
-#ifdef K3_NO_SNAP
-    snap = nullptr;
-#endif
     fold_mbs<K3_RD_X>(G, L, tid, i0, i1, row0, tok_base, mboff, arena, snap);
     wbar(L);
     for (int s = tid; s < NSLOT; s += K3T) st_sc1(xstats + s, G.stats[s]);
@@ -1689,7 +1693,7 @@ __device__ void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uin
     wbar(L);
     if (tid == 0) st_sc1(&XH->fold_ptr, (int32_t)i1);
   } else {
-    fold_mbs<K3_RD_BATCH>(G, L, tid, i0, i1, row0, tok_base, mboff, arena);
+    fold_mbs<K3_RD_BATCH>(G, L, tid, i0, i1, row0, tok_base, mboff, arena, snap);
   }
 }
 
@@ -1810,6 +1814,7 @@ struct K3Args {
   uint8_t* xs;      // K3X: n x xs_fb bytes of cross-workgroup frame state
   size_t xs_fb;
   int nwg;          // K3X: workgroups per frame
+  uint32_t* wsnap;  // K3 (not K3X: xs holds its snapshots): n x vp8g_wsnap_bytes, or NULL
   // token arena (NULL: the per-MB slot layout, compacted at frame end). Each
   // worker takes VP8G_ARENA_CHUNK-token chunks from *arena_top and writes
   // every MB's tokens once, contiguously, at the chunk's next free position
@@ -1878,6 +1883,12 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
   const int f = X ? (int)blockIdx.x / nwg : (int)blockIdx.x;
   const int blk = X ? (int)blockIdx.x % nwg : 0;
   uint8_t* xs = X ? a.xs + (size_t)f * a.xs_fb : nullptr;
+  // the statistics snapshots of row y's folds (fold_mbs): K3X per row in
+  // xsync, K3 per worker (its row is folded before it starts the next)
+  auto snap_of = [&](int y) -> uint32_t* {
+    if constexpr (X) return xs_snap_row(xs, mbw, mbh, y);
+    else return a.wsnap ? a.wsnap + ((size_t)f * 4 + wk) * xs_snaps_per_row(mbw) * NSLOT : nullptr;
+  };
   XHdr* XH = reinterpret_cast<XHdr*>(xs);
   int32_t* xrowdone = reinterpret_cast<int32_t*>(xs + XS_ROWDONE);
   uint32_t* xrec = reinterpret_cast<uint32_t*>(xs + xs_rec_off(mbh));
@@ -2037,7 +2048,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           const uint64_t tr_f = TR_NOW();
           TR_ADD(K3TR_REFR_WAIT, tr_f - tr_w);
           fold_rows<X>(G, L, tid, fold_from, mb, (uint32_t)y * mbw, tok_base, mboff, xs, a.arena,
-                       X ? xs_snap_row(xs, mbw, mbh, y) : nullptr);
+                       snap_of(y));
           const uint32_t cp_from = fold_from;
           fold_from = mb;
           wbar(L);
@@ -2634,15 +2645,18 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           vm_drain();
           if (tid == 0) st_sc1(&xrowdone[y], x + 1);
         }
+      }
 #ifndef K3_NO_SNAP
-        // statistics snapshot at every XS_SNAP_MBS-th column (see fold_mbs)
-        if ((x + 1) % XS_SNAP_MBS == 0 && x + 1 < mbw) {
-          uint32_t* sr = xs_snap_row(xs, mbw, mbh, y) + (size_t)((x + 1) / XS_SNAP_MBS - 1) * NSLOT;
+      // statistics snapshot at every XS_SNAP_MBS-th column (see fold_mbs)
+      if ((x + 1) % XS_SNAP_MBS == 0 && x + 1 < mbw) {
+        uint32_t* sr = snap_of(y);
+        if (sr) {
+          sr += (size_t)((x + 1) / XS_SNAP_MBS - 1) * NSLOT;
           for (int s = tid; s < NSLOT; s += K3T) st_sc1(sr + s, L.rdelta[s]);
           vm_drain();
         }
-#endif
       }
+#endif
       K3_STAMP(6);
       TR_SINCE(K3TR_MB, tr_mb);
     }
@@ -2657,7 +2671,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     const uint64_t tr_ff = TR_NOW();
     TR_ADD(K3TR_FOLD_WAIT, tr_ff - tr_fw);
     fold_rows<X>(G, L, tid, fold_from, (uint32_t)(y + 1) * mbw, (uint32_t)y * mbw, tok_base,
-                 mboff, xs, a.arena, X ? xs_snap_row(xs, mbw, mbh, y) : nullptr);
+                 mboff, xs, a.arena, snap_of(y));
     TR_SINCE(K3TR_FOLD, tr_ff);
     report_rows<X>(G, L, P, tid, (uint32_t)(y + 1) * mbw, mbw, XH);
     wbar(L);
@@ -3117,7 +3131,7 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
                                   uint16_t* tokens, size_t tok_cap, uint8_t* mbinfo,
                                   uint32_t* mboff, int trellis, vp8g_frame_result* results,
                                   uint8_t* rerun_state, uint8_t* recon, uint8_t* xsync,
-                                  const vp8g_arena* arena, void* stream) {
+                                  uint32_t* wsnap, const vp8g_arena* arena, void* stream) {
 #ifdef WEBP_AMD_DIAG
   // diagnostic build only (make diag -> libwebp_amd_diag.so; the product
   // library has no switch): WEBP_AMD_K3 = 1 single-wavefront twin,
@@ -3148,6 +3162,7 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   a.segmap = segmap; a.params = params; a.tokens = tokens; a.tok_cap = tok_cap;
   a.mbinfo = mbinfo; a.mboff = mboff; a.results = results; a.rerun = rerun_state;
   a.xs = xsync; a.xs_fb = vp8g_xsync_bytes(w, h); a.nwg = 1;
+  a.wsnap = wsnap;
   a.arena = nullptr; a.arena_cap = 0; a.arena_top = nullptr; a.mbpos = nullptr;
   if (arena) {   // one arena per launch: the bump pointer starts at 0
     a.arena = arena->tokens;

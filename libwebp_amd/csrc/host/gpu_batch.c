@@ -168,6 +168,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   CHK(hipMalloc((void**)&b->d_rerun, N * VP8G_RERUN_STATE_BYTES));
   if (N <= VP8G_XSPLIT_MAX_FRAMES)   /* few frames: K3 splits each over several CUs */
     CHK(hipMalloc((void**)&b->d_xsync, N * vp8g_xsync_bytes(width, height)));
+  CHK(hipMalloc((void**)&b->d_wsnap, N * vp8g_wsnap_bytes(width, height)));
   CHK(hipMalloc((void**)&b->d_results, N * sizeof(vp8g_frame_result)));
   /* K4 streams: one per token partition; the WebPEncode pool changes the
    * config of an engine between calls, so room for the most partitions */
@@ -218,7 +219,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipFree(b->d_g2l); hipFree(b->d_rgba); hipFree(b->d_yuv); hipFree(b->d_aflags); hipFree(b->d_alpha);
   hipFree(b->d_uva); hipFree(b->d_amode); hipFree(b->d_segmap); hipFree(b->d_params); hipFree(b->d_tokens);
   hipFree(b->d_arena); hipFree(b->d_arena_top); hipFree(b->d_mbpos); hipFree(b->d_rerun_snap);
-  hipFree(b->d_mbinfo); hipFree(b->d_mboff); hipFree(b->d_rerun); hipFree(b->d_xsync); hipFree(b->d_results); hipFree(b->d_psize); hipFree(b->d_emeta);
+  hipFree(b->d_mbinfo); hipFree(b->d_mboff); hipFree(b->d_rerun); hipFree(b->d_xsync); hipFree(b->d_wsnap); hipFree(b->d_results); hipFree(b->d_psize); hipFree(b->d_emeta);
   hipFree(b->d_poff); hipFree(b->d_part); hipFree(b->d_pinfo);
   hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs); hipFree(b->d_nbuf);
   hipFree(b->d_eimg);
@@ -547,7 +548,7 @@ static int launch_k3(WebPGpuBatch* b, int n, uint8_t* recon) {
      outgrew tok_cap (k3_settle) */
   if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
                           b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5, b->d_results,
-                          b->d_rerun, recon, b->d_xsync, ap, st))
+                          b->d_rerun, recon, b->d_xsync, b->d_wsnap, ap, st))
     return 0;
   return 1;
 fail:
@@ -677,7 +678,7 @@ static int lowmem_passes(WebPGpuBatch* b, int n) {
     first = 0;
     if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params,
                             b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5,
-                            b->d_results, b->d_rerun, NULL, b->d_xsync, NULL, st))
+                            b->d_results, b->d_rerun, NULL, b->d_xsync, b->d_wsnap, NULL, st))
       return 0;
     if (!vp8g_launch_lowmem(b->d_tokens, b->tok_cap, b->d_mboff, b->d_results, b->d_mbinfo,
                             (int)nmb, n, b->d_lmi, b->d_active, 0, b->d_lmstats, b->d_lmi + N, st))
@@ -743,7 +744,7 @@ static int lowmem_passes(WebPGpuBatch* b, int n) {
                      hipMemcpyHostToDevice, st));
   if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
                           b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5, b->d_results,
-                          b->d_rerun, b->cfg.autofilter ? b->d_recon : NULL, b->d_xsync, NULL, st))
+                          b->d_rerun, b->cfg.autofilter ? b->d_recon : NULL, b->d_xsync, b->d_wsnap, NULL, st))
     return 0;
   CHK(hipEventRecord(b->ev[3], st));
   CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
@@ -848,7 +849,7 @@ static int statloop_search(WebPGpuBatch* b, int n) {
     /* RD_OPT_BASIC: the instantiation without trellis paths (it sums R + H) */
     if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params,
                             b->d_tokens, b->tok_cap, b->d_mbinfo, b->d_mboff, 0,
-                            b->d_results, b->d_rerun, NULL, b->d_xsync, NULL, st))
+                            b->d_results, b->d_rerun, NULL, b->d_xsync, b->d_wsnap, NULL, st))
       return 0;
     if (!vp8g_launch_lowmem(b->d_tokens, b->tok_cap, b->d_mboff, b->d_results, b->d_mbinfo,
                             (int)nmb, n, b->d_lmi, b->d_active, 0, b->d_lmstats, b->d_lmi + N, st))
@@ -956,7 +957,7 @@ static int statloop_search(WebPGpuBatch* b, int n) {
   }
   if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
                           b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5, b->d_results,
-                          b->d_rerun, b->cfg.autofilter ? b->d_recon : NULL, b->d_xsync, NULL, st))
+                          b->d_rerun, b->cfg.autofilter ? b->d_recon : NULL, b->d_xsync, b->d_wsnap, NULL, st))
     return 0;
   CHK(hipEventRecord(b->ev[3], st));
   CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),

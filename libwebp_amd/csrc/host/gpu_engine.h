@@ -86,6 +86,7 @@ struct WebPGpuBatch {
   uint32_t* d_mboff;         /* K3 scratch: compact-stream offset per MB */
   uint8_t* d_rerun;          /* K3 cost state carried from pass to pass */
   uint8_t* d_xsync;          /* K3X cross-workgroup frame state (max_frames <= 64) */
+  uint32_t* d_wsnap;         /* K3 row-fold statistics snapshots (vp8g_wsnap_bytes) */
   /* size search between passes (allocated on first use) */
   uint8_t* h_state;          /* pinned copy of d_rerun */
   uint8_t* d_active;         /* frames whose token bits are estimated */

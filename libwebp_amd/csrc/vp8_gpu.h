@@ -165,7 +165,8 @@ int vp8g_launch_encode(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h,
                        const vp8g_frame_params* params, uint16_t* tokens,
                        size_t tok_cap, uint8_t* mbinfo, uint32_t* mboff, int trellis,
                        vp8g_frame_result* results, uint8_t* rerun_state, uint8_t* recon,
-                       uint8_t* xsync, const vp8g_arena* arena, void* stream);
+                       uint8_t* xsync, uint32_t* wsnap, const vp8g_arena* arena,
+                       void* stream);
 
 /* With an arena, K3 writes every MB's tokens once into the arena and the
  * frames' compact streams are laid out by this gather (frame f at tokens +
@@ -184,6 +185,11 @@ int vp8g_launch_gather(uint16_t* tokens, size_t tok_cap, const uint16_t* arena,
  * launch). */
 #define VP8G_XSPLIT_MAX_FRAMES 64
 size_t vp8g_xsync_bytes(int w, int h);
+/* wsnap (NULL: none): n x vp8g_wsnap_bytes(w, h), the statistics snapshots
+ * of K3's row folds (each MB worker's pending deltas every 16 MBs of its row,
+ * so the exact replay of a counter's halving starts near it); written before
+ * they are read, no reset needed */
+size_t vp8g_wsnap_bytes(int w, int h);
 
 /* Autofilter (config->autofilter, filter_enc.c:156-212): per frame the
  * segment filter levels and the filter header fields used for the search */

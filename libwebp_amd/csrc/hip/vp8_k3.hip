@@ -30,7 +30,9 @@
 // a cross-worker wait that has not been satisfied after this long (100 MHz
 // s_memrealtime ticks, 30 s) is a bug: the frame is aborted with an error
 // instead of hanging the GPU
+#ifndef K3_WAIT_TICKS
 #define K3_WAIT_TICKS (30ull * 100000000ull)
+#endif
 
 // LDS shared by all of a frame's workers: cost tables of the current epoch,
 // token statistics, quantiser/segment parameters and frame-level counters.
@@ -225,6 +227,48 @@ __device__ __forceinline__ void wbar(K3S& L) {
     while (ld_uni(&L.bar) < target) __builtin_amdgcn_s_sleep(K3_WBAR_SLEEP);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
+#ifdef K3_BARCHECK
+// diagnostic build (-DK3_CHECK -DK3_BARCHECK): a worker barrier that has not
+// completed after K3_BAR_TICKS records, per workgroup / worker / wave, the
+// source line of the barrier, the counter before the arrival, the target and
+// the counter seen, the worker's MB; then the worker gives up (its barriers
+// release, its row loop ends) so the launch drains and the records come back
+#ifndef K3_BAR_TICKS
+#define K3_BAR_TICKS (5ull * 100000000ull)
+#endif
+__device__ uint32_t g_k3bar[1024][4][4][8];
+__device__ __noinline__ void wbar_late(K3S& L, uint32_t old, uint32_t target, int line) {
+  const uint32_t lane = threadIdx.x & 63, wv = (threadIdx.x >> 6) & 3, wk = (threadIdx.x >> 8) & 3;
+  const uint32_t seen = ld_uni(&L.bar);
+  uint32_t v = 0x80000000u;
+  v = lane == 0 ? (uint32_t)line : v;
+  v = lane == 1 ? old : v;
+  v = lane == 2 ? target : v;
+  v = lane == 3 ? seen : v;
+  v = lane == 4 ? (uint32_t)L.ck_y : v;
+  v = lane == 5 ? (uint32_t)L.ck_x : v;
+  v = lane == 6 ? 0u : v;
+  if (blockIdx.x < 1024 && lane < 8) g_k3bar[blockIdx.x][wk][wv][lane] = v;
+  L.myabort = 1;
+  atomicOr(&L.bar, WBAR_RELEASE);
+}
+__device__ __forceinline__ void wbar_at(K3S& L, int line) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  const uint32_t old = lane0_add(&L.bar, 1u);
+  const uint32_t target = (old & ~3u) + 4u;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  if ((old & 3u) != 3u)
+    while (ld_uni(&L.bar) < target) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > K3_BAR_TICKS) {
+        wbar_late(L, old, target, line);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(K3_WBAR_SLEEP);
+    }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+#define wbar(L) wbar_at(L, __LINE__)
+#endif
 #define WB() wbar(L)
 
 // all-threads AND over the worker
@@ -1263,6 +1307,7 @@ enum {
 };
 #ifdef K3_TRACE
 #define K3TR_MAXB 1024
+static_assert(K3TR_N == 16, "L.trace[16]");
 __device__ unsigned long long g_k3trace[K3TR_MAXB][4][K3TR_N];
 #define TR_NOW() __builtin_amdgcn_s_memtime()
 // (the worker's first wave adds, every lane the same value: a wave-uniform
@@ -1391,7 +1436,9 @@ __host__ __device__ inline size_t xs_rec_off(int mbh) {
 // (count << 16 | ones per slot, cumulative since the row's last fold point),
 // so that a fold's replay finds the block holding a counter's halving point
 // without scanning the row's tokens up to it
+#ifndef XS_SNAP_MBS
 #define XS_SNAP_MBS 16
+#endif
 __host__ __device__ inline int xs_snaps_per_row(int mbw) { return (mbw + XS_SNAP_MBS - 1) / XS_SNAP_MBS; }
 __host__ __device__ inline size_t xs_snap_off(int mbw, int mbh) {
   return (xs_rec_off(mbh) + 4 * XS_REC_WORDS * (size_t)mbw * mbh + 255) & ~(size_t)255;
@@ -1477,8 +1524,13 @@ __device__ __forceinline__ void publish(int32_t* p, int32_t v) {
 #ifndef K3_RD_BATCH
 #define K3_RD_BATCH 8   // (batch K3: 4 99.05 ms, 8 98.4; r5s26)
 #endif
+#ifdef K3_FOLD_INLINE
+#define K3_FOLD_ATTR __device__ __forceinline__
+#else
+#define K3_FOLD_ATTR __device__
+#endif
 template <int RD>
-__device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t row0,
+K3_FOLD_ATTR void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t row0,
                          uint16_t* tok_base, uint32_t* mboff, const uint16_t* arena,
                          const uint32_t* snap = nullptr) {
   // MBs [i0, i1) of this worker's row (first MB row0): record where their
@@ -1524,10 +1576,10 @@ __device__ void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint
   if (L.mark_any) {
 #ifdef K3_TRACE
     const uint64_t tr_rp = TR_NOW();
-    if (tid == 0) {
+    {   // (every lane counts: no lane-masked region in the trace build)
       int nm = 0;
       for (int wd = 0; wd < 33; ++wd) nm += __popc(G.mark[wd]);
-      L.trace[K3TR_NREPLAY] += nm;
+      TR_ADD(K3TR_NREPLAY, nm);
     }
 #endif
     // exact in-order replay of each marked counter by one wave: its tokens only
@@ -1991,7 +2043,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
   uint8_t* ul = L.ul_mem + 1;
   uint8_t* vl = L.vl_mem + 1;
 #ifdef K3_TRACE
-  if (tid < K3TR_N) L.trace[tid] = 0;
+  if (__builtin_amdgcn_readfirstlane(tid) < 64) L.trace[tid & (K3TR_N - 1)] = 0;
   const uint64_t tr_start = TR_NOW();
 #endif
 
@@ -2172,9 +2224,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       } else if (y > 0) {
 #ifdef K3_TRACE
         const uint64_t tr_w = TR_NOW();
-        if (__hip_atomic_load(&rowdone[y - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
-            min(x + 2, mbw))
-          TR_ADD(K3TR_NROWWAIT, 1);
+        TR_ADD(K3TR_NROWWAIT, ld_uni(&rowdone[y - 1]) < min(x + 2, mbw) ? 1 : 0);
 #endif
         if (!wait_ge(G, L, &rowdone[y - 1], min(x + 2, mbw), 3)) break;
         TR_SINCE(K3TR_ROW_WAIT, tr_w);
@@ -3013,6 +3063,12 @@ extern "C" __attribute__((visibility("default"))) int vp8g_k3_check(unsigned lon
   return hipMemcpyToSymbol(HIP_SYMBOL(g_k3check), z, sizeof(z), 0, hipMemcpyHostToDevice) ==
          hipSuccess;
 }
+#ifdef K3_BARCHECK
+extern "C" __attribute__((visibility("default"))) int vp8g_k3_bar(uint32_t* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k3bar), sizeof(g_k3bar), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess;
+}
+#endif
 // check build: the hang records [1024][4][8] (see g_k3hang), then cleared
 extern "C" __attribute__((visibility("default"))) int vp8g_k3_hang(uint32_t* out) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k3hang), sizeof(g_k3hang), 0,

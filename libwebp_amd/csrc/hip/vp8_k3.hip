@@ -273,10 +273,13 @@ __device__ __forceinline__ void wbar_at(K3S& L, int line) {
 
 // all-threads AND over the worker
 __device__ __forceinline__ int wbar_and(K3S& L, int v) {
+  // wave-uniform throughout: every lane stores its wave's vote (same value,
+  // same word: no lane mask), the result goes through readfirstlane, so a
+  // branch on it is a scalar branch
   const int all = __all(v);
-  if ((threadIdx.x & 63) == 0) L.redw[(threadIdx.x >> 6) & 3] = all;
+  L.redw[(__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6) & 3] = all;
   wbar(L);
-  return L.redw[0] & L.redw[1] & L.redw[2] & L.redw[3];
+  return __builtin_amdgcn_readfirstlane(L.redw[0] & L.redw[1] & L.redw[2] & L.redw[3]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1436,9 +1439,13 @@ __host__ __device__ inline size_t xs_rec_off(int mbh) {
 // (count << 16 | ones per slot, cumulative since the row's last fold point),
 // so that a fold's replay finds the block holding a counter's halving point
 // without scanning the row's tokens up to it
+#ifndef K3_DFULL   // (a test build lowers it so that the early folds run)
+#define K3_DFULL 0xe000u
+#endif
 #ifndef XS_SNAP_MBS
 #define XS_SNAP_MBS 16
 #endif
+static_assert(K3_DFULL + XS_SNAP_MBS * 288 < 0x10000u, "pending deltas stay 16-bit");
 __host__ __device__ inline int xs_snaps_per_row(int mbw) { return (mbw + XS_SNAP_MBS - 1) / XS_SNAP_MBS; }
 __host__ __device__ inline size_t xs_snap_off(int mbw, int mbh) {
   return (xs_rec_off(mbh) + 4 * XS_REC_WORDS * (size_t)mbw * mbh + 255) & ~(size_t)255;
@@ -2696,17 +2703,47 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           if (tid == 0) st_sc1(&xrowdone[y], x + 1);
         }
       }
-#ifndef K3_NO_SNAP
-      // statistics snapshot at every XS_SNAP_MBS-th column (see fold_mbs)
       if ((x + 1) % XS_SNAP_MBS == 0 && x + 1 < mbw) {
+        // every XS_SNAP_MBS-th column: the statistics snapshot (see fold_mbs),
+        // and the 16-bit count / ones of the row's pending deltas checked: an
+        // MB adds at most 288 to one slot (9 positions of a band, 2 counted
+        // tokens each, 16 blocks), so a pending field past K3_DFULL folds the
+        // row's MBs so far now, long before it could wrap (a very wide,
+        // noisy picture at high quality)
         uint32_t* sr = snap_of(y);
-        if (sr) {
-          sr += (size_t)((x + 1) / XS_SNAP_MBS - 1) * NSLOT;
-          for (int s = tid; s < NSLOT; s += K3T) st_sc1(sr + s, L.rdelta[s]);
-          vm_drain();
+#ifdef K3_NO_SNAP
+        sr = nullptr;
+#endif
+        if (sr) sr += (size_t)((x + 1) / XS_SNAP_MBS - 1) * NSLOT;
+        uint32_t big = 0;
+        for (int s = tid; s < NSLOT; s += K3T) {
+          const uint32_t d = L.rdelta[s];
+          if (sr) st_sc1(sr + s, d);
+          big |= (uint32_t)((d >> 16) >= K3_DFULL) | (uint32_t)((d & 0xffffu) >= K3_DFULL);
+        }
+        if (sr) vm_drain();
+#ifdef K3_NO_DFULL   // (A/B) without the check
+        big = 0;
+        if (false) {
+#else
+        if (!wbar_and(L, big == 0)) {   // (a wave-uniform result: a scalar branch)
+#endif
+          const uint32_t mb1 = mb + 1;
+          if constexpr (X) {
+            if (!wait_gx(G, L, &XH->fold_ptr, (int32_t)fold_from, XH)) break;
+          } else {
+            if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from, 4)) break;
+          }
+          fold_rows<X>(G, L, tid, fold_from, mb1, (uint32_t)y * mbw, tok_base, mboff, xs,
+                       a.arena, snap_of(y));
+          const uint32_t cp_from = fold_from;
+          fold_from = mb1;
+          wbar(L);
+          if (a.arena)
+            copy_folded(L, tid, cp_from, mb1, (uint32_t)y * mbw, L.fold_base, tok_base, a.tok_cap,
+                        a.arena);
         }
       }
-#endif
       K3_STAMP(6);
       TR_SINCE(K3TR_MB, tr_mb);
     }

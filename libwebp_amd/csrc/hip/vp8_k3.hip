@@ -1440,12 +1440,16 @@ __host__ __device__ inline size_t xs_rec_off(int mbh) {
 // so that a fold's replay finds the block holding a counter's halving point
 // without scanning the row's tokens up to it
 #ifndef K3_DFULL   // (a test build lowers it so that the early folds run)
-#define K3_DFULL 0xe000u
+#define K3_DFULL 0xc000u
+#endif
+#ifndef K3_DFULL_EVERY   // columns between two checks (a multiple of XS_SNAP_MBS)
+#define K3_DFULL_EVERY 32
 #endif
 #ifndef XS_SNAP_MBS
 #define XS_SNAP_MBS 16
 #endif
-static_assert(K3_DFULL + XS_SNAP_MBS * 288 < 0x10000u, "pending deltas stay 16-bit");
+static_assert(K3_DFULL + K3_DFULL_EVERY * 288 < 0x10000u, "pending deltas stay 16-bit");
+static_assert(K3_DFULL_EVERY % XS_SNAP_MBS == 0, "checked at snapshot columns");
 __host__ __device__ inline int xs_snaps_per_row(int mbw) { return (mbw + XS_SNAP_MBS - 1) / XS_SNAP_MBS; }
 __host__ __device__ inline size_t xs_snap_off(int mbw, int mbh) {
   return (xs_rec_off(mbh) + 4 * XS_REC_WORDS * (size_t)mbw * mbh + 255) & ~(size_t)255;
@@ -2704,12 +2708,12 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         }
       }
       if ((x + 1) % XS_SNAP_MBS == 0 && x + 1 < mbw) {
-        // every XS_SNAP_MBS-th column: the statistics snapshot (see fold_mbs),
-        // and the 16-bit count / ones of the row's pending deltas checked: an
-        // MB adds at most 288 to one slot (9 positions of a band, 2 counted
-        // tokens each, 16 blocks), so a pending field past K3_DFULL folds the
-        // row's MBs so far now, long before it could wrap (a very wide,
-        // noisy picture at high quality)
+        // every XS_SNAP_MBS-th column: the statistics snapshot (see fold_mbs);
+        // every K3_DFULL_EVERY-th the 16-bit count / ones of the row's pending
+        // deltas checked: an MB adds at most 288 to one slot (9 positions of a
+        // band, 2 counted tokens each, 16 blocks), so a pending field past
+        // K3_DFULL folds the row's MBs so far now, before it could wrap (a
+        // very wide, noisy picture at high quality)
         uint32_t* sr = snap_of(y);
 #ifdef K3_NO_SNAP
         sr = nullptr;
@@ -2726,7 +2730,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         big = 0;
         if (false) {
 #else
-        if (!wbar_and(L, big == 0)) {   // (a wave-uniform result: a scalar branch)
+        if ((x + 1) % K3_DFULL_EVERY == 0 &&
+            !wbar_and(L, big == 0)) {   // (a wave-uniform result: a scalar branch)
 #endif
           const uint32_t mb1 = mb + 1;
           if constexpr (X) {

@@ -710,7 +710,7 @@ def lossy_line(args, world, B, W, H, elapsed, tails, total_bytes, ntok, solo=Non
                                          "the other instance's kernels beside it); "
                                          "k_encode_solo_ms: one step on one instance alone, "
                                          "the time `achieved` uses (≈ rocprof's average, "
-                                         "profiles/r5/final/kernel_stats_solo_r5fe.csv: 97.13 ms)",
+                                         "profiles/r5/final/kernel_stats_solo_r5fg.csv: 96.74 ms)",
                      "algorithmic_bytes_per_launch": k3_bytes,
                      # the roof that binds K3: vector issue
                      "issue": issue},

@@ -9,7 +9,9 @@
 // E_i the number of renormalisation shifts from token i (inclusive) to the
 // end of the stream including the finishing pad bits, and S the total shift
 // count. (Checked against the reference coder; tests/test_emit_model.py.)
-// So a frame's tokens are cut into segments and:
+// So a stream's tokens are cut into segments (k_emit_desc: every
+// EMIT_SEG tokens of a compact stream, or of each of K3's token rows, where
+// the tokens were written once; a segment never crosses a row) and:
 //   (tokens are resolved to (bit, probability) under the frame's final
 //   probabilities by each kernel below as it stages them in LDS)
 //   E1 k_emit_img      per segment, the few ranges it can start with (the end
@@ -92,6 +94,7 @@ __global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ to
                                                  size_t tok_cap,
                                                  const vp8g_frame_result* __restrict__ results,
                                                  const vp8g_emit_meta* __restrict__ meta,
+                                                 const vp8g_emit_desc* __restrict__ desc,
                                                  uint8_t* __restrict__ img) {
   __shared__ __align__(16) uint16_t tk[IMG_G * IMG_ROW];
   __shared__ __align__(4) uint8_t prob[VP8G_NUM_SLOTS];
@@ -101,7 +104,7 @@ __global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ to
   const vp8g_emit_meta M = meta[f];
   const uint32_t sbase = blockIdx.x * IMG_G;
   if (sbase >= M.nseg) return;   // whole wave
-  const uint16_t* ftok = tokens + M.tok_off;
+  const vp8g_emit_desc* D = desc + M.seg_base;
   load_probas(prob, results, M, lane, 64);
   __syncthreads();
 #pragma unroll
@@ -109,9 +112,23 @@ __global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ to
     const int q = lane + 64 * t, sg = q / (EMIT_IMG / 8), part = q % (EMIT_IMG / 8);
     const uint32_t s = sbase + sg;
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (s > 0 && s < M.nseg)
-      v = resolve_quad(
-          *reinterpret_cast<const uint4*>(ftok + (size_t)s * EMIT_SEG - EMIT_IMG + 8 * part), prob);
+    if (s > 0 && s < M.nseg) {
+      // the previous segment's last EMIT_IMG tokens; it ends at its row's end
+      // (any token) when it is a row's last segment: then 8 single loads
+      const vp8g_emit_desc pd = D[s - 1];
+      if (pd.len >= EMIT_IMG) {
+        const uint64_t b = pd.off + pd.len - EMIT_IMG + 8 * part;
+        uint4 raw;
+        if ((b & 7) == 0) {
+          raw = *reinterpret_cast<const uint4*>(tokens + b);
+        } else {
+          const uint16_t* pt = tokens + b;
+          raw = make_uint4(pt[0] | ((uint32_t)pt[1] << 16), pt[2] | ((uint32_t)pt[3] << 16),
+                           pt[4] | ((uint32_t)pt[5] << 16), pt[6] | ((uint32_t)pt[7] << 16));
+        }
+        v = resolve_quad(raw, prob);
+      }
+    }
     *reinterpret_cast<uint4*>(&tk[sg * IMG_ROW + 8 * part]) = v;
   }
   // this lane's piece of the maps: segment mg, word mw
@@ -170,6 +187,10 @@ __global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ to
     if (mw == 0) { out[0] = 1; out[1] = 254; }
     return;
   }
+  if (D[ms - 1].len < EMIT_IMG) {   // after a row's short last segment: all 128 ranges
+    if (mw == 0) out[0] = 0xff;
+    return;
+  }
   if (cnt > EMIT_SLOTS) {   // too many: the map kernel covers all 128 ranges
     if (mw == 0) out[0] = 0xff;
     return;
@@ -196,11 +217,13 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
                                                   size_t tok_cap,
                                                   const vp8g_frame_result* __restrict__ results,
                                                   const vp8g_emit_meta* __restrict__ meta,
+                                                  const vp8g_emit_desc* __restrict__ desc,
                                                   const uint8_t* __restrict__ img,
                                                   uint8_t* __restrict__ emap,
                                                   uint16_t* __restrict__ eshift) {
   __shared__ __align__(16) uint16_t stage[MAP_G * MAP_ROW];
   __shared__ __align__(4) uint8_t prob[VP8G_NUM_SLOTS];
+  __shared__ vp8g_emit_desc ld[MAP_G];
   const int f = blockIdx.y, lane = threadIdx.x;
   const vp8g_emit_meta M = meta[f];
   const uint32_t sbase = blockIdx.x * MAP_G;
@@ -217,16 +240,17 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
     if (lane >= o) incl += v;
   }
   const int total = __shfl(incl, MAP_G - 1);
-  const uint16_t* ftok = tokens + M.tok_off;
+  if (lane < MAP_G && sbase + lane < M.nseg) ld[lane] = desc[M.seg_base + sbase + lane];
   load_probas(prob, results, M, lane, 64);
   __syncthreads();
   auto load = [&](uint32_t c0, uint4* v) {
 #pragma unroll
     for (int t = 0; t < MAP_PIECES; ++t) {
       const int q = lane + 64 * t, sg = q / (MAP_CH / 8), part = q % (MAP_CH / 8);
-      const uint32_t i = (sbase + sg) * EMIT_SEG + c0 + 8 * part;
+      const uint32_t i = c0 + 8 * part;
       v[t] = make_uint4(0, 0, 0, 0);
-      if (sbase + sg < M.nseg && i < M.ntok) v[t] = *reinterpret_cast<const uint4*>(ftok + i);
+      if (sbase + sg < M.nseg && i < ld[sg].len)
+        v[t] = *reinterpret_cast<const uint4*>(tokens + ld[sg].off + i);
     }
   };
   for (int p0 = 0; p0 < total; p0 += 64) {
@@ -242,7 +266,7 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
     const uint8_t* im = img + ((size_t)M.seg_base + s) * (EMIT_SLOTS + 1);
     const int k = p - excl;
     const int r0 = !live ? 127 : im[0] == 0xff ? 127 + k : im[1 + k];
-    const uint32_t cnt = live ? min((uint32_t)EMIT_SEG, M.ntok - s * EMIT_SEG) : 0u;
+    const uint32_t cnt = live ? ld[g].len : 0u;
     const uint16_t* st = stage + (live ? g : 0) * MAP_ROW;
     int r = r0;
     uint32_t S = 0;
@@ -266,7 +290,7 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
           for (int kk = 0; kk < 8; ++kk) S += chain_step(r, (w[kk >> 1] >> (16 * (kk & 1))) & 0xffff);
         }
       } else {
-        for (uint32_t i = 0; i < n; ++i) S += chain_step(r, st[i]);   // frame's last segment
+        for (uint32_t i = 0; i < n; ++i) S += chain_step(r, st[i]);   // a row's / stream's last segment
       }
     }
     if (live) {
@@ -348,15 +372,15 @@ __global__ __launch_bounds__(64) void k_emit_compose(vp8g_emit_meta* __restrict_
 
 // a chunk of 64 segments x SEG_CH tokens in two steps: global -> registers (issued early, so the
 // loads fly while the previous chunk is processed), registers -> LDS
-__device__ __forceinline__ void seg_chunk_fetch(uint4 v[8], const uint16_t* base, uint32_t s0,
-                                                uint32_t nseg, uint32_t ntok, uint32_t c0,
-                                                int lane) {
+__device__ __forceinline__ void seg_chunk_fetch(uint4 v[8], const uint16_t* tokens,
+                                                const vp8g_emit_desc* ld, uint32_t s0,
+                                                uint32_t nseg, uint32_t c0, int lane) {
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
     const int q = lane + 64 * t, sg = q >> 3, part = q & 7;
-    const uint32_t i = (s0 + sg) * EMIT_SEG + c0 + 8 * part;
+    const uint32_t i = c0 + 8 * part;
     v[t] = make_uint4(0, 0, 0, 0);
-    if (s0 + sg < nseg && i < ntok) v[t] = *reinterpret_cast<const uint4*>(base + i);
+    if (s0 + sg < nseg && i < ld[sg].len) v[t] = *reinterpret_cast<const uint4*>(tokens + ld[sg].off + i);
   }
 }
 __device__ __forceinline__ void seg_chunk_put(uint32_t* lds, const uint4 v[8], int lane) {
@@ -427,9 +451,11 @@ __device__ __forceinline__ void seg_unstage(seg_sink& o, const uint32_t* stg, in
 __global__ __launch_bounds__(64) void k_emit_seg(const uint16_t* __restrict__ tokens, size_t tok_cap,
                                                  const vp8g_frame_result* __restrict__ results,
                                                  const vp8g_emit_meta* __restrict__ meta,
+                                                 const vp8g_emit_desc* __restrict__ desc,
                                                  vp8g_emit_seg* __restrict__ segs,
                                                  uint32_t* __restrict__ nbuf) {
   __shared__ uint32_t lds[64 * SEG_ROW];
+  __shared__ vp8g_emit_desc ld[64];
   __shared__ uint32_t stg[SEG_STG * 64];
   __shared__ __align__(4) uint8_t prob[VP8G_NUM_SLOTS];
   const int f = blockIdx.y, lane = threadIdx.x;
@@ -438,15 +464,14 @@ __global__ __launch_bounds__(64) void k_emit_seg(const uint16_t* __restrict__ to
   if (s0 >= M.nseg) return;   // whole wave
   const bool valid = s < M.nseg;
   const vp8g_emit_seg g = valid ? segs[M.seg_base + s] : vp8g_emit_seg{0, 0, 254, 0};
-  const uint32_t i0 = s * EMIT_SEG;
-  const uint32_t cnt = valid ? min((uint32_t)EMIT_SEG, M.ntok - i0) : 0u;
-  const uint16_t* base = tokens + M.tok_off;
+  const vp8g_emit_desc dd = valid ? desc[M.seg_base + s] : vp8g_emit_desc{0, 0, 0};
+  ld[lane] = dd;
+  const uint32_t cnt = dd.len;
   const uint32_t* row = lds + lane * SEG_ROW;
   // the chunks this wave needs: up to its longest segment
-  const uint32_t last_s = min(s0 + 64, M.nseg) - 1;
-  const uint32_t span = min((uint32_t)EMIT_SEG, M.ntok - last_s * EMIT_SEG) == EMIT_SEG || last_s > s0
-                            ? (uint32_t)EMIT_SEG
-                            : M.ntok - last_s * EMIT_SEG;
+  uint32_t span = cnt;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) span = max(span, (uint32_t)__shfl_xor((int)span, o));
   seg_sink o{nbuf + M.nb_base, (int)g.T, (int)(g.T + g.S), 0u, 0u};
   int p = o.top;                 // the bit the next c lands on
   int B = (o.top - 7) & ~31;     // window [B, B + 64); top - B in [7, 38]
@@ -455,11 +480,12 @@ __global__ __launch_bounds__(64) void k_emit_seg(const uint16_t* __restrict__ to
   load_probas(prob, results, M, lane, 64);
   int r = g.rs;
   uint4 nv[8];
-  seg_chunk_fetch(nv, base, s0, M.nseg, M.ntok, 0, lane);
+  __syncthreads();   // the wave's descriptors in LDS
+  seg_chunk_fetch(nv, tokens, ld, s0, M.nseg, 0, lane);
   for (uint32_t c0 = 0; c0 < span; c0 += SEG_CH) {
     seg_chunk_put(lds, nv, lane);
     __syncthreads();
-    if (c0 + SEG_CH < span) seg_chunk_fetch(nv, base, s0, M.nseg, M.ntok, c0 + SEG_CH, lane);
+    if (c0 + SEG_CH < span) seg_chunk_fetch(nv, tokens, ld, s0, M.nseg, c0 + SEG_CH, lane);
 #pragma unroll 2
     for (int k = 0; k < SEG_CH / 2; ++k) {
       const uint32_t w = resolve_pair(row[k], prob);
@@ -548,24 +574,77 @@ __global__ __launch_bounds__(256) void k_emit_bytes(uint16_t* __restrict__ token
   }
 }
 
+// E0: the segments. A compact stream is cut every EMIT_SEG tokens; a row
+// stream (K3's token rows: the tokens stay where K3 wrote them) every
+// EMIT_SEG tokens of each row, so a segment never crosses a row and every
+// segment starts at a multiple of 8 tokens. One workgroup per stream; a row
+// stream's exact segment count replaces the host's bound in its meta.
+#define DESC_T 256
+__global__ __launch_bounds__(DESC_T) void k_emit_desc(vp8g_emit_meta* __restrict__ meta,
+                                                      const uint32_t* __restrict__ rowtok,
+                                                      vp8g_emit_desc* __restrict__ desc) {
+  const int st = blockIdx.x, t = threadIdx.x;
+  const vp8g_emit_meta M = meta[st];
+  vp8g_emit_desc* D = desc + M.seg_base;
+  if (M.nrows == 0) {
+    const uint32_t nseg = (M.ntok + EMIT_SEG - 1) / EMIT_SEG;
+    for (uint32_t s = t; s < nseg; s += DESC_T)
+      D[s] = vp8g_emit_desc{M.tok_off + (uint64_t)s * EMIT_SEG,
+                            min((uint32_t)EMIT_SEG, M.ntok - s * EMIT_SEG), 0u};
+    if (t == 0) meta[st].nseg = nseg;
+    return;
+  }
+  const uint32_t* rt = rowtok + (size_t)M.frame * M.nrows;
+  const uint32_t per = (M.nrows + DESC_T - 1) / DESC_T;
+  const uint32_t r0 = min(t * per, M.nrows), r1 = min(r0 + per, M.nrows);
+  uint32_t cnt = 0;
+  for (uint32_t r = r0; r < r1; ++r) cnt += (rt[r] + EMIT_SEG - 1) / EMIT_SEG;
+  __shared__ uint32_t wsum[DESC_T / 64];
+  const int lane = t & 63, wv = t >> 6;
+  uint32_t incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(incl, o);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  uint32_t s = incl - cnt, total = 0;
+#pragma unroll
+  for (int k = 0; k < DESC_T / 64; ++k) {
+    s += k < wv ? wsum[k] : 0u;
+    total += wsum[k];
+  }
+  for (uint32_t r = r0; r < r1; ++r) {
+    const uint32_t n = rt[r];
+    for (uint32_t k = 0; k < n; k += EMIT_SEG)
+      D[s++] = vp8g_emit_desc{M.tok_off + (uint64_t)r * M.rowcap + k, min((uint32_t)EMIT_SEG, n - k),
+                              0u};
+  }
+  if (t == 0) meta[st].nseg = total;
+}
+
 extern "C" int vp8g_launch_check(const char* what);
 
 extern "C" int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
                                 const vp8g_frame_result* results, vp8g_emit_meta* meta,
-                                uint32_t max_ntok, uint32_t max_seg, uint8_t* emap,
-                                uint16_t* eshift, uint8_t* img, vp8g_emit_seg* segs,
-                                uint32_t* nbuf, uint32_t* out_size, void* stream) {
+                                const uint32_t* rowtok, uint32_t max_ntok, uint32_t max_seg,
+                                uint8_t* emap, uint16_t* eshift, uint8_t* img, vp8g_emit_desc* desc,
+                                vp8g_emit_seg* segs, uint32_t* nbuf, uint32_t* out_size,
+                                void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (n <= 0) return 1;
   (void)max_ntok;   // the token consumers resolve the probabilities themselves
+  hipLaunchKernelGGL(k_emit_desc, dim3(n), dim3(DESC_T), 0, st, meta, rowtok, desc);
+  if (!vp8g_launch_check("k_emit_desc")) return 0;
   if (max_seg) {
     hipLaunchKernelGGL(k_emit_img, dim3((max_seg + IMG_G - 1) / IMG_G, n), dim3(64), 0, st,
                        (const uint16_t*)tokens, tok_cap, results, (const vp8g_emit_meta*)meta,
-                       img);
+                       (const vp8g_emit_desc*)desc, img);
     if (!vp8g_launch_check("k_emit_img")) return 0;
     hipLaunchKernelGGL(k_emit_maps, dim3((max_seg + MAP_G - 1) / MAP_G, n), dim3(64), 0, st,
                        (const uint16_t*)tokens, tok_cap, results, (const vp8g_emit_meta*)meta,
-                       (const uint8_t*)img, emap, eshift);
+                       (const vp8g_emit_desc*)desc, (const uint8_t*)img, emap, eshift);
     if (!vp8g_launch_check("k_emit_maps")) return 0;
   }
   hipLaunchKernelGGL(k_emit_compose, dim3(n), dim3(64), 0, st, meta, (const uint8_t*)emap,
@@ -574,7 +653,7 @@ extern "C" int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
   const uint32_t sb = (max_seg + 63) / 64;
   if (sb) {
     hipLaunchKernelGGL(k_emit_seg, dim3(sb, n), dim3(64), 0, st, tokens, tok_cap, results,
-                       (const vp8g_emit_meta*)meta, segs, nbuf);
+                       (const vp8g_emit_meta*)meta, (const vp8g_emit_desc*)desc, segs, nbuf);
     if (!vp8g_launch_check("k_emit_seg")) return 0;
     hipLaunchKernelGGL(k_emit_carry, dim3(sb, n), dim3(64), 0, st, (const vp8g_emit_meta*)meta,
                        (const vp8g_emit_seg*)segs, nbuf);
@@ -592,32 +671,40 @@ extern "C" int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
 // encoder rarely makes (long all-ones runs: the carry paths). Streams are
 // concatenated in host_tokens; stream s's bytes go to host_out + s * out_stride,
 // its size to out_size[s]. Returns 0 on any HIP error or a too small stride.
-extern "C" __attribute__((visibility("default"))) int vp8g_emit_streams(
-    const uint16_t* host_tokens, const uint32_t* ntok, int n, uint8_t* host_out,
-    uint32_t out_stride, uint32_t* out_size) {
+// rowlen > 0: each stream is laid out as K3's token rows are -- rows of
+// rowlen tokens (the last one shorter) rowcap = round8(rowlen) + 8 apart --
+// and coded as a row stream (vp8g_emit_rows)
+static int emit_streams(const uint16_t* host_tokens, const uint32_t* ntok, int n, uint32_t rowlen,
+                        uint8_t* host_out, uint32_t out_stride, uint32_t* out_size) {
   if (n <= 0) return 1;
   vp8g_emit_meta* meta = (vp8g_emit_meta*)calloc((size_t)n, sizeof(vp8g_emit_meta));
   if (!meta) return 0;
+  const uint32_t rowcap = rowlen ? ((rowlen + 7) & ~7u) + 8 : 0;
   size_t off = 0, segs = 0, words = 0, src = 0;
-  uint32_t max_ntok = 0, max_seg = 0;
+  uint32_t max_ntok = 0, max_seg = 0, nrt = 0;   // nrt: rows of every row stream (the rest empty)
+  for (int s = 0; s < n && rowlen; ++s) nrt = max(nrt, (ntok[s] + rowlen - 1) / rowlen);
   for (int s = 0; s < n; ++s) {
     vp8g_emit_meta& m = meta[s];
     m.ntok = ntok[s];
     m.frame = (uint32_t)s;
     m.tok_off = off;
-    m.nseg = (m.ntok + EMIT_SEG - 1) / EMIT_SEG;
+    m.nrows = rowlen ? nrt : 0;
+    m.rowcap = rowcap;
+    m.nseg = (m.ntok + EMIT_SEG - 1) / EMIT_SEG + m.nrows;
     m.seg_base = (uint32_t)segs;
     m.nb_base = (uint32_t)words;
     segs += m.nseg;
     words += (7 * (size_t)m.ntok + 17 + 8 + 63) / 32 + 4;
-    off += ((size_t)m.ntok + 64 + 7) & ~(size_t)7;   // room for the bytes of a short stream
+    const size_t room = rowlen ? (size_t)m.nrows * rowcap : (size_t)m.ntok;
+    off += (room + 64 + 7) & ~(size_t)7;   // room for the bytes of a short stream
     max_ntok = m.ntok > max_ntok ? m.ntok : max_ntok;
     max_seg = m.nseg > max_seg ? m.nseg : max_seg;
     if ((7ull * m.ntok + 48) / 8 + 2 > out_stride) { free(meta); return 0; }
   }
   uint16_t* d_tok = nullptr; vp8g_frame_result* d_res = nullptr; vp8g_emit_meta* d_meta = nullptr;
   uint8_t *d_emap = nullptr, *d_img = nullptr; uint16_t* d_eshift = nullptr;
-  vp8g_emit_seg* d_segs = nullptr; uint32_t *d_nbuf = nullptr, *d_size = nullptr;
+  vp8g_emit_seg* d_segs = nullptr; uint32_t *d_nbuf = nullptr, *d_size = nullptr, *d_rt = nullptr;
+  vp8g_emit_desc* d_desc = nullptr;
   const size_t cs = segs + 1;
   bool ok = hipMalloc((void**)&d_tok, off * 2) == hipSuccess &&
             hipMalloc((void**)&d_res, (size_t)n * sizeof(vp8g_frame_result)) == hipSuccess &&
@@ -625,21 +712,33 @@ extern "C" __attribute__((visibility("default"))) int vp8g_emit_streams(
             hipMalloc((void**)&d_emap, cs * 128) == hipSuccess &&
             hipMalloc((void**)&d_eshift, cs * 128 * sizeof(uint16_t)) == hipSuccess &&
             hipMalloc((void**)&d_img, cs * 17) == hipSuccess &&
+            hipMalloc((void**)&d_desc, cs * sizeof(vp8g_emit_desc)) == hipSuccess &&
             hipMalloc((void**)&d_segs, cs * sizeof(vp8g_emit_seg)) == hipSuccess &&
             hipMalloc((void**)&d_nbuf, (words + 1) * sizeof(uint32_t)) == hipSuccess &&
+            hipMalloc((void**)&d_rt, ((size_t)n * nrt + 1) * sizeof(uint32_t)) == hipSuccess &&
             hipMalloc((void**)&d_size, (size_t)n * sizeof(uint32_t)) == hipSuccess;
   ok = ok && hipMemset(d_res, 0, (size_t)n * sizeof(vp8g_frame_result)) == hipSuccess &&
        hipMemset(d_nbuf, 0, (words + 1) * sizeof(uint32_t)) == hipSuccess &&
-       hipMemset(d_tok, 0, off * 2) == hipSuccess &&
-       hipMemcpy(d_meta, meta, (size_t)n * sizeof(vp8g_emit_meta), hipMemcpyHostToDevice) == hipSuccess;
+       hipMemset(d_rt, 0, ((size_t)n * nrt + 1) * sizeof(uint32_t)) == hipSuccess &&
+       hipMemset(d_tok, 0, off * 2) == hipSuccess;
   for (int s = 0; ok && s < n; ++s) {
-    if (meta[s].ntok)
-      ok = hipMemcpy(d_tok + meta[s].tok_off, host_tokens + src, meta[s].ntok * 2,
-                     hipMemcpyHostToDevice) == hipSuccess;
+    if (!rowlen) {
+      if (meta[s].ntok)
+        ok = hipMemcpy(d_tok + meta[s].tok_off, host_tokens + src, meta[s].ntok * 2,
+                       hipMemcpyHostToDevice) == hipSuccess;
+    } else {   // row r of stream s: tokens [r * rowlen, ...) at tok_off + r * rowcap
+      for (uint32_t r = 0; ok && r * rowlen < meta[s].ntok; ++r) {
+        const uint32_t len = min(rowlen, meta[s].ntok - r * rowlen);
+        ok = hipMemcpy(d_tok + meta[s].tok_off + (size_t)r * rowcap, host_tokens + src + (size_t)r * rowlen,
+                       len * 2, hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(d_rt + (size_t)s * meta[s].nrows + r, &len, 4, hipMemcpyHostToDevice) == hipSuccess;
+      }
+    }
     src += meta[s].ntok;
   }
-  ok = ok && vp8g_launch_emit(d_tok, off, n, d_res, d_meta, max_ntok, max_seg, d_emap, d_eshift,
-                              d_img, d_segs, d_nbuf, d_size, 0);
+  ok = ok && hipMemcpy(d_meta, meta, (size_t)n * sizeof(vp8g_emit_meta), hipMemcpyHostToDevice) == hipSuccess;
+  ok = ok && vp8g_launch_emit(d_tok, off, n, d_res, d_meta, d_rt, max_ntok, max_seg, d_emap,
+                              d_eshift, d_img, d_desc, d_segs, d_nbuf, d_size, 0);
   ok = ok && hipDeviceSynchronize() == hipSuccess &&
        hipMemcpy(out_size, d_size, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost) == hipSuccess;
   for (int s = 0; ok && s < n; ++s) {
@@ -648,10 +747,24 @@ extern "C" __attribute__((visibility("default"))) int vp8g_emit_streams(
       ok = hipMemcpy(host_out + (size_t)s * out_stride, d_tok + meta[s].tok_off, out_size[s],
                      hipMemcpyDeviceToHost) == hipSuccess;
   }
-  void* bufs[] = {d_tok, d_res, d_meta, d_emap, d_eshift, d_img, d_segs, d_nbuf, d_size};
+  void* bufs[] = {d_tok, d_res, d_meta, d_emap, d_eshift, d_img, d_desc, d_segs, d_nbuf, d_rt, d_size};
   for (void* b : bufs) (void)hipFree(b);
   free(meta);
   return ok ? 1 : 0;
+}
+
+extern "C" __attribute__((visibility("default"))) int vp8g_emit_streams(
+    const uint16_t* host_tokens, const uint32_t* ntok, int n, uint8_t* host_out,
+    uint32_t out_stride, uint32_t* out_size) {
+  return emit_streams(host_tokens, ntok, n, 0, host_out, out_stride, out_size);
+}
+
+// the same streams laid out and coded as K3's token rows of rowlen tokens
+extern "C" __attribute__((visibility("default"))) int vp8g_emit_rows(
+    const uint16_t* host_tokens, const uint32_t* ntok, int n, uint32_t rowlen, uint8_t* host_out,
+    uint32_t out_stride, uint32_t* out_size) {
+  if (rowlen == 0) return 0;
+  return emit_streams(host_tokens, ntok, n, rowlen, host_out, out_stride, out_size);
 }
 
 // Gather every stream's bytes (at its token offset) into one packed buffer at
@@ -787,13 +900,146 @@ extern "C" int vp8g_launch_partition(uint16_t* tokens, size_t tok_cap, int n,
   return vp8g_launch_check("k_partition");
 }
 
+// Partition 0's MB part (tree_enc.c:313-347: segment id, skip flag, intra-16
+// or the 16 intra-4 modes, chroma mode) as fixed-probability tokens behind
+// the frame's header tokens (vp8h_p0_header), for K4 to code as one more
+// stream. The host's code_intra_modes (host/vp8_host.c) is the same walk.
+// One 1,024-thread workgroup per frame: a thread takes a run of consecutive
+// raster MBs, counts their tokens, a block scan places the runs, then every
+// thread writes its MBs' tokens. The intra-4 contexts are read from mbinfo
+// directly: left = the previous MB of the row, top = the MB above, B_DC_PRED
+// (0) across the picture edges; an intra-16 MB's mode fills its 16 entries.
+#define P0T 1024
+__constant__ uint8_t kP0PathLen[10] = {1, 2, 3, 5, 6, 6, 5, 6, 7, 7};
+// intra-4 mode tree (tree_enc.c:270-295): nodes and bits along each mode's path
+__constant__ uint8_t kP0PathNode[10][7] = {
+    {0}, {0, 1}, {0, 1, 2}, {0, 1, 2, 3, 4}, {0, 1, 2, 3, 4, 5}, {0, 1, 2, 3, 4, 5},
+    {0, 1, 2, 3, 6}, {0, 1, 2, 3, 6, 7}, {0, 1, 2, 3, 6, 7, 8}, {0, 1, 2, 3, 6, 7, 8}};
+__constant__ uint8_t kP0PathBit[10][7] = {
+    {0}, {1, 0}, {1, 1, 0}, {1, 1, 1, 0, 0}, {1, 1, 1, 0, 1, 0}, {1, 1, 1, 0, 1, 1},
+    {1, 1, 1, 1, 0}, {1, 1, 1, 1, 1, 0}, {1, 1, 1, 1, 1, 1, 0}, {1, 1, 1, 1, 1, 1, 1}};
+
+__device__ __forceinline__ uint16_t p0t(int bit, int prob) {
+  return (uint16_t)((bit ? 0x8000u : 0u) | 0x4000u | (unsigned)prob);
+}
+__device__ __forceinline__ uint32_t p0_mb_count(const uint8_t* info, int upd, int use_skip) {
+  uint32_t n = (upd ? 2u : 0u) + (use_skip ? 1u : 0u) + 1u;
+  if (info[0]) {
+    n += 2;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) n += kP0PathLen[info[4 + k] < 10 ? info[4 + k] : 0];
+  }
+  const int uvm = info[1];
+  return n + (uvm == 0 ? 1u : uvm == 2 ? 2u : 3u);
+}
+
+__global__ __launch_bounds__(P0T) void k_p0_modes(const uint8_t* __restrict__ mbinfo, int mbw,
+                                                 int mbh, const vp8g_p0_par* __restrict__ par,
+                                                 const uint16_t* __restrict__ hdr,
+                                                 uint16_t* __restrict__ tokens,
+                                                 vp8g_emit_meta* __restrict__ meta, int meta_base) {
+  const int f = blockIdx.x, t = threadIdx.x, nmb = mbw * mbh;
+  const vp8g_p0_par P = par[f];
+  vp8g_emit_meta* M = meta + meta_base + f;
+  if (P.nhdr == 0xffffffffu) {   // the frame failed: an empty stream
+    if (t == 0) { M->ntok = 0; M->nseg = 0; }
+    return;
+  }
+  uint16_t* out = tokens + M->tok_off;
+  const uint16_t* h = hdr + (size_t)f * VP8G_P0_HDR_CAP;
+  for (uint32_t k = t; k < P.nhdr; k += P0T) out[k] = h[k];
+  const uint8_t* info = mbinfo + (size_t)f * nmb * VP8G_MBINFO_BYTES;
+  const int per = (nmb + P0T - 1) / P0T;
+  const int m0 = min(t * per, nmb), m1 = min(m0 + per, nmb);
+  uint32_t cnt = 0;
+  for (int m = m0; m < m1; ++m)
+    cnt += p0_mb_count(info + (size_t)m * VP8G_MBINFO_BYTES, P.update_map, P.use_skip);
+  // exclusive scan of the runs' counts over the workgroup
+  __shared__ uint32_t wsum[P0T / 64];
+  const int lane = t & 63, wv = t >> 6;
+  uint32_t incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(incl, o);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+#pragma unroll
+  for (int k = 0; k < P0T / 64; ++k) {
+    const uint32_t v = wsum[k];
+    before += k < wv ? v : 0u;
+    total += v;
+  }
+  uint32_t pos = P.nhdr + before + incl - cnt;
+  for (int m = m0; m < m1; ++m) {
+    const int x = m % mbw, y = m / mbw;
+    const uint8_t* in = info + (size_t)m * VP8G_MBINFO_BYTES;
+    const uint8_t* modes = in + 4;
+    if (P.update_map) {   // segment id tree (tree_enc.c:313-321)
+      const int sg = in[2];
+      out[pos] = p0t(sg >= 2, P.seg_probas[0]);
+      out[pos + 1] = p0t(sg & 1, P.seg_probas[1 + (sg >= 2)]);
+      pos += 2;
+    }
+    if (P.use_skip) out[pos++] = p0t(in[3] != 0, P.skip_proba);   // :323-325
+    const int i16 = in[0] != 0;
+    out[pos++] = p0t(i16, 145);
+    if (i16) {   // PutI16Mode (:257-266): DC 0, TM 1, V 2, H 3
+      const int md = modes[0];
+      const int b0 = md == 1 || md == 3;
+      out[pos] = p0t(b0, 156);
+      out[pos + 1] = b0 ? p0t(md == 1, 128) : p0t(md == 2, 163);
+      pos += 2;
+    } else {     // PutI4Mode (:268-295) with the neighbours' modes as context
+      const uint8_t* above = y > 0 ? in - (size_t)mbw * VP8G_MBINFO_BYTES + 4 + 12 : nullptr;
+      const uint8_t* leftm = x > 0 ? in - VP8G_MBINFO_BYTES + 4 : nullptr;
+      for (int yy = 0; yy < 4; ++yy) {
+        int left = leftm ? leftm[4 * yy + 3] : 0;
+        for (int xx = 0; xx < 4; ++xx) {
+          const int top = yy == 0 ? (above ? above[xx] : 0) : modes[4 * (yy - 1) + xx];
+          const uint8_t* pr = kVP8BModeProba[top < 10 ? top : 0][left < 10 ? left : 0];
+          const int md = modes[4 * yy + xx] < 10 ? modes[4 * yy + xx] : 0;
+          const int len = kP0PathLen[md];
+          for (int k = 0; k < len; ++k) out[pos + k] = p0t(kP0PathBit[md][k], pr[kP0PathNode[md][k]]);
+          pos += len;
+          left = md;
+        }
+      }
+    }
+    const int uvm = in[1];   // PutUVMode (:297-303): DC, then V / H / TM
+    out[pos++] = p0t(uvm != 0, 142);
+    if (uvm != 0) {
+      out[pos++] = p0t(uvm != 2, 114);
+      if (uvm != 2) out[pos++] = p0t(uvm != 3, 183);
+    }
+  }
+  if (t == 0) {
+    const uint32_t ntok = P.nhdr + total;
+    M->ntok = ntok;
+    M->nseg = (ntok + EMIT_SEG - 1) / EMIT_SEG;
+  }
+}
+
+extern "C" int vp8g_launch_p0_modes(const uint8_t* mbinfo, int mbw, int mbh, int n,
+                                    const vp8g_p0_par* par, const uint16_t* hdr, uint16_t* tokens,
+                                    vp8g_emit_meta* meta, int meta_base, void* stream) {
+  if (n <= 0) return 1;
+  hipLaunchKernelGGL(k_p0_modes, dim3(n), dim3(P0T), 0, (hipStream_t)stream, mbinfo, mbw, mbh, par,
+                     hdr, tokens, meta, meta_base);
+  return vp8g_launch_check("k_p0_modes");
+}
+
 // VP8EstimateTokenSize (token_enc.c:226-247) between the passes of a size
 // search: sum of VP8BitCost(bit, p) over a frame's compact token stream, p the
 // fixed probability of the token or the frame's probability table entry.
 // Grid (chunks, n); probability and entropy tables staged in LDS; one
 // 64-bit atomic per workgroup.
 __global__ __launch_bounds__(256) void k_token_cost(const uint16_t* __restrict__ tokens,
-                                                    size_t tok_cap,
+                                                    size_t tok_cap, uint32_t rowcap,
+                                                    const uint32_t* __restrict__ rowtok, int mbh,
                                                     const vp8g_frame_result* __restrict__ res,
                                                     const uint8_t* __restrict__ state,
                                                     const uint8_t* __restrict__ active,
@@ -807,13 +1053,18 @@ __global__ __launch_bounds__(256) void k_token_cost(const uint16_t* __restrict__
   for (int s = threadIdx.x; s < VP8G_NUM_SLOTS; s += 256) prob[s] = coeffs[s];
   ecost[threadIdx.x] = kVP8EntropyCost[threadIdx.x];
   __syncthreads();
-  const uint32_t nt = res[f].ntokens;
   const uint16_t* t = tokens + (size_t)f * tok_cap;
   uint32_t acc = 0;   // < 2^32: a chunk of the grid stride holds few tokens per thread
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nt; i += gridDim.x * 256) {
-    const uint32_t tk = t[i];
-    const int p = (tk & 0x4000u) ? (int)(tk & 0xffu) : (int)prob[tk & 0x3fffu];
-    acc += (tk & 0x8000u) ? ecost[255 - p] : ecost[p];
+  // the compact stream, or K3's token rows one after another
+  const int nr = rowtok ? mbh : 1;
+  for (int y = 0; y < nr; ++y) {
+    const uint32_t nt = rowtok ? rowtok[(size_t)f * mbh + y] : res[f].ntokens;
+    const uint16_t* tr = t + (size_t)y * rowcap;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nt; i += gridDim.x * 256) {
+      const uint32_t tk = tr[i];
+      const int p = (tk & 0x4000u) ? (int)(tk & 0xffu) : (int)prob[tk & 0x3fffu];
+      acc += (tk & 0x8000u) ? ecost[255 - p] : ecost[p];
+    }
   }
   unsigned long long v = acc;
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -822,7 +1073,8 @@ __global__ __launch_bounds__(256) void k_token_cost(const uint16_t* __restrict__
   if (threadIdx.x == 0) atomicAdd(&bits[f], wsum[0] + wsum[1] + wsum[2] + wsum[3]);
 }
 
-extern "C" int vp8g_launch_token_cost(const uint16_t* tokens, size_t tok_cap, int n,
+extern "C" int vp8g_launch_token_cost(const uint16_t* tokens, size_t tok_cap, const vp8g_rows* rows,
+                                      int mbh, int n,
                                       const vp8g_frame_result* results, const uint8_t* state,
                                       const uint8_t* active, unsigned long long* bits,
                                       void* stream) {
@@ -833,7 +1085,8 @@ extern "C" int vp8g_launch_token_cost(const uint16_t* tokens, size_t tok_cap, in
   // each token costs < 2^12, so the 32-bit per-thread sum cannot wrap below
   // 2^20 tokens per thread (2.7e10 tokens per frame)
   hipLaunchKernelGGL(k_token_cost, dim3(128, n), dim3(256), 0, (hipStream_t)stream, tokens,
-                     tok_cap, results, state, active, bits);
+                     tok_cap, rows ? rows->rowcap : 0u, rows ? rows->rowtok : nullptr, mbh, results,
+                     state, active, bits);
   return vp8g_launch_check("k_token_cost");
 }
 

@@ -116,22 +116,22 @@ struct K3S {
   // written), and the token count of each MB of its current row
   uint32_t rdelta[NSLOT];
   uint16_t rowcnt[1024];           // mbw <= 1024 (width <= 16383)
-  // token arena (K3Args::arena): this worker's current chunk [cpos, cend),
-  // and where each MB of its current row put its tokens
-  uint32_t cpos, cend;
+  // token rows (K3Args::rowtok): tokens this worker's current row has
+  // written so far, and where in the row each of its MBs put them
+  uint32_t rowfill;
   uint32_t rowpos[1024];
 #ifdef K3_TRACE
   unsigned long long trace[16];    // diagnostic build: per-worker cycle / event counts (K3TR_*)
 #endif
 #ifdef K3_CHECK
-  uint32_t ck_nmb, ck_cap;         // check build: the frame's MBs, the arena's end (+ sink)
+  uint32_t ck_nmb, ck_cap;         // check build: the frame's MBs, a token row's room
   int32_t ck_y, ck_x;              // the MB the worker is at (the hang record)
   uint32_t ck_rowdone;             // LDS offset of rowdone[0]
 #endif
 };
 
 // Index checks (-DK3_CHECK, diagnostic build libwebp_amd_check.so): every
-// global address k_encode computes from LDS state (arena chunk positions,
+// global address k_encode computes from LDS state (token row positions,
 // per-MB token counts and positions, compact-stream offsets, MB indices) is
 // checked before the access; a failing check records the first failure
 // (site, workgroup, worker, MB, value, bound) and counts the rest, and the
@@ -187,7 +187,7 @@ __device__ uint32_t g_k3hang[1024][4][10];
 // inside the lane-0 branch of a barrier arrival, in the else arm of an
 // if / else -- so some or all lanes keep stale registers (the row index, the
 // row-wavefront word's address, the thread id). Four diagnostic builds
-// stalled, faulted or leaked arena chunks that way; tools/isa_lane0_check.py
+// stalled, faulted or leaked token-arena chunks that way; tools/isa_lane0_check.py
 // finds the pattern in every one of them and checks every shipped code
 // object (build() fails on it). Hence: the arrival is one asm statement that
 // switches to lane 0 and back itself, and every poll loop tests a
@@ -1535,18 +1535,27 @@ __device__ __forceinline__ void publish(int32_t* p, int32_t v) {
 #ifndef K3_RD_BATCH
 #define K3_RD_BATCH 8   // (batch K3: 4 99.05 ms, 8 98.4; r5s26)
 #endif
-#ifdef K3_FOLD_INLINE
-#define K3_FOLD_ATTR __device__ __forceinline__
-#else
+// The statistics fold is inlined into the MB loop (round 6): as an
+// out-of-line call (b59c671 .. round 5) the worker's LDS state went to it as
+// flat pointers and the caller saved its live registers to scratch around
+// the call, and builds with that call faulted (illegal address) or hung
+// depending on the code around it; inlined it also
+// needs less scratch (headline kernel 120 -> 80 B/lane). -DK3_FOLD_CALL
+// restores the call (A/B).
+#ifdef K3_FOLD_CALL
 #define K3_FOLD_ATTR __device__
+#else
+#define K3_FOLD_ATTR __device__ __forceinline__
 #endif
 template <int RD>
 K3_FOLD_ATTR void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t row0,
-                         uint16_t* tok_base, uint32_t* mboff, const uint16_t* arena,
+                         uint16_t* tok_base, uint32_t* mboff, const uint16_t* rowbase,
                          const uint32_t* snap = nullptr) {
-  // MBs [i0, i1) of this worker's row (first MB row0): record where their
-  // tokens go in the frame's compact stream (moved there at frame end, see
-  // compact_tokens), then add their statistics in one step.
+  const bool rows = rowbase != nullptr;   // token rows: this row's tokens at rowbase
+  // MBs [i0, i1) of this worker's row (first MB row0): their token count
+  // (and, in the slot layout, where their tokens go in the frame's compact
+  // stream, moved there at frame end by compact_tokens), then their
+  // statistics added in one step.
   // Called once every earlier MB is folded (G.fold_ptr == i0).
   const uint32_t base = G.ntok;
   const uint32_t ln = (uint32_t)tid & 63;
@@ -1561,7 +1570,7 @@ K3_FOLD_ATTR void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, ui
         const uint32_t u = __shfl_up(incl, o);
         if (ln >= (uint32_t)o) incl += u;
       }
-      if (i < i1 && K3CK(i < CK_NMB(L, i + 1), 10, i, 0, i)) mboff[i] = off + incl - v;
+      if (!rows && i < i1 && K3CK(i < CK_NMB(L, i + 1), 10, i, 0, i)) mboff[i] = off + incl - v;
       off += __shfl(incl, 63);
     }
     if (ln == 0) { L.fold_total = off - base; L.fold_base = base; L.mark_any = 0; }
@@ -1636,12 +1645,14 @@ K3_FOLD_ATTR void fold_mbs(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, ui
               istart = row0 + (c0 / XS_SNAP_MBS + (uint32_t)nok) * XS_SNAP_MBS;
             }
           }
-          for (uint32_t i = istart; i < i1 && n; ++i) {
+          // (a frame whose token rows overflowed is encoded again: no walk
+          // through tokens that were never written)
+          for (uint32_t i = istart; i < i1 && n && !(G.tok_err & VP8G_ERR_ARENA); ++i) {
             const uint32_t nt = L.rowcnt[i - row0];
-            const uint16_t* tk = arena ? arena + L.rowpos[i - row0]
-                                       : tok_base + (size_t)i * VP8G_MAX_TOKENS_PER_MB;
-            if (arena && !K3CK((unsigned long long)L.rowpos[i - row0] + nt <= CK_CAP(L, ~0u), 11,
-                               L.rowpos[i - row0], nt, i))
+            const uint16_t* tk = rows ? rowbase + L.rowpos[i - row0]
+                                      : tok_base + (size_t)i * VP8G_MAX_TOKENS_PER_MB;
+            if (rows && !K3CK((unsigned long long)L.rowpos[i - row0] + nt <= CK_CAP(L, ~0u), 11,
+                              L.rowpos[i - row0], nt, i))
               break;
             // RD 64-token chunks per step, all loads issued before the first
             // ballot, and the step's count / ones of ss taken first from
@@ -1734,9 +1745,9 @@ __device__ __forceinline__ void report_rows(K3G& G, K3S& L, const vp8g_frame_par
 // back after, then the fold pointer published (folds are serialised in
 // raster order by fold_ptr, so one worker of the frame folds at a time)
 template <bool X>
-__device__ void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t row0,
+K3_FOLD_ATTR void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t row0,
                           uint16_t* tok_base, uint32_t* mboff, uint8_t* xs,
-                          const uint16_t* arena, const uint32_t* snap = nullptr) {
+                          const uint16_t* rowbase, const uint32_t* snap = nullptr) {
 #ifdef K3_NO_SNAP
   snap = nullptr;
 #endif
@@ -1748,7 +1759,7 @@ __device__ void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uin
       if (tid == 0) G.ntok = ld_sc1(&XH->ntok);
       wbar(L);
     }
-    fold_mbs<K3_RD_X>(G, L, tid, i0, i1, row0, tok_base, mboff, arena, snap);
+    fold_mbs<K3_RD_X>(G, L, tid, i0, i1, row0, tok_base, mboff, rowbase, snap);
     wbar(L);
     for (int s = tid; s < NSLOT; s += K3T) st_sc1(xstats + s, G.stats[s]);
     if (tid == 0) st_sc1(&XH->ntok, G.ntok);
@@ -1756,48 +1767,7 @@ __device__ void fold_rows(K3G& G, K3S& L, int tid, uint32_t i0, uint32_t i1, uin
     wbar(L);
     if (tid == 0) st_sc1(&XH->fold_ptr, (int32_t)i1);
   } else {
-    fold_mbs<K3_RD_BATCH>(G, L, tid, i0, i1, row0, tok_base, mboff, arena, snap);
-  }
-}
-
-// Arena mode: once MBs [i0, i1) of the worker's row are folded (their
-// compact offsets fixed from `base` = L.fold_base of that fold), their tokens
-// move from the worker's arena chunk to the frame's compact stream, one MB per
-// wave at a time, off the fold chain (fold_ptr / the epoch are published
-// first). An MB that would end beyond tok_cap is left out: the frame's count
-// then exceeds tok_cap and the host gathers it again into a wider buffer.
-__device__ void copy_folded(K3S& L, int tid, uint32_t i0, uint32_t i1, uint32_t row0,
-                            uint32_t base, uint16_t* tok_base, size_t tok_cap,
-                            const uint16_t* arena) {
-  const uint32_t ln = (uint32_t)tid & 63, wv = (uint32_t)tid >> 6;
-  uint32_t off = base;
-  for (uint32_t c = i0; c < i1; c += 64) {
-    const uint32_t i = c + ln;
-    const uint32_t v = i < i1 ? L.rowcnt[i - row0] : 0u;
-    uint32_t incl = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t u = __shfl_up(incl, o);
-      if (ln >= (uint32_t)o) incl += u;
-    }
-    const uint32_t excl = off + incl - v;
-    const uint32_t nc = min(64u, i1 - c);
-    for (uint32_t k = wv; k < nc; k += 4) {
-      const uint32_t d = __shfl(excl, (int)k), n = __shfl(v, (int)k);
-      if ((size_t)d + n > tok_cap) continue;   // wave-uniform
-      if (!K3CK((unsigned long long)L.rowpos[c + k - row0] + n <= CK_CAP(L, ~0u), 12,
-                L.rowpos[c + k - row0], n, c + k))
-        continue;
-      const uint16_t* src = arena + L.rowpos[c + k - row0];
-      uint16_t* dst = tok_base + d;
-      uint32_t q = ln;
-      for (; q + 192 < n; q += 256) {   // four loads in flight per lane
-        const uint16_t t0 = src[q], t1 = src[q + 64], t2 = src[q + 128], t3 = src[q + 192];
-        dst[q] = t0; dst[q + 64] = t1; dst[q + 128] = t2; dst[q + 192] = t3;
-      }
-      for (; q < n; q += 64) dst[q] = src[q];
-    }
-    off += __shfl(incl, 63);
+    fold_mbs<K3_RD_BATCH>(G, L, tid, i0, i1, row0, tok_base, mboff, rowbase, snap);
   }
 }
 
@@ -1878,37 +1848,13 @@ struct K3Args {
   size_t xs_fb;
   int nwg;          // K3X: workgroups per frame
   uint32_t* wsnap;  // K3 (not K3X: xs holds its snapshots): n x vp8g_wsnap_bytes, or NULL
-  // token arena (NULL: the per-MB slot layout, compacted at frame end). Each
-  // worker takes VP8G_ARENA_CHUNK-token chunks from *arena_top and writes
-  // every MB's tokens once, contiguously, at the chunk's next free position
-  // (mbpos, n x nmb); k_gather_tokens lays the frames' streams out later.
-  // Past arena_cap the tokens go to the sink chunk behind it and the frame
-  // reports VP8G_ERR_ARENA.
-  uint16_t* arena;
-  uint32_t arena_cap;
-  unsigned long long* arena_top;
-  uint32_t* mbpos;
+  // token rows (vp8g_rows; NULL: the per-MB slot layout, compacted at frame
+  // end): MB row y's tokens at tok_base + y * rowcap in raster order, the
+  // row's count to rowtok[f * mbh + y]; a row past rowcap writes nothing
+  // more and the frame reports VP8G_ERR_ARENA
+  uint32_t rowcap;
+  uint32_t* rowtok;
 };
-
-// a new chunk for this worker once fewer than one MB's worst case is left
-// (one lane; the caller orders it before the chunk's readers). Once the
-// arena is exhausted nothing bumps the pointer any more (a worker that sees
-// it at or past the end stays on the sink), and the pointer is 64-bit, so
-// it can never wrap back into live chunks of other frames.
-__device__ __forceinline__ void arena_refill(K3S& L, K3G& G, const K3Args& a) {
-  if (L.cend - L.cpos >= (uint32_t)VP8G_MAX_TOKENS_PER_MB) return;
-  const unsigned long long cap = a.arena_cap;
-  unsigned long long p = __hip_atomic_load(a.arena_top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (p + VP8G_ARENA_CHUNK <= cap) p = atomicAdd(a.arena_top, (unsigned long long)VP8G_ARENA_CHUNK);
-  if (p + VP8G_ARENA_CHUNK <= cap) {
-    L.cpos = (uint32_t)p;
-    L.cend = (uint32_t)p + VP8G_ARENA_CHUNK;
-  } else {   // exhausted: the sink (its contents are never read)
-    L.cpos = a.arena_cap;
-    L.cend = a.arena_cap + VP8G_MAX_TOKENS_PER_MB;
-    atomicOr(&G.tok_err, VP8G_ERR_ARENA);
-  }
-}
 
 // TR: the method >= 5 instantiation carries the trellis paths; m3/m4 frames
 // run a kernel without them (smaller register footprint).
@@ -1968,6 +1914,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
   const vp8g_frame_params* P = a.params + f;
   const uint8_t* segmap = a.segmap + (size_t)f * nmb;
   uint16_t* tok_base = a.tokens + f * a.tok_cap;
+  const bool rows = a.rowtok != nullptr;   // token rows (else per-MB slots)
+  auto rowbase_of = [&](int y) -> const uint16_t* {
+    return rows ? tok_base + (size_t)y * a.rowcap : nullptr;
+  };
   uint8_t* mbinfo = a.mbinfo + (size_t)f * nmb * VP8G_MBINFO_BYTES;
   uint32_t* mboff = a.mboff + (size_t)f * nmb;
 
@@ -2014,16 +1964,15 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     G.fs.nb[0] = G.fs.nb[1] = G.fs.nb[2] = 0;
     G.fold_ptr = 0; G.ntok = 0; G.tok_err = 0; G.epoch = 0; G.abort = 0;
   }
-  if (tid == 0) { L.bar = 0; L.myabort = 0; L.cpos = 0; L.cend = 0; }
+  if (tid == 0) { L.bar = 0; L.myabort = 0; L.rowfill = 0; }
 #ifdef K3_CHECK
   if (tid == 0) {
-    L.ck_nmb = (uint32_t)nmb; L.ck_cap = a.arena_cap + VP8G_MAX_TOKENS_PER_MB;
+    L.ck_nmb = (uint32_t)nmb; L.ck_cap = a.rowcap;
     L.ck_rowdone = (uint32_t)((uintptr_t)rowdone - (uintptr_t)smem);
     L.ck_y = -1; L.ck_x = 0;
   }
 #endif
   __syncthreads();
-  if (a.arena && tid == 0) arena_refill(L, G, a);
   if (wk == 0) level_costs_w(G, G.coeffs, tid);
   __syncthreads();
   if (rerun) {   // the level costs came from rstate[0..]; the probabilities are the loop-end ones
@@ -2063,6 +2012,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     if (tid < 16) yl[tid] = 129;
     if (tid < 8) { ul[tid] = 129; vl[tid] = 129; }
     if (tid == 0) {
+      L.rowfill = 0;
       yl[-1] = ul[-1] = vl[-1] = (y > 0) ? 129 : 127;
       L.lderr[0][0] = L.lderr[0][1] = L.lderr[1][0] = L.lderr[1][1] = 0;
     }
@@ -2110,12 +2060,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           }
           const uint64_t tr_f = TR_NOW();
           TR_ADD(K3TR_REFR_WAIT, tr_f - tr_w);
-          fold_rows<X>(G, L, tid, fold_from, mb, (uint32_t)y * mbw, tok_base, mboff, xs, a.arena,
+          fold_rows<X>(G, L, tid, fold_from, mb, (uint32_t)y * mbw, tok_base, mboff, xs, rowbase_of(y),
                        snap_of(y));
-          const uint32_t cp_from = fold_from;
           fold_from = mb;
           wbar(L);
-          const uint32_t cp_base = L.fold_base;
           const uint64_t tr_r = TR_NOW();
           TR_ADD(K3TR_FOLD, tr_r - tr_f);
           const int dirty = finalize_probas_wg(G, L, tid);
@@ -2153,8 +2101,6 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           }
           if (tid == 0) publish(&G.epoch, ep);
           TR_SINCE(K3TR_REFRESH, tr_r);
-          if (a.arena)
-            copy_folded(L, tid, cp_from, mb, (uint32_t)y * mbw, cp_base, tok_base, a.tok_cap, a.arena);
         } else if (X) {
           // the frame's refresher published epoch ep; the first worker of this
           // workgroup to need it copies the probabilities (and, if they
@@ -2541,9 +2487,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       // ---- tokens (token_enc.c:113-193) into this MB's slot; one (block,
       // zigzag position) item per thread, counts + scan + writes in parallel
       const int first_blk = is_i16 ? 0 : 1;
-      // this MB's place in the arena: read before the scan barrier below,
-      // after which thread 0 of wave 0 moves the chunk position on
-      const uint32_t tpos = a.arena ? L.cpos : 0u;
+      // this MB's place in its row: read before the scan barrier below, after
+      // which one thread moves the row's fill on
+      const uint32_t rfill = rows ? L.rowfill : 0u;
       uint64_t nzb = 0;
       int lvi[2], lvp[2];
 #pragma unroll
@@ -2609,14 +2555,19 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           if (w2 < wv) { pre0 += s0; pre1 += s1; }
           tot0 += s0; tot1 += s1;
         }
-        uint16_t* slot = a.arena ? a.arena + tpos : tok_base + (size_t)mb * VP8G_MAX_TOKENS_PER_MB;
+        uint16_t* slot = rows ? tok_base + (size_t)y * a.rowcap + rfill
+                              : tok_base + (size_t)mb * VP8G_MAX_TOKENS_PER_MB;
         const int off0 = pre0 + inc0 - cnt[0];
         const int off1 = tot0 + pre1 + inc1 - cnt[1];
+        // a row that would pass its room writes nothing more: the frame is
+        // encoded again with wider rows (VP8G_ERR_ARENA; worker-uniform)
+        const bool over = rows && rfill + (uint32_t)(tot0 + tot1) > a.rowcap;
+        if (over) { cnt[0] = 0; cnt[1] = 0; }
 #ifdef K3_CHECK
-        if (a.arena) {
-          const unsigned long long top = (unsigned long long)tpos + tot0 + tot1;
-          if (!K3CK(top <= CK_CAP(L, ~0u) && tot0 + tot1 <= VP8G_MAX_TOKENS_PER_MB, 15, tpos,
-                    tot0 + tot1, mb)) {
+        if (rows) {
+          const unsigned long long top = (unsigned long long)rfill + tot0 + tot1;
+          if (!over && !K3CK(top <= CK_CAP(L, ~0u) && tot0 + tot1 <= VP8G_MAX_TOKENS_PER_MB, 15,
+                             rfill, tot0 + tot1, mb)) {
             cnt[0] = 0; cnt[1] = 0;
           }
         }
@@ -2629,11 +2580,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
                            last[1], slot + off1, L.rdelta);
         if (rtid == 0) {
           L.rowcnt[x] = (uint16_t)(tot0 + tot1);
-          if (a.arena) {
-            L.rowpos[x] = tpos;
-            if (K3CK(mb < (uint32_t)nmb, 16, mb, nmb, mb)) a.mbpos[(size_t)f * nmb + mb] = tpos;
-            L.cpos = tpos + (uint32_t)(tot0 + tot1);
-            arena_refill(L, G, a);   // read by the next MB after the boundary barrier
+          if (rows) {
+            L.rowpos[x] = rfill;
+            L.rowfill = rfill + (uint32_t)(tot0 + tot1);   // read by the next MB after the barriers
+            if (over) atomicOr(&G.tok_err, VP8G_ERR_ARENA);
           }
         }
       }
@@ -2739,14 +2689,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           } else {
             if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from, 4)) break;
           }
-          fold_rows<X>(G, L, tid, fold_from, mb1, (uint32_t)y * mbw, tok_base, mboff, xs,
-                       a.arena, snap_of(y));
-          const uint32_t cp_from = fold_from;
+          fold_rows<X>(G, L, tid, fold_from, mb1, (uint32_t)y * mbw, tok_base, mboff, xs, rowbase_of(y),
+                       snap_of(y));
           fold_from = mb1;
           wbar(L);
-          if (a.arena)
-            copy_folded(L, tid, cp_from, mb1, (uint32_t)y * mbw, L.fold_base, tok_base, a.tok_cap,
-                        a.arena);
         }
       }
       K3_STAMP(6);
@@ -2763,13 +2709,11 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     const uint64_t tr_ff = TR_NOW();
     TR_ADD(K3TR_FOLD_WAIT, tr_ff - tr_fw);
     fold_rows<X>(G, L, tid, fold_from, (uint32_t)(y + 1) * mbw, (uint32_t)y * mbw, tok_base,
-                 mboff, xs, a.arena, snap_of(y));
+                 mboff, xs, rowbase_of(y), snap_of(y));
     TR_SINCE(K3TR_FOLD, tr_ff);
     report_rows<X>(G, L, P, tid, (uint32_t)(y + 1) * mbw, mbw, XH);
+    if (rows && tid == 0) a.rowtok[(size_t)f * mbh + y] = L.rowfill;   // K4's row length
     wbar(L);
-    if (a.arena)
-      copy_folded(L, tid, fold_from, (uint32_t)(y + 1) * mbw, (uint32_t)y * mbw, L.fold_base,
-                  tok_base, a.tok_cap, a.arena);
     K3_STAMP(7);
   }
 
@@ -2794,7 +2738,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     }
     return;
   }
-  if (!a.arena && !G.abort && !G.tok_err) compact_tokens(G, tok_base, mboff, nmb);
+  if (!rows && !G.abort && !G.tok_err) compact_tokens(G, tok_base, mboff, nmb);
   __syncthreads();
   if (wk == 0) {
     for (int s = tid; s < NSLOT && !(G.tok_err & VP8G_ERR_ARENA); s += K3T) {
@@ -2862,7 +2806,7 @@ __global__ __launch_bounds__(K3T) void k_encode_xtail(K3Args a) {
   }
   __syncthreads();
   const int err = XH->uabort ? 2 | (6 << 4) : XH->abort ? 2 : XH->tok_err;
-  if (!err && !a.arena) compact_tokens(G, tok_base, mboff, nmb);
+  if (!err && !a.rowtok) compact_tokens(G, tok_base, mboff, nmb);
   __syncthreads();
   for (int s = tid; s < NSLOT && !(XH->tok_err & VP8G_ERR_ARENA); s += K3T) {
     if (lcver > 0) rstate[s] = xs[XS_LCOEFFS + s];   // the level costs' probabilities
@@ -3051,49 +2995,6 @@ static int launch_k3_default(const K3Args& a, int n, bool trellis, bool af, void
                  : launch_k3_t<4, false>(a, n, false, stream);
 }
 
-// The frames' compact token streams from the arena (K3Args::arena): frame f's
-// stream at tokens + f * tok_cap in raster MB order, each MB's run of tokens
-// moved by one wave from arena + mbpos to its compact offset (mboff, the
-// frame's statistics fold computed it); the last MB ends at the frame's
-// token count. Frames that were not encoded by the launch (pass_mode 2),
-// failed, or do not fit tok_cap are left alone (the host checks the counts).
-__global__ __launch_bounds__(256) void k_gather_tokens(uint16_t* __restrict__ tokens,
-                                                       size_t tok_cap,
-                                                       const uint16_t* __restrict__ arena,
-                                                       const uint32_t* __restrict__ mbpos,
-                                                       const uint32_t* __restrict__ mboff, int nmb,
-                                                       const vp8g_frame_params* __restrict__ params,
-                                                       const vp8g_frame_result* __restrict__ results) {
-  const int f = blockIdx.y, ln = threadIdx.x & 63;
-  const int mb = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (mb >= nmb || params[f].pass_mode == 2) return;
-  const vp8g_frame_result* R = results + f;
-  const uint32_t ntok = R->ntokens;
-  if (R->error || ntok > tok_cap) return;
-  const size_t fm = (size_t)f * nmb;
-  const uint32_t d = mboff[fm + mb];
-  const uint32_t e = mb + 1 < nmb ? mboff[fm + mb + 1] : ntok;
-  const uint16_t* src = arena + mbpos[fm + mb];
-  uint16_t* dst = tokens + (size_t)f * tok_cap + d;
-  const uint32_t n = e - d;
-  uint32_t c = ln;
-  for (; c + 192 < n; c += 256) {   // four loads in flight per lane
-    const uint16_t t0 = src[c], t1 = src[c + 64], t2 = src[c + 128], t3 = src[c + 192];
-    dst[c] = t0; dst[c + 64] = t1; dst[c + 128] = t2; dst[c + 192] = t3;
-  }
-  for (; c < n; c += 64) dst[c] = src[c];
-}
-
-extern "C" int vp8g_launch_gather(uint16_t* tokens, size_t tok_cap, const uint16_t* arena,
-                                  const uint32_t* mbpos, const uint32_t* mboff, int w, int h, int n,
-                                  const vp8g_frame_params* params,
-                                  const vp8g_frame_result* results, void* stream) {
-  const int nmb = ((w + 15) >> 4) * ((h + 15) >> 4);
-  hipLaunchKernelGGL(k_gather_tokens, dim3((nmb + 3) / 4, n), dim3(256), 0, (hipStream_t)stream,
-                     tokens, tok_cap, arena, mbpos, mboff, nmb, params, results);
-  return vp8g_launch_check("k_gather_tokens");
-}
-
 #ifdef K3_CHECK
 // check build: the index-check record (count, site, workgroup, thread, MB,
 // value, bound) since the last call, then cleared
@@ -3229,7 +3130,7 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
                                   uint16_t* tokens, size_t tok_cap, uint8_t* mbinfo,
                                   uint32_t* mboff, int trellis, vp8g_frame_result* results,
                                   uint8_t* rerun_state, uint8_t* recon, uint8_t* xsync,
-                                  uint32_t* wsnap, const vp8g_arena* arena, void* stream) {
+                                  uint32_t* wsnap, const vp8g_rows* rows, void* stream) {
 #ifdef WEBP_AMD_DIAG
   // diagnostic build only (make diag -> libwebp_amd_diag.so; the product
   // library has no switch): WEBP_AMD_K3 = 1 single-wavefront twin,
@@ -3261,17 +3162,8 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   a.mbinfo = mbinfo; a.mboff = mboff; a.results = results; a.rerun = rerun_state;
   a.xs = xsync; a.xs_fb = vp8g_xsync_bytes(w, h); a.nwg = 1;
   a.wsnap = wsnap;
-  a.arena = nullptr; a.arena_cap = 0; a.arena_top = nullptr; a.mbpos = nullptr;
-  if (arena) {   // one arena per launch: the bump pointer starts at 0
-    a.arena = arena->tokens;
-    a.arena_cap = arena->cap;
-    a.arena_top = arena->top;
-    a.mbpos = arena->mbpos;
-    if (hipMemsetAsync(arena->top, 0, sizeof(unsigned long long), (hipStream_t)stream) != hipSuccess) {
-      vp8g_set_error("k_encode", "arena reset failed");
-      return 0;
-    }
-  }
+  a.rowcap = rows ? rows->rowcap : 0u;
+  a.rowtok = rows ? rows->rowtok : nullptr;
   if (xsync != nullptr && recon == nullptr && variant == 0) {
     const int nwg = k3x_take(n, a.mbh, 2);
     if (nwg > 1)

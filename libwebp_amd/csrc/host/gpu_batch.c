@@ -133,9 +133,13 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   b->dither = b->sharp ? 0.f : vp8h_import_dithering(config);
   b->threads = host_threads > 0 ? host_threads : default_threads(device);
   b->host_emit = 0;
-  {   /* test knob: start with a one-chunk arena and 4096-token streams, so
-         the first call re-runs K3 with a grown arena and gathers the streams
-         again (k3_settle's two fallbacks) */
+  {   /* where partition 0 is coded: WEBP_AMD_P0=host / gpu, else by the rank's
+         host-thread budget (use_gpu_p0) */
+    const char* e = getenv("WEBP_AMD_P0");
+    b->gpu_p0 = e && !strcmp(e, "gpu") ? 1 : e && !strcmp(e, "host") ? 0 : -1;
+  }
+  {   /* test knob: start with token rows of 64 tokens, so the first call
+         re-runs K3 with wider rows (k3_settle's regrow) */
     const char* tt = getenv("WEBP_AMD_TEST_TINY_TOKENS");
     b->tiny_tokens = tt && tt[0] == '1';
   }
@@ -172,7 +176,7 @@ WebPGpuBatch* WebPGpuBatchNew(int device, int width, int height, int max_frames,
   CHK(hipMalloc((void**)&b->d_results, N * sizeof(vp8g_frame_result)));
   /* K4 streams: one per token partition; the WebPEncode pool changes the
    * config of an engine between calls, so room for the most partitions */
-  const size_t NS = N * VP8G_MAX_PARTS;
+  const size_t NS = N * (VP8G_MAX_PARTS + 1);   /* + partition 0 (gpu_p0) */
   CHK(hipMalloc((void**)&b->d_psize, NS * sizeof(uint32_t)));
   CHK(hipMalloc((void**)&b->d_emeta, NS * sizeof(vp8g_emit_meta)));
   CHK(hipMalloc((void**)&b->d_pinfo, N * 16 * sizeof(uint32_t)));
@@ -218,7 +222,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipFree(b->d_rgba2);
   hipFree(b->d_g2l); hipFree(b->d_rgba); hipFree(b->d_yuv); hipFree(b->d_aflags); hipFree(b->d_alpha);
   hipFree(b->d_uva); hipFree(b->d_amode); hipFree(b->d_segmap); hipFree(b->d_params); hipFree(b->d_tokens);
-  hipFree(b->d_arena); hipFree(b->d_arena_top); hipFree(b->d_mbpos); hipFree(b->d_rerun_snap);
+  hipFree(b->d_rowtok); hipHostFree(b->h_rowtok); hipFree(b->d_rerun_snap); hipFree(b->d_edesc);
   hipFree(b->d_mbinfo); hipFree(b->d_mboff); hipFree(b->d_rerun); hipFree(b->d_xsync); hipFree(b->d_wsnap); hipFree(b->d_results); hipFree(b->d_psize); hipFree(b->d_emeta);
   hipFree(b->d_poff); hipFree(b->d_part); hipFree(b->d_pinfo);
   hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs); hipFree(b->d_nbuf);
@@ -237,6 +241,7 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
   hipHostFree(b->h_segmap); hipHostFree(b->h_params); hipHostFree(b->h_mbinfo);
   hipHostFree(b->h_results); hipHostFree(b->h_tokens); hipHostFree(b->h_psize);
   hipHostFree(b->h_part); hipHostFree(b->h_emeta); hipHostFree(b->h_poff); hipHostFree(b->h_pinfo);
+  hipHostFree(b->h_p0hdr); hipHostFree(b->h_p0par); hipFree(b->d_p0hdr); hipFree(b->d_p0par);
   vp8l_engine_free(b->l);
   vp8l_engine_free(b->la);
   hipFree(b->d_aplane);
@@ -260,7 +265,8 @@ void WebPGpuBatchDelete(WebPGpuBatch* b) {
 
 typedef struct {
   WebPGpuBatch* b;
-  int phase;   /* 0: partition 0; 1: partition 1 + RIFF write; 2: frame setup */
+  int phase;   /* 0: partition 0; 1: partition 1 + RIFF write; 2: frame setup;
+                  3: partition 0's header tokens (gpu_p0) */
   vp8g_job job;
 } TailJob;
 
@@ -282,6 +288,24 @@ static void frame_head(WebPGpuBatch* b, int f) {
                             &b->p0[f], b->hdr + 2 * f);
 }
 
+/* Partition 0 on the device (gpu_p0): the frame header as tokens for
+ * k_p0_modes, which appends the MB modes; K4 codes the stream. */
+static void frame_head_dev(WebPGpuBatch* b, int f) {
+  vp8h_frame* fr = &b->frames[f];
+  const vp8g_frame_result* res = &b->h_results[f];
+  b->out_size[f] = 0;
+  vp8h_bw_free(&b->p0[f]);
+  int nh = -1;
+  if (b->err[f] == VP8_ENC_OK && res->error)
+    b->err[f] = (res->error >> 4) == 6 ? VP8_ENC_ERROR_USER_ABORT : VP8_ENC_ERROR_OUT_OF_MEMORY;
+  if (b->err[f] == VP8_ENC_OK) {
+    nh = vp8h_p0_header(fr, res, b->h_p0hdr + (size_t)f * VP8G_P0_HDR_CAP, VP8G_P0_HDR_CAP,
+                        b->hdr + 2 * f);
+    if (nh < 0) b->err[f] = VP8_ENC_ERROR_OUT_OF_MEMORY;
+  }
+  vp8h_p0_par(fr, res, nh, &b->h_p0par[f]);
+}
+
 /* Join partition 0 with partition 1 (K4's bytes, or coded here under
  * WEBP_AMD_HOST_EMIT=1) into the RIFF/WEBP file. */
 static void frame_finish(WebPGpuBatch* b, int f) {
@@ -299,6 +323,18 @@ static void frame_finish(WebPGpuBatch* b, int f) {
       memset(&part1[p], 0, sizeof(part1[p]));
       part1[p].buf = b->h_part + b->h_poff[s];
       part1[p].pos = b->h_psize[s];
+    }
+  }
+  if (b->p0_dev) {   /* partition 0 coded by K4: borrowed from the packed bytes */
+    const size_t s = (size_t)b->last_ns + f;
+    memset(&b->p0[f], 0, sizeof(b->p0[f]));
+    b->p0[f].buf = b->h_part + b->h_poff[s];
+    b->p0[f].pos = b->h_psize[s];
+    b->hdr[2 * f + 1] = (int)b->h_psize[s] - b->hdr[2 * f];
+    if (b->h_psize[s] >= (1u << 19)) {   /* syntax_enc.c / vp8h_build_p0's check */
+      b->err[f] = VP8_ENC_ERROR_PARTITION0_OVERFLOW;
+      memset(&b->p0[f], 0, sizeof(b->p0[f]));
+      return;
     }
   }
   int err = VP8_ENC_OK;
@@ -336,6 +372,7 @@ static void tail_item(void* arg, int f) {
   TailJob* j = (TailJob*)arg;
   if (j->phase == 0) frame_head(j->b, f);
   else if (j->phase == 1) frame_finish(j->b, f);
+  else if (j->phase == 3) frame_head_dev(j->b, f);
   else frame_setup(j->b, f);
 }
 
@@ -468,47 +505,68 @@ fail:
 }
 
 /* ---- token buffers ----------------------------------------------------
- * The token loop (methods 3-6 without low_memory) runs K3 with an arena:
- * every MB's tokens are written once into a worker's arena chunk and moved
- * by K3 to the frame's compact stream at d_tokens + f * tok_cap once their
- * row is folded; tok_cap follows the largest stream seen (k_gather_tokens
- * redoes a stream that did not fit). The other paths (methods 0-2, low_memory, VP8EncLoop's
- * searches) keep per-MB slots of the worst case VP8G_MAX_TOKENS_PER_MB. */
-static int arena_mode(const WebPGpuBatch* b) {
-  return b->cfg.method >= 3 && !b->cfg.low_memory;
+ * The token loop (methods 3-6 without low_memory) runs K3 with token rows:
+ * every MB's tokens are written once, where K4 reads them -- frame f's MB
+ * row y at d_tokens + f * tok_cap + y * rowcap, the MBs of the row one after
+ * another in raster order (vp8g_rows) -- and a row that runs out of room
+ * makes k3_settle widen the rows and run the launch again. The other paths
+ * (methods 0-2, low_memory, VP8EncLoop's searches) keep per-MB slots of the
+ * worst case VP8G_MAX_TOKENS_PER_MB and a compact stream per frame. Both
+ * take d_tokens with a frame stride of tok_cap tokens; behind the frames'
+ * slabs lies each frame's partition-0 stream (gpu_p0). */
+static int rows_mode(const WebPGpuBatch* b) {
+  return b->cfg.method >= 3 && !b->cfg.low_memory && !b->host_emit;
+}
+
+/* d_tokens with a frame stride of tok_cap tokens; the first keep frames'
+ * token rows (rowcap apart, the old layout) move to the new layout */
+static int alloc_tokens(WebPGpuBatch* b, size_t tok_cap, size_t rowcap, int keep) {
+  uint16_t* old = b->d_tokens;
+  const size_t old_rowcap = b->rowcap, old_cap = b->tok_cap;
+  uint16_t* nt = NULL;
+  const size_t p0cap = vp8g_p0_cap(b->nmb);
+  CHK(hipMalloc((void**)&nt, (size_t)b->max_frames * (tok_cap + p0cap) * sizeof(uint16_t)));
+  if (old && keep > 0 && old_rowcap) {   /* row y of frame f: f * cap + y * rowcap */
+    for (int f = 0; f < keep; ++f)
+      CHK(hipMemcpy2DAsync(nt + (size_t)f * tok_cap, rowcap * sizeof(uint16_t),
+                           old + (size_t)f * old_cap, old_rowcap * sizeof(uint16_t),
+                           old_rowcap * sizeof(uint16_t), (size_t)b->mbh, hipMemcpyDeviceToDevice,
+                           b->stream));
+    CHK(hipStreamSynchronize(b->stream));
+  }
+  hipFree(old);
+  b->d_tokens = nt;
+  b->tok_cap = tok_cap;
+  b->p0_cap = p0cap;
+  /* the widest rows the stride holds (token rows may use a slot-sized buffer) */
+  b->rowcap = (tok_cap / (size_t)b->mbh) & ~(size_t)7;
+  return 1;
+fail:
+  hipFree(nt);
+  return 0;
 }
 
 /* d_tokens with a stride of at least cap tokens per frame (grows only) */
 static int ensure_tok_cap(WebPGpuBatch* b, size_t cap) {
   cap = (cap + 255) & ~(size_t)255;
   if (b->d_tokens && b->tok_cap >= cap) return 1;
-  hipFree(b->d_tokens);
-  b->d_tokens = NULL;
-  b->tok_cap = 0;
-  CHK(hipMalloc((void**)&b->d_tokens, (size_t)b->max_frames * cap * sizeof(uint16_t)));
-  b->tok_cap = cap;
-  return 1;
-fail:
-  return 0;
+  return alloc_tokens(b, cap, 0, 0);
 }
 
-/* the arena with at least cap tokens (grows only; u32 positions) */
-static int ensure_arena(WebPGpuBatch* b, size_t cap) {
-  const size_t lim = 0xfff00000u - VP8G_MAX_TOKENS_PER_MB;
-  if (cap > lim) cap = lim;
-  if (b->d_arena && b->arena_cap >= cap) return 1;
-  hipFree(b->d_arena);
-  b->d_arena = NULL;
-  b->arena_cap = 0;
-  CHK(hipMalloc((void**)&b->d_arena, (cap + VP8G_MAX_TOKENS_PER_MB) * sizeof(uint16_t)));
-  b->arena_cap = cap;
-  if (!b->d_arena_top) {
-    const size_t N = (size_t)b->max_frames;
-    CHK(hipMalloc((void**)&b->d_arena_top, sizeof(unsigned long long)));
-    CHK(hipMalloc((void**)&b->d_mbpos, N * b->nmb * sizeof(uint32_t)));
-    CHK(hipMalloc((void**)&b->d_rerun_snap, N * VP8G_RERUN_STATE_BYTES));
+/* token rows of at least rowcap tokens (grows only, at most the worst case
+ * of a row); keep: frames whose rows must survive a regrow */
+static int ensure_rows(WebPGpuBatch* b, size_t rowcap, int keep) {
+  const size_t most = (size_t)VP8G_MAX_TOKENS_PER_MB * b->mbw;
+  rowcap = (rowcap + 7) & ~(size_t)7;
+  if (rowcap > most) rowcap = (most + 7) & ~(size_t)7;
+  if (!b->d_rowtok) {
+    CHK(hipMalloc((void**)&b->d_rowtok, (size_t)b->max_frames * b->mbh * sizeof(uint32_t)));
+    CHK(hipHostMalloc((void**)&b->h_rowtok, (size_t)b->max_frames * b->mbh * sizeof(uint32_t), 0));
+    CHK(hipMalloc((void**)&b->d_rerun_snap, (size_t)b->max_frames * VP8G_RERUN_STATE_BYTES));
   }
-  return 1;
+  if (b->d_tokens && b->rowcap >= rowcap) return 1;
+  /* the K4 reads of a row's last 8-token piece stay inside the slab: + 8 */
+  return alloc_tokens(b, (size_t)b->mbh * rowcap + 8, rowcap, keep);
 fail:
   return 0;
 }
@@ -516,39 +574,34 @@ fail:
 /* the token buffers of this run's path (before K3's first launch) */
 static int tokens_for_run(WebPGpuBatch* b) {
   const size_t nmb = (size_t)b->nmb;
-  if (!arena_mode(b)) return ensure_tok_cap(b, nmb * VP8G_MAX_TOKENS_PER_MB);
-  if (b->tiny_tokens)   /* test knob: both fallbacks of k3_settle run on the first call */
-    return ensure_tok_cap(b, 4096) && ensure_arena(b, (size_t)VP8G_ARENA_CHUNK);
-  /* ~1.2x the tokens of a -q 75 frame of natural content per MB to start
-   * with, and room for every worker's partly used last chunk */
-  return ensure_tok_cap(b, nmb * 1536 + 4096) &&
-         ensure_arena(b, (size_t)b->max_frames * nmb * 1024 + 768 * (size_t)VP8G_ARENA_CHUNK);
+  if (!rows_mode(b)) return ensure_tok_cap(b, nmb * VP8G_MAX_TOKENS_PER_MB);
+  if (b->tiny_tokens)   /* test knob: k3_settle's regrow runs on the first call */
+    return ensure_rows(b, 64, 0);
+  /* ~2.3x the tokens per MB of a -q 75 frame of natural content in a row
+   * (batches); single pictures (K3X) start at 4096 per MB (a 4096-wide q90
+   * m6 row holds ~2900 per MB) */
+  return ensure_rows(b, (size_t)b->mbw * (b->max_frames <= VP8G_XSPLIT_MAX_FRAMES ? 4096 : 2048), 0);
 }
 
 /* K3 over the frames of h_params (already on the device). The caller copies
  * the results back and calls k3_settle. */
 static int launch_k3(WebPGpuBatch* b, int n, uint8_t* recon) {
   hipStream_t st = b->stream;
-  vp8g_arena A, *ap = NULL;
-  if (arena_mode(b)) {
+  vp8g_rows R, *rp = NULL;
+  if (rows_mode(b)) {
     int reread = 0;   /* a pass that starts from d_rerun: keep a copy for a re-run */
     for (int f = 0; f < n; ++f)
       reread |= b->h_params[f].pass_mode == 1 || b->h_params[f].pass_mode == 3;
     if (reread)
       CHK(hipMemcpyAsync(b->d_rerun_snap, b->d_rerun, (size_t)n * VP8G_RERUN_STATE_BYTES,
                          hipMemcpyDeviceToDevice, st));
-    A.tokens = b->d_arena;
-    A.cap = (uint32_t)b->arena_cap;
-    A.top = b->d_arena_top;
-    A.mbpos = b->d_mbpos;
-    ap = &A;
+    R.rowcap = (uint32_t)b->rowcap;
+    R.rowtok = b->d_rowtok;
+    rp = &R;
   }
-  /* in arena mode K3 itself moves each folded row's tokens to the compact
-     stream (copy_folded); k_gather_tokens only redoes it for a stream that
-     outgrew tok_cap (k3_settle) */
   if (!vp8g_launch_encode(b->d_yuv, b->yfb, b->w, b->h, n, b->d_segmap, b->d_params, b->d_tokens,
                           b->tok_cap, b->d_mbinfo, b->d_mboff, b->cfg.method >= 5, b->d_results,
-                          b->d_rerun, recon, b->d_xsync, b->d_wsnap, ap, st))
+                          b->d_rerun, recon, b->d_xsync, b->d_wsnap, rp, st))
     return 0;
   return 1;
 fail:
@@ -556,49 +609,41 @@ fail:
 }
 
 /* after launch_k3 and the results' copy to h_results (stream drained): a
- * launch whose arena ran out runs again with twice the arena (from the
- * saved d_rerun); streams longer than tok_cap are gathered again into a
- * wider d_tokens. Returns 2 when K3 ran again (d_rerun changed), 1 else. */
+ * launch in which some frame's token row ran out of room runs again (from
+ * the saved d_rerun) with rows wide enough for the longest row it reported
+ * (K3 counts a row's tokens on after the room is gone). The frames this
+ * launch skipped (pass_mode 2) keep their rows. Returns 2 when K3 ran again
+ * (d_rerun changed), 1 else. */
 static int k3_settle(WebPGpuBatch* b, int n, uint8_t* recon) {
-  if (!arena_mode(b)) return 1;
+  if (!rows_mode(b)) return 1;
   hipStream_t st = b->stream;
   int rerun = 0;
   for (int tries = 0;; ++tries) {
     int over = 0;
-    size_t longest = 0, total = 0;
-    for (int f = 0; f < n; ++f) {
-      const vp8g_frame_result* R = &b->h_results[f];
-      if (b->h_params[f].pass_mode == 2) continue;
-      total += R->ntokens;   /* counted by the fold even for tokens that went to the sink */
-      if (R->error & VP8G_ERR_ARENA) over = 1;
-      else if (!R->error && R->ntokens > longest) longest = R->ntokens;
+    for (int f = 0; f < n; ++f)
+      if (b->h_params[f].pass_mode != 2 && (b->h_results[f].error & VP8G_ERR_ARENA)) over = 1;
+    if (!over) return rerun ? 2 : 1;
+    const size_t nr = (size_t)n * b->mbh;
+    CHK(hipMemcpy(b->h_rowtok, b->d_rowtok, nr * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    size_t longest = 0;
+    for (int f = 0; f < n; ++f)
+      if (b->h_params[f].pass_mode != 2)
+        for (int y = 0; y < b->mbh; ++y)
+          if (b->h_rowtok[(size_t)f * b->mbh + y] > longest) longest = b->h_rowtok[(size_t)f * b->mbh + y];
+    size_t want = longest + longest / 8 + 64;
+    if (want < 2 * b->rowcap) want = 2 * b->rowcap;
+    if (tries > 4 || b->rowcap >= (size_t)VP8G_MAX_TOKENS_PER_MB * b->mbw || !ensure_rows(b, want, n)) {
+      vp8g_set_error("k_encode", "token rows cannot grow");
+      return 0;
     }
-    if (over) {
-      /* the tokens this launch needs (+ a partly used last chunk per worker
-       * and 1/8 headroom), at least twice the old arena */
-      size_t want = total + total / 8 + 1024 * (size_t)VP8G_ARENA_CHUNK;
-      if (want < 2 * (size_t)b->arena_cap) want = 2 * (size_t)b->arena_cap;
-      if (tries > 6 || b->arena_cap >= 0xfff00000u - VP8G_MAX_TOKENS_PER_MB ||
-          !ensure_arena(b, want)) {
-        vp8g_set_error("k_encode", "token arena cannot grow");
-        return 0;
-      }
-      int reread = 0;
-      for (int f = 0; f < n; ++f)
-        reread |= b->h_params[f].pass_mode == 1 || b->h_params[f].pass_mode == 3;
-      if (reread)
-        CHK(hipMemcpyAsync(b->d_rerun, b->d_rerun_snap, (size_t)n * VP8G_RERUN_STATE_BYTES,
-                           hipMemcpyDeviceToDevice, st));
-      if (!launch_k3(b, n, recon)) return 0;
-      rerun = 1;
-    } else if (longest + 64 > b->tok_cap) {
-      if (!ensure_tok_cap(b, longest + longest / 4 + 64) ||
-          !vp8g_launch_gather(b->d_tokens, b->tok_cap, b->d_arena, b->d_mbpos, b->d_mboff, b->w,
-                              b->h, n, b->d_params, b->d_results, st))
-        return 0;
-    } else {
-      return rerun ? 2 : 1;
-    }
+    int reread = 0;
+    for (int f = 0; f < n; ++f)
+      reread |= b->h_params[f].pass_mode == 1 || b->h_params[f].pass_mode == 3;
+    if (reread)
+      CHK(hipMemcpyAsync(b->d_rerun, b->d_rerun_snap, (size_t)n * VP8G_RERUN_STATE_BYTES,
+                         hipMemcpyDeviceToDevice, st));
+    if (!launch_k3(b, n, recon)) return 0;
+    rerun = 1;
     CHK(hipMemcpyAsync(b->h_results, b->d_results, n * sizeof(vp8g_frame_result),
                        hipMemcpyDeviceToHost, st));
     CHK(hipStreamSynchronize(st));
@@ -1101,8 +1146,9 @@ static int run_passes(WebPGpuBatch* b, int n) {
       CHK(hipMemcpyAsync(b->d_rerun, b->h_state, (size_t)n * VP8G_RERUN_STATE_BYTES,
                          hipMemcpyHostToDevice, st));
       CHK(hipMemcpyAsync(b->d_active, b->h_active, n, hipMemcpyHostToDevice, st));
-      if (!vp8g_launch_token_cost(b->d_tokens, b->tok_cap, n, b->d_results, b->d_rerun,
-                                  b->d_active, b->d_tbits, st))
+      vp8g_rows R = {(uint32_t)b->rowcap, b->d_rowtok};
+      if (!vp8g_launch_token_cost(b->d_tokens, b->tok_cap, rows_mode(b) ? &R : NULL, b->mbh, n,
+                                  b->d_results, b->d_rerun, b->d_active, b->d_tbits, st))
         return 0;
       CHK(hipMemcpyAsync(b->h_tbits, b->d_tbits, n * sizeof(unsigned long long),
                          hipMemcpyDeviceToHost, st));
@@ -1161,6 +1207,17 @@ fail:
   return 0;
 }
 
+/* Partition 0 on the device when asked (WEBP_AMD_P0=gpu), or, by default,
+ * when the rank's host-thread budget is small: coding it is ~1 ms of one CPU
+ * per 1080p frame (the intra-4 modes), which a budget of a few threads shared
+ * by several engines cannot keep up with, while on the
+ * device it adds a K4 stream of ~1/13 of the frame's tokens. */
+#define P0_DEVICE_BELOW 8   /* host threads per rank */
+static int use_gpu_p0(const WebPGpuBatch* b) {
+  if (b->gpu_p0 >= 0) return b->gpu_p0;
+  return b->threads < P0_DEVICE_BELOW;
+}
+
 int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   const size_t nmb = (size_t)b->nmb;
   double t0 = now_us(), t1, t2, t3, t4;
@@ -1169,6 +1226,18 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   int head_running = 0;
   b->timings[9] = 0;
   if (!tokens_for_run(b)) return 0;
+  if (getenv("WEBP_AMD_FAULT_REPORT")) {   /* diagnostics: buffer ranges for a fault address */
+    vp8g_fault_report_init();
+    fprintf(stderr,
+            "WEBP_AMD_BUFFERS tokens %p +%zu yuv %p +%zu mbinfo %p +%zu mboff %p +%zu "
+            "wsnap %p +%zu results %p +%zu params %p segmap %p rowtok %p\n",
+            (void*)b->d_tokens, (size_t)b->max_frames * (b->tok_cap + b->p0_cap) * 2, (void*)b->d_yuv,
+            (size_t)b->max_frames * b->yfb, (void*)b->d_mbinfo, (size_t)b->max_frames * nmb * 20,
+            (void*)b->d_mboff, (size_t)b->max_frames * nmb * 4, (void*)b->d_wsnap,
+            (size_t)b->max_frames * vp8g_wsnap_bytes(b->w, b->h), (void*)b->d_results,
+            (size_t)b->max_frames * sizeof(vp8g_frame_result), (void*)b->d_params,
+            (void*)b->d_segmap, (void*)b->d_rowtok);
+  }
   if (!encode_alpha(b, n)) return 0;
   if (!b->ev0_recorded) CHK(hipEventRecord(b->ev[0], st));
   b->ev0_recorded = 0;
@@ -1199,10 +1268,57 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
                        hipMemcpyDeviceToHost, st));
     CHK(hipStreamSynchronize(st));
   }
+  /* partition 0: coded on the host threads while K4 runs, or (gpu_p0) its
+     header tokens built here and the rest done by k_p0_modes + K4 */
+  const int p0dev = !b->host_emit && use_gpu_p0(b);
+  b->p0_dev = p0dev;
+  b->last_ns = ns;
+  if (p0dev) {
+    if (!b->h_p0hdr) {
+      const size_t N = (size_t)b->max_frames;
+      CHK(hipHostMalloc((void**)&b->h_p0hdr, N * VP8G_P0_HDR_CAP * sizeof(uint16_t), 0));
+      CHK(hipHostMalloc((void**)&b->h_p0par, N * sizeof(vp8g_p0_par), 0));
+      CHK(hipMalloc((void**)&b->d_p0hdr, N * VP8G_P0_HDR_CAP * sizeof(uint16_t)));
+      CHK(hipMalloc((void**)&b->d_p0par, N * sizeof(vp8g_p0_par)));
+    }
+    run_tails(b, n, 3);
+    uint32_t nh_max = 0;
+    for (int f = 0; f < n; ++f)
+      if (b->h_p0par[f].nhdr != 0xffffffffu && b->h_p0par[f].nhdr > nh_max) nh_max = b->h_p0par[f].nhdr;
+    CHK(hipMemcpy2DAsync(b->d_p0hdr, VP8G_P0_HDR_CAP * sizeof(uint16_t), b->h_p0hdr,
+                         VP8G_P0_HDR_CAP * sizeof(uint16_t), nh_max * sizeof(uint16_t) + 2, n,
+                         hipMemcpyHostToDevice, st));
+    CHK(hipMemcpyAsync(b->d_p0par, b->h_p0par, n * sizeof(vp8g_p0_par), hipMemcpyHostToDevice, st));
+  }
+  const int nst = ns + (p0dev ? n : 0);   /* K4 streams: partitions, then partition 0 */
   if (!b->host_emit) {   /* K4 on the device, sized from the token counts */
+    const int rows = rows_mode(b) && np == 1;
     uint32_t max_ntok = 0, max_seg = 0;
     size_t segs = 0, words = 0;
-    for (int s = 0; s < ns; ++s) {
+    for (int s = ns; s < nst; ++s) {   /* partition 0: k_p0_modes sets ntok / nseg */
+      const int f = s - ns;
+      vp8g_emit_meta* m = &b->h_emeta[s];
+      const uint32_t bound = (uint32_t)(b->p0_cap - VP8G_EMIT_SEG);
+      m->ntok = bound;
+      m->frame = (uint32_t)f;
+      m->nrows = 0;
+      m->rowcap = 0;
+      m->pad = 0;
+      m->tok_off = (uint64_t)b->max_frames * b->tok_cap + (uint64_t)f * b->p0_cap;
+      m->nseg = (bound + VP8G_EMIT_SEG - 1) / VP8G_EMIT_SEG;
+    }
+    for (int s = 0; s < nst; ++s) {
+      if (s >= ns) {   /* partition 0 (bounds; its meta fields above) */
+        vp8g_emit_meta* m = &b->h_emeta[s];
+        m->seg_base = (uint32_t)segs;
+        m->nb_base = (uint32_t)words;
+        m->S = m->L = 0;
+        segs += m->nseg;
+        words += (7 * (size_t)m->ntok + 17 + 8 + 63) / 32 + 4;
+        if (m->ntok > max_ntok) max_ntok = m->ntok;
+        if (m->nseg > max_seg) max_seg = m->nseg;
+        continue;
+      }
       const int f = s / np, p = s % np;
       vp8g_emit_meta* m = &b->h_emeta[s];
       const uint32_t* pi = np > 1 ? b->h_pinfo + 16 * (size_t)f : NULL;
@@ -1211,9 +1327,13 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
       const int ok = !b->h_results[f].error && !(pi && pi[0] == 0xffffffffu);
       m->ntok = !ok ? 0 : pi ? pi[8 + p] : b->h_results[f].ntokens;
       m->frame = (uint32_t)f;
-      m->reserved = 0;
+      /* the token loop's streams lie in K3's token rows (k_emit_desc cuts them
+         row by row: the count below is a bound, set exactly on the device) */
+      m->nrows = rows && ok ? (uint32_t)b->mbh : 0;
+      m->rowcap = rows ? (uint32_t)b->rowcap : 0;
+      m->pad = 0;
       m->tok_off = (uint64_t)f * b->tok_cap + (ok && pi ? pi[p] : 0);
-      m->nseg = (m->ntok + VP8G_EMIT_SEG - 1) / VP8G_EMIT_SEG;
+      m->nseg = (m->ntok + VP8G_EMIT_SEG - 1) / VP8G_EMIT_SEG + (ok ? m->nrows : 0);
       m->seg_base = (uint32_t)segs;
       m->nb_base = (uint32_t)words;
       m->S = m->L = 0;
@@ -1224,10 +1344,12 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
     }
     if (segs > b->emit_seg_cap) {
       hipFree(b->d_emap); hipFree(b->d_eshift); hipFree(b->d_esegs); hipFree(b->d_eimg);
-      b->d_emap = NULL; b->d_eshift = NULL; b->d_esegs = NULL; b->d_eimg = NULL;
+      hipFree(b->d_edesc);
+      b->d_emap = NULL; b->d_eshift = NULL; b->d_esegs = NULL; b->d_eimg = NULL; b->d_edesc = NULL;
       b->emit_seg_cap = 0;
       const size_t cap = segs + segs / 4 + 64;
       CHK(hipMalloc((void**)&b->d_emap, cap * 128));
+      CHK(hipMalloc((void**)&b->d_edesc, cap * sizeof(vp8g_emit_desc)));
       CHK(hipMalloc((void**)&b->d_eshift, cap * 128 * sizeof(uint16_t)));
       CHK(hipMalloc((void**)&b->d_esegs, cap * sizeof(vp8g_emit_seg)));
       CHK(hipMalloc((void**)&b->d_eimg, cap * 17));
@@ -1242,17 +1364,21 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
     }
     CHK(hipEventRecord(b->ev[5], st));
     CHK(hipMemsetAsync(b->d_nbuf, 0, words * sizeof(uint32_t), st));
-    CHK(hipMemcpyAsync(b->d_emeta, b->h_emeta, ns * sizeof(vp8g_emit_meta),
+    CHK(hipMemcpyAsync(b->d_emeta, b->h_emeta, nst * sizeof(vp8g_emit_meta),
                        hipMemcpyHostToDevice, st));
-    if (!vp8g_launch_emit(b->d_tokens, b->tok_cap, ns, b->d_results, b->d_emeta, max_ntok,
-                          max_seg, b->d_emap, b->d_eshift, b->d_eimg, b->d_esegs, b->d_nbuf,
-                          b->d_psize, st))
+    if (p0dev && !vp8g_launch_p0_modes(b->d_mbinfo, b->mbw, b->mbh, n, b->d_p0par, b->d_p0hdr,
+                                       b->d_tokens, b->d_emeta, ns, st))
+      return 0;
+    if (!vp8g_launch_emit(b->d_tokens, b->tok_cap, nst, b->d_results, b->d_emeta, b->d_rowtok,
+                          max_ntok, max_seg, b->d_emap, b->d_eshift, b->d_eimg, b->d_edesc,
+                          b->d_esegs, b->d_nbuf, b->d_psize, st))
       return 0;
     CHK(hipEventRecord(b->ev[4], st));
-    CHK(hipMemcpyAsync(b->h_psize, b->d_psize, ns * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    /* partition 0 on the host threads while K4 runs on the device */
-    tail_spawn(&head, b, n, 0, b->threads - 1);
-    head_running = 1;
+    CHK(hipMemcpyAsync(b->h_psize, b->d_psize, nst * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    if (!p0dev) {   /* partition 0 on the host threads while K4 runs on the device */
+      tail_spawn(&head, b, n, 0, b->threads - 1);
+      head_running = 1;
+    }
     CHK(hipStreamSynchronize(st));
   }
   t3 = now_us();
@@ -1276,11 +1402,11 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
     /* one packed D2H of every frame's token partitions (k_pack) */
     uint32_t max_size = 0;
     b->h_poff[0] = 0;
-    for (int s = 0; s < ns; ++s) {
+    for (int s = 0; s < nst; ++s) {
       b->h_poff[s + 1] = b->h_poff[s] + ((b->h_psize[s] + 15u) & ~15u);
       if (b->h_psize[s] > max_size) max_size = b->h_psize[s];
     }
-    const size_t total = b->h_poff[ns];
+    const size_t total = b->h_poff[nst];
     if (total > b->h_part_cap) {
       hipHostFree(b->h_part);
       b->h_part = NULL;
@@ -1298,9 +1424,9 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
       b->d_part_cap = cap;
     }
     if (total) {
-      CHK(hipMemcpyAsync(b->d_poff, b->h_poff, (ns + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
+      CHK(hipMemcpyAsync(b->d_poff, b->h_poff, (nst + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
                          st));
-      if (!vp8g_launch_pack(b->d_tokens, b->d_emeta, ns, b->d_poff, b->d_psize, max_size, b->d_part,
+      if (!vp8g_launch_pack(b->d_tokens, b->d_emeta, nst, b->d_poff, b->d_psize, max_size, b->d_part,
                             st))
         goto fail;
       CHK(hipStreamSynchronize(st));   /* then the bytes come back on a copy engine */
@@ -1313,7 +1439,7 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   if (head_running) {
     tail_join(&head);
     head_running = 0;
-  } else {
+  } else if (!p0dev) {
     run_tails(b, n, 0);
   }
   const double t4b = now_us();
@@ -1458,15 +1584,33 @@ static int byte_is_pinned(const void* p) {
   return at.type == hipMemoryTypeHost;
 }
 
-/* the whole range [p, p + n) page-locked: its first and last byte and one
- * byte every 64 MB between (a caller may have hipHostRegister-ed only part
- * of a buffer; the SDMA engine must not read pageable pages) */
+/* the whole range [p, p + n) page-locked (a caller may have hipHostRegister-ed
+ * only part of a buffer, or several pieces of it; the SDMA engine must not
+ * read pageable pages): walk the registrations that cover it, from each one's
+ * start address and size, until the range is covered -- a gap, or a byte HIP
+ * does not know, means pageable. Should the runtime not report a range
+ * (older runtimes), every 64 MB and the last byte are sampled instead. */
 static int host_is_pinned(const void* p, size_t n) {
   const uint8_t* c = (const uint8_t*)p;
-  if (n == 0) return byte_is_pinned(c);
-  for (size_t o = 0; o < n; o += (size_t)64 << 20)
-    if (!byte_is_pinned(c + o)) return 0;
-  return byte_is_pinned(c + n - 1);
+  const uint8_t* end = c + (n ? n : 1);
+  while (c < end) {
+    if (!byte_is_pinned(c)) return 0;
+    void* base = NULL;
+    size_t size = 0;
+    if (hipPointerGetAttribute(&base, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
+                               (hipDeviceptr_t)(uintptr_t)c) != hipSuccess ||
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE,
+                               (hipDeviceptr_t)(uintptr_t)c) != hipSuccess ||
+        !base || size == 0 || (const uint8_t*)base > c ||
+        (const uint8_t*)base + size <= c) {
+      (void)hipGetLastError();
+      for (size_t o = (size_t)(c - (const uint8_t*)p); o < n; o += (size_t)64 << 20)
+        if (!byte_is_pinned((const uint8_t*)p + o)) return 0;
+      return byte_is_pinned(end - 1);
+    }
+    c = (const uint8_t*)base + size;   /* the next registration, if any, starts here */
+  }
+  return 1;
 }
 
 /* Encode n frames from host memory; with `next` (pinned, same geometry),

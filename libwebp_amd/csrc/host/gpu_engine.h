@@ -73,15 +73,15 @@ struct WebPGpuBatch {
   uint8_t* d_segmap;
   vp8g_frame_params* d_params;
   uint16_t* d_tokens;         /* per-frame compact streams, stride tok_cap tokens */
-  /* token arena of the token loop (methods 3-6 without low_memory): K3
-   * writes each MB's tokens once into it and k_gather_tokens lays out the
-   * streams (allocated on first use, grown when a launch runs out) */
-  uint16_t* d_arena;
-  size_t arena_cap;          /* tokens (a sink of VP8G_MAX_TOKENS_PER_MB follows) */
-  unsigned long long* d_arena_top;
-  int tiny_tokens;   /* WEBP_AMD_TEST_TINY_TOKENS=1 (tests): tiny initial token buffers */
-  uint32_t* d_mbpos;
-  uint8_t* d_rerun_snap;     /* d_rerun before a pass that re-reads it (arena re-runs) */
+  /* token rows of the token loop (methods 3-6 without low_memory): K3
+   * writes each MB's tokens once, row y of frame f at d_tokens + f * tok_cap
+   * + y * rowcap, and K4 reads them there (vp8g_rows; grown when a row runs
+   * out of room) */
+  size_t rowcap;
+  uint32_t* d_rowtok;        /* n x mbh row token counts */
+  uint32_t* h_rowtok;
+  int tiny_tokens;   /* WEBP_AMD_TEST_TINY_TOKENS=1 (tests): tiny initial token rows */
+  uint8_t* d_rerun_snap;     /* d_rerun before a pass that re-reads it (regrow re-runs) */
   uint8_t* d_mbinfo;
   uint32_t* d_mboff;         /* K3 scratch: compact-stream offset per MB */
   uint8_t* d_rerun;          /* K3 cost state carried from pass to pass */
@@ -114,6 +114,7 @@ struct WebPGpuBatch {
   uint32_t* h_pinfo;
   vp8g_emit_meta* h_emeta;
   uint8_t* d_emap;           /* K4 scratch, grown on demand */
+  vp8g_emit_desc* d_edesc;   /* K4 segment descriptors */
   uint16_t* d_eshift;
   uint8_t* d_eimg;           /* possible start ranges per segment (17 B each) */
   vp8g_emit_seg* d_esegs;
@@ -143,6 +144,17 @@ struct WebPGpuBatch {
   uint8_t* d_part;           /* packed partition-1 bytes (k_pack), grown on demand */
   size_t d_part_cap;
   vp8h_bw* p0;               /* partition 0 of each frame, coded while K4 runs */
+  /* partition 0 as K4 streams (k_p0_modes; gpu_p0): the header tokens per
+     frame (host-built, pinned) and k_p0_modes' parameters; the streams' tokens
+     follow the frames' token slabs in d_tokens (p0_cap tokens per frame) */
+  int gpu_p0;                /* 0 host, 1 device, -1 by the rank's thread budget */
+  int p0_dev;                /* the last call put partition 0 on the device */
+  int last_ns;               /* its token-partition streams (partition 0 follows) */
+  size_t p0_cap;
+  uint16_t* h_p0hdr;
+  uint16_t* d_p0hdr;
+  vp8g_p0_par* h_p0par;
+  vp8g_p0_par* d_p0par;
   uint16_t* h_tokens;
   size_t* tok_off;
   vp8h_frame* frames;

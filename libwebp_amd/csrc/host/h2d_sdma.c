@@ -18,6 +18,7 @@
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #include <pthread.h>
+#include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -154,3 +155,23 @@ int d2h_sdma_download(int device, void* dst, const void* src, size_t bytes) {
   dev_agents* d = &g_dev[device];
   return sdma_copy(&d->down, dst, d->cpu, src, d->gpu, bytes);
 }
+
+/* GPU memory-fault report (diagnostics, WEBP_AMD_FAULT_REPORT=1): the
+ * runtime's memory-fault event carries the faulting virtual address and the
+ * reason; HIP itself only returns "an illegal memory access". Printed to
+ * stderr next to the engines' buffer ranges (gpu_batch.c), it names the
+ * buffer (or none) an access went out of. */
+static hsa_status_t fault_event(const hsa_amd_event_t* ev, void* data) {
+  (void)data;
+  if (ev->event_type == HSA_AMD_GPU_MEMORY_FAULT_EVENT)
+    fprintf(stderr, "WEBP_AMD_FAULT address 0x%llx reason 0x%x\n",
+            (unsigned long long)ev->memory_fault.virtual_address,
+            (unsigned)ev->memory_fault.fault_reason_mask);
+  return HSA_STATUS_SUCCESS;
+}
+static pthread_once_t g_fault_once = PTHREAD_ONCE_INIT;
+static void fault_init(void) {
+  if (hsa_amd_register_system_event_handler(fault_event, NULL) != HSA_STATUS_SUCCESS)
+    fprintf(stderr, "WEBP_AMD_FAULT report: handler not registered\n");
+}
+void vp8g_fault_report_init(void) { pthread_once(&g_fault_once, fault_init); }

@@ -19,4 +19,7 @@ void h2d_sdma_finish(uint64_t handle);
  * The caller has drained the stream that produced `src`. */
 int d2h_sdma_download(int device, void* dst, const void* src, size_t bytes);
 
+/* WEBP_AMD_FAULT_REPORT=1: print GPU memory faults (address, reason) to stderr */
+void vp8g_fault_report_init(void);
+
 #endif

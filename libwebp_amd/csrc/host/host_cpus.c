@@ -208,13 +208,17 @@ int vp8g_rank_threads(int device) {
   return n < 1 ? 1 : (int)n;
 }
 
-/* One persistent pool of host threads per device (so per rank): budget - 1
- * threads pinned like vp8g_thread_create, fed from a queue of jobs. A job
+/* One persistent pool of host threads per process (a rank is one process
+ * per GPU, so per rank): budget - 1 threads pinned like vp8g_thread_create
+ * for the first device that submits work, fed from a queue of jobs. A job
  * is n independent items (one frame each); any idle pool thread takes items
  * of the oldest job that still has some, up to the job's width at once, and
  * the submitting thread takes items too when it joins. The pool is
  * work-conserving (one engine alone gets every thread, several share them)
- * and never holds more threads than the budget, however many engines. */
+ * and never holds more threads than the budget, however many engines -- or
+ * devices: a process that drives several GPUs shares the one pool between
+ * them instead of starting a full-budget pool per device, which would
+ * oversubscribe the quota by the device count. */
 typedef struct {
   pthread_mutex_t lock;
   pthread_cond_t work, done;
@@ -222,7 +226,7 @@ typedef struct {
   int started, nthreads, busy;
 } DevPool;
 
-static DevPool g_pool[MAX_DEV];
+static DevPool g_pool;
 static pthread_mutex_t g_pools_lock = PTHREAD_MUTEX_INITIALIZER;
 
 static int pool_size(int device) {
@@ -259,7 +263,7 @@ static void* pool_thread(void* arg) {
 
 static DevPool* pool_get(int device) {
   if (device < 0 || device >= MAX_DEV) device = 0;
-  DevPool* P = &g_pool[device];
+  DevPool* P = &g_pool;
   pthread_mutex_lock(&g_pools_lock);
   if (!P->started) {
     pthread_mutex_init(&P->lock, NULL);
@@ -323,10 +327,10 @@ int WebPGpuHostThreadBudget(int device, int* busy) {
   const int n = pool_size(device);
   if (busy) {
     *busy = 0;
-    if (device >= 0 && device < MAX_DEV && g_pool[device].started) {
-      pthread_mutex_lock(&g_pool[device].lock);
-      *busy = g_pool[device].busy;
-      pthread_mutex_unlock(&g_pool[device].lock);
+    if (g_pool.started) {
+      pthread_mutex_lock(&g_pool.lock);
+      *busy = g_pool.busy;
+      pthread_mutex_unlock(&g_pool.lock);
     }
   }
   return n;

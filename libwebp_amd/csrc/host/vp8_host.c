@@ -633,7 +633,7 @@ void vp8h_bw_init(vp8h_bw* bw, size_t expected) {
 }
 
 void vp8h_bw_free(vp8h_bw* bw) {
-  free(bw->buf);
+  if (bw->cap) free(bw->buf);   /* cap 0: the bytes are borrowed (K4's packed output) */
   bw->buf = NULL;
   bw->cap = bw->pos = 0;
 }
@@ -686,11 +686,6 @@ static inline int bw_put_uniform(vp8h_bw* bw, int bit) { return bw_put(bw, bit, 
 
 static void bw_put_bits(vp8h_bw* bw, uint32_t v, int n) {
   for (uint32_t m = 1u << (n - 1); m; m >>= 1) bw_put_uniform(bw, (v & m) != 0);
-}
-static void bw_put_signed(vp8h_bw* bw, int v, int n) {
-  if (!bw_put_uniform(bw, v != 0)) return;
-  if (v < 0) bw_put_bits(bw, ((uint32_t)(-v) << 1) | 1, n + 1);
-  else bw_put_bits(bw, (uint32_t)v << 1, n + 1);
 }
 
 void vp8h_bw_finish(vp8h_bw* bw) {
@@ -833,8 +828,30 @@ static void put_le32(uint8_t* p, uint32_t v) {
   p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
 }
 
-int vp8h_build_p0(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* mbinfo,
-                  vp8h_bw* out0, int* hdr_bytes) {
+/* The frame header part of partition 0 (syntax_enc.c:187-245 PutSegmentHeader
+ * .. PutQuant, tree_enc.c:485-504 VP8WriteProbas, the skip probability) as
+ * fixed-probability K4 tokens (bit << 15 | 0x4000 | probability): coded here
+ * by vp8h_build_p0, or appended to by k_p0_modes and coded by K4. */
+typedef struct {
+  uint16_t* t;
+  int n, cap;
+} p0_hdr;
+static inline int hput(p0_hdr* h, int bit, int prob) {
+  if (h->n < h->cap) h->t[h->n] = (uint16_t)((bit ? 0x8000u : 0u) | 0x4000u | (unsigned)prob);
+  ++h->n;
+  return bit;
+}
+static void hput_bits(p0_hdr* h, uint32_t v, int n) {   /* VP8PutBits */
+  for (uint32_t m = 1u << (n - 1); m; m >>= 1) hput(h, (v & m) != 0, 128);
+}
+static void hput_signed(p0_hdr* h, int v, int n) {      /* VP8PutSignedBits */
+  if (!hput(h, v != 0, 128)) return;
+  if (v < 0) hput_bits(h, ((uint32_t)(-v) << 1) | 1, n + 1);
+  else hput_bits(h, (uint32_t)v << 1, n + 1);
+}
+
+int vp8h_p0_header(vp8h_frame* fr, const vp8g_frame_result* res, uint16_t* tok, int cap,
+                   int* hdr_bytes0) {
   /* VP8AdjustFilterStrength (filter_enc.c:194-233): with the autofilter the
    * engine has already set seg_fstrength from the SSIM statistics */
   if (!fr->autofilter && fr->filter_strength > 0) {
@@ -847,45 +864,71 @@ int vp8h_build_p0(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* m
     }
     fr->f_level = max_level;
   }
-  vp8h_bw bw;
-  vp8h_bw_init(&bw, (size_t)fr->mbw * fr->mbh * 7 / 8 + 1024);
-  *out0 = bw;   /* handed back even on error so the caller can free it */
-  bw_put_uniform(&bw, 0);   /* colorspace */
-  bw_put_uniform(&bw, 0);   /* clamping type */
-  if (bw_put_uniform(&bw, fr->num_segments > 1)) {
-    bw_put_uniform(&bw, fr->update_map);
-    bw_put_uniform(&bw, 1);   /* update segment feature data */
-    bw_put_uniform(&bw, 1);   /* absolute values */
-    for (int s = 0; s < 4; ++s) bw_put_signed(&bw, fr->seg_quant[s], 7);
-    for (int s = 0; s < 4; ++s) bw_put_signed(&bw, fr->seg_fstrength[s], 6);
+  p0_hdr h = {tok, 0, cap}, *H = &h;
+  hput(H, 0, 128);   /* colorspace */
+  hput(H, 0, 128);   /* clamping type */
+  if (hput(H, fr->num_segments > 1, 128)) {
+    hput(H, fr->update_map, 128);
+    hput(H, 1, 128);   /* update segment feature data */
+    hput(H, 1, 128);   /* absolute values */
+    for (int s = 0; s < 4; ++s) hput_signed(H, fr->seg_quant[s], 7);
+    for (int s = 0; s < 4; ++s) hput_signed(H, fr->seg_fstrength[s], 6);
     if (fr->update_map)
       for (int s = 0; s < 3; ++s)
-        if (bw_put_uniform(&bw, fr->seg_probas[s] != 255u)) bw_put_bits(&bw, fr->seg_probas[s], 8);
+        if (hput(H, fr->seg_probas[s] != 255u, 128)) hput_bits(H, fr->seg_probas[s], 8);
   }
-  bw_put_uniform(&bw, fr->f_simple);
-  bw_put_bits(&bw, (uint32_t)fr->f_level, 6);
-  bw_put_bits(&bw, (uint32_t)fr->f_sharpness, 3);
-  bw_put_uniform(&bw, 0);          /* no loop-filter deltas */
-  bw_put_bits(&bw, fr->num_parts == 8 ? 3 : fr->num_parts == 4 ? 2 : fr->num_parts == 2 ? 1 : 0,
-              2);                  /* token partitions (syntax_enc.c:283-285) */
-  bw_put_bits(&bw, (uint32_t)fr->base_quant, 7);
-  bw_put_signed(&bw, 0, 4);        /* dq_y1_dc */
-  bw_put_signed(&bw, 0, 4);        /* dq_y2_dc */
-  bw_put_signed(&bw, 0, 4);        /* dq_y2_ac */
-  bw_put_signed(&bw, fr->dq_uv_dc, 4);
-  bw_put_signed(&bw, fr->dq_uv_ac, 4);
-  bw_put_uniform(&bw, 0);          /* no probability refresh */
+  hput(H, fr->f_simple, 128);
+  hput_bits(H, (uint32_t)fr->f_level, 6);
+  hput_bits(H, (uint32_t)fr->f_sharpness, 3);
+  hput(H, 0, 128);          /* no loop-filter deltas */
+  hput_bits(H, fr->num_parts == 8 ? 3 : fr->num_parts == 4 ? 2 : fr->num_parts == 2 ? 1 : 0,
+            2);             /* token partitions (syntax_enc.c:283-285) */
+  hput_bits(H, (uint32_t)fr->base_quant, 7);
+  hput_signed(H, 0, 4);     /* dq_y1_dc */
+  hput_signed(H, 0, 4);     /* dq_y2_dc */
+  hput_signed(H, 0, 4);     /* dq_y2_ac */
+  hput_signed(H, fr->dq_uv_dc, 4);
+  hput_signed(H, fr->dq_uv_ac, 4);
+  hput(H, 0, 128);          /* no probability refresh */
   const uint8_t* p0 = &kVP8CoeffProba0[0][0][0][0];
   const uint8_t* pu = &kVP8CoeffUpdateProba[0][0][0][0];
   for (int s = 0; s < VP8G_NUM_SLOTS; ++s) {
     const int v = res->probas[s];
-    if (bw_put(&bw, v != p0[s], pu[s])) bw_put_bits(&bw, (uint32_t)v, 8);
+    if (hput(H, v != p0[s], pu[s])) hput_bits(H, (uint32_t)v, 8);
   }
   /* skip probability (tree_enc.c:500-502): only the RD_OPT_NONE loop uses it */
-  const int use_skip = res->use_skip != 0;
-  if (bw_put_uniform(&bw, use_skip)) bw_put_bits(&bw, (uint32_t)res->skip_proba, 8);
+  if (hput(H, res->use_skip != 0, 128)) hput_bits(H, (uint32_t)res->skip_proba, 8);
+  if (h.n > cap) return -1;
+  if (hdr_bytes0) {   /* the bytes the coder has written after the header (WebPAuxStats) */
+    vp8h_bw bw;
+    vp8h_bw_init(&bw, 2048);
+    vp8h_emit_tokens(&bw, tok, (size_t)h.n, NULL);
+    *hdr_bytes0 = bw.error ? 0 : (int)bw.pos;
+    vp8h_bw_free(&bw);
+  }
+  return h.n;
+}
+
+void vp8h_p0_par(const vp8h_frame* fr, const vp8g_frame_result* res, int nhdr, vp8g_p0_par* p) {
+  memset(p, 0, sizeof(*p));
+  p->nhdr = nhdr < 0 ? 0xffffffffu : (uint32_t)nhdr;
+  p->update_map = (uint8_t)(fr->update_map != 0);
+  p->use_skip = (uint8_t)(res->use_skip != 0);
+  p->skip_proba = (uint8_t)res->skip_proba;
+  for (int s = 0; s < 3; ++s) p->seg_probas[s] = fr->seg_probas[s];
+}
+
+int vp8h_build_p0(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* mbinfo,
+                  vp8h_bw* out0, int* hdr_bytes) {
+  uint16_t tok[VP8G_P0_HDR_CAP];
+  vp8h_bw bw;
+  vp8h_bw_init(&bw, (size_t)fr->mbw * fr->mbh * 7 / 8 + 1024);
+  *out0 = bw;   /* handed back even on error so the caller can free it */
+  const int nh = vp8h_p0_header(fr, res, tok, VP8G_P0_HDR_CAP, NULL);
+  if (nh < 0) return VP8_ENC_ERROR_OUT_OF_MEMORY;
+  vp8h_emit_tokens(&bw, tok, (size_t)nh, NULL);
   const size_t hdr_pos = bw.pos;
-  code_intra_modes(&bw, fr, mbinfo, use_skip, res->skip_proba);
+  code_intra_modes(&bw, fr, mbinfo, res->use_skip != 0, res->skip_proba);
   vp8h_bw_finish(&bw);
   *out0 = bw;
   if (hdr_bytes) { hdr_bytes[0] = (int)hdr_pos; hdr_bytes[1] = (int)(bw.pos - hdr_pos); }

@@ -147,6 +147,13 @@ void vp8h_emit_tokens(vp8h_bw* bw, const uint16_t* tokens, size_t n, const uint8
  * coded while K4 codes partition 1; the RIFF write joins them. */
 int vp8h_build_p0(vp8h_frame* fr, const vp8g_frame_result* res, const uint8_t* mbinfo,
                   vp8h_bw* p0, int* hdr_bytes);
+/* partition 0's frame header as fixed-probability tokens (at most cap; -1
+ * if more), after VP8AdjustFilterStrength; *hdr_bytes0 (if not NULL): the
+ * bytes a coder has written after them (WebPAuxStats header_bytes[0]) */
+int vp8h_p0_header(vp8h_frame* fr, const vp8g_frame_result* res, uint16_t* tok, int cap,
+                   int* hdr_bytes0);
+/* what k_p0_modes needs of the frame (nhdr < 0: no stream) */
+void vp8h_p0_par(const vp8h_frame* fr, const vp8g_frame_result* res, int nhdr, vp8g_p0_par* p);
 /* ALPH chunk payload: header byte (compression | filter << 2 | levels << 4,
  * alpha_enc.c:168-170) and the data (bare VP8L stream or raw plane) */
 typedef struct {

@@ -27,10 +27,8 @@ extern "C" {
 #define VP8G_NUM_SLOTS 1056        /* 4 types x 8 bands x 3 ctx x 11 probas */
 #define VP8G_MBINFO_BYTES 20       /* type, uv_mode, segment, skip, modes[16] */
 #define VP8G_MAX_TOKENS_PER_MB 7680 /* 25 blocks x 16 coeffs x 19 tokens + EOBs */
-/* token arena (K3 with an arena): tokens per chunk a worker takes at a time,
- * and the frame error bit of a launch whose arena ran out (the host grows the
- * arena and runs the pass again) */
-#define VP8G_ARENA_CHUNK (128 * 1024)
+/* the frame error bit of a launch whose token rows ran out of room (the
+ * host grows the rows and runs the pass again; see vp8g_rows) */
 #define VP8G_ERR_ARENA 0x100
 
 /* one quantiser matrix, src/enc/vp8i_enc.h:181-187 */
@@ -142,40 +140,32 @@ int vp8g_launch_analysis(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int 
                          int n, uint8_t* mb_alpha, uint16_t* mb_uva, int fast_q,
                          uint8_t* mb_amode, void* stream);
 
-/* K3: RD search + tokens. Each frame's tokens end up as one compact stream
- * at the start of its tok_cap region (per-MB slots of
- * VP8G_MAX_TOKENS_PER_MB are used as scratch); mboff is scratch of n * nmb
- * uint32 (each MB's offset in the compact stream). trellis != 0 reserves the
+/* K3: RD search + tokens. Without rows, each frame's tokens end up as one
+ * compact stream at the start of its tok_cap region (per-MB slots of
+ * VP8G_MAX_TOKENS_PER_MB are used as scratch; mboff is scratch of n * nmb
+ * uint32, each MB's offset in the compact stream). trellis != 0 reserves the
  * trellis LDS (method >= 5). recon (n x nmb x 512 bytes, or NULL) receives
  * each MB's reconstruction in the 32-byte-stride layout of the reference's
  * yuv_out_ (Y | U | V side by side, src/enc/vp8i_enc.h:72-78) for the
- * autofilter. */
-/* the token arena of a K3 launch (see vp8g_launch_encode): cap tokens plus
- * a sink of VP8G_MAX_TOKENS_PER_MB behind them, the bump pointer (reset by
- * the launch) and n x nmb MB positions */
+ * autofilter.
+ * With rows (the token loop): every token is written once, where K4 reads
+ * it -- MB row y of frame f at tokens + f * tok_cap + y * rowcap, its MBs'
+ * tokens one after another in raster order (the row's owner knows its own
+ * offsets; only the frame-wide stream offsets wait for the rows above, and
+ * nothing needs them). The row's count goes to rowtok[f * mbh + y]; a row that
+ * would pass rowcap writes nothing more and the frame reports VP8G_ERR_ARENA
+ * (the host grows rowcap and runs the launch again). mboff is not written. */
 typedef struct {
-  uint16_t* tokens;
-  uint32_t cap;
-  unsigned long long* top;   /* 64-bit bump pointer: cannot wrap past cap */
-  uint32_t* mbpos;
-} vp8g_arena;
+  uint32_t rowcap;           /* tokens per MB row (a multiple of 8) */
+  uint32_t* rowtok;          /* n x mbh row token counts */
+} vp8g_rows;
 
 int vp8g_launch_encode(const uint8_t* yuv, size_t yuv_frame_bytes, int w, int h,
                        int n, const uint8_t* segmap,
                        const vp8g_frame_params* params, uint16_t* tokens,
                        size_t tok_cap, uint8_t* mbinfo, uint32_t* mboff, int trellis,
                        vp8g_frame_result* results, uint8_t* rerun_state, uint8_t* recon,
-                       uint8_t* xsync, uint32_t* wsnap, const vp8g_arena* arena,
-                       void* stream);
-
-/* With an arena, K3 writes every MB's tokens once into the arena and the
- * frames' compact streams are laid out by this gather (frame f at tokens +
- * f * tok_cap; frames with ntokens > tok_cap, errors or pass_mode 2 are
- * skipped). Without one, K3 writes per-MB slots of VP8G_MAX_TOKENS_PER_MB and
- * compacts each frame's stream itself. */
-int vp8g_launch_gather(uint16_t* tokens, size_t tok_cap, const uint16_t* arena,
-                       const uint32_t* mbpos, const uint32_t* mboff, int w, int h, int n,
-                       const vp8g_frame_params* params, const vp8g_frame_result* results,
+                       uint8_t* xsync, uint32_t* wsnap, const vp8g_rows* rows,
                        void* stream);
 
 /* K3X: when a launch has few frames (n <= VP8G_XSPLIT_MAX_FRAMES) and xsync
@@ -232,25 +222,37 @@ int vp8g_launch_lowmem(uint16_t* tokens, size_t tok_cap, const uint32_t* mboff,
                        const int32_t* nb_stat, const uint8_t* active, int mode, uint32_t* stats,
                        int32_t* nskip, void* stream);
 
-/* VP8EstimateTokenSize (token_enc.c:226-247) of each frame's compact token
- * stream under the probabilities at state + f * VP8G_RERUN_STATE_BYTES +
- * VP8G_STATE_COEFFS; frames with active[f] == 0 are skipped. bits[f] (device,
- * zeroed here) receives the sum in 1/256 bit. */
-int vp8g_launch_token_cost(const uint16_t* tokens, size_t tok_cap, int n,
+/* VP8EstimateTokenSize (token_enc.c:226-247) of each frame's token stream
+ * (compact, or with rows != NULL in K3's token rows) under the probabilities
+ * at state + f * VP8G_RERUN_STATE_BYTES + VP8G_STATE_COEFFS; frames with
+ * active[f] == 0 are skipped. bits[f] (device, zeroed here) receives the sum
+ * in 1/256 bit. */
+int vp8g_launch_token_cost(const uint16_t* tokens, size_t tok_cap, const vp8g_rows* rows, int mbh,
+                           int n,
                            const vp8g_frame_result* results, const uint8_t* state,
                            const uint8_t* active, unsigned long long* bits, void* stream);
 
 /* K4: boolean coder for the token partitions, parallel inside each stream
- * (hip/vp8_emit.hip). A stream is one token partition of one frame: its
- * tokens start at tokens + tok_off (a multiple of 8 tokens) and take their
- * probabilities from results[frame]; the coded bytes replace them there.
- * Per-stream bookkeeping: ntok, the segment count and the first segment /
+ * (hip/vp8_emit.hip). A stream is one token partition of one frame (or its
+ * partition 0): its tokens take their probabilities from results[frame] and
+ * lie either compact at tokens + tok_off (a multiple of 8 tokens; nrows 0)
+ * or in nrows token rows (vp8g_rows) from tokens + tok_off, rowcap apart,
+ * their lengths in rowtok[frame * nrows ..]; the coded bytes go to tokens +
+ * tok_off. The stream is cut into segments of at most VP8G_EMIT_SEG tokens
+ * that never cross a row (k_emit_desc: vp8g_emit_desc per segment).
+ * Per-stream bookkeeping: ntok, the segment count (an upper bound from the
+ * host for row streams, set exactly on the device) and the first segment /
  * first N-array word of the stream (host), S and L (device). */
 typedef struct {
   uint32_t ntok, nseg, seg_base, nb_base, S, L;
-  uint32_t frame, reserved;
+  uint32_t frame, nrows;
   uint64_t tok_off;
+  uint32_t rowcap, pad;
 } vp8g_emit_meta;
+typedef struct {
+  uint64_t off;    /* the segment's first token: tokens + off (a multiple of 8) */
+  uint32_t len, pad;
+} vp8g_emit_desc;
 #define VP8G_MAX_PARTS 8   /* token partitions per frame (syntax_enc.c:283) */
 typedef struct {
   uint32_t T;      /* bit offset of the segment's part of N */
@@ -262,14 +264,40 @@ typedef struct {
 /* n streams; out_size[s] = the byte count of stream s */
 int vp8g_launch_emit(uint16_t* tokens, size_t tok_cap, int n,
                      const vp8g_frame_result* results, vp8g_emit_meta* meta,
-                     uint32_t max_ntok, uint32_t max_seg, uint8_t* emap, uint16_t* eshift,
-                     uint8_t* img, vp8g_emit_seg* segs, uint32_t* nbuf, uint32_t* out_size,
-                     void* stream);
+                     const uint32_t* rowtok, uint32_t max_ntok, uint32_t max_seg, uint8_t* emap,
+                     uint16_t* eshift, uint8_t* img, vp8g_emit_desc* desc, vp8g_emit_seg* segs,
+                     uint32_t* nbuf, uint32_t* out_size, void* stream);
 
 /* K4 alone on caller-given fixed-probability token streams (host memory in
  * and out; test hook, see hip/vp8_emit.hip) */
 int vp8g_emit_streams(const uint16_t* host_tokens, const uint32_t* ntok, int n, uint8_t* host_out,
                       uint32_t out_stride, uint32_t* out_size);
+
+/* Partition 0 as a K4 stream (syntax_enc.c:187-310, tree_enc.c:313-347,
+ * 485-504): the host turns each frame's header (segment / filter / quant
+ * headers, probability updates, skip probability) into fixed-probability
+ * tokens (vp8h_p0_header, at most VP8G_P0_HDR_CAP), k_p0_modes appends the
+ * per-MB segment ids, skip flags and intra modes from K3's mbinfo and K4
+ * codes the stream beside the token partitions. vp8g_p0_par carries what
+ * the MB part needs; the frame's p0 tokens start at tokens + tok_off of its
+ * stream (room for vp8g_p0_cap(nmb) tokens), and k_p0_modes writes the
+ * stream's ntok / nseg into its K4 meta. */
+#define VP8G_P0_HDR_CAP 10240   /* >= 2 + 59 + 21 + 7 + 30 + 1 + 1056 * 9 + 9 header tokens */
+typedef struct {
+  uint32_t nhdr;                /* header tokens; 0xffffffff: no stream (frame failed) */
+  uint8_t update_map, use_skip, skip_proba, pad;
+  uint8_t seg_probas[3], pad2;
+} vp8g_p0_par;
+/* tokens of one frame's partition 0: header + <= 119 per MB (2 segment,
+ * 1 skip, 1 + 16 x 7 luma, 3 chroma), + a K4 segment of slack, 8-aligned */
+static inline size_t vp8g_p0_cap(int nmb) {
+  return ((size_t)VP8G_P0_HDR_CAP + 119 * (size_t)nmb + VP8G_EMIT_SEG + 7) & ~(size_t)7;
+}
+/* n frames: frame f's stream is meta[meta_base + f], its header tokens at
+ * hdr + f * VP8G_P0_HDR_CAP */
+int vp8g_launch_p0_modes(const uint8_t* mbinfo, int mbw, int mbh, int n, const vp8g_p0_par* par,
+                         const uint16_t* hdr, uint16_t* tokens, vp8g_emit_meta* meta,
+                         int meta_base, void* stream);
 
 /* K4 tail: copy each stream's bytes (size[s] bytes at tokens +
  * meta[s].tok_off) to dst + off[s]; off[s] must be 16-byte aligned. */

@@ -59,3 +59,32 @@ def test_emit_streams_match_reference_coder():
         window_coder(toks, 2048, 32, carries)
         assert got[i] == want, (i, len(toks))
     assert carries.get("carries", 0) > 0   # the streams took the carry path
+
+
+def _run_rows(streams, rowlen):
+    """The same streams laid out as K3's token rows (vp8g_emit_rows: rows of
+    rowlen tokens, rowcap = round8(rowlen) + 8 apart) and coded in place."""
+    lib = libwebp_amd.load()
+    f = lib.vp8g_emit_rows
+    f.restype = C.c_int
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]
+    flat = np.array([(b << 15) | (1 << 14) | p for s in streams for b, p in s], np.uint16)
+    ntok = np.array([len(s) for s in streams], np.uint32)
+    stride = int((7 * int(ntok.max()) + 48) // 8 + 16)
+    out = np.zeros((len(streams), stride), np.uint8)
+    size = np.zeros(len(streams), np.uint32)
+    assert f(flat.ctypes.data if flat.size else None, ntok.ctypes.data, len(streams), rowlen,
+             out.ctypes.data, stride, size.ctypes.data) == 1
+    return [out[i, :size[i]].tobytes() for i in range(len(streams))]
+
+
+@pytest.mark.parametrize("rowlen", [100, 255, 256, 1001, 2048, 2050, 5003])
+def test_emit_row_streams_match_reference_coder(rowlen):
+    """Row streams (the token loop's layout, tokens read where K3 wrote them):
+    segments cut per row, rows shorter than the 256-token look-back (the next
+    segment then starts from all 128 ranges), row ends off the 8-token grid
+    (the look-back read token by token), rows longer than a segment."""
+    streams = _streams()
+    got = _run_rows(streams, rowlen)
+    for i, toks in enumerate(streams):
+        assert got[i] == ref_coder(toks), (i, len(toks), rowlen)

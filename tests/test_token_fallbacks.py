@@ -1,13 +1,14 @@
-"""The two fallbacks of the token buffers (host/gpu_batch.c k3_settle), run
-on purpose: WEBP_AMD_TEST_TINY_TOKENS=1 starts an engine with a one-chunk
-token arena and 4096-token compact streams, so its first K3 launch runs out
-of arena (every worker past the first lands on the sink, VP8G_ERR_ARENA),
-K3 runs again from the saved pass state (d_rerun_snap) with an arena grown to
-the launch's token count, and the streams longer than tok_cap are laid out
-again by k_gather_tokens into a wider buffer. The bitstreams must equal the
-reference's known answers: the m4 survey KATs (K3 and K3X), an m6 sweep case
-(trellis kernel) and multi-pass size / PSNR searches (pass state restored
-before the re-run)."""
+"""The token rows' regrow (host/gpu_batch.c k3_settle), run on purpose:
+WEBP_AMD_TEST_TINY_TOKENS=1 starts an engine with token rows of 64 tokens,
+so in its first K3 launch every MB row runs out of room (K3 stops writing
+the row and reports VP8G_ERR_ARENA, counting the row's tokens on); the host
+reads the rows' counts, widens the rows to hold the longest, keeps the rows
+of the frames the launch skipped (a partition-0 re-run's final frames) and
+runs the launch again from the saved pass state (d_rerun_snap). The
+bitstreams must equal the reference's known answers: the m4 survey KATs (K3
+and K3X), an m6 sweep case (trellis kernel) and multi-pass size / PSNR
+searches (pass state restored before the re-run, the token-cost estimate
+read from the rows)."""
 import hashlib
 import json
 import os

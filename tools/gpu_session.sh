@@ -26,6 +26,21 @@ if has trace; then   # K3 per-worker wait / stage accounting (diagnostic build; 
   WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_tracecheck.so run timeout -k 10 150 \
     python3 tools/k3_trace.py 1920 1080 256 4 75 $O/k3_trace_256.json > $O/k3_trace_256.log 2>&1 || exit 1
 fi
+if has budget; then   # the 8-rank host budget on one GPU (quota 16 / 8 ranks = 2 threads) next
+  # to the whole-box budget, same box, default line (6 engines, host input); partition 0
+  # where the budget puts it (default) and forced to the other side
+  run timeout -k 10 300 python3 bench.py --no-cpu > $O/bench_budget16.json 2> $O/bench_budget16.err || exit 1
+  WEBP_AMD_CPU_QUOTA=16 LOCAL_WORLD_SIZE=8 run timeout -k 10 300 python3 bench.py --no-cpu \
+    > $O/bench_budget2.json 2> $O/bench_budget2.err || exit 1
+  WEBP_AMD_P0=gpu run timeout -k 10 300 python3 bench.py --no-cpu > $O/bench_budget16_p0gpu.json \
+    2> $O/bench_budget16_p0gpu.err || exit 1
+  WEBP_AMD_P0=host WEBP_AMD_CPU_QUOTA=16 LOCAL_WORLD_SIZE=8 run timeout -k 10 300 python3 bench.py \
+    --no-cpu > $O/bench_budget2_p0host.json 2> $O/bench_budget2_p0host.err || exit 1
+fi
+if has p0tests; then   # partition 0 on the device + the core parity tests
+  run timeout -k 10 400 python -u -m pytest tests/test_p0_device.py tests/test_gpu_parity.py -m gpu -x -v \
+    --timeout 200 --timeout-method thread > $O/gpu_p0tests.log 2>&1 || exit 1
+fi
 if has trace4; then   # the same for config 4 (one 4096^2 q90 m6 frame, K3X)
   WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_tracecheck.so run timeout -k 10 150 \
     python3 tools/k3_trace.py 4096 4096 1 6 90 $O/k3_trace_cfg4.json > $O/k3_trace_cfg4.log 2>&1 || exit 1
@@ -158,6 +173,20 @@ if has calib; then
   for C in FETCH_SIZE WRITE_SIZE; do
     run timeout -s KILL 60 rocprofv3 --pmc $C --output-format csv -d $O/calib_$C -o run \
       -- $R/tools/bin/pmc_calib > $O/calib_$C.log 2>&1 || exit 1
+  done
+fi
+# (last: these may fault the GPU, and nothing runs after a fault)
+cd $R
+if has tracebare; then   # the bare trace build (-DK3_TRACE) at 256 frames; the runtime's
+  # fault report (address, reason) with AMD_LOG_LEVEL=1. Last step: it may fault.
+  AMD_LOG_LEVEL=1 WEBP_AMD_FAULT_REPORT=1 WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_trace.so run timeout -k 10 150 \
+    python3 tools/k3_trace.py 1920 1080 256 4 75 $O/k3_trace_bare_256.json > $O/k3_trace_bare_256.log 2>&1 || exit 1
+fi
+if has tracediff; then   # bare trace builds of other K3 sources (make ab AB=<name>
+  # ABSRC=... ABFLAGS=-DK3_TRACE), in the order of $TRACE_ABS; stops at the first failure
+  for A in $TRACE_ABS; do
+    AMD_LOG_LEVEL=1 WEBP_AMD_FAULT_REPORT=1 WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_$A.so run timeout -k 10 150 \
+      python3 tools/k3_trace.py 1920 1080 256 4 75 $O/k3_trace_$A.json > $O/k3_trace_$A.log 2>&1 || exit 1
   done
 fi
 echo "session $TAG done" >> $O/steps.log

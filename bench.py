@@ -674,6 +674,10 @@ def lossy_line(args, world, B, W, H, elapsed, tails, total_bytes, ntok, solo=Non
     k3_s = avg(6) / 1e6
     k3_solo = solo[6] / 1e6 if solo else k3_s   # the roofline uses the uncontended time
     achieved = k3_bytes / k3_solo / 1e9 if k3_solo > 0 else 0.0
+    # SURVEY.md 8(d)'s unit: 7 W H + coded bytes per frame (RGBA read, YUV
+    # written and read back, the file), over the same K3 time
+    s8d_bytes = int(B * (7 * W * H + total_bytes / (world * B)))
+    s8d_achieved = s8d_bytes / k3_solo / 1e9 if k3_solo > 0 else 0.0
     traffic, tsrc = (None, None)
     issue = None
     if not (args.sharp_yuv or args.low_memory or args.stub):
@@ -712,6 +716,13 @@ def lossy_line(args, world, B, W, H, elapsed, tails, total_bytes, ntok, solo=Non
                                          "the time `achieved` uses (≈ rocprof's average, "
                                          "profiles/r5/final/kernel_stats_solo_r5fg.csv: 96.74 ms)",
                      "algorithmic_bytes_per_launch": k3_bytes,
+                     "s8d": {"bytes_per_launch": s8d_bytes,
+                             "achieved": round(s8d_achieved, 3),
+                             "frac": round(s8d_achieved / HBM_PEAK_GBS, 6),
+                             "note": "SURVEY.md 8(d)'s algorithmic bytes (7 W H + coded bytes "
+                                     "per frame) over k_encode_solo_ms; `achieved` / `frac` "
+                                     "above count K3's own reads and writes (YUV, mode info, "
+                                     "results, tokens)"},
                      # the roof that binds K3: vector issue
                      "issue": issue},
         "stage_ms": {k: round(avg(i) / 1e3, 3) for k, i in

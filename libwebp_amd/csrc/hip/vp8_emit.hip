@@ -113,11 +113,13 @@ __global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ to
     const uint32_t s = sbase + sg;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (s > 0 && s < M.nseg) {
-      // the previous segment's last EMIT_IMG tokens; it ends at its row's end
-      // (any token) when it is a row's last segment: then 8 single loads
-      const vp8g_emit_desc pd = D[s - 1];
-      if (pd.len >= EMIT_IMG) {
-        const uint64_t b = pd.off + pd.len - EMIT_IMG + 8 * part;
+      // the EMIT_IMG tokens before the segment in stream order: the previous
+      // segment's last ones -- token by token when it is a row's last segment
+      // (its end is off the 8-token grid) -- reaching back into the segment
+      // before it when that one is shorter (a row's short last segment)
+      const vp8g_emit_desc d1 = D[s - 1];
+      if (d1.len >= EMIT_IMG) {
+        const uint64_t b = d1.off + d1.len - EMIT_IMG + 8 * part;
         uint4 raw;
         if ((b & 7) == 0) {
           raw = *reinterpret_cast<const uint4*>(tokens + b);
@@ -127,6 +129,23 @@ __global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ to
                            pt[4] | ((uint32_t)pt[5] << 16), pt[6] | ((uint32_t)pt[7] << 16));
         }
         v = resolve_quad(raw, prob);
+      } else if (s >= 2) {
+        const vp8g_emit_desc d2 = D[s - 2];
+        if (d1.len + d2.len >= EMIT_IMG) {
+          uint32_t w[4];
+#pragma unroll
+          for (int k = 0; k < 8; k += 2) {
+            uint32_t pr[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const uint32_t back = EMIT_IMG - (8 * part + k + h);   // 1..256 before the start
+              pr[h] = back <= d1.len ? tokens[d1.off + d1.len - back]
+                                     : tokens[d2.off + d2.len - (back - d1.len)];
+            }
+            w[k >> 1] = pr[0] | (pr[1] << 16);
+          }
+          v = resolve_quad(make_uint4(w[0], w[1], w[2], w[3]), prob);
+        }
       }
     }
     *reinterpret_cast<uint4*>(&tk[sg * IMG_ROW + 8 * part]) = v;
@@ -187,8 +206,8 @@ __global__ __launch_bounds__(64) void k_emit_img(const uint16_t* __restrict__ to
     if (mw == 0) { out[0] = 1; out[1] = 254; }
     return;
   }
-  if (D[ms - 1].len < EMIT_IMG) {   // after a row's short last segment: all 128 ranges
-    if (mw == 0) out[0] = 0xff;
+  if (D[ms - 1].len < EMIT_IMG && (ms < 2 || D[ms - 1].len + D[ms - 2].len < EMIT_IMG)) {
+    if (mw == 0) out[0] = 0xff;   // fewer than EMIT_IMG tokens to look back on: all 128 ranges
     return;
   }
   if (cnt > EMIT_SLOTS) {   // too many: the map kernel covers all 128 ranges
@@ -243,14 +262,22 @@ __global__ __launch_bounds__(64) void k_emit_maps(const uint16_t* __restrict__ t
   if (lane < MAP_G && sbase + lane < M.nseg) ld[lane] = desc[M.seg_base + sbase + lane];
   load_probas(prob, results, M, lane, 64);
   __syncthreads();
+  uint64_t pofs[MAP_PIECES];   // the descriptor of each of the lane's pieces, in registers
+  uint32_t plen[MAP_PIECES];
+#pragma unroll
+  for (int t = 0; t < MAP_PIECES; ++t) {
+    const int sg = (lane + 64 * t) / (MAP_CH / 8);
+    const bool in = sbase + sg < M.nseg;
+    pofs[t] = in ? ld[sg].off : 0;
+    plen[t] = in ? ld[sg].len : 0u;
+  }
   auto load = [&](uint32_t c0, uint4* v) {
 #pragma unroll
     for (int t = 0; t < MAP_PIECES; ++t) {
-      const int q = lane + 64 * t, sg = q / (MAP_CH / 8), part = q % (MAP_CH / 8);
+      const int part = (lane + 64 * t) % (MAP_CH / 8);
       const uint32_t i = c0 + 8 * part;
       v[t] = make_uint4(0, 0, 0, 0);
-      if (sbase + sg < M.nseg && i < ld[sg].len)
-        v[t] = *reinterpret_cast<const uint4*>(tokens + ld[sg].off + i);
+      if (i < plen[t]) v[t] = *reinterpret_cast<const uint4*>(tokens + pofs[t] + i);
     }
   };
   for (int p0 = 0; p0 < total; p0 += 64) {
@@ -372,15 +399,16 @@ __global__ __launch_bounds__(64) void k_emit_compose(vp8g_emit_meta* __restrict_
 
 // a chunk of 64 segments x SEG_CH tokens in two steps: global -> registers (issued early, so the
 // loads fly while the previous chunk is processed), registers -> LDS
+// (pofs / plen: the segment descriptor of each of the lane's 8 pieces, held
+// in registers for the whole kernel: the fetch is address arithmetic only)
 __device__ __forceinline__ void seg_chunk_fetch(uint4 v[8], const uint16_t* tokens,
-                                                const vp8g_emit_desc* ld, uint32_t s0,
-                                                uint32_t nseg, uint32_t c0, int lane) {
+                                                const uint64_t pofs[8], const uint32_t plen[8],
+                                                uint32_t c0, int lane) {
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
-    const int q = lane + 64 * t, sg = q >> 3, part = q & 7;
-    const uint32_t i = c0 + 8 * part;
+    const uint32_t i = c0 + 8 * (lane & 7);
     v[t] = make_uint4(0, 0, 0, 0);
-    if (s0 + sg < nseg && i < ld[sg].len) v[t] = *reinterpret_cast<const uint4*>(tokens + ld[sg].off + i);
+    if (i < plen[t]) v[t] = *reinterpret_cast<const uint4*>(tokens + pofs[t] + i);
   }
 }
 __device__ __forceinline__ void seg_chunk_put(uint32_t* lds, const uint4 v[8], int lane) {
@@ -481,11 +509,20 @@ __global__ __launch_bounds__(64) void k_emit_seg(const uint16_t* __restrict__ to
   int r = g.rs;
   uint4 nv[8];
   __syncthreads();   // the wave's descriptors in LDS
-  seg_chunk_fetch(nv, tokens, ld, s0, M.nseg, 0, lane);
+  uint64_t pofs[8];
+  uint32_t plen[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {   // piece t of this lane: segment (lane + 64 t) >> 3, part lane & 7
+    const int sg = (lane + 64 * t) >> 3;
+    const bool in = s0 + sg < M.nseg;
+    pofs[t] = in ? ld[sg].off : 0;
+    plen[t] = in ? ld[sg].len : 0u;
+  }
+  seg_chunk_fetch(nv, tokens, pofs, plen, 0, lane);
   for (uint32_t c0 = 0; c0 < span; c0 += SEG_CH) {
     seg_chunk_put(lds, nv, lane);
     __syncthreads();
-    if (c0 + SEG_CH < span) seg_chunk_fetch(nv, tokens, ld, s0, M.nseg, c0 + SEG_CH, lane);
+    if (c0 + SEG_CH < span) seg_chunk_fetch(nv, tokens, pofs, plen, c0 + SEG_CH, lane);
 #pragma unroll 2
     for (int k = 0; k < SEG_CH / 2; ++k) {
       const uint32_t w = resolve_pair(row[k], prob);

@@ -3165,10 +3165,20 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   a.rowcap = rows ? rows->rowcap : 0u;
   a.rowtok = rows ? rows->rowtok : nullptr;
   if (xsync != nullptr && recon == nullptr && variant == 0) {
-    const int nwg = k3x_take(n, a.mbh, 2);
-    if (nwg > 1)
+    // K3X workers per workgroup: 2 (rows handed over in LDS inside a
+    // workgroup), or 1 (WEBP_AMD_K3X_NW=1: every row on a CU of its own)
+    static const int xnw = [] {
+      const char* v = getenv("WEBP_AMD_K3X_NW");
+      return (v && v[0] == '1') ? 1 : 2;
+    }();
+    const int nwg = k3x_take(n, a.mbh, xnw);
+    if (nwg > 1) {
+      if (xnw == 1)
+        return trellis ? launch_k3x_budget<1, true>(a, n, nwg, stream)
+                       : launch_k3x_budget<1, false>(a, n, nwg, stream);
       return trellis ? launch_k3x_budget<2, true>(a, n, nwg, stream)
                      : launch_k3x_budget<2, false>(a, n, nwg, stream);
+    }
   }
 #ifdef WEBP_AMD_DIAG
   if (variant == 2) return launch_k3<1>(a, n, trellis != 0, stream);

@@ -538,8 +538,11 @@ static int alloc_tokens(WebPGpuBatch* b, size_t tok_cap, size_t rowcap, int keep
   b->d_tokens = nt;
   b->tok_cap = tok_cap;
   b->p0_cap = p0cap;
-  /* the widest rows the stride holds (token rows may use a slot-sized buffer) */
-  b->rowcap = (tok_cap / (size_t)b->mbh) & ~(size_t)7;
+  /* the rows: as asked, else the widest the stride holds (a slot-sized
+     buffer); a multiple of 64 tokens, so every row and every K4 segment
+     starts on a 128-byte line (K4 stages segments in 128-byte strips: a
+     strip across two lines doubled k_emit_seg's reads, r6i) */
+  b->rowcap = rowcap ? rowcap : (tok_cap / (size_t)b->mbh) & ~(size_t)63;
   return 1;
 fail:
   hipFree(nt);
@@ -557,16 +560,17 @@ static int ensure_tok_cap(WebPGpuBatch* b, size_t cap) {
  * of a row); keep: frames whose rows must survive a regrow */
 static int ensure_rows(WebPGpuBatch* b, size_t rowcap, int keep) {
   const size_t most = (size_t)VP8G_MAX_TOKENS_PER_MB * b->mbw;
-  rowcap = (rowcap + 7) & ~(size_t)7;
-  if (rowcap > most) rowcap = (most + 7) & ~(size_t)7;
+  rowcap = (rowcap + 63) & ~(size_t)63;
+  if (rowcap > most) rowcap = (most + 63) & ~(size_t)63;
   if (!b->d_rowtok) {
     CHK(hipMalloc((void**)&b->d_rowtok, (size_t)b->max_frames * b->mbh * sizeof(uint32_t)));
     CHK(hipHostMalloc((void**)&b->h_rowtok, (size_t)b->max_frames * b->mbh * sizeof(uint32_t), 0));
     CHK(hipMalloc((void**)&b->d_rerun_snap, (size_t)b->max_frames * VP8G_RERUN_STATE_BYTES));
   }
   if (b->d_tokens && b->rowcap >= rowcap) return 1;
-  /* the K4 reads of a row's last 8-token piece stay inside the slab: + 8 */
-  return alloc_tokens(b, (size_t)b->mbh * rowcap + 8, rowcap, keep);
+  /* the K4 reads of a row's last 8-token piece stay inside the slab: + 8;
+     frames 512-byte aligned */
+  return alloc_tokens(b, ((size_t)b->mbh * rowcap + 8 + 255) & ~(size_t)255, rowcap, keep);
 fail:
   return 0;
 }

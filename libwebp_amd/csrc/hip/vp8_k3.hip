@@ -3165,11 +3165,12 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   a.rowcap = rows ? rows->rowcap : 0u;
   a.rowtok = rows ? rows->rowtok : nullptr;
   if (xsync != nullptr && recon == nullptr && variant == 0) {
-    // K3X workers per workgroup: 2 (rows handed over in LDS inside a
-    // workgroup), or 1 (WEBP_AMD_K3X_NW=1: every row on a CU of its own)
+    // K3X workers per workgroup: 1, every row on a CU of its own (config 4
+    // 262 -> 233 ms, one 1080p frame 43.2 -> 40.9 ms, profiles/r6/k3x), or 2
+    // (WEBP_AMD_K3X_NW=2: rows handed over in LDS inside a workgroup)
     static const int xnw = [] {
       const char* v = getenv("WEBP_AMD_K3X_NW");
-      return (v && v[0] == '1') ? 1 : 2;
+      return (v && v[0] == '2') ? 2 : 1;
     }();
     const int nwg = k3x_take(n, a.mbh, xnw);
     if (nwg > 1) {

@@ -657,7 +657,7 @@ __device__ Trellis16 trellis16(const K3G& G, int c, bool act, int ctx0, int type
 
 template <bool TRELLIS>
 __device__ void eval_i16(const K3G& G, K3S& L, const vp8g_seg& S,
-                         const MBCtx& ctx, int tid) {
+                         const MBCtx& ctx, int tid, K3S& B) {
   const int m = tid >> 6, lane = tid & 63, g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
   const int bsub = lane >> 4;
   int co[4];
@@ -795,7 +795,7 @@ __device__ void eval_i16(const K3G& G, K3S& L, const vp8g_seg& S,
     L.mres[m][2] = rate + rdc;
     L.mres[m][3] = (int)(nzm | (dcnz ? (1u << 24) : 0u));
   }
-  WB();
+  wbar(B);   // (B: the worker running this, L: the MB state it evaluates)
 }
 
 // ---------------------------------------------------------------------------
@@ -804,7 +804,7 @@ __device__ void eval_i16(const K3G& G, K3S& L, const vp8g_seg& S,
 // mres[m] = {SSE, rate, non-zero AC count, nz bits}.
 
 __device__ void eval_uv(const K3G& G, K3S& L, const vp8g_seg& S, const MBCtx& ctx, int tid, int x0,
-                        const int8_t* topderr, int use_derr) {
+                        const int8_t* topderr, int use_derr, K3S& B) {
   const int m = tid >> 6, lane = tid & 63, g = lane & 48, j = lane & 15, x = j & 3, y = j >> 2;
   const int bsub = lane >> 4;
   int co[2];
@@ -891,7 +891,7 @@ __device__ void eval_uv(const K3G& G, K3S& L, const vp8g_seg& S, const MBCtx& ct
     L.mres[m][2] = flatc;
     L.mres[m][3] = (int)nzm;
   }
-  WB();
+  wbar(B);
 }
 
 // ---------------------------------------------------------------------------
@@ -1474,6 +1474,15 @@ struct K3XL {
   uint8_t lcoeffs[NSLOT];
   int32_t lcver;    // lcver of the level costs in G.lcost
   int32_t claim;    // highest epoch some worker of this workgroup refreshes to
+  // helper pairs (k_encode<.., HP>): worker 1 evaluates each MB's intra-16
+  // and chroma candidates in worker 0's MB state while worker 0 runs the
+  // intra-4 search; MBs handed over / finished (raster index + 1), the MB's
+  // context, and the helper's two decisions
+  int32_t hp_go, hp_done;
+  uint32_t hp_ctx_t, hp_ctx_l;
+  int32_t hp_seg, hp_best16, hp_bu, hp_pad;
+  uint32_t hp_nz16, hp_pad2;
+  score_t hp_D16, hp_SD16, hp_H16, hp_R16, hp_bH, hp_bsc;
 };
 
 __device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
@@ -1861,7 +1870,11 @@ struct K3Args {
 // AF: also store each MB's reconstruction for the autofilter
 // X: K3X, the frame's rows are dealt to a.nwg workgroups (blocks of NW rows
 // round-robin); k_encode_xtail finishes the frame
-template <int NW, bool TR, bool AF = false, bool X = false, int WPE = 1, int PAD = 0>
+// HP: K3X helper pairs (NW = 2): each workgroup runs one row at a time, worker
+// 0 the MB loop and worker 1 each MB's intra-16 and chroma evaluation beside
+// worker 0's intra-4 search (K3XL::hp_*)
+template <int NW, bool TR, bool AF = false, bool X = false, int WPE = 1, int PAD = 0,
+          bool HP = false>
 __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode(K3Args a) {
   extern __shared__ __align__(16) uint8_t smem[];
   const int mbw = a.mbw, mbh = a.mbh, nmb = mbw * mbh;
@@ -1887,6 +1900,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
   uint8_t* xpredtop = reinterpret_cast<uint8_t*>(xnzw + mbw);
   int8_t* xtopderr = reinterpret_cast<int8_t*>(xpredtop + 4 * mbw);
   const bool xr = X && wk == 0;   // this worker reads the x copies
+  static_assert(!HP || (X && NW == 2 && !AF), "helper pairs: K3X, one main and one helper worker");
+  constexpr int RW = HP ? 1 : NW;  // rows a workgroup runs at once
 
   const int nwg = X ? a.nwg : 1;
   const int f = X ? (int)blockIdx.x / nwg : (int)blockIdx.x;
@@ -1955,7 +1970,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     for (int k = gt; k < 16 * mbw; k += NW * K3T) xuvtop[k] = 127;
     for (int k = gt; k < mbw; k += NW * K3T) xnzw[k] = 0;
     for (int k = gt; k < 4 * mbw; k += NW * K3T) { xpredtop[k] = 0; xtopderr[k] = 0; }
-    if (gt == 0) { XL.lcver = 0; XL.claim = 0; }
+    if (gt == 0) { XL.lcver = 0; XL.claim = 0; XL.hp_go = 0; XL.hp_done = 0; }
   }
   if (gt < 4) G.max_edge[gt] = 0;
   if (gt == 0) {
@@ -2007,7 +2022,102 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
   const uint64_t tr_start = TR_NOW();
 #endif
 
-  for (int y = blk * NW + wk; y < mbh && !L.myabort; y += NW * nwg) {
+  if constexpr (HP) {
+    if (wk == 1) {
+      // the helper: for every MB of the main worker's rows, once the main has
+      // published it (predictions and source measure in M), the intra-16
+      // candidates and choice (quant_enc.c:1002-1058, StoreMaxDelta) and the
+      // chroma candidates and choice with StoreDiffusionErrors
+      // (quant_enc.c:1169-1217); its own barriers (L), M's data
+      K3S& M = reinterpret_cast<K3S*>(smem + sizeof(K3G) + PAD)[0];
+      const int8_t* derrx = xtopderr;   // the row above's DC errors, pulled by the main
+      for (int y = blk; y < mbh && !L.myabort; y += nwg) {
+        for (int x = 0; x < mbw; ++x) {
+          const int tid = opaque(tid_k), lane = tid & 63;
+          const uint32_t mb = (uint32_t)y * mbw + x;
+          if (!wait_ge(G, L, &XL.hp_go, (int32_t)mb + 1, 8)) break;
+          const int segid = __builtin_amdgcn_readfirstlane(XL.hp_seg);
+          const vp8g_seg& S = G.seg[segid];
+          MBCtx ctx;
+          ctx.t = __builtin_amdgcn_readfirstlane(XL.hp_ctx_t);
+          ctx.l = __builtin_amdgcn_readfirstlane(XL.hp_ctx_l);
+          if constexpr (TR) {
+            if (trellis_all) eval_i16<true>(G, M, S, ctx, tid, L);
+            else eval_i16<false>(G, M, S, ctx, tid, L);
+          } else {
+            eval_i16<false>(G, M, S, ctx, tid, L);
+          }
+          int best16 = 0;
+          uint32_t nz16 = 0;
+          score_t D16 = 0, SD16 = 0, H16 = 0, R16 = 0;
+          {
+            const int v0 = M.yin[0];
+            int same = 1;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int p = lane + 64 * q;
+              same &= M.yin[(p >> 4) * BPS + (p & 15)] == v0;
+            }
+            int flat = __all(same);
+            score_t best16_score = 0;
+            for (int mm = 0; mm < 4; ++mm) {
+              score_t Dm = M.mres[mm][0];
+              score_t SDm = S.tlambda ? (score_t)((S.tlambda * M.mres[mm][1] + 128) >> 8) : 0;
+              const score_t Hm = kVP8ModeCostI16[mm];
+              const score_t Rm = M.mres[mm][2];
+              if (flat) {
+                flat = (M.mres[mm][3] & 0xffff) == 0;
+                if (flat) { Dm *= 2; SDm *= 2; }
+              }
+              const score_t sc = (Rm + Hm) * S.lambda_i16 + 256 * (Dm + SDm);
+              if (mm == 0 || sc < best16_score) {
+                best16_score = sc; best16 = mm;
+                D16 = Dm; SD16 = SDm; H16 = Hm; R16 = Rm;
+                nz16 = (uint32_t)M.mres[mm][3];
+              }
+            }
+          }
+          if (tid < 64) {   // (a whole wave)
+            XL.hp_best16 = best16; XL.hp_nz16 = nz16;
+            XL.hp_D16 = D16; XL.hp_SD16 = SD16; XL.hp_H16 = H16; XL.hp_R16 = R16;
+          }
+          if ((nz16 & 0x100ffff) == 0x1000000 && D16 > S.min_disto) {   // StoreMaxDelta
+            int mv = iabs_(M.lvdc[best16][1]);
+            mv = max(mv, iabs_(M.lvdc[best16][2]));
+            mv = max(mv, iabs_(M.lvdc[best16][4]));
+            if (tid == 0) atomicMax(&G.max_edge[segid], mv);
+          }
+          // the chroma candidates overwrite M.mres: every wave has read it
+          wbar(L);
+          eval_uv(G, M, S, ctx, tid, x, derrx, use_derr, L);
+          int bu = 0;
+          score_t bsc = 0, bH = 0;
+          for (int mm = 0; mm < 4; ++mm) {
+            const score_t Dm = M.mres[mm][0], Hm = kVP8ModeCostUV[mm];
+            score_t Rm = M.mres[mm][1];
+            if (mm > 0 && M.mres[mm][2] <= 2) Rm += 140 * 8;
+            const score_t sc = (Rm + Hm) * S.lambda_uv + 256 * Dm;
+            if (mm == 0 || sc < bsc) { bsc = sc; bu = mm; bH = Hm; }
+          }
+          if (tid < 64) { XL.hp_bu = bu; XL.hp_bH = bH; XL.hp_bsc = bsc; }
+          if (use_derr && tid < 2) {   // StoreDiffusionErrors (quant_enc.c:909-920)
+            const int cch = tid;
+            int8_t* top = topderr + 4 * x + 2 * cch;
+            int8_t* left = M.lderr[cch];
+            const int8_t* e = M.uvderr[bu][cch];
+            left[0] = e[0];
+            left[1] = (int8_t)(3 * e[2] >> 2);
+            top[0] = e[1];
+            top[1] = (int8_t)(e[2] - left[1]);
+          }
+          wbar(L);
+          if (tid == 0) publish(&XL.hp_done, (int32_t)mb + 1);
+        }
+      }
+    }
+  }
+  for (int y = blk * RW + (HP ? 0 : wk); (!HP || wk == 0) && y < mbh && !L.myabort;
+       y += RW * nwg) {
     // InitLeft (iterator_enc.c:22-32)
     if (tid < 16) yl[tid] = 129;
     if (tid < 8) { ul[tid] = 129; vl[tid] = 129; }
@@ -2277,16 +2387,83 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       wbar(L);
       K3_STAMP(1);
 
+      int best16 = 0, is_i16 = 1, bu = 0;
+      uint64_t tr_uv = 0;
+      score_t rd_score = 0, rdH = 0;
+      uint32_t rd_nz = 0;
+      if constexpr (HP) {
+        // hand the MB to the helper, run the intra-4 search without the
+        // intra-16 bound (the bound only ends early a search whose score, which
+        // only grows, would lose anyway: the same choice), then take the
+        // helper's intra-16 and chroma results
+        if (tid == 0) {
+          XL.hp_ctx_t = ctx.t; XL.hp_ctx_l = ctx.l; XL.hp_seg = segid;
+          publish(&XL.hp_go, (int32_t)mb + 1);
+        }
+        K3_STAMP(2);
+        const uint64_t tr_i4 = TR_NOW();
+        constexpr score_t kNoBound = (score_t)0x7fffffffffffffffll;
+        I4Result r4;
+        r4.ok = 0; r4.H = 0; r4.score = 0; r4.nz = 0;
+        if (max_i4_bits > 0) {
+          if constexpr (TR) {
+            r4 = trellis_all ? run_i4<true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
+                                            kNoBound, max_i4_bits, substamps)
+                             : run_i4<false>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
+                                             kNoBound, max_i4_bits, substamps);
+          } else {
+            r4 = run_i4<false>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true, kNoBound,
+                               max_i4_bits, substamps);
+          }
+        }
+        tr_uv = TR_NOW();
+        TR_ADD(K3TR_I4, tr_uv - tr_i4);
+        if (!wait_ge(G, L, &XL.hp_done, (int32_t)mb + 1, 7)) break;
+        K3_STAMP(3);
+        best16 = __builtin_amdgcn_readfirstlane(XL.hp_best16);
+        const score_t D16 = XL.hp_D16, SD16 = XL.hp_SD16, H16 = XL.hp_H16, R16 = XL.hp_R16;
+        const uint32_t nz16 = __builtin_amdgcn_readfirstlane(XL.hp_nz16);
+        const score_t rd16 = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
+        if (tid < 64) {   // whole wave 0: a lone-lane store here spills
+          L.mdist = (int32_t)D16;
+          L.ry16 = (int32_t)R16;
+        }
+        if (r4.ok && r4.score < rd16) {
+          is_i16 = 0;
+          if (tid == 0) L.mdist = L.d4acc;
+          rdH = r4.H;
+          rd_score = r4.score;
+          rd_nz = r4.nz;
+          L.yout[(tid >> 4) * BPS + (tid & 15)] = L.acc_out[tid];
+          (&L.fin_ac[0][0])[tid] = (&L.acc_ac[0][0])[tid];
+        } else {
+          rdH = H16;
+          rd_score = rd16;
+          rd_nz = nz16;
+          L.yout[(tid >> 4) * BPS + (tid & 15)] = L.rec16[best16][tid];
+          (&L.fin_ac[0][0])[tid] = (&L.lv16[best16][0][0])[tid];
+          if (tid < 16) { L.fin_dc[tid] = L.lvdc[best16][tid]; L.modes[tid] = best16; }
+        }
+        bu = __builtin_amdgcn_readfirstlane(XL.hp_bu);
+        rdH += XL.hp_bH;
+        rd_score += XL.hp_bsc;
+        if (tid == 0) L.mdist += L.mres[bu][0];
+        rd_nz |= (uint32_t)L.mres[bu][3] << 16;
+        if (tid < 128) {
+          L.yout[(tid >> 4) * BPS + 16 + (tid & 15)] = L.recuv[bu][tid];
+          (&L.fin_uv[0][0])[tid] = (&L.lvuv[bu][0][0])[tid];
+        }
+        wbar(L);
+      } else {
       // ---- Intra16 (quant_enc.c:1002-1058)
       const uint64_t tr_i16 = TR_NOW();
       if constexpr (TR) {
-        if (trellis_all) eval_i16<true>(G, L, S, ctx, tid);
-        else eval_i16<false>(G, L, S, ctx, tid);
+        if (trellis_all) eval_i16<true>(G, L, S, ctx, tid, L);
+        else eval_i16<false>(G, L, S, ctx, tid, L);
       } else {
-        eval_i16<false>(G, L, S, ctx, tid);
+        eval_i16<false>(G, L, S, ctx, tid, L);
       }
       TR_SINCE(K3TR_I16, tr_i16);
-      int best16 = 0;
       uint32_t nz16 = 0;
       score_t D16 = 0, SD16 = 0, H16 = 0, R16 = 0;
       {
@@ -2321,10 +2498,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       L.yout[(tid >> 4) * BPS + (tid & 15)] = L.rec16[best16][tid];
       (&L.fin_ac[0][0])[tid] = (&L.lv16[best16][0][0])[tid];
       if (tid < 16) { L.fin_dc[tid] = L.lvdc[best16][tid]; L.modes[tid] = best16; }
-      score_t rd_score = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
-      score_t rdH = H16;
-      uint32_t rd_nz = nz16;
-      int is_i16 = 1;
+      rd_score = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
+      rdH = H16;
+      rd_nz = nz16;
+      is_i16 = 1;
       if (tid < 64) {   // whole wave 0: a lone-lane store here spills
         L.mdist = (int32_t)D16;
         L.ry16 = (int32_t)R16;
@@ -2368,13 +2545,12 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         // barriers order it before the readers -- info, SSE, tokens)
       }
       K3_STAMP(3);
-      const uint64_t tr_uv = TR_NOW();
+      tr_uv = TR_NOW();
       TR_ADD(K3TR_I4, tr_uv - tr_i4);
 
       // ---- UV (quant_enc.c:1169-1217)
-      int bu = 0;
       {
-        eval_uv(G, L, S, ctx, tid, x, derrrd, use_derr);
+        eval_uv(G, L, S, ctx, tid, x, derrrd, use_derr, L);
         score_t bsc = 0, bH = 0;
         for (int mm = 0; mm < 4; ++mm) {
           const score_t Dm = L.mres[mm][0], Hm = kVP8ModeCostUV[mm];
@@ -2403,6 +2579,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         }
         wbar(L);
       }
+      }   // (!HP)
 
       // ---- m5: final re-quantisation of the chosen modes with trellis
       // (SimpleQuantize, quant_enc.c:1222-1245; RD_OPT_TRELLIS, :1384-1387)
@@ -2410,7 +2587,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         uint32_t nzq = 0;
         if constexpr (!TR) {
         } else if (is_i16) {
-          eval_i16<true>(G, L, S, ctx, tid);
+          eval_i16<true>(G, L, S, ctx, tid, L);
           L.yout[(tid >> 4) * BPS + (tid & 15)] = L.rec16[best16][tid];
           (&L.fin_ac[0][0])[tid] = (&L.lv16[best16][0][0])[tid];
           if (tid < 16) L.fin_dc[tid] = L.lvdc[best16][tid];
@@ -2423,7 +2600,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           nzq = r4.nz;
         }
         wbar(L);
-        eval_uv(G, L, S, ctx, tid, x, topderr, use_derr);   // derr state already updated
+        eval_uv(G, L, S, ctx, tid, x, topderr, use_derr, L);   // derr state already updated
         if (tid < 128) {
           L.yout[(tid >> 4) * BPS + 16 + (tid & 15)] = L.recuv[bu][tid];
           (&L.fin_uv[0][0])[tid] = (&L.lvuv[bu][0][0])[tid];
@@ -2643,7 +2820,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       if constexpr (X) {
         // the last worker's row feeds worker 0 of the next workgroup: its
         // boundary record for column x, drained, then the column count
-        if (wk == NW - 1 && y < mbh - 1 && tid < 64) {
+        if (wk == (HP ? 0 : NW - 1) && y < mbh - 1 && tid < 64) {
           if (tid < 11) {
             uint32_t v;
             if (tid < 4) v = reinterpret_cast<const uint32_t*>(ytop + 16 * x)[tid];
@@ -2901,7 +3078,7 @@ static size_t k3x_lds_extra(int mbw) {
   return ((sizeof(K3XL) + 15) & ~(size_t)15) + 44 * (size_t)mbw + 32;
 }
 
-template <int NW, bool TR>
+template <int NW, bool TR, bool HP = false>
 static int launch_k3x(K3Args a, int n, int nwg, void* stream) {
   const size_t lds = k3_lds_bytes<NW>(a.mbw, a.mbh, TR) + k3x_lds_extra(a.mbw);
   const size_t lds_tail = sizeof(K3G) + sizeof(K3S);
@@ -2913,7 +3090,7 @@ static int launch_k3x(K3Args a, int n, int nwg, void* stream) {
   static std::once_flag once;
   static hipError_t attr_err = hipSuccess;
   std::call_once(once, [] {
-    attr_err = hipFuncSetAttribute((const void*)k_encode<NW, TR, false, true>,
+    attr_err = hipFuncSetAttribute((const void*)k_encode<NW, TR, false, true, 1, 0, HP>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (attr_err == hipSuccess)
       attr_err = hipFuncSetAttribute((const void*)k_encode_xtail,
@@ -2929,16 +3106,16 @@ static int launch_k3x(K3Args a, int n, int nwg, void* stream) {
     vp8g_set_error("k_encode (K3X)", "xsync reset failed");
     return 0;
   }
-  hipLaunchKernelGGL((k_encode<NW, TR, false, true>), dim3(n * nwg), dim3(NW * K3T), lds,
+  hipLaunchKernelGGL((k_encode<NW, TR, false, true, 1, 0, HP>), dim3(n * nwg), dim3(NW * K3T), lds,
                      (hipStream_t)stream, a);
   if (!vp8g_launch_check("k_encode (K3X)")) return 0;
   hipLaunchKernelGGL(k_encode_xtail, dim3(n), dim3(K3T), lds_tail, (hipStream_t)stream, a);
   return vp8g_launch_check("k_encode_xtail");
 }
 
-template <int NW, bool TR>
+template <int NW, bool TR, bool HP = false>
 static int launch_k3x_budget(const K3Args& a, int n, int nwg, void* stream) {
-  const int ok = launch_k3x<NW, TR>(a, n, nwg, stream);
+  const int ok = launch_k3x<NW, TR, HP>(a, n, nwg, stream);
   // give the workgroups back once the stream has passed the kernels (at once
   // if they never got enqueued)
   if (!ok || hipLaunchHostFunc((hipStream_t)stream, k3x_release,
@@ -3165,15 +3342,20 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   a.rowcap = rows ? rows->rowcap : 0u;
   a.rowtok = rows ? rows->rowtok : nullptr;
   if (xsync != nullptr && recon == nullptr && variant == 0) {
-    // K3X workers per workgroup: 1, every row on a CU of its own (config 4
-    // 262 -> 233 ms, one 1080p frame 43.2 -> 40.9 ms, profiles/r6/k3x), or 2
-    // (WEBP_AMD_K3X_NW=2: rows handed over in LDS inside a workgroup)
+    // K3X workgroups: a helper pair per row, every row on a CU of its own,
+    // intra-16 and chroma evaluated beside intra-4 (config 4 236 -> 192 ms,
+    // one 1080p frame 40.8 -> 39.1 ms against one worker, profiles/r6/k3x);
+    // A/B: WEBP_AMD_K3X_NW=1 one worker (262 -> 233 / 43.2 -> 40.9 ms against
+    // 2), =2 two workers with rows handed over in LDS
     static const int xnw = [] {
       const char* v = getenv("WEBP_AMD_K3X_NW");
-      return (v && v[0] == '2') ? 2 : 1;
+      return (v && v[0] == '2') ? 2 : (v && v[0] == '1') ? 1 : 3;
     }();
-    const int nwg = k3x_take(n, a.mbh, xnw);
+    const int nwg = k3x_take(n, a.mbh, xnw == 2 ? 2 : 1);
     if (nwg > 1) {
+      if (xnw == 3)
+        return trellis ? launch_k3x_budget<2, true, true>(a, n, nwg, stream)
+                       : launch_k3x_budget<2, false, true>(a, n, nwg, stream);
       if (xnw == 1)
         return trellis ? launch_k3x_budget<1, true>(a, n, nwg, stream)
                        : launch_k3x_budget<1, false>(a, n, nwg, stream);

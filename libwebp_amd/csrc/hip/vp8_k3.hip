@@ -2035,7 +2035,11 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         for (int x = 0; x < mbw; ++x) {
           const int tid = opaque(tid_k), lane = tid & 63;
           const uint32_t mb = (uint32_t)y * mbw + x;
+          const uint64_t tr_w = TR_NOW();
           if (!wait_ge(G, L, &XL.hp_go, (int32_t)mb + 1, 8)) break;
+          const uint64_t tr_e = TR_NOW();
+          TR_ADD(K3TR_ROW_WAIT, tr_e - tr_w);   // (helper: waiting for the main)
+          TR_ADD(K3TR_NMB, 1);
           const int segid = __builtin_amdgcn_readfirstlane(XL.hp_seg);
           const vp8g_seg& S = G.seg[segid];
           MBCtx ctx;
@@ -2112,6 +2116,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           }
           wbar(L);
           if (tid == 0) publish(&XL.hp_done, (int32_t)mb + 1);
+          TR_SINCE(K3TR_I16, tr_e);   // (helper: intra-16 + chroma)
         }
       }
     }
@@ -2215,7 +2220,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           // the frame's refresher published epoch ep; the first worker of this
           // workgroup to need it copies the probabilities (and, if they
           // changed, recomputes the level costs) for the whole workgroup
+          const uint64_t tr_w = TR_NOW();
           if (!wait_gx(G, L, &XH->epoch, ep, XH)) break;
+          TR_SINCE(K3TR_EPOCH_WAIT, tr_w);
+          const uint64_t tr_r = TR_NOW();
           if (tid == 0) L.redw[0] = atomicMax(&XL.claim, ep) < ep;
           wbar(L);
           const int mine = L.redw[0];
@@ -2236,6 +2244,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           } else {
             if (!wait_ge(G, L, &G.epoch, ep, 2)) break;
           }
+          TR_SINCE(K3TR_REFRESH, tr_r);
         } else {
           const uint64_t tr_w = TR_NOW();
           if (!wait_ge(G, L, &G.epoch, ep, 2)) break;
@@ -2274,7 +2283,12 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
 #endif
       if (xr) {
         if (y > 0) {
+#ifdef K3_TRACE
+          const uint64_t tr_w = TR_NOW();
+          TR_ADD(K3TR_NROWWAIT, ld_sc1(&xrowdone[y - 1]) < min(x + 2, mbw) ? 1 : 0);
+#endif
           if (!wait_gx(G, L, &xrowdone[y - 1], min(x + 2, mbw), XH)) break;
+          TR_SINCE(K3TR_ROW_WAIT, tr_w);
           // pull the boundary records of columns x, x + 1 (x = 0) or x + 1
           const int c0 = x == 0 ? 0 : x + 1;
           const int nc = x == 0 ? min(2, mbw) : (x + 1 < mbw ? 1 : 0);

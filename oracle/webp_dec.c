@@ -956,8 +956,17 @@ static int copy_distance(int sym, LBits* b) {   /* GetCopyDistance, vp8l_dec.c:1
 }
 
 /* DecodeImageData, vp8l_dec.c:1138-1275 (colour cache filled in pixel order) */
+/* analysis only (odec_vp8l_stats): the main image's coding, filled by the
+ * level-0 decode of the calling thread */
+static _Thread_local long long* t_lstats;      /* requested */
+static _Thread_local long long* t_lstats_px;   /* armed for the main image's pixels */
+enum { LS_HDR_BITS, LS_NGROUPS, LS_HBITS, LS_CACHE_BITS, LS_NLIT, LS_NCOPY, LS_NCACHE,
+       LS_BLIT, LS_BCOPY, LS_BCACHE, LS_COPY_PX, LS_N };
+
 static int decode_pixels(LBits* b, uint32_t* data, int xs, int ys, int cache_bits,
                          const HGroup* groups, const uint32_t* himg, int hbits) {
+  long long* st = t_lstats_px;
+  t_lstats_px = NULL;
   const int hxs = hbits ? subsample(xs, hbits) : 0;
   uint32_t* cache = cache_bits ? (uint32_t*)calloc((size_t)1 << cache_bits, 4) : NULL;
   if (cache_bits && !cache) return 0;
@@ -972,6 +981,7 @@ static int decode_pixels(LBits* b, uint32_t* data, int xs, int ys, int cache_bit
   while (pos < total && ok) {
     const int x = (int)(pos % xs), y = (int)(pos / xs);
     const HGroup* g = groups + (hbits ? himg[(y >> hbits) * hxs + (x >> hbits)] : 0);
+    const size_t p0 = b->pos, pos0 = pos;
     const int code = huff_read(&g->h[0], b);
     if (code < 256) {
       const int r = huff_read(&g->h[1], b), bl = huff_read(&g->h[2], b);
@@ -999,6 +1009,12 @@ static int decode_pixels(LBits* b, uint32_t* data, int xs, int ys, int cache_bit
     }
     CACHE_UPTO(pos);
     if (b->eos) ok = 0;
+    if (st) {
+      const int k = code < 256 ? 0 : code < 256 + 24 ? 1 : 2;
+      st[LS_NLIT + k] += 1;
+      st[LS_BLIT + k] += (long long)(b->pos - p0);
+      if (k == 1) st[LS_COPY_PX] += (long long)(pos - pos0);
+    }
   }
 #undef CACHE_UPTO
   free(cache);
@@ -1195,6 +1211,13 @@ static uint32_t* decode_image_stream(LBits* b, int xs, int ys, int level0, int* 
   }
   if (ok) {
     data = (uint32_t*)malloc((size_t)txs * ys * 4 + 4);
+    if (level0 && t_lstats) {
+      t_lstats[LS_HDR_BITS] = (long long)b->pos;
+      t_lstats[LS_NGROUPS] = ngroups;
+      t_lstats[LS_HBITS] = hbits;
+      t_lstats[LS_CACHE_BITS] = cache_bits;
+      t_lstats_px = t_lstats;
+    }
     ok = data && decode_pixels(b, data, txs, ys, cache_bits, groups, himg, hbits);
   }
   if (groups)
@@ -1383,6 +1406,20 @@ static int parse_container(const uint8_t* d, size_t n, Chunks* c) {
     return 1;
   }
   return 0;
+}
+
+/* analysis only: how a VP8L file's main image is coded -- out[LS_N]: header
+ * bits (transforms, cache, meta image, codes), code groups, meta bits, cache
+ * bits, literal / copy / cache-hit counts and their bits, pixels copied */
+int odec_vp8l_stats(const uint8_t* data, size_t size, long long* out) {
+  for (int i = 0; i < LS_N; ++i) out[i] = 0;
+  if (size < 20 || memcmp(data + 12, "VP8L", 4)) return 0;
+  int w = 0, h = 0;
+  t_lstats = out;
+  uint32_t* argb = vp8l_decode(data + 20, size - 20, &w, &h);
+  t_lstats = NULL;
+  free(argb);
+  return argb != NULL;
 }
 
 int odec_info(const uint8_t* data, size_t size, int* w, int* h, int* has_alpha, int* lossless) {

@@ -2304,6 +2304,50 @@ __device__ __forceinline__ uint32_t lz_dcode(const uint8_t* dcodes, int nd, uint
   return c ? c : d + 120;
 }
 
+// The first parse of the cost-model route (model: lz_greedy): per segment
+// from its start, the longer of the chain match and the local match (the
+// chain's on ties), cut at the segment end, when it is at least
+// LZ_GREEDY_MIN long, else a literal. One wave per segment: the lengths
+// staged in LDS, lane 0 walks them (a copy's distance is read at its start
+// only), the wave writes the segment's ops.
+#define LZ_GREEDY_MIN 3
+__global__ __launch_bounds__(64) void k_lz_greedy(int npix, const uint32_t* __restrict__ hoff,
+                                                  const uint16_t* __restrict__ hlen,
+                                                  const uint32_t* __restrict__ loff,
+                                                  const uint16_t* __restrict__ llen,
+                                                  const uint8_t* __restrict__ dcodes, int nd,
+                                                  uint32_t* __restrict__ ops) {
+  __shared__ uint16_t hl[LZ_SEG], ll[LZ_SEG];
+  __shared__ uint32_t op[LZ_SEG];
+  const int f = blockIdx.y, ln = lane_id();
+  const int s = blockIdx.x * LZ_SEG, m = min(npix, s + LZ_SEG) - s;
+  const size_t base = (size_t)f * npix + s;
+  for (int i = ln; i < m; i += 64) {
+    hl[i] = hlen[base + i];
+    ll[i] = llen[base + i];
+    op[i] = 0u;
+  }
+  __syncthreads();
+  if (ln == 0) {
+    int j = 0;
+    while (j < m) {
+      const int a = min((int)hl[j], m - j), b = min((int)ll[j], m - j);
+      const bool loc = b > a;
+      const int L = loc ? b : a;
+      if (L >= LZ_GREEDY_MIN) {
+        const uint32_t d = loc ? loff[base + j] : hoff[base + j];
+        op[j] = 2u | ((uint32_t)(L - 1) << 2) | (lz_dcode(dcodes, nd, d) << 14);
+        for (int t = j + 1; t < j + L; ++t) op[t] = 3u;
+        j += L;
+      } else {
+        ++j;
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = ln; i < m; i += 64) ops[base + i] = op[i];
+}
+
 // The cost-model parse of one segment (model: lz_dp): one wave per segment,
 // the path costs / choices in LDS; per position the literal (lane 0), then
 // the chain match and then the local match, each with one lane per length of
@@ -3529,10 +3573,6 @@ extern "C" int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
             hipSuccess)
       return 0;
     const int nseg = (npix + LZ_SEG - 1) / LZ_SEG;
-    hipLaunchKernelGGL(k_vp8l_match, dim3(p->h, p->n), dim3(64), 0, st, argb, minb,
-                       (const uint2*)nullptr, 1, *p, ops);
-    hipLaunchKernelGGL(k_vp8l_parse, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, *p, ops, prov,
-                       (const uint8_t*)cbits);   // the greedy parse: first costs
     hipLaunchKernelGGL(k_lz_runs, dim3((npix + LZ_RUN_PIECE - 1) / LZ_RUN_PIECE, p->n), dim3(64), 0,
                        st, argb, npix, lz->runs);
     hipLaunchKernelGGL(k_lz_chain, dim3(p->n), dim3(64), 0, st, argb, npix,
@@ -3541,6 +3581,10 @@ extern "C" int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
                        npix, (const int32_t*)lz->chain, lz->hoff, lz->hlen);
     hipLaunchKernelGGL(k_lz_local, dim3(nseg, p->n), dim3(64), 0, st, argb, *p, lz->loff,
                        lz->llen);
+    hipLaunchKernelGGL(k_lz_greedy, dim3(nseg, p->n), dim3(64), 0, st, npix,
+                       (const uint32_t*)lz->hoff, (const uint16_t*)lz->hlen,
+                       (const uint32_t*)lz->loff, (const uint16_t*)lz->llen, lz->dcodes, lz->nd,
+                       ops);   // the first parse: first costs
     for (int round = 0; round < 2; ++round) {
       hipLaunchKernelGGL(k_lz_costs, dim3(p->n), dim3(1024), 0, st, argb, (const uint32_t*)ops,
                          npix, flog2, lz->costs);

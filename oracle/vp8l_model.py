@@ -831,7 +831,8 @@ def parse(argb, hit, dists, lens=None):
 #     length with cost intervals; here each match offers the lengths
 #     LZ_LENGTHS <= its length and itself), on independent LZ_SEG-pixel
 #     segments of the frame (lz_dp), with per-symbol costs from a first parse:
-#     the greedy parse, then the first cost-model parse (two rounds);
+#     a greedy parse over the same two matches (lz_greedy), then the first
+#     cost-model parse (two rounds);
 #   * no colour cache (a palette index costs about what a cache index does;
 #     measured smaller on the fixtures).
 LZ_SEG = 4096
@@ -842,6 +843,7 @@ LZ_WINDOW_CAP = (1 << 18) - 121           # distance code + 120 fits the 18-bit 
 LZ_LENGTHS = sorted(set(range(2, 17)) | {v for j in range(2, 13) for v in (1 << j, (1 << j) + 1)
                                          if v <= LZ_MAX_LENGTH})
 LZ_INF = (1 << 31) - 1
+LZ_GREEDY_MIN = 3
 
 
 def lz_pair_hash(a, b):
@@ -958,6 +960,37 @@ def lz_local(flat, W):
     return off, ln
 
 
+def lz_greedy(flat, W, cands):
+    """The first parse of the cost-model route (round 6; before, the greedy
+    parse over the 4 local candidates): per LZ_SEG segment from its start,
+    the longer of the chain match and the local match (the chain's on ties),
+    cut at the segment end, when it is at least LZ_GREEDY_MIN long, else a
+    literal -- the role of the reference's first parse, BackwardReferencesLz77
+    (backward_references_enc.c:515-575: the chain's match from MIN_LENGTH 4,
+    with a look-ahead), whose symbol statistics seed TraceBackwards' cost
+    model. Returns act, clen, ccode (flat)."""
+    n = len(flat)
+    act = np.zeros(n, dtype=np.int64)
+    clen = np.zeros(n, dtype=np.int64)
+    ccode = np.zeros(n, dtype=np.int64)
+    (ho, hl), (lo, ll) = [([int(v) for v in o], [int(v) for v in l]) for o, l in cands]
+    for s in range(0, n, LZ_SEG):
+        e = min(n, s + LZ_SEG)
+        i = s
+        while i < e:
+            a, b = min(hl[i], e - i), min(ll[i], e - i)
+            L, d = (b, lo[i]) if b > a else (a, ho[i])
+            if L >= LZ_GREEDY_MIN:
+                act[i] = 2
+                act[i + 1:i + L] = 3
+                clen[i] = L
+                ccode[i] = distance_code(W, d)
+                i += L
+            else:
+                i += 1
+    return act, clen, ccode
+
+
 def lz_pop_costs(h):
     """1/256 bit per symbol: log2(total) - log2(count) (log2 0 := 0), all 0
     for fewer than two used symbols (ConvertPopulationCountTableToBitEstimates,
@@ -1053,13 +1086,13 @@ def lz_dp(flat, W, costs, cands):
 
 
 def palette_parse(argb, dists, lens):
-    """The parse of a colour-indexed frame (see above): greedy parse without
-    cache -> costs -> cost-model parse -> its costs -> cost-model parse."""
+    """The parse of a colour-indexed frame (see above): greedy parse over the
+    two matches (lz_greedy) -> costs -> cost-model parse -> its costs ->
+    cost-model parse. (dists, lens: unused since round 6.)"""
     H, W = argb.shape
     flat = argb.ravel().astype(np.int64)
-    act, clen, ccode = parse(argb, np.zeros((H, W), dtype=bool), dists, lens)
     cands = [lz_hash_search(flat, W), lz_local(flat, W)]
-    act, clen, ccode = act.ravel(), clen.ravel(), ccode.ravel()
+    act, clen, ccode = lz_greedy(flat, W, cands)
     for _ in range(2):
         act, clen, ccode = lz_dp(flat, W, lz_costs(flat, act, clen, ccode, W), cands)
     return act.reshape(H, W), clen.reshape(H, W), ccode.reshape(H, W)

@@ -2252,19 +2252,25 @@ __global__ __launch_bounds__(64) void k_lz_local(const uint32_t* __restrict__ ar
 }
 
 // Symbol costs of a frame's parse (model: lz_costs / lz_pop_costs): one
-// workgroup per frame, histograms in LDS, 1/256 bit per symbol.
+// workgroup per frame, histograms in LDS, 1/256 bit per symbol. est (may be
+// null): the parse's bits under those costs, extra bits included (model:
+// lz_est_bits).
 __global__ __launch_bounds__(1024) void k_lz_costs(const uint32_t* __restrict__ argb,
                                                    const uint32_t* __restrict__ ops, int npix,
                                                    const int32_t* __restrict__ frac,
-                                                   int32_t* __restrict__ costs) {
+                                                   int32_t* __restrict__ costs,
+                                                   unsigned long long* __restrict__ est) {
   __shared__ uint32_t h[LZ_NCOST];
   __shared__ uint32_t tot[5], nz[5];
+  __shared__ unsigned long long xbits, bits;
   const int f = blockIdx.x, tid = threadIdx.x;
   const uint32_t* E = argb + (size_t)f * npix;
   const uint32_t* O = ops + (size_t)f * npix;
   for (int i = tid; i < LZ_NCOST; i += 1024) h[i] = 0;
   if (tid < 5) { tot[tid] = 0; nz[tid] = 0; }
+  if (tid == 0) { xbits = 0; bits = 0; }
   __syncthreads();
+  uint32_t myx = 0;   // this thread's extra bits
   for (int q = tid; q < npix; q += 1024) {
     const uint32_t op = O[q], act = op & 3;
     if (act == 0) {
@@ -2277,23 +2283,45 @@ __global__ __launch_bounds__(1024) void k_lz_costs(const uint32_t* __restrict__ 
       int sym, nb; uint32_t ex;
       prefix_enc(((op >> 2) & 0xfff) + 1, sym, nb, ex);
       atomicAdd(&h[256 + sym], 1u);
+      myx += (uint32_t)nb;
       prefix_enc(op >> 14, sym, nb, ex);
       atomicAdd(&h[1048 + sym], 1u);
+      myx += (uint32_t)nb;
     }
   }
+  if (est && myx) atomicAdd(&xbits, (unsigned long long)myx);
   __syncthreads();
   auto alph = [](int i) { return i < 280 ? 0 : i < 536 ? 1 : i < 792 ? 2 : i < 1048 ? 3 : 4; };
   for (int i = tid; i < LZ_NCOST; i += 1024)
     if (h[i]) { atomicAdd(&tot[alph(i)], h[i]); atomicAdd(&nz[alph(i)], 1u); }
   __syncthreads();
   int32_t* out = costs + (size_t)f * LZ_NCOST;
+  unsigned long long mine = 0;
   for (int i = tid; i < LZ_NCOST; i += 1024) {
     const int a = alph(i);
     int32_t c = 0;
     if (nz[a] > 1)
       c = (flog2_fx(frac, tot[a]) - (h[i] ? flog2_fx(frac, h[i]) : 0)) >> 4;
     out[i] = c;
+    mine += (unsigned long long)h[i] * (unsigned long long)c;
   }
+  if (est) {
+    if (mine) atomicAdd(&bits, mine);
+    __syncthreads();
+    if (tid == 0) est[f] = bits + 256ull * xbits;
+  }
+}
+
+// The first parse of the cost-model route (model: palette_parse): per frame
+// the cheaper of the two first parses' costs (the row parse on ties)
+__global__ __launch_bounds__(256) void k_lz_pick(const unsigned long long* __restrict__ est_row,
+                                                 const unsigned long long* __restrict__ est_chain,
+                                                 const int32_t* __restrict__ costs_row,
+                                                 int32_t* __restrict__ costs) {
+  const int f = blockIdx.x;
+  if (est_chain[f] < est_row[f]) return;   // costs hold the chain parse's already
+  for (int i = threadIdx.x; i < LZ_NCOST; i += 256)
+    costs[(size_t)f * LZ_NCOST + i] = costs_row[(size_t)f * LZ_NCOST + i];
 }
 
 // VP8L distance code of a distance (model: distance_code): the plane code
@@ -3573,6 +3601,13 @@ extern "C" int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
             hipSuccess)
       return 0;
     const int nseg = (npix + LZ_SEG - 1) / LZ_SEG;
+    // first parse A: the greedy row parse over the 4 local candidates
+    hipLaunchKernelGGL(k_vp8l_match, dim3(p->h, p->n), dim3(64), 0, st, argb, minb,
+                       (const uint2*)nullptr, 1, *p, ops);
+    hipLaunchKernelGGL(k_vp8l_parse, dim3((p->h + 63) / 64, p->n), dim3(64), 0, st, *p, ops, prov,
+                       (const uint8_t*)cbits);
+    hipLaunchKernelGGL(k_lz_costs, dim3(p->n), dim3(1024), 0, st, argb, (const uint32_t*)ops,
+                       npix, flog2, lz->costs_row, lz->est);
     hipLaunchKernelGGL(k_lz_runs, dim3((npix + LZ_RUN_PIECE - 1) / LZ_RUN_PIECE, p->n), dim3(64), 0,
                        st, argb, npix, lz->runs);
     hipLaunchKernelGGL(k_lz_chain, dim3(p->n), dim3(64), 0, st, argb, npix,
@@ -3581,13 +3616,21 @@ extern "C" int vp8l_launch_analyze(const uint32_t* argb, const vp8l_params* p,
                        npix, (const int32_t*)lz->chain, lz->hoff, lz->hlen);
     hipLaunchKernelGGL(k_lz_local, dim3(nseg, p->n), dim3(64), 0, st, argb, *p, lz->loff,
                        lz->llen);
+    // first parse B: greedy over the chain and local matches; the cheaper
+    // of A and B under their own costs seeds the first cost-model parse
     hipLaunchKernelGGL(k_lz_greedy, dim3(nseg, p->n), dim3(64), 0, st, npix,
                        (const uint32_t*)lz->hoff, (const uint16_t*)lz->hlen,
                        (const uint32_t*)lz->loff, (const uint16_t*)lz->llen, lz->dcodes, lz->nd,
-                       ops);   // the first parse: first costs
+                       ops);
+    hipLaunchKernelGGL(k_lz_costs, dim3(p->n), dim3(1024), 0, st, argb, (const uint32_t*)ops,
+                       npix, flog2, lz->costs, lz->est + p->n);
+    hipLaunchKernelGGL(k_lz_pick, dim3(p->n), dim3(256), 0, st, (const unsigned long long*)lz->est,
+                       (const unsigned long long*)lz->est + p->n, (const int32_t*)lz->costs_row,
+                       lz->costs);
     for (int round = 0; round < 2; ++round) {
-      hipLaunchKernelGGL(k_lz_costs, dim3(p->n), dim3(1024), 0, st, argb, (const uint32_t*)ops,
-                         npix, flog2, lz->costs);
+      if (round)
+        hipLaunchKernelGGL(k_lz_costs, dim3(p->n), dim3(1024), 0, st, argb, (const uint32_t*)ops,
+                           npix, flog2, lz->costs, (unsigned long long*)nullptr);
       hipLaunchKernelGGL(k_lz_dp, dim3(nseg, p->n), dim3(64), 0, st, argb, p->w, npix,
                          (const int32_t*)lz->costs, (const uint32_t*)lz->hoff,
                          (const uint16_t*)lz->hlen, (const uint32_t*)lz->loff,

@@ -63,6 +63,7 @@ void vp8l_engine_free(vp8l_engine* l) {
   free(l->hdr_bytes); free(l->out_off); free(l->out_size); free(l->err);
   hipFree(l->lz.runs); hipFree(l->lz.htab); hipFree(l->lz.chain); hipFree(l->lz.hoff);
   hipFree(l->lz.hlen); hipFree(l->lz.loff); hipFree(l->lz.llen); hipFree(l->lz.costs);
+  hipFree(l->lz.costs_row); hipFree(l->lz.est);
   hipFree(l->d_dcodes);
   hipFree(l->d_dpcand); hipFree(l->d_dpcost);
   for (int i = 0; i < 5; ++i)
@@ -128,6 +129,8 @@ static vp8l_engine* engine_alloc(const vp8l_params* p, int max_frames, int metho
     CHK(hipMalloc((void**)&l->lz.loff, N * np * sizeof(uint32_t)));
     CHK(hipMalloc((void**)&l->lz.llen, N * np * sizeof(uint16_t)));
     CHK(hipMalloc((void**)&l->lz.costs, N * VP8L_LZ_NCOST * sizeof(int32_t)));
+    CHK(hipMalloc((void**)&l->lz.costs_row, N * VP8L_LZ_NCOST * sizeof(int32_t)));
+    CHK(hipMalloc((void**)&l->lz.est, 2 * N * sizeof(unsigned long long)));
     {
       const int nd = vp8l_plane_dcodes(w, NULL);
       uint8_t* tab = (uint8_t*)malloc((size_t)nd);

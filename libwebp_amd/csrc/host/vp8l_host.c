@@ -198,7 +198,8 @@ void vp8l_setup_palette_params(vp8l_params* p, int w, int h, int n, int method, 
   p->hb = vp8l_histo_bits_palette(method, w, h);
   p->tb = 2;   /* unused: no predictor */
   const int nht = sub_sample(pw, p->hb) * sub_sample(h, p->hb);
-  p->k = nht < VP8L_KMAX ? nht : VP8L_KMAX;
+  /* at most VP8L_KMAX_PALETTE code groups (model: KMAX_PALETTE) */
+  p->k = nht < VP8L_KMAX_PALETTE ? nht : VP8L_KMAX_PALETTE;
 }
 
 static int32_t g_nlogn[4097];

@@ -178,6 +178,8 @@ int vp8l_launch_palette_apply(const uint8_t* rgba, size_t fstride, int rstride,
 /* L2..L5: cache sizes, provisional parse, cache-size choice (cbits[f]),
  * row parse, tile features, clustering. tabs: DEVICE tables (nlogn 4097 |
  * log2 fraction 1024, in 1/4096 bit). */
+/* Colour-indexed frames: at most this many code groups (model: KMAX_PALETTE) */
+#define VP8L_KMAX_PALETTE 8
 /* Colour-indexed frames: buffers of the cost-model parse (L3p kernels) */
 #define VP8L_LZ_NCOST (280 + 3 * 256 + 40)
 #define VP8L_LZ_HASH_SIZE (1 << 18)
@@ -190,6 +192,8 @@ typedef struct {
   uint32_t* loff;              /* n x npix: the best of the 4 candidate distances */
   uint16_t* llen;
   int32_t* costs;              /* n x VP8L_LZ_NCOST symbol costs (1/256 bit) */
+  int32_t* costs_row;          /* n x VP8L_LZ_NCOST: those of the greedy row parse */
+  unsigned long long* est;     /* 2n: the two first parses' bits (row, chain) */
   const uint8_t* dcodes;       /* distance -> plane code for distances < nd (0: none) */
   int nd;
 } vp8l_lz;

@@ -1016,6 +1016,20 @@ def lz_costs(flat, act, clen, ccode, W):
             lz_pop_costs(np.bincount(ds, minlength=NUM_DIST)))
 
 
+def lz_est_bits(flat, act, clen, ccode, W):
+    """A parse's bits (1/256) under its own symbol costs (lz_costs): every
+    symbol's cost plus the length / distance extra bits."""
+    cG, cR, cB, cA, cD = lz_costs(flat, act, clen, ccode, W)
+    a = np.asarray(flat, dtype=np.int64)
+    la = a[act == 0]
+    cp = act == 2
+    ls, lnb, _ = prefix_arrays(clen[cp])
+    ds, dnb, _ = prefix_arrays(ccode[cp])
+    return int(cG[(la >> 8) & 255].sum() + cR[(la >> 16) & 255].sum() + cB[la & 255].sum() +
+               cA[(la >> 24) & 255].sum() + cG[256 + ls].sum() + cD[ds].sum() +
+               256 * (lnb.sum() + dnb.sum()))
+
+
 def lz_dp(flat, W, costs, cands):
     """Shortest-path parse per LZ_SEG segment. Per position, in order: the
     literal, then each (distance, length) of cands at the lengths
@@ -1086,13 +1100,20 @@ def lz_dp(flat, W, costs, cands):
 
 
 def palette_parse(argb, dists, lens):
-    """The parse of a colour-indexed frame (see above): greedy parse over the
-    two matches (lz_greedy) -> costs -> cost-model parse -> its costs ->
-    cost-model parse. (dists, lens: unused since round 6.)"""
+    """The parse of a colour-indexed frame (see above): a first parse -> its
+    costs -> cost-model parse -> its costs -> cost-model parse. The first
+    parse is the cheaper, under its own symbol costs (lz_est_bits), of the
+    greedy row parse over the 4 local candidates and the greedy parse over
+    the two matches (lz_greedy; the row parse on ties) -- the reference
+    likewise keeps the cheapest of its first parses (GetBackwardReferences,
+    backward_references_enc.c:934-998)."""
     H, W = argb.shape
     flat = argb.ravel().astype(np.int64)
     cands = [lz_hash_search(flat, W), lz_local(flat, W)]
-    act, clen, ccode = lz_greedy(flat, W, cands)
+    row = [v.ravel() for v in parse(argb, np.zeros((H, W), dtype=bool), dists, lens)]
+    chain = lz_greedy(flat, W, cands)
+    act, clen, ccode = (chain if lz_est_bits(flat, *chain, W) < lz_est_bits(flat, *row, W)
+                        else row)
     for _ in range(2):
         act, clen, ccode = lz_dp(flat, W, lz_costs(flat, act, clen, ccode, W), cands)
     return act.reshape(H, W), clen.reshape(H, W), ccode.reshape(H, W)
@@ -1475,6 +1496,10 @@ def flog2(v):
 
 
 KMAX = 16
+# colour-indexed frames: at most 8 code groups (their few-symbol codes make a
+# group's header a larger share: 320x240 4-colour graphics 2372 -> 2298 B,
+# reference 2302)
+KMAX_PALETTE = 8
 CLUSTER_ITERS = 6
 
 
@@ -1960,7 +1985,7 @@ def encode(rgba, method=4, cache_bits=AUTO_CACHE, kmax=KMAX, return_parts=False,
     tile = (np.arange(H) >> hb)[:, None] * tw + (np.arange(PW) >> hb)[None, :]
     Ht = tile_histograms(S, tile, nt, al)
     npix = np.bincount(tile.ravel(), minlength=nt)
-    K = min(kmax, nt)
+    K = min(kmax if pal is None else min(kmax, KMAX_PALETTE), nt)
     assign = cluster_tiles(Ht, npix, al, K) if K > 1 else np.zeros(nt, dtype=np.int64)
     assign_raw = assign.copy()
     hc_raw = np.zeros((KMAX, al.ns), dtype=np.int64)

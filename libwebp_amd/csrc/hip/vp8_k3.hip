@@ -2000,7 +2000,11 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
   __syncthreads();
 
   const int rd_opt = P->rd_opt;
+#ifdef K3_NO_I4   // (timing build only, wrong output: no intra-4 search)
+  const int max_i4_bits = 0;
+#else
   const int max_i4_bits = P->max_i4_header_bits;
+#endif
   const int use_derr = P->use_derr;
   const int max_count = P->max_count;
   const bool trellis_all = TR && rd_opt >= 3;

@@ -925,6 +925,8 @@ __device__ __forceinline__ uint64_t k3_clock() {
   } while (0)
 #endif
 
+constexpr score_t kI4NoBound = (score_t)0x7fffffffffffffffll;
+
 struct I4Result {
   int ok;
   score_t H, score;
@@ -968,12 +970,21 @@ __device__ __forceinline__ int edge_off0(int k) {
   return (((4 - k) * 24) & m) | ((k - 4) & ~m);
 }
 
-template <bool TRELLIS>
+// HPB (K3X helper pairs): the search starts without the intra-16 bound and
+// takes it (*bound) once *bound_flag >= bound_at, i.e. once the helper has
+// published its intra-16 choice: from then on it ends early like the
+// sequential search (the same choice: the running score only grows). The
+// flag is read by wave 0 before a sub-block's barrier and handed to the
+// other waves through L.redw[2 + parity] (two slots: wave 0 can store the
+// next sub-block's reading before a slower wave has read this one's), so
+// all waves switch together.
+template <bool TRELLIS, bool HPB = false>
 __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
                            const MBCtx& ctx, int tid, int x0,
                            int mbw, const uint8_t* predtop, const uint8_t* yl,
                            const uint8_t* yt, bool search, score_t rd_score, int max_bits,
-                           uint64_t* sp) {
+                           uint64_t* sp, const int32_t* bound_flag = nullptr,
+                           int32_t bound_at = 0, const score_t* bound = nullptr) {
 #ifdef K3_SUBPROF
   uint64_t sp_last = k3_clock();
 #endif
@@ -1093,7 +1104,17 @@ __device__ I4Result run_i4(const K3G& G, K3S& L, const vp8g_seg& S,
     }
     }   // busy
     SUBST(5);
+    bool hpb_have = false;
+    if constexpr (HPB) {
+      hpb_have = rd_score != kI4NoBound;
+      if (!hpb_have && tid < 64)   // (a whole wave: a lone-lane store here spills)
+        L.redw[2 + (i4 & 1)] =
+            __hip_atomic_load(bound_flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= bound_at;
+    }
     WB();
+    if constexpr (HPB) {
+      if (!hpb_have && __builtin_amdgcn_readfirstlane(L.redw[2 + (i4 & 1)])) rd_score = *bound;
+    }
     int bm;
     if (search) {
       // argmin, ties to the lower mode. The slot read here was last written
@@ -1479,10 +1500,12 @@ struct K3XL {
   // intra-4 search; MBs handed over / finished (raster index + 1), the MB's
   // context, and the helper's two decisions
   int32_t hp_go, hp_done;
+  int32_t hp_i16, hp_pad3;   // MBs whose intra-16 choice (hp_rd16) is out (raster index + 1)
   uint32_t hp_ctx_t, hp_ctx_l;
   int32_t hp_seg, hp_best16, hp_bu, hp_pad;
   uint32_t hp_nz16, hp_pad2;
   score_t hp_D16, hp_SD16, hp_H16, hp_R16, hp_bH, hp_bsc;
+  score_t hp_rd16;   // the intra-16 choice's score with lambda_mode (the intra-4 bound)
 };
 
 __device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
@@ -1970,7 +1993,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     for (int k = gt; k < 16 * mbw; k += NW * K3T) xuvtop[k] = 127;
     for (int k = gt; k < mbw; k += NW * K3T) xnzw[k] = 0;
     for (int k = gt; k < 4 * mbw; k += NW * K3T) { xpredtop[k] = 0; xtopderr[k] = 0; }
-    if (gt == 0) { XL.lcver = 0; XL.claim = 0; XL.hp_go = 0; XL.hp_done = 0; }
+    if (gt == 0) { XL.lcver = 0; XL.claim = 0; XL.hp_go = 0; XL.hp_done = 0; XL.hp_i16 = 0; }
   }
   if (gt < 4) G.max_edge[gt] = 0;
   if (gt == 0) {
@@ -2088,6 +2111,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           if (tid < 64) {   // (a whole wave)
             XL.hp_best16 = best16; XL.hp_nz16 = nz16;
             XL.hp_D16 = D16; XL.hp_SD16 = SD16; XL.hp_H16 = H16; XL.hp_R16 = R16;
+            XL.hp_rd16 = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
           }
           if ((nz16 & 0x100ffff) == 0x1000000 && D16 > S.min_disto) {   // StoreMaxDelta
             int mv = iabs_(M.lvdc[best16][1]);
@@ -2095,8 +2119,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
             mv = max(mv, iabs_(M.lvdc[best16][4]));
             if (tid == 0) atomicMax(&G.max_edge[segid], mv);
           }
-          // the chroma candidates overwrite M.mres: every wave has read it
+          // the chroma candidates overwrite M.mres: every wave has read it;
+          // the intra-16 score goes out now (the search's bound)
           wbar(L);
+          if (tid == 0) publish(&XL.hp_i16, (int32_t)mb + 1);
           eval_uv(G, M, S, ctx, tid, x, derrx, use_derr, L);
           int bu = 0;
           score_t bsc = 0, bH = 0;
@@ -2420,18 +2446,20 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         }
         K3_STAMP(2);
         const uint64_t tr_i4 = TR_NOW();
-        constexpr score_t kNoBound = (score_t)0x7fffffffffffffffll;
         I4Result r4;
         r4.ok = 0; r4.H = 0; r4.score = 0; r4.nz = 0;
         if (max_i4_bits > 0) {
+          const int32_t at = (int32_t)mb + 1;
           if constexpr (TR) {
-            r4 = trellis_all ? run_i4<true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
-                                            kNoBound, max_i4_bits, substamps)
-                             : run_i4<false>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
-                                             kNoBound, max_i4_bits, substamps);
+            r4 = trellis_all ? run_i4<true, true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
+                                                  kI4NoBound, max_i4_bits, substamps, &XL.hp_i16,
+                                                  at, &XL.hp_rd16)
+                             : run_i4<false, true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
+                                                   kI4NoBound, max_i4_bits, substamps, &XL.hp_i16,
+                                                   at, &XL.hp_rd16);
           } else {
-            r4 = run_i4<false>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true, kNoBound,
-                               max_i4_bits, substamps);
+            r4 = run_i4<false, true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true, kI4NoBound,
+                                     max_i4_bits, substamps, &XL.hp_i16, at, &XL.hp_rd16);
           }
         }
         tr_uv = TR_NOW();

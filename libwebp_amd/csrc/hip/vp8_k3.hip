@@ -1501,6 +1501,8 @@ struct K3XL {
   // context, and the helper's two decisions
   int32_t hp_go, hp_done;
   int32_t hp_i16, hp_pad3;   // MBs whose intra-16 choice (hp_rd16) is out (raster index + 1)
+  int32_t hp_pre;            // the MB whose source the helper has loaded into its yin (+ 1)
+  int32_t hp_bnd;            // MBs whose boundary (ytop, uvtop, nzw, predtop, topderr) is out
   uint32_t hp_ctx_t, hp_ctx_l;
   int32_t hp_seg, hp_best16, hp_bu, hp_pad;
   uint32_t hp_nz16, hp_pad2;
@@ -1993,7 +1995,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     for (int k = gt; k < 16 * mbw; k += NW * K3T) xuvtop[k] = 127;
     for (int k = gt; k < mbw; k += NW * K3T) xnzw[k] = 0;
     for (int k = gt; k < 4 * mbw; k += NW * K3T) { xpredtop[k] = 0; xtopderr[k] = 0; }
-    if (gt == 0) { XL.lcver = 0; XL.claim = 0; XL.hp_go = 0; XL.hp_done = 0; XL.hp_i16 = 0; }
+    if (gt == 0) {
+      XL.lcver = 0; XL.claim = 0;
+      XL.hp_go = 0; XL.hp_done = 0; XL.hp_i16 = 0; XL.hp_pre = 0; XL.hp_bnd = 0;
+    }
   }
   if (gt < 4) G.max_edge[gt] = 0;
   if (gt == 0) {
@@ -2147,6 +2152,31 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           wbar(L);
           if (tid == 0) publish(&XL.hp_done, (int32_t)mb + 1);
           TR_SINCE(K3TR_I16, tr_e);   // (helper: intra-16 + chroma)
+          // the next MB's source into this worker's yin (the main copies it
+          // from LDS instead of waiting for its own global loads)
+          if (x + 1 < mbw) {
+            load_mb(Yp, Up, Vp, w, h, x + 1, y, L.yin, tid, K3T);
+            wbar(L);
+            if (tid == 0) publish(&XL.hp_pre, (int32_t)mb + 2);
+          }
+          // column x's boundary record for the next row's workgroup, off the
+          // main worker's path (the stores' drain)
+          if (y < mbh - 1) {
+            if (!wait_ge(G, L, &XL.hp_bnd, (int32_t)mb + 1, 9)) break;
+            if (tid < 64) {
+              if (tid < 11) {
+                uint32_t v;
+                if (tid < 4) v = reinterpret_cast<const uint32_t*>(ytop + 16 * x)[tid];
+                else if (tid < 8) v = reinterpret_cast<const uint32_t*>(uvtop + 16 * x)[tid - 4];
+                else if (tid == 8) v = nzw[x];
+                else if (tid == 9) v = reinterpret_cast<const uint32_t*>(predtop + 4 * x)[0];
+                else v = reinterpret_cast<const uint32_t*>(topderr + 4 * x)[0];
+                st_sc1(xrec + ((size_t)y * mbw + x) * XS_REC_WORDS + tid, v);
+              }
+              vm_drain();
+              if (tid == 0) st_sc1(&xrowdone[y], x + 1);
+            }
+          }
         }
       }
     }
@@ -2394,7 +2424,14 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
 #ifdef K3_PF
       put_mb256(pf, L.yin, tid);
 #else
-      load_mb(Yp, Up, Vp, w, h, x, y, L.yin, tid, K3T);
+      if (HP && x > 0) {   // the source the helper loaded (LDS to LDS)
+        if (!wait_ge(G, L, &XL.hp_pre, (int32_t)mb + 1, 10)) break;
+        const K3S& Hs = reinterpret_cast<const K3S*>(smem + sizeof(K3G) + PAD)[1];
+        if (tid < 16 * BPS / 4)
+          reinterpret_cast<uint32_t*>(L.yin)[tid] = reinterpret_cast<const uint32_t*>(Hs.yin)[tid];
+      } else {
+        load_mb(Yp, Up, Vp, w, h, x, y, L.yin, tid, K3T);
+      }
 #endif
       wbar(L);
       int segid = segmap[mb];
@@ -2444,6 +2481,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           XL.hp_ctx_t = ctx.t; XL.hp_ctx_l = ctx.l; XL.hp_seg = segid;
           publish(&XL.hp_go, (int32_t)mb + 1);
         }
+        TR_SINCE(K3TR_I16, tr_mb);   // (main worker of a pair: load + predictions)
         K3_STAMP(2);
         const uint64_t tr_i4 = TR_NOW();
         I4Result r4;
@@ -2866,7 +2904,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       if constexpr (X) {
         // the last worker's row feeds worker 0 of the next workgroup: its
         // boundary record for column x, drained, then the column count
-        if (wk == (HP ? 0 : NW - 1) && y < mbh - 1 && tid < 64) {
+        const uint64_t tr_x = TR_NOW();
+        if (HP) {   // the helper publishes the record
+          if (tid == 0) publish(&XL.hp_bnd, (int32_t)mb + 1);
+        } else if (wk == NW - 1 && y < mbh - 1 && tid < 64) {
           if (tid < 11) {
             uint32_t v;
             if (tid < 4) v = reinterpret_cast<const uint32_t*>(ytop + 16 * x)[tid];
@@ -2879,6 +2920,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           vm_drain();
           if (tid == 0) st_sc1(&xrowdone[y], x + 1);
         }
+        TR_SINCE(K3TR_REPLAY, tr_x);   // (K3X: the boundary record's publish)
       }
       if ((x + 1) % XS_SNAP_MBS == 0 && x + 1 < mbw) {
         // every XS_SNAP_MBS-th column: the statistics snapshot (see fold_mbs);

@@ -1553,6 +1553,23 @@ __device__ __forceinline__ void probas_from_x(uint8_t* dst, const uint8_t* xsrc,
     reinterpret_cast<uint32_t*>(dst)[k] = ld_sc1(reinterpret_cast<const uint32_t*>(xsrc) + k);
 }
 
+// the four 16x16 and four chroma predictions of an MB (quant_enc.c:469-479)
+__device__ __forceinline__ void predict_mb(K3S& L, const uint8_t* yl, const uint8_t* ul,
+                                           const uint8_t* vl, const uint8_t* yt, const uint8_t* uvt,
+                                           bool hl, bool ht, int tid) {
+  const int dcy = dc_value(yl, yt, hl, ht, 16, 5);
+  for (int k = tid; k < 1024; k += K3T) {
+    const int m = k >> 8, p = k & 255;
+    L.p16[m][p] = pred_sample(m, 16, p & 15, p >> 4, yl, yt, hl, ht, dcy);
+  }
+  const int dcu = dc_value(ul, uvt, hl, ht, 8, 4);
+  const int dcv = dc_value(vl, uvt + 8, hl, ht, 8, 4);
+  for (int k = tid; k < 512; k += K3T) {
+    const int m = k >> 7, p = k & 127, px = p & 15, py = p >> 4, c = px >> 3;
+    L.puv[m][p] = pred_sample(m, 8, px & 7, py, c ? vl : ul, uvt + 8 * c, hl, ht, c ? dcv : dcu);
+  }
+}
+
 __device__ __forceinline__ void publish(int32_t* p, int32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -2077,6 +2094,11 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           MBCtx ctx;
           ctx.t = __builtin_amdgcn_readfirstlane(XL.hp_ctx_t);
           ctx.l = __builtin_amdgcn_readfirstlane(XL.hp_ctx_l);
+          // the 16x16 and chroma predictions from the main's edges (its left
+          // samples and the row above it pulled, unchanged until this MB is done)
+          predict_mb(M, M.yl_mem + 1, M.ul_mem + 1, M.vl_mem + 1, xytop + 16 * x, xuvtop + 16 * x,
+                     x > 0, y > 0, tid);
+          wbar(L);
           if constexpr (TR) {
             if (trellis_all) eval_i16<true>(G, M, S, ctx, tid, L);
             else eval_i16<false>(G, M, S, ctx, tid, L);
@@ -2445,19 +2467,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       MBCtx ctx;
       nz_flags(xr ? xnzw[x] : nzw[x], nzw[x - 1], left_dc, ctx);
 
-      // ---- predictions (quant_enc.c:469-479)
+      // ---- predictions (quant_enc.c:469-479; a helper pair's helper makes
+      // them, the main worker's intra-4 search does not read them)
       {
-        const int dcy = dc_value(yl, yt, hl, ht, 16, 5);
-        for (int k = tid; k < 1024; k += K3T) {
-          const int m = k >> 8, p = k & 255;
-          L.p16[m][p] = pred_sample(m, 16, p & 15, p >> 4, yl, yt, hl, ht, dcy);
-        }
-        const int dcu = dc_value(ul, uvt, hl, ht, 8, 4);
-        const int dcv = dc_value(vl, uvt + 8, hl, ht, 8, 4);
-        for (int k = tid; k < 512; k += K3T) {
-          const int m = k >> 7, p = k & 127, px = p & 15, py = p >> 4, c = px >> 3;
-          L.puv[m][p] = pred_sample(m, 8, px & 7, py, c ? vl : ul, uvt + 8 * c, hl, ht, c ? dcv : dcu);
-        }
+        if (!HP) predict_mb(L, yl, ul, vl, yt, uvt, hl, ht, tid);
         // texture (Hadamard) measure of the 16 source blocks, shared by the
         // intra16 and intra4 distortions (VP8TDisto4x4 / 16x16)
         const int b = tid >> 4, j = tid & 15;

@@ -1503,6 +1503,9 @@ struct K3XL {
   int32_t hp_i16, hp_pad3;   // MBs whose intra-16 choice (hp_rd16) is out (raster index + 1)
   int32_t hp_pre;            // the MB whose source the helper has loaded into its yin (+ 1)
   int32_t hp_bnd;            // MBs whose boundary (ytop, uvtop, nzw, predtop, topderr) is out
+  int32_t hp_tokgo, hp_tok;  // MBs handed to / tokenized by the helper (+ 1)
+  uint32_t tk_ctx_t, tk_ctx_l;
+  int32_t tk_first, tk_pad;  // the handed MB's context and first block (0: intra-16)
   uint32_t hp_ctx_t, hp_ctx_l;
   int32_t hp_seg, hp_best16, hp_bu, hp_pad;
   uint32_t hp_nz16, hp_pad2;
@@ -2015,6 +2018,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
     if (gt == 0) {
       XL.lcver = 0; XL.claim = 0;
       XL.hp_go = 0; XL.hp_done = 0; XL.hp_i16 = 0; XL.hp_pre = 0; XL.hp_bnd = 0;
+      XL.hp_tokgo = 0; XL.hp_tok = 0;
     }
   }
   if (gt < 4) G.max_edge[gt] = 0;
@@ -2181,6 +2185,90 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
             wbar(L);
             if (tid == 0) publish(&XL.hp_pre, (int32_t)mb + 2);
           }
+          // ---- this MB's tokens (token_enc.c:113-193) into its row slot, off
+          // the main worker's path: the main has committed the MB and made
+          // its blocks' last non-zero positions (M.blast); one (block,
+          // position) item per thread, counts + scan + writes in parallel,
+          // the statistics into the main's pending deltas
+          {
+            if (!wait_ge(G, L, &XL.hp_tokgo, (int32_t)mb + 1, 11)) break;
+            const int rtid = opaque(rtid_k);
+            const int first_blk = __builtin_amdgcn_readfirstlane(XL.tk_first);
+            const bool is_i16 = first_blk == 0;
+            MBCtx tc;
+            tc.t = __builtin_amdgcn_readfirstlane(XL.tk_ctx_t);
+            tc.l = __builtin_amdgcn_readfirstlane(XL.tk_ctx_l);
+            const uint32_t rfill = rows ? M.rowfill : 0u;
+            const uint64_t nzb = __ballot(lane >= first_blk && lane < 25 && M.blast[lane] >= 0);
+            auto blk_param = [&](int k) -> int {
+              if (k < first_blk || k >= 25) return -1;
+              if (k == 0) return 1 | ((tc.top(8) + tc.left(8)) << 8);
+              if (k <= 16) {
+                const int b = k - 1, bx = b & 3, by = b >> 2;
+                const int t = by == 0 ? tc.top(bx) : (int)((nzb >> (k - 4)) & 1);
+                const int l = bx == 0 ? tc.left(by) : (int)((nzb >> (k - 1)) & 1);
+                return (is_i16 ? 0 | (1 << 4) : 3) | ((t + l) << 8);
+              }
+              const int b = k - 17, ch = b >> 2, k4 = b & 3, bx = k4 & 1, by = k4 >> 1;
+              const int t = by == 0 ? tc.top(4 + 2 * ch + bx) : (int)((nzb >> (k - 2)) & 1);
+              const int l = bx == 0 ? tc.left(4 + 2 * ch + by) : (int)((nzb >> (k - 1)) & 1);
+              return 2 | ((t + l) << 8);
+            };
+            int lvi[2], lvp[2], cnt[2], bi[2], last[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const int item = rtid + K3T * q, k = item >> 4, n = item & 15;
+              int v = 0, vp = 0;
+              if (k < 25 && k >= first_blk) {
+                const int16_t* lvb = blk_levels(M, k);
+                v = lvb[n];
+                vp = n > 0 ? lvb[n - 1] : 0;
+              }
+              lvi[q] = v;
+              lvp[q] = vp;
+              bi[q] = blk_param(k);
+              last[q] = k < 25 ? M.blast[k] : -1;
+              cnt[q] = bi[q] < 0 ? 0 : pos_count((bi[q] >> 4) & 15, n, lvi[q], lvp[q], last[q]);
+            }
+            int inc0 = cnt[0], inc1 = cnt[1];
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+              const int v0 = __shfl_up(inc0, off), v1 = __shfl_up(inc1, off);
+              if (lane >= off) { inc0 += v0; inc1 += v1; }
+            }
+            const int wv = rtid >> 6;
+            if (lane == 63) { L.wsum[0][wv] = inc0; L.wsum[1][wv] = inc1; }
+            wbar(L);
+            int pre0 = 0, pre1 = 0, tot0 = 0, tot1 = 0;
+#pragma unroll
+            for (int w2 = 0; w2 < 4; ++w2) {
+              const int s0 = L.wsum[0][w2], s1 = L.wsum[1][w2];
+              if (w2 < wv) { pre0 += s0; pre1 += s1; }
+              tot0 += s0; tot1 += s1;
+            }
+            uint16_t* slot = rows ? tok_base + (size_t)y * a.rowcap + rfill
+                                  : tok_base + (size_t)mb * VP8G_MAX_TOKENS_PER_MB;
+            const int off0 = pre0 + inc0 - cnt[0];
+            const int off1 = tot0 + pre1 + inc1 - cnt[1];
+            const bool over = rows && rfill + (uint32_t)(tot0 + tot1) > a.rowcap;
+            if (over) { cnt[0] = 0; cnt[1] = 0; }
+            if (cnt[0])
+              pos_tokens<true>(bi[0] & 15, (bi[0] >> 4) & 15, bi[0] >> 8, rtid & 15, lvi[0], lvp[0],
+                               last[0], slot + off0, M.rdelta);
+            if (cnt[1])
+              pos_tokens<true>(bi[1] & 15, (bi[1] >> 4) & 15, bi[1] >> 8, rtid & 15, lvi[1], lvp[1],
+                               last[1], slot + off1, M.rdelta);
+            if (rtid == 0) {
+              M.rowcnt[x] = (uint16_t)(tot0 + tot1);
+              if (rows) {
+                M.rowpos[x] = rfill;
+                M.rowfill = rfill + (uint32_t)(tot0 + tot1);
+                if (over) atomicOr(&G.tok_err, VP8G_ERR_ARENA);
+              }
+            }
+            wbar(L);
+            if (tid == 0) publish(&XL.hp_tok, (int32_t)mb + 1);
+          }
           // column x's boundary record for the next row's workgroup, off the
           // main worker's path (the stores' drain)
           if (y < mbh - 1) {
@@ -2254,6 +2342,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
             if (!wait_gx(G, L, &XH->fold_ptr, (int32_t)fold_from, XH)) break;
           } else {
             if (!wait_ge(G, L, (const int32_t*)&G.fold_ptr, (int32_t)fold_from, 1)) break;
+          }
+          if constexpr (HP) {   // the helper's tokens of this row's MBs before this one
+            if (x > 0 && !wait_ge(G, L, &XL.hp_tok, (int32_t)mb, 11)) break;
           }
           const uint64_t tr_f = TR_NOW();
           TR_ADD(K3TR_REFR_WAIT, tr_f - tr_w);
@@ -2784,6 +2875,12 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       // every wave derives the blocks' nz bits and its items' block
       // parameters itself (no second barrier): type | first << 4 | ctx << 8
       nzb = __ballot(lane >= first_blk && lane < 25 && L.blast[lane] >= 0);
+      if constexpr (HP) {   // the helper writes the tokens (see there)
+        if (tid == 0) {
+          XL.tk_ctx_t = ctx.t; XL.tk_ctx_l = ctx.l; XL.tk_first = first_blk;
+          publish(&XL.hp_tokgo, (int32_t)mb + 1);
+        }
+      }
       auto blk_param = [&](int k) -> int {
         if (k < first_blk || k >= 25) return -1;
         if (k == 0) return 1 | ((ctx.top(8) + ctx.left(8)) << 8);
@@ -2798,7 +2895,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         const int l = bx == 0 ? ctx.left(4 + 2 * ch + by) : (int)((nzb >> (k - 1)) & 1);
         return 2 | ((t + l) << 8);
       };
-      {
+      if constexpr (!HP) {
         int cnt[2], bi[2], last[2];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -2936,6 +3033,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         TR_SINCE(K3TR_REPLAY, tr_x);   // (K3X: the boundary record's publish)
       }
       if ((x + 1) % XS_SNAP_MBS == 0 && x + 1 < mbw) {
+        if constexpr (HP) {   // the helper's tokens (and their pending deltas) up to here
+          if (!wait_ge(G, L, &XL.hp_tok, (int32_t)mb + 1, 11)) break;
+        }
         // every XS_SNAP_MBS-th column: the statistics snapshot (see fold_mbs);
         // every K3_DFULL_EVERY-th the 16-bit count / ones of the row's pending
         // deltas checked: an MB adds at most 288 to one slot (9 positions of a
@@ -2977,6 +3077,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       TR_SINCE(K3TR_MB, tr_mb);
     }
     if (L.myabort) break;
+    if constexpr (HP) {   // the helper's tokens of the whole row
+      if (!wait_ge(G, L, &XL.hp_tok, (int32_t)(y + 1) * mbw, 11)) break;
+    }
     // row end: fold this row's remaining MBs once the rows above are folded
     const uint64_t tr_fw = TR_NOW();
     if constexpr (X) {

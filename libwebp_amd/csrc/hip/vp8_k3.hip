@@ -2199,7 +2199,23 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
             tc.t = __builtin_amdgcn_readfirstlane(XL.tk_ctx_t);
             tc.l = __builtin_amdgcn_readfirstlane(XL.tk_ctx_l);
             const uint32_t rfill = rows ? M.rowfill : 0u;
-            const uint64_t nzb = __ballot(lane >= first_blk && lane < 25 && M.blast[lane] >= 0);
+            int lvi[2], lvp[2], cnt[2], bi[2], last[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const int item = rtid + K3T * q, k = item >> 4, n = item & 15;
+              int v = 0, vp = 0;
+              if (k < 25 && k >= first_blk) {
+                const int16_t* lvb = blk_levels(M, k);
+                v = lvb[n];
+                vp = n > 0 ? lvb[n - 1] : 0;
+              }
+              lvi[q] = v;
+              lvp[q] = vp;
+              const int lq = max16(v != 0 ? n : -1);
+              if (n == 0 && k < 32) L.blast[k] = lq;
+            }
+            wbar(L);
+            const uint64_t nzb = __ballot(lane >= first_blk && lane < 25 && L.blast[lane] >= 0);
             auto blk_param = [&](int k) -> int {
               if (k < first_blk || k >= 25) return -1;
               if (k == 0) return 1 | ((tc.top(8) + tc.left(8)) << 8);
@@ -2214,20 +2230,11 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
               const int l = bx == 0 ? tc.left(4 + 2 * ch + by) : (int)((nzb >> (k - 1)) & 1);
               return 2 | ((t + l) << 8);
             };
-            int lvi[2], lvp[2], cnt[2], bi[2], last[2];
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
               const int item = rtid + K3T * q, k = item >> 4, n = item & 15;
-              int v = 0, vp = 0;
-              if (k < 25 && k >= first_blk) {
-                const int16_t* lvb = blk_levels(M, k);
-                v = lvb[n];
-                vp = n > 0 ? lvb[n - 1] : 0;
-              }
-              lvi[q] = v;
-              lvp[q] = vp;
               bi[q] = blk_param(k);
-              last[q] = k < 25 ? M.blast[k] : -1;
+              last[q] = k < 25 ? L.blast[k] : -1;
               cnt[q] = bi[q] < 0 ? 0 : pos_count((bi[q] >> 4) & 15, n, lvi[q], lvp[q], last[q]);
             }
             int inc0 = cnt[0], inc1 = cnt[1];
@@ -2857,29 +2864,36 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       const uint32_t rfill = rows ? L.rowfill : 0u;
       uint64_t nzb = 0;
       int lvi[2], lvp[2];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {   // items rtid and rtid + 256 = block*16 + pos
-        const int item = rtid + K3T * q, k = item >> 4, n = item & 15;
-        int v = 0, vp = 0;
-        if (k < 25 && k >= first_blk) {
-          const int16_t* lvb = blk_levels(L, k);
-          v = lvb[n];
-          vp = n > 0 ? lvb[n - 1] : 0;
-        }
-        lvi[q] = v;
-        lvp[q] = vp;
-        const int last = max16(v != 0 ? n : -1);
-        if (n == 0 && k < 32) L.blast[k] = last;
-      }
-      wbar(L);
-      // every wave derives the blocks' nz bits and its items' block
-      // parameters itself (no second barrier): type | first << 4 | ctx << 8
-      nzb = __ballot(lane >= first_blk && lane < 25 && L.blast[lane] >= 0);
-      if constexpr (HP) {   // the helper writes the tokens (see there)
+      if constexpr (HP) {
+        // the helper writes the tokens (see there); the blocks' nz bits come
+        // from the decision's (rd_nz: luma blocks 0-15 -- AC only for
+        // intra-16 --, chroma << 16, the intra-16 DC block << 24), in token
+        // block order (0 = Y2, 1-16 luma, 17-24 chroma)
+        nzb = ((uint64_t)(rd_nz & 0xffffu) << 1) | ((uint64_t)((rd_nz >> 16) & 0xffu) << 17) |
+              (is_i16 ? (uint64_t)((rd_nz >> 24) & 1u) : 0ull);
         if (tid == 0) {
           XL.tk_ctx_t = ctx.t; XL.tk_ctx_l = ctx.l; XL.tk_first = first_blk;
           publish(&XL.hp_tokgo, (int32_t)mb + 1);
         }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {   // items rtid and rtid + 256 = block*16 + pos
+          const int item = rtid + K3T * q, k = item >> 4, n = item & 15;
+          int v = 0, vp = 0;
+          if (k < 25 && k >= first_blk) {
+            const int16_t* lvb = blk_levels(L, k);
+            v = lvb[n];
+            vp = n > 0 ? lvb[n - 1] : 0;
+          }
+          lvi[q] = v;
+          lvp[q] = vp;
+          const int last = max16(v != 0 ? n : -1);
+          if (n == 0 && k < 32) L.blast[k] = last;
+        }
+        wbar(L);
+        // every wave derives the blocks' nz bits and its items' block
+        // parameters itself (no second barrier): type | first << 4 | ctx << 8
+        nzb = __ballot(lane >= first_blk && lane < 25 && L.blast[lane] >= 0);
       }
       auto blk_param = [&](int k) -> int {
         if (k < first_blk || k >= 25) return -1;

@@ -1217,9 +1217,15 @@ fail:
  * by several engines cannot keep up with, while on the
  * device it adds a K4 stream of ~1/13 of the frame's tokens. */
 #define P0_DEVICE_BELOW 8   /* host threads per rank */
-static int use_gpu_p0(const WebPGpuBatch* b) {
+/* Partition 0 on the device when the host has few threads (the 8-rank
+ * budget) or the call has few frames: a single picture's host tail (1.2 ms
+ * for 1080p) is latency with nothing beside it to hide behind, the device
+ * path adds 0.3 ms of K4 (one 1080p frame 32.4 -> 31.6 ms,
+ * profiles/r6/k3x/p0/); a batch's host tails overlap the other instances'
+ * kernels (256 x 1080p at 16 threads: 4782 host vs 4663 MP/s device) */
+static int use_gpu_p0(const WebPGpuBatch* b, int n) {
   if (b->gpu_p0 >= 0) return b->gpu_p0;
-  return b->threads < P0_DEVICE_BELOW;
+  return b->threads < P0_DEVICE_BELOW || n <= VP8G_XSPLIT_MAX_FRAMES;
 }
 
 int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
@@ -1274,7 +1280,7 @@ int vp8g_engine_run_yuv(WebPGpuBatch* b, int n) {
   }
   /* partition 0: coded on the host threads while K4 runs, or (gpu_p0) its
      header tokens built here and the rest done by k_p0_modes + K4 */
-  const int p0dev = !b->host_emit && use_gpu_p0(b);
+  const int p0dev = !b->host_emit && use_gpu_p0(b, n);
   b->p0_dev = p0dev;
   b->last_ns = ns;
   if (p0dev) {

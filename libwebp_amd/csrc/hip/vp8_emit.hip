@@ -941,9 +941,11 @@ extern "C" int vp8g_launch_partition(uint16_t* tokens, size_t tok_cap, int n,
 // or the 16 intra-4 modes, chroma mode) as fixed-probability tokens behind
 // the frame's header tokens (vp8h_p0_header), for K4 to code as one more
 // stream. The host's code_intra_modes (host/vp8_host.c) is the same walk.
-// One 1,024-thread workgroup per frame: a thread takes a run of consecutive
-// raster MBs, counts their tokens, a block scan places the runs, then every
-// thread writes its MBs' tokens. The intra-4 contexts are read from mbinfo
+// G 1,024-thread workgroups per frame, each a chunk of <= 1,024 raster MBs
+// (one frame on one CU took 334 us at 1080p, on the latency path of a single
+// picture): a workgroup counts the tokens of the MBs before its chunk (a
+// block sum), a thread takes a run of consecutive MBs of the chunk, counts
+// them, a block scan places the runs, then every thread writes its MBs' tokens. The intra-4 contexts are read from mbinfo
 // directly: left = the previous MB of the row, top = the MB above, B_DC_PRED
 // (0) across the picture edges; an intra-16 MB's mode fills its 16 entries.
 #define P0T 1024
@@ -975,26 +977,43 @@ __global__ __launch_bounds__(P0T) void k_p0_modes(const uint8_t* __restrict__ mb
                                                  int mbh, const vp8g_p0_par* __restrict__ par,
                                                  const uint16_t* __restrict__ hdr,
                                                  uint16_t* __restrict__ tokens,
-                                                 vp8g_emit_meta* __restrict__ meta, int meta_base) {
-  const int f = blockIdx.x, t = threadIdx.x, nmb = mbw * mbh;
+                                                 vp8g_emit_meta* __restrict__ meta, int meta_base,
+                                                 int G) {
+  const int f = blockIdx.x / G, g = blockIdx.x % G, t = threadIdx.x, nmb = mbw * mbh;
   const vp8g_p0_par P = par[f];
   vp8g_emit_meta* M = meta + meta_base + f;
   if (P.nhdr == 0xffffffffu) {   // the frame failed: an empty stream
-    if (t == 0) { M->ntok = 0; M->nseg = 0; }
+    if (g == 0 && t == 0) { M->ntok = 0; M->nseg = 0; }
     return;
   }
   uint16_t* out = tokens + M->tok_off;
-  const uint16_t* h = hdr + (size_t)f * VP8G_P0_HDR_CAP;
-  for (uint32_t k = t; k < P.nhdr; k += P0T) out[k] = h[k];
+  if (g == 0) {
+    const uint16_t* h = hdr + (size_t)f * VP8G_P0_HDR_CAP;
+    for (uint32_t k = t; k < P.nhdr; k += P0T) out[k] = h[k];
+  }
   const uint8_t* info = mbinfo + (size_t)f * nmb * VP8G_MBINFO_BYTES;
-  const int per = (nmb + P0T - 1) / P0T;
-  const int m0 = min(t * per, nmb), m1 = min(m0 + per, nmb);
+  const int lane = t & 63, wv = t >> 6;
+  __shared__ uint32_t wsum[P0T / 64];
+  // the tokens of the MBs before this workgroup's chunk
+  const int chunk = (nmb + G - 1) / G;
+  const int c0 = min(g * chunk, nmb), c1 = min(c0 + chunk, nmb);
+  uint32_t prior = 0;
+  for (int m = t; m < c0; m += P0T)
+    prior += p0_mb_count(info + (size_t)m * VP8G_MBINFO_BYTES, P.update_map, P.use_skip);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) prior += __shfl_xor(prior, o);
+  if (lane == 0) wsum[wv] = prior;
+  __syncthreads();
+  prior = 0;
+#pragma unroll
+  for (int k = 0; k < P0T / 64; ++k) prior += wsum[k];
+  __syncthreads();   // wsum is reused by the scan below
+  const int per = (c1 - c0 + P0T - 1) / P0T;
+  const int m0 = min(c0 + t * per, c1), m1 = min(m0 + per, c1);
   uint32_t cnt = 0;
   for (int m = m0; m < m1; ++m)
     cnt += p0_mb_count(info + (size_t)m * VP8G_MBINFO_BYTES, P.update_map, P.use_skip);
   // exclusive scan of the runs' counts over the workgroup
-  __shared__ uint32_t wsum[P0T / 64];
-  const int lane = t & 63, wv = t >> 6;
   uint32_t incl = cnt;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -1010,7 +1029,7 @@ __global__ __launch_bounds__(P0T) void k_p0_modes(const uint8_t* __restrict__ mb
     before += k < wv ? v : 0u;
     total += v;
   }
-  uint32_t pos = P.nhdr + before + incl - cnt;
+  uint32_t pos = P.nhdr + prior + before + incl - cnt;
   for (int m = m0; m < m1; ++m) {
     const int x = m % mbw, y = m / mbw;
     const uint8_t* in = info + (size_t)m * VP8G_MBINFO_BYTES;
@@ -1053,8 +1072,8 @@ __global__ __launch_bounds__(P0T) void k_p0_modes(const uint8_t* __restrict__ mb
       if (uvm != 2) out[pos++] = p0t(uvm != 3, 183);
     }
   }
-  if (t == 0) {
-    const uint32_t ntok = P.nhdr + total;
+  if (g == G - 1 && t == 0) {   // the last chunk ends the stream
+    const uint32_t ntok = P.nhdr + prior + total;
     M->ntok = ntok;
     M->nseg = (ntok + EMIT_SEG - 1) / EMIT_SEG;
   }
@@ -1064,8 +1083,9 @@ extern "C" int vp8g_launch_p0_modes(const uint8_t* mbinfo, int mbw, int mbh, int
                                     const vp8g_p0_par* par, const uint16_t* hdr, uint16_t* tokens,
                                     vp8g_emit_meta* meta, int meta_base, void* stream) {
   if (n <= 0) return 1;
-  hipLaunchKernelGGL(k_p0_modes, dim3(n), dim3(P0T), 0, (hipStream_t)stream, mbinfo, mbw, mbh, par,
-                     hdr, tokens, meta, meta_base);
+  const int G = (mbw * mbh + P0T - 1) / P0T;   // chunks of <= P0T MBs per frame
+  hipLaunchKernelGGL(k_p0_modes, dim3(n * G), dim3(P0T), 0, (hipStream_t)stream, mbinfo, mbw, mbh,
+                     par, hdr, tokens, meta, meta_base, G);
   return vp8g_launch_check("k_p0_modes");
 }
 

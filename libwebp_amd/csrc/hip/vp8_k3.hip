@@ -2183,6 +2183,13 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           if (x + 1 < mbw) {
             load_mb(Yp, Up, Vp, w, h, x + 1, y, L.yin, tid, K3T);
             wbar(L);
+            {   // and its texture measure (see the main worker's)
+              const int b = tid >> 4, j = tid & 15;
+              const int src = L.yin[(4 * (b >> 2) + (j >> 2)) * BPS + 4 * (b & 3) + (j & 3)];
+              const int hs = sum16(ttrans_lane(src, j, G.wy[j]));
+              if (j == 0) L.hsrc[b] = hs;
+            }
+            wbar(L);
             if (tid == 0) publish(&XL.hp_pre, (int32_t)mb + 2);
           }
           // ---- this MB's tokens (token_enc.c:113-193) into its row slot, off
@@ -2549,6 +2556,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         const K3S& Hs = reinterpret_cast<const K3S*>(smem + sizeof(K3G) + PAD)[1];
         if (tid < 16 * BPS / 4)
           reinterpret_cast<uint32_t*>(L.yin)[tid] = reinterpret_cast<const uint32_t*>(Hs.yin)[tid];
+        else if (tid < 16 * BPS / 4 + 16)
+          L.hsrc[tid - 16 * BPS / 4] = Hs.hsrc[tid - 16 * BPS / 4];
       } else {
         load_mb(Yp, Up, Vp, w, h, x, y, L.yin, tid, K3T);
       }
@@ -2567,7 +2576,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
 
       // ---- predictions (quant_enc.c:469-479; a helper pair's helper makes
       // them, the main worker's intra-4 search does not read them)
-      {
+      if (!(HP && x > 0)) {   // (a pair's helper made the measure with the source)
         if (!HP) predict_mb(L, yl, ul, vl, yt, uvt, hl, ht, tid);
         // texture (Hadamard) measure of the 16 source blocks, shared by the
         // intra16 and intra4 distortions (VP8TDisto4x4 / 16x16)
@@ -2575,8 +2584,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         const int src = L.yin[(4 * (b >> 2) + (j >> 2)) * BPS + 4 * (b & 3) + (j & 3)];
         const int hs = sum16(ttrans_lane(src, j, G.wy[j]));
         if (j == 0) L.hsrc[b] = hs;
+        wbar(L);
       }
-      wbar(L);
       K3_STAMP(1);
 
       int best16 = 0, is_i16 = 1, bu = 0;
@@ -2613,7 +2622,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         }
         tr_uv = TR_NOW();
         TR_ADD(K3TR_I4, tr_uv - tr_i4);
-        if (!wait_ge(G, L, &XL.hp_done, (int32_t)mb + 1, 7)) break;
+        // the luma choice as soon as the intra-16 one is out (the chroma one
+        // may still be running)
+        if (!wait_ge(G, L, &XL.hp_i16, (int32_t)mb + 1, 7)) break;
         K3_STAMP(3);
         best16 = __builtin_amdgcn_readfirstlane(XL.hp_best16);
         const score_t D16 = XL.hp_D16, SD16 = XL.hp_SD16, H16 = XL.hp_H16, R16 = XL.hp_R16;
@@ -2639,6 +2650,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           (&L.fin_ac[0][0])[tid] = (&L.lv16[best16][0][0])[tid];
           if (tid < 16) { L.fin_dc[tid] = L.lvdc[best16][tid]; L.modes[tid] = best16; }
         }
+        if (!wait_ge(G, L, &XL.hp_done, (int32_t)mb + 1, 7)) break;
         bu = __builtin_amdgcn_readfirstlane(XL.hp_bu);
         rdH += XL.hp_bH;
         rd_score += XL.hp_bsc;

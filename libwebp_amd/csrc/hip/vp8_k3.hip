@@ -927,6 +927,15 @@ __device__ __forceinline__ uint64_t k3_clock() {
 
 constexpr score_t kI4NoBound = (score_t)0x7fffffffffffffffll;
 
+// a search's result is the same in every lane; read back through
+// readfirstlane, branches on it are scalar
+__device__ __forceinline__ score_t uni64(score_t v) {
+  const uint64_t u = (uint64_t)v;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32));
+  return (score_t)(((uint64_t)hi << 32) | lo);
+}
+
 struct I4Result {
   int ok;
   score_t H, score;
@@ -1506,6 +1515,12 @@ struct K3XL {
   int32_t hp_tokgo, hp_tok;  // MBs handed to / tokenized by the helper (+ 1)
   uint32_t tk_ctx_t, tk_ctx_l;
   int32_t tk_first, tk_pad;  // the handed MB's context and first block (0: intra-16)
+  // intra-4 pairs (k_encode<3, .., HP, P3>): the partner's go (MB + 1) and
+  // skip, the pair barrier, the decided sub-blocks' nz bits, the stop flags
+  int32_t p_go, p_skip;
+  uint32_t p_bar, p_pad;
+  int32_t p_nz[16];
+  int32_t p_stop[2];
   uint32_t hp_ctx_t, hp_ctx_l;
   int32_t hp_seg, hp_best16, hp_bu, hp_pad;
   uint32_t hp_nz16, hp_pad2;
@@ -1575,6 +1590,181 @@ __device__ __forceinline__ void predict_mb(K3S& L, const uint8_t* yl, const uint
 
 __device__ __forceinline__ void publish(int32_t* p, int32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// barrier of an intra-4 pair (the main and the partner worker: 8 waves),
+// the worker barrier's form (wbar) with 8 arrivals per generation
+__device__ __forceinline__ void pbar(uint32_t* ctr) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  const uint32_t old = lane0_add(ctr, 1u);
+  const uint32_t target = (old & ~7u) + 8u;
+  if ((old & 7u) != 7u)
+    while (ld_uni(ctr) < target) __builtin_amdgcn_s_sleep(K3_WBAR_SLEEP);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// The intra-4 search of a helper pair with a partner worker (k_encode<3, ..,
+// HP, P3>): the 16 sub-blocks in the wavefront order t = bx + 2 by, 10 steps,
+// steps 2-7 holding two sub-blocks (kI4Pair: role 0 = the main worker, role 1
+// = the partner). A sub-block's candidates depend only on the sub-blocks to
+// its left, top, top-left and top-right, all decided at earlier steps, so
+// every choice is the sequential search's (quant_enc.c:1072-1165); the
+// running score, header bits and distortion / rate sums are the same sums in
+// another order, and the search ends (i16 wins) exactly when the sequential
+// one would, since those sums only grow. Per step: each worker evaluates its
+// sub-block's 10 candidates (the canvas is complete: a second pair barrier
+// after the commits), a pair barrier, both read the choices, the owners
+// commit to the main's canvas / acc_out / acc_ac / modes, the main
+// accumulates both and sets the stop flag, a second pair barrier.
+__constant__ int8_t kI4Pair[10][2] = {{0, -1}, {1, -1}, {2, 4},  {3, 5},   {6, 8},
+                                      {7, 9},  {10, 12}, {11, 13}, {14, -1}, {15, -1}};
+template <bool TRELLIS>
+__device__ I4Result run_i4_pair(const K3G& G, K3S& W, K3S& Lm, K3S& Lp, K3XL& XL, int role,
+                                const vp8g_seg& S, const MBCtx& ctx, int tid, int x0, int mbw,
+                                const uint8_t* predtop, const uint8_t* yl, const uint8_t* yt,
+                                score_t rd_score, int max_bits, const int32_t* bound_flag,
+                                int32_t bound_at, const score_t* bound) {
+  if (role == 0) {   // the canvas (as run_i4), then the partner may start
+    for (int k = tid; k < 21; k += K3T) {
+      uint8_t v;
+      if (k == 0) v = yl[-1];
+      else if (k <= 16) v = yt[k - 1];
+      else v = (x0 < mbw - 1) ? yt[16 + k - 17] : yt[15];
+      Lm.canvas[0][k] = v;
+    }
+    if (tid < 16) Lm.canvas[1 + tid][0] = yl[tid];
+    if (tid >= 64 && tid < 76) {
+      const int k = tid - 64;
+      Lm.canvas[4 * (1 + (k >> 2))][17 + (k & 3)] = (x0 < mbw - 1) ? yt[16 + (k & 3)] : yt[15];
+    }
+    if (tid == 0) { Lm.d4acc = 0; Lm.r4acc = 0; XL.p_stop[0] = 0; XL.p_stop[1] = 0; }
+  }
+  if (tid == 0) { W.best4[0] = ~0ull; W.best4[1] = ~0ull; W.best4[2] = ~0ull; }
+  pbar(&XL.p_bar);
+  const int m = tid >> 4, j = tid & 15, g = (tid & 63) & 48, x = j & 3, y = j >> 2;
+  const bool act = tid < 160;
+  const int wj = G.wy[j];
+  const P4Lane pl = p4_lane(G.p4[act ? tid : 0], x, y);
+  const int offa = edge_off0(pl.ia), offb = edge_off0(pl.ib), offc = edge_off0(pl.ic);
+  const vp8g_mtx& M = S.y1;
+  const uint32_t q_sh = M.sharpen[j], q_zt = M.zthresh[j], q_iq = M.iq[j], q_bias = M.bias[j];
+  const int q_q = M.q[j];
+  const uint8_t* cv = &Lm.canvas[0][0];
+  score_t acc_score = (score_t)211 * S.lambda_mode, accH = 211;
+  uint32_t acc_nz = 0;
+  int total_hdr = 0;
+  I4Result res;
+  res.ok = 1;
+  for (int t = 0; t < 10; ++t) {
+    const int b = kI4Pair[t][role];   // worker-uniform
+    const int par = t & 1;
+    int rec = 0, level = 0, nzb = 0;
+    if (b >= 0 && (tid >> 6) != 3) {   // (the 4th wave holds no mode)
+      const int bx = b & 3, by = b >> 2;
+      const int left_m = bx == 0 ? Lm.predleft[by] : Lm.modes[b - 1];
+      const int top_m = by == 0 ? predtop[4 * x0 + bx] : Lm.modes[b - 4];
+      const int tn = by == 0 ? (int)((ctx.t >> bx) & 1) : XL.p_nz[b - 4];
+      const int ln = bx == 0 ? (int)((ctx.l >> by) & 1) : XL.p_nz[b - 1];
+      const int ctx4 = tn + ln;
+      const int src = Lm.yin[(4 * by + y) * BPS + 4 * bx + x];
+      const uint8_t* cb = cv + 96 * by + 4 * bx;
+      int pr = clip8((pl.wa * cb[offa] + pl.wb * cb[offb] + pl.wc * cb[offc] + pl.rnd) >> pl.sh);
+      if (pl.dc) {
+        int s4 = 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s4 += cb[edge_off0(k)] + cb[edge_off0(5 + k)];
+        pr = s4 >> 3;
+      }
+      const int c = fdct_lane(src - pr, j);
+      int dq;
+      if constexpr (TRELLIS) {
+        const Trellis16 tr = trellis16(G, c, act, ctx4, 3, S.y1, S.lambda_trellis_i4);
+        level = tr.level;
+        dq = tr.dq;
+      } else {
+        const int neg = c < 0;
+        const uint32_t coeff = (uint32_t)(neg ? -c : c) + q_sh;
+        level = min((int)((__umul24(coeff, q_iq) + q_bias) >> QFIX), MAX_LEVEL);
+        level = coeff > q_zt ? level : 0;
+        level = neg ? -level : level;
+        dq = (int16_t)__mul24(level, q_q);
+      }
+      rec = idct_lane(dq, pr, j);
+      const uint64_t bnz = __ballot(act && level != 0);
+      const uint64_t bac = __ballot(act && level != 0 && j != 0);
+      nzb = ((bnz >> g) & 0xffff) != 0;
+      const int D = sum16((src - rec) * (src - rec));
+      int SD = 0;
+      if (S.tlambda) {
+        const int td = sum16(ttrans_lane(rec, j, wj)) - Lm.hsrc[b];
+        SD = (S.tlambda * (iabs_(td) >> 5) + 128) >> 8;
+      }
+      const int cntnz = __popcll((bac >> g) & 0xffff);
+      const int R0 = (m > 0 && cntnz <= 3) ? 140 : 0;
+      const int Rc = rate_lane(G, level, j, g, ctx4, 3, 0);
+      if (act && j == 0) {
+        const int H = G.mcost4[(top_m * 10 + left_m) * 10 + m];
+        const score_t dist = 256 * (score_t)(D + SD);
+        const score_t sc = (score_t)(R0 + Rc + H) * S.lambda_i4 + dist;
+        atomicMin(&W.best4[t % 3], ((unsigned long long)sc << 4) | (unsigned)m);
+        W.sm4[par][m] = (score_t)(R0 + Rc + H) * S.lambda_mode + dist;
+        W.r4[par][m][0] = H;
+        W.r4[par][m][1] = nzb;
+        W.r4[par][m][2] = R0 + Rc;
+        W.r4[par][m][3] = D;
+      }
+    }
+    bool have = true;
+    if (role == 0) {   // the intra-16 bound, as run_i4<.., HPB>
+      have = rd_score != kI4NoBound;
+      if (!have && tid < 64)
+        Lm.redw[2 + par] =
+            __hip_atomic_load(bound_flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= bound_at;
+    }
+    pbar(&XL.p_bar);
+    if (role == 0 && !have && __builtin_amdgcn_readfirstlane(Lm.redw[2 + par])) rd_score = *bound;
+    if (b >= 0) {
+      const int bm = (int)(W.best4[t % 3] & 15);
+      const int bx = b & 3, by = b >> 2;
+      if (act && m == bm) {   // the winning mode's lanes commit their own results
+        Lm.canvas[4 * by + 1 + y][4 * bx + 1 + x] = (uint8_t)rec;
+        Lm.acc_out[(4 * by + y) * 16 + 4 * bx + x] = (uint8_t)rec;
+        Lm.acc_ac[b][zz_inv(j)] = (int16_t)level;
+      }
+      if (tid == 0) {
+        Lm.modes[b] = (uint8_t)bm;
+        XL.p_nz[b] = W.r4[par][bm][1];
+        W.best4[(t + 2) % 3] = ~0ull;
+      }
+    }
+    if (role == 0) {   // the main worker accumulates both sub-blocks, in block order
+      bool stop = false;
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int bb = kI4Pair[t][r];
+        if (bb < 0) continue;
+        const K3S& O = r == 0 ? W : Lp;
+        const int bm = (int)(O.best4[t % 3] & 15);
+        const int H = O.r4[par][bm][0], bnzv = O.r4[par][bm][1];
+        if (tid == 0) {
+          Lm.d4acc += O.r4[par][bm][3];
+          Lm.r4acc += O.r4[par][bm][2];
+        }
+        accH += H;
+        acc_score += O.sm4[par][bm];
+        acc_nz |= (uint32_t)bnzv << bb;
+        total_hdr += H;
+      }
+      stop = acc_score >= rd_score || total_hdr > max_bits;
+      if (tid < 64) XL.p_stop[par] = stop;
+    }
+    pbar(&XL.p_bar);
+    if (__builtin_amdgcn_readfirstlane(XL.p_stop[par])) { res.ok = 0; break; }
+  }
+  res.H = accH;
+  res.score = acc_score;
+  res.nz = acc_nz;
+  return res;
 }
 
 // Fold MBs [i0, i1) into the statistics in raster order: each MB's tokens
@@ -1919,7 +2109,7 @@ struct K3Args {
 // 0 the MB loop and worker 1 each MB's intra-16 and chroma evaluation beside
 // worker 0's intra-4 search (K3XL::hp_*)
 template <int NW, bool TR, bool AF = false, bool X = false, int WPE = 1, int PAD = 0,
-          bool HP = false>
+          bool HP = false, bool P3 = false>
 __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode(K3Args a) {
   extern __shared__ __align__(16) uint8_t smem[];
   const int mbw = a.mbw, mbh = a.mbh, nmb = mbw * mbh;
@@ -1945,7 +2135,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
   uint8_t* xpredtop = reinterpret_cast<uint8_t*>(xnzw + mbw);
   int8_t* xtopderr = reinterpret_cast<int8_t*>(xpredtop + 4 * mbw);
   const bool xr = X && wk == 0;   // this worker reads the x copies
-  static_assert(!HP || (X && NW == 2 && !AF), "helper pairs: K3X, one main and one helper worker");
+  static_assert(!HP || (X && NW == (P3 ? 3 : 2) && !AF),
+                "helper pairs: K3X, one main, one helper (and an intra-4 partner) worker");
   constexpr int RW = HP ? 1 : NW;  // rows a workgroup runs at once
 
   const int nwg = X ? a.nwg : 1;
@@ -2019,6 +2210,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       XL.lcver = 0; XL.claim = 0;
       XL.hp_go = 0; XL.hp_done = 0; XL.hp_i16 = 0; XL.hp_pre = 0; XL.hp_bnd = 0;
       XL.hp_tokgo = 0; XL.hp_tok = 0;
+      XL.p_go = 0; XL.p_skip = 0; XL.p_bar = 0;
     }
   }
   if (gt < 4) G.max_edge[gt] = 0;
@@ -2301,6 +2493,31 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
               if (tid == 0) st_sc1(&xrowdone[y], x + 1);
             }
           }
+        }
+      }
+    }
+  }
+  if constexpr (P3) {
+    if (wk == 2) {
+      // the intra-4 partner: its half of each MB's search (run_i4_pair)
+      K3S& M = reinterpret_cast<K3S*>(smem + sizeof(K3G) + PAD)[0];
+      for (int y = blk; y < mbh && !L.myabort; y += nwg) {
+        for (int x = 0; x < mbw; ++x) {
+          const int rtid = opaque(rtid_k);
+          const uint32_t mb = (uint32_t)y * mbw + x;
+          if (!wait_ge(G, L, &XL.p_go, (int32_t)mb + 1, 12)) break;
+          if (__builtin_amdgcn_readfirstlane(XL.p_skip)) continue;
+          const int segid = __builtin_amdgcn_readfirstlane(XL.hp_seg);
+          const vp8g_seg& S = G.seg[segid];
+          MBCtx ctx;
+          ctx.t = __builtin_amdgcn_readfirstlane(XL.hp_ctx_t);
+          ctx.l = __builtin_amdgcn_readfirstlane(XL.hp_ctx_l);
+          if (__builtin_amdgcn_readfirstlane((int)trellis_all))   // (a scalar branch)
+            (void)run_i4_pair<true>(G, L, M, L, XL, 1, S, ctx, rtid, x, mbw, xpredtop,
+                                    M.yl_mem + 1, xytop + 16 * x, 0, 0, nullptr, 0, nullptr);
+          else
+            (void)run_i4_pair<false>(G, L, M, L, XL, 1, S, ctx, rtid, x, mbw, xpredtop,
+                                     M.yl_mem + 1, xytop + 16 * x, 0, 0, nullptr, 0, nullptr);
         }
       }
     }
@@ -2606,7 +2823,26 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         const uint64_t tr_i4 = TR_NOW();
         I4Result r4;
         r4.ok = 0; r4.H = 0; r4.score = 0; r4.nz = 0;
-        if (max_i4_bits > 0) {
+        if constexpr (P3) {   // the partner's go (or skip)
+          if (tid == 0) {
+            XL.p_skip = max_i4_bits <= 0;
+            publish(&XL.p_go, (int32_t)mb + 1);
+          }
+        }
+        if (P3 && max_i4_bits > 0) {
+          K3S& Lp = reinterpret_cast<K3S*>(smem + sizeof(K3G) + PAD)[2 % NW];
+          const int32_t at = (int32_t)mb + 1;
+          if (__builtin_amdgcn_readfirstlane((int)trellis_all))   // (a scalar branch)
+            r4 = run_i4_pair<true>(G, L, L, Lp, XL, 0, S, ctx, rtid, x, mbw, predrd, yl, yt,
+                                   kI4NoBound, max_i4_bits, &XL.hp_i16, at, &XL.hp_rd16);
+          else
+            r4 = run_i4_pair<false>(G, L, L, Lp, XL, 0, S, ctx, rtid, x, mbw, predrd, yl, yt,
+                                    kI4NoBound, max_i4_bits, &XL.hp_i16, at, &XL.hp_rd16);
+          r4.ok = __builtin_amdgcn_readfirstlane(r4.ok);
+          r4.nz = (uint32_t)__builtin_amdgcn_readfirstlane((int)r4.nz);
+          r4.H = uni64(r4.H);
+          r4.score = uni64(r4.score);
+        } else if (max_i4_bits > 0) {
           const int32_t at = (int32_t)mb + 1;
           if constexpr (TR) {
             r4 = trellis_all ? run_i4<true, true>(G, L, S, ctx, rtid, x, mbw, predrd, yl, yt, true,
@@ -3308,7 +3544,7 @@ static size_t k3x_lds_extra(int mbw) {
   return ((sizeof(K3XL) + 15) & ~(size_t)15) + 44 * (size_t)mbw + 32;
 }
 
-template <int NW, bool TR, bool HP = false>
+template <int NW, bool TR, bool HP = false, bool P3 = false>
 static int launch_k3x(K3Args a, int n, int nwg, void* stream) {
   const size_t lds = k3_lds_bytes<NW>(a.mbw, a.mbh, TR) + k3x_lds_extra(a.mbw);
   const size_t lds_tail = sizeof(K3G) + sizeof(K3S);
@@ -3320,7 +3556,7 @@ static int launch_k3x(K3Args a, int n, int nwg, void* stream) {
   static std::once_flag once;
   static hipError_t attr_err = hipSuccess;
   std::call_once(once, [] {
-    attr_err = hipFuncSetAttribute((const void*)k_encode<NW, TR, false, true, 1, 0, HP>,
+    attr_err = hipFuncSetAttribute((const void*)k_encode<NW, TR, false, true, 1, 0, HP, P3>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (attr_err == hipSuccess)
       attr_err = hipFuncSetAttribute((const void*)k_encode_xtail,
@@ -3336,16 +3572,16 @@ static int launch_k3x(K3Args a, int n, int nwg, void* stream) {
     vp8g_set_error("k_encode (K3X)", "xsync reset failed");
     return 0;
   }
-  hipLaunchKernelGGL((k_encode<NW, TR, false, true, 1, 0, HP>), dim3(n * nwg), dim3(NW * K3T), lds,
+  hipLaunchKernelGGL((k_encode<NW, TR, false, true, 1, 0, HP, P3>), dim3(n * nwg), dim3(NW * K3T), lds,
                      (hipStream_t)stream, a);
   if (!vp8g_launch_check("k_encode (K3X)")) return 0;
   hipLaunchKernelGGL(k_encode_xtail, dim3(n), dim3(K3T), lds_tail, (hipStream_t)stream, a);
   return vp8g_launch_check("k_encode_xtail");
 }
 
-template <int NW, bool TR, bool HP = false>
+template <int NW, bool TR, bool HP = false, bool P3 = false>
 static int launch_k3x_budget(const K3Args& a, int n, int nwg, void* stream) {
-  const int ok = launch_k3x<NW, TR, HP>(a, n, nwg, stream);
+  const int ok = launch_k3x<NW, TR, HP, P3>(a, n, nwg, stream);
   // give the workgroups back once the stream has passed the kernels (at once
   // if they never got enqueued)
   if (!ok || hipLaunchHostFunc((hipStream_t)stream, k3x_release,
@@ -3579,10 +3815,13 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
     // 2), =2 two workers with rows handed over in LDS
     static const int xnw = [] {
       const char* v = getenv("WEBP_AMD_K3X_NW");
-      return (v && v[0] == '2') ? 2 : (v && v[0] == '1') ? 1 : 3;
+      return (v && v[0] == '2') ? 2 : (v && v[0] == '1') ? 1 : (v && v[0] == 'p') ? 4 : 3;
     }();
     const int nwg = k3x_take(n, a.mbh, xnw == 2 ? 2 : 1);
     if (nwg > 1) {
+      if (xnw == 4)   // (A/B) helper pair + intra-4 partner
+        return trellis ? launch_k3x_budget<3, true, true, true>(a, n, nwg, stream)
+                       : launch_k3x_budget<3, false, true, true>(a, n, nwg, stream);
       if (xnw == 3)
         return trellis ? launch_k3x_budget<2, true, true>(a, n, nwg, stream)
                        : launch_k3x_budget<2, false, true>(a, n, nwg, stream);

@@ -122,6 +122,19 @@ if has k3xhp; then   # K3X helper pairs (WEBP_AMD_K3X_NW=h) against one worker: 
       --no-cpu --engines 1 > $O/single_nw$NWX.json 2> $O/single_nw$NWX.err || exit 1
   done
 fi
+if has k3xp; then   # K3X helper pairs with an intra-4 partner (WEBP_AMD_K3X_NW=p) against the
+  # helper pairs (default): parity tests first, then config 4 and one 1080p frame each way
+  WEBP_AMD_K3X_NW=p run timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_concurrency.py \
+    tests/test_token_fallbacks.py tests/test_early_fold.py tests/test_progress.py -m gpu -x -v --timeout 200 \
+    --timeout-method thread > $O/k3xp_tests.log 2>&1 || exit 1
+  for NWX in p h; do
+    WEBP_AMD_K3X_NW=$NWX run timeout -k 10 300 python3 bench.py --batch 1 --width 4096 --height 4096 --quality 90 \
+      --method 6 --steps 2 --warmup 1 --no-host-input --no-cpu --engines 1 > $O/cfg4_nw$NWX.json \
+      2> $O/cfg4_nw$NWX.err || exit 1
+    WEBP_AMD_K3X_NW=$NWX run timeout -k 10 300 python3 bench.py --batch 1 --steps 10 --warmup 2 --no-host-input \
+      --no-cpu --engines 1 > $O/single_nw$NWX.json 2> $O/single_nw$NWX.err || exit 1
+  done
+fi
 if has k3xhw; then   # K3X one row worker with the hardware barrier (WEBP_AMD_K3X_NW=1) against
   # the helper pairs (default): parity tests first, then config 4 and one 1080p frame each way
   WEBP_AMD_K3X_NW=1 run timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_concurrency.py \

@@ -2514,10 +2514,12 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           ctx.l = __builtin_amdgcn_readfirstlane(XL.hp_ctx_l);
           if (__builtin_amdgcn_readfirstlane((int)trellis_all))   // (a scalar branch)
             (void)run_i4_pair<true>(G, L, M, L, XL, 1, S, ctx, rtid, x, mbw, xpredtop,
-                                    M.yl_mem + 1, xytop + 16 * x, 0, 0, nullptr, 0, nullptr);
+                                    M.yl_mem + 1, xytop + 16 * x, kI4NoBound, max_i4_bits,
+                                    &XL.hp_i16, (int32_t)mb + 1, &XL.hp_rd16);
           else
             (void)run_i4_pair<false>(G, L, M, L, XL, 1, S, ctx, rtid, x, mbw, xpredtop,
-                                     M.yl_mem + 1, xytop + 16 * x, 0, 0, nullptr, 0, nullptr);
+                                     M.yl_mem + 1, xytop + 16 * x, kI4NoBound, max_i4_bits,
+                                     &XL.hp_i16, (int32_t)mb + 1, &XL.hp_rd16);
         }
       }
     }
@@ -2838,6 +2840,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           else
             r4 = run_i4_pair<false>(G, L, L, Lp, XL, 0, S, ctx, rtid, x, mbw, predrd, yl, yt,
                                     kI4NoBound, max_i4_bits, &XL.hp_i16, at, &XL.hp_rd16);
+          // (the result is the same in every lane: scalar branches on it)
           r4.ok = __builtin_amdgcn_readfirstlane(r4.ok);
           r4.nz = (uint32_t)__builtin_amdgcn_readfirstlane((int)r4.nz);
           r4.H = uni64(r4.H);
@@ -2865,7 +2868,8 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         best16 = __builtin_amdgcn_readfirstlane(XL.hp_best16);
         const score_t D16 = XL.hp_D16, SD16 = XL.hp_SD16, H16 = XL.hp_H16, R16 = XL.hp_R16;
         const uint32_t nz16 = __builtin_amdgcn_readfirstlane(XL.hp_nz16);
-        const score_t rd16 = (R16 + H16) * S.lambda_mode + 256 * (D16 + SD16);
+        // (worker-uniform, through readfirstlane: the branches on the choice are scalar)
+        const score_t rd16 = uni64((R16 + H16) * S.lambda_mode + 256 * (D16 + SD16));
         if (tid < 64) {   // whole wave 0: a lone-lane store here spills
           L.mdist = (int32_t)D16;
           L.ry16 = (int32_t)R16;
@@ -3808,20 +3812,26 @@ extern "C" int vp8g_launch_encode(const uint8_t* yuv, size_t yfb, int w, int h, 
   a.rowcap = rows ? rows->rowcap : 0u;
   a.rowtok = rows ? rows->rowtok : nullptr;
   if (xsync != nullptr && recon == nullptr && variant == 0) {
-    // K3X workgroups: a helper pair per row, every row on a CU of its own,
-    // intra-16 and chroma evaluated beside intra-4 (config 4 236 -> 192 ms,
-    // one 1080p frame 40.8 -> 39.1 ms against one worker, profiles/r6/k3x);
-    // A/B: WEBP_AMD_K3X_NW=1 one worker (262 -> 233 / 43.2 -> 40.9 ms against
-    // 2), =2 two workers with rows handed over in LDS
+    // K3X workgroups, one MB row each, every row on a CU of its own: a
+    // helper pair (the MB loop + a helper for intra-16, chroma, tokens,
+    // source and boundary hand-offs; m3/m4) or, for the trellis methods
+    // (m5/m6), a helper pair plus an intra-4 partner taking the second
+    // sub-block of the 10-step wavefront (config 4 158 -> 147 ms; at m4 the
+    // pair barriers cost more than the steps save: 30.8 -> 31.7 ms,
+    // profiles/r6/k3x/partner). A/B: WEBP_AMD_K3X_NW=h / p all frames one
+    // way, =1 one worker (262 -> 233 / 43.2 -> 40.9 ms against 2), =2 two
+    // workers with rows handed over in LDS
     static const int xnw = [] {
       const char* v = getenv("WEBP_AMD_K3X_NW");
-      return (v && v[0] == '2') ? 2 : (v && v[0] == '1') ? 1 : (v && v[0] == 'p') ? 4 : 3;
+      return (v && v[0] == '2') ? 2 : (v && v[0] == '1') ? 1 : (v && v[0] == 'p') ? 4
+             : (v && v[0] == 'h') ? 3 : 0;
     }();
     const int nwg = k3x_take(n, a.mbh, xnw == 2 ? 2 : 1);
     if (nwg > 1) {
-      if (xnw == 4)   // (A/B) helper pair + intra-4 partner
+      if (xnw == 4 || (xnw == 0 && trellis))
         return trellis ? launch_k3x_budget<3, true, true, true>(a, n, nwg, stream)
                        : launch_k3x_budget<3, false, true, true>(a, n, nwg, stream);
+      if (xnw == 0) return launch_k3x_budget<2, false, true>(a, n, nwg, stream);
       if (xnw == 3)
         return trellis ? launch_k3x_budget<2, true, true>(a, n, nwg, stream)
                        : launch_k3x_budget<2, false, true>(a, n, nwg, stream);

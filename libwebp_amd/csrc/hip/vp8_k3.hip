@@ -1459,6 +1459,7 @@ static_assert(sizeof(XHdr) <= XS_HDR, "XHdr outgrew its slot");
 #define XS_LCOEFFS (XS_COEFFS + NSLOT)
 #define XS_ROWDONE (XS_LCOEFFS + NSLOT)
 #define XS_REC_WORDS 12
+#define XS_PULL_COLS 16   // boundary records one row-above wait may pull
 static_assert(sizeof(XHdr) <= XS_HDR, "xsync header");
 static_assert(NSLOT % 4 == 0, "probabilities move as words");
 
@@ -1509,7 +1510,8 @@ struct K3XL {
   // intra-4 search; MBs handed over / finished (raster index + 1), the MB's
   // context, and the helper's two decisions
   int32_t hp_go, hp_done;
-  int32_t hp_i16, hp_pad3;   // MBs whose intra-16 choice (hp_rd16) is out (raster index + 1)
+  int32_t hp_i16;            // MBs whose intra-16 choice (hp_rd16) is out (raster index + 1)
+  int32_t hp_nseg;           // the segment of the MB whose source is in the helper's yin
   int32_t hp_pre;            // the MB whose source the helper has loaded into its yin (+ 1)
   int32_t hp_bnd;            // MBs whose boundary (ytop, uvtop, nzw, predtop, topderr) is out
   int32_t hp_tokgo, hp_tok;  // MBs handed to / tokenized by the helper (+ 1)
@@ -1521,6 +1523,7 @@ struct K3XL {
   uint32_t p_bar, p_pad;
   int32_t p_nz[16];
   int32_t p_stop[2];
+  int32_t xseen[4];   // the main worker's waves' polls of the row above (wait_gx_seen)
   uint32_t hp_ctx_t, hp_ctx_l;
   int32_t hp_seg, hp_best16, hp_bu, hp_pad;
   uint32_t hp_nz16, hp_pad2;
@@ -1558,6 +1561,33 @@ __device__ bool wait_gx(K3G& G, K3S& L, const int32_t* p, int32_t v, XHdr* XH) {
     __builtin_amdgcn_s_sleep(4);
   }
   wbar(L);
+  return L.myabort == 0;
+}
+
+// wait_gx that also hands back how far *p had got: the smallest of the
+// waves' last polls (each >= v), so each wave's later sc1 loads of what that
+// value covers still follow its own matching poll; slot: one word per wave
+__device__ bool wait_gx_seen(K3G& G, K3S& L, const int32_t* p, int32_t v, XHdr* XH, int32_t* slot,
+                             int tid, int32_t& seen) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  int32_t o;
+  while ((o = __builtin_amdgcn_readfirstlane(ld_sc1(p))) < v) {
+    if (ld_uni(&G.abort) || __builtin_amdgcn_readfirstlane(ld_sc1(&XH->abort)) ||
+        __builtin_amdgcn_s_memrealtime() - t0 > K3_WAIT_TICKS) {
+      L.myabort = 1;
+      atomicOr(&L.bar, WBAR_RELEASE);
+      G.abort = 1;
+      st_sc1(&XH->abort, 1);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+  if ((tid & 63) == 0) slot[tid >> 6] = o;
+  wbar(L);
+  int32_t m = slot[0];
+#pragma unroll
+  for (int k = 1; k < K3T / 64; ++k) m = min(m, slot[k]);
+  seen = __builtin_amdgcn_readfirstlane(m);
   return L.myabort == 0;
 }
 
@@ -2267,6 +2297,17 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
   const uint64_t tr_start = TR_NOW();
 #endif
 
+#ifndef K3X_MAIN_PRIO
+#define K3X_MAIN_PRIO 2
+#endif
+  if constexpr (HP) {
+    // each SIMD runs one wave of every worker: the main worker's (and the
+    // intra-4 partner's) waves, on the MB's critical path, win the SIMD's
+    // issue arbitration over the helper's, which fills the gaps (config 4
+    // 149.5 -> 141.1 ms; the helper raised to 3 while its intra-16 bound is
+    // pending instead: 148.1 ms, single 1080p 30.6 -> 31.1 ms; profiles/r6/k3x/prio)
+    if (wk != 1) __builtin_amdgcn_s_setprio(K3X_MAIN_PRIO);
+  }
   if constexpr (HP) {
     if (wk == 1) {
       // the helper: for every MB of the main worker's rows, once the main has
@@ -2296,8 +2337,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
                      x > 0, y > 0, tid);
           wbar(L);
           if constexpr (TR) {
-            if (trellis_all) eval_i16<true>(G, M, S, ctx, tid, L);
-            else eval_i16<false>(G, M, S, ctx, tid, L);
+            if (__builtin_amdgcn_readfirstlane((int)trellis_all))   // (a scalar branch)
+              eval_i16<true>(G, M, S, ctx, tid, L);
+            else
+              eval_i16<false>(G, M, S, ctx, tid, L);
           } else {
             eval_i16<false>(G, M, S, ctx, tid, L);
           }
@@ -2373,7 +2416,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           // the next MB's source into this worker's yin (the main copies it
           // from LDS instead of waiting for its own global loads)
           if (x + 1 < mbw) {
+            const int nseg = segmap[mb + 1];
             load_mb(Yp, Up, Vp, w, h, x + 1, y, L.yin, tid, K3T);
+            if (tid == 0) XL.hp_nseg = nseg;
             wbar(L);
             {   // and its texture measure (see the main worker's)
               const int b = tid >> 4, j = tid & 15;
@@ -2539,6 +2584,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       L.epseen = __hip_atomic_load(&G.epoch, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
     int left_dc = 0;
     uint32_t fold_from = (uint32_t)y * mbw;   // first MB of this row not folded yet
+    int xpc = 0;   // K3X: columns of the row above pulled so far
 #ifdef K3_PF   // (A/B) each MB fetches the next one's source during its token stage
     uint32_t pf = K3T == 256 ? fetch_mb256(Yp, Up, Vp, w, h, 0, y, tid) : 0u;
 #endif
@@ -2693,11 +2739,18 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           const uint64_t tr_w = TR_NOW();
           TR_ADD(K3TR_NROWWAIT, ld_sc1(&xrowdone[y - 1]) < min(x + 2, mbw) ? 1 : 0);
 #endif
-          if (!wait_gx(G, L, &xrowdone[y - 1], min(x + 2, mbw), XH)) break;
+          // MB x needs columns x and x + 1 of the row above; every column
+          // that row has published by the time of the wait is pulled at once
+          // (up to XS_PULL_COLS), so while it runs ahead the next MBs skip
+          // the poll and the record loads
+          const int need = min(x + 2, mbw);
+          int32_t seen = xpc;
+          if (xpc < need &&
+              !wait_gx_seen(G, L, &xrowdone[y - 1], need, XH, XL.xseen, tid, seen)) break;
           TR_SINCE(K3TR_ROW_WAIT, tr_w);
-          // pull the boundary records of columns x, x + 1 (x = 0) or x + 1
-          const int c0 = x == 0 ? 0 : x + 1;
-          const int nc = x == 0 ? min(2, mbw) : (x + 1 < mbw ? 1 : 0);
+          const int c0 = xpc;
+          const int nc = min(min((int)seen, mbw), c0 + XS_PULL_COLS) - c0;
+          xpc = c0 + max(nc, 0);
           if (tid < XS_REC_WORDS * nc) {
             const int c = c0 + tid / XS_REC_WORDS, k = tid % XS_REC_WORDS;
             const uint32_t v = ld_sc1(xrec + ((size_t)(y - 1) * mbw + c) * XS_REC_WORDS + k);
@@ -2782,7 +2835,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       }
 #endif
       wbar(L);
-      int segid = segmap[mb];
+      int segid = HP && x > 0 ? XL.hp_nseg : segmap[mb];   // (HP: read with the source)
       if (!K3CK(segid >= 0 && segid < 4, 13, segid, 4, mb)) segid = 0;
       const vp8g_seg& S = G.seg[segid];
       const bool hl = x > 0, ht = y > 0;
@@ -3033,7 +3086,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       if (TR && rd_opt == 2) {
         uint32_t nzq = 0;
         if constexpr (!TR) {
-        } else if (is_i16) {
+        } else if (__builtin_amdgcn_readfirstlane((int)is_i16)) {   // (a scalar branch)
           eval_i16<true>(G, L, S, ctx, tid, L);
           L.yout[(tid >> 4) * BPS + (tid & 15)] = L.rec16[best16][tid];
           (&L.fin_ac[0][0])[tid] = (&L.lv16[best16][0][0])[tid];
@@ -3382,6 +3435,10 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       for (int c = 0; c < 4; ++c) atomicMax(&XH->max_edge[c], G.max_edge[c]);
       if (G.tok_err) atomicOr(&XH->tok_err, G.tok_err);
       if (G.abort) atomicOr(&XH->abort, 1);
+#ifdef K3_SUBPROF   // row 0's main worker's intra-4 split (k_encode_xtail keeps it)
+      if (blk == 0)
+        for (int i = 0; i < 8; ++i) a.results[f].stamps[i] = subacc[i];
+#endif
     }
     return;
   }
@@ -3475,7 +3532,9 @@ __global__ __launch_bounds__(K3T) void k_encode_xtail(K3Args a) {
     R->skip_proba = 255;
     R->block_count[0] = XH->nb[0]; R->block_count[1] = XH->nb[1];
     R->block_count[2] = XH->nb[2];
+#if !defined(K3_SUBPROF)   // (that build: row 0's main worker's, from k_encode)
     for (int i = 0; i < 8; ++i) R->stamps[i] = 0;
+#endif
   }
 }
 // ---------------------------------------------------------------------------

@@ -1517,6 +1517,8 @@ struct K3XL {
   int32_t hp_tokgo, hp_tok;  // MBs handed to / tokenized by the helper (+ 1)
   uint32_t tk_ctx_t, tk_ctx_l;
   int32_t tk_first, tk_pad;  // the handed MB's context and first block (0: intra-16)
+  uint32_t dk_ctx_t, dk_ctx_l;   // the same, of an MB whose tokens the helper put off
+  int32_t dk_first, dk_pad;
   // intra-4 pairs (k_encode<3, .., HP, P3>): the partner's go (MB + 1) and
   // skip, the pair barrier, the decided sub-blocks' nz bits, the stop flags
   int32_t p_go, p_skip;
@@ -2318,9 +2320,98 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
       K3S& M = reinterpret_cast<K3S*>(smem + sizeof(K3G) + PAD)[0];
       const int8_t* derrx = xtopderr;   // the row above's DC errors, pulled by the main
       for (int y = blk; y < mbh && !L.myabort; y += nwg) {
+        bool dk_pending = false;   // the previous MB's tokens are still to write
         for (int x = 0; x < mbw; ++x) {
           const int tid = opaque(tid_k), lane = tid & 63;
           const uint32_t mb = (uint32_t)y * mbw + x;
+          // one MB's tokens and their statistics into the main's pending
+          // deltas (levels from Lv: the main's, or this worker's copy)
+          auto mb_tokens = [&](const K3S& Lv, int xx, uint32_t mbx, uint32_t tct, uint32_t tcl,
+                               int tfirst) {
+            const int rtid = opaque(rtid_k);
+            const int first_blk = __builtin_amdgcn_readfirstlane(tfirst);
+            const bool is_i16 = first_blk == 0;
+            MBCtx tc;
+            tc.t = __builtin_amdgcn_readfirstlane(tct);
+            tc.l = __builtin_amdgcn_readfirstlane(tcl);
+            const uint32_t rfill = rows ? M.rowfill : 0u;
+            int lvi[2], lvp[2], cnt[2], bi[2], last[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const int item = rtid + K3T * q, k = item >> 4, n = item & 15;
+              int v = 0, vp = 0;
+              if (k < 25 && k >= first_blk) {
+                const int16_t* lvb = blk_levels(Lv, k);
+                v = lvb[n];
+                vp = n > 0 ? lvb[n - 1] : 0;
+              }
+              lvi[q] = v;
+              lvp[q] = vp;
+              const int lq = max16(v != 0 ? n : -1);
+              if (n == 0 && k < 32) L.blast[k] = lq;
+            }
+            wbar(L);
+            const uint64_t nzb = __ballot(lane >= first_blk && lane < 25 && L.blast[lane] >= 0);
+            auto blk_param = [&](int k) -> int {
+              if (k < first_blk || k >= 25) return -1;
+              if (k == 0) return 1 | ((tc.top(8) + tc.left(8)) << 8);
+              if (k <= 16) {
+                const int b = k - 1, bx = b & 3, by = b >> 2;
+                const int t = by == 0 ? tc.top(bx) : (int)((nzb >> (k - 4)) & 1);
+                const int l = bx == 0 ? tc.left(by) : (int)((nzb >> (k - 1)) & 1);
+                return (is_i16 ? 0 | (1 << 4) : 3) | ((t + l) << 8);
+              }
+              const int b = k - 17, ch = b >> 2, k4 = b & 3, bx = k4 & 1, by = k4 >> 1;
+              const int t = by == 0 ? tc.top(4 + 2 * ch + bx) : (int)((nzb >> (k - 2)) & 1);
+              const int l = bx == 0 ? tc.left(4 + 2 * ch + by) : (int)((nzb >> (k - 1)) & 1);
+              return 2 | ((t + l) << 8);
+            };
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const int item = rtid + K3T * q, k = item >> 4, n = item & 15;
+              bi[q] = blk_param(k);
+              last[q] = k < 25 ? L.blast[k] : -1;
+              cnt[q] = bi[q] < 0 ? 0 : pos_count((bi[q] >> 4) & 15, n, lvi[q], lvp[q], last[q]);
+            }
+            int inc0 = cnt[0], inc1 = cnt[1];
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+              const int v0 = __shfl_up(inc0, off), v1 = __shfl_up(inc1, off);
+              if (lane >= off) { inc0 += v0; inc1 += v1; }
+            }
+            const int wv = rtid >> 6;
+            if (lane == 63) { L.wsum[0][wv] = inc0; L.wsum[1][wv] = inc1; }
+            wbar(L);
+            int pre0 = 0, pre1 = 0, tot0 = 0, tot1 = 0;
+#pragma unroll
+            for (int w2 = 0; w2 < 4; ++w2) {
+              const int s0 = L.wsum[0][w2], s1 = L.wsum[1][w2];
+              if (w2 < wv) { pre0 += s0; pre1 += s1; }
+              tot0 += s0; tot1 += s1;
+            }
+            uint16_t* slot = rows ? tok_base + (size_t)y * a.rowcap + rfill
+                                  : tok_base + (size_t)mbx * VP8G_MAX_TOKENS_PER_MB;
+            const int off0 = pre0 + inc0 - cnt[0];
+            const int off1 = tot0 + pre1 + inc1 - cnt[1];
+            const bool over = rows && rfill + (uint32_t)(tot0 + tot1) > a.rowcap;
+            if (over) { cnt[0] = 0; cnt[1] = 0; }
+            if (cnt[0])
+              pos_tokens<true>(bi[0] & 15, (bi[0] >> 4) & 15, bi[0] >> 8, rtid & 15, lvi[0], lvp[0],
+                               last[0], slot + off0, M.rdelta);
+            if (cnt[1])
+              pos_tokens<true>(bi[1] & 15, (bi[1] >> 4) & 15, bi[1] >> 8, rtid & 15, lvi[1], lvp[1],
+                               last[1], slot + off1, M.rdelta);
+            if (rtid == 0) {
+              M.rowcnt[xx] = (uint16_t)(tot0 + tot1);
+              if (rows) {
+                M.rowpos[xx] = rfill;
+                M.rowfill = rfill + (uint32_t)(tot0 + tot1);
+                if (over) atomicOr(&G.tok_err, VP8G_ERR_ARENA);
+              }
+            }
+            wbar(L);
+            if (tid == 0) publish(&XL.hp_tok, (int32_t)mbx + 1);
+          };
           const uint64_t tr_w = TR_NOW();
           if (!wait_ge(G, L, &XL.hp_go, (int32_t)mb + 1, 8)) break;
           const uint64_t tr_e = TR_NOW();
@@ -2429,96 +2520,42 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
             wbar(L);
             if (tid == 0) publish(&XL.hp_pre, (int32_t)mb + 2);
           }
+          // the previous MB's tokens, when they were put off (below): after
+          // this MB's intra-16 bound, chroma choice and the next source are
+          // out, from the levels copied then
+          if (x > 0 && dk_pending) {
+            mb_tokens(L, x - 1, mb - 1, XL.dk_ctx_t, XL.dk_ctx_l, XL.dk_first);
+            dk_pending = false;
+          }
           // ---- this MB's tokens (token_enc.c:113-193) into its row slot, off
-          // the main worker's path: the main has committed the MB and made
-          // its blocks' last non-zero positions (M.blast); one (block,
-          // position) item per thread, counts + scan + writes in parallel,
-          // the statistics into the main's pending deltas
+          // the main worker's path, once the main has committed the MB: now,
+          // when the main waits for them before its next MB (a statistics
+          // snapshot column, the row's end, an epoch refresh next), else put
+          // off until the next MB's intra-16 bound, chroma choice and source
+          // are out (the main's search takes the bound sooner), from a copy of
+          // the levels (the main overwrites its own once it has that bound)
           {
             if (!wait_ge(G, L, &XL.hp_tokgo, (int32_t)mb + 1, 11)) break;
-            const int rtid = opaque(rtid_k);
-            const int first_blk = __builtin_amdgcn_readfirstlane(XL.tk_first);
-            const bool is_i16 = first_blk == 0;
-            MBCtx tc;
-            tc.t = __builtin_amdgcn_readfirstlane(XL.tk_ctx_t);
-            tc.l = __builtin_amdgcn_readfirstlane(XL.tk_ctx_l);
-            const uint32_t rfill = rows ? M.rowfill : 0u;
-            int lvi[2], lvp[2], cnt[2], bi[2], last[2];
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-              const int item = rtid + K3T * q, k = item >> 4, n = item & 15;
-              int v = 0, vp = 0;
-              if (k < 25 && k >= first_blk) {
-                const int16_t* lvb = blk_levels(M, k);
-                v = lvb[n];
-                vp = n > 0 ? lvb[n - 1] : 0;
+            const int nx = (int)mb + 1;
+            const bool now = x == mbw - 1 || ((x + 1) % XS_SNAP_MBS == 0) ||
+                             (nx >= max_count && (nx - max_count) % (max_count + 1) == 0);
+            if (now) {
+              mb_tokens(M, x, mb, XL.tk_ctx_t, XL.tk_ctx_l, XL.tk_first);
+            } else {
+              if (tid < 8)
+                reinterpret_cast<uint32_t*>(L.fin_dc)[tid] = reinterpret_cast<const uint32_t*>(M.fin_dc)[tid];
+              else if (tid < 8 + 128)
+                reinterpret_cast<uint32_t*>(&L.fin_ac[0][0])[tid - 8] =
+                    reinterpret_cast<const uint32_t*>(&M.fin_ac[0][0])[tid - 8];
+              else if (tid < 8 + 128 + 64)
+                reinterpret_cast<uint32_t*>(&L.fin_uv[0][0])[tid - 136] =
+                    reinterpret_cast<const uint32_t*>(&M.fin_uv[0][0])[tid - 136];
+              if (tid == 0) {
+                XL.dk_ctx_t = XL.tk_ctx_t; XL.dk_ctx_l = XL.tk_ctx_l; XL.dk_first = XL.tk_first;
               }
-              lvi[q] = v;
-              lvp[q] = vp;
-              const int lq = max16(v != 0 ? n : -1);
-              if (n == 0 && k < 32) L.blast[k] = lq;
+              wbar(L);
+              dk_pending = true;
             }
-            wbar(L);
-            const uint64_t nzb = __ballot(lane >= first_blk && lane < 25 && L.blast[lane] >= 0);
-            auto blk_param = [&](int k) -> int {
-              if (k < first_blk || k >= 25) return -1;
-              if (k == 0) return 1 | ((tc.top(8) + tc.left(8)) << 8);
-              if (k <= 16) {
-                const int b = k - 1, bx = b & 3, by = b >> 2;
-                const int t = by == 0 ? tc.top(bx) : (int)((nzb >> (k - 4)) & 1);
-                const int l = bx == 0 ? tc.left(by) : (int)((nzb >> (k - 1)) & 1);
-                return (is_i16 ? 0 | (1 << 4) : 3) | ((t + l) << 8);
-              }
-              const int b = k - 17, ch = b >> 2, k4 = b & 3, bx = k4 & 1, by = k4 >> 1;
-              const int t = by == 0 ? tc.top(4 + 2 * ch + bx) : (int)((nzb >> (k - 2)) & 1);
-              const int l = bx == 0 ? tc.left(4 + 2 * ch + by) : (int)((nzb >> (k - 1)) & 1);
-              return 2 | ((t + l) << 8);
-            };
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-              const int item = rtid + K3T * q, k = item >> 4, n = item & 15;
-              bi[q] = blk_param(k);
-              last[q] = k < 25 ? L.blast[k] : -1;
-              cnt[q] = bi[q] < 0 ? 0 : pos_count((bi[q] >> 4) & 15, n, lvi[q], lvp[q], last[q]);
-            }
-            int inc0 = cnt[0], inc1 = cnt[1];
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-              const int v0 = __shfl_up(inc0, off), v1 = __shfl_up(inc1, off);
-              if (lane >= off) { inc0 += v0; inc1 += v1; }
-            }
-            const int wv = rtid >> 6;
-            if (lane == 63) { L.wsum[0][wv] = inc0; L.wsum[1][wv] = inc1; }
-            wbar(L);
-            int pre0 = 0, pre1 = 0, tot0 = 0, tot1 = 0;
-#pragma unroll
-            for (int w2 = 0; w2 < 4; ++w2) {
-              const int s0 = L.wsum[0][w2], s1 = L.wsum[1][w2];
-              if (w2 < wv) { pre0 += s0; pre1 += s1; }
-              tot0 += s0; tot1 += s1;
-            }
-            uint16_t* slot = rows ? tok_base + (size_t)y * a.rowcap + rfill
-                                  : tok_base + (size_t)mb * VP8G_MAX_TOKENS_PER_MB;
-            const int off0 = pre0 + inc0 - cnt[0];
-            const int off1 = tot0 + pre1 + inc1 - cnt[1];
-            const bool over = rows && rfill + (uint32_t)(tot0 + tot1) > a.rowcap;
-            if (over) { cnt[0] = 0; cnt[1] = 0; }
-            if (cnt[0])
-              pos_tokens<true>(bi[0] & 15, (bi[0] >> 4) & 15, bi[0] >> 8, rtid & 15, lvi[0], lvp[0],
-                               last[0], slot + off0, M.rdelta);
-            if (cnt[1])
-              pos_tokens<true>(bi[1] & 15, (bi[1] >> 4) & 15, bi[1] >> 8, rtid & 15, lvi[1], lvp[1],
-                               last[1], slot + off1, M.rdelta);
-            if (rtid == 0) {
-              M.rowcnt[x] = (uint16_t)(tot0 + tot1);
-              if (rows) {
-                M.rowpos[x] = rfill;
-                M.rowfill = rfill + (uint32_t)(tot0 + tot1);
-                if (over) atomicOr(&G.tok_err, VP8G_ERR_ARENA);
-              }
-            }
-            wbar(L);
-            if (tid == 0) publish(&XL.hp_tok, (int32_t)mb + 1);
           }
           // column x's boundary record for the next row's workgroup, off the
           // main worker's path (the stores' drain)

@@ -192,6 +192,17 @@ if has prof; then
   run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run \
     -- $BENCH --steps 2 --warmup 1 > $O/prof.log 2>&1 || exit 1
 fi
+if has xprof; then   # one 1080p frame and config 4 (K3X): kernel stats
+  run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/xstats -o run \
+    -- python3 $R/bench.py --batch 1 --steps 10 --warmup 2 --no-host-input --no-cpu --engines 1 \
+    > $O/xprof.log 2>&1 || exit 1
+  run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/x4stats -o run \
+    -- python3 $R/bench.py --batch 1 --width 4096 --height 4096 --quality 90 --method 6 --steps 2 \
+    --warmup 1 --no-host-input --no-cpu --engines 1 > $O/x4prof.log 2>&1 || exit 1
+fi
+if has smoke; then
+  run timeout -k 10 300 python3 -c 'import sys, os; sys.path.insert(0, os.getcwd()); import __graft_entry__ as g; g.smoke()' > $O/smoke.log 2>&1 || exit 1
+fi
 if has hprof; then   # host-input bench (SDMA upload): kernel timeline
   run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/hstats -o run \
     -- python3 $R/bench.py --no-cpu --steps 3 --warmup 1 > $O/hprof.log 2>&1 || exit 1

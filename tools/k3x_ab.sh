@@ -10,3 +10,8 @@ for r in 1 2; do for v in "$@"; do
   WEBP_AMD_LIB=$lib timeout -k 10 120 python3 bench.py --batch 1 --steps 10 --warmup 2 --no-host-input --no-cpu --engines 1 > $O/single_${v}_$r.json 2> $O/single_${v}_$r.err || exit 1
   WEBP_AMD_LIB=$lib timeout -k 10 200 python3 bench.py --batch 1 --width 4096 --height 4096 --quality 90 --method 6 --steps 2 --warmup 1 --no-host-input --no-cpu --engines 1 > $O/cfg4_${v}_$r.json 2> $O/cfg4_${v}_$r.err || exit 1
 done; done
+if [ -n "$K3X_NWP" ]; then   # the partner form on one 1080p frame, the product library
+  for r in 1 2; do
+    WEBP_AMD_K3X_NW=p timeout -k 10 120 python3 bench.py --batch 1 --steps 10 --warmup 2 --no-host-input --no-cpu --engines 1 > $O/single_nwp_$r.json 2> $O/single_nwp_$r.err || exit 1
+  done
+fi

@@ -21,9 +21,9 @@ if has h2d; then   # H2D / D2H copy rates from pinned host memory (host-input le
   HSA_ENABLE_SDMA=0 run timeout -k 10 120 python3 tools/h2d_probe.py 256 > $O/h2d_nosdma.json \
     2> $O/h2d_nosdma.err || exit 1
 fi
-if has trace; then   # K3 per-worker wait / stage accounting (diagnostic build; the
-  # trace + index-check build: the bare trace build faults at 256 frames)
-  WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_tracecheck.so run timeout -k 10 150 \
+if has trace; then   # K3 per-worker wait / stage accounting (the bare trace build: its
+  # round-5 fault at 256 frames was found and removed in round 6)
+  WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_trace.so run timeout -k 10 150 \
     python3 tools/k3_trace.py 1920 1080 256 4 75 $O/k3_trace_256.json > $O/k3_trace_256.log 2>&1 || exit 1
 fi
 if has budget; then   # the 8-rank host budget on one GPU (quota 16 / 8 ranks = 2 threads) next
@@ -42,7 +42,7 @@ if has p0tests; then   # partition 0 on the device + the core parity tests
     --timeout 200 --timeout-method thread > $O/gpu_p0tests.log 2>&1 || exit 1
 fi
 if has trace4; then   # the same for config 4 (one 4096^2 q90 m6 frame, K3X)
-  WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_tracecheck.so run timeout -k 10 150 \
+  WEBP_AMD_LIB=$R/libwebp_amd/libwebp_amd_trace.so run timeout -k 10 150 \
     python3 tools/k3_trace.py 4096 4096 1 6 90 $O/k3_trace_cfg4.json > $O/k3_trace_cfg4.log 2>&1 || exit 1
 fi
 if has tests; then

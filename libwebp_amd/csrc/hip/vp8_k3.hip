@@ -1402,6 +1402,8 @@ __device__ __forceinline__ int tok_stat_slot(uint32_t t) {
 }
 
 // worker-uniform wait until *p >= v (another worker of this workgroup publishes *p)
+// (SL: s_sleep units between polls)
+template <int SL = 2>
 __device__ bool wait_ge(K3G& G, K3S& L, const int32_t* p, int32_t v, int site) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while (ld_uni(p, __ATOMIC_ACQUIRE) < v) {
@@ -1428,7 +1430,7 @@ __device__ bool wait_ge(K3G& G, K3S& L, const int32_t* p, int32_t v, int site) {
       if (!G.abort) G.abort = site;     // the wait that gave up (in the result's error)
       break;
     }
-    __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_s_sleep(SL);
   }
   wbar(L);
   return L.myabort == 0;
@@ -2299,6 +2301,9 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
   const uint64_t tr_start = TR_NOW();
 #endif
 
+#ifndef K3X_HELPER_SLEEP   // s_sleep units between a helper's / partner's polls (single
+#define K3X_HELPER_SLEEP 2    // 1080p 30.3-30.5 ms at 2, 30.6-30.7 at 0, 30.55 at 10 vs 30.26
+#endif                        // at 2 on another box; profiles/r6/k3x/sleep)
 #ifndef K3X_MAIN_PRIO
 #define K3X_MAIN_PRIO 2
 #endif
@@ -2413,7 +2418,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
             if (tid == 0) publish(&XL.hp_tok, (int32_t)mbx + 1);
           };
           const uint64_t tr_w = TR_NOW();
-          if (!wait_ge(G, L, &XL.hp_go, (int32_t)mb + 1, 8)) break;
+          if (!wait_ge<K3X_HELPER_SLEEP>(G, L, &XL.hp_go, (int32_t)mb + 1, 8)) break;
           const uint64_t tr_e = TR_NOW();
           TR_ADD(K3TR_ROW_WAIT, tr_e - tr_w);   // (helper: waiting for the main)
           TR_ADD(K3TR_NMB, 1);
@@ -2535,7 +2540,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           // are out (the main's search takes the bound sooner), from a copy of
           // the levels (the main overwrites its own once it has that bound)
           {
-            if (!wait_ge(G, L, &XL.hp_tokgo, (int32_t)mb + 1, 11)) break;
+            if (!wait_ge<K3X_HELPER_SLEEP>(G, L, &XL.hp_tokgo, (int32_t)mb + 1, 11)) break;
             const int nx = (int)mb + 1;
             const bool now = x == mbw - 1 || ((x + 1) % XS_SNAP_MBS == 0) ||
                              (nx >= max_count && (nx - max_count) % (max_count + 1) == 0);
@@ -2560,7 +2565,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
           // column x's boundary record for the next row's workgroup, off the
           // main worker's path (the stores' drain)
           if (y < mbh - 1) {
-            if (!wait_ge(G, L, &XL.hp_bnd, (int32_t)mb + 1, 9)) break;
+            if (!wait_ge<K3X_HELPER_SLEEP>(G, L, &XL.hp_bnd, (int32_t)mb + 1, 9)) break;
             if (tid < 64) {
               if (tid < 11) {
                 uint32_t v;
@@ -2587,7 +2592,7 @@ __global__ __launch_bounds__(NW * K3T) __attribute__((amdgpu_waves_per_eu(WPE)))
         for (int x = 0; x < mbw; ++x) {
           const int rtid = opaque(rtid_k);
           const uint32_t mb = (uint32_t)y * mbw + x;
-          if (!wait_ge(G, L, &XL.p_go, (int32_t)mb + 1, 12)) break;
+          if (!wait_ge<K3X_HELPER_SLEEP>(G, L, &XL.p_go, (int32_t)mb + 1, 12)) break;
           if (__builtin_amdgcn_readfirstlane(XL.p_skip)) continue;
           const int segid = __builtin_amdgcn_readfirstlane(XL.hp_seg);
           const vp8g_seg& S = G.seg[segid];

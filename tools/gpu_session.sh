@@ -6,6 +6,7 @@
 set -o pipefail
 TAG=${1:-s}; shift
 STEPS=${*:-tests bench stages prof pmc sq calib}
+START=$(pwd)   # (the smoke step imports __graft_entry__ from here)
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/$TAG; mkdir -p $O
 cd $R
 has() { [[ " $STEPS " == *" $1 "* ]]; }
@@ -201,7 +202,7 @@ if has xprof; then   # one 1080p frame and config 4 (K3X): kernel stats
     --warmup 1 --no-host-input --no-cpu --engines 1 > $O/x4prof.log 2>&1 || exit 1
 fi
 if has smoke; then
-  run timeout -k 10 300 python3 -c 'import sys, os; sys.path.insert(0, os.getcwd()); import __graft_entry__ as g; g.smoke()' > $O/smoke.log 2>&1 || exit 1
+  (cd $START && run timeout -k 10 300 python3 -c 'import __graft_entry__ as g; g.smoke()') > $O/smoke.log 2>&1 || exit 1
 fi
 if has hprof; then   # host-input bench (SDMA upload): kernel timeline
   run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/hstats -o run \
